@@ -1,0 +1,162 @@
+#!/usr/bin/env python3
+"""Headline benchmark: MNIST CNN data-parallel training throughput on MI355X.
+
+Metric (BASELINE.json): images/sec for the WHOLE job, MNIST CNN DDP, B=64 per rank
+(weak scaling), fp32, synthetic 28x28 data generated on device, random-init weights.
+Each timed step is a full training step: forward, backward, bucketed RCCL all-reduce
+(N>1), SGD(momentum 0.9, wd 1e-4) update.
+
+    python bench.py --gpus 1 --steps 200 --warmup 20
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 200 --warmup 20
+
+Timing: W untimed warm-up steps (the first also captures the hipGraph), then barrier +
+device sync, K timed steps, barrier + device sync; the time is the MAX over ranks.
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+METRIC = "images/sec (whole node) MNIST CNN DDP at 1/2/4/8 MI355X; scaling efficiency"
+BASELINE_VALUE = None  # BASELINE.json "published": {} -- no MNIST number exists upstream
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=64, help="per-rank batch (reference: 64)")
+    ap.add_argument("--impl", choices=["fused", "layers", "torch"], default="fused",
+                    help="fused: native hipGraph step (default); layers: mxddp ops + DDP reducer; "
+                         "torch: stock PyTorch-ROCm DDP (comparison only)")
+    ap.add_argument("--variant", type=int, default=1, help="fused kernel variant (0 = generic igemm)")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--seed", type=int, default=1)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+
+    from mxddp.parallel import comm as C
+
+    ws_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws_env != a.gpus:
+        if ws_env == 1 and a.gpus > 1:
+            print(f"bench.py: --gpus {a.gpus} needs a launcher (torch.distributed.run)", file=sys.stderr)
+            sys.exit(2)
+    inf = C.init_distributed(use_gpu=True)
+    dev = inf.device
+    comm = C.rccl_comm()
+    B = a.batch
+
+    if a.impl == "fused":
+        from mxddp.engine import FusedMnistTrainer
+
+        tr = FusedMnistTrainer(batch=B, device=dev, comm=comm, seed=a.seed, variant=a.variant,
+                               use_graph=not a.no_graph)
+        run = tr.step
+    else:
+        run = _layers_or_torch(a, torch, inf, dev, comm, B)
+
+    run(a.warmup)
+    torch.cuda.synchronize(dev)
+    C.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run(a.steps)
+    torch.cuda.synchronize(dev)
+    C.barrier()
+    torch.cuda.synchronize(dev)
+    dt = C.all_reduce_max(time.perf_counter() - t0)
+
+    if a.impl == "fused":
+        loss_sum, correct = tr.read_metrics()
+        seen = (a.warmup + a.steps) * B
+        extra = {"train_loss_avg": loss_sum / seen, "train_acc": correct / seen}
+    else:
+        extra = {}
+    if inf.rank == 0:
+        total_imgs = a.gpus * B * a.steps
+        value = total_imgs / dt
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "images/sec",
+            "n_gpus": a.gpus,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 3),
+            "dtype": "fp32",
+            "data": "synthetic (on-device class-conditional 28x28, random-init weights)",
+            "config": {"model": "mnist_cnn", "global_batch": B * a.gpus, "per_rank_batch": B, "seq_len": None,
+                       "image": "1x28x28", "parallelism": f"dp{a.gpus}", "impl": a.impl,
+                       "graph": (a.impl == "fused" and not a.no_graph)},
+            **extra,
+        }
+        print(json.dumps(out), flush=True)
+    C.shutdown()
+
+
+def _layers_or_torch(a, torch, inf, dev, comm, B):
+    """Layer-by-layer paths (mxddp ops + mxddp DDP, or stock torch DDP for comparison)."""
+    import torch.nn.functional as F
+
+    from mxddp import native
+    from mxddp.models import MnistCNN
+
+    torch.manual_seed(a.seed)
+    model = MnistCNN().to(dev)
+    if a.impl == "layers":
+        from mxddp import ops
+        from mxddp.optim import SGD
+        from mxddp.parallel.ddp import DistributedDataParallel as DDP
+
+        net = DDP(model)
+        opt = SGD(net.flat, lr=0.1, momentum=0.9, weight_decay=1e-4)
+        loss_fn = ops.cross_entropy
+    else:
+        import torch.nn as nn
+
+        ref = nn.Sequential(nn.Conv2d(1, 32, 3), nn.ReLU(), nn.Conv2d(32, 64, 3), nn.ReLU(), nn.MaxPool2d(2),
+                            nn.Flatten(), nn.Linear(9216, 128), nn.ReLU(), nn.Linear(128, 10)).to(dev)
+        if inf.world_size > 1:
+            import torch.distributed as dist
+
+            raise SystemExit("--impl torch is single-GPU only in this harness")
+        net = ref
+        opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+        loss_fn = lambda o, t: F.cross_entropy(o, t)  # noqa: E731
+    Cn = native()
+    tmpl = torch.empty(10 * 784, device=dev)
+    ctr = torch.zeros(4, dtype=torch.int32, device=dev)
+    x = torch.empty(B, 1, 28, 28, device=dev)
+    y = torch.empty(B, dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    Cn.synth_templates(tmpl.data_ptr(), 10, 784, a.seed, st)
+
+    def run(n):
+        for _ in range(n):
+            Cn.synth_batch(x.data_ptr(), y.data_ptr(), tmpl.data_ptr(), B, 784, 10, a.seed + inf.rank, ctr.data_ptr(),
+                           torch.cuda.current_stream(dev).cuda_stream)
+            opt.zero_grad()
+            out = net(x)
+            loss = loss_fn(out, y.long())
+            loss.backward()
+            opt.step()
+
+    return run
+
+
+if __name__ == "__main__":
+    main()

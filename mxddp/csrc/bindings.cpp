@@ -1,0 +1,224 @@
+// pybind11 surface of the mxddp native extension.  Device buffers cross the boundary as
+// raw addresses (ints) and streams as hipStream_t handles, so this TU never includes
+// torch headers: the Python layer (mxddp/ops) owns tensors, validates shapes / dtypes /
+// devices, and passes `tensor.data_ptr()` and `torch.cuda.current_stream().cuda_stream`.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "comm.h"
+#include "common.h"
+#include "mnist_engine.h"
+#include "ops.h"
+#include "reducer.h"
+
+namespace py = pybind11;
+using namespace mx;
+
+namespace {
+template <class T>
+T* P(uintptr_t v) { return reinterpret_cast<T*>(v); }
+hipStream_t S(uintptr_t v) { return reinterpret_cast<hipStream_t>(v); }
+ConvShape CS(int N, int C, int H, int W, int K, int R, int S_, int sh, int sw, int ph, int pw, int dh, int dw) {
+  return ConvShape::make(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw);
+}
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "mxddp native kernels (gfx950), RCCL communicator, reducer and fused engines";
+  m.attr("ARCH") = "gfx950";
+
+  // ---------------------------------------------------------------- GEMM-shaped ops
+  m.def("conv2d_fwd", [](uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y, int N, int C, int H, int W, int K, int R,
+                         int S_, int sh, int sw, int ph, int pw, int dh, int dw, bool relu, uintptr_t st) {
+    conv2d_fwd(P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y),
+               CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw), relu, S(st));
+  });
+  m.def("conv2d_dgrad", [](uintptr_t dy, uintptr_t w, uintptr_t dx, int N, int C, int H, int W, int K, int R, int S_,
+                           int sh, int sw, int ph, int pw, int dh, int dw, uintptr_t mask, bool acc, uintptr_t st) {
+    conv2d_dgrad(P<const float>(dy), P<const float>(w), P<float>(dx), CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw),
+                 P<const float>(mask), acc, S(st));
+  });
+  m.def("conv2d_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw_, int N, int C, int H, int W, int K, int R, int S_,
+                           int sh, int sw, int ph, int pw, int dh, int dw, bool acc, uintptr_t st) {
+    conv2d_wgrad(P<const float>(dy), P<const float>(x), P<float>(dw_), CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw),
+                 acc, S(st));
+  });
+  m.def("linear_fwd", [](uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y, int M, int N, int K, bool relu,
+                         uintptr_t st) {
+    linear_fwd(P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), M, N, K, relu, S(st));
+  });
+  m.def("linear_dgrad", [](uintptr_t dy, uintptr_t w, uintptr_t dx, int M, int N, int K, uintptr_t mask, bool acc,
+                           uintptr_t st) {
+    linear_dgrad(P<const float>(dy), P<const float>(w), P<float>(dx), M, N, K, P<const float>(mask), acc, S(st));
+  });
+  m.def("linear_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, int M, int N, int K, bool acc, uintptr_t st) {
+    linear_wgrad(P<const float>(dy), P<const float>(x), P<float>(dw), M, N, K, acc, S(st));
+  });
+
+  // ---------------------------------------------------------------- elementwise
+  m.def("relu_fwd", [](uintptr_t x, uintptr_t y, int64_t n, uintptr_t st) { relu_fwd(P<const float>(x), P<float>(y), n, S(st)); });
+  m.def("relu_bwd", [](uintptr_t dy, uintptr_t y, uintptr_t dx, int64_t n, uintptr_t st) {
+    relu_bwd(P<const float>(dy), P<const float>(y), P<float>(dx), n, S(st));
+  });
+  m.def("bias_grad", [](uintptr_t dy, uintptr_t db, int outer, int C, int inner, bool acc, uintptr_t st) {
+    bias_grad(P<const float>(dy), P<float>(db), outer, C, inner, acc, S(st));
+  });
+  m.def("add_inplace", [](uintptr_t y, uintptr_t x, int64_t n, uintptr_t st) { add_inplace(P<float>(y), P<const float>(x), n, S(st)); });
+  m.def("scale_inplace", [](uintptr_t y, float a, int64_t n, uintptr_t st) { scale_inplace(P<float>(y), a, n, S(st)); });
+  m.def("fill", [](uintptr_t y, float v, int64_t n, uintptr_t st) { fill(P<float>(y), v, n, S(st)); });
+  m.def("maxpool2d_fwd", [](uintptr_t x, uintptr_t y, uintptr_t idx, int N, int C, int H, int W, int kh, int kw, int sh,
+                            int sw, int ph, int pw, int P_, int Q, uintptr_t st) {
+    maxpool2d_fwd(P<const float>(x), P<float>(y), P<int32_t>(idx), N, C, H, W, kh, kw, sh, sw, ph, pw, P_, Q, S(st));
+  });
+  m.def("maxpool2d_bwd", [](uintptr_t dy, uintptr_t idx, uintptr_t dx, int N, int C, int H, int W, int P_, int Q,
+                            uintptr_t st) {
+    maxpool2d_bwd(P<const float>(dy), P<const int32_t>(idx), P<float>(dx), N, C, H, W, P_, Q, S(st));
+  });
+  m.def("avgpool2d_fwd", [](uintptr_t x, uintptr_t y, int N, int C, int H, int W, int kh, int kw, int sh, int sw, int ph,
+                            int pw, int P_, int Q, uintptr_t st) {
+    avgpool2d_fwd(P<const float>(x), P<float>(y), N, C, H, W, kh, kw, sh, sw, ph, pw, P_, Q, S(st));
+  });
+  m.def("avgpool2d_bwd", [](uintptr_t dy, uintptr_t dx, int N, int C, int H, int W, int kh, int kw, int sh, int sw,
+                            int ph, int pw, int P_, int Q, uintptr_t st) {
+    avgpool2d_bwd(P<const float>(dy), P<float>(dx), N, C, H, W, kh, kw, sh, sw, ph, pw, P_, Q, S(st));
+  });
+  m.def("xent_fwd_bwd", [](uintptr_t logits, uintptr_t y, uintptr_t logp, uintptr_t dlogits, uintptr_t loss_sum,
+                           uintptr_t correct, int B, int C, float scale, uintptr_t st) {
+    xent_fwd_bwd(P<const float>(logits), P<const int32_t>(y), P<float>(logp), P<float>(dlogits), P<float>(loss_sum),
+                 P<float>(correct), B, C, scale, S(st));
+  });
+  m.def("bn_fwd_train", [](uintptr_t x, uintptr_t g, uintptr_t b, uintptr_t y, uintptr_t mean, uintptr_t invstd,
+                           uintptr_t rm, uintptr_t rv, int N, int C, int HW, float mom, float eps, bool relu,
+                           uintptr_t st) {
+    bn_fwd_train(P<const float>(x), P<const float>(g), P<const float>(b), P<float>(y), P<float>(mean), P<float>(invstd),
+                 P<float>(rm), P<float>(rv), N, C, HW, mom, eps, relu, S(st));
+  });
+  m.def("bn_fwd_eval", [](uintptr_t x, uintptr_t g, uintptr_t b, uintptr_t y, uintptr_t rm, uintptr_t rv, int N, int C,
+                          int HW, float eps, bool relu, uintptr_t st) {
+    bn_fwd_eval(P<const float>(x), P<const float>(g), P<const float>(b), P<float>(y), P<const float>(rm),
+                P<const float>(rv), N, C, HW, eps, relu, S(st));
+  });
+  m.def("bn_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t yr, uintptr_t g, uintptr_t mean, uintptr_t invstd,
+                     uintptr_t dx, uintptr_t dg, uintptr_t db, int N, int C, int HW, bool acc, uintptr_t st) {
+    bn_bwd(P<const float>(dy), P<const float>(x), P<const float>(yr), P<const float>(g), P<const float>(mean),
+           P<const float>(invstd), P<float>(dx), P<float>(dg), P<float>(db), N, C, HW, acc, S(st));
+  });
+  m.def("shortcut_pad_add", [](uintptr_t x, uintptr_t y, int N, int Cin, int H, int W, int Cout, int P_, int Q,
+                               int stride, uintptr_t st) {
+    shortcut_pad_add(P<const float>(x), P<float>(y), N, Cin, H, W, Cout, P_, Q, stride, S(st));
+  });
+  m.def("shortcut_pad_add_bwd", [](uintptr_t dy, uintptr_t dx, int N, int Cin, int H, int W, int Cout, int P_, int Q,
+                                   int stride, bool acc, uintptr_t st) {
+    shortcut_pad_add_bwd(P<const float>(dy), P<float>(dx), N, Cin, H, W, Cout, P_, Q, stride, acc, S(st));
+  });
+
+  // ---------------------------------------------------------------- optim / data
+  m.def("sgd_step", [](uintptr_t p, uintptr_t g, uintptr_t buf, uintptr_t lr, float gscale, float mom, float wd,
+                       int64_t n, bool first, uintptr_t st) {
+    sgd_step(P<float>(p), P<const float>(g), P<float>(buf), P<const float>(lr), gscale, mom, wd, n, first, S(st));
+  });
+  m.def("adam_step", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t lr, uintptr_t step,
+                        float gscale, float b1, float b2, float eps, float wd, int64_t n, uintptr_t st) {
+    adam_step(P<float>(p), P<const float>(g), P<float>(mm), P<float>(v), P<const float>(lr), P<const int32_t>(step),
+              gscale, b1, b2, eps, wd, n, S(st));
+  });
+  m.def("synth_templates", [](uintptr_t t, int C, int D, uint64_t seed, uintptr_t st) {
+    synth_templates(P<float>(t), C, D, seed, S(st));
+  });
+  m.def("synth_batch", [](uintptr_t x, uintptr_t y, uintptr_t t, int B, int D, int C, uint64_t seed, uintptr_t ctr,
+                          uintptr_t st) {
+    synth_batch(P<float>(x), P<int32_t>(y), P<const float>(t), B, D, C, seed, P<int32_t>(ctr), S(st));
+  });
+  m.def("augment_crop_flip_norm", [](uintptr_t x, uintptr_t y, int N, int C, int H, int W, int pad, uintptr_t mean,
+                                     uintptr_t stdv, uint64_t seed, uintptr_t ctr, uintptr_t st) {
+    augment_crop_flip_norm(P<const float>(x), P<float>(y), N, C, H, W, pad, P<const float>(mean), P<const float>(stdv),
+                           seed, P<int32_t>(ctr), S(st));
+  });
+  m.def("count_correct", [](uintptr_t logits, uintptr_t y, uintptr_t correct, int B, int C, uintptr_t st) {
+    count_correct(P<const float>(logits), P<const int32_t>(y), P<float>(correct), B, C, S(st));
+  });
+
+  // ---------------------------------------------------------------- communication
+  py::enum_<DType>(m, "DType")
+      .value("f32", DType::kF32).value("bf16", DType::kBF16).value("f16", DType::kF16)
+      .value("i32", DType::kI32).value("i64", DType::kI64).value("u8", DType::kU8);
+  py::enum_<RedOp>(m, "RedOp")
+      .value("sum", RedOp::kSum).value("avg", RedOp::kAvg).value("max", RedOp::kMax)
+      .value("min", RedOp::kMin).value("prod", RedOp::kProd);
+  py::class_<Comm>(m, "Comm")
+      .def(py::init([](py::bytes uid, int rank, int ws, int dev) { return new Comm(std::string(uid), rank, ws, dev); }))
+      .def_static("new_unique_id", []() { return py::bytes(Comm::new_unique_id()); })
+      .def_static("init_all", [](const std::vector<int>& devs) {
+        auto v = Comm::init_all(devs);
+        py::list out;
+        for (auto* c : v) out.append(py::cast(c, py::return_value_policy::take_ownership));
+        return out;
+      })
+      .def("all_reduce", [](Comm& c, uintptr_t s, uintptr_t r, size_t n, DType t, RedOp o, uintptr_t st) {
+        c.all_reduce(P<const void>(s), P<void>(r), n, t, o, S(st));
+      })
+      .def("broadcast", [](Comm& c, uintptr_t s, uintptr_t r, size_t n, DType t, int root, uintptr_t st) {
+        c.broadcast(P<const void>(s), P<void>(r), n, t, root, S(st));
+      })
+      .def("reduce_scatter", [](Comm& c, uintptr_t s, uintptr_t r, size_t n, DType t, RedOp o, uintptr_t st) {
+        c.reduce_scatter(P<const void>(s), P<void>(r), n, t, o, S(st));
+      })
+      .def("all_gather", [](Comm& c, uintptr_t s, uintptr_t r, size_t n, DType t, uintptr_t st) {
+        c.all_gather(P<const void>(s), P<void>(r), n, t, S(st));
+      })
+      .def("all_to_all", [](Comm& c, uintptr_t s, uintptr_t r, size_t n, DType t, uintptr_t st) {
+        c.all_to_all(P<const void>(s), P<void>(r), n, t, S(st));
+      })
+      .def("send", [](Comm& c, uintptr_t b, size_t n, DType t, int peer, uintptr_t st) { c.send(P<const void>(b), n, t, peer, S(st)); })
+      .def("recv", [](Comm& c, uintptr_t b, size_t n, DType t, int peer, uintptr_t st) { c.recv(P<void>(b), n, t, peer, S(st)); })
+      .def("check_async_error", &Comm::check_async_error)
+      .def("abort", &Comm::abort)
+      .def_static("group_start", &Comm::group_start)
+      .def_static("group_end", &Comm::group_end)
+      .def_property_readonly("rank", &Comm::rank)
+      .def_property_readonly("world_size", &Comm::world_size)
+      .def_property_readonly("device", &Comm::device);
+
+  py::class_<Reducer>(m, "Reducer")
+      .def(py::init([](Comm* comm, uintptr_t flat, DType t, const std::vector<std::pair<size_t, size_t>>& buckets,
+                       const std::vector<int>& param_bucket, RedOp op, bool timing) {
+             std::vector<Reducer::BucketSpec> b;
+             for (auto& x : buckets) b.push_back({x.first, x.second});
+             return new Reducer(comm, flat, t, b, param_bucket, op, timing);
+           }),
+           py::arg("comm").none(true), py::arg("flat_grad"), py::arg("dtype"), py::arg("buckets"),
+           py::arg("param_bucket"), py::arg("op") = RedOp::kSum, py::arg("timing") = false,
+           py::keep_alive<1, 2>())
+      .def("prepare", &Reducer::prepare)
+      .def("mark_ready", [](Reducer& r, int p, uintptr_t st) { r.mark_ready(p, S(st)); })
+      .def("mark_bucket_ready", [](Reducer& r, int b, uintptr_t st) { r.mark_bucket_ready(b, S(st)); })
+      .def("finalize", [](Reducer& r, uintptr_t st) { r.finalize(S(st)); })
+      .def("comm_stream", [](Reducer& r) { return reinterpret_cast<uintptr_t>(r.comm_stream()); })
+      .def("last_comm_ms", &Reducer::last_comm_ms)
+      .def_property_readonly("num_buckets", &Reducer::num_buckets)
+      .def_property_readonly("launched", &Reducer::launched);
+
+  // ---------------------------------------------------------------- fused MNIST engine
+  m.def("mnist_workspace_bytes", &MnistLayout::workspace_bytes);
+  m.attr("MNIST_NUM_PARAMS") = MnistLayout::total;
+  py::class_<MnistEngine>(m, "MnistEngine")
+      .def(py::init([](int B, uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t ws, size_t wsb, Comm* comm,
+                       uint64_t seed, float momentum, float wd, uintptr_t lr, uintptr_t metrics, int variant) {
+             return new MnistEngine(B, p, g, mom, ws, wsb, comm, seed, momentum, wd, lr, metrics, variant);
+           }),
+           py::arg("batch"), py::arg("params"), py::arg("grads"), py::arg("mom"), py::arg("workspace"),
+           py::arg("workspace_bytes"), py::arg("comm").none(true), py::arg("seed"), py::arg("momentum"),
+           py::arg("weight_decay"), py::arg("lr_dev"), py::arg("metrics_dev"), py::arg("variant") = 1,
+           py::keep_alive<1, 8>())
+      .def("step", &MnistEngine::step)
+      .def("capture", &MnistEngine::capture)
+      .def("replay", &MnistEngine::replay)
+      .def("forward_only", &MnistEngine::forward_only)
+      .def("sync", &MnistEngine::sync, py::call_guard<py::gil_scoped_release>())
+      .def("set_external_batch", &MnistEngine::set_external_batch)
+      .def("last_comm_ms", &MnistEngine::last_comm_ms)
+      .def_property_readonly("stream", &MnistEngine::stream)
+      .def_property_readonly("x_ptr", &MnistEngine::x_ptr)
+      .def_property_readonly("y_ptr", &MnistEngine::y_ptr)
+      .def_property_readonly("captured", &MnistEngine::captured);
+}

@@ -1,0 +1,120 @@
+#include "comm.h"
+
+#include "common.h"
+
+namespace mx {
+
+#define MX_NCCL_CHECK(expr)                                                                     \
+  do {                                                                                           \
+    ncclResult_t r_ = (expr);                                                                    \
+    if (r_ != ncclSuccess)                                                                       \
+      throw std::runtime_error(std::string("RCCL error '") + ncclGetErrorString(r_) + "' at " + \
+                               __FILE__ ":" + std::to_string(__LINE__) + ": " #expr);           \
+  } while (0)
+
+ncclDataType_t to_nccl(DType t) {
+  switch (t) {
+    case DType::kF32: return ncclFloat32;
+    case DType::kBF16: return ncclBfloat16;
+    case DType::kF16: return ncclFloat16;
+    case DType::kI32: return ncclInt32;
+    case DType::kI64: return ncclInt64;
+    case DType::kU8: return ncclUint8;
+  }
+  throw std::runtime_error("bad dtype");
+}
+
+ncclRedOp_t to_nccl(RedOp o) {
+  switch (o) {
+    case RedOp::kSum: return ncclSum;
+    case RedOp::kAvg: return ncclAvg;
+    case RedOp::kMax: return ncclMax;
+    case RedOp::kMin: return ncclMin;
+    case RedOp::kProd: return ncclProd;
+  }
+  throw std::runtime_error("bad op");
+}
+
+size_t dtype_size(DType t) {
+  switch (t) {
+    case DType::kF32: case DType::kI32: return 4;
+    case DType::kBF16: case DType::kF16: return 2;
+    case DType::kI64: return 8;
+    case DType::kU8: return 1;
+  }
+  return 0;
+}
+
+std::string Comm::new_unique_id() {
+  ncclUniqueId id;
+  MX_NCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+Comm::Comm(const std::string& uid, int rank, int world_size, int device)
+    : rank_(rank), ws_(world_size), device_(device) {
+  MX_CHECK(uid.size() == sizeof(ncclUniqueId), "unique id has wrong size");
+  ncclUniqueId id;
+  std::memcpy(&id, uid.data(), sizeof(id));
+  MX_HIP_CHECK(hipSetDevice(device));
+  MX_NCCL_CHECK(ncclCommInitRank(&comm_, world_size, id, rank));
+}
+
+Comm::Comm(ncclComm_t c, int rank, int world_size, int device)
+    : comm_(c), rank_(rank), ws_(world_size), device_(device) {}
+
+Comm::~Comm() {
+  if (comm_ && !aborted_) ncclCommDestroy(comm_);
+}
+
+std::vector<Comm*> Comm::init_all(const std::vector<int>& devices) {
+  std::vector<ncclComm_t> comms(devices.size());
+  MX_NCCL_CHECK(ncclCommInitAll(comms.data(), (int)devices.size(), devices.data()));
+  std::vector<Comm*> out;
+  for (size_t i = 0; i < devices.size(); ++i) out.push_back(new Comm(comms[i], (int)i, (int)devices.size(), devices[i]));
+  return out;
+}
+
+void Comm::all_reduce(const void* send, void* recv, size_t count, DType t, RedOp op, hipStream_t st) {
+  MX_NCCL_CHECK(ncclAllReduce(send, recv, count, to_nccl(t), to_nccl(op), comm_, st));
+}
+void Comm::broadcast(const void* send, void* recv, size_t count, DType t, int root, hipStream_t st) {
+  MX_NCCL_CHECK(ncclBroadcast(send, recv, count, to_nccl(t), root, comm_, st));
+}
+void Comm::reduce_scatter(const void* send, void* recv, size_t recv_count, DType t, RedOp op, hipStream_t st) {
+  MX_NCCL_CHECK(ncclReduceScatter(send, recv, recv_count, to_nccl(t), to_nccl(op), comm_, st));
+}
+void Comm::all_gather(const void* send, void* recv, size_t send_count, DType t, hipStream_t st) {
+  MX_NCCL_CHECK(ncclAllGather(send, recv, send_count, to_nccl(t), comm_, st));
+}
+void Comm::all_to_all(const void* send, void* recv, size_t count, DType t, hipStream_t st) {
+  const size_t esz = dtype_size(t);
+  MX_NCCL_CHECK(ncclGroupStart());
+  for (int p = 0; p < ws_; ++p) {
+    MX_NCCL_CHECK(ncclSend(static_cast<const char*>(send) + p * count * esz, count, to_nccl(t), p, comm_, st));
+    MX_NCCL_CHECK(ncclRecv(static_cast<char*>(recv) + p * count * esz, count, to_nccl(t), p, comm_, st));
+  }
+  MX_NCCL_CHECK(ncclGroupEnd());
+}
+void Comm::send(const void* buf, size_t count, DType t, int peer, hipStream_t st) {
+  MX_NCCL_CHECK(ncclSend(buf, count, to_nccl(t), peer, comm_, st));
+}
+void Comm::recv(void* buf, size_t count, DType t, int peer, hipStream_t st) {
+  MX_NCCL_CHECK(ncclRecv(buf, count, to_nccl(t), peer, comm_, st));
+}
+void Comm::check_async_error() const {
+  ncclResult_t r = ncclSuccess;
+  MX_NCCL_CHECK(ncclCommGetAsyncError(comm_, &r));
+  if (r != ncclSuccess && r != ncclInProgress)
+    throw std::runtime_error(std::string("RCCL async error: ") + ncclGetErrorString(r));
+}
+void Comm::abort() {
+  if (comm_ && !aborted_) {
+    ncclCommAbort(comm_);
+    aborted_ = true;
+  }
+}
+void Comm::group_start() { MX_NCCL_CHECK(ncclGroupStart()); }
+void Comm::group_end() { MX_NCCL_CHECK(ncclGroupEnd()); }
+
+}  // namespace mx

@@ -1,0 +1,60 @@
+// RCCL communicator owned by mxddp (one per process and device; or one per device
+// for the in-process replica engine).  The ncclUniqueId is exchanged through the
+// torch.distributed TCPStore by the Python layer (mxddp/parallel/comm.py), mirroring
+// the reference's `dist.init_process_group(nccl, tcp://...)` rendezvous
+// (pytorch/distributed_data_parallel.py:61-62) but giving us our own communicator
+// and HIP streams, so collectives can be issued from C++ and captured in hipGraphs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <string>
+#include <vector>
+
+namespace mx {
+
+enum class DType : int { kF32 = 0, kBF16 = 1, kF16 = 2, kI32 = 3, kI64 = 4, kU8 = 5 };
+enum class RedOp : int { kSum = 0, kAvg = 1, kMax = 2, kMin = 3, kProd = 4 };
+
+ncclDataType_t to_nccl(DType t);
+ncclRedOp_t to_nccl(RedOp o);
+size_t dtype_size(DType t);
+
+class Comm {
+ public:
+  Comm(const std::string& unique_id, int rank, int world_size, int device);
+  explicit Comm(ncclComm_t c, int rank, int world_size, int device);  // adopt (replica engine)
+  ~Comm();
+  Comm(const Comm&) = delete;
+  Comm& operator=(const Comm&) = delete;
+
+  static std::string new_unique_id();
+  // ncclCommInitAll over `devices` in one process (replica / MirroredStrategy mode)
+  static std::vector<Comm*> init_all(const std::vector<int>& devices);
+
+  void all_reduce(const void* send, void* recv, size_t count, DType t, RedOp op, hipStream_t st);
+  void broadcast(const void* send, void* recv, size_t count, DType t, int root, hipStream_t st);
+  void reduce_scatter(const void* send, void* recv, size_t recv_count, DType t, RedOp op, hipStream_t st);
+  void all_gather(const void* send, void* recv, size_t send_count, DType t, hipStream_t st);
+  void all_to_all(const void* send, void* recv, size_t count_per_peer, DType t, hipStream_t st);
+  void send(const void* buf, size_t count, DType t, int peer, hipStream_t st);
+  void recv(void* buf, size_t count, DType t, int peer, hipStream_t st);
+  // Raise if RCCL reported an asynchronous error (failure detection at step boundaries).
+  void check_async_error() const;
+  void abort();
+
+  static void group_start();
+  static void group_end();
+
+  int rank() const { return rank_; }
+  int world_size() const { return ws_; }
+  int device() const { return device_; }
+  ncclComm_t raw() const { return comm_; }
+
+ private:
+  ncclComm_t comm_ = nullptr;
+  int rank_ = 0, ws_ = 1, device_ = 0;
+  bool aborted_ = false;
+};
+
+}  // namespace mx

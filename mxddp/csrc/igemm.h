@@ -1,0 +1,157 @@
+// Implicit-GEMM engine on fp32-input MFMA (v_mfma_f32_16x16x4_f32), gfx950.
+//
+// One templated kernel drives every GEMM-shaped op of the framework (conv fwd /
+// dgrad / wgrad in NCHW, linear fwd / dgrad / wgrad).  An "Op" describes how to
+// gather the A[m][k] and B[k][n] operands from global memory (im2col on the fly,
+// nothing materialised) and how to store C[m][n] (bias / ReLU / mask / split-K
+// atomics fused into the epilogue).
+//
+// Block = 256 threads = 4 waves in a WM x WN grid; block tile BM x BN, k-tile BK.
+// Operand tiles are staged global -> registers -> LDS (k-major, rows padded so the
+// two 16-lane groups of a ds_read_b32 half-wave hit disjoint banks), double-buffered
+// with one barrier per k-tile.  Each wave owns (BM/WM) x (BN/WN) outputs as
+// TM x TN MFMA 16x16 accumulators.  fp32 in, fp32 accumulate: exact fp32 numerics
+// (gfx950 has no xf32), at the f32 matrix rate.
+//
+// Reference behaviour being replaced: cuDNN conv / cuBLAS GEMM reached through
+// nn.Conv2d / nn.Linear in pytorch/model.py:28-32,62-63,77 and the Keras/Chainer
+// layers (tensorflow2/mnist_single.py:17-26, chainer/train_mnist.py:19-21).
+#pragma once
+#include "common.h"
+
+namespace mx {
+
+template <class Op, int BM, int BN, int BK, int WM, int WN>
+__global__ __launch_bounds__(256) void igemm_f32_kernel(Op op, int k_split_len) {
+  static_assert(WM * WN == 4, "4 waves per block");
+  static_assert(BM % (16 * WM) == 0 && BN % (16 * WN) == 0, "wave tile must be 16-multiple");
+  static_assert((BM * BK) % 256 == 0 && (BN * BK) % 256 == 0, "tile loads must split evenly");
+  static_assert(BK % 4 == 0, "BK multiple of MFMA K (4)");
+  constexpr int LDA = BM + 16, LDB = BN + 16;  // (LD % 32 == 16): k-row groups on disjoint banks
+  constexpr int EA = BM * BK / 256, EB = BN * BK / 256;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+
+  __shared__ float As[2][BK * LDA];
+  __shared__ float Bs[2][BK * LDB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_n = (op.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+  const int kbeg = blockIdx.z * k_split_len;
+  const int kend = min(op.K, kbeg + k_split_len);
+  if (kbeg >= kend) return;
+
+  typename Op::APre apre[EA];
+  typename Op::BPre bpre[EB];
+  int a_kl[EA], a_ml[EA], b_kl[EB], b_nl[EB];
+#pragma unroll
+  for (int i = 0; i < EA; ++i) {
+    const int e = tid + 256 * i;
+    if constexpr (Op::A_MFAST) { a_ml[i] = e % BM; a_kl[i] = e / BM; }
+    else { a_kl[i] = e % BK; a_ml[i] = e / BK; }
+    apre[i] = op.a_pre(m0 + a_ml[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < EB; ++i) {
+    const int e = tid + 256 * i;
+    if constexpr (Op::B_NFAST) { b_nl[i] = e % BN; b_kl[i] = e / BN; }
+    else { b_kl[i] = e % BK; b_nl[i] = e / BK; }
+    bpre[i] = op.b_pre(n0 + b_nl[i]);
+  }
+
+  float ra[EA], rb[EB];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < EA; ++i) {
+      const int k = k0 + a_kl[i];
+      ra[i] = (k < kend) ? op.a_load(apre[i], k) : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < EB; ++i) {
+      const int k = k0 + b_kl[i];
+      rb[i] = (k < kend) ? op.b_load(bpre[i], k) : 0.f;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < EA; ++i) As[buf][a_kl[i] * LDA + a_ml[i]] = ra[i];
+#pragma unroll
+    for (int i = 0; i < EB; ++i) Bs[buf][b_kl[i] * LDB + b_nl[i]] = rb[i];
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = (kend - kbeg + BK - 1) / BK;
+  gload(kbeg);
+  sstore(0);
+  __syncthreads();
+  const int a_off = (lane >> 4) * LDA + wm * (BM / WM) + (lane & 15);
+  const int b_off = (lane >> 4) * LDB + wn * (BN / WN) + (lane & 15);
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) gload(kbeg + (t + 1) * BK);
+    const float* as = &As[cur][a_off];
+    const float* bs = &Bs[cur][b_off];
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      float a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = as[kk * 4 * LDA + i * 16];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = bs[kk * 4 * LDB + j * 16];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nt) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // C/D map of 16x16x4 f32: col = lane & 15, row = (lane >> 4) * 4 + reg.
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
+        if (m < op.M && n < op.N) op.store(m, n, acc[i][j][r], blockIdx.z);
+      }
+    }
+}
+
+// Host-side launcher.  `splits` > 1 splits the reduction dimension over gridDim.z;
+// the Op's store() must then accumulate atomically (output pre-zeroed).
+template <class Op, int BM, int BN, int BK, int WM, int WN>
+inline void igemm_launch(const Op& op, int splits, hipStream_t st) {
+  if (op.M <= 0 || op.N <= 0) return;
+  const int tiles = cdiv(op.M, BM) * cdiv(op.N, BN);
+  if (op.K <= 0) return;
+  splits = splits < 1 ? 1 : splits;
+  int klen = cdiv(cdiv(op.K, splits), BK) * BK;
+  splits = cdiv(op.K, klen);
+  dim3 grid(tiles, 1, splits);
+  hipLaunchKernelGGL((igemm_f32_kernel<Op, BM, BN, BK, WM, WN>), grid, dim3(256), 0, st, op, klen);
+  MX_HIP_CHECK(hipGetLastError());
+}
+
+// Choose a split-K factor so that the grid roughly fills the chip (256 CUs) without
+// making each split shorter than `min_k` reduction elements.
+inline int pick_splits(int tiles, int K, int min_k = 256, int target_blocks = 512) {
+  if (tiles >= target_blocks) return 1;
+  int s = target_blocks / (tiles > 0 ? tiles : 1);
+  int max_s = K / min_k;
+  if (s > max_s) s = max_s;
+  return s < 1 ? 1 : s;
+}
+
+}  // namespace mx

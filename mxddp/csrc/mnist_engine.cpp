@@ -1,0 +1,182 @@
+#include "mnist_engine.h"
+
+#include "common.h"
+#include "ops.h"
+#include "mnist_kernels.h"
+
+namespace mx {
+
+namespace {
+constexpr size_t kAlign = 64;  // floats (256 B)
+inline size_t al(size_t n) { return (n + kAlign - 1) / kAlign * kAlign; }
+struct Carve {
+  char* base;
+  size_t off = 0, cap;
+  template <class T>
+  T* take(size_t n) {
+    T* p = reinterpret_cast<T*>(base + off * 4);
+    off += al(n * sizeof(T) / 4 + 1);
+    MX_CHECK(off * 4 <= cap, "mnist engine workspace too small");
+    return p;
+  }
+};
+size_t ws_floats(int B) {
+  size_t t = 0;
+  auto add = [&](size_t n) { t += al(n + 1); };
+  add(B * 784);            // x
+  add(B);                  // y
+  add((size_t)B * 21632);  // a1
+  add((size_t)B * 36864);  // c2
+  add((size_t)B * 9216);   // pool
+  add((size_t)B * 9216);   // idx
+  add(B * 128);            // h
+  add(B * 10);             // logits
+  add(B * 10);             // dlogits
+  add(B * 128);            // dh
+  add((size_t)B * 9216);   // dp
+  add((size_t)B * 36864);  // dc2
+  add((size_t)B * 21632);  // da1
+  add(10 * 784);           // templates
+  add(4);                  // counter
+  add(mnist_fused_scratch_floats(B));
+  return t;
+}
+}  // namespace
+
+size_t MnistLayout::workspace_bytes(int B) { return ws_floats(B) * 4; }
+
+MnistEngine::MnistEngine(int batch, uintptr_t params, uintptr_t grads, uintptr_t mom, uintptr_t workspace,
+                         size_t workspace_bytes, Comm* comm, uint64_t seed, float momentum, float weight_decay,
+                         uintptr_t lr_dev, uintptr_t metrics_dev, int kernel_variant)
+    : B_(batch), p_(reinterpret_cast<float*>(params)), g_(reinterpret_cast<float*>(grads)),
+      m_(reinterpret_cast<float*>(mom)), lr_(reinterpret_cast<float*>(lr_dev)),
+      metrics_(reinterpret_cast<float*>(metrics_dev)), comm_(comm), seed_(seed), momentum_(momentum),
+      wd_(weight_decay), variant_(kernel_variant) {
+  MX_CHECK(B_ > 0, "batch must be positive");
+  Carve c{reinterpret_cast<char*>(workspace), 0, workspace_bytes};
+  x_ = c.take<float>(B_ * 784);
+  y_ = c.take<int32_t>(B_);
+  a1_ = c.take<float>((size_t)B_ * 21632);
+  c2_ = c.take<float>((size_t)B_ * 36864);
+  pool_ = c.take<float>((size_t)B_ * 9216);
+  idx_ = c.take<int32_t>((size_t)B_ * 9216);
+  h_ = c.take<float>(B_ * 128);
+  logits_ = c.take<float>(B_ * 10);
+  dlogits_ = c.take<float>(B_ * 10);
+  dh_ = c.take<float>(B_ * 128);
+  dp_ = c.take<float>((size_t)B_ * 9216);
+  dc2_ = c.take<float>((size_t)B_ * 36864);
+  da1_ = c.take<float>((size_t)B_ * 21632);
+  tmpl_ = c.take<float>(10 * 784);
+  counter_ = c.take<int32_t>(4);
+  scratch_ = c.take<float>(mnist_fused_scratch_floats(B_));
+  MX_HIP_CHECK(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
+  MX_HIP_CHECK(hipMemsetAsync(counter_, 0, 16, s_));
+  synth_templates(tmpl_, 10, 784, seed_ ^ 0x5eedull, s_);  // identical on every rank
+  // Two buckets in backward order: [fc1.w .. fc2.b] (4.72 MB, ready right after the fc
+  // backward) and [conv1.w .. conv2.b] (75 KB, ready at the end).  The big bucket's
+  // all-reduce overlaps the whole conv backward.
+  std::vector<Reducer::BucketSpec> buckets = {
+      {MnistLayout::fw1, MnistLayout::total - MnistLayout::fw1},
+      {0, MnistLayout::fw1},
+  };
+  reducer_ = std::make_unique<Reducer>(comm_, reinterpret_cast<uintptr_t>(g_), DType::kF32, buckets,
+                                       std::vector<int>{1, 1, 1, 1, 0, 0, 0, 0}, RedOp::kSum, false);
+  MX_HIP_CHECK(hipStreamSynchronize(s_));
+}
+
+MnistEngine::~MnistEngine() {
+  if (exec_) hipGraphExecDestroy(exec_);
+  if (graph_) hipGraphDestroy(graph_);
+  reducer_.reset();
+  if (s_) hipStreamDestroy(s_);
+}
+
+void MnistEngine::fwd(const float* x, float* logits_out, int B) {
+  using L = MnistLayout;
+  const ConvShape s1 = ConvShape::make(B, 1, 28, 28, 32, 3, 3, 1, 1, 0, 0);
+  const ConvShape s2 = ConvShape::make(B, 32, 26, 26, 64, 3, 3, 1, 1, 0, 0);
+  conv2d_fwd(x, p_ + L::w1, p_ + L::b1, a1_, s1, true, s_);
+  conv2d_fwd(a1_, p_ + L::w2, p_ + L::b2, c2_, s2, true, s_);
+  maxpool2d_fwd(c2_, pool_, idx_, B, 64, 24, 24, 2, 2, 2, 2, 0, 0, 12, 12, s_);
+  linear_fwd(pool_, p_ + L::fw1, p_ + L::fb1, h_, B, 128, 9216, false, s_);
+  relu_fwd(h_, h_, (int64_t)B * 128, s_);
+  linear_fwd(h_, p_ + L::fw2, p_ + L::fb2, logits_out, B, 10, 128, false, s_);
+}
+
+void MnistEngine::launch_step() {
+  using L = MnistLayout;
+  const int B = B_;
+  const int ws = comm_ ? comm_->world_size() : 1;
+  reducer_->prepare();
+  if (!external_batch_) synth_batch(x_, y_, tmpl_, B, 784, 10, seed_ + (comm_ ? comm_->rank() : 0) * 7919ull, counter_, s_);
+  if (variant_ == 0) {
+    // ---- reference path: generic implicit-GEMM kernels (one op per launch)
+    const ConvShape s1 = ConvShape::make(B, 1, 28, 28, 32, 3, 3, 1, 1, 0, 0);
+    const ConvShape s2 = ConvShape::make(B, 32, 26, 26, 64, 3, 3, 1, 1, 0, 0);
+    fwd(x_, logits_, B);
+    xent_fwd_bwd(logits_, y_, nullptr, dlogits_, metrics_, metrics_ + 1, B, 10, 1.f / B, s_);
+    linear_wgrad(dlogits_, h_, g_ + L::fw2, B, 10, 128, false, s_);
+    bias_grad(dlogits_, g_ + L::fb2, B, 10, 1, false, s_);
+    linear_dgrad(dlogits_, p_ + L::fw2, dh_, B, 10, 128, h_, false, s_);
+    linear_wgrad(dh_, pool_, g_ + L::fw1, B, 128, 9216, false, s_);
+    bias_grad(dh_, g_ + L::fb1, B, 128, 1, false, s_);
+    linear_dgrad(dh_, p_ + L::fw1, dp_, B, 128, 9216, nullptr, false, s_);
+    reducer_->mark_bucket_ready(0, s_);
+    maxpool2d_bwd(dp_, idx_, dc2_, B, 64, 24, 24, 12, 12, s_);
+    relu_bwd(dc2_, c2_, dc2_, (int64_t)B * 36864, s_);
+    conv2d_wgrad(dc2_, a1_, g_ + L::w2, s2, false, s_);
+    bias_grad(dc2_, g_ + L::b2, B, 64, 576, false, s_);
+    conv2d_dgrad(dc2_, p_ + L::w2, da1_, s2, a1_, false, s_);
+    conv2d_wgrad(da1_, x_, g_ + L::w1, s1, false, s_);
+    bias_grad(da1_, g_ + L::b1, B, 32, 676, false, s_);
+    reducer_->mark_bucket_ready(1, s_);
+  } else {
+    // ---- fused path (mnist_kernels.hip)
+    MnistFused f{B, x_, y_, p_, g_, a1_, pool_, idx_, h_, dh_, dp_, scratch_, metrics_};
+    mnist_fused_forward(f, s_);
+    mnist_fused_head(f, s_);
+    mnist_fused_fc1_bwd(f, s_);
+    reducer_->mark_bucket_ready(0, s_);
+    mnist_fused_conv_bwd(f, s_);
+    reducer_->mark_bucket_ready(1, s_);
+  }
+  reducer_->finalize(s_);
+  sgd_step(p_, g_, m_, lr_, 1.f / ws, momentum_, wd_, (int64_t)L::total, false, s_);
+  if (variant_ != 0) mnist_fused_post_step(MnistFused{B, x_, y_, p_, g_, a1_, pool_, idx_, h_, dh_, dp_, scratch_, metrics_}, s_);
+}
+
+void MnistEngine::step() { launch_step(); }
+
+void MnistEngine::capture() {
+  if (exec_) return;
+  MX_HIP_CHECK(hipStreamSynchronize(s_));
+  MX_HIP_CHECK(hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal));
+  try {
+    launch_step();
+  } catch (...) {
+    hipGraph_t g;
+    hipStreamEndCapture(s_, &g);
+    if (g) hipGraphDestroy(g);
+    throw;
+  }
+  MX_HIP_CHECK(hipStreamEndCapture(s_, &graph_));
+  MX_HIP_CHECK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+  MX_HIP_CHECK(hipGraphUpload(exec_, s_));
+}
+
+void MnistEngine::replay(int n) {
+  for (int i = 0; i < n; ++i) {
+    if (exec_) MX_HIP_CHECK(hipGraphLaunch(exec_, s_));
+    else launch_step();
+  }
+}
+
+void MnistEngine::forward_only(uintptr_t x, uintptr_t logits, int B) {
+  MX_CHECK(B <= B_, "eval batch larger than engine batch");
+  fwd(reinterpret_cast<const float*>(x), reinterpret_cast<float*>(logits), B);
+}
+
+void MnistEngine::sync() { MX_HIP_CHECK(hipStreamSynchronize(s_)); }
+
+}  // namespace mx

@@ -1,0 +1,70 @@
+// Native data-parallel training step for the north-star MNIST CNN
+//   conv(1->32,3)+ReLU -> conv(32->64,3)+ReLU -> maxpool2 -> fc(9216->128)+ReLU -> fc(128->10)
+//   -> log_softmax + NLL (mean), SGD(momentum, weight decay)
+// (north star op list in BASELINE.json).
+//
+// The whole step -- on-device synthetic batch, forward, backward, bucketed RCCL gradient
+// all-reduce on a side stream overlapped with the conv backward, and the fused flat SGD
+// update -- is issued from C++ into one HIP stream pair and captured ONCE into a hipGraph;
+// every training step is then a single graph launch (no Python, no host sync).
+//
+// Parameters / grads / momentum are three flat fp32 buffers in PyTorch state_dict order
+// (conv1.weight, conv1.bias, conv2.weight, conv2.bias, fc1.weight, fc1.bias, fc2.weight,
+// fc2.bias) owned by the Python side, so checkpoints keep the reference layout
+// (pytorch/distributed_data_parallel.py:103-115).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+
+#include "comm.h"
+#include "reducer.h"
+
+namespace mx {
+
+struct MnistLayout {
+  static constexpr int kC1 = 32, kC2 = 64, kH = 28, kH1 = 26, kH2 = 24, kHP = 12, kF1 = 128, kNC = 10;
+  static constexpr size_t w1 = 0, b1 = 288, w2 = 320, b2 = 18752, fw1 = 18816, fb1 = 1198464, fw2 = 1198592,
+                          fb2 = 1199872, total = 1199882;
+  static size_t workspace_bytes(int B);
+};
+
+class MnistEngine {
+ public:
+  MnistEngine(int batch, uintptr_t params, uintptr_t grads, uintptr_t mom, uintptr_t workspace,
+              size_t workspace_bytes, Comm* comm, uint64_t seed, float momentum, float weight_decay,
+              uintptr_t lr_dev, uintptr_t metrics_dev, int kernel_variant);
+  ~MnistEngine();
+
+  void step();               // one training step, eager launches on stream()
+  void capture();            // record the step into a hipGraph (call after a warm-up step)
+  void replay(int n);        // n graph launches (falls back to step() if not captured)
+  void forward_only(uintptr_t x, uintptr_t logits, int B);  // eval helper (no grads)
+  void sync();
+  uintptr_t stream() const { return reinterpret_cast<uintptr_t>(s_); }
+  uintptr_t x_ptr() const { return reinterpret_cast<uintptr_t>(x_); }
+  uintptr_t y_ptr() const { return reinterpret_cast<uintptr_t>(y_); }
+  void set_external_batch(bool on) { external_batch_ = on; }
+  float last_comm_ms() { return reducer_ ? reducer_->last_comm_ms() : 0.f; }
+  bool captured() const { return exec_ != nullptr; }
+
+ private:
+  void launch_step();
+  void fwd(const float* x, float* logits_out, int B);
+  int B_;
+  float *p_, *g_, *m_;
+  float *x_, *a1_, *c2_, *pool_, *h_, *logits_, *dlogits_, *dh_, *dp_, *dc2_, *da1_, *tmpl_, *scratch_;
+  int32_t *y_, *idx_, *counter_;
+  float *lr_, *metrics_;
+  Comm* comm_;
+  std::unique_ptr<Reducer> reducer_;
+  uint64_t seed_;
+  float momentum_, wd_;
+  int variant_;
+  bool external_batch_ = false;
+  hipStream_t s_ = nullptr;
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t exec_ = nullptr;
+};
+
+}  // namespace mx

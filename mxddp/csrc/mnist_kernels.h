@@ -1,0 +1,32 @@
+// Fused CDNA4 kernels for the MNIST CNN training step (see mnist_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace mx {
+
+struct MnistFused {
+  int B;
+  float* x;        // [B,1,28,28]
+  int32_t* y;      // [B]
+  float* p;        // flat params (MnistLayout offsets)
+  float* g;        // flat grads
+  float* a1;       // [B,32,26,26] post-ReLU conv1
+  float* pool;     // [B,64,12,12] post-ReLU pooled conv2
+  int32_t* idx;    // [B,64,12,12] argmax (0..3) within the 2x2 window, 4 = dead (max <= 0)
+  float* h;        // [B,128] fc1 pre-activation accumulator
+  float* dh;       // [B,128] grad wrt fc1 pre-activation
+  float* dp;       // [B,9216] grad wrt pooled activation
+  float* scratch;  // packed weights + split-K partials
+  float* metrics;  // [0] loss sum, [1] correct count (accumulated on device)
+};
+
+size_t mnist_fused_scratch_floats(int B);
+void mnist_fused_forward(const MnistFused& f, hipStream_t st);
+void mnist_fused_head(const MnistFused& f, hipStream_t st);
+void mnist_fused_fc1_bwd(const MnistFused& f, hipStream_t st);
+void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st);
+void mnist_fused_post_step(const MnistFused& f, hipStream_t st);
+
+}  // namespace mx

@@ -1,0 +1,111 @@
+// Host-callable launchers for every mxddp HIP kernel (fp32 unless noted).
+// All pointers are device pointers; all launches are asynchronous on `st` and
+// graph-capturable (no allocation, no synchronisation inside).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace mx {
+
+struct ConvShape {
+  int N, C, H, W;        // input
+  int K, R, S;           // filters
+  int P, Q;              // output spatial
+  int str_h, str_w, pad_h, pad_w, dil_h, dil_w;
+  static ConvShape make(int N, int C, int H, int W, int K, int R, int S, int sh, int sw, int ph,
+                        int pw, int dh = 1, int dw = 1) {
+    ConvShape c{N, C, H, W, K, R, S, 0, 0, sh, sw, ph, pw, dh, dw};
+    c.P = (H + 2 * ph - dh * (R - 1) - 1) / sh + 1;
+    c.Q = (W + 2 * pw - dw * (S - 1) - 1) / sw + 1;
+    return c;
+  }
+};
+
+// ---- GEMM-shaped (ops_gemm.hip) ----
+void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s,
+                bool relu, hipStream_t st);
+// dx = conv_transpose(dy, w) [* (mask > 0)], stored (=) or accumulated (+=).
+void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s,
+                  const float* relu_mask, bool accumulate, hipStream_t st);
+// dw (+)= sum_{n,p,q} dy * im2col(x)
+void conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate,
+                  hipStream_t st);
+// y[M,N] = x[M,K] @ w[N,K]^T + b  (optional ReLU)
+void linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int N, int K,
+                bool relu, hipStream_t st);
+// dx[M,K] (+)= dy[M,N] @ w[N,K]  [* (mask > 0)]
+void linear_dgrad(const float* dy, const float* w, float* dx, int M, int N, int K,
+                  const float* relu_mask, bool accumulate, hipStream_t st);
+// dw[N,K] (+)= dy[M,N]^T @ x[M,K]
+void linear_wgrad(const float* dy, const float* x, float* dw, int M, int N, int K, bool accumulate,
+                  hipStream_t st);
+
+// ---- elementwise / reductions (ops_elementwise.hip) ----
+void relu_fwd(const float* x, float* y, int64_t n, hipStream_t st);
+void relu_bwd(const float* dy, const float* y, float* dx, int64_t n, hipStream_t st);
+// db[c] (+)= sum over (outer, inner) of dy[outer][c][inner]
+void bias_grad(const float* dy, float* db, int outer, int C, int inner, bool accumulate,
+               hipStream_t st);
+void add_inplace(float* y, const float* x, int64_t n, hipStream_t st);
+void scale_inplace(float* y, float a, int64_t n, hipStream_t st);
+void fill(float* y, float v, int64_t n, hipStream_t st);
+
+// maxpool 2D (NCHW); idx stores the flat argmax offset inside the input plane.
+void maxpool2d_fwd(const float* x, float* y, int32_t* idx, int N, int C, int H, int W, int kh, int kw,
+                   int sh, int sw, int ph, int pw, int P, int Q, hipStream_t st);
+void maxpool2d_bwd(const float* dy, const int32_t* idx, float* dx, int N, int C, int H, int W, int P,
+                   int Q, hipStream_t st);
+// avgpool 2D (count_include_pad=True semantics of nn.AvgPool2d, ceil_mode clipping)
+void avgpool2d_fwd(const float* x, float* y, int N, int C, int H, int W, int kh, int kw, int sh, int sw,
+                   int ph, int pw, int P, int Q, hipStream_t st);
+void avgpool2d_bwd(const float* dy, float* dx, int N, int C, int H, int W, int kh, int kw, int sh,
+                   int sw, int ph, int pw, int P, int Q, hipStream_t st);
+
+// Fused log_softmax + NLL (mean) forward + backward in one pass.
+//  logits [B,C] -> loss_sum (atomic += sum of -logp[y]), correct (atomic += #argmax==y),
+//  dlogits = (softmax - onehot) * grad_scale  (if dlogits != nullptr), logp (optional).
+// `probs_input`=true treats logits as already-softmaxed probabilities (Keras softmax head).
+void xent_fwd_bwd(const float* logits, const int32_t* y, float* logp, float* dlogits,
+                  float* loss_sum, float* correct, int B, int C, float grad_scale, hipStream_t st);
+
+// BatchNorm2d (training): batch stats, running-stat update, normalise (+ optional ReLU).
+void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* y, float* mean,
+                  float* invstd, float* run_mean, float* run_var, int N, int C, int HW,
+                  float momentum, float eps, bool relu, hipStream_t st);
+void bn_fwd_eval(const float* x, const float* gamma, const float* beta, float* y,
+                 const float* run_mean, const float* run_var, int N, int C, int HW, float eps,
+                 bool relu, hipStream_t st);
+void bn_bwd(const float* dy, const float* x, const float* y_relu, const float* gamma,
+            const float* mean, const float* invstd, float* dx, float* dgamma, float* dbeta, int N,
+            int C, int HW, bool accumulate_params, hipStream_t st);
+
+// PyramidNet shortcut: y[n,c,:,:] += (c < Cin ? pool(x)[n,c] : 0); pool = 2x2 avg, ceil.
+void shortcut_pad_add(const float* x, float* y, int N, int Cin, int H, int W, int Cout, int P, int Q,
+                      int stride, hipStream_t st);
+void shortcut_pad_add_bwd(const float* dy, float* dx, int N, int Cin, int H, int W, int Cout, int P,
+                          int Q, int stride, bool accumulate, hipStream_t st);
+
+// ---- optimizers (ops_optim.hip): flat multi-tensor, fp32 master ----
+// SGD (PyTorch semantics): g' = g*gscale + wd*p; buf = mom*buf + g' (buf=g' at first step); p -= lr*buf
+// `lr` is read from device memory so a captured graph follows LR schedules.
+void sgd_step(float* p, const float* g, float* buf, const float* lr, float gscale, float momentum,
+              float wd, int64_t n, bool first_step, hipStream_t st);
+// Adam (PyTorch/Keras semantics, bias-corrected); step counter read from device memory.
+void adam_step(float* p, const float* g, float* m, float* v, const float* lr, const int32_t* step,
+               float gscale, float b1, float b2, float eps, float wd, int64_t n, hipStream_t st);
+
+// ---- data (ops_data.hip) ----
+// Class-conditional synthetic images: x = 0.5*template[y] + 0.5*noise, y ~ U{0..C-1}.
+// Deterministic in (seed, counter[0]); counter is incremented on device after each batch.
+void synth_batch(float* x, int32_t* y, const float* templates, int B, int D, int C, uint64_t seed,
+                 int32_t* counter, hipStream_t st);
+void synth_templates(float* templates, int C, int D, uint64_t seed, hipStream_t st);
+// On-device CIFAR-style augmentation: random crop (pad 4) + h-flip + normalize (NCHW).
+void augment_crop_flip_norm(const float* x, float* y, int N, int C, int H, int W, int pad,
+                            const float* mean, const float* std, uint64_t seed, int32_t* counter,
+                            hipStream_t st);
+// argmax(logits)==y counts (metrics)
+void count_correct(const float* logits, const int32_t* y, float* correct, int B, int C, hipStream_t st);
+
+}  // namespace mx

@@ -1,0 +1,298 @@
+// Conv2d / Linear forward + backward as Ops of the MFMA implicit-GEMM engine.
+// NCHW fp32, arbitrary stride / padding / dilation and non-tile-multiple channel
+// counts (PyramidNet-110 has 103 distinct (C_in, C_out) pairs).
+#include "igemm.h"
+#include "ops.h"
+
+namespace mx {
+namespace {
+
+enum StoreMode { kStore = 0, kAccum = 1, kAtomic = 2 };
+
+__device__ __forceinline__ void emit(float* out, int64_t idx, float v, int mode) {
+  if (mode == kStore) out[idx] = v;
+  else if (mode == kAccum) out[idx] += v;
+  else atomicAdd(out + idx, v);
+}
+
+// ------------------------------------------------------------------ conv geometry
+struct ConvG {
+  int N, C, H, W, K, R, S, P, Q, sh, sw, ph, pw, dh, dw;
+  int PQ, RS, HW;
+  FastDiv fPQ, fQ, fRS, fS, fHW, fW;
+  explicit ConvG(const ConvShape& s)
+      : N(s.N), C(s.C), H(s.H), W(s.W), K(s.K), R(s.R), S(s.S), P(s.P), Q(s.Q), sh(s.str_h),
+        sw(s.str_w), ph(s.pad_h), pw(s.pad_w), dh(s.dil_h), dw(s.dil_w) {
+    PQ = P * Q;
+    RS = R * S;
+    HW = H * W;
+    fPQ = FastDiv(PQ);
+    fQ = FastDiv(Q);
+    fRS = FastDiv(RS);
+    fS = FastDiv(S);
+    fHW = FastDiv(HW);
+    fW = FastDiv(W);
+  }
+};
+
+// Forward: C[m=(n,p,q)][kout] = sum_{k=(c,r,s)} x[n,c,p*sh-ph+r*dh, q*sw-pw+s*dw] * w[kout,c,r,s]
+struct ConvFwdOp {
+  static constexpr bool A_MFAST = true;   // consecutive q -> coalesced input rows
+  static constexpr bool B_NFAST = false;  // weights read along (c,r,s)
+  int M, N, K;
+  ConvG g;
+  const float* x;
+  const float* w;
+  const float* bias;
+  float* y;
+  bool relu;
+  struct APre { int64_t base; int h0, w0; bool ok; };
+  struct BPre { int64_t base; bool ok; };
+  __device__ APre a_pre(int m) const {
+    APre a;
+    a.ok = m < M;
+    const int mm = a.ok ? m : 0;
+    const int n = g.fPQ.div(mm), pq = mm - n * g.PQ;
+    const int p = g.fQ.div(pq), q = pq - p * g.Q;
+    a.h0 = p * g.sh - g.ph;
+    a.w0 = q * g.sw - g.pw;
+    a.base = (int64_t)n * g.C * g.HW;
+    return a;
+  }
+  __device__ float a_load(const APre& a, int k) const {
+    const int c = g.fRS.div(k), rs = k - c * g.RS;
+    const int r = g.fS.div(rs), s = rs - r * g.S;
+    const int h = a.h0 + r * g.dh, ww = a.w0 + s * g.dw;
+    if (!a.ok || (unsigned)h >= (unsigned)g.H || (unsigned)ww >= (unsigned)g.W) return 0.f;
+    return x[a.base + (int64_t)c * g.HW + h * g.W + ww];
+  }
+  __device__ BPre b_pre(int n) const { return BPre{(int64_t)(n < N ? n : 0) * K, n < N}; }
+  __device__ float b_load(const BPre& b, int k) const { return b.ok ? w[b.base + k] : 0.f; }
+  __device__ void store(int m, int n, float v, int) const {
+    const int nb = g.fPQ.div(m), pq = m - nb * g.PQ;
+    if (bias) v += bias[n];
+    if (relu) v = fmaxf(v, 0.f);
+    y[((int64_t)nb * g.K + n) * g.PQ + pq] = v;
+  }
+};
+
+// Data gradient: C[m=(n,h,w)][c] = sum_{k=(kout,r,s)} dy[n,kout,p,q] * w[kout,c,r,s]
+//   with p = (h + ph - r*dh)/sh when divisible and in range.
+struct ConvDgradOp {
+  static constexpr bool A_MFAST = true;
+  static constexpr bool B_NFAST = true;
+  int M, N, K;
+  ConvG g;
+  const float* dy;
+  const float* w;
+  float* dx;
+  const float* mask;
+  int mode;
+  struct APre { int64_t base; int h, w; bool ok; };
+  struct BPre { int n; bool ok; };
+  __device__ APre a_pre(int m) const {
+    APre a;
+    a.ok = m < M;
+    const int mm = a.ok ? m : 0;
+    const int n = g.fHW.div(mm), hw = mm - n * g.HW;
+    a.h = g.fW.div(hw);
+    a.w = hw - a.h * g.W;
+    a.base = (int64_t)n * g.K * g.PQ;
+    return a;
+  }
+  __device__ float a_load(const APre& a, int k) const {
+    const int ko = g.fRS.div(k), rs = k - ko * g.RS;
+    const int r = g.fS.div(rs), s = rs - r * g.S;
+    int ph_ = a.h + g.ph - r * g.dh, pw_ = a.w + g.pw - s * g.dw;
+    if (!a.ok || ph_ < 0 || pw_ < 0) return 0.f;
+    int p = ph_, q = pw_;
+    if (g.sh != 1) { p = ph_ / g.sh; if (p * g.sh != ph_) return 0.f; }
+    if (g.sw != 1) { q = pw_ / g.sw; if (q * g.sw != pw_) return 0.f; }
+    if (p >= g.P || q >= g.Q) return 0.f;
+    return dy[a.base + (int64_t)ko * g.PQ + p * g.Q + q];
+  }
+  __device__ BPre b_pre(int n) const { return BPre{n, n < N}; }
+  __device__ float b_load(const BPre& b, int k) const {
+    if (!b.ok) return 0.f;
+    const int ko = g.fRS.div(k), rs = k - ko * g.RS;
+    return w[((int64_t)ko * g.C + b.n) * g.RS + rs];
+  }
+  __device__ void store(int m, int n, float v, int) const {
+    const int nb = g.fHW.div(m), hw = m - nb * g.HW;
+    const int64_t idx = ((int64_t)nb * g.C + n) * g.HW + hw;
+    if (mask && !(mask[idx] > 0.f)) v = 0.f;
+    emit(dx, idx, v, mode);
+  }
+};
+
+// Weight gradient: C[kout][n=(c,r,s)] = sum_{k=(n,p,q)} dy[n,kout,p,q] * x[n,c,h,w]
+struct ConvWgradOp {
+  static constexpr bool A_MFAST = false;  // consecutive k = consecutive q: coalesced dy rows
+  static constexpr bool B_NFAST = false;  // consecutive k: coalesced x rows
+  int M, N, K;
+  ConvG g;
+  const float* dy;
+  const float* x;
+  float* dw;
+  int mode;
+  struct APre { int m; bool ok; };
+  struct BPre { int64_t coff; int r, s; bool ok; };
+  __device__ APre a_pre(int m) const { return APre{m, m < M}; }
+  __device__ float a_load(const APre& a, int k) const {
+    if (!a.ok) return 0.f;
+    const int nb = g.fPQ.div(k), pq = k - nb * g.PQ;
+    return dy[((int64_t)nb * g.K + a.m) * g.PQ + pq];
+  }
+  __device__ BPre b_pre(int n) const {
+    BPre b;
+    b.ok = n < N;
+    const int nn = b.ok ? n : 0;
+    const int c = g.fRS.div(nn), rs = nn - c * g.RS;
+    b.r = g.fS.div(rs);
+    b.s = rs - b.r * g.S;
+    b.r *= g.dh;
+    b.s *= g.dw;
+    b.coff = (int64_t)c * g.HW;
+    return b;
+  }
+  __device__ float b_load(const BPre& b, int k) const {
+    const int nb = g.fPQ.div(k), pq = k - nb * g.PQ;
+    const int p = g.fQ.div(pq), q = pq - p * g.Q;
+    const int h = p * g.sh - g.ph + b.r, ww = q * g.sw - g.pw + b.s;
+    if (!b.ok || (unsigned)h >= (unsigned)g.H || (unsigned)ww >= (unsigned)g.W) return 0.f;
+    return x[(int64_t)nb * g.C * g.HW + b.coff + h * g.W + ww];
+  }
+  __device__ void store(int m, int n, float v, int) const { emit(dw, (int64_t)m * N + n, v, mode); }
+};
+
+// ------------------------------------------------------------------ linear
+struct LinFwdOp {  // y[M,N] = x[M,K] w[N,K]^T + b
+  static constexpr bool A_MFAST = false;
+  static constexpr bool B_NFAST = false;
+  int M, N, K;
+  const float* x;
+  const float* w;
+  const float* b;
+  float* y;
+  bool relu;
+  int mode;
+  struct Pre { int64_t base; bool ok; };
+  using APre = Pre;
+  using BPre = Pre;
+  __device__ Pre a_pre(int m) const { return Pre{(int64_t)(m < M ? m : 0) * K, m < M}; }
+  __device__ float a_load(const Pre& a, int k) const { return a.ok ? x[a.base + k] : 0.f; }
+  __device__ Pre b_pre(int n) const { return Pre{(int64_t)(n < N ? n : 0) * K, n < N}; }
+  __device__ float b_load(const Pre& p, int k) const { return p.ok ? w[p.base + k] : 0.f; }
+  __device__ void store(int m, int n, float v, int split) const {
+    if (b && split == 0) v += b[n];
+    if (relu) v = fmaxf(v, 0.f);
+    emit(y, (int64_t)m * N + n, v, mode);
+  }
+};
+
+struct LinDgradOp {  // dx[M,Kin] = dy[M,Nout] w[Nout,Kin]; GEMM N=Kin, K=Nout
+  static constexpr bool A_MFAST = false;
+  static constexpr bool B_NFAST = true;
+  int M, N, K;
+  const float* dy;
+  const float* w;
+  float* dx;
+  const float* mask;
+  int mode;
+  struct APre { int64_t base; bool ok; };
+  struct BPre { int n; bool ok; };
+  __device__ APre a_pre(int m) const { return APre{(int64_t)(m < M ? m : 0) * K, m < M}; }
+  __device__ float a_load(const APre& a, int k) const { return a.ok ? dy[a.base + k] : 0.f; }
+  __device__ BPre b_pre(int n) const { return BPre{n, n < N}; }
+  __device__ float b_load(const BPre& b, int k) const { return b.ok ? w[(int64_t)k * N + b.n] : 0.f; }
+  __device__ void store(int m, int n, float v, int) const {
+    const int64_t idx = (int64_t)m * N + n;
+    if (mask && !(mask[idx] > 0.f)) v = 0.f;
+    emit(dx, idx, v, mode);
+  }
+};
+
+struct LinWgradOp {  // dw[Nout,Kin] = dy[B,Nout]^T x[B,Kin]; GEMM M=Nout, N=Kin, K=B
+  static constexpr bool A_MFAST = true;
+  static constexpr bool B_NFAST = true;
+  int M, N, K;
+  const float* dy;
+  const float* x;
+  float* dw;
+  int mode;
+  struct APre { int m; bool ok; };
+  struct BPre { int n; bool ok; };
+  __device__ APre a_pre(int m) const { return APre{m, m < M}; }
+  __device__ float a_load(const APre& a, int k) const { return a.ok ? dy[(int64_t)k * M + a.m] : 0.f; }
+  __device__ BPre b_pre(int n) const { return BPre{n, n < N}; }
+  __device__ float b_load(const BPre& b, int k) const { return b.ok ? x[(int64_t)k * N + b.n] : 0.f; }
+  __device__ void store(int m, int n, float v, int) const { emit(dw, (int64_t)m * N + n, v, mode); }
+};
+
+template <class Op>
+void run(Op& op, int splits, hipStream_t st) {
+  igemm_launch<Op, 64, 64, 16, 2, 2>(op, splits, st);
+}
+
+}  // namespace
+
+void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s,
+                bool relu, hipStream_t st) {
+  ConvFwdOp op{s.N * s.P * s.Q, s.K, s.C * s.R * s.S, ConvG(s), x, w, bias, y, relu};
+  run(op, 1, st);
+}
+
+void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s,
+                  const float* relu_mask, bool accumulate, hipStream_t st) {
+  ConvDgradOp op{s.N * s.H * s.W, s.C, s.K * s.R * s.S, ConvG(s), dy, w, dx, relu_mask,
+                 accumulate ? kAccum : kStore};
+  run(op, 1, st);
+}
+
+void conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate,
+                  hipStream_t st) {
+  ConvWgradOp op{s.K, s.C * s.R * s.S, s.N * s.P * s.Q, ConvG(s), dy, x, dw, kAtomic};
+  const int tiles = cdiv(op.M, 64) * cdiv(op.N, 64);
+  const int splits = pick_splits(tiles, op.K, 512, 768);
+  if (splits == 1) {
+    op.mode = accumulate ? kAccum : kStore;
+  } else if (!accumulate) {
+    MX_HIP_CHECK(hipMemsetAsync(dw, 0, sizeof(float) * (size_t)op.M * op.N, st));
+  }
+  run(op, splits, st);
+}
+
+void linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int N, int K,
+                bool relu, hipStream_t st) {
+  LinFwdOp op{M, N, K, x, w, b, y, relu, kStore};
+  const int tiles = cdiv(M, 64) * cdiv(N, 64);
+  int splits = relu ? 1 : pick_splits(tiles, K, 256, 256);
+  if (splits > 1) {
+    op.mode = kAtomic;
+    MX_HIP_CHECK(hipMemsetAsync(y, 0, sizeof(float) * (size_t)M * N, st));
+  }
+  run(op, splits, st);
+}
+
+void linear_dgrad(const float* dy, const float* w, float* dx, int M, int N, int K,
+                  const float* relu_mask, bool accumulate, hipStream_t st) {
+  // GEMM view: M x K(out=Kin) reduction over N(out features)
+  LinDgradOp op{M, K, N, dy, w, dx, relu_mask, accumulate ? kAccum : kStore};
+  run(op, 1, st);
+}
+
+void linear_wgrad(const float* dy, const float* x, float* dw, int M, int N, int K, bool accumulate,
+                  hipStream_t st) {
+  LinWgradOp op{N, K, M, dy, x, dw, kStore};
+  const int tiles = cdiv(N, 64) * cdiv(K, 64);
+  const int splits = pick_splits(tiles, M, 256, 512);
+  if (splits == 1) {
+    op.mode = accumulate ? kAccum : kStore;
+  } else {
+    op.mode = kAtomic;
+    if (!accumulate) MX_HIP_CHECK(hipMemsetAsync(dw, 0, sizeof(float) * (size_t)N * K, st));
+  }
+  run(op, splits, st);
+}
+
+}  // namespace mx

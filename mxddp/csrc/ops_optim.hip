@@ -1,0 +1,91 @@
+// Flat multi-tensor optimizers over one contiguous fp32 parameter buffer.
+// Replace per-parameter torch.optim.SGD (pytorch/distributed_data_parallel.py:94-95)
+// and Keras / Chainer Adam (tensorflow2/mnist_single.py:78, chainer/train_mnist.py:69).
+// The DDP 1/world_size gradient average is folded in as `gscale` (no extra pass).
+#include "common.h"
+#include "ops.h"
+
+namespace mx {
+namespace {
+
+__global__ void sgd_k(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
+                      const float* __restrict__ lr_ptr, float gscale, float mom, float wd, int64_t n, int first) {
+  const float lr = *lr_ptr;
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  float4* b4 = reinterpret_cast<float4*>(buf);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pv = p4[i], gv = g4[i];
+    float gg[4] = {gv.x * gscale + wd * pv.x, gv.y * gscale + wd * pv.y, gv.z * gscale + wd * pv.z,
+                   gv.w * gscale + wd * pv.w};
+    if (mom != 0.f) {
+      float4 bv = first ? make_float4(gg[0], gg[1], gg[2], gg[3]) : b4[i];
+      if (!first) {
+        bv.x = mom * bv.x + gg[0];
+        bv.y = mom * bv.y + gg[1];
+        bv.z = mom * bv.z + gg[2];
+        bv.w = mom * bv.w + gg[3];
+      }
+      b4[i] = bv;
+      gg[0] = bv.x; gg[1] = bv.y; gg[2] = bv.z; gg[3] = bv.w;
+    }
+    pv.x -= lr * gg[0];
+    pv.y -= lr * gg[1];
+    pv.z -= lr * gg[2];
+    pv.w -= lr * gg[3];
+    p4[i] = pv;
+  }
+  for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    float gg = g[i] * gscale + wd * p[i];
+    if (mom != 0.f) {
+      const float b = first ? gg : mom * buf[i] + gg;
+      buf[i] = b;
+      gg = b;
+    }
+    p[i] -= lr * gg;
+  }
+}
+
+__global__ void adam_k(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                       float* __restrict__ v, const float* __restrict__ lr_ptr, const int32_t* __restrict__ step_ptr,
+                       float gscale, float b1, float b2, float eps, float wd, int64_t n) {
+  const float lr = *lr_ptr;
+  const int t = *step_ptr;  // 1-based step count of THIS update
+  const float bc1 = 1.f - powf(b1, (float)t), bc2 = 1.f - powf(b2, (float)t);
+  const float step_size = lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gg = g[i] * gscale + wd * p[i];
+    const float mi = b1 * m[i] + (1.f - b1) * gg;
+    const float vi = b2 * v[i] + (1.f - b2) * gg * gg;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] -= step_size * mi / (sqrtf(vi) / bc2s + eps);
+  }
+}
+
+int grid_for(int64_t n) {
+  int64_t g = (n / 4 + 255) / 256;
+  if (g > 2048) g = 2048;
+  return g < 1 ? 1 : (int)g;
+}
+
+}  // namespace
+
+void sgd_step(float* p, const float* g, float* buf, const float* lr, float gscale, float momentum, float wd,
+              int64_t n, bool first_step, hipStream_t st) {
+  MX_CHECK(((uintptr_t)p % 16 == 0) && ((uintptr_t)g % 16 == 0) && ((uintptr_t)buf % 16 == 0),
+           "sgd_step: buffers must be 16-byte aligned");
+  hipLaunchKernelGGL(sgd_k, dim3(grid_for(n)), dim3(256), 0, st, p, g, buf, lr, gscale, momentum, wd, n,
+                     first_step ? 1 : 0);
+}
+
+void adam_step(float* p, const float* g, float* m, float* v, const float* lr, const int32_t* step, float gscale,
+               float b1, float b2, float eps, float wd, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(adam_k, dim3(grid_for(n * 4)), dim3(256), 0, st, p, g, m, v, lr, step, gscale, b1, b2, eps,
+                     wd, n);
+}
+
+}  // namespace mx

@@ -1,0 +1,66 @@
+// Gradient-bucket reducer: the MI355X-native replacement for torch DDP's C++ Reducer
+// (reached via DistributedDataParallel at pytorch/distributed_data_parallel.py:74).
+//
+//  * gradients live in ONE flat buffer; every parameter's .grad is a view into it, so a
+//    bucket is a contiguous [offset, offset+numel) slice: no copy-in / copy-out;
+//  * buckets are assigned in reverse registration order (the order backward produces
+//    grads) by the Python layer; each bucket counts down as its params become ready;
+//  * a ready bucket is launched strictly in bucket order (all ranks must issue RCCL
+//    collectives in the same order): event recorded on the compute stream, the comm
+//    stream waits on it, then an in-place RCCL all-reduce runs on the comm stream and
+//    overlaps the remaining backward;
+//  * finalize() makes the compute stream wait on the comm stream before the optimizer.
+//  * debug checks: a parameter marked twice in one backward, or a bucket launched
+//    before all of its parameters were marked, raises (race detection).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "comm.h"
+
+namespace mx {
+
+class Reducer {
+ public:
+  struct BucketSpec {
+    size_t offset, numel;
+  };
+  Reducer(Comm* comm, uintptr_t flat_grad, DType dtype, const std::vector<BucketSpec>& buckets,
+          const std::vector<int>& param_bucket, RedOp op, bool timing);
+  ~Reducer();
+
+  void prepare();                                   // start of a backward pass
+  void mark_ready(int param_idx, hipStream_t compute);
+  void mark_bucket_ready(int bucket, hipStream_t compute);  // fused engines: whole bucket at once
+  void finalize(hipStream_t compute);               // launch stragglers; compute waits on comm
+  hipStream_t comm_stream() const { return comm_stream_; }
+  int num_buckets() const { return (int)buckets_.size(); }
+  int launched() const { return next_; }
+  // milliseconds between first bucket launch and comm completion of the last step
+  // (requires timing=true; synchronises on the comm stream's end event).
+  float last_comm_ms();
+  void set_comm(Comm* c) { comm_ = c; }
+
+ private:
+  void launch_ready(hipStream_t compute);
+  struct Bucket {
+    size_t offset, numel;
+    int total, pending;
+    bool ready;
+    hipEvent_t ev;
+  };
+  Comm* comm_;
+  char* flat_;
+  DType dtype_;
+  RedOp op_;
+  std::vector<Bucket> buckets_;
+  std::vector<int> param_bucket_;
+  std::vector<char> marked_;
+  int next_ = 0;
+  hipStream_t comm_stream_ = nullptr;
+  hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
+  bool timing_ = false, timed_ = false;
+};
+
+}  // namespace mx

@@ -1,0 +1,133 @@
+"""Python face of the native fused MNIST-CNN DDP training step (``mxddp._C.MnistEngine``).
+
+One ``FusedMnistTrainer.step()`` = one hipGraph launch that runs: Philox synthetic batch
+(or a caller-provided batch) -> fused forward -> fused backward -> bucketed RCCL
+all-reduce on a side stream (2 buckets, overlapped with the conv backward) -> flat SGD
+with momentum / weight decay / 1/world_size folded in.  Loss and accuracy accumulate on
+device and are read only at log intervals (fixes the two host syncs per step of
+pytorch/distributed_data_parallel.py:135-138).
+
+The parameters are one flat fp32 buffer in MnistCNN ``state_dict`` order, so
+``state_dict()`` is key-for-key the reference-style checkpoint of ``models.MnistCNN``.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import native
+from .models.mnist_cnn import MnistCNN
+
+_LAYOUT = [  # (name, shape) in state_dict order == flat offsets of MnistLayout (mnist_engine.h)
+    ("conv1.weight", (32, 1, 3, 3)), ("conv1.bias", (32,)),
+    ("conv2.weight", (64, 32, 3, 3)), ("conv2.bias", (64,)),
+    ("fc1.weight", (128, 9216)), ("fc1.bias", (128,)),
+    ("fc2.weight", (10, 128)), ("fc2.bias", (10,)),
+]
+
+
+class FusedMnistTrainer:
+    def __init__(self, batch: int = 64, device: torch.device | int = 0, comm=None, seed: int = 1, lr: float = 0.1,
+                 momentum: float = 0.9, weight_decay: float = 1e-4, variant: int = 1, use_graph: bool = True,
+                 init_model: MnistCNN | None = None):
+        C = native()
+        self.C = C
+        self.device = torch.device("cuda", device) if isinstance(device, int) else device
+        self.batch = batch
+        self.comm = comm
+        self.use_graph = use_graph
+        n = C.MNIST_NUM_PARAMS
+        if init_model is None:
+            torch.manual_seed(seed)
+            init_model = MnistCNN()
+        sd = init_model.state_dict()
+        flat = torch.cat([sd[k].detach().reshape(-1).float().cpu() for k, _ in _LAYOUT])
+        assert flat.numel() == n
+        self.params = flat.to(self.device)
+        self.grads = torch.zeros(n, device=self.device)
+        self.mom = torch.zeros(n, device=self.device)
+        self.lr = torch.full((1,), lr, device=self.device)
+        self._lr_host = lr
+        self.metrics = torch.zeros(4, device=self.device)
+        wsb = C.mnist_workspace_bytes(batch)
+        self.workspace = torch.empty(wsb // 4 + 64, dtype=torch.float32, device=self.device)
+        torch.cuda.synchronize(self.device)
+        if comm is not None and comm.world_size > 1:  # DDP ctor semantics: rank 0's weights everywhere
+            st = torch.cuda.current_stream(self.device).cuda_stream
+            comm.broadcast(self.params.data_ptr(), self.params.data_ptr(), n, C.DType.f32, 0, st)
+            torch.cuda.synchronize(self.device)
+        self.eng = C.MnistEngine(batch, self.params.data_ptr(), self.grads.data_ptr(), self.mom.data_ptr(),
+                                 self.workspace.data_ptr(), wsb, comm, seed, momentum, weight_decay,
+                                 self.lr.data_ptr(), self.metrics.data_ptr(), variant)
+        self.stream = torch.cuda.ExternalStream(self.eng.stream, device=self.device)
+        self.steps = 0
+        self.world_size = comm.world_size if comm is not None else 1
+
+    # --------------------------------------------------------------- stepping
+    def step(self, n: int = 1):
+        """Run n training steps (graph replays once captured; first call warms up + captures)."""
+        if self.use_graph and not self.eng.captured:
+            self.eng.step()          # warm-up: lazy RCCL/kernel init outside the capture
+            self.eng.sync()
+            self.eng.capture()
+            n -= 1
+            self.steps += 1
+        if n > 0:
+            self.eng.replay(n)
+            self.steps += n
+
+    def set_batch(self, x: torch.Tensor, y: torch.Tensor):
+        """Use a caller-provided batch instead of the on-device generator (real MNIST)."""
+        self.eng.set_external_batch(True)
+        with torch.cuda.stream(self.stream):
+            self._x_view().copy_(x.reshape(self.batch, 1, 28, 28), non_blocking=True)
+            self._y_view().copy_(y.to(torch.int32), non_blocking=True)
+
+    def _x_view(self):
+        off = (self.eng.x_ptr - self.workspace.data_ptr()) // 4
+        return self.workspace[off:off + self.batch * 784].view(self.batch, 1, 28, 28)
+
+    def _y_view(self):
+        off = (self.eng.y_ptr - self.workspace.data_ptr()) // 4
+        return self.workspace[off:off + self.batch].view(torch.int32)
+
+    def set_lr(self, lr: float):
+        if lr != self._lr_host:
+            with torch.cuda.stream(self.stream):
+                self.lr.fill_(lr)
+            self._lr_host = lr
+
+    def synchronize(self):
+        self.eng.sync()
+
+    def read_metrics(self, reset: bool = True):
+        """(loss_sum, correct) accumulated since the last reset (one host sync)."""
+        self.eng.sync()
+        m = self.metrics[:2].tolist()
+        if reset:
+            with torch.cuda.stream(self.stream):
+                self.metrics.zero_()
+            self.eng.sync()
+        return m[0], m[1]
+
+    # --------------------------------------------------------------- state
+    def state_dict(self) -> dict:
+        self.eng.sync()
+        out, off = {}, 0
+        for name, shape in _LAYOUT:
+            k = 1
+            for s in shape:
+                k *= s
+            out[name] = self.params[off:off + k].view(shape).detach().cpu().clone()
+            off += k
+        return out
+
+    def load_state_dict(self, sd: dict):
+        flat = torch.cat([sd[k].detach().reshape(-1).float().cpu() for k, _ in _LAYOUT])
+        self.eng.sync()
+        self.params.copy_(flat.to(self.device))
+        torch.cuda.synchronize(self.device)
+
+    def to_module(self) -> MnistCNN:
+        m = MnistCNN()
+        m.load_state_dict(self.state_dict())
+        return m

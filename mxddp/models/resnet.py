@@ -1,0 +1,73 @@
+"""ResNet-50 (BASELINE.json config 5 only: not in the reference).  torchvision-style
+topology and parameter names (conv1/bn1/layer1..4/fc, Bottleneck with downsample.0/.1),
+25,557,032 parameters, on mxddp kernels.  ReLU is fused into the BN that precedes it.
+"""
+from __future__ import annotations
+
+import torch.nn as nn
+
+from .. import ops
+from .layers import BatchNorm2d, Conv2d, Linear, MaxPool2d
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: nn.Module | None = None):
+        super().__init__()
+        self.conv1 = Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = BatchNorm2d(planes, fuse_relu=True)
+        self.conv2 = Conv2d(planes, planes, 3, stride, 1, bias=False)
+        self.bn2 = BatchNorm2d(planes, fuse_relu=True)
+        self.conv3 = Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        out = self.bn3(self.conv3(self.bn2(self.conv2(self.bn1(self.conv1(x))))))
+        return ops.relu(out + idt)
+
+
+class ResNet(nn.Module):
+    input_shape = (3, 224, 224)
+
+    def __init__(self, layers=(3, 4, 6, 3), num_classes: int = 1000):
+        super().__init__()
+        self.num_classes = num_classes
+        self.inplanes = 64
+        self.conv1 = Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = BatchNorm2d(64, fuse_relu=True)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = MaxPool2d(3, 2, 1)
+        self.layer1 = self._make(64, layers[0], 1)
+        self.layer2 = self._make(128, layers[1], 2)
+        self.layer3 = self._make(256, layers[2], 2)
+        self.layer4 = self._make(512, layers[3], 2)
+        self.fc = Linear(512 * 4, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+
+    def _make(self, planes, blocks, stride):
+        down = None
+        if stride != 1 or self.inplanes != planes * 4:
+            down = nn.Sequential(Conv2d(self.inplanes, planes * 4, 1, stride, bias=False), BatchNorm2d(planes * 4))
+        layers = [Bottleneck(self.inplanes, planes, stride, down)]
+        self.inplanes = planes * 4
+        layers += [Bottleneck(self.inplanes, planes) for _ in range(1, blocks)]
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.maxpool(self.bn1(self.conv1(x)))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = ops.avg_pool2d(x, (x.shape[2], x.shape[3]))
+        return self.fc(x.flatten(1))
+
+
+def resnet50(num_classes: int = 1000) -> ResNet:
+    return ResNet((3, 4, 6, 3), num_classes)

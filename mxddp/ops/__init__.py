@@ -1,0 +1,368 @@
+"""Differentiable ops backed by the gfx950 HIP kernels in ``mxddp/csrc``.
+
+Every op has two implementations selected by the *device of its input* only:
+
+* CUDA (= ROCm HIP) tensors -> the native kernels (``mxddp._C``).  There is no silent
+  fallback: if the extension cannot be loaded the op raises.
+* CPU tensors -> plain PyTorch reference math (BASELINE config 1, CPU single process,
+  and the fp32 oracle that the GPU numerics tests compare against).
+
+Reference call sites replaced (cuDNN/cuBLAS/ATen via torch.nn in the reference):
+conv / BN / pool / linear in ``pytorch/model.py:28-33,62-77``, CrossEntropyLoss in
+``pytorch/single_gpu.py:70``, Keras layers in ``tensorflow2/mnist_single.py:16-26``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .. import native
+
+__all__ = [
+    "conv2d", "linear", "relu", "max_pool2d", "avg_pool2d", "batch_norm", "cross_entropy",
+    "shortcut_pad_add", "stream_of",
+]
+
+
+def stream_of(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _check(t: torch.Tensor, name: str):
+    if t.dtype != torch.float32:
+        raise TypeError(f"mxddp native op: {name} must be float32, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"mxddp native op: {name} must be contiguous")
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
+
+
+# --------------------------------------------------------------------------- conv2d
+class _Conv2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, padding, dilation, relu):
+        C = native()
+        x = x.contiguous()
+        _check(x, "input"); _check(w, "weight")
+        N, Cin, H, W = x.shape
+        K, Cw, R, S = w.shape
+        if Cw != Cin:
+            raise ValueError(f"conv2d: weight expects {Cw} input channels, got {Cin}")
+        sh, sw = stride; ph, pw = padding; dh, dw = dilation
+        P = (H + 2 * ph - dh * (R - 1) - 1) // sh + 1
+        Q = (W + 2 * pw - dw * (S - 1) - 1) // sw + 1
+        y = torch.empty((N, K, P, Q), device=x.device, dtype=x.dtype)
+        st = stream_of(x)
+        C.conv2d_fwd(x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph, pw,
+                     dh, dw, bool(relu), st)
+        ctx.geom = (N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw, P, Q)
+        ctx.relu = relu
+        ctx.has_bias = b is not None
+        ctx.save_for_backward(x, w, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        x, w, y = ctx.saved_tensors
+        N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw, P, Q = ctx.geom
+        dy = dy.contiguous()
+        st = stream_of(dy)
+        if ctx.relu:
+            g = torch.empty_like(dy)
+            C.relu_bwd(dy.data_ptr(), y.data_ptr(), g.data_ptr(), dy.numel(), st)
+            dy = g
+        dx = dw_ = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            C.conv2d_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph, pw,
+                           dh, dw, 0, False, st)
+        if ctx.needs_input_grad[1]:
+            dw_ = torch.empty_like(w)
+            C.conv2d_wgrad(dy.data_ptr(), x.data_ptr(), dw_.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph, pw,
+                           dh, dw, False, st)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = torch.empty((K,), device=dy.device, dtype=dy.dtype)
+            C.bias_grad(dy.data_ptr(), db.data_ptr(), N, K, P * Q, False, st)
+        return dx, dw_, db, None, None, None, None
+
+
+def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, relu=False):
+    stride, padding, dilation = _pair(stride), _pair(padding), _pair(dilation)
+    if x.is_cuda:
+        return _Conv2d.apply(x, w, b, stride, padding, dilation, relu)
+    y = F.conv2d(x, w, b, stride, padding, dilation)
+    return F.relu(y) if relu else y
+
+
+# --------------------------------------------------------------------------- linear
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, relu):
+        C = native()
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        _check(x2, "input"); _check(w, "weight")
+        M, K = x2.shape
+        N = w.shape[0]
+        y = torch.empty((M, N), device=x.device, dtype=x.dtype)
+        st = stream_of(x)
+        C.linear_fwd(x2.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), M, N, K, False, st)
+        if relu:
+            C.relu_fwd(y.data_ptr(), y.data_ptr(), y.numel(), st)
+        ctx.relu = relu
+        ctx.has_bias = b is not None
+        ctx.in_shape = x.shape
+        ctx.save_for_backward(x2, w, y if relu else None)
+        return y.reshape(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        x2, w, y = ctx.saved_tensors
+        M, K = x2.shape
+        N = w.shape[0]
+        dy = dy.reshape(M, N).contiguous()
+        st = stream_of(dy)
+        if ctx.relu:
+            g = torch.empty_like(dy)
+            C.relu_bwd(dy.data_ptr(), y.data_ptr(), g.data_ptr(), dy.numel(), st)
+            dy = g
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((M, K), device=dy.device, dtype=dy.dtype)
+            C.linear_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), M, N, K, 0, False, st)
+            dx = dx.reshape(ctx.in_shape)
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty_like(w)
+            C.linear_wgrad(dy.data_ptr(), x2.data_ptr(), dw.data_ptr(), M, N, K, False, st)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = torch.empty((N,), device=dy.device, dtype=dy.dtype)
+            C.bias_grad(dy.data_ptr(), db.data_ptr(), M, N, 1, False, st)
+        return dx, dw, db, None
+
+
+def linear(x, w, b=None, relu=False):
+    if x.is_cuda:
+        return _Linear.apply(x, w, b, relu)
+    y = F.linear(x, w, b)
+    return F.relu(y) if relu else y
+
+
+# --------------------------------------------------------------------------- relu
+class _Relu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        native().relu_fwd(x.data_ptr(), y.data_ptr(), x.numel(), stream_of(x))
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        native().relu_bwd(dy.data_ptr(), y.data_ptr(), dx.data_ptr(), dy.numel(), stream_of(dy))
+        return dx
+
+
+def relu(x):
+    return _Relu.apply(x) if x.is_cuda else F.relu(x)
+
+
+# --------------------------------------------------------------------------- pooling
+def _pool_out(H, k, s, p, ceil):
+    if ceil:
+        o = -(-(H + 2 * p - k) // s) + 1
+        if (o - 1) * s >= H + p:  # last window must start inside the (left-padded) input
+            o -= 1
+    else:
+        o = (H + 2 * p - k) // s + 1
+    return o
+
+
+class _MaxPool2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p, ceil):
+        x = x.contiguous()
+        _check(x, "input")
+        N, Cc, H, W = x.shape
+        P, Q = _pool_out(H, k[0], s[0], p[0], ceil), _pool_out(W, k[1], s[1], p[1], ceil)
+        y = torch.empty((N, Cc, P, Q), device=x.device, dtype=x.dtype)
+        idx = torch.empty((N, Cc, P, Q), device=x.device, dtype=torch.int32)
+        native().maxpool2d_fwd(x.data_ptr(), y.data_ptr(), idx.data_ptr(), N, Cc, H, W, k[0], k[1], s[0], s[1],
+                               p[0], p[1], P, Q, stream_of(x))
+        ctx.save_for_backward(idx)
+        ctx.shape = (N, Cc, H, W, P, Q)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        N, Cc, H, W, P, Q = ctx.shape
+        dy = dy.contiguous()
+        dx = torch.empty((N, Cc, H, W), device=dy.device, dtype=dy.dtype)
+        native().maxpool2d_bwd(dy.data_ptr(), idx.data_ptr(), dx.data_ptr(), N, Cc, H, W, P, Q, stream_of(dy))
+        return dx, None, None, None, None
+
+
+def max_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False):
+    k = _pair(kernel_size)
+    s = _pair(stride if stride is not None else kernel_size)
+    p = _pair(padding)
+    if x.is_cuda:
+        return _MaxPool2d.apply(x, k, s, p, ceil_mode)
+    return F.max_pool2d(x, k, s, p, ceil_mode=ceil_mode)
+
+
+class _AvgPool2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p, ceil):
+        x = x.contiguous()
+        _check(x, "input")
+        N, Cc, H, W = x.shape
+        P, Q = _pool_out(H, k[0], s[0], p[0], ceil), _pool_out(W, k[1], s[1], p[1], ceil)
+        y = torch.empty((N, Cc, P, Q), device=x.device, dtype=x.dtype)
+        native().avgpool2d_fwd(x.data_ptr(), y.data_ptr(), N, Cc, H, W, k[0], k[1], s[0], s[1], p[0], p[1], P, Q,
+                               stream_of(x))
+        ctx.args = (N, Cc, H, W, k, s, p, P, Q)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, Cc, H, W, k, s, p, P, Q = ctx.args
+        dy = dy.contiguous()
+        dx = torch.empty((N, Cc, H, W), device=dy.device, dtype=dy.dtype)
+        native().avgpool2d_bwd(dy.data_ptr(), dx.data_ptr(), N, Cc, H, W, k[0], k[1], s[0], s[1], p[0], p[1], P, Q,
+                               stream_of(dy))
+        return dx, None, None, None, None
+
+
+def avg_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False):
+    k = _pair(kernel_size)
+    s = _pair(stride if stride is not None else kernel_size)
+    p = _pair(padding)
+    if x.is_cuda:
+        return _AvgPool2d.apply(x, k, s, p, ceil_mode)
+    return F.avg_pool2d(x, k, s, p, ceil_mode=ceil_mode)
+
+
+# --------------------------------------------------------------------------- batch norm
+class _BatchNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, running_mean, running_var, training, momentum, eps, relu):
+        C = native()
+        x = x.contiguous()
+        _check(x, "input")
+        N, Cc = x.shape[0], x.shape[1]
+        HW = x.numel() // (N * Cc)
+        y = torch.empty_like(x)
+        st = stream_of(x)
+        if training:
+            mean = torch.empty((Cc,), device=x.device, dtype=torch.float32)
+            invstd = torch.empty_like(mean)
+            C.bn_fwd_train(x.data_ptr(), _p(gamma), _p(beta), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                           _p(running_mean), _p(running_var), N, Cc, HW, float(momentum), float(eps), bool(relu), st)
+        else:
+            mean = running_mean
+            invstd = (running_var + eps).rsqrt()
+            C.bn_fwd_eval(x.data_ptr(), _p(gamma), _p(beta), y.data_ptr(), running_mean.data_ptr(),
+                          running_var.data_ptr(), N, Cc, HW, float(eps), bool(relu), st)
+        ctx.save_for_backward(x, gamma, mean, invstd, y if relu else None)
+        ctx.dims = (N, Cc, HW)
+        ctx.has_affine = gamma is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, mean, invstd, y = ctx.saved_tensors
+        N, Cc, HW = ctx.dims
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        dg = torch.empty((Cc,), device=x.device) if ctx.has_affine else None
+        db = torch.empty((Cc,), device=x.device) if ctx.has_affine else None
+        native().bn_bwd(dy.data_ptr(), x.data_ptr(), _p(y), _p(gamma), mean.data_ptr(), invstd.data_ptr(),
+                        dx.data_ptr(), _p(dg), _p(db), N, Cc, HW, False, stream_of(dy))
+        return dx, dg, db, None, None, None, None, None, None
+
+
+def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum=0.1, eps=1e-5, relu=False):
+    if x.is_cuda:
+        return _BatchNorm.apply(x, gamma, beta, running_mean, running_var, training, momentum, eps, relu)
+    y = F.batch_norm(x, running_mean, running_var, gamma, beta, training, momentum, eps)
+    return F.relu(y) if relu else y
+
+
+# --------------------------------------------------------------------------- loss
+class _CrossEntropy(torch.autograd.Function):
+    """Fused log_softmax + NLL (mean).  Forward computes loss AND dlogits in one kernel."""
+
+    @staticmethod
+    def forward(ctx, logits, target):
+        C = native()
+        logits = logits.contiguous()
+        _check(logits, "logits")
+        B, K = logits.shape
+        tgt = target.to(torch.int32).contiguous()
+        acc = torch.zeros(2, device=logits.device, dtype=torch.float32)
+        dl = torch.empty_like(logits)
+        C.xent_fwd_bwd(logits.data_ptr(), tgt.data_ptr(), 0, dl.data_ptr(), acc.data_ptr(), acc.data_ptr() + 4,
+                       B, K, 1.0 / B, stream_of(logits))
+        ctx.save_for_backward(dl)
+        ctx.mark_non_differentiable(acc)
+        return acc[0] / B, acc[1]
+
+    @staticmethod
+    def backward(ctx, dloss, _dcorrect):
+        (dl,) = ctx.saved_tensors
+        return dl * dloss, None
+
+
+def cross_entropy(logits, target, return_correct=False):
+    """Mean cross-entropy = NLL(log_softmax(logits)); optionally also #correct (on device)."""
+    if logits.is_cuda:
+        loss, correct = _CrossEntropy.apply(logits, target)
+    else:
+        loss = F.cross_entropy(logits, target)
+        correct = (logits.argmax(1) == target).sum().to(torch.float32)
+    return (loss, correct) if return_correct else loss
+
+
+# --------------------------------------------------------------------------- PyramidNet shortcut
+class _ShortcutAdd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, out, x, stride):
+        out = out.contiguous()
+        x = x.contiguous()
+        N, Cin, H, W = x.shape
+        _, Cout, P, Q = out.shape
+        y = out.clone()
+        native().shortcut_pad_add(x.data_ptr(), y.data_ptr(), N, Cin, H, W, Cout, P, Q, stride, stream_of(x))
+        ctx.dims = (N, Cin, H, W, Cout, P, Q, stride)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, Cin, H, W, Cout, P, Q, stride = ctx.dims
+        dy = dy.contiguous()
+        dx = torch.empty((N, Cin, H, W), device=dy.device, dtype=dy.dtype)
+        native().shortcut_pad_add_bwd(dy.data_ptr(), dx.data_ptr(), N, Cin, H, W, Cout, P, Q, stride, False,
+                                      stream_of(dy))
+        return dy, dx, None
+
+
+def shortcut_pad_add(out, x, stride):
+    """out + AvgPool2d(2,2,ceil)(F.pad(x, channels -> out.C)) (pytorch/model.py:17-21,49)."""
+    if out.is_cuda:
+        return _ShortcutAdd.apply(out, x, stride)
+    sc = F.pad(x, (0, 0, 0, 0, 0, out.shape[1] - x.shape[1]))
+    if stride == 2:
+        sc = F.avg_pool2d(sc, 2, 2, ceil_mode=True)
+    return out + sc

@@ -1,0 +1,141 @@
+"""Process-group bootstrap + the mxddp RCCL communicator.
+
+Rendezvous (reference: ``dist.init_process_group(backend, init_method, world_size, rank)``
+at pytorch/distributed_data_parallel.py:61-62):
+
+* the torchrun env contract (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT)
+  when set, otherwise the reference's explicit ``--init-method tcp://h:p --rank r
+  --world-size w`` manual mode;
+* the torch c10d ``TCPStore`` created by ``init_process_group`` is the control plane
+  (barriers, object exchange, the ncclUniqueId hand-off);
+* the data plane on GPU is OUR RCCL communicator (``mxddp._C.Comm``): rank 0 creates the
+  ncclUniqueId, publishes it in the store, every rank calls ncclCommInitRank.  Collectives
+  are issued from C++ on streams we own (reducer side stream, graph capture).
+* on CPU the data plane is gloo through torch.distributed.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from .. import native
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    local_world_size: int = 1
+    backend: str = "gloo"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+_INFO: DistInfo | None = None
+_COMM = None
+
+
+def env_dist() -> dict:
+    """torchrun-style env contract (empty dict when not launched by a spawner)."""
+    if "RANK" in os.environ and "WORLD_SIZE" in os.environ:
+        return {
+            "rank": int(os.environ["RANK"]),
+            "world_size": int(os.environ["WORLD_SIZE"]),
+            "local_rank": int(os.environ.get("LOCAL_RANK", os.environ["RANK"])),
+            "local_world_size": int(os.environ.get("LOCAL_WORLD_SIZE", os.environ["WORLD_SIZE"])),
+        }
+    return {}
+
+
+def init_distributed(backend: str | None = None, init_method: str | None = None, rank: int | None = None,
+                     world_size: int | None = None, local_rank: int | None = None, use_gpu: bool | None = None,
+                     timeout_s: float = 1800.0) -> DistInfo:
+    """Initialise the process group (idempotent) and pick this rank's device."""
+    global _INFO
+    if _INFO is not None:
+        return _INFO
+    env = env_dist()
+    rank = env.get("rank", rank if rank is not None else 0)
+    world_size = env.get("world_size", world_size if world_size is not None else 1)
+    local_rank = env.get("local_rank", local_rank if local_rank is not None else rank)
+    lws = env.get("local_world_size", world_size)
+    if use_gpu is None:
+        use_gpu = torch.cuda.is_available()
+    if backend is None:
+        backend = "nccl" if use_gpu else "gloo"
+    if backend == "nccl" and not use_gpu:
+        raise RuntimeError("--dist-backend nccl (RCCL) needs a GPU; use gloo for CPU runs")
+    if use_gpu:
+        ndev = torch.cuda.device_count()
+        dev_index = local_rank % max(ndev, 1)
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
+    else:
+        device = torch.device("cpu")
+    if world_size > 1 and not dist.is_initialized():
+        if init_method is None and "MASTER_ADDR" in os.environ:
+            init_method = "env://"
+        # control plane always gloo (TCPStore + CPU collectives); RCCL data plane is ours.
+        dist.init_process_group("gloo", init_method=init_method, world_size=world_size, rank=rank,
+                                timeout=datetime.timedelta(seconds=timeout_s))
+    _INFO = DistInfo(rank, world_size, local_rank, lws, backend, device)
+    return _INFO
+
+
+def info() -> DistInfo:
+    return _INFO if _INFO is not None else DistInfo()
+
+
+def rccl_comm():
+    """This rank's RCCL communicator (created on first use; None when world_size == 1)."""
+    global _COMM
+    inf = info()
+    if inf.world_size == 1 or inf.device.type != "cuda":
+        return None
+    if _COMM is None:
+        C = native()
+        store = dist.distributed_c10d._get_default_store()
+        key = "mxddp/rccl_uid/0"
+        if inf.rank == 0:
+            store.set(key, C.Comm.new_unique_id())
+        uid = store.get(key)
+        _COMM = C.Comm(uid, inf.rank, inf.world_size, inf.device.index)
+    return _COMM
+
+
+def barrier():
+    if dist.is_initialized():
+        dist.barrier()
+
+
+def all_reduce_max(value: float) -> float:
+    """Host-side max over ranks (used for timing: the bench takes the slowest rank)."""
+    if not dist.is_initialized():
+        return value
+    t = torch.tensor([value], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_reduce_sum(values):
+    if not dist.is_initialized():
+        return list(values)
+    t = torch.tensor(list(values), dtype=torch.float64)
+    dist.all_reduce(t)
+    return t.tolist()
+
+
+def shutdown():
+    global _INFO, _COMM
+    _COMM = None
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    _INFO = None

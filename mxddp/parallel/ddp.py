@@ -1,0 +1,186 @@
+"""DistributedDataParallel on the mxddp bucket reducer.
+
+Same contract as ``torch.nn.parallel.DistributedDataParallel`` as the reference uses it
+(pytorch/distributed_data_parallel.py:74; semantics verified in SURVEY §2.2):
+
+1. rank 0's parameters (and buffers) are broadcast at wrap time;
+2. gradients are all-reduced and AVERAGED over ranks every backward, bucketed in reverse
+   parameter order (first bucket 1 MB, then 25 MB caps), launched asynchronously as each
+   bucket fills so communication overlaps the rest of backward;
+3. floating buffers (BN running stats) are broadcast from rank 0 before every forward
+   (``broadcast_buffers=True``);
+4. ``.module`` is the wrapped model, so ``ddp.module.state_dict()`` has no ``module.``
+   prefix (checkpoint layout, pytorch/distributed_data_parallel.py:109-113).
+
+GPU: gradients live in one flat buffer (mxddp.parallel.flat); each bucket is an in-place
+RCCL all-reduce on the reducer's side HIP stream (C++ ``mxddp._C.Reducer``), fenced by
+events.  CPU: the same bucketing over gloo with async work handles.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .. import native
+from . import comm as _comm
+from .flat import FlatParams, flatten_buffers
+
+
+def assign_buckets(numels: list[int], offsets: list[int], total: int, bucket_cap_mb: float = 25.0,
+                   first_bucket_cap_mb: float = 1.0, elem_size: int = 4):
+    """Greedy reverse-order bucketing (DDP's policy).  Returns (buckets, param_bucket) with
+    buckets as contiguous (offset, numel) slices of the flat buffer, bucket 0 = the LAST
+    parameters (the first gradients produced by backward)."""
+    buckets: list[tuple[int, int]] = []
+    param_bucket = [0] * len(numels)
+    cap = first_bucket_cap_mb * 1024 * 1024
+    cur, cur_bytes, end = [], 0, total
+    for i in reversed(range(len(numels))):
+        cur.append(i)
+        cur_bytes += numels[i] * elem_size
+        if cur_bytes >= cap:
+            start = offsets[cur[-1]]
+            buckets.append((start, end - start))
+            for j in cur:
+                param_bucket[j] = len(buckets) - 1
+            end, cur, cur_bytes = start, [], 0
+            cap = bucket_cap_mb * 1024 * 1024
+    if cur:
+        start = offsets[cur[-1]]
+        buckets.append((start, end - start))
+        for j in cur:
+            param_bucket[j] = len(buckets) - 1
+    return buckets, param_bucket
+
+
+class DistributedDataParallel(nn.Module):
+    def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers: bool = True,
+                 bucket_cap_mb: float = 25.0, first_bucket_cap_mb: float = 1.0, average: bool = True,
+                 timing: bool = False):
+        super().__init__()
+        self.module = module
+        inf = _comm.info()
+        self.world_size, self.rank = inf.world_size, inf.rank
+        self.device = next(module.parameters()).device
+        self.flat = FlatParams(module, self.device)
+        self.flat_buffers = flatten_buffers(module, self.device) if broadcast_buffers else None
+        self.broadcast_buffers = broadcast_buffers and self.flat_buffers is not None
+        numels = [p.numel() for p in self.flat.params]
+        self.buckets, self.param_bucket = assign_buckets(numels, self.flat.offsets, self.flat.numel, bucket_cap_mb,
+                                                         first_bucket_cap_mb)
+        self.average = average
+        self._comm = _comm.rccl_comm() if self.device.type == "cuda" else None
+        self._sync_params()
+        if self.device.type == "cuda":
+            C = native()
+            self.reducer = C.Reducer(self._comm, self.flat.grad.data_ptr(), C.DType.f32, self.buckets,
+                                     self.param_bucket, C.RedOp.avg if average else C.RedOp.sum, timing)
+        else:
+            self.reducer = _GlooReducer(self.flat.grad, self.buckets, self.param_bucket, average, self.world_size)
+        self._queued = False
+        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(self.flat.params)]
+
+    # ------------------------------------------------------------------ sync helpers
+    def _broadcast(self, t: torch.Tensor):
+        if self.world_size == 1:
+            return
+        if self._comm is not None:
+            C = native()
+            self._comm.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), C.DType.f32, 0,
+                                 torch.cuda.current_stream(self.device).cuda_stream)
+        else:
+            dist.broadcast(t, 0)
+
+    def _sync_params(self):
+        with torch.no_grad():
+            self._broadcast(self.flat.data)
+            if self.flat_buffers is not None:
+                self._broadcast(self.flat_buffers)
+
+    # ------------------------------------------------------------------ hooks
+    def _make_hook(self, i: int):
+        def hook(p):
+            if not self._queued:
+                self._queued = True
+                torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+            st = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
+            self.reducer.mark_ready(i, st)
+        return hook
+
+    def _finalize(self):
+        st = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
+        self.reducer.finalize(st)
+        self._queued = False
+
+    def forward(self, *args, **kwargs):
+        self.flat.attach_grads()
+        if self.broadcast_buffers and self.world_size > 1 and self.module.training:
+            with torch.no_grad():
+                self._broadcast(self.flat_buffers)
+        if torch.is_grad_enabled():
+            self.reducer.prepare()
+        return self.module(*args, **kwargs)
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.flat.zero_grad()
+
+    @property
+    def flat_params(self) -> FlatParams:
+        return self.flat
+
+
+class _GlooReducer:
+    """CPU twin of mxddp._C.Reducer: contiguous flat-buffer buckets, async gloo all-reduce
+    launched in bucket order as buckets fill, joined in finalize()."""
+
+    def __init__(self, flat_grad, buckets, param_bucket, average, world_size):
+        self.flat, self.buckets, self.param_bucket = flat_grad, buckets, param_bucket
+        self.average, self.ws = average, world_size
+        self.total = [0] * len(buckets)
+        for b in param_bucket:
+            self.total[b] += 1
+        self.prepare()
+
+    def prepare(self):
+        self.pending = list(self.total)
+        self.ready = [False] * len(self.buckets)
+        self.marked = set()
+        self.next = 0
+        self.works = []
+
+    def mark_ready(self, p, _stream=0):
+        if p in self.marked:
+            raise RuntimeError("parameter marked ready twice in one backward pass")
+        self.marked.add(p)
+        b = self.param_bucket[p]
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            self.ready[b] = True
+            self._launch()
+
+    def mark_bucket_ready(self, b, _stream=0):
+        self.pending[b] = 0
+        self.ready[b] = True
+        self._launch()
+
+    def _launch(self):
+        while self.next < len(self.buckets) and self.ready[self.next]:
+            off, n = self.buckets[self.next]
+            if self.ws > 1:
+                self.works.append((off, n, dist.all_reduce(self.flat[off:off + n], async_op=True)))
+            self.next += 1
+
+    def finalize(self, _stream=0):
+        for i in range(len(self.buckets)):
+            self.ready[i] = True
+        self._launch()
+        for off, n, w in self.works:
+            w.wait()
+            if self.average:
+                self.flat[off:off + n].div_(self.ws)
+        self.works = []
+
+    @property
+    def num_buckets(self):
+        return len(self.buckets)

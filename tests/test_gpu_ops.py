@@ -1,0 +1,169 @@
+"""Numerics of every HIP kernel vs a plain PyTorch fp32 reference of the same op (CPU).
+
+Asymmetric random operands everywhere (a symmetric operand hides a row/col swap,
+cdna_hip_programming.md §3), and shapes that are not tile multiples.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from mxddp import ops  # noqa: E402
+
+CONV_CASES = [
+    # N, C, H, W, K, R, S, stride, pad
+    (4, 1, 28, 28, 32, 3, 3, 1, 0),      # mnist conv1
+    (3, 32, 26, 26, 64, 3, 3, 1, 0),     # mnist conv2
+    (2, 21, 16, 16, 26, 3, 3, 1, 1),     # pyramidnet-like odd channels
+    (2, 101, 32, 32, 106, 3, 3, 2, 1),   # pyramidnet stride-2 entry
+    (2, 3, 33, 31, 17, 7, 7, 2, 3),      # resnet stem-like, odd spatial
+    (2, 64, 14, 14, 40, 1, 1, 1, 0),     # 1x1
+]
+
+
+def _rel(a, b):
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("relu", [False, True])
+def test_conv2d_fwd_bwd(cuda, case, relu):
+    N, C, H, W, K, R, S, st, pd = case
+    torch.manual_seed(0)
+    x = torch.randn(N, C, H, W)
+    w = torch.randn(K, C, R, S) * 0.1
+    b = torch.randn(K)
+    xr, wr, br = (t.clone().requires_grad_() for t in (x, w, b))
+    yr = F.conv2d(xr, wr, br, st, pd)
+    if relu:
+        yr = F.relu(yr)
+    gy = torch.randn_like(yr)
+    yr.backward(gy)
+    xg, wg, bg = (t.to(cuda).requires_grad_() for t in (x, w, b))
+    y = ops.conv2d(xg, wg, bg, st, pd, relu=relu)
+    y.backward(gy.to(cuda))
+    torch.cuda.synchronize()
+    assert _rel(y.cpu(), yr.detach()) < 1e-4
+    assert _rel(xg.grad.cpu(), xr.grad) < 1e-4
+    assert _rel(wg.grad.cpu(), wr.grad) < 1e-4
+    assert _rel(bg.grad.cpu(), br.grad) < 1e-4
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 128, 9216), (64, 10, 128), (100, 1000, 784), (7, 33, 65)])
+def test_linear_fwd_bwd(cuda, M, N, K):
+    torch.manual_seed(1)
+    x, w, b = torch.randn(M, K), torch.randn(N, K) * 0.05, torch.randn(N)
+    xr, wr, br = (t.clone().requires_grad_() for t in (x, w, b))
+    yr = F.relu(F.linear(xr, wr, br))
+    gy = torch.randn_like(yr)
+    yr.backward(gy)
+    xg, wg, bg = (t.to(cuda).requires_grad_() for t in (x, w, b))
+    y = ops.linear(xg, wg, bg, relu=True)
+    y.backward(gy.to(cuda))
+    torch.cuda.synchronize()
+    assert _rel(y.cpu(), yr.detach()) < 1e-4
+    assert _rel(xg.grad.cpu(), xr.grad) < 1e-4
+    assert _rel(wg.grad.cpu(), wr.grad) < 1e-4
+    assert _rel(bg.grad.cpu(), br.grad) < 1e-4
+
+
+@pytest.mark.parametrize("k,s,p,ceil", [(2, 2, 0, False), (3, 2, 1, False), (2, 2, 0, True)])
+def test_pools(cuda, k, s, p, ceil):
+    torch.manual_seed(2)
+    x = torch.randn(2, 5, 13, 11)
+    for fn_ref, fn in ((F.max_pool2d, ops.max_pool2d), (F.avg_pool2d, ops.avg_pool2d)):
+        xr = x.clone().requires_grad_()
+        yr = fn_ref(xr, k, s, p, ceil_mode=ceil)
+        gy = torch.randn_like(yr)
+        yr.backward(gy)
+        xg = x.to(cuda).requires_grad_()
+        y = fn(xg, k, s, p, ceil_mode=ceil)
+        y.backward(gy.to(cuda))
+        assert _rel(y.detach().cpu(), yr.detach()) < 1e-5
+        assert _rel(xg.grad.cpu(), xr.grad) < 1e-5
+
+
+def test_cross_entropy(cuda):
+    torch.manual_seed(3)
+    logits = torch.randn(64, 10) * 3
+    y = torch.randint(0, 10, (64,))
+    lr = logits.clone().requires_grad_()
+    ref = F.cross_entropy(lr, y)
+    ref.backward()
+    lg = logits.to(cuda).requires_grad_()
+    loss, correct = ops.cross_entropy(lg, y.to(cuda), return_correct=True)
+    loss.backward()
+    assert abs(loss.item() - ref.item()) < 1e-5
+    assert correct.item() == (logits.argmax(1) == y).sum().item()
+    assert _rel(lg.grad.cpu(), lr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("relu", [False, True])
+def test_batchnorm(cuda, relu):
+    torch.manual_seed(4)
+    x = torch.randn(8, 21, 9, 7) * 2 + 0.5
+    g, b = torch.rand(21) + 0.5, torch.randn(21)
+    rm, rv = torch.zeros(21), torch.ones(21)
+    xr, gr, br = (t.clone().requires_grad_() for t in (x, g, b))
+    yr = F.batch_norm(xr, rm, rv, gr, br, True, 0.1, 1e-5)
+    if relu:
+        yr = F.relu(yr)
+    gy = torch.randn_like(yr)
+    yr.backward(gy)
+    rmg, rvg = torch.zeros(21, device=cuda), torch.ones(21, device=cuda)
+    xg, gg, bg = (t.to(cuda).requires_grad_() for t in (x, g, b))
+    y = ops.batch_norm(xg, gg, bg, rmg, rvg, True, 0.1, 1e-5, relu=relu)
+    y.backward(gy.to(cuda))
+    assert _rel(y.detach().cpu(), yr.detach()) < 1e-4
+    assert _rel(xg.grad.cpu(), xr.grad) < 1e-4
+    assert _rel(gg.grad.cpu(), gr.grad) < 1e-4
+    assert _rel(bg.grad.cpu(), br.grad) < 1e-4
+    assert _rel(rmg.cpu(), rm) < 1e-5 and _rel(rvg.cpu(), rv) < 1e-5
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_shortcut(cuda, stride):
+    torch.manual_seed(5)
+    x = torch.randn(2, 21, 9, 9)
+    P = 9 if stride == 1 else 5
+    out = torch.randn(2, 26, P, P)
+    xr, orr = x.clone().requires_grad_(), out.clone().requires_grad_()
+    yr = ops.shortcut_pad_add(orr, xr, stride)  # CPU reference path = F.pad + avg_pool
+    gy = torch.randn_like(yr)
+    yr.backward(gy)
+    xg, og = x.to(cuda).requires_grad_(), out.to(cuda).requires_grad_()
+    y = ops.shortcut_pad_add(og, xg, stride)
+    y.backward(gy.to(cuda))
+    assert _rel(y.detach().cpu(), yr.detach()) < 1e-5
+    assert _rel(xg.grad.cpu(), xr.grad) < 1e-5
+    assert _rel(og.grad.cpu(), orr.grad) < 1e-5
+
+
+def test_sgd_adam_flat(cuda):
+    import torch.nn as nn
+
+    from mxddp.optim import SGD, Adam
+    from mxddp.parallel.flat import FlatParams
+
+    for Opt, ref_cls, kw in ((SGD, torch.optim.SGD, dict(lr=0.1, momentum=0.9, weight_decay=1e-4)),
+                             (Adam, torch.optim.Adam, dict(lr=1e-3, weight_decay=0.0))):
+        torch.manual_seed(6)
+        m_ref = nn.Linear(37, 19)
+        m = nn.Linear(37, 19)
+        m.load_state_dict(m_ref.state_dict())
+        m = m.to(cuda)
+        flat = FlatParams(m)
+        opt = Opt(flat, **kw)
+        ref = ref_cls(m_ref.parameters(), **kw)
+        for step in range(3):
+            gs = [torch.randn_like(p) for p in m_ref.parameters()]
+            for p, g in zip(m_ref.parameters(), gs):
+                p.grad = g.clone()
+            for p, g in zip(m.parameters(), gs):
+                p.grad.copy_(g)
+            ref.step()
+            opt.step()
+        torch.cuda.synchronize()
+        for p, q in zip(m.parameters(), m_ref.parameters()):
+            assert _rel(p.detach().cpu(), q.detach()) < 1e-5, Opt.__name__
