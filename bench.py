@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--variant", type=int, default=1, help="fused kernel variant (0 = generic igemm)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--lr", type=float, default=0.01, help="SGD lr (momentum 0.9, wd 1e-4 as the reference)")
     return ap.parse_args()
 
 
@@ -60,7 +61,7 @@ def main():
     if a.impl == "fused":
         from mxddp.engine import FusedMnistTrainer
 
-        tr = FusedMnistTrainer(batch=B, device=dev, comm=comm, seed=a.seed, variant=a.variant,
+        tr = FusedMnistTrainer(batch=B, device=dev, comm=comm, seed=a.seed, variant=a.variant, lr=a.lr,
                                use_graph=not a.no_graph)
         run = tr.step
     else:

@@ -20,6 +20,7 @@ struct MnistFused {
   float* dp;       // [B,9216] grad wrt pooled activation
   float* scratch;  // packed weights + split-K partials
   float* metrics;  // [0] loss sum, [1] correct count (accumulated on device)
+  int32_t* counter;  // synthetic-data batch counter (bumped by F1), may be null
 };
 
 size_t mnist_fused_scratch_floats(int B);
@@ -27,6 +28,5 @@ void mnist_fused_forward(const MnistFused& f, hipStream_t st);
 void mnist_fused_head(const MnistFused& f, hipStream_t st);
 void mnist_fused_fc1_bwd(const MnistFused& f, hipStream_t st);
 void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st);
-void mnist_fused_post_step(const MnistFused& f, hipStream_t st);
 
 }  // namespace mx

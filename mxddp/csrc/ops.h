@@ -99,7 +99,7 @@ void adam_step(float* p, const float* g, float* m, float* v, const float* lr, co
 // Class-conditional synthetic images: x = 0.5*template[y] + 0.5*noise, y ~ U{0..C-1}.
 // Deterministic in (seed, counter[0]); counter is incremented on device after each batch.
 void synth_batch(float* x, int32_t* y, const float* templates, int B, int D, int C, uint64_t seed,
-                 int32_t* counter, hipStream_t st);
+                 int32_t* counter, hipStream_t st, bool bump = true);
 void synth_templates(float* templates, int C, int D, uint64_t seed, hipStream_t st);
 // On-device CIFAR-style augmentation: random crop (pad 4) + h-flip + normalize (NCHW).
 void augment_crop_flip_norm(const float* x, float* y, int N, int C, int H, int W, int pad,

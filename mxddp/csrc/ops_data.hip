@@ -109,10 +109,10 @@ void synth_templates(float* templates, int C, int D, uint64_t seed, hipStream_t 
 }
 
 void synth_batch(float* x, int32_t* y, const float* templates, int B, int D, int C, uint64_t seed, int32_t* counter,
-                 hipStream_t st) {
+                 hipStream_t st, bool bump) {
   hipLaunchKernelGGL(synth_batch_k, dim3(B < 1024 ? B : 1024), dim3(256), 0, st, x, y, templates, B, D, C, seed,
                      counter);
-  hipLaunchKernelGGL(bump_counter_k, dim3(1), dim3(1), 0, st, counter);
+  if (bump) hipLaunchKernelGGL(bump_counter_k, dim3(1), dim3(1), 0, st, counter);
 }
 
 void augment_crop_flip_norm(const float* x, float* y, int N, int C, int H, int W, int pad, const float* mean,
