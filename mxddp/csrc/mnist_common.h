@@ -1,0 +1,28 @@
+// Shared pieces of the fused MNIST kernels (mnist_kernels.hip, mnist_conv_bwd.hip).
+#pragma once
+#include "common.h"
+#include "mnist_engine.h"
+#include "mnist_kernels.h"
+
+namespace mx {
+namespace mnist {
+
+using L = MnistLayout;
+constexpr int kPack = 18432;  // 64*32*9 conv2 weights
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float sel4(const float4& v, int j) {
+  return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
+}
+
+struct Scratch {  // carve of MnistFused::scratch (floats)
+  float* wf;      // conv2 fwd B-fragments   [18 q][4 w][64 lane][4 j]
+  float* wd;      // conv2 dgrad B-fragments [9 r][4 s][2 nt][64 lane][4 j]
+  float* wacc;    // conv2 wgrad accumulator [9 r][64 co][32 ci]
+};
+inline Scratch carve(float* s) { return Scratch{s, s + kPack, s + 2 * kPack}; }
+
+}  // namespace mnist
+}  // namespace mx

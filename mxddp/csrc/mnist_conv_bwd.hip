@@ -1,0 +1,283 @@
+// Fused conv backward of the MNIST-CNN step (fp32 MFMA): F6 conv2 weight grad, F7 conv2 data
+// grad + conv1 ReLU mask + conv1 weight/bias grad.  See mnist_kernels.hip for the step map.
+//
+// dY2 (grad wrt the conv2 pre-activation, B x 64 x 24 x 24, 75 % zeros from the 2x2 max-pool)
+// is NEVER materialised.  Both kernels stage the compact pooled form -- dp (B x 64 x 144,
+// already zeroed on dead windows by F5) and the uint8 argmax map q written by F2 -- into LDS
+// with plain coalesced copies, and expand on the fly while forming MFMA operands:
+//   dY2[co][oy][ox] = (q[co][oy/2][ox/2] == 2*(oy&1) + (ox&1)) ? dp[co][oy/2][ox/2] : 0.
+// The expansion is 1 compare + 1 select per element on the VALU, which co-issues with the
+// MFMA pipe; LDS traffic for the A operand drops 4x versus a dense dY2 tile.
+#include "mnist_common.h"
+
+namespace mx {
+namespace mnist {
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// F6: conv2 weight grad.  wacc[r][co][ci] += sum_pos dY2[b][co][pos] * a1[b][ci][pos + (ky,kx)]
+// Block = (image b, tap r); wave w owns co tile w (16) x both ci tiles (32).  GEMM K = the 576
+// output positions, walked in 16-position groups: lane group g takes positions 16s+4g .. +3,
+// i.e. 4 consecutive columns of one output row = 2 pooling windows -> A = expand(dp float2,
+// q u16), B = a1 window row (LDS float4).  LDS: dp [64][148] (pitch 148 words: the 16 co rows
+// x 2 lane groups of a ds_read_b64 half-wave land on 64 distinct banks), q [64][144] bytes,
+// a1 window chunk [32][196] (8 output rows; pitch 196 = 784 B = 16 mod 256 for ds_read_b128).
+constexpr int kF6DpP = 148, kF6Rows = 8, kF6Pos = kF6Rows * 24, kF6BP = 196;
+constexpr size_t kF6Lds = sizeof(float) * (64 * kF6DpP + 32 * kF6BP) + 64 * 144;
+__global__ __launch_bounds__(256) void f6_conv2_wgrad_kernel(MnistFused f, Scratch sc) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* dps = sm;                                              // [64][148]
+  float* Bs = dps + 64 * kF6DpP;                                // [32][196]
+  uint8_t* qs = reinterpret_cast<uint8_t*>(Bs + 32 * kF6BP);    // [64][144]
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);  // an image's 9 tap blocks share one XCD L2
+  const int r = bid % 9, b = bid / 9;
+  const int ky = r / 3, kx = r - 3 * ky;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  // compact dY2 of image b: dp (float4 granules) and q (uint32 granules), fully coalesced
+  {
+    const float4* src = reinterpret_cast<const float4*>(f.dp + (size_t)b * 9216);
+    const uint32_t* qsrc = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(f.idx) + (size_t)b * 9216);
+    float4 v[9];
+    uint32_t qv[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      v[k] = src[tid + 256 * k];
+      qv[k] = qsrc[tid + 256 * k];
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int i = tid + 256 * k, co = i / 36, c4 = (i - co * 36) * 4;
+      *reinterpret_cast<float4*>(dps + co * kF6DpP + c4) = v[k];
+      *reinterpret_cast<uint32_t*>(qs + co * 144 + c4) = qv[k];
+    }
+  }
+  const float* a1b = f.a1 + (size_t)b * 32 * 676 + ky * 26 + kx;
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const float* dpr = dps + (16 * w + m) * kF6DpP;
+  const uint8_t* qr = qs + (16 * w + m) * 144;
+  // a1 window rows oy0+ky .. +7, cols kx .. kx+23 for all 32 ci: 24 values per thread; the
+  // next chunk's loads are issued before this chunk's MFMAs (register double buffer).
+  float v[24];
+  auto load_chunk = [&](int oy0) {
+#pragma unroll
+    for (int k = 0; k < 24; ++k) {
+      const int i = tid + 256 * k, ci = i / kF6Pos, pos = i - ci * kF6Pos, row = pos / 24, col = pos - row * 24;
+      v[k] = a1b[ci * 676 + (oy0 + row) * 26 + col];
+    }
+  };
+  load_chunk(0);
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    const int oy0 = ch * kF6Rows;
+    if (ch > 0) __syncthreads();  // previous chunk's reads of Bs are done
+#pragma unroll
+    for (int k = 0; k < 24; ++k) {
+      const int i = tid + 256 * k, ci = i / kF6Pos, pos = i - ci * kF6Pos;
+      Bs[ci * kF6BP + pos] = v[k];
+    }
+    __syncthreads();
+    if (ch < 2) load_chunk(oy0 + kF6Rows);
+    const float* br0 = Bs + m * kF6BP + 4 * g;
+    const float* br1 = Bs + (16 + m) * kF6BP + 4 * g;
+#pragma unroll
+    for (int s = 0; s < kF6Pos / 16; ++s) {
+      const int p0 = oy0 * 24 + 16 * s + 4 * g;  // absolute output position of j = 0
+      const int oy = p0 / 24, ox = p0 - oy * 24;  // ox % 4 == 0 -> two whole windows
+      const int w0 = (oy >> 1) * 12 + (ox >> 1);
+      const int t0 = (oy & 1) << 1;
+      const float2 d = *reinterpret_cast<const float2*>(dpr + w0);
+      const uint32_t qq = *reinterpret_cast<const uint16_t*>(qr + w0);
+      const uint32_t q0 = qq & 0xFF, q1 = qq >> 8;
+      const float a0 = q0 == (uint32_t)t0 ? d.x : 0.f;
+      const float a1 = q0 == (uint32_t)t0 + 1 ? d.x : 0.f;
+      const float a2 = q1 == (uint32_t)t0 ? d.y : 0.f;
+      const float a3 = q1 == (uint32_t)t0 + 1 ? d.y : 0.f;
+      const float4 b0 = *reinterpret_cast<const float4*>(br0 + 16 * s);
+      const float4 b1 = *reinterpret_cast<const float4*>(br1 + 16 * s);
+      acc[0] = mfma4(a0, b0.x, acc[0]);
+      acc[1] = mfma4(a0, b1.x, acc[1]);
+      acc[0] = mfma4(a1, b0.y, acc[0]);
+      acc[1] = mfma4(a1, b1.y, acc[1]);
+      acc[0] = mfma4(a2, b0.z, acc[0]);
+      acc[1] = mfma4(a2, b1.z, acc[1]);
+      acc[0] = mfma4(a3, b0.w, acc[0]);
+      acc[1] = mfma4(a3, b1.w, acc[1]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int co = 16 * w + 4 * g + j, ci = 16 * c + m;
+      atomicAdd(sc.wacc + (r * 64 + co) * 32 + ci, acc[c][j]);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// F7: conv2 data grad + conv1 ReLU mask + conv1 weight/bias grad (+ wacc -> conv2.weight grad).
+// GEMM: M = 64 input positions of image b per block (4 M-tiles -> waves), N = 32 ci,
+// K = (r, co) = 576.  A = dY2[co][iy-ky][ix-kx] expanded from the compact pooled tiles in LDS:
+// 4 pooled rows x 14 window columns (a dead halo of one window on each side, so no bounds
+// checks), channel pitch 60 words (lane groups 16 banks apart).  B = pre-packed conv2 weight
+// fragments from L2, prefetched one tap ahead.  The epilogue masks with a1 > 0 and contracts
+// with the 3x3 patches of x (LDS): dW1[ci][r] and db1[ci] are reduced in registers ->
+// cross-lane -> LDS -> one atomic per value per block.  dA1 never touches HBM.
+constexpr int kF7WR = 4, kF7WC = 14, kF7CoP = 60;
+constexpr size_t kF7Lds = sizeof(float) * (64 * kF7CoP + 784 + 1280) + 64 * kF7CoP;
+__global__ __launch_bounds__(256) void f7_conv2_dgrad_kernel(MnistFused f, Scratch sc) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* dps = sm;                                                  // [64][60] (4 x 14 used)
+  float* xs = dps + 64 * kF7CoP;                                    // [784]
+  float* red = xs + 784;                                            // [4][32][10]
+  uint8_t* qs = reinterpret_cast<uint8_t*>(red + 1280);             // [64][60]
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);  // an image's 11 blocks share one XCD L2
+  const int b = bid / 11, chunk = bid - b * 11;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  const uint8_t* idx = reinterpret_cast<const uint8_t*>(f.idx) + (size_t)b * 9216;
+  const float* dpb = f.dp + (size_t)b * 9216;
+  // side duty: canonical conv2.weight grad from the [r][co][ci] accumulator (F6 finished)
+  for (int i = blockIdx.x * 256 + tid; i < kPack; i += gridDim.x * 256) {
+    const int co = i / 288, rem = i - co * 288, ci = rem / 9, rr = rem - ci * 9;
+    f.g[L::w2 + i] = sc.wacc[(rr * 64 + co) * 32 + ci];
+  }
+  const int p0 = chunk * 64;
+  const int row0 = p0 / 26 - 2;           // first conv2-output row any tap of this chunk reads
+  const int wy0 = row0 >> 1;              // first pooled row staged (arithmetic shift: -1 ok)
+  {
+    float dv[14];
+    uint32_t qv[14];
+#pragma unroll
+    for (int k = 0; k < 14; ++k) {  // 64 co x 4 x 14 = 3584 = 14 x 256
+      const int i = tid + 256 * k, co = i / (kF7WR * kF7WC), rem = i - co * (kF7WR * kF7WC);
+      const int wyl = rem / kF7WC, wx = rem - wyl * kF7WC - 1, wy = wy0 + wyl;
+      // unconditional (clamped) loads: a select around a load would make hipcc branch and
+      // drain vmcnt per element; the halo is applied after all loads are in flight
+      const int o = co * 144 + min(max(wy, 0), 11) * 12 + min(max(wx, 0), 11);
+      dv[k] = dpb[o];
+      qv[k] = idx[o];
+    }
+    float xv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xv[k] = f.x[b * 784 + min(tid + 256 * k, 783)];
+#pragma unroll
+    for (int k = 0; k < 14; ++k) {
+      const int i = tid + 256 * k, co = i / (kF7WR * kF7WC), rem = i - co * (kF7WR * kF7WC);
+      const int wyl = rem / kF7WC, wx = rem - wyl * kF7WC - 1, wy = wy0 + wyl;
+      const bool ok = wy >= 0 && wy < 12 && wx >= 0 && wx < 12;
+      dps[co * kF7CoP + rem] = ok ? dv[k] : 0.f;
+      qs[co * kF7CoP + rem] = ok ? (uint8_t)qv[k] : (uint8_t)4;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (tid + 256 * k < 784) xs[tid + 256 * k] = xv[k];
+  }
+  __syncthreads();
+  const int pos = min(p0 + 16 * w + m, 675);  // this lane's A row (clamped tail rows are discarded)
+  const int iy = pos / 26, ix = pos - iy * 26;
+  const float4* wd = reinterpret_cast<const float4*>(sc.wd) + lane;
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  float4 bc[8], bn[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) bc[i] = wd[i * 64];
+#pragma unroll 1
+  for (int r = 0; r < 9; ++r) {
+    if (r < 8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) bn[i] = wd[((r + 1) * 8 + i) * 64];
+    }
+    const int ky = r / 3, kx = r - 3 * ky;
+    const int oy = iy - ky, ox = ix - kx;               // may be -2..-1 or 24..25: dead halo
+    const int wb = ((oy >> 1) - wy0) * kF7WC + (ox >> 1) + 1 + 4 * g * kF7CoP;
+    const uint32_t tgt = (uint32_t)(((oy & 1) << 1) | (ox & 1));
+    const float* dpp = dps + wb;
+    const uint8_t* qp = qs + wb;
+    // All 32 LDS reads of this tap first, unconditionally; the expansion is a multiply by
+    // the 0/1 match (a select around a load lets hipcc turn it into a serialised,
+    // predicated read -> one LDS round trip per MFMA pair).
+    float dv[16];
+    uint32_t qv[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int co_off = (16 * (k >> 2) + (k & 3)) * kF7CoP;  // co = 16s + 4g + j
+      dv[k] = dpp[co_off];
+      qv[k] = qp[co_off];
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a = dv[4 * s + j] * (float)(qv[4 * s + j] == tgt);
+        acc[0] = mfma4(a, sel4(bc[2 * s], j), acc[0]);
+        acc[1] = mfma4(a, sel4(bc[2 * s + 1], j), acc[1]);
+      }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) bc[i] = bn[i];
+  }
+  // epilogue: acc[c][j] = dA1 at position p = p0 + 16w + 4g + j, channel ci = 16c + m
+  float part[2][10];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) part[c][k] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int p = p0 + 16 * w + 4 * g + j;
+    if (p < 676) {
+      const int py = p / 26, px = p - py * 26;
+      const float* xp = xs + py * 28 + px;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int ci = 16 * c + m;
+        const float a1v = f.a1[((size_t)b * 32 + ci) * 676 + p];
+        const float gv = a1v > 0.f ? acc[c][j] : 0.f;
+        part[c][9] += gv;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) part[c][ky * 3 + kx] = fmaf(gv, xp[ky * 28 + kx], part[c][ky * 3 + kx]);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      float v = part[c][k];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      part[c][k] = v;
+    }
+  if (g == 0) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int k = 0; k < 10; ++k) red[(w * 32 + 16 * c + m) * 10 + k] = part[c][k];
+  }
+  __syncthreads();
+  for (int i = tid; i < 320; i += 256) {
+    const float v = red[i] + red[320 + i] + red[640 + i] + red[960 + i];
+    const int ci = i / 10, k = i - ci * 10;
+    if (k < 9) atomicAdd(f.g + L::w1 + ci * 9 + k, v);  // conv1.weight grad [32][9]
+    else atomicAdd(f.g + L::b1 + ci, v);                // conv1.bias grad [32]
+  }
+}
+
+}  // namespace
+}  // namespace mnist
+
+using namespace mnist;
+
+void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    MX_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f6_conv2_wgrad_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  const Scratch sc = carve(f.scratch);
+  hipLaunchKernelGGL(f6_conv2_wgrad_kernel, dim3(9 * f.B), dim3(256), kF6Lds, st, f, sc);
+  hipLaunchKernelGGL(f7_conv2_dgrad_kernel, dim3(f.B * 11), dim3(256), kF7Lds, st, f, sc);
+  MX_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace mx

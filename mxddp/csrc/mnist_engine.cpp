@@ -109,10 +109,9 @@ void MnistEngine::launch_step() {
   const int B = B_;
   const int ws = comm_ ? comm_->world_size() : 1;
   reducer_->prepare();
-  // variant 1 bumps the batch counter inside F1 (one launch fewer)
-  if (!external_batch_)
-    synth_batch(x_, y_, tmpl_, B, 784, 10, seed_ + (comm_ ? comm_->rank() : 0) * 7919ull, counter_, s_,
-                variant_ == 0);
+  const uint64_t data_seed = seed_ + (comm_ ? comm_->rank() : 0) * 7919ull;  // per-rank shard
+  // variant 1 generates the batch inside F1 (no separate launch)
+  if (!external_batch_ && variant_ == 0) synth_batch(x_, y_, tmpl_, B, 784, 10, data_seed, counter_, s_, true);
   if (variant_ == 0) {
     // ---- reference path: generic implicit-GEMM kernels (one op per launch)
     const ConvShape s1 = ConvShape::make(B, 1, 28, 28, 32, 3, 3, 1, 1, 0, 0);
@@ -136,8 +135,8 @@ void MnistEngine::launch_step() {
     reducer_->mark_bucket_ready(1, s_);
   } else {
     // ---- fused path (mnist_kernels.hip)
-    MnistFused f{B, x_, y_, p_, g_, a1_, pool_, idx_, h_, dh_, dp_, scratch_, metrics_,
-                 external_batch_ ? nullptr : counter_};
+    MnistFused f{B,  x_,      y_,       p_,      g_,    a1_,       pool_,           idx_, h_,
+                 dh_, dp_,    scratch_, metrics_, counter_, tmpl_, data_seed, external_batch_ ? 0 : 1};
     mnist_fused_forward(f, s_);
     mnist_fused_head(f, s_);
     mnist_fused_fc1_bwd(f, s_);

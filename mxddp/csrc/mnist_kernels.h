@@ -8,19 +8,22 @@ namespace mx {
 
 struct MnistFused {
   int B;
-  float* x;        // [B,1,28,28]
-  int32_t* y;      // [B]
-  float* p;        // flat params (MnistLayout offsets)
-  float* g;        // flat grads
-  float* a1;       // [B,32,26,26] post-ReLU conv1
-  float* pool;     // [B,64,12,12] post-ReLU pooled conv2
-  int32_t* idx;    // [B,64,12,12] argmax (0..3) within the 2x2 window, 4 = dead (max <= 0)
-  float* h;        // [B,128] fc1 pre-activation accumulator
-  float* dh;       // [B,128] grad wrt fc1 pre-activation
-  float* dp;       // [B,9216] grad wrt pooled activation
-  float* scratch;  // packed weights + split-K partials
-  float* metrics;  // [0] loss sum, [1] correct count (accumulated on device)
-  int32_t* counter;  // synthetic-data batch counter (bumped by F1), may be null
+  float* x;              // [B,1,28,28]
+  int32_t* y;            // [B]
+  float* p;              // flat params (MnistLayout offsets)
+  float* g;              // flat grads
+  float* a1;             // [B,32,26,26] post-ReLU conv1
+  float* pool;           // [B,64,12,12] post-ReLU pooled conv2
+  int32_t* idx;          // used as uint8 [B,64,12,12]: argmax 0..3 inside the 2x2 window, 4 = dead
+  float* h;              // [B,128] fc1 pre-activation accumulator
+  float* dh;             // [B,128] grad wrt fc1 pre-activation
+  float* dp;             // [B,9216] grad wrt pooled activation (0 on dead windows)
+  float* scratch;        // packed weights + accumulators
+  float* metrics;        // [0] loss sum, [1] correct count (accumulated on device)
+  int32_t* counter;      // synthetic-data batch counter
+  const float* tmpl;     // class templates [10][784] for the on-device generator
+  uint64_t seed;         // per-rank generator seed
+  int synth;             // 1: F1 generates the batch on device; 0: x/y provided by the caller
 };
 
 size_t mnist_fused_scratch_floats(int B);

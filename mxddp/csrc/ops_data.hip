@@ -6,32 +6,16 @@
 // counted on device, so the training step never waits on the host.
 #include "common.h"
 #include "ops.h"
+#include "rng.h"
 
 namespace mx {
 namespace {
-
-struct Philox {
-  // Philox4x32-10 (Salmon et al., SC'11): counter (c0..c3), key (k0,k1) -> 4 x u32
-  __device__ static uint4 gen(uint4 c, uint2 k) {
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-      const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
-      c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
-      k.x += 0x9E3779B9u;
-      k.y += 0xBB67AE85u;
-    }
-    return c;
-  }
-};
-
-__device__ __forceinline__ float u01(uint32_t v) { return (v >> 8) * (1.0f / 16777216.0f); }
 
 __global__ void synth_templates_k(float* t, int C, int D, uint64_t seed) {
   const int64_t total = (int64_t)C * D;
   const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32) ^ 0x7A3Bu);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint4 r = Philox::gen(make_uint4((uint32_t)i, 0xC1A55u, 0, 0), key);
+    const uint4 r = philox4x32(make_uint4((uint32_t)i, 0xC1A55u, 0, 0), key);
     t[i] = u01(r.x);
   }
 }
@@ -39,23 +23,20 @@ __global__ void synth_templates_k(float* t, int C, int D, uint64_t seed) {
 __global__ void synth_batch_k(float* __restrict__ x, int32_t* __restrict__ y, const float* __restrict__ tmpl, int B,
                               int D, int C, uint64_t seed, int32_t* counter) {
   const uint32_t ctr = (uint32_t)*counter;
-  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
-  // one block per sample; lane 0 draws the label
+  const uint2 key = synth_key(seed);
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
-    const uint4 lr = Philox::gen(make_uint4(ctr, (uint32_t)b, 0xFFFFFFFFu, 0), key);
-    const int label = (int)(lr.x % (uint32_t)C);
+    const int label = synth_label(ctr, b, C, key);
     if (threadIdx.x == 0) y[b] = label;
     const float* tp = tmpl + (int64_t)label * D;
     float* xp = x + (int64_t)b * D;
     for (int d = threadIdx.x * 4; d < D; d += blockDim.x * 4) {
-      const uint4 r = Philox::gen(make_uint4(ctr, (uint32_t)b, (uint32_t)d, 1), key);
+      const uint4 r = synth_noise4(ctr, b, d, key);
       const uint32_t rv[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (d + j < D) xp[d + j] = 0.5f * tp[d + j] + 0.5f * u01(rv[j]);
     }
   }
-  __syncthreads();
 }
 
 __global__ void bump_counter_k(int32_t* counter) { *counter += 1; }
@@ -70,7 +51,7 @@ __global__ void augment_k(const float* __restrict__ x, float* __restrict__ y, in
     const int w = i % W, h = (i / W) % H;
     const int c = (i / ((int64_t)H * W)) % C;
     const int n = i / ((int64_t)C * H * W);
-    const uint4 r = Philox::gen(make_uint4(ctr, (uint32_t)n, 0xAu, 0), key);
+    const uint4 r = philox4x32(make_uint4(ctr, (uint32_t)n, 0xAu, 0), key);
     const int dy = (int)(r.x % (uint32_t)(2 * pad + 1)) - pad;
     const int dx = (int)(r.y % (uint32_t)(2 * pad + 1)) - pad;
     const bool flip = r.z & 1u;

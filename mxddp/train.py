@@ -1,0 +1,448 @@
+"""mxddp trainer CLI: one entry point for every training mode of the reference.
+
+Flag surface = a superset of ``pytorch/distributed_data_parallel.py:18-48`` (same long and
+short flags, same defaults), so reference launch lines keep working::
+
+    python -m mxddp.train -b 64 -e 10 --lr 0.1 --init-method tcp://127.0.0.1:13456 \
+        --dist-backend nccl --rank 0 --world-size 1 -sm
+
+plus ``--model`` (mnist_cnn | keras_cnn | mlp | pyramidnet110 | resnet50), ``--data``
+(auto | synthetic | real), ``--mode`` (ddp | single | replica), ``--engine`` (auto | fused |
+layers), ``--nproc-per-node`` (single-node torchrun-style spawner), ``--resume``, ...
+
+Modes:
+  ddp      one process per GPU (torch DDP / TF2 MultiWorkerMirrored / ChainerMN);
+  single   one process, one device -- GPU or CPU (pytorch/single_gpu.py, mnist_single.py,
+           chainer/train_mnist.py);
+  replica  one process, N GPUs, global batch split (nn.DataParallel / MirroredStrategy /
+           ParallelUpdater).
+Log lines and checkpoint files follow the reference formats byte for byte.
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import sys
+import time
+
+import torch
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="mxddp: MI355X-native data-parallel training")
+    # ---- reference flags (pytorch/distributed_data_parallel.py:18-48)
+    p.add_argument("--train-dir", "-td", type=str, default="./train_dir")
+    p.add_argument("--dataset-dir", "-dd", type=str, default="./data")
+    p.add_argument("--batch-size", "-b", type=int, default=64,
+                   help="batch per NODE launch, divided by the processes spawned on it (reference semantics)")
+    p.add_argument("--num-workers", type=int, default=4, help="accepted for compatibility (data is device-resident)")
+    p.add_argument("--test-batch-size", "-tb", "--test-batchsize", type=int, default=1000)
+    p.add_argument("--epochs", "-e", type=int, default=10)
+    p.add_argument("--gpu-nums", "-g", type=int, default=0, help="replica mode: GPUs to use (0 = all visible)")
+    p.add_argument("--learning-rate", "--lr", "-lr", type=float, default=None,
+                   help="default: 0.1 for SGD models (reference), 1e-3 for Adam models (Keras/Chainer)")
+    p.add_argument("--momentum", type=float, default=None)
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--log-interval", "-li", type=int, default=20)
+    p.add_argument("--save-model", "-sm", action="store_true", default=False)
+    p.add_argument("--weight-decay", "--wd", "-wd", type=float, default=None)
+    p.add_argument("--init-method", default="tcp://127.0.0.1:13456", type=str)
+    p.add_argument("--dist-backend", default="nccl", type=str, help="nccl (= RCCL on MI355X) or gloo")
+    p.add_argument("--rank", default=0, type=int)
+    p.add_argument("--world-size", default=1, type=int)
+    # ---- mxddp extensions
+    p.add_argument("--model", default="pyramidnet110",
+                   help="mnist_cnn | keras_cnn | mlp | pyramidnet110 | resnet50 (default: the reference's model)")
+    p.add_argument("--data", default="auto", choices=["auto", "synthetic", "real"])
+    p.add_argument("--steps-per-epoch", type=int, default=None, help="synthetic data: batches per epoch")
+    p.add_argument("--mode", default="auto", choices=["auto", "ddp", "single", "replica"])
+    p.add_argument("--engine", default="auto", choices=["auto", "fused", "layers"],
+                   help="fused = native hipGraph step (mnist_cnn + SGD on GPU); layers = HIP ops + DDP reducer")
+    p.add_argument("--optimizer", default=None, choices=[None, "sgd", "adam"])
+    p.add_argument("--lr-step-size", type=int, default=None, help="StepLR step (epochs); 0 = off; default 2 in ddp")
+    p.add_argument("--lr-gamma", type=float, default=0.1)
+    p.add_argument("--per-rank-batch", type=int, default=None, help="override: batch per process")
+    p.add_argument("--nproc-per-node", type=int, default=1, help="spawn this many ranks on this node")
+    p.add_argument("--cpu", action="store_true", help="force the CPU path (gloo)")
+    p.add_argument("--no-graph", action="store_true", help="fused engine: launch eagerly instead of hipGraph replay")
+    p.add_argument("--bucket-cap-mb", type=float, default=25.0)
+    p.add_argument("--resume", type=str, default="", help="training-state file (mxddp_state_<rank>.pt) to resume")
+    p.add_argument("--save-every", type=int, default=0, help="write the full training state every N epochs")
+    p.add_argument("--eval", action="store_true", help="evaluate on the test split after training")
+    p.add_argument("--metrics-jsonl", type=str, default="", help="append JSONL metrics here")
+    p.add_argument("--max-steps", type=int, default=0, help="stop after this many steps (0 = full epochs)")
+    p.add_argument("--sync-set-epoch", action="store_true", default=True)
+    return p
+
+
+def _resolve(args, spec, inf):
+    opt = args.optimizer or spec.optimizer
+    lr = args.learning_rate if args.learning_rate is not None else (spec.lr if opt == spec.optimizer else
+                                                                   (0.1 if opt == "sgd" else 1e-3))
+    mom = args.momentum if args.momentum is not None else (spec.momentum if opt == "sgd" else 0.0)
+    if opt == "sgd" and args.momentum is None and spec.optimizer != "sgd":
+        mom = 0.9
+    wd = args.weight_decay if args.weight_decay is not None else spec.weight_decay
+    mode = args.mode
+    if mode == "auto":
+        mode = "ddp"  # the reference's primary script; world_size 1 is a valid DDP job
+    if args.lr_step_size is None:
+        args.lr_step_size = 2 if mode == "ddp" else 0  # StepLR(2, 0.1) only in the DDP script
+    if args.per_rank_batch:
+        bs = args.per_rank_batch
+    elif mode == "replica":
+        bs = args.batch_size  # global batch split across replicas (DataParallel semantics)
+    else:
+        bs = max(1, args.batch_size // max(1, inf.local_world_size))  # pytorch/distributed_data_parallel.py:71
+    return opt, lr, mom, wd, mode, bs
+
+
+def main(argv=None) -> int:
+    args = build_parser().parse_args(argv)
+    from .parallel import comm as C
+
+    if args.nproc_per_node > 1 and "LOCAL_RANK" not in os.environ:
+        from .launch import spawn_self
+
+        return spawn_self(args.nproc_per_node, argv if argv is not None else sys.argv[1:], module="mxddp.train")
+
+    use_gpu = torch.cuda.is_available() and not args.cpu
+    backend = args.dist_backend if use_gpu else "gloo"
+    inf = C.init_distributed(backend=backend, init_method=args.init_method, rank=args.rank,
+                             world_size=args.world_size, use_gpu=use_gpu)
+    from .models import get_spec
+    from .utils.seed import seed_everything
+
+    seed_everything(args.seed)
+    spec = get_spec(args.model)
+    opt_name, lr, mom, wd, mode, bs = _resolve(args, spec, inf)
+    if mode == "single" and inf.world_size > 1:
+        raise SystemExit("--mode single cannot run with world_size > 1")
+    engine = args.engine
+    if engine == "auto":
+        engine = "fused" if (args.model == "mnist_cnn" and use_gpu and opt_name == "sgd" and mode != "replica"
+                             and bs % 16 == 0 and 16 <= bs <= 128) else "layers"
+    if inf.is_main:
+        print(f"==> mxddp | model {args.model} | mode {mode} | engine {engine} | world {inf.world_size} | "
+              f"device {inf.device} | batch/rank {bs} | {opt_name} lr {lr} mom {mom} wd {wd}", flush=True)
+    from .utils.logging import MetricsWriter
+
+    mw = MetricsWriter(args.metrics_jsonl if (args.metrics_jsonl and inf.is_main) else None)
+    try:
+        if engine == "fused":
+            _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw)
+        elif mode == "replica":
+            _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw)
+        else:
+            _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw)
+    finally:
+        mw.close()
+        C.shutdown()
+    return 0
+
+
+# ====================================================================================== helpers
+def _make_opt(name, flat, lr, mom, wd, spec):
+    from .optim import SGD, Adam
+
+    if name == "sgd":
+        return SGD(flat, lr=lr, momentum=mom, weight_decay=wd)
+    # Keras (1e-7) / Chainer (1e-8) epsilon-hat Adam for the reference Adam models
+    return Adam(flat, lr=lr, eps=1e-7 if spec.name == "keras_cnn" else 1e-8, weight_decay=wd, eps_hat=True)
+
+
+def _log_step(inf, mode, epoch, bi, nb, loss, acc, bt):
+    from .utils import logging as L
+
+    if mode == "ddp":
+        print(L.ddp_step_line(inf.rank, epoch, bi, nb, loss, acc, bt), flush=True)
+    elif inf.is_main:
+        print(L.single_step_line(epoch, bi, nb, loss, acc, bt), flush=True)
+
+
+def _log_epoch(inf, mode, seconds):
+    from .utils import logging as L
+
+    if mode == "ddp":
+        print(L.ddp_epoch_line(inf.rank, seconds), flush=True)
+    elif inf.is_main:
+        print(L.single_epoch_line(seconds), flush=True)
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+@torch.no_grad()
+def evaluate(model, loader, device) -> tuple[float, float]:
+    from . import ops
+
+    model.eval()
+    tot_loss = torch.zeros((), device=device)
+    tot_corr = torch.zeros((), device=device)
+    n = 0
+    for x, y in loader:
+        loss, corr = ops.cross_entropy(model(x), y, return_correct=True)
+        tot_loss += loss * x.shape[0]
+        tot_corr += corr
+        n += x.shape[0]
+    model.train()
+    return (tot_loss / max(n, 1)).item(), (100.0 * tot_corr / max(n, 1)).item()
+
+
+def _maybe_eval(args, inf, spec, model, bs, mw):
+    if not args.eval:
+        return
+    from .data import build_loader
+
+    loader, kind = build_loader(spec.dataset, args.data, args.dataset_dir, args.test_batch_size, inf.device, 1, 0,
+                                args.seed + 99, spec.input_shape, spec.num_classes, train=False,
+                                steps=max(1, math.ceil(10000 / args.test_batch_size)))
+    loss, acc = evaluate(model, loader, inf.device)
+    if inf.is_main:
+        print(f"Test ({kind}): loss {loss:.4f} | acc {acc:.3f}", flush=True)
+    mw.write(kind="eval", loss=loss, acc=acc)
+
+
+def _save_final(args, inf, mode, state_dict):
+    if not args.save_model:
+        return
+    from .utils.checkpoint import save_model
+
+    path = save_model(state_dict, args.train_dir, "replica" if mode == "replica" else
+                      ("ddp" if mode == "ddp" else "single"), inf.rank)
+    if mode == "ddp":
+        print("From Rank: {}, model saved.".format(inf.rank), flush=True)
+    elif inf.is_main:
+        print(f"model saved to {path}", flush=True)
+
+
+# ====================================================================================== layers
+def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
+    from . import ops
+    from .data import build_loader
+    from .models import build_model
+    from .optim import StepLR
+    from .parallel.ddp import DistributedDataParallel as DDP
+    from .parallel.flat import FlatParams
+    from .utils.checkpoint import load_training_state, save_training_state
+
+    dev = inf.device
+    torch.manual_seed(args.seed)
+    model = build_model(spec.name).to(dev)
+    if mode == "ddp":
+        net = DDP(model, bucket_cap_mb=args.bucket_cap_mb)
+        flat = net.flat
+    else:
+        net, flat = model, FlatParams(model, dev)
+    opt = _make_opt(opt_name, flat, lr, mom, wd, spec)
+    sched = StepLR(opt, args.lr_step_size, args.lr_gamma) if args.lr_step_size else None
+    start_epoch = 1
+    if args.resume:
+        st = load_training_state(args.resume)
+        model.load_state_dict(st["model"])
+        opt.load_state_dict(st["optimizer"])
+        if sched and st.get("scheduler"):
+            sched.load_state_dict(st["scheduler"])
+        start_epoch = st["epoch"] + 1
+    if inf.is_main:
+        print("From Rank: {}, The number of parameters of model is {}".format(
+            inf.rank, sum(p.numel() for p in model.parameters())), flush=True)
+    loader, kind = build_loader(spec.dataset, args.data, args.dataset_dir, bs, dev, inf.world_size, inf.rank,
+                                args.seed, spec.input_shape, spec.num_classes, train=True,
+                                steps=args.steps_per_epoch)
+    if inf.is_main:
+        print(f"==> data: {kind}, {len(loader)} batches/epoch", flush=True)
+    step = 0
+    for epoch in range(start_epoch, args.epochs + 1):
+        if hasattr(loader, "sampler"):
+            loader.sampler.set_epoch(epoch)
+        net.train()
+        loss_acc = torch.zeros((), device=dev)
+        corr_acc = torch.zeros((), device=dev)
+        total = 0
+        t_epoch = t_log = time.time()
+        last_log = 0
+        for bi, (x, y) in enumerate(loader):
+            opt.zero_grad()
+            out = net(x)
+            loss, corr = ops.cross_entropy(out, y, return_correct=True)
+            loss.backward()
+            opt.step()
+            loss_acc += loss.detach()
+            corr_acc += corr
+            total += x.shape[0]
+            step += 1
+            if bi % args.log_interval == 0:
+                _sync(dev)
+                now = time.time()
+                bt = (now - t_log) / max(1, bi - last_log) if bi else now - t_log
+                t_log, last_log = now, bi
+                l_avg, acc = loss_acc.item() / (bi + 1), 100.0 * corr_acc.item() / total
+                _log_step(inf, mode, epoch, bi, len(loader), l_avg, acc, bt)
+                mw.write(kind="step", epoch=epoch, step=step, loss=l_avg, acc=acc, batch_time=bt,
+                         img_per_s=x.shape[0] * inf.world_size / max(bt, 1e-9))
+            if args.max_steps and step >= args.max_steps:
+                break
+        _sync(dev)
+        _log_epoch(inf, mode, time.time() - t_epoch)
+        if sched:
+            sched.step()
+        if args.save_every and epoch % args.save_every == 0:
+            save_training_state(args.train_dir, inf.rank, model.state_dict(), opt.state_dict(),
+                                sched.state_dict() if sched else None, epoch, step)
+        if args.max_steps and step >= args.max_steps:
+            break
+    _maybe_eval(args, inf, spec, model, bs, mw)
+    _save_final(args, inf, mode, model.state_dict())
+
+
+# ====================================================================================== replica
+def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
+    from . import ops
+    from .data import build_loader
+    from .models import build_model
+    from .optim import StepLR
+    from .parallel.replica import ReplicaGroup
+
+    if inf.world_size > 1:
+        raise SystemExit("replica mode is single-process (use --mode ddp for multi-process)")
+    if inf.device.type == "cuda":
+        n = args.gpu_nums or torch.cuda.device_count()
+        devices = [torch.device("cuda", i) for i in range(n)]
+    else:
+        devices = [torch.device("cpu")]
+    torch.manual_seed(args.seed)
+    model = build_model(spec.name)
+    group = ReplicaGroup(model, devices, lambda f: _make_opt(opt_name, f, lr, mom, wd, spec))
+    scheds = [StepLR(o, args.lr_step_size, args.lr_gamma) for o in group.optimizers] if args.lr_step_size else []
+    loader, kind = build_loader(spec.dataset, args.data, args.dataset_dir, bs, devices[0], 1, 0, args.seed,
+                                spec.input_shape, spec.num_classes, train=True, steps=args.steps_per_epoch)
+    print(f"==> replica mode on {len(devices)} device(s), global batch {bs}, data {kind}", flush=True)
+    loss_fn = lambda o, t: ops.cross_entropy(o, t, return_correct=True)  # noqa: E731
+    step = 0
+    for epoch in range(1, args.epochs + 1):
+        if hasattr(loader, "sampler"):
+            loader.sampler.set_epoch(epoch)
+        loss_acc = torch.zeros((), device=devices[0])
+        corr_acc = torch.zeros((), device=devices[0])
+        total = 0
+        t_epoch = t_log = time.time()
+        last_log = 0
+        for bi, (x, y) in enumerate(loader):
+            ls, c = group.step(x, y, loss_fn)
+            loss_acc += ls / x.shape[0]
+            corr_acc += c
+            total += x.shape[0]
+            step += 1
+            if bi % args.log_interval == 0:
+                _sync(devices[0])
+                now = time.time()
+                bt = (now - t_log) / max(1, bi - last_log) if bi else now - t_log
+                t_log, last_log = now, bi
+                _log_step(inf, "single", epoch, bi, len(loader), loss_acc.item() / (bi + 1),
+                          100.0 * corr_acc.item() / total, bt)
+            if args.max_steps and step >= args.max_steps:
+                break
+        _sync(devices[0])
+        _log_epoch(inf, "single", time.time() - t_epoch)
+        for s in scheds:
+            s.step()
+        if args.max_steps and step >= args.max_steps:
+            break
+    _maybe_eval(args, inf, spec, group.module, bs, mw)
+    _save_final(args, inf, "replica", group.module.state_dict())
+
+
+# ====================================================================================== fused
+def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
+    from .data import build_loader
+    from .engine import FusedMnistTrainer
+    from .models import build_model
+    from .parallel import comm as C
+    from .utils.checkpoint import load_training_state, save_training_state
+
+    dev = inf.device
+    torch.manual_seed(args.seed)
+    init = build_model("mnist_cnn")
+    start_epoch = 1
+    if args.resume:
+        st = load_training_state(args.resume)
+        init.load_state_dict(st["model"])
+        start_epoch = st["epoch"] + 1
+    tr = FusedMnistTrainer(batch=bs, device=dev, comm=C.rccl_comm(), seed=args.seed, lr=lr, momentum=mom,
+                           weight_decay=wd, use_graph=not args.no_graph, init_model=init)
+    if args.resume and "momentum" in st.get("optimizer", {}):
+        tr.mom.copy_(st["optimizer"]["momentum"].to(dev))
+    loader, kind = build_loader("mnist", args.data, args.dataset_dir, bs, dev, inf.world_size, inf.rank, args.seed,
+                                spec.input_shape, 10, train=True, steps=args.steps_per_epoch)
+    synthetic = kind == "synthetic"
+    if inf.is_main:
+        print("From Rank: {}, The number of parameters of model is {}".format(inf.rank, 1199882), flush=True)
+        print(f"==> data: {kind}, {len(loader)} batches/epoch, fused hipGraph step={'off' if args.no_graph else 'on'}",
+              flush=True)
+    step = 0
+    base_lr = lr
+    for epoch in range(start_epoch, args.epochs + 1):
+        if args.lr_step_size:
+            tr.set_lr(base_lr * args.lr_gamma ** ((epoch - 1) // args.lr_step_size))
+        if hasattr(loader, "sampler"):
+            loader.sampler.set_epoch(epoch)
+        nb = len(loader)
+        t_epoch = t_log = time.time()
+        loss_tot, corr_tot, seen = 0.0, 0.0, 0
+        bi = 0
+        if synthetic:
+            while bi < nb:
+                n = 1 if bi % args.log_interval == 0 else min(args.log_interval - bi % args.log_interval, nb - bi)
+                tr.step(n)
+                bi += n
+                step += n
+                if (bi - 1) % args.log_interval == 0 or bi == nb:
+                    ls, cs = tr.read_metrics()
+                    loss_tot += ls
+                    corr_tot += cs
+                    seen_now = bi * bs
+                    now = time.time()
+                    bt = (now - t_log) / max(1, n)
+                    t_log = now
+                    _log_step(inf, mode, epoch, bi - 1, nb, loss_tot / seen_now, 100.0 * corr_tot / seen_now, bt)
+                    mw.write(kind="step", epoch=epoch, step=step, loss=loss_tot / seen_now, acc=100.0 * corr_tot / seen_now,
+                             batch_time=bt, img_per_s=bs * inf.world_size / max(bt, 1e-9))
+                if args.max_steps and step >= args.max_steps:
+                    break
+        else:
+            for x, y in loader:
+                if x.shape[0] != bs:
+                    continue  # the captured graph has a fixed batch (drop_last semantics)
+                tr.set_batch(x, y)
+                tr.step(1)
+                step += 1
+                if bi % args.log_interval == 0:
+                    ls, cs = tr.read_metrics()
+                    loss_tot += ls
+                    corr_tot += cs
+                    seen = (bi + 1) * bs
+                    now = time.time()
+                    bt = (now - t_log) / max(1, args.log_interval if bi else 1)
+                    t_log = now
+                    _log_step(inf, mode, epoch, bi, nb, loss_tot / seen, 100.0 * corr_tot / seen, bt)
+                bi += 1
+                if args.max_steps and step >= args.max_steps:
+                    break
+        tr.synchronize()
+        _log_epoch(inf, mode, time.time() - t_epoch)
+        if args.save_every and epoch % args.save_every == 0:
+            save_training_state(args.train_dir, inf.rank, tr.state_dict(), {"momentum": tr.mom.cpu(), "lr": tr._lr_host},
+                                {"base_lr": base_lr}, epoch, step)
+        if args.max_steps and step >= args.max_steps:
+            break
+    model = tr.to_module().to(dev)
+    _maybe_eval(args, inf, spec, model, bs, mw)
+    _save_final(args, inf, mode, tr.state_dict())
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,135 @@
+"""T2: distributed semantics on CPU with gloo, world_size 2.
+
+Golden equivalence: DDP at world_size N with per-rank batch b must equal single-process
+training on the concatenated batch N*b (gradients averaged over ranks), and rank 0's
+weights must win at wrap time.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from mxddp.models import build_model
+from mxddp.parallel.ddp import assign_buckets
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _batches(steps, global_b, shape, seed=123):
+    g = torch.Generator().manual_seed(seed)
+    return [(torch.rand((global_b,) + shape, generator=g), torch.randint(0, 10, (global_b,), generator=g))
+            for _ in range(steps)]
+
+
+def _worker(rank, ws, port, model_name, steps, b, q, perturb):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from mxddp import ops
+    from mxddp.optim import SGD
+    from mxddp.parallel import comm
+    from mxddp.parallel.ddp import DistributedDataParallel as DDP
+
+    comm.init_distributed(rank=rank, world_size=ws, use_gpu=False, init_method=f"tcp://127.0.0.1:{port}")
+    torch.manual_seed(0)
+    model = build_model(model_name)
+    if perturb and rank == 1:
+        with torch.no_grad():
+            for p in model.parameters():
+                p.add_(1.0)
+    ddp = DDP(model)
+    opt = SGD(ddp.flat, lr=0.05, momentum=0.9, weight_decay=1e-4)
+    shape = model.input_shape
+    for x, y in _batches(steps, ws * b, shape):
+        xs, ys = x[rank * b:(rank + 1) * b], y[rank * b:(rank + 1) * b]
+        opt.zero_grad()
+        loss = ops.cross_entropy(ddp(xs), ys)
+        loss.backward()
+        opt.step()
+    q.put((rank, {k: v.detach().numpy().copy() for k, v in model.state_dict().items()}, len(ddp.buckets)))
+    comm.shutdown()
+
+
+def _run_ddp(model_name, ws=2, steps=3, b=4, perturb=False):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, ws, port, model_name, steps, b, q, perturb)) for r in range(ws)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in range(ws):
+        r, sd, nb = q.get(timeout=240)
+        out[r] = ({k: torch.from_numpy(v) for k, v in sd.items()}, nb)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
+
+
+@pytest.mark.parametrize("model_name", ["mnist_cnn", "mlp"])
+def test_ddp_matches_single_process_large_batch(model_name):
+    ws, steps, b = 2, 3, 4
+    out = _run_ddp(model_name, ws, steps, b, perturb=True)
+    # reference: plain torch, global batch, torch.optim.SGD
+    torch.manual_seed(0)
+    ref = build_model(model_name)
+    opt = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+    for x, y in _batches(steps, ws * b, ref.input_shape):
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(ref(x), y).backward()
+        opt.step()
+    ref_sd = ref.state_dict()
+    for r in range(ws):
+        sd = out[r][0]
+        for k, v in ref_sd.items():
+            assert torch.allclose(sd[k], v, rtol=1e-4, atol=1e-5), (r, k, (sd[k] - v).abs().max())
+    # ranks identical to each other (rank-0 broadcast beat the perturbation on rank 1)
+    for k in out[0][0]:
+        assert torch.equal(out[0][0][k], out[1][0][k]), k
+
+
+def test_bucket_assignment_mnist_two_buckets():
+    m = build_model("mnist_cnn")
+    numels = [p.numel() for p in m.parameters()]
+    offs, o = [], 0
+    for n in numels:
+        offs.append(o)
+        o += (n + 15) // 16 * 16
+    buckets, pb = assign_buckets(numels, offs, o)
+    assert len(buckets) == 2  # 4.72 MB + 0.075 MB
+    assert abs(buckets[0][1] * 4 / 1e6 - 4.72) < 0.01
+    assert abs(buckets[1][1] * 4 / 1e6 - 0.075) < 0.002
+    assert pb == [1, 1, 1, 1, 0, 0, 0, 0]
+    # buckets tile the flat buffer contiguously from the end
+    assert buckets[0][0] + buckets[0][1] == o and buckets[1][0] == 0 and buckets[1][1] == buckets[0][0]
+
+
+def test_bucket_assignment_pyramidnet_five_buckets():
+    m = build_model("pyramidnet110")
+    numels = [p.numel() for p in m.parameters()]
+    offs, o = [], 0
+    for n in numels:
+        offs.append(o)
+        o += (n + 15) // 16 * 16
+    buckets, _ = assign_buckets(numels, offs, o)
+    mb = [n * 4 / 1e6 for _, n in buckets]
+    # SURVEY §2.6 N4 (torch's own _compute_bucket_assignment_by_size): 2.66/28.10/26.47/26.66/13.12 MB
+    expect = [2.66, 28.10, 26.47, 26.66, 13.12]
+    assert len(mb) == 5
+    for a, e in zip(mb, expect):
+        assert abs(a - e) / e < 0.01, (mb, expect)
+
+
+def test_gloo_reducer_rejects_double_mark():
+    from mxddp.parallel.ddp import _GlooReducer
+
+    r = _GlooReducer(torch.zeros(32), [(16, 16), (0, 16)], [1, 0], True, 1)
+    r.mark_ready(0)
+    with pytest.raises(RuntimeError):
+        r.mark_ready(0)

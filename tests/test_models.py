@@ -1,0 +1,77 @@
+"""T0: model topology golden values on the CPU path."""
+import pytest
+import torch
+
+from mxddp.models import MODELS, build_model
+from mxddp.models.layers import count_params
+from mxddp.models.pyramidnet import channel_schedule
+
+GOLDEN_PARAMS = {
+    "mnist_cnn": 1_199_882,
+    "keras_cnn": 93_322,
+    "mlp": 1_796_010,
+    "pyramidnet110": 24_253_410,
+    "resnet50": 25_557_032,
+}
+
+
+@pytest.mark.parametrize("name", sorted(GOLDEN_PARAMS))
+def test_param_counts(name):
+    assert count_params(build_model(name)) == GOLDEN_PARAMS[name]
+
+
+def test_pyramidnet_state_dict_layout():
+    sd = build_model("pyramidnet110").state_dict()
+    keys = list(sd)
+    assert len(keys) == 880
+    assert keys[:4] == ["conv1.weight", "bn1.weight", "bn1.bias", "bn1.running_mean"]
+    assert keys[-3:] == ["bn_out.num_batches_tracked", "fc_out.weight", "fc_out.bias"]
+    assert sum(1 for k in keys if k.endswith("num_batches_tracked")) == 155  # 155 BN layers
+    assert sum(1 for k in keys if k.endswith("conv1.weight") or k.endswith("conv2.weight")) == 103
+
+
+def test_pyramidnet_channel_schedule():
+    sched, out = channel_schedule()
+    assert len(sched) == 51 and out == 271
+    assert sched[0] == (16, 21, 1)
+    assert sched[17][2] == 2 and sched[17][0] == 101 and sched[17][1] == 106  # stage-2 entry
+    assert sched[34][2] == 2 and sched[34][0] == 186 and sched[34][1] == 191  # stage-3 entry
+    assert len({(a, b) for a, b, _ in sched}) == 51
+
+
+@pytest.mark.parametrize("name,shape", [("mnist_cnn", (2, 1, 28, 28)), ("keras_cnn", (2, 1, 28, 28)),
+                                        ("mlp", (2, 1, 28, 28)), ("pyramidnet110", (2, 3, 32, 32))])
+def test_forward_backward_cpu(name, shape):
+    m = build_model(name)
+    x = torch.randn(shape)
+    out = m(x)
+    assert out.shape == (2, 10)
+    out.sum().backward()
+    assert all(p.grad is not None for p in m.parameters())
+
+
+def test_resnet50_forward_small():
+    m = build_model("resnet50")
+    out = m(torch.randn(1, 3, 64, 64))
+    assert out.shape == (1, 1000)
+
+
+def test_state_dict_loads_into_plain_torch_module():
+    """Checkpoint compatibility: our MnistCNN state_dict loads into a torch.nn reference net."""
+    import torch.nn as nn
+
+    class Ref(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.conv1 = nn.Conv2d(1, 32, 3, 1)
+            self.conv2 = nn.Conv2d(32, 64, 3, 1)
+            self.fc1 = nn.Linear(9216, 128)
+            self.fc2 = nn.Linear(128, 10)
+
+    ref = Ref()
+    ref.load_state_dict(build_model("mnist_cnn").state_dict(), strict=True)
+
+
+def test_registry_specs():
+    assert set(MODELS) == set(GOLDEN_PARAMS)
+    assert MODELS["keras_cnn"].optimizer == "adam" and MODELS["pyramidnet110"].optimizer == "sgd"
