@@ -135,11 +135,6 @@ __global__ __launch_bounds__(256) void f7_conv2_dgrad_kernel(MnistFused f, Scrat
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
   const uint8_t* idx = reinterpret_cast<const uint8_t*>(f.idx) + (size_t)b * 9216;
   const float* dpb = f.dp + (size_t)b * 9216;
-  // side duty: canonical conv2.weight grad from the [r][co][ci] accumulator (F6 finished)
-  for (int i = blockIdx.x * 256 + tid; i < kPack; i += gridDim.x * 256) {
-    const int co = i / 288, rem = i - co * 288, ci = rem / 9, rr = rem - ci * 9;
-    f.g[L::w2 + i] = sc.wacc[(rr * 64 + co) * 32 + ci];
-  }
   const int p0 = chunk * 64;
   const int row0 = p0 / 26 - 2;           // first conv2-output row any tap of this chunk reads
   const int wy0 = row0 >> 1;              // first pooled row staged (arithmetic shift: -1 ok)
@@ -254,11 +249,32 @@ __global__ __launch_bounds__(256) void f7_conv2_dgrad_kernel(MnistFused f, Scrat
       for (int k = 0; k < 10; ++k) red[(w * 32 + 16 * c + m) * 10 + k] = part[c][k];
   }
   __syncthreads();
+  // per-image partial slab (11 chunk blocks per address instead of all 704 blocks hammering
+  // the same 320 words: same-address float atomics serialise at the memory side)
+  float* g1 = sc.g1 + b * 320;
   for (int i = tid; i < 320; i += 256) {
     const float v = red[i] + red[320 + i] + red[640 + i] + red[960 + i];
     const int ci = i / 10, k = i - ci * 10;
-    if (k < 9) atomicAdd(f.g + L::w1 + ci * 9 + k, v);  // conv1.weight grad [32][9]
-    else atomicAdd(f.g + L::b1 + ci, v);                // conv1.bias grad [32]
+    if (k < 9) atomicAdd(g1 + ci * 9 + k, v);  // conv1.weight grad [32][9]
+    else atomicAdd(g1 + 288 + ci, v);          // conv1.bias grad [32]
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// F8: finalize bucket 1: conv2.weight grad = transpose of the [r][co][ci] accumulator into
+// the canonical [co][ci][ky][kx] layout; conv1 weight/bias grads = sum over the per-image
+// partial slabs (a coalesced column sum, 64 loads in flight per thread).
+__global__ __launch_bounds__(256) void f8_finalize_kernel(MnistFused f, Scratch sc) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < kPack) {
+    const int co = i / 288, rem = i - co * 288, ci = rem / 9, rr = rem - ci * 9;
+    f.g[L::w2 + i] = sc.wacc[(rr * 64 + co) * 32 + ci];
+  } else if (i < kPack + 320) {
+    const int j = i - kPack;
+    float s = 0.f;
+#pragma unroll 16
+    for (int b = 0; b < f.B; ++b) s += sc.g1[b * 320 + j];
+    f.g[L::w1 + j] = s;  // conv1.weight [288] followed by conv1.bias [32] in the flat layout
   }
 }
 
@@ -277,6 +293,7 @@ void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st) {
   const Scratch sc = carve(f.scratch);
   hipLaunchKernelGGL(f6_conv2_wgrad_kernel, dim3(9 * f.B), dim3(256), kF6Lds, st, f, sc);
   hipLaunchKernelGGL(f7_conv2_dgrad_kernel, dim3(f.B * 11), dim3(256), kF7Lds, st, f, sc);
+  hipLaunchKernelGGL(f8_finalize_kernel, dim3((kPack + 320 + 255) / 256), dim3(256), 0, st, f, sc);
   MX_HIP_CHECK(hipGetLastError());
 }
 

@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void f1_conv1_kernel(MnistFused f, Scratch sc)
     sc.wacc[i] = 0.f;
   }
   for (int i = gtid; i < f.B * 128; i += gsz) f.h[i] = 0.f;
-  if (gtid < 320) f.g[L::w1 + gtid] = 0.f;                        // conv1 w+b grads (F7 atomics)
+  for (int i = gtid; i < f.B * 320; i += gsz) sc.g1[i] = 0.f;     // conv1 grad per-image partials (F7)
   if (gtid < 64) f.g[L::b2 + gtid] = 0.f;                         // conv2 bias grad (F5 atomics)
   if (gtid < 1280 + 10) f.g[L::fw2 + gtid] = 0.f;                 // fc2 w+b grads (F4 atomics)
   if (gtid < 128) f.g[L::fb1 + gtid] = 0.f;                       // fc1 bias grad (F4 atomics)
@@ -411,7 +411,7 @@ __global__ __launch_bounds__(256) void f5_fc1_bwd_kernel(MnistFused f) {
 
 using namespace mnist;
 
-size_t mnist_fused_scratch_floats(int) { return 3 * (size_t)kPack; }
+size_t mnist_fused_scratch_floats(int B) { return scratch_floats(B); }
 
 static void check(const MnistFused& f) {
   MX_CHECK(f.B % 16 == 0 && f.B >= 16 && f.B <= 128, "fused MNIST engine needs batch % 16 == 0 and 16 <= B <= 128");
