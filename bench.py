@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--lr", type=float, default=0.01, help="SGD lr (momentum 0.9, wd 1e-4 as the reference)")
+    ap.add_argument("--model", default="mnist_cnn",
+                    help="headline: mnist_cnn (fused).  Others run the layers path: keras_cnn, mlp, pyramidnet110, resnet50")
     return ap.parse_args()
 
 
@@ -58,6 +60,8 @@ def main():
     comm = C.rccl_comm()
     B = a.batch
 
+    if a.model != "mnist_cnn" and a.impl == "fused":
+        a.impl = "layers"
     if a.impl == "fused":
         from mxddp.engine import FusedMnistTrainer
 
@@ -100,7 +104,7 @@ def main():
             "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 3),
             "dtype": "fp32",
             "data": "synthetic (on-device class-conditional 28x28, random-init weights)",
-            "config": {"model": "mnist_cnn", "global_batch": B * a.gpus, "per_rank_batch": B, "seq_len": None,
+            "config": {"model": a.model, "global_batch": B * a.gpus, "per_rank_batch": B, "seq_len": None,
                        "image": "1x28x28", "parallelism": f"dp{a.gpus}", "impl": a.impl,
                        "graph": (a.impl == "fused" and not a.no_graph)},
             **extra,
@@ -114,10 +118,11 @@ def _layers_or_torch(a, torch, inf, dev, comm, B):
     import torch.nn.functional as F
 
     from mxddp import native
-    from mxddp.models import MnistCNN
+    from mxddp.models import build_model, get_spec
 
     torch.manual_seed(a.seed)
-    model = MnistCNN().to(dev)
+    spec = get_spec(a.model)
+    model = build_model(a.model).to(dev)
     if a.impl == "layers":
         from mxddp import ops
         from mxddp.optim import SGD
@@ -129,8 +134,10 @@ def _layers_or_torch(a, torch, inf, dev, comm, B):
     else:
         import torch.nn as nn
 
-        ref = nn.Sequential(nn.Conv2d(1, 32, 3), nn.ReLU(), nn.Conv2d(32, 64, 3), nn.ReLU(), nn.MaxPool2d(2),
-                            nn.Flatten(), nn.Linear(9216, 128), nn.ReLU(), nn.Linear(128, 10)).to(dev)
+        from mxddp import ops as _ops
+
+        _ops.torch_reference_mode().__enter__()  # stock PyTorch-ROCm kernels for every op
+        ref = model
         if inf.world_size > 1:
             import torch.distributed as dist
 
@@ -139,16 +146,20 @@ def _layers_or_torch(a, torch, inf, dev, comm, B):
         opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
         loss_fn = lambda o, t: F.cross_entropy(o, t)  # noqa: E731
     Cn = native()
-    tmpl = torch.empty(10 * 784, device=dev)
+    D = 1
+    for s_ in spec.input_shape:
+        D *= s_
+    nc = spec.num_classes
+    tmpl = torch.empty(nc * D, device=dev)
     ctr = torch.zeros(4, dtype=torch.int32, device=dev)
-    x = torch.empty(B, 1, 28, 28, device=dev)
+    x = torch.empty((B,) + tuple(spec.input_shape), device=dev)
     y = torch.empty(B, dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
-    Cn.synth_templates(tmpl.data_ptr(), 10, 784, a.seed, st)
+    Cn.synth_templates(tmpl.data_ptr(), nc, D, a.seed, st)
 
     def run(n):
         for _ in range(n):
-            Cn.synth_batch(x.data_ptr(), y.data_ptr(), tmpl.data_ptr(), B, 784, 10, a.seed + inf.rank, ctr.data_ptr(),
+            Cn.synth_batch(x.data_ptr(), y.data_ptr(), tmpl.data_ptr(), B, D, nc, a.seed + inf.rank, ctr.data_ptr(),
                            torch.cuda.current_stream(dev).cuda_stream)
             opt.zero_grad()
             out = net(x)

@@ -211,7 +211,8 @@ PYBIND11_MODULE(_C, m) {
            py::arg("weight_decay"), py::arg("lr_dev"), py::arg("metrics_dev"), py::arg("variant") = 1,
            py::keep_alive<1, 8>())
       .def("step", &MnistEngine::step)
-      .def("capture", &MnistEngine::capture)
+      .def("capture", &MnistEngine::capture, py::arg("mode") = -1)
+      .def_property_readonly("graph_mode", &MnistEngine::graph_mode)
       .def("replay", &MnistEngine::replay)
       .def("forward_only", &MnistEngine::forward_only)
       .def("sync", &MnistEngine::sync, py::call_guard<py::gil_scoped_release>())

@@ -88,6 +88,10 @@ MnistEngine::MnistEngine(int batch, uintptr_t params, uintptr_t grads, uintptr_t
 MnistEngine::~MnistEngine() {
   if (exec_) hipGraphExecDestroy(exec_);
   if (graph_) hipGraphDestroy(graph_);
+  for (int k = 0; k < 3; ++k) {
+    if (seg_exec_[k]) hipGraphExecDestroy(seg_exec_[k]);
+    if (seg_graph_[k]) hipGraphDestroy(seg_graph_[k]);
+  }
   reducer_.reset();
   if (s_) hipStreamDestroy(s_);
 }
@@ -104,73 +108,110 @@ void MnistEngine::fwd(const float* x, float* logits_out, int B) {
   linear_fwd(h_, p_ + L::fw2, p_ + L::fb2, logits_out, B, 10, 128, false, s_);
 }
 
-void MnistEngine::launch_step() {
+MnistFused MnistEngine::fused_args() const {
+  const uint64_t data_seed = seed_ + (comm_ ? comm_->rank() : 0) * 7919ull;  // per-rank data shard
+  return MnistFused{B_,   x_,       y_,       p_,       g_,    a1_,       pool_,           idx_, h_,
+                    dh_,  dp_,      scratch_, metrics_, counter_, tmpl_, data_seed, external_batch_ ? 0 : 1};
+}
+
+// Segment 0: batch + forward + head + fc backward  -> bucket 0 (fc grads, 4.72 MB) is complete.
+void MnistEngine::segment(int k) {
   using L = MnistLayout;
   const int B = B_;
-  const int ws = comm_ ? comm_->world_size() : 1;
-  reducer_->prepare();
-  const uint64_t data_seed = seed_ + (comm_ ? comm_->rank() : 0) * 7919ull;  // per-rank shard
-  // variant 1 generates the batch inside F1 (no separate launch)
-  if (!external_batch_ && variant_ == 0) synth_batch(x_, y_, tmpl_, B, 784, 10, data_seed, counter_, s_, true);
-  if (variant_ == 0) {
-    // ---- reference path: generic implicit-GEMM kernels (one op per launch)
-    const ConvShape s1 = ConvShape::make(B, 1, 28, 28, 32, 3, 3, 1, 1, 0, 0);
-    const ConvShape s2 = ConvShape::make(B, 32, 26, 26, 64, 3, 3, 1, 1, 0, 0);
-    fwd(x_, logits_, B);
-    xent_fwd_bwd(logits_, y_, nullptr, dlogits_, metrics_, metrics_ + 1, B, 10, 1.f / B, s_);
-    linear_wgrad(dlogits_, h_, g_ + L::fw2, B, 10, 128, false, s_);
-    bias_grad(dlogits_, g_ + L::fb2, B, 10, 1, false, s_);
-    linear_dgrad(dlogits_, p_ + L::fw2, dh_, B, 10, 128, h_, false, s_);
-    linear_wgrad(dh_, pool_, g_ + L::fw1, B, 128, 9216, false, s_);
-    bias_grad(dh_, g_ + L::fb1, B, 128, 1, false, s_);
-    linear_dgrad(dh_, p_ + L::fw1, dp_, B, 128, 9216, nullptr, false, s_);
-    reducer_->mark_bucket_ready(0, s_);
-    maxpool2d_bwd(dp_, idx_, dc2_, B, 64, 24, 24, 12, 12, s_);
-    relu_bwd(dc2_, c2_, dc2_, (int64_t)B * 36864, s_);
-    conv2d_wgrad(dc2_, a1_, g_ + L::w2, s2, false, s_);
-    bias_grad(dc2_, g_ + L::b2, B, 64, 576, false, s_);
-    conv2d_dgrad(dc2_, p_ + L::w2, da1_, s2, a1_, false, s_);
-    conv2d_wgrad(da1_, x_, g_ + L::w1, s1, false, s_);
-    bias_grad(da1_, g_ + L::b1, B, 32, 676, false, s_);
-    reducer_->mark_bucket_ready(1, s_);
-  } else {
-    // ---- fused path (mnist_kernels.hip)
-    MnistFused f{B,  x_,      y_,       p_,      g_,    a1_,       pool_,           idx_, h_,
-                 dh_, dp_,    scratch_, metrics_, counter_, tmpl_, data_seed, external_batch_ ? 0 : 1};
-    mnist_fused_forward(f, s_);
-    mnist_fused_head(f, s_);
-    mnist_fused_fc1_bwd(f, s_);
-    reducer_->mark_bucket_ready(0, s_);
-    mnist_fused_conv_bwd(f, s_);
-    reducer_->mark_bucket_ready(1, s_);
+  const ConvShape s1 = ConvShape::make(B, 1, 28, 28, 32, 3, 3, 1, 1, 0, 0);
+  const ConvShape s2 = ConvShape::make(B, 32, 26, 26, 64, 3, 3, 1, 1, 0, 0);
+  if (k == 0) {
+    if (variant_ == 0) {  // reference path: generic implicit-GEMM kernels, one op per launch
+      if (!external_batch_) synth_batch(x_, y_, tmpl_, B, 784, 10, fused_args().seed, counter_, s_, true);
+      fwd(x_, logits_, B);
+      xent_fwd_bwd(logits_, y_, nullptr, dlogits_, metrics_, metrics_ + 1, B, 10, 1.f / B, s_);
+      linear_wgrad(dlogits_, h_, g_ + L::fw2, B, 10, 128, false, s_);
+      bias_grad(dlogits_, g_ + L::fb2, B, 10, 1, false, s_);
+      linear_dgrad(dlogits_, p_ + L::fw2, dh_, B, 10, 128, h_, false, s_);
+      linear_wgrad(dh_, pool_, g_ + L::fw1, B, 128, 9216, false, s_);
+      bias_grad(dh_, g_ + L::fb1, B, 128, 1, false, s_);
+      linear_dgrad(dh_, p_ + L::fw1, dp_, B, 128, 9216, nullptr, false, s_);
+    } else {  // fused path (mnist_kernels.hip): the batch is generated inside F1
+      const MnistFused f = fused_args();
+      mnist_fused_forward(f, s_);
+      mnist_fused_head(f, s_);
+      mnist_fused_fc1_bwd(f, s_);
+    }
+  } else if (k == 1) {  // conv backward -> bucket 1 (conv grads, 75 KB) complete
+    if (variant_ == 0) {
+      maxpool2d_bwd(dp_, idx_, dc2_, B, 64, 24, 24, 12, 12, s_);
+      relu_bwd(dc2_, c2_, dc2_, (int64_t)B * 36864, s_);
+      conv2d_wgrad(dc2_, a1_, g_ + L::w2, s2, false, s_);
+      bias_grad(dc2_, g_ + L::b2, B, 64, 576, false, s_);
+      conv2d_dgrad(dc2_, p_ + L::w2, da1_, s2, a1_, false, s_);
+      conv2d_wgrad(da1_, x_, g_ + L::w1, s1, false, s_);
+      bias_grad(da1_, g_ + L::b1, B, 32, 676, false, s_);
+    } else {
+      mnist_fused_conv_bwd(fused_args(), s_);
+    }
+  } else {  // optimizer: flat SGD, DDP's 1/world_size average folded into the update
+    const int ws = comm_ ? comm_->world_size() : 1;
+    sgd_step(p_, g_, m_, lr_, 1.f / ws, momentum_, wd_, (int64_t)L::total, false, s_);
   }
-  reducer_->finalize(s_);
-  sgd_step(p_, g_, m_, lr_, 1.f / ws, momentum_, wd_, (int64_t)L::total, false, s_);
+}
+
+void MnistEngine::launch_step() {
+  reducer_->prepare();
+  segment(0);
+  reducer_->mark_bucket_ready(0, s_);  // fc grads all-reduce on the side stream ...
+  segment(1);                          // ... overlapped with the whole conv backward
+  reducer_->mark_bucket_ready(1, s_);
+  reducer_->finalize(s_);              // compute stream waits for the comm stream
+  segment(2);
 }
 
 void MnistEngine::step() { launch_step(); }
 
-void MnistEngine::capture() {
-  if (exec_) return;
-  MX_HIP_CHECK(hipStreamSynchronize(s_));
+hipGraphExec_t MnistEngine::capture_fn(const std::function<void()>& fn, hipGraph_t* g) {
   MX_HIP_CHECK(hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal));
   try {
-    launch_step();
+    fn();
   } catch (...) {
-    hipGraph_t g;
-    hipStreamEndCapture(s_, &g);
-    if (g) hipGraphDestroy(g);
+    hipGraph_t tmp = nullptr;
+    hipStreamEndCapture(s_, &tmp);
+    if (tmp) hipGraphDestroy(tmp);
     throw;
   }
-  MX_HIP_CHECK(hipStreamEndCapture(s_, &graph_));
-  MX_HIP_CHECK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
-  MX_HIP_CHECK(hipGraphUpload(exec_, s_));
+  MX_HIP_CHECK(hipStreamEndCapture(s_, g));
+  hipGraphExec_t exec = nullptr;
+  MX_HIP_CHECK(hipGraphInstantiate(&exec, *g, nullptr, nullptr, 0));
+  MX_HIP_CHECK(hipGraphUpload(exec, s_));
+  return exec;
+}
+
+void MnistEngine::capture(int mode) {
+  if (exec_ || seg_exec_[0]) return;
+  const bool multi = comm_ && comm_->world_size() > 1;
+  if (mode < 0) mode = multi ? 2 : 1;  // default: collectives stay outside graphs when ws > 1
+  MX_HIP_CHECK(hipStreamSynchronize(s_));
+  graph_mode_ = mode;
+  if (mode == 1) {  // whole step, RCCL collectives included (one launch per step)
+    exec_ = capture_fn([this] { launch_step(); }, &graph_);
+  } else if (mode == 2) {  // three compute graphs; the two collectives are issued eagerly between them
+    for (int k = 0; k < 3; ++k) seg_exec_[k] = capture_fn([this, k] { segment(k); }, &seg_graph_[k]);
+  }
 }
 
 void MnistEngine::replay(int n) {
   for (int i = 0; i < n; ++i) {
-    if (exec_) MX_HIP_CHECK(hipGraphLaunch(exec_, s_));
-    else launch_step();
+    if (graph_mode_ == 1 && exec_) {
+      MX_HIP_CHECK(hipGraphLaunch(exec_, s_));
+    } else if (graph_mode_ == 2 && seg_exec_[0]) {
+      reducer_->prepare();
+      MX_HIP_CHECK(hipGraphLaunch(seg_exec_[0], s_));
+      reducer_->mark_bucket_ready(0, s_);
+      MX_HIP_CHECK(hipGraphLaunch(seg_exec_[1], s_));
+      reducer_->mark_bucket_ready(1, s_);
+      reducer_->finalize(s_);
+      MX_HIP_CHECK(hipGraphLaunch(seg_exec_[2], s_));
+    } else {
+      launch_step();
+    }
   }
 }
 

@@ -15,9 +15,11 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <memory>
 
 #include "comm.h"
+#include "mnist_kernels.h"
 #include "reducer.h"
 
 namespace mx {
@@ -37,8 +39,12 @@ class MnistEngine {
   ~MnistEngine();
 
   void step();               // one training step, eager launches on stream()
-  void capture();            // record the step into a hipGraph (call after a warm-up step)
-  void replay(int n);        // n graph launches (falls back to step() if not captured)
+  // Record the step into hipGraph(s) (call after a warm-up step).  mode 1: one graph for the
+  // whole step, RCCL collectives captured inside; mode 2: three compute graphs with the two
+  // bucket all-reduces issued eagerly between them; -1: 1 when world_size == 1, else 2.
+  void capture(int mode = -1);
+  void replay(int n);        // n steps via the captured graph(s) (eager if not captured)
+  int graph_mode() const { return graph_mode_; }
   void forward_only(uintptr_t x, uintptr_t logits, int B);  // eval helper (no grads)
   void sync();
   uintptr_t stream() const { return reinterpret_cast<uintptr_t>(s_); }
@@ -46,10 +52,16 @@ class MnistEngine {
   uintptr_t y_ptr() const { return reinterpret_cast<uintptr_t>(y_); }
   void set_external_batch(bool on) { external_batch_ = on; }
   float last_comm_ms() { return reducer_ ? reducer_->last_comm_ms() : 0.f; }
-  bool captured() const { return exec_ != nullptr; }
+  bool captured() const { return exec_ != nullptr || seg_exec_[0] != nullptr; }
 
  private:
   void launch_step();
+  void segment(int k);
+  MnistFused fused_args() const;
+  hipGraphExec_t capture_fn(const std::function<void()>& fn, hipGraph_t* g);
+  hipGraph_t seg_graph_[3] = {nullptr, nullptr, nullptr};
+  hipGraphExec_t seg_exec_[3] = {nullptr, nullptr, nullptr};
+  int graph_mode_ = 0;
   void fwd(const float* x, float* logits_out, int B);
   int B_;
   float *p_, *g_, *m_;

@@ -12,6 +12,8 @@ The parameters are one flat fp32 buffer in MnistCNN ``state_dict`` order, so
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import native
@@ -28,9 +30,10 @@ _LAYOUT = [  # (name, shape) in state_dict order == flat offsets of MnistLayout 
 class FusedMnistTrainer:
     def __init__(self, batch: int = 64, device: torch.device | int = 0, comm=None, seed: int = 1, lr: float = 0.1,
                  momentum: float = 0.9, weight_decay: float = 1e-4, variant: int = 1, use_graph: bool = True,
-                 init_model: MnistCNN | None = None):
+                 init_model: MnistCNN | None = None, graph_mode: int | None = None):
         C = native()
         self.C = C
+        self.graph_mode = graph_mode
         self.device = torch.device("cuda", device) if isinstance(device, int) else device
         self.batch = batch
         self.comm = comm
@@ -68,7 +71,10 @@ class FusedMnistTrainer:
         if self.use_graph and not self.eng.captured:
             self.eng.step()          # warm-up: lazy RCCL/kernel init outside the capture
             self.eng.sync()
-            self.eng.capture()
+            # MXDDP_GRAPH_MODE: 1 = one graph incl. RCCL collectives, 2 = compute graphs with
+            # eager collectives in between; default 1 at world_size 1, 2 otherwise.
+            mode = self.graph_mode if self.graph_mode is not None else int(os.environ.get("MXDDP_GRAPH_MODE", "-1"))
+            self.eng.capture(mode)
             n -= 1
             self.steps += 1
         if n > 0:

@@ -50,8 +50,8 @@ def get_spec(name: str) -> ModelSpec:
         raise ValueError(f"unknown model {name!r}; choose from {sorted(MODELS)}") from None
 
 
-def build_model(name: str) -> nn.Module:
-    return get_spec(name).factory()
+def build_model(name: str, **kwargs) -> nn.Module:
+    return get_spec(name).factory(**kwargs)
 
 
 __all__ = ["MODELS", "ModelSpec", "get_spec", "build_model", "MnistCNN", "KerasCNN", "MLP", "PyramidNet",

@@ -24,6 +24,27 @@ __all__ = [
 ]
 
 
+_TORCH_REFERENCE = False  # bench/debug only: route GPU tensors through stock PyTorch ops
+
+
+class torch_reference_mode:
+    """Context manager: run GPU tensors through stock PyTorch-ROCm ops instead of the mxddp
+    kernels.  Used only by ``bench.py --impl torch`` to measure the baseline; never a default."""
+
+    def __enter__(self):
+        global _TORCH_REFERENCE
+        self._prev, _TORCH_REFERENCE = _TORCH_REFERENCE, True
+        return self
+
+    def __exit__(self, *exc):
+        global _TORCH_REFERENCE
+        _TORCH_REFERENCE = self._prev
+
+
+def _native(t: torch.Tensor) -> bool:
+    return t.is_cuda and not _TORCH_REFERENCE
+
+
 def stream_of(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
@@ -95,7 +116,7 @@ class _Conv2d(torch.autograd.Function):
 
 def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, relu=False):
     stride, padding, dilation = _pair(stride), _pair(padding), _pair(dilation)
-    if x.is_cuda:
+    if _native(x):
         return _Conv2d.apply(x, w, b, stride, padding, dilation, relu)
     y = F.conv2d(x, w, b, stride, padding, dilation)
     return F.relu(y) if relu else y
@@ -148,7 +169,7 @@ class _Linear(torch.autograd.Function):
 
 
 def linear(x, w, b=None, relu=False):
-    if x.is_cuda:
+    if _native(x):
         return _Linear.apply(x, w, b, relu)
     y = F.linear(x, w, b)
     return F.relu(y) if relu else y
@@ -174,7 +195,7 @@ class _Relu(torch.autograd.Function):
 
 
 def relu(x):
-    return _Relu.apply(x) if x.is_cuda else F.relu(x)
+    return _Relu.apply(x) if _native(x) else F.relu(x)
 
 
 # --------------------------------------------------------------------------- pooling
@@ -217,7 +238,7 @@ def max_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False):
     k = _pair(kernel_size)
     s = _pair(stride if stride is not None else kernel_size)
     p = _pair(padding)
-    if x.is_cuda:
+    if _native(x):
         return _MaxPool2d.apply(x, k, s, p, ceil_mode)
     return F.max_pool2d(x, k, s, p, ceil_mode=ceil_mode)
 
@@ -249,7 +270,7 @@ def avg_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False):
     k = _pair(kernel_size)
     s = _pair(stride if stride is not None else kernel_size)
     p = _pair(padding)
-    if x.is_cuda:
+    if _native(x):
         return _AvgPool2d.apply(x, k, s, p, ceil_mode)
     return F.avg_pool2d(x, k, s, p, ceil_mode=ceil_mode)
 
@@ -294,7 +315,7 @@ class _BatchNorm(torch.autograd.Function):
 
 
 def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum=0.1, eps=1e-5, relu=False):
-    if x.is_cuda:
+    if _native(x):
         return _BatchNorm.apply(x, gamma, beta, running_mean, running_var, training, momentum, eps, relu)
     y = F.batch_norm(x, running_mean, running_var, gamma, beta, training, momentum, eps)
     return F.relu(y) if relu else y
@@ -327,7 +348,7 @@ class _CrossEntropy(torch.autograd.Function):
 
 def cross_entropy(logits, target, return_correct=False):
     """Mean cross-entropy = NLL(log_softmax(logits)); optionally also #correct (on device)."""
-    if logits.is_cuda:
+    if _native(logits):
         loss, correct = _CrossEntropy.apply(logits, target)
     else:
         loss = F.cross_entropy(logits, target)
@@ -360,7 +381,7 @@ class _ShortcutAdd(torch.autograd.Function):
 
 def shortcut_pad_add(out, x, stride):
     """out + AvgPool2d(2,2,ceil)(F.pad(x, channels -> out.C)) (pytorch/model.py:17-21,49)."""
-    if out.is_cuda:
+    if _native(out):
         return _ShortcutAdd.apply(out, x, stride)
     sc = F.pad(x, (0, 0, 0, 0, 0, out.shape[1] - x.shape[1]))
     if stride == 2:

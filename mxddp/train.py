@@ -70,6 +70,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--resume", type=str, default="", help="training-state file (mxddp_state_<rank>.pt) to resume")
     p.add_argument("--save-every", type=int, default=0, help="write the full training state every N epochs")
     p.add_argument("--eval", action="store_true", help="evaluate on the test split after training")
+    p.add_argument("--eval-every", type=int, default=0, help="evaluate every N epochs (Chainer Evaluator)")
+    p.add_argument("--mlp-units", type=int, default=1000, help="mlp hidden width (Chainer --unit)")
     p.add_argument("--metrics-jsonl", type=str, default="", help="append JSONL metrics here")
     p.add_argument("--max-steps", type=int, default=0, help="stop after this many steps (0 = full epochs)")
     p.add_argument("--sync-set-epoch", action="store_true", default=True)
@@ -143,6 +145,10 @@ def main(argv=None) -> int:
 
 
 # ====================================================================================== helpers
+def _model_kwargs(args, spec) -> dict:
+    return {"n_units": args.mlp_units} if spec.name == "mlp" else {}
+
+
 def _make_opt(name, flat, lr, mom, wd, spec):
     from .optim import SGD, Adam
 
@@ -192,18 +198,28 @@ def evaluate(model, loader, device) -> tuple[float, float]:
     return (tot_loss / max(n, 1)).item(), (100.0 * tot_corr / max(n, 1)).item()
 
 
-def _maybe_eval(args, inf, spec, model, bs, mw):
-    if not args.eval:
+def _maybe_eval(args, inf, spec, model, bs, mw, epoch=None, force=False):
+    """Held-out evaluation (TF2 model.evaluate, Chainer Evaluator).  Under DDP each rank
+    evaluates its shard of the test set and the sums are all-reduced (ChainerMN
+    create_multi_node_evaluator semantics, chainer/train_mnist_multi.py:102-104)."""
+    periodic = epoch is not None and args.eval_every and epoch % args.eval_every == 0
+    if not (force and args.eval) and not periodic:
         return
     from .data import build_loader
+    from .parallel import comm as C
 
-    loader, kind = build_loader(spec.dataset, args.data, args.dataset_dir, args.test_batch_size, inf.device, 1, 0,
+    ws, rank = (inf.world_size, inf.rank)
+    tb = max(1, min(args.test_batch_size, math.ceil(10000 / ws)))
+    loader, kind = build_loader(spec.dataset, args.data, args.dataset_dir, tb, inf.device, ws, rank,
                                 args.seed + 99, spec.input_shape, spec.num_classes, train=False,
-                                steps=max(1, math.ceil(10000 / args.test_batch_size)))
+                                steps=max(1, math.ceil(10000 / ws / tb)))
     loss, acc = evaluate(model, loader, inf.device)
+    if ws > 1:
+        loss, acc = [v / ws for v in C.all_reduce_sum([loss, acc])]
     if inf.is_main:
-        print(f"Test ({kind}): loss {loss:.4f} | acc {acc:.3f}", flush=True)
-    mw.write(kind="eval", loss=loss, acc=acc)
+        tag = f"epoch {epoch} " if epoch is not None else ""
+        print(f"Test ({kind}) {tag}: loss {loss:.4f} | acc {acc:.3f}", flush=True)
+    mw.write(kind="eval", epoch=epoch, loss=loss, acc=acc)
 
 
 def _save_final(args, inf, mode, state_dict):
@@ -231,7 +247,7 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
 
     dev = inf.device
     torch.manual_seed(args.seed)
-    model = build_model(spec.name).to(dev)
+    model = build_model(spec.name, **_model_kwargs(args, spec)).to(dev)
     if mode == "ddp":
         net = DDP(model, bucket_cap_mb=args.bucket_cap_mb)
         flat = net.flat
@@ -290,12 +306,13 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
         _log_epoch(inf, mode, time.time() - t_epoch)
         if sched:
             sched.step()
+        _maybe_eval(args, inf, spec, model, bs, mw, epoch=epoch)
         if args.save_every and epoch % args.save_every == 0:
             save_training_state(args.train_dir, inf.rank, model.state_dict(), opt.state_dict(),
                                 sched.state_dict() if sched else None, epoch, step)
         if args.max_steps and step >= args.max_steps:
             break
-    _maybe_eval(args, inf, spec, model, bs, mw)
+    _maybe_eval(args, inf, spec, model, bs, mw, force=True)
     _save_final(args, inf, mode, model.state_dict())
 
 
@@ -315,7 +332,7 @@ def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
     else:
         devices = [torch.device("cpu")]
     torch.manual_seed(args.seed)
-    model = build_model(spec.name)
+    model = build_model(spec.name, **_model_kwargs(args, spec))
     group = ReplicaGroup(model, devices, lambda f: _make_opt(opt_name, f, lr, mom, wd, spec))
     scheds = [StepLR(o, args.lr_step_size, args.lr_gamma) for o in group.optimizers] if args.lr_step_size else []
     loader, kind = build_loader(spec.dataset, args.data, args.dataset_dir, bs, devices[0], 1, 0, args.seed,
@@ -350,9 +367,10 @@ def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
         _log_epoch(inf, "single", time.time() - t_epoch)
         for s in scheds:
             s.step()
+        _maybe_eval(args, inf, spec, group.module, bs, mw, epoch=epoch)
         if args.max_steps and step >= args.max_steps:
             break
-    _maybe_eval(args, inf, spec, group.module, bs, mw)
+    _maybe_eval(args, inf, spec, group.module, bs, mw, force=True)
     _save_final(args, inf, "replica", group.module.state_dict())
 
 
@@ -440,7 +458,7 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
         if args.max_steps and step >= args.max_steps:
             break
     model = tr.to_module().to(dev)
-    _maybe_eval(args, inf, spec, model, bs, mw)
+    _maybe_eval(args, inf, spec, model, bs, mw, force=True)
     _save_final(args, inf, mode, tr.state_dict())
 
 

@@ -20,7 +20,7 @@ def _ref_steps(model, xs, ys, steps, lr=0.1, mom=0.9, wd=1e-4):
 
 
 @pytest.mark.parametrize("variant", [0, 1])
-@pytest.mark.parametrize("graph", [False, True])
+@pytest.mark.parametrize("graph", [0, 1, 2])
 def test_fused_engine_matches_reference(cuda, variant, graph):
     from mxddp.engine import FusedMnistTrainer
     from mxddp.models import MnistCNN
@@ -28,7 +28,8 @@ def test_fused_engine_matches_reference(cuda, variant, graph):
     torch.manual_seed(0)
     ref = MnistCNN()  # CPU, torch ops
     B, steps = 32, 4
-    tr = FusedMnistTrainer(batch=B, device=cuda, comm=None, init_model=ref, variant=variant, use_graph=graph)
+    tr = FusedMnistTrainer(batch=B, device=cuda, comm=None, init_model=ref, variant=variant, use_graph=graph > 0,
+                           graph_mode=graph if graph else None)
     xs = [torch.rand(B, 1, 28, 28) for _ in range(steps)]
     ys = [torch.randint(0, 10, (B,)) for _ in range(steps)]
     losses = []
