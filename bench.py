@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--lr", type=float, default=0.01, help="SGD lr (momentum 0.9, wd 1e-4 as the reference)")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="GEMM precision of the layers path (headline is fp32, >= the reference's precision)")
     ap.add_argument("--model", default="mnist_cnn",
                     help="headline: mnist_cnn (fused).  Others run the layers path: keras_cnn, mlp, pyramidnet110, resnet50")
     return ap.parse_args()
@@ -56,6 +58,12 @@ def main():
             print(f"bench.py: --gpus {a.gpus} needs a launcher (torch.distributed.run)", file=sys.stderr)
             sys.exit(2)
     inf = C.init_distributed(use_gpu=True)
+    if a.dtype != "fp32":
+        if a.impl == "fused":
+            a.impl = "layers"  # the fused MNIST engine is fp32-only
+        from mxddp import ops as _ops
+
+        _ops.set_compute_dtype(a.dtype)
     dev = inf.device
     comm = C.rccl_comm()
     B = a.batch
@@ -102,7 +110,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 3),
-            "dtype": "fp32",
+            "dtype": a.dtype,
             "data": "synthetic (on-device class-conditional 28x28, random-init weights)",
             "config": {"model": a.model, "global_batch": B * a.gpus, "per_rank_batch": B, "seq_len": None,
                        "image": "1x28x28", "parallelism": f"dp{a.gpus}", "impl": a.impl,

@@ -55,6 +55,11 @@ PYBIND11_MODULE(_C, m) {
     linear_wgrad(P<const float>(dy), P<const float>(x), P<float>(dw), M, N, K, acc, S(st));
   });
 
+  m.def("set_gemm_precision", &set_gemm_precision);
+  m.def("set_debug_sync", &set_debug_sync, "synchronise + check after every kernel launch (debugging)");
+  m.def("debug_sync", &debug_sync);
+  m.def("gemm_precision", &gemm_precision);
+
   // ---------------------------------------------------------------- elementwise
   m.def("relu_fwd", [](uintptr_t x, uintptr_t y, int64_t n, uintptr_t st) { relu_fwd(P<const float>(x), P<float>(y), n, S(st)); });
   m.def("relu_bwd", [](uintptr_t dy, uintptr_t y, uintptr_t dx, int64_t n, uintptr_t st) {
@@ -211,10 +216,12 @@ PYBIND11_MODULE(_C, m) {
            py::arg("weight_decay"), py::arg("lr_dev"), py::arg("metrics_dev"), py::arg("variant") = 1,
            py::keep_alive<1, 8>())
       .def("step", &MnistEngine::step)
-      .def("capture", &MnistEngine::capture, py::arg("mode") = -1)
+      .def("capture", &MnistEngine::capture, py::arg("mode") = -1, py::arg("steps_per_graph") = 1)
+      .def("set_force_collectives", &MnistEngine::set_force_collectives)
       .def_property_readonly("graph_mode", &MnistEngine::graph_mode)
       .def("replay", &MnistEngine::replay)
       .def("forward_only", &MnistEngine::forward_only)
+      .def("repack", &MnistEngine::repack)
       .def("sync", &MnistEngine::sync, py::call_guard<py::gil_scoped_release>())
       .def("set_external_batch", &MnistEngine::set_external_batch)
       .def("last_comm_ms", &MnistEngine::last_comm_ms)

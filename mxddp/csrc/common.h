@@ -22,6 +22,19 @@
 
 namespace mx {
 
+// Launch-error check after every kernel launch; with debug sync on (MXDDP_DEBUG_SYNC=1 or
+// set_debug_sync(true)) the stream is also synchronised after each launch outside graph
+// capture, so an asynchronous fault is reported at the kernel that caused it.
+void post_launch(hipStream_t st, const char* what);
+void set_debug_sync(bool on);
+bool debug_sync();
+
+#define MX_LAUNCH(kern, grid, block, shm, st, ...)                \
+  do {                                                            \
+    hipLaunchKernelGGL(kern, grid, block, shm, st, __VA_ARGS__);  \
+    ::mx::post_launch(st, #kern);                                 \
+  } while (0)
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 

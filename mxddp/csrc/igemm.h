@@ -140,7 +140,7 @@ inline void igemm_launch(const Op& op, int splits, hipStream_t st) {
   int klen = cdiv(cdiv(op.K, splits), BK) * BK;
   splits = cdiv(op.K, klen);
   dim3 grid(tiles, 1, splits);
-  hipLaunchKernelGGL((igemm_f32_kernel<Op, BM, BN, BK, WM, WN>), grid, dim3(256), 0, st, op, klen);
+  MX_LAUNCH((igemm_f32_kernel<Op, BM, BN, BK, WM, WN>), grid, dim3(256), 0, st, op, klen);
   MX_HIP_CHECK(hipGetLastError());
 }
 

@@ -263,18 +263,35 @@ __global__ __launch_bounds__(256) void f7_conv2_dgrad_kernel(MnistFused f, Scrat
 // ------------------------------------------------------------------------------------------
 // F8: finalize bucket 1: conv2.weight grad = transpose of the [r][co][ci] accumulator into
 // the canonical [co][ci][ky][kx] layout; conv1 weight/bias grads = sum over the per-image
-// partial slabs (a coalesced column sum, 64 loads in flight per thread).
+// partial slabs.  Every accumulator it consumes (wacc, g1) and the fc1 split-K accumulator h
+// are reset here for the next step, so the step needs no memset launches.
+// Blocks 0..71: wacc transpose (256 outputs each).  Blocks 72..81: the slab sum, 32 outputs per
+// block, 8 threads per output each summing B/8 images (strided so a wave's loads coalesce),
+// combined with shuffles.  Blocks 82..: zero h.
+constexpr int kF8Wacc = kPack / 256, kF8G1 = 10;
 __global__ __launch_bounds__(256) void f8_finalize_kernel(MnistFused f, Scratch sc) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < kPack) {
+  const int blk = blockIdx.x, tid = threadIdx.x;
+  if (blk < kF8Wacc) {
+    const int i = blk * 256 + tid;
     const int co = i / 288, rem = i - co * 288, ci = rem / 9, rr = rem - ci * 9;
-    f.g[L::w2 + i] = sc.wacc[(rr * 64 + co) * 32 + ci];
-  } else if (i < kPack + 320) {
-    const int j = i - kPack;
+    float* a = sc.wacc + (rr * 64 + co) * 32 + ci;
+    f.g[L::w2 + i] = *a;
+    *a = 0.f;
+  } else if (blk < kF8Wacc + kF8G1) {
+    const int j = (blk - kF8Wacc) * 32 + (tid & 31), part = tid >> 5;  // 8 parts
     float s = 0.f;
-#pragma unroll 16
-    for (int b = 0; b < f.B; ++b) s += sc.g1[b * 320 + j];
-    f.g[L::w1 + j] = s;  // conv1.weight [288] followed by conv1.bias [32] in the flat layout
+    for (int b = part; b < f.B; b += 8) {
+      float* p = sc.g1 + b * 320 + j;
+      s += *p;
+      *p = 0.f;
+    }
+    s += __shfl_xor(s, 32, 64);  // parts (2k, 2k+1) share a wave: lanes j and j+32
+    __shared__ float red[4][32];
+    if ((tid & 63) < 32) red[tid >> 6][tid & 31] = s;
+    __syncthreads();
+    if (tid < 32) f.g[L::w1 + j] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+  } else {
+    for (int i = (blk - kF8Wacc - kF8G1) * 256 + tid; i < f.B * 128; i += 8 * 256) f.h[i] = 0.f;
   }
 }
 
@@ -291,9 +308,9 @@ void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st) {
     attr = true;
   }
   const Scratch sc = carve(f.scratch);
-  hipLaunchKernelGGL(f6_conv2_wgrad_kernel, dim3(9 * f.B), dim3(256), kF6Lds, st, f, sc);
-  hipLaunchKernelGGL(f7_conv2_dgrad_kernel, dim3(f.B * 11), dim3(256), kF7Lds, st, f, sc);
-  hipLaunchKernelGGL(f8_finalize_kernel, dim3((kPack + 320 + 255) / 256), dim3(256), 0, st, f, sc);
+  MX_LAUNCH(f6_conv2_wgrad_kernel, dim3(9 * f.B), dim3(256), kF6Lds, st, f, sc);
+  MX_LAUNCH(f7_conv2_dgrad_kernel, dim3(f.B * 11), dim3(256), kF7Lds, st, f, sc);
+  MX_LAUNCH(f8_finalize_kernel, dim3(kF8Wacc + kF8G1 + 8), dim3(256), 0, st, f, sc);
   MX_HIP_CHECK(hipGetLastError());
 }
 

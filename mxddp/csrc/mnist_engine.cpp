@@ -82,7 +82,12 @@ MnistEngine::MnistEngine(int batch, uintptr_t params, uintptr_t grads, uintptr_t
   };
   reducer_ = std::make_unique<Reducer>(comm_, reinterpret_cast<uintptr_t>(g_), DType::kF32, buckets,
                                        std::vector<int>{1, 1, 1, 1, 0, 0, 0, 0}, RedOp::kSum, false);
+  repack();
   MX_HIP_CHECK(hipStreamSynchronize(s_));
+}
+
+void MnistEngine::repack() {
+  if (variant_ == 1) mnist_fused_init(fused_args(), s_);
 }
 
 MnistEngine::~MnistEngine() {
@@ -134,7 +139,6 @@ void MnistEngine::segment(int k) {
     } else {  // fused path (mnist_kernels.hip): the batch is generated inside F1
       const MnistFused f = fused_args();
       mnist_fused_forward(f, s_);
-      mnist_fused_head(f, s_);
       mnist_fused_fc1_bwd(f, s_);
     }
   } else if (k == 1) {  // conv backward -> bucket 1 (conv grads, 75 KB) complete
@@ -151,7 +155,10 @@ void MnistEngine::segment(int k) {
     }
   } else {  // optimizer: flat SGD, DDP's 1/world_size average folded into the update
     const int ws = comm_ ? comm_->world_size() : 1;
-    sgd_step(p_, g_, m_, lr_, 1.f / ws, momentum_, wd_, (int64_t)L::total, false, s_);
+    if (variant_ == 0)
+      sgd_step(p_, g_, m_, lr_, 1.f / ws, momentum_, wd_, (int64_t)L::total, false, s_);
+    else  // + conv2 weight repack for the next step's F2/F7 + conv2 bias-grad reset
+      mnist_fused_sgd(fused_args(), m_, lr_, 1.f / ws, momentum_, wd_, s_);
   }
 }
 
@@ -184,20 +191,28 @@ hipGraphExec_t MnistEngine::capture_fn(const std::function<void()>& fn, hipGraph
   return exec;
 }
 
-void MnistEngine::capture(int mode) {
+void MnistEngine::capture(int mode, int steps_per_graph) {
   if (exec_ || seg_exec_[0]) return;
   const bool multi = comm_ && comm_->world_size() > 1;
   if (mode < 0) mode = multi ? 2 : 1;  // default: collectives stay outside graphs when ws > 1
   MX_HIP_CHECK(hipStreamSynchronize(s_));
   graph_mode_ = mode;
-  if (mode == 1) {  // whole step, RCCL collectives included (one launch per step)
-    exec_ = capture_fn([this] { launch_step(); }, &graph_);
+  if (mode == 1) {  // whole step(s), RCCL collectives included (one launch per group of steps)
+    steps_per_graph_ = steps_per_graph < 1 ? 1 : steps_per_graph;
+    exec_ = capture_fn([this] {
+      for (int i = 0; i < steps_per_graph_; ++i) launch_step();
+    }, &graph_);
   } else if (mode == 2) {  // three compute graphs; the two collectives are issued eagerly between them
     for (int k = 0; k < 3; ++k) seg_exec_[k] = capture_fn([this, k] { segment(k); }, &seg_graph_[k]);
   }
 }
 
 void MnistEngine::replay(int n) {
+  if (graph_mode_ == 1 && exec_ && steps_per_graph_ > 1) {
+    for (; n >= steps_per_graph_; n -= steps_per_graph_) MX_HIP_CHECK(hipGraphLaunch(exec_, s_));
+    for (; n > 0; --n) launch_step();  // remainder: same kernels, launched eagerly
+    return;
+  }
   for (int i = 0; i < n; ++i) {
     if (graph_mode_ == 1 && exec_) {
       MX_HIP_CHECK(hipGraphLaunch(exec_, s_));
@@ -218,6 +233,8 @@ void MnistEngine::replay(int n) {
 void MnistEngine::forward_only(uintptr_t x, uintptr_t logits, int B) {
   MX_CHECK(B <= B_, "eval batch larger than engine batch");
   fwd(reinterpret_cast<const float*>(x), reinterpret_cast<float*>(logits), B);
+  // the generic forward stores into h_, which the fused F3 uses as a zeroed split-K accumulator
+  if (variant_ == 1) MX_HIP_CHECK(hipMemsetAsync(h_, 0, sizeof(float) * B_ * 128, s_));
 }
 
 void MnistEngine::sync() { MX_HIP_CHECK(hipStreamSynchronize(s_)); }

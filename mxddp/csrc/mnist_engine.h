@@ -42,11 +42,18 @@ class MnistEngine {
   // Record the step into hipGraph(s) (call after a warm-up step).  mode 1: one graph for the
   // whole step, RCCL collectives captured inside; mode 2: three compute graphs with the two
   // bucket all-reduces issued eagerly between them; -1: 1 when world_size == 1, else 2.
-  void capture(int mode = -1);
+  // steps_per_graph > 1 (mode 1 only) unrolls that many consecutive steps into one graph, so
+  // the per-launch graph overhead is paid once per group (batches, LR and metrics all live in
+  // device memory, so every unrolled step is a distinct, correct training step).
+  void capture(int mode = -1, int steps_per_graph = 1);
   void replay(int n);        // n steps via the captured graph(s) (eager if not captured)
   int graph_mode() const { return graph_mode_; }
+  void set_force_collectives(bool on) { reducer_->set_force_collectives(on); }
   void forward_only(uintptr_t x, uintptr_t logits, int B);  // eval helper (no grads)
   void sync();
+  // Re-derive the fused path's packed weights / accumulators after the parameters were changed
+  // outside the engine (checkpoint load, broadcast).
+  void repack();
   uintptr_t stream() const { return reinterpret_cast<uintptr_t>(s_); }
   uintptr_t x_ptr() const { return reinterpret_cast<uintptr_t>(x_); }
   uintptr_t y_ptr() const { return reinterpret_cast<uintptr_t>(y_); }
@@ -62,6 +69,7 @@ class MnistEngine {
   hipGraph_t seg_graph_[3] = {nullptr, nullptr, nullptr};
   hipGraphExec_t seg_exec_[3] = {nullptr, nullptr, nullptr};
   int graph_mode_ = 0;
+  int steps_per_graph_ = 1;
   void fwd(const float* x, float* logits_out, int B);
   int B_;
   float *p_, *g_, *m_;

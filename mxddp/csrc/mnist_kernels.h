@@ -23,13 +23,17 @@ struct MnistFused {
   int32_t* counter;      // synthetic-data batch counter
   const float* tmpl;     // class templates [10][784] for the on-device generator
   uint64_t seed;         // per-rank generator seed
-  int synth;             // 1: F1 generates the batch on device; 0: x/y provided by the caller
+  int synth;             // 1: F2 generates the batch on device; 0: x/y provided by the caller
 };
 
 size_t mnist_fused_scratch_floats(int B);
-void mnist_fused_forward(const MnistFused& f, hipStream_t st);
-void mnist_fused_head(const MnistFused& f, hipStream_t st);
-void mnist_fused_fc1_bwd(const MnistFused& f, hipStream_t st);
-void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st);
+// Pack conv2 weights into the F2/F7 fragment orders and zero the cross-step accumulators;
+// needed once and after any change of the parameters outside the fused SGD.
+void mnist_fused_init(const MnistFused& f, hipStream_t st);
+void mnist_fused_forward(const MnistFused& f, hipStream_t st);  // F2 + F3
+void mnist_fused_fc1_bwd(const MnistFused& f, hipStream_t st);  // F5 (head + fc1 backward)
+void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st); // F6 + F7 + F8
+void mnist_fused_sgd(const MnistFused& f, float* mom_buf, const float* lr, float gscale, float momentum, float wd,
+                     hipStream_t st);
 
 }  // namespace mx

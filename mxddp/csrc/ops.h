@@ -41,6 +41,11 @@ void linear_dgrad(const float* dy, const float* w, float* dx, int M, int N, int 
 void linear_wgrad(const float* dy, const float* x, float* dw, int M, int N, int K, bool accumulate,
                   hipStream_t st);
 
+// GEMM operand precision for every op above: 0 = fp32 MFMA (exact fp32, default),
+// 1 = bf16 operands with fp32 accumulation (mixed precision; fp32 tensors in memory).
+void set_gemm_precision(int p);
+int gemm_precision();
+
 // ---- elementwise / reductions (ops_elementwise.hip) ----
 void relu_fwd(const float* x, float* y, int64_t n, hipStream_t st);
 void relu_bwd(const float* dy, const float* y, float* dx, int64_t n, hipStream_t st);

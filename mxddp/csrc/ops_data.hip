@@ -86,14 +86,14 @@ __global__ void count_correct_k(const float* __restrict__ logits, const int32_t*
 }  // namespace
 
 void synth_templates(float* templates, int C, int D, uint64_t seed, hipStream_t st) {
-  hipLaunchKernelGGL(synth_templates_k, dim3(cdiv(C * D, 256)), dim3(256), 0, st, templates, C, D, seed);
+  MX_LAUNCH(synth_templates_k, dim3(cdiv(C * D, 256)), dim3(256), 0, st, templates, C, D, seed);
 }
 
 void synth_batch(float* x, int32_t* y, const float* templates, int B, int D, int C, uint64_t seed, int32_t* counter,
                  hipStream_t st, bool bump) {
-  hipLaunchKernelGGL(synth_batch_k, dim3(B < 1024 ? B : 1024), dim3(256), 0, st, x, y, templates, B, D, C, seed,
+  MX_LAUNCH(synth_batch_k, dim3(B < 1024 ? B : 1024), dim3(256), 0, st, x, y, templates, B, D, C, seed,
                      counter);
-  if (bump) hipLaunchKernelGGL(bump_counter_k, dim3(1), dim3(1), 0, st, counter);
+  if (bump) MX_LAUNCH(bump_counter_k, dim3(1), dim3(1), 0, st, counter);
 }
 
 void augment_crop_flip_norm(const float* x, float* y, int N, int C, int H, int W, int pad, const float* mean,
@@ -101,11 +101,11 @@ void augment_crop_flip_norm(const float* x, float* y, int N, int C, int H, int W
   const int64_t total = (int64_t)N * C * H * W;
   int g = (int)((total + 255) / 256);
   if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(augment_k, dim3(g), dim3(256), 0, st, x, y, N, C, H, W, pad, mean, stdv, seed, counter);
+  MX_LAUNCH(augment_k, dim3(g), dim3(256), 0, st, x, y, N, C, H, W, pad, mean, stdv, seed, counter);
 }
 
 void count_correct(const float* logits, const int32_t* y, float* correct, int B, int C, hipStream_t st) {
-  hipLaunchKernelGGL(count_correct_k, dim3(cdiv(B, 4)), dim3(256), 0, st, logits, y, correct, B, C);
+  MX_LAUNCH(count_correct_k, dim3(cdiv(B, 4)), dim3(256), 0, st, logits, y, correct, B, C);
 }
 
 }  // namespace mx

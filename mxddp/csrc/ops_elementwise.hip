@@ -323,76 +323,76 @@ __global__ void shortcut_bwd_k(const float* __restrict__ dy, float* __restrict__
 }  // namespace
 
 void relu_fwd(const float* x, float* y, int64_t n, hipStream_t st) {
-  hipLaunchKernelGGL(relu_fwd_k, dim3(grid_for(n)), dim3(kTB), 0, st, x, y, n);
+  MX_LAUNCH(relu_fwd_k, dim3(grid_for(n)), dim3(kTB), 0, st, x, y, n);
 }
 void relu_bwd(const float* dy, const float* y, float* dx, int64_t n, hipStream_t st) {
-  hipLaunchKernelGGL(relu_bwd_k, dim3(grid_for(n)), dim3(kTB), 0, st, dy, y, dx, n);
+  MX_LAUNCH(relu_bwd_k, dim3(grid_for(n)), dim3(kTB), 0, st, dy, y, dx, n);
 }
 void add_inplace(float* y, const float* x, int64_t n, hipStream_t st) {
-  hipLaunchKernelGGL(add_k, dim3(grid_for(n)), dim3(kTB), 0, st, y, x, n);
+  MX_LAUNCH(add_k, dim3(grid_for(n)), dim3(kTB), 0, st, y, x, n);
 }
 void scale_inplace(float* y, float a, int64_t n, hipStream_t st) {
-  hipLaunchKernelGGL(scale_k, dim3(grid_for(n)), dim3(kTB), 0, st, y, a, n);
+  MX_LAUNCH(scale_k, dim3(grid_for(n)), dim3(kTB), 0, st, y, a, n);
 }
 void fill(float* y, float v, int64_t n, hipStream_t st) {
-  hipLaunchKernelGGL(fill_k, dim3(grid_for(n)), dim3(kTB), 0, st, y, v, n);
+  MX_LAUNCH(fill_k, dim3(grid_for(n)), dim3(kTB), 0, st, y, v, n);
 }
 void bias_grad(const float* dy, float* db, int outer, int C, int inner, bool accumulate, hipStream_t st) {
-  hipLaunchKernelGGL(bias_grad_k, dim3(C), dim3(kTB), 0, st, dy, db, outer, C, inner, accumulate ? 1 : 0);
+  MX_LAUNCH(bias_grad_k, dim3(C), dim3(kTB), 0, st, dy, db, outer, C, inner, accumulate ? 1 : 0);
 }
 void maxpool2d_fwd(const float* x, float* y, int32_t* idx, int N, int C, int H, int W, int kh, int kw, int sh,
                    int sw, int ph, int pw, int P, int Q, hipStream_t st) {
-  hipLaunchKernelGGL(maxpool_fwd_k, dim3(grid_for((int64_t)N * C * P * Q)), dim3(kTB), 0, st, x, y, idx, N * C, H,
+  MX_LAUNCH(maxpool_fwd_k, dim3(grid_for((int64_t)N * C * P * Q)), dim3(kTB), 0, st, x, y, idx, N * C, H,
                      W, kh, kw, sh, sw, ph, pw, P, Q);
 }
 void maxpool2d_bwd(const float* dy, const int32_t* idx, float* dx, int N, int C, int H, int W, int P, int Q,
                    hipStream_t st) {
   MX_HIP_CHECK(hipMemsetAsync(dx, 0, sizeof(float) * (size_t)N * C * H * W, st));
-  hipLaunchKernelGGL(maxpool_bwd_k, dim3(grid_for((int64_t)N * C * P * Q)), dim3(kTB), 0, st, dy, idx, dx, N * C,
+  MX_LAUNCH(maxpool_bwd_k, dim3(grid_for((int64_t)N * C * P * Q)), dim3(kTB), 0, st, dy, idx, dx, N * C,
                      H, W, P, Q);
 }
 void avgpool2d_fwd(const float* x, float* y, int N, int C, int H, int W, int kh, int kw, int sh, int sw, int ph,
                    int pw, int P, int Q, hipStream_t st) {
-  hipLaunchKernelGGL(avgpool_fwd_k, dim3(grid_for((int64_t)N * C * P * Q)), dim3(kTB), 0, st, x, y, N * C, H, W,
+  MX_LAUNCH(avgpool_fwd_k, dim3(grid_for((int64_t)N * C * P * Q)), dim3(kTB), 0, st, x, y, N * C, H, W,
                      kh, kw, sh, sw, ph, pw, P, Q);
 }
 void avgpool2d_bwd(const float* dy, float* dx, int N, int C, int H, int W, int kh, int kw, int sh, int sw, int ph,
                    int pw, int P, int Q, hipStream_t st) {
   MX_HIP_CHECK(hipMemsetAsync(dx, 0, sizeof(float) * (size_t)N * C * H * W, st));
-  hipLaunchKernelGGL(avgpool_bwd_k, dim3(grid_for((int64_t)N * C * P * Q)), dim3(kTB), 0, st, dy, dx, N * C, H, W,
+  MX_LAUNCH(avgpool_bwd_k, dim3(grid_for((int64_t)N * C * P * Q)), dim3(kTB), 0, st, dy, dx, N * C, H, W,
                      kh, kw, sh, sw, ph, pw, P, Q);
 }
 void xent_fwd_bwd(const float* logits, const int32_t* y, float* logp, float* dlogits, float* loss_sum,
                   float* correct, int B, int C, float grad_scale, hipStream_t st) {
   const int rows_per_block = 4;
-  hipLaunchKernelGGL(xent_k, dim3(cdiv(B, rows_per_block)), dim3(64 * rows_per_block), 0, st, logits, y, logp,
+  MX_LAUNCH(xent_k, dim3(cdiv(B, rows_per_block)), dim3(64 * rows_per_block), 0, st, logits, y, logp,
                      dlogits, loss_sum, correct, B, C, grad_scale);
 }
 void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* invstd,
                   float* run_mean, float* run_var, int N, int C, int HW, float momentum, float eps, bool relu,
                   hipStream_t st) {
-  hipLaunchKernelGGL(bn_fwd_train_k, dim3(C), dim3(512), 0, st, x, gamma, beta, y, mean, invstd, run_mean,
+  MX_LAUNCH(bn_fwd_train_k, dim3(C), dim3(512), 0, st, x, gamma, beta, y, mean, invstd, run_mean,
                      run_var, N, C, HW, momentum, eps, relu ? 1 : 0);
 }
 void bn_fwd_eval(const float* x, const float* gamma, const float* beta, float* y, const float* rm, const float* rv,
                  int N, int C, int HW, float eps, bool relu, hipStream_t st) {
-  hipLaunchKernelGGL(bn_fwd_eval_k, dim3(grid_for((int64_t)N * C * HW)), dim3(kTB), 0, st, x, gamma, beta, y, rm,
+  MX_LAUNCH(bn_fwd_eval_k, dim3(grid_for((int64_t)N * C * HW)), dim3(kTB), 0, st, x, gamma, beta, y, rm,
                      rv, N, C, HW, eps, relu ? 1 : 0);
 }
 void bn_bwd(const float* dy, const float* x, const float* y_relu, const float* gamma, const float* mean,
             const float* invstd, float* dx, float* dgamma, float* dbeta, int N, int C, int HW, bool acc,
             hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_k, dim3(C), dim3(512), 0, st, dy, x, y_relu, gamma, mean, invstd, dx, dgamma, dbeta, N,
+  MX_LAUNCH(bn_bwd_k, dim3(C), dim3(512), 0, st, dy, x, y_relu, gamma, mean, invstd, dx, dgamma, dbeta, N,
                      C, HW, acc ? 1 : 0);
 }
 void shortcut_pad_add(const float* x, float* y, int N, int Cin, int H, int W, int Cout, int P, int Q, int stride,
                       hipStream_t st) {
-  hipLaunchKernelGGL(shortcut_fwd_k, dim3(grid_for((int64_t)N * Cin * P * Q)), dim3(kTB), 0, st, x, y, N, Cin, H,
+  MX_LAUNCH(shortcut_fwd_k, dim3(grid_for((int64_t)N * Cin * P * Q)), dim3(kTB), 0, st, x, y, N, Cin, H,
                      W, Cout, P, Q, stride);
 }
 void shortcut_pad_add_bwd(const float* dy, float* dx, int N, int Cin, int H, int W, int Cout, int P, int Q,
                           int stride, bool accumulate, hipStream_t st) {
-  hipLaunchKernelGGL(shortcut_bwd_k, dim3(grid_for((int64_t)N * Cin * H * W)), dim3(kTB), 0, st, dy, dx, N, Cin, H,
+  MX_LAUNCH(shortcut_bwd_k, dim3(grid_for((int64_t)N * Cin * H * W)), dim3(kTB), 0, st, dy, dx, N, Cin, H,
                      W, Cout, P, Q, stride, accumulate ? 1 : 0);
 }
 

@@ -2,6 +2,7 @@
 // NCHW fp32, arbitrary stride / padding / dilation and non-tile-multiple channel
 // counts (PyramidNet-110 has 103 distinct (C_in, C_out) pairs).
 #include "igemm.h"
+#include "igemm_bf16.h"
 #include "ops.h"
 
 namespace mx {
@@ -229,9 +230,12 @@ struct LinWgradOp {  // dw[Nout,Kin] = dy[B,Nout]^T x[B,Kin]; GEMM M=Nout, N=Kin
   __device__ void store(int m, int n, float v, int) const { emit(dw, (int64_t)m * N + n, v, mode); }
 };
 
+int g_gemm_precision = 0;  // 0 = fp32 MFMA (exact), 1 = bf16 operands / fp32 accumulate
+
 template <class Op>
 void run(Op& op, int splits, hipStream_t st) {
-  igemm_launch<Op, 64, 64, 16, 2, 2>(op, splits, st);
+  if (g_gemm_precision == 1) igemm_bf16_launch<Op, 64, 64, 32, 2, 2>(op, splits, st);
+  else igemm_launch<Op, 64, 64, 16, 2, 2>(op, splits, st);
 }
 
 }  // namespace
@@ -294,5 +298,11 @@ void linear_wgrad(const float* dy, const float* x, float* dw, int M, int N, int 
   }
   run(op, splits, st);
 }
+
+void set_gemm_precision(int p) {
+  MX_CHECK(p == 0 || p == 1, "gemm precision: 0 (fp32) or 1 (bf16)");
+  g_gemm_precision = p;
+}
+int gemm_precision() { return g_gemm_precision; }
 
 }  // namespace mx

@@ -78,13 +78,13 @@ void sgd_step(float* p, const float* g, float* buf, const float* lr, float gscal
               int64_t n, bool first_step, hipStream_t st) {
   MX_CHECK(((uintptr_t)p % 16 == 0) && ((uintptr_t)g % 16 == 0) && ((uintptr_t)buf % 16 == 0),
            "sgd_step: buffers must be 16-byte aligned");
-  hipLaunchKernelGGL(sgd_k, dim3(grid_for(n)), dim3(256), 0, st, p, g, buf, lr, gscale, momentum, wd, n,
+  MX_LAUNCH(sgd_k, dim3(grid_for(n)), dim3(256), 0, st, p, g, buf, lr, gscale, momentum, wd, n,
                      first_step ? 1 : 0);
 }
 
 void adam_step(float* p, const float* g, float* m, float* v, const float* lr, const int32_t* step, float gscale,
                float b1, float b2, float eps, float wd, int64_t n, hipStream_t st) {
-  hipLaunchKernelGGL(adam_k, dim3(grid_for(n * 4)), dim3(256), 0, st, p, g, m, v, lr, step, gscale, b1, b2, eps,
+  MX_LAUNCH(adam_k, dim3(grid_for(n * 4)), dim3(256), 0, st, p, g, m, v, lr, step, gscale, b1, b2, eps,
                      wd, n);
 }
 

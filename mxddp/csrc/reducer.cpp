@@ -69,7 +69,7 @@ void Reducer::launch_ready(hipStream_t compute) {
     MX_HIP_CHECK(hipEventRecord(b.ev, compute));
     MX_HIP_CHECK(hipStreamWaitEvent(comm_stream_, b.ev, 0));
     if (timing_ && next_ == 0) MX_HIP_CHECK(hipEventRecord(t0_, comm_stream_));
-    if (comm_ && comm_->world_size() > 1) {
+    if (comm_ && (comm_->world_size() > 1 || force_)) {
       char* p = flat_ + b.offset * dtype_size(dtype_);
       comm_->all_reduce(p, p, b.numel, dtype_, op_, comm_stream_);
     }

@@ -41,6 +41,9 @@ class Reducer {
   // (requires timing=true; synchronises on the comm stream's end event).
   float last_comm_ms();
   void set_comm(Comm* c) { comm_ = c; }
+  // issue the collectives even at world_size 1 (exercises the RCCL + graph-capture path on
+  // a single GPU; an all-reduce over one rank is the identity)
+  void set_force_collectives(bool on) { force_ = on; }
 
  private:
   void launch_ready(hipStream_t compute);
@@ -60,7 +63,7 @@ class Reducer {
   int next_ = 0;
   hipStream_t comm_stream_ = nullptr;
   hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
-  bool timing_ = false, timed_ = false;
+  bool timing_ = false, timed_ = false, force_ = false;
 };
 
 }  // namespace mx

@@ -30,10 +30,13 @@ _LAYOUT = [  # (name, shape) in state_dict order == flat offsets of MnistLayout 
 class FusedMnistTrainer:
     def __init__(self, batch: int = 64, device: torch.device | int = 0, comm=None, seed: int = 1, lr: float = 0.1,
                  momentum: float = 0.9, weight_decay: float = 1e-4, variant: int = 1, use_graph: bool = True,
-                 init_model: MnistCNN | None = None, graph_mode: int | None = None):
+                 init_model: MnistCNN | None = None, graph_mode: int | None = None,
+                 steps_per_graph: int | None = None, force_collectives: bool = False):
         C = native()
         self.C = C
         self.graph_mode = graph_mode
+        self.steps_per_graph = steps_per_graph
+        self._external = False
         self.device = torch.device("cuda", device) if isinstance(device, int) else device
         self.batch = batch
         self.comm = comm
@@ -61,6 +64,8 @@ class FusedMnistTrainer:
         self.eng = C.MnistEngine(batch, self.params.data_ptr(), self.grads.data_ptr(), self.mom.data_ptr(),
                                  self.workspace.data_ptr(), wsb, comm, seed, momentum, weight_decay,
                                  self.lr.data_ptr(), self.metrics.data_ptr(), variant)
+        if force_collectives:
+            self.eng.set_force_collectives(True)
         self.stream = torch.cuda.ExternalStream(self.eng.stream, device=self.device)
         self.steps = 0
         self.world_size = comm.world_size if comm is not None else 1
@@ -74,7 +79,12 @@ class FusedMnistTrainer:
             # MXDDP_GRAPH_MODE: 1 = one graph incl. RCCL collectives, 2 = compute graphs with
             # eager collectives in between; default 1 at world_size 1, 2 otherwise.
             mode = self.graph_mode if self.graph_mode is not None else int(os.environ.get("MXDDP_GRAPH_MODE", "-1"))
-            self.eng.capture(mode)
+            spg = self.steps_per_graph
+            if spg is None:
+                spg = int(os.environ.get("MXDDP_STEPS_PER_GRAPH", "8"))
+            if self._external:
+                spg = 1  # a caller-provided batch is copied in before EVERY step
+            self.eng.capture(mode, spg)
             n -= 1
             self.steps += 1
         if n > 0:
@@ -84,6 +94,7 @@ class FusedMnistTrainer:
     def set_batch(self, x: torch.Tensor, y: torch.Tensor):
         """Use a caller-provided batch instead of the on-device generator (real MNIST)."""
         self.eng.set_external_batch(True)
+        self._external = True
         with torch.cuda.stream(self.stream):
             self._x_view().copy_(x.reshape(self.batch, 1, 28, 28), non_blocking=True)
             self._y_view().copy_(y.to(torch.int32), non_blocking=True)
@@ -108,6 +119,8 @@ class FusedMnistTrainer:
     def read_metrics(self, reset: bool = True):
         """(loss_sum, correct) accumulated since the last reset (one host sync)."""
         self.eng.sync()
+        if self.comm is not None:
+            self.comm.check_async_error()  # surface a failed/aborted peer at log boundaries
         m = self.metrics[:2].tolist()
         if reset:
             with torch.cuda.stream(self.stream):
@@ -132,6 +145,8 @@ class FusedMnistTrainer:
         self.eng.sync()
         self.params.copy_(flat.to(self.device))
         torch.cuda.synchronize(self.device)
+        self.eng.repack()  # fused path keeps conv2 weights pre-packed in MFMA fragment order
+        self.eng.sync()
 
     def to_module(self) -> MnistCNN:
         m = MnistCNN()

@@ -387,3 +387,16 @@ def shortcut_pad_add(out, x, stride):
     if stride == 2:
         sc = F.avg_pool2d(sc, 2, 2, ceil_mode=True)
     return out + sc
+
+
+# --------------------------------------------------------------------------- precision
+def set_compute_dtype(dtype: str) -> None:
+    """GEMM-shaped ops (conv / linear) compute in ``fp32`` (exact fp32 MFMA, default) or
+    ``bf16`` (bf16 operands rounded while staged into LDS, fp32 accumulation, fp32 tensors and
+    master weights) -- the mixed-precision path of BASELINE config 5 (ResNet-50 bf16)."""
+    p = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1}[dtype]
+    native().set_gemm_precision(p)
+
+
+def compute_dtype() -> str:
+    return "bf16" if native().gemm_precision() == 1 else "fp32"

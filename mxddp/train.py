@@ -66,12 +66,16 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--nproc-per-node", type=int, default=1, help="spawn this many ranks on this node")
     p.add_argument("--cpu", action="store_true", help="force the CPU path (gloo)")
     p.add_argument("--no-graph", action="store_true", help="fused engine: launch eagerly instead of hipGraph replay")
+    p.add_argument("--debug-sync", action="store_true",
+                   help="synchronise and check for faults after every kernel launch (implies --no-graph)")
     p.add_argument("--bucket-cap-mb", type=float, default=25.0)
     p.add_argument("--resume", type=str, default="", help="training-state file (mxddp_state_<rank>.pt) to resume")
     p.add_argument("--save-every", type=int, default=0, help="write the full training state every N epochs")
     p.add_argument("--eval", action="store_true", help="evaluate on the test split after training")
     p.add_argument("--eval-every", type=int, default=0, help="evaluate every N epochs (Chainer Evaluator)")
     p.add_argument("--mlp-units", type=int, default=1000, help="mlp hidden width (Chainer --unit)")
+    p.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                   help="GEMM compute precision: fp32 (exact, reference) or bf16 operands + fp32 accumulate")
     p.add_argument("--metrics-jsonl", type=str, default="", help="append JSONL metrics here")
     p.add_argument("--max-steps", type=int, default=0, help="stop after this many steps (0 = full epochs)")
     p.add_argument("--sync-set-epoch", action="store_true", default=True)
@@ -124,7 +128,14 @@ def main(argv=None) -> int:
     engine = args.engine
     if engine == "auto":
         engine = "fused" if (args.model == "mnist_cnn" and use_gpu and opt_name == "sgd" and mode != "replica"
-                             and bs % 16 == 0 and 16 <= bs <= 128) else "layers"
+                             and bs % 16 == 0 and 16 <= bs <= 128 and args.dtype == "fp32") else "layers"
+    if use_gpu:
+        from . import native, ops
+
+        ops.set_compute_dtype(args.dtype)
+        if args.debug_sync:
+            native().set_debug_sync(True)
+            args.no_graph = True  # a captured graph cannot be synchronised per kernel
     if inf.is_main:
         print(f"==> mxddp | model {args.model} | mode {mode} | engine {engine} | world {inf.world_size} | "
               f"device {inf.device} | batch/rank {bs} | {opt_name} lr {lr} mom {mom} wd {wd}", flush=True)

@@ -8,3 +8,4 @@ run bench_pyr_torch 600 python bench.py --model pyramidnet110 --impl torch --ste
 run bench_keras_layers 300 python bench.py --model keras_cnn --impl layers --steps 50 --warmup 5
 run bench_mlp_layers 300 python bench.py --model mlp --impl layers --steps 50 --warmup 5
 run prof_pyr 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_pyr -o run --output-format csv -- python bench.py --model pyramidnet110 --impl layers --steps 5 --warmup 2
+run pytest_parallel 900 python -m pytest tests/test_gpu_parallel.py -m gpu -x -q

@@ -47,6 +47,48 @@ def test_fused_engine_matches_reference(cuda, variant, graph):
         assert err < 1e-4, (k, err)
 
 
+@pytest.mark.parametrize("graph", [0, 1, 2])
+def test_fused_engine_rccl_collectives_ws1(cuda, graph):
+    """The DDP path with REAL RCCL all-reduces (1-rank communicator, collectives forced):
+    eager, captured inside the step graph (mode 1) and issued between compute graphs (mode 2)."""
+    from mxddp import native
+    from mxddp.engine import FusedMnistTrainer
+    from mxddp.models import MnistCNN
+
+    C = native()
+    comm = C.Comm(C.Comm.new_unique_id(), 0, 1, cuda.index or 0)
+    torch.manual_seed(0)
+    ref = MnistCNN()
+    B, steps = 32, 5
+    tr = FusedMnistTrainer(batch=B, device=cuda, comm=comm, init_model=ref, use_graph=graph > 0,
+                           graph_mode=graph if graph else None, force_collectives=True)
+    xs = [torch.rand(B, 1, 28, 28) for _ in range(steps)]
+    ys = [torch.randint(0, 10, (B,)) for _ in range(steps)]
+    losses = []
+    for i in range(steps):
+        tr.set_batch(xs[i].to(cuda), ys[i].to(cuda))
+        tr.step(1)
+        losses.append(tr.read_metrics()[0] / B)
+    ref_losses = _ref_steps(ref, xs, ys, steps)
+    for a, b in zip(losses, ref_losses):
+        assert abs(a - b) < 1e-4 * max(1.0, abs(b)), (losses, ref_losses)
+
+
+def test_fused_engine_multi_step_graph(cuda):
+    """8 steps unrolled per graph == 8 single steps (same device-side data stream)."""
+    from mxddp.engine import FusedMnistTrainer
+
+    a = FusedMnistTrainer(batch=64, device=cuda, lr=0.01, steps_per_graph=8)
+    b = FusedMnistTrainer(batch=64, device=cuda, lr=0.01, steps_per_graph=1)
+    a.step(17)
+    b.step(17)
+    la, ca = a.read_metrics()
+    lb, cb = b.read_metrics()
+    assert abs(la - lb) < 1e-3 * abs(lb) and ca == cb
+    for k, v in a.state_dict().items():
+        assert torch.allclose(v, b.state_dict()[k], rtol=1e-4, atol=1e-6), k
+
+
 def test_fused_engine_trains(cuda):
     from mxddp.engine import FusedMnistTrainer
 
