@@ -37,6 +37,14 @@ def parse():
                          "torch: stock PyTorch-ROCm DDP (comparison only)")
     ap.add_argument("--variant", type=int, default=1, help="fused kernel variant (0 = generic igemm)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph-mode", type=int, default=None, choices=[0, 1, 2],
+                    help="fused engine: 0 = eager launches, 1 = whole step(s) incl. RCCL in one graph, 2 = compute "
+                         "graphs + eager collectives (default: 1 at world size 1, else autotuned; env MXDDP_GRAPH_MODE)")
+    ap.add_argument("--no-autotune", action="store_true",
+                    help="fused engine, world size > 1: skip timing the launch strategies before the warm-up")
+    ap.add_argument("--steps-per-graph", type=int, default=None, help="fused engine, graph mode 1: steps unrolled per graph")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="fused engine: issue the RCCL bucket all-reduces even at world size 1 (measures the DDP path)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--lr", type=float, default=0.01, help="SGD lr (momentum 0.9, wd 1e-4 as the reference)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
@@ -65,7 +73,7 @@ def main():
 
         _ops.set_compute_dtype(a.dtype)
     dev = inf.device
-    comm = C.rccl_comm()
+    comm = C.rccl_comm(force=a.force_collectives)
     B = a.batch
 
     if a.model != "mnist_cnn" and a.impl == "fused":
@@ -74,8 +82,12 @@ def main():
         from mxddp.engine import FusedMnistTrainer
 
         tr = FusedMnistTrainer(batch=B, device=dev, comm=comm, seed=a.seed, variant=a.variant, lr=a.lr,
-                               use_graph=not a.no_graph)
+                               use_graph=not a.no_graph, graph_mode=a.graph_mode, steps_per_graph=a.steps_per_graph,
+                               force_collectives=a.force_collectives)
         run = tr.step
+        if a.graph_mode is None and not a.no_autotune and tr.eng.reducer_active:
+            tr.step(1)
+            tr.autotune()  # untimed: a few real steps per candidate strategy, before the warm-up
     else:
         run = _layers_or_torch(a, torch, inf, dev, comm, B)
 
@@ -114,7 +126,10 @@ def main():
             "data": "synthetic (on-device class-conditional 28x28, random-init weights)",
             "config": {"model": a.model, "global_batch": B * a.gpus, "per_rank_batch": B, "seq_len": None,
                        "image": "1x28x28", "parallelism": f"dp{a.gpus}", "impl": a.impl,
-                       "graph": (a.impl == "fused" and not a.no_graph)},
+                       "graph": (a.impl == "fused" and not a.no_graph),
+                       **({"graph_mode": tr.eng.graph_mode, "overlap": tr.eng.overlap,
+                           "force_collectives": a.force_collectives, "autotune": tr.tuned}
+                          if a.impl == "fused" else {})},
             **extra,
         }
         print(json.dumps(out), flush=True)

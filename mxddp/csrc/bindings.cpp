@@ -34,10 +34,13 @@ PYBIND11_MODULE(_C, m) {
                CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw), relu, S(st));
   });
   m.def("conv2d_dgrad", [](uintptr_t dy, uintptr_t w, uintptr_t dx, int N, int C, int H, int W, int K, int R, int S_,
-                           int sh, int sw, int ph, int pw, int dh, int dw, uintptr_t mask, bool acc, uintptr_t st) {
+                           int sh, int sw, int ph, int pw, int dh, int dw, uintptr_t mask, bool acc, uintptr_t st,
+                           uintptr_t wt_scratch) {
     conv2d_dgrad(P<const float>(dy), P<const float>(w), P<float>(dx), CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw),
-                 P<const float>(mask), acc, S(st));
-  });
+                 P<const float>(mask), acc, S(st), P<float>(wt_scratch));
+  }, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("N"), py::arg("C"), py::arg("H"), py::arg("W"), py::arg("K"),
+     py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"),
+     py::arg("dw"), py::arg("mask"), py::arg("acc"), py::arg("st"), py::arg("wt_scratch") = 0);
   m.def("conv2d_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw_, int N, int C, int H, int W, int K, int R, int S_,
                            int sh, int sw, int ph, int pw, int dh, int dw, bool acc, uintptr_t st) {
     conv2d_wgrad(P<const float>(dy), P<const float>(x), P<float>(dw_), CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw),
@@ -92,11 +95,13 @@ PYBIND11_MODULE(_C, m) {
     xent_fwd_bwd(P<const float>(logits), P<const int32_t>(y), P<float>(logp), P<float>(dlogits), P<float>(loss_sum),
                  P<float>(correct), B, C, scale, S(st));
   });
+  m.def("bn_splits", &bn_splits);
   m.def("bn_fwd_train", [](uintptr_t x, uintptr_t g, uintptr_t b, uintptr_t y, uintptr_t mean, uintptr_t invstd,
                            uintptr_t rm, uintptr_t rv, int N, int C, int HW, float mom, float eps, bool relu,
-                           uintptr_t st) {
+                           uintptr_t acc, uintptr_t acc_next, int hiwater, uintptr_t st) {
     bn_fwd_train(P<const float>(x), P<const float>(g), P<const float>(b), P<float>(y), P<float>(mean), P<float>(invstd),
-                 P<float>(rm), P<float>(rv), N, C, HW, mom, eps, relu, S(st));
+                 P<float>(rm), P<float>(rv), N, C, HW, mom, eps, relu, P<float>(acc), P<float>(acc_next), hiwater,
+                 S(st));
   });
   m.def("bn_fwd_eval", [](uintptr_t x, uintptr_t g, uintptr_t b, uintptr_t y, uintptr_t rm, uintptr_t rv, int N, int C,
                           int HW, float eps, bool relu, uintptr_t st) {
@@ -104,9 +109,11 @@ PYBIND11_MODULE(_C, m) {
                 P<const float>(rv), N, C, HW, eps, relu, S(st));
   });
   m.def("bn_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t yr, uintptr_t g, uintptr_t mean, uintptr_t invstd,
-                     uintptr_t dx, uintptr_t dg, uintptr_t db, int N, int C, int HW, bool acc, uintptr_t st) {
+                     uintptr_t dx, uintptr_t dg, uintptr_t db, int N, int C, int HW, bool acc, uintptr_t a0,
+                     uintptr_t a1, int hiwater, uintptr_t st) {
     bn_bwd(P<const float>(dy), P<const float>(x), P<const float>(yr), P<const float>(g), P<const float>(mean),
-           P<const float>(invstd), P<float>(dx), P<float>(dg), P<float>(db), N, C, HW, acc, S(st));
+           P<const float>(invstd), P<float>(dx), P<float>(dg), P<float>(db), N, C, HW, acc, P<float>(a0),
+           P<float>(a1), hiwater, S(st));
   });
   m.def("shortcut_pad_add", [](uintptr_t x, uintptr_t y, int N, int Cin, int H, int W, int Cout, int P_, int Q,
                                int stride, uintptr_t st) {
@@ -201,7 +208,10 @@ PYBIND11_MODULE(_C, m) {
       .def("comm_stream", [](Reducer& r) { return reinterpret_cast<uintptr_t>(r.comm_stream()); })
       .def("last_comm_ms", &Reducer::last_comm_ms)
       .def_property_readonly("num_buckets", &Reducer::num_buckets)
-      .def_property_readonly("launched", &Reducer::launched);
+      .def_property_readonly("launched", &Reducer::launched)
+      .def("set_overlap", &Reducer::set_overlap)
+      .def("set_force_collectives", &Reducer::set_force_collectives)
+      .def_property_readonly("active", &Reducer::active);
 
   // ---------------------------------------------------------------- fused MNIST engine
   m.def("mnist_workspace_bytes", &MnistLayout::workspace_bytes);
@@ -219,6 +229,10 @@ PYBIND11_MODULE(_C, m) {
       .def("capture", &MnistEngine::capture, py::arg("mode") = -1, py::arg("steps_per_graph") = 1)
       .def("set_force_collectives", &MnistEngine::set_force_collectives)
       .def_property_readonly("graph_mode", &MnistEngine::graph_mode)
+      .def("set_overlap", &MnistEngine::set_overlap)
+      .def_property_readonly("overlap", &MnistEngine::overlap)
+      .def_property_readonly("reducer_active", &MnistEngine::reducer_active)
+      .def("uncapture", &MnistEngine::uncapture)
       .def("replay", &MnistEngine::replay)
       .def("forward_only", &MnistEngine::forward_only)
       .def("repack", &MnistEngine::repack)

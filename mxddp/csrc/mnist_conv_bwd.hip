@@ -19,79 +19,83 @@ namespace {
 // Block = (image b, tap r); wave w owns co tile w (16) x both ci tiles (32).  GEMM K = the 576
 // output positions, walked in 16-position groups: lane group g takes positions 16s+4g .. +3,
 // i.e. 4 consecutive columns of one output row = 2 pooling windows -> A = expand(dp float2,
-// q u16), B = a1 window row (LDS float4).  LDS: dp [64][148] (pitch 148 words: the 16 co rows
-// x 2 lane groups of a ds_read_b64 half-wave land on 64 distinct banks), q [64][144] bytes,
-// a1 window chunk [32][196] (8 output rows; pitch 196 = 784 B = 16 mod 256 for ds_read_b128).
-constexpr int kF6DpP = 148, kF6Rows = 8, kF6Pos = kF6Rows * 24, kF6BP = 196;
-constexpr size_t kF6Lds = sizeof(float) * (64 * kF6DpP + 32 * kF6BP) + 64 * 144;
+// 2-bit argmax codes), B = a1 window row (LDS float4).  LDS (52.9 KB -> 3 blocks per CU, so
+// the 576-block grid runs in ONE round on 256 CUs): dp [64][148] (pitch 148: the 16 co rows x
+// 2 lane groups of a ds_read_b64 half-wave land on distinct banks), argmax codes packed 4 per
+// byte [64][36] (dead windows have dp = 0, so their code is irrelevant), a1 window chunk
+// [32][100] (4 output rows; pitch 100 = 25 x 16 B, odd, for ds_read_b128).
+constexpr int kF6DpP = 148, kF6Rows = 4, kF6Pos = kF6Rows * 24, kF6BP = 100, kF6Chunks = 24 / kF6Rows;
+constexpr size_t kF6Lds = sizeof(float) * (64 * kF6DpP + 32 * kF6BP) + 64 * 36;
 __global__ __launch_bounds__(256) void f6_conv2_wgrad_kernel(MnistFused f, Scratch sc) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* dps = sm;                                              // [64][148]
-  float* Bs = dps + 64 * kF6DpP;                                // [32][196]
-  uint8_t* qs = reinterpret_cast<uint8_t*>(Bs + 32 * kF6BP);    // [64][144]
+  float* Bs = dps + 64 * kF6DpP;                                // [32][100]
+  uint8_t* qs = reinterpret_cast<uint8_t*>(Bs + 32 * kF6BP);    // [64][36] packed 2-bit codes
   const int bid = xcd_remap(blockIdx.x, gridDim.x);  // an image's 9 tap blocks share one XCD L2
   const int r = bid % 9, b = bid / 9;
   const int ky = r / 3, kx = r - 3 * ky;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
-  // compact dY2 of image b: dp (float4 granules) and q (uint32 granules), fully coalesced
-  {
-    const float4* src = reinterpret_cast<const float4*>(f.dp + (size_t)b * 9216);
-    const uint32_t* qsrc = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(f.idx) + (size_t)b * 9216);
-    float4 v[9];
-    uint32_t qv[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-      v[k] = src[tid + 256 * k];
-      qv[k] = qsrc[tid + 256 * k];
-    }
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-      const int i = tid + 256 * k, co = i / 36, c4 = (i - co * 36) * 4;
-      *reinterpret_cast<float4*>(dps + co * kF6DpP + c4) = v[k];
-      *reinterpret_cast<uint32_t*>(qs + co * 144 + c4) = qv[k];
-    }
-  }
   const float* a1b = f.a1 + (size_t)b * 32 * 676 + ky * 26 + kx;
-  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-  const float* dpr = dps + (16 * w + m) * kF6DpP;
-  const uint8_t* qr = qs + (16 * w + m) * 144;
-  // a1 window rows oy0+ky .. +7, cols kx .. kx+23 for all 32 ci: 24 values per thread; the
+  // a1 window rows oy0+ky .. +3, cols kx .. kx+23 for all 32 ci: 12 values per thread; the
   // next chunk's loads are issued before this chunk's MFMAs (register double buffer).
-  float v[24];
+  constexpr int kPer = 32 * kF6Pos / 256;
+  float v[kPer];
   auto load_chunk = [&](int oy0) {
 #pragma unroll
-    for (int k = 0; k < 24; ++k) {
+    for (int k = 0; k < kPer; ++k) {
       const int i = tid + 256 * k, ci = i / kF6Pos, pos = i - ci * kF6Pos, row = pos / 24, col = pos - row * 24;
       v[k] = a1b[ci * 676 + (oy0 + row) * 26 + col];
     }
   };
-  load_chunk(0);
+  // compact dY2 of image b: dp (float4 granules) and argmax codes (uint32 = 4 windows -> 1 byte)
+  {
+    const float4* src = reinterpret_cast<const float4*>(f.dp + (size_t)b * 9216);
+    const uint32_t* qsrc = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(f.idx) + (size_t)b * 9216);
+    float4 dv[9];
+    uint32_t qv[9];
 #pragma unroll
-  for (int ch = 0; ch < 3; ++ch) {
+    for (int k = 0; k < 9; ++k) {
+      dv[k] = src[tid + 256 * k];
+      qv[k] = qsrc[tid + 256 * k];
+    }
+    load_chunk(0);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int i = tid + 256 * k, co = i / 36, c4 = (i - co * 36) * 4;
+      *reinterpret_cast<float4*>(dps + co * kF6DpP + c4) = dv[k];
+      const uint32_t q = qv[k] & 0x03030303u;
+      qs[i] = (uint8_t)(q | (q >> 6) | (q >> 12) | (q >> 18));
+    }
+  }
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const float* dpr = dps + (16 * w + m) * kF6DpP;
+  const uint8_t* qr = qs + (16 * w + m) * 36;
+#pragma unroll
+  for (int ch = 0; ch < kF6Chunks; ++ch) {
     const int oy0 = ch * kF6Rows;
     if (ch > 0) __syncthreads();  // previous chunk's reads of Bs are done
 #pragma unroll
-    for (int k = 0; k < 24; ++k) {
+    for (int k = 0; k < kPer; ++k) {
       const int i = tid + 256 * k, ci = i / kF6Pos, pos = i - ci * kF6Pos;
       Bs[ci * kF6BP + pos] = v[k];
     }
     __syncthreads();
-    if (ch < 2) load_chunk(oy0 + kF6Rows);
+    if (ch + 1 < kF6Chunks) load_chunk(oy0 + kF6Rows);
     const float* br0 = Bs + m * kF6BP + 4 * g;
     const float* br1 = Bs + (16 + m) * kF6BP + 4 * g;
 #pragma unroll
     for (int s = 0; s < kF6Pos / 16; ++s) {
       const int p0 = oy0 * 24 + 16 * s + 4 * g;  // absolute output position of j = 0
       const int oy = p0 / 24, ox = p0 - oy * 24;  // ox % 4 == 0 -> two whole windows
-      const int w0 = (oy >> 1) * 12 + (ox >> 1);
-      const int t0 = (oy & 1) << 1;
+      const int w0 = (oy >> 1) * 12 + (ox >> 1);  // even
+      const uint32_t t0 = (oy & 1) << 1;
       const float2 d = *reinterpret_cast<const float2*>(dpr + w0);
-      const uint32_t qq = *reinterpret_cast<const uint16_t*>(qr + w0);
-      const uint32_t q0 = qq & 0xFF, q1 = qq >> 8;
-      const float a0 = q0 == (uint32_t)t0 ? d.x : 0.f;
-      const float a1 = q0 == (uint32_t)t0 + 1 ? d.x : 0.f;
-      const float a2 = q1 == (uint32_t)t0 ? d.y : 0.f;
-      const float a3 = q1 == (uint32_t)t0 + 1 ? d.y : 0.f;
+      const uint32_t qq = (uint32_t)qr[w0 >> 2] >> ((w0 & 3) * 2);
+      const uint32_t q0 = qq & 3, q1 = (qq >> 2) & 3;
+      const float a0 = q0 == t0 ? d.x : 0.f;
+      const float a1 = q0 == t0 + 1 ? d.x : 0.f;
+      const float a2 = q1 == t0 ? d.y : 0.f;
+      const float a3 = q1 == t0 + 1 ? d.y : 0.f;
       const float4 b0 = *reinterpret_cast<const float4*>(br0 + 16 * s);
       const float4 b1 = *reinterpret_cast<const float4*>(br1 + 16 * s);
       acc[0] = mfma4(a0, b0.x, acc[0]);

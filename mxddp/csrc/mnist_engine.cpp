@@ -90,13 +90,23 @@ void MnistEngine::repack() {
   if (variant_ == 1) mnist_fused_init(fused_args(), s_);
 }
 
-MnistEngine::~MnistEngine() {
+void MnistEngine::uncapture() {
+  if (s_) MX_HIP_CHECK(hipStreamSynchronize(s_));
   if (exec_) hipGraphExecDestroy(exec_);
   if (graph_) hipGraphDestroy(graph_);
+  exec_ = nullptr;
+  graph_ = nullptr;
   for (int k = 0; k < 3; ++k) {
     if (seg_exec_[k]) hipGraphExecDestroy(seg_exec_[k]);
     if (seg_graph_[k]) hipGraphDestroy(seg_graph_[k]);
+    seg_exec_[k] = nullptr;
+    seg_graph_[k] = nullptr;
   }
+  graph_mode_ = 0;
+}
+
+MnistEngine::~MnistEngine() {
+  uncapture();
   reducer_.reset();
   if (s_) hipStreamDestroy(s_);
 }
@@ -194,7 +204,9 @@ hipGraphExec_t MnistEngine::capture_fn(const std::function<void()>& fn, hipGraph
 void MnistEngine::capture(int mode, int steps_per_graph) {
   if (exec_ || seg_exec_[0]) return;
   const bool multi = comm_ && comm_->world_size() > 1;
-  if (mode < 0) mode = multi ? 2 : 1;  // default: collectives stay outside graphs when ws > 1
+  // default: one graph at world size 1; eager launches (mode 0) when real collectives run --
+  // the caller (FusedMnistTrainer.autotune) may pick a graph mode after timing the options.
+  if (mode < 0) mode = multi ? 0 : 1;
   MX_HIP_CHECK(hipStreamSynchronize(s_));
   graph_mode_ = mode;
   if (mode == 1) {  // whole step(s), RCCL collectives included (one launch per group of steps)

@@ -49,6 +49,10 @@ class MnistEngine {
   void replay(int n);        // n steps via the captured graph(s) (eager if not captured)
   int graph_mode() const { return graph_mode_; }
   void set_force_collectives(bool on) { reducer_->set_force_collectives(on); }
+  void set_overlap(bool on) { reducer_->set_overlap(on); }  // see Reducer::set_overlap
+  bool overlap() const { return reducer_->overlap(); }
+  bool reducer_active() const { return reducer_->active(); }
+  void uncapture();  // drop captured graphs (back to eager; capture() may be called again)
   void forward_only(uintptr_t x, uintptr_t logits, int B);  // eval helper (no grads)
   void sync();
   // Re-derive the fused path's packed weights / accumulators after the parameters were changed

@@ -25,9 +25,16 @@ struct ConvShape {
 // ---- GEMM-shaped (ops_gemm.hip) ----
 void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s,
                 bool relu, hipStream_t st);
-// dx = conv_transpose(dy, w) [* (mask > 0)], stored (=) or accumulated (+=).
+// dx = conv_transpose(dy, w) [* (mask > 0)], stored (=) or accumulated (+=).  `wt_scratch`
+// (K*C*9 floats, optional) enables the direct 3x3 path (conv3x3.hip) for eligible shapes.
 void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s,
-                  const float* relu_mask, bool accumulate, hipStream_t st);
+                  const float* relu_mask, bool accumulate, hipStream_t st, float* wt_scratch = nullptr);
+// Direct-LDS 3x3 stride-1 pad-1 convolution (conv3x3.hip), fp32 MFMA; W <= 64.
+bool conv3x3_eligible(const ConvShape& s);
+void conv3x3_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s, bool relu,
+                 hipStream_t st);
+void conv3x3_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s, const float* relu_mask,
+                   bool accumulate, float* wt_scratch, hipStream_t st);
 // dw (+)= sum_{n,p,q} dy * im2col(x)
 void conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate,
                   hipStream_t st);
@@ -75,15 +82,21 @@ void xent_fwd_bwd(const float* logits, const int32_t* y, float* logp, float* dlo
                   float* loss_sum, float* correct, int B, int C, float grad_scale, hipStream_t st);
 
 // BatchNorm2d (training): batch stats, running-stat update, normalise (+ optional ReLU).
+// Split reduction (ops_bn.hip) into per-channel accumulators acc[C][2] that must be zero on
+// entry; the elementwise pass zeroes acc_next[hiwater][2] for the following call (double
+// buffering: alternate the two buffers between consecutive calls on the same stream; hiwater =
+// the largest C used on the pair so far).
+int bn_splits(int N, int C, int HW);
 void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* y, float* mean,
                   float* invstd, float* run_mean, float* run_var, int N, int C, int HW,
-                  float momentum, float eps, bool relu, hipStream_t st);
+                  float momentum, float eps, bool relu, float* acc, float* acc_next, int hiwater,
+                  hipStream_t st);
 void bn_fwd_eval(const float* x, const float* gamma, const float* beta, float* y,
                  const float* run_mean, const float* run_var, int N, int C, int HW, float eps,
                  bool relu, hipStream_t st);
 void bn_bwd(const float* dy, const float* x, const float* y_relu, const float* gamma,
             const float* mean, const float* invstd, float* dx, float* dgamma, float* dbeta, int N,
-            int C, int HW, bool accumulate_params, hipStream_t st);
+            int C, int HW, bool accumulate_params, float* acc, float* acc_next, int hiwater, hipStream_t st);
 
 // PyramidNet shortcut: y[n,c,:,:] += (c < Cin ? pool(x)[n,c] : 0); pool = 2x2 avg, ceil.
 void shortcut_pad_add(const float* x, float* y, int N, int Cin, int H, int W, int Cout, int P, int Q,

@@ -194,43 +194,6 @@ __device__ float block_sum(float v, float* red) {
   return t;
 }
 
-__global__ __launch_bounds__(512) void bn_fwd_train_k(const float* __restrict__ x, const float* __restrict__ gamma,
-                                                      const float* __restrict__ beta, float* __restrict__ y,
-                                                      float* __restrict__ mean_out, float* __restrict__ invstd_out,
-                                                      float* __restrict__ run_mean, float* __restrict__ run_var,
-                                                      int N, int C, int HW, float momentum, float eps, int relu) {
-  __shared__ float red[8];
-  const int c = blockIdx.x;
-  const int64_t cnt = (int64_t)N * HW;
-  float s = 0.f;
-  for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-    const int64_t n = i / HW, hw = i - n * HW;
-    s += x[(n * C + c) * HW + hw];
-  }
-  const float mean = block_sum<512>(s, red) / (float)cnt;
-  float v = 0.f;
-  for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-    const int64_t n = i / HW, hw = i - n * HW;
-    const float d = x[(n * C + c) * HW + hw] - mean;
-    v += d * d;
-  }
-  const float var = block_sum<512>(v, red) / (float)cnt;
-  const float inv = rsqrtf(var + eps);
-  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-  for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-    const int64_t n = i / HW, hw = i - n * HW;
-    const int64_t o = (n * C + c) * HW + hw;
-    float r = (x[o] - mean) * inv * g + b;
-    y[o] = relu ? fmaxf(r, 0.f) : r;
-  }
-  if (threadIdx.x == 0) {
-    mean_out[c] = mean;
-    invstd_out[c] = inv;
-    if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
-    if (run_var) run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * (float)cnt / (float)(cnt > 1 ? cnt - 1 : 1);
-  }
-}
-
 __global__ void bn_fwd_eval_k(const float* __restrict__ x, const float* __restrict__ gamma,
                               const float* __restrict__ beta, float* __restrict__ y, const float* __restrict__ rm,
                               const float* __restrict__ rv, int N, int C, int HW, float eps, int relu) {
@@ -239,42 +202,6 @@ __global__ void bn_fwd_eval_k(const float* __restrict__ x, const float* __restri
     const int c = (i / HW) % C;
     float r = (x[i] - rm[c]) * rsqrtf(rv[c] + eps) * (gamma ? gamma[c] : 1.f) + (beta ? beta[c] : 0.f);
     y[i] = relu ? fmaxf(r, 0.f) : r;
-  }
-}
-
-__global__ __launch_bounds__(512) void bn_bwd_k(const float* __restrict__ dy, const float* __restrict__ x,
-                                                const float* __restrict__ y_relu, const float* __restrict__ gamma,
-                                                const float* __restrict__ mean, const float* __restrict__ invstd,
-                                                float* __restrict__ dx, float* __restrict__ dgamma,
-                                                float* __restrict__ dbeta, int N, int C, int HW, int acc_params) {
-  __shared__ float red[8];
-  const int c = blockIdx.x;
-  const int64_t cnt = (int64_t)N * HW;
-  const float mu = mean[c], inv = invstd[c];
-  float sdy = 0.f, sdyx = 0.f;
-  for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-    const int64_t n = i / HW, hw = i - n * HW;
-    const int64_t o = (n * C + c) * HW + hw;
-    float g = dy[o];
-    if (y_relu && !(y_relu[o] > 0.f)) g = 0.f;
-    sdy += g;
-    sdyx += g * (x[o] - mu) * inv;
-  }
-  const float db = block_sum<512>(sdy, red);
-  const float dg = block_sum<512>(sdyx, red);
-  const float gm = gamma ? gamma[c] : 1.f;
-  const float k = gm * inv / (float)cnt;
-  for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-    const int64_t n = i / HW, hw = i - n * HW;
-    const int64_t o = (n * C + c) * HW + hw;
-    float g = dy[o];
-    if (y_relu && !(y_relu[o] > 0.f)) g = 0.f;
-    const float xh = (x[o] - mu) * inv;
-    dx[o] = k * ((float)cnt * g - db - xh * dg);
-  }
-  if (threadIdx.x == 0) {
-    if (dgamma) dgamma[c] = acc_params ? dgamma[c] + dg : dg;
-    if (dbeta) dbeta[c] = acc_params ? dbeta[c] + db : db;
   }
 }
 
@@ -368,22 +295,10 @@ void xent_fwd_bwd(const float* logits, const int32_t* y, float* logp, float* dlo
   MX_LAUNCH(xent_k, dim3(cdiv(B, rows_per_block)), dim3(64 * rows_per_block), 0, st, logits, y, logp,
                      dlogits, loss_sum, correct, B, C, grad_scale);
 }
-void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* invstd,
-                  float* run_mean, float* run_var, int N, int C, int HW, float momentum, float eps, bool relu,
-                  hipStream_t st) {
-  MX_LAUNCH(bn_fwd_train_k, dim3(C), dim3(512), 0, st, x, gamma, beta, y, mean, invstd, run_mean,
-                     run_var, N, C, HW, momentum, eps, relu ? 1 : 0);
-}
 void bn_fwd_eval(const float* x, const float* gamma, const float* beta, float* y, const float* rm, const float* rv,
                  int N, int C, int HW, float eps, bool relu, hipStream_t st) {
   MX_LAUNCH(bn_fwd_eval_k, dim3(grid_for((int64_t)N * C * HW)), dim3(kTB), 0, st, x, gamma, beta, y, rm,
                      rv, N, C, HW, eps, relu ? 1 : 0);
-}
-void bn_bwd(const float* dy, const float* x, const float* y_relu, const float* gamma, const float* mean,
-            const float* invstd, float* dx, float* dgamma, float* dbeta, int N, int C, int HW, bool acc,
-            hipStream_t st) {
-  MX_LAUNCH(bn_bwd_k, dim3(C), dim3(512), 0, st, dy, x, y_relu, gamma, mean, invstd, dx, dgamma, dbeta, N,
-                     C, HW, acc ? 1 : 0);
 }
 void shortcut_pad_add(const float* x, float* y, int N, int Cin, int H, int W, int Cout, int P, int Q, int stride,
                       hipStream_t st) {

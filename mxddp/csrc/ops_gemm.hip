@@ -242,12 +242,15 @@ void run(Op& op, int splits, hipStream_t st) {
 
 void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s,
                 bool relu, hipStream_t st) {
+  if (g_gemm_precision == 0 && conv3x3_eligible(s)) return conv3x3_fwd(x, w, bias, y, s, relu, st);
   ConvFwdOp op{s.N * s.P * s.Q, s.K, s.C * s.R * s.S, ConvG(s), x, w, bias, y, relu};
   run(op, 1, st);
 }
 
 void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s,
-                  const float* relu_mask, bool accumulate, hipStream_t st) {
+                  const float* relu_mask, bool accumulate, hipStream_t st, float* wt_scratch) {
+  if (wt_scratch && g_gemm_precision == 0 && conv3x3_eligible(s))
+    return conv3x3_dgrad(dy, w, dx, s, relu_mask, accumulate, wt_scratch, st);
   ConvDgradOp op{s.N * s.H * s.W, s.C, s.K * s.R * s.S, ConvG(s), dy, w, dx, relu_mask,
                  accumulate ? kAccum : kStore};
   run(op, 1, st);

@@ -62,16 +62,24 @@ void Reducer::mark_bucket_ready(int bi, hipStream_t compute) {
   launch_ready(compute);
 }
 
+bool Reducer::active() const { return comm_ && (comm_->world_size() > 1 || force_); }
+
 void Reducer::launch_ready(hipStream_t compute) {
+  const bool act = active();
   while (next_ < (int)buckets_.size() && buckets_[next_].ready) {
     Bucket& b = buckets_[next_];
     MX_CHECK(b.pending == 0, "bucket launched before all its gradients were ready");
-    MX_HIP_CHECK(hipEventRecord(b.ev, compute));
-    MX_HIP_CHECK(hipStreamWaitEvent(comm_stream_, b.ev, 0));
-    if (timing_ && next_ == 0) MX_HIP_CHECK(hipEventRecord(t0_, comm_stream_));
-    if (comm_ && (comm_->world_size() > 1 || force_)) {
+    if (act) {  // no collectives -> no fences either (a fence alone costs a few us of GPU idle)
+      hipStream_t st = compute;
+      if (overlap_) {
+        MX_HIP_CHECK(hipEventRecord(b.ev, compute));
+        MX_HIP_CHECK(hipStreamWaitEvent(comm_stream_, b.ev, 0));
+        st = comm_stream_;
+        side_used_ = true;
+      }
+      if (timing_ && next_ == 0) MX_HIP_CHECK(hipEventRecord(t0_, st));
       char* p = flat_ + b.offset * dtype_size(dtype_);
-      comm_->all_reduce(p, p, b.numel, dtype_, op_, comm_stream_);
+      comm_->all_reduce(p, p, b.numel, dtype_, op_, st);
     }
     ++next_;
   }
@@ -85,12 +93,16 @@ void Reducer::finalize(hipStream_t compute) {
     }
   }
   launch_ready(compute);
+  if (!active()) return;
   if (timing_) {
-    MX_HIP_CHECK(hipEventRecord(t1_, comm_stream_));
+    MX_HIP_CHECK(hipEventRecord(t1_, side_used_ ? comm_stream_ : compute));
     timed_ = true;
   }
-  MX_HIP_CHECK(hipEventRecord(done_, comm_stream_));
-  MX_HIP_CHECK(hipStreamWaitEvent(compute, done_, 0));
+  if (side_used_) {
+    MX_HIP_CHECK(hipEventRecord(done_, comm_stream_));
+    MX_HIP_CHECK(hipStreamWaitEvent(compute, done_, 0));
+    side_used_ = false;
+  }
 }
 
 float Reducer::last_comm_ms() {

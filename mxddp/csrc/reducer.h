@@ -44,6 +44,14 @@ class Reducer {
   // issue the collectives even at world_size 1 (exercises the RCCL + graph-capture path on
   // a single GPU; an all-reduce over one rank is the identity)
   void set_force_collectives(bool on) { force_ = on; }
+  // overlap = true: each bucket's all-reduce runs on the side comm stream as soon as it is ready
+  // (event fence compute -> comm, and compute waits on comm at finalize).  overlap = false: the
+  // all-reduces are issued in order on the compute stream itself -- no cross-stream fences,
+  // which on ROCm cost several us each, but no overlap with the rest of the backward.
+  void set_overlap(bool on) { overlap_ = on; }
+  bool overlap() const { return overlap_; }
+  // true when collectives are actually issued (world size > 1, or forced for testing)
+  bool active() const;
 
  private:
   void launch_ready(hipStream_t compute);
@@ -63,7 +71,7 @@ class Reducer {
   int next_ = 0;
   hipStream_t comm_stream_ = nullptr;
   hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
-  bool timing_ = false, timed_ = false, force_ = false;
+  bool timing_ = false, timed_ = false, force_ = false, overlap_ = true, side_used_ = false;
 };
 
 }  // namespace mx

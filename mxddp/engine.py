@@ -13,6 +13,7 @@ The parameters are one flat fp32 buffer in MnistCNN ``state_dict`` order, so
 from __future__ import annotations
 
 import os
+import time
 
 import torch
 
@@ -37,6 +38,8 @@ class FusedMnistTrainer:
         self.graph_mode = graph_mode
         self.steps_per_graph = steps_per_graph
         self._external = False
+        self._capture_done = False
+        self.tuned = None
         self.device = torch.device("cuda", device) if isinstance(device, int) else device
         self.batch = batch
         self.comm = comm
@@ -73,23 +76,78 @@ class FusedMnistTrainer:
     # --------------------------------------------------------------- stepping
     def step(self, n: int = 1):
         """Run n training steps (graph replays once captured; first call warms up + captures)."""
-        if self.use_graph and not self.eng.captured:
+        if self.use_graph and not self._capture_done:
             self.eng.step()          # warm-up: lazy RCCL/kernel init outside the capture
             self.eng.sync()
-            # MXDDP_GRAPH_MODE: 1 = one graph incl. RCCL collectives, 2 = compute graphs with
-            # eager collectives in between; default 1 at world_size 1, 2 otherwise.
-            mode = self.graph_mode if self.graph_mode is not None else int(os.environ.get("MXDDP_GRAPH_MODE", "-1"))
-            spg = self.steps_per_graph
-            if spg is None:
-                spg = int(os.environ.get("MXDDP_STEPS_PER_GRAPH", "8"))
-            if self._external:
-                spg = 1  # a caller-provided batch is copied in before EVERY step
-            self.eng.capture(mode, spg)
+            self._capture(self._default_mode())
             n -= 1
             self.steps += 1
         if n > 0:
             self.eng.replay(n)
             self.steps += n
+
+    def _default_mode(self) -> int:
+        # MXDDP_GRAPH_MODE: 0 = eager launches, 1 = whole step(s) incl. RCCL collectives in one
+        # graph, 2 = compute graphs with eager collectives in between.  Default (-1): 1 at
+        # world size 1, eager when real collectives run (see autotune()).
+        if self.graph_mode is not None:
+            return self.graph_mode
+        return int(os.environ.get("MXDDP_GRAPH_MODE", "-1"))
+
+    def _capture(self, mode: int, spg: int | None = None):
+        if spg is None:
+            spg = self.steps_per_graph
+        if spg is None:
+            spg = int(os.environ.get("MXDDP_STEPS_PER_GRAPH", "8"))
+        if self._external:
+            spg = 1  # a caller-provided batch is copied in before EVERY step
+        self.eng.capture(mode, spg)
+        self._capture_done = True
+
+    def autotune(self, trial_steps: int = 24, include_graphs: bool | None = None) -> dict:
+        """Pick the fastest launch strategy for the DDP step on THIS machine by timing a few real
+        training steps of each (they count as warm-up).  Candidates: eager launches with the
+        fc-bucket all-reduce overlapped on the side stream vs. all collectives in order on the
+        compute stream (no cross-stream fences); optionally (MXDDP_AUTOTUNE_GRAPHS=1) the same
+        two captured as one hipGraph with RCCL inside.  The slowest rank's time decides, so every
+        rank picks the same strategy.  Returns {candidate: ms/step}."""
+        from .parallel import comm as pc
+
+        if include_graphs is None:
+            include_graphs = os.environ.get("MXDDP_AUTOTUNE_GRAPHS", "0") == "1"
+        if not self.eng.reducer_active or self._external:
+            return {}
+        cands = [(0, True), (0, False)]
+        if include_graphs and self.use_graph:
+            cands += [(1, True), (1, False)]
+        results = {}
+        for mode, ov in cands:
+            self.eng.uncapture()
+            self.eng.set_overlap(ov)
+            try:
+                if mode:
+                    self._capture(mode)
+                self.eng.replay(2)
+                self.eng.sync()
+                pc.barrier()
+                t0 = time.perf_counter()
+                self.eng.replay(trial_steps)
+                self.eng.sync()
+                dt = pc.all_reduce_max(time.perf_counter() - t0)
+            except RuntimeError:
+                dt = pc.all_reduce_max(float("inf"))
+            self.steps += 2 + trial_steps
+            results[(mode, ov)] = dt / trial_steps * 1e3
+        best = min(results, key=results.get)
+        self.eng.uncapture()
+        self.eng.set_overlap(best[1])
+        if best[0]:
+            self._capture(best[0])
+        self._capture_done = True
+        self.read_metrics(reset=True)
+        self.tuned = {"graph_mode": best[0], "overlap": best[1], "trials_ms": {f"{m}/{'ovl' if o else 'inl'}": round(v, 4)
+                                                                              for (m, o), v in results.items()}}
+        return results
 
     def set_batch(self, x: torch.Tensor, y: torch.Tensor):
         """Use a caller-provided batch instead of the on-device generator (real MNIST)."""

@@ -102,8 +102,10 @@ class _Conv2d(torch.autograd.Function):
         dx = dw_ = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
+            # scratch for the direct 3x3 path's flipped/transposed weights (ignored otherwise)
+            wt = torch.empty_like(w) if (R == 3 and S == 3 and sh == sw == 1 and ph == pw == 1) else None
             C.conv2d_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph, pw,
-                           dh, dw, 0, False, st)
+                           dh, dw, 0, False, st, 0 if wt is None else wt.data_ptr())
         if ctx.needs_input_grad[1]:
             dw_ = torch.empty_like(w)
             C.conv2d_wgrad(dy.data_ptr(), x.data_ptr(), dw_.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph, pw,
@@ -289,8 +291,10 @@ class _BatchNorm(torch.autograd.Function):
         if training:
             mean = torch.empty((Cc,), device=x.device, dtype=torch.float32)
             invstd = torch.empty_like(mean)
+            acc, acc_next, hi = _bn_acc(x.device, "fwd", Cc)
             C.bn_fwd_train(x.data_ptr(), _p(gamma), _p(beta), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
-                           _p(running_mean), _p(running_var), N, Cc, HW, float(momentum), float(eps), bool(relu), st)
+                           _p(running_mean), _p(running_var), N, Cc, HW, float(momentum), float(eps), bool(relu),
+                           acc.data_ptr(), acc_next.data_ptr(), hi, st)
         else:
             mean = running_mean
             invstd = (running_var + eps).rsqrt()
@@ -309,9 +313,30 @@ class _BatchNorm(torch.autograd.Function):
         dx = torch.empty_like(x)
         dg = torch.empty((Cc,), device=x.device) if ctx.has_affine else None
         db = torch.empty((Cc,), device=x.device) if ctx.has_affine else None
+        acc, acc_next, hi = _bn_acc(x.device, "bwd", Cc)
         native().bn_bwd(dy.data_ptr(), x.data_ptr(), _p(y), _p(gamma), mean.data_ptr(), invstd.data_ptr(),
-                        dx.data_ptr(), _p(dg), _p(db), N, Cc, HW, False, stream_of(dy))
+                        dx.data_ptr(), _p(dg), _p(db), N, Cc, HW, False, acc.data_ptr(), acc_next.data_ptr(), hi,
+                        stream_of(dy))
         return dx, dg, db, None, None, None, None, None, None
+
+
+_BN_ACC: dict = {}
+
+
+def _bn_acc(device, kind, C):
+    """Double-buffered per-channel accumulators of the split-reduction BN kernels (ops_bn.hip):
+    call k reduces into buffer k%2 (zero) and re-zeroes the other one for call k+1, up to the
+    widest C used so far ("hiwater").  One pair per (device, fwd|bwd); calls are stream-ordered
+    on the device's current stream."""
+    key = (device, kind)
+    st = _BN_ACC.get(key)
+    if st is None or st[0].shape[1] < 2 * C:
+        st = [torch.zeros((2, 2 * max(C, 4096)), dtype=torch.float32, device=device), 0, 0]
+        _BN_ACC[key] = st
+    buf, p, hi = st
+    hi = max(hi, C)
+    st[1], st[2] = p ^ 1, hi
+    return buf[p], buf[p ^ 1], hi
 
 
 def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum=0.1, eps=1e-5, relu=False):

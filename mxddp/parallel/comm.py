@@ -94,12 +94,16 @@ def info() -> DistInfo:
     return _INFO if _INFO is not None else DistInfo()
 
 
-def rccl_comm():
-    """This rank's RCCL communicator (created on first use; None when world_size == 1)."""
+def rccl_comm(force: bool = False):
+    """This rank's RCCL communicator (created on first use; None when world_size == 1 unless
+    ``force``: a 1-rank communicator exercises the full RCCL path for tests/benchmarks)."""
     global _COMM
     inf = info()
-    if inf.world_size == 1 or inf.device.type != "cuda":
+    if (inf.world_size == 1 and not force) or inf.device.type != "cuda":
         return None
+    if _COMM is None and inf.world_size == 1:
+        C = native()
+        _COMM = C.Comm(C.Comm.new_unique_id(), 0, 1, inf.device.index)
     if _COMM is None:
         C = native()
         store = dist.distributed_c10d._get_default_store()

@@ -101,3 +101,25 @@ def test_fused_engine_trains(cuda):
     l1, c1 = tr.read_metrics()
     assert l1 / (20 * 64) < 0.5 * l0 / (5 * 64)
     assert c1 / (20 * 64) > 0.8
+
+
+def test_fused_engine_autotune_keeps_training_exact(cuda):
+    """Strategy autotuning (eager/graph x overlapped/in-order collectives) only changes HOW the
+    step is launched: the trained weights equal an untuned engine's after the same step count."""
+    from mxddp import native
+    from mxddp.engine import FusedMnistTrainer
+
+    C = native()
+    comm = C.Comm(C.Comm.new_unique_id(), 0, 1, cuda.index or 0)
+    a = FusedMnistTrainer(batch=64, device=cuda, lr=0.01, comm=comm, force_collectives=True)
+    b = FusedMnistTrainer(batch=64, device=cuda, lr=0.01)
+    a.step(1)
+    res = a.autotune(trial_steps=4, include_graphs=True)
+    assert len(res) == 4 and a.tuned is not None
+    a.step(10)
+    b.step(1 + 4 * (2 + 4) + 10)
+    assert a.steps == b.steps
+    # same device-side data stream and update rule; only the (nondeterministic) order of the
+    # fp32 split-K atomics differs between two engines, so allow rounding-level drift
+    for k, v in a.state_dict().items():
+        assert torch.allclose(v, b.state_dict()[k], rtol=1e-3, atol=2e-5), k

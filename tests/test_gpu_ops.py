@@ -19,6 +19,15 @@ CONV_CASES = [
     (2, 101, 32, 32, 106, 3, 3, 2, 1),   # pyramidnet stride-2 entry
     (2, 3, 33, 31, 17, 7, 7, 2, 3),      # resnet stem-like, odd spatial
     (2, 64, 14, 14, 40, 1, 1, 1, 0),     # 1x1
+    # direct-LDS 3x3 s1 p1 path (conv3x3.hip): every supported width, C not a multiple of 8,
+    # K not a multiple of 64, partial row tiles (H not a multiple of 64/W)
+    (2, 13, 32, 32, 70, 3, 3, 1, 1),
+    (3, 40, 8, 8, 130, 3, 3, 1, 1),
+    (2, 9, 7, 7, 20, 3, 3, 1, 1),
+    (2, 17, 14, 14, 33, 3, 3, 1, 1),
+    (1, 12, 28, 27 + 1, 65, 3, 3, 1, 1),
+    (1, 8, 56, 56, 24, 3, 3, 1, 1),
+    (2, 5, 13, 16, 7, 3, 3, 1, 1),
 ]
 
 
@@ -99,19 +108,23 @@ def test_cross_entropy(cuda):
     assert _rel(lg.grad.cpu(), lr.grad) < 1e-5
 
 
+@pytest.mark.parametrize("shape,offset", [((8, 21, 9, 7), 0.5), ((64, 16, 32, 32), 3.0), ((64, 271, 8, 8), -20.0),
+                                          ((3, 5, 7, 7), 0.0), ((32, 64, 56, 56), 1.0)])
 @pytest.mark.parametrize("relu", [False, True])
-def test_batchnorm(cuda, relu):
+def test_batchnorm(cuda, relu, shape, offset):
+    """Split-reduction BN (vector and scalar paths, 1..64 splits, large mean offset) vs torch fp32."""
     torch.manual_seed(4)
-    x = torch.randn(8, 21, 9, 7) * 2 + 0.5
-    g, b = torch.rand(21) + 0.5, torch.randn(21)
-    rm, rv = torch.zeros(21), torch.ones(21)
+    C = shape[1]
+    x = torch.randn(*shape) * 2 + offset
+    g, b = torch.rand(C) + 0.5, torch.randn(C)
+    rm, rv = torch.zeros(C), torch.ones(C)
     xr, gr, br = (t.clone().requires_grad_() for t in (x, g, b))
     yr = F.batch_norm(xr, rm, rv, gr, br, True, 0.1, 1e-5)
     if relu:
         yr = F.relu(yr)
     gy = torch.randn_like(yr)
     yr.backward(gy)
-    rmg, rvg = torch.zeros(21, device=cuda), torch.ones(21, device=cuda)
+    rmg, rvg = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
     xg, gg, bg = (t.to(cuda).requires_grad_() for t in (x, g, b))
     y = ops.batch_norm(xg, gg, bg, rmg, rvg, True, 0.1, 1e-5, relu=relu)
     y.backward(gy.to(cuda))
@@ -120,6 +133,9 @@ def test_batchnorm(cuda, relu):
     assert _rel(gg.grad.cpu(), gr.grad) < 1e-4
     assert _rel(bg.grad.cpu(), br.grad) < 1e-4
     assert _rel(rmg.cpu(), rm) < 1e-5 and _rel(rvg.cpu(), rv) < 1e-5
+    # a second call reuses the self-resetting ticket counters
+    y2 = ops.batch_norm(xg.detach(), gg, bg, rmg, rvg, True, 0.1, 1e-5, relu=relu)
+    assert _rel(y2.cpu(), yr.detach()) < 1e-4
 
 
 @pytest.mark.parametrize("stride", [1, 2])

@@ -56,21 +56,24 @@ def test_replica_group_single_device(cuda):
 
 @pytest.mark.parametrize("name", ["pyramidnet110", "resnet50"])
 def test_model_forward_backward_vs_torch(cuda, name):
-    """Full-model numerics: mxddp HIP path vs PyTorch fp32 CPU on the same weights and batch."""
+    """Full-model numerics: mxddp HIP path (fp32) vs a float64 CPU reference on the same weights
+    and batch, judged against stock PyTorch-ROCm's own fp32 GPU error on the same problem."""
+    import copy
+
     from mxddp import ops
     from mxddp.models import build_model
 
     torch.manual_seed(0)
     m = build_model(name)
     # batch 8: BN backward at tiny batch is a catastrophic cancellation of three nearly equal
-    # terms, which amplifies summation-order noise in BOTH implementations
+    # terms, which amplifies summation-order noise in ANY fp32 implementation
     shape = (8, 3, 32, 32) if name == "pyramidnet110" else (8, 3, 64, 64)
     x = torch.randn(shape)
     y = torch.randint(0, 10, (8,))
-    ref_loss = F.cross_entropy(m(x), y)
+    m64 = copy.deepcopy(m).double()
+    ref_loss = F.cross_entropy(m64(x.double()), y)
     ref_loss.backward()
-    ref = torch.cat([p.grad.reshape(-1).clone() for p in m.parameters()])
-    m.zero_grad()
+    ref = torch.cat([p.grad.reshape(-1).float().clone() for p in m64.parameters()])
     mg = m.to(cuda)
 
     def grads(reference_mode):
@@ -86,8 +89,9 @@ def test_model_forward_backward_vs_torch(cuda, name):
         return loss.item(), torch.cat([p.grad.reshape(-1).cpu() for p in mg.parameters()])
 
     loss, got = grads(False)
-    _, tgpu = grads(True)
-    assert abs(loss - ref_loss.item()) < 1e-3 * max(1.0, abs(ref_loss.item()))
+    tloss, tgpu = grads(True)
+    ref_l = ref_loss.item()
+    assert abs(loss - ref_l) < max(1e-3 * max(1.0, abs(ref_l)), 3 * abs(tloss - ref_l)), (loss, tloss, ref_l)
     rel = ((got - ref).norm() / ref.norm()).item()  # whole-model gradient, relative L2
     # deep nets amplify fp32 summation-order noise; the bar is "no worse than stock
     # PyTorch-ROCm's own GPU kernels are vs the CPU" (with a floor)
