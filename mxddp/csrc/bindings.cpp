@@ -238,6 +238,7 @@ PYBIND11_MODULE(_C, m) {
       .def("repack", &MnistEngine::repack)
       .def("sync", &MnistEngine::sync, py::call_guard<py::gil_scoped_release>())
       .def("set_external_batch", &MnistEngine::set_external_batch)
+      .def("set_trace", &MnistEngine::set_trace)
       .def("last_comm_ms", &MnistEngine::last_comm_ms)
       .def_property_readonly("stream", &MnistEngine::stream)
       .def_property_readonly("x_ptr", &MnistEngine::x_ptr)

@@ -22,6 +22,8 @@
 #include "common.h"
 #include "ops.h"
 
+#include <algorithm>
+
 namespace mx {
 
 namespace {
@@ -163,6 +165,132 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(C3Args a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Weight gradient of a 3x3 s1 p1 conv: dw[co][ci][tap] += sum_{n,h,w} dy[n][co][h][w] *
+// x[n][ci][h+ky-1][w+kx-1].  GEMM: M = 64 output channels (A = dy tile in LDS), N = 16 input
+// channels x 9 taps = 144 columns (B = im2col of the x patch in LDS, per-lane constant (ci, tap)
+// offset + a compile-time position offset), K = output positions, walked one 64-position tile
+// (TH full rows) at a time over a group of G images.  Wave w owns output channels 16w..16w+15
+// x all 9 column tiles (9 accumulators).  W % 4 == 0 so a 4-position k-group never straddles a
+// row.  Block results are atomically added into dw (G images per block bound the contention).
+struct C3WArgs {
+  const float* dy;  // [N][K][H][W]
+  const float* x;   // [N][C][H][W]
+  float* dw;        // [K][C][3][3]
+  int N, C, H, K;
+  int tiles_h, ktiles, cchunks, G, ngroups;
+};
+constexpr int kWCi = 16, kDP = 66;  // dy tile pitch: 16 co rows x 2 lane groups -> distinct banks
+
+template <int W>
+struct C3WGeom {
+  static constexpr int TH = 64 / W, NP = TH * W, PW = W + 2, PR = TH + 2, RP = PW, CHP = pad16mod32(PR * PW);
+  static constexpr int pelems = kWCi * PR * PW, EP = (pelems + 255) / 256;
+  static constexpr size_t lds = sizeof(float) * ((size_t)64 * kDP + (size_t)kWCi * CHP);
+};
+
+template <int W>
+__global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(C3WArgs a) {
+  using G = C3WGeom<W>;
+  static_assert(W % 4 == 0, "k-groups of 4 positions must not straddle rows");
+  constexpr int TH = G::TH, NP = G::NP, PW = G::PW, PR = G::PR, RP = G::RP, CHP = G::CHP;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* Ds = sm;               // [64 co][66]
+  float* Ps = sm + 64 * kDP;    // [16 ci][CHP]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, l16 = lane & 15;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kt = bid % a.ktiles, r1 = bid / a.ktiles;
+  const int cc = r1 % a.cchunks, ng = r1 / a.cchunks;
+  const int co0 = kt * 64, c0 = cc * kWCi;
+  const int n_beg = ng * a.G, n_end = min(a.N, n_beg + a.G);
+  const size_t HW = (size_t)a.H * W;
+
+  int bo[9];  // per-lane B offset of column 16j + l16 = (ci, tap)
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int c = 16 * j + l16, ci = c / 9, tap = c - 9 * ci;
+    bo[j] = ci * CHP + (tap / 3) * RP + (tap % 3) + g;
+  }
+  // dy tile: thread t -> co row t/4, 16 consecutive positions from (t%4)*16 (float4 x 4)
+  const int drow = tid >> 2, dq = tid & 3;
+  const bool drow_ok = co0 + drow < a.K;
+  float4 rd[4];
+  float rp[G::EP];
+  auto gload = [&](int n, int th) {
+    const int h0 = th * TH;
+    const float* dyp = a.dy + ((size_t)n * a.K + min(co0 + drow, a.K - 1)) * HW + (size_t)h0 * W;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = dq * 16 + 4 * i;
+      rd[i] = (drow_ok && p < NP && h0 + p / W < a.H) ? *reinterpret_cast<const float4*>(dyp + p)
+                                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const float* xb = a.x + ((size_t)n * a.C + c0) * HW;
+#pragma unroll
+    for (int i = 0; i < G::EP; ++i) {
+      const int e = tid + 256 * i;
+      float v = 0.f;
+      if (e < G::pelems) {
+        const int ci = e / (PR * PW), rem = e - ci * (PR * PW), r = rem / PW, c = rem - r * PW;
+        const int h = h0 + r - 1, ww = c - 1;
+        if (c0 + ci < a.C && (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)W)
+          v = xb[(size_t)ci * HW + (size_t)h * W + ww];
+      }
+      rp[i] = v;
+    }
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(Ds + drow * kDP + dq * 16 + 4 * i) = rd[i];
+#pragma unroll
+    for (int i = 0; i < G::EP; ++i) {
+      const int e = tid + 256 * i;
+      if (e < G::pelems) {
+        const int ci = e / (PR * PW), rem = e - ci * (PR * PW), r = rem / PW, c = rem - r * PW;
+        Ps[ci * CHP + r * RP + c] = rp[i];
+      }
+    }
+  };
+
+  f32x4 acc[9];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ntiles = (n_end - n_beg) * a.tiles_h;
+  gload(n_beg, 0);
+  const float* ap = Ds + (16 * w + l16) * kDP + g;
+  for (int t = 0; t < ntiles; ++t) {
+    if (t) __syncthreads();
+    sstore();
+    __syncthreads();
+    if (t + 1 < ntiles) gload(n_beg + (t + 1) / a.tiles_h, (t + 1) % a.tiles_h);
+#pragma unroll
+    for (int s = 0; s < NP / 4; ++s) {
+      const int pr = (4 * s) / W, pc = (4 * s) % W;  // position 4s + g -> (pr, pc + g)
+      const float av = ap[4 * s];
+#pragma unroll
+      for (int j = 0; j < 9; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, Ps[bo[j] + pr * RP + pc], acc[j], 0, 0, 0);
+    }
+  }
+  // C: row = co (16w + 4g + r), column = 16j + l16 -> (ci, tap)
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int c = 16 * j + l16, ci = c / 9, tap = c - 9 * ci;
+    if (c0 + ci >= a.C) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + 16 * w + 4 * g + r;
+      if (co < a.K) atomicAdd(a.dw + ((size_t)co * a.C + c0 + ci) * 9 + tap, acc[j][r]);
+    }
+  }
+}
+
+template <int W>
+void launch_wgrad_w(const C3WArgs& a, hipStream_t st) {
+  const int blocks = a.ngroups * a.cchunks * a.ktiles;
+  MX_LAUNCH(conv3x3_wgrad_kernel<W>, dim3(blocks), dim3(256), C3WGeom<W>::lds, st, a);
+}
+
 // w'[ci][co][8 - tap] = w[co][ci][tap]: weights of the equivalent forward conv for dgrad.
 __global__ void flip_transpose_k(const float* __restrict__ w, float* __restrict__ wt, int K, int C) {
   const int total = K * C * 9;
@@ -217,6 +345,37 @@ bool conv3x3_eligible(const ConvShape& s) {
 void conv3x3_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s, bool relu,
                  hipStream_t st) {
   launch(x, w, bias, nullptr, y, s.N, s.C, s.H, s.W, s.K, relu, false, st);
+}
+
+bool conv3x3_wgrad_eligible(const ConvShape& s) {
+  return conv3x3_eligible(s) && s.W % 4 == 0;
+}
+
+void conv3x3_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate, hipStream_t st) {
+  if (!accumulate) MX_HIP_CHECK(hipMemsetAsync(dw, 0, sizeof(float) * (size_t)s.K * s.C * 9, st));
+  C3WArgs a{};
+  a.dy = dy;
+  a.x = x;
+  a.dw = dw;
+  a.N = s.N;
+  a.C = s.C;
+  a.H = s.H;
+  a.K = s.K;
+  a.tiles_h = cdiv(s.H, 64 / s.W);
+  a.ktiles = cdiv(s.K, 64);
+  a.cchunks = cdiv(s.C, kWCi);
+  // images per block: enough blocks to fill the chip (~768), as few atomics per address as that allows
+  const int per_img = a.ktiles * a.cchunks;
+  a.G = std::max(1, (s.N * per_img) / 768);
+  a.ngroups = cdiv(s.N, a.G);
+  switch (s.W) {
+    case 8: return launch_wgrad_w<8>(a, st);
+    case 16: return launch_wgrad_w<16>(a, st);
+    case 28: return launch_wgrad_w<28>(a, st);
+    case 32: return launch_wgrad_w<32>(a, st);
+    case 56: return launch_wgrad_w<56>(a, st);
+    default: MX_CHECK(false, "conv3x3_wgrad: unsupported width");
+  }
 }
 
 void conv3x3_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s, const float* relu_mask,

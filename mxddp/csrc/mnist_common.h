@@ -17,6 +17,14 @@ __device__ __forceinline__ float sel4(const float4& v, int j) {
   return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
 }
 
+// Phase timestamps for in-kernel profiling (MnistFused::trace, off = null): blocks 0..63 of
+// kernel `kid` record the 100 MHz wall clock at phase `ph` (<8) from thread 0.
+#define MX_TRACE(f, kid, ph)                                                                        \
+  do {                                                                                              \
+    if ((f).trace && threadIdx.x == 0 && blockIdx.x < 64)                                           \
+      (f).trace[((kid) * 64 + blockIdx.x) * 8 + (ph)] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
 struct Scratch {  // carve of MnistFused::scratch (floats)
   float* wf;      // conv2 fwd B-fragments   [18 q][4 w][64 lane][4 j]
   float* wd;      // conv2 dgrad B-fragments [9 r][4 s][2 nt][64 lane][4 j]

@@ -27,6 +27,7 @@ namespace {
 constexpr int kF6DpP = 148, kF6Rows = 4, kF6Pos = kF6Rows * 24, kF6BP = 100, kF6Chunks = 24 / kF6Rows;
 constexpr size_t kF6Lds = sizeof(float) * (64 * kF6DpP + 32 * kF6BP) + 64 * 36;
 __global__ __launch_bounds__(256) void f6_conv2_wgrad_kernel(MnistFused f, Scratch sc) {
+  MX_TRACE(f, 3, 0);
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* dps = sm;                                              // [64][148]
   float* Bs = dps + 64 * kF6DpP;                                // [32][100]
@@ -80,6 +81,7 @@ __global__ __launch_bounds__(256) void f6_conv2_wgrad_kernel(MnistFused f, Scrat
       Bs[ci * kF6BP + pos] = v[k];
     }
     __syncthreads();
+    if (ch == 0) MX_TRACE(f, 3, 1);
     if (ch + 1 < kF6Chunks) load_chunk(oy0 + kF6Rows);
     const float* br0 = Bs + m * kF6BP + 4 * g;
     const float* br1 = Bs + (16 + m) * kF6BP + 4 * g;
@@ -108,6 +110,7 @@ __global__ __launch_bounds__(256) void f6_conv2_wgrad_kernel(MnistFused f, Scrat
       acc[1] = mfma4(a3, b1.w, acc[1]);
     }
   }
+  MX_TRACE(f, 3, 2);
 #pragma unroll
   for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -115,6 +118,7 @@ __global__ __launch_bounds__(256) void f6_conv2_wgrad_kernel(MnistFused f, Scrat
       const int co = 16 * w + 4 * g + j, ci = 16 * c + m;
       atomicAdd(sc.wacc + (r * 64 + co) * 32 + ci, acc[c][j]);
     }
+  MX_TRACE(f, 3, 3);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -129,6 +133,7 @@ __global__ __launch_bounds__(256) void f6_conv2_wgrad_kernel(MnistFused f, Scrat
 constexpr int kF7WR = 4, kF7WC = 14, kF7CoP = 60;
 constexpr size_t kF7Lds = sizeof(float) * (64 * kF7CoP + 784 + 1280) + 64 * kF7CoP;
 __global__ __launch_bounds__(256) void f7_conv2_dgrad_kernel(MnistFused f, Scratch sc) {
+  MX_TRACE(f, 4, 0);
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* dps = sm;                                                  // [64][60] (4 x 14 used)
   float* xs = dps + 64 * kF7CoP;                                    // [784]
@@ -171,6 +176,7 @@ __global__ __launch_bounds__(256) void f7_conv2_dgrad_kernel(MnistFused f, Scrat
       if (tid + 256 * k < 784) xs[tid + 256 * k] = xv[k];
   }
   __syncthreads();
+  MX_TRACE(f, 4, 1);
   const int pos = min(p0 + 16 * w + m, 675);  // this lane's A row (clamped tail rows are discarded)
   const int iy = pos / 26, ix = pos - iy * 26;
   const float4* wd = reinterpret_cast<const float4*>(sc.wd) + lane;
@@ -212,6 +218,7 @@ __global__ __launch_bounds__(256) void f7_conv2_dgrad_kernel(MnistFused f, Scrat
 #pragma unroll
     for (int i = 0; i < 8; ++i) bc[i] = bn[i];
   }
+  MX_TRACE(f, 4, 2);
   // epilogue: acc[c][j] = dA1 at position p = p0 + 16w + 4g + j, channel ci = 16c + m
   float part[2][10];
 #pragma unroll
@@ -262,6 +269,7 @@ __global__ __launch_bounds__(256) void f7_conv2_dgrad_kernel(MnistFused f, Scrat
     if (k < 9) atomicAdd(g1 + ci * 9 + k, v);  // conv1.weight grad [32][9]
     else atomicAdd(g1 + 288 + ci, v);          // conv1.bias grad [32]
   }
+  MX_TRACE(f, 4, 3);
 }
 
 // ------------------------------------------------------------------------------------------

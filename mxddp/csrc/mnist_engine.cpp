@@ -125,8 +125,26 @@ void MnistEngine::fwd(const float* x, float* logits_out, int B) {
 
 MnistFused MnistEngine::fused_args() const {
   const uint64_t data_seed = seed_ + (comm_ ? comm_->rank() : 0) * 7919ull;  // per-rank data shard
-  return MnistFused{B_,   x_,       y_,       p_,       g_,    a1_,       pool_,           idx_, h_,
-                    dh_,  dp_,      scratch_, metrics_, counter_, tmpl_, data_seed, external_batch_ ? 0 : 1};
+  MnistFused f{};
+  f.B = B_;
+  f.x = x_;
+  f.y = y_;
+  f.p = p_;
+  f.g = g_;
+  f.a1 = a1_;
+  f.pool = pool_;
+  f.idx = idx_;
+  f.h = h_;
+  f.dh = dh_;
+  f.dp = dp_;
+  f.scratch = scratch_;
+  f.metrics = metrics_;
+  f.counter = counter_;
+  f.tmpl = tmpl_;
+  f.seed = data_seed;
+  f.trace = trace_;
+  f.synth = external_batch_ ? 0 : 1;
+  return f;
 }
 
 // Segment 0: batch + forward + head + fc backward  -> bucket 0 (fc grads, 4.72 MB) is complete.

@@ -62,6 +62,9 @@ class MnistEngine {
   uintptr_t x_ptr() const { return reinterpret_cast<uintptr_t>(x_); }
   uintptr_t y_ptr() const { return reinterpret_cast<uintptr_t>(y_); }
   void set_external_batch(bool on) { external_batch_ = on; }
+  // in-kernel phase timestamps (MnistFused::trace); 0 = off.  Eager steps only: a captured
+  // graph keeps the arguments it was captured with.
+  void set_trace(uintptr_t buf) { trace_ = reinterpret_cast<uint32_t*>(buf); }
   float last_comm_ms() { return reducer_ ? reducer_->last_comm_ms() : 0.f; }
   bool captured() const { return exec_ != nullptr || seg_exec_[0] != nullptr; }
 
@@ -73,6 +76,7 @@ class MnistEngine {
   hipGraph_t seg_graph_[3] = {nullptr, nullptr, nullptr};
   hipGraphExec_t seg_exec_[3] = {nullptr, nullptr, nullptr};
   int graph_mode_ = 0;
+  uint32_t* trace_ = nullptr;
   int steps_per_graph_ = 1;
   void fwd(const float* x, float* logits_out, int B);
   int B_;

@@ -23,6 +23,7 @@ struct MnistFused {
   int32_t* counter;      // synthetic-data batch counter
   const float* tmpl;     // class templates [10][784] for the on-device generator
   uint64_t seed;         // per-rank generator seed
+  uint32_t* trace;       // optional per-phase timestamps (s_memrealtime, 100 MHz) for profiling, or null
   int synth;             // 1: F2 generates the batch on device; 0: x/y provided by the caller
 };
 

@@ -35,6 +35,8 @@ void conv3x3_fwd(const float* x, const float* w, const float* bias, float* y, co
                  hipStream_t st);
 void conv3x3_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s, const float* relu_mask,
                    bool accumulate, float* wt_scratch, hipStream_t st);
+bool conv3x3_wgrad_eligible(const ConvShape& s);  // + W % 4 == 0
+void conv3x3_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate, hipStream_t st);
 // dw (+)= sum_{n,p,q} dy * im2col(x)
 void conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate,
                   hipStream_t st);

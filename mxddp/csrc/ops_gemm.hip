@@ -258,6 +258,7 @@ void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s
 
 void conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate,
                   hipStream_t st) {
+  if (g_gemm_precision == 0 && conv3x3_wgrad_eligible(s)) return conv3x3_wgrad(dy, x, dw, s, accumulate, st);
   ConvWgradOp op{s.K, s.C * s.R * s.S, s.N * s.P * s.Q, ConvG(s), dy, x, dw, kAtomic};
   const int tiles = cdiv(op.M, 64) * cdiv(op.N, 64);
   const int splits = pick_splits(tiles, op.K, 512, 768);

@@ -186,6 +186,38 @@ class FusedMnistTrainer:
             self.eng.sync()
         return m[0], m[1]
 
+    def phase_profile(self, steps: int = 20) -> dict:
+        """In-kernel phase timings of the fused step (MnistFused::trace, s_memrealtime at 100 MHz):
+        runs `steps` eager steps with blocks 0..63 of each kernel stamping their phase
+        boundaries, and returns {kernel: [median us from phase 0 to phase k, ...]}."""
+        names = ["F2_fwd", "F3_fc1", "F5_head_fc1bwd", "F6_wgrad", "F7_dgrad"]
+        buf = torch.zeros(7 * 64 * 8, dtype=torch.int32, device=self.device)
+        self.eng.set_trace(buf.data_ptr())
+        acc = {n: [] for n in names}
+        try:
+            for _ in range(steps):
+                buf.zero_()
+                self.eng.step()
+                self.eng.sync()
+                t = buf.view(7, 64, 8).cpu().to(torch.int64)
+                for k, n in enumerate(names):
+                    t0 = t[k, :, 0]
+                    rows = []
+                    for ph in range(1, 8):
+                        v = t[k, :, ph]
+                        ok = v != 0
+                        if ok.any():
+                            rows.append(((v[ok] - t0[ok]) & 0xFFFFFFFF).double().median().item() * 0.01)
+                    acc[n].append(rows)
+        finally:
+            self.eng.set_trace(0)
+        out = {}
+        for n, runs in acc.items():
+            runs = [r for r in runs[1:] if r]  # drop the first (cold) step
+            if runs:
+                out[n] = [round(sum(r[i] for r in runs) / len(runs), 2) for i in range(min(len(r) for r in runs))]
+        return out
+
     # --------------------------------------------------------------- state
     def state_dict(self) -> dict:
         self.eng.sync()
