@@ -32,9 +32,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--batch", type=int, default=64, help="per-rank batch (reference: 64)")
-    ap.add_argument("--impl", choices=["fused", "layers", "torch"], default="fused",
+    ap.add_argument("--impl", choices=["fused", "layers", "torch", "replica"], default="fused",
                     help="fused: native hipGraph step (default); layers: mxddp ops + DDP reducer; "
-                         "torch: stock PyTorch-ROCm DDP (comparison only)")
+                         "torch: stock PyTorch-ROCm DDP (comparison only); replica: ONE process drives --gpus "
+                         "GPUs (MirroredStrategy / DataParallel parity, BASELINE config 4; not via torchrun)")
     ap.add_argument("--variant", type=int, default=1, help="fused kernel variant (0 = generic igemm)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--graph-mode", type=int, default=None, choices=[0, 1, 2],
@@ -61,6 +62,11 @@ def main():
     from mxddp.parallel import comm as C
 
     ws_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.impl == "replica":
+        if ws_env != 1:
+            print("bench.py: --impl replica is single-process (do not launch it with torchrun)", file=sys.stderr)
+            sys.exit(2)
+        return _replica(a)
     if ws_env != a.gpus:
         if ws_env == 1 and a.gpus > 1:
             print(f"bench.py: --gpus {a.gpus} needs a launcher (torch.distributed.run)", file=sys.stderr)
@@ -109,6 +115,9 @@ def main():
     else:
         extra = {}
     if inf.rank == 0:
+        from mxddp.models import get_spec
+
+        spec = get_spec(a.model)
         total_imgs = a.gpus * B * a.steps
         value = total_imgs / dt
         out = {
@@ -123,9 +132,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 3),
             "dtype": a.dtype,
-            "data": "synthetic (on-device class-conditional 28x28, random-init weights)",
+            "data": _data_desc(spec),
             "config": {"model": a.model, "global_batch": B * a.gpus, "per_rank_batch": B, "seq_len": None,
-                       "image": "1x28x28", "parallelism": f"dp{a.gpus}", "impl": a.impl,
+                       "image": "x".join(map(str, spec.input_shape)), "parallelism": f"dp{a.gpus}", "impl": a.impl,
                        "graph": (a.impl == "fused" and not a.no_graph),
                        **({"graph_mode": tr.eng.graph_mode, "overlap": tr.eng.overlap,
                            "force_collectives": a.force_collectives, "autotune": tr.tuned}
@@ -134,6 +143,72 @@ def main():
         }
         print(json.dumps(out), flush=True)
     C.shutdown()
+
+
+def _replica(a):
+    """In-process replica DP over --gpus GPUs (mxddp.parallel.replica): per-replica batch --batch,
+    global batch --batch x --gpus, grouped RCCL all-reduce, flat optimizer per replica."""
+    import torch
+
+    from mxddp import native, ops
+    from mxddp.models import build_model, get_spec
+    from mxddp.optim import SGD, Adam
+    from mxddp.parallel.replica import ReplicaGroup
+
+    if a.dtype != "fp32":
+        ops.set_compute_dtype(a.dtype)
+    devices = [torch.device("cuda", i) for i in range(a.gpus)]
+    spec = get_spec(a.model)
+    torch.manual_seed(a.seed)
+
+    def make_opt(flat):
+        if spec.optimizer == "adam":
+            return Adam(flat, lr=spec.lr, eps=1e-7, eps_hat=True)
+        return SGD(flat, lr=a.lr, momentum=0.9, weight_decay=1e-4)
+
+    grp = ReplicaGroup(build_model(a.model), devices, make_opt)
+    B = a.batch * a.gpus
+    D = 1
+    for s_ in spec.input_shape:
+        D *= s_
+    C = native()
+    dev = devices[0]
+    tmpl = torch.empty(spec.num_classes * D, device=dev)
+    ctr = torch.zeros(4, dtype=torch.int32, device=dev)
+    x = torch.empty((B,) + tuple(spec.input_shape), device=dev)
+    y = torch.empty(B, dtype=torch.int32, device=dev)
+    C.synth_templates(tmpl.data_ptr(), spec.num_classes, D, a.seed, torch.cuda.current_stream(dev).cuda_stream)
+    loss_fn = lambda o, t: ops.cross_entropy(o, t, return_correct=True)  # noqa: E731
+
+    def run(n):
+        for _ in range(n):
+            C.synth_batch(x.data_ptr(), y.data_ptr(), tmpl.data_ptr(), B, D, spec.num_classes, a.seed, ctr.data_ptr(),
+                          torch.cuda.current_stream(dev).cuda_stream)
+            grp.step(x, y.long(), loss_fn)
+
+    def sync_all():
+        for d in devices:
+            torch.cuda.synchronize(d)
+
+    run(a.warmup)
+    sync_all()
+    t0 = time.perf_counter()
+    run(a.steps)
+    sync_all()
+    dt = time.perf_counter() - t0
+    value = B * a.steps / dt
+    print(json.dumps({
+        "metric": METRIC, "value": round(value, 1), "unit": "images/sec", "n_gpus": a.gpus, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": a.dtype, "data": _data_desc(spec),
+        "config": {"model": a.model, "global_batch": B, "per_rank_batch": a.batch, "seq_len": None,
+                   "image": "x".join(map(str, spec.input_shape)), "parallelism": f"replica{a.gpus}",
+                   "impl": "replica"}}), flush=True)
+
+
+def _data_desc(spec):
+    shape = "x".join(map(str, spec.input_shape[1:]))
+    return f"synthetic (on-device class-conditional {shape}, random-init weights)"
 
 
 def _layers_or_torch(a, torch, inf, dev, comm, B):
@@ -180,13 +255,20 @@ def _layers_or_torch(a, torch, inf, dev, comm, B):
     st = torch.cuda.current_stream(dev).cuda_stream
     Cn.synth_templates(tmpl.data_ptr(), nc, D, a.seed, st)
 
+    import contextlib
+
+    # stock-PyTorch comparison at the same compute precision: bf16 autocast (MIOpen/hipBLASLt bf16)
+    amp = (torch.autocast("cuda", dtype=torch.bfloat16) if (a.impl == "torch" and a.dtype == "bf16")
+           else contextlib.nullcontext())
+
     def run(n):
         for _ in range(n):
             Cn.synth_batch(x.data_ptr(), y.data_ptr(), tmpl.data_ptr(), B, D, nc, a.seed + inf.rank, ctr.data_ptr(),
                            torch.cuda.current_stream(dev).cuda_stream)
             opt.zero_grad()
-            out = net(x)
-            loss = loss_fn(out, y.long())
+            with amp:
+                out = net(x)
+                loss = loss_fn(out, y.long())
             loss.backward()
             opt.step()
 

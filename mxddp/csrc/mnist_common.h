@@ -17,13 +17,14 @@ __device__ __forceinline__ float sel4(const float4& v, int j) {
   return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
 }
 
-// Phase timestamps for in-kernel profiling (MnistFused::trace, off = null): blocks 0..63 of
+// Phase timestamps for in-kernel profiling (MnistFused::trace, off = null): blocks 0..1023 of
 // kernel `kid` record the 100 MHz wall clock at phase `ph` (<8) from thread 0.
-#define MX_TRACE(f, kid, ph)                                                                        \
+#define MX_TRACE_B(f, kid, ph, blk)                                                                 \
   do {                                                                                              \
-    if ((f).trace && threadIdx.x == 0 && blockIdx.x < 64)                                           \
-      (f).trace[((kid) * 64 + blockIdx.x) * 8 + (ph)] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
+    if ((f).trace && threadIdx.x == 0 && (blk) < 1024)                                              \
+      (f).trace[((kid) * 1024 + (blk)) * 8 + (ph)] = (uint32_t)__builtin_amdgcn_s_memrealtime();    \
   } while (0)
+#define MX_TRACE(f, kid, ph) MX_TRACE_B(f, kid, ph, (int)blockIdx.x)
 
 struct Scratch {  // carve of MnistFused::scratch (floats)
   float* wf;      // conv2 fwd B-fragments   [18 q][4 w][64 lane][4 j]

@@ -19,47 +19,42 @@ namespace {
 // Block = (image b, tap r); wave w owns co tile w (16) x both ci tiles (32).  GEMM K = the 576
 // output positions, walked in 16-position groups: lane group g takes positions 16s+4g .. +3,
 // i.e. 4 consecutive columns of one output row = 2 pooling windows -> A = expand(dp float2,
-// 2-bit argmax codes), B = a1 window row (LDS float4).  LDS (52.9 KB -> 3 blocks per CU, so
-// the 576-block grid runs in ONE round on 256 CUs): dp [64][148] (pitch 148: the 16 co rows x
-// 2 lane groups of a ds_read_b64 half-wave land on distinct banks), argmax codes packed 4 per
-// byte [64][36] (dead windows have dp = 0, so their code is irrelevant), a1 window chunk
-// [32][100] (4 output rows; pitch 100 = 25 x 16 B, odd, for ds_read_b128).
-constexpr int kF6DpP = 148, kF6Rows = 4, kF6Pos = kF6Rows * 24, kF6BP = 100, kF6Chunks = 24 / kF6Rows;
-constexpr size_t kF6Lds = sizeof(float) * (64 * kF6DpP + 32 * kF6BP) + 64 * 36;
-__global__ __launch_bounds__(256) void f6_conv2_wgrad_kernel(MnistFused f, Scratch sc) {
-  MX_TRACE(f, 3, 0);
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+// 2-bit argmax codes), B = a1 window row (LDS float4).  a1 is never read from HBM: each
+// 2-row chunk of the shifted a1 window is recomputed from the 28x28 input image in LDS
+// (conv1 + ReLU, 54 FMAs per thread per chunk, weights in registers), so F2 does not have to
+// publish a1 at all.  LDS (51.3 KB -> 3 blocks per CU): dp [64][148] (pitch 148: the 16 co
+// rows x 2 lane groups of a ds_read_b64 half-wave land on distinct banks), a1 chunk [32][52]
+// (pitch 52 = 13 x 16 B, odd, for ds_read_b128), x [784], conv1 w/b [320], argmax codes packed
+// 4 per byte [64][36] (dead windows have dp = 0, so their code is irrelevant).
+constexpr int kF6DpP = 148, kF6Rows = 2, kF6Pos = kF6Rows * 24, kF6BP = 52, kF6Chunks = 24 / kF6Rows;
+constexpr size_t kF6Lds = sizeof(float) * (64 * kF6DpP + 32 * kF6BP + 784 + 320) + 64 * 36;
+__device__ __forceinline__ void f6_body(const MnistFused& f, const Scratch& sc, float* sm, int braw, int nblk) {
+  MX_TRACE_B(f, 3, 0, braw);
   float* dps = sm;                                              // [64][148]
-  float* Bs = dps + 64 * kF6DpP;                                // [32][100]
-  uint8_t* qs = reinterpret_cast<uint8_t*>(Bs + 32 * kF6BP);    // [64][36] packed 2-bit codes
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);  // an image's 9 tap blocks share one XCD L2
+  float* Bs = dps + 64 * kF6DpP;                                // [32][52]
+  float* xs = Bs + 32 * kF6BP;                                  // [28][28]
+  float* w1s = xs + 784;                                        // conv1 w [32][9], b [32]
+  uint8_t* qs = reinterpret_cast<uint8_t*>(w1s + 320);          // [64][36] packed 2-bit codes
+  const int bid = xcd_remap(braw, nblk);  // an image's 9 tap blocks share one XCD L2
   const int r = bid % 9, b = bid / 9;
   const int ky = r / 3, kx = r - 3 * ky;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
-  const float* a1b = f.a1 + (size_t)b * 32 * 676 + ky * 26 + kx;
-  // a1 window rows oy0+ky .. +3, cols kx .. kx+23 for all 32 ci: 12 values per thread; the
-  // next chunk's loads are issued before this chunk's MFMAs (register double buffer).
-  constexpr int kPer = 32 * kF6Pos / 256;
-  float v[kPer];
-  auto load_chunk = [&](int oy0) {
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int i = tid + 256 * k, ci = i / kF6Pos, pos = i - ci * kF6Pos, row = pos / 24, col = pos - row * 24;
-      v[k] = a1b[ci * 676 + (oy0 + row) * 26 + col];
-    }
-  };
   // compact dY2 of image b: dp (float4 granules) and argmax codes (uint32 = 4 windows -> 1 byte)
   {
     const float4* src = reinterpret_cast<const float4*>(f.dp + (size_t)b * 9216);
     const uint32_t* qsrc = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(f.idx) + (size_t)b * 9216);
     float4 dv[9];
     uint32_t qv[9];
+    float xv[4], wv2[2];
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
       dv[k] = src[tid + 256 * k];
       qv[k] = qsrc[tid + 256 * k];
     }
-    load_chunk(0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xv[k] = f.x[b * 784 + min(tid + 256 * k, 783)];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) wv2[k] = f.p[L::w1 + min(tid + 256 * k, 319)];
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
       const int i = tid + 256 * k, co = i / 36, c4 = (i - co * 36) * 4;
@@ -67,22 +62,56 @@ __global__ __launch_bounds__(256) void f6_conv2_wgrad_kernel(MnistFused f, Scrat
       const uint32_t q = qv[k] & 0x03030303u;
       qs[i] = (uint8_t)(q | (q >> 6) | (q >> 12) | (q >> 18));
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (tid + 256 * k < 784) xs[tid + 256 * k] = xv[k];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (tid + 256 * k < 320) w1s[tid + 256 * k] = wv2[k];
   }
+  __syncthreads();
+  MX_TRACE_B(f, 3, 1, braw);
+  // conv1 role of this thread: channel cw, chunk row rr, 6 output columns from 6*cg
+  const int cw = tid >> 3, rr = (tid >> 2) & 1, cg = tid & 3;
+  float wk[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) wk[k] = w1s[cw * 9 + k];
+  const float bk = w1s[288 + cw];
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   const float* dpr = dps + (16 * w + m) * kF6DpP;
   const uint8_t* qr = qs + (16 * w + m) * 36;
+  // a1[cw][oy0 + ky + rr][kx + 6cg .. +5] = ReLU(conv1(x)) for chunk row oy0, into registers;
+  // chunk c+1 is computed in the same basic block as chunk c's MFMAs so the scheduler can
+  // interleave the FMAs with the (long-latency) MFMA issue
+  float av1[6];
+  auto conv1_chunk = [&](int oy0) {
+    const float* xp = xs + (oy0 + ky + rr) * 28 + kx + 6 * cg;
+    float xr[3][8];
 #pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) xr[dy][c] = xp[dy * 28 + c];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      float v = bk;
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) v = fmaf(xr[dy][c + dx], wk[dy * 3 + dx], v);
+      av1[c] = fmaxf(v, 0.f);
+    }
+  };
+  float* bo = Bs + cw * kF6BP + rr * 24 + 6 * cg;
+  conv1_chunk(0);
+#pragma unroll 1
   for (int ch = 0; ch < kF6Chunks; ++ch) {
     const int oy0 = ch * kF6Rows;
     if (ch > 0) __syncthreads();  // previous chunk's reads of Bs are done
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int i = tid + 256 * k, ci = i / kF6Pos, pos = i - ci * kF6Pos;
-      Bs[ci * kF6BP + pos] = v[k];
-    }
+    for (int c = 0; c < 6; ++c) bo[c] = av1[c];
     __syncthreads();
-    if (ch == 0) MX_TRACE(f, 3, 1);
-    if (ch + 1 < kF6Chunks) load_chunk(oy0 + kF6Rows);
+    // next chunk (clamped on the last iteration: branch-free, so it shares the MFMA block)
+    conv1_chunk(min(oy0 + kF6Rows, 24 - kF6Rows));
     const float* br0 = Bs + m * kF6BP + 4 * g;
     const float* br1 = Bs + (16 + m) * kF6BP + 4 * g;
 #pragma unroll
@@ -110,7 +139,7 @@ __global__ __launch_bounds__(256) void f6_conv2_wgrad_kernel(MnistFused f, Scrat
       acc[1] = mfma4(a3, b1.w, acc[1]);
     }
   }
-  MX_TRACE(f, 3, 2);
+  MX_TRACE_B(f, 3, 2, braw);
 #pragma unroll
   for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -118,7 +147,7 @@ __global__ __launch_bounds__(256) void f6_conv2_wgrad_kernel(MnistFused f, Scrat
       const int co = 16 * w + 4 * g + j, ci = 16 * c + m;
       atomicAdd(sc.wacc + (r * 64 + co) * 32 + ci, acc[c][j]);
     }
-  MX_TRACE(f, 3, 3);
+  MX_TRACE_B(f, 3, 3, braw);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -127,19 +156,20 @@ __global__ __launch_bounds__(256) void f6_conv2_wgrad_kernel(MnistFused f, Scrat
 // K = (r, co) = 576.  A = dY2[co][iy-ky][ix-kx] expanded from the compact pooled tiles in LDS:
 // 4 pooled rows x 14 window columns (a dead halo of one window on each side, so no bounds
 // checks), channel pitch 60 words (lane groups 16 banks apart).  B = pre-packed conv2 weight
-// fragments from L2, prefetched one tap ahead.  The epilogue masks with a1 > 0 and contracts
+// fragments from L2, prefetched one tap ahead.  The epilogue masks with a1 > 0 (conv1
+// recomputed from x and w1 in LDS: a1 is never stored) and contracts
 // with the 3x3 patches of x (LDS): dW1[ci][r] and db1[ci] are reduced in registers ->
 // cross-lane -> LDS -> one atomic per value per block.  dA1 never touches HBM.
 constexpr int kF7WR = 4, kF7WC = 14, kF7CoP = 60;
-constexpr size_t kF7Lds = sizeof(float) * (64 * kF7CoP + 784 + 1280) + 64 * kF7CoP;
-__global__ __launch_bounds__(256) void f7_conv2_dgrad_kernel(MnistFused f, Scratch sc) {
-  MX_TRACE(f, 4, 0);
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+constexpr size_t kF7Lds = sizeof(float) * (64 * kF7CoP + 784 + 320 + 1280) + 64 * kF7CoP;
+__device__ __forceinline__ void f7_body(const MnistFused& f, const Scratch& sc, float* sm, int braw, int nblk) {
+  MX_TRACE_B(f, 4, 0, braw);
   float* dps = sm;                                                  // [64][60] (4 x 14 used)
   float* xs = dps + 64 * kF7CoP;                                    // [784]
-  float* red = xs + 784;                                            // [4][32][10]
+  float* w1s = xs + 784;                                            // conv1 w [32][9], b [32]
+  float* red = w1s + 320;                                           // [4][32][10]
   uint8_t* qs = reinterpret_cast<uint8_t*>(red + 1280);             // [64][60]
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);  // an image's 11 blocks share one XCD L2
+  const int bid = xcd_remap(braw, nblk);  // an image's 11 blocks share one XCD L2
   const int b = bid / 11, chunk = bid - b * 11;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
   const uint8_t* idx = reinterpret_cast<const uint8_t*>(f.idx) + (size_t)b * 9216;
@@ -160,9 +190,11 @@ __global__ __launch_bounds__(256) void f7_conv2_dgrad_kernel(MnistFused f, Scrat
       dv[k] = dpb[o];
       qv[k] = idx[o];
     }
-    float xv[4];
+    float xv[4], wv2[2];
 #pragma unroll
     for (int k = 0; k < 4; ++k) xv[k] = f.x[b * 784 + min(tid + 256 * k, 783)];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) wv2[k] = f.p[L::w1 + min(tid + 256 * k, 319)];
 #pragma unroll
     for (int k = 0; k < 14; ++k) {
       const int i = tid + 256 * k, co = i / (kF7WR * kF7WC), rem = i - co * (kF7WR * kF7WC);
@@ -174,9 +206,12 @@ __global__ __launch_bounds__(256) void f7_conv2_dgrad_kernel(MnistFused f, Scrat
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (tid + 256 * k < 784) xs[tid + 256 * k] = xv[k];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (tid + 256 * k < 320) w1s[tid + 256 * k] = wv2[k];
   }
   __syncthreads();
-  MX_TRACE(f, 4, 1);
+  MX_TRACE_B(f, 4, 1, braw);
   const int pos = min(p0 + 16 * w + m, 675);  // this lane's A row (clamped tail rows are discarded)
   const int iy = pos / 26, ix = pos - iy * 26;
   const float4* wd = reinterpret_cast<const float4*>(sc.wd) + lane;
@@ -218,7 +253,7 @@ __global__ __launch_bounds__(256) void f7_conv2_dgrad_kernel(MnistFused f, Scrat
 #pragma unroll
     for (int i = 0; i < 8; ++i) bc[i] = bn[i];
   }
-  MX_TRACE(f, 4, 2);
+  MX_TRACE_B(f, 4, 2, braw);
   // epilogue: acc[c][j] = dA1 at position p = p0 + 16w + 4g + j, channel ci = 16c + m
   float part[2][10];
 #pragma unroll
@@ -234,7 +269,9 @@ __global__ __launch_bounds__(256) void f7_conv2_dgrad_kernel(MnistFused f, Scrat
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int ci = 16 * c + m;
-        const float a1v = f.a1[((size_t)b * 32 + ci) * 676 + p];
+        float a1v = w1s[288 + ci];  // conv1 pre-activation at p, recomputed (a1 is not stored)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) a1v = fmaf(xp[(k / 3) * 28 + k % 3], w1s[ci * 9 + k], a1v);
         const float gv = a1v > 0.f ? acc[c][j] : 0.f;
         part[c][9] += gv;
 #pragma unroll
@@ -269,7 +306,22 @@ __global__ __launch_bounds__(256) void f7_conv2_dgrad_kernel(MnistFused f, Scrat
     if (k < 9) atomicAdd(g1 + ci * 9 + k, v);  // conv1.weight grad [32][9]
     else atomicAdd(g1 + 288 + ci, v);          // conv1.bias grad [32]
   }
-  MX_TRACE(f, 4, 3);
+  MX_TRACE_B(f, 4, 3, braw);
+}
+
+// ------------------------------------------------------------------------------------------
+// F6 + F7 in ONE launch: blocks [0, 9B) run the weight gradient, the rest the data gradient.
+// The two are independent; sharing a grid lets the dispatcher backfill CUs as blocks retire
+// (576 + 704 blocks over 256 CUs at 3 per CU), so one kernel's prologue/epilogue latency and
+// the 2-vs-3-blocks-per-CU imbalance of each kernel alone are covered by the other's MFMA work.
+// 9B is a multiple of 8, so the F7 part keeps its XCD-aware block mapping.
+__global__ __launch_bounds__(256) void f67_conv2_bwd_kernel(MnistFused f, Scratch sc) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int n6 = 9 * f.B;
+  if ((int)blockIdx.x < n6)
+    f6_body(f, sc, sm, blockIdx.x, n6);
+  else
+    f7_body(f, sc, sm, blockIdx.x - n6, 11 * f.B);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -315,13 +367,13 @@ using namespace mnist;
 void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    MX_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f6_conv2_wgrad_kernel),
+    MX_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f67_conv2_bwd_kernel),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const Scratch sc = carve(f.scratch);
-  MX_LAUNCH(f6_conv2_wgrad_kernel, dim3(9 * f.B), dim3(256), kF6Lds, st, f, sc);
-  MX_LAUNCH(f7_conv2_dgrad_kernel, dim3(f.B * 11), dim3(256), kF7Lds, st, f, sc);
+  constexpr size_t lds = kF6Lds > kF7Lds ? kF6Lds : kF7Lds;
+  MX_LAUNCH(f67_conv2_bwd_kernel, dim3(9 * f.B + 11 * f.B), dim3(256), lds, st, f, sc);
   MX_LAUNCH(f8_finalize_kernel, dim3(kF8Wacc + kF8G1 + 8), dim3(256), 0, st, f, sc);
   MX_HIP_CHECK(hipGetLastError());
 }

@@ -166,6 +166,69 @@ struct ConvWgradOp {
   __device__ void store(int m, int n, float v, int) const { emit(dw, (int64_t)m * N + n, v, mode); }
 };
 
+// ------------------------------------------------------------------ 1x1 stride-1 convs
+// (ResNet bottlenecks): plain batched GEMMs over (n, hw) with channel-strided operands; no
+// im2col index math per element.
+struct Conv1x1FwdOp {  // y[n,k,hw] = sum_c x[n,c,hw] w[k,c]
+  static constexpr bool A_MFAST = true;   // consecutive m = consecutive hw
+  static constexpr bool B_NFAST = false;  // w rows contiguous along c
+  int M, N, K;
+  int HW;
+  FastDiv fHW;
+  const float* x;
+  const float* w;
+  const float* bias;
+  float* y;
+  bool relu;
+  struct APre { int64_t base; bool ok; };
+  struct BPre { int64_t base; bool ok; };
+  __device__ APre a_pre(int m) const {
+    const int mm = m < M ? m : 0, nb = fHW.div(mm), hw = mm - nb * HW;
+    return APre{(int64_t)nb * K * HW + hw, m < M};
+  }
+  __device__ float a_load(const APre& a, int k) const { return a.ok ? x[a.base + (int64_t)k * HW] : 0.f; }
+  __device__ BPre b_pre(int n) const { return BPre{(int64_t)(n < N ? n : 0) * K, n < N}; }
+  __device__ float b_load(const BPre& b, int k) const { return b.ok ? w[b.base + k] : 0.f; }
+  __device__ void store(int m, int n, float v, int) const {
+    const int nb = fHW.div(m), hw = m - nb * HW;
+    if (bias) v += bias[n];
+    if (relu) v = fmaxf(v, 0.f);
+    y[((int64_t)nb * N + n) * HW + hw] = v;
+  }
+};
+
+struct Conv1x1DgradOp {  // dx[n,c,hw] = sum_k dy[n,k,hw] w[k,c]
+  static constexpr bool A_MFAST = true;
+  static constexpr bool B_NFAST = true;   // w[k, c]: consecutive c contiguous
+  int M, N, K;
+  int HW;
+  FastDiv fHW;
+  const float* dy;
+  const float* w;
+  float* dx;
+  const float* mask;
+  int mode;
+  struct APre { int64_t base; bool ok; };
+  struct BPre { int n; bool ok; };
+  __device__ APre a_pre(int m) const {
+    const int mm = m < M ? m : 0, nb = fHW.div(mm), hw = mm - nb * HW;
+    return APre{(int64_t)nb * K * HW + hw, m < M};
+  }
+  __device__ float a_load(const APre& a, int k) const { return a.ok ? dy[a.base + (int64_t)k * HW] : 0.f; }
+  __device__ BPre b_pre(int n) const { return BPre{n, n < N}; }
+  __device__ float b_load(const BPre& b, int k) const { return b.ok ? w[(int64_t)k * N + b.n] : 0.f; }
+  __device__ void store(int m, int n, float v, int) const {
+    const int nb = fHW.div(m), hw = m - nb * HW;
+    const int64_t idx = ((int64_t)nb * N + n) * HW + hw;
+    if (mask && !(mask[idx] > 0.f)) v = 0.f;
+    emit(dx, idx, v, mode);
+  }
+};
+
+bool is_1x1_s1(const ConvShape& s) {
+  return s.R == 1 && s.S == 1 && s.str_h == 1 && s.str_w == 1 && s.pad_h == 0 && s.pad_w == 0;
+}
+
 // ------------------------------------------------------------------ linear
 struct LinFwdOp {  // y[M,N] = x[M,K] w[N,K]^T + b
   static constexpr bool A_MFAST = false;
@@ -243,6 +306,10 @@ void run(Op& op, int splits, hipStream_t st) {
 void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s,
                 bool relu, hipStream_t st) {
   if (g_gemm_precision == 0 && conv3x3_eligible(s)) return conv3x3_fwd(x, w, bias, y, s, relu, st);
+  if (is_1x1_s1(s)) {
+    Conv1x1FwdOp op{s.N * s.H * s.W, s.K, s.C, s.H * s.W, FastDiv(s.H * s.W), x, w, bias, y, relu};
+    return run(op, 1, st);
+  }
   ConvFwdOp op{s.N * s.P * s.Q, s.K, s.C * s.R * s.S, ConvG(s), x, w, bias, y, relu};
   run(op, 1, st);
 }
@@ -251,6 +318,11 @@ void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s
                   const float* relu_mask, bool accumulate, hipStream_t st, float* wt_scratch) {
   if (wt_scratch && g_gemm_precision == 0 && conv3x3_eligible(s))
     return conv3x3_dgrad(dy, w, dx, s, relu_mask, accumulate, wt_scratch, st);
+  if (is_1x1_s1(s)) {
+    Conv1x1DgradOp op{s.N * s.H * s.W, s.C, s.K, s.H * s.W, FastDiv(s.H * s.W), dy, w, dx, relu_mask,
+                      accumulate ? kAccum : kStore};
+    return run(op, 1, st);
+  }
   ConvDgradOp op{s.N * s.H * s.W, s.C, s.K * s.R * s.S, ConvG(s), dy, w, dx, relu_mask,
                  accumulate ? kAccum : kStore};
   run(op, 1, st);

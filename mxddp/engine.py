@@ -187,35 +187,49 @@ class FusedMnistTrainer:
         return m[0], m[1]
 
     def phase_profile(self, steps: int = 20) -> dict:
-        """In-kernel phase timings of the fused step (MnistFused::trace, s_memrealtime at 100 MHz):
-        runs `steps` eager steps with blocks 0..63 of each kernel stamping their phase
-        boundaries, and returns {kernel: [median us from phase 0 to phase k, ...]}."""
+        """In-kernel phase timings of the fused step (MnistFused::trace, s_memrealtime at 100 MHz).
+        Runs `steps` eager steps with every block of each fused kernel stamping its phase
+        boundaries.  Returns per kernel: block start spread (us after the first block started;
+        median / max), block duration (median / max) and the median time from block start to
+        each phase mark."""
         names = ["F2_fwd", "F3_fc1", "F5_head_fc1bwd", "F6_wgrad", "F7_dgrad"]
-        buf = torch.zeros(7 * 64 * 8, dtype=torch.int32, device=self.device)
+        buf = torch.zeros(7 * 1024 * 8, dtype=torch.int32, device=self.device)
         self.eng.set_trace(buf.data_ptr())
         acc = {n: [] for n in names}
         try:
             for _ in range(steps):
-                buf.zero_()
+                with torch.cuda.stream(self.stream):  # the engine's stream, not torch's current one
+                    buf.zero_()
                 self.eng.step()
                 self.eng.sync()
-                t = buf.view(7, 64, 8).cpu().to(torch.int64)
+                t = buf.view(7, 1024, 8).cpu().to(torch.int64) & 0xFFFFFFFF
                 for k, n in enumerate(names):
                     t0 = t[k, :, 0]
-                    rows = []
-                    for ph in range(1, 8):
-                        v = t[k, :, ph]
-                        ok = v != 0
-                        if ok.any():
-                            rows.append(((v[ok] - t0[ok]) & 0xFFFFFFFF).double().median().item() * 0.01)
-                    acc[n].append(rows)
+                    live = t0 != 0
+                    if not live.any():
+                        continue
+                    t0 = t0[live]
+                    tk = t[k][live]
+                    last = tk.max(dim=1).values
+                    rec = {"start_med": (t0 - t0.min()).double().median().item() * 0.01,
+                           "start_max": (t0 - t0.min()).max().item() * 0.01,
+                           "dur_med": (last - t0).double().median().item() * 0.01,
+                           "dur_max": (last - t0).max().item() * 0.01,
+                           "kernel": (last.max() - t0.min()).item() * 0.01}
+                    rec["phases"] = [((tk[:, ph] - t0)[tk[:, ph] != 0]).double().median().item() * 0.01
+                                     for ph in range(1, 8) if (tk[:, ph] != 0).any()]
+                    acc[n].append(rec)
         finally:
             self.eng.set_trace(0)
         out = {}
         for n, runs in acc.items():
-            runs = [r for r in runs[1:] if r]  # drop the first (cold) step
-            if runs:
-                out[n] = [round(sum(r[i] for r in runs) / len(runs), 2) for i in range(min(len(r) for r in runs))]
+            runs = runs[1:]  # drop the first (cold) step
+            if not runs:
+                continue
+            avg = {k: round(sum(r[k] for r in runs) / len(runs), 2) for k in runs[0] if k != "phases"}
+            m = min(len(r["phases"]) for r in runs)
+            avg["phases"] = [round(sum(r["phases"][i] for r in runs) / len(runs), 2) for i in range(m)]
+            out[n] = avg
         return out
 
     # --------------------------------------------------------------- state

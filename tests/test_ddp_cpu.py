@@ -133,3 +133,48 @@ def test_gloo_reducer_rejects_double_mark():
     r.mark_ready(0)
     with pytest.raises(RuntimeError):
         r.mark_ready(0)
+
+
+def _uid_worker(rank, ws, port, q):
+    """rccl_comm()'s rendezvous with the native communicator faked: every rank must receive rank
+    0's ncclUniqueId bytes through the TCPStore and build its Comm with (uid, rank, ws, device)."""
+    from mxddp.parallel import comm
+
+    comm.init_distributed(rank=rank, world_size=ws, use_gpu=False, init_method=f"tcp://127.0.0.1:{port}")
+
+    class FakeComm:
+        @staticmethod
+        def new_unique_id():
+            return bytes(range(128)) if rank == 0 else b"wrong-rank-generated-id"
+
+        def __init__(self, uid, r, w, dev):
+            self.args = (bytes(uid), r, w, dev)
+
+    class FakeNative:
+        Comm = FakeComm
+
+    orig_native, orig_info = comm.native, comm._INFO
+    comm.native = lambda: FakeNative
+    comm._INFO = comm.DistInfo(rank, ws, rank, ws, "nccl", torch.device("cuda", rank))
+    try:
+        c = comm.rccl_comm()
+        q.put((rank, c.args[0] == bytes(range(128)), c.args[1:]))
+    finally:
+        comm.native, comm._INFO = orig_native, orig_info
+        comm._COMM = None
+        comm.shutdown()
+
+
+def test_rccl_uid_rendezvous_ws4():
+    ws, port = 4, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_uid_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(ws))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for r, (rank, same_uid, rest) in enumerate(res):
+        assert rank == r and same_uid and rest == (r, ws, r), res
