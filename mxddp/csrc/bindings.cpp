@@ -29,10 +29,19 @@ PYBIND11_MODULE(_C, m) {
 
   // ---------------------------------------------------------------- GEMM-shaped ops
   m.def("conv2d_fwd", [](uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y, int N, int C, int H, int W, int K, int R,
-                         int S_, int sh, int sw, int ph, int pw, int dh, int dw, bool relu, uintptr_t st) {
+                         int S_, int sh, int sw, int ph, int pw, int dh, int dw, bool relu, uintptr_t st,
+                         uintptr_t scratch) {
     conv2d_fwd(P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y),
-               CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw), relu, S(st));
+               CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw), relu, S(st), P<float>(scratch));
+  }, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("y"), py::arg("N"), py::arg("C"), py::arg("H"), py::arg("W"),
+     py::arg("K"), py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
+     py::arg("dh"), py::arg("dw"), py::arg("relu"), py::arg("st"), py::arg("scratch") = 0);
+  m.def("conv_scratch_floats", [](int N, int C, int H, int W, int K, int R, int S_, int sh, int sw, int ph, int pw,
+                                  int dh, int dw) {
+    return conv_scratch_floats(CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw));
   });
+  m.def("set_conv_algo", &set_conv_algo, "3x3 s1 convs: 0 = auto (Winograd F(2x2,3x3) where eligible), 1 = direct");
+  m.def("conv_algo", &conv_algo);
   m.def("conv2d_dgrad", [](uintptr_t dy, uintptr_t w, uintptr_t dx, int N, int C, int H, int W, int K, int R, int S_,
                            int sh, int sw, int ph, int pw, int dh, int dw, uintptr_t mask, bool acc, uintptr_t st,
                            uintptr_t wt_scratch) {
@@ -42,9 +51,16 @@ PYBIND11_MODULE(_C, m) {
      py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"),
      py::arg("dw"), py::arg("mask"), py::arg("acc"), py::arg("st"), py::arg("wt_scratch") = 0);
   m.def("conv2d_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw_, int N, int C, int H, int W, int K, int R, int S_,
-                           int sh, int sw, int ph, int pw, int dh, int dw, bool acc, uintptr_t st) {
+                           int sh, int sw, int ph, int pw, int dh, int dw, bool acc, uintptr_t st,
+                           uintptr_t scratch) {
     conv2d_wgrad(P<const float>(dy), P<const float>(x), P<float>(dw_), CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw),
-                 acc, S(st));
+                 acc, S(st), P<float>(scratch));
+  }, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("N"), py::arg("C"), py::arg("H"), py::arg("W"), py::arg("K"),
+     py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"),
+     py::arg("dwd"), py::arg("acc"), py::arg("st"), py::arg("scratch") = 0);
+  m.def("conv_wgrad_scratch_floats", [](int N, int C, int H, int W, int K, int R, int S_, int sh, int sw, int ph,
+                                        int pw, int dh, int dw) {
+    return conv_wgrad_scratch_floats(CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw));
   });
   m.def("linear_fwd", [](uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y, int M, int N, int K, bool relu,
                          uintptr_t st) {

@@ -24,9 +24,9 @@ struct ConvShape {
 
 // ---- GEMM-shaped (ops_gemm.hip) ----
 void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s,
-                bool relu, hipStream_t st);
+                bool relu, hipStream_t st, float* scratch = nullptr);
 // dx = conv_transpose(dy, w) [* (mask > 0)], stored (=) or accumulated (+=).  `wt_scratch`
-// (K*C*9 floats, optional) enables the direct 3x3 path (conv3x3.hip) for eligible shapes.
+// (conv_scratch_floats(s) floats, optional) enables the Winograd / direct 3x3 paths.
 void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s,
                   const float* relu_mask, bool accumulate, hipStream_t st, float* wt_scratch = nullptr);
 // Direct-LDS 3x3 stride-1 pad-1 convolution (conv3x3.hip), fp32 MFMA; W <= 64.
@@ -37,9 +37,27 @@ void conv3x3_dgrad(const float* dy, const float* w, float* dx, const ConvShape& 
                    bool accumulate, float* wt_scratch, hipStream_t st);
 bool conv3x3_wgrad_eligible(const ConvShape& s);  // + W % 4 == 0
 void conv3x3_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate, hipStream_t st);
+// Fused Winograd F(2x2,3x3) on fp32 MFMA (winograd.hip): 3x3 s1 p1, square 8/16/32 images.
+// `scratch` holds the transformed filters: wino_scratch_floats(s) floats.
+bool wino_eligible(const ConvShape& s);
+size_t wino_scratch_floats(const ConvShape& s);
+void wino_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s, bool relu,
+              float* scratch, hipStream_t st);
+void wino_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s, const float* relu_mask,
+                bool accumulate, float* scratch, hipStream_t st);
+// partial-sum scratch: wino_wgrad_scratch_floats(s) floats (0 = none needed)
+size_t wino_wgrad_scratch_floats(const ConvShape& s);
+void wino_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate, float* scratch,
+                hipStream_t st);
+// 3x3 s1 algorithm: 0 = auto (Winograd where eligible, else direct-LDS), 1 = direct-LDS only.
+void set_conv_algo(int a);
+int conv_algo();
+// floats of scratch conv2d_fwd / conv2d_dgrad can use for this shape (0 = none needed)
+size_t conv_scratch_floats(const ConvShape& s);
 // dw (+)= sum_{n,p,q} dy * im2col(x)
 void conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate,
-                  hipStream_t st);
+                  hipStream_t st, float* scratch = nullptr);
+size_t conv_wgrad_scratch_floats(const ConvShape& s);
 // y[M,N] = x[M,K] @ w[N,K]^T + b  (optional ReLU)
 void linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int N, int K,
                 bool relu, hipStream_t st);

@@ -303,8 +303,31 @@ void run(Op& op, int splits, hipStream_t st) {
 
 }  // namespace
 
+namespace {
+int init_conv_algo() {
+  const char* e = std::getenv("MXDDP_CONV_ALGO");
+  return (e && std::string(e) == "direct") ? 1 : 0;
+}
+int g_conv_algo = init_conv_algo();
+bool use_wino(const ConvShape& s) { return g_gemm_precision == 0 && g_conv_algo == 0 && wino_eligible(s); }
+}  // namespace
+
+void set_conv_algo(int a) {
+  MX_CHECK(a == 0 || a == 1, "conv algo: 0 (auto: Winograd where eligible) or 1 (direct)");
+  g_conv_algo = a;
+}
+int conv_algo() { return g_conv_algo; }
+
+size_t conv_scratch_floats(const ConvShape& s) {
+  if (g_gemm_precision != 0) return 0;
+  if (wino_eligible(s)) return std::max(wino_scratch_floats(s), (size_t)s.K * s.C * 9);
+  if (conv3x3_eligible(s)) return (size_t)s.K * s.C * 9;
+  return 0;
+}
+
 void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s,
-                bool relu, hipStream_t st) {
+                bool relu, hipStream_t st, float* scratch) {
+  if (scratch && use_wino(s)) return wino_fwd(x, w, bias, y, s, relu, scratch, st);
   if (g_gemm_precision == 0 && conv3x3_eligible(s)) return conv3x3_fwd(x, w, bias, y, s, relu, st);
   if (is_1x1_s1(s)) {
     Conv1x1FwdOp op{s.N * s.H * s.W, s.K, s.C, s.H * s.W, FastDiv(s.H * s.W), x, w, bias, y, relu};
@@ -316,6 +339,7 @@ void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, con
 
 void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s,
                   const float* relu_mask, bool accumulate, hipStream_t st, float* wt_scratch) {
+  if (wt_scratch && use_wino(s)) return wino_dgrad(dy, w, dx, s, relu_mask, accumulate, wt_scratch, st);
   if (wt_scratch && g_gemm_precision == 0 && conv3x3_eligible(s))
     return conv3x3_dgrad(dy, w, dx, s, relu_mask, accumulate, wt_scratch, st);
   if (is_1x1_s1(s)) {
@@ -328,8 +352,12 @@ void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s
   run(op, 1, st);
 }
 
+size_t conv_wgrad_scratch_floats(const ConvShape& s) { return use_wino(s) ? wino_wgrad_scratch_floats(s) : 0; }
+
 void conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate,
-                  hipStream_t st) {
+                  hipStream_t st, float* scratch) {
+  if (use_wino(s) && (scratch || wino_wgrad_scratch_floats(s) == 0))
+    return wino_wgrad(dy, x, dw, s, accumulate, scratch, st);
   if (g_gemm_precision == 0 && conv3x3_wgrad_eligible(s)) return conv3x3_wgrad(dy, x, dw, s, accumulate, st);
   ConvWgradOp op{s.K, s.C * s.R * s.S, s.N * s.P * s.Q, ConvG(s), dy, x, dw, kAtomic};
   const int tiles = cdiv(op.M, 64) * cdiv(op.N, 64);

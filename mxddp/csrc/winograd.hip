@@ -1,0 +1,559 @@
+// Fused Winograd F(2x2, 3x3) convolution on fp32 MFMA (v_mfma_f32_16x16x4_f32), gfx950.
+//
+// 3x3 / stride-1 / pad-1 convolutions (PyramidNet: 101 of its 103 convs) computed as 16
+// independent GEMMs in the Winograd domain: M[xi][co][tile] = sum_ci U[xi][co][ci] V[xi][ci][tile]
+// with U = G g G^T (filters, transformed once per call by wino_wtrans_k) and V = B^T d B (4x4
+// input windows, transformed in registers inside the GEMM kernel).  The output transform
+// Y = A^T M A needs all 16 xi of one (co, tile): every one of the 16 GEMMs uses the SAME MFMA
+// fragment layout, so the 16 values of an output tile sit in the same lane and register slot of
+// the 16 accumulators and the transform is lane-local (no LDS round trip, no second kernel).
+// 2.25x fewer MFMA FLOPs than the direct convolution; all arithmetic is fp32 (the 1/2 factors
+// of G are exact), the same algorithm family cuDNN / MIOpen select for fp32 3x3 convolutions.
+//
+// Forward / data gradient (wino_fwd_kernel): block = 32 output channels x 32 output tiles
+// (2x2 pixels each), 4 waves in 2 x 2, each 16 channels x 16 tiles = 1 MFMA tile x 16 xi
+// = 64 accumulator registers (3 blocks / 12 waves per CU).  Per chunk of 8 input channels: each
+// thread transforms one 4x4 window (prefetched into registers during the previous chunk's
+// MFMAs) into V in LDS, copies its part of the chunk's U slice (float4) into LDS, then 32 MFMAs
+// per wave.  The data gradient is the same
+// kernel on dy with the flipped / transposed filters (wino_wtrans_k, dgrad=1).  When the grid
+// would not fill the chip (8x8 images) the input channels are split across blocks (atomics).
+//
+// Weight gradient (wino_wgrad_kernel): F(3x3, 2x2): dW = A'^T [ sum_tiles (G' dy G'^T) o
+// (B^T x B) ] A', 16 GEMMs reducing over output tiles.  Block = 32 co x 32 ci x a range of
+// 8-tile chunks; the 3x3 result of each (co, ci) is formed lane-locally and written to a
+// per-range partial plane, summed in a fixed order by a second kernel (deterministic).
+//
+// Replaces (reference): cuDNN conv fwd / bwd-data / bwd-filter for pytorch/model.py:28-32.
+#include "common.h"
+#include "ops.h"
+
+#include <algorithm>
+#include <cstdlib>
+
+namespace mx {
+
+namespace {
+
+constexpr int kCC = 8;   // reduction rows per chunk (2 MFMA k-steps of 4)
+constexpr int kP = 48;   // LDS pitch of 32-wide rows: the 4 lane groups of an MFMA operand read
+                         // land on banks 0/48/32/16 (mod 64) -> conflict-free
+constexpr size_t kLds = sizeof(float) * (2 * 16 * kCC * kP);  // 49,152 B -> 3 blocks/CU
+
+// V = B^T d B, B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]]  (d, v: row-major 4x4)
+__device__ __forceinline__ void in_transform(const float* d, float* v) {
+  float e[16];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    e[0 + j] = d[0 + j] - d[8 + j];
+    e[4 + j] = d[4 + j] + d[8 + j];
+    e[8 + j] = d[8 + j] - d[4 + j];
+    e[12 + j] = d[4 + j] - d[12 + j];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[4 * i + 0] = e[4 * i + 0] - e[4 * i + 2];
+    v[4 * i + 1] = e[4 * i + 1] + e[4 * i + 2];
+    v[4 * i + 2] = e[4 * i + 2] - e[4 * i + 1];
+    v[4 * i + 3] = e[4 * i + 1] - e[4 * i + 3];
+  }
+}
+
+// U = G g G^T, G = [[1,0,0],[1/2,1/2,1/2],[1/2,-1/2,1/2],[0,0,1]]  (g: 3x3 row-major)
+__device__ __forceinline__ void filter_transform(const float* g, float* u) {
+  float t[12];  // 4x3
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    t[0 + j] = g[j];
+    t[3 + j] = 0.5f * (g[j] + g[3 + j] + g[6 + j]);
+    t[6 + j] = 0.5f * (g[j] - g[3 + j] + g[6 + j]);
+    t[9 + j] = g[6 + j];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    u[4 * i + 0] = t[3 * i];
+    u[4 * i + 1] = 0.5f * (t[3 * i] + t[3 * i + 1] + t[3 * i + 2]);
+    u[4 * i + 2] = 0.5f * (t[3 * i] - t[3 * i + 1] + t[3 * i + 2]);
+    u[4 * i + 3] = t[3 * i + 2];
+  }
+}
+
+// W = G' y G'^T, G' = [[1,0],[1/2,1/2],[1/2,-1/2],[0,1]]  (y: 2x2 row-major) -- F(3x3, 2x2)
+__device__ __forceinline__ void dy_transform(const float* y, float* w) {
+  float t[8];  // 4x2
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    t[0 + j] = y[j];
+    t[2 + j] = 0.5f * (y[j] + y[2 + j]);
+    t[4 + j] = 0.5f * (y[j] - y[2 + j]);
+    t[6 + j] = y[2 + j];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    w[4 * i + 0] = t[2 * i];
+    w[4 * i + 1] = 0.5f * (t[2 * i] + t[2 * i + 1]);
+    w[4 * i + 2] = 0.5f * (t[2 * i] - t[2 * i + 1]);
+    w[4 * i + 3] = t[2 * i + 1];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Filter transform: U[xi][ci][co] (ci padded to Cip = 8k, co padded to Cop = 32k, zeros in the
+// padding).  fwd: co = k, ci = c, g = w[k][c].  dgrad: co = c, ci = k, g = flip(w[k][c]).
+__global__ void wino_wtrans_k(const float* __restrict__ w, float* __restrict__ U, int K, int C, int Cip,
+                              int Cop, int dgrad) {
+  const int total = Cip * Cop;
+  const size_t plane = (size_t)Cip * Cop;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int ci = i / Cop, co = i - ci * Cop;
+    const int k = dgrad ? ci : co, c = dgrad ? co : ci;
+    float g[9], u[16];
+    if (k < K && c < C) {
+      const float* src = w + ((size_t)k * C + c) * 9;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) g[t] = dgrad ? src[8 - t] : src[t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) g[t] = 0.f;
+    }
+    filter_transform(g, u);
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) U[xi * plane + i] = u[xi];
+  }
+}
+
+// One chunk (8 reduction rows) of the 16 Winograd-domain GEMMs: 32 MFMAs, each fed by one A and
+// one B operand read from LDS.  The schedule is pinned to a software pipeline (8 operand reads
+// ahead, then {1 MFMA, 2 reads}): left alone the scheduler hoists all 64 reads above the first
+// MFMA, which costs 64 registers and pushes the kernel off 3 waves per SIMD (pinned in the
+// forward kernel; the weight-gradient kernel fits without it and measured worse with it).
+template <bool kPin>
+__device__ __forceinline__ void mfma_chunk(const float* ap, const float* bp, f32x4* acc) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) {
+      const int ro = (xi * kCC + 4 * s) * kP;
+      acc[xi] = __builtin_amdgcn_mfma_f32_16x16x4f32(ap[ro], bp[ro], acc[xi], 0, 0, 0);
+    }
+  if constexpr (kPin) {
+  __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // DS read
+#pragma unroll
+  for (int i = 0; i < 30; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+  }
+  __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+  }
+}
+
+struct WinoArgs {
+  const float* x;     // [N][Ci][W][W]
+  const float* U;     // [16][Cip][Cop]
+  const float* bias;  // [Co] or null
+  const float* mask;  // [N][Co][W][W] or null
+  float* y;           // [N][Co][W][W]
+  int N, Ci, Co, Cip, Cop;
+  int tblocks, ktiles, splits, chunks_per_split;
+  int relu, accumulate;  // accumulate: 0 store, 1 y += result, 2 atomicAdd (split reduction)
+};
+
+// 4x4 window of one (plane, tile).  Every load is issued (clamped to the plane's first element
+// when outside the image) and the zeros are selected later, in zero_outside() at LDS-store time:
+// selecting right after the loads would make the wave wait for them before the MFMAs they are
+// meant to overlap.  Offsets are 32-bit byte offsets from the kernel-uniform tensor base
+// (saddr + voffset loads) and are made opaque to the loop, so the compiler recomputes the 16
+// window offsets per chunk instead of hoisting them into 16 long-lived registers.
+template <int W>
+__device__ __forceinline__ void load_window(const float* __restrict__ base, uint32_t plane, int off, unsigned m,
+                                            float* d) {
+  asm volatile("" : "+v"(off), "+v"(m));
+  const char* b = reinterpret_cast<const char*>(base);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const bool ok = (m >> e) & 1u;
+    const uint32_t byte = 4u * (plane + (ok ? (uint32_t)(off + (e >> 2) * W + (e & 3)) : 0u));
+    d[e] = *reinterpret_cast<const float*>(b + byte);
+  }
+}
+
+__device__ __forceinline__ void zero_outside(float* d, unsigned m) {
+#pragma unroll
+  for (int e = 0; e < 16; ++e) d[e] = (m >> e) & 1u ? d[e] : 0.f;
+}
+
+template <int W>
+__device__ __forceinline__ unsigned window_mask(int h0, int w0) {
+  unsigned m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if ((unsigned)(h0 + i) < (unsigned)W && (unsigned)(w0 + j) < (unsigned)W) m |= 1u << (4 * i + j);
+  return m;
+}
+
+// Block: 32 output channels x 32 output tiles; wave (wm, wn) owns 16 x 16 of it for all 16 xi
+// (16 accumulators = 64 registers) -> ~120 VGPRs, 3 blocks (12 waves) per CU.
+template <int W, int kOcc>
+__global__ __launch_bounds__(256, kOcc) void wino_fwd_kernel(WinoArgs a) {
+  constexpr int TW = W / 2, TPI = TW * TW, HW = W * W;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* As = sm;                   // U slice [16][8 ci][kP] (32 co)
+  float* Bs = sm + 16 * kCC * kP;   // V slice [16][8 ci][kP] (32 tiles)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kt = bid % a.ktiles, r1 = bid / a.ktiles;
+  const int tb = r1 % a.tblocks, sp = r1 / a.tblocks;
+  const int co0 = kt * 32;
+  const int ntiles = a.N * TPI;
+  const int ch_beg = sp * a.chunks_per_split, ch_end = min(a.Cip / kCC, ch_beg + a.chunks_per_split);
+
+  // transform role: tile tid & 31 of the block, input channel tid >> 5 of each chunk
+  const int tt = tid & 31, cl = tid >> 5;
+  const int my_t = tb * 32 + tt;
+  const bool t_ok = my_t < ntiles;
+  const int tn = t_ok ? my_t / TPI : 0, trem = t_ok ? my_t - tn * TPI : 0;
+  const int th = trem / TW, tw = trem - th * TW;
+  const unsigned vmask = t_ok ? window_mask<W>(2 * th - 1, 2 * tw - 1) : 0u;
+  const uint32_t xn = (uint32_t)tn * a.Ci * HW;
+  const int woff = (2 * th - 1) * W + 2 * tw - 1;
+  // U slice copy role: 16 xi x 8 ci rows of 32 floats = 1024 float4, 4 per thread: thread t
+  // copies float4 (t & 7) of row (xi, ci) = (4q + (t >> 6), (t >> 3) & 7), q = 0..3
+  const uint32_t u_lane = 4u * (((uint32_t)(tid >> 6) * a.Cip + ((tid >> 3) & 7)) * a.Cop + co0 + 4 * (tid & 7));
+  const uint32_t u_q = 4u * 4u * a.Cip * a.Cop, u_ch = 4u * kCC * a.Cop;  // byte strides
+  float* as_st = As + (tid >> 3) * kP + 4 * (tid & 7);                       // + q * 32 rows
+
+  float raw[16];
+  f32x4 ru[4];
+  unsigned rmask = 0;
+  auto gload = [&](int ch) {
+    const int c = ch * kCC + cl;
+    rmask = c < a.Ci ? vmask : 0u;
+    load_window<W>(a.x, xn + (uint32_t)min(c, a.Ci - 1) * HW, woff, rmask, raw);
+    const char* ub = reinterpret_cast<const char*>(a.U) + (size_t)ch * u_ch;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ru[q] = *reinterpret_cast<const f32x4*>(ub + u_lane + q * u_q);
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4*>(as_st + q * 32 * kP) = ru[q];
+    float v[16];
+    zero_outside(raw, rmask);
+    in_transform(raw, v);
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) Bs[(xi * kCC + cl) * kP + tt] = v[xi];
+  };
+
+  f32x4 acc[16];
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi) acc[xi] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const float* ap = As + g * kP + 16 * wm + l16;
+  const float* bp = Bs + g * kP + 16 * wn + l16;
+  if (ch_beg < ch_end) gload(ch_beg);
+  for (int ch = ch_beg; ch < ch_end; ++ch) {
+    if (ch != ch_beg) __syncthreads();  // previous chunk's LDS reads are done
+    sstore();
+    __syncthreads();
+    if (ch + 1 < ch_end) gload(ch + 1);
+    mfma_chunk<true>(ap, bp, acc);
+  }
+
+  // epilogue: row = output channel, column = output tile; Y = A^T M A, A^T = [[1,1,1,0],[0,1,-1,-1]]
+  const int T = tb * 32 + 16 * wn + l16;
+  if (T >= ntiles) return;
+  const int n = T / TPI, rem = T - n * TPI, oh = 2 * (rem / TW), ow = 2 * (rem % TW);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int co = co0 + 16 * wm + 4 * g + r;
+    if (co >= a.Co) continue;
+    float t0[4], t1[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      t0[c] = acc[0 + c][r] + acc[4 + c][r] + acc[8 + c][r];
+      t1[c] = acc[4 + c][r] - acc[8 + c][r] - acc[12 + c][r];
+    }
+    const float y[2][2] = {{t0[0] + t0[1] + t0[2], t0[1] - t0[2] - t0[3]},
+                           {t1[0] + t1[1] + t1[2], t1[1] - t1[2] - t1[3]}};
+    const float bv = (a.bias && sp == 0) ? a.bias[co] : 0.f;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const size_t o = ((size_t)n * a.Co + co) * HW + (size_t)(oh + p) * W + ow;
+      float2 v = make_float2(y[p][0] + bv, y[p][1] + bv);
+      if (a.accumulate == 2) {
+        atomicAdd(a.y + o, v.x);
+        atomicAdd(a.y + o + 1, v.y);
+        continue;
+      }
+      if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); }
+      if (a.mask) {
+        const float2 mk = *reinterpret_cast<const float2*>(a.mask + o);
+        if (!(mk.x > 0.f)) v.x = 0.f;
+        if (!(mk.y > 0.f)) v.y = 0.f;
+      }
+      if (a.accumulate) {
+        const float2 old = *reinterpret_cast<const float2*>(a.y + o);
+        v.x += old.x;
+        v.y += old.y;
+      }
+      *reinterpret_cast<float2*>(a.y + o) = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+struct WinoWArgs {
+  const float* dy;  // [N][K][W][W]
+  const float* x;   // [N][C][W][W]
+  float* out;       // nblk == 1: dw [K][C][3][3]; else partials [nblk][K][C][9]
+  int N, C, K;
+  int ktiles, ctiles, nchunks, chunks_per_block;
+  int accumulate;   // nblk == 1 only: dw += result
+};
+
+// Block: 32 co x 32 ci x a range of 8-tile chunks; wave (wm, wn) owns 16 co x 16 ci for all 16 xi.
+template <int W>
+__global__ __launch_bounds__(256, 3) void wino_wgrad_kernel(WinoWArgs a) {
+  constexpr int TW = W / 2, TPI = TW * TW, HW = W * W;
+  static_assert(TPI % 8 == 0, "8-tile chunks must not straddle images");
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* As = sm;                   // transformed dy [16][8 tiles][kP] (32 co)
+  float* Bs = sm + 16 * kCC * kP;   // transformed x  [16][8 tiles][kP] (32 ci)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kt = bid % a.ktiles, r1 = bid / a.ktiles;
+  const int ct = r1 % a.ctiles, rb = r1 / a.ctiles;
+  const int k0 = kt * 32, c0 = ct * 32;
+  const int ch_beg = rb * a.chunks_per_block, ch_end = min(a.nchunks, ch_beg + a.chunks_per_block);
+
+  const int tt = tid & 7, cl = tid >> 3;  // tile within the chunk; channel row (co for dy, ci for x)
+  const bool k_ok = k0 + cl < a.K, c_ok = c0 + cl < a.C;
+  const float* dyk = a.dy + (size_t)min(k0 + cl, a.K - 1) * HW;
+  const uint32_t xc = (uint32_t)min(c0 + cl, a.C - 1) * HW;
+  float rdy[4], rx[16];
+  unsigned xmask = 0;
+  auto gload = [&](int ch) {
+    const int T = ch * 8 + tt, n = T / TPI, rem = T - n * TPI, th = rem / TW, tw = rem - th * TW;
+    const float* p = dyk + (size_t)n * a.K * HW + (2 * th) * W + 2 * tw;
+    const float2 r0 = *reinterpret_cast<const float2*>(p), r1v = *reinterpret_cast<const float2*>(p + W);
+    rdy[0] = r0.x;
+    rdy[1] = r0.y;
+    rdy[2] = r1v.x;
+    rdy[3] = r1v.y;
+    xmask = c_ok ? window_mask<W>(2 * th - 1, 2 * tw - 1) : 0u;
+    load_window<W>(a.x, xc + (uint32_t)n * a.C * HW, (2 * th - 1) * W + 2 * tw - 1, xmask, rx);
+  };
+  auto sstore = [&]() {
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rdy[i] = k_ok ? rdy[i] : 0.f;
+    zero_outside(rx, xmask);
+    dy_transform(rdy, v);
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) As[(xi * kCC + tt) * kP + cl] = v[xi];
+    in_transform(rx, v);
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) Bs[(xi * kCC + tt) * kP + cl] = v[xi];
+  };
+
+  f32x4 acc[16];
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi) acc[xi] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const float* ap = As + g * kP + 16 * wm + l16;
+  const float* bp = Bs + g * kP + 16 * wn + l16;
+  if (ch_beg < ch_end) gload(ch_beg);
+  for (int ch = ch_beg; ch < ch_end; ++ch) {
+    if (ch != ch_beg) __syncthreads();
+    sstore();
+    __syncthreads();
+    if (ch + 1 < ch_end) gload(ch + 1);
+    mfma_chunk<false>(ap, bp, acc);
+  }
+
+  // epilogue: row = co, column = ci; dW = A'^T M A', A'^T = [[1,1,1,0],[0,1,-1,0],[0,1,1,-1]]
+  const int ci = c0 + 16 * wn + l16;
+  if (ci >= a.C) return;
+  const size_t plane = (size_t)a.K * a.C * 9;
+  float* dst_base = a.out + (size_t)rb * plane;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int co = k0 + 16 * wm + 4 * g + r;
+    if (co >= a.K) continue;
+    float t[3][4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float m0 = acc[c][r], m1 = acc[4 + c][r], m2 = acc[8 + c][r], m3 = acc[12 + c][r];
+      t[0][c] = m0 + m1 + m2;
+      t[1][c] = m1 - m2;
+      t[2][c] = m1 + m2 - m3;
+    }
+    float* dst = dst_base + ((size_t)co * a.C + ci) * 9;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      float v0 = t[ky][0] + t[ky][1] + t[ky][2], v1 = t[ky][1] - t[ky][2], v2 = t[ky][1] + t[ky][2] - t[ky][3];
+      if (a.accumulate) {
+        v0 += dst[3 * ky];
+        v1 += dst[3 * ky + 1];
+        v2 += dst[3 * ky + 2];
+      }
+      dst[3 * ky] = v0;
+      dst[3 * ky + 1] = v1;
+      dst[3 * ky + 2] = v2;
+    }
+  }
+}
+
+// dw (+)= sum over nblk partial planes (fixed order -> deterministic)
+__global__ void wino_wgrad_reduce_k(const float* __restrict__ part, float* __restrict__ dw, int64_t plane, int nblk,
+                                    int accumulate) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < plane; i += (int64_t)gridDim.x * 256) {
+    float s = accumulate ? dw[i] : 0.f;
+    for (int b = 0; b < nblk; ++b) s += part[b * plane + i];
+    dw[i] = s;
+  }
+}
+
+int pad_to(int v, int m) { return (v + m - 1) / m * m; }
+
+void launch_fwd(const float* x, const float* w, const float* bias, const float* mask, float* y, int N, int Ci,
+                int Co, int Wd, bool relu, bool accumulate, bool dgrad, float* U, int K_w, int C_w,
+                hipStream_t st) {
+  const int Cip = pad_to(Ci, kCC), Cop = pad_to(Co, 32);
+  {
+    const int total = Cip * Cop;
+    MX_LAUNCH(wino_wtrans_k, dim3(std::min(cdiv(total, 256), 2048)), dim3(256), 0, st, w, U, K_w, C_w, Cip, Cop,
+              dgrad ? 1 : 0);
+  }
+  WinoArgs a{};
+  a.x = x;
+  a.U = U;
+  a.bias = bias;
+  a.mask = mask;
+  a.y = y;
+  a.N = N;
+  a.Ci = Ci;
+  a.Co = Co;
+  a.Cip = Cip;
+  a.Cop = Cop;
+  const int tpi = (Wd / 2) * (Wd / 2);
+  a.tblocks = cdiv(N * tpi, 32);
+  a.ktiles = Cop / 32;
+  const int nch = Cip / kCC;
+  // split the input channels when the grid would not fill 256 CUs x 3 blocks (e.g. 8x8 images);
+  // only for plain outputs (no ReLU / mask), each split adds its partial result atomically
+  int splits = 1;
+  const int base = a.tblocks * a.ktiles;
+  if (!relu && !mask && base < 768) splits = std::max(1, std::min(cdiv(768, base), nch / 4));
+  a.chunks_per_split = cdiv(nch, splits);
+  a.splits = cdiv(nch, a.chunks_per_split);
+  a.relu = relu;
+  if (a.splits > 1) {
+    if (!accumulate) MX_HIP_CHECK(hipMemsetAsync(y, 0, sizeof(float) * (size_t)N * Co * Wd * Wd, st));
+    a.accumulate = 2;
+  } else {
+    a.accumulate = accumulate ? 1 : 0;
+  }
+  const dim3 grid(a.tblocks * a.ktiles * a.splits);
+  static const int occ = [] {
+    const char* e = std::getenv("MXDDP_WINO_OCC");
+    return e ? std::atoi(e) : 2;
+  }();
+  if (occ == 3) {
+    switch (Wd) {
+      case 8: MX_LAUNCH((wino_fwd_kernel<8, 3>), grid, dim3(256), kLds, st, a); break;
+      case 16: MX_LAUNCH((wino_fwd_kernel<16, 3>), grid, dim3(256), kLds, st, a); break;
+      case 32: MX_LAUNCH((wino_fwd_kernel<32, 3>), grid, dim3(256), kLds, st, a); break;
+      default: MX_CHECK(false, "winograd: unsupported width");
+    }
+    return;
+  }
+  switch (Wd) {
+    case 8: MX_LAUNCH((wino_fwd_kernel<8, 2>), grid, dim3(256), kLds, st, a); break;
+    case 16: MX_LAUNCH((wino_fwd_kernel<16, 2>), grid, dim3(256), kLds, st, a); break;
+    case 32: MX_LAUNCH((wino_fwd_kernel<32, 2>), grid, dim3(256), kLds, st, a); break;
+    default: MX_CHECK(false, "winograd: unsupported width");
+  }
+}
+
+struct WgradPlan {
+  int ktiles, ctiles, nchunks, cpb, nblk;
+};
+WgradPlan wgrad_plan(const ConvShape& s) {
+  WgradPlan p{};
+  p.ktiles = cdiv(s.K, 32);
+  p.ctiles = cdiv(s.C, 32);
+  p.nchunks = s.N * (s.W / 2) * (s.W / 2) / 8;
+  // ~3 blocks per CU, >= 8 chunks (256 MFMAs per wave) per block; partial planes capped at
+  // 8M floats of scratch (small layers may use many, large ones at least 16)
+  const int tiles = p.ktiles * p.ctiles;
+  const int cap = std::max(16, (int)std::min<int64_t>(1024, (8ll << 20) / ((int64_t)s.K * s.C * 9)));
+  int nblk = std::max(1, std::min(cdiv(768, tiles), cap));
+  nblk = std::min(nblk, std::max(1, p.nchunks / 8));
+  p.cpb = cdiv(p.nchunks, nblk);
+  p.nblk = cdiv(p.nchunks, p.cpb);
+  return p;
+}
+
+}  // namespace
+
+bool wino_eligible(const ConvShape& s) {
+  return s.R == 3 && s.S == 3 && s.str_h == 1 && s.str_w == 1 && s.pad_h == 1 && s.pad_w == 1 && s.dil_h == 1 &&
+         s.dil_w == 1 && s.H == s.W && s.P == s.H && s.Q == s.W && (s.W == 8 || s.W == 16 || s.W == 32);
+}
+
+size_t wino_scratch_floats(const ConvShape& s) {
+  // fwd: Cip(C) x Cop(K); dgrad: Cip(K) x Cop(C)
+  const size_t f = (size_t)pad_to(s.C, kCC) * pad_to(s.K, 32), d = (size_t)pad_to(s.K, kCC) * pad_to(s.C, 32);
+  return 16 * std::max(f, d);
+}
+
+size_t wino_wgrad_scratch_floats(const ConvShape& s) {
+  const WgradPlan p = wgrad_plan(s);
+  return p.nblk > 1 ? (size_t)p.nblk * s.K * s.C * 9 : 0;
+}
+
+void wino_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s, bool relu,
+              float* scratch, hipStream_t st) {
+  launch_fwd(x, w, bias, nullptr, y, s.N, s.C, s.K, s.W, relu, false, false, scratch, s.K, s.C, st);
+}
+
+void wino_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s, const float* relu_mask,
+                bool accumulate, float* scratch, hipStream_t st) {
+  launch_fwd(dy, w, nullptr, relu_mask, dx, s.N, s.K, s.C, s.W, false, accumulate, true, scratch, s.K, s.C, st);
+}
+
+void wino_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate, float* scratch,
+                hipStream_t st) {
+  const WgradPlan p = wgrad_plan(s);
+  MX_CHECK(p.nblk == 1 || scratch, "winograd wgrad: partial-sum scratch required");
+  WinoWArgs a{};
+  a.dy = dy;
+  a.x = x;
+  a.out = p.nblk > 1 ? scratch : dw;
+  a.N = s.N;
+  a.C = s.C;
+  a.K = s.K;
+  a.ktiles = p.ktiles;
+  a.ctiles = p.ctiles;
+  a.nchunks = p.nchunks;
+  a.chunks_per_block = p.cpb;
+  a.accumulate = (p.nblk == 1 && accumulate) ? 1 : 0;
+  const dim3 grid(p.ktiles * p.ctiles * p.nblk);
+  switch (s.W) {
+    case 8: MX_LAUNCH(wino_wgrad_kernel<8>, grid, dim3(256), kLds, st, a); break;
+    case 16: MX_LAUNCH(wino_wgrad_kernel<16>, grid, dim3(256), kLds, st, a); break;
+    case 32: MX_LAUNCH(wino_wgrad_kernel<32>, grid, dim3(256), kLds, st, a); break;
+    default: MX_CHECK(false, "winograd wgrad: unsupported width");
+  }
+  if (p.nblk > 1) {
+    const int64_t plane = (int64_t)s.K * s.C * 9;
+    MX_LAUNCH(wino_wgrad_reduce_k, dim3((unsigned)std::min<int64_t>((plane + 255) / 256, 2048)), dim3(256), 0, st,
+              scratch, dw, plane, p.nblk, accumulate ? 1 : 0);
+  }
+}
+
+}  // namespace mx

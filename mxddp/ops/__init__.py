@@ -80,8 +80,10 @@ class _Conv2d(torch.autograd.Function):
         Q = (W + 2 * pw - dw * (S - 1) - 1) // sw + 1
         y = torch.empty((N, K, P, Q), device=x.device, dtype=x.dtype)
         st = stream_of(x)
+        ns = C.conv_scratch_floats(N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw)
+        scr = torch.empty((ns,), device=x.device, dtype=x.dtype) if ns else None
         C.conv2d_fwd(x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph, pw,
-                     dh, dw, bool(relu), st)
+                     dh, dw, bool(relu), st, _p(scr))
         ctx.geom = (N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw, P, Q)
         ctx.relu = relu
         ctx.has_bias = b is not None
@@ -102,14 +104,17 @@ class _Conv2d(torch.autograd.Function):
         dx = dw_ = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            # scratch for the direct 3x3 path's flipped/transposed weights (ignored otherwise)
-            wt = torch.empty_like(w) if (R == 3 and S == 3 and sh == sw == 1 and ph == pw == 1) else None
+            # scratch for the 3x3 paths' transformed / flipped filters (none needed otherwise)
+            ns = C.conv_scratch_floats(N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw)
+            wt = torch.empty((ns,), device=dy.device, dtype=dy.dtype) if ns else None
             C.conv2d_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph, pw,
                            dh, dw, 0, False, st, 0 if wt is None else wt.data_ptr())
         if ctx.needs_input_grad[1]:
             dw_ = torch.empty_like(w)
+            ns = C.conv_wgrad_scratch_floats(N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw)
+            ws = torch.empty((ns,), device=dy.device, dtype=dy.dtype) if ns else None
             C.conv2d_wgrad(dy.data_ptr(), x.data_ptr(), dw_.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph, pw,
-                           dh, dw, False, st)
+                           dh, dw, False, st, _p(ws))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = torch.empty((K,), device=dy.device, dtype=dy.dtype)
             C.bias_grad(dy.data_ptr(), db.data_ptr(), N, K, P * Q, False, st)

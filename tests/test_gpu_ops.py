@@ -28,6 +28,9 @@ CONV_CASES = [
     (1, 12, 28, 27 + 1, 65, 3, 3, 1, 1),
     (1, 8, 56, 56, 24, 3, 3, 1, 1),
     (2, 5, 13, 16, 7, 3, 3, 1, 1),
+    # Winograd F(2x2,3x3) path (winograd.hip): split-C grid (8x8, many channels), partial tile blocks
+    (16, 191, 8, 8, 196, 3, 3, 1, 1),
+    (4, 101, 16, 16, 106, 3, 3, 1, 1),
 ]
 
 
@@ -57,6 +60,48 @@ def test_conv2d_fwd_bwd(cuda, case, relu):
     assert _rel(xg.grad.cpu(), xr.grad) < 1e-4
     assert _rel(wg.grad.cpu(), wr.grad) < 1e-4
     assert _rel(bg.grad.cpu(), br.grad) < 1e-4
+
+
+WINO_CASES = [
+    # N, C, W, K  (3x3 s1 p1, square)
+    (2, 16, 32, 21),
+    (3, 37, 16, 45),
+    (5, 191, 8, 196),
+    (64, 271, 8, 10),
+    (1, 8, 8, 8),
+]
+
+
+@pytest.mark.parametrize("case", WINO_CASES)
+def test_winograd_vs_direct_fp64(cuda, case):
+    """Winograd and direct-LDS 3x3 paths against an fp64 oracle: Winograd's extra rounding
+    (transforms) must stay within a small factor of the direct path's fp32 error."""
+    import mxddp
+
+    C_ = mxddp.native()
+    N, C, W, K = case
+    torch.manual_seed(1)
+    x = torch.randn(N, C, W, W)
+    w = torch.randn(K, C, 3, 3) / (3 * C ** 0.5)
+    gy = torch.randn(N, K, W, W)
+    xr, wr = x.double().requires_grad_(), w.double().requires_grad_()
+    yr = F.conv2d(xr, wr, None, 1, 1)
+    yr.backward(gy.double())
+    errs = {}
+    prev = C_.conv_algo()
+    try:
+        for algo in (0, 1):
+            C_.set_conv_algo(algo)
+            xg, wg = x.to(cuda).requires_grad_(), w.to(cuda).requires_grad_()
+            y = ops.conv2d(xg, wg, None, 1, 1)
+            y.backward(gy.to(cuda))
+            torch.cuda.synchronize()
+            errs[algo] = [_rel(y.cpu().double(), yr.detach()), _rel(xg.grad.cpu().double(), xr.grad),
+                          _rel(wg.grad.cpu().double(), wr.grad)]
+    finally:
+        C_.set_conv_algo(prev)
+    for e_w, e_d in zip(errs[0], errs[1]):
+        assert e_w < 2e-5 and e_w < 8 * e_d + 1e-6, errs
 
 
 @pytest.mark.parametrize("M,N,K", [(64, 128, 9216), (64, 10, 128), (100, 1000, 784), (7, 33, 65)])
