@@ -114,11 +114,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_splits", &bn_splits);
   m.def("bn_fwd_train", [](uintptr_t x, uintptr_t g, uintptr_t b, uintptr_t y, uintptr_t mean, uintptr_t invstd,
                            uintptr_t rm, uintptr_t rv, int N, int C, int HW, float mom, float eps, bool relu,
-                           uintptr_t acc, uintptr_t acc_next, int hiwater, uintptr_t st) {
+                           uintptr_t acc, uintptr_t acc_next, int hiwater, uintptr_t st, uintptr_t nbt) {
     bn_fwd_train(P<const float>(x), P<const float>(g), P<const float>(b), P<float>(y), P<float>(mean), P<float>(invstd),
                  P<float>(rm), P<float>(rv), N, C, HW, mom, eps, relu, P<float>(acc), P<float>(acc_next), hiwater,
-                 S(st));
-  });
+                 S(st), P<int64_t>(nbt));
+  }, py::arg("x"), py::arg("g"), py::arg("b"), py::arg("y"), py::arg("mean"), py::arg("invstd"), py::arg("rm"),
+     py::arg("rv"), py::arg("N"), py::arg("C"), py::arg("HW"), py::arg("mom"), py::arg("eps"), py::arg("relu"),
+     py::arg("acc"), py::arg("acc_next"), py::arg("hiwater"), py::arg("st"), py::arg("num_batches") = 0);
   m.def("bn_fwd_eval", [](uintptr_t x, uintptr_t g, uintptr_t b, uintptr_t y, uintptr_t rm, uintptr_t rv, int N, int C,
                           int HW, float eps, bool relu, uintptr_t st) {
     bn_fwd_eval(P<const float>(x), P<const float>(g), P<const float>(b), P<float>(y), P<const float>(rm),

@@ -110,7 +110,7 @@ int bn_splits(int N, int C, int HW);
 void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* y, float* mean,
                   float* invstd, float* run_mean, float* run_var, int N, int C, int HW,
                   float momentum, float eps, bool relu, float* acc, float* acc_next, int hiwater,
-                  hipStream_t st);
+                  hipStream_t st, int64_t* num_batches = nullptr);  // num_batches: += 1 on device
 void bn_fwd_eval(const float* x, const float* gamma, const float* beta, float* y,
                  const float* run_mean, const float* run_var, int N, int C, int HW, float eps,
                  bool relu, hipStream_t st);

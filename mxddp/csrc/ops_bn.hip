@@ -115,10 +115,14 @@ __global__ __launch_bounds__(kBnTB) void bn_apply_k(const float* __restrict__ x,
                                                     float* __restrict__ invstd_out, float* __restrict__ run_mean,
                                                     float* __restrict__ run_var, float* __restrict__ y, int C, int HW,
                                                     FastDiv dhw, FastDiv dc, int64_t total, float cnt, float eps,
-                                                    float momentum, int relu, int hiwater) {
+                                                    float momentum, int relu, int hiwater,
+                                                    int64_t* __restrict__ num_batches) {
   const int64_t step = (int64_t)gridDim.x * kBnTB;
-  if (blockIdx.x == 0)  // channels >= C that an earlier, wider call left dirty in acc_next
+  if (blockIdx.x == 0) {  // channels >= C that an earlier, wider call left dirty in acc_next
     for (int k = 2 * C + threadIdx.x; k < 2 * hiwater; k += kBnTB) acc_next[k] = 0.f;
+    // BatchNorm2d.num_batches_tracked += 1, here instead of a separate launch per layer
+    if (num_batches && threadIdx.x == 0) *num_batches += 1;
+  }
   const int vw = VEC ? 4 : 1;
   const int plane = HW / vw;  // vector elements per (n, c) plane
   for (int64_t i = blockIdx.x * (int64_t)kBnTB + threadIdx.x; i < total / vw; i += step) {
@@ -280,7 +284,7 @@ int bn_splits(int N, int C, int HW) {
 
 void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* invstd,
                   float* run_mean, float* run_var, int N, int C, int HW, float momentum, float eps, bool relu,
-                  float* acc, float* acc_next, int hiwater, hipStream_t st) {
+                  float* acc, float* acc_next, int hiwater, hipStream_t st, int64_t* num_batches) {
   MX_CHECK((int64_t)N * C * HW < (1ll << 31), "bn: tensor too large for 32-bit index math");
   const int S = bn_splits(N, C, HW);
   const bool vec = HW % 4 == 0;
@@ -290,11 +294,11 @@ void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* 
   if (vec) {
     MX_LAUNCH(bn_stats_k<true>, dim3(S, C), dim3(kBnTB), 0, st, x, N, C, HW, S, dv, acc);
     MX_LAUNCH(bn_apply_k<true>, dim3(apply_grid(total / 4)), dim3(kBnTB), 0, st, x, gamma, beta, acc, acc_next, mean,
-              invstd, run_mean, run_var, y, C, HW, dv, dc, total, cnt, eps, momentum, relu ? 1 : 0, hiwater);
+              invstd, run_mean, run_var, y, C, HW, dv, dc, total, cnt, eps, momentum, relu ? 1 : 0, hiwater, num_batches);
   } else {
     MX_LAUNCH(bn_stats_k<false>, dim3(S, C), dim3(kBnTB), 0, st, x, N, C, HW, S, dv, acc);
     MX_LAUNCH(bn_apply_k<false>, dim3(apply_grid(total)), dim3(kBnTB), 0, st, x, gamma, beta, acc, acc_next, mean,
-              invstd, run_mean, run_var, y, C, HW, dv, dc, total, cnt, eps, momentum, relu ? 1 : 0, hiwater);
+              invstd, run_mean, run_var, y, C, HW, dv, dc, total, cnt, eps, momentum, relu ? 1 : 0, hiwater, num_batches);
   }
 }
 

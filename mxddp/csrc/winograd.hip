@@ -377,8 +377,8 @@ __global__ __launch_bounds__(256, 3) void wino_wgrad_kernel(WinoWArgs a) {
   // epilogue: row = co, column = ci; dW = A'^T M A', A'^T = [[1,1,1,0],[0,1,-1,0],[0,1,1,-1]]
   const int ci = c0 + 16 * wn + l16;
   if (ci >= a.C) return;
-  const size_t plane = (size_t)a.K * a.C * 9;
-  float* dst_base = a.out + (size_t)rb * plane;
+  const size_t pstride = ((size_t)a.K * a.C * 9 + 3) & ~(size_t)3;  // 16-byte aligned partial planes
+  float* dst_base = a.out + (size_t)rb * pstride;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int co = k0 + 16 * wm + 4 * g + r;
@@ -407,13 +407,54 @@ __global__ __launch_bounds__(256, 3) void wino_wgrad_kernel(WinoWArgs a) {
   }
 }
 
-// dw (+)= sum over nblk partial planes (fixed order -> deterministic)
-__global__ void wino_wgrad_reduce_k(const float* __restrict__ part, float* __restrict__ dw, int64_t plane, int nblk,
-                                    int accumulate) {
+// dw (+)= sum over nblk partial planes (fixed order -> deterministic).  float4 lanes, four
+// independent partial sums so the loads of four planes are in flight at once.
+__global__ void wino_wgrad_reduce_k(const float* __restrict__ part, float* __restrict__ dw, int64_t plane,
+                                    int64_t pstride, int nblk, int accumulate) {
+  // partial plane b starts at part + b * pstride (pstride = plane rounded up to 4 floats)
+  const int64_t n4 = plane >> 2, s4 = pstride >> 2;
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  float4* d4 = reinterpret_cast<float4*>(dw);
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 s[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    int b = 0;
+    for (; b + 4 <= nblk; b += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 v = p4[(b + u) * s4 + i];
+        s[u].x += v.x; s[u].y += v.y; s[u].z += v.z; s[u].w += v.w;
+      }
+    }
+    for (; b < nblk; ++b) {
+      const float4 v = p4[b * s4 + i];
+      s[0].x += v.x; s[0].y += v.y; s[0].z += v.z; s[0].w += v.w;
+    }
+    float4 r = make_float4((s[0].x + s[1].x) + (s[2].x + s[3].x), (s[0].y + s[1].y) + (s[2].y + s[3].y),
+                           (s[0].z + s[1].z) + (s[2].z + s[3].z), (s[0].w + s[1].w) + (s[2].w + s[3].w));
+    if (accumulate) {
+      const float4 o = d4[i];
+      r.x += o.x; r.y += o.y; r.z += o.z; r.w += o.w;
+    }
+    d4[i] = r;
+  }
+  // tail (plane % 4), one thread
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (int64_t i = n4 << 2; i < plane; ++i) {
+      float t = accumulate ? dw[i] : 0.f;
+      for (int b = 0; b < nblk; ++b) t += part[b * pstride + i];
+      dw[i] = t;
+    }
+}
+
+// same reduction for a destination that is not 16-byte aligned
+__global__ void wino_wgrad_reduce_scalar_k(const float* __restrict__ part, float* __restrict__ dw, int64_t plane,
+                                           int64_t pstride, int nblk, int accumulate) {
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < plane; i += (int64_t)gridDim.x * 256) {
-    float s = accumulate ? dw[i] : 0.f;
-    for (int b = 0; b < nblk; ++b) s += part[b * plane + i];
-    dw[i] = s;
+    float t = accumulate ? dw[i] : 0.f;
+    for (int b = 0; b < nblk; ++b) t += part[b * pstride + i];
+    dw[i] = t;
   }
 }
 
@@ -487,8 +528,10 @@ WgradPlan wgrad_plan(const ConvShape& s) {
   p.ktiles = cdiv(s.K, 32);
   p.ctiles = cdiv(s.C, 32);
   p.nchunks = s.N * (s.W / 2) * (s.W / 2) / 8;
-  // ~3 blocks per CU, >= 8 chunks (256 MFMAs per wave) per block; partial planes capped at
-  // 8M floats of scratch (small layers may use many, large ones at least 16)
+  // ~3 blocks per CU, >= 8 chunks (256 MFMAs per wave) per block; the partial planes capped at
+  // 8M floats of scratch (small layers may use many, large ones at least 16).  Filling the chip
+  // wins over partial-sum traffic: with a 2M cap the PyramidNet step lost 3 ms of wgrad time to
+  // gain 1 ms of reduction time.
   const int tiles = p.ktiles * p.ctiles;
   const int cap = std::max(16, (int)std::min<int64_t>(1024, (8ll << 20) / ((int64_t)s.K * s.C * 9)));
   int nblk = std::max(1, std::min(cdiv(768, tiles), cap));
@@ -513,7 +556,7 @@ size_t wino_scratch_floats(const ConvShape& s) {
 
 size_t wino_wgrad_scratch_floats(const ConvShape& s) {
   const WgradPlan p = wgrad_plan(s);
-  return p.nblk > 1 ? (size_t)p.nblk * s.K * s.C * 9 : 0;
+  return p.nblk > 1 ? (size_t)p.nblk * (((size_t)s.K * s.C * 9 + 3) & ~(size_t)3) : 0;
 }
 
 void wino_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s, bool relu,
@@ -550,9 +593,14 @@ void wino_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, 
     default: MX_CHECK(false, "winograd wgrad: unsupported width");
   }
   if (p.nblk > 1) {
-    const int64_t plane = (int64_t)s.K * s.C * 9;
-    MX_LAUNCH(wino_wgrad_reduce_k, dim3((unsigned)std::min<int64_t>((plane + 255) / 256, 2048)), dim3(256), 0, st,
-              scratch, dw, plane, p.nblk, accumulate ? 1 : 0);
+    const int64_t plane = (int64_t)s.K * s.C * 9, pstride = (plane + 3) & ~(int64_t)3;
+    if (reinterpret_cast<uintptr_t>(dw) & 15) {
+      MX_LAUNCH(wino_wgrad_reduce_scalar_k, dim3((unsigned)std::min<int64_t>((plane + 255) / 256, 2048)), dim3(256), 0,
+                st, scratch, dw, plane, pstride, p.nblk, accumulate ? 1 : 0);
+      return;
+    }
+    MX_LAUNCH(wino_wgrad_reduce_k, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((plane / 4 + 255) / 256, 2048))),
+              dim3(256), 0, st, scratch, dw, plane, pstride, p.nblk, accumulate ? 1 : 0);
   }
 }
 

@@ -56,13 +56,12 @@ class BatchNorm2d(nn.BatchNorm2d):
 
     def forward(self, x):
         training = self.training or not self.track_running_stats
-        if self.training and self.track_running_stats:
-            self.num_batches_tracked.add_(1)
+        nbt = self.num_batches_tracked if (self.training and self.track_running_stats) else None
         mom = self.momentum if self.momentum is not None else 0.1
         return ops.batch_norm(x, self.weight, self.bias,
                               self.running_mean if self.track_running_stats else None,
                               self.running_var if self.track_running_stats else None,
-                              training, mom, self.eps, relu=self.fuse_relu)
+                              training, mom, self.eps, relu=self.fuse_relu, num_batches=nbt)
 
 
 def count_params(model: nn.Module) -> int:

@@ -64,6 +64,29 @@ def _pair(v):
     return (v, v) if isinstance(v, int) else tuple(v)
 
 
+# ------------------------------------------------------------- direct gradient writing
+# Parameters re-homed into a flat buffer (mxddp.parallel.flat.FlatParams) carry
+# ``_mx_grad_ready``: their ``.grad`` is a view of the flat gradient buffer, so the backward
+# kernels accumulate straight into it (accumulate=True; zero_grad zeroes the buffer once per
+# step) and the op returns None to autograd.  That removes one temporary gradient tensor and
+# one autograd accumulation kernel per parameter per step (415 for PyramidNet).  Autograd still
+# runs the parameter's AccumulateGrad node (with no gradient) and its post-accumulate-grad
+# hooks, so DDP's bucket-readiness hook fires exactly as on the returned-gradient path.
+def _grad_sink(p):
+    if p is None or not p.requires_grad:
+        return None
+    cb = getattr(p, "_mx_grad_ready", None)
+    g = p.grad
+    if cb is None or g is None or not g.is_contiguous() or g.dtype != torch.float32:
+        return None
+    return g
+
+
+def _grad_done(p):
+    """Gradient written in place; readiness is signalled by autograd's post-accumulate hook."""
+    return None
+
+
 # --------------------------------------------------------------------------- conv2d
 class _Conv2d(torch.autograd.Function):
     @staticmethod
@@ -87,6 +110,7 @@ class _Conv2d(torch.autograd.Function):
         ctx.geom = (N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw, P, Q)
         ctx.relu = relu
         ctx.has_bias = b is not None
+        ctx.bias_ref = b
         ctx.save_for_backward(x, w, y if relu else None)
         return y
 
@@ -109,15 +133,24 @@ class _Conv2d(torch.autograd.Function):
             wt = torch.empty((ns,), device=dy.device, dtype=dy.dtype) if ns else None
             C.conv2d_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph, pw,
                            dh, dw, 0, False, st, 0 if wt is None else wt.data_ptr())
+        b = ctx.bias_ref
         if ctx.needs_input_grad[1]:
-            dw_ = torch.empty_like(w)
+            sink = _grad_sink(w)
+            dw_ = sink if sink is not None else torch.empty_like(w)
             ns = C.conv_wgrad_scratch_floats(N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw)
             ws = torch.empty((ns,), device=dy.device, dtype=dy.dtype) if ns else None
             C.conv2d_wgrad(dy.data_ptr(), x.data_ptr(), dw_.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph, pw,
-                           dh, dw, False, st, _p(ws))
+                           dh, dw, sink is not None, st, _p(ws))
+            if sink is not None:
+                _grad_done(w)
+                dw_ = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = torch.empty((K,), device=dy.device, dtype=dy.dtype)
-            C.bias_grad(dy.data_ptr(), db.data_ptr(), N, K, P * Q, False, st)
+            sink = _grad_sink(b)
+            db = sink if sink is not None else torch.empty((K,), device=dy.device, dtype=dy.dtype)
+            C.bias_grad(dy.data_ptr(), db.data_ptr(), N, K, P * Q, sink is not None, st)
+            if sink is not None:
+                _grad_done(b)
+                db = None
         return dx, dw_, db, None, None, None, None
 
 
@@ -145,6 +178,7 @@ class _Linear(torch.autograd.Function):
             C.relu_fwd(y.data_ptr(), y.data_ptr(), y.numel(), st)
         ctx.relu = relu
         ctx.has_bias = b is not None
+        ctx.bias_ref = b
         ctx.in_shape = x.shape
         ctx.save_for_backward(x2, w, y if relu else None)
         return y.reshape(*x.shape[:-1], N)
@@ -167,11 +201,20 @@ class _Linear(torch.autograd.Function):
             C.linear_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), M, N, K, 0, False, st)
             dx = dx.reshape(ctx.in_shape)
         if ctx.needs_input_grad[1]:
-            dw = torch.empty_like(w)
-            C.linear_wgrad(dy.data_ptr(), x2.data_ptr(), dw.data_ptr(), M, N, K, False, st)
+            sink = _grad_sink(w)
+            dw = sink if sink is not None else torch.empty_like(w)
+            C.linear_wgrad(dy.data_ptr(), x2.data_ptr(), dw.data_ptr(), M, N, K, sink is not None, st)
+            if sink is not None:
+                _grad_done(w)
+                dw = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = torch.empty((N,), device=dy.device, dtype=dy.dtype)
-            C.bias_grad(dy.data_ptr(), db.data_ptr(), M, N, 1, False, st)
+            b = ctx.bias_ref
+            sink = _grad_sink(b)
+            db = sink if sink is not None else torch.empty((N,), device=dy.device, dtype=dy.dtype)
+            C.bias_grad(dy.data_ptr(), db.data_ptr(), M, N, 1, sink is not None, st)
+            if sink is not None:
+                _grad_done(b)
+                db = None
         return dx, dw, db, None
 
 
@@ -285,7 +328,7 @@ def avg_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False):
 # --------------------------------------------------------------------------- batch norm
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, running_mean, running_var, training, momentum, eps, relu):
+    def forward(ctx, x, gamma, beta, running_mean, running_var, training, momentum, eps, relu, num_batches=None):
         C = native()
         x = x.contiguous()
         _check(x, "input")
@@ -299,7 +342,7 @@ class _BatchNorm(torch.autograd.Function):
             acc, acc_next, hi = _bn_acc(x.device, "fwd", Cc)
             C.bn_fwd_train(x.data_ptr(), _p(gamma), _p(beta), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
                            _p(running_mean), _p(running_var), N, Cc, HW, float(momentum), float(eps), bool(relu),
-                           acc.data_ptr(), acc_next.data_ptr(), hi, st)
+                           acc.data_ptr(), acc_next.data_ptr(), hi, st, _p(num_batches))
         else:
             mean = running_mean
             invstd = (running_var + eps).rsqrt()
@@ -308,6 +351,7 @@ class _BatchNorm(torch.autograd.Function):
         ctx.save_for_backward(x, gamma, mean, invstd, y if relu else None)
         ctx.dims = (N, Cc, HW)
         ctx.has_affine = gamma is not None
+        ctx.affine_refs = (gamma, beta)
         return y
 
     @staticmethod
@@ -316,13 +360,23 @@ class _BatchNorm(torch.autograd.Function):
         N, Cc, HW = ctx.dims
         dy = dy.contiguous()
         dx = torch.empty_like(x)
-        dg = torch.empty((Cc,), device=x.device) if ctx.has_affine else None
-        db = torch.empty((Cc,), device=x.device) if ctx.has_affine else None
+        g_ref, b_ref = ctx.affine_refs
+        gs, bs = (_grad_sink(g_ref), _grad_sink(b_ref)) if ctx.has_affine else (None, None)
+        direct = gs is not None and bs is not None
+        if direct:
+            dg, db = gs, bs
+        else:
+            dg = torch.empty((Cc,), device=x.device) if ctx.has_affine else None
+            db = torch.empty((Cc,), device=x.device) if ctx.has_affine else None
         acc, acc_next, hi = _bn_acc(x.device, "bwd", Cc)
         native().bn_bwd(dy.data_ptr(), x.data_ptr(), _p(y), _p(gamma), mean.data_ptr(), invstd.data_ptr(),
-                        dx.data_ptr(), _p(dg), _p(db), N, Cc, HW, False, acc.data_ptr(), acc_next.data_ptr(), hi,
+                        dx.data_ptr(), _p(dg), _p(db), N, Cc, HW, direct, acc.data_ptr(), acc_next.data_ptr(), hi,
                         stream_of(dy))
-        return dx, dg, db, None, None, None, None, None, None
+        if direct:
+            _grad_done(g_ref)
+            _grad_done(b_ref)
+            dg = db = None
+        return dx, dg, db, None, None, None, None, None, None, None
 
 
 _BN_ACC: dict = {}
@@ -344,9 +398,15 @@ def _bn_acc(device, kind, C):
     return buf[p], buf[p ^ 1], hi
 
 
-def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum=0.1, eps=1e-5, relu=False):
+def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum=0.1, eps=1e-5, relu=False,
+               num_batches=None):
+    """``num_batches`` (int64 tensor, GPU path): incremented on device by the BN kernel
+    (BatchNorm2d.num_batches_tracked) instead of a separate launch per layer."""
     if _native(x):
-        return _BatchNorm.apply(x, gamma, beta, running_mean, running_var, training, momentum, eps, relu)
+        return _BatchNorm.apply(x, gamma, beta, running_mean, running_var, training, momentum, eps, relu,
+                                num_batches if training else None)
+    if num_batches is not None and training:
+        num_batches.add_(1)
     y = F.batch_norm(x, running_mean, running_var, gamma, beta, training, momentum, eps)
     return F.relu(y) if relu else y
 
@@ -394,10 +454,12 @@ class _ShortcutAdd(torch.autograd.Function):
         x = x.contiguous()
         N, Cin, H, W = x.shape
         _, Cout, P, Q = out.shape
-        y = out.clone()
-        native().shortcut_pad_add(x.data_ptr(), y.data_ptr(), N, Cin, H, W, Cout, P, Q, stride, stream_of(x))
+        # in place: `out` (the block's last BN output) has no other consumer and BN's backward
+        # does not read its own output, so the residual add needs no copy
+        native().shortcut_pad_add(x.data_ptr(), out.data_ptr(), N, Cin, H, W, Cout, P, Q, stride, stream_of(x))
+        ctx.mark_dirty(out)
         ctx.dims = (N, Cin, H, W, Cout, P, Q, stride)
-        return y
+        return out
 
     @staticmethod
     def backward(ctx, dy):
@@ -412,6 +474,8 @@ class _ShortcutAdd(torch.autograd.Function):
 def shortcut_pad_add(out, x, stride):
     """out + AvgPool2d(2,2,ceil)(F.pad(x, channels -> out.C)) (pytorch/model.py:17-21,49)."""
     if _native(out):
+        if out.is_leaf and out.requires_grad:  # the in-place add needs a non-leaf (or grad-free) tensor
+            out = out.clone()
         return _ShortcutAdd.apply(out, x, stride)
     sc = F.pad(x, (0, 0, 0, 0, 0, out.shape[1] - x.shape[1]))
     if stride == 2:

@@ -79,6 +79,8 @@ class DistributedDataParallel(nn.Module):
         else:
             self.reducer = _GlooReducer(self.flat.grad, self.buckets, self.param_bucket, average, self.world_size)
         self._queued = False
+        # fires on both gradient paths: returned gradients and gradients the GPU kernels wrote
+        # straight into the flat buffer (mxddp.ops._grad_sink; AccumulateGrad still runs)
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(self.flat.params)]
 
     # ------------------------------------------------------------------ sync helpers

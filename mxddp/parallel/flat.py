@@ -22,6 +22,10 @@ def _al(n: int) -> int:
     return (n + _ALIGN - 1) // _ALIGN * _ALIGN
 
 
+def _noop():
+    return None
+
+
 class FlatParams:
     def __init__(self, module: nn.Module, device: torch.device | None = None):
         self.params = [p for p in module.parameters() if p.requires_grad]
@@ -38,6 +42,10 @@ class FlatParams:
             for p, o in zip(self.params, self.offsets):
                 self.data[o:o + p.numel()].copy_(p.detach().reshape(-1))
                 p.data = self.data[o:o + p.numel()].view_as(p)
+        # marker for direct gradient writing (mxddp.ops._grad_sink): GPU backward kernels
+        # accumulate into p.grad (a view of self.grad) instead of returning a gradient
+        for p in self.params:
+            p._mx_grad_ready = _noop
         self.attach_grads()
 
     def attach_grads(self) -> None:

@@ -180,8 +180,10 @@ def test_batchnorm(cuda, relu, shape, offset):
     agree = ((y.detach().cpu() > 0) == (yr.detach() > 0)) if relu else torch.ones_like(yr, dtype=torch.bool)
     assert agree.float().mean().item() > 1 - 1e-5
     assert _rel(xg.grad.cpu() * agree, xr.grad * agree) < 1e-4
-    assert _rel(gg.grad.cpu(), gr.grad) < 2e-3 if relu else _rel(gg.grad.cpu(), gr.grad) < 1e-4
-    assert _rel(bg.grad.cpu(), br.grad) < 1e-4
+    # dgamma / dbeta sum dy over the ReLU mask: a threshold disagreement (atomic reduction order
+    # moves the batch mean by an ulp) shifts them by that element's dy
+    assert _rel(gg.grad.cpu(), gr.grad) < (2e-3 if relu else 1e-4)
+    assert _rel(bg.grad.cpu(), br.grad) < (2e-3 if relu else 1e-4)
     assert _rel(rmg.cpu(), rm) < 1e-5 and _rel(rvg.cpu(), rv) < 1e-5
     # a second call reuses the self-resetting ticket counters
     y2 = ops.batch_norm(xg.detach(), gg, bg, rmg, rvg, True, 0.1, 1e-5, relu=relu)
