@@ -318,11 +318,31 @@ void set_conv_algo(int a) {
 }
 int conv_algo() { return g_conv_algo; }
 
+// dgrad of a stride-1 convolution = forward convolution of dy with the flipped, transposed
+// filters w'[c][k][R-1-r][S-1-s] and padding R-1-p (conv2d_dgrad uses it when it is allowed a
+// scratch buffer and needs no ReLU mask / accumulation): the forward gather is much cheaper
+// than the generic dgrad gather with its stride / divisibility tests.
+bool dgrad_as_fwd(const ConvShape& s) {
+  return s.str_h == 1 && s.str_w == 1 && s.dil_h == 1 && s.dil_w == 1 && !(s.R == 1 && s.S == 1) &&
+         s.pad_h <= s.R - 1 && s.pad_w <= s.S - 1;
+}
+
+__global__ void flip_transpose_any_k(const float* __restrict__ w, float* __restrict__ wt, int K, int C, int RS) {
+  const int64_t total = (int64_t)K * C * RS;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int tap = (int)(i % RS);
+    const int64_t kc = i / RS;
+    const int c = (int)(kc % C), k = (int)(kc / C);
+    wt[((int64_t)c * K + k) * RS + (RS - 1 - tap)] = w[i];
+  }
+}
+
 size_t conv_scratch_floats(const ConvShape& s) {
-  if (g_gemm_precision != 0) return 0;
-  if (wino_eligible(s)) return std::max(wino_scratch_floats(s), (size_t)s.K * s.C * 9);
-  if (conv3x3_eligible(s)) return (size_t)s.K * s.C * 9;
-  return 0;
+  size_t n = dgrad_as_fwd(s) ? (size_t)s.K * s.C * s.R * s.S : 0;
+  if (g_gemm_precision != 0) return n;
+  if (wino_eligible(s)) n = std::max(n, wino_scratch_floats(s));
+  if (conv3x3_eligible(s)) n = std::max(n, (size_t)s.K * s.C * 9);
+  return n;
 }
 
 void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s,
@@ -342,6 +362,14 @@ void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s
   if (wt_scratch && use_wino(s)) return wino_dgrad(dy, w, dx, s, relu_mask, accumulate, wt_scratch, st);
   if (wt_scratch && g_gemm_precision == 0 && conv3x3_eligible(s))
     return conv3x3_dgrad(dy, w, dx, s, relu_mask, accumulate, wt_scratch, st);
+  if (wt_scratch && !relu_mask && !accumulate && dgrad_as_fwd(s)) {
+    const int64_t total = (int64_t)s.K * s.C * s.R * s.S;
+    MX_LAUNCH(flip_transpose_any_k, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 2048)), dim3(256), 0, st, w,
+              wt_scratch, s.K, s.C, s.R * s.S);
+    const ConvShape t = ConvShape::make(s.N, s.K, s.P, s.Q, s.C, s.R, s.S, 1, 1, s.R - 1 - s.pad_h, s.S - 1 - s.pad_w);
+    ConvFwdOp op{t.N * t.P * t.Q, t.K, t.C * t.R * t.S, ConvG(t), dy, wt_scratch, nullptr, dx, false};
+    return run(op, 1, st);
+  }
   if (is_1x1_s1(s)) {
     Conv1x1DgradOp op{s.N * s.H * s.W, s.C, s.K, s.H * s.W, FastDiv(s.H * s.W), dy, w, dx, relu_mask,
                       accumulate ? kAccum : kStore};

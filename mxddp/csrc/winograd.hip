@@ -304,6 +304,190 @@ __global__ __launch_bounds__(256, kOcc) void wino_fwd_kernel(WinoArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Forward / data gradient, patch-staged (the default): block = 32 output channels x 64 output
+// tiles, 4 waves in 2 x 2, each 16 channels x 32 tiles (2 MFMA tiles) x 16 xi = 128 accumulator
+// registers, 2 blocks (8 waves) per CU.  Per chunk of 8 input channels the block's zero-padded
+// input patch (full rows: 8 x 10 x 34 for 32x32 images, the whole 18 x 18 image for 16x16, four
+// 10 x 10 images for 8x8) is staged in LDS from coalesced row loads whose offsets and border
+// masks are computed once per thread; each thread then reads its two 4x4 windows from the patch
+// with constant offsets, transforms them and writes V.  Compared with per-window global loads
+// this moves ~2.5x fewer bytes per MFMA through the load path and removes the per-element mask
+// arithmetic.  Pipeline per chunk (two barriers):
+//   A: U(ch) regs -> LDS, patch(ch) windows -> V in LDS
+//   B: patch(ch+1) regs -> LDS patch (its reads ended at B); issue U(ch+1), patch(ch+2) loads;
+//      64 MFMAs per wave on U(ch), V(ch)
+template <int W>
+struct PatchGeom {
+  static constexpr int TW = W / 2, TPI = TW * TW, HW = W * W;
+  static constexpr int IMGS = TPI >= 64 ? 1 : 64 / TPI;   // images per block
+  static constexpr int TR = (TPI >= 64 ? 64 : TPI) / TW;  // tile rows per image in the block
+  static constexpr int PRI = 2 * TR + 2, PW = W + 2;      // patch rows per image, patch row width
+  static constexpr int P1 = IMGS * PRI * PW;              // patch floats per channel
+  static constexpr int EP = (kCC * P1 + 255) / 256;       // patch floats per thread per chunk
+  static constexpr int kBP = 80;                          // V pitch (64 tiles + 16)
+  static constexpr int AS = 16 * kCC * kP, BS = 16 * kCC * kBP, PS = kCC * P1;
+};
+
+template <int W>
+__global__ __launch_bounds__(256, 2) void wino_fwd_patch_kernel(WinoArgs a) {
+  using G = PatchGeom<W>;
+  constexpr int TW = G::TW, TPI = G::TPI, HW = G::HW, PRI = G::PRI, PW = G::PW, P1 = G::P1, EP = G::EP;
+  constexpr int kBP = G::kBP;
+  __shared__ __attribute__((aligned(16))) float As[G::AS];  // U slice [16][8 ci][kP] (32 co)
+  __shared__ __attribute__((aligned(16))) float Bs[G::BS];  // V slice [16][8 ci][kBP] (64 tiles)
+  __shared__ __attribute__((aligned(16))) float Ps[G::PS];  // input patch [8 ci][IMGS][PRI][PW]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kt = bid % a.ktiles, r1 = bid / a.ktiles;
+  const int tb = r1 % a.tblocks, sp = r1 / a.tblocks;
+  const int co0 = kt * 32;
+  const int ntiles = a.N * TPI;
+  const int ch_beg = sp * a.chunks_per_split, ch_end = min(a.Cip / kCC, ch_beg + a.chunks_per_split);
+  // first tile of the block -> first image and first tile row
+  const int T0 = tb * 64, n0 = T0 / TPI, th0 = (T0 - n0 * TPI) / TW;
+
+  // ---- patch load role (loop-invariant offsets + spatial masks, computed once)
+  uint32_t poff[EP];
+  unsigned pvalid = 0;  // bit i: element i is inside the image (and the block's images)
+  int pci[EP];          // channel within the chunk of element i (>= kCC: no element)
+#pragma unroll
+  for (int i = 0; i < EP; ++i) {
+    const int e = tid + 256 * i;
+    const int ci = e / P1, rem = e - ci * P1;
+    const int il = rem / (PRI * PW), r2 = rem - il * (PRI * PW), pr = r2 / PW, pc = r2 - pr * PW;
+    const int n = n0 + il, h = 2 * th0 - 1 + pr, w = pc - 1;
+    const bool ok = e < kCC * P1 && n < a.N && (unsigned)h < (unsigned)W && (unsigned)w < (unsigned)W;
+    pci[i] = e < kCC * P1 ? ci : kCC;
+    poff[i] = ok ? (uint32_t)((n * a.Ci + ci) * HW + h * W + w) : 0u;
+    if (ok) pvalid |= 1u << i;
+  }
+  float rp[EP];
+  auto pload = [&](int ch) {  // patch of chunk ch -> registers (masked at store time)
+    const uint32_t cbase = (uint32_t)(ch * kCC) * HW;
+#pragma unroll
+    for (int i = 0; i < EP; ++i) rp[i] = a.x[((pvalid >> i) & 1u) ? poff[i] + cbase : 0u];
+  };
+  auto pstore = [&](int ch) {
+#pragma unroll
+    for (int i = 0; i < EP; ++i) {
+      const int e = tid + 256 * i;
+      const bool ok = ((pvalid >> i) & 1u) && ch * kCC + pci[i] < a.Ci;
+      if (e < kCC * P1) Ps[e] = ok ? rp[i] : 0.f;
+    }
+  };
+
+  // ---- U copy role: 16 xi x 8 ci rows of 32 floats = 1024 float4, 4 per thread
+  const uint32_t u_lane = 4u * (((uint32_t)(tid >> 6) * a.Cip + ((tid >> 3) & 7)) * a.Cop + co0 + 4 * (tid & 7));
+  const uint32_t u_q = 4u * 4u * a.Cip * a.Cop, u_ch = 4u * kCC * a.Cop;  // byte strides
+  float* as_st = As + (tid >> 3) * kP + 4 * (tid & 7);                       // + q * 32 rows
+  f32x4 ru[4];
+  auto uload = [&](int ch) {
+    const char* ub = reinterpret_cast<const char*>(a.U) + (size_t)ch * u_ch;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ru[q] = *reinterpret_cast<const f32x4*>(ub + u_lane + q * u_q);
+  };
+
+  // ---- transform role: tile tid & 63, channels (tid >> 6) and (tid >> 6) + 4 of the chunk
+  const int tt = tid & 63, csub = tid >> 6;
+  int wbase;
+  {
+    const int il = tt / (G::TR * TW), rem = tt - il * (G::TR * TW), trw = rem / TW, tcl = rem - trw * TW;
+    wbase = il * PRI * PW + 2 * trw * PW + 2 * tcl;
+  }
+
+  f32x4 acc[16][2];
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[xi][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const float* ap = As + g * kP + 16 * wm + l16;
+  const float* bp = Bs + g * kBP + 32 * wn + l16;
+  if (ch_beg < ch_end) {
+    pload(ch_beg);
+    uload(ch_beg);
+    pstore(ch_beg);  // waits for the first patch only
+    if (ch_beg + 1 < ch_end) pload(ch_beg + 1);
+  }
+  for (int ch = ch_beg; ch < ch_end; ++ch) {
+    __syncthreads();  // A: previous MFMAs done with As/Bs; patch(ch) visible
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4*>(as_st + q * 32 * kP) = ru[q];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int cl = csub + 4 * p;
+      const float* src = Ps + cl * P1 + wbase;
+      float d[16], v[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) d[e] = src[(e >> 2) * PW + (e & 3)];
+      in_transform(d, v);
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) Bs[(xi * kCC + cl) * kBP + tt] = v[xi];
+    }
+    __syncthreads();  // B: V(ch) complete; patch(ch) reads done
+    if (ch + 1 < ch_end) {
+      pstore(ch + 1);
+      uload(ch + 1);
+      if (ch + 2 < ch_end) pload(ch + 2);
+    }
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int ro = xi * kCC + 4 * s;
+        const float av = ap[ro * kP];
+        acc[xi][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bp[ro * kBP], acc[xi][0], 0, 0, 0);
+        acc[xi][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bp[ro * kBP + 16], acc[xi][1], 0, 0, 0);
+      }
+  }
+
+  // epilogue: row = output channel, column = output tile; Y = A^T M A, A^T = [[1,1,1,0],[0,1,-1,-1]]
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int T = tb * 64 + 32 * wn + 16 * j + l16;
+    if (T >= ntiles) continue;
+    const int n = T / TPI, rem = T - n * TPI, oh = 2 * (rem / TW), ow = 2 * (rem % TW);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + 16 * wm + 4 * g + r;
+      if (co >= a.Co) continue;
+      float t0[4], t1[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        t0[c] = acc[0 + c][j][r] + acc[4 + c][j][r] + acc[8 + c][j][r];
+        t1[c] = acc[4 + c][j][r] - acc[8 + c][j][r] - acc[12 + c][j][r];
+      }
+      const float y[2][2] = {{t0[0] + t0[1] + t0[2], t0[1] - t0[2] - t0[3]},
+                             {t1[0] + t1[1] + t1[2], t1[1] - t1[2] - t1[3]}};
+      const float bv = (a.bias && sp == 0) ? a.bias[co] : 0.f;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const size_t o = ((size_t)n * a.Co + co) * HW + (size_t)(oh + p) * W + ow;
+        float2 v = make_float2(y[p][0] + bv, y[p][1] + bv);
+        if (a.accumulate == 2) {
+          atomicAdd(a.y + o, v.x);
+          atomicAdd(a.y + o + 1, v.y);
+          continue;
+        }
+        if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); }
+        if (a.mask) {
+          const float2 mk = *reinterpret_cast<const float2*>(a.mask + o);
+          if (!(mk.x > 0.f)) v.x = 0.f;
+          if (!(mk.y > 0.f)) v.y = 0.f;
+        }
+        if (a.accumulate) {
+          const float2 old = *reinterpret_cast<const float2*>(a.y + o);
+          v.x += old.x;
+          v.y += old.y;
+        }
+        *reinterpret_cast<float2*>(a.y + o) = v;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 struct WinoWArgs {
   const float* dy;  // [N][K][W][W]
   const float* x;   // [N][C][W][W]
@@ -480,15 +664,25 @@ void launch_fwd(const float* x, const float* w, const float* bias, const float* 
   a.Co = Co;
   a.Cip = Cip;
   a.Cop = Cop;
+  // 3 = patch-staged 32 x 64 blocks (fastest on 32x32 images), 2 = per-window 32 x 32 blocks
+  // (fastest on 16x16 / 8x8, where the larger block leaves too few blocks to fill the chip);
+  // measured per shape by scripts/bench_conv.py.  MXDDP_WINO_FWD=2|3 forces one.
+  static const int forced = [] {
+    const char* e = std::getenv("MXDDP_WINO_FWD");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int variant = forced ? forced : (Wd == 32 ? 3 : 2);
   const int tpi = (Wd / 2) * (Wd / 2);
-  a.tblocks = cdiv(N * tpi, 32);
+  const int tile_blk = variant == 3 ? 64 : 32;
+  a.tblocks = cdiv(N * tpi, tile_blk);
   a.ktiles = Cop / 32;
   const int nch = Cip / kCC;
-  // split the input channels when the grid would not fill 256 CUs x 3 blocks (e.g. 8x8 images);
-  // only for plain outputs (no ReLU / mask), each split adds its partial result atomically
+  // split the input channels when the grid would not fill the CUs (e.g. 8x8 images); only for
+  // plain outputs (no ReLU / mask), each split adds its partial result atomically
+  const int slots = variant == 3 ? 512 : 768;
   int splits = 1;
   const int base = a.tblocks * a.ktiles;
-  if (!relu && !mask && base < 768) splits = std::max(1, std::min(cdiv(768, base), nch / 4));
+  if (!relu && !mask && base < slots) splits = std::max(1, std::min(cdiv(slots, base), nch / 4));
   a.chunks_per_split = cdiv(nch, splits);
   a.splits = cdiv(nch, a.chunks_per_split);
   a.relu = relu;
@@ -499,6 +693,15 @@ void launch_fwd(const float* x, const float* w, const float* bias, const float* 
     a.accumulate = accumulate ? 1 : 0;
   }
   const dim3 grid(a.tblocks * a.ktiles * a.splits);
+  if (variant == 3) {
+    switch (Wd) {
+      case 8: MX_LAUNCH(wino_fwd_patch_kernel<8>, grid, dim3(256), 0, st, a); break;
+      case 16: MX_LAUNCH(wino_fwd_patch_kernel<16>, grid, dim3(256), 0, st, a); break;
+      case 32: MX_LAUNCH(wino_fwd_patch_kernel<32>, grid, dim3(256), 0, st, a); break;
+      default: MX_CHECK(false, "winograd: unsupported width");
+    }
+    return;
+  }
   static const int occ = [] {
     const char* e = std::getenv("MXDDP_WINO_OCC");
     return e ? std::atoi(e) : 2;
