@@ -74,6 +74,61 @@ PYBIND11_MODULE(_C, m) {
     linear_wgrad(P<const float>(dy), P<const float>(x), P<float>(dw), M, N, K, acc, S(st));
   });
 
+  // ---------------------------------------------------------------- channels-last bf16 (nhwc_bf16.hip)
+  m.def("nhwc_from_nchw", [](uintptr_t x, uintptr_t y, int N, int C, int H, int W, int Cp, uintptr_t st) {
+    nhwc_from_nchw(P<const float>(x), P<uint16_t>(y), N, C, H, W, Cp, S(st));
+  });
+  m.def("nhwc_repack_weight", [](uintptr_t w, uintptr_t wt, int K, int C, int R, int S_, int Cp, bool dgrad,
+                                 uintptr_t st) {
+    nhwc_repack_weight(P<const float>(w), P<uint16_t>(wt), K, C, R, S_, Cp, dgrad, S(st));
+  });
+  m.def("nhwc_conv_fwd", [](uintptr_t x, uintptr_t wt, uintptr_t y, int N, int H, int W, int Cp, int K, int R, int S_,
+                            int sh, int sw, int ph, int pw, int P_, int Q, uintptr_t st) {
+    nhwc_conv_fwd(P<const uint16_t>(x), P<const uint16_t>(wt), P<uint16_t>(y), N, H, W, Cp, K, R, S_, sh, sw, ph, pw,
+                  P_, Q, S(st));
+  });
+  m.def("nhwc_conv_dgrad", [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int N, int H, int W, int C, int K, int R,
+                              int S_, int sh, int sw, int ph, int pw, int P_, int Q, uintptr_t st) {
+    nhwc_conv_dgrad(P<const uint16_t>(dy), P<const uint16_t>(wt), P<uint16_t>(dx), N, H, W, C, K, R, S_, sh, sw, ph,
+                    pw, P_, Q, S(st));
+  });
+  m.def("nhwc_conv_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, int N, int H, int W, int Cin, int Cp, int K,
+                              int R, int S_, int sh, int sw, int ph, int pw, int P_, int Q, bool acc, uintptr_t scratch,
+                              uintptr_t st) {
+    nhwc_conv_wgrad(P<const uint16_t>(dy), P<const uint16_t>(x), P<float>(dw), N, H, W, Cin, Cp, K, R, S_, sh, sw, ph,
+                    pw, P_, Q, acc, P<float>(scratch), S(st));
+  });
+  m.def("nhwc_wgrad_scratch_floats", &nhwc_wgrad_scratch_floats);
+  m.def("nhwc_bn_fwd", [](uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t g, uintptr_t b, uintptr_t mean,
+                          uintptr_t invstd, uintptr_t rm, uintptr_t rv, uintptr_t nbt, int Npix, int C, float mom,
+                          float eps, bool relu, uintptr_t scratch, uintptr_t st) {
+    nhwc_bn_fwd(P<const uint16_t>(x), P<const uint16_t>(res), P<uint16_t>(y), P<const float>(g), P<const float>(b),
+                P<float>(mean), P<float>(invstd), P<float>(rm), P<float>(rv), P<int64_t>(nbt), Npix, C, mom, eps, relu,
+                P<float>(scratch), S(st));
+  });
+  m.def("nhwc_bn_scratch_floats", &nhwc_bn_scratch_floats);
+  m.def("nhwc_bn_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t y, uintptr_t g, uintptr_t mean, uintptr_t invstd,
+                          uintptr_t dx, uintptr_t dres, uintptr_t dg, uintptr_t db, int Npix, int C, bool relu,
+                          bool accp, uintptr_t scratch, uintptr_t st) {
+    nhwc_bn_bwd(P<const uint16_t>(dy), P<const uint16_t>(x), P<const uint16_t>(y), P<const float>(g),
+                P<const float>(mean), P<const float>(invstd), P<uint16_t>(dx), P<uint16_t>(dres), P<float>(dg),
+                P<float>(db), Npix, C, relu, accp, P<float>(scratch), S(st));
+  });
+  m.def("nhwc_maxpool_fwd", [](uintptr_t x, uintptr_t y, uintptr_t arg, int N, int H, int W, int C, int P_, int Q,
+                               int k, int s, int p, uintptr_t st) {
+    nhwc_maxpool_fwd(P<const uint16_t>(x), P<uint16_t>(y), P<uint8_t>(arg), N, H, W, C, P_, Q, k, s, p, S(st));
+  });
+  m.def("nhwc_maxpool_bwd", [](uintptr_t dy, uintptr_t arg, uintptr_t dx, int N, int H, int W, int C, int P_, int Q,
+                               int k, int s, int p, uintptr_t st) {
+    nhwc_maxpool_bwd(P<const uint16_t>(dy), P<const uint8_t>(arg), P<uint16_t>(dx), N, H, W, C, P_, Q, k, s, p, S(st));
+  });
+  m.def("nhwc_gap_fwd", [](uintptr_t x, uintptr_t y, int N, int HW, int C, uintptr_t st) {
+    nhwc_gap_fwd(P<const uint16_t>(x), P<float>(y), N, HW, C, S(st));
+  });
+  m.def("nhwc_gap_bwd", [](uintptr_t dy, uintptr_t dx, int N, int HW, int C, uintptr_t st) {
+    nhwc_gap_bwd(P<const float>(dy), P<uint16_t>(dx), N, HW, C, S(st));
+  });
+
   m.def("set_gemm_precision", &set_gemm_precision);
   m.def("set_debug_sync", &set_debug_sync, "synchronise + check after every kernel launch (debugging)");
   m.def("debug_sync", &debug_sync);

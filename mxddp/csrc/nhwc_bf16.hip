@@ -1,0 +1,890 @@
+// Channels-last (NHWC) bf16 training kernels for gfx950: the ResNet-50 mixed-precision path
+// (BASELINE.json config 5).  Activations are bf16 [N][H][W][C] (C a multiple of 8), master
+// weights / gradients fp32 in torch layout [K][C][R][S], statistics and accumulation fp32.
+//
+// Why NHWC: every implicit-GEMM operand element is then a 16-byte vector of 8 consecutive
+// channels of one pixel, so the im2col gather is one 16-byte load per (pixel, r, s, 8 channels)
+// with a single bounds test, instead of a per-element index computation and 4-byte load as in
+// NCHW.  The reduction dimension of the forward / data-gradient GEMM is (r, s, c) with c
+// fastest, exactly the order of the MFMA operand fragments (8 consecutive k per lane).
+//
+// conv_nhwc_kernel   forward and data gradient.  GEMM rows = output channels (A = weights
+//                    [Ng][R*S*Ca] bf16, k-contiguous), columns = output pixels (B = the 16-byte
+//                    gather), v_mfma_f32_16x16x32_bf16, 128 x 128 (or 64 x 128) tiles, BK = 32,
+//                    register-staged double-buffered LDS.  The C/D layout puts 4 consecutive
+//                    output channels of one pixel in a lane: one 8-byte bf16 store each.
+//                    Data gradient: the same GEMM over dy with weights [Cin][R][S][Kout] and
+//                    the transposed-convolution gather (stride 1 or 2).
+// wgrad_nhwc_kernel  dW[k][(r,s,c)] = sum_pixels dy[pix][k] x[pix'][c]: the reduction runs over
+//                    pixels, which are the SLOW dimension of both NHWC operands, so the LDS
+//                    tiles are stored pixel-major as loaded and read with the gfx950 transpose
+//                    read ds_read_b64_tr_b16 (4 pixels x 16 channels per 16-lane group,
+//                    delivered channel-major); split over pixel ranges into fp32 partial
+//                    planes, summed in a fixed order and scattered to [K][C][R][S] by a second
+//                    kernel (deterministic; no same-address atomics).
+// BN / pooling       per-channel statistics with 8-channel vectors per thread; fused ReLU and
+//                    fused residual add + ReLU (Bottleneck tail) in the apply kernels.
+//
+// Replaces (reference): cuDNN conv / BN via torch.nn in a channels_last + autocast(bf16)
+// ResNet-50; BASELINE.json config 5 (not in the reference repository).
+#include "common.h"
+#include "igemm_bf16.h"
+#include "ops.h"
+
+#include <algorithm>
+
+namespace mx {
+
+namespace {
+
+using bf16 = unsigned short;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // register-promotable (HIP's uint4 arrays are not)
+
+__device__ __forceinline__ float bf2f(uint32_t v16) { return __uint_as_float(v16 << 16); }
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+// 8 bf16 (one uint4) <-> 8 floats
+__device__ __forceinline__ void unpack8(const uint4& u, float* f) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = bf2f(w[i] & 0xffffu);
+    f[2 * i + 1] = bf2f(w[i] >> 16);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+}
+
+// ------------------------------------------------------------------------------------------
+// forward / data-gradient implicit GEMM
+struct ConvNArgs {
+  const bf16* act;  // gathered tensor [N][IH][IW][Ca]
+  const bf16* wt;   // [Ng][Kg], Kg = R * S * Ca
+  bf16* out;        // [M][Ng]  (M = N * OH * OW output pixels)
+  int M, Ng, Kg, Ca;
+  int OH, OW, IH, IW;
+  int S, sh, sw, ph, pw;
+  int dgrad;        // 0: y = conv(x); 1: dx = conv_transpose(dy) (sh, sw in {1, 2})
+  FastDiv fOW, fOHW, fCa, fS;
+};
+
+template <int TM, int TN>
+__global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
+  // BK = 64 (two MFMA k-steps per stage) keeps each stage's MFMA phase long enough to cover the
+  // next stage's global loads; LDS rows of 72 bf16 = 144 B = 9 x 16 B (odd) -> the 16 rows read
+  // by a 16-lane group hit 16 distinct 16-byte slots.
+  constexpr int BK = 64, LD = BK + 8;
+  constexpr int EA = TM * 8 / 256, EB = TN * 8 / 256;  // 16-byte vectors per thread per stage
+  constexpr int WMT = TM / 32, WNT = TN / 32;           // 16x16 MFMA tiles per wave (wave tile = TM/2 x TN/2)
+  __shared__ __attribute__((aligned(16))) bf16 As[2][TM * LD];
+  __shared__ __attribute__((aligned(16))) bf16 Bs[2][TN * LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int tiles_m = (a.Ng + TM - 1) / TM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ch0 = (bid % tiles_m) * TM, px0 = (bid / tiles_m) * TN;
+  const int kv = tid & 7, row0 = tid >> 3;  // vector kv of rows row0 + 32 i
+
+  int pn[EB], poh[EB], pow_[EB];
+  bool pok[EB];
+#pragma unroll
+  for (int i = 0; i < EB; ++i) {
+    const int m = px0 + row0 + 32 * i;
+    pok[i] = m < a.M;
+    const int mm = pok[i] ? m : 0;
+    pn[i] = (int)a.fOHW.div((uint32_t)mm);
+    const int rem = mm - pn[i] * a.OH * a.OW;
+    poh[i] = (int)a.fOW.div((uint32_t)rem);
+    pow_[i] = rem - poh[i] * a.OW;
+  }
+  u32x4 ra[EA], rb[EB];
+  const u32x4 z4 = {0u, 0u, 0u, 0u};
+  auto gload = [&](int k0) {
+    const int k = k0 + 8 * kv;
+    const bool kok = k < a.Kg;
+    const int kk = kok ? k : 0;
+    const int rs = (int)a.fCa.div((uint32_t)kk), c = kk - rs * a.Ca;
+    const int r = (int)a.fS.div((uint32_t)rs), s = rs - r * a.S;
+#pragma unroll
+    for (int i = 0; i < EA; ++i) {
+      const int row = ch0 + row0 + 32 * i;
+      ra[i] = (kok && row < a.Ng) ? *reinterpret_cast<const u32x4*>(a.wt + (size_t)row * a.Kg + k) : z4;
+    }
+#pragma unroll
+    for (int i = 0; i < EB; ++i) {
+      int ih, iw;
+      bool ok = pok[i] && kok;
+      if (!a.dgrad) {
+        ih = poh[i] * a.sh - a.ph + r;
+        iw = pow_[i] * a.sw - a.pw + s;
+      } else {  // transposed conv: output pixel (h, w) gathers dy[(h + ph - r) / sh] when divisible
+        const int th = poh[i] + a.ph - r, tw = pow_[i] + a.pw - s;
+        ih = a.sh == 1 ? th : th >> 1;
+        iw = a.sw == 1 ? tw : tw >> 1;
+        ok = ok && th >= 0 && tw >= 0 && ih * a.sh == th && iw * a.sw == tw;
+      }
+      ok = ok && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
+      rb[i] = ok ? *reinterpret_cast<const u32x4*>(a.act + (((size_t)pn[i] * a.IH + ih) * a.IW + iw) * a.Ca + c)
+                 : z4;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < EA; ++i) *reinterpret_cast<u32x4*>(&As[buf][(row0 + 32 * i) * LD + 8 * kv]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < EB; ++i) *reinterpret_cast<u32x4*>(&Bs[buf][(row0 + 32 * i) * LD + 8 * kv]) = rb[i];
+  };
+
+  f32x4 acc[WMT][WNT];
+#pragma unroll
+  for (int i = 0; i < WMT; ++i)
+#pragma unroll
+    for (int j = 0; j < WNT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = (a.Kg + BK - 1) / BK;
+  const int a_row = wm * (TM / 2) + (lane & 15), b_row = wn * (TN / 2) + (lane & 15), koff = 8 * (lane >> 4);
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) gload((t + 1) * BK);
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 av[WMT], bv[WNT];
+#pragma unroll
+      for (int i = 0; i < WMT; ++i)
+        av[i] = *reinterpret_cast<const bf16x8*>(&As[cur][(a_row + 16 * i) * LD + 32 * ks + koff]);
+#pragma unroll
+      for (int j = 0; j < WNT; ++j)
+        bv[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][(b_row + 16 * j) * LD + 32 * ks + koff]);
+#pragma unroll
+      for (int i = 0; i < WMT; ++i)
+#pragma unroll
+        for (int j = 0; j < WNT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nt) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // C/D: row (output channel) = 4 * (lane >> 4) + r, column (pixel) = lane & 15
+#pragma unroll
+  for (int i = 0; i < WMT; ++i) {
+    const int ch = ch0 + wm * (TM / 2) + 16 * i + 4 * (lane >> 4);
+    if (ch >= a.Ng) continue;
+#pragma unroll
+    for (int j = 0; j < WNT; ++j) {
+      const int px = px0 + wn * (TN / 2) + 16 * j + (lane & 15);
+      if (px >= a.M) continue;
+      *reinterpret_cast<uint2*>(a.out + (size_t)px * a.Ng + ch) =
+          make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// weight gradient: rows = output channels k, columns = (r, s, c), reduction over pixels
+struct WgNArgs {
+  const bf16* dy;  // [Npix][Kout]
+  const bf16* x;   // [N][H][W][Ca]
+  float* part;     // fp32 partials [splits][Kout][Ng]
+  int Npix, Kout, Ca, Cin, H, W, P, Q, R, S, sh, sw, ph, pw, Ng;
+  int chunk;       // pixels per split (multiple of 32)
+  FastDiv fQ, fPQ, fCa, fS;
+};
+
+constexpr int kWP = 128 + 8;  // LDS pitch of a 128-channel pixel row (272 B; tr reads need 8-B alignment)
+
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* tile, int col0, int lane) {
+  // MFMA operand for "row" = channel col0 + (lane & 15), k = pixels 8 * (lane >> 4) .. + 7 from a
+  // pixel-major [32][kWP] tile: two transposed reads of 4 pixels x 16 channels each.
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const bf16* p0 = tile + (8 * g + q) * kWP + col0 + 4 * p;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * kWP));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+__global__ __launch_bounds__(256) void wgrad_nhwc_kernel(WgNArgs a) {
+  constexpr int BK = 64;  // pixels per stage (two MFMA k-steps)
+  __shared__ __attribute__((aligned(16))) bf16 As[2][BK * kWP];  // dy tile  [pixel][k]
+  __shared__ __attribute__((aligned(16))) bf16 Bs[2][BK * kWP];  // x gather [pixel][(r,s,c)]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int tiles_m = (a.Kout + 127) / 128, tiles_n = (a.Ng + 127) / 128;
+  const int bid = blockIdx.x;
+  const int tm = bid % tiles_m, r1 = bid / tiles_m, tn = r1 % tiles_n, sp = r1 / tiles_n;
+  const int m0 = tm * 128, n0 = tn * 128;
+  const int pbeg = sp * a.chunk, pend = min(a.Npix, pbeg + a.chunk);
+  if (pbeg >= pend) return;
+  // load roles: vector v = tid + 256 i -> pixel row v >> 4 (0..63), 8-channel vector v & 15
+  const int cv = tid & 15, prow0 = tid >> 4;
+  // B column decomposition (fixed per thread): column n0 + 8 cv -> (r, s, c)
+  const int col = n0 + 8 * cv;
+  const bool col_ok = col < a.Ng;
+  const int colc = col_ok ? col : 0;
+  const int rs = (int)a.fCa.div((uint32_t)colc), bc = colc - rs * a.Ca;
+  const int br = (int)a.fS.div((uint32_t)rs), bs = rs - br * a.S;
+  const bool k_ok = m0 + 8 * cv < a.Kout;
+  u32x4 ra[4], rb[4];
+  const u32x4 z4 = {0u, 0u, 0u, 0u};
+  auto gload = [&](int p0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pix = p0 + prow0 + 16 * i;
+      const bool ok = pix < pend;
+      ra[i] = (ok && k_ok) ? *reinterpret_cast<const u32x4*>(a.dy + (size_t)pix * a.Kout + m0 + 8 * cv) : z4;
+      const int pp = ok ? pix : 0;
+      const int n = (int)a.fPQ.div((uint32_t)pp), rem = pp - n * a.P * a.Q;
+      const int p = (int)a.fQ.div((uint32_t)rem), q = rem - p * a.Q;
+      const int h = p * a.sh - a.ph + br, w = q * a.sw - a.pw + bs;
+      const bool xok = ok && col_ok && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      rb[i] = xok ? *reinterpret_cast<const u32x4*>(a.x + (((size_t)n * a.H + h) * a.W + w) * a.Ca + bc) : z4;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<u32x4*>(&As[buf][(prow0 + 16 * i) * kWP + 8 * cv]) = ra[i];
+      *reinterpret_cast<u32x4*>(&Bs[buf][(prow0 + 16 * i) * kWP + 8 * cv]) = rb[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = (pend - pbeg + BK - 1) / BK;
+  gload(pbeg);
+  sstore(0);
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) gload(pbeg + (t + 1) * BK);
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 av[4], bv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) av[i] = tr_frag(As[cur] + 32 * ks * kWP, wm * 64 + 16 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bv[j] = tr_frag(Bs[cur] + 32 * ks * kWP, wn * 64 + 16 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nt) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  float* pl = a.part + (size_t)sp * a.Kout * a.Ng;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int cn = n0 + wn * 64 + 16 * j + (lane & 15);
+    if (cn >= a.Ng) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = m0 + wm * 64 + 16 * i + 4 * (lane >> 4) + r;
+        if (k < a.Kout) pl[(size_t)k * a.Ng + cn] = acc[i][j][r];
+      }
+    }
+  }
+}
+
+// dw[k][c][r][s] (+)= sum over splits of part[sp][k][(r, s, c)] (c < Cin; padded channels dropped)
+__global__ void wgrad_nhwc_reduce_k(const float* __restrict__ part, float* __restrict__ dw, int splits, int Kout,
+                                    int Ng, int Ca, int Cin, int RS, int accumulate) {
+  const int64_t plane = (int64_t)Kout * Ng;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < plane; i += (int64_t)gridDim.x * 256) {
+    const int n = (int)(i % Ng), k = (int)(i / Ng);
+    const int rs = n / Ca, c = n - rs * Ca;
+    if (c >= Cin) continue;
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    int sp = 0;
+    for (; sp + 4 <= splits; sp += 4)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t[u] += part[(sp + u) * plane + i];
+    for (; sp < splits; ++sp) t[0] += part[sp * plane + i];
+    const float v = (t[0] + t[1]) + (t[2] + t[3]);
+    float* d = dw + ((int64_t)k * Cin + c) * RS + rs;
+    *d = accumulate ? *d + v : v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// layout / weight conversion
+// x fp32 [N][C][H][W] -> bf16 [N][H][W][Cp] (zeros for c >= C)
+__global__ void nchw_to_nhwc_k(const float* __restrict__ x, bf16* __restrict__ y, int N, int C, int HW, int Cp) {
+  const int64_t total = (int64_t)N * HW * Cp;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % Cp);
+    const int64_t nhw = i / Cp;
+    const int n = (int)(nhw / HW), hw = (int)(nhw - (int64_t)n * HW);
+    y[i] = c < C ? f2bf(x[((int64_t)n * C + c) * HW + hw]) : (bf16)0;
+  }
+}
+
+// w fp32 [K][C][R][S] -> fwd: bf16 [K][R][S][Cp] (zero-padded channels); dgrad: bf16 [C][R][S][K]
+__global__ void wrepack_k(const float* __restrict__ w, bf16* __restrict__ wt, int K, int C, int R, int S, int Cp,
+                          int dgrad) {
+  const int RS = R * S;
+  const int64_t total = dgrad ? (int64_t)C * RS * K : (int64_t)K * RS * Cp;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    if (!dgrad) {
+      const int c = (int)(i % Cp);
+      const int64_t krs = i / Cp;
+      const int rs = (int)(krs % RS), k = (int)(krs / RS);
+      wt[i] = c < C ? f2bf(w[((int64_t)k * C + c) * RS + rs]) : (bf16)0;
+    } else {
+      const int k = (int)(i % K);
+      const int64_t crs = i / K;
+      const int rs = (int)(crs % RS), c = (int)(crs / RS);
+      wt[i] = f2bf(w[((int64_t)k * C + c) * RS + rs]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// BatchNorm over [Npix][C] (C % 8 == 0, 256 % (C / 8) == 0 or C / 8 a multiple of 256), three
+// launches per direction:
+//   partial  grid (gx, gy): each block reduces its pixel slice to per-channel partial sums and
+//            WRITES them to part[blockIdx.x][2C] (no atomics: gx ~ 256 blocks keep HBM busy, and
+//            same-address atomics from that many blocks serialise);
+//   finalize one thread per channel sums the gx partials in a fixed order (deterministic) and
+//            produces the per-channel affine coefficients (+ saved mean / invstd, running stats,
+//            num_batches_tracked; backward: dgamma / dbeta);
+//   apply    each block stages the coefficients of all C channels in LDS, then streams 8-channel
+//            vectors: one FMA per element (+ residual, ReLU).
+// Forward partials are sums of (x - K) and (x - K)^2 with K = x[pixel 0][c] (well conditioned
+// when |mean| >> std); backward partials are sum(g) and sum(g (x - mean)), g = dy masked by the
+// fused ReLU.  Thread (in a 256-thread block) owns vector v = tid % V of pixels tid / V + k * PPI.
+constexpr int kBnT = 256;
+
+struct BnNArgs {
+  const bf16* x;      // BN input
+  const bf16* res;    // residual added after the affine map (or null)
+  bf16* y;            // output
+  const bf16* dy;     // bwd: gradient wrt y
+  bf16* dx;           // bwd: gradient wrt x
+  bf16* dres;         // bwd: gradient wrt res (= relu-masked dy), or null
+  const float* gamma;
+  const float* beta;
+  float* mean;        // [C] out (fwd) / in (bwd)
+  float* invstd;      // [C]
+  float* run_mean;
+  float* run_var;
+  float* part;        // [gx][2C] partial sums
+  float* coef;        // fwd [C][2] (scale, shift); bwd [C][3] (A, D, B): dx = A g + D x + B
+  float* dgamma;
+  float* dbeta;
+  int64_t* num_batches;
+  int Npix, C, relu, gx, acc_params;
+  float momentum, eps;
+};
+
+template <bool BWD>
+__global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
+  const int V = a.C >> 3;
+  const int vv = V >= kBnT ? kBnT : V;
+  const int ppi = kBnT / vv;
+  const int vbase = (V >= kBnT) ? blockIdx.y * kBnT : 0;
+  const int v = vbase + threadIdx.x % vv, pr = threadIdx.x / vv;
+  float s1[8], s2[8], K[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+  if (!BWD) {
+    unpack8(*reinterpret_cast<const uint4*>(a.x + 8 * v), K);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) K[e] = a.mean[8 * v + e];
+  }
+  for (int p = blockIdx.x * ppi + pr; p < a.Npix; p += gridDim.x * ppi) {
+    float xv[8];
+    unpack8(*reinterpret_cast<const uint4*>(a.x + (size_t)p * a.C + 8 * v), xv);
+    if (!BWD) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = xv[e] - K[e];
+        s1[e] += d;
+        s2[e] = fmaf(d, d, s2[e]);
+      }
+    } else {
+      float g[8];
+      unpack8(*reinterpret_cast<const uint4*>(a.dy + (size_t)p * a.C + 8 * v), g);
+      if (a.relu) {
+        float yv[8];
+        unpack8(*reinterpret_cast<const uint4*>(a.y + (size_t)p * a.C + 8 * v), yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = yv[e] > 0.f ? g[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += g[e];
+        s2[e] = fmaf(g[e], xv[e] - K[e], s2[e]);
+      }
+    }
+  }
+  __shared__ float red[kBnT * 16];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[threadIdx.x * 16 + e] = s1[e];
+    red[threadIdx.x * 16 + 8 + e] = s2[e];
+  }
+  __syncthreads();
+  if (pr == 0) {
+    for (int k = 1; k < ppi; ++k) {
+      const float* o = red + (threadIdx.x + k * vv) * 16;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += o[e];
+        s2[e] += o[8 + e];
+      }
+    }
+    float* dst = a.part + (size_t)blockIdx.x * 2 * a.C + 16 * v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      dst[2 * e] = s1[e];
+      dst[2 * e + 1] = s2[e];
+    }
+  }
+}
+
+template <bool BWD>
+__global__ __launch_bounds__(256) void bn_nhwc_finalize_k(BnNArgs a) {
+  // block = 32 channels x 8 row groups; each thread sums every 8th partial row (4 independent
+  // loads in flight), the 8 row-group sums are combined in a fixed order (deterministic)
+  __shared__ float red[2][8][32];
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5, c = blockIdx.x * 32 + cl;
+  const size_t pitch = 2 * (size_t)a.C;
+  float s1 = 0.f, s2 = 0.f;
+  if (c < a.C) {
+    float t1[4] = {0.f, 0.f, 0.f, 0.f}, t2[4] = {0.f, 0.f, 0.f, 0.f};
+    int b = rg;
+    for (; b + 24 < a.gx; b += 32) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* p = a.part + (size_t)(b + 8 * u) * pitch + 2 * c;
+        t1[u] += p[0];
+        t2[u] += p[1];
+      }
+    }
+    for (; b < a.gx; b += 8) {
+      const float* p = a.part + (size_t)b * pitch + 2 * c;
+      t1[0] += p[0];
+      t2[0] += p[1];
+    }
+    s1 = (t1[0] + t1[1]) + (t1[2] + t1[3]);
+    s2 = (t2[0] + t2[1]) + (t2[2] + t2[3]);
+  }
+  red[0][rg][cl] = s1;
+  red[1][rg][cl] = s2;
+  __syncthreads();
+  if (rg != 0 || c >= a.C) return;
+  s1 = 0.f;
+  s2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    s1 += red[0][k][cl];
+    s2 += red[1][k][cl];
+  }
+  const float cnt = (float)a.Npix;
+  if (!BWD && a.num_batches && c == 0) *a.num_batches += 1;
+  const float gm = a.gamma ? a.gamma[c] : 1.f;
+  if (!BWD) {
+    const float K = bf2f(a.x[c]);
+    const float m1 = s1 / cnt;
+    const float var = fmaxf(s2 / cnt - m1 * m1, 0.f);
+    const float mean = K + m1, inv = rsqrtf(var + a.eps);
+    a.mean[c] = mean;
+    a.invstd[c] = inv;
+    if (a.run_mean) a.run_mean[c] = (1.f - a.momentum) * a.run_mean[c] + a.momentum * mean;
+    if (a.run_var) a.run_var[c] = (1.f - a.momentum) * a.run_var[c] + a.momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
+    const float sc = inv * gm;
+    a.coef[2 * c] = sc;
+    a.coef[2 * c + 1] = (a.beta ? a.beta[c] : 0.f) - mean * sc;
+  } else {
+    const float inv = a.invstd[c], mu = a.mean[c];
+    const float db = s1, dg = s2 * inv;
+    if (a.dgamma) a.dgamma[c] = a.acc_params ? a.dgamma[c] + dg : dg;
+    if (a.dbeta) a.dbeta[c] = a.acc_params ? a.dbeta[c] + db : db;
+    // dx = k (cnt g - db - (x - mu) inv dg), k = gamma inv / cnt
+    const float k = gm * inv / cnt;
+    a.coef[3 * c] = k * cnt;
+    a.coef[3 * c + 1] = -k * inv * dg;
+    a.coef[3 * c + 2] = -k * db + k * inv * dg * mu;
+  }
+}
+
+// forward apply: y = relu?(x * scale + shift (+ res))
+__global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a) {
+  __shared__ float cs[2 * 2048];
+  for (int i = threadIdx.x; i < 2 * a.C; i += kBnT) cs[i] = a.coef[i];
+  __syncthreads();
+  const int V = a.C >> 3;
+  const int64_t total = (int64_t)a.Npix * V;
+  for (int64_t i = blockIdx.x * (int64_t)kBnT + threadIdx.x; i < total; i += (int64_t)gridDim.x * kBnT) {
+    const int v = (int)(i % V);
+    float xv[8];
+    unpack8(reinterpret_cast<const uint4*>(a.x)[i], xv);
+    float rv[8];
+    if (a.res) unpack8(reinterpret_cast<const uint4*>(a.res)[i], rv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float o = fmaf(xv[e], cs[16 * v + 2 * e], cs[16 * v + 2 * e + 1]);
+      if (a.res) o += rv[e];
+      xv[e] = a.relu ? fmaxf(o, 0.f) : o;
+    }
+    reinterpret_cast<uint4*>(a.y)[i] = pack8(xv);
+  }
+}
+
+// backward apply: dx = A g + D x + B; dres = g (the residual branch gradient)
+__global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a) {
+  __shared__ float cs[3 * 2048];
+  for (int i = threadIdx.x; i < 3 * a.C; i += kBnT) cs[i] = a.coef[i];
+  __syncthreads();
+  const int V = a.C >> 3;
+  const int64_t total = (int64_t)a.Npix * V;
+  for (int64_t i = blockIdx.x * (int64_t)kBnT + threadIdx.x; i < total; i += (int64_t)gridDim.x * kBnT) {
+    const int v = (int)(i % V);
+    float g[8], xv[8];
+    unpack8(reinterpret_cast<const uint4*>(a.dy)[i], g);
+    unpack8(reinterpret_cast<const uint4*>(a.x)[i], xv);
+    if (a.relu) {
+      float yv[8];
+      unpack8(reinterpret_cast<const uint4*>(a.y)[i], yv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = yv[e] > 0.f ? g[e] : 0.f;
+    }
+    if (a.dres) reinterpret_cast<uint4*>(a.dres)[i] = pack8(g);
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float* k = cs + 3 * (8 * v + e);
+      o[e] = fmaf(k[0], g[e], fmaf(k[1], xv[e], k[2]));
+    }
+    reinterpret_cast<uint4*>(a.dx)[i] = pack8(o);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// max pool (k x k, stride, pad) with uint8 argmax tap; backward gathers over covering windows
+__global__ void maxpool_nhwc_k(const bf16* __restrict__ x, bf16* __restrict__ y, uint8_t* __restrict__ arg, int N,
+                               int H, int W, int C, int P, int Q, int k, int st, int pd) {
+  const int V = C >> 3;
+  const int64_t total = (int64_t)N * P * Q * V;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int v = (int)(i % V);
+    const int64_t pix = i / V;
+    const int q = (int)(pix % Q), p = (int)((pix / Q) % P), n = (int)(pix / ((int64_t)P * Q));
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int r = 0; r < k; ++r)
+      for (int s = 0; s < k; ++s) {
+        const int h = p * st - pd + r, w = q * st - pd + s;
+        if ((unsigned)h >= (unsigned)H || (unsigned)w >= (unsigned)W) continue;
+        float xv[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + (((size_t)n * H + h) * W + w) * C + 8 * v), xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (xv[e] > best[e]) { best[e] = xv[e]; bi[e] = (uint8_t)(r * k + s); }
+      }
+    reinterpret_cast<uint4*>(y)[i] = pack8(best);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) arg[i * 8 + e] = bi[e];
+  }
+}
+
+__global__ void maxpool_nhwc_bwd_k(const bf16* __restrict__ dy, const uint8_t* __restrict__ arg, bf16* __restrict__ dx,
+                                   int N, int H, int W, int C, int P, int Q, int k, int st, int pd) {
+  const int V = C >> 3;
+  const int64_t total = (int64_t)N * H * W * V;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int v = (int)(i % V);
+    const int64_t pix = i / V;
+    const int w = (int)(pix % W), h = (int)((pix / W) % H), n = (int)(pix / ((int64_t)H * W));
+    float g[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = 0.f;
+    for (int r = 0; r < k; ++r) {
+      const int tp = h + pd - r;
+      if (tp < 0 || tp % st) continue;
+      const int p = tp / st;
+      if (p >= P) continue;
+      for (int s = 0; s < k; ++s) {
+        const int tq = w + pd - s;
+        if (tq < 0 || tq % st) continue;
+        const int q = tq / st;
+        if (q >= Q) continue;
+        const int64_t o = (((int64_t)n * P + p) * Q + q) * V + v;
+        float dv[8];
+        unpack8(reinterpret_cast<const uint4*>(dy)[o], dv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (arg[o * 8 + e] == (uint8_t)(r * k + s)) g[e] += dv[e];
+      }
+    }
+    reinterpret_cast<uint4*>(dx)[i] = pack8(g);
+  }
+}
+
+// global average pool: bf16 [N][HW][C] -> fp32 [N][C]; backward broadcasts dy / HW
+__global__ void gap_nhwc_k(const bf16* __restrict__ x, float* __restrict__ y, int N, int HW, int C) {
+  const int n = blockIdx.y;
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < C; c += gridDim.x * 256) {
+    float s = 0.f;
+    for (int p = 0; p < HW; ++p) s += bf2f(x[((size_t)n * HW + p) * C + c]);
+    y[(size_t)n * C + c] = s / (float)HW;
+  }
+}
+
+__global__ void gap_nhwc_bwd_k(const float* __restrict__ dy, bf16* __restrict__ dx, int N, int HW, int C) {
+  const int64_t total = (int64_t)N * HW * C;
+  const float inv = 1.f / (float)HW;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const int n = (int)(i / ((int64_t)HW * C));
+    dx[i] = f2bf(dy[(size_t)n * C + c] * inv);
+  }
+}
+
+int grid_for(int64_t n, int cap = 4096) {
+  const int64_t g = (n + 255) / 256;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+void nhwc_from_nchw(const float* x, uint16_t* y, int N, int C, int H, int W, int Cp, hipStream_t st) {
+  MX_LAUNCH(nchw_to_nhwc_k, dim3(grid_for((int64_t)N * H * W * Cp)), dim3(256), 0, st, x, y, N, C, H * W, Cp);
+}
+
+void nhwc_repack_weight(const float* w, uint16_t* wt, int K, int C, int R, int S, int Cp, bool dgrad, hipStream_t st) {
+  MX_LAUNCH(wrepack_k, dim3(grid_for((int64_t)K * (dgrad ? C : Cp) * R * S)), dim3(256), 0, st, w, wt, K, C, R, S,
+            Cp, dgrad ? 1 : 0);
+}
+
+static void launch_conv(ConvNArgs& a, hipStream_t st) {
+  MX_CHECK(a.Kg % 8 == 0 && a.Ca % 8 == 0 && a.Ng % 4 == 0, "nhwc conv: channels must be multiples of 8");
+  a.fOW = FastDiv(a.OW);
+  a.fOHW = FastDiv(a.OH * a.OW);
+  a.fCa = FastDiv(a.Ca);
+  a.fS = FastDiv(a.S);
+  // largest tile whose grid still gives every CU two blocks (layer3/4 of ResNet-50 have only
+  // 1.5k-6k output pixels at batch 32): 128 x 128, then 64 x 128, then 64 x 64
+  const int b128 = cdiv(a.Ng, 128) * cdiv(a.M, 128), b64 = cdiv(a.Ng, 64) * cdiv(a.M, 128);
+  if (a.Ng > 64 && b128 >= 512) {
+    MX_LAUNCH((conv_nhwc_kernel<128, 128>), dim3(b128), dim3(256), 0, st, a);
+  } else if (b64 >= 512 || a.Ng <= 64 && a.M >= 128 * 256) {
+    MX_LAUNCH((conv_nhwc_kernel<64, 128>), dim3(b64), dim3(256), 0, st, a);
+  } else {
+    MX_LAUNCH((conv_nhwc_kernel<64, 64>), dim3(cdiv(a.Ng, 64) * cdiv(a.M, 64)), dim3(256), 0, st, a);
+  }
+}
+
+void nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int H, int W, int Cp, int K, int R,
+                   int S, int sh, int sw, int ph, int pw, int P, int Q, hipStream_t st) {
+  ConvNArgs a{};
+  a.act = x;
+  a.wt = wt;
+  a.out = y;
+  a.M = N * P * Q;
+  a.Ng = K;
+  a.Kg = R * S * Cp;
+  a.Ca = Cp;
+  a.OH = P;
+  a.OW = Q;
+  a.IH = H;
+  a.IW = W;
+  a.S = S;
+  a.sh = sh;
+  a.sw = sw;
+  a.ph = ph;
+  a.pw = pw;
+  a.dgrad = 0;
+  launch_conv(a, st);
+}
+
+void nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
+                     int S, int sh, int sw, int ph, int pw, int P, int Q, hipStream_t st) {
+  MX_CHECK((sh == 1 || sh == 2) && (sw == 1 || sw == 2), "nhwc dgrad: stride 1 or 2");
+  ConvNArgs a{};
+  a.act = dy;
+  a.wt = wt_d;
+  a.out = dx;
+  a.M = N * H * W;
+  a.Ng = C;
+  a.Kg = R * S * K;
+  a.Ca = K;
+  a.OH = H;
+  a.OW = W;
+  a.IH = P;
+  a.IW = Q;
+  a.S = S;
+  a.sh = sh;
+  a.sw = sw;
+  a.ph = ph;
+  a.pw = pw;
+  a.dgrad = 1;
+  launch_conv(a, st);
+}
+
+static int wgrad_splits(int Npix, int K, int Ng) {
+  const int tiles = cdiv(K, 128) * cdiv(Ng, 128);
+  // ~2 blocks per CU, >= 512 pixels (8 stages) per block, partial planes <= 32M floats
+  int splits = std::max(1, cdiv(512, tiles));
+  splits = std::min(splits, std::max(1, Npix / 512));
+  splits = std::min(splits, std::max(1, (int)((32ll << 20) / ((int64_t)K * Ng))));
+  const int chunk = cdiv(cdiv(Npix, splits), 64) * 64;
+  return cdiv(Npix, chunk);
+}
+
+size_t nhwc_wgrad_scratch_floats(int N, int Cp, int K, int R, int S, int P, int Q) {
+  const int Ng = R * S * Cp;
+  return (size_t)wgrad_splits(N * P * Q, K, Ng) * K * Ng;
+}
+
+void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, int H, int W, int Cin, int Cp, int K,
+                     int R, int S, int sh, int sw, int ph, int pw, int P, int Q, bool accumulate, float* scratch,
+                     hipStream_t st) {
+  MX_CHECK(Cp % 8 == 0 && K % 8 == 0, "nhwc wgrad: channels must be multiples of 8");
+  WgNArgs a{};
+  a.dy = dy;
+  a.x = x;
+  a.part = scratch;
+  a.Npix = N * P * Q;
+  a.Kout = K;
+  a.Ca = Cp;
+  a.Cin = Cin;
+  a.H = H;
+  a.W = W;
+  a.P = P;
+  a.Q = Q;
+  a.R = R;
+  a.S = S;
+  a.sh = sh;
+  a.sw = sw;
+  a.ph = ph;
+  a.pw = pw;
+  a.Ng = R * S * Cp;
+  a.fQ = FastDiv(Q);
+  a.fPQ = FastDiv(P * Q);
+  a.fCa = FastDiv(Cp);
+  a.fS = FastDiv(S);
+  const int tiles = cdiv(K, 128) * cdiv(a.Ng, 128);
+  const int splits = wgrad_splits(a.Npix, K, a.Ng);
+  a.chunk = cdiv(cdiv(a.Npix, splits), 64) * 64;
+  MX_LAUNCH(wgrad_nhwc_kernel, dim3(tiles * splits), dim3(256), 0, st, a);
+  MX_LAUNCH(wgrad_nhwc_reduce_k, dim3(grid_for((int64_t)K * a.Ng, 2048)), dim3(256), 0, st, scratch, dw, splits, K,
+            a.Ng, Cp, Cin, R * S, accumulate ? 1 : 0);
+}
+
+static dim3 bn_grid(int Npix, int C) {
+  const int V = C / 8, vv = V >= kBnT ? kBnT : V, ppi = kBnT / vv;
+  const int gy = V >= kBnT ? V / kBnT : 1;
+  // ~256 blocks in total, at least 8 pixel rows per thread
+  const int gx = std::max(1, std::min(cdiv(Npix, ppi * 8), std::max(1, 256 / gy)));
+  return dim3(gx, gy);
+}
+
+size_t nhwc_bn_scratch_floats(int Npix, int C) {
+  const dim3 g = bn_grid(Npix, C);
+  return (size_t)g.x * 2 * C + 3 * (size_t)C;  // partials + coefficients
+}
+
+void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* gamma, const float* beta,
+                 float* mean, float* invstd, float* run_mean, float* run_var, int64_t* num_batches, int Npix, int C,
+                 float momentum, float eps, bool relu, float* scratch, hipStream_t st) {
+  const int V = C / 8;
+  MX_CHECK(C % 8 == 0 && C <= 2048 && (V >= kBnT ? V % kBnT == 0 : kBnT % V == 0),
+           "nhwc bn: unsupported channel count");
+  const dim3 g = bn_grid(Npix, C);
+  BnNArgs a{};
+  a.Npix = Npix;
+  a.C = C;
+  a.x = x;
+  a.res = res;
+  a.y = y;
+  a.gamma = gamma;
+  a.beta = beta;
+  a.mean = mean;
+  a.invstd = invstd;
+  a.run_mean = run_mean;
+  a.run_var = run_var;
+  a.part = scratch;
+  a.coef = scratch + (size_t)g.x * 2 * C;
+  a.gx = g.x;
+  a.num_batches = num_batches;
+  a.relu = relu;
+  a.momentum = momentum;
+  a.eps = eps;
+  MX_LAUNCH(bn_nhwc_partial_k<false>, g, dim3(kBnT), 0, st, a);
+  MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 32)), dim3(256), 0, st, a);
+  MX_LAUNCH(bn_nhwc_apply_k, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a);
+}
+
+void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma, const float* mean,
+                 const float* invstd, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, int Npix, int C,
+                 bool relu, bool accumulate_params, float* scratch, hipStream_t st) {
+  const int V = C / 8;
+  MX_CHECK(C % 8 == 0 && C <= 2048 && (V >= kBnT ? V % kBnT == 0 : kBnT % V == 0),
+           "nhwc bn: unsupported channel count");
+  const dim3 g = bn_grid(Npix, C);
+  BnNArgs a{};
+  a.Npix = Npix;
+  a.C = C;
+  a.dy = dy;
+  a.x = x;
+  a.y = const_cast<uint16_t*>(y);
+  a.gamma = gamma;
+  a.mean = const_cast<float*>(mean);
+  a.invstd = const_cast<float*>(invstd);
+  a.dx = dx;
+  a.dres = dres;
+  a.dgamma = dgamma;
+  a.dbeta = dbeta;
+  a.part = scratch;
+  a.coef = scratch + (size_t)g.x * 2 * C;
+  a.gx = g.x;
+  a.relu = relu;
+  a.acc_params = accumulate_params;
+  MX_LAUNCH(bn_nhwc_partial_k<true>, g, dim3(kBnT), 0, st, a);
+  MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 32)), dim3(256), 0, st, a);
+  MX_LAUNCH(bn_nhwc_bwd_apply_k, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a);
+}
+
+void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, int k,
+                      int s, int p, hipStream_t st) {
+  MX_LAUNCH(maxpool_nhwc_k, dim3(grid_for((int64_t)N * P * Q * (C / 8))), dim3(256), 0, st, x, y, arg, N, H, W, C, P,
+            Q, k, s, p);
+}
+
+void nhwc_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int P, int Q,
+                      int k, int s, int p, hipStream_t st) {
+  MX_LAUNCH(maxpool_nhwc_bwd_k, dim3(grid_for((int64_t)N * H * W * (C / 8))), dim3(256), 0, st, dy, arg, dx, N, H, W,
+            C, P, Q, k, s, p);
+}
+
+void nhwc_gap_fwd(const uint16_t* x, float* y, int N, int HW, int C, hipStream_t st) {
+  MX_LAUNCH(gap_nhwc_k, dim3(cdiv(C, 256), N), dim3(256), 0, st, x, y, N, HW, C);
+}
+
+void nhwc_gap_bwd(const float* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st) {
+  MX_LAUNCH(gap_nhwc_bwd_k, dim3(grid_for((int64_t)N * HW * C)), dim3(256), 0, st, dy, dx, N, HW, C);
+}
+
+}  // namespace mx

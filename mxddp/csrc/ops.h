@@ -124,6 +124,36 @@ void shortcut_pad_add(const float* x, float* y, int N, int Cin, int H, int W, in
 void shortcut_pad_add_bwd(const float* dy, float* dx, int N, int Cin, int H, int W, int Cout, int P,
                           int Q, int stride, bool accumulate, hipStream_t st);
 
+// ---- channels-last bf16 path (nhwc_bf16.hip): activations bf16 [N][H][W][C], C % 8 == 0 ----
+void nhwc_from_nchw(const float* x, uint16_t* y, int N, int C, int H, int W, int Cp, hipStream_t st);
+// fwd: bf16 [K][R][S][Cp] (channel-padded); dgrad: bf16 [C][R][S][K]
+void nhwc_repack_weight(const float* w, uint16_t* wt, int K, int C, int R, int S, int Cp, bool dgrad, hipStream_t st);
+void nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int H, int W, int Cp, int K, int R,
+                   int S, int sh, int sw, int ph, int pw, int P, int Q, hipStream_t st);
+void nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
+                     int S, int sh, int sw, int ph, int pw, int P, int Q, hipStream_t st);
+// dw fp32 [K][Cin][R][S] (+)= ...; x has Cp >= Cin channels (padding ignored);
+// scratch: nhwc_wgrad_scratch_floats(...) floats of per-split partial sums
+size_t nhwc_wgrad_scratch_floats(int N, int Cp, int K, int R, int S, int P, int Q);
+void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, int H, int W, int Cin, int Cp, int K,
+                     int R, int S, int sh, int sw, int ph, int pw, int P, int Q, bool accumulate, float* scratch,
+                     hipStream_t st);
+// y = relu?(bn(x) + res); scratch: nhwc_bn_scratch_floats(Npix, C) floats (partial sums +
+// per-channel coefficients, fully rewritten by every call)
+size_t nhwc_bn_scratch_floats(int Npix, int C);
+void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* gamma, const float* beta,
+                 float* mean, float* invstd, float* run_mean, float* run_var, int64_t* num_batches, int Npix, int C,
+                 float momentum, float eps, bool relu, float* scratch, hipStream_t st);
+void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma, const float* mean,
+                 const float* invstd, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, int Npix, int C,
+                 bool relu, bool accumulate_params, float* scratch, hipStream_t st);
+void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, int k,
+                      int s, int p, hipStream_t st);
+void nhwc_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int P, int Q,
+                      int k, int s, int p, hipStream_t st);
+void nhwc_gap_fwd(const uint16_t* x, float* y, int N, int HW, int C, hipStream_t st);
+void nhwc_gap_bwd(const float* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st);
+
 // ---- optimizers (ops_optim.hip): flat multi-tensor, fp32 master ----
 // SGD (PyTorch semantics): g' = g*gscale + wd*p; buf = mom*buf + g' (buf=g' at first step); p -= lr*buf
 // `lr` is read from device memory so a captured graph follows LR schedules.

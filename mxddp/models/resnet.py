@@ -1,6 +1,13 @@
 """ResNet-50 (BASELINE.json config 5 only: not in the reference).  torchvision-style
 topology and parameter names (conv1/bn1/layer1..4/fc, Bottleneck with downsample.0/.1),
 25,557,032 parameters, on mxddp kernels.  ReLU is fused into the BN that precedes it.
+
+Two execution paths over the same parameters (identical ``state_dict``):
+
+* NCHW fp32 (CPU, and GPU at compute dtype fp32): ``mxddp.ops`` layer kernels;
+* channels-last bf16 (GPU at compute dtype bf16, the config-5 benchmark): activations bf16
+  NHWC end to end (``mxddp.ops.nhwc``), vectorized implicit-GEMM MFMA convolutions, BN with the
+  Bottleneck's residual add + ReLU fused into its apply kernel, fp32 master weights / grads.
 """
 from __future__ import annotations
 
@@ -8,6 +15,10 @@ import torch.nn as nn
 
 from .. import ops
 from .layers import BatchNorm2d, Conv2d, Linear, MaxPool2d
+
+
+def _nhwc_mode(x) -> bool:
+    return x.is_cuda and ops.compute_dtype() == "bf16"
 
 
 class Bottleneck(nn.Module):
@@ -28,6 +39,18 @@ class Bottleneck(nn.Module):
         idt = x if self.downsample is None else self.downsample(x)
         out = self.bn3(self.conv3(self.bn2(self.conv2(self.bn1(self.conv1(x))))))
         return ops.relu(out + idt)
+
+    def forward_nhwc(self, x):
+        from ..ops import nhwc as N
+
+        if self.downsample is None:
+            idt = x
+        else:
+            dc, dbn = self.downsample[0], self.downsample[1]
+            idt = N.batch_norm(N.conv2d(x, dc.weight, dc.stride, dc.padding), dbn)
+        out = N.batch_norm(N.conv2d(x, self.conv1.weight), self.bn1, relu=True)
+        out = N.batch_norm(N.conv2d(out, self.conv2.weight, self.conv2.stride, self.conv2.padding), self.bn2, relu=True)
+        return N.batch_norm(N.conv2d(out, self.conv3.weight), self.bn3, relu=True, res=idt)
 
 
 class ResNet(nn.Module):
@@ -63,10 +86,24 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
+        if _nhwc_mode(x):
+            return self.forward_nhwc(x)
         x = self.maxpool(self.bn1(self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = ops.avg_pool2d(x, (x.shape[2], x.shape[3]))
         return self.fc(x.flatten(1))
+
+
+    def forward_nhwc(self, x):
+        from ..ops import nhwc as N
+
+        y = N.to_nhwc(x)
+        y = N.batch_norm(N.conv2d(y, self.conv1.weight, self.conv1.stride, self.conv1.padding), self.bn1, relu=True)
+        y = N.max_pool2d(y, 3, 2, 1)
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for blk in layer:
+                y = blk.forward_nhwc(y)
+        return self.fc(N.global_avg_pool(y))
 
 
 def resnet50(num_classes: int = 1000) -> ResNet:

@@ -1,0 +1,200 @@
+"""Channels-last bf16 ops (``mxddp/csrc/nhwc_bf16.hip``): the ResNet-50 mixed-precision path
+(BASELINE.json config 5: "ResNet-50 synthetic-ImageNet DDP bf16").
+
+Activations are bf16 tensors of logical shape ``[N, H, W, C]`` (contiguous, C a multiple of 8;
+the 3-channel image is zero-padded to 8).  Parameters stay fp32 torch-layout ``nn.Conv2d`` /
+``nn.BatchNorm2d`` tensors (same ``state_dict`` as the NCHW model); each convolution repacks its
+fp32 weights into the bf16 GEMM layout it needs (a few MB, once per call) and weight gradients
+are accumulated in fp32 straight into the flat DDP gradient buffer when one is attached
+(``mxddp.ops._grad_sink``).  Batch-norm statistics, accumulation and the optimizer are fp32.
+
+GPU only: there is no CPU twin of these kernels (the CPU path of ResNet-50 is the NCHW fp32
+model in ``mxddp.models.resnet``, which is also the oracle of ``tests/test_gpu_nhwc.py``).
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import native
+from . import _grad_sink, _p, stream_of
+
+BF16 = torch.bfloat16
+
+
+def _out(H, k, s, p):
+    return (H + 2 * p - k) // s + 1
+
+
+class _ToNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cp):
+        x = x.contiguous()
+        N, C, H, W = x.shape
+        y = torch.empty((N, H, W, cp), device=x.device, dtype=BF16)
+        native().nhwc_from_nchw(x.data_ptr(), y.data_ptr(), N, C, H, W, cp, stream_of(x))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        return None, None  # network input: no gradient
+
+
+def to_nhwc(x: torch.Tensor, cp: int | None = None) -> torch.Tensor:
+    """fp32 NCHW -> bf16 NHWC with channels zero-padded to ``cp`` (default: next multiple of 8)."""
+    C = x.shape[1]
+    return _ToNHWC.apply(x, cp or (C + 7) // 8 * 8)
+
+
+class _Conv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride, pad):
+        Cn = native()
+        N, H, W, Cp = x.shape
+        K, C, R, S = w.shape
+        sh, sw = stride
+        ph, pw = pad
+        P, Q = _out(H, R, sh, ph), _out(W, S, sw, pw)
+        st = stream_of(x)
+        wt = torch.empty((K * R * S * Cp,), device=x.device, dtype=BF16)
+        Cn.nhwc_repack_weight(w.data_ptr(), wt.data_ptr(), K, C, R, S, Cp, False, st)
+        y = torch.empty((N, P, Q, K), device=x.device, dtype=BF16)
+        Cn.nhwc_conv_fwd(x.data_ptr(), wt.data_ptr(), y.data_ptr(), N, H, W, Cp, K, R, S, sh, sw, ph, pw, P, Q, st)
+        ctx.save_for_backward(x, w)
+        ctx.geom = (N, H, W, Cp, K, C, R, S, sh, sw, ph, pw, P, Q)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        Cn = native()
+        x, w = ctx.saved_tensors
+        N, H, W, Cp, K, C, R, S, sh, sw, ph, pw, P, Q = ctx.geom
+        dy = dy.contiguous()
+        st = stream_of(dy)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if Cp != C:
+                raise NotImplementedError("nhwc conv: input gradient of a channel-padded input")
+            wtd = torch.empty((C * R * S * K,), device=dy.device, dtype=BF16)
+            Cn.nhwc_repack_weight(w.data_ptr(), wtd.data_ptr(), K, C, R, S, Cp, True, st)
+            dx = torch.empty((N, H, W, C), device=dy.device, dtype=BF16)
+            Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx.data_ptr(), N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q,
+                               st)
+        if ctx.needs_input_grad[1]:
+            sink = _grad_sink(w)
+            dw = sink if sink is not None else torch.empty_like(w)
+            part = torch.empty((Cn.nhwc_wgrad_scratch_floats(N, Cp, K, R, S, P, Q),), device=dy.device,
+                               dtype=torch.float32)
+            Cn.nhwc_conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), N, H, W, C, Cp, K, R, S, sh, sw, ph, pw,
+                               P, Q, sink is not None, part.data_ptr(), st)
+            if sink is not None:
+                dw = None
+        return dx, dw, None, None
+
+
+def conv2d(x, w, stride=1, padding=0):
+    s = (stride, stride) if isinstance(stride, int) else tuple(stride)
+    p = (padding, padding) if isinstance(padding, int) else tuple(padding)
+    return _Conv.apply(x, w, s, p)
+
+
+class _BN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, rm, rv, nbt, res, relu, momentum, eps):
+        Cn = native()
+        N, H, W, C = x.shape
+        npix = N * H * W
+        y = torch.empty_like(x)
+        mean = torch.empty((C,), device=x.device, dtype=torch.float32)
+        invstd = torch.empty_like(mean)
+        scr = torch.empty((Cn.nhwc_bn_scratch_floats(npix, C),), device=x.device, dtype=torch.float32)
+        Cn.nhwc_bn_fwd(x.data_ptr(), _p(res), y.data_ptr(), _p(gamma), _p(beta), mean.data_ptr(), invstd.data_ptr(),
+                       _p(rm), _p(rv), _p(nbt), npix, C, float(momentum), float(eps), bool(relu), scr.data_ptr(),
+                       stream_of(x))
+        ctx.save_for_backward(x, y, gamma, mean, invstd)
+        ctx.relu, ctx.has_res = bool(relu), res is not None
+        ctx.refs = (gamma, beta)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        Cn = native()
+        x, y, gamma, mean, invstd = ctx.saved_tensors
+        N, H, W, C = x.shape
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if ctx.has_res else None
+        g_ref, b_ref = ctx.refs
+        gs, bs = _grad_sink(g_ref), _grad_sink(b_ref)
+        direct = gs is not None and bs is not None
+        dg, db = (gs, bs) if direct else (torch.empty((C,), device=x.device), torch.empty((C,), device=x.device))
+        scr = torch.empty((Cn.nhwc_bn_scratch_floats(N * H * W, C),), device=x.device, dtype=torch.float32)
+        Cn.nhwc_bn_bwd(dy.data_ptr(), x.data_ptr(), y.data_ptr(), _p(gamma), mean.data_ptr(), invstd.data_ptr(),
+                       dx.data_ptr(), _p(dres), dg.data_ptr(), db.data_ptr(), N * H * W, C, ctx.relu, direct,
+                       scr.data_ptr(), stream_of(dy))
+        if direct:
+            dg = db = None
+        return dx, dg, db, None, None, None, dres, None, None, None
+
+
+def batch_norm(x, bn: torch.nn.BatchNorm2d, relu: bool = False, res: torch.Tensor | None = None):
+    """Training-mode BN of an NHWC bf16 tensor with the module's parameters / buffers (running
+    stats and num_batches_tracked updated on device), fused ReLU and residual add (y = relu(bn(x) +
+    res)).  Eval mode uses the running statistics (plain tensor math)."""
+    if bn.training or not bn.track_running_stats:
+        mom = bn.momentum if bn.momentum is not None else 0.1
+        nbt = bn.num_batches_tracked if (bn.training and bn.track_running_stats) else None
+        return _BN.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, res, relu, mom, bn.eps)
+    y = (x.float() - bn.running_mean) * torch.rsqrt(bn.running_var + bn.eps) * bn.weight + bn.bias
+    if res is not None:
+        y = y + res.float()
+    return (y.relu() if relu else y).to(BF16)
+
+
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        N, H, W, C = x.shape
+        P, Q = _out(H, k, s, p), _out(W, k, s, p)
+        y = torch.empty((N, P, Q, C), device=x.device, dtype=BF16)
+        arg = torch.empty((N, P, Q, C), device=x.device, dtype=torch.uint8)
+        native().nhwc_maxpool_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), N, H, W, C, P, Q, k, s, p, stream_of(x))
+        ctx.save_for_backward(arg)
+        ctx.geom = (N, H, W, C, P, Q, k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        N, H, W, C, P, Q, k, s, p = ctx.geom
+        dy = dy.contiguous()
+        dx = torch.empty((N, H, W, C), device=dy.device, dtype=BF16)
+        native().nhwc_maxpool_bwd(dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), N, H, W, C, P, Q, k, s, p,
+                                  stream_of(dy))
+        return dx, None, None, None
+
+
+def max_pool2d(x, k, s, p):
+    return _MaxPool.apply(x, k, s, p)
+
+
+class _GAP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        N, H, W, C = x.shape
+        y = torch.empty((N, C), device=x.device, dtype=torch.float32)
+        native().nhwc_gap_fwd(x.data_ptr(), y.data_ptr(), N, H * W, C, stream_of(x))
+        ctx.geom = (N, H, W, C)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, C = ctx.geom
+        dy = dy.contiguous()
+        dx = torch.empty((N, H, W, C), device=dy.device, dtype=BF16)
+        native().nhwc_gap_bwd(dy.data_ptr(), dx.data_ptr(), N, H * W, C, stream_of(dy))
+        return dx
+
+
+def global_avg_pool(x):
+    """bf16 [N, H, W, C] -> fp32 [N, C] (the classifier runs on fp32 features)."""
+    return _GAP.apply(x)
