@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--steps-per-graph", type=int, default=None, help="fused engine, graph mode 1: steps unrolled per graph")
     ap.add_argument("--force-collectives", action="store_true",
                     help="fused engine: issue the RCCL bucket all-reduces even at world size 1 (measures the DDP path)")
+    ap.add_argument("--channels-last", action="store_true",
+                    help="--impl torch: channels_last memory format (stock PyTorch's NHWC convs, for a fair bf16 baseline)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--lr", type=float, default=0.01, help="SGD lr (momentum 0.9, wd 1e-4 as the reference)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
@@ -135,7 +137,7 @@ def main():
             "data": _data_desc(spec),
             "config": {"model": a.model, "global_batch": B * a.gpus, "per_rank_batch": B, "seq_len": None,
                        "image": "x".join(map(str, spec.input_shape)), "parallelism": f"dp{a.gpus}", "impl": a.impl,
-                       "graph": (a.impl == "fused" and not a.no_graph),
+                       "graph": (a.impl == "fused" and not a.no_graph) or getattr(a, "layers_graph", False),
                        **({"graph_mode": tr.eng.graph_mode, "overlap": tr.eng.overlap,
                            "force_collectives": a.force_collectives, "autotune": tr.tuned}
                           if a.impl == "fused" else {})},
@@ -240,6 +242,8 @@ def _layers_or_torch(a, torch, inf, dev, comm, B):
             import torch.distributed as dist
 
             raise SystemExit("--impl torch is single-GPU only in this harness")
+        if a.channels_last:
+            ref = ref.to(memory_format=torch.channels_last)
         net = ref
         opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
         loss_fn = lambda o, t: F.cross_entropy(o, t)  # noqa: E731
@@ -261,18 +265,45 @@ def _layers_or_torch(a, torch, inf, dev, comm, B):
     amp = (torch.autocast("cuda", dtype=torch.bfloat16) if (a.impl == "torch" and a.dtype == "bf16")
            else contextlib.nullcontext())
 
-    def run(n):
-        for _ in range(n):
-            Cn.synth_batch(x.data_ptr(), y.data_ptr(), tmpl.data_ptr(), B, D, nc, a.seed + inf.rank, ctr.data_ptr(),
-                           torch.cuda.current_stream(dev).cuda_stream)
-            opt.zero_grad()
-            with amp:
-                out = net(x)
-                loss = loss_fn(out, y.long())
-            loss.backward()
-            opt.step()
+    from mxddp import ops as _mx_ops
 
-    return run
+    def step():
+        if a.impl == "layers":
+            _mx_ops.bn_reset_accumulators()  # graph replays start from the captured BN state
+        Cn.synth_batch(x.data_ptr(), y.data_ptr(), tmpl.data_ptr(), B, D, nc, a.seed + inf.rank, ctr.data_ptr(),
+                       torch.cuda.current_stream(dev).cuda_stream)
+        opt.zero_grad()
+        with amp:
+            out = net(x.contiguous(memory_format=torch.channels_last) if a.channels_last else x)
+            loss = loss_fn(out, y.long())
+        loss.backward()
+        opt.step()
+
+    def run_eager(n):
+        for _ in range(n):
+            step()
+
+    # Whole-step hipGraph for the single-GPU layer path: the ~700 (ResNet-50) to ~1,500
+    # (PyramidNet) kernel launches of a step are replayed without Python / autograd overhead.
+    # Every op of the step is graph-safe (no host sync; LR, step counters and the synthetic
+    # data counter live on the device).
+    if a.impl == "layers" and not a.no_graph and inf.world_size == 1:
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            run_eager(2)  # allocator / autograd warm-up outside the capture
+        torch.cuda.current_stream(dev).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+
+        def run_graph(n):
+            for _ in range(n):
+                graph.replay()
+
+        a.layers_graph = True
+        return run_graph
+    return run_eager
 
 
 if __name__ == "__main__":

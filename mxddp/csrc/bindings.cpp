@@ -78,19 +78,21 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_from_nchw", [](uintptr_t x, uintptr_t y, int N, int C, int H, int W, int Cp, uintptr_t st) {
     nhwc_from_nchw(P<const float>(x), P<uint16_t>(y), N, C, H, W, Cp, S(st));
   });
-  m.def("nhwc_repack_weight", [](uintptr_t w, uintptr_t wt, int K, int C, int R, int S_, int Cp, bool dgrad,
+  m.def("nhwc_repack_weight", [](uintptr_t w, uintptr_t wt, uintptr_t wtd, int K, int C, int R, int S_, int Cp,
                                  uintptr_t st) {
-    nhwc_repack_weight(P<const float>(w), P<uint16_t>(wt), K, C, R, S_, Cp, dgrad, S(st));
+    nhwc_repack_weight(P<const float>(w), P<uint16_t>(wt), P<uint16_t>(wtd), K, C, R, S_, Cp, S(st));
   });
   m.def("nhwc_conv_fwd", [](uintptr_t x, uintptr_t wt, uintptr_t y, int N, int H, int W, int Cp, int K, int R, int S_,
-                            int sh, int sw, int ph, int pw, int P_, int Q, uintptr_t st) {
+                            int sh, int sw, int ph, int pw, int P_, int Q, uintptr_t scratch, uintptr_t st) {
     nhwc_conv_fwd(P<const uint16_t>(x), P<const uint16_t>(wt), P<uint16_t>(y), N, H, W, Cp, K, R, S_, sh, sw, ph, pw,
-                  P_, Q, S(st));
+                  P_, Q, P<float>(scratch), S(st));
   });
+  m.def("nhwc_conv_scratch_floats", &nhwc_conv_scratch_floats);
   m.def("nhwc_conv_dgrad", [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int N, int H, int W, int C, int K, int R,
-                              int S_, int sh, int sw, int ph, int pw, int P_, int Q, uintptr_t st) {
+                              int S_, int sh, int sw, int ph, int pw, int P_, int Q, uintptr_t scratch,
+                              uintptr_t st) {
     nhwc_conv_dgrad(P<const uint16_t>(dy), P<const uint16_t>(wt), P<uint16_t>(dx), N, H, W, C, K, R, S_, sh, sw, ph,
-                    pw, P_, Q, S(st));
+                    pw, P_, Q, P<float>(scratch), S(st));
   });
   m.def("nhwc_conv_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, int N, int H, int W, int Cin, int Cp, int K,
                               int R, int S_, int sh, int sw, int ph, int pw, int P_, int Q, bool acc, uintptr_t scratch,

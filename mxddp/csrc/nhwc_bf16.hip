@@ -68,6 +68,8 @@ struct ConvNArgs {
   int OH, OW, IH, IW;
   int S, sh, sw, ph, pw;
   int dgrad;        // 0: y = conv(x); 1: dx = conv_transpose(dy) (sh, sw in {1, 2})
+  int kt_per_split; // split-K: blockIdx.y covers k-tiles [y * kt_per_split, ...)
+  float* part;      // split-K > 1: fp32 partials [splits][M][Ng] (else null: bf16 store)
   FastDiv fOW, fOHW, fCa, fS;
 };
 
@@ -143,14 +145,15 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
 #pragma unroll
     for (int j = 0; j < WNT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nt = (a.Kg + BK - 1) / BK;
+  const int kt0 = blockIdx.y * a.kt_per_split;
+  const int nt = min((a.Kg + BK - 1) / BK - kt0, a.kt_per_split);
   const int a_row = wm * (TM / 2) + (lane & 15), b_row = wn * (TN / 2) + (lane & 15), koff = 8 * (lane >> 4);
-  gload(0);
+  gload(kt0 * BK);
   sstore(0);
   __syncthreads();
   for (int t = 0; t < nt; ++t) {
     const int cur = t & 1;
-    if (t + 1 < nt) gload((t + 1) * BK);
+    if (t + 1 < nt) gload((kt0 + t + 1) * BK);
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8 av[WMT], bv[WNT];
@@ -171,17 +174,59 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
   }
 
   // C/D: row (output channel) = 4 * (lane >> 4) + r, column (pixel) = lane & 15
+  if (a.part) {  // split-K: fp32 partials, summed by conv_nhwc_splitk_reduce_k
+#pragma unroll
+    for (int i = 0; i < WMT; ++i) {
+      const int ch = ch0 + wm * (TM / 2) + 16 * i + 4 * (lane >> 4);
+      if (ch >= a.Ng) continue;
+#pragma unroll
+      for (int j = 0; j < WNT; ++j) {
+        const int px = px0 + wn * (TN / 2) + 16 * j + (lane & 15);
+        if (px >= a.M) continue;
+        *reinterpret_cast<float4*>(a.part + ((size_t)blockIdx.y * a.M + px) * a.Ng + ch) =
+            make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+    }
+    return;
+  }
+  // bf16 output staged through LDS ([TN pixels][TM channels]) so the global stores are full
+  // 16-byte vectors along each pixel's channel row (an 8-byte store per lane straight from the
+  // MFMA layout touches 16 rows per 16 lanes)
+  constexpr int CP = TM + 8;  // pitch (bf16): 16-byte aligned rows, rotating banks
+  static_assert(TN * CP <= 2 * TM * LD, "C tile must fit in the A operand buffers");
+  bf16* Cs = &As[0][0];  // the k loop ended on a barrier: the operand buffers are free
 #pragma unroll
   for (int i = 0; i < WMT; ++i) {
-    const int ch = ch0 + wm * (TM / 2) + 16 * i + 4 * (lane >> 4);
-    if (ch >= a.Ng) continue;
+    const int cl = wm * (TM / 2) + 16 * i + 4 * (lane >> 4);
 #pragma unroll
     for (int j = 0; j < WNT; ++j) {
-      const int px = px0 + wn * (TN / 2) + 16 * j + (lane & 15);
-      if (px >= a.M) continue;
-      *reinterpret_cast<uint2*>(a.out + (size_t)px * a.Ng + ch) =
+      const int pl = wn * (TN / 2) + 16 * j + (lane & 15);
+      *reinterpret_cast<uint2*>(Cs + pl * CP + cl) =
           make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
     }
+  }
+  __syncthreads();
+  constexpr int VPR = TM / 8;  // 16-byte vectors per pixel row
+#pragma unroll
+  for (int v = tid; v < TN * VPR; v += 256) {
+    const int row = v / VPR, cv = v - row * VPR;
+    const int px = px0 + row, ch = ch0 + 8 * cv;
+    if (px < a.M && ch < a.Ng)
+      *reinterpret_cast<u32x4*>(a.out + (size_t)px * a.Ng + ch) = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
+  }
+}
+
+// split-K epilogue: out (bf16) = sum over splits of the fp32 partials (fixed order)
+__global__ void conv_nhwc_splitk_reduce_k(const float* __restrict__ part, bf16* __restrict__ out, int64_t n4,
+                                          int splits) {
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 s = p4[i];
+    for (int sp = 1; sp < splits; ++sp) {
+      const float4 v = p4[sp * n4 + i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    reinterpret_cast<uint2*>(out)[i] = make_uint2(pack2(s.x, s.y), pack2(s.z, s.w));
   }
 }
 
@@ -335,22 +380,24 @@ __global__ void nchw_to_nhwc_k(const float* __restrict__ x, bf16* __restrict__ y
   }
 }
 
-// w fp32 [K][C][R][S] -> fwd: bf16 [K][R][S][Cp] (zero-padded channels); dgrad: bf16 [C][R][S][K]
-__global__ void wrepack_k(const float* __restrict__ w, bf16* __restrict__ wt, int K, int C, int R, int S, int Cp,
-                          int dgrad) {
+// w fp32 [K][C][R][S] -> fwd: bf16 [K][R][S][Cp] (zero-padded channels) and/or dgrad: bf16
+// [C][R][S][K]; both layouts in one pass when both pointers are given (one launch per conv)
+__global__ void wrepack_k(const float* __restrict__ w, bf16* __restrict__ wt, bf16* __restrict__ wtd, int K, int C,
+                          int R, int S, int Cp) {
   const int RS = R * S;
-  const int64_t total = dgrad ? (int64_t)C * RS * K : (int64_t)K * RS * Cp;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    if (!dgrad) {
+  const int64_t tf = wt ? (int64_t)K * RS * Cp : 0, td = wtd ? (int64_t)C * RS * K : 0;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < tf + td; i += (int64_t)gridDim.x * 256) {
+    if (i < tf) {
       const int c = (int)(i % Cp);
       const int64_t krs = i / Cp;
       const int rs = (int)(krs % RS), k = (int)(krs / RS);
       wt[i] = c < C ? f2bf(w[((int64_t)k * C + c) * RS + rs]) : (bf16)0;
     } else {
-      const int k = (int)(i % K);
-      const int64_t crs = i / K;
+      const int64_t j = i - tf;
+      const int k = (int)(j % K);
+      const int64_t crs = j / K;
       const int rs = (int)(crs % RS), c = (int)(crs / RS);
-      wt[i] = f2bf(w[((int64_t)k * C + c) * RS + rs]);
+      wtd[j] = f2bf(w[((int64_t)k * C + c) * RS + rs]);
     }
   }
 }
@@ -673,31 +720,72 @@ void nhwc_from_nchw(const float* x, uint16_t* y, int N, int C, int H, int W, int
   MX_LAUNCH(nchw_to_nhwc_k, dim3(grid_for((int64_t)N * H * W * Cp)), dim3(256), 0, st, x, y, N, C, H * W, Cp);
 }
 
-void nhwc_repack_weight(const float* w, uint16_t* wt, int K, int C, int R, int S, int Cp, bool dgrad, hipStream_t st) {
-  MX_LAUNCH(wrepack_k, dim3(grid_for((int64_t)K * (dgrad ? C : Cp) * R * S)), dim3(256), 0, st, w, wt, K, C, R, S,
-            Cp, dgrad ? 1 : 0);
+void nhwc_repack_weight(const float* w, uint16_t* wt, uint16_t* wtd, int K, int C, int R, int S, int Cp,
+                        hipStream_t st) {
+  const int64_t total = (wt ? (int64_t)K * Cp * R * S : 0) + (wtd ? (int64_t)K * C * R * S : 0);
+  MX_LAUNCH(wrepack_k, dim3(grid_for(total)), dim3(256), 0, st, w, wt, wtd, K, C, R, S, Cp);
 }
 
-static void launch_conv(ConvNArgs& a, hipStream_t st) {
-  MX_CHECK(a.Kg % 8 == 0 && a.Ca % 8 == 0 && a.Ng % 4 == 0, "nhwc conv: channels must be multiples of 8");
+struct ConvPlan {
+  int tm, tn, blocks, splits, kt_per_split;
+};
+
+// largest tile whose grid still gives every CU two blocks (layer3/4 of ResNet-50 have only
+// 1.5k-6k output pixels at batch 32): 128 x 128, then 64 x 128, then 64 x 64; when even 64 x 64
+// leaves the chip under-filled, split the reduction (k-tiles) over blockIdx.y with fp32
+// partials (>= 8 k-tiles per split)
+static ConvPlan conv_plan(int M, int Ng, int Kg) {
+  ConvPlan p{};
+  const int b128 = cdiv(Ng, 128) * cdiv(M, 128), b64 = cdiv(Ng, 64) * cdiv(M, 128);
+  if (Ng > 64 && b128 >= 512) {
+    p.tm = 128; p.tn = 128; p.blocks = b128;
+  } else if (b64 >= 512 || (Ng <= 64 && M >= 128 * 256)) {
+    p.tm = 64; p.tn = 128; p.blocks = b64;
+  } else {
+    p.tm = 64; p.tn = 64; p.blocks = cdiv(Ng, 64) * cdiv(M, 64);
+  }
+  const int nkt = cdiv(Kg, 64);
+  p.splits = 1;
+  if (p.blocks < 512) p.splits = std::max(1, std::min(cdiv(512, p.blocks), nkt / 8));
+  p.kt_per_split = cdiv(nkt, p.splits);
+  p.splits = cdiv(nkt, p.kt_per_split);
+  return p;
+}
+
+size_t nhwc_conv_scratch_floats(int M, int Ng, int Kg) {
+  const ConvPlan p = conv_plan(M, Ng, Kg);
+  return p.splits > 1 ? (size_t)p.splits * M * Ng : 0;
+}
+
+static void launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
+  MX_CHECK(a.Kg % 8 == 0 && a.Ca % 8 == 0 && a.Ng % 8 == 0, "nhwc conv: channels must be multiples of 8");
   a.fOW = FastDiv(a.OW);
   a.fOHW = FastDiv(a.OH * a.OW);
   a.fCa = FastDiv(a.Ca);
   a.fS = FastDiv(a.S);
-  // largest tile whose grid still gives every CU two blocks (layer3/4 of ResNet-50 have only
-  // 1.5k-6k output pixels at batch 32): 128 x 128, then 64 x 128, then 64 x 64
-  const int b128 = cdiv(a.Ng, 128) * cdiv(a.M, 128), b64 = cdiv(a.Ng, 64) * cdiv(a.M, 128);
-  if (a.Ng > 64 && b128 >= 512) {
-    MX_LAUNCH((conv_nhwc_kernel<128, 128>), dim3(b128), dim3(256), 0, st, a);
-  } else if (b64 >= 512 || a.Ng <= 64 && a.M >= 128 * 256) {
-    MX_LAUNCH((conv_nhwc_kernel<64, 128>), dim3(b64), dim3(256), 0, st, a);
+  ConvPlan p = conv_plan(a.M, a.Ng, a.Kg);
+  if (!scratch) {  // no partial buffer: no split
+    p.splits = 1;
+    p.kt_per_split = cdiv(a.Kg, 64);
+  }
+  a.kt_per_split = p.kt_per_split;
+  a.part = p.splits > 1 ? scratch : nullptr;
+  const dim3 grid(p.blocks, p.splits);
+  if (p.tm == 128) {
+    MX_LAUNCH((conv_nhwc_kernel<128, 128>), grid, dim3(256), 0, st, a);
+  } else if (p.tn == 128) {
+    MX_LAUNCH((conv_nhwc_kernel<64, 128>), grid, dim3(256), 0, st, a);
   } else {
-    MX_LAUNCH((conv_nhwc_kernel<64, 64>), dim3(cdiv(a.Ng, 64) * cdiv(a.M, 64)), dim3(256), 0, st, a);
+    MX_LAUNCH((conv_nhwc_kernel<64, 64>), grid, dim3(256), 0, st, a);
+  }
+  if (p.splits > 1) {
+    const int64_t n4 = (int64_t)a.M * a.Ng / 4;
+    MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, p.splits);
   }
 }
 
 void nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int H, int W, int Cp, int K, int R,
-                   int S, int sh, int sw, int ph, int pw, int P, int Q, hipStream_t st) {
+                   int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st) {
   ConvNArgs a{};
   a.act = x;
   a.wt = wt;
@@ -716,11 +804,11 @@ void nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, in
   a.ph = ph;
   a.pw = pw;
   a.dgrad = 0;
-  launch_conv(a, st);
+  launch_conv(a, scratch, st);
 }
 
 void nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
-                     int S, int sh, int sw, int ph, int pw, int P, int Q, hipStream_t st) {
+                     int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st) {
   MX_CHECK((sh == 1 || sh == 2) && (sw == 1 || sw == 2), "nhwc dgrad: stride 1 or 2");
   ConvNArgs a{};
   a.act = dy;
@@ -740,7 +828,7 @@ void nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int
   a.ph = ph;
   a.pw = pw;
   a.dgrad = 1;
-  launch_conv(a, st);
+  launch_conv(a, scratch, st);
 }
 
 static int wgrad_splits(int Npix, int K, int Ng) {

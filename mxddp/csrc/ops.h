@@ -126,12 +126,16 @@ void shortcut_pad_add_bwd(const float* dy, float* dx, int N, int Cin, int H, int
 
 // ---- channels-last bf16 path (nhwc_bf16.hip): activations bf16 [N][H][W][C], C % 8 == 0 ----
 void nhwc_from_nchw(const float* x, uint16_t* y, int N, int C, int H, int W, int Cp, hipStream_t st);
-// fwd: bf16 [K][R][S][Cp] (channel-padded); dgrad: bf16 [C][R][S][K]
-void nhwc_repack_weight(const float* w, uint16_t* wt, int K, int C, int R, int S, int Cp, bool dgrad, hipStream_t st);
+// wt (or null): fwd layout bf16 [K][R][S][Cp] (channel-padded); wtd (or null): dgrad layout bf16 [C][R][S][K]
+void nhwc_repack_weight(const float* w, uint16_t* wt, uint16_t* wtd, int K, int C, int R, int S, int Cp,
+                        hipStream_t st);
+// scratch (or null = no split-K): nhwc_conv_scratch_floats(M = output pixels, Ng = output
+// channels, Kg = R*S*input channels) floats of fp32 split-K partials
+size_t nhwc_conv_scratch_floats(int M, int Ng, int Kg);
 void nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int H, int W, int Cp, int K, int R,
-                   int S, int sh, int sw, int ph, int pw, int P, int Q, hipStream_t st);
+                   int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st);
 void nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
-                     int S, int sh, int sw, int ph, int pw, int P, int Q, hipStream_t st);
+                     int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st);
 // dw fp32 [K][Cin][R][S] (+)= ...; x has Cp >= Cin channels (padding ignored);
 // scratch: nhwc_wgrad_scratch_floats(...) floats of per-split partial sums
 size_t nhwc_wgrad_scratch_floats(int N, int Cp, int K, int R, int S, int P, int Q);

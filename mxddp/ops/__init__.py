@@ -398,6 +398,15 @@ def _bn_acc(device, kind, C):
     return buf[p], buf[p ^ 1], hi
 
 
+def bn_reset_accumulators() -> None:
+    """Zero the BN accumulator pairs and restart their double-buffer parity.  Call at the start
+    of a step that is captured in a HIP graph: a replay then starts from the same accumulator
+    state as the capture did, whatever the number of BN calls per step."""
+    for st in _BN_ACC.values():
+        st[0].zero_()
+        st[1] = 0
+
+
 def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum=0.1, eps=1e-5, relu=False,
                num_batches=None):
     """``num_batches`` (int64 tensor, GPU path): incremented on device by the BN kernel

@@ -45,6 +45,11 @@ def to_nhwc(x: torch.Tensor, cp: int | None = None) -> torch.Tensor:
     return _ToNHWC.apply(x, cp or (C + 7) // 8 * 8)
 
 
+def _splitk_scratch(M, Ng, Kg, device):
+    n = native().nhwc_conv_scratch_floats(M, Ng, Kg)
+    return torch.empty((n,), device=device, dtype=torch.float32) if n else None
+
+
 class _Conv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, pad):
@@ -56,9 +61,15 @@ class _Conv(torch.autograd.Function):
         P, Q = _out(H, R, sh, ph), _out(W, S, sw, pw)
         st = stream_of(x)
         wt = torch.empty((K * R * S * Cp,), device=x.device, dtype=BF16)
-        Cn.nhwc_repack_weight(w.data_ptr(), wt.data_ptr(), K, C, R, S, Cp, False, st)
+        # the data-gradient layout is produced in the same launch when backward will need it
+        need_dx = ctx.needs_input_grad[0] and Cp == C
+        wtd = torch.empty((C * R * S * K,), device=x.device, dtype=BF16) if need_dx else None
+        Cn.nhwc_repack_weight(w.data_ptr(), wt.data_ptr(), _p(wtd), K, C, R, S, Cp, st)
         y = torch.empty((N, P, Q, K), device=x.device, dtype=BF16)
-        Cn.nhwc_conv_fwd(x.data_ptr(), wt.data_ptr(), y.data_ptr(), N, H, W, Cp, K, R, S, sh, sw, ph, pw, P, Q, st)
+        scr = _splitk_scratch(N * P * Q, K, R * S * Cp, x.device)
+        Cn.nhwc_conv_fwd(x.data_ptr(), wt.data_ptr(), y.data_ptr(), N, H, W, Cp, K, R, S, sh, sw, ph, pw, P, Q,
+                         _p(scr), st)
+        ctx.wtd = wtd
         ctx.save_for_backward(x, w)
         ctx.geom = (N, H, W, Cp, K, C, R, S, sh, sw, ph, pw, P, Q)
         return y
@@ -74,11 +85,14 @@ class _Conv(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if Cp != C:
                 raise NotImplementedError("nhwc conv: input gradient of a channel-padded input")
-            wtd = torch.empty((C * R * S * K,), device=dy.device, dtype=BF16)
-            Cn.nhwc_repack_weight(w.data_ptr(), wtd.data_ptr(), K, C, R, S, Cp, True, st)
+            wtd = ctx.wtd
+            if wtd is None:
+                wtd = torch.empty((C * R * S * K,), device=dy.device, dtype=BF16)
+                Cn.nhwc_repack_weight(w.data_ptr(), 0, wtd.data_ptr(), K, C, R, S, Cp, st)
             dx = torch.empty((N, H, W, C), device=dy.device, dtype=BF16)
+            scr = _splitk_scratch(N * H * W, C, R * S * K, dy.device)
             Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx.data_ptr(), N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q,
-                               st)
+                               _p(scr), st)
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(w)
             dw = sink if sink is not None else torch.empty_like(w)
