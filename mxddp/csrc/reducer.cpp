@@ -6,59 +6,37 @@ namespace mx {
 
 Reducer::Reducer(Comm* comm, uintptr_t flat_grad, DType dtype, const std::vector<BucketSpec>& buckets,
                  const std::vector<int>& param_bucket, RedOp op, bool timing)
-    : comm_(comm), flat_(reinterpret_cast<char*>(flat_grad)), dtype_(dtype), op_(op),
-      param_bucket_(param_bucket), timing_(timing) {
-  for (const auto& b : buckets) buckets_.push_back(Bucket{b.offset, b.numel, 0, 0, false, nullptr});
-  for (int pb : param_bucket_) {
-    MX_CHECK(pb >= 0 && pb < (int)buckets_.size(), "param assigned to unknown bucket");
-    buckets_[pb].total++;
-  }
-  for (auto& b : buckets_) MX_HIP_CHECK(hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
+    : comm_(comm), flat_(reinterpret_cast<char*>(flat_grad)), dtype_(dtype), op_(op), timing_(timing) {
+  std::vector<std::pair<size_t, size_t>> spans;
+  for (const auto& b : buckets) spans.emplace_back(b.offset, b.numel);
+  sched_ = BucketSchedule(spans, param_bucket);
+  ev_.assign(buckets.size(), nullptr);
+  for (auto& e : ev_) MX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   MX_HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
   MX_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
   if (timing_) {
     MX_HIP_CHECK(hipEventCreate(&t0_));
     MX_HIP_CHECK(hipEventCreate(&t1_));
   }
-  marked_.assign(param_bucket_.size(), 0);
-  prepare();
 }
 
 Reducer::~Reducer() {
-  for (auto& b : buckets_)
-    if (b.ev) hipEventDestroy(b.ev);
+  for (auto e : ev_)
+    if (e) hipEventDestroy(e);
   if (done_) hipEventDestroy(done_);
   if (t0_) hipEventDestroy(t0_);
   if (t1_) hipEventDestroy(t1_);
   if (comm_stream_) hipStreamDestroy(comm_stream_);
 }
 
-void Reducer::prepare() {
-  for (auto& b : buckets_) {
-    b.pending = b.total;
-    b.ready = false;
-  }
-  std::fill(marked_.begin(), marked_.end(), 0);
-  next_ = 0;
-}
+void Reducer::prepare() { sched_.prepare(); }
 
 void Reducer::mark_ready(int p, hipStream_t compute) {
-  MX_CHECK(p >= 0 && p < (int)param_bucket_.size(), "mark_ready: bad parameter index");
-  MX_CHECK(!marked_[p], "parameter marked ready twice in one backward pass (reentrant backward or "
-                        "shared parameter); reducer state would race");
-  marked_[p] = 1;
-  Bucket& b = buckets_[param_bucket_[p]];
-  if (--b.pending == 0) {
-    b.ready = true;
-    launch_ready(compute);
-  }
+  if (sched_.mark(p)) launch_ready(compute);
 }
 
 void Reducer::mark_bucket_ready(int bi, hipStream_t compute) {
-  MX_CHECK(bi >= 0 && bi < (int)buckets_.size(), "mark_bucket_ready: bad bucket");
-  Bucket& b = buckets_[bi];
-  b.pending = 0;
-  b.ready = true;
+  sched_.mark_bucket(bi);
   launch_ready(compute);
 }
 
@@ -66,32 +44,25 @@ bool Reducer::active() const { return comm_ && (comm_->world_size() > 1 || force
 
 void Reducer::launch_ready(hipStream_t compute) {
   const bool act = active();
-  while (next_ < (int)buckets_.size() && buckets_[next_].ready) {
-    Bucket& b = buckets_[next_];
-    MX_CHECK(b.pending == 0, "bucket launched before all its gradients were ready");
+  for (int bi = sched_.pop_ready(); bi >= 0; bi = sched_.pop_ready()) {
+    const BucketSchedule::Bucket& b = sched_.bucket(bi);
     if (act) {  // no collectives -> no fences either (a fence alone costs a few us of GPU idle)
       hipStream_t st = compute;
       if (overlap_) {
-        MX_HIP_CHECK(hipEventRecord(b.ev, compute));
-        MX_HIP_CHECK(hipStreamWaitEvent(comm_stream_, b.ev, 0));
+        MX_HIP_CHECK(hipEventRecord(ev_[bi], compute));
+        MX_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_[bi], 0));
         st = comm_stream_;
         side_used_ = true;
       }
-      if (timing_ && next_ == 0) MX_HIP_CHECK(hipEventRecord(t0_, st));
+      if (timing_ && bi == 0) MX_HIP_CHECK(hipEventRecord(t0_, st));
       char* p = flat_ + b.offset * dtype_size(dtype_);
       comm_->all_reduce(p, p, b.numel, dtype_, op_, st);
     }
-    ++next_;
   }
 }
 
 void Reducer::finalize(hipStream_t compute) {
-  for (auto& b : buckets_) {
-    if (!b.ready) {  // unused parameters: reduce whatever the bucket holds (zeros on this rank)
-      b.pending = 0;
-      b.ready = true;
-    }
-  }
+  sched_.release_all();  // unused parameters: reduce whatever the bucket holds (zeros on this rank)
   launch_ready(compute);
   if (!active()) return;
   if (timing_) {

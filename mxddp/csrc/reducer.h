@@ -17,6 +17,7 @@
 
 #include <vector>
 
+#include "bucket_schedule.h"
 #include "comm.h"
 
 namespace mx {
@@ -35,8 +36,8 @@ class Reducer {
   void mark_bucket_ready(int bucket, hipStream_t compute);  // fused engines: whole bucket at once
   void finalize(hipStream_t compute);               // launch stragglers; compute waits on comm
   hipStream_t comm_stream() const { return comm_stream_; }
-  int num_buckets() const { return (int)buckets_.size(); }
-  int launched() const { return next_; }
+  int num_buckets() const { return sched_.size(); }
+  int launched() const { return sched_.launched(); }
   // milliseconds between first bucket launch and comm completion of the last step
   // (requires timing=true; synchronises on the comm stream's end event).
   float last_comm_ms();
@@ -55,20 +56,12 @@ class Reducer {
 
  private:
   void launch_ready(hipStream_t compute);
-  struct Bucket {
-    size_t offset, numel;
-    int total, pending;
-    bool ready;
-    hipEvent_t ev;
-  };
   Comm* comm_;
   char* flat_;
   DType dtype_;
   RedOp op_;
-  std::vector<Bucket> buckets_;
-  std::vector<int> param_bucket_;
-  std::vector<char> marked_;
-  int next_ = 0;
+  BucketSchedule sched_;          // host state machine (bucket_schedule.h)
+  std::vector<hipEvent_t> ev_;    // per-bucket compute -> comm fence
   hipStream_t comm_stream_ = nullptr;
   hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
   bool timing_ = false, timed_ = false, force_ = false, overlap_ = true, side_used_ = false;

@@ -16,8 +16,8 @@
 // thread transforms one 4x4 window (prefetched into registers during the previous chunk's
 // MFMAs) into V in LDS, copies its part of the chunk's U slice (float4) into LDS, then 32 MFMAs
 // per wave.  The data gradient is the same
-// kernel on dy with the flipped / transposed filters (wino_wtrans_k, dgrad=1).  When the grid
-// would not fill the chip (8x8 images) the input channels are split across blocks (atomics).
+// kernel on dy with the flipped / transposed filters (wino_wtrans_k, dgrad=1).  (Splitting the
+// input channels across blocks with atomic accumulation is available but measured slower.)
 //
 // Weight gradient (wino_wgrad_kernel): F(3x3, 2x2): dW = A'^T [ sum_tiles (G' dy G'^T) o
 // (B^T x B) ] A', 16 GEMMs reducing over output tiles.  Block = 32 co x 32 ci x a range of
@@ -679,7 +679,14 @@ void launch_fwd(const float* x, const float* w, const float* bias, const float* 
   const int nch = Cip / kCC;
   // split the input channels when the grid would not fill the CUs (e.g. 8x8 images); only for
   // plain outputs (no ReLU / mask), each split adds its partial result atomically
-  const int slots = variant == 3 ? 512 : 768;
+  static const int slots_env = [] {
+    const char* e = std::getenv("MXDDP_WINO_SLOTS");
+    return e ? std::atoi(e) : -1;
+  }();
+  // Measured (scripts/bench_conv.py): splitting the input channels over blocks with atomic
+  // accumulation LOSES on every PyramidNet shape (8x8: 63 -> 45 us without it), the atomics
+  // and the output memset cost more than the extra blocks gain.  Off unless MXDDP_WINO_SLOTS.
+  const int slots = slots_env >= 0 ? slots_env : 0;
   int splits = 1;
   const int base = a.tblocks * a.ktiles;
   if (!relu && !mask && base < slots) splits = std::max(1, std::min(cdiv(slots, base), nch / 4));
