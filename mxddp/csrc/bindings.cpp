@@ -30,12 +30,18 @@ PYBIND11_MODULE(_C, m) {
   // ---------------------------------------------------------------- GEMM-shaped ops
   m.def("conv2d_fwd", [](uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y, int N, int C, int H, int W, int K, int R,
                          int S_, int sh, int sw, int ph, int pw, int dh, int dw, bool relu, uintptr_t st,
-                         uintptr_t scratch) {
+                         uintptr_t scratch, uintptr_t dgrad_filters) {
     conv2d_fwd(P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y),
-               CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw), relu, S(st), P<float>(scratch));
+               CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw), relu, S(st), P<float>(scratch),
+               P<float>(dgrad_filters));
   }, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("y"), py::arg("N"), py::arg("C"), py::arg("H"), py::arg("W"),
      py::arg("K"), py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
-     py::arg("dh"), py::arg("dw"), py::arg("relu"), py::arg("st"), py::arg("scratch") = 0);
+     py::arg("dh"), py::arg("dw"), py::arg("relu"), py::arg("st"), py::arg("scratch") = 0,
+     py::arg("dgrad_filters") = 0);
+  m.def("conv_dgrad_filter_floats", [](int N, int C, int H, int W, int K, int R, int S_, int sh, int sw, int ph,
+                                       int pw, int dh, int dw) {
+    return conv_dgrad_filter_floats(CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw));
+  });
   m.def("conv_scratch_floats", [](int N, int C, int H, int W, int K, int R, int S_, int sh, int sw, int ph, int pw,
                                   int dh, int dw) {
     return conv_scratch_floats(CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw));
@@ -44,12 +50,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_algo", &conv_algo);
   m.def("conv2d_dgrad", [](uintptr_t dy, uintptr_t w, uintptr_t dx, int N, int C, int H, int W, int K, int R, int S_,
                            int sh, int sw, int ph, int pw, int dh, int dw, uintptr_t mask, bool acc, uintptr_t st,
-                           uintptr_t wt_scratch) {
+                           uintptr_t wt_scratch, bool pretransformed) {
     conv2d_dgrad(P<const float>(dy), P<const float>(w), P<float>(dx), CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw),
-                 P<const float>(mask), acc, S(st), P<float>(wt_scratch));
+                 P<const float>(mask), acc, S(st), P<float>(wt_scratch), pretransformed);
   }, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("N"), py::arg("C"), py::arg("H"), py::arg("W"), py::arg("K"),
      py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"),
-     py::arg("dw"), py::arg("mask"), py::arg("acc"), py::arg("st"), py::arg("wt_scratch") = 0);
+     py::arg("dw"), py::arg("mask"), py::arg("acc"), py::arg("st"), py::arg("wt_scratch") = 0,
+     py::arg("pretransformed") = false);
   m.def("conv2d_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw_, int N, int C, int H, int W, int K, int R, int S_,
                            int sh, int sw, int ph, int pw, int dh, int dw, bool acc, uintptr_t st,
                            uintptr_t scratch) {

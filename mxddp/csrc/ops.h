@@ -23,12 +23,17 @@ struct ConvShape {
 };
 
 // ---- GEMM-shaped (ops_gemm.hip) ----
+// dgrad_filters (optional, conv_dgrad_filter_floats(s) floats; 0 = not applicable): the forward
+// also prepares the filters the Winograd data gradient will use (pass them to conv2d_dgrad with
+// pretransformed = true)
 void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s,
-                bool relu, hipStream_t st, float* scratch = nullptr);
+                bool relu, hipStream_t st, float* scratch = nullptr, float* dgrad_filters = nullptr);
+size_t conv_dgrad_filter_floats(const ConvShape& s);
 // dx = conv_transpose(dy, w) [* (mask > 0)], stored (=) or accumulated (+=).  `wt_scratch`
 // (conv_scratch_floats(s) floats, optional) enables the Winograd / direct 3x3 paths.
 void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s,
-                  const float* relu_mask, bool accumulate, hipStream_t st, float* wt_scratch = nullptr);
+                  const float* relu_mask, bool accumulate, hipStream_t st, float* wt_scratch = nullptr,
+                  bool pretransformed = false);
 // Direct-LDS 3x3 stride-1 pad-1 convolution (conv3x3.hip), fp32 MFMA; W <= 64.
 bool conv3x3_eligible(const ConvShape& s);
 void conv3x3_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s, bool relu,
@@ -41,10 +46,13 @@ void conv3x3_wgrad(const float* dy, const float* x, float* dw, const ConvShape& 
 // `scratch` holds the transformed filters: wino_scratch_floats(s) floats.
 bool wino_eligible(const ConvShape& s);
 size_t wino_scratch_floats(const ConvShape& s);
+// U_dgrad_out (optional, wino_dgrad_filter_floats(s)): also write the data-gradient filters
 void wino_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s, bool relu,
-              float* scratch, hipStream_t st);
+              float* scratch, hipStream_t st, float* U_dgrad_out = nullptr);
+size_t wino_dgrad_filter_floats(const ConvShape& s);
+// pretransformed: `scratch` already holds the filters written by wino_fwd(..., U_dgrad_out)
 void wino_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s, const float* relu_mask,
-                bool accumulate, float* scratch, hipStream_t st);
+                bool accumulate, float* scratch, hipStream_t st, bool pretransformed = false);
 // partial-sum scratch: wino_wgrad_scratch_floats(s) floats (0 = none needed)
 size_t wino_wgrad_scratch_floats(const ConvShape& s);
 void wino_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate, float* scratch,

@@ -264,6 +264,128 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_apply_k(const float* __restrict_
   }
 }
 
+// Channel-slice elementwise passes: grid (S, C) exactly like the reductions, so every block
+// works on one channel and derives that channel's coefficients ONCE (uniform scalars) instead
+// of per element (the flat grid-stride versions above recompute mean / invstd and a 64-bit
+// channel index for every element).
+template <bool VEC>
+__global__ __launch_bounds__(kBnTB) void bn_apply_slice_k(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, const float* __restrict__ acc,
+                                                          float* __restrict__ acc_next, float* __restrict__ mean_out,
+                                                          float* __restrict__ invstd_out, float* __restrict__ run_mean,
+                                                          float* __restrict__ run_var, float* __restrict__ y, int N,
+                                                          int C, int HW, int S, FastDiv dv, float cnt, float eps,
+                                                          float momentum, int relu, int hiwater,
+                                                          int64_t* __restrict__ num_batches) {
+  const int s = blockIdx.x, c = blockIdx.y;
+  if (s == 0 && c == 0) {
+    for (int k = 2 * C + threadIdx.x; k < 2 * hiwater; k += kBnTB) acc_next[k] = 0.f;
+    if (num_batches && threadIdx.x == 0) *num_batches += 1;
+  }
+  const FwdStat st = fwd_stat(x, acc, c, HW, cnt, eps);
+  const float sc = st.inv * (gamma ? gamma[c] : 1.f);
+  const float sh = (beta ? beta[c] : 0.f) - st.mean * sc;
+  if (s == 0 && threadIdx.x == 0) {
+    mean_out[c] = st.mean;
+    invstd_out[c] = st.inv;
+    if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * st.mean;
+    if (run_var) {
+      const float m1 = acc[2 * c] / cnt;
+      const float var = fmaxf(acc[2 * c + 1] / cnt - m1 * m1, 0.f);
+      run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
+    }
+  }
+  // every block of channel c has read acc[2c] (above) before block 0 of the NEXT call zeroes it
+  // (stream order); acc_next is only zeroed here, never read
+  if (s == 0 && threadIdx.x == 0) {
+    acc_next[2 * c] = 0.f;
+    acc_next[2 * c + 1] = 0.f;
+  }
+  const Slice sl = slice_of(s, S, N);
+  if (VEC) {
+    const int hw4 = HW >> 2;
+    const int total = (sl.n1 - sl.n0) * hw4;
+    for (int i = threadIdx.x; i < total; i += kBnTB) {
+      const int n = sl.n0 + (int)dv.div(i), j = i - (n - sl.n0) * hw4;
+      const size_t o = ((size_t)n * C + c) * hw4 + j;
+      float4 v = reinterpret_cast<const float4*>(x)[o];
+      v.x = fmaf(v.x, sc, sh);
+      v.y = fmaf(v.y, sc, sh);
+      v.z = fmaf(v.z, sc, sh);
+      v.w = fmaf(v.w, sc, sh);
+      if (relu) {
+        v.x = fmaxf(v.x, 0.f);
+        v.y = fmaxf(v.y, 0.f);
+        v.z = fmaxf(v.z, 0.f);
+        v.w = fmaxf(v.w, 0.f);
+      }
+      reinterpret_cast<float4*>(y)[o] = v;
+    }
+  } else {
+    const int total = (sl.n1 - sl.n0) * HW;
+    for (int i = threadIdx.x; i < total; i += kBnTB) {
+      const int n = sl.n0 + (int)dv.div(i), j = i - (n - sl.n0) * HW;
+      const size_t o = ((size_t)n * C + c) * HW + j;
+      const float r = fmaf(x[o], sc, sh);
+      y[o] = relu ? fmaxf(r, 0.f) : r;
+    }
+  }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kBnTB) void bn_bwd_apply_slice_k(
+    const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ yr,
+    const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ acc, float* __restrict__ acc_next, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    float* __restrict__ dx, int N, int C, int HW, int S, FastDiv dv, float cnt, int acc_params, int hiwater) {
+  const int s = blockIdx.x, c = blockIdx.y;
+  if (s == 0 && c == 0)
+    for (int k = 2 * C + threadIdx.x; k < 2 * hiwater; k += kBnTB) acc_next[k] = 0.f;
+  const float inv = invstd[c], mu = mean[c];
+  const float db = acc[2 * c], dg = acc[2 * c + 1] * inv;
+  const float k = (gamma ? gamma[c] : 1.f) * inv / cnt;
+  const float A = k * cnt, D = -k * dg * inv, Bc = -k * db + k * dg * inv * mu;
+  if (s == 0 && threadIdx.x == 0) {
+    if (dgamma) dgamma[c] = acc_params ? dgamma[c] + dg : dg;
+    if (dbeta) dbeta[c] = acc_params ? dbeta[c] + db : db;
+    acc_next[2 * c] = 0.f;
+    acc_next[2 * c + 1] = 0.f;
+  }
+  const Slice sl = slice_of(s, S, N);
+  if (VEC) {
+    const int hw4 = HW >> 2;
+    const int total = (sl.n1 - sl.n0) * hw4;
+    for (int i = threadIdx.x; i < total; i += kBnTB) {
+      const int n = sl.n0 + (int)dv.div(i), j = i - (n - sl.n0) * hw4;
+      const size_t o = ((size_t)n * C + c) * hw4 + j;
+      float4 g = reinterpret_cast<const float4*>(dy)[o];
+      const float4 v = reinterpret_cast<const float4*>(x)[o];
+      if (yr) {
+        const float4 r = reinterpret_cast<const float4*>(yr)[o];
+        g.x = r.x > 0.f ? g.x : 0.f;
+        g.y = r.y > 0.f ? g.y : 0.f;
+        g.z = r.z > 0.f ? g.z : 0.f;
+        g.w = r.w > 0.f ? g.w : 0.f;
+      }
+      float4 out;
+      out.x = fmaf(A, g.x, fmaf(D, v.x, Bc));
+      out.y = fmaf(A, g.y, fmaf(D, v.y, Bc));
+      out.z = fmaf(A, g.z, fmaf(D, v.z, Bc));
+      out.w = fmaf(A, g.w, fmaf(D, v.w, Bc));
+      reinterpret_cast<float4*>(dx)[o] = out;
+    }
+  } else {
+    const int total = (sl.n1 - sl.n0) * HW;
+    for (int i = threadIdx.x; i < total; i += kBnTB) {
+      const int n = sl.n0 + (int)dv.div(i), j = i - (n - sl.n0) * HW;
+      const size_t o = ((size_t)n * C + c) * HW + j;
+      float g = dy[o];
+      if (yr && !(yr[o] > 0.f)) g = 0.f;
+      dx[o] = fmaf(A, g, fmaf(D, x[o], Bc));
+    }
+  }
+}
+
 int apply_grid(int64_t n) {
   const int64_t g = (n + kBnTB - 1) / kBnTB;
   return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
@@ -293,12 +415,12 @@ void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* 
   const float cnt = (float)N * (float)HW;
   if (vec) {
     MX_LAUNCH(bn_stats_k<true>, dim3(S, C), dim3(kBnTB), 0, st, x, N, C, HW, S, dv, acc);
-    MX_LAUNCH(bn_apply_k<true>, dim3(apply_grid(total / 4)), dim3(kBnTB), 0, st, x, gamma, beta, acc, acc_next, mean,
-              invstd, run_mean, run_var, y, C, HW, dv, dc, total, cnt, eps, momentum, relu ? 1 : 0, hiwater, num_batches);
+    MX_LAUNCH(bn_apply_slice_k<true>, dim3(S, C), dim3(kBnTB), 0, st, x, gamma, beta, acc, acc_next, mean, invstd,
+              run_mean, run_var, y, N, C, HW, S, dv, cnt, eps, momentum, relu ? 1 : 0, hiwater, num_batches);
   } else {
     MX_LAUNCH(bn_stats_k<false>, dim3(S, C), dim3(kBnTB), 0, st, x, N, C, HW, S, dv, acc);
-    MX_LAUNCH(bn_apply_k<false>, dim3(apply_grid(total)), dim3(kBnTB), 0, st, x, gamma, beta, acc, acc_next, mean,
-              invstd, run_mean, run_var, y, C, HW, dv, dc, total, cnt, eps, momentum, relu ? 1 : 0, hiwater, num_batches);
+    MX_LAUNCH(bn_apply_slice_k<false>, dim3(S, C), dim3(kBnTB), 0, st, x, gamma, beta, acc, acc_next, mean, invstd,
+              run_mean, run_var, y, N, C, HW, S, dv, cnt, eps, momentum, relu ? 1 : 0, hiwater, num_batches);
   }
 }
 
@@ -313,12 +435,12 @@ void bn_bwd(const float* dy, const float* x, const float* y_relu, const float* g
   const float cnt = (float)N * (float)HW;
   if (vec) {
     MX_LAUNCH(bn_bwd_reduce_k<true>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, mean, N, C, HW, S, dv, acc);
-    MX_LAUNCH(bn_bwd_apply_k<true>, dim3(apply_grid(total / 4)), dim3(kBnTB), 0, st, dy, x, y_relu, gamma, mean,
-              invstd, acc, acc_next, dgamma, dbeta, dx, C, HW, dv, dc, total, cnt, accp ? 1 : 0, hiwater);
+    MX_LAUNCH(bn_bwd_apply_slice_k<true>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, gamma, mean, invstd, acc,
+              acc_next, dgamma, dbeta, dx, N, C, HW, S, dv, cnt, accp ? 1 : 0, hiwater);
   } else {
     MX_LAUNCH(bn_bwd_reduce_k<false>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, mean, N, C, HW, S, dv, acc);
-    MX_LAUNCH(bn_bwd_apply_k<false>, dim3(apply_grid(total)), dim3(kBnTB), 0, st, dy, x, y_relu, gamma, mean, invstd,
-              acc, acc_next, dgamma, dbeta, dx, C, HW, dv, dc, total, cnt, accp ? 1 : 0, hiwater);
+    MX_LAUNCH(bn_bwd_apply_slice_k<false>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, gamma, mean, invstd, acc,
+              acc_next, dgamma, dbeta, dx, N, C, HW, S, dv, cnt, accp ? 1 : 0, hiwater);
   }
 }
 

@@ -337,17 +337,49 @@ __global__ void flip_transpose_any_k(const float* __restrict__ w, float* __restr
   }
 }
 
+// dgrad of a 3x3 / stride-2 / pad-1 conv = the stride-1 transposed conv of dy zero-inserted to
+// the input resolution (u[2p][2q] = dy[p][q], zeros elsewhere):
+//   dx[h] = sum_r dy[(h + 1 - r) / 2] w[r] = sum_r' u[h - 1 + r'] w[2 - r'],
+// i.e. exactly the stride-1 Winograd data gradient of shape (N, C, H, W, K) run on u.  4x the
+// ideal MFMA work, but through the 2.25x-cheaper Winograd kernel instead of the generic dgrad
+// gather that multiplies 3 of every 4 taps by zero anyway.
+ConvShape s2_as_s1(const ConvShape& s) { return ConvShape::make(s.N, s.C, s.H, s.W, s.K, 3, 3, 1, 1, 1, 1); }
+
+bool wino_s2_dgrad(const ConvShape& s) {
+  return g_gemm_precision == 0 && g_conv_algo == 0 && s.R == 3 && s.S == 3 && s.str_h == 2 && s.str_w == 2 &&
+         s.pad_h == 1 && s.pad_w == 1 && s.dil_h == 1 && s.dil_w == 1 && s.H == s.W && s.H % 2 == 0 &&
+         s.P * 2 == s.H && s.Q * 2 == s.W && wino_eligible(s2_as_s1(s));
+}
+
+__global__ void zero_insert2_k(const float* __restrict__ dy, float* __restrict__ u, int64_t planes, int P, int Q) {
+  const int H = 2 * P, W = 2 * Q;
+  const int64_t total = planes * H * W;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int w = (int)(i % W);
+    const int64_t r = i / W;
+    const int h = (int)(r % H);
+    const int64_t pl = r / H;
+    u[i] = ((h | w) & 1) ? 0.f : dy[(pl * P + (h >> 1)) * Q + (w >> 1)];
+  }
+}
+
 size_t conv_scratch_floats(const ConvShape& s) {
   size_t n = dgrad_as_fwd(s) ? (size_t)s.K * s.C * s.R * s.S : 0;
+  if (wino_s2_dgrad(s)) {
+    const ConvShape t = s2_as_s1(s);
+    n = std::max(n, wino_scratch_floats(t) + (size_t)s.N * s.K * s.H * s.W);
+  }
   if (g_gemm_precision != 0) return n;
   if (wino_eligible(s)) n = std::max(n, wino_scratch_floats(s));
   if (conv3x3_eligible(s)) n = std::max(n, (size_t)s.K * s.C * 9);
   return n;
 }
 
+size_t conv_dgrad_filter_floats(const ConvShape& s) { return use_wino(s) ? wino_dgrad_filter_floats(s) : 0; }
+
 void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s,
-                bool relu, hipStream_t st, float* scratch) {
-  if (scratch && use_wino(s)) return wino_fwd(x, w, bias, y, s, relu, scratch, st);
+                bool relu, hipStream_t st, float* scratch, float* dgrad_filters) {
+  if (scratch && use_wino(s)) return wino_fwd(x, w, bias, y, s, relu, scratch, st, dgrad_filters);
   if (g_gemm_precision == 0 && conv3x3_eligible(s)) return conv3x3_fwd(x, w, bias, y, s, relu, st);
   if (is_1x1_s1(s)) {
     Conv1x1FwdOp op{s.N * s.H * s.W, s.K, s.C, s.H * s.W, FastDiv(s.H * s.W), x, w, bias, y, relu};
@@ -358,10 +390,19 @@ void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, con
 }
 
 void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s,
-                  const float* relu_mask, bool accumulate, hipStream_t st, float* wt_scratch) {
-  if (wt_scratch && use_wino(s)) return wino_dgrad(dy, w, dx, s, relu_mask, accumulate, wt_scratch, st);
+                  const float* relu_mask, bool accumulate, hipStream_t st, float* wt_scratch, bool pretransformed) {
+  if (wt_scratch && use_wino(s))
+    return wino_dgrad(dy, w, dx, s, relu_mask, accumulate, wt_scratch, st, pretransformed);
   if (wt_scratch && g_gemm_precision == 0 && conv3x3_eligible(s))
     return conv3x3_dgrad(dy, w, dx, s, relu_mask, accumulate, wt_scratch, st);
+  if (wt_scratch && wino_s2_dgrad(s)) {
+    const ConvShape t = s2_as_s1(s);
+    float* u = wt_scratch + wino_scratch_floats(t);
+    const int64_t total = (int64_t)s.N * s.K * s.H * s.W;
+    MX_LAUNCH(zero_insert2_k, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 4096)), dim3(256), 0, st, dy, u,
+              (int64_t)s.N * s.K, s.P, s.Q);
+    return wino_dgrad(u, w, dx, t, relu_mask, accumulate, wt_scratch, st);
+  }
   if (wt_scratch && !relu_mask && !accumulate && dgrad_as_fwd(s)) {
     const int64_t total = (int64_t)s.K * s.C * s.R * s.S;
     MX_LAUNCH(flip_transpose_any_k, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 2048)), dim3(256), 0, st, w,

@@ -122,6 +122,33 @@ __global__ void wino_wtrans_k(const float* __restrict__ w, float* __restrict__ U
   }
 }
 
+// Both layouts in one launch (forward U and the data-gradient U of the backward pass): the
+// forward call precomputes what the backward will need, saving one launch per conv per step.
+__global__ void wino_wtrans2_k(const float* __restrict__ w, float* __restrict__ Uf, float* __restrict__ Ud, int K,
+                               int C, int Cipf, int Copf, int Cipd, int Copd) {
+  const int tf = Cipf * Copf, td = Cipd * Copd;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < tf + td; i += gridDim.x * 256) {
+    const bool dg = i >= tf;
+    const int j = dg ? i - tf : i, Cop = dg ? Copd : Copf;
+    const size_t plane = dg ? (size_t)td : (size_t)tf;
+    float* U = dg ? Ud : Uf;
+    const int ci = j / Cop, co = j - ci * Cop;
+    const int k = dg ? ci : co, c = dg ? co : ci;
+    float g[9], u[16];
+    if (k < K && c < C) {
+      const float* src = w + ((size_t)k * C + c) * 9;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) g[t] = dg ? src[8 - t] : src[t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) g[t] = 0.f;
+    }
+    filter_transform(g, u);
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) U[xi * plane + j] = u[xi];
+  }
+}
+
 // One chunk (8 reduction rows) of the 16 Winograd-domain GEMMs: 32 MFMAs, each fed by one A and
 // one B operand read from LDS.  The schedule is pinned to a software pipeline (8 operand reads
 // ahead, then {1 MFMA, 2 reads}): left alone the scheduler hoists all 64 reads above the first
@@ -646,9 +673,14 @@ int pad_to(int v, int m) { return (v + m - 1) / m * m; }
 
 void launch_fwd(const float* x, const float* w, const float* bias, const float* mask, float* y, int N, int Ci,
                 int Co, int Wd, bool relu, bool accumulate, bool dgrad, float* U, int K_w, int C_w,
-                hipStream_t st) {
+                hipStream_t st, float* U_dgrad_out = nullptr, bool pretransformed = false) {
   const int Cip = pad_to(Ci, kCC), Cop = pad_to(Co, 32);
-  {
+  if (U_dgrad_out) {  // forward call that also prepares the backward's filters (one launch)
+    const int Cipd = pad_to(K_w, kCC), Copd = pad_to(C_w, 32);
+    const int total = Cip * Cop + Cipd * Copd;
+    MX_LAUNCH(wino_wtrans2_k, dim3(std::min(cdiv(total, 256), 2048)), dim3(256), 0, st, w, U, U_dgrad_out, K_w, C_w,
+              Cip, Cop, Cipd, Copd);
+  } else if (!pretransformed) {
     const int total = Cip * Cop;
     MX_LAUNCH(wino_wtrans_k, dim3(std::min(cdiv(total, 256), 2048)), dim3(256), 0, st, w, U, K_w, C_w, Cip, Cop,
               dgrad ? 1 : 0);
@@ -770,13 +802,16 @@ size_t wino_wgrad_scratch_floats(const ConvShape& s) {
 }
 
 void wino_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s, bool relu,
-              float* scratch, hipStream_t st) {
-  launch_fwd(x, w, bias, nullptr, y, s.N, s.C, s.K, s.W, relu, false, false, scratch, s.K, s.C, st);
+              float* scratch, hipStream_t st, float* U_dgrad_out) {
+  launch_fwd(x, w, bias, nullptr, y, s.N, s.C, s.K, s.W, relu, false, false, scratch, s.K, s.C, st, U_dgrad_out);
 }
 
+size_t wino_dgrad_filter_floats(const ConvShape& s) { return 16 * (size_t)pad_to(s.K, kCC) * pad_to(s.C, 32); }
+
 void wino_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s, const float* relu_mask,
-                bool accumulate, float* scratch, hipStream_t st) {
-  launch_fwd(dy, w, nullptr, relu_mask, dx, s.N, s.K, s.C, s.W, false, accumulate, true, scratch, s.K, s.C, st);
+                bool accumulate, float* scratch, hipStream_t st, bool pretransformed) {
+  launch_fwd(dy, w, nullptr, relu_mask, dx, s.N, s.K, s.C, s.W, false, accumulate, true, scratch, s.K, s.C, st,
+             nullptr, pretransformed);
 }
 
 void wino_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate, float* scratch,

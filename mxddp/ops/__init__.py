@@ -105,8 +105,13 @@ class _Conv2d(torch.autograd.Function):
         st = stream_of(x)
         ns = C.conv_scratch_floats(N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw)
         scr = torch.empty((ns,), device=x.device, dtype=x.dtype) if ns else None
+        # Winograd layers: the forward's filter-transform launch also writes the backward's
+        # data-gradient filters (one launch per conv per step instead of two)
+        nd = C.conv_dgrad_filter_floats(N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw) if ctx.needs_input_grad[0] else 0
+        wd = torch.empty((nd,), device=x.device, dtype=x.dtype) if nd else None
         C.conv2d_fwd(x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph, pw,
-                     dh, dw, bool(relu), st, _p(scr))
+                     dh, dw, bool(relu), st, _p(scr), _p(wd))
+        ctx.dgrad_filters = wd
         ctx.geom = (N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw, P, Q)
         ctx.relu = relu
         ctx.has_bias = b is not None
@@ -129,10 +134,12 @@ class _Conv2d(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             # scratch for the 3x3 paths' transformed / flipped filters (none needed otherwise)
-            ns = C.conv_scratch_floats(N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw)
-            wt = torch.empty((ns,), device=dy.device, dtype=dy.dtype) if ns else None
+            wt, pre = ctx.dgrad_filters, True
+            if wt is None:
+                ns = C.conv_scratch_floats(N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw)
+                wt, pre = (torch.empty((ns,), device=dy.device, dtype=dy.dtype) if ns else None), False
             C.conv2d_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph, pw,
-                           dh, dw, 0, False, st, 0 if wt is None else wt.data_ptr())
+                           dh, dw, 0, False, st, 0 if wt is None else wt.data_ptr(), pre)
         b = ctx.bias_ref
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(w)

@@ -16,7 +16,8 @@ CONV_CASES = [
     (4, 1, 28, 28, 32, 3, 3, 1, 0),      # mnist conv1
     (3, 32, 26, 26, 64, 3, 3, 1, 0),     # mnist conv2
     (2, 21, 16, 16, 26, 3, 3, 1, 1),     # pyramidnet-like odd channels
-    (2, 101, 32, 32, 106, 3, 3, 2, 1),   # pyramidnet stride-2 entry
+    (2, 101, 32, 32, 106, 3, 3, 2, 1),   # pyramidnet stride-2 entry (dgrad: zero-insert + Winograd)
+    (3, 186, 16, 16, 191, 3, 3, 2, 1),   # pyramidnet stride-2 entry of stage 3
     (2, 3, 33, 31, 17, 7, 7, 2, 3),      # resnet stem-like, odd spatial
     (2, 64, 14, 14, 40, 1, 1, 1, 0),     # 1x1
     # direct-LDS 3x3 s1 p1 path (conv3x3.hip): every supported width, C not a multiple of 8,
