@@ -5,8 +5,9 @@
 // elements are split over S workgroups (grid = S x C, S chosen so the grid has >= ~2048
 // workgroups), each reducing its slice with float4 loads and adding its two partial sums into
 // per-channel accumulators with device-scope float atomics (2 atomics per workgroup).  The
-// second, elementwise launch derives the per-channel statistics from the accumulators on the
-// fly and applies the affine map (forward) or the dx formula (backward).
+// second, elementwise launch uses the same S x C grid: each block derives its channel's
+// statistics from the accumulators once and applies the affine map (forward) or the dx
+// formula (backward) to its slice.
 //
 // No inter-workgroup fences: a last-arriver scheme needs a device-scope release per workgroup,
 // which on a multi-XCD part writes back the XCD's L2 and cost 2-3x the whole reduction.  The
@@ -105,64 +106,6 @@ __device__ __forceinline__ FwdStat fwd_stat(const float* __restrict__ x, const f
   return FwdStat{K + m1, rsqrtf(var + eps)};
 }
 
-// y = (x - mean) * invstd * gamma + beta (+ ReLU).  The thread owning the first float4 (or
-// element) of channel c in image 0 also publishes mean/invstd, updates the running stats and
-// zeroes channel c of the next call's accumulator.
-template <bool VEC>
-__global__ __launch_bounds__(kBnTB) void bn_apply_k(const float* __restrict__ x, const float* __restrict__ gamma,
-                                                    const float* __restrict__ beta, const float* __restrict__ acc,
-                                                    float* __restrict__ acc_next, float* __restrict__ mean_out,
-                                                    float* __restrict__ invstd_out, float* __restrict__ run_mean,
-                                                    float* __restrict__ run_var, float* __restrict__ y, int C, int HW,
-                                                    FastDiv dhw, FastDiv dc, int64_t total, float cnt, float eps,
-                                                    float momentum, int relu, int hiwater,
-                                                    int64_t* __restrict__ num_batches) {
-  const int64_t step = (int64_t)gridDim.x * kBnTB;
-  if (blockIdx.x == 0) {  // channels >= C that an earlier, wider call left dirty in acc_next
-    for (int k = 2 * C + threadIdx.x; k < 2 * hiwater; k += kBnTB) acc_next[k] = 0.f;
-    // BatchNorm2d.num_batches_tracked += 1, here instead of a separate launch per layer
-    if (num_batches && threadIdx.x == 0) *num_batches += 1;
-  }
-  const int vw = VEC ? 4 : 1;
-  const int plane = HW / vw;  // vector elements per (n, c) plane
-  for (int64_t i = blockIdx.x * (int64_t)kBnTB + threadIdx.x; i < total / vw; i += step) {
-    const uint32_t nc = dhw.div((uint32_t)i);
-    const int c = (int)(nc - dc.div(nc) * C);
-    const FwdStat st = fwd_stat(x, acc, c, HW, cnt, eps);
-    const float sc = st.inv * (gamma ? gamma[c] : 1.f);
-    const float sh = (beta ? beta[c] : 0.f) - st.mean * sc;
-    if (i < (int64_t)plane * C && i - (int64_t)c * plane == 0) {  // image 0, first element of c
-      mean_out[c] = st.mean;
-      invstd_out[c] = st.inv;
-      if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * st.mean;
-      if (run_var) {
-        const float m1 = acc[2 * c] / cnt;
-        const float var = fmaxf(acc[2 * c + 1] / cnt - m1 * m1, 0.f);
-        run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
-      }
-      acc_next[2 * c] = 0.f;
-      acc_next[2 * c + 1] = 0.f;
-    }
-    if (VEC) {
-      float4 v = reinterpret_cast<const float4*>(x)[i];
-      v.x = fmaf(v.x, sc, sh);
-      v.y = fmaf(v.y, sc, sh);
-      v.z = fmaf(v.z, sc, sh);
-      v.w = fmaf(v.w, sc, sh);
-      if (relu) {
-        v.x = fmaxf(v.x, 0.f);
-        v.y = fmaxf(v.y, 0.f);
-        v.z = fmaxf(v.z, 0.f);
-        v.w = fmaxf(v.w, 0.f);
-      }
-      reinterpret_cast<float4*>(y)[i] = v;
-    } else {
-      const float r = fmaf(x[i], sc, sh);
-      y[i] = relu ? fmaxf(r, 0.f) : r;
-    }
-  }
-}
-
 // ------------------------------------------------------------------ backward
 // partial sums of g and g * (x - mean), g = dy masked by the fused ReLU (y_relu > 0).
 template <bool VEC>
@@ -211,63 +154,12 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_reduce_k(const float* __restrict
   }
 }
 
-// dx = k * (cnt*g - db - xhat*dg), xhat = (x - mean) * invstd, k = gamma * invstd / cnt,
-// db = sum(g), dg = sum(g * xhat).  The owner thread of channel c (image 0, first element)
-// writes dgamma / dbeta and zeroes the next call's accumulator.
-template <bool VEC>
-__global__ __launch_bounds__(kBnTB) void bn_bwd_apply_k(const float* __restrict__ dy, const float* __restrict__ x,
-                                                        const float* __restrict__ yr, const float* __restrict__ gamma,
-                                                        const float* __restrict__ mean, const float* __restrict__ invstd,
-                                                        const float* __restrict__ acc, float* __restrict__ acc_next,
-                                                        float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                        float* __restrict__ dx, int C, int HW, FastDiv dhw, FastDiv dc,
-                                                        int64_t total, float cnt, int acc_params, int hiwater) {
-  const int64_t step = (int64_t)gridDim.x * kBnTB;
-  if (blockIdx.x == 0)
-    for (int k = 2 * C + threadIdx.x; k < 2 * hiwater; k += kBnTB) acc_next[k] = 0.f;
-  const int vw = VEC ? 4 : 1;
-  const int plane = HW / vw;
-  for (int64_t i = blockIdx.x * (int64_t)kBnTB + threadIdx.x; i < total / vw; i += step) {
-    const uint32_t nc = dhw.div((uint32_t)i);
-    const int c = (int)(nc - dc.div(nc) * C);
-    const float inv = invstd[c], mu = mean[c];
-    const float db = acc[2 * c], dg = acc[2 * c + 1] * inv;
-    const float k = (gamma ? gamma[c] : 1.f) * inv / cnt;
-    const float A = k * cnt, D = -k * dg * inv, Bc = -k * db + k * dg * inv * mu;
-    if (i < (int64_t)plane * C && i - (int64_t)c * plane == 0) {
-      if (dgamma) dgamma[c] = acc_params ? dgamma[c] + dg : dg;
-      if (dbeta) dbeta[c] = acc_params ? dbeta[c] + db : db;
-      acc_next[2 * c] = 0.f;
-      acc_next[2 * c + 1] = 0.f;
-    }
-    if (VEC) {
-      float4 g = reinterpret_cast<const float4*>(dy)[i];
-      const float4 v = reinterpret_cast<const float4*>(x)[i];
-      if (yr) {
-        const float4 r = reinterpret_cast<const float4*>(yr)[i];
-        g.x = r.x > 0.f ? g.x : 0.f;
-        g.y = r.y > 0.f ? g.y : 0.f;
-        g.z = r.z > 0.f ? g.z : 0.f;
-        g.w = r.w > 0.f ? g.w : 0.f;
-      }
-      float4 o;
-      o.x = fmaf(A, g.x, fmaf(D, v.x, Bc));
-      o.y = fmaf(A, g.y, fmaf(D, v.y, Bc));
-      o.z = fmaf(A, g.z, fmaf(D, v.z, Bc));
-      o.w = fmaf(A, g.w, fmaf(D, v.w, Bc));
-      reinterpret_cast<float4*>(dx)[i] = o;
-    } else {
-      float g = dy[i];
-      if (yr && !(yr[i] > 0.f)) g = 0.f;
-      dx[i] = fmaf(A, g, fmaf(D, x[i], Bc));
-    }
-  }
-}
-
-// Channel-slice elementwise passes: grid (S, C) exactly like the reductions, so every block
-// works on one channel and derives that channel's coefficients ONCE (uniform scalars) instead
-// of per element (the flat grid-stride versions above recompute mean / invstd and a 64-bit
-// channel index for every element).
+// Elementwise passes: grid (S, C) exactly like the reductions, so every block works on one
+// channel slice and derives that channel's coefficients ONCE (uniform scalars); a flat
+// grid-stride version that recomputed mean / invstd and the channel index per element was
+// measured slower.  dx = k * (cnt*g - db - xhat*dg), xhat = (x - mean) * invstd,
+// k = gamma * invstd / cnt, db = sum(g), dg = sum(g * xhat).  Block (0, c) publishes the
+// channel's statistics / dgamma / dbeta and zeroes channel c of the next call's accumulator.
 template <bool VEC>
 __global__ __launch_bounds__(kBnTB) void bn_apply_slice_k(const float* __restrict__ x, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, const float* __restrict__ acc,
@@ -386,10 +278,6 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_apply_slice_k(
   }
 }
 
-int apply_grid(int64_t n) {
-  const int64_t g = (n + kBnTB - 1) / kBnTB;
-  return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
-}
 
 }  // namespace
 

@@ -741,19 +741,7 @@ void launch_fwd(const float* x, const float* w, const float* bias, const float* 
     }
     return;
   }
-  static const int occ = [] {
-    const char* e = std::getenv("MXDDP_WINO_OCC");
-    return e ? std::atoi(e) : 2;
-  }();
-  if (occ == 3) {
-    switch (Wd) {
-      case 8: MX_LAUNCH((wino_fwd_kernel<8, 3>), grid, dim3(256), kLds, st, a); break;
-      case 16: MX_LAUNCH((wino_fwd_kernel<16, 3>), grid, dim3(256), kLds, st, a); break;
-      case 32: MX_LAUNCH((wino_fwd_kernel<32, 3>), grid, dim3(256), kLds, st, a); break;
-      default: MX_CHECK(false, "winograd: unsupported width");
-    }
-    return;
-  }
+  // 2 waves / SIMD: at 3 the 16 accumulators + prefetch registers spill (measured slower)
   switch (Wd) {
     case 8: MX_LAUNCH((wino_fwd_kernel<8, 2>), grid, dim3(256), kLds, st, a); break;
     case 16: MX_LAUNCH((wino_fwd_kernel<16, 2>), grid, dim3(256), kLds, st, a); break;
