@@ -73,8 +73,12 @@ struct ConvNArgs {
   FastDiv fOW, fOHW, fCa, fS;
 };
 
-template <int TM, int TN>
+template <int TM, int TN, bool kWide>
 __global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
+  // kWide (Ca % 64 == 0, every ResNet layer but the 8-channel stem): the 64 k of a stage lie in
+  // ONE filter tap (r, s), so the tap decomposition is a per-stage scalar and each 16-byte
+  // operand load is a per-lane base plus a uniform offset (a few VALU per load instead of two
+  // divisions and a 64-bit address per load).
   // BK = 64 (two MFMA k-steps per stage) keeps each stage's MFMA phase long enough to cover the
   // next stage's global loads; LDS rows of 72 bf16 = 144 B = 9 x 16 B (odd) -> the 16 rows read
   // by a 16-lane group hit 16 distinct 16-byte slots.
@@ -103,7 +107,47 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
   }
   u32x4 ra[EA], rb[EB];
   const u32x4 z4 = {0u, 0u, 0u, 0u};
+  // wide path: per-lane byte bases (loop invariant)
+  uint32_t abase[EA], pbase[EB];
+  int ihb[EB], iwb[EB];
+  if constexpr (kWide) {
+#pragma unroll
+    for (int i = 0; i < EA; ++i) abase[i] = 2u * ((uint32_t)(ch0 + row0 + 32 * i) * a.Kg + 8 * kv);
+#pragma unroll
+    for (int i = 0; i < EB; ++i) {
+      pbase[i] = 2u * ((uint32_t)pn[i] * a.IH * a.IW * a.Ca + 8 * kv);
+      ihb[i] = a.dgrad ? poh[i] + a.ph : poh[i] * a.sh - a.ph;
+      iwb[i] = a.dgrad ? pow_[i] + a.pw : pow_[i] * a.sw - a.pw;
+    }
+  }
   auto gload = [&](int k0) {
+    if constexpr (kWide) {
+      const int rs = (int)a.fCa.div((uint32_t)k0), c0 = k0 - rs * a.Ca;  // uniform
+      const int r = (int)a.fS.div((uint32_t)rs), s = rs - r * a.S;
+      const char* wb = reinterpret_cast<const char*>(a.wt) + 2u * (uint32_t)k0;
+#pragma unroll
+      for (int i = 0; i < EA; ++i)
+        ra[i] = (ch0 + row0 + 32 * i < a.Ng) ? *reinterpret_cast<const u32x4*>(wb + abase[i]) : z4;
+      const char* xb = reinterpret_cast<const char*>(a.act) + 2u * (uint32_t)c0;
+#pragma unroll
+      for (int i = 0; i < EB; ++i) {
+        int ih, iw;
+        bool ok = pok[i];
+        if (!a.dgrad) {
+          ih = ihb[i] + r;
+          iw = iwb[i] + s;
+        } else {
+          const int th = ihb[i] - r, tw = iwb[i] - s;
+          ih = a.sh == 1 ? th : th >> 1;
+          iw = a.sw == 1 ? tw : tw >> 1;
+          ok = ok && th >= 0 && tw >= 0 && ih * a.sh == th && iw * a.sw == tw;
+        }
+        ok = ok && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
+        const uint32_t off = pbase[i] + 2u * (uint32_t)((ih * a.IW + iw) * a.Ca);
+        rb[i] = ok ? *reinterpret_cast<const u32x4*>(xb + off) : z4;
+      }
+      return;
+    }
     const int k = k0 + 8 * kv;
     const bool kok = k < a.Kg;
     const int kk = kok ? k : 0;
@@ -771,12 +815,19 @@ static void launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   a.kt_per_split = p.kt_per_split;
   a.part = p.splits > 1 ? scratch : nullptr;
   const dim3 grid(p.blocks, p.splits);
+  // wide path: whole 64-k stages inside one tap, and every byte offset fits 32 bits
+  const bool wide = a.Ca % 64 == 0 && a.Kg % 64 == 0 &&
+                    (int64_t)a.IH * a.IW * a.Ca * (a.M / (a.OH * a.OW) + 1) < (1ll << 30) &&
+                    (int64_t)a.Ng * a.Kg < (1ll << 30);
   if (p.tm == 128) {
-    MX_LAUNCH((conv_nhwc_kernel<128, 128>), grid, dim3(256), 0, st, a);
+    if (wide) MX_LAUNCH((conv_nhwc_kernel<128, 128, true>), grid, dim3(256), 0, st, a);
+    else MX_LAUNCH((conv_nhwc_kernel<128, 128, false>), grid, dim3(256), 0, st, a);
   } else if (p.tn == 128) {
-    MX_LAUNCH((conv_nhwc_kernel<64, 128>), grid, dim3(256), 0, st, a);
+    if (wide) MX_LAUNCH((conv_nhwc_kernel<64, 128, true>), grid, dim3(256), 0, st, a);
+    else MX_LAUNCH((conv_nhwc_kernel<64, 128, false>), grid, dim3(256), 0, st, a);
   } else {
-    MX_LAUNCH((conv_nhwc_kernel<64, 64>), grid, dim3(256), 0, st, a);
+    if (wide) MX_LAUNCH((conv_nhwc_kernel<64, 64, true>), grid, dim3(256), 0, st, a);
+    else MX_LAUNCH((conv_nhwc_kernel<64, 64, false>), grid, dim3(256), 0, st, a);
   }
   if (p.splits > 1) {
     const int64_t n4 = (int64_t)a.M * a.Ng / 4;
