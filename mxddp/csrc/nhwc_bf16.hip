@@ -500,29 +500,49 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) K[e] = a.mean[8 * v + e];
   }
-  for (int p = blockIdx.x * ppi + pr; p < a.Npix; p += gridDim.x * ppi) {
-    float xv[8];
-    unpack8(*reinterpret_cast<const uint4*>(a.x + (size_t)p * a.C + 8 * v), xv);
-    if (!BWD) {
+  // UNR pixel rows per iteration with all their loads issued before any use: one 16-byte load
+  // in flight per thread cannot cover HBM latency with ~256 blocks
+  constexpr int UNR = BWD ? 2 : 4;
+  const int pstep = gridDim.x * ppi;
+  for (int p0 = blockIdx.x * ppi + pr; p0 < a.Npix; p0 += UNR * pstep) {
+    uint4 xr[UNR], gr[UNR], yr[UNR];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float d = xv[e] - K[e];
-        s1[e] += d;
-        s2[e] = fmaf(d, d, s2[e]);
+    for (int u = 0; u < UNR; ++u) {
+      const int p = p0 + u * pstep;
+      const bool ok = p < a.Npix;
+      const size_t o = (size_t)(ok ? p : 0) * a.C + 8 * v;
+      xr[u] = ok ? *reinterpret_cast<const uint4*>(a.x + o) : make_uint4(0u, 0u, 0u, 0u);
+      if (BWD) {
+        gr[u] = ok ? *reinterpret_cast<const uint4*>(a.dy + o) : make_uint4(0u, 0u, 0u, 0u);
+        if (a.relu) yr[u] = ok ? *reinterpret_cast<const uint4*>(a.y + o) : make_uint4(0u, 0u, 0u, 0u);
       }
-    } else {
-      float g[8];
-      unpack8(*reinterpret_cast<const uint4*>(a.dy + (size_t)p * a.C + 8 * v), g);
-      if (a.relu) {
-        float yv[8];
-        unpack8(*reinterpret_cast<const uint4*>(a.y + (size_t)p * a.C + 8 * v), yv);
+    }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) g[e] = yv[e] > 0.f ? g[e] : 0.f;
-      }
+    for (int u = 0; u < UNR; ++u) {
+      if (p0 + u * pstep >= a.Npix) break;
+      float xv[8];
+      unpack8(xr[u], xv);
+      if (!BWD) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        s1[e] += g[e];
-        s2[e] = fmaf(g[e], xv[e] - K[e], s2[e]);
+        for (int e = 0; e < 8; ++e) {
+          const float d = xv[e] - K[e];
+          s1[e] += d;
+          s2[e] = fmaf(d, d, s2[e]);
+        }
+      } else {
+        float g[8];
+        unpack8(gr[u], g);
+        if (a.relu) {
+          float yv[8];
+          unpack8(yr[u], yv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) g[e] = yv[e] > 0.f ? g[e] : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s1[e] += g[e];
+          s2[e] = fmaf(g[e], xv[e] - K[e], s2[e]);
+        }
       }
     }
   }
@@ -552,25 +572,26 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
 }
 
 template <bool BWD>
-__global__ __launch_bounds__(256) void bn_nhwc_finalize_k(BnNArgs a) {
-  // block = 32 channels x 8 row groups; each thread sums every 8th partial row (4 independent
-  // loads in flight), the 8 row-group sums are combined in a fixed order (deterministic)
-  __shared__ float red[2][8][32];
+__global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
+  // block = 32 channels x 32 row groups; each thread sums every 32nd partial row (4 independent
+  // loads in flight), the 32 row-group sums are combined in a fixed order (deterministic)
+  constexpr int RG = 32;
+  __shared__ float red[2][RG][32];
   const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5, c = blockIdx.x * 32 + cl;
   const size_t pitch = 2 * (size_t)a.C;
   float s1 = 0.f, s2 = 0.f;
   if (c < a.C) {
     float t1[4] = {0.f, 0.f, 0.f, 0.f}, t2[4] = {0.f, 0.f, 0.f, 0.f};
     int b = rg;
-    for (; b + 24 < a.gx; b += 32) {
+    for (; b + 3 * RG < a.gx; b += 4 * RG) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const float* p = a.part + (size_t)(b + 8 * u) * pitch + 2 * c;
+        const float* p = a.part + (size_t)(b + RG * u) * pitch + 2 * c;
         t1[u] += p[0];
         t2[u] += p[1];
       }
     }
-    for (; b < a.gx; b += 8) {
+    for (; b < a.gx; b += RG) {
       const float* p = a.part + (size_t)b * pitch + 2 * c;
       t1[0] += p[0];
       t2[0] += p[1];
@@ -585,7 +606,7 @@ __global__ __launch_bounds__(256) void bn_nhwc_finalize_k(BnNArgs a) {
   s1 = 0.f;
   s2 = 0.f;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
+  for (int k = 0; k < RG; ++k) {
     s1 += red[0][k][cl];
     s2 += red[1][k][cl];
   }
@@ -935,8 +956,8 @@ void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, in
 static dim3 bn_grid(int Npix, int C) {
   const int V = C / 8, vv = V >= kBnT ? kBnT : V, ppi = kBnT / vv;
   const int gy = V >= kBnT ? V / kBnT : 1;
-  // ~256 blocks in total, at least 8 pixel rows per thread
-  const int gx = std::max(1, std::min(cdiv(Npix, ppi * 8), std::max(1, 256 / gy)));
+  // ~1024 blocks in total (4 per CU), at least 8 pixel rows per thread
+  const int gx = std::max(1, std::min(cdiv(Npix, ppi * 8), std::max(1, 1024 / gy)));
   return dim3(gx, gy);
 }
 
@@ -972,7 +993,7 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
   a.momentum = momentum;
   a.eps = eps;
   MX_LAUNCH(bn_nhwc_partial_k<false>, g, dim3(kBnT), 0, st, a);
-  MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 32)), dim3(256), 0, st, a);
+  MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 32)), dim3(1024), 0, st, a);
   MX_LAUNCH(bn_nhwc_apply_k, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a);
 }
 
@@ -1002,7 +1023,7 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
   a.relu = relu;
   a.acc_params = accumulate_params;
   MX_LAUNCH(bn_nhwc_partial_k<true>, g, dim3(kBnT), 0, st, a);
-  MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 32)), dim3(256), 0, st, a);
+  MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 32)), dim3(1024), 0, st, a);
   MX_LAUNCH(bn_nhwc_bwd_apply_k, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a);
 }
 
