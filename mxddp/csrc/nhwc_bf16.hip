@@ -638,55 +638,84 @@ __global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
   }
 }
 
-// forward apply: y = relu?(x * scale + shift (+ res))
-__global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a) {
+// forward apply: y = relu?(x * scale + shift (+ res)).  32-bit indices (checked on the host),
+// the channel vector via a multiply-high division, two vectors per iteration with their loads
+// issued first.
+__global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
   __shared__ float cs[2 * 2048];
   for (int i = threadIdx.x; i < 2 * a.C; i += kBnT) cs[i] = a.coef[i];
   __syncthreads();
   const int V = a.C >> 3;
-  const int64_t total = (int64_t)a.Npix * V;
-  for (int64_t i = blockIdx.x * (int64_t)kBnT + threadIdx.x; i < total; i += (int64_t)gridDim.x * kBnT) {
-    const int v = (int)(i % V);
-    float xv[8];
-    unpack8(reinterpret_cast<const uint4*>(a.x)[i], xv);
-    float rv[8];
-    if (a.res) unpack8(reinterpret_cast<const uint4*>(a.res)[i], rv);
+  const int total = a.Npix * V, step = gridDim.x * kBnT;
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  for (int i0 = blockIdx.x * kBnT + threadIdx.x; i0 < total; i0 += 2 * step) {
+    uint4 xr[2], rr[2];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float o = fmaf(xv[e], cs[16 * v + 2 * e], cs[16 * v + 2 * e + 1]);
-      if (a.res) o += rv[e];
-      xv[e] = a.relu ? fmaxf(o, 0.f) : o;
+    for (int u = 0; u < 2; ++u) {
+      const int i = i0 + u * step;
+      xr[u] = i < total ? reinterpret_cast<const uint4*>(a.x)[i] : z;
+      if (a.res) rr[u] = i < total ? reinterpret_cast<const uint4*>(a.res)[i] : z;
     }
-    reinterpret_cast<uint4*>(a.y)[i] = pack8(xv);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = i0 + u * step;
+      if (i >= total) break;
+      const int v = i - (int)fV.div((uint32_t)i) * V;
+      float xv[8], rv[8];
+      unpack8(xr[u], xv);
+      if (a.res) unpack8(rr[u], rv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float o = fmaf(xv[e], cs[16 * v + 2 * e], cs[16 * v + 2 * e + 1]);
+        if (a.res) o += rv[e];
+        xv[e] = a.relu ? fmaxf(o, 0.f) : o;
+      }
+      reinterpret_cast<uint4*>(a.y)[i] = pack8(xv);
+    }
   }
 }
 
 // backward apply: dx = A g + D x + B; dres = g (the residual branch gradient)
-__global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a) {
+__global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv fV) {
   __shared__ float cs[3 * 2048];
   for (int i = threadIdx.x; i < 3 * a.C; i += kBnT) cs[i] = a.coef[i];
   __syncthreads();
   const int V = a.C >> 3;
-  const int64_t total = (int64_t)a.Npix * V;
-  for (int64_t i = blockIdx.x * (int64_t)kBnT + threadIdx.x; i < total; i += (int64_t)gridDim.x * kBnT) {
-    const int v = (int)(i % V);
-    float g[8], xv[8];
-    unpack8(reinterpret_cast<const uint4*>(a.dy)[i], g);
-    unpack8(reinterpret_cast<const uint4*>(a.x)[i], xv);
-    if (a.relu) {
-      float yv[8];
-      unpack8(reinterpret_cast<const uint4*>(a.y)[i], yv);
+  const int total = a.Npix * V, step = gridDim.x * kBnT;
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  for (int i0 = blockIdx.x * kBnT + threadIdx.x; i0 < total; i0 += 2 * step) {
+    uint4 gr[2], xr[2], yr[2];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) g[e] = yv[e] > 0.f ? g[e] : 0.f;
+    for (int u = 0; u < 2; ++u) {
+      const int i = i0 + u * step;
+      const bool ok = i < total;
+      gr[u] = ok ? reinterpret_cast<const uint4*>(a.dy)[i] : z;
+      xr[u] = ok ? reinterpret_cast<const uint4*>(a.x)[i] : z;
+      if (a.relu) yr[u] = ok ? reinterpret_cast<const uint4*>(a.y)[i] : z;
     }
-    if (a.dres) reinterpret_cast<uint4*>(a.dres)[i] = pack8(g);
-    float o[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float* k = cs + 3 * (8 * v + e);
-      o[e] = fmaf(k[0], g[e], fmaf(k[1], xv[e], k[2]));
+    for (int u = 0; u < 2; ++u) {
+      const int i = i0 + u * step;
+      if (i >= total) break;
+      const int v = i - (int)fV.div((uint32_t)i) * V;
+      float g[8], xv[8];
+      unpack8(gr[u], g);
+      unpack8(xr[u], xv);
+      if (a.relu) {
+        float yv[8];
+        unpack8(yr[u], yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = yv[e] > 0.f ? g[e] : 0.f;
+      }
+      if (a.dres) reinterpret_cast<uint4*>(a.dres)[i] = pack8(g);
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float* k = cs + 3 * (8 * v + e);
+        o[e] = fmaf(k[0], g[e], fmaf(k[1], xv[e], k[2]));
+      }
+      reinterpret_cast<uint4*>(a.dx)[i] = pack8(o);
     }
-    reinterpret_cast<uint4*>(a.dx)[i] = pack8(o);
   }
 }
 
@@ -994,7 +1023,8 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
   a.eps = eps;
   MX_LAUNCH(bn_nhwc_partial_k<false>, g, dim3(kBnT), 0, st, a);
   MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 32)), dim3(1024), 0, st, a);
-  MX_LAUNCH(bn_nhwc_apply_k, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a);
+  MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
+  MX_LAUNCH(bn_nhwc_apply_k, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));
 }
 
 void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma, const float* mean,
@@ -1024,7 +1054,8 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
   a.acc_params = accumulate_params;
   MX_LAUNCH(bn_nhwc_partial_k<true>, g, dim3(kBnT), 0, st, a);
   MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 32)), dim3(1024), 0, st, a);
-  MX_LAUNCH(bn_nhwc_bwd_apply_k, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a);
+  MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
+  MX_LAUNCH(bn_nhwc_bwd_apply_k, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));
 }
 
 void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, int k,
