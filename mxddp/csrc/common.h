@@ -28,6 +28,8 @@ namespace mx {
 void post_launch(hipStream_t st, const char* what);
 void set_debug_sync(bool on);
 bool debug_sync();
+// compute units of the current device (cached per device)
+int device_cu_count();
 
 #define MX_LAUNCH(kern, grid, block, shm, st, ...)                \
   do {                                                            \

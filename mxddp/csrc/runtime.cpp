@@ -22,6 +22,18 @@ bool debug_sync() {
 
 void set_debug_sync(bool on) { g_debug_sync.store(on ? 1 : 0, std::memory_order_relaxed); }
 
+int device_cu_count() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  MX_HIP_CHECK(hipGetDevice(&dev));
+  int v = dev < 64 ? cache[dev].load(std::memory_order_relaxed) : 0;
+  if (v <= 0) {
+    MX_HIP_CHECK(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev));
+    if (dev < 64) cache[dev].store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+
 void post_launch(hipStream_t st, const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess)
