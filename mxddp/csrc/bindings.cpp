@@ -89,6 +89,10 @@ PYBIND11_MODULE(_C, m) {
                                  uintptr_t st) {
     nhwc_repack_weight(P<const float>(w), P<uint16_t>(wt), P<uint16_t>(wtd), K, C, R, S_, Cp, S(st));
   });
+  m.def("nhwc_repack_blocks", &nhwc_repack_blocks);
+  m.def("nhwc_repack_many", [](uintptr_t desc, int n, int total_blocks, uintptr_t st) {
+    nhwc_repack_many(P<const int64_t>(desc), n, total_blocks, S(st));
+  });
   m.def("nhwc_conv_fwd", [](uintptr_t x, uintptr_t wt, uintptr_t y, int N, int H, int W, int Cp, int K, int R, int S_,
                             int sh, int sw, int ph, int pw, int P_, int Q, uintptr_t scratch, uintptr_t st) {
     nhwc_conv_fwd(P<const uint16_t>(x), P<const uint16_t>(wt), P<uint16_t>(y), N, H, W, Cp, K, R, S_, sh, sw, ph, pw,

@@ -446,6 +446,38 @@ __global__ void wrepack_k(const float* __restrict__ w, bf16* __restrict__ wt, bf
   }
 }
 
+// Every convolution of a model in ONE launch (nhwc_repack_many): desc[i] = {w, wt, wtd, K, C,
+// R*S, Cp, first block}; block b finds its convolution by binary search over the first-block
+// column, then strides over that convolution's elements (32-bit indices, 8 per thread).
+constexpr int kRepackPerBlock = 256 * 8;
+
+__global__ __launch_bounds__(256) void wrepack_many_k(const int64_t* __restrict__ desc, int n) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (desc[mid * 8 + 7] <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1;
+  }
+  const int64_t* d = desc + lo * 8;
+  const float* w = reinterpret_cast<const float*>(d[0]);
+  bf16* wt = reinterpret_cast<bf16*>(d[1]);
+  bf16* wtd = reinterpret_cast<bf16*>(d[2]);
+  const int K = (int)d[3], C = (int)d[4], RS = (int)d[5], Cp = (int)d[6], b0 = (int)d[7];
+  const int nb = (lo + 1 < n ? (int)desc[(lo + 1) * 8 + 7] : (int)gridDim.x) - b0;
+  const int tf = wt ? K * RS * Cp : 0, td = wtd ? C * RS * K : 0;
+  for (int i = ((int)blockIdx.x - b0) * 256 + threadIdx.x; i < tf + td; i += nb * 256) {
+    if (i < tf) {
+      const int c = i % Cp, krs = i / Cp;
+      const int rs = krs % RS, k = krs / RS;
+      wt[i] = c < C ? f2bf(w[(k * C + c) * RS + rs]) : (bf16)0;
+    } else {
+      const int j = i - tf;
+      const int k = j % K, crs = j / K;
+      const int rs = crs % RS, c = crs / RS;
+      wtd[j] = f2bf(w[(k * C + c) * RS + rs]);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // BatchNorm over [Npix][C] (C % 8 == 0, 256 % (C / 8) == 0 or C / 8 a multiple of 256), three
 // launches per direction:
@@ -818,6 +850,17 @@ void nhwc_repack_weight(const float* w, uint16_t* wt, uint16_t* wtd, int K, int 
                         hipStream_t st) {
   const int64_t total = (wt ? (int64_t)K * Cp * R * S : 0) + (wtd ? (int64_t)K * C * R * S : 0);
   MX_LAUNCH(wrepack_k, dim3(grid_for(total)), dim3(256), 0, st, w, wt, wtd, K, C, R, S, Cp);
+}
+
+int nhwc_repack_blocks(int K, int C, int R, int S, int Cp, bool fwd, bool dgrad) {
+  const int64_t n = (fwd ? (int64_t)K * R * S * Cp : 0) + (dgrad ? (int64_t)K * C * R * S : 0);
+  MX_CHECK(n < (1ll << 31), "nhwc repack: weight too large for 32-bit indices");
+  return std::max(1, (int)((n + kRepackPerBlock - 1) / kRepackPerBlock));
+}
+
+void nhwc_repack_many(const int64_t* desc, int n, int total_blocks, hipStream_t st) {
+  if (n <= 0) return;
+  MX_LAUNCH(wrepack_many_k, dim3(total_blocks), dim3(256), 0, st, desc, n);
 }
 
 struct ConvPlan {

@@ -137,6 +137,10 @@ void nhwc_from_nchw(const float* x, uint16_t* y, int N, int C, int H, int W, int
 // wt (or null): fwd layout bf16 [K][R][S][Cp] (channel-padded); wtd (or null): dgrad layout bf16 [C][R][S][K]
 void nhwc_repack_weight(const float* w, uint16_t* wt, uint16_t* wtd, int K, int C, int R, int S, int Cp,
                         hipStream_t st);
+// all convolutions of a model in one launch: desc = device int64 [n][8] rows {w, wt, wtd (or 0), K,
+// C, R*S, Cp, first block}, first blocks = prefix sums of nhwc_repack_blocks(...)
+int nhwc_repack_blocks(int K, int C, int R, int S, int Cp, bool fwd, bool dgrad);
+void nhwc_repack_many(const int64_t* desc, int n, int total_blocks, hipStream_t st);
 // scratch (or null = no split-K): nhwc_conv_scratch_floats(M = output pixels, Ng = output
 // channels, Kg = R*S*input channels) floats of fp32 split-K partials
 size_t nhwc_conv_scratch_floats(int M, int Ng, int Kg);

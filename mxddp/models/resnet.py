@@ -40,17 +40,22 @@ class Bottleneck(nn.Module):
         out = self.bn3(self.conv3(self.bn2(self.conv2(self.bn1(self.conv1(x))))))
         return ops.relu(out + idt)
 
-    def forward_nhwc(self, x):
+    def convs(self):
+        c = [self.conv1, self.conv2, self.conv3]
+        return c + ([self.downsample[0]] if self.downsample is not None else [])
+
+    def forward_nhwc(self, x, pack=None):
         from ..ops import nhwc as N
 
         if self.downsample is None:
             idt = x
         else:
             dc, dbn = self.downsample[0], self.downsample[1]
-            idt = N.batch_norm(N.conv2d(x, dc.weight, dc.stride, dc.padding), dbn)
-        out = N.batch_norm(N.conv2d(x, self.conv1.weight), self.bn1, relu=True)
-        out = N.batch_norm(N.conv2d(out, self.conv2.weight, self.conv2.stride, self.conv2.padding), self.bn2, relu=True)
-        return N.batch_norm(N.conv2d(out, self.conv3.weight), self.bn3, relu=True, res=idt)
+            idt = N.batch_norm(N.conv2d(x, dc.weight, dc.stride, dc.padding, pack), dbn)
+        out = N.batch_norm(N.conv2d(x, self.conv1.weight, pack=pack), self.bn1, relu=True)
+        out = N.batch_norm(N.conv2d(out, self.conv2.weight, self.conv2.stride, self.conv2.padding, pack), self.bn2,
+                           relu=True)
+        return N.batch_norm(N.conv2d(out, self.conv3.weight, pack=pack), self.bn3, relu=True, res=idt)
 
 
 class ResNet(nn.Module):
@@ -94,15 +99,36 @@ class ResNet(nn.Module):
         return self.fc(x.flatten(1))
 
 
+    def _weight_pack(self):
+        """All 53 conv weights repacked to bf16 in one launch per forward (mxddp.ops.nhwc.WeightPack);
+        the pack is rebuilt only when a weight's storage or the grad mode changes."""
+        import torch
+
+        from ..ops import nhwc as N
+
+        grad = torch.is_grad_enabled()
+        specs = [(self.conv1.weight, 8, False)]
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for blk in layer:
+                specs += [(c.weight, c.weight.shape[1], grad) for c in blk.convs()]
+        pack = getattr(self, "_nhwc_pack", None)
+        if pack is None or not pack.matches(specs):
+            pack = N.WeightPack(specs)
+            self._nhwc_pack = pack
+        pack.refresh()
+        return pack
+
     def forward_nhwc(self, x):
         from ..ops import nhwc as N
 
+        pack = self._weight_pack()
         y = N.to_nhwc(x)
-        y = N.batch_norm(N.conv2d(y, self.conv1.weight, self.conv1.stride, self.conv1.padding), self.bn1, relu=True)
+        y = N.batch_norm(N.conv2d(y, self.conv1.weight, self.conv1.stride, self.conv1.padding, pack), self.bn1,
+                         relu=True)
         y = N.max_pool2d(y, 3, 2, 1)
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:
-                y = blk.forward_nhwc(y)
+                y = blk.forward_nhwc(y, pack)
         return self.fc(N.global_avg_pool(y))
 
 

@@ -50,9 +50,54 @@ def _splitk_scratch(M, Ng, Kg, device):
     return torch.empty((n,), device=device, dtype=torch.float32) if n else None
 
 
+class WeightPack:
+    """Every convolution weight of a model repacked to its bf16 GEMM layouts in ONE launch per
+    forward (``refresh()``), instead of one repack launch per convolution.
+
+    ``specs``: (weight, Cp, need_dgrad) per convolution; the forward layout [K][R][S][Cp] and,
+    when ``need_dgrad``, the data-gradient layout [C][R][S][K] live in one bf16 buffer.  The
+    descriptor table (device int64, one row per convolution) is built once; the pack stays valid
+    while the weights keep their storage (``matches()``), e.g. views into a FlatParams buffer."""
+
+    def __init__(self, specs):
+        Cn = native()
+        dev = specs[0][0].device
+        rows, self._views, off, blk = [], {}, 0, 0
+        layout = []
+        for w, cp, nd in specs:
+            K, C, R, S = w.shape
+            nf, ndg = K * R * S * cp, (C * R * S * K if nd else 0)
+            layout.append((off, nf, off + (nf + 63) // 64 * 64 if nd else -1, ndg))
+            off += (nf + 63) // 64 * 64 + (ndg + 63) // 64 * 64
+        self.buf = torch.empty((max(off, 1),), device=dev, dtype=BF16)
+        for (w, cp, nd), (of, nf, od, ndg) in zip(specs, layout):
+            K, C, R, S = w.shape
+            wt = self.buf[of:of + nf]
+            wtd = self.buf[od:od + ndg] if nd else None
+            self._views[id(w)] = (wt, wtd)
+            rows.append([w.data_ptr(), wt.data_ptr(), _p(wtd), K, C, R * S, cp, blk])
+            blk += Cn.nhwc_repack_blocks(K, C, R, S, cp, True, bool(nd))
+        self.blocks = blk
+        self.desc = torch.tensor(rows, dtype=torch.int64).to(dev)
+        self._key = tuple((id(w), w.data_ptr()) for w, _, _ in specs)
+        self._specs = [(w, cp, nd) for w, cp, nd in specs]
+
+    def matches(self, specs) -> bool:
+        return len(specs) == len(self._key) and all(
+            (id(w), w.data_ptr()) == k and (cp, nd) == (c2, n2)
+            for (w, cp, nd), k, (_, c2, n2) in zip(specs, self._key, self._specs))
+
+    def refresh(self, stream=None):
+        st = stream if stream is not None else torch.cuda.current_stream(self.buf.device).cuda_stream
+        native().nhwc_repack_many(self.desc.data_ptr(), self.desc.shape[0], self.blocks, st)
+
+    def get(self, w):
+        return self._views.get(id(w))
+
+
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad):
+    def forward(ctx, x, w, stride, pad, packed=None):
         Cn = native()
         N, H, W, Cp = x.shape
         K, C, R, S = w.shape
@@ -60,11 +105,14 @@ class _Conv(torch.autograd.Function):
         ph, pw = pad
         P, Q = _out(H, R, sh, ph), _out(W, S, sw, pw)
         st = stream_of(x)
-        wt = torch.empty((K * R * S * Cp,), device=x.device, dtype=BF16)
-        # the data-gradient layout is produced in the same launch when backward will need it
         need_dx = ctx.needs_input_grad[0] and Cp == C
-        wtd = torch.empty((C * R * S * K,), device=x.device, dtype=BF16) if need_dx else None
-        Cn.nhwc_repack_weight(w.data_ptr(), wt.data_ptr(), _p(wtd), K, C, R, S, Cp, st)
+        if packed is not None and (packed[1] is not None or not need_dx):
+            wt, wtd = packed  # repacked for the whole model by WeightPack.refresh()
+        else:
+            wt = torch.empty((K * R * S * Cp,), device=x.device, dtype=BF16)
+            # the data-gradient layout is produced in the same launch when backward will need it
+            wtd = torch.empty((C * R * S * K,), device=x.device, dtype=BF16) if need_dx else None
+            Cn.nhwc_repack_weight(w.data_ptr(), wt.data_ptr(), _p(wtd), K, C, R, S, Cp, st)
         y = torch.empty((N, P, Q, K), device=x.device, dtype=BF16)
         scr = _splitk_scratch(N * P * Q, K, R * S * Cp, x.device)
         Cn.nhwc_conv_fwd(x.data_ptr(), wt.data_ptr(), y.data_ptr(), N, H, W, Cp, K, R, S, sh, sw, ph, pw, P, Q,
@@ -102,13 +150,14 @@ class _Conv(torch.autograd.Function):
                                P, Q, sink is not None, part.data_ptr(), st)
             if sink is not None:
                 dw = None
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
-def conv2d(x, w, stride=1, padding=0):
+def conv2d(x, w, stride=1, padding=0, pack: WeightPack | None = None):
+    """bf16 NHWC convolution; ``pack`` supplies weights already repacked by WeightPack.refresh()."""
     s = (stride, stride) if isinstance(stride, int) else tuple(stride)
     p = (padding, padding) if isinstance(padding, int) else tuple(padding)
-    return _Conv.apply(x, w, s, p)
+    return _Conv.apply(x, w, s, p, pack.get(w) if pack is not None else None)
 
 
 class _BN(torch.autograd.Function):

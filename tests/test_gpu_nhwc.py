@@ -110,6 +110,31 @@ def test_bn_nhwc(cuda, C, relu, res):
     assert int(bn.num_batches_tracked) == 1
 
 
+def test_weight_pack_matches_per_conv_repack(cuda):
+    """One-launch repack of many convolutions == the per-convolution repack (both layouts, padded
+    stem channels, a conv without the data-gradient layout)."""
+    from mxddp import native
+
+    Cn = native()
+    torch.manual_seed(8)
+    specs = [(torch.randn(64, 3, 7, 7, device=cuda), 8, False), (torch.randn(40, 64, 3, 3, device=cuda), 64, True),
+             (torch.randn(256, 64, 1, 1, device=cuda), 64, True), (torch.randn(24, 16, 3, 3, device=cuda), 16, False)]
+    pack = nhwc.WeightPack(specs)
+    pack.refresh()
+    st = torch.cuda.current_stream().cuda_stream
+    for w, cp, nd in specs:
+        K, C, R, S = w.shape
+        wt = torch.empty(K * R * S * cp, device=cuda, dtype=torch.bfloat16)
+        wtd = torch.empty(C * R * S * K, device=cuda, dtype=torch.bfloat16)
+        Cn.nhwc_repack_weight(w.data_ptr(), wt.data_ptr(), wtd.data_ptr(), K, C, R, S, cp, st)
+        pwt, pwtd = pack.get(w)
+        assert torch.equal(pwt, wt)
+        assert (pwtd is not None) == nd
+        if nd:
+            assert torch.equal(pwtd, wtd)
+    assert pack.matches(specs) and not pack.matches(specs[:2])
+
+
 def test_pools_nhwc(cuda):
     torch.manual_seed(3)
     x = torch.randn(2, 13, 11, 16).to(torch.bfloat16)
