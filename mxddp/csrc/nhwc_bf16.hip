@@ -66,11 +66,16 @@ struct ConvNArgs {
   bf16* out;        // [M][Ng]  (M = N * OH * OW output pixels)
   int M, Ng, Kg, Ca;
   int OH, OW, IH, IW;
-  int S, sh, sw, ph, pw;
+  int R, S, sh, sw, ph, pw;
   int dgrad;        // 0: y = conv(x); 1: dx = conv_transpose(dy) (sh, sw in {1, 2})
   int kt_per_split; // split-K: blockIdx.y covers k-tiles [y * kt_per_split, ...)
   float* part;      // split-K > 1: fp32 partials [splits][M][Ng] (else null: bf16 store)
-  FastDiv fOW, fOHW, fCa, fS;
+  // par = 1 (stride-2 data gradient, even OH / OW, wide path): blockIdx.z = output parity class
+  // (h & 1, w & 1); class pixels are (n, 2 i + h&1, 2 j + w&1), i < Hc, j < Wc, and only the
+  // taps of matching parity contribute, so each class is a dense stride-1 GEMM over its own
+  // taps (the zero-inserted transposed gather would multiply 3 zeros out of 4)
+  int par, Hc, Wc;
+  FastDiv fOW, fOHW, fCa, fS, fWc, fHWc;
 };
 
 template <int TM, int TN, bool kWide>
@@ -93,17 +98,39 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
   const int ch0 = (bid % tiles_m) * TM, px0 = (bid / tiles_m) * TN;
   const int kv = tid & 7, row0 = tid >> 3;  // vector kv of rows row0 + 32 i
 
+  // parity class (par mode): its pixel count, tap origin (r0, s0), taps per row and GEMM depth
+  const int pca = a.par ? (int)blockIdx.z >> 1 : 0, pcb = a.par ? (int)blockIdx.z & 1 : 0;
+  const int r0 = a.par ? (pca + a.ph) & 1 : 0, s0 = a.par ? (pcb + a.pw) & 1 : 0;
+  const int nS = a.par ? (a.S - s0 + 1) >> 1 : a.S;
+  const int Kgc = a.par ? ((a.R - r0 + 1) >> 1) * nS * a.Ca : a.Kg;
+  const int Mc = a.par ? a.M >> 2 : a.M;
+  // output pixel of GEMM column m (the full dx index in par mode)
+  auto pfull = [&](int m) -> int {
+    if (!a.par) return m;
+    const int n = (int)a.fHWc.div((uint32_t)m), rem = m - n * a.Hc * a.Wc;
+    const int i = (int)a.fWc.div((uint32_t)rem), j = rem - i * a.Wc;
+    return (n * a.OH + 2 * i + pca) * a.OW + 2 * j + pcb;
+  };
+
   int pn[EB], poh[EB], pow_[EB];
   bool pok[EB];
 #pragma unroll
   for (int i = 0; i < EB; ++i) {
     const int m = px0 + row0 + 32 * i;
-    pok[i] = m < a.M;
+    pok[i] = m < Mc;
     const int mm = pok[i] ? m : 0;
-    pn[i] = (int)a.fOHW.div((uint32_t)mm);
-    const int rem = mm - pn[i] * a.OH * a.OW;
-    poh[i] = (int)a.fOW.div((uint32_t)rem);
-    pow_[i] = rem - poh[i] * a.OW;
+    if (a.par) {
+      pn[i] = (int)a.fHWc.div((uint32_t)mm);
+      const int rem = mm - pn[i] * a.Hc * a.Wc;
+      const int ii = (int)a.fWc.div((uint32_t)rem);
+      poh[i] = 2 * ii + pca;
+      pow_[i] = 2 * (rem - ii * a.Wc) + pcb;
+    } else {
+      pn[i] = (int)a.fOHW.div((uint32_t)mm);
+      const int rem = mm - pn[i] * a.OH * a.OW;
+      poh[i] = (int)a.fOW.div((uint32_t)rem);
+      pow_[i] = rem - poh[i] * a.OW;
+    }
   }
   u32x4 ra[EA], rb[EB];
   const u32x4 z4 = {0u, 0u, 0u, 0u};
@@ -123,8 +150,17 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
   auto gload = [&](int k0) {
     if constexpr (kWide) {
       const int rs = (int)a.fCa.div((uint32_t)k0), c0 = k0 - rs * a.Ca;  // uniform
-      const int r = (int)a.fS.div((uint32_t)rs), s = rs - r * a.S;
-      const char* wb = reinterpret_cast<const char*>(a.wt) + 2u * (uint32_t)k0;
+      int r, s, kw = k0;
+      if (a.par) {  // class tap rs -> (r0 + 2 ri, s0 + 2 si); weight column of that tap
+        const int ri = rs / nS, si = rs - ri * nS;
+        r = r0 + 2 * ri;
+        s = s0 + 2 * si;
+        kw = (r * a.S + s) * a.Ca + c0;
+      } else {
+        r = (int)a.fS.div((uint32_t)rs);
+        s = rs - r * a.S;
+      }
+      const char* wb = reinterpret_cast<const char*>(a.wt) + 2u * (uint32_t)kw;
 #pragma unroll
       for (int i = 0; i < EA; ++i)
         ra[i] = (ch0 + row0 + 32 * i < a.Ng) ? *reinterpret_cast<const u32x4*>(wb + abase[i]) : z4;
@@ -190,10 +226,13 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
     for (int j = 0; j < WNT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int kt0 = blockIdx.y * a.kt_per_split;
-  const int nt = min((a.Kg + BK - 1) / BK - kt0, a.kt_per_split);
+  // nt <= 0: a split (or a parity class without taps) with nothing to reduce writes zeros
+  const int nt = min((Kgc + BK - 1) / BK - kt0, a.kt_per_split);
   const int a_row = wm * (TM / 2) + (lane & 15), b_row = wn * (TN / 2) + (lane & 15), koff = 8 * (lane >> 4);
-  gload(kt0 * BK);
-  sstore(0);
+  if (nt > 0) {
+    gload(kt0 * BK);
+    sstore(0);
+  }
   __syncthreads();
   for (int t = 0; t < nt; ++t) {
     const int cur = t & 1;
@@ -226,8 +265,8 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
 #pragma unroll
       for (int j = 0; j < WNT; ++j) {
         const int px = px0 + wn * (TN / 2) + 16 * j + (lane & 15);
-        if (px >= a.M) continue;
-        *reinterpret_cast<float4*>(a.part + ((size_t)blockIdx.y * a.M + px) * a.Ng + ch) =
+        if (px >= Mc) continue;
+        *reinterpret_cast<float4*>(a.part + ((size_t)blockIdx.y * a.M + pfull(px)) * a.Ng + ch) =
             make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
       }
     }
@@ -255,8 +294,9 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
   for (int v = tid; v < TN * VPR; v += 256) {
     const int row = v / VPR, cv = v - row * VPR;
     const int px = px0 + row, ch = ch0 + 8 * cv;
-    if (px < a.M && ch < a.Ng)
-      *reinterpret_cast<u32x4*>(a.out + (size_t)px * a.Ng + ch) = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
+    if (px < Mc && ch < a.Ng)
+      *reinterpret_cast<u32x4*>(a.out + (size_t)pfull(px) * a.Ng + ch) =
+          *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
   }
 }
 
@@ -889,6 +929,25 @@ static ConvPlan conv_plan(int M, int Ng, int Kg) {
   return p;
 }
 
+// kernel variant, parity mode and tile plan of one convolution (shared by the launch and the
+// scratch-size queries, so the caller's split-K buffer always matches the launch)
+struct ConvSetup {
+  ConvPlan p;
+  bool wide, par;
+};
+
+static ConvSetup conv_setup(const ConvNArgs& a) {
+  ConvSetup c{};
+  // wide path: whole 64-k stages inside one tap, and every byte offset fits 32 bits
+  c.wide = a.Ca % 64 == 0 && a.Kg % 64 == 0 &&
+           (int64_t)a.IH * a.IW * a.Ca * (a.M / (a.OH * a.OW) + 1) < (1ll << 30) &&
+           (int64_t)a.Ng * a.Kg < (1ll << 30);
+  c.par = c.wide && a.dgrad && a.sh == 2 && a.sw == 2 && a.OH % 2 == 0 && a.OW % 2 == 0;
+  // parity classes: a quarter of the pixels each, at most ceil(R/2) x ceil(S/2) taps
+  c.p = c.par ? conv_plan(a.M / 4, a.Ng, ((a.R + 1) / 2) * ((a.S + 1) / 2) * a.Ca) : conv_plan(a.M, a.Ng, a.Kg);
+  return c;
+}
+
 size_t nhwc_conv_scratch_floats(int M, int Ng, int Kg) {
   const ConvPlan p = conv_plan(M, Ng, Kg);
   return p.splits > 1 ? (size_t)p.splits * M * Ng : 0;
@@ -900,18 +959,23 @@ static void launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   a.fOHW = FastDiv(a.OH * a.OW);
   a.fCa = FastDiv(a.Ca);
   a.fS = FastDiv(a.S);
-  ConvPlan p = conv_plan(a.M, a.Ng, a.Kg);
+  const ConvSetup cs = conv_setup(a);
+  ConvPlan p = cs.p;
+  const bool wide = cs.wide;
+  a.par = cs.par ? 1 : 0;
+  if (cs.par) {
+    a.Hc = a.OH / 2;
+    a.Wc = a.OW / 2;
+    a.fWc = FastDiv(a.Wc);
+    a.fHWc = FastDiv(a.Hc * a.Wc);
+  }
   if (!scratch) {  // no partial buffer: no split
     p.splits = 1;
     p.kt_per_split = cdiv(a.Kg, 64);
   }
   a.kt_per_split = p.kt_per_split;
   a.part = p.splits > 1 ? scratch : nullptr;
-  const dim3 grid(p.blocks, p.splits);
-  // wide path: whole 64-k stages inside one tap, and every byte offset fits 32 bits
-  const bool wide = a.Ca % 64 == 0 && a.Kg % 64 == 0 &&
-                    (int64_t)a.IH * a.IW * a.Ca * (a.M / (a.OH * a.OW) + 1) < (1ll << 30) &&
-                    (int64_t)a.Ng * a.Kg < (1ll << 30);
+  const dim3 grid(p.blocks, p.splits, cs.par ? 4 : 1);
   if (p.tm == 128) {
     if (wide) MX_LAUNCH((conv_nhwc_kernel<128, 128, true>), grid, dim3(256), 0, st, a);
     else MX_LAUNCH((conv_nhwc_kernel<128, 128, false>), grid, dim3(256), 0, st, a);
@@ -942,6 +1006,7 @@ void nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, in
   a.OW = Q;
   a.IH = H;
   a.IW = W;
+  a.R = R;
   a.S = S;
   a.sh = sh;
   a.sw = sw;
@@ -951,8 +1016,8 @@ void nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, in
   launch_conv(a, scratch, st);
 }
 
-void nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
-                     int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st) {
+static ConvNArgs dgrad_args(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K,
+                            int R, int S, int sh, int sw, int ph, int pw, int P, int Q) {
   MX_CHECK((sh == 1 || sh == 2) && (sw == 1 || sw == 2), "nhwc dgrad: stride 1 or 2");
   ConvNArgs a{};
   a.act = dy;
@@ -966,12 +1031,26 @@ void nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int
   a.OW = W;
   a.IH = P;
   a.IW = Q;
+  a.R = R;
   a.S = S;
   a.sh = sh;
   a.sw = sw;
   a.ph = ph;
   a.pw = pw;
   a.dgrad = 1;
+  return a;
+}
+
+size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
+                                      int P, int Q) {
+  const ConvNArgs a = dgrad_args(nullptr, nullptr, nullptr, N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q);
+  const ConvPlan p = conv_setup(a).p;
+  return p.splits > 1 ? (size_t)p.splits * a.M * a.Ng : 0;
+}
+
+void nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
+                     int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st) {
+  ConvNArgs a = dgrad_args(dy, wt_d, dx, N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q);
   launch_conv(a, scratch, st);
 }
 

@@ -138,7 +138,8 @@ class _Conv(torch.autograd.Function):
                 wtd = torch.empty((C * R * S * K,), device=dy.device, dtype=BF16)
                 Cn.nhwc_repack_weight(w.data_ptr(), 0, wtd.data_ptr(), K, C, R, S, Cp, st)
             dx = torch.empty((N, H, W, C), device=dy.device, dtype=BF16)
-            scr = _splitk_scratch(N * H * W, C, R * S * K, dy.device)
+            n = Cn.nhwc_conv_dgrad_scratch_floats(N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q)
+            scr = torch.empty((n,), device=dy.device, dtype=torch.float32) if n else None
             Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx.data_ptr(), N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q,
                                _p(scr), st)
         if ctx.needs_input_grad[1]:

@@ -54,7 +54,7 @@ def main():
         dx = torch.empty_like(x)
         dw = torch.empty_like(w)
         sf = Cn.nhwc_conv_scratch_floats(N * P * Q, K, R * R * C)
-        sd = Cn.nhwc_conv_scratch_floats(N * H * W, C, R * R * K)
+        sd = Cn.nhwc_conv_dgrad_scratch_floats(N, H, W, C, K, R, R, s, s, p, p, P, Q)
         sw = Cn.nhwc_wgrad_scratch_floats(N, C, K, R, R, P, Q)
         scr = torch.empty(max(sf, sd, sw, 1), device=dev)
         flops = 2.0 * N * P * Q * K * C * R * R

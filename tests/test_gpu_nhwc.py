@@ -28,6 +28,10 @@ CONV = [
     (2, 128, 14, 14, 256, 1, 2, 0),
     (1, 256, 7, 7, 512, 3, 1, 1),
     (2, 8, 30, 30, 64, 7, 2, 3),   # stem-like (channel-padded input)
+    # stride-2 data gradients on the parity-class path (wide, even input), incl. split-K
+    (2, 64, 14, 14, 128, 3, 2, 1),
+    (2, 256, 8, 8, 512, 3, 2, 1),
+    (3, 128, 12, 10, 64, 1, 2, 0),
 ]
 
 
