@@ -325,50 +325,60 @@ struct WgNArgs {
   FastDiv fQ, fPQ, fCa, fS;
 };
 
-constexpr int kWP = 128 + 8;  // LDS pitch of a 128-channel pixel row (272 B; tr reads need 8-B alignment)
-
-__device__ __forceinline__ bf16x8 tr_frag(const bf16* tile, int col0, int lane) {
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* tile, int pitch, int col0, int lane) {
   // MFMA operand for "row" = channel col0 + (lane & 15), k = pixels 8 * (lane >> 4) .. + 7 from a
-  // pixel-major [32][kWP] tile: two transposed reads of 4 pixels x 16 channels each.
+  // pixel-major [32][pitch] tile: two transposed reads of 4 pixels x 16 channels each.
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-  const bf16* p0 = tile + (8 * g + q) * kWP + col0 + 4 * p;
+  const bf16* p0 = tile + (8 * g + q) * pitch + col0 + 4 * p;
   const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * kWP));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * pitch));
   bf16x8 r;
   r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
   return r;
 }
 
+// TM x TN output tile (output channels x (r, s, c) columns), TM, TN in {64, 128}: 64-wide tiles
+// for the 64-channel layers (a 128-wide tile over a 64-channel operand computes 50-75 % zeros)
+template <int TM, int TN>
 __global__ __launch_bounds__(256) void wgrad_nhwc_kernel(WgNArgs a) {
-  constexpr int BK = 64;  // pixels per stage (two MFMA k-steps)
-  __shared__ __attribute__((aligned(16))) bf16 As[2][BK * kWP];  // dy tile  [pixel][k]
-  __shared__ __attribute__((aligned(16))) bf16 Bs[2][BK * kWP];  // x gather [pixel][(r,s,c)]
+  constexpr int BK = 64;                   // pixels per stage (two MFMA k-steps)
+  constexpr int PA = TM + 8, PB = TN + 8;  // LDS pitches (8-byte aligned rows for the tr reads)
+  constexpr int VA = TM / 8, VB = TN / 8;  // 16-byte vectors per pixel row
+  constexpr int EA = BK * VA / 256, EB = BK * VB / 256;
+  constexpr int WMT = TM / 32, WNT = TN / 32;
+  __shared__ __attribute__((aligned(16))) bf16 As[2][BK * PA];  // dy tile  [pixel][k]
+  __shared__ __attribute__((aligned(16))) bf16 Bs[2][BK * PB];  // x gather [pixel][(r,s,c)]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
-  const int tiles_m = (a.Kout + 127) / 128, tiles_n = (a.Ng + 127) / 128;
+  const int tiles_m = (a.Kout + TM - 1) / TM, tiles_n = (a.Ng + TN - 1) / TN;
   const int bid = blockIdx.x;
   const int tm = bid % tiles_m, r1 = bid / tiles_m, tn = r1 % tiles_n, sp = r1 / tiles_n;
-  const int m0 = tm * 128, n0 = tn * 128;
+  const int m0 = tm * TM, n0 = tn * TN;
   const int pbeg = sp * a.chunk, pend = min(a.Npix, pbeg + a.chunk);
   if (pbeg >= pend) return;
-  // load roles: vector v = tid + 256 i -> pixel row v >> 4 (0..63), 8-channel vector v & 15
-  const int cv = tid & 15, prow0 = tid >> 4;
-  // B column decomposition (fixed per thread): column n0 + 8 cv -> (r, s, c)
-  const int col = n0 + 8 * cv;
+  // load roles (fixed per thread: 256 is a multiple of VA and VB): A vector cva of pixel rows
+  // rowa0 + (256 / VA) i, B vector cvb of rows rowb0 + (256 / VB) i
+  const int cva = tid % VA, rowa0 = tid / VA, cvb = tid % VB, rowb0 = tid / VB;
+  // B column decomposition (fixed per thread): column n0 + 8 cvb -> (r, s, c)
+  const int col = n0 + 8 * cvb;
   const bool col_ok = col < a.Ng;
   const int colc = col_ok ? col : 0;
   const int rs = (int)a.fCa.div((uint32_t)colc), bc = colc - rs * a.Ca;
   const int br = (int)a.fS.div((uint32_t)rs), bs = rs - br * a.S;
-  const bool k_ok = m0 + 8 * cv < a.Kout;
-  u32x4 ra[4], rb[4];
+  const bool k_ok = m0 + 8 * cva < a.Kout;
+  u32x4 ra[EA], rb[EB];
   const u32x4 z4 = {0u, 0u, 0u, 0u};
   auto gload = [&](int p0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int pix = p0 + prow0 + 16 * i;
+    for (int i = 0; i < EA; ++i) {
+      const int pix = p0 + rowa0 + (256 / VA) * i;
+      ra[i] = (pix < pend && k_ok) ? *reinterpret_cast<const u32x4*>(a.dy + (size_t)pix * a.Kout + m0 + 8 * cva) : z4;
+    }
+#pragma unroll
+    for (int i = 0; i < EB; ++i) {
+      const int pix = p0 + rowb0 + (256 / VB) * i;
       const bool ok = pix < pend;
-      ra[i] = (ok && k_ok) ? *reinterpret_cast<const u32x4*>(a.dy + (size_t)pix * a.Kout + m0 + 8 * cv) : z4;
       const int pp = ok ? pix : 0;
       const int n = (int)a.fPQ.div((uint32_t)pp), rem = pp - n * a.P * a.Q;
       const int p = (int)a.fQ.div((uint32_t)rem), q = rem - p * a.Q;
@@ -379,17 +389,18 @@ __global__ __launch_bounds__(256) void wgrad_nhwc_kernel(WgNArgs a) {
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<u32x4*>(&As[buf][(prow0 + 16 * i) * kWP + 8 * cv]) = ra[i];
-      *reinterpret_cast<u32x4*>(&Bs[buf][(prow0 + 16 * i) * kWP + 8 * cv]) = rb[i];
-    }
+    for (int i = 0; i < EA; ++i)
+      *reinterpret_cast<u32x4*>(&As[buf][(rowa0 + (256 / VA) * i) * PA + 8 * cva]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < EB; ++i)
+      *reinterpret_cast<u32x4*>(&Bs[buf][(rowb0 + (256 / VB) * i) * PB + 8 * cvb]) = rb[i];
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[WMT][WNT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < WMT; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < WNT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nt = (pend - pbeg + BK - 1) / BK;
   gload(pbeg);
@@ -400,15 +411,15 @@ __global__ __launch_bounds__(256) void wgrad_nhwc_kernel(WgNArgs a) {
     if (t + 1 < nt) gload(pbeg + (t + 1) * BK);
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8 av[4], bv[4];
+      bf16x8 av[WMT], bv[WNT];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) av[i] = tr_frag(As[cur] + 32 * ks * kWP, wm * 64 + 16 * i, lane);
+      for (int i = 0; i < WMT; ++i) av[i] = tr_frag(As[cur] + 32 * ks * PA, PA, wm * (TM / 2) + 16 * i, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bv[j] = tr_frag(Bs[cur] + 32 * ks * kWP, wn * 64 + 16 * j, lane);
+      for (int j = 0; j < WNT; ++j) bv[j] = tr_frag(Bs[cur] + 32 * ks * PB, PB, wn * (TN / 2) + 16 * j, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < WMT; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < WNT; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
     if (t + 1 < nt) sstore(cur ^ 1);
@@ -417,37 +428,61 @@ __global__ __launch_bounds__(256) void wgrad_nhwc_kernel(WgNArgs a) {
 
   float* pl = a.part + (size_t)sp * a.Kout * a.Ng;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int cn = n0 + wn * 64 + 16 * j + (lane & 15);
+  for (int j = 0; j < WNT; ++j) {
+    const int cn = n0 + wn * (TN / 2) + 16 * j + (lane & 15);
     if (cn >= a.Ng) continue;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < WMT; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int k = m0 + wm * 64 + 16 * i + 4 * (lane >> 4) + r;
+        const int k = m0 + wm * (TM / 2) + 16 * i + 4 * (lane >> 4) + r;
         if (k < a.Kout) pl[(size_t)k * a.Ng + cn] = acc[i][j][r];
       }
     }
   }
 }
 
-// dw[k][c][r][s] (+)= sum over splits of part[sp][k][(r, s, c)] (c < Cin; padded channels dropped)
-__global__ void wgrad_nhwc_reduce_k(const float* __restrict__ part, float* __restrict__ dw, int splits, int Kout,
-                                    int Ng, int Ca, int Cin, int RS, int accumulate) {
-  const int64_t plane = (int64_t)Kout * Ng;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < plane; i += (int64_t)gridDim.x * 256) {
-    const int n = (int)(i % Ng), k = (int)(i / Ng);
-    const int rs = n / Ca, c = n - rs * Ca;
-    if (c >= Cin) continue;
-    float t[4] = {0.f, 0.f, 0.f, 0.f};
-    int sp = 0;
-    for (; sp + 4 <= splits; sp += 4)
+// dw[k][c][r][s] (+)= sum over splits of part[sp][k][(r, s, c)] (c < Cin; padded channels dropped).
+// Block = (256 / G) float4 column quads x G split groups: thread (q, g) sums splits g, g + G, ...
+// of its quad (float4 loads, 4 consecutive columns of one tap since Ca % 8 == 0), the G group
+// sums are combined in LDS in a fixed order (deterministic).  Many splits (the 56 x 56 layers
+// have ~200) are spread over the G groups instead of one thread's serial chain.
+__global__ __launch_bounds__(256) void wgrad_nhwc_reduce_k(const float* __restrict__ part, float* __restrict__ dw,
+                                                            int splits, int Kout, int Ng, int Ca, int Cin, int RS,
+                                                            int accumulate, int G) {
+  __shared__ float4 red[256];
+  const int plane4 = Kout * Ng / 4, QB = 256 / G;
+  const int q = threadIdx.x % QB, g = threadIdx.x / QB;
+  const int i = blockIdx.x * QB + q;
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  float4 t0 = make_float4(0.f, 0.f, 0.f, 0.f), t1 = t0;
+  if (i < plane4) {
+    int sp = g;
+    for (; sp + G < splits; sp += 2 * G) {
+      const float4 u = p4[(size_t)sp * plane4 + i], v = p4[(size_t)(sp + G) * plane4 + i];
+      t0.x += u.x; t0.y += u.y; t0.z += u.z; t0.w += u.w;
+      t1.x += v.x; t1.y += v.y; t1.z += v.z; t1.w += v.w;
+    }
+    if (sp < splits) {
+      const float4 u = p4[(size_t)sp * plane4 + i];
+      t0.x += u.x; t0.y += u.y; t0.z += u.z; t0.w += u.w;
+    }
+  }
+  red[threadIdx.x] = make_float4(t0.x + t1.x, t0.y + t1.y, t0.z + t1.z, t0.w + t1.w);
+  __syncthreads();
+  if (g != 0 || i >= plane4) return;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < G; ++k) {
+    const float4 r = red[k * QB + q];
+    v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+  }
+  const int e = 4 * i, k = e / Ng, n = e - k * Ng;
+  const int rs = n / Ca, c = n - rs * Ca;
+  float* d = dw + ((size_t)k * Cin + c) * RS + rs;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) t[u] += part[(sp + u) * plane + i];
-    for (; sp < splits; ++sp) t[0] += part[sp * plane + i];
-    const float v = (t[0] + t[1]) + (t[2] + t[3]);
-    float* d = dw + ((int64_t)k * Cin + c) * RS + rs;
-    *d = accumulate ? *d + v : v;
+  for (int j = 0; j < 4; ++j) {
+    if (c + j >= Cin) break;
+    d[(size_t)j * RS] = accumulate ? d[(size_t)j * RS] + v[j] : v[j];
   }
 }
 
@@ -1054,8 +1089,15 @@ void nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int
   launch_conv(a, scratch, st);
 }
 
+static void wgrad_tile(int K, int Ng, int& tm, int& tn) {
+  tm = K <= 64 ? 64 : 128;
+  tn = Ng <= 64 ? 64 : 128;
+}
+
 static int wgrad_splits(int Npix, int K, int Ng) {
-  const int tiles = cdiv(K, 128) * cdiv(Ng, 128);
+  int tm, tn;
+  wgrad_tile(K, Ng, tm, tn);
+  const int tiles = cdiv(K, tm) * cdiv(Ng, tn);
   // ~2 blocks per CU, >= 512 pixels (8 stages) per block, partial planes <= 32M floats
   int splits = std::max(1, cdiv(512, tiles));
   splits = std::min(splits, std::max(1, Npix / 512));
@@ -1096,12 +1138,22 @@ void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, in
   a.fPQ = FastDiv(P * Q);
   a.fCa = FastDiv(Cp);
   a.fS = FastDiv(S);
-  const int tiles = cdiv(K, 128) * cdiv(a.Ng, 128);
+  int tm, tn;
+  wgrad_tile(K, a.Ng, tm, tn);
+  const int tiles = cdiv(K, tm) * cdiv(a.Ng, tn);
   const int splits = wgrad_splits(a.Npix, K, a.Ng);
   a.chunk = cdiv(cdiv(a.Npix, splits), 64) * 64;
-  MX_LAUNCH(wgrad_nhwc_kernel, dim3(tiles * splits), dim3(256), 0, st, a);
-  MX_LAUNCH(wgrad_nhwc_reduce_k, dim3(grid_for((int64_t)K * a.Ng, 2048)), dim3(256), 0, st, scratch, dw, splits, K,
-            a.Ng, Cp, Cin, R * S, accumulate ? 1 : 0);
+  const dim3 grid(tiles * splits);
+  if (tm == 128 && tn == 128) MX_LAUNCH((wgrad_nhwc_kernel<128, 128>), grid, dim3(256), 0, st, a);
+  else if (tm == 128) MX_LAUNCH((wgrad_nhwc_kernel<128, 64>), grid, dim3(256), 0, st, a);
+  else if (tn == 128) MX_LAUNCH((wgrad_nhwc_kernel<64, 128>), grid, dim3(256), 0, st, a);
+  else MX_LAUNCH((wgrad_nhwc_kernel<64, 64>), grid, dim3(256), 0, st, a);
+  MX_CHECK((int64_t)K * a.Ng < (1ll << 31), "nhwc wgrad: weight too large for 32-bit indices");
+  int G = 1;  // split groups per reduce block: enough that each thread sums <= ~8 splits
+  while (G < 16 && G * 8 < splits) G *= 2;
+  const int plane4 = K * a.Ng / 4;
+  MX_LAUNCH(wgrad_nhwc_reduce_k, dim3(cdiv(plane4, 256 / G)), dim3(256), 0, st, scratch, dw, splits, K, a.Ng, Cp, Cin,
+            R * S, accumulate ? 1 : 0, G);
 }
 
 static dim3 bn_grid(int Npix, int C) {

@@ -32,6 +32,7 @@ CONV = [
     (2, 64, 14, 14, 128, 3, 2, 1),
     (2, 256, 8, 8, 512, 3, 2, 1),
     (3, 128, 12, 10, 64, 1, 2, 0),
+    (2, 64, 9, 11, 64, 1, 1, 0),     # 64 x 64 weight-gradient tile
 ]
 
 
