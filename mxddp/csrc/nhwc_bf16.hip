@@ -680,63 +680,82 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
 
 template <bool BWD>
 __global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
-  // block = 32 channels x 32 row groups; each thread sums every 32nd partial row (4 independent
-  // loads in flight), the 32 row-group sums are combined in a fixed order (deterministic)
-  constexpr int RG = 32;
-  __shared__ float red[2][RG][32];
-  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5, c = blockIdx.x * 32 + cl;
+  // block = 8 channels x 128 row groups: each thread sums <= gx / 128 (<= 8) partial rows with
+  // every load issued up front (one memory round trip, not a dependent chain), the 128 group
+  // sums are tree-combined in LDS in a fixed order (deterministic).  The per-channel inputs of
+  // the finalize (gamma, beta, running stats, x[0][c]) are loaded by the 8 owner threads before
+  // the reduction so their latency overlaps it.
+  constexpr int RG = 128, MAXR = 8;
+  __shared__ float red[2][RG][8];
+  const int cl = threadIdx.x & 7, rg = threadIdx.x >> 3, c = blockIdx.x * 8 + cl;
+  const bool cok = c < a.C;
   const size_t pitch = 2 * (size_t)a.C;
   float s1 = 0.f, s2 = 0.f;
-  if (c < a.C) {
-    float t1[4] = {0.f, 0.f, 0.f, 0.f}, t2[4] = {0.f, 0.f, 0.f, 0.f};
-    int b = rg;
-    for (; b + 3 * RG < a.gx; b += 4 * RG) {
+  if (cok) {
+    float t1[MAXR], t2[MAXR];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float* p = a.part + (size_t)(b + RG * u) * pitch + 2 * c;
-        t1[u] += p[0];
-        t2[u] += p[1];
+    for (int u = 0; u < MAXR; ++u) {
+      const int b = rg + RG * u;
+      const bool ok = b < a.gx;
+      const float* q = a.part + (size_t)(ok ? b : 0) * pitch + 2 * c;
+      t1[u] = ok ? q[0] : 0.f;
+      t2[u] = ok ? q[1] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < MAXR; ++u) {
+      s1 += t1[u];
+      s2 += t2[u];
+    }
+  }
+  // per-channel inputs of the finalize, fetched while the reduction runs
+  float gm = 1.f, bt = 0.f, rm = 0.f, rv = 0.f, K0 = 0.f, mu = 0.f, inv = 0.f, dg0 = 0.f, db0 = 0.f;
+  if (rg == 0 && cok) {
+    gm = a.gamma ? a.gamma[c] : 1.f;
+    if (!BWD) {
+      bt = a.beta ? a.beta[c] : 0.f;
+      rm = a.run_mean ? a.run_mean[c] : 0.f;
+      rv = a.run_var ? a.run_var[c] : 0.f;
+      K0 = bf2f(a.x[c]);
+    } else {
+      mu = a.mean[c];
+      inv = a.invstd[c];
+      if (a.acc_params) {
+        dg0 = a.dgamma ? a.dgamma[c] : 0.f;
+        db0 = a.dbeta ? a.dbeta[c] : 0.f;
       }
     }
-    for (; b < a.gx; b += RG) {
-      const float* p = a.part + (size_t)b * pitch + 2 * c;
-      t1[0] += p[0];
-      t2[0] += p[1];
-    }
-    s1 = (t1[0] + t1[1]) + (t1[2] + t1[3]);
-    s2 = (t2[0] + t2[1]) + (t2[2] + t2[3]);
   }
   red[0][rg][cl] = s1;
   red[1][rg][cl] = s2;
-  __syncthreads();
-  if (rg != 0 || c >= a.C) return;
-  s1 = 0.f;
-  s2 = 0.f;
 #pragma unroll
-  for (int k = 0; k < RG; ++k) {
-    s1 += red[0][k][cl];
-    s2 += red[1][k][cl];
+  for (int h = RG / 2; h > 0; h >>= 1) {
+    __syncthreads();
+    if (rg < h) {
+      red[0][rg][cl] += red[0][rg + h][cl];
+      red[1][rg][cl] += red[1][rg + h][cl];
+    }
   }
+  __syncthreads();
+  if (rg != 0 || !cok) return;
+  s1 = red[0][0][cl];
+  s2 = red[1][0][cl];
   const float cnt = (float)a.Npix;
-  if (!BWD && a.num_batches && c == 0) *a.num_batches += 1;
-  const float gm = a.gamma ? a.gamma[c] : 1.f;
   if (!BWD) {
-    const float K = bf2f(a.x[c]);
+    if (a.num_batches && c == 0) *a.num_batches += 1;
     const float m1 = s1 / cnt;
     const float var = fmaxf(s2 / cnt - m1 * m1, 0.f);
-    const float mean = K + m1, inv = rsqrtf(var + a.eps);
+    const float mean = K0 + m1, iv = rsqrtf(var + a.eps);
     a.mean[c] = mean;
-    a.invstd[c] = inv;
-    if (a.run_mean) a.run_mean[c] = (1.f - a.momentum) * a.run_mean[c] + a.momentum * mean;
-    if (a.run_var) a.run_var[c] = (1.f - a.momentum) * a.run_var[c] + a.momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
-    const float sc = inv * gm;
+    a.invstd[c] = iv;
+    if (a.run_mean) a.run_mean[c] = (1.f - a.momentum) * rm + a.momentum * mean;
+    if (a.run_var) a.run_var[c] = (1.f - a.momentum) * rv + a.momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
+    const float sc = iv * gm;
     a.coef[2 * c] = sc;
-    a.coef[2 * c + 1] = (a.beta ? a.beta[c] : 0.f) - mean * sc;
+    a.coef[2 * c + 1] = bt - mean * sc;
   } else {
-    const float inv = a.invstd[c], mu = a.mean[c];
     const float db = s1, dg = s2 * inv;
-    if (a.dgamma) a.dgamma[c] = a.acc_params ? a.dgamma[c] + dg : dg;
-    if (a.dbeta) a.dbeta[c] = a.acc_params ? a.dbeta[c] + db : db;
+    if (a.dgamma) a.dgamma[c] = dg0 + dg;
+    if (a.dbeta) a.dbeta[c] = db0 + db;
     // dx = k (cnt g - db - (x - mu) inv dg), k = gamma inv / cnt
     const float k = gm * inv / cnt;
     a.coef[3 * c] = k * cnt;
@@ -1160,6 +1179,7 @@ static dim3 bn_grid(int Npix, int C) {
   const int V = C / 8, vv = V >= kBnT ? kBnT : V, ppi = kBnT / vv;
   const int gy = V >= kBnT ? V / kBnT : 1;
   // ~1024 blocks in total (4 per CU), at least 8 pixel rows per thread
+  // (<= 1024 partial rows: the finalize reads at most 8 per thread x 128 row groups)
   const int gx = std::max(1, std::min(cdiv(Npix, ppi * 8), std::max(1, 1024 / gy)));
   return dim3(gx, gy);
 }
@@ -1196,7 +1216,7 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
   a.momentum = momentum;
   a.eps = eps;
   MX_LAUNCH(bn_nhwc_partial_k<false>, g, dim3(kBnT), 0, st, a);
-  MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 32)), dim3(1024), 0, st, a);
+  MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
   MX_LAUNCH(bn_nhwc_apply_k, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));
 }
@@ -1227,7 +1247,7 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
   a.relu = relu;
   a.acc_params = accumulate_params;
   MX_LAUNCH(bn_nhwc_partial_k<true>, g, dim3(kBnT), 0, st, a);
-  MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 32)), dim3(1024), 0, st, a);
+  MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
   MX_LAUNCH(bn_nhwc_bwd_apply_k, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));
 }
