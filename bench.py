@@ -24,6 +24,17 @@ import time
 
 METRIC = "images/sec (whole node) MNIST CNN DDP at 1/2/4/8 MI355X; scaling efficiency"
 BASELINE_VALUE = None  # BASELINE.json "published": {} -- no MNIST number exists upstream
+# secondary models: their own metric names (the headline METRIC is the default mnist_cnn run)
+MODEL_METRIC = {
+    "resnet50": "images/sec (whole node) ResNet-50 synthetic-ImageNet DDP (BASELINE config 5)",
+    "pyramidnet110": "images/sec (whole node) PyramidNet-110 CIFAR-10 DDP (reference pytorch/README.md benchmark)",
+    "keras_cnn": "images/sec (whole node) Keras MNIST CNN (reference tensorflow2/) on the mxddp layers path",
+    "mlp": "images/sec (whole node) Chainer MNIST MLP (reference chainer/) on the mxddp layers path",
+}
+
+
+def _metric(model: str) -> str:
+    return MODEL_METRIC.get(model, METRIC)
 
 
 def parse():
@@ -123,7 +134,7 @@ def main():
         total_imgs = a.gpus * B * a.steps
         value = total_imgs / dt
         out = {
-            "metric": METRIC,
+            "metric": _metric(a.model),
             "value": round(value, 1),
             "unit": "images/sec",
             "n_gpus": a.gpus,
@@ -200,7 +211,7 @@ def _replica(a):
     dt = time.perf_counter() - t0
     value = B * a.steps / dt
     print(json.dumps({
-        "metric": METRIC, "value": round(value, 1), "unit": "images/sec", "n_gpus": a.gpus, "steps": a.steps,
+        "metric": _metric(a.model), "value": round(value, 1), "unit": "images/sec", "n_gpus": a.gpus, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": a.dtype, "data": _data_desc(spec),
         "config": {"model": a.model, "global_batch": B, "per_rank_batch": a.batch, "seq_len": None,
