@@ -85,9 +85,12 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
   // operand load is a per-lane base plus a uniform offset (a few VALU per load instead of two
   // divisions and a 64-bit address per load).
   // BK = 64 (two MFMA k-steps per stage) keeps each stage's MFMA phase long enough to cover the
-  // next stage's global loads; LDS rows of 72 bf16 = 144 B = 9 x 16 B (odd) -> the 16 rows read
-  // by a 16-lane group hit 16 distinct 16-byte slots.
-  constexpr int BK = 64, LD = BK + 8;
+  // next stage's global loads.  LDS rows of 80 bf16 = 160 B = 10 x 16 B: a ds_read_b128 lane group
+  // ({0-3,12-15,20-27}, ... : 8 rows at one 16-B column and 8 rows at the next) then hits 16
+  // distinct 16-byte bank slots (conflict-free, found by enumerating pitches against the
+  // gfx950 lane groups); the 144-B pitch it replaces was conflict-free only for plain 16-row
+  // groups and measured more bank-conflict cycles than LDS-active cycles.
+  constexpr int BK = 64, LD = BK + 16;
   constexpr int EA = TM * 8 / 256, EB = TN * 8 / 256;  // 16-byte vectors per thread per stage
   constexpr int WMT = TM / 32, WNT = TN / 32;           // 16x16 MFMA tiles per wave (wave tile = TM/2 x TN/2)
   __shared__ __attribute__((aligned(16))) bf16 As[2][TM * LD];

@@ -29,9 +29,17 @@ def main():
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
 
-    with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
         run(1)
         torch.cuda.synchronize()
+    # device-side events: memcpy / memset / copy kernels, with the CPU op that issued them
+    dev = Counter()
+    for ev in prof.events():
+        n = ev.name.lower()
+        if ("memcpy" in n or "memset" in n or "copy" in n) and ev.device_type.name == "CUDA":
+            dev[ev.name] += 1
+    print("device events:", dict(dev))
+    print(prof.key_averages(group_by_stack_n=6).table(sort_by="count", row_limit=25, max_name_column_width=60))
     cnt = Counter()
     for ev in prof.events():
         if ev.name in ("aten::copy_", "aten::add", "aten::add_", "aten::zero_", "aten::fill_", "aten::clone",
