@@ -78,8 +78,10 @@ struct ConvNArgs {
   FastDiv fOW, fOHW, fCa, fS, fWc, fHWc;
 };
 
+// __launch_bounds__(256, 2): at least two waves per SIMD (<= 256 VGPRs); the LDS tiles allow two
+// 256-thread blocks per CU anyway, so a larger register budget would only lose occupancy
 template <int TM, int TN, bool kWide>
-__global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
+__global__ __launch_bounds__(256, 2) void conv_nhwc_kernel(ConvNArgs a) {
   // kWide (Ca % 64 == 0, every ResNet layer but the 8-channel stem): the 64 k of a stage lie in
   // ONE filter tap (r, s), so the tap decomposition is a per-stage scalar and each 16-byte
   // operand load is a per-lane base plus a uniform offset (a few VALU per load instead of two
@@ -135,7 +137,9 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
       pow_[i] = rem - poh[i] * a.OW;
     }
   }
-  u32x4 ra[EA], rb[EB];
+  // two register stages: the loads of k-tile t + 2 are issued while tile t is computed, so each
+  // has a whole compute phase plus a barrier to land (one stage hid L2 latency only)
+  u32x4 ra0[EA], rb0[EB], ra1[EA], rb1[EB];  // (set 1 unused by the one-stage 128 x 128 tile)
   const u32x4 z4 = {0u, 0u, 0u, 0u};
   // wide path: per-lane byte bases (loop invariant)
   uint32_t abase[EA], pbase[EB];
@@ -150,7 +154,7 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
       iwb[i] = a.dgrad ? pow_[i] + a.pw : pow_[i] * a.sw - a.pw;
     }
   }
-  auto gload = [&](int k0) {
+  auto gload = [&](int k0, u32x4 (&ra)[EA], u32x4 (&rb)[EB]) {
     if constexpr (kWide) {
       const int rs = (int)a.fCa.div((uint32_t)k0), c0 = k0 - rs * a.Ca;  // uniform
       int r, s, kw = k0;
@@ -215,7 +219,7 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
                  : z4;
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, const u32x4 (&ra)[EA], const u32x4 (&rb)[EB]) {
 #pragma unroll
     for (int i = 0; i < EA; ++i) *reinterpret_cast<u32x4*>(&As[buf][(row0 + 32 * i) * LD + 8 * kv]) = ra[i];
 #pragma unroll
@@ -232,14 +236,7 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
   // nt <= 0: a split (or a parity class without taps) with nothing to reduce writes zeros
   const int nt = min((Kgc + BK - 1) / BK - kt0, a.kt_per_split);
   const int a_row = wm * (TM / 2) + (lane & 15), b_row = wn * (TN / 2) + (lane & 15), koff = 8 * (lane >> 4);
-  if (nt > 0) {
-    gload(kt0 * BK);
-    sstore(0);
-  }
-  __syncthreads();
-  for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nt) gload((kt0 + t + 1) * BK);
+  auto compute = [&](int cur) {
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8 av[WMT], bv[WNT];
@@ -255,8 +252,42 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(ConvNArgs a) {
         for (int j = 0; j < WNT; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
-    if (t + 1 < nt) sstore(cur ^ 1);
+  };
+  if constexpr (TM * TN <= 64 * 128) {
+    if (nt > 0) {
+      gload(kt0 * BK, ra0, rb0);
+      if (nt > 1) gload((kt0 + 1) * BK, ra1, rb1);
+      sstore(0, ra0, rb0);
+    }
     __syncthreads();
+    // unrolled by two so each register stage is a compile-time array (runtime-indexed register
+    // arrays would go to scratch): even steps compute buffer 0 and hold stage set 1, odd steps
+    // the reverse
+    for (int t = 0; t < nt; t += 2) {
+      if (t + 2 < nt) gload((kt0 + t + 2) * BK, ra0, rb0);
+      compute(0);
+      if (t + 1 < nt) sstore(1, ra1, rb1);
+      __syncthreads();
+      if (t + 1 >= nt) break;
+      if (t + 3 < nt) gload((kt0 + t + 3) * BK, ra1, rb1);
+      compute(1);
+      if (t + 2 < nt) sstore(0, ra0, rb0);
+      __syncthreads();
+    }
+  } else {
+    // 128 x 128: one register stage (two would exceed 256 VGPRs and spill)
+    if (nt > 0) {
+      gload(kt0 * BK, ra0, rb0);
+      sstore(0, ra0, rb0);
+    }
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+      const int cur = t & 1;
+      if (t + 1 < nt) gload((kt0 + t + 1) * BK, ra0, rb0);
+      compute(cur);
+      if (t + 1 < nt) sstore(cur ^ 1, ra0, rb0);
+      __syncthreads();
+    }
   }
 
   // C/D: row (output channel) = 4 * (lane >> 4) + r, column (pixel) = lane & 15
