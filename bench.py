@@ -276,11 +276,7 @@ def _layers_or_torch(a, torch, inf, dev, comm, B):
     amp = (torch.autocast("cuda", dtype=torch.bfloat16) if (a.impl == "torch" and a.dtype == "bf16")
            else contextlib.nullcontext())
 
-    from mxddp import ops as _mx_ops
-
     def step():
-        if a.impl == "layers":
-            _mx_ops.bn_reset_accumulators()  # graph replays start from the captured BN state
         Cn.synth_batch(x.data_ptr(), y.data_ptr(), tmpl.data_ptr(), B, D, nc, a.seed + inf.rank, ctr.data_ptr(),
                        torch.cuda.current_stream(dev).cuda_stream)
         opt.zero_grad()

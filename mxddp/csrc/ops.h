@@ -110,21 +110,21 @@ void xent_fwd_bwd(const float* logits, const int32_t* y, float* logp, float* dlo
                   float* loss_sum, float* correct, int B, int C, float grad_scale, hipStream_t st);
 
 // BatchNorm2d (training): batch stats, running-stat update, normalise (+ optional ReLU).
-// Split reduction (ops_bn.hip) into per-channel accumulators acc[C][2] that must be zero on
-// entry; the elementwise pass zeroes acc_next[hiwater][2] for the following call (double
-// buffering: alternate the two buffers between consecutive calls on the same stream; hiwater =
-// the largest C used on the pair so far).
+// Split reduction (ops_bn.hip): S x C workgroups write partial sums to `part`
+// (bn_partial_floats(N, C, HW) floats, fully rewritten by every call), the elementwise pass sums
+// its channel's partials in a fixed order (deterministic, no atomics).
 int bn_splits(int N, int C, int HW);
+size_t bn_partial_floats(int N, int C, int HW);
 void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* y, float* mean,
                   float* invstd, float* run_mean, float* run_var, int N, int C, int HW,
-                  float momentum, float eps, bool relu, float* acc, float* acc_next, int hiwater,
-                  hipStream_t st, int64_t* num_batches = nullptr);  // num_batches: += 1 on device
+                  float momentum, float eps, bool relu, float* part, hipStream_t st,
+                  int64_t* num_batches = nullptr);  // num_batches: += 1 on device
 void bn_fwd_eval(const float* x, const float* gamma, const float* beta, float* y,
                  const float* run_mean, const float* run_var, int N, int C, int HW, float eps,
                  bool relu, hipStream_t st);
 void bn_bwd(const float* dy, const float* x, const float* y_relu, const float* gamma,
             const float* mean, const float* invstd, float* dx, float* dgamma, float* dbeta, int N,
-            int C, int HW, bool accumulate_params, float* acc, float* acc_next, int hiwater, hipStream_t st);
+            int C, int HW, bool accumulate_params, float* part, hipStream_t st);
 
 // PyramidNet shortcut: y[n,c,:,:] += (c < Cin ? pool(x)[n,c] : 0); pool = 2x2 avg, ceil.
 void shortcut_pad_add(const float* x, float* y, int N, int Cin, int H, int W, int Cout, int P, int Q,

@@ -3,18 +3,12 @@
 // A block-per-channel BN launches only C workgroups (16..271 for PyramidNet, 64..2048 for
 // ResNet-50) on a 256-CU part and walks each channel serially.  Here every channel's N*HW
 // elements are split over S workgroups (grid = S x C, S chosen so the grid has >= ~2048
-// workgroups), each reducing its slice with float4 loads and adding its two partial sums into
-// per-channel accumulators with device-scope float atomics (2 atomics per workgroup).  The
-// second, elementwise launch uses the same S x C grid: each block derives its channel's
-// statistics from the accumulators once and applies the affine map (forward) or the dx
-// formula (backward) to its slice.
-//
-// No inter-workgroup fences: a last-arriver scheme needs a device-scope release per workgroup,
-// which on a multi-XCD part writes back the XCD's L2 and cost 2-3x the whole reduction.  The
-// accumulators are double-buffered instead: call k reduces into buffer k%2 (zero), and its
-// elementwise kernel re-zeroes the OTHER buffer for call k+1 (stream order makes this safe) --
-// every channel up to `hiwater`, the widest C any call has used on these buffers, since an
-// earlier wider call may have left channels >= C dirty.
+// workgroups), each reducing its slice with float4 loads and WRITING its two partial sums to
+// part[c][s][2].  The second, elementwise launch uses the same S x C grid: each block first sums
+// its channel's S partials (a block reduction in a fixed order: deterministic, and no
+// same-address float atomics, which serialise at ~50 ns per arrival across the XCDs), then
+// applies the affine map (forward) or the dx formula (backward) to its slice.  The partials are
+// fully rewritten by every call, so a captured graph replays with no reset.
 //
 // Numerics: forward partials are sums of (x - K) and (x - K)^2 with a per-channel shift
 // K = x[0, c, 0, 0] (identical in every split), which keeps E[x^2] - E[x]^2 well conditioned
@@ -50,6 +44,17 @@ __device__ __forceinline__ float2 block_sum2(float a, float b, float* red) {
   return t;
 }
 
+// sum of channel c's S partial pairs (S <= 4 x kBnTB), fixed order; every thread gets the result
+__device__ __forceinline__ float2 channel_sums(const float* __restrict__ part, int c, int S, float* red) {
+  float a = 0.f, b = 0.f;
+  for (int t = threadIdx.x; t < S; t += kBnTB) {
+    const float2 v = reinterpret_cast<const float2*>(part)[(size_t)c * S + t];
+    a += v.x;
+    b += v.y;
+  }
+  return block_sum2(a, b, red);
+}
+
 // Slice of channel c handled by workgroup s: images [n0, n1), all HW.
 struct Slice {
   int n0, n1;
@@ -62,7 +67,7 @@ __device__ __forceinline__ Slice slice_of(int s, int S, int N) {
 // ------------------------------------------------------------------ forward statistics
 template <bool VEC>
 __global__ __launch_bounds__(kBnTB) void bn_stats_k(const float* __restrict__ x, int N, int C, int HW, int S, FastDiv dv,
-                                                    float* __restrict__ acc) {
+                                                    float* __restrict__ part) {
   __shared__ float red[2 * kBnTB / 64];
   const int s = blockIdx.x, c = blockIdx.y;
   const Slice sl = slice_of(s, S, N);
@@ -88,22 +93,7 @@ __global__ __launch_bounds__(kBnTB) void bn_stats_k(const float* __restrict__ x,
     }
   }
   const float2 t = block_sum2(s1, s2, red);
-  if (threadIdx.x == 0) {
-    atomicAdd(acc + 2 * c, t.x);
-    atomicAdd(acc + 2 * c + 1, t.y);
-  }
-}
-
-// Per-channel statistic helpers shared by the elementwise kernels.
-struct FwdStat {
-  float mean, inv;
-};
-__device__ __forceinline__ FwdStat fwd_stat(const float* __restrict__ x, const float* __restrict__ acc, int c, int HW,
-                                            float cnt, float eps) {
-  const float K = x[(size_t)c * HW];
-  const float m1 = acc[2 * c] / cnt;
-  const float var = fmaxf(acc[2 * c + 1] / cnt - m1 * m1, 0.f);
-  return FwdStat{K + m1, rsqrtf(var + eps)};
+  if (threadIdx.x == 0) reinterpret_cast<float2*>(part)[(size_t)c * S + s] = t;
 }
 
 // ------------------------------------------------------------------ backward
@@ -112,7 +102,7 @@ template <bool VEC>
 __global__ __launch_bounds__(kBnTB) void bn_bwd_reduce_k(const float* __restrict__ dy, const float* __restrict__ x,
                                                          const float* __restrict__ yr, const float* __restrict__ mean,
                                                          int N, int C, int HW, int S, FastDiv dv,
-                                                         float* __restrict__ acc) {
+                                                         float* __restrict__ part) {
   __shared__ float red[2 * kBnTB / 64];
   const int s = blockIdx.x, c = blockIdx.y;
   const Slice sl = slice_of(s, S, N);
@@ -148,10 +138,7 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_reduce_k(const float* __restrict
     }
   }
   const float2 t = block_sum2(s1, s2, red);
-  if (threadIdx.x == 0) {
-    atomicAdd(acc + 2 * c, t.x);
-    atomicAdd(acc + 2 * c + 1, t.y);
-  }
+  if (threadIdx.x == 0) reinterpret_cast<float2*>(part)[(size_t)c * S + s] = t;
 }
 
 // Elementwise passes: grid (S, C) exactly like the reductions, so every block works on one
@@ -162,36 +149,27 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_reduce_k(const float* __restrict
 // channel's statistics / dgamma / dbeta and zeroes channel c of the next call's accumulator.
 template <bool VEC>
 __global__ __launch_bounds__(kBnTB) void bn_apply_slice_k(const float* __restrict__ x, const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, const float* __restrict__ acc,
-                                                          float* __restrict__ acc_next, float* __restrict__ mean_out,
-                                                          float* __restrict__ invstd_out, float* __restrict__ run_mean,
-                                                          float* __restrict__ run_var, float* __restrict__ y, int N,
-                                                          int C, int HW, int S, FastDiv dv, float cnt, float eps,
-                                                          float momentum, int relu, int hiwater,
+                                                          const float* __restrict__ beta, const float* __restrict__ part,
+                                                          float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                                                          float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                          float* __restrict__ y, int N, int C, int HW, int S, FastDiv dv,
+                                                          float cnt, float eps, float momentum, int relu,
                                                           int64_t* __restrict__ num_batches) {
+  __shared__ float red[2 * kBnTB / 64];
   const int s = blockIdx.x, c = blockIdx.y;
-  if (s == 0 && c == 0) {
-    for (int k = 2 * C + threadIdx.x; k < 2 * hiwater; k += kBnTB) acc_next[k] = 0.f;
-    if (num_batches && threadIdx.x == 0) *num_batches += 1;
-  }
-  const FwdStat st = fwd_stat(x, acc, c, HW, cnt, eps);
-  const float sc = st.inv * (gamma ? gamma[c] : 1.f);
-  const float sh = (beta ? beta[c] : 0.f) - st.mean * sc;
+  if (s == 0 && c == 0 && num_batches && threadIdx.x == 0) *num_batches += 1;
+  const float K = x[(size_t)c * HW];  // the statistics kernel's shift
+  const float2 t = channel_sums(part, c, S, red);
+  const float m1 = t.x / cnt;
+  const float var = fmaxf(t.y / cnt - m1 * m1, 0.f);
+  const float mu = K + m1, inv = rsqrtf(var + eps);
+  const float sc = inv * (gamma ? gamma[c] : 1.f);
+  const float sh = (beta ? beta[c] : 0.f) - mu * sc;
   if (s == 0 && threadIdx.x == 0) {
-    mean_out[c] = st.mean;
-    invstd_out[c] = st.inv;
-    if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * st.mean;
-    if (run_var) {
-      const float m1 = acc[2 * c] / cnt;
-      const float var = fmaxf(acc[2 * c + 1] / cnt - m1 * m1, 0.f);
-      run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
-    }
-  }
-  // every block of channel c has read acc[2c] (above) before block 0 of the NEXT call zeroes it
-  // (stream order); acc_next is only zeroed here, never read
-  if (s == 0 && threadIdx.x == 0) {
-    acc_next[2 * c] = 0.f;
-    acc_next[2 * c + 1] = 0.f;
+    mean_out[c] = mu;
+    invstd_out[c] = inv;
+    if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
+    if (run_var) run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
   }
   const Slice sl = slice_of(s, S, N);
   if (VEC) {
@@ -228,20 +206,18 @@ template <bool VEC>
 __global__ __launch_bounds__(kBnTB) void bn_bwd_apply_slice_k(
     const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ yr,
     const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
-    const float* __restrict__ acc, float* __restrict__ acc_next, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    float* __restrict__ dx, int N, int C, int HW, int S, FastDiv dv, float cnt, int acc_params, int hiwater) {
+    const float* __restrict__ part, float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dx, int N,
+    int C, int HW, int S, FastDiv dv, float cnt, int acc_params) {
+  __shared__ float red[2 * kBnTB / 64];
   const int s = blockIdx.x, c = blockIdx.y;
-  if (s == 0 && c == 0)
-    for (int k = 2 * C + threadIdx.x; k < 2 * hiwater; k += kBnTB) acc_next[k] = 0.f;
   const float inv = invstd[c], mu = mean[c];
-  const float db = acc[2 * c], dg = acc[2 * c + 1] * inv;
+  const float2 t = channel_sums(part, c, S, red);
+  const float db = t.x, dg = t.y * inv;
   const float k = (gamma ? gamma[c] : 1.f) * inv / cnt;
   const float A = k * cnt, D = -k * dg * inv, Bc = -k * db + k * dg * inv * mu;
   if (s == 0 && threadIdx.x == 0) {
     if (dgamma) dgamma[c] = acc_params ? dgamma[c] + dg : dg;
     if (dbeta) dbeta[c] = acc_params ? dbeta[c] + db : db;
-    acc_next[2 * c] = 0.f;
-    acc_next[2 * c + 1] = 0.f;
   }
   const Slice sl = slice_of(s, S, N);
   if (VEC) {
@@ -292,43 +268,45 @@ int bn_splits(int N, int C, int HW) {
   return (N + per - 1) / per;
 }
 
+size_t bn_partial_floats(int N, int C, int HW) { return 2 * (size_t)bn_splits(N, C, HW) * C; }
+
 void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* invstd,
                   float* run_mean, float* run_var, int N, int C, int HW, float momentum, float eps, bool relu,
-                  float* acc, float* acc_next, int hiwater, hipStream_t st, int64_t* num_batches) {
+                  float* part, hipStream_t st, int64_t* num_batches) {
   MX_CHECK((int64_t)N * C * HW < (1ll << 31), "bn: tensor too large for 32-bit index math");
   const int S = bn_splits(N, C, HW);
+  MX_CHECK(S <= 4 * kBnTB, "bn: too many splits");
   const bool vec = HW % 4 == 0;
-  const FastDiv dv(vec ? HW / 4 : HW), dc(C);
-  const int64_t total = (int64_t)N * C * HW;
+  const FastDiv dv(vec ? HW / 4 : HW);
   const float cnt = (float)N * (float)HW;
   if (vec) {
-    MX_LAUNCH(bn_stats_k<true>, dim3(S, C), dim3(kBnTB), 0, st, x, N, C, HW, S, dv, acc);
-    MX_LAUNCH(bn_apply_slice_k<true>, dim3(S, C), dim3(kBnTB), 0, st, x, gamma, beta, acc, acc_next, mean, invstd,
-              run_mean, run_var, y, N, C, HW, S, dv, cnt, eps, momentum, relu ? 1 : 0, hiwater, num_batches);
+    MX_LAUNCH(bn_stats_k<true>, dim3(S, C), dim3(kBnTB), 0, st, x, N, C, HW, S, dv, part);
+    MX_LAUNCH(bn_apply_slice_k<true>, dim3(S, C), dim3(kBnTB), 0, st, x, gamma, beta, part, mean, invstd, run_mean,
+              run_var, y, N, C, HW, S, dv, cnt, eps, momentum, relu ? 1 : 0, num_batches);
   } else {
-    MX_LAUNCH(bn_stats_k<false>, dim3(S, C), dim3(kBnTB), 0, st, x, N, C, HW, S, dv, acc);
-    MX_LAUNCH(bn_apply_slice_k<false>, dim3(S, C), dim3(kBnTB), 0, st, x, gamma, beta, acc, acc_next, mean, invstd,
-              run_mean, run_var, y, N, C, HW, S, dv, cnt, eps, momentum, relu ? 1 : 0, hiwater, num_batches);
+    MX_LAUNCH(bn_stats_k<false>, dim3(S, C), dim3(kBnTB), 0, st, x, N, C, HW, S, dv, part);
+    MX_LAUNCH(bn_apply_slice_k<false>, dim3(S, C), dim3(kBnTB), 0, st, x, gamma, beta, part, mean, invstd, run_mean,
+              run_var, y, N, C, HW, S, dv, cnt, eps, momentum, relu ? 1 : 0, num_batches);
   }
 }
 
 void bn_bwd(const float* dy, const float* x, const float* y_relu, const float* gamma, const float* mean,
-            const float* invstd, float* dx, float* dgamma, float* dbeta, int N, int C, int HW, bool accp, float* acc,
-            float* acc_next, int hiwater, hipStream_t st) {
+            const float* invstd, float* dx, float* dgamma, float* dbeta, int N, int C, int HW, bool accp, float* part,
+            hipStream_t st) {
   MX_CHECK((int64_t)N * C * HW < (1ll << 31), "bn: tensor too large for 32-bit index math");
   const int S = bn_splits(N, C, HW);
+  MX_CHECK(S <= 4 * kBnTB, "bn: too many splits");
   const bool vec = HW % 4 == 0;
-  const FastDiv dv(vec ? HW / 4 : HW), dc(C);
-  const int64_t total = (int64_t)N * C * HW;
+  const FastDiv dv(vec ? HW / 4 : HW);
   const float cnt = (float)N * (float)HW;
   if (vec) {
-    MX_LAUNCH(bn_bwd_reduce_k<true>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, mean, N, C, HW, S, dv, acc);
-    MX_LAUNCH(bn_bwd_apply_slice_k<true>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, gamma, mean, invstd, acc,
-              acc_next, dgamma, dbeta, dx, N, C, HW, S, dv, cnt, accp ? 1 : 0, hiwater);
+    MX_LAUNCH(bn_bwd_reduce_k<true>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, mean, N, C, HW, S, dv, part);
+    MX_LAUNCH(bn_bwd_apply_slice_k<true>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, gamma, mean, invstd, part,
+              dgamma, dbeta, dx, N, C, HW, S, dv, cnt, accp ? 1 : 0);
   } else {
-    MX_LAUNCH(bn_bwd_reduce_k<false>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, mean, N, C, HW, S, dv, acc);
-    MX_LAUNCH(bn_bwd_apply_slice_k<false>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, gamma, mean, invstd, acc,
-              acc_next, dgamma, dbeta, dx, N, C, HW, S, dv, cnt, accp ? 1 : 0, hiwater);
+    MX_LAUNCH(bn_bwd_reduce_k<false>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, mean, N, C, HW, S, dv, part);
+    MX_LAUNCH(bn_bwd_apply_slice_k<false>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, gamma, mean, invstd, part,
+              dgamma, dbeta, dx, N, C, HW, S, dv, cnt, accp ? 1 : 0);
   }
 }
 

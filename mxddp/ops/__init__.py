@@ -346,10 +346,10 @@ class _BatchNorm(torch.autograd.Function):
         if training:
             mean = torch.empty((Cc,), device=x.device, dtype=torch.float32)
             invstd = torch.empty_like(mean)
-            acc, acc_next, hi = _bn_acc(x.device, "fwd", Cc)
+            part = _bn_part(x.device, C.bn_partial_floats(N, Cc, HW))
             C.bn_fwd_train(x.data_ptr(), _p(gamma), _p(beta), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
                            _p(running_mean), _p(running_var), N, Cc, HW, float(momentum), float(eps), bool(relu),
-                           acc.data_ptr(), acc_next.data_ptr(), hi, st, _p(num_batches))
+                           part.data_ptr(), st, _p(num_batches))
         else:
             mean = running_mean
             invstd = (running_var + eps).rsqrt()
@@ -375,10 +375,9 @@ class _BatchNorm(torch.autograd.Function):
         else:
             dg = torch.empty((Cc,), device=x.device) if ctx.has_affine else None
             db = torch.empty((Cc,), device=x.device) if ctx.has_affine else None
-        acc, acc_next, hi = _bn_acc(x.device, "bwd", Cc)
+        part = _bn_part(x.device, native().bn_partial_floats(N, Cc, HW))
         native().bn_bwd(dy.data_ptr(), x.data_ptr(), _p(y), _p(gamma), mean.data_ptr(), invstd.data_ptr(),
-                        dx.data_ptr(), _p(dg), _p(db), N, Cc, HW, direct, acc.data_ptr(), acc_next.data_ptr(), hi,
-                        stream_of(dy))
+                        dx.data_ptr(), _p(dg), _p(db), N, Cc, HW, direct, part.data_ptr(), stream_of(dy))
         if direct:
             _grad_done(g_ref)
             _grad_done(b_ref)
@@ -386,32 +385,19 @@ class _BatchNorm(torch.autograd.Function):
         return dx, dg, db, None, None, None, None, None, None, None
 
 
-_BN_ACC: dict = {}
+_BN_PART: dict = {}
 
 
-def _bn_acc(device, kind, C):
-    """Double-buffered per-channel accumulators of the split-reduction BN kernels (ops_bn.hip):
-    call k reduces into buffer k%2 (zero) and re-zeroes the other one for call k+1, up to the
-    widest C used so far ("hiwater").  One pair per (device, fwd|bwd); calls are stream-ordered
-    on the device's current stream."""
-    key = (device, kind)
-    st = _BN_ACC.get(key)
-    if st is None or st[0].shape[1] < 2 * C:
-        st = [torch.zeros((2, 2 * max(C, 4096)), dtype=torch.float32, device=device), 0, 0]
-        _BN_ACC[key] = st
-    buf, p, hi = st
-    hi = max(hi, C)
-    st[1], st[2] = p ^ 1, hi
-    return buf[p], buf[p ^ 1], hi
-
-
-def bn_reset_accumulators() -> None:
-    """Zero the BN accumulator pairs and restart their double-buffer parity.  Call at the start
-    of a step that is captured in a HIP graph: a replay then starts from the same accumulator
-    state as the capture did, whatever the number of BN calls per step."""
-    for st in _BN_ACC.values():
-        st[0].zero_()
-        st[1] = 0
+def _bn_part(device, n):
+    """Partial-sum scratch of the split-reduction BN kernels (ops_bn.hip), one per device: every
+    call rewrites what it reads and BN calls are stream-ordered, so one buffer serves them all
+    (and a captured graph replays without any reset).  Grows only, so captured pointers stay
+    valid once the warm-up has seen the widest layer."""
+    buf = _BN_PART.get(device)
+    if buf is None or buf.numel() < n:
+        buf = torch.empty((max(n, 8192),), dtype=torch.float32, device=device)
+        _BN_PART[device] = buf
+    return buf
 
 
 def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum=0.1, eps=1e-5, relu=False,
