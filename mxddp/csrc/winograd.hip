@@ -618,32 +618,42 @@ __global__ __launch_bounds__(256, 3) void wino_wgrad_kernel(WinoWArgs a) {
   }
 }
 
-// dw (+)= sum over nblk partial planes (fixed order -> deterministic).  float4 lanes, four
-// independent partial sums so the loads of four planes are in flight at once.
-__global__ void wino_wgrad_reduce_k(const float* __restrict__ part, float* __restrict__ dw, int64_t plane,
-                                    int64_t pstride, int nblk, int accumulate) {
+// dw (+)= sum over nblk partial planes (fixed order -> deterministic).  Block = (256 / G) float4
+// quads x G plane groups: thread (q, g) sums planes g, g + G, ... of its quad (two independent
+// partial sums), the G group sums are combined in LDS in a fixed order.  Small PyramidNet layers
+// have ~200 planes: spreading them over G groups replaces one thread's ~50 dependent memory
+// round trips by a few.
+__global__ __launch_bounds__(256) void wino_wgrad_reduce_k(const float* __restrict__ part, float* __restrict__ dw,
+                                                            int64_t plane, int64_t pstride, int nblk, int accumulate,
+                                                            int G) {
   // partial plane b starts at part + b * pstride (pstride = plane rounded up to 4 floats)
+  __shared__ float4 red[256];
   const int64_t n4 = plane >> 2, s4 = pstride >> 2;
+  const int QB = 256 / G, q = threadIdx.x % QB, g = threadIdx.x / QB;
+  const int64_t i = (int64_t)blockIdx.x * QB + q;
   const float4* p4 = reinterpret_cast<const float4*>(part);
-  float4* d4 = reinterpret_cast<float4*>(dw);
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    float4 s[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) s[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    int b = 0;
-    for (; b + 4 <= nblk; b += 4) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float4 v = p4[(b + u) * s4 + i];
-        s[u].x += v.x; s[u].y += v.y; s[u].z += v.z; s[u].w += v.w;
-      }
+  float4 t0 = make_float4(0.f, 0.f, 0.f, 0.f), t1 = t0;
+  if (i < n4) {
+    int b = g;
+    for (; b + G < nblk; b += 2 * G) {
+      const float4 u = p4[b * s4 + i], v = p4[(b + G) * s4 + i];
+      t0.x += u.x; t0.y += u.y; t0.z += u.z; t0.w += u.w;
+      t1.x += v.x; t1.y += v.y; t1.z += v.z; t1.w += v.w;
     }
-    for (; b < nblk; ++b) {
-      const float4 v = p4[b * s4 + i];
-      s[0].x += v.x; s[0].y += v.y; s[0].z += v.z; s[0].w += v.w;
+    if (b < nblk) {
+      const float4 u = p4[b * s4 + i];
+      t0.x += u.x; t0.y += u.y; t0.z += u.z; t0.w += u.w;
     }
-    float4 r = make_float4((s[0].x + s[1].x) + (s[2].x + s[3].x), (s[0].y + s[1].y) + (s[2].y + s[3].y),
-                           (s[0].z + s[1].z) + (s[2].z + s[3].z), (s[0].w + s[1].w) + (s[2].w + s[3].w));
+  }
+  red[threadIdx.x] = make_float4(t0.x + t1.x, t0.y + t1.y, t0.z + t1.z, t0.w + t1.w);
+  __syncthreads();
+  if (g == 0 && i < n4) {
+    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < G; ++k) {
+      const float4 v = red[k * QB + q];
+      r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+    }
+    float4* d4 = reinterpret_cast<float4*>(dw);
     if (accumulate) {
       const float4 o = d4[i];
       r.x += o.x; r.y += o.y; r.z += o.z; r.w += o.w;
@@ -652,10 +662,10 @@ __global__ void wino_wgrad_reduce_k(const float* __restrict__ part, float* __res
   }
   // tail (plane % 4), one thread
   if (blockIdx.x == 0 && threadIdx.x == 0)
-    for (int64_t i = n4 << 2; i < plane; ++i) {
-      float t = accumulate ? dw[i] : 0.f;
-      for (int b = 0; b < nblk; ++b) t += part[b * pstride + i];
-      dw[i] = t;
+    for (int64_t k = n4 << 2; k < plane; ++k) {
+      float t = accumulate ? dw[k] : 0.f;
+      for (int b = 0; b < nblk; ++b) t += part[b * pstride + k];
+      dw[k] = t;
     }
 }
 
@@ -832,8 +842,12 @@ void wino_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, 
                 st, scratch, dw, plane, pstride, p.nblk, accumulate ? 1 : 0);
       return;
     }
-    MX_LAUNCH(wino_wgrad_reduce_k, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((plane / 4 + 255) / 256, 2048))),
-              dim3(256), 0, st, scratch, dw, plane, pstride, p.nblk, accumulate ? 1 : 0);
+    int G = 1;  // plane groups per reduce block: each thread sums <= ~8 planes
+    while (G < 16 && G * 8 < p.nblk) G *= 2;
+    const int64_t blocks = std::max<int64_t>(1, (plane / 4 + 256 / G - 1) / (256 / G));
+    MX_CHECK(blocks < (1ll << 31), "winograd wgrad: reduce grid too large");
+    MX_LAUNCH(wino_wgrad_reduce_k, dim3((unsigned)blocks), dim3(256), 0, st, scratch, dw, plane, pstride, p.nblk,
+              accumulate ? 1 : 0, G);
   }
 }
 
