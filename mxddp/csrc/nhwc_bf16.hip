@@ -359,18 +359,26 @@ struct WgNArgs {
   FastDiv fQ, fPQ, fCa, fS;
 };
 
+// Weight-gradient LDS tiles are pixel-major [64 pixels][pitch] with pitch = width + 32 and the
+// 16-byte chunks of rows 8-15 (mod 16) XOR-swizzled by 2: with that, both the ds_read_b64_tr_b16
+// fragment reads (a 32-lane group reads rows {0-3, 8-11} (+4) x 32 bytes) and the ds_write_b128
+// staging stores are bank-conflict-free (found by enumerating pitches and XOR swizzles against
+// the gfx950 lane groups; the plain +8 pitch measured ~1 conflict cycle per LDS cycle).
+__device__ __forceinline__ int wg_swz(int row) { return ((row >> 3) & 1) * 2; }
+
 __device__ __forceinline__ bf16x8 tr_frag(const bf16* tile, int pitch, int col0, int lane) {
   // MFMA operand for "row" = channel col0 + (lane & 15), k = pixels 8 * (lane >> 4) .. + 7 from a
   // pixel-major [32][pitch] tile: two transposed reads of 4 pixels x 16 channels each.
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-  const bf16* p0 = tile + (8 * g + q) * pitch + col0 + 4 * p;
+  const int r = 8 * g + q;  // rows r and r + 4 share the swizzle (same bit 3)
+  const bf16* p0 = tile + r * pitch + ((((col0 >> 3) + (p >> 1)) ^ wg_swz(r)) << 3) + 4 * (p & 1);
   const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
   const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * pitch));
-  bf16x8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-  return r;
+  bf16x8 res;
+  res[0] = lo[0]; res[1] = lo[1]; res[2] = lo[2]; res[3] = lo[3];
+  res[4] = hi[0]; res[5] = hi[1]; res[6] = hi[2]; res[7] = hi[3];
+  return res;
 }
 
 // TM x TN output tile (output channels x (r, s, c) columns), TM, TN in {64, 128}: 64-wide tiles
@@ -378,7 +386,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* tile, int pitch, int col0,
 template <int TM, int TN>
 __global__ __launch_bounds__(256) void wgrad_nhwc_kernel(WgNArgs a) {
   constexpr int BK = 64;                   // pixels per stage (two MFMA k-steps)
-  constexpr int PA = TM + 8, PB = TN + 8;  // LDS pitches (8-byte aligned rows for the tr reads)
+  constexpr int PA = TM + 32, PB = TN + 32;  // LDS pitches (see wg_swz)
   constexpr int VA = TM / 8, VB = TN / 8;  // 16-byte vectors per pixel row
   constexpr int EA = BK * VA / 256, EB = BK * VB / 256;
   constexpr int WMT = TM / 32, WNT = TN / 32;
@@ -423,11 +431,15 @@ __global__ __launch_bounds__(256) void wgrad_nhwc_kernel(WgNArgs a) {
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < EA; ++i)
-      *reinterpret_cast<u32x4*>(&As[buf][(rowa0 + (256 / VA) * i) * PA + 8 * cva]) = ra[i];
+    for (int i = 0; i < EA; ++i) {
+      const int r = rowa0 + (256 / VA) * i;
+      *reinterpret_cast<u32x4*>(&As[buf][r * PA + 8 * (cva ^ wg_swz(r))]) = ra[i];
+    }
 #pragma unroll
-    for (int i = 0; i < EB; ++i)
-      *reinterpret_cast<u32x4*>(&Bs[buf][(rowb0 + (256 / VB) * i) * PB + 8 * cvb]) = rb[i];
+    for (int i = 0; i < EB; ++i) {
+      const int r = rowb0 + (256 / VB) * i;
+      *reinterpret_cast<u32x4*>(&Bs[buf][r * PB + 8 * (cvb ^ wg_swz(r))]) = rb[i];
+    }
   };
 
   f32x4 acc[WMT][WNT];
