@@ -32,6 +32,7 @@
 #include "ops.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace mx {
 
@@ -331,6 +332,151 @@ __global__ __launch_bounds__(256, 2) void conv_nhwc_kernel(ConvNArgs a) {
     if (px < Mc && ch < a.Ng)
       *reinterpret_cast<u32x4*>(a.out + (size_t)pfull(px) * a.Ng + ch) =
           *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Large-layer forward / stride-1 data gradient: TM (64 | 128) output channels x 256 pixels per
+// 512-thread block, one block per CU, operands staged global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4: no VGPR round trip, no ds_write) into THREE stage buffers, so two
+// k-tiles are in flight while the third is computed; the wait before each stage is a counted
+// vmcnt (the other stage's loads stay in flight) plus a raw s_barrier (a __syncthreads() would
+// drain every LDS-DMA).
+//   LDS image per operand: rows of 64 k (128 B), each wave-instruction fills 8 rows x 8 16-byte
+//   chunks lane-linearly; the chunk a lane fetches is XOR-swizzled by (row & 7) on the SOURCE
+//   address, which makes the ds_read_b128 fragment reads conflict-free for the gfx950 lane
+//   groups (enumerated, see conv_nhwc_kernel's pitch note).
+//   Padding / out-of-range rows: the lane loads 16 zero bytes from g_zero16 instead.
+__device__ uint4 g_zero16;
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// device-only wrapper: the builtin needs a gfx950 target feature, which the host pass of an
+// (implicitly host-device) lambda would reject, silently dropping the kernel's host stub
+__device__ __forceinline__ void glds16(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds(src, (lds_void_t*)lds, 16, 0, 0);
+}
+
+template <int TM>
+__global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
+  constexpr int TN = 256, BK = 64, NS = 3;
+  constexpr int AB = TM * 128, SB = AB + TN * 128;   // bytes: A image, whole stage
+  constexpr int NA = TM / 64, NB = 4, NPW = NA + NB;  // LDS-DMA instructions per wave per stage
+  constexpr int WM = TM / 64, WN = 8 / WM, WPX = TN / WN, WMT = 4, WNT = WPX / 16;
+  __shared__ __attribute__((aligned(1024))) char smem[NS * SB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave / WN, wn = wave % WN;
+  const int tiles_m = (a.Ng + TM - 1) / TM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ch0 = (bid % tiles_m) * TM, px0 = (bid / tiles_m) * TN;
+  const char* zero = reinterpret_cast<const char*>(&g_zero16);
+
+  // per-lane A rows (NA) and B rows (NB): slot = (wave * N + j) * 64 + lane -> row = slot >> 3
+  const int pch = lane & 7;  // physical chunk this lane fills
+  int arow[NA];
+  uint32_t abase[NA];
+  bool aok[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    arow[j] = ((wave * NA + j) * 64 + lane) >> 3;
+    aok[j] = ch0 + arow[j] < a.Ng;
+    abase[j] = 2u * ((uint32_t)(ch0 + (aok[j] ? arow[j] : 0)) * a.Kg + 8 * (pch ^ (arow[j] & 7)));
+  }
+  uint32_t pbase[NB];
+  int ihb[NB], iwb[NB], lchb[NB];
+  bool pok[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int row = ((wave * NB + j) * 64 + lane) >> 3;
+    const int m = px0 + row;
+    pok[j] = m < a.M;
+    const int mm = pok[j] ? m : 0;
+    const int n = (int)a.fOHW.div((uint32_t)mm), rem = mm - n * a.OH * a.OW;
+    const int oh = (int)a.fOW.div((uint32_t)rem), ow = rem - oh * a.OW;
+    pbase[j] = 2u * ((uint32_t)n * a.IH * a.IW * a.Ca);
+    ihb[j] = a.dgrad ? oh + a.ph : oh * a.sh - a.ph;
+    iwb[j] = a.dgrad ? ow + a.pw : ow * a.sw - a.pw;
+    lchb[j] = 8 * (pch ^ (row & 7));
+  }
+
+  auto issue = [&](int t, int buf) {
+    const int k0 = t * BK;
+    const int rs = (int)a.fCa.div((uint32_t)k0), c0 = k0 - rs * a.Ca;  // uniform: one tap per stage
+    const int r = (int)a.fS.div((uint32_t)rs), s = rs - r * a.S;
+    char* st = smem + buf * SB;
+    const char* wb = reinterpret_cast<const char*>(a.wt) + 2u * (uint32_t)k0;
+#pragma unroll
+    for (int j = 0; j < NA; ++j)
+      glds16(aok[j] ? (const void*)(wb + abase[j]) : (const void*)zero, st + (wave * NA + j) * 1024);
+    const char* xb = reinterpret_cast<const char*>(a.act) + 2u * (uint32_t)c0;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int ih = a.dgrad ? ihb[j] - r : ihb[j] + r, iw = a.dgrad ? iwb[j] - s : iwb[j] + s;
+      const bool ok = pok[j] && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
+      const char* src = xb + pbase[j] + 2u * (uint32_t)((ih * a.IW + iw) * a.Ca + lchb[j]);
+      glds16(ok ? (const void*)src : (const void*)zero, st + AB + (wave * NB + j) * 1024);
+    }
+  };
+
+  f32x4 acc[WMT][WNT];
+#pragma unroll
+  for (int i = 0; i < WMT; ++i)
+#pragma unroll
+    for (int j = 0; j < WNT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = a.Kg / BK;
+  issue(0, 0);
+  if (nt > 1) issue(1, 1);
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage t landed for every wave; stage t-1's buffer is free
+    if (t + 2 < nt) issue(t + 2, (t + 2) % NS);
+    const char* sA = smem + (t % NS) * SB;
+    const char* sB = sA + AB;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int lch = 4 * ks + (lane >> 4);
+      bf16x8 av[WMT], bv[WNT];
+#pragma unroll
+      for (int i = 0; i < WMT; ++i) {
+        const int row = wm * 64 + 16 * i + (lane & 15);
+        av[i] = *reinterpret_cast<const bf16x8*>(sA + row * 128 + 16 * (lch ^ (row & 7)));
+      }
+#pragma unroll
+      for (int j = 0; j < WNT; ++j) {
+        const int row = wn * WPX + 16 * j + (lane & 15);
+        bv[j] = *reinterpret_cast<const bf16x8*>(sB + row * 128 + 16 * (lch ^ (row & 7)));
+      }
+#pragma unroll
+      for (int i = 0; i < WMT; ++i)
+#pragma unroll
+        for (int j = 0; j < WNT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // every wave done with the stage buffers (no LDS-DMA outstanding)
+  // bf16 output staged through LDS ([TN pixels][TM channels], pitch TM + 8) -> 16-byte stores
+  constexpr int CP = TM + 8;
+  static_assert(TN * CP * 2 <= NS * SB, "C tile must fit in the stage buffers");
+  bf16* Cs = reinterpret_cast<bf16*>(smem);
+#pragma unroll
+  for (int i = 0; i < WMT; ++i) {
+    const int cl = wm * 64 + 16 * i + 4 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < WNT; ++j) {
+      const int pl = wn * WPX + 16 * j + (lane & 15);
+      *reinterpret_cast<uint2*>(Cs + pl * CP + cl) =
+          make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
+    }
+  }
+  __syncthreads();
+  constexpr int VPR = TM / 8;
+#pragma unroll
+  for (int v = tid; v < TN * VPR; v += 512) {
+    const int row = v / VPR, cv = v - row * VPR;
+    const int px = px0 + row, ch = ch0 + 8 * cv;
+    if (px < a.M && ch < a.Ng)
+      *reinterpret_cast<u32x4*>(a.out + (size_t)px * a.Ng + ch) = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
   }
 }
 
@@ -1053,6 +1199,28 @@ size_t nhwc_conv_scratch_floats(int M, int Ng, int Kg) {
   return p.splits > 1 ? (size_t)p.splits * M * Ng : 0;
 }
 
+// LDS-DMA kernel selection: 0 = never, 1 = large layers (default), 2 = wherever eligible (tests)
+static int g_conv_glds = -1;
+void nhwc_conv_set_glds(int mode) { g_conv_glds = mode; }
+static int conv_glds_mode() {
+  if (g_conv_glds < 0) {
+    const char* e = std::getenv("MXDDP_CONV_GLDS");
+    g_conv_glds = (e && *e) ? std::atoi(e) : 1;
+  }
+  return g_conv_glds;
+}
+
+// the LDS-DMA kernel: wide path, forward or stride-1 data gradient, and (mode 1) enough
+// 256-pixel tiles to give every CU a block
+static int glds_tile_m(const ConvNArgs& a, bool wide) {
+  const int mode = conv_glds_mode();
+  if (mode == 0 || !wide || (a.dgrad && (a.sh != 1 || a.sw != 1))) return 0;
+  const int tm = a.Ng >= 128 ? 128 : 64;
+  const int64_t blocks = (int64_t)cdiv(a.Ng, tm) * cdiv(a.M, 256);
+  if (mode == 1 && blocks < 256) return 0;
+  return tm;
+}
+
 static void launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   MX_CHECK(a.Kg % 8 == 0 && a.Ca % 8 == 0 && a.Ng % 8 == 0, "nhwc conv: channels must be multiples of 8");
   a.fOW = FastDiv(a.OW);
@@ -1062,6 +1230,13 @@ static void launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   const ConvSetup cs = conv_setup(a);
   ConvPlan p = cs.p;
   const bool wide = cs.wide;
+  if (const int gtm = cs.par ? 0 : glds_tile_m(a, wide)) {
+    a.par = 0;
+    const dim3 grid(cdiv(a.Ng, gtm) * cdiv(a.M, 256));
+    if (gtm == 128) MX_LAUNCH((conv_nhwc_glds_kernel<128>), grid, dim3(512), 0, st, a);
+    else MX_LAUNCH((conv_nhwc_glds_kernel<64>), grid, dim3(512), 0, st, a);
+    return;
+  }
   a.par = cs.par ? 1 : 0;
   if (cs.par) {
     a.Hc = a.OH / 2;

@@ -59,6 +59,34 @@ def test_conv_nhwc(cuda, case):
     assert _rel(wg.grad.cpu(), wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("case", [(2, 64, 14, 14, 192, 3, 1, 1), (3, 128, 13, 11, 64, 1, 1, 0),
+                                  (2, 64, 15, 15, 128, 3, 2, 1), (1, 128, 9, 9, 256, 3, 1, 1)])
+def test_conv_glds_kernel(cuda, case):
+    """The LDS-DMA three-stage kernel, forced on every eligible layer (forward and stride-1 data
+    gradient; partial channel / pixel tiles, stride-2 forward) vs the fp32 reference."""
+    from mxddp import native
+
+    C_ = native()
+    N, C, H, W, K, R, st, pd = case
+    torch.manual_seed(11)
+    x = torch.randn(N, H, W, C).to(torch.bfloat16)
+    w = torch.randn(K, C, R, R) * (2.0 / (C * R * R)) ** 0.5
+    xr = _nchw(x).requires_grad_()
+    yr = F.conv2d(xr, w.to(torch.bfloat16).float(), None, st, pd)
+    gy = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(gy)
+    C_.nhwc_conv_set_glds(2)
+    try:
+        xg = x.to(cuda).requires_grad_()
+        y = nhwc.conv2d(xg, w.to(cuda), st, pd)
+        y.backward(gy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(cuda))
+        torch.cuda.synchronize()
+    finally:
+        C_.nhwc_conv_set_glds(1)
+    assert _rel(_nchw(y), yr.detach()) < 1e-2
+    assert _rel(_nchw(xg.grad), xr.grad) < 1e-2
+
+
 def test_conv_nhwc_padded_input_channels(cuda):
     """3-channel image padded to 8: the padding must not leak into outputs or weight grads."""
     torch.manual_seed(1)
