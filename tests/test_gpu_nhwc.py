@@ -72,19 +72,22 @@ def test_conv_glds_kernel(cuda, case):
     x = torch.randn(N, H, W, C).to(torch.bfloat16)
     w = torch.randn(K, C, R, R) * (2.0 / (C * R * R)) ** 0.5
     xr = _nchw(x).requires_grad_()
-    yr = F.conv2d(xr, w.to(torch.bfloat16).float(), None, st, pd)
+    wr = w.to(torch.bfloat16).float().requires_grad_()
+    yr = F.conv2d(xr, wr, None, st, pd)
     gy = torch.randn_like(yr).to(torch.bfloat16).float()
     yr.backward(gy)
     C_.nhwc_conv_set_glds(2)
     try:
         xg = x.to(cuda).requires_grad_()
-        y = nhwc.conv2d(xg, w.to(cuda), st, pd)
+        wg = w.to(cuda).requires_grad_()
+        y = nhwc.conv2d(xg, wg, st, pd)
         y.backward(gy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(cuda))
         torch.cuda.synchronize()
     finally:
         C_.nhwc_conv_set_glds(1)
     assert _rel(_nchw(y), yr.detach()) < 1e-2
     assert _rel(_nchw(xg.grad), xr.grad) < 1e-2
+    assert _rel(wg.grad.cpu(), wr.grad) < 1e-2
 
 
 def test_conv_nhwc_padded_input_channels(cuda):
