@@ -1211,13 +1211,15 @@ static int conv_glds_mode() {
 }
 
 // the LDS-DMA kernel: wide path, forward or stride-1 data gradient, and (mode 1) enough
-// 256-pixel tiles to give every CU a block
+// 256-pixel tiles for ~3/4 of the CUs
 static int glds_tile_m(const ConvNArgs& a, bool wide) {
   const int mode = conv_glds_mode();
   if (mode == 0 || !wide || (a.dgrad && (a.sh != 1 || a.sw != 1))) return 0;
   const int tm = a.Ng >= 128 ? 128 : 64;
   const int64_t blocks = (int64_t)cdiv(a.Ng, tm) * cdiv(a.M, 256);
-  if (mode == 1 && blocks < 256) return 0;
+  // measured per layer at batch 32 / 64 (scripts/gpu_glds_sweep.sh): a win from ~200 blocks up
+  // (0.75 of the 256 CUs), a loss at <= 112 (the register-staged kernel splits K instead)
+  if (mode == 1 && blocks < 192) return 0;
   return tm;
 }
 
