@@ -398,8 +398,9 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
     lchb[j] = 8 * (pch ^ (row & 7));
   }
 
+  const int kt0 = blockIdx.y * a.kt_per_split;
   auto issue = [&](int t, int buf) {
-    const int k0 = t * BK;
+    const int k0 = (kt0 + t) * BK;
     const int rs = (int)a.fCa.div((uint32_t)k0), c0 = k0 - rs * a.Ca;  // uniform: one tap per stage
     const int r = (int)a.fS.div((uint32_t)rs), s = rs - r * a.S;
     char* st = smem + buf * SB;
@@ -423,8 +424,9 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
 #pragma unroll
     for (int j = 0; j < WNT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nt = a.Kg / BK;
-  issue(0, 0);
+  // split-K over blockIdx.y (fp32 partials, summed by conv_nhwc_splitk_reduce_k)
+  const int nt = min(a.Kg / BK - kt0, a.kt_per_split);
+  if (nt > 0) issue(0, 0);
   if (nt > 1) issue(1, 1);
   for (int t = 0; t < nt; ++t) {
     if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
@@ -453,6 +455,21 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
         for (int j = 0; j < WNT; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
+  }
+  if (a.part) {  // split-K: fp32 partials of 4 consecutive channels per lane
+#pragma unroll
+    for (int i = 0; i < WMT; ++i) {
+      const int ch = ch0 + wm * 64 + 16 * i + 4 * (lane >> 4);
+      if (ch >= a.Ng) continue;
+#pragma unroll
+      for (int j = 0; j < WNT; ++j) {
+        const int px = px0 + wn * WPX + 16 * j + (lane & 15);
+        if (px < a.M)
+          *reinterpret_cast<float4*>(a.part + ((size_t)blockIdx.y * a.M + px) * a.Ng + ch) =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+    }
+    return;
   }
   __syncthreads();  // every wave done with the stage buffers (no LDS-DMA outstanding)
   // bf16 output staged through LDS ([TN pixels][TM channels], pitch TM + 8) -> 16-byte stores
@@ -1194,10 +1211,6 @@ static ConvSetup conv_setup(const ConvNArgs& a) {
   return c;
 }
 
-size_t nhwc_conv_scratch_floats(int M, int Ng, int Kg) {
-  const ConvPlan p = conv_plan(M, Ng, Kg);
-  return p.splits > 1 ? (size_t)p.splits * M * Ng : 0;
-}
 
 // LDS-DMA kernel selection: 0 = never, 1 = large layers (default), 2 = wherever eligible (tests)
 static int g_conv_glds = -1;
@@ -1212,15 +1225,41 @@ static int conv_glds_mode() {
 
 // the LDS-DMA kernel: wide path, forward or stride-1 data gradient, and (mode 1) enough
 // 256-pixel tiles for ~3/4 of the CUs
-static int glds_tile_m(const ConvNArgs& a, bool wide) {
-  const int mode = conv_glds_mode();
-  if (mode == 0 || !wide || (a.dgrad && (a.sh != 1 || a.sw != 1))) return 0;
-  const int tm = a.Ng >= 128 ? 128 : 64;
-  const int64_t blocks = (int64_t)cdiv(a.Ng, tm) * cdiv(a.M, 256);
-  // measured per layer at batch 32 / 64 (scripts/gpu_glds_sweep.sh): a win from ~200 blocks up
-  // (0.75 of the 256 CUs), a loss at <= 112 (the register-staged kernel splits K instead)
-  if (mode == 1 && blocks < 192) return 0;
-  return tm;
+struct GldsPlan {
+  int tm, splits, kt_per_split;  // tm == 0: not used
+};
+
+static GldsPlan glds_plan_mnk(int M, int Ng, int Kg) {
+  GldsPlan g{};
+  g.tm = Ng >= 128 ? 128 : 64;
+  const int tiles = cdiv(Ng, g.tm) * cdiv(M, 256);
+  const int nkt = Kg / 64;
+  // split the reduction (>= 8 k-tiles per split) until ~one block per CU
+  g.splits = std::max(1, std::min(cdiv(256, tiles), nkt / 8));
+  g.kt_per_split = cdiv(nkt, g.splits);
+  g.splits = cdiv(nkt, g.kt_per_split);
+  // measured per layer at batch 32 / 64 (scripts/gpu_glds_sweep.sh, bench_nhwc_layers.py): a
+  // win from ~200 blocks up (0.75 of the 256 CUs), a loss at <= 112; with split-K a win only when
+  // the layer has few tiles (<= 50: long per-split reductions), a loss at ~100 tiles x 2 splits
+  if (conv_glds_mode() == 1 && (tiles * g.splits < 192 || (g.splits > 1 && tiles > 64))) g.tm = 0;
+  return g;
+}
+
+// the LDS-DMA kernel: wide path, forward or stride-1 data gradient
+static GldsPlan glds_plan(const ConvNArgs& a, bool wide, bool par) {
+  if (conv_glds_mode() == 0 || !wide || par || (a.dgrad && (a.sh != 1 || a.sw != 1))) return GldsPlan{};
+  return glds_plan_mnk(a.M, a.Ng, a.Kg);
+}
+
+size_t nhwc_conv_scratch_floats(int M, int Ng, int Kg) {
+  // either kernel may run (the LDS-DMA one needs a wide layer: Kg % 64 == 0 is necessary)
+  const ConvPlan p = conv_plan(M, Ng, Kg);
+  size_t n = p.splits > 1 ? (size_t)p.splits * M * Ng : 0;
+  if (Kg % 64 == 0) {
+    const GldsPlan g = glds_plan_mnk(M, Ng, Kg);
+    if (g.tm && g.splits > 1) n = std::max(n, (size_t)g.splits * M * Ng);
+  }
+  return n;
 }
 
 static void launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
@@ -1232,11 +1271,18 @@ static void launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   const ConvSetup cs = conv_setup(a);
   ConvPlan p = cs.p;
   const bool wide = cs.wide;
-  if (const int gtm = cs.par ? 0 : glds_tile_m(a, wide)) {
+  const GldsPlan gp = glds_plan(a, wide, cs.par);
+  if (gp.tm && (gp.splits == 1 || scratch)) {
     a.par = 0;
-    const dim3 grid(cdiv(a.Ng, gtm) * cdiv(a.M, 256));
-    if (gtm == 128) MX_LAUNCH((conv_nhwc_glds_kernel<128>), grid, dim3(512), 0, st, a);
+    a.kt_per_split = gp.kt_per_split;
+    a.part = gp.splits > 1 ? scratch : nullptr;
+    const dim3 grid(cdiv(a.Ng, gp.tm) * cdiv(a.M, 256), gp.splits);
+    if (gp.tm == 128) MX_LAUNCH((conv_nhwc_glds_kernel<128>), grid, dim3(512), 0, st, a);
     else MX_LAUNCH((conv_nhwc_glds_kernel<64>), grid, dim3(512), 0, st, a);
+    if (gp.splits > 1) {
+      const int64_t n4 = (int64_t)a.M * a.Ng / 4;
+      MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, gp.splits);
+    }
     return;
   }
   a.par = cs.par ? 1 : 0;
@@ -1321,8 +1367,10 @@ static ConvNArgs dgrad_args(const uint16_t* dy, const uint16_t* wt_d, uint16_t* 
 size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
                                       int P, int Q) {
   const ConvNArgs a = dgrad_args(nullptr, nullptr, nullptr, N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q);
-  const ConvPlan p = conv_setup(a).p;
-  return p.splits > 1 ? (size_t)p.splits * a.M * a.Ng : 0;
+  const ConvSetup cs = conv_setup(a);
+  const GldsPlan g = glds_plan(a, cs.wide, cs.par);
+  const int splits = g.tm ? g.splits : cs.p.splits;
+  return splits > 1 ? (size_t)splits * a.M * a.Ng : 0;
 }
 
 void nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,

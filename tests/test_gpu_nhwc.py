@@ -60,7 +60,8 @@ def test_conv_nhwc(cuda, case):
 
 
 @pytest.mark.parametrize("case", [(2, 64, 14, 14, 192, 3, 1, 1), (3, 128, 13, 11, 64, 1, 1, 0),
-                                  (2, 64, 15, 15, 128, 3, 2, 1), (1, 128, 9, 9, 256, 3, 1, 1)])
+                                  (2, 64, 15, 15, 128, 3, 2, 1), (1, 128, 9, 9, 256, 3, 1, 1),
+                                  (1, 256, 7, 7, 128, 3, 1, 1)])  # long reduction: split-K partials
 def test_conv_glds_kernel(cuda, case):
     """The LDS-DMA three-stage kernel, forced on every eligible layer (forward and stride-1 data
     gradient; partial channel / pixel tiles, stride-2 forward) vs the fp32 reference."""
