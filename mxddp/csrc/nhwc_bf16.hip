@@ -1389,7 +1389,11 @@ static int wgrad_splits(int Npix, int K, int Ng) {
   wgrad_tile(K, Ng, tm, tn);
   const int tiles = cdiv(K, tm) * cdiv(Ng, tn);
   // ~2 blocks per CU, >= 512 pixels (8 stages) per block, partial planes <= 32M floats
-  int splits = std::max(1, cdiv(512, tiles));
+  static const int target = [] {
+    const char* e = std::getenv("MXDDP_WGRAD_BLOCKS");
+    return (e && *e) ? std::max(1, std::atoi(e)) : 512;
+  }();
+  int splits = std::max(1, cdiv(target, tiles));
   splits = std::min(splits, std::max(1, Npix / 512));
   splits = std::min(splits, std::max(1, (int)((32ll << 20) / ((int64_t)K * Ng))));
   const int chunk = cdiv(cdiv(Npix, splits), 64) * 64;
