@@ -103,10 +103,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_conv_scratch_floats", &nhwc_conv_scratch_floats);
   m.def("nhwc_conv_dgrad", [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int N, int H, int W, int C, int K, int R,
                               int S_, int sh, int sw, int ph, int pw, int P_, int Q, uintptr_t scratch,
-                              uintptr_t st) {
+                              uintptr_t st, uintptr_t addend) {
     nhwc_conv_dgrad(P<const uint16_t>(dy), P<const uint16_t>(wt), P<uint16_t>(dx), N, H, W, C, K, R, S_, sh, sw, ph,
-                    pw, P_, Q, P<float>(scratch), S(st));
-  });
+                    pw, P_, Q, P<float>(scratch), S(st), P<const uint16_t>(addend));
+  }, py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("K"),
+     py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("P"), py::arg("Q"),
+     py::arg("scratch"), py::arg("st"), py::arg("addend") = 0);
   m.def("nhwc_conv_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, int N, int H, int W, int Cin, int Cp, int K,
                               int R, int S_, int sh, int sw, int ph, int pw, int P_, int Q, bool acc, uintptr_t scratch,
                               uintptr_t st) {

@@ -58,6 +58,16 @@ __device__ __forceinline__ void unpack8(const uint4& u, float* f) {
 __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }
+// 8 bf16 c + 8 bf16 d, summed in fp32 and rounded once
+__device__ __forceinline__ u32x4 add8(u32x4 c, u32x4 d) {
+  float x[8], y[8];
+  unpack8(make_uint4(c[0], c[1], c[2], c[3]), x);
+  unpack8(make_uint4(d[0], d[1], d[2], d[3]), y);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) x[e] += y[e];
+  const uint4 r = pack8(x);
+  return u32x4{r.x, r.y, r.z, r.w};
+}
 
 // ------------------------------------------------------------------------------------------
 // forward / data-gradient implicit GEMM
@@ -76,6 +86,8 @@ struct ConvNArgs {
   // taps of matching parity contribute, so each class is a dense stride-1 GEMM over its own
   // taps (the zero-inserted transposed gather would multiply 3 zeros out of 4)
   int par, Hc, Wc;
+  const bf16* addend;  // data gradient: added to the result in the epilogue ([M][Ng], or null) -- a
+                       // residual block's two input-gradient branches joined without another pass
   FastDiv fOW, fOHW, fCa, fS, fWc, fHWc;
 };
 
@@ -330,8 +342,12 @@ __global__ __launch_bounds__(256, 2) void conv_nhwc_kernel(ConvNArgs a) {
     const int row = v / VPR, cv = v - row * VPR;
     const int px = px0 + row, ch = ch0 + 8 * cv;
     if (px < Mc && ch < a.Ng)
-      *reinterpret_cast<u32x4*>(a.out + (size_t)pfull(px) * a.Ng + ch) =
-          *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
+    {
+      const size_t o = (size_t)pfull(px) * a.Ng + ch;
+      u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
+      if (a.addend) v = add8(v, *reinterpret_cast<const u32x4*>(a.addend + o));
+      *reinterpret_cast<u32x4*>(a.out + o) = v;
+    }
   }
 }
 
@@ -493,19 +509,28 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
     const int row = v / VPR, cv = v - row * VPR;
     const int px = px0 + row, ch = ch0 + 8 * cv;
     if (px < a.M && ch < a.Ng)
-      *reinterpret_cast<u32x4*>(a.out + (size_t)px * a.Ng + ch) = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
+    {
+      const size_t o = (size_t)px * a.Ng + ch;
+      u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
+      if (a.addend) v = add8(v, *reinterpret_cast<const u32x4*>(a.addend + o));
+      *reinterpret_cast<u32x4*>(a.out + o) = v;
+    }
   }
 }
 
 // split-K epilogue: out (bf16) = sum over splits of the fp32 partials (fixed order)
 __global__ void conv_nhwc_splitk_reduce_k(const float* __restrict__ part, bf16* __restrict__ out, int64_t n4,
-                                          int splits) {
+                                          int splits, const bf16* __restrict__ addend) {
   const float4* p4 = reinterpret_cast<const float4*>(part);
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     float4 s = p4[i];
     for (int sp = 1; sp < splits; ++sp) {
       const float4 v = p4[sp * n4 + i];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    if (addend) {
+      const uint2 d = reinterpret_cast<const uint2*>(addend)[i];
+      s.x += bf2f(d.x & 0xffffu); s.y += bf2f(d.x >> 16); s.z += bf2f(d.y & 0xffffu); s.w += bf2f(d.y >> 16);
     }
     reinterpret_cast<uint2*>(out)[i] = make_uint2(pack2(s.x, s.y), pack2(s.z, s.w));
   }
@@ -1281,7 +1306,8 @@ static void launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     else MX_LAUNCH((conv_nhwc_glds_kernel<64>), grid, dim3(512), 0, st, a);
     if (gp.splits > 1) {
       const int64_t n4 = (int64_t)a.M * a.Ng / 4;
-      MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, gp.splits);
+      MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, gp.splits,
+                a.addend);
     }
     return;
   }
@@ -1311,7 +1337,8 @@ static void launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   }
   if (p.splits > 1) {
     const int64_t n4 = (int64_t)a.M * a.Ng / 4;
-    MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, p.splits);
+    MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, p.splits,
+              a.addend);
   }
 }
 
@@ -1374,8 +1401,10 @@ size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, 
 }
 
 void nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
-                     int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st) {
+                     int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st,
+                     const uint16_t* addend) {
   ConvNArgs a = dgrad_args(dy, wt_d, dx, N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q);
+  a.addend = addend;
   launch_conv(a, scratch, st);
 }
 

@@ -151,8 +151,10 @@ void nhwc_conv_set_glds(int mode);
 // split-K scratch of nhwc_conv_dgrad (floats; 0 = none needed)
 size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
                                       int P, int Q);
+// addend (optional, bf16 [N][H][W][C]): dx = conv_transpose(dy) + addend, summed in the epilogue
 void nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
-                     int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st);
+                     int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st,
+                     const uint16_t* addend = nullptr);
 // dw fp32 [K][Cin][R][S] (+)= ...; x has Cp >= Cin channels (padding ignored);
 // scratch: nhwc_wgrad_scratch_floats(...) floats of per-split partial sums
 size_t nhwc_wgrad_scratch_floats(int N, int Cp, int K, int R, int S, int P, int Q);

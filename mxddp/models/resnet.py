@@ -47,15 +47,18 @@ class Bottleneck(nn.Module):
     def forward_nhwc(self, x, pack=None):
         from ..ops import nhwc as N
 
+        join = None
         if self.downsample is None:
-            idt = x
+            # identity shortcut: its gradient is added inside conv1's data-gradient epilogue
+            join = N.GradJoin()
+            x, idt = N.fork(x, join)
         else:
             dc, dbn = self.downsample[0], self.downsample[1]
             idt = N.batch_norm(N.conv2d(x, dc.weight, dc.stride, dc.padding, pack), dbn)
-        out = N.batch_norm(N.conv2d(x, self.conv1.weight, pack=pack), self.bn1, relu=True)
+        out = N.batch_norm(N.conv2d(x, self.conv1.weight, pack=pack, join=join), self.bn1, relu=True)
         out = N.batch_norm(N.conv2d(out, self.conv2.weight, self.conv2.stride, self.conv2.padding, pack), self.bn2,
                            relu=True)
-        return N.batch_norm(N.conv2d(out, self.conv3.weight, pack=pack), self.bn3, relu=True, res=idt)
+        return N.batch_norm(N.conv2d(out, self.conv3.weight, pack=pack), self.bn3, relu=True, res=idt, join=join)
 
 
 class ResNet(nn.Module):

@@ -95,9 +95,45 @@ class WeightPack:
         return self._views.get(id(w))
 
 
+class GradJoin:
+    """Joins the two input-gradient branches of a residual block without a separate add: the
+    block's last batch norm (whose ``res`` is the identity shortcut) leaves its shortcut gradient
+    here, and the block's first convolution adds it in its data-gradient epilogue
+    (``nhwc_conv_dgrad(..., addend)``).  ``fork`` then passes that sum through unchanged."""
+
+    def __init__(self):
+        self.dres = None
+        self.consumed = False
+
+
+class _Fork(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, join):
+        ctx.join = join
+        return x.view_as(x), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g_main, g_short):
+        j = ctx.join
+        if j.consumed:  # g_main already includes g_short (added by the conv's epilogue)
+            out = g_main
+        elif g_main is None or g_short is None:
+            out = g_main if g_short is None else g_short
+        else:
+            out = g_main + g_short
+        j.dres, j.consumed = None, False
+        return out, None
+
+
+def fork(x, join: GradJoin):
+    """(main, shortcut) aliases of a residual block's input; pass ``join`` to the block's first
+    conv2d and last batch_norm so the two gradients are summed inside the conv's epilogue."""
+    return _Fork.apply(x, join)
+
+
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad, packed=None):
+    def forward(ctx, x, w, stride, pad, packed=None, join=None):
         Cn = native()
         N, H, W, Cp = x.shape
         K, C, R, S = w.shape
@@ -118,6 +154,7 @@ class _Conv(torch.autograd.Function):
         Cn.nhwc_conv_fwd(x.data_ptr(), wt.data_ptr(), y.data_ptr(), N, H, W, Cp, K, R, S, sh, sw, ph, pw, P, Q,
                          _p(scr), st)
         ctx.wtd = wtd
+        ctx.join = join
         ctx.save_for_backward(x, w)
         ctx.geom = (N, H, W, Cp, K, C, R, S, sh, sw, ph, pw, P, Q)
         return y
@@ -140,8 +177,12 @@ class _Conv(torch.autograd.Function):
             dx = torch.empty((N, H, W, C), device=dy.device, dtype=BF16)
             n = Cn.nhwc_conv_dgrad_scratch_floats(N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q)
             scr = torch.empty((n,), device=dy.device, dtype=torch.float32) if n else None
+            j = ctx.join
+            add = j.dres if j is not None and j.dres is not None and j.dres.shape == dx.shape else None
             Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx.data_ptr(), N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q,
-                               _p(scr), st)
+                               _p(scr), st, _p(add))
+            if add is not None:
+                j.consumed = True
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(w)
             dw = sink if sink is not None else torch.empty_like(w)
@@ -151,19 +192,20 @@ class _Conv(torch.autograd.Function):
                                P, Q, sink is not None, part.data_ptr(), st)
             if sink is not None:
                 dw = None
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
-def conv2d(x, w, stride=1, padding=0, pack: WeightPack | None = None):
-    """bf16 NHWC convolution; ``pack`` supplies weights already repacked by WeightPack.refresh()."""
+def conv2d(x, w, stride=1, padding=0, pack: WeightPack | None = None, join: GradJoin | None = None):
+    """bf16 NHWC convolution; ``pack`` supplies weights already repacked by WeightPack.refresh(),
+    ``join`` (see ``fork``) adds a residual block's shortcut gradient to this conv's input gradient."""
     s = (stride, stride) if isinstance(stride, int) else tuple(stride)
     p = (padding, padding) if isinstance(padding, int) else tuple(padding)
-    return _Conv.apply(x, w, s, p, pack.get(w) if pack is not None else None)
+    return _Conv.apply(x, w, s, p, pack.get(w) if pack is not None else None, join)
 
 
 class _BN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, rm, rv, nbt, res, relu, momentum, eps):
+    def forward(ctx, x, gamma, beta, rm, rv, nbt, res, relu, momentum, eps, join=None):
         Cn = native()
         N, H, W, C = x.shape
         npix = N * H * W
@@ -176,6 +218,7 @@ class _BN(torch.autograd.Function):
                        stream_of(x))
         ctx.save_for_backward(x, y, gamma, mean, invstd)
         ctx.relu, ctx.has_res = bool(relu), res is not None
+        ctx.join = join
         ctx.refs = (gamma, beta)
         return y
 
@@ -197,17 +240,20 @@ class _BN(torch.autograd.Function):
                        scr.data_ptr(), stream_of(dy))
         if direct:
             dg = db = None
-        return dx, dg, db, None, None, None, dres, None, None, None
+        if ctx.join is not None and dres is not None:
+            ctx.join.dres = dres  # picked up by the block's first conv (data-gradient epilogue)
+        return dx, dg, db, None, None, None, dres, None, None, None, None
 
 
-def batch_norm(x, bn: torch.nn.BatchNorm2d, relu: bool = False, res: torch.Tensor | None = None):
+def batch_norm(x, bn: torch.nn.BatchNorm2d, relu: bool = False, res: torch.Tensor | None = None,
+               join: GradJoin | None = None):
     """Training-mode BN of an NHWC bf16 tensor with the module's parameters / buffers (running
     stats and num_batches_tracked updated on device), fused ReLU and residual add (y = relu(bn(x) +
     res)).  Eval mode uses the running statistics (plain tensor math)."""
     if bn.training or not bn.track_running_stats:
         mom = bn.momentum if bn.momentum is not None else 0.1
         nbt = bn.num_batches_tracked if (bn.training and bn.track_running_stats) else None
-        return _BN.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, res, relu, mom, bn.eps)
+        return _BN.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, res, relu, mom, bn.eps, join)
     y = (x.float() - bn.running_mean) * torch.rsqrt(bn.running_var + bn.eps) * bn.weight + bn.bias
     if res is not None:
         y = y + res.float()

@@ -91,6 +91,35 @@ def test_conv_glds_kernel(cuda, case):
     assert _rel(wg.grad.cpu(), wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("case", [(1, 256, 7, 7, 512, 3, 1, 1), (2, 64, 14, 14, 256, 1, 1, 0)])
+def test_conv_dgrad_addend(cuda, case):
+    """dx = conv_transpose(dy) + addend fused in the data-gradient epilogue (split-K reduction and
+    direct epilogue) == the two computed separately."""
+    from mxddp import native
+
+    Cn = native()
+    N, C, H, W, K, R, st, pd = case
+    torch.manual_seed(12)
+    P, Q = (H + 2 * pd - R) // st + 1, (W + 2 * pd - R) // st + 1
+    dy = torch.randn(N, P, Q, K, device=cuda).to(torch.bfloat16)
+    w = torch.randn(K, C, R, R, device=cuda) * 0.05
+    add = torch.randn(N, H, W, C, device=cuda).to(torch.bfloat16)
+    s = torch.cuda.current_stream().cuda_stream
+    wtd = torch.empty(C * R * R * K, device=cuda, dtype=torch.bfloat16)
+    Cn.nhwc_repack_weight(w.data_ptr(), 0, wtd.data_ptr(), K, C, R, R, C, s)
+    n = Cn.nhwc_conv_dgrad_scratch_floats(N, H, W, C, K, R, R, st, st, pd, pd, P, Q)
+    scr = torch.empty(max(n, 1), device=cuda)
+    dx0 = torch.empty(N, H, W, C, device=cuda, dtype=torch.bfloat16)
+    dx1 = torch.empty_like(dx0)
+    Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx0.data_ptr(), N, H, W, C, K, R, R, st, st, pd, pd, P, Q,
+                       scr.data_ptr() if n else 0, s)
+    Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx1.data_ptr(), N, H, W, C, K, R, R, st, st, pd, pd, P, Q,
+                       scr.data_ptr() if n else 0, s, add.data_ptr())
+    torch.cuda.synchronize()
+    ref = dx0.float() + add.float()
+    assert _rel(dx1, ref) < 1e-2
+
+
 def test_conv_nhwc_padded_input_channels(cuda):
     """3-channel image padded to 8: the padding must not leak into outputs or weight grads."""
     torch.manual_seed(1)
