@@ -822,6 +822,8 @@ struct BnNArgs {
   float* dbeta;
   int64_t* num_batches;
   int Npix, C, relu, gx, acc_params;
+  const float* fcoef;  // bwd, ReLU without residual: the forward's [C][2] (scale, shift); the mask
+                       // is then (x * scale + shift > 0) and y is not read (one tensor less)
   float momentum, eps;
 };
 
@@ -832,7 +834,7 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
   const int ppi = kBnT / vv;
   const int vbase = (V >= kBnT) ? blockIdx.y * kBnT : 0;
   const int v = vbase + threadIdx.x % vv, pr = threadIdx.x / vv;
-  float s1[8], s2[8], K[8];
+  float s1[8], s2[8], K[8], mc[16];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
   if (!BWD) {
@@ -840,7 +842,15 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
   } else {
 #pragma unroll
     for (int e = 0; e < 8; ++e) K[e] = a.mean[8 * v + e];
+    if (a.fcoef) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 q = reinterpret_cast<const float4*>(a.fcoef + 16 * v)[j];
+        mc[4 * j] = q.x; mc[4 * j + 1] = q.y; mc[4 * j + 2] = q.z; mc[4 * j + 3] = q.w;
+      }
+    }
   }
+  const bool ymask = BWD && a.relu && !a.fcoef;
   // UNR pixel rows per iteration with all their loads issued before any use: one 16-byte load
   // in flight per thread cannot cover HBM latency with ~256 blocks
   constexpr int UNR = BWD ? 2 : 4;
@@ -855,7 +865,7 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
       xr[u] = ok ? *reinterpret_cast<const uint4*>(a.x + o) : make_uint4(0u, 0u, 0u, 0u);
       if (BWD) {
         gr[u] = ok ? *reinterpret_cast<const uint4*>(a.dy + o) : make_uint4(0u, 0u, 0u, 0u);
-        if (a.relu) yr[u] = ok ? *reinterpret_cast<const uint4*>(a.y + o) : make_uint4(0u, 0u, 0u, 0u);
+        if (ymask) yr[u] = ok ? *reinterpret_cast<const uint4*>(a.y + o) : make_uint4(0u, 0u, 0u, 0u);
       }
     }
 #pragma unroll
@@ -873,11 +883,14 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
       } else {
         float g[8];
         unpack8(gr[u], g);
-        if (a.relu) {
+        if (ymask) {
           float yv[8];
           unpack8(yr[u], yv);
 #pragma unroll
           for (int e = 0; e < 8; ++e) g[e] = yv[e] > 0.f ? g[e] : 0.f;
+        } else if (a.relu) {  // the forward's exact fp32 pre-activation (same fmaf, same operands)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) g[e] = fmaf(xv[e], mc[2 * e], mc[2 * e + 1]) > 0.f ? g[e] : 0.f;
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -1035,10 +1048,15 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
   }
 }
 
-// backward apply: dx = A g + D x + B; dres = g (the residual branch gradient)
+// backward apply: dx = A g + D x + B; dres = g (the residual branch gradient).  XM: the ReLU mask
+// from x and the forward's (scale, shift) (C <= 512, no residual), else from y.
+template <bool XM>
 __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv fV) {
-  __shared__ float cs[3 * 2048];
+  constexpr int MAXC = XM ? 512 : 2048;
+  __shared__ float cs[(XM ? 5 : 3) * MAXC];
   for (int i = threadIdx.x; i < 3 * a.C; i += kBnT) cs[i] = a.coef[i];
+  if (XM)
+    for (int i = threadIdx.x; i < 2 * a.C; i += kBnT) cs[3 * MAXC + i] = a.fcoef[i];
   __syncthreads();
   const int V = a.C >> 3;
   const int total = a.Npix * V, step = gridDim.x * kBnT;
@@ -1051,7 +1069,7 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv f
       const bool ok = i < total;
       gr[u] = ok ? reinterpret_cast<const uint4*>(a.dy)[i] : z;
       xr[u] = ok ? reinterpret_cast<const uint4*>(a.x)[i] : z;
-      if (a.relu) yr[u] = ok ? reinterpret_cast<const uint4*>(a.y)[i] : z;
+      if (!XM && a.relu) yr[u] = ok ? reinterpret_cast<const uint4*>(a.y)[i] : z;
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -1061,7 +1079,11 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv f
       float g[8], xv[8];
       unpack8(gr[u], g);
       unpack8(xr[u], xv);
-      if (a.relu) {
+      if (XM) {
+        const float* m = cs + 3 * MAXC + 16 * v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = fmaf(xv[e], m[2 * e], m[2 * e + 1]) > 0.f ? g[e] : 0.f;
+      } else if (a.relu) {
         float yv[8];
         unpack8(yr[u], yv);
 #pragma unroll
@@ -1495,7 +1517,7 @@ size_t nhwc_bn_scratch_floats(int Npix, int C) {
 
 void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* gamma, const float* beta,
                  float* mean, float* invstd, float* run_mean, float* run_var, int64_t* num_batches, int Npix, int C,
-                 float momentum, float eps, bool relu, float* scratch, hipStream_t st) {
+                 float momentum, float eps, bool relu, float* scratch, hipStream_t st, float* coef_out) {
   const int V = C / 8;
   MX_CHECK(C % 8 == 0 && C <= 2048 && (V >= kBnT ? V % kBnT == 0 : kBnT % V == 0),
            "nhwc bn: unsupported channel count");
@@ -1513,7 +1535,7 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
   a.run_mean = run_mean;
   a.run_var = run_var;
   a.part = scratch;
-  a.coef = scratch + (size_t)g.x * 2 * C;
+  a.coef = coef_out ? coef_out : scratch + (size_t)g.x * 2 * C;  // kept for the backward's ReLU mask
   a.gx = g.x;
   a.num_batches = num_batches;
   a.relu = relu;
@@ -1527,7 +1549,7 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
 
 void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma, const float* mean,
                  const float* invstd, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, int Npix, int C,
-                 bool relu, bool accumulate_params, float* scratch, hipStream_t st) {
+                 bool relu, bool accumulate_params, float* scratch, hipStream_t st, const float* fcoef) {
   const int V = C / 8;
   MX_CHECK(C % 8 == 0 && C <= 2048 && (V >= kBnT ? V % kBnT == 0 : kBnT % V == 0),
            "nhwc bn: unsupported channel count");
@@ -1550,10 +1572,12 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
   a.gx = g.x;
   a.relu = relu;
   a.acc_params = accumulate_params;
+  a.fcoef = (relu && fcoef && C <= 512) ? fcoef : nullptr;
   MX_LAUNCH(bn_nhwc_partial_k<true>, g, dim3(kBnT), 0, st, a);
   MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
-  MX_LAUNCH(bn_nhwc_bwd_apply_k, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));
+  if (a.fcoef) MX_LAUNCH(bn_nhwc_bwd_apply_k<true>, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));
+  else MX_LAUNCH(bn_nhwc_bwd_apply_k<false>, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));
 }
 
 void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, int k,

@@ -213,9 +213,13 @@ class _BN(torch.autograd.Function):
         mean = torch.empty((C,), device=x.device, dtype=torch.float32)
         invstd = torch.empty_like(mean)
         scr = torch.empty((Cn.nhwc_bn_scratch_floats(npix, C),), device=x.device, dtype=torch.float32)
+        # ReLU without residual: keep the affine coefficients, the backward rebuilds the mask from x
+        fcoef = torch.empty((2 * C,), device=x.device, dtype=torch.float32) if (relu and res is None and C <= 512) \
+            else None
         Cn.nhwc_bn_fwd(x.data_ptr(), _p(res), y.data_ptr(), _p(gamma), _p(beta), mean.data_ptr(), invstd.data_ptr(),
                        _p(rm), _p(rv), _p(nbt), npix, C, float(momentum), float(eps), bool(relu), scr.data_ptr(),
-                       stream_of(x))
+                       stream_of(x), _p(fcoef))
+        ctx.fcoef = fcoef
         ctx.save_for_backward(x, y, gamma, mean, invstd)
         ctx.relu, ctx.has_res = bool(relu), res is not None
         ctx.join = join
@@ -237,7 +241,7 @@ class _BN(torch.autograd.Function):
         scr = torch.empty((Cn.nhwc_bn_scratch_floats(N * H * W, C),), device=x.device, dtype=torch.float32)
         Cn.nhwc_bn_bwd(dy.data_ptr(), x.data_ptr(), y.data_ptr(), _p(gamma), mean.data_ptr(), invstd.data_ptr(),
                        dx.data_ptr(), _p(dres), dg.data_ptr(), db.data_ptr(), N * H * W, C, ctx.relu, direct,
-                       scr.data_ptr(), stream_of(dy))
+                       scr.data_ptr(), stream_of(dy), _p(ctx.fcoef))
         if direct:
             dg = db = None
         if ctx.join is not None and dres is not None:
