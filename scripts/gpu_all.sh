@@ -7,3 +7,4 @@ run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 run bench_default 300 python bench.py
 run bench_pyr 300 python bench.py --model pyramidnet110 --impl layers --steps 20 --warmup 3
 run bench_rn 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3
+run bench_rn_b256 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3
