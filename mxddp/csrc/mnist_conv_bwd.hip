@@ -8,6 +8,9 @@
 //   dY2[co][oy][ox] = (q[co][oy/2][ox/2] == 2*(oy&1) + (ox&1)) ? dp[co][oy/2][ox/2] : 0.
 // The expansion is 1 compare + 1 select per element on the VALU, which co-issues with the
 // MFMA pipe; LDS traffic for the A operand drops 4x versus a dense dY2 tile.
+#include <cstdlib>
+#include <string>
+
 #include "mnist_common.h"
 
 namespace mx {
@@ -147,6 +150,168 @@ __device__ __forceinline__ void f6_body(const MnistFused& f, const Scratch& sc, 
       const int co = 16 * w + 4 * g + j, ci = 16 * c + m;
       atomicAdd(sc.wacc + (r * 64 + co) * 32 + ci, acc[c][j]);
     }
+  MX_TRACE_B(f, 3, 3, braw);
+}
+
+// ------------------------------------------------------------------------------------------
+// F6W: the same conv2 weight gradient as Winograd F(2x2,3x3): 2.25x fewer MFMAs.  The 2x2 output
+// tiles of conv2 are exactly the pool windows, so dY2 of tile t has ONE nonzero (value dp, argmax
+// code q) and its Winograd transform A dY A^T = dp * a(qy) a(qx)^T (a(0) = (1,1,1,0),
+// a(1) = (0,1,-1,-1)) is built in registers.  16 GEMMs (one per Winograd point xi) over
+// K = 144 tiles: dU[xi][co][ci] = sum_t W[xi][co][t] V[xi][t][ci], V = B^T a1_t B; then
+// dw = G^T dU G lane-locally (all 16 xi of a (co, ci) sit in one lane) and one atomic per
+// weight per block, into the same [tap][co][ci] accumulator as F6.
+// Block = (image, ci half): all 144 tiles, so the atomics per image stay 64x32x9 as in F6.
+// Wave w = co 16w..16w+15.  6 chunks of 2 tile rows: (A) conv1 + ReLU of the 6 a1 rows of the
+// chunk for the block's 16 ci -> LDS, (B) V of 24 tiles x 16 ci -> LDS ([t][ci][20]: conflict-free
+// ds_read_b128 of the 16 xi), (C) 6 k-steps of 16 MFMAs; K inside a chunk is ordered
+// t = 6g + s (lane group g) so a lane's dp / q operands are 6 contiguous windows (float2 / u16
+// loads, prefetched one chunk ahead).
+constexpr int kF6WA1P = 157, kF6WVP = 20;
+constexpr size_t kF6WLds = sizeof(float) * (784 + 160 + 16 * kF6WA1P + 24 * 16 * kF6WVP);
+__device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc, float* sm, int braw, int nblk) {
+  MX_TRACE_B(f, 3, 0, braw);
+  float* xs = sm;             // [784]
+  float* w1s = xs + 784;      // conv1 w [16][9] then b [16] of this ci half
+  float* a1s = w1s + 160;     // [16 ci][157]: 6 a1 rows x 26
+  float* vs = a1s + 16 * kF6WA1P;  // [24 t][16 ci][20]
+  const int bid = xcd_remap(braw, nblk);
+  const int b = bid >> 1, h = bid & 1;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  {
+    const float4 xv = reinterpret_cast<const float4*>(f.x + b * 784)[min(tid, 195)];
+    const float wv = tid < 144 ? f.p[L::w1 + 144 * h + tid] : f.p[L::b1 + 16 * h + min(tid - 144, 15)];
+    if (tid < 196) *reinterpret_cast<float4*>(xs + 4 * tid) = xv;
+    if (tid < 160) w1s[tid] = wv;
+  }
+  const int co = 16 * w + m;  // A row of this lane
+  const float* dpl = f.dp + (size_t)b * 9216 + co * 144 + 6 * g;
+  const uint16_t* qpl = reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(f.idx) + (size_t)b * 9216 + co * 144 + 6 * g);
+  float2 dn[3];
+  uint16_t qn[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    dn[k] = *reinterpret_cast<const float2*>(dpl + 2 * k);
+    qn[k] = qpl[k];
+  }
+  f32x4 acc[16];
+#pragma unroll
+  for (int x = 0; x < 16; ++x) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  MX_TRACE_B(f, 3, 1, braw);
+  float w1b[3];  // conv1 B fragments: tap 4ks + g of channel m (taps 9..11 are padding)
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) w1b[ks] = 4 * ks + g < 9 ? w1s[m * 9 + 4 * ks + g] : 0.f;
+  const float b1v = w1s[144 + m];
+#pragma unroll 1
+  for (int c = 0; c < 6; ++c) {
+    // (A) a1 rows 4c .. 4c+5 (x rows 4c .. 4c+7 <= 27) for the 16 ci on MFMA: M = 156 positions
+    // (10 tiles of 16, wave w takes tiles w, w+4, w+8), N = 16 ci, K = 9 taps padded to 12
+    for (int mt = w; mt < 10; mt += 4) {
+      const int p = min(16 * mt + m, 155), r = p / 26, col = p - 26 * r;
+      const float* xp = xs + (4 * c + r) * 28 + col;
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const int t = 4 * ks + g;
+        const float av = t < 9 ? xp[(t / 3) * 28 + t % 3] : 0.f;
+        a = mfma4(av, w1b[ks], a);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = 16 * mt + 4 * g + j;
+        if (q < 156) a1s[m * kF6WA1P + q] = fmaxf(a[j] + b1v, 0.f);
+      }
+    }
+    __syncthreads();
+    // (B) V = B^T d B of 24 tiles x 16 ci; tile tl: a1 rows 2(tl/12).., cols 2(tl%12)..
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = tid + 256 * k;
+      if (i < 384) {
+        const int ci = i & 15, tl = i >> 4, tyl = tl / 12, tx = tl - 12 * tyl;
+        const float* ap = a1s + ci * kF6WA1P + 2 * tyl * 26 + 2 * tx;
+        float d[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) d[r][cc] = ap[r * 26 + cc];
+        float e[4][4];
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+          e[0][cc] = d[0][cc] - d[2][cc];
+          e[1][cc] = d[1][cc] + d[2][cc];
+          e[2][cc] = d[2][cc] - d[1][cc];
+          e[3][cc] = d[1][cc] - d[3][cc];
+        }
+        float4* vp = reinterpret_cast<float4*>(vs + (tl * 16 + ci) * kF6WVP);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          vp[r] = make_float4(e[r][0] - e[r][2], e[r][1] + e[r][2], e[r][2] - e[r][1], e[r][1] - e[r][3]);
+      }
+    }
+    // this chunk's dp / q operands; prefetch the next chunk's
+    float dv[6];
+    uint32_t qv[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      dv[2 * k] = dn[k].x;
+      dv[2 * k + 1] = dn[k].y;
+      qv[2 * k] = qn[k] & 0xffu;
+      qv[2 * k + 1] = qn[k] >> 8;
+    }
+    if (c < 5) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        dn[k] = *reinterpret_cast<const float2*>(dpl + 24 * (c + 1) + 2 * k);
+        qn[k] = qpl[12 * (c + 1) + k];
+      }
+    }
+    __syncthreads();
+    // (C) k-step s: tile t = 6g + s of the chunk
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const float4* vp = reinterpret_cast<const float4*>(vs + ((6 * g + s) * 16 + m) * kF6WVP);
+      const float4 b0 = vp[0], b1 = vp[1], b2 = vp[2], b3 = vp[3];
+      const float v = dv[s];
+      const bool qy = (qv[s] >> 1) & 1, qx = qv[s] & 1;
+      const float vy[4] = {qy ? 0.f : v, v, qy ? -v : v, qy ? -v : 0.f};
+      const float4 bb[4] = {b0, b1, b2, b3};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float w0 = qx ? 0.f : vy[i], w2 = qx ? -vy[i] : vy[i], w3 = qx ? -vy[i] : 0.f;
+        acc[4 * i + 0] = mfma4(w0, bb[i].x, acc[4 * i + 0]);
+        acc[4 * i + 1] = mfma4(vy[i], bb[i].y, acc[4 * i + 1]);
+        acc[4 * i + 2] = mfma4(w2, bb[i].z, acc[4 * i + 2]);
+        acc[4 * i + 3] = mfma4(w3, bb[i].w, acc[4 * i + 3]);
+      }
+    }
+  }
+  MX_TRACE_B(f, 3, 2, braw);
+  // dw = G^T dU G, G^T = [1 .5 .5 0; 0 .5 -.5 0; 0 .5 .5 1]; acc[4i + j'][j] = dU[i][j'] of
+  // (co = 16w + 4g + j, ci = 16h + m)
+  const int ci = 16 * h + m;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int cj = 16 * w + 4 * g + j;
+    float t[3][4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const float m0 = acc[jj][j], m1 = acc[4 + jj][j], m2 = acc[8 + jj][j], m3 = acc[12 + jj][j];
+      t[0][jj] = m0 + 0.5f * (m1 + m2);
+      t[1][jj] = 0.5f * (m1 - m2);
+      t[2][jj] = 0.5f * (m1 + m2) + m3;
+    }
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const float o0 = t[ky][0] + 0.5f * (t[ky][1] + t[ky][2]);
+      const float o1 = 0.5f * (t[ky][1] - t[ky][2]);
+      const float o2 = 0.5f * (t[ky][1] + t[ky][2]) + t[ky][3];
+      atomicAdd(sc.wacc + ((ky * 3 + 0) * 64 + cj) * 32 + ci, o0);
+      atomicAdd(sc.wacc + ((ky * 3 + 1) * 64 + cj) * 32 + ci, o1);
+      atomicAdd(sc.wacc + ((ky * 3 + 2) * 64 + cj) * 32 + ci, o2);
+    }
+  }
   MX_TRACE_B(f, 3, 3, braw);
 }
 
@@ -310,18 +475,232 @@ __device__ __forceinline__ void f7_body(const MnistFused& f, const Scratch& sc, 
 }
 
 // ------------------------------------------------------------------------------------------
+// F7W: the same data gradient (+ conv1 mask / weight grads) as Winograd F(2x2,3x3) on fp32 MFMA:
+// 2.25x fewer MFMAs.  dA1 (26x26) = full correlation of dY2 with the flipped filter, in 13x13
+// output tiles of 2x2.  Tile (ty, tx) reads the 4x4 patch of zero-padded dY2 at rows 2ty-2..2ty+1,
+// cols 2tx-2..2tx+1 = exactly the 2x2 pool windows (ty-1..ty, tx-1..tx), each holding ONE nonzero
+// (its argmax), so the input transform V = B^T d B is built from 4 (value, code) pairs straight
+// out of the compact LDS tiles.  16 GEMMs (one per Winograd point xi, K = 64 co) share one MFMA
+// fragment layout, so the output transform A^T M A of a (tile, ci) is lane-local.
+// Block = (image, chunk of 32 tiles); wave w = (M-group w&1: 16 tiles, ci half w>>1: 16 ci);
+// 16 k-steps of 4 co x 16 xi MFMAs.  B fragments (G w' G^T, written by F2) stream from L2 one
+// k-step ahead.  Epilogue as F7: conv1 recomputed for the ReLU mask, conv1 weight/bias grads
+// reduced in registers -> lanes -> LDS -> per-image slab atomics.
+constexpr int kF7WChunks = 6, kF7WRows = 5, kF7WCols = 14, kF7WCoP = 80;
+constexpr size_t kF7WLds = sizeof(float) * (64 * kF7WCoP + 784 + 320 + 640) + 64 * kF7WCoP;
+__device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc, float* sm, int braw, int nblk) {
+  MX_TRACE_B(f, 4, 0, braw);
+  float* dps = sm;                                      // [64 co][80]: 5 window rows x 14 cols
+  float* xs = dps + 64 * kF7WCoP;                       // [784]
+  float* w1s = xs + 784;                                // conv1 w [32][9], b [32]
+  float* red = w1s + 320;                               // [2 M-groups][32 ci][10]
+  uint8_t* qs = reinterpret_cast<uint8_t*>(red + 640);  // [64 co][80] argmax codes
+  const int bid = xcd_remap(braw, nblk);  // an image's 6 blocks share one XCD L2
+  const int b = bid / kF7WChunks, chunk = bid - b * kF7WChunks;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  const int mg = w & 1, half = w >> 1;
+  const int t0 = 32 * chunk, tyf = t0 / 13;  // first tile row of the chunk
+  const int wy0 = tyf - 1;                   // first window row staged (may be -1: halo)
+  {
+    // per co the 5 staged window rows are 60 contiguous floats of dp (rows of 12): 15 float4 /
+    // uint32 (4 argmax codes) granules; rows outside 0..11 and the halo columns become zeros
+    const float4* dpb = reinterpret_cast<const float4*>(f.dp + (size_t)b * 9216);
+    const uint32_t* qb = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(f.idx) + (size_t)b * 9216);
+    constexpr int kN = 64 * kF7WRows * 3, kIt = (kN + 255) / 256;  // 960 granules -> 4
+    float4 dv[kIt];
+    uint32_t qv[kIt];
+#pragma unroll
+    for (int k = 0; k < kIt; ++k) {  // clamped unconditional loads, halo applied afterwards
+      const int i = min(tid + 256 * k, kN - 1), co = i / (kF7WRows * 3), rem = i - co * (kF7WRows * 3);
+      const int wyl = rem / 3, c4 = rem - wyl * 3, wy = min(max(wy0 + wyl, 0), 11);
+      const int o = co * 36 + wy * 3 + c4;  // float4 granule index
+      dv[k] = dpb[o];
+      qv[k] = qb[o];
+    }
+    const float4 xv = reinterpret_cast<const float4*>(f.x + b * 784)[min(tid, 195)];
+    const float4 wv = reinterpret_cast<const float4*>(f.p + L::w1)[min(tid, 79)];
+#pragma unroll
+    for (int k = 0; k < kIt; ++k) {
+      const int i = tid + 256 * k;
+      if (i < kN) {
+        const int co = i / (kF7WRows * 3), rem = i - co * (kF7WRows * 3);
+        const int wyl = rem / 3, c4 = rem - wyl * 3, wy = wy0 + wyl;
+        const bool ok = wy >= 0 && wy < 12;
+        float* dd = dps + co * kF7WCoP + wyl * kF7WCols + 1 + 4 * c4;  // staged column wx + 1
+        uint8_t* qd = qs + co * kF7WCoP + wyl * kF7WCols + 1 + 4 * c4;
+        const float4 v = dv[k];
+        dd[0] = ok ? v.x : 0.f;
+        dd[1] = ok ? v.y : 0.f;
+        dd[2] = ok ? v.z : 0.f;
+        dd[3] = ok ? v.w : 0.f;
+        const uint32_t q = ok ? qv[k] : 0x04040404u;
+        qd[0] = (uint8_t)q;
+        qd[1] = (uint8_t)(q >> 8);
+        qd[2] = (uint8_t)(q >> 16);
+        qd[3] = (uint8_t)(q >> 24);
+        if (c4 == 0) {  // halo columns -1 and 12
+          dd[-1] = 0.f;
+          qd[-1] = 4;
+        } else if (c4 == 2) {
+          dd[4] = 0.f;
+          qd[4] = 4;
+        }
+      }
+    }
+    if (tid < 196) *reinterpret_cast<float4*>(xs + 4 * tid) = xv;
+    if (tid < 80) *reinterpret_cast<float4*>(w1s + 4 * tid) = wv;
+  }
+  __syncthreads();
+  MX_TRACE_B(f, 4, 1, braw);
+  f32x4 acc[16];
+#pragma unroll
+  for (int x = 0; x < 16; ++x) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (t0 + 16 * mg < 169) {  // the last chunk's second M-group has no tile
+    const int tl = min(t0 + 16 * mg + m, 168);  // A row of this lane (clamped rows are discarded)
+    const int ty = tl / 13, tx = tl - 13 * ty;
+    // window (ty-1, tx-1) sits at staged row ty-1-wy0 = ty-tyf, column tx-1+1 = tx
+    const float* dpp = dps + (ty - tyf) * kF7WCols + tx + g * kF7WCoP;
+    const uint8_t* qp = qs + (ty - tyf) * kF7WCols + tx + g * kF7WCoP;
+    const float4* wu = reinterpret_cast<const float4*>(sc.wu) + (half * 64 + lane) * 4;
+    // fully unrolled; B fragments prefetched kF7WPf k-steps ahead (indices fold to registers)
+    constexpr int kF7WPf = 2;
+    float4 bq[16][4];
+#pragma unroll
+    for (int s = 0; s < kF7WPf; ++s)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) bq[s][k] = wu[s * 512 + k];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s + kF7WPf < 16) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bq[s + kF7WPf][k] = wu[(s + kF7WPf) * 512 + k];
+      }
+      const float4* bc = bq[s];
+      const int off = 4 * s * kF7WCoP;  // co = 4s + g
+      float v[4];
+      uint32_t q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // windows (a, c) = (k>>1, k&1) at +a*14 + c
+        const int o = off + (k >> 1) * kF7WCols + (k & 1);
+        v[k] = dpp[o];
+        q[k] = qp[o];
+      }
+      // d[r][c] = nonzero of window (r>>1, c>>1) if its argmax code is 2*(r&1) + (c&1)
+      float d[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int k = (r >> 1) * 2 + (c >> 1);
+          d[r][c] = q[k] == (uint32_t)(((r & 1) << 1) | (c & 1)) ? v[k] : 0.f;
+        }
+      // V = B^T d B, B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1]
+      float e[4][4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        e[0][c] = d[0][c] - d[2][c];
+        e[1][c] = d[1][c] + d[2][c];
+        e[2][c] = d[2][c] - d[1][c];
+        e[3][c] = d[1][c] - d[3][c];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v0 = e[i][0] - e[i][2], v1 = e[i][1] + e[i][2], v2 = e[i][2] - e[i][1], v3 = e[i][1] - e[i][3];
+        acc[4 * i + 0] = mfma4(v0, bc[i].x, acc[4 * i + 0]);
+        acc[4 * i + 1] = mfma4(v1, bc[i].y, acc[4 * i + 1]);
+        acc[4 * i + 2] = mfma4(v2, bc[i].z, acc[4 * i + 2]);
+        acc[4 * i + 3] = mfma4(v3, bc[i].w, acc[4 * i + 3]);
+      }
+    }
+  }
+  MX_TRACE_B(f, 4, 2, braw);
+  // epilogue: acc[xi][j] = Winograd-domain dA1 of tile t0 + 16mg + 4g + j, channel ci = 16half + m
+  const int ci = 16 * half + m;
+  float wk[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) wk[k] = w1s[ci * 9 + k];
+  const float bk = w1s[288 + ci];
+  float part[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) part[k] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int t = t0 + 16 * mg + 4 * g + j;
+    if (t < 169) {
+      const int ty = t / 13, tx = t - 13 * ty;
+      // Y = A^T M A, A^T = [1 1 1 0; 0 1 -1 -1]
+      float p0[4], p1[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        p0[c] = acc[c][j] + acc[4 + c][j] + acc[8 + c][j];
+        p1[c] = acc[4 + c][j] - acc[8 + c][j] - acc[12 + c][j];
+      }
+      float y[2][2];
+      y[0][0] = p0[0] + p0[1] + p0[2];
+      y[0][1] = p0[1] - p0[2] - p0[3];
+      y[1][0] = p1[0] + p1[1] + p1[2];
+      y[1][1] = p1[1] - p1[2] - p1[3];
+      float xp[4][4];  // x patch rows 2ty.., cols 2tx.. (the 3x3 conv1 windows of the 4 outputs)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) xp[r][c] = xs[(2 * ty + r) * 28 + 2 * tx + c];
+#pragma unroll
+      for (int py = 0; py < 2; ++py)
+#pragma unroll
+        for (int px = 0; px < 2; ++px) {
+          float a1v = bk;  // conv1 pre-activation (a1 is not stored)
+#pragma unroll
+          for (int k = 0; k < 9; ++k) a1v = fmaf(xp[py + k / 3][px + k % 3], wk[k], a1v);
+          const float gv = a1v > 0.f ? y[py][px] : 0.f;
+          part[9] += gv;
+#pragma unroll
+          for (int k = 0; k < 9; ++k) part[k] = fmaf(gv, xp[py + k / 3][px + k % 3], part[k]);
+        }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    float v = part[k];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    part[k] = v;
+  }
+  if (g == 0) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) red[(mg * 32 + ci) * 10 + k] = part[k];
+  }
+  __syncthreads();
+  float* g1 = sc.g1 + b * 320;
+  for (int i = tid; i < 320; i += 256) {
+    const float v = red[i] + red[320 + i];
+    const int c = i / 10, k = i - c * 10;
+    if (k < 9) atomicAdd(g1 + c * 9 + k, v);
+    else atomicAdd(g1 + 288 + c, v);
+  }
+  MX_TRACE_B(f, 4, 3, braw);
+}
+
+// ------------------------------------------------------------------------------------------
 // F6 + F7 in ONE launch: blocks [0, 9B) run the weight gradient, the rest the data gradient.
 // The two are independent; sharing a grid lets the dispatcher backfill CUs as blocks retire
 // (576 + 704 blocks over 256 CUs at 3 per CU), so one kernel's prologue/epilogue latency and
 // the 2-vs-3-blocks-per-CU imbalance of each kernel alone are covered by the other's MFMA work.
 // 9B is a multiple of 8, so the F7 part keeps its XCD-aware block mapping.
-__global__ __launch_bounds__(256) void f67_conv2_bwd_kernel(MnistFused f, Scratch sc) {
+template <bool kWino>
+__global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scratch sc) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int n6 = 9 * f.B;
-  if ((int)blockIdx.x < n6)
-    f6_body(f, sc, sm, blockIdx.x, n6);
-  else
+  const int n6 = (kWino ? 2 : 9) * f.B;
+  if ((int)blockIdx.x < n6) {
+    if (kWino)
+      f6w_body(f, sc, sm, blockIdx.x, n6);
+    else
+      f6_body(f, sc, sm, blockIdx.x, n6);
+  } else if (kWino) {
+    f7w_body(f, sc, sm, blockIdx.x - n6, kF7WChunks * f.B);
+  } else {
     f7_body(f, sc, sm, blockIdx.x - n6, 11 * f.B);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -364,16 +743,31 @@ __global__ __launch_bounds__(256) void f8_finalize_kernel(MnistFused f, Scratch 
 
 using namespace mnist;
 
+// F7 variant: 1 = Winograd (default), 0 = direct implicit GEMM (MXDDP_MNIST_F7=direct).
+static bool f7_wino() {
+  static const int v = [] {
+    const char* e = std::getenv("MXDDP_MNIST_F7");
+    return (e && std::string(e) == "direct") ? 0 : 1;
+  }();
+  return v == 1;
+}
+
 void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    MX_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f67_conv2_bwd_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    for (const void* fn : {reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true>),
+                           reinterpret_cast<const void*>(f67_conv2_bwd_kernel<false>)})
+      MX_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const Scratch sc = carve(f.scratch);
-  constexpr size_t lds = kF6Lds > kF7Lds ? kF6Lds : kF7Lds;
-  MX_LAUNCH(f67_conv2_bwd_kernel, dim3(9 * f.B + 11 * f.B), dim3(256), lds, st, f, sc);
+  if (f7_wino()) {
+    constexpr size_t lds = kF6WLds > kF7WLds ? kF6WLds : kF7WLds;
+    MX_LAUNCH(f67_conv2_bwd_kernel<true>, dim3(2 * f.B + kF7WChunks * f.B), dim3(256), lds, st, f, sc);
+  } else {
+    constexpr size_t lds = kF6Lds > kF7Lds ? kF6Lds : kF7Lds;
+    MX_LAUNCH(f67_conv2_bwd_kernel<false>, dim3(9 * f.B + 11 * f.B), dim3(256), lds, st, f, sc);
+  }
   MX_LAUNCH(f8_finalize_kernel, dim3(kF8Wacc + kF8G1 + 8), dim3(256), 0, st, f, sc);
   MX_HIP_CHECK(hipGetLastError());
 }

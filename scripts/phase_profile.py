@@ -2,9 +2,12 @@
 import json
 import sys
 
-import torch
+import os
 
-from mxddp.engine import FusedMnistTrainer
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import torch  # noqa: E402
+
+from mxddp.engine import FusedMnistTrainer  # noqa: E402
 
 tr = FusedMnistTrainer(batch=int(sys.argv[1]) if len(sys.argv) > 1 else 64, device=0, lr=0.01, use_graph=False)
 tr.step(20)
