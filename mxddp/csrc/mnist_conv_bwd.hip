@@ -169,6 +169,8 @@ __device__ __forceinline__ void f6_body(const MnistFused& f, const Scratch& sc, 
 // loads, prefetched one chunk ahead).
 constexpr int kF6WA1P = 157, kF6WVP = 20;
 constexpr size_t kF6WLds = sizeof(float) * (784 + 160 + 16 * kF6WA1P + 24 * 16 * kF6WVP);
+// kF6WSplit = blocks per (image, ci half), each 6 / kF6WSplit chunks
+template <int kF6WSplit>
 __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc, float* sm, int braw, int nblk) {
   MX_TRACE_B(f, 3, 0, braw);
   float* xs = sm;             // [784]
@@ -176,7 +178,7 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
   float* a1s = w1s + 160;     // [16 ci][157]: 6 a1 rows x 26
   float* vs = a1s + 16 * kF6WA1P;  // [24 t][16 ci][20]
   const int bid = xcd_remap(braw, nblk);
-  const int b = bid >> 1, h = bid & 1;
+  const int b = bid / (2 * kF6WSplit), h = bid & 1, c0 = ((bid >> 1) % kF6WSplit) * (6 / kF6WSplit);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
   {
     const float4 xv = reinterpret_cast<const float4*>(f.x + b * 784)[min(tid, 195)];
@@ -191,8 +193,8 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
   uint16_t qn[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    dn[k] = *reinterpret_cast<const float2*>(dpl + 2 * k);
-    qn[k] = qpl[k];
+    dn[k] = *reinterpret_cast<const float2*>(dpl + 24 * c0 + 2 * k);
+    qn[k] = qpl[12 * c0 + k];
   }
   f32x4 acc[16];
 #pragma unroll
@@ -204,7 +206,7 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
   for (int ks = 0; ks < 3; ++ks) w1b[ks] = 4 * ks + g < 9 ? w1s[m * 9 + 4 * ks + g] : 0.f;
   const float b1v = w1s[144 + m];
 #pragma unroll 1
-  for (int c = 0; c < 6; ++c) {
+  for (int c = c0; c < c0 + 6 / kF6WSplit; ++c) {
     // (A) a1 rows 4c .. 4c+5 (x rows 4c .. 4c+7 <= 27) for the 16 ci on MFMA: M = 156 positions
     // (10 tiles of 16, wave w takes tiles w, w+4, w+8), N = 16 ci, K = 9 taps padded to 12
     for (int mt = w; mt < 10; mt += 4) {
@@ -260,7 +262,7 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
       qv[2 * k] = qn[k] & 0xffu;
       qv[2 * k + 1] = qn[k] >> 8;
     }
-    if (c < 5) {
+    if (c + 1 < c0 + 6 / kF6WSplit) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         dn[k] = *reinterpret_cast<const float2*>(dpl + 24 * (c + 1) + 2 * k);
@@ -687,13 +689,13 @@ __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc,
 // (576 + 704 blocks over 256 CUs at 3 per CU), so one kernel's prologue/epilogue latency and
 // the 2-vs-3-blocks-per-CU imbalance of each kernel alone are covered by the other's MFMA work.
 // 9B is a multiple of 8, so the F7 part keeps its XCD-aware block mapping.
-template <bool kWino>
+template <bool kWino, int kF6WSplit = 1>
 __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scratch sc) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int n6 = (kWino ? 2 : 9) * f.B;
+  const int n6 = (kWino ? 2 * kF6WSplit : 9) * f.B;
   if ((int)blockIdx.x < n6) {
     if (kWino)
-      f6w_body(f, sc, sm, blockIdx.x, n6);
+      f6w_body<kF6WSplit>(f, sc, sm, blockIdx.x, n6);
     else
       f6_body(f, sc, sm, blockIdx.x, n6);
   } else if (kWino) {
@@ -743,7 +745,9 @@ __global__ __launch_bounds__(256) void f8_finalize_kernel(MnistFused f, Scratch 
 
 using namespace mnist;
 
-// F7 variant: 1 = Winograd (default), 0 = direct implicit GEMM (MXDDP_MNIST_F7=direct).
+// F7 variant: Winograd (default) or direct implicit GEMM (MXDDP_MNIST_F7=direct); Winograd
+// weight-gradient blocks per (image, ci half): MXDDP_F6W_SPLIT = 1 (default: 748k img/s; 2: 725k,
+// 3: 695k -- more blocks double the weight-gradient atomics and slow the F7W blocks).
 static bool f7_wino() {
   static const int v = [] {
     const char* e = std::getenv("MXDDP_MNIST_F7");
@@ -751,19 +755,38 @@ static bool f7_wino() {
   }();
   return v == 1;
 }
+static int f6w_split() {
+  static const int v = [] {
+    const char* e = std::getenv("MXDDP_F6W_SPLIT");
+    const int s = e ? std::atoi(e) : 1;
+    return (s == 2 || s == 3) ? s : 1;
+  }();
+  return v;
+}
+
+template <int kSplit>
+static void launch_f67_wino(const MnistFused& f, const Scratch& sc, hipStream_t st) {
+  constexpr size_t lds = kF6WLds > kF7WLds ? kF6WLds : kF7WLds;
+  MX_LAUNCH((f67_conv2_bwd_kernel<true, kSplit>), dim3(2 * kSplit * f.B + kF7WChunks * f.B), dim3(256), lds, st, f, sc);
+}
 
 void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    for (const void* fn : {reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true>),
+    for (const void* fn : {reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 1>),
+                           reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 2>),
+                           reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 3>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<false>)})
       MX_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const Scratch sc = carve(f.scratch);
   if (f7_wino()) {
-    constexpr size_t lds = kF6WLds > kF7WLds ? kF6WLds : kF7WLds;
-    MX_LAUNCH(f67_conv2_bwd_kernel<true>, dim3(2 * f.B + kF7WChunks * f.B), dim3(256), lds, st, f, sc);
+    switch (f6w_split()) {
+      case 2: launch_f67_wino<2>(f, sc, st); break;
+      case 3: launch_f67_wino<3>(f, sc, st); break;
+      default: launch_f67_wino<1>(f, sc, st); break;
+    }
   } else {
     constexpr size_t lds = kF6Lds > kF7Lds ? kF6Lds : kF7Lds;
     MX_LAUNCH(f67_conv2_bwd_kernel<false>, dim3(9 * f.B + 11 * f.B), dim3(256), lds, st, f, sc);
