@@ -32,13 +32,14 @@ struct Scratch {  // carve of MnistFused::scratch (floats)
   float* wacc;    // conv2 wgrad accumulator [9 r][64 co][32 ci]
   float* wu;      // conv2 dgrad Winograd filters G w' G^T (w' = w flipped) as F7W B-fragments
                   // [16 k-step][2 ci-half][64 lane][16 xi]
-  float* g1;      // conv1 grad partials per image [B][320] (w[32][9] then b[32])
+  float* g1;      // conv1 grad partial slabs [kG1Slabs][320] (w[32][9] then b[32]), slab = image & 7
 };
 constexpr int kWinoPack = 16 * 2048;  // 16 Winograd-domain values per (co, ci)
+constexpr int kG1Slabs = 8;           // conv1-grad atomics spread over 8 slabs (image & 7)
 inline Scratch carve(float* s) {
   return Scratch{s, s + kPack, s + 2 * kPack, s + 3 * kPack, s + 3 * kPack + kWinoPack};
 }
-inline size_t scratch_floats(int B) { return 3 * (size_t)kPack + kWinoPack + (size_t)B * 320; }
+inline size_t scratch_floats(int) { return 3 * (size_t)kPack + kWinoPack + (size_t)kG1Slabs * 320; }
 
 }  // namespace mnist
 }  // namespace mx

@@ -464,9 +464,9 @@ __device__ __forceinline__ void f7_body(const MnistFused& f, const Scratch& sc, 
       for (int k = 0; k < 10; ++k) red[(w * 32 + 16 * c + m) * 10 + k] = part[c][k];
   }
   __syncthreads();
-  // per-image partial slab (11 chunk blocks per address instead of all 704 blocks hammering
+  // one of 8 partial slabs (image & 7: 88 blocks per address instead of all 704 hammering
   // the same 320 words: same-address float atomics serialise at the memory side)
-  float* g1 = sc.g1 + b * 320;
+  float* g1 = sc.g1 + (b & (kG1Slabs - 1)) * 320;
   for (int i = tid; i < 320; i += 256) {
     const float v = red[i] + red[320 + i] + red[640 + i] + red[960 + i];
     const int ci = i / 10, k = i - ci * 10;
@@ -487,7 +487,7 @@ __device__ __forceinline__ void f7_body(const MnistFused& f, const Scratch& sc, 
 // Block = (image, chunk of 32 tiles); wave w = (M-group w&1: 16 tiles, ci half w>>1: 16 ci);
 // 16 k-steps of 4 co x 16 xi MFMAs.  B fragments (G w' G^T, written by F2) stream from L2 one
 // k-step ahead.  Epilogue as F7: conv1 recomputed for the ReLU mask, conv1 weight/bias grads
-// reduced in registers -> lanes -> LDS -> per-image slab atomics.
+// reduced in registers -> lanes -> LDS -> slab atomics (slab = image & 7).
 constexpr int kF7WChunks = 6, kF7WRows = 5, kF7WCols = 14, kF7WCoP = 80;
 constexpr size_t kF7WLds = sizeof(float) * (64 * kF7WCoP + 784 + 320 + 640) + 64 * kF7WCoP;
 __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc, float* sm, int braw, int nblk) {
@@ -673,7 +673,7 @@ __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc,
     for (int k = 0; k < 10; ++k) red[(mg * 32 + ci) * 10 + k] = part[k];
   }
   __syncthreads();
-  float* g1 = sc.g1 + b * 320;
+  float* g1 = sc.g1 + (b & (kG1Slabs - 1)) * 320;
   for (int i = tid; i < 320; i += 256) {
     const float v = red[i] + red[320 + i];
     const int c = i / 10, k = i - c * 10;
@@ -710,10 +710,9 @@ __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scr
 // the canonical [co][ci][ky][kx] layout; conv1 weight/bias grads = sum over the per-image
 // partial slabs.  Every accumulator it consumes (wacc, g1) and the fc1 split-K accumulator h
 // are reset here for the next step, so the step needs no memset launches.
-// Blocks 0..71: wacc transpose (256 outputs each).  Blocks 72..81: the slab sum, 32 outputs per
-// block, 8 threads per output each summing B/8 images (strided so a wave's loads coalesce),
-// combined with shuffles.  Blocks 82..: zero h.
-constexpr int kF8Wacc = kPack / 256, kF8G1 = 10;
+// Blocks 0..71: wacc transpose (256 outputs each).  Blocks 72..73: the 8-slab sum, one output
+// per thread.  Blocks 74..: zero h.
+constexpr int kF8Wacc = kPack / 256, kF8G1 = 2;
 __global__ __launch_bounds__(256) void f8_finalize_kernel(MnistFused f, Scratch sc) {
   const int blk = blockIdx.x, tid = threadIdx.x;
   if (blk < kF8Wacc) {
@@ -723,18 +722,18 @@ __global__ __launch_bounds__(256) void f8_finalize_kernel(MnistFused f, Scratch 
     f.g[L::w2 + i] = *a;
     *a = 0.f;
   } else if (blk < kF8Wacc + kF8G1) {
-    const int j = (blk - kF8Wacc) * 32 + (tid & 31), part = tid >> 5;  // 8 parts
-    float s = 0.f;
-    for (int b = part; b < f.B; b += 8) {
-      float* p = sc.g1 + b * 320 + j;
-      s += *p;
-      *p = 0.f;
+    const int j = (blk - kF8Wacc) * 256 + tid;  // conv1 w/b grads: fixed-order sum of the slabs
+    if (j < 320) {
+      float v[kG1Slabs], s = 0.f;
+#pragma unroll
+      for (int k = 0; k < kG1Slabs; ++k) v[k] = sc.g1[k * 320 + j];
+#pragma unroll
+      for (int k = 0; k < kG1Slabs; ++k) {
+        s += v[k];
+        sc.g1[k * 320 + j] = 0.f;
+      }
+      f.g[L::w1 + j] = s;
     }
-    s += __shfl_xor(s, 32, 64);  // parts (2k, 2k+1) share a wave: lanes j and j+32
-    __shared__ float red[4][32];
-    if ((tid & 63) < 32) red[tid >> 6][tid & 31] = s;
-    __syncthreads();
-    if (tid < 32) f.g[L::w1 + j] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
   } else {
     for (int i = (blk - kF8Wacc - kF8G1) * 256 + tid; i < f.B * 128; i += 8 * 256) f.h[i] = 0.f;
   }
@@ -770,7 +769,7 @@ static void launch_f67_wino(const MnistFused& f, const Scratch& sc, hipStream_t 
   MX_LAUNCH((f67_conv2_bwd_kernel<true, kSplit>), dim3(2 * kSplit * f.B + kF7WChunks * f.B), dim3(256), lds, st, f, sc);
 }
 
-void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st) {
+void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_sgd) {
   static bool attr = false;
   if (!attr) {
     for (const void* fn : {reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 1>),
@@ -791,7 +790,7 @@ void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st) {
     constexpr size_t lds = kF6Lds > kF7Lds ? kF6Lds : kF7Lds;
     MX_LAUNCH(f67_conv2_bwd_kernel<false>, dim3(9 * f.B + 11 * f.B), dim3(256), lds, st, f, sc);
   }
-  MX_LAUNCH(f8_finalize_kernel, dim3(kF8Wacc + kF8G1 + 8), dim3(256), 0, st, f, sc);
+  if (!finalize_in_sgd) MX_LAUNCH(f8_finalize_kernel, dim3(kF8Wacc + kF8G1 + 8), dim3(256), 0, st, f, sc);
   MX_HIP_CHECK(hipGetLastError());
 }
 

@@ -179,14 +179,15 @@ void MnistEngine::segment(int k) {
       conv2d_wgrad(da1_, x_, g_ + L::w1, s1, false, s_);
       bias_grad(da1_, g_ + L::b1, B, 32, 676, false, s_);
     } else {
-      mnist_fused_conv_bwd(fused_args(), s_);
+      // no gradient collectives this step: F8's finalize folds into the SGD launch
+      mnist_fused_conv_bwd(fused_args(), s_, !reducer_->active());
     }
   } else {  // optimizer: flat SGD, DDP's 1/world_size average folded into the update
     const int ws = comm_ ? comm_->world_size() : 1;
     if (variant_ == 0)
       sgd_step(p_, g_, m_, lr_, 1.f / ws, momentum_, wd_, (int64_t)L::total, false, s_);
     else  // + conv2 weight repack for the next step's F2/F7 + conv2 bias-grad reset
-      mnist_fused_sgd(fused_args(), m_, lr_, 1.f / ws, momentum_, wd_, s_);
+      mnist_fused_sgd(fused_args(), m_, lr_, 1.f / ws, momentum_, wd_, s_, !reducer_->active());
   }
 }
 

@@ -48,7 +48,12 @@ class MnistEngine {
   void capture(int mode = -1, int steps_per_graph = 1);
   void replay(int n);        // n steps via the captured graph(s) (eager if not captured)
   int graph_mode() const { return graph_mode_; }
-  void set_force_collectives(bool on) { reducer_->set_force_collectives(on); }
+  // captured graphs bake in whether collectives run (and whether F8 folds into the SGD launch):
+  // changing it drops them (eager until capture() is called again)
+  void set_force_collectives(bool on) {
+    if (on != reducer_->forced()) uncapture();
+    reducer_->set_force_collectives(on);
+  }
   void set_overlap(bool on) { reducer_->set_overlap(on); }  // see Reducer::set_overlap
   bool overlap() const { return reducer_->overlap(); }
   bool reducer_active() const { return reducer_->active(); }

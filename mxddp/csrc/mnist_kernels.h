@@ -33,8 +33,9 @@ size_t mnist_fused_scratch_floats(int B);
 void mnist_fused_init(const MnistFused& f, hipStream_t st);
 void mnist_fused_forward(const MnistFused& f, hipStream_t st);  // F2 + F3
 void mnist_fused_fc1_bwd(const MnistFused& f, hipStream_t st);  // F5 (head + fc1 backward)
-void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st); // F6 + F7 + F8
+// F6 + F7 (+ F8 unless `finalize_in_sgd`: then mnist_fused_sgd(..., finalize = true) does F8's work)
+void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_sgd = false);
 void mnist_fused_sgd(const MnistFused& f, float* mom_buf, const float* lr, float gscale, float momentum, float wd,
-                     hipStream_t st);
+                     hipStream_t st, bool finalize = false);
 
 }  // namespace mx

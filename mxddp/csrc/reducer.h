@@ -45,6 +45,7 @@ class Reducer {
   // issue the collectives even at world_size 1 (exercises the RCCL + graph-capture path on
   // a single GPU; an all-reduce over one rank is the identity)
   void set_force_collectives(bool on) { force_ = on; }
+  bool forced() const { return force_; }
   // overlap = true: each bucket's all-reduce runs on the side comm stream as soon as it is ready
   // (event fence compute -> comm, and compute waits on comm at finalize).  overlap = false: the
   // all-reduces are issued in order on the compute stream itself -- no cross-stream fences,
