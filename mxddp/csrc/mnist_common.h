@@ -33,13 +33,16 @@ struct Scratch {  // carve of MnistFused::scratch (floats)
   float* wu;      // conv2 dgrad Winograd filters G w' G^T (w' = w flipped) as F7W B-fragments
                   // [16 k-step][2 ci-half][64 lane][16 xi]
   float* g1;      // conv1 grad partial slabs [kG1Slabs][320] (w[32][9] then b[32]), slab = image & 7
+  float* wv;      // conv2 forward Winograd filters G w G^T as F2W B-fragments
+                  // [4 w][16 xi][2 s4][64 lane][4 j]
 };
 constexpr int kWinoPack = 16 * 2048;  // 16 Winograd-domain values per (co, ci)
 constexpr int kG1Slabs = 8;           // conv1-grad atomics spread over 8 slabs (image & 7)
 inline Scratch carve(float* s) {
-  return Scratch{s, s + kPack, s + 2 * kPack, s + 3 * kPack, s + 3 * kPack + kWinoPack};
+  float* g1 = s + 3 * kPack + kWinoPack;
+  return Scratch{s, s + kPack, s + 2 * kPack, s + 3 * kPack, g1, g1 + kG1Slabs * 320};
 }
-inline size_t scratch_floats(int) { return 3 * (size_t)kPack + kWinoPack + (size_t)kG1Slabs * 320; }
+inline size_t scratch_floats(int) { return 3 * (size_t)kPack + 2 * (size_t)kWinoPack + (size_t)kG1Slabs * 320; }
 
 }  // namespace mnist
 }  // namespace mx

@@ -747,7 +747,7 @@ using namespace mnist;
 // F7 variant: Winograd (default) or direct implicit GEMM (MXDDP_MNIST_F7=direct); Winograd
 // weight-gradient blocks per (image, ci half): MXDDP_F6W_SPLIT = 1 (default: 748k img/s; 2: 725k,
 // 3: 695k -- more blocks double the weight-gradient atomics and slow the F7W blocks).
-static bool f7_wino() {
+bool mnist_f7_wino() {
   static const int v = [] {
     const char* e = std::getenv("MXDDP_MNIST_F7");
     return (e && std::string(e) == "direct") ? 0 : 1;
@@ -780,7 +780,7 @@ void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_
     attr = true;
   }
   const Scratch sc = carve(f.scratch);
-  if (f7_wino()) {
+  if (mnist_f7_wino()) {
     switch (f6w_split()) {
       case 2: launch_f67_wino<2>(f, sc, st); break;
       case 3: launch_f67_wino<3>(f, sc, st); break;

@@ -28,6 +28,7 @@ struct MnistFused {
 };
 
 size_t mnist_fused_scratch_floats(int B);
+bool mnist_f7_wino();  // conv2 data gradient as Winograd (default) vs direct (MXDDP_MNIST_F7=direct)
 // Pack conv2 weights into the F2/F7 fragment orders and zero the cross-step accumulators;
 // needed once and after any change of the parameters outside the fused SGD.
 void mnist_fused_init(const MnistFused& f, hipStream_t st);

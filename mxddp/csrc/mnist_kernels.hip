@@ -76,20 +76,161 @@ __device__ __forceinline__ void wino_dgrad_filter(const MnistFused& f, const Scr
   for (int k = 0; k < 4; ++k) dst[k] = make_float4(u[4 * k], u[4 * k + 1], u[4 * k + 2], u[4 * k + 3]);
 }
 
+// F2W B operand: U = G w G^T for (co, ci) (forward = plain correlation, no flip), u[4a + b] with
+// a the ky-side and b the kx-side Winograd point.  Stored at ((((co/16)*16 + xi)*2 + s/4)*64 +
+// lane)*4 + (s&3) for k-step s = ci/4, lane = (co & 15) + 16*(ci & 3): a wave (= 16 output
+// channels) reads one float4 per lane per (xi, 4 k-steps).
+__device__ __forceinline__ int wv_index(int co, int ci, int xi) {
+  const int s = ci >> 2, l = (co & 15) + 16 * (ci & 3);
+  return ((((co >> 4) * 16 + xi) * 2 + (s >> 2)) * 64 + l) * 4 + (s & 3);
+}
+// Every packed form of conv2 weight pair (co, ci) (taps w[0..8] = w[co][ci][ky][kx]):
+// F2 / F7 direct fragments and the F2W Winograd filter.
+// (pack_direct = false: only the Winograd filter -- the direct F2 / F7 kernels are not in use)
+__device__ __forceinline__ void conv2_pack_pair(const Scratch& sc, int pair, const float w[9], bool pack_direct = true) {
+  const int co = pair >> 5, ci = pair & 31;
+  if (pack_direct) {
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      sc.wf[wf_index(co, ci, r)] = w[r];
+      sc.wd[wd_index(co, ci, r)] = w[r];
+    }
+  }
+  float t[4][3];
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    t[0][b] = w[b];
+    t[1][b] = 0.5f * (w[b] + w[3 + b] + w[6 + b]);
+    t[2][b] = 0.5f * (w[b] - w[3 + b] + w[6 + b]);
+    t[3][b] = w[6 + b];
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    sc.wv[wv_index(co, ci, 4 * a + 0)] = t[a][0];
+    sc.wv[wv_index(co, ci, 4 * a + 1)] = 0.5f * (t[a][0] + t[a][1] + t[a][2]);
+    sc.wv[wv_index(co, ci, 4 * a + 2)] = 0.5f * (t[a][0] - t[a][1] + t[a][2]);
+    sc.wv[wv_index(co, ci, 4 * a + 3)] = t[a][2];
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // K0 (once, and after any external weight load): pack conv2 weights, zero accumulators.
 __global__ __launch_bounds__(256) void k_init(MnistFused f, Scratch sc) {
   const int gtid = blockIdx.x * 256 + threadIdx.x, gsz = gridDim.x * 256;
-  for (int i = gtid; i < kPack; i += gsz) {
-    const int co = i / 288, rem = i - co * 288, ci = rem / 9, r = rem - ci * 9;
-    const float v = f.p[L::w2 + i];
-    sc.wf[wf_index(co, ci, r)] = v;
-    sc.wd[wd_index(co, ci, r)] = v;
-    sc.wacc[i] = 0.f;
+  for (int i = gtid; i < kPack; i += gsz) sc.wacc[i] = 0.f;
+  for (int i = gtid; i < 2048; i += gsz) {
+    float w[9];
+#pragma unroll
+    for (int r = 0; r < 9; ++r) w[r] = f.p[L::w2 + i * 9 + r];
+    conv2_pack_pair(sc, i, w);
   }
   for (int i = gtid; i < f.B * 128; i += gsz) f.h[i] = 0.f;
   for (int i = gtid; i < kG1Slabs * 320; i += gsz) sc.g1[i] = 0.f;
   if (gtid < 64) f.g[L::b2 + gtid] = 0.f;
+}
+
+constexpr int kF2RowP = 40, kF2ChP = 176;  // F2 a1 tile pitches (see f2_fwd_kernel)
+
+// F2W stage 2 (see f2_fwd_kernel): a1 tile [32 ci][4 rows][26] (pitches kF2ChP / kF2RowP) in
+// `tile` -> pooled conv2 outputs of pooled row py of image b.
+__device__ __forceinline__ void f2_stage2_wino(const MnistFused& f, const Scratch& sc, float* tile, int b, int py,
+                                               int w, int lane, const float4 (&bp)[4]) {
+  const int tid = threadIdx.x;
+  // (a) input transform: items (ci, t) = it / 12, it % 12, two per thread (384 items)
+  float v[2][16];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int it = tid + 256 * k;
+    if (it < 384) {
+      const int ci = it / 12, t = it - 12 * (it / 12);
+      const float* d = tile + ci * kF2ChP + 2 * t;
+      float x[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[i][j] = d[i * kF2RowP + j];
+      float r[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        r[0][j] = x[0][j] - x[2][j];
+        r[1][j] = x[1][j] + x[2][j];
+        r[2][j] = x[2][j] - x[1][j];
+        r[3][j] = x[1][j] - x[3][j];
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        v[k][4 * a + 0] = r[a][0] - r[a][2];
+        v[k][4 * a + 1] = r[a][1] + r[a][2];
+        v[k][4 * a + 2] = r[a][2] - r[a][1];
+        v[k][4 * a + 3] = r[a][1] - r[a][3];
+      }
+    }
+  }
+  __syncthreads();  // every a1 read done: V overwrites the tile
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int it = tid + 256 * k;
+    if (it < 384) {
+      const int ci = it / 12, t = it - 12 * (it / 12);
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) tile[xi * 512 + ci * 16 + t] = v[k][xi];
+    }
+  }
+  __syncthreads();
+  MX_TRACE(f, 0, 3);
+  // (b) 16 GEMMs; lane: A row = tile m, k = ci 4s + g; B col = co 16w + m
+  const int m = lane & 15, g = lane >> 4;
+  const float4* up = reinterpret_cast<const float4*>(sc.wv) + (size_t)w * 16 * 2 * 64 + lane;
+  // Points are processed in pairs: two independent accumulator chains interleave, so a
+  // dependent MFMA never waits on its predecessor's latency; the next pair's B fragments are
+  // in flight during the current pair's MFMAs.
+  f32x4 acc[16];
+  float4 bc[4] = {bp[0], bp[1], bp[2], bp[3]};  // xi = 0, 1 fragments, loaded at kernel start
+#pragma unroll
+  for (int xp = 0; xp < 8; ++xp) {
+    float4 bn[4] = {bc[0], bc[1], bc[2], bc[3]};
+    if (xp < 7) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bn[q] = up[(2 * xp + 2 + (q >> 1)) * 128 + 64 * (q & 1)];
+    }
+    acc[2 * xp] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc[2 * xp + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* a = tile + 2 * xp * 512 + g * 16 + m;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      acc[2 * xp] = mfma4(a[64 * s], sel4(bc[s >> 2], s & 3), acc[2 * xp]);
+      acc[2 * xp + 1] = mfma4(a[512 + 64 * s], sel4(bc[2 + (s >> 2)], s & 3), acc[2 * xp + 1]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bc[q] = bn[q];
+  }
+  MX_TRACE(f, 0, 4);
+  // (c) lane holds points xi of tiles 4g + j (j < 4), channel co: inverse transform + pool
+  if (g < 3) {
+    const int co = 16 * w + m;
+    const float bias = f.p[L::b2 + co];
+    uint8_t* idx = reinterpret_cast<uint8_t*>(f.idx);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float r0[4], r1[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        r0[c] = acc[c][j] + acc[4 + c][j] + acc[8 + c][j];
+        r1[c] = acc[4 + c][j] - acc[8 + c][j] - acc[12 + c][j];
+      }
+      const float y[4] = {r0[0] + r0[1] + r0[2], r0[1] - r0[2] - r0[3], r1[0] + r1[1] + r1[2],
+                          r1[1] - r1[2] - r1[3]};  // (dy, dx) = (0,0) (0,1) (1,0) (1,1)
+      float best = y[0];
+      int q = 0;
+#pragma unroll
+      for (int e = 1; e < 4; ++e)
+        if (y[e] > best) { best = y[e]; q = e; }
+      const float vv = best + bias;
+      const int o = ((b * 64 + co) * 12 + py) * 12 + 4 * g + j;
+      f.pool[o] = vv > 0.f ? vv : 0.f;
+      idx[o] = vv > 0.f ? (uint8_t)q : (uint8_t)4;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -106,20 +247,34 @@ __global__ __launch_bounds__(256) void k_init(MnistFused f, Scratch sc) {
 // [32 ci][4 rows][26] has row pitch 40 and channel pitch 176 (= 8, 16 mod 32 banks): the 32
 // lanes of each ds_read_b32 half-wave hit 32 distinct banks.  B fragments for all 72 k-steps
 // (18 float4 per lane, pre-packed by the previous SGD) are loaded once into registers.
-constexpr int kF2RowP = 40, kF2ChP = 176;
+//
+// kWino (default; MXDDP_MNIST_F2=direct selects the above): stage 2 as Winograd F(2x2,3x3).  The
+// block's 12 pooling windows are exactly 12 Winograd output tiles, so the per-tile inverse
+// transform ends in the 2x2 max-pool.  V = B^T d B of every (tile, ci) goes to LDS over the a1
+// tile ([16 xi][32 ci][16 tiles], tiles 12..15 unused rows), then 16 GEMMs (one per Winograd
+// point) M = 16 tiles x N = 64 co (wave w: 16 co) x K = 32 ci: 128 MFMAs per wave instead of
+// 216.  The 16 accumulators of a lane hold all 16 points of its (tile, co), so A^T M A, bias,
+// max-pool, argmax and ReLU happen in registers.
+template <bool kWino>
 __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
   MX_TRACE(f, 0, 0);
-  __shared__ float tile[32 * kF2ChP];
+  __shared__ float tile[kWino ? 16 * 32 * 16 : 32 * kF2ChP];
   __shared__ float xs[6 * 28];
   __shared__ float w1s[288 + 32];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);  // an image's 12 blocks share one XCD L2
   const int b = bid / 12, py = bid - b * 12;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int row0 = 2 * py;  // first input row of this block's conv1 rows
-  float4 bq[18];
-  const float4* wf = reinterpret_cast<const float4*>(sc.wf) + w * 64 + lane;
+  float4 bq[kWino ? 4 : 18];
+  if constexpr (kWino) {  // F2W: first B fragments (points 0, 1) in flight during stage 1
+    const float4* up = reinterpret_cast<const float4*>(sc.wv) + (size_t)w * 16 * 2 * 64 + lane;
 #pragma unroll
-  for (int q = 0; q < 18; ++q) bq[q] = wf[q * 256];
+    for (int q = 0; q < 4; ++q) bq[q] = up[(q >> 1) * 128 + 64 * (q & 1)];
+  } else {
+    const float4* wf = reinterpret_cast<const float4*>(sc.wf) + w * 64 + lane;
+#pragma unroll
+    for (int q = 0; q < 18; ++q) bq[q] = wf[q * 256];
+  }
   // ---- stage 1a: input rows row0 .. row0+5 (+ publish the rows this block owns)
   const int own_lo = row0, own_hi = py == 11 ? 28 : row0 + 2;  // x rows written by this block
   if (f.synth) {
@@ -179,6 +334,9 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
   __syncthreads();
   MX_TRACE(f, 0, 2);
   MX_TRACE(f, 0, 3);
+  if constexpr (kWino) {
+    f2_stage2_wino(f, sc, tile, b, py, w, lane, *reinterpret_cast<const float4(*)[4]>(bq));
+  } else {
   // ---- stage 2: conv2 implicit GEMM + pool
   const int m = lane & 15, g = lane >> 4;
   const int base = g * kF2ChP + ((m >> 1) & 1) * kF2RowP + 2 * (m >> 2) + (m & 1);
@@ -209,6 +367,7 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
     const int o = ((b * 64 + co) * 12 + py) * 12 + 4 * t + g;
     f.pool[o] = v > 0.f ? v : 0.f;
     idx[o] = v > 0.f ? (uint8_t)q : (uint8_t)4;
+  }
   }
   // side job of the first 8 blocks: this step's conv2 data-gradient Winograd filters for F7W
   if (blockIdx.x < 8) wino_dgrad_filter(f, sc, blockIdx.x * 256 + tid);
@@ -516,7 +675,7 @@ __global__ __launch_bounds__(256) void f5_head_fc1_bwd_kernel(MnistFused f) {
 template <bool kFin>
 __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc, float* __restrict__ buf,
                                                        const float* __restrict__ lr_ptr, float gscale, float mom,
-                                                       float wd) {
+                                                       float wd, bool pack_direct) {
   const float lr = *lr_ptr;
   float4* p4 = reinterpret_cast<float4*>(f.p);
   float4* g4 = reinterpret_cast<float4*>(f.g);
@@ -527,37 +686,27 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
     for (int i = blockIdx.x * 256 + threadIdx.x; i < f.B * 32; i += gridDim.x * 256)
       h4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  constexpr int kW2a = (int)L::w2 / 4, kW2b = ((int)L::w2 + kPack) / 4;  // conv2 weights (float4 range)
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
+    if (i >= kW2a && i < kW2b) continue;  // per (co, ci) pair below
     float4 pv = p4[i];
     float4 gv = g4[i];
-    if (kFin && i < (int)(L::w2 + kPack) / 4) {
-      if (i < (int)L::w2 / 4) {  // conv1 w/b: fixed-order sum of the 8 slabs
-        float4* sl = reinterpret_cast<float4*>(sc.g1) + i;
-        float4 v[kG1Slabs];
+    if (kFin && i < kW2a) {  // conv1 w/b: fixed-order sum of the 8 slabs
+      float4* sl = reinterpret_cast<float4*>(sc.g1) + i;
+      float4 v[kG1Slabs];
 #pragma unroll
-        for (int k = 0; k < kG1Slabs; ++k) v[k] = sl[k * 80];
-        float4 a = v[0];
+      for (int k = 0; k < kG1Slabs; ++k) v[k] = sl[k * 80];
+      float4 a = v[0];
 #pragma unroll
-        for (int k = 1; k < kG1Slabs; ++k) {
-          a.x += v[k].x;
-          a.y += v[k].y;
-          a.z += v[k].z;
-          a.w += v[k].w;
-        }
-#pragma unroll
-        for (int k = 0; k < kG1Slabs; ++k) sl[k * 80] = make_float4(0.f, 0.f, 0.f, 0.f);
-        gv = a;
-      } else {  // conv2 w: transpose out of the [tap][co][ci] accumulator
-        float e[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int c = 4 * i + j - (int)L::w2, co = c / 288, rem = c - co * 288, ci = rem / 9, r = rem - ci * 9;
-          float* a = sc.wacc + (r * 64 + co) * 32 + ci;
-          e[j] = *a;
-          *a = 0.f;
-        }
-        gv = make_float4(e[0], e[1], e[2], e[3]);
+      for (int k = 1; k < kG1Slabs; ++k) {
+        a.x += v[k].x;
+        a.y += v[k].y;
+        a.z += v[k].z;
+        a.w += v[k].w;
       }
+#pragma unroll
+      for (int k = 0; k < kG1Slabs; ++k) sl[k * 80] = make_float4(0.f, 0.f, 0.f, 0.f);
+      gv = a;
       g4[i] = gv;
     }
     float4 bv = b4[i];
@@ -571,18 +720,34 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
     pv.w -= lr * bv.w;
     b4[i] = bv;
     p4[i] = pv;
-    const int e0 = 4 * i;
-    if (e0 >= (int)L::w2 && e0 < (int)L::w2 + kPack) {
-      const float pe[4] = {pv.x, pv.y, pv.z, pv.w};
+    if (i >= kW2b && i < kW2b + 16) g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);  // conv2 bias grad reset
+  }
+  // conv2 weights: one thread per (co, ci) pair updates its 9 taps and writes every packed form
+  // (kFin: the gradient is read -- and reset -- straight from the [tap][co][ci] accumulator).
+  // The pairs go to wave 0 of the grid's last 32 blocks (one main-loop pass each: 32 CUs share
+  // the scattered stores); all 27 loads are issued before any store.
+  const int pair = ((int)blockIdx.x - ((int)gridDim.x - 32)) * 64 + (int)threadIdx.x;
+  if (blockIdx.x + 32 >= gridDim.x && threadIdx.x < 64 && pair >= 0 && pair < 2048) {
+    const int co = pair >> 5, ci = pair & 31, e0 = (int)L::w2 + pair * 9;
+    float gg[9], pe[9], bb[9];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = e0 + j - (int)L::w2, co = c / 288, rem = c - co * 288, ci = rem / 9, r = rem - ci * 9;
-        sc.wf[wf_index(co, ci, r)] = pe[j];
-        sc.wd[wd_index(co, ci, r)] = pe[j];
-      }
-    } else if (e0 >= (int)L::b2 && e0 < (int)L::b2 + 64) {
-      g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < 9; ++r) {
+      gg[r] = kFin ? sc.wacc[(r * 64 + co) * 32 + ci] : f.g[e0 + r];
+      pe[r] = f.p[e0 + r];
+      bb[r] = buf[e0 + r];
     }
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      bb[r] = mom * bb[r] + (gg[r] * gscale + wd * pe[r]);
+      pe[r] -= lr * bb[r];
+      if (kFin) {
+        sc.wacc[(r * 64 + co) * 32 + ci] = 0.f;
+        f.g[e0 + r] = gg[r];
+      }
+      buf[e0 + r] = bb[r];
+      f.p[e0 + r] = pe[r];
+    }
+    conv2_pack_pair(sc, pair, pe, pack_direct);
   }
   if (blockIdx.x == 0 && threadIdx.x < (int)(L::total - 4 * n4)) {  // 2-element tail (fc2.bias)
     const int e = 4 * n4 + threadIdx.x;
@@ -619,6 +784,15 @@ static void set_lds_limits() {
   done = true;
 }
 
+// F2 variant: Winograd conv2 (default) or direct implicit GEMM (MXDDP_MNIST_F2=direct).
+static bool f2_wino() {
+  static const int v = [] {
+    const char* e = std::getenv("MXDDP_MNIST_F2");
+    return (e && std::string(e) == "direct") ? 0 : 1;
+  }();
+  return v == 1;
+}
+
 void mnist_fused_init(const MnistFused& f, hipStream_t st) {
   check(f);
   set_lds_limits();
@@ -630,7 +804,10 @@ void mnist_fused_forward(const MnistFused& f, hipStream_t st) {
   check(f);
   set_lds_limits();
   const Scratch sc = carve(f.scratch);
-  MX_LAUNCH(f2_fwd_kernel, dim3(f.B * 12), dim3(256), 0, st, f, sc);
+  if (f2_wino())
+    MX_LAUNCH(f2_fwd_kernel<true>, dim3(f.B * 12), dim3(256), 0, st, f, sc);
+  else
+    MX_LAUNCH(f2_fwd_kernel<false>, dim3(f.B * 12), dim3(256), 0, st, f, sc);
   MX_LAUNCH(f3_fc1_kernel, dim3((9216 / kF3Chunk) * 4), dim3(256), 0, st, f);
   MX_HIP_CHECK(hipGetLastError());
 }
@@ -657,10 +834,10 @@ void mnist_fused_sgd(const MnistFused& f, float* mom_buf, const float* lr, float
                      hipStream_t st, bool finalize) {
   if (finalize)
     MX_LAUNCH(sgd_pack_kernel<true>, dim3(1024), dim3(256), 0, st, f, carve(f.scratch), mom_buf, lr, gscale,
-              momentum, wd);
+              momentum, wd, !(f2_wino() && mnist_f7_wino()));
   else
     MX_LAUNCH(sgd_pack_kernel<false>, dim3(1024), dim3(256), 0, st, f, carve(f.scratch), mom_buf, lr, gscale,
-              momentum, wd);
+              momentum, wd, !(f2_wino() && mnist_f7_wino()));
   MX_HIP_CHECK(hipGetLastError());
 }
 
