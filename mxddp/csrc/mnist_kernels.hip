@@ -549,16 +549,21 @@ __global__ __launch_bounds__(256) void f5_head_fc1_bwd_kernel(MnistFused f) {
   __syncthreads();
   MX_TRACE(f, 2, 3);
   if (blockIdx.x < 10 && tid <= 128) {  // fc2 grad row c = blockIdx.x (+ its bias grad) from h and dlogits
+    // 8 independent partial sums (B % 16 == 0): no serial LDS-latency chain, so blocks 0..9
+    // finish with the rest of the grid
     const int c = blockIdx.x;
-    float acc = 0.f;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (tid < 128) {
-#pragma unroll 8
-      for (int b = 0; b < B; ++b) acc = fmaf(lg[b * kF5LgP + c], dhs[b * kF5DhP + tid], acc);
-      f.g[L::fw2 + c * 128 + tid] = acc;
+      for (int b = 0; b < B; b += 8)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = fmaf(lg[(b + k) * kF5LgP + c], dhs[(b + k) * kF5DhP + tid], acc[k]);
     } else {
-      for (int b = 0; b < B; ++b) acc += lg[b * kF5LgP + c];
-      f.g[L::fb2 + c] = acc;
+      for (int b = 0; b < B; b += 8)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += lg[(b + k) * kF5LgP + c];
     }
+    const float sum = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    f.g[tid < 128 ? L::fw2 + c * 128 + tid : L::fb2 + c] = sum;
   }
   if (blockIdx.x == 0 && tid == 0 && f.metrics) {
     atomicAdd(f.metrics, misc[2]);
@@ -586,10 +591,11 @@ __global__ __launch_bounds__(256) void f5_head_fc1_bwd_kernel(MnistFused f) {
   __syncthreads();
   MX_TRACE(f, 2, 4);
   if (blockIdx.x == 10 && tid < 128) {
-    float acc = 0.f;
-#pragma unroll 8
-    for (int b = 0; b < B; ++b) acc += dhs[b * kF5DhP + tid];
-    f.g[L::fb1 + tid] = acc;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < B; b += 8)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += dhs[(b + k) * kF5DhP + tid];
+    f.g[L::fb1 + tid] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   }
   // ---- dW1 tiles: rows n (8 M-tiles, wave w takes 2w, 2w+1), cols kF5NT N-tiles, K = B
   {

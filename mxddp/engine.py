@@ -218,6 +218,11 @@ class FusedMnistTrainer:
                            "kernel": (last.max() - t0.min()).item() * 0.01}
                     rec["phases"] = [((tk[:, ph] - t0)[tk[:, ph] != 0]).double().median().item() * 0.01
                                      for ph in range(1, 8) if (tk[:, ph] != 0).any()]
+                    # the 4 slowest blocks: (block, start, phase marks) in us after the kernel's first start
+                    ids = torch.nonzero(live).flatten()
+                    t00 = t0.min()
+                    rec["slowest"] = [(int(ids[i]), [round((int(v) - int(t00)) * 0.01, 2) for v in tk[i] if v != 0])
+                                      for i in torch.argsort(last, descending=True)[:4].tolist()]
                     acc[n].append(rec)
         finally:
             self.eng.set_trace(0)
@@ -226,7 +231,8 @@ class FusedMnistTrainer:
             runs = runs[1:]  # drop the first (cold) step
             if not runs:
                 continue
-            avg = {k: round(sum(r[k] for r in runs) / len(runs), 2) for k in runs[0] if k != "phases"}
+            avg = {k: round(sum(r[k] for r in runs) / len(runs), 2) for k in runs[0] if k not in ("phases", "slowest")}
+            avg["slowest_last_step"] = runs[-1]["slowest"]
             m = min(len(r["phases"]) for r in runs)
             avg["phases"] = [round(sum(r["phases"][i] for r in runs) / len(runs), 2) for i in range(m)]
             out[n] = avg
