@@ -521,6 +521,7 @@ __global__ __launch_bounds__(256) void f5_head_fc1_bwd_kernel(MnistFused f) {
   __syncthreads();
   MX_TRACE(f, 2, 2);
   // ---- head: softmax / NLL / accuracy / dlogits (one thread per row)
+  float loss_v = 0.f, corr_v = 0.f;
   if (tid < B) {
     float* l = lg + tid * kF5LgP;
     float mx = l[0];
@@ -536,15 +537,20 @@ __global__ __launch_bounds__(256) void f5_head_fc1_bwd_kernel(MnistFused f) {
     float ly = 0.f;
 #pragma unroll
     for (int c = 0; c < 10; ++c) ly = c == y ? l[c] : ly;
-    if (blockIdx.x == 0) {
-      atomicAdd(&misc[2], lse - ly);
-      atomicAdd(&misc[3], am == y ? 1.f : 0.f);
-    }
+    loss_v = lse - ly;
+    corr_v = am == y ? 1.f : 0.f;
     const float inv = 1.f / (float)B;
 #pragma unroll
     for (int c = 0; c < 10; ++c) l[c] = (__expf(l[c] - lse) - (c == y ? 1.f : 0.f)) * inv;
 #pragma unroll
     for (int c = 10; c < 16; ++c) l[c] = 0.f;
+  }
+  if (blockIdx.x == 0 && 64 * w < B) {  // batch loss / correct: one LDS atomic per wave
+    const float ls = wave_sum(loss_v), cs = wave_sum(corr_v);
+    if (lane == 0) {
+      atomicAdd(&misc[2], ls);
+      atomicAdd(&misc[3], cs);
+    }
   }
   __syncthreads();
   MX_TRACE(f, 2, 3);
