@@ -27,14 +27,20 @@ def native():
     global _C, _C_ERR
     if _C is not None:
         return _C
+    from . import _build
+
+    if os.path.exists(_build.ext_path()) and _build.is_stale():
+        # the in-tree module was built from different sources: rebuild, or refuse to run it
+        if os.environ.get("MXDDP_NO_AUTOBUILD") or not os.path.exists(_build.HIPCC):
+            raise ImportError(f"{_build.ext_path()} is stale (csrc changed since it was built); "
+                              "run `python -m mxddp._build`")
+        _build.build(verbose=True)
     try:
         _C = importlib.import_module("mxddp._C")
     except ImportError as e:  # not built yet
         if os.environ.get("MXDDP_NO_AUTOBUILD"):
             _C_ERR = e
             raise
-        from . import _build
-
         _build.build(verbose=True)
         _C = importlib.import_module("mxddp._C")
     return _C

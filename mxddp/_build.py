@@ -86,6 +86,30 @@ def _sources() -> list[str]:
     return sorted(srcs)
 
 
+def stamp_path() -> str:
+    return ext_path() + ".srcsha"
+
+
+def source_digest() -> str:
+    """Digest of every source and header under csrc plus the compile flags: the built module
+    records it (``_C*.so.srcsha``) and ``mxddp.native()`` refuses a module whose digest no
+    longer matches the tree (a stale .so shipped to a GPU box after a csrc edit)."""
+    h = hashlib.sha256(" ".join(_common_flags()).encode())
+    for p in sorted(_sources() + glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)):
+        with open(p, "rb") as f:
+            h.update(os.path.relpath(p, CSRC).encode())
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def is_stale() -> bool:
+    try:
+        with open(stamp_path()) as f:
+            return f.read().strip() != source_digest()
+    except OSError:
+        return True
+
+
 def _compile_one(src: str, flags: list[str], hdr_digest: str, force: bool) -> tuple[str, bool]:
     rel = os.path.relpath(src, CSRC).replace(os.sep, "__")
     obj = os.path.join(BUILD_DIR, rel + ".o")
@@ -107,7 +131,18 @@ def _compile_one(src: str, flags: list[str], hdr_digest: str, force: bool) -> tu
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
+    """Compile + link under an exclusive file lock (several ranks may call native() at once)."""
+    import fcntl
+
     os.makedirs(BUILD_DIR, exist_ok=True)
+    with open(os.path.join(BUILD_DIR, ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not force and os.path.exists(ext_path()) and not is_stale():
+            return ext_path()  # another process finished the build while we waited
+        return _build_locked(force, verbose)
+
+
+def _build_locked(force: bool, verbose: bool) -> str:
     flags = _common_flags()
     hdr = _headers_digest()
     srcs = _sources()
@@ -143,6 +178,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
         os.replace(out + ".tmp", out)
         if verbose:
             print(f"[mxddp build] linked {os.path.relpath(out, os.path.dirname(PKG_DIR))}", flush=True)
+    with open(stamp_path(), "w") as f:
+        f.write(source_digest())
     return out
 
 
