@@ -148,7 +148,8 @@ def main():
             "data": _data_desc(spec),
             "config": {"model": a.model, "global_batch": B * a.gpus, "per_rank_batch": B, "seq_len": None,
                        "image": "x".join(map(str, spec.input_shape)), "parallelism": f"dp{a.gpus}", "impl": a.impl,
-                       "graph": (a.impl == "fused" and not a.no_graph) or getattr(a, "layers_graph", False),
+                       # how the timed steps were actually launched (autotune may pick eager mode 0)
+                       "graph": (a.impl == "fused" and tr.eng.graph_mode != 0) or getattr(a, "layers_graph", False),
                        **({"graph_mode": tr.eng.graph_mode, "overlap": tr.eng.overlap,
                            "force_collectives": a.force_collectives, "autotune": tr.tuned}
                           if a.impl == "fused" else {})},

@@ -124,18 +124,26 @@ class FusedMnistTrainer:
         for mode, ov in cands:
             self.eng.uncapture()
             self.eng.set_overlap(ov)
-            try:
+            failed = 0.0
+            try:  # capture issues no collective, so a local failure here is safe to agree on
                 if mode:
                     self._capture(mode)
-                self.eng.replay(2)
-                self.eng.sync()
-                pc.barrier()
-                t0 = time.perf_counter()
-                self.eng.replay(trial_steps)
-                self.eng.sync()
-                dt = pc.all_reduce_max(time.perf_counter() - t0)
             except RuntimeError:
-                dt = pc.all_reduce_max(float("inf"))
+                failed = 1.0
+            # every rank reaches this all-reduce before any RCCL work of the candidate, so a
+            # candidate that failed to capture on ANY rank is skipped by ALL ranks together
+            if pc.all_reduce_max(failed) > 0:
+                self.eng.uncapture()
+                results[(mode, ov)] = float("inf")
+                continue
+            # replay errors are not swallowed: peers may already be inside the collectives
+            self.eng.replay(2)
+            self.eng.sync()
+            pc.barrier()
+            t0 = time.perf_counter()
+            self.eng.replay(trial_steps)
+            self.eng.sync()
+            dt = pc.all_reduce_max(time.perf_counter() - t0)
             self.steps += 2 + trial_steps
             results[(mode, ov)] = dt / trial_steps * 1e3
         best = min(results, key=results.get)
