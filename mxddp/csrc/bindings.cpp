@@ -9,6 +9,7 @@
 #include "common.h"
 #include "mnist_engine.h"
 #include "ops.h"
+#include "peer.h"
 #include "reducer.h"
 
 namespace py = pybind11;
@@ -284,6 +285,34 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("world_size", &Comm::world_size)
       .def_property_readonly("device", &Comm::device);
 
+  py::class_<PeerComm>(m, "PeerComm")
+      .def(py::init<int, int, int, size_t, int>(), py::arg("rank"), py::arg("world_size"), py::arg("device"),
+           py::arg("cap_bytes") = size_t(64) << 20, py::arg("blocks") = 64)
+      .def("handles", [](const PeerComm& p) { return py::bytes(p.handles()); })
+      .def("open", [](PeerComm& p, const std::vector<py::bytes>& all) {
+        std::vector<std::string> v;
+        for (auto& b : all) v.push_back(std::string(b));
+        p.open(v);
+      })
+      .def("all_reduce", [](PeerComm& p, uintptr_t data, size_t n, DType t, uintptr_t st) {
+        p.all_reduce(P<void>(data), n, t, S(st));
+      })
+      .def("error", &PeerComm::error)
+      .def("reset_error", &PeerComm::reset_error)
+      .def("set_blocks", &PeerComm::set_blocks)
+      .def("set_fence", &PeerComm::set_fence)
+      .def("set_timeout_ms", &PeerComm::set_timeout_ms)
+      .def_property_readonly("blocks", &PeerComm::blocks)
+      .def_property_readonly("fence", &PeerComm::fence)
+      .def_property_readonly("rank", &PeerComm::rank)
+      .def_property_readonly("world_size", &PeerComm::world_size)
+      .def_property_readonly("mem_kind", &PeerComm::mem_kind)
+      .def_property_readonly("cap_bytes", &PeerComm::cap_bytes)
+      .def_static("partition", [](long long count, int ws, int blocks, int vec) {
+        auto q = PeerPartition::make(count, ws, blocks, vec);
+        return std::make_pair(q.chunk, q.slice);
+      });
+
   py::class_<Reducer>(m, "Reducer")
       .def(py::init([](Comm* comm, uintptr_t flat, DType t, const std::vector<std::pair<size_t, size_t>>& buckets,
                        const std::vector<int>& param_bucket, RedOp op, bool timing) {
@@ -303,6 +332,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("num_buckets", &Reducer::num_buckets)
       .def_property_readonly("launched", &Reducer::launched)
       .def("set_overlap", &Reducer::set_overlap)
+      .def("set_peer", &Reducer::set_peer, py::arg("peer").none(true), py::keep_alive<1, 2>())
       .def("set_force_collectives", &Reducer::set_force_collectives)
       .def_property_readonly("active", &Reducer::active);
 
@@ -323,6 +353,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_force_collectives", &MnistEngine::set_force_collectives)
       .def_property_readonly("graph_mode", &MnistEngine::graph_mode)
       .def("set_overlap", &MnistEngine::set_overlap)
+      .def("set_peer", &MnistEngine::set_peer, py::arg("peer").none(true), py::keep_alive<1, 2>())
+      .def_property_readonly("peer_active", &MnistEngine::peer_active)
       .def_property_readonly("overlap", &MnistEngine::overlap)
       .def_property_readonly("reducer_active", &MnistEngine::reducer_active)
       .def("uncapture", &MnistEngine::uncapture)

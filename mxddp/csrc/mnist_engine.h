@@ -55,6 +55,13 @@ class MnistEngine {
     reducer_->set_force_collectives(on);
   }
   void set_overlap(bool on) { reducer_->set_overlap(on); }  // see Reducer::set_overlap
+  // gradient transport: nullptr = RCCL, else the direct xGMI peer all-reduce (peer.h); drops
+  // captured graphs (they bake in the collective kernels)
+  void set_peer(PeerComm* p) {
+    if (p != reducer_->peer()) uncapture();
+    reducer_->set_peer(p);
+  }
+  bool peer_active() const { return reducer_->peer() != nullptr; }
   bool overlap() const { return reducer_->overlap(); }
   bool reducer_active() const { return reducer_->active(); }
   void uncapture();  // drop captured graphs (back to eager; capture() may be called again)

@@ -1,0 +1,270 @@
+// Two-shot peer all-reduce kernel (design: peer.h).
+//
+// One workgroup = 256 threads = 4 waves; block b owns slice b of every rank's chunk, so the
+// only synchronisation is between block b of this rank and block b of each peer:
+//
+//   flag set 0 (scatter done)  sig[0][b][p] on rank q == "rank p stored its chunk q slice b
+//                               into q's scatter slot p"
+//   flag set 1 (reduce done)   sig[1][b][p] on rank q == "rank p stored reduced chunk p
+//                               slice b into q's gather slot p"
+//
+// Flags carry a per-block call counter (epoch), so they never need resetting and graph
+// replays work with fixed kernel arguments.  Slot reuse across calls is safe: rank p can
+// only start call k+1's scatter into q after q's block b set its call-k flag 1, which q does
+// after it finished reading its scatter slots of call k (program order + vmcnt(0)).
+#include "common.h"
+#include "peer.h"
+
+namespace mx {
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// 16-byte register vector (a native vector type: HIP's uint4 is a union-based struct that
+// keeps arrays of it out of registers)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// elements of T per 16-byte vector
+template <class T>
+struct Vec {
+  static constexpr int N = 16 / sizeof(T);
+};
+
+__device__ __forceinline__ float bf16_to_f(uint32_t h) { return __uint_as_float(h << 16); }
+__device__ __forceinline__ uint32_t f_to_bf16(float f) {  // round to nearest even
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (u >> 16) | ((u & 0xffffu) ? 0x40u : 0u);  // inf / nan
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+// accumulate a 16-byte vector into 8 (bf16) or 4 (f32) float lanes
+template <class T>
+__device__ __forceinline__ void acc16(float* a, u32x4 v, bool first) {
+  const uint32_t w[4] = {v[0], v[1], v[2], v[3]};
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = first ? __uint_as_float(w[i]) : a[i] + __uint_as_float(w[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float lo = bf16_to_f(w[i] & 0xffffu), hi = bf16_to_f(w[i] >> 16);
+      a[2 * i] = first ? lo : a[2 * i] + lo;
+      a[2 * i + 1] = first ? hi : a[2 * i + 1] + hi;
+    }
+  }
+}
+
+template <class T>
+__device__ __forceinline__ u32x4 pack16(const float* a) {
+  u32x4 v;
+  if constexpr (sizeof(T) == 4) {
+    v = u32x4{__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]), __float_as_uint(a[3])};
+  } else {
+    v = u32x4{f_to_bf16(a[0]) | (f_to_bf16(a[1]) << 16), f_to_bf16(a[2]) | (f_to_bf16(a[3]) << 16),
+              f_to_bf16(a[4]) | (f_to_bf16(a[5]) << 16), f_to_bf16(a[6]) | (f_to_bf16(a[7]) << 16)};
+  }
+  return v;
+}
+
+template <class T>
+__device__ __forceinline__ float ld_elem(const T* p, bool nt) {
+  if constexpr (sizeof(T) == 4) {
+    const uint32_t u = nt ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p))
+                          : *reinterpret_cast<const uint32_t*>(p);
+    return __uint_as_float(u);
+  } else {
+    const uint16_t u = nt ? __builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(p))
+                          : *reinterpret_cast<const uint16_t*>(p);
+    return bf16_to_f(u);
+  }
+}
+template <class T>
+__device__ __forceinline__ void st_elem(T* p, float f) {
+  if constexpr (sizeof(T) == 4) *reinterpret_cast<float*>(p) = f;
+  else *reinterpret_cast<uint16_t*>(p) = static_cast<uint16_t>(f_to_bf16(f));
+}
+
+__device__ __forceinline__ uint32_t* flag_at(uint32_t* sig, int set, int b, int p) {
+  return sig + ((size_t)set * kPeerMaxBlocks + b) * kPeerMaxRanks + p;
+}
+
+// lanes 0..ws-1 (except `rank`) of wave 0 each wait for one peer's flag; bounded.
+__device__ __forceinline__ void wait_peers(const PeerArgs& a, int set, int b, uint32_t ep) {
+  const int t = threadIdx.x;
+  if (t < a.ws && t != a.rank) {
+    uint32_t* f = flag_at(a.sig[a.rank], set, b, t);
+    const long long t0 = wall_clock64();
+    while (static_cast<int32_t>(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - ep) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > a.timeout) {
+        __hip_atomic_store(a.err, 1 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+  if ((a.fence & 2) && t < kWave) {  // acquire (only needed when the exchange memory is cached)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    vm_drain();
+  }
+  __syncthreads();
+}
+
+// every wave's stores drained, then one lane per peer publishes `ep` in that peer's flag
+__device__ __forceinline__ void signal_peers(const PeerArgs& a, int set, int b, uint32_t ep) {
+  vm_drain();
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < kWave) {
+    if (a.fence & 1) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      vm_drain();
+    }
+    if (t < a.ws && t != a.rank)
+      __hip_atomic_store(flag_at(a.sig[t], set, b, a.rank), ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+template <class T, int W>
+__global__ __launch_bounds__(kThreads) void peer_all_reduce_kernel(PeerArgs a, PeerPartition part) {
+  constexpr int V = Vec<T>::N;
+  const int b = blockIdx.x, r = a.rank, t = threadIdx.x;
+  __shared__ uint32_t s_ep;
+  if (t == 0) s_ep = a.epoch[b] + 1;
+  __syncthreads();
+  const uint32_t ep = s_ep;
+  T* data = static_cast<T*>(a.data);
+  const long long c = part.chunk, lo = (long long)b * part.slice;
+  const long long slot = a.slot_bytes / (long long)sizeof(T);  // elements per slot
+  const long long hi = lo + part.slice < c ? lo + part.slice : c;
+  // per peer j = 1..W-1 (rank p = (r + j) % W, rotated so the W-1 links start on different
+  // peers): elements of chunk p this block owns, and the pointers it touches (SGPRs)
+  long long n[W];
+  const T* src[W];   // phase 1: my chunk p         | phase 3: my gather slot p
+  T* dst[W];         // phase 1: rank p's scatter slot r | phase 2: rank p's gather slot r
+  const T* gat[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    const int p = (r + j) % W;
+    const long long np = a.count - (long long)p * c;
+    const long long e = (np < hi ? np : hi) - lo;
+    n[j] = e > 0 ? e : 0;
+    src[j] = data + (long long)p * c + lo;
+    dst[j] = reinterpret_cast<T*>(a.xbuf[p]) + (long long)r * slot + lo;
+    gat[j] = reinterpret_cast<const T*>(a.xbuf[r]) + (long long)(W + p) * slot + lo;
+  }
+  // vectors every peer's chunk has (all but the last chunk are full): unconditional, unrolled
+  long long nvmin = n[1] / V;
+#pragma unroll
+  for (int j = 2; j < W; ++j) nvmin = n[j] / V < nvmin ? n[j] / V : nvmin;
+
+  // 1. scatter: chunk p slice b -> rank p's scatter slot r, all W-1 links at once (every
+  //    thread has one 16-byte load per peer in flight before it stores)
+  for (long long i = t; i < nvmin; i += kThreads) {
+    u32x4 v[W - 1];
+#pragma unroll
+    for (int j = 1; j < W; ++j) v[j - 1] = reinterpret_cast<const u32x4*>(src[j])[i];
+#pragma unroll
+    for (int j = 1; j < W; ++j) reinterpret_cast<u32x4*>(dst[j])[i] = v[j - 1];
+  }
+#pragma unroll
+  for (int j = 1; j < W; ++j) {  // the short (last) chunk's remainder
+    for (long long i = nvmin + t; i < n[j] / V; i += kThreads)
+      reinterpret_cast<u32x4*>(dst[j])[i] = reinterpret_cast<const u32x4*>(src[j])[i];
+    for (long long i = n[j] / V * V + t; i < n[j]; i += kThreads) dst[j][i] = src[j][i];
+  }
+  signal_peers(a, 0, b, ep);
+  wait_peers(a, 0, b, ep);
+
+  // 2. reduce chunk r slice b over all ranks in rank order 0..W-1 (identical on every rank),
+  //    write it back and push it into every peer's gather slot r
+  {
+    const long long nr = n[0];
+    T* mine = data + (long long)r * c + lo;
+    const T* scat = reinterpret_cast<const T*>(a.xbuf[r]) + lo;
+    for (long long i = t; i < nr / V; i += kThreads) {
+      u32x4 v[W];
+#pragma unroll
+      for (int p = 0; p < W; ++p)
+        v[p] = p == r ? reinterpret_cast<const u32x4*>(mine)[i]
+                      : reinterpret_cast<const u32x4*>(scat + (long long)p * slot)[i];
+      float acc[V];
+#pragma unroll
+      for (int p = 0; p < W; ++p) acc16<T>(acc, v[p], p == 0);
+      const u32x4 out = pack16<T>(acc);
+      reinterpret_cast<u32x4*>(mine)[i] = out;
+#pragma unroll
+      for (int j = 1; j < W; ++j)
+        reinterpret_cast<u32x4*>(dst[j] + (long long)W * slot)[i] = out;  // gather slot r of rank p
+    }
+    for (long long i = nr / V * V + t; i < nr; i += kThreads) {
+      float acc = 0.f;
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        const float v = p == r ? ld_elem<T>(mine + i, false) : ld_elem<T>(scat + (long long)p * slot + i, true);
+        acc = p == 0 ? v : acc + v;
+      }
+      st_elem<T>(mine + i, acc);
+      const T rounded = mine[i];
+#pragma unroll
+      for (int j = 1; j < W; ++j) (dst[j] + (long long)W * slot)[i] = rounded;
+    }
+  }
+  signal_peers(a, 1, b, ep);
+  wait_peers(a, 1, b, ep);
+
+  // 3. gather: reduced chunk p slice b from gather slot p
+  for (long long i = t; i < nvmin; i += kThreads) {
+    u32x4 v[W - 1];
+#pragma unroll
+    for (int j = 1; j < W; ++j) v[j - 1] = reinterpret_cast<const u32x4*>(gat[j])[i];
+#pragma unroll
+    for (int j = 1; j < W; ++j) reinterpret_cast<u32x4*>(const_cast<T*>(src[j]))[i] = v[j - 1];
+  }
+#pragma unroll
+  for (int j = 1; j < W; ++j) {
+    T* out = const_cast<T*>(src[j]);
+    for (long long i = nvmin + t; i < n[j] / V; i += kThreads)
+      reinterpret_cast<u32x4*>(out)[i] = reinterpret_cast<const u32x4*>(gat[j])[i];
+    for (long long i = n[j] / V * V + t; i < n[j]; i += kThreads) out[i] = gat[j][i];
+  }
+  if (t == 0) a.epoch[b] = ep;
+}
+
+}  // namespace
+
+PeerPartition PeerPartition::make(long long count, int ws, int blocks, int vec) {
+  PeerPartition p;
+  p.chunk = ((count + ws - 1) / ws + vec - 1) / vec * vec;
+  p.slice = ((p.chunk + blocks - 1) / blocks + vec - 1) / vec * vec;
+  return p;
+}
+
+void peer_all_reduce_launch(const PeerArgs& a, DType t, int blocks, hipStream_t st) {
+  const int esz = static_cast<int>(dtype_size(t));
+  const PeerPartition part = PeerPartition::make(a.count, a.ws, blocks, 16 / esz);
+  MX_CHECK(part.chunk * esz <= a.slot_bytes, "peer all-reduce: bucket larger than the exchange slot");
+  MX_CHECK(reinterpret_cast<uintptr_t>(a.data) % 16 == 0, "peer all-reduce: data must be 16-byte aligned");
+  MX_CHECK(t == DType::kF32 || t == DType::kBF16, "peer all-reduce: f32 or bf16 only");
+  const bool f = t == DType::kF32;
+#define MX_PEER_CASE(NW)                                                                                 \
+  case NW:                                                                                               \
+    if (f) MX_LAUNCH((peer_all_reduce_kernel<float, NW>), dim3(blocks), dim3(kThreads), 0, st, a, part); \
+    else MX_LAUNCH((peer_all_reduce_kernel<uint16_t, NW>), dim3(blocks), dim3(kThreads), 0, st, a, part); \
+    break;
+  switch (a.ws) {
+    MX_PEER_CASE(2)
+    MX_PEER_CASE(3)
+    MX_PEER_CASE(4)
+    MX_PEER_CASE(5)
+    MX_PEER_CASE(6)
+    MX_PEER_CASE(7)
+    MX_PEER_CASE(8)
+    default: throw std::runtime_error("peer all-reduce: 2..8 ranks");
+  }
+#undef MX_PEER_CASE
+}
+
+}  // namespace mx

@@ -56,7 +56,10 @@ void Reducer::launch_ready(hipStream_t compute) {
       }
       if (timing_ && bi == 0) MX_HIP_CHECK(hipEventRecord(t0_, st));
       char* p = flat_ + b.offset * dtype_size(dtype_);
-      comm_->all_reduce(p, p, b.numel, dtype_, op_, st);
+      if (peer_ && op_ == RedOp::kSum && peer_->world_size() > 1)
+        peer_->all_reduce(p, b.numel, dtype_, st);
+      else
+        comm_->all_reduce(p, p, b.numel, dtype_, op_, st);
     }
   }
 }

@@ -19,6 +19,7 @@
 
 #include "bucket_schedule.h"
 #include "comm.h"
+#include "peer.h"
 
 namespace mx {
 
@@ -54,10 +55,15 @@ class Reducer {
   bool overlap() const { return overlap_; }
   // true when collectives are actually issued (world size > 1, or forced for testing)
   bool active() const;
+  // transport for sum all-reduces: RCCL (nullptr, default) or the direct xGMI peer transport
+  // (peer.h).  Every rank must make the same choice.
+  void set_peer(PeerComm* p) { peer_ = p; }
+  PeerComm* peer() const { return peer_; }
 
  private:
   void launch_ready(hipStream_t compute);
   Comm* comm_;
+  PeerComm* peer_ = nullptr;
   char* flat_;
   DType dtype_;
   RedOp op_;

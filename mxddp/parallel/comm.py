@@ -139,6 +139,9 @@ def all_reduce_sum(values):
 
 def shutdown():
     global _INFO, _COMM
+    from . import peer as _peer
+
+    _peer.shutdown()
     _COMM = None
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -1,0 +1,103 @@
+"""Bootstrap + validation of the direct xGMI peer all-reduce (``mxddp._C.PeerComm``, csrc/peer.h).
+
+The reference's DDP all-reduces gradient buckets with NCCL's ring
+(pytorch/distributed_data_parallel.py:74,132).  On one 8x MI355X node every GPU has a
+point-to-point xGMI link to each peer, so a two-shot all-reduce that uses all 7 links at once
+(the peer transport) can beat a ring on latency-bound bucket sizes.  This module
+
+* creates one PeerComm per rank and exchanges the HIP IPC handles of the exchange buffers
+  through the control-plane process group (gloo / TCPStore), single node only;
+* validates it against RCCL on random data before anything uses it (every rank must agree,
+  so a transport that is wrong on ANY rank is dropped by ALL ranks together);
+* is what ``FusedMnistTrainer.autotune`` and ``DistributedDataParallel`` pick from.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+from .. import native
+from . import comm as _comm
+
+_PEER = None
+
+
+def _agree_ok(ok: bool) -> bool:
+    """True only if every rank reports ok (one host all-reduce every rank reaches)."""
+    return _comm.all_reduce_max(0.0 if ok else 1.0) == 0.0
+
+
+def peer_comm(cap_bytes: int = 64 << 20, blocks: int | None = None):
+    """This rank's PeerComm (created on first use), or None when the job is not a single-node
+    GPU job of 2..8 ranks or the IPC mapping failed on any rank."""
+    global _PEER
+    if _PEER is not None:
+        return _PEER
+    inf = _comm.info()
+    if inf.world_size < 2 or inf.world_size > 8 or inf.device.type != "cuda" or not dist.is_initialized():
+        return None
+    if inf.local_world_size != inf.world_size:
+        return None  # xGMI peers are on the same node only
+    if os.environ.get("MXDDP_PEER", "1") == "0":
+        return None
+    C = native()
+    if blocks is None:
+        blocks = int(os.environ.get("MXDDP_PEER_BLOCKS", "64"))
+    pc, err = None, ""
+    try:
+        pc = C.PeerComm(inf.rank, inf.world_size, inf.device.index, cap_bytes, blocks)
+        mine = pc.handles()
+    except RuntimeError as e:  # allocation / IPC export failed here
+        mine, err = b"", str(e)
+    allh = [None] * inf.world_size
+    dist.all_gather_object(allh, mine)
+    ok = all(h for h in allh)
+    if ok:
+        try:
+            pc.open(allh)
+        except RuntimeError as e:
+            ok, err = False, str(e)
+    if not _agree_ok(ok):
+        if inf.is_main:
+            print(f"[mxddp] peer transport unavailable ({err or 'on another rank'}); using RCCL", flush=True)
+        return None
+    _comm.barrier()
+    _PEER = pc
+    return pc
+
+
+def validate(pc, rccl, dtype: str = "f32", numel: int = 1_181_066, iters: int = 3) -> bool:
+    """Run the peer all-reduce and RCCL's on the same random per-rank data and compare.
+    Collective over all ranks; returns the agreed verdict."""
+    inf = _comm.info()
+    C = native()
+    dev = inf.device
+    tdt = torch.float32 if dtype == "f32" else torch.bfloat16
+    cdt = C.DType.f32 if dtype == "f32" else C.DType.bf16
+    ok = True
+    st = torch.cuda.current_stream(dev).cuda_stream
+    g = torch.Generator(device="cpu").manual_seed(1234 + inf.rank)
+    for _ in range(iters):
+        x = torch.randn(numel, generator=g).to(dev, tdt)
+        a, b = x.clone(), x.clone()
+        pc.reset_error()
+        pc.all_reduce(a.data_ptr(), numel, cdt, st)
+        rccl.all_reduce(b.data_ptr(), b.data_ptr(), numel, cdt, C.RedOp.sum, st)
+        torch.cuda.synchronize(dev)
+        if pc.error():
+            ok = False
+            break
+        tol = 1e-5 * inf.world_size if dtype == "f32" else 2e-2
+        err = (a.float() - b.float()).abs().max().item()
+        scale = b.float().abs().max().item() + 1e-6
+        if not (err <= tol * scale):
+            ok = False
+            break
+    return _agree_ok(ok)
+
+
+def shutdown():
+    global _PEER
+    _PEER = None

@@ -1,0 +1,150 @@
+"""Peer (direct xGMI) all-reduce, csrc/peer.h: W processes on ONE MI355X, each an independent
+rank with its own HIP context, exchanging IPC handles of the uncached exchange buffers --
+the same code path as W GPUs of one node, minus the links.  Checks, against a plain PyTorch
+fp32 sum in the kernel's fixed rank order:
+
+* bit-exact results (f32 and bf16) for counts that exercise every tail case and bucket
+  splitting (exchange capacity smaller than the bucket), under UNEVEN load (ranks delayed
+  by random host sleeps and by a large GEMM queued in front of the all-reduce);
+* hipGraph capture + replay (fixed kernel arguments, per-block epochs in device memory);
+* a peer that never arrives: the kernel gives up after the timeout and reports which peer,
+  instead of spinning forever.
+"""
+import os
+import random
+import socket
+import traceback
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+COUNTS = [1, 3, 8, 17, 1000, 4097, 65_543, 300_001, 1_181_066]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _data(rank, count, rep, dtype):
+    g = torch.Generator().manual_seed(rank * 1_000_003 + count * 7 + rep)
+    return torch.randn(count, generator=g).to(dtype)
+
+
+def _expected(ws, count, rep, dtype):
+    acc = _data(0, count, rep, dtype).float()
+    for p in range(1, ws):
+        acc = acc + _data(p, count, rep, dtype).float()
+    return acc.to(dtype)
+
+
+def _worker(rank, ws, port, mode, q):
+    try:
+        import torch.distributed as dist
+
+        from mxddp import native
+
+        C = native()
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=ws)
+        cap = 256 << 10 if mode == "numerics" else 8 << 20  # small exchange: forces bucket splitting
+        pc = C.PeerComm(rank, ws, 0, cap, 16)
+        allh = [None] * ws
+        dist.all_gather_object(allh, pc.handles())
+        pc.open(allh)
+        dist.barrier()
+        st = torch.cuda.current_stream().cuda_stream
+        bad = []
+        if mode == "numerics":
+            rnd = random.Random(rank)
+            big = torch.randn(4096, 4096, device="cuda")
+            for dt, cdt in ((torch.float32, C.DType.f32), (torch.bfloat16, C.DType.bf16)):
+                for count in COUNTS:
+                    for rep in range(2):
+                        x = _data(rank, count, rep, dt).cuda()
+                        dist.barrier()
+                        if rnd.random() < 0.5:
+                            torch.cuda._sleep(int(rnd.random() * 2_000_000))  # GPU-side delay
+                        if rank == ws - 1:
+                            big = big @ big * 1e-3  # queued work ahead of the all-reduce
+                        pc.all_reduce(x.data_ptr(), count, cdt, st)
+                        torch.cuda.synchronize()
+                        want = _expected(ws, count, rep, dt)
+                        if pc.error() or not torch.equal(x.cpu(), want):
+                            nbad = int((x.cpu() != want).sum())
+                            bad.append((str(dt), count, rep, pc.error(), nbad))
+        elif mode == "graph":
+            count = 1_181_066
+            src = torch.empty(count, device="cuda")
+            buf = torch.empty(count, device="cuda")
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                buf.copy_(src)
+                pc.all_reduce(buf.data_ptr(), count, C.DType.f32, torch.cuda.current_stream().cuda_stream)
+            for rep in range(6):
+                src.copy_(_data(rank, count, rep, torch.float32).cuda())
+                torch.cuda.synchronize()
+                dist.barrier()
+                g.replay()
+                torch.cuda.synchronize()
+                if pc.error() or not torch.equal(buf.cpu(), _expected(ws, count, rep, torch.float32)):
+                    bad.append(("graph", rep, pc.error()))
+        elif mode == "timeout":
+            pc.set_timeout_ms(300)
+            x = torch.ones(10_000, device="cuda")
+            if rank == 0:
+                pc.all_reduce(x.data_ptr(), x.numel(), C.DType.f32, st)  # rank 1 never joins
+                torch.cuda.synchronize()
+                if pc.error() != 2:
+                    bad.append(("timeout error word", pc.error()))
+            dist.barrier()
+        dist.barrier()
+        q.put((rank, bad, pc.mem_kind))
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, ["exception: " + traceback.format_exc()], ""))
+
+
+def _run(ws, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    env_keep = dict(os.environ)
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, mode, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(ws):
+            rank, bad, kind = q.get(timeout=240)
+            out[rank] = (bad, kind)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+        os.environ.clear()
+        os.environ.update(env_keep)
+    for r in range(ws):
+        assert r in out, f"rank {r} did not report"
+        assert out[r][0] == [], f"rank {r}: {out[r][0]}"
+    return out[0][1]
+
+
+@pytest.mark.parametrize("ws", [2, 8])
+def test_peer_all_reduce_exact(cuda, ws):
+    kind = _run(ws, "numerics")
+    print("exchange memory:", kind)
+
+
+def test_peer_all_reduce_graph_replay(cuda):
+    _run(4, "graph")
+
+
+def test_peer_all_reduce_timeout_reports_missing_peer(cuda):
+    _run(2, "timeout")
