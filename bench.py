@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--steps-per-graph", type=int, default=None, help="fused engine, graph mode 1: steps unrolled per graph")
     ap.add_argument("--force-collectives", action="store_true",
                     help="fused engine: issue the RCCL bucket all-reduces even at world size 1 (measures the DDP path)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "peer"],
+                    help="fused engine, world size > 1: gradient all-reduce over RCCL's ring, the direct xGMI "
+                         "peer all-reduce, or auto (validated + timed during the untimed warm-up)")
     ap.add_argument("--channels-last", action="store_true",
                     help="--impl torch: channels_last memory format (stock PyTorch's NHWC convs, for a fair bf16 baseline)")
     ap.add_argument("--seed", type=int, default=1)
@@ -102,7 +105,7 @@ def main():
 
         tr = FusedMnistTrainer(batch=B, device=dev, comm=comm, seed=a.seed, variant=a.variant, lr=a.lr,
                                use_graph=not a.no_graph, graph_mode=a.graph_mode, steps_per_graph=a.steps_per_graph,
-                               force_collectives=a.force_collectives)
+                               force_collectives=a.force_collectives, transport=a.transport)
         run = tr.step
         if a.graph_mode is None and not a.no_autotune and tr.eng.reducer_active:
             tr.step(1)
@@ -151,7 +154,7 @@ def main():
                        # how the timed steps were actually launched (autotune may pick eager mode 0)
                        "graph": (a.impl == "fused" and tr.eng.graph_mode != 0) or getattr(a, "layers_graph", False),
                        **({"graph_mode": tr.eng.graph_mode, "overlap": tr.eng.overlap,
-                           "force_collectives": a.force_collectives, "autotune": tr.tuned}
+                           "transport": tr.active_transport, "force_collectives": a.force_collectives, "autotune": tr.tuned}
                           if a.impl == "fused" else {})},
             **extra,
         }

@@ -124,7 +124,8 @@ void MnistEngine::fwd(const float* x, float* logits_out, int B) {
 }
 
 MnistFused MnistEngine::fused_args() const {
-  const uint64_t data_seed = seed_ + (comm_ ? comm_->rank() : 0) * 7919ull;  // per-rank data shard
+  const int rank = comm_ ? comm_->rank() : (reducer_ && reducer_->peer() ? reducer_->peer()->rank() : 0);
+  const uint64_t data_seed = seed_ + rank * 7919ull;  // per-rank data shard
   MnistFused f{};
   f.B = B_;
   f.x = x_;
@@ -183,7 +184,7 @@ void MnistEngine::segment(int k) {
       mnist_fused_conv_bwd(fused_args(), s_, !reducer_->active());
     }
   } else {  // optimizer: flat SGD, DDP's 1/world_size average folded into the update
-    const int ws = comm_ ? comm_->world_size() : 1;
+    const int ws = world_size();
     if (variant_ == 0)
       sgd_step(p_, g_, m_, lr_, 1.f / ws, momentum_, wd_, (int64_t)L::total, false, s_);
     else  // + conv2 weight repack for the next step's F2/F7 + conv2 bias-grad reset
@@ -222,7 +223,7 @@ hipGraphExec_t MnistEngine::capture_fn(const std::function<void()>& fn, hipGraph
 
 void MnistEngine::capture(int mode, int steps_per_graph) {
   if (exec_ || seg_exec_[0]) return;
-  const bool multi = comm_ && comm_->world_size() > 1;
+  const bool multi = world_size() > 1;
   // default: one graph at world size 1; eager launches (mode 0) when real collectives run --
   // the caller (FusedMnistTrainer.autotune) may pick a graph mode after timing the options.
   if (mode < 0) mode = multi ? 0 : 1;

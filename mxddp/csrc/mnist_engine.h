@@ -62,6 +62,11 @@ class MnistEngine {
     reducer_->set_peer(p);
   }
   bool peer_active() const { return reducer_->peer() != nullptr; }
+  // data-parallel degree: the RCCL communicator's, else the peer transport's (a peer-only job,
+  // e.g. several ranks sharing one GPU in tests)
+  int world_size() const {
+    return comm_ ? comm_->world_size() : (reducer_->peer() ? reducer_->peer()->world_size() : 1);
+  }
   bool overlap() const { return reducer_->overlap(); }
   bool reducer_active() const { return reducer_->active(); }
   void uncapture();  // drop captured graphs (back to eager; capture() may be called again)

@@ -40,7 +40,9 @@ void Reducer::mark_bucket_ready(int bi, hipStream_t compute) {
   launch_ready(compute);
 }
 
-bool Reducer::active() const { return comm_ && (comm_->world_size() > 1 || force_); }
+bool Reducer::active() const {
+  return (comm_ && (comm_->world_size() > 1 || force_)) || (peer_ && peer_->world_size() > 1);
+}
 
 void Reducer::launch_ready(hipStream_t compute) {
   const bool act = active();
@@ -56,10 +58,12 @@ void Reducer::launch_ready(hipStream_t compute) {
       }
       if (timing_ && bi == 0) MX_HIP_CHECK(hipEventRecord(t0_, st));
       char* p = flat_ + b.offset * dtype_size(dtype_);
-      if (peer_ && op_ == RedOp::kSum && peer_->world_size() > 1)
+      if (peer_ && op_ == RedOp::kSum && peer_->world_size() > 1) {
         peer_->all_reduce(p, b.numel, dtype_, st);
-      else
+      } else {
+        MX_CHECK(comm_ != nullptr, "reducer: no RCCL communicator for this collective");
         comm_->all_reduce(p, p, b.numel, dtype_, op_, st);
+      }
     }
   }
 }

@@ -32,7 +32,8 @@ class FusedMnistTrainer:
     def __init__(self, batch: int = 64, device: torch.device | int = 0, comm=None, seed: int = 1, lr: float = 0.1,
                  momentum: float = 0.9, weight_decay: float = 1e-4, variant: int = 1, use_graph: bool = True,
                  init_model: MnistCNN | None = None, graph_mode: int | None = None,
-                 steps_per_graph: int | None = None, force_collectives: bool = False):
+                 steps_per_graph: int | None = None, force_collectives: bool = False, transport: str = "auto",
+                 peer=None):
         C = native()
         self.C = C
         self.graph_mode = graph_mode
@@ -71,7 +72,25 @@ class FusedMnistTrainer:
             self.eng.set_force_collectives(True)
         self.stream = torch.cuda.ExternalStream(self.eng.stream, device=self.device)
         self.steps = 0
-        self.world_size = comm.world_size if comm is not None else 1
+        self.world_size = comm.world_size if comm is not None else (peer.world_size if peer is not None else 1)
+        # gradient transport (world size > 1): RCCL, or the direct xGMI peer all-reduce
+        # (parallel/peer.py) -- validated against RCCL on every rank before it may be used;
+        # "auto" lets autotune() time both
+        self.transport = transport
+        self.peer = None
+        if peer is not None:  # caller-provided peer transport (peer-only job: no RCCL communicator)
+            self.peer, self.transport = peer, "peer"
+            self.eng.set_peer(peer)
+        elif self.world_size > 1 and transport in ("auto", "peer"):
+            from .parallel import peer as _peer
+
+            pc = _peer.peer_comm()
+            if pc is not None and _peer.validate(pc, comm):
+                self.peer = pc
+            elif transport == "peer":
+                raise RuntimeError("peer transport requested but unavailable / failed validation")
+        if self.peer is not None and transport == "peer":
+            self.eng.set_peer(self.peer)
 
     # --------------------------------------------------------------- stepping
     def step(self, n: int = 1):
@@ -106,23 +125,31 @@ class FusedMnistTrainer:
 
     def autotune(self, trial_steps: int = 24, include_graphs: bool | None = None) -> dict:
         """Pick the fastest launch strategy for the DDP step on THIS machine by timing a few real
-        training steps of each (they count as warm-up).  Candidates: eager launches with the
-        fc-bucket all-reduce overlapped on the side stream vs. all collectives in order on the
-        compute stream (no cross-stream fences); optionally (MXDDP_AUTOTUNE_GRAPHS=1) the same
-        two captured as one hipGraph with RCCL inside.  The slowest rank's time decides, so every
-        rank picks the same strategy.  Returns {candidate: ms/step}."""
+        training steps of each (they count as warm-up).  Candidates: gradient transport (RCCL
+        ring, or the direct xGMI peer all-reduce when it validated) x (fc-bucket all-reduce
+        overlapped on the side stream, or in order on the compute stream) x (eager launches, or
+        the whole step captured in one hipGraph).  Peer-transport graphs are always tried (the
+        peer kernel is an ordinary kernel); RCCL-in-graph only with MXDDP_AUTOTUNE_GRAPHS=1.
+        The slowest rank's time decides, so every rank picks the same strategy.  Returns
+        {candidate: ms/step}."""
         from .parallel import comm as pc
 
         if include_graphs is None:
             include_graphs = os.environ.get("MXDDP_AUTOTUNE_GRAPHS", "0") == "1"
         if not self.eng.reducer_active or self._external:
             return {}
-        cands = [(0, True), (0, False)]
-        if include_graphs and self.use_graph:
-            cands += [(1, True), (1, False)]
+        transports = ["rccl", "peer"] if self.peer is not None else ["rccl"]
+        if self.transport in ("rccl", "peer"):
+            transports = [self.transport] if self.transport in transports else ["rccl"]
+        cands = []
+        for tr in transports:
+            cands += [(tr, 0, True), (tr, 0, False)]
+            if self.use_graph and (include_graphs or tr == "peer"):
+                cands += [(tr, 1, True), (tr, 1, False)]
         results = {}
-        for mode, ov in cands:
+        for tr, mode, ov in cands:
             self.eng.uncapture()
+            self.eng.set_peer(self.peer if tr == "peer" else None)
             self.eng.set_overlap(ov)
             failed = 0.0
             try:  # capture issues no collective, so a local failure here is safe to agree on
@@ -130,11 +157,11 @@ class FusedMnistTrainer:
                     self._capture(mode)
             except RuntimeError:
                 failed = 1.0
-            # every rank reaches this all-reduce before any RCCL work of the candidate, so a
+            # every rank reaches this all-reduce before any collective of the candidate, so a
             # candidate that failed to capture on ANY rank is skipped by ALL ranks together
             if pc.all_reduce_max(failed) > 0:
                 self.eng.uncapture()
-                results[(mode, ov)] = float("inf")
+                results[(tr, mode, ov)] = float("inf")
                 continue
             # replay errors are not swallowed: peers may already be inside the collectives
             self.eng.replay(2)
@@ -144,18 +171,31 @@ class FusedMnistTrainer:
             self.eng.replay(trial_steps)
             self.eng.sync()
             dt = pc.all_reduce_max(time.perf_counter() - t0)
+            self._check_peer()
             self.steps += 2 + trial_steps
-            results[(mode, ov)] = dt / trial_steps * 1e3
+            results[(tr, mode, ov)] = dt / trial_steps * 1e3
         best = min(results, key=results.get)
         self.eng.uncapture()
-        self.eng.set_overlap(best[1])
-        if best[0]:
-            self._capture(best[0])
+        self.eng.set_peer(self.peer if best[0] == "peer" else None)
+        self.eng.set_overlap(best[2])
+        if best[1]:
+            self._capture(best[1])
         self._capture_done = True
         self.read_metrics(reset=True)
-        self.tuned = {"graph_mode": best[0], "overlap": best[1], "trials_ms": {f"{m}/{'ovl' if o else 'inl'}": round(v, 4)
-                                                                              for (m, o), v in results.items()}}
+        self.tuned = {"transport": best[0], "graph_mode": best[1], "overlap": best[2],
+                      "trials_ms": {f"{t}/{m}/{'ovl' if o else 'inl'}": round(v, 4)
+                                    for (t, m, o), v in results.items()}}
         return results
+
+    def _check_peer(self):
+        if self.peer is not None and self.peer.error():
+            raise RuntimeError(f"peer all-reduce: rank {self.peer.error() - 1} never arrived (timeout)")
+
+    @property
+    def active_transport(self) -> str:
+        if self.world_size == 1 and not self.eng.reducer_active:
+            return "none"
+        return "peer" if self.eng.peer_active else "rccl"
 
     def set_batch(self, x: torch.Tensor, y: torch.Tensor):
         """Use a caller-provided batch instead of the on-device generator (real MNIST)."""
@@ -187,6 +227,7 @@ class FusedMnistTrainer:
         self.eng.sync()
         if self.comm is not None:
             self.comm.check_async_error()  # surface a failed/aborted peer at log boundaries
+        self._check_peer()
         m = self.metrics[:2].tolist()
         if reset:
             with torch.cuda.stream(self.stream):

@@ -7,6 +7,8 @@ fp32 sum in the kernel's fixed rank order:
   splitting (exchange capacity smaller than the bucket), under UNEVEN load (ranks delayed
   by random host sleeps and by a large GEMM queued in front of the all-reduce);
 * hipGraph capture + replay (fixed kernel arguments, per-block epochs in device memory);
+* the fused MNIST DDP training step over the peer transport (eager, and captured in a
+  hipGraph) equals one process training on the concatenated global batch;
 * a peer that never arrives: the kernel gives up after the timeout and reports which peer,
   instead of spinning forever.
 """
@@ -94,6 +96,40 @@ def _worker(rank, ws, port, mode, q):
                 torch.cuda.synchronize()
                 if pc.error() or not torch.equal(buf.cpu(), _expected(ws, count, rep, torch.float32)):
                     bad.append(("graph", rep, pc.error()))
+        elif mode in ("trainer", "trainer_graph"):
+            # fused MNIST DDP step over the peer transport == one process on the global batch
+            from mxddp.engine import FusedMnistTrainer
+            from mxddp.models import MnistCNN
+
+            b, steps = 16, 4
+            torch.manual_seed(0)
+            init = MnistCNN()
+            g = torch.Generator().manual_seed(5)
+            batches = [(torch.rand(ws * b, 1, 28, 28, generator=g), torch.randint(0, 10, (ws * b,), generator=g))
+                       for _ in range(steps)]
+            tr = FusedMnistTrainer(batch=b, device=0, comm=None, peer=pc, lr=0.05, init_model=init,
+                                   use_graph=mode == "trainer_graph", graph_mode=1)
+            for x, y in batches:
+                tr.set_batch(x[rank * b:(rank + 1) * b].cuda(), y[rank * b:(rank + 1) * b].cuda())
+                tr.step(1)
+            tr.synchronize()
+            if pc.error():
+                bad.append(("peer error", pc.error()))
+            mine = tr.params.cpu()
+            allp = [None] * ws
+            dist.all_gather_object(allp, mine)
+            if any(not torch.equal(allp[0], t) for t in allp):
+                bad.append("ranks diverged")
+            if rank == 0:
+                ref = FusedMnistTrainer(batch=ws * b, device=0, comm=None, lr=0.05, init_model=init, use_graph=False)
+                for x, y in batches:
+                    ref.set_batch(x.cuda(), y.cuda())
+                    ref.step(1)
+                ref.synchronize()
+                d = (ref.params.cpu() - mine).abs().max().item()
+                moved = (ref.params.cpu() - torch.cat([v.reshape(-1) for v in init.state_dict().values()])).abs().max()
+                if not d < 2e-5 or not moved > 1e-3:
+                    bad.append(("ddp != global batch", d, float(moved)))
         elif mode == "timeout":
             pc.set_timeout_ms(300)
             x = torch.ones(10_000, device="cuda")
@@ -144,6 +180,11 @@ def test_peer_all_reduce_exact(cuda, ws):
 
 def test_peer_all_reduce_graph_replay(cuda):
     _run(4, "graph")
+
+
+@pytest.mark.parametrize("mode", ["trainer", "trainer_graph"])
+def test_fused_trainer_peer_ddp_matches_global_batch(cuda, mode):
+    _run(2 if mode == "trainer" else 4, mode)
 
 
 def test_peer_all_reduce_timeout_reports_missing_peer(cuda):
