@@ -287,7 +287,7 @@ PYBIND11_MODULE(_C, m) {
 
   py::class_<PeerComm>(m, "PeerComm")
       .def(py::init<int, int, int, size_t, int>(), py::arg("rank"), py::arg("world_size"), py::arg("device"),
-           py::arg("cap_bytes") = size_t(64) << 20, py::arg("blocks") = 64)
+           py::arg("cap_bytes") = size_t(32) << 20, py::arg("blocks") = 64)
       .def("handles", [](const PeerComm& p) { return py::bytes(p.handles()); })
       .def("open", [](PeerComm& p, const std::vector<py::bytes>& all) {
         std::vector<std::string> v;

@@ -46,7 +46,7 @@ PeerComm::PeerComm(int rank, int world_size, int device, size_t cap_bytes, int b
   cap_ = (cap_bytes + 15) / 16 * 16;
   // one slot holds one rank's chunk (rounded to the 16-byte vector): ceil(cap / ws) + 16
   slot_bytes_ = ((cap_ + ws_ - 1) / ws_ + 16 + 255) / 256 * 256;
-  xbytes_ = 2ull * ws_ * slot_bytes_;  // scatter region + gather region
+  xbytes_ = 4ull * ws_ * slot_bytes_;  // (scatter + gather region) x 2 call parities
   sbytes_ = kSigBytes;
   std::string k1, k2;
   xbuf_ = alloc_shared(xbytes_, &k1);

@@ -45,7 +45,7 @@ struct PeerArgs {
   int* err;                       // host-mapped error word
   void* data;                     // bucket (in place)
   long long count;                // elements
-  long long slot_bytes;           // bytes of one slot (region = W slots)
+  long long slot_bytes;           // bytes of one slot (region = W slots; 2 regions x 2 parities)
   long long timeout;              // s_memrealtime ticks (100 MHz)
   int rank, ws;
   int fence;                      // bit 0: system release before flag stores; bit 1: acquire after waits

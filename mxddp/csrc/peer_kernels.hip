@@ -9,9 +9,12 @@
 //                               slice b into q's gather slot p"
 //
 // Flags carry a per-block call counter (epoch), so they never need resetting and graph
-// replays work with fixed kernel arguments.  Slot reuse across calls is safe: rank p can
-// only start call k+1's scatter into q after q's block b set its call-k flag 1, which q does
-// after it finished reading its scatter slots of call k (program order + vmcnt(0)).
+// replays work with fixed kernel arguments.  Exchange slots are double-buffered by call
+// parity: consecutive calls may have different bucket sizes, hence a different block ->
+// region mapping, so block b of rank p in call k+1 may write bytes that ANOTHER block of rank
+// q still reads in call k.  Call k+1 therefore uses the other half, which q last read in call
+// k-1 -- and that call has fully completed on q, since q's block b reached call k (stream
+// order) before it released p's block b into call k+1 (flag set 1 of call k).
 #include "common.h"
 #include "peer.h"
 
@@ -138,6 +141,7 @@ __global__ __launch_bounds__(kThreads) void peer_all_reduce_kernel(PeerArgs a, P
   T* data = static_cast<T*>(a.data);
   const long long c = part.chunk, lo = (long long)b * part.slice;
   const long long slot = a.slot_bytes / (long long)sizeof(T);  // elements per slot
+  const long long half = (long long)(ep & 1u) * 2 * W * slot;    // this call's buffer half
   const long long hi = lo + part.slice < c ? lo + part.slice : c;
   // per peer j = 1..W-1 (rank p = (r + j) % W, rotated so the W-1 links start on different
   // peers): elements of chunk p this block owns, and the pointers it touches (SGPRs)
@@ -152,8 +156,8 @@ __global__ __launch_bounds__(kThreads) void peer_all_reduce_kernel(PeerArgs a, P
     const long long e = (np < hi ? np : hi) - lo;
     n[j] = e > 0 ? e : 0;
     src[j] = data + (long long)p * c + lo;
-    dst[j] = reinterpret_cast<T*>(a.xbuf[p]) + (long long)r * slot + lo;
-    gat[j] = reinterpret_cast<const T*>(a.xbuf[r]) + (long long)(W + p) * slot + lo;
+    dst[j] = reinterpret_cast<T*>(a.xbuf[p]) + half + (long long)r * slot + lo;
+    gat[j] = reinterpret_cast<const T*>(a.xbuf[r]) + half + (long long)(W + p) * slot + lo;
   }
   // vectors every peer's chunk has (all but the last chunk are full): unconditional, unrolled
   long long nvmin = n[1] / V;
@@ -183,7 +187,7 @@ __global__ __launch_bounds__(kThreads) void peer_all_reduce_kernel(PeerArgs a, P
   {
     const long long nr = n[0];
     T* mine = data + (long long)r * c + lo;
-    const T* scat = reinterpret_cast<const T*>(a.xbuf[r]) + lo;
+    const T* scat = reinterpret_cast<const T*>(a.xbuf[r]) + half + lo;
     for (long long i = t; i < nr / V; i += kThreads) {
       u32x4 v[W];
 #pragma unroll

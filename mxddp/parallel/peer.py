@@ -29,7 +29,7 @@ def _agree_ok(ok: bool) -> bool:
     return _comm.all_reduce_max(0.0 if ok else 1.0) == 0.0
 
 
-def peer_comm(cap_bytes: int = 64 << 20, blocks: int | None = None):
+def peer_comm(cap_bytes: int = 32 << 20, blocks: int | None = None):
     """This rank's PeerComm (created on first use), or None when the job is not a single-node
     GPU job of 2..8 ranks or the IPC mapping failed on any rank."""
     global _PEER

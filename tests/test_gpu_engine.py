@@ -47,6 +47,33 @@ def test_fused_engine_matches_reference(cuda, variant, graph):
         assert err < 1e-4, (k, err)
 
 
+@pytest.mark.parametrize("B", [16, 48, 64, 128])
+def test_fused_engine_batch_sizes_match_reference(cuda, B):
+    """Every batch the fused engine accepts (16..128, multiples of 16) against the fp32 reference."""
+    from mxddp.engine import FusedMnistTrainer
+    from mxddp.models import MnistCNN
+
+    torch.manual_seed(0)
+    ref = MnistCNN()
+    steps = 3
+    tr = FusedMnistTrainer(batch=B, device=cuda, comm=None, init_model=ref, use_graph=False)
+    g = torch.Generator().manual_seed(B)
+    xs = [torch.rand(B, 1, 28, 28, generator=g) for _ in range(steps)]
+    ys = [torch.randint(0, 10, (B,), generator=g) for _ in range(steps)]
+    losses = []
+    for i in range(steps):
+        tr.set_batch(xs[i].to(cuda), ys[i].to(cuda))
+        tr.step(1)
+        losses.append(tr.read_metrics()[0] / B)
+    ref_losses = _ref_steps(ref, xs, ys, steps)
+    for a, b in zip(losses, ref_losses):
+        assert abs(a - b) < 1e-4 * max(1.0, abs(b)), (B, losses, ref_losses)
+    sd = tr.state_dict()
+    for k, v in ref.state_dict().items():
+        err = (sd[k] - v).abs().max().item() / (v.abs().max().item() + 1e-6)
+        assert err < 1e-4, (B, k, err)
+
+
 @pytest.mark.parametrize("graph", [0, 1, 2])
 def test_fused_engine_rccl_collectives_ws1(cuda, graph):
     """The DDP path with REAL RCCL all-reduces (1-rank communicator, collectives forced):

@@ -6,6 +6,8 @@ fp32 sum in the kernel's fixed rank order:
 * bit-exact results (f32 and bf16) for counts that exercise every tail case and bucket
   splitting (exchange capacity smaller than the bucket), under UNEVEN load (ranks delayed
   by random host sleeps and by a large GEMM queued in front of the all-reduce);
+* back-to-back calls of different sizes with no host sync (exchange slots double-buffered by
+  call parity, since the block -> region mapping changes with the size);
 * hipGraph capture + replay (fixed kernel arguments, per-block epochs in device memory);
 * the fused MNIST DDP training step over the peer transport (eager, and captured in a
   hipGraph) equals one process training on the concatenated global batch;
@@ -79,6 +81,21 @@ def _worker(rank, ws, port, mode, q):
                         if pc.error() or not torch.equal(x.cpu(), want):
                             nbad = int((x.cpu() != want).sum())
                             bad.append((str(dt), count, rep, pc.error(), nbad))
+        elif mode == "burst":
+            # back-to-back calls of DIFFERENT sizes with no host sync in between (the engine's fc
+            # bucket then conv bucket): one rank starts late, so the others run a call ahead
+            sizes = [1_181_066, 18_816, 1000, 300_001, 17, 1_181_066, 18_816, 65_543] * 3
+            for it in range(3):
+                xs = [_data(rank, n, it, torch.float32).cuda() for n in sizes]
+                dist.barrier()
+                if rank == it % ws:
+                    torch.cuda._sleep(3_000_000)
+                for x in xs:
+                    pc.all_reduce(x.data_ptr(), x.numel(), C.DType.f32, st)
+                torch.cuda.synchronize()
+                for n, x in zip(sizes, xs):
+                    if pc.error() or not torch.equal(x.cpu(), _expected(ws, n, it, torch.float32)):
+                        bad.append(("burst", it, n, pc.error()))
         elif mode == "graph":
             count = 1_181_066
             src = torch.empty(count, device="cuda")
@@ -176,6 +193,11 @@ def _run(ws, mode):
 def test_peer_all_reduce_exact(cuda, ws):
     kind = _run(ws, "numerics")
     print("exchange memory:", kind)
+
+
+@pytest.mark.parametrize("ws", [2, 8])
+def test_peer_all_reduce_back_to_back_sizes(cuda, ws):
+    _run(ws, "burst")
 
 
 def test_peer_all_reduce_graph_replay(cuda):
