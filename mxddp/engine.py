@@ -60,6 +60,8 @@ class FusedMnistTrainer:
         self.metrics = torch.zeros(4, device=self.device)
         wsb = C.mnist_workspace_bytes(batch)
         self.workspace = torch.empty(wsb // 4 + 64, dtype=torch.float32, device=self.device)
+        if os.environ.get("MXDDP_POISON_WORKSPACE"):  # debug: NaN-fill to catch reads before writes
+            self.workspace.fill_(float("nan"))
         torch.cuda.synchronize(self.device)
         if comm is not None and comm.world_size > 1:  # DDP ctor semantics: rank 0's weights everywhere
             st = torch.cuda.current_stream(self.device).cuda_stream
@@ -201,9 +203,17 @@ class FusedMnistTrainer:
         """Use a caller-provided batch instead of the on-device generator (real MNIST)."""
         self.eng.set_external_batch(True)
         self._external = True
+        # x / y were produced (and allocated) on the caller's stream: the engine stream waits for
+        # that work, and the allocator is told the engine stream still reads them -- otherwise the
+        # caller's next batch can reuse their memory before this step's copy has run
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
             self._x_view().copy_(x.reshape(self.batch, 1, 28, 28), non_blocking=True)
             self._y_view().copy_(y.to(torch.int32), non_blocking=True)
+        for t in (x, y):
+            if t.is_cuda:
+                t.record_stream(self.stream)
 
     def _x_view(self):
         off = (self.eng.x_ptr - self.workspace.data_ptr()) // 4

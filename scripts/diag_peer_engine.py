@@ -68,6 +68,19 @@ def worker(rank, ws, port, q):
         solo2.step(1)
     solo2.synchronize()
     res["solo2"] = [round((solo2.params.cpu() - w_).abs().max().item(), 7), solo2.params.cpu()[18816:18819].tolist()]
+    os.environ["MXDDP_POISON_WORKSPACE"] = "1"
+    solo3 = FusedMnistTrainer(batch=ws * b, device=0, comm=None, lr=lr, init_model=init, use_graph=False)
+    for x, y in batches:
+        solo3.set_batch(x.cuda(), y.cuda())
+        solo3.step(1)
+    solo3.synchronize()
+    del os.environ["MXDDP_POISON_WORKSPACE"]
+    d3 = (solo3.params.cpu() - w_).abs()
+    off, per = 0, {}
+    for k, v in init.state_dict().items():
+        per[k] = d3[off:off + v.numel()].max().item()
+        off += v.numel()
+    res["solo3_poisoned"] = per
     for same in (True, False):
         for ov in (True, False):
             tr = FusedMnistTrainer(batch=b, device=0, comm=None, peer=pc, lr=lr, init_model=init, use_graph=False)
