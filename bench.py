@@ -103,9 +103,19 @@ def main():
     if a.impl == "fused":
         from mxddp.engine import FusedMnistTrainer
 
+        peer = None
+        if comm is None and inf.world_size > 1:  # ranks share a GPU (rehearsal): peer transport only
+            from mxddp.parallel import peer as P
+
+            peer = P.peer_comm()
+            if peer is None:
+                raise SystemExit("bench.py: ranks share a GPU and the peer transport is unavailable")
+            if inf.rank == 0:
+                print(f"bench.py: {inf.local_world_size} ranks share {torch.cuda.device_count()} GPU(s): "
+                      "peer transport only (functional rehearsal, not a scaling measurement)", file=sys.stderr)
         tr = FusedMnistTrainer(batch=B, device=dev, comm=comm, seed=a.seed, variant=a.variant, lr=a.lr,
                                use_graph=not a.no_graph, graph_mode=a.graph_mode, steps_per_graph=a.steps_per_graph,
-                               force_collectives=a.force_collectives, transport=a.transport)
+                               force_collectives=a.force_collectives, transport=a.transport, peer=peer)
         run = tr.step
         if a.graph_mode is None and not a.no_autotune and tr.eng.reducer_active:
             tr.step(1)
@@ -158,6 +168,8 @@ def main():
                           if a.impl == "fused" else {})},
             **extra,
         }
+        if C.shared_devices():
+            out["shared_gpu_rehearsal"] = True  # several ranks on one GPU: not a scaling number
         print(json.dumps(out), flush=True)
     C.shutdown()
 

@@ -101,6 +101,8 @@ def rccl_comm(force: bool = False):
     inf = info()
     if (inf.world_size == 1 and not force) or inf.device.type != "cuda":
         return None
+    if inf.world_size > 1 and shared_devices():
+        return None  # RCCL refuses several ranks on one GPU; such jobs use the peer transport
     if _COMM is None and inf.world_size == 1:
         C = native()
         _COMM = C.Comm(C.Comm.new_unique_id(), 0, 1, inf.device.index)
@@ -113,6 +115,13 @@ def rccl_comm(force: bool = False):
         uid = store.get(key)
         _COMM = C.Comm(uid, inf.rank, inf.world_size, inf.device.index)
     return _COMM
+
+
+def shared_devices() -> bool:
+    """True when this node runs more ranks than it has GPUs (ranks share a device: a functional
+    rehearsal of a multi-GPU job on a 1-GPU box).  RCCL cannot build a communicator then."""
+    inf = info()
+    return inf.device.type == "cuda" and inf.local_world_size > torch.cuda.device_count()
 
 
 def barrier():
