@@ -294,9 +294,9 @@ PYBIND11_MODULE(_C, m) {
         for (auto& b : all) v.push_back(std::string(b));
         p.open(v);
       })
-      .def("all_reduce", [](PeerComm& p, uintptr_t data, size_t n, DType t, uintptr_t st) {
-        p.all_reduce(P<void>(data), n, t, S(st));
-      })
+      .def("all_reduce", [](PeerComm& p, uintptr_t data, size_t n, DType t, uintptr_t st, RedOp op) {
+        p.all_reduce(P<void>(data), n, t, S(st), op);
+      }, py::arg("data"), py::arg("count"), py::arg("dtype"), py::arg("stream"), py::arg("op") = RedOp::kSum)
       .def("error", &PeerComm::error)
       .def("reset_error", &PeerComm::reset_error)
       .def("set_blocks", &PeerComm::set_blocks)

@@ -114,8 +114,9 @@ void PeerComm::set_blocks(int b) {
 int PeerComm::error() const { return __atomic_load_n(err_host_, __ATOMIC_ACQUIRE); }
 void PeerComm::reset_error() { __atomic_store_n(err_host_, 0, __ATOMIC_RELEASE); }
 
-void PeerComm::all_reduce(void* data, size_t count, DType t, hipStream_t st) {
+void PeerComm::all_reduce(void* data, size_t count, DType t, hipStream_t st, RedOp op) {
   if (ws_ == 1 || count == 0) return;
+  MX_CHECK(op == RedOp::kSum || op == RedOp::kAvg, "peer transport: sum or average only");
   MX_CHECK(opened_, "peer transport: open() the peer handles first");
   const size_t esz = dtype_size(t);
   const size_t per = cap_ / esz;  // elements per launch
@@ -131,6 +132,7 @@ void PeerComm::all_reduce(void* data, size_t count, DType t, hipStream_t st) {
   a.rank = rank_;
   a.ws = ws_;
   a.fence = fence_;
+  a.scale = op == RedOp::kAvg ? 1.f / static_cast<float>(ws_) : 1.f;
   for (size_t off = 0; off < count; off += per) {
     a.data = static_cast<char*>(data) + off * esz;
     a.count = static_cast<long long>(count - off < per ? count - off : per);

@@ -47,6 +47,7 @@ struct PeerArgs {
   long long count;                // elements
   long long slot_bytes;           // bytes of one slot (region = W slots; 2 regions x 2 parities)
   long long timeout;              // s_memrealtime ticks (100 MHz)
+  float scale;                    // applied to the sum (1 = sum, 1/ws = average)
   int rank, ws;
   int fence;                      // bit 0: system release before flag stores; bit 1: acquire after waits
 };
@@ -69,8 +70,9 @@ class PeerComm {
 
   std::string handles() const;                       // this rank's IPC handles (opaque bytes)
   void open(const std::vector<std::string>& all);    // every rank's handles, rank order
-  // in-place sum all-reduce of `count` elements (f32 or bf16) on `st`; graph-capturable
-  void all_reduce(void* data, size_t count, DType t, hipStream_t st);
+  // in-place all-reduce of `count` elements (f32 or bf16) on `st`: sum, or average
+  // (RedOp::kAvg, the sum times 1/world_size); graph-capturable
+  void all_reduce(void* data, size_t count, DType t, hipStream_t st, RedOp op = RedOp::kSum);
   int error() const;                                 // 0 = ok; else 1 + (peer that timed out)
   void reset_error();
   void set_blocks(int b);

@@ -197,6 +197,10 @@ __global__ __launch_bounds__(kThreads) void peer_all_reduce_kernel(PeerArgs a, P
       float acc[V];
 #pragma unroll
       for (int p = 0; p < W; ++p) acc16<T>(acc, v[p], p == 0);
+      if (a.scale != 1.f) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] *= a.scale;
+      }
       const u32x4 out = pack16<T>(acc);
       reinterpret_cast<u32x4*>(mine)[i] = out;
 #pragma unroll
@@ -210,6 +214,7 @@ __global__ __launch_bounds__(kThreads) void peer_all_reduce_kernel(PeerArgs a, P
         const float v = p == r ? ld_elem<T>(mine + i, false) : ld_elem<T>(scat + (long long)p * slot + i, true);
         acc = p == 0 ? v : acc + v;
       }
+      if (a.scale != 1.f) acc *= a.scale;
       st_elem<T>(mine + i, acc);
       const T rounded = mine[i];
 #pragma unroll

@@ -58,8 +58,8 @@ void Reducer::launch_ready(hipStream_t compute) {
       }
       if (timing_ && bi == 0) MX_HIP_CHECK(hipEventRecord(t0_, st));
       char* p = flat_ + b.offset * dtype_size(dtype_);
-      if (peer_ && op_ == RedOp::kSum && peer_->world_size() > 1) {
-        peer_->all_reduce(p, b.numel, dtype_, st);
+      if (peer_ && (op_ == RedOp::kSum || op_ == RedOp::kAvg) && peer_->world_size() > 1) {
+        peer_->all_reduce(p, b.numel, dtype_, st, op_);
       } else {
         MX_CHECK(comm_ != nullptr, "reducer: no RCCL communicator for this collective");
         comm_->all_reduce(p, p, b.numel, dtype_, op_, st);

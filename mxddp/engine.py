@@ -204,16 +204,14 @@ class FusedMnistTrainer:
         self.eng.set_external_batch(True)
         self._external = True
         # x / y were produced (and allocated) on the caller's stream: the engine stream waits for
-        # that work, and the allocator is told the engine stream still reads them -- otherwise the
+        # that work before copying, and the caller's stream waits for the copy -- otherwise the
         # caller's next batch can reuse their memory before this step's copy has run
         cur = torch.cuda.current_stream(self.device)
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
             self._x_view().copy_(x.reshape(self.batch, 1, 28, 28), non_blocking=True)
             self._y_view().copy_(y.to(torch.int32), non_blocking=True)
-        for t in (x, y):
-            if t.is_cuda:
-                t.record_stream(self.stream)
+        cur.wait_stream(self.stream)
 
     def _x_view(self):
         off = (self.eng.x_ptr - self.workspace.data_ptr()) // 4

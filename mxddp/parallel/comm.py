@@ -121,7 +121,8 @@ def shared_devices() -> bool:
     """True when this node runs more ranks than it has GPUs (ranks share a device: a functional
     rehearsal of a multi-GPU job on a 1-GPU box).  RCCL cannot build a communicator then."""
     inf = info()
-    return inf.device.type == "cuda" and inf.local_world_size > torch.cuda.device_count()
+    n = torch.cuda.device_count()
+    return inf.device.type == "cuda" and 0 < n < inf.local_world_size
 
 
 def barrier():

@@ -57,7 +57,7 @@ def assign_buckets(numels: list[int], offsets: list[int], total: int, bucket_cap
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers: bool = True,
                  bucket_cap_mb: float = 25.0, first_bucket_cap_mb: float = 1.0, average: bool = True,
-                 timing: bool = False):
+                 timing: bool = False, transport: str = "auto"):
         super().__init__()
         self.module = module
         inf = _comm.info()
@@ -78,10 +78,41 @@ class DistributedDataParallel(nn.Module):
                                      self.param_bucket, C.RedOp.avg if average else C.RedOp.sum, timing)
         else:
             self.reducer = _GlooReducer(self.flat.grad, self.buckets, self.param_bucket, average, self.world_size)
+        self.transport = "rccl" if self.device.type == "cuda" else "gloo"
+        self.transport_ms = None
+        if self.device.type == "cuda" and self.world_size > 1:
+            self._select_transport(transport)
         self._queued = False
         # fires on both gradient paths: returned gradients and gradients the GPU kernels wrote
         # straight into the flat buffer (mxddp.ops._grad_sink; AccumulateGrad still runs)
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(self.flat.params)]
+
+    def _select_transport(self, transport: str):
+        """Gradient all-reduce transport: RCCL's ring or the direct xGMI peer all-reduce
+        (parallel/peer.py).  "auto" validates the peer transport against RCCL and times both on
+        this model's buckets; ranks sharing one GPU (no RCCL) must use the peer transport."""
+        from . import peer as _peer
+
+        if transport == "rccl" and self._comm is not None:
+            return
+        pc = _peer.peer_comm()
+        if self._comm is None:
+            if pc is None:
+                raise RuntimeError("DDP: no RCCL communicator (ranks share a GPU) and no peer transport")
+            self.reducer.set_peer(pc)
+            self.transport = "peer"
+            return
+        if pc is None or not _peer.validate(pc, self._comm):
+            if transport == "peer":
+                raise RuntimeError("DDP: peer transport requested but unavailable / failed validation")
+            return
+        if transport == "auto":
+            choice, self.transport_ms = _peer.pick_transport(pc, self._comm, [n for _, n in self.buckets])
+        else:
+            choice = "peer"
+        if choice == "peer":
+            self.reducer.set_peer(pc)
+            self.transport = "peer"
 
     # ------------------------------------------------------------------ sync helpers
     def _broadcast(self, t: torch.Tensor):
@@ -91,6 +122,10 @@ class DistributedDataParallel(nn.Module):
             C = native()
             self._comm.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), C.DType.f32, 0,
                                  torch.cuda.current_stream(self.device).cuda_stream)
+        elif t.is_cuda:  # ranks sharing a GPU: no RCCL, broadcast through the gloo control plane
+            h = t.cpu()
+            dist.broadcast(h, 0)
+            t.copy_(h)
         else:
             dist.broadcast(t, 0)
 

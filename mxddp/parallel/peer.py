@@ -98,6 +98,40 @@ def validate(pc, rccl, dtype: str = "f32", numel: int = 1_181_066, iters: int = 
     return _agree_ok(ok)
 
 
+def pick_transport(pc, rccl, numels: list[int], dtype: str = "f32", iters: int = 10) -> tuple[str, dict]:
+    """Time one pass of all-reduces over buckets of `numels` elements with each transport (the
+    DDP reducer's buckets), slowest rank decides; every rank returns the same choice."""
+    import time
+
+    inf = _comm.info()
+    C = native()
+    dev = inf.device
+    tdt = torch.float32 if dtype == "f32" else torch.bfloat16
+    cdt = C.DType.f32 if dtype == "f32" else C.DType.bf16
+    bufs = [torch.zeros(n, dtype=tdt, device=dev) for n in numels]
+    st = torch.cuda.current_stream(dev).cuda_stream
+    res = {}
+    for name in ("rccl", "peer"):
+        def one_pass():
+            for b in bufs:
+                if name == "peer":
+                    pc.all_reduce(b.data_ptr(), b.numel(), cdt, st)
+                else:
+                    rccl.all_reduce(b.data_ptr(), b.data_ptr(), b.numel(), cdt, C.RedOp.sum, st)
+        one_pass()
+        torch.cuda.synchronize(dev)
+        _comm.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            one_pass()
+        torch.cuda.synchronize(dev)
+        res[name] = _comm.all_reduce_max(time.perf_counter() - t0) / iters * 1e3
+    if pc.error():
+        res["peer"] = float("inf")
+    res["peer"] = _comm.all_reduce_max(res["peer"])
+    return min(res, key=res.get), res
+
+
 def shutdown():
     global _PEER
     _PEER = None

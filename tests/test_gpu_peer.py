@@ -46,7 +46,67 @@ def _expected(ws, count, rep, dtype):
     return acc.to(dtype)
 
 
+def _ddp_layers_worker(rank, ws, port, q):
+    """mxddp DistributedDataParallel (layers path, bucket reducer) with ranks sharing the GPU:
+    the reducer's peer transport (average) against one process on the global batch."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(ws))
+    from mxddp import ops
+    from mxddp.models import build_model
+    from mxddp.optim import SGD
+    from mxddp.parallel import comm as PC
+    from mxddp.parallel.ddp import DistributedDataParallel as DDP
+    from mxddp.parallel.flat import FlatParams
+
+    PC.init_distributed(use_gpu=True)
+    bad = []
+    b, steps = 8, 3
+    torch.manual_seed(0)
+    init = build_model("keras_cnn")
+    sd0 = {k: v.clone() for k, v in init.state_dict().items()}
+    g = torch.Generator().manual_seed(7)
+    batches = [(torch.rand(ws * b, 1, 28, 28, generator=g), torch.randint(0, 10, (ws * b,), generator=g))
+               for _ in range(steps)]
+    ddp = DDP(init.cuda(), bucket_cap_mb=0.1)  # several buckets
+    if ddp.transport != "peer":
+        bad.append(("transport", ddp.transport))
+    opt = SGD(ddp.flat, lr=0.05, momentum=0.9, weight_decay=1e-4)
+    for x, y in batches:
+        opt.zero_grad()
+        ops.cross_entropy(ddp(x[rank * b:(rank + 1) * b].cuda()), y[rank * b:(rank + 1) * b].cuda()).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    mine = ddp.flat.data.cpu()
+    allp = [None] * ws
+    torch.distributed.all_gather_object(allp, mine)
+    if any(not torch.equal(allp[0], t) for t in allp):
+        bad.append("ranks diverged")
+    if rank == 0:
+        ref = build_model("keras_cnn")
+        ref.load_state_dict(sd0)
+        ref = ref.cuda()
+        flat = FlatParams(ref, torch.device("cuda", 0))
+        ropt = SGD(flat, lr=0.05, momentum=0.9, weight_decay=1e-4)
+        for x, y in batches:
+            ropt.zero_grad()
+            flat.attach_grads()
+            ops.cross_entropy(ref(x.cuda()), y.cuda()).backward()
+            ropt.step()
+        torch.cuda.synchronize()
+        d = (flat.data.cpu() - mine).abs().max().item()
+        if not d < 1e-5:
+            bad.append(("ddp != global batch", d, len(ddp.buckets)))
+    q.put((rank, bad, ddp.transport))
+    PC.shutdown()
+
+
 def _worker(rank, ws, port, mode, q):
+    if mode == "ddp_layers":
+        try:
+            return _ddp_layers_worker(rank, ws, port, q)
+        except Exception:
+            q.put((rank, ["exception: " + traceback.format_exc()], ""))
+            return
     try:
         import torch.distributed as dist
 
@@ -207,6 +267,10 @@ def test_peer_all_reduce_graph_replay(cuda):
 @pytest.mark.parametrize("mode", ["trainer", "trainer_graph"])
 def test_fused_trainer_peer_ddp_matches_global_batch(cuda, mode):
     _run(2 if mode == "trainer" else 4, mode)
+
+
+def test_ddp_layers_peer_transport_matches_global_batch(cuda):
+    _run(2, "ddp_layers")
 
 
 def test_peer_all_reduce_timeout_reports_missing_peer(cuda):
