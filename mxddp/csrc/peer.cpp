@@ -52,7 +52,11 @@ PeerComm::PeerComm(int rank, int world_size, int device, size_t cap_bytes, int b
   xbuf_ = alloc_shared(xbytes_, &k1);
   sig_ = reinterpret_cast<uint32_t*>(alloc_shared(sbytes_, &k2));
   mem_kind_ = k1 == k2 ? k1 : k1 + "+" + k2;
-  if (mem_kind_ != "uncached") fence_ = 3;
+  // uncached exchange memory: remote stores bypass the producer's L2 and every load of
+  // exchanged bytes is `nt` from uncached memory (bypasses L1 and L2), so the consumer needs no
+  // acquire; the release before each flag store is kept (it orders the flag behind the payload's
+  // write acknowledgements on every path).  Cached fallbacks run both fences.
+  fence_ = mem_kind_ == "uncached" ? 1 : 3;
   MX_HIP_CHECK(hipMemset(sig_, 0, sbytes_));
   MX_HIP_CHECK(hipMalloc(&epoch_, kPeerMaxBlocks * sizeof(uint32_t)));
   MX_HIP_CHECK(hipMemset(epoch_, 0, kPeerMaxBlocks * sizeof(uint32_t)));

@@ -17,8 +17,8 @@
 // workgroup: block b of rank r only waits for block b of the peers (flags, no grid barrier).
 // The exchange buffers and flags live in UNCACHED device memory (hipDeviceMallocUncached)
 // shared between the processes through HIP IPC handles: remote stores land in the owner's
-// HBM, and local reads of them bypass L2 (plus `nt` loads to bypass L1), so no cache holds
-// a stale copy.  Every wait is bounded: a peer that never arrives sets an error word in
+// HBM, and local reads of them are `nt` loads of uncached memory (bypass L1 and L2), so no
+// cache holds a stale copy.  Every wait is bounded: a peer that never arrives sets an error word in
 // host-mapped memory and the kernel exits (PeerComm::error()), so a broken peer can never
 // leave waves spinning on the GPU.
 //
@@ -97,8 +97,8 @@ class PeerComm {
   char* peer_x_[kPeerMaxRanks] = {};
   uint32_t* peer_sig_[kPeerMaxRanks] = {};
   bool opened_ = false;
-  int fence_ = 3;
-  long long timeout_ = 500000000;  // 5 s
+  int fence_ = 1;
+  long long timeout_ = 3000000000ll;  // 30 s
   std::string mem_kind_;
 };
 

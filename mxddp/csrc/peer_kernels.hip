@@ -193,7 +193,7 @@ __global__ __launch_bounds__(kThreads) void peer_all_reduce_kernel(PeerArgs a, P
 #pragma unroll
       for (int p = 0; p < W; ++p)
         v[p] = p == r ? reinterpret_cast<const u32x4*>(mine)[i]
-                      : reinterpret_cast<const u32x4*>(scat + (long long)p * slot)[i];
+                      : __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(scat + (long long)p * slot) + i);
       float acc[V];
 #pragma unroll
       for (int p = 0; p < W; ++p) acc16<T>(acc, v[p], p == 0);
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(kThreads) void peer_all_reduce_kernel(PeerArgs a, P
   for (long long i = t; i < nvmin; i += kThreads) {
     u32x4 v[W - 1];
 #pragma unroll
-    for (int j = 1; j < W; ++j) v[j - 1] = reinterpret_cast<const u32x4*>(gat[j])[i];
+    for (int j = 1; j < W; ++j) v[j - 1] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(gat[j]) + i);
 #pragma unroll
     for (int j = 1; j < W; ++j) reinterpret_cast<u32x4*>(const_cast<T*>(src[j]))[i] = v[j - 1];
   }
@@ -236,8 +236,8 @@ __global__ __launch_bounds__(kThreads) void peer_all_reduce_kernel(PeerArgs a, P
   for (int j = 1; j < W; ++j) {
     T* out = const_cast<T*>(src[j]);
     for (long long i = nvmin + t; i < n[j] / V; i += kThreads)
-      reinterpret_cast<u32x4*>(out)[i] = reinterpret_cast<const u32x4*>(gat[j])[i];
-    for (long long i = n[j] / V * V + t; i < n[j]; i += kThreads) out[i] = gat[j][i];
+      reinterpret_cast<u32x4*>(out)[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(gat[j]) + i);
+    for (long long i = n[j] / V * V + t; i < n[j]; i += kThreads) out[i] = __builtin_nontemporal_load(gat[j] + i);
   }
   if (t == 0) a.epoch[b] = ep;
 }
