@@ -122,7 +122,9 @@ def translate(script: str, argv: list[str]) -> list[str]:
         a = _tf2_parser(multi, mirror).parse_args(argv)
         out = ["--model", "keras_cnn", "--optimizer", "adam", "-td", a.train_dir, "-dd", a.dataset_dir,
                "-tb", str(a.test_batchsize), "-e", str(a.epochs), "--log-interval", str(a.log_interval),
-               "--save-every", "1", "--eval", "--lr-step-size", "0"]
+               "--save-every", "1", "--eval", "--eval-every", "1", "--lr-step-size", "0",  # fit(validation_data)
+               # TensorBoard(log_dir=train_dir, histogram_freq=1) + model.summary()
+               "--tensorboard-dir", a.train_dir, "--histogram-freq", "1", "--summary"]
         if a.learning_rate is not None:
             out += ["--lr", str(a.learning_rate)]
         if multi:
@@ -142,7 +144,9 @@ def translate(script: str, argv: list[str]) -> list[str]:
         a = _chainer_parser(kind).parse_args(argv)
         out = ["--model", "mlp", "--optimizer", "adam", "--mlp-units", str(a.unit), "-e", str(a.epoch),
                "-td", a.out, "-dd", a.dataset_dir, "--eval-every", "1", "--lr-step-size", "0",
-               "--metrics-jsonl", f"{a.out}/log.jsonl", "-sm"]
+               "--metrics-jsonl", f"{a.out}/log.jsonl", "-sm",
+               # LogReport (<out>/log), PrintReport, dump_graph('main/loss') (<out>/cg.dot)
+               "--chainer-out", a.out]
         if a.resume:
             out += ["--resume", a.resume]
         if kind == "single":

@@ -79,7 +79,60 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--metrics-jsonl", type=str, default="", help="append JSONL metrics here")
     p.add_argument("--max-steps", type=int, default=0, help="stop after this many steps (0 = full epochs)")
     p.add_argument("--sync-set-epoch", action="store_true", default=True)
+    p.add_argument("--tensorboard-dir", type=str, default="",
+                   help="write TensorBoard event files here (TF2 TensorBoard callback; rank 0 only)")
+    p.add_argument("--histogram-freq", type=int, default=1, help="TensorBoard weight histograms every N epochs (0 = off)")
+    p.add_argument("--chainer-out", type=str, default="",
+                   help="Chainer trainer extensions: LogReport (<dir>/log), PrintReport, dump_graph (<dir>/cg.dot)")
+    p.add_argument("--summary", action="store_true", help="print a Keras-style model summary")
     return p
+
+
+class _Reporter:
+    """Per-epoch reporting of the reference frameworks' trainer extensions: TensorBoard scalars +
+    weight histograms (TF2), Chainer LogReport / PrintReport / dump_graph.  Rank 0 only."""
+
+    def __init__(self, args, inf):
+        from .utils.report import LogReport, PrintReport
+        from .utils.tensorboard import SummaryWriter
+
+        main = inf.is_main
+        self.tb = SummaryWriter(args.tensorboard_dir, enabled=main) if args.tensorboard_dir else None
+        self.hist_freq = args.histogram_freq
+        self.log = LogReport(args.chainer_out, enabled=main) if args.chainer_out else None
+        self.pr = PrintReport(enabled=main, out=lambda s: print(s, flush=True)) if args.chainer_out else None
+        self.graph_path = os.path.join(args.chainer_out, "cg.dot") if (args.chainer_out and main) else None
+        self.t0 = time.time()
+
+    def first_loss(self, loss, model):
+        if self.graph_path is not None and loss.grad_fn is not None:
+            from .utils.report import dump_graph
+
+            dump_graph(loss, self.graph_path, dict(model.named_parameters()))
+            self.graph_path = None
+
+    def epoch_end(self, epoch, step, loss, acc, val, model):
+        if self.tb is not None:
+            self.tb.add_scalar("epoch_loss", loss, epoch)
+            self.tb.add_scalar("epoch_accuracy", acc, epoch)
+            if val is not None:
+                self.tb.add_scalar("epoch_val_loss", val[0], epoch)
+                self.tb.add_scalar("epoch_val_accuracy", val[1] / 100.0, epoch)
+            if self.hist_freq and epoch % self.hist_freq == 0 and model is not None:
+                for n, p in model.named_parameters():
+                    self.tb.add_histogram(n, p, epoch)
+            self.tb.flush()
+        if self.log is not None:
+            e = {"epoch": epoch, "iteration": step, "main/loss": loss, "main/accuracy": acc,
+                 "elapsed_time": time.time() - self.t0}
+            if val is not None:
+                e["validation/main/loss"], e["validation/main/accuracy"] = val[0], val[1] / 100.0
+            self.log.append(e)
+            self.pr(e)
+
+    def close(self):
+        if self.tb is not None:
+            self.tb.close()
 
 
 def _resolve(args, spec, inf):
@@ -215,7 +268,7 @@ def _maybe_eval(args, inf, spec, model, bs, mw, epoch=None, force=False):
     create_multi_node_evaluator semantics, chainer/train_mnist_multi.py:102-104)."""
     periodic = epoch is not None and args.eval_every and epoch % args.eval_every == 0
     if not (force and args.eval) and not periodic:
-        return
+        return None
     from .data import build_loader
     from .parallel import comm as C
 
@@ -231,6 +284,7 @@ def _maybe_eval(args, inf, spec, model, bs, mw, epoch=None, force=False):
         tag = f"epoch {epoch} " if epoch is not None else ""
         print(f"Test ({kind}) {tag}: loss {loss:.4f} | acc {acc:.3f}", flush=True)
     mw.write(kind="eval", epoch=epoch, loss=loss, acc=acc)
+    return loss, acc
 
 
 def _save_final(args, inf, mode, state_dict):
@@ -282,6 +336,11 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
                                 steps=args.steps_per_epoch)
     if inf.is_main:
         print(f"==> data: {kind}, {len(loader)} batches/epoch", flush=True)
+        if args.summary:
+            from .utils.report import model_summary
+
+            print(model_summary(model, spec.input_shape, spec.name), flush=True)
+    rep = _Reporter(args, inf)
     step = 0
     for epoch in range(start_epoch, args.epochs + 1):
         if hasattr(loader, "sampler"):
@@ -296,6 +355,8 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
             opt.zero_grad()
             out = net(x)
             loss, corr = ops.cross_entropy(out, y, return_correct=True)
+            if step == 0:
+                rep.first_loss(loss, model)
             loss.backward()
             opt.step()
             loss_acc += loss.detach()
@@ -317,13 +378,16 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
         _log_epoch(inf, mode, time.time() - t_epoch)
         if sched:
             sched.step()
-        _maybe_eval(args, inf, spec, model, bs, mw, epoch=epoch)
+        val = _maybe_eval(args, inf, spec, model, bs, mw, epoch=epoch)
+        nb_done = bi + 1
+        rep.epoch_end(epoch, step, loss_acc.item() / max(1, nb_done), corr_acc.item() / max(1, total), val, model)
         if args.save_every and epoch % args.save_every == 0:
             save_training_state(args.train_dir, inf.rank, model.state_dict(), opt.state_dict(),
                                 sched.state_dict() if sched else None, epoch, step)
         if args.max_steps and step >= args.max_steps:
             break
     _maybe_eval(args, inf, spec, model, bs, mw, force=True)
+    rep.close()
     _save_final(args, inf, mode, model.state_dict())
 
 
@@ -349,7 +413,17 @@ def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
     loader, kind = build_loader(spec.dataset, args.data, args.dataset_dir, bs, devices[0], 1, 0, args.seed,
                                 spec.input_shape, spec.num_classes, train=True, steps=args.steps_per_epoch)
     print(f"==> replica mode on {len(devices)} device(s), global batch {bs}, data {kind}", flush=True)
+    if args.summary:
+        from .utils.report import model_summary
+
+        print(model_summary(group.module, spec.input_shape, spec.name), flush=True)
     loss_fn = lambda o, t: ops.cross_entropy(o, t, return_correct=True)  # noqa: E731
+    rep = _Reporter(args, inf)
+    if rep.graph_path is not None:  # dump_graph from one replica-0 forward on a slice of the first batch
+        x0, y0 = next(iter(loader))
+        rep.first_loss(loss_fn(group.module(x0[:max(1, x0.shape[0] // len(devices))].to(devices[0])),
+                               y0[:max(1, x0.shape[0] // len(devices))].to(devices[0]))[0], group.module)
+        group.zero_grad()
     step = 0
     for epoch in range(1, args.epochs + 1):
         if hasattr(loader, "sampler"):
@@ -378,10 +452,13 @@ def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
         _log_epoch(inf, "single", time.time() - t_epoch)
         for s in scheds:
             s.step()
-        _maybe_eval(args, inf, spec, group.module, bs, mw, epoch=epoch)
+        val = _maybe_eval(args, inf, spec, group.module, bs, mw, epoch=epoch)
+        rep.epoch_end(epoch, step, loss_acc.item() / max(1, bi + 1), corr_acc.item() / max(1, total), val,
+                      group.module)
         if args.max_steps and step >= args.max_steps:
             break
     _maybe_eval(args, inf, spec, group.module, bs, mw, force=True)
+    rep.close()
     _save_final(args, inf, "replica", group.module.state_dict())
 
 
@@ -412,6 +489,16 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
         print("From Rank: {}, The number of parameters of model is {}".format(inf.rank, 1199882), flush=True)
         print(f"==> data: {kind}, {len(loader)} batches/epoch, fused hipGraph step={'off' if args.no_graph else 'on'}",
               flush=True)
+    rep = _Reporter(args, inf)
+    if rep.graph_path is not None or (args.summary and inf.is_main):  # layer model: same graph / shapes
+        from . import ops as _ops
+
+        probe = tr.to_module()
+        if args.summary and inf.is_main:
+            from .utils.report import model_summary
+
+            print(model_summary(probe, spec.input_shape, spec.name), flush=True)
+        rep.first_loss(_ops.cross_entropy(probe(torch.zeros(2, 1, 28, 28)), torch.zeros(2, dtype=torch.long)), probe)
     step = 0
     base_lr = lr
     for epoch in range(start_epoch, args.epochs + 1):
@@ -463,6 +550,12 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
                     break
         tr.synchronize()
         _log_epoch(inf, mode, time.time() - t_epoch)
+        if rep.tb is not None or rep.log is not None:
+            ls, cs = tr.read_metrics()  # remainder since the last log line
+            loss_tot, corr_tot = loss_tot + ls, corr_tot + cs
+            seen = max(1, bi * bs)
+            rep.epoch_end(epoch, step, loss_tot / seen, corr_tot / seen, None,
+                          tr.to_module() if rep.tb is not None else None)
         if args.save_every and epoch % args.save_every == 0:
             save_training_state(args.train_dir, inf.rank, tr.state_dict(), {"momentum": tr.mom.cpu(), "lr": tr._lr_host},
                                 {"base_lr": base_lr}, epoch, step)
@@ -470,6 +563,7 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
             break
     model = tr.to_module().to(dev)
     _maybe_eval(args, inf, spec, model, bs, mw, force=True)
+    rep.close()
     _save_final(args, inf, mode, tr.state_dict())
 
 

@@ -3,6 +3,7 @@ from __future__ import annotations
 
 import datetime
 import json
+import os
 import time
 
 
@@ -32,6 +33,8 @@ class MetricsWriter:
 
     def __init__(self, path: str | None):
         self.path = path
+        if path and os.path.dirname(path):
+            os.makedirs(os.path.dirname(path), exist_ok=True)
         self._f = open(path, "a") if path else None
 
     def write(self, **rec):
