@@ -189,6 +189,8 @@ def _replica(a):
     devices = [torch.device("cuda", i) for i in range(a.gpus)]
     spec = get_spec(a.model)
     torch.manual_seed(a.seed)
+    if a.model == "mnist_cnn" and a.dtype == "fp32" and not a.no_graph:
+        return _replica_fused(a, devices, spec)
 
     def make_opt(flat):
         if spec.optimizer == "adam":
@@ -233,6 +235,32 @@ def _replica(a):
         "config": {"model": a.model, "global_batch": B, "per_rank_batch": a.batch, "seq_len": None,
                    "image": "x".join(map(str, spec.input_shape)), "parallelism": f"replica{a.gpus}",
                    "impl": "replica"}}), flush=True)
+
+
+def _replica_fused(a, devices, spec):
+    """In-process replicas of the fused MNIST engine (one per GPU, peer transport opened in-process,
+    every replica's step one hipGraph launch): MirroredStrategy / DataParallel semantics."""
+    import torch
+
+    from mxddp.parallel.replica import FusedMnistReplicas
+
+    rep = FusedMnistReplicas(devices, batch=a.batch, lr=a.lr, seed=a.seed, steps_per_graph=a.steps_per_graph)
+    rep.step(a.warmup)
+    rep.synchronize()
+    t0 = time.perf_counter()
+    rep.step(a.steps)
+    rep.synchronize()
+    dt = time.perf_counter() - t0
+    B = a.batch * len(devices)
+    value = B * a.steps / dt
+    print(json.dumps({
+        "metric": _metric(a.model), "value": round(value, 1), "unit": "images/sec", "n_gpus": a.gpus, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": a.dtype, "data": _data_desc(spec),
+        "config": {"model": a.model, "global_batch": B, "per_rank_batch": a.batch, "seq_len": None,
+                   "image": "x".join(map(str, spec.input_shape)), "parallelism": f"replica{a.gpus}",
+                   "impl": "replica-fused", "transport": "peer (in-process)" if len(devices) > 1 else "none",
+                   "graph": True}}), flush=True)
 
 
 def _data_desc(spec):

@@ -294,6 +294,7 @@ PYBIND11_MODULE(_C, m) {
         for (auto& b : all) v.push_back(std::string(b));
         p.open(v);
       })
+      .def("open_local", &PeerComm::open_local)
       .def("all_reduce", [](PeerComm& p, uintptr_t data, size_t n, DType t, uintptr_t st, RedOp op) {
         p.all_reduce(P<void>(data), n, t, S(st), op);
       }, py::arg("data"), py::arg("count"), py::arg("dtype"), py::arg("stream"), py::arg("op") = RedOp::kSum)

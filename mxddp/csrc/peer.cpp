@@ -74,7 +74,7 @@ PeerComm::~PeerComm() {
   hipSetDevice(dev_);
   hipDeviceSynchronize();
   for (int p = 0; p < ws_; ++p) {
-    if (p == rank_ || !opened_) continue;
+    if (p == rank_ || !opened_ || local_) continue;
     if (peer_x_[p]) hipIpcCloseMemHandle(peer_x_[p]);
     if (peer_sig_[p]) hipIpcCloseMemHandle(peer_sig_[p]);
   }
@@ -108,6 +108,29 @@ void PeerComm::open(const std::vector<std::string>& all) {
     peer_sig_[p] = static_cast<uint32_t*>(s);
   }
   opened_ = true;
+}
+
+void PeerComm::open_local(const std::vector<PeerComm*>& all) {
+  MX_CHECK(!opened_, "peer transport already opened");
+  MX_CHECK(static_cast<int>(all.size()) == ws_, "peer transport: need one PeerComm per rank");
+  MX_HIP_CHECK(hipSetDevice(dev_));
+  for (int p = 0; p < ws_; ++p) {
+    MX_CHECK(all[p] && all[p]->ws_ == ws_ && all[p]->rank_ == p, "peer transport: replicas out of rank order");
+    MX_CHECK(all[p]->blocks_ == blocks_ && all[p]->slot_bytes_ == slot_bytes_, "peer transport: replica shapes differ");
+    if (p == rank_) continue;
+    const int d = all[p]->dev_;
+    if (d != dev_) {
+      int can = 0;
+      MX_HIP_CHECK(hipDeviceCanAccessPeer(&can, dev_, d));
+      MX_CHECK(can, "peer transport: no peer access between the replicas' devices");
+      const hipError_t e = hipDeviceEnablePeerAccess(d, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) MX_HIP_CHECK(e);
+      (void)hipGetLastError();
+    }
+    peer_x_[p] = all[p]->xbuf_;
+    peer_sig_[p] = all[p]->sig_;
+  }
+  opened_ = local_ = true;
 }
 
 void PeerComm::set_blocks(int b) {

@@ -70,6 +70,9 @@ class PeerComm {
 
   std::string handles() const;                       // this rank's IPC handles (opaque bytes)
   void open(const std::vector<std::string>& all);    // every rank's handles, rank order
+  // in-process replicas (one PeerComm per device, one process): map the other ranks' buffers
+  // directly (device peer access instead of IPC); `all` in rank order
+  void open_local(const std::vector<PeerComm*>& all);
   // in-place all-reduce of `count` elements (f32 or bf16) on `st`: sum, or average
   // (RedOp::kAvg, the sum times 1/world_size); graph-capturable
   void all_reduce(void* data, size_t count, DType t, hipStream_t st, RedOp op = RedOp::kSum);
@@ -96,7 +99,7 @@ class PeerComm {
   int* err_dev_ = nullptr;
   char* peer_x_[kPeerMaxRanks] = {};
   uint32_t* peer_sig_[kPeerMaxRanks] = {};
-  bool opened_ = false;
+  bool opened_ = false, local_ = false;
   int fence_ = 1;
   long long timeout_ = 3000000000ll;  // 30 s
   std::string mem_kind_;

@@ -406,6 +406,10 @@ def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
         devices = [torch.device("cuda", i) for i in range(n)]
     else:
         devices = [torch.device("cpu")]
+    if (spec.name == "mnist_cnn" and opt_name == "sgd" and devices[0].type == "cuda" and args.dtype == "fp32"
+            and args.engine != "layers" and bs % len(devices) == 0 and (bs // len(devices)) % 16 == 0
+            and 16 <= bs // len(devices) <= 128):
+        return _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw)
     torch.manual_seed(args.seed)
     model = build_model(spec.name, **_model_kwargs(args, spec))
     group = ReplicaGroup(model, devices, lambda f: _make_opt(opt_name, f, lr, mom, wd, spec))
@@ -460,6 +464,67 @@ def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
     _maybe_eval(args, inf, spec, group.module, bs, mw, force=True)
     rep.close()
     _save_final(args, inf, "replica", group.module.state_dict())
+
+
+def _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw):
+    """Replica mode for the MNIST CNN on the fused engine: one FusedMnistTrainer per GPU in this
+    process, gradients averaged by the in-process peer transport (parallel/replica.py)."""
+    from .data import build_loader
+    from .models import build_model
+    from .parallel.replica import FusedMnistReplicas
+
+    torch.manual_seed(args.seed)
+    rep = FusedMnistReplicas(devices, batch=bs // len(devices), lr=lr, momentum=mom, weight_decay=wd, seed=args.seed,
+                             init_model=build_model("mnist_cnn"), use_graph=not args.no_graph)
+    loader, kind = build_loader("mnist", args.data, args.dataset_dir, bs, devices[0], 1, 0, args.seed,
+                                spec.input_shape, 10, train=True, steps=args.steps_per_epoch)
+    print(f"==> replica mode (fused engine) on {len(devices)} device(s), global batch {bs}, data {kind}", flush=True)
+    rep_ = _Reporter(args, inf)
+    step, base_lr = 0, lr
+    for epoch in range(1, args.epochs + 1):
+        if args.lr_step_size:
+            for t in rep.trainers:
+                t.set_lr(base_lr * args.lr_gamma ** ((epoch - 1) // args.lr_step_size))
+        if hasattr(loader, "sampler"):
+            loader.sampler.set_epoch(epoch)
+        nb, bi = len(loader), 0
+        t_epoch = t_log = time.time()
+        loss_tot = corr_tot = 0.0
+        it = None if kind == "synthetic" else iter(loader)
+        while bi < nb:
+            if it is None:
+                n = 1 if bi % args.log_interval == 0 else min(args.log_interval - bi % args.log_interval, nb - bi)
+                rep.step(n)
+            else:
+                x, y = next(it)
+                if x.shape[0] != bs:
+                    bi += 1
+                    continue
+                n = 1
+                rep.set_batch(x, y)
+                rep.step(1)
+            bi += n
+            step += n
+            if (bi - 1) % args.log_interval == 0 or bi == nb:
+                ls, cs = rep.read_metrics()
+                loss_tot, corr_tot = loss_tot + ls, corr_tot + cs
+                now = time.time()
+                _log_step(inf, "single", epoch, bi - 1, nb, loss_tot / (bi * bs), 100.0 * corr_tot / (bi * bs),
+                          (now - t_log) / max(1, n))
+                t_log = now
+            if args.max_steps and step >= args.max_steps:
+                break
+        rep.synchronize()
+        _log_epoch(inf, "single", time.time() - t_epoch)
+        model = rep.to_module().to(devices[0])
+        val = _maybe_eval(args, inf, spec, model, bs, mw, epoch=epoch)
+        rep_.epoch_end(epoch, step, loss_tot / max(1, bi * bs), corr_tot / max(1, bi * bs), val, model)
+        if args.max_steps and step >= args.max_steps:
+            break
+    model = rep.to_module().to(devices[0])
+    _maybe_eval(args, inf, spec, model, bs, mw, force=True)
+    rep_.close()
+    _save_final(args, inf, "replica", rep.state_dict())  # save_model adds the module. prefix
 
 
 # ====================================================================================== fused

@@ -275,3 +275,71 @@ def test_ddp_layers_peer_transport_matches_global_batch(cuda):
 
 def test_peer_all_reduce_timeout_reports_missing_peer(cuda):
     _run(2, "timeout")
+
+
+def _replicas_worker(graph, q):
+    try:
+        from mxddp.engine import FusedMnistTrainer
+        from mxddp.models import MnistCNN
+        from mxddp.parallel.replica import FusedMnistReplicas
+
+        cuda = torch.device("cuda", 0)
+        torch.manual_seed(0)
+        init = MnistCNN()
+        b, steps = 16, 4
+        g = torch.Generator().manual_seed(11)
+        batches = [(torch.rand(2 * b, 1, 28, 28, generator=g), torch.randint(0, 10, (2 * b,), generator=g))
+                   for _ in range(steps)]
+        rep = FusedMnistReplicas([cuda, cuda], batch=b, lr=0.05, init_model=init, use_graph=graph)
+        for x, y in batches:
+            rep.set_batch(x.to(cuda), y.to(cuda))
+            rep.step(1)
+        rep.synchronize()
+        p0, p1 = rep.trainers[0].params.cpu(), rep.trainers[1].params.cpu()
+        bad = []
+        if not torch.equal(p0, p1):
+            bad.append("replicas diverged")
+        ref = FusedMnistTrainer(batch=2 * b, device=cuda, comm=None, lr=0.05, init_model=init, use_graph=False)
+        for x, y in batches:
+            ref.set_batch(x.to(cuda), y.to(cuda))
+            ref.step(1)
+        ref.synchronize()
+        d = (ref.params.cpu() - p0).abs().max().item()
+        if not d < 2e-5:
+            bad.append(("replicas != global batch", d))
+        ls, _ = rep.read_metrics()
+        lr_, _ = ref.read_metrics()
+        if not abs(ls - lr_) < 1e-3 * abs(lr_):
+            bad.append(("loss", ls, lr_))
+        q.put((0, bad, ""))
+    except Exception:
+        q.put((0, ["exception: " + traceback.format_exc()], ""))
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_fused_replicas_in_process_match_global_batch(cuda, graph):
+    """In-process replica mode (MirroredStrategy / DataParallel parity) on the fused engine: two
+    replicas (here both on the one GPU, peer transport opened in-process) trained on the two
+    halves of a global batch == one trainer on the whole batch; replicas stay identical.
+    Runs in a fresh process with 8 HIP hardware queues: replicas sharing ONE device must not
+    share a hardware queue (a replica's all-reduce kernel waits for the other's, which would
+    be queued behind it) -- on a multi-GPU node every replica has its own device's queues."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    old = os.environ.get("GPU_MAX_HW_QUEUES")
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+    try:
+        p = ctx.Process(target=_replicas_worker, args=(graph, q))
+        p.start()
+    finally:
+        if old is None:
+            del os.environ["GPU_MAX_HW_QUEUES"]
+        else:
+            os.environ["GPU_MAX_HW_QUEUES"] = old
+    try:
+        _, bad, _ = q.get(timeout=200)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert bad == [], bad
