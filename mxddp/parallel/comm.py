@@ -44,13 +44,29 @@ _COMM = None
 
 
 def env_dist() -> dict:
-    """torchrun-style env contract (empty dict when not launched by a spawner)."""
+    """torchrun-style env contract (empty dict when not launched by a spawner).  Under SLURM
+    (``srun python -m mxddp.train ...``, one task per GPU) the rank layout comes from
+    SLURM_PROCID / SLURM_NTASKS / SLURM_LOCALID / SLURM_NTASKS_PER_NODE, and the rendezvous
+    host from MASTER_ADDR or SLURM_LAUNCH_NODE_IPADDR (the reference claims SLURM support but
+    ships none: README.md:11)."""
     if "RANK" in os.environ and "WORLD_SIZE" in os.environ:
         return {
             "rank": int(os.environ["RANK"]),
             "world_size": int(os.environ["WORLD_SIZE"]),
             "local_rank": int(os.environ.get("LOCAL_RANK", os.environ["RANK"])),
             "local_world_size": int(os.environ.get("LOCAL_WORLD_SIZE", os.environ["WORLD_SIZE"])),
+        }
+    if "SLURM_PROCID" in os.environ and "SLURM_NTASKS" in os.environ:
+        ws = int(os.environ["SLURM_NTASKS"])
+        per_node = os.environ.get("SLURM_NTASKS_PER_NODE", str(ws)).split("(")[0].split(",")[0]
+        if "MASTER_ADDR" not in os.environ and "SLURM_LAUNCH_NODE_IPADDR" in os.environ:
+            os.environ["MASTER_ADDR"] = os.environ["SLURM_LAUNCH_NODE_IPADDR"]
+        os.environ.setdefault("MASTER_PORT", str(29500 + int(os.environ.get("SLURM_JOB_ID", "0")) % 1000))
+        return {
+            "rank": int(os.environ["SLURM_PROCID"]),
+            "world_size": ws,
+            "local_rank": int(os.environ.get("SLURM_LOCALID", "0")),
+            "local_world_size": int(per_node) if per_node.isdigit() else ws,
         }
     return {}
 

@@ -51,6 +51,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--dist-backend", default="nccl", type=str, help="nccl (= RCCL on MI355X) or gloo")
     p.add_argument("--rank", default=0, type=int)
     p.add_argument("--world-size", default=1, type=int)
+    p.add_argument("--rdzv-timeout", type=float, default=float(os.environ.get("MXDDP_RDZV_TIMEOUT", "1800")),
+                   help="seconds a rank waits for the others at rendezvous / collectives (control plane)")
     # ---- mxddp extensions
     p.add_argument("--model", default="pyramidnet110",
                    help="mnist_cnn | keras_cnn | mlp | pyramidnet110 | resnet50 (default: the reference's model)")
@@ -169,7 +171,7 @@ def main(argv=None) -> int:
     use_gpu = torch.cuda.is_available() and not args.cpu
     backend = args.dist_backend if use_gpu else "gloo"
     inf = C.init_distributed(backend=backend, init_method=args.init_method, rank=args.rank,
-                             world_size=args.world_size, use_gpu=use_gpu)
+                             world_size=args.world_size, use_gpu=use_gpu, timeout_s=args.rdzv_timeout)
     from .models import get_spec
     from .utils.seed import seed_everything
 

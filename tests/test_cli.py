@@ -106,3 +106,22 @@ def test_training_state_roundtrip(tmp_path):
     st = load_training_state(p)  # weights_only=True inside
     assert st["epoch"] == 2 and st["step"] == 100 and st["scheduler"]["last_epoch"] == 2
     assert torch.equal(st["optimizer"]["momentum_buffer"], torch.ones(3))
+
+
+def test_slurm_env_contract(monkeypatch):
+    """srun-launched ranks (no torchrun env): rank layout from SLURM_* variables."""
+    from mxddp.parallel import comm
+
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("SLURM_PROCID", "11")
+    monkeypatch.setenv("SLURM_NTASKS", "16")
+    monkeypatch.setenv("SLURM_LOCALID", "3")
+    monkeypatch.setenv("SLURM_NTASKS_PER_NODE", "8(x2)")
+    monkeypatch.setenv("SLURM_LAUNCH_NODE_IPADDR", "10.0.0.7")
+    monkeypatch.setenv("SLURM_JOB_ID", "4242")
+    e = comm.env_dist()
+    assert e == {"rank": 11, "world_size": 16, "local_rank": 3, "local_world_size": 8}
+    import os
+
+    assert os.environ["MASTER_ADDR"] == "10.0.0.7" and os.environ["MASTER_PORT"] == str(29500 + 242)
