@@ -112,7 +112,7 @@ def test_slurm_env_contract(monkeypatch):
     """srun-launched ranks (no torchrun env): rank layout from SLURM_* variables."""
     from mxddp.parallel import comm
 
-    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR"):
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("SLURM_PROCID", "11")
     monkeypatch.setenv("SLURM_NTASKS", "16")
