@@ -303,6 +303,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_blocks", &PeerComm::set_blocks)
       .def("set_fence", &PeerComm::set_fence)
       .def("set_timeout_ms", &PeerComm::set_timeout_ms)
+      .def("set_oneshot_bytes", &PeerComm::set_oneshot_bytes)
+      .def_property_readonly("oneshot_bytes", &PeerComm::oneshot_bytes)
       .def_property_readonly("blocks", &PeerComm::blocks)
       .def_property_readonly("fence", &PeerComm::fence)
       .def_property_readonly("rank", &PeerComm::rank)

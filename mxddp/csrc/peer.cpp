@@ -65,6 +65,7 @@ PeerComm::PeerComm(int rank, int world_size, int device, size_t cap_bytes, int b
   MX_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0));
   if (const char* t = std::getenv("MXDDP_PEER_TIMEOUT_MS")) set_timeout_ms(std::atof(t));
   else timeout_ = 3000000000ll;  // 30 s: a slow rank (checkpoint, evaluation) is not an error
+  if (const char* o = std::getenv("MXDDP_PEER_ONESHOT_BYTES")) oneshot_bytes_ = std::atoll(o);
   MX_HIP_CHECK(hipDeviceSynchronize());
   peer_x_[rank_] = xbuf_;
   peer_sig_[rank_] = sig_;
@@ -163,7 +164,7 @@ void PeerComm::all_reduce(void* data, size_t count, DType t, hipStream_t st, Red
   for (size_t off = 0; off < count; off += per) {
     a.data = static_cast<char*>(data) + off * esz;
     a.count = static_cast<long long>(count - off < per ? count - off : per);
-    peer_all_reduce_launch(a, t, blocks_, st);
+    peer_all_reduce_launch(a, t, blocks_, st, oneshot_bytes_);
   }
 }
 

@@ -13,7 +13,10 @@
 //                 every peer's gather slot r;
 //   3. gather   : rank r copies the other W-1 reduced chunks from its gather slots.
 //
-// Each link carries 2 * S / W bytes per bucket (S = bucket bytes).  Synchronisation is per
+// Each link carries 2 * S / W bytes per bucket (S = bucket bytes).  Buckets up to 256 KB take a
+// one-shot kernel instead (every rank pushes its whole bucket to every peer, one flag round, each
+// rank sums all W copies in rank order): S bytes per link, but one synchronisation round
+// fewer, which is what a small all-reduce costs.  Synchronisation is per
 // workgroup: block b of rank r only waits for block b of the peers (flags, no grid barrier).
 // The exchange buffers and flags live in UNCACHED device memory (hipDeviceMallocUncached)
 // shared between the processes through HIP IPC handles: remote stores land in the owner's
@@ -81,6 +84,9 @@ class PeerComm {
   void set_blocks(int b);
   void set_fence(int f) { fence_ = f; }
   void set_timeout_ms(double ms) { timeout_ = static_cast<long long>(ms * 1e5); }
+  // buckets up to this size take the one-shot kernel (every rank must use the same value)
+  void set_oneshot_bytes(long long b) { oneshot_bytes_ = b; }
+  long long oneshot_bytes() const { return oneshot_bytes_; }
   int blocks() const { return blocks_; }
   int fence() const { return fence_; }
   int rank() const { return rank_; }
@@ -102,9 +108,12 @@ class PeerComm {
   bool opened_ = false, local_ = false;
   int fence_ = 1;
   long long timeout_ = 3000000000ll;  // 30 s
+  long long oneshot_bytes_ = 256 << 10;
   std::string mem_kind_;
 };
 
-void peer_all_reduce_launch(const PeerArgs& a, DType t, int blocks, hipStream_t st);
+// buckets of at most `oneshot_bytes` use the one-shot kernel (one flag round), larger ones the
+// two-shot kernel
+void peer_all_reduce_launch(const PeerArgs& a, DType t, int blocks, hipStream_t st, long long oneshot_bytes);
 
 }  // namespace mx

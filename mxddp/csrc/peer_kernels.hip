@@ -242,6 +242,72 @@ __global__ __launch_bounds__(kThreads) void peer_all_reduce_kernel(PeerArgs a, P
   if (t == 0) a.epoch[b] = ep;
 }
 
+// One-shot variant for small buckets (the MNIST conv bucket is 75 KB): every rank pushes its
+// WHOLE slice b to every peer's scatter slot r, ONE flag round, then each rank sums all W slots
+// in rank order locally -- the same operands in the same order everywhere, so every rank ends
+// with identical values.  Each link carries S bytes instead of 2 S / W, but one synchronisation
+// round is saved, which is what a small all-reduce costs.  Same slots / flags / parity as the
+// two-shot kernel (only flag set 0), so the two may alternate freely call by call.
+template <class T, int W>
+__global__ __launch_bounds__(kThreads) void peer_all_reduce_oneshot_kernel(PeerArgs a, long long slice) {
+  constexpr int V = Vec<T>::N;
+  const int b = blockIdx.x, r = a.rank, t = threadIdx.x;
+  __shared__ uint32_t s_ep;
+  if (t == 0) s_ep = a.epoch[b] + 1;
+  __syncthreads();
+  const uint32_t ep = s_ep;
+  const long long slot = a.slot_bytes / (long long)sizeof(T);
+  const long long half = (long long)(ep & 1u) * 2 * W * slot;
+  const long long lo = (long long)b * slice;
+  const long long rem = a.count - lo;
+  const long long n = rem < 0 ? 0 : (rem < slice ? rem : slice);
+  T* mine = static_cast<T*>(a.data) + lo;
+  T* dst[W];
+#pragma unroll
+  for (int j = 1; j < W; ++j) dst[j] = reinterpret_cast<T*>(a.xbuf[(r + j) % W]) + half + (long long)r * slot + lo;
+  // 1. push: one load, W-1 remote stores per 16-byte vector
+  for (long long i = t; i < n / V; i += kThreads) {
+    const u32x4 v = reinterpret_cast<const u32x4*>(mine)[i];
+#pragma unroll
+    for (int j = 1; j < W; ++j) reinterpret_cast<u32x4*>(dst[j])[i] = v;
+  }
+  for (long long i = n / V * V + t; i < n; i += kThreads) {
+    const T v = mine[i];
+#pragma unroll
+    for (int j = 1; j < W; ++j) dst[j][i] = v;
+  }
+  signal_peers(a, 0, b, ep);
+  wait_peers(a, 0, b, ep);
+  // 2. sum the W contributions in rank order 0..W-1
+  const T* scat = reinterpret_cast<const T*>(a.xbuf[r]) + half + lo;
+  for (long long i = t; i < n / V; i += kThreads) {
+    u32x4 v[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p)
+      v[p] = p == r ? reinterpret_cast<const u32x4*>(mine)[i]
+                    : __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(scat + (long long)p * slot) + i);
+    float acc[V];
+#pragma unroll
+    for (int p = 0; p < W; ++p) acc16<T>(acc, v[p], p == 0);
+    if (a.scale != 1.f) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] *= a.scale;
+    }
+    reinterpret_cast<u32x4*>(mine)[i] = pack16<T>(acc);
+  }
+  for (long long i = n / V * V + t; i < n; i += kThreads) {
+    float acc = 0.f;
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      const float v = p == r ? ld_elem<T>(mine + i, false) : ld_elem<T>(scat + (long long)p * slot + i, true);
+      acc = p == 0 ? v : acc + v;
+    }
+    if (a.scale != 1.f) acc *= a.scale;
+    st_elem<T>(mine + i, acc);
+  }
+  if (t == 0) a.epoch[b] = ep;
+}
+
 }  // namespace
 
 PeerPartition PeerPartition::make(long long count, int ws, int blocks, int vec) {
@@ -251,17 +317,23 @@ PeerPartition PeerPartition::make(long long count, int ws, int blocks, int vec) 
   return p;
 }
 
-void peer_all_reduce_launch(const PeerArgs& a, DType t, int blocks, hipStream_t st) {
+void peer_all_reduce_launch(const PeerArgs& a, DType t, int blocks, hipStream_t st, long long oneshot_bytes) {
   const int esz = static_cast<int>(dtype_size(t));
-  const PeerPartition part = PeerPartition::make(a.count, a.ws, blocks, 16 / esz);
+  const int vec = 16 / esz;
+  const PeerPartition part = PeerPartition::make(a.count, a.ws, blocks, vec);
   MX_CHECK(part.chunk * esz <= a.slot_bytes, "peer all-reduce: bucket larger than the exchange slot");
   MX_CHECK(reinterpret_cast<uintptr_t>(a.data) % 16 == 0, "peer all-reduce: data must be 16-byte aligned");
   MX_CHECK(t == DType::kF32 || t == DType::kBF16, "peer all-reduce: f32 or bf16 only");
   const bool f = t == DType::kF32;
-#define MX_PEER_CASE(NW)                                                                                 \
-  case NW:                                                                                               \
-    if (f) MX_LAUNCH((peer_all_reduce_kernel<float, NW>), dim3(blocks), dim3(kThreads), 0, st, a, part); \
-    else MX_LAUNCH((peer_all_reduce_kernel<uint16_t, NW>), dim3(blocks), dim3(kThreads), 0, st, a, part); \
+  // every rank makes the same choice (a function of the count only)
+  const bool one = a.count * esz <= oneshot_bytes && a.count * esz <= a.slot_bytes;
+  const long long slice = ((a.count + blocks - 1) / blocks + vec - 1) / vec * vec;
+#define MX_PEER_CASE(NW)                                                                                    \
+  case NW:                                                                                                  \
+    if (one && f) MX_LAUNCH((peer_all_reduce_oneshot_kernel<float, NW>), dim3(blocks), dim3(kThreads), 0, st, a, slice); \
+    else if (one) MX_LAUNCH((peer_all_reduce_oneshot_kernel<uint16_t, NW>), dim3(blocks), dim3(kThreads), 0, st, a, slice); \
+    else if (f) MX_LAUNCH((peer_all_reduce_kernel<float, NW>), dim3(blocks), dim3(kThreads), 0, st, a, part); \
+    else MX_LAUNCH((peer_all_reduce_kernel<uint16_t, NW>), dim3(blocks), dim3(kThreads), 0, st, a, part);    \
     break;
   switch (a.ws) {
     MX_PEER_CASE(2)

@@ -40,13 +40,14 @@ def worker(rank, ws, port, a, q):
         dist.broadcast_object_list(uid, 0)
         rccl = C.Comm(uid[0], rank, ws, dev)
     res = {}
-    for blocks in a.blocks:
-        for fence in a.fences:
+    for blocks, fence, one in [(b_, f_, o_) for b_ in a.blocks for f_ in a.fences for o_ in a.oneshot]:
+        if True:
             pc = C.PeerComm(rank, ws, dev, 64 << 20, blocks)
             allh = [None] * ws
             dist.all_gather_object(allh, pc.handles())
             pc.open(allh)
             pc.set_fence(fence)
+            pc.set_oneshot_bytes(one)
             st = torch.cuda.current_stream().cuda_stream
             for n in a.sizes:
                 x = torch.randn(n, device="cuda")
@@ -61,7 +62,7 @@ def worker(rank, ws, port, a, q):
                 dt = (time.perf_counter() - t0) / a.iters * 1e6
                 t = torch.tensor([dt], dtype=torch.float64)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                res[f"peer b={blocks} fence={fence} n={n}"] = round(float(t), 2)
+                res[f"peer b={blocks} fence={fence} oneshot<={one} n={n}"] = round(float(t), 2)
             if pc.error():
                 res["peer_error"] = pc.error()
             dist.barrier()
@@ -94,6 +95,8 @@ def main():
     ap.add_argument("--sizes", type=lambda s: [int(v) for v in s.split(",")], default=[18816, 1181066, 6553600])
     ap.add_argument("--blocks", type=lambda s: [int(v) for v in s.split(",")], default=[64])
     ap.add_argument("--fences", type=lambda s: [int(v) for v in s.split(",")], default=[3])
+    ap.add_argument("--oneshot", type=lambda s: [int(v) for v in s.split(",")], default=[262144],
+                    help="one-shot kernel threshold(s) in bytes (0 = always two-shot)")
     ap.add_argument("--iters", type=int, default=50)
     a = ap.parse_args()
     ctx = mp.get_context("spawn")
