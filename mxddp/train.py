@@ -71,6 +71,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--debug-sync", action="store_true",
                    help="synchronise and check for faults after every kernel launch (implies --no-graph)")
     p.add_argument("--bucket-cap-mb", type=float, default=25.0)
+    p.add_argument("--transport", default="auto", choices=["auto", "rccl", "peer"],
+                   help="gradient all-reduce: RCCL ring, direct xGMI peer all-reduce, or auto (validated + timed)")
     p.add_argument("--resume", type=str, default="", help="training-state file (mxddp_state_<rank>.pt) to resume")
     p.add_argument("--save-every", type=int, default=0, help="write the full training state every N epochs")
     p.add_argument("--eval", action="store_true", help="evaluate on the test split after training")
@@ -316,7 +318,7 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
     torch.manual_seed(args.seed)
     model = build_model(spec.name, **_model_kwargs(args, spec)).to(dev)
     if mode == "ddp":
-        net = DDP(model, bucket_cap_mb=args.bucket_cap_mb)
+        net = DDP(model, bucket_cap_mb=args.bucket_cap_mb, transport=args.transport if dev.type == "cuda" else "auto")
         flat = net.flat
     else:
         net, flat = model, FlatParams(model, dev)
@@ -545,8 +547,17 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
         st = load_training_state(args.resume)
         init.load_state_dict(st["model"])
         start_epoch = st["epoch"] + 1
-    tr = FusedMnistTrainer(batch=bs, device=dev, comm=C.rccl_comm(), seed=args.seed, lr=lr, momentum=mom,
-                           weight_decay=wd, use_graph=not args.no_graph, init_model=init)
+    comm = C.rccl_comm()
+    peer = None
+    if comm is None and inf.world_size > 1:  # ranks share a GPU: no RCCL, the peer transport carries the DDP
+        from .parallel import peer as _peer
+
+        peer = _peer.peer_comm()
+        if peer is None:
+            raise SystemExit("ranks share a GPU and the peer transport is unavailable")
+    tr = FusedMnistTrainer(batch=bs, device=dev, comm=comm, seed=args.seed, lr=lr, momentum=mom,
+                           weight_decay=wd, use_graph=not args.no_graph, init_model=init, transport=args.transport,
+                           peer=peer)
     if args.resume and "momentum" in st.get("optimizer", {}):
         tr.mom.copy_(st["optimizer"]["momentum"].to(dev))
     loader, kind = build_loader("mnist", args.data, args.dataset_dir, bs, dev, inf.world_size, inf.rank, args.seed,
@@ -568,6 +579,14 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
         rep.first_loss(_ops.cross_entropy(probe(torch.zeros(2, 1, 28, 28)), torch.zeros(2, dtype=torch.long)), probe)
     step = 0
     base_lr = lr
+    if tr.eng.reducer_active and synthetic and not args.no_graph:
+        # pick transport / overlap / graph mode on this machine (a few real training steps, counted)
+        tr.step(1)
+        tr.autotune()
+        tr.read_metrics(reset=True)
+        step = tr.steps
+        if inf.is_main:
+            print(f"==> DDP step strategy: {tr.tuned}", flush=True)
     for epoch in range(start_epoch, args.epochs + 1):
         if args.lr_step_size:
             tr.set_lr(base_lr * args.lr_gamma ** ((epoch - 1) // args.lr_step_size))
