@@ -124,7 +124,9 @@ def translate(script: str, argv: list[str]) -> list[str]:
                "-tb", str(a.test_batchsize), "-e", str(a.epochs), "--log-interval", str(a.log_interval),
                "--save-every", "1", "--eval", "--eval-every", "1", "--lr-step-size", "0",  # fit(validation_data)
                # TensorBoard(log_dir=train_dir, histogram_freq=1) + model.summary()
-               "--tensorboard-dir", a.train_dir, "--histogram-freq", "1", "--summary"]
+               "--tensorboard-dir", a.train_dir, "--histogram-freq", "1", "--summary",
+               # ModelCheckpoint(ckpt_{epoch}, weights only) + load latest before evaluate
+               "--epoch-checkpoints"]
         if a.learning_rate is not None:
             out += ["--lr", str(a.learning_rate)]
         if multi:

@@ -89,6 +89,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--chainer-out", type=str, default="",
                    help="Chainer trainer extensions: LogReport (<dir>/log), PrintReport, dump_graph (<dir>/cg.dot)")
     p.add_argument("--summary", action="store_true", help="print a Keras-style model summary")
+    p.add_argument("--epoch-checkpoints", action="store_true",
+                   help="Keras ModelCheckpoint: weights-only <train-dir>/ckpt_<epoch>.pth every epoch (rank 0); "
+                        "with --eval the final evaluation reloads the latest one first")
     return p
 
 
@@ -291,6 +294,23 @@ def _maybe_eval(args, inf, spec, model, bs, mw, epoch=None, force=False):
     return loss, acc
 
 
+def _reload_latest(args, inf, model):
+    """tensorflow2/mnist_single.py:88-92: reload the latest epoch checkpoint before evaluating."""
+    from .parallel import comm as C
+    from .utils.checkpoint import latest_checkpoint
+
+    C.barrier()  # rank 0 wrote it
+    path = latest_checkpoint(args.train_dir)
+    if path is None:
+        return
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    with torch.no_grad():
+        for k, v in model.state_dict().items():
+            v.copy_(sd[k].to(v.device))
+    if inf.is_main:
+        print(f"==> restored {os.path.basename(path)} for evaluation", flush=True)
+
+
 def _save_final(args, inf, mode, state_dict):
     if not args.save_model:
         return
@@ -388,8 +408,14 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
         if args.save_every and epoch % args.save_every == 0:
             save_training_state(args.train_dir, inf.rank, model.state_dict(), opt.state_dict(),
                                 sched.state_dict() if sched else None, epoch, step)
+        if args.epoch_checkpoints and inf.is_main:
+            from .utils.checkpoint import save_epoch_weights
+
+            save_epoch_weights(model.state_dict(), args.train_dir, epoch)
         if args.max_steps and step >= args.max_steps:
             break
+    if args.epoch_checkpoints and args.eval:
+        _reload_latest(args, inf, model)
     _maybe_eval(args, inf, spec, model, bs, mw, force=True)
     rep.close()
     _save_final(args, inf, mode, model.state_dict())

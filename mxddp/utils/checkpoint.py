@@ -79,3 +79,25 @@ def save_training_state(train_dir: str, rank: int, model_sd: dict, opt_sd: dict 
 
 def load_training_state(path: str) -> dict:
     return torch.load(path, map_location="cpu", weights_only=True)
+
+
+# ----------------------------------------------------------------------------- Keras ModelCheckpoint
+# tensorflow2/mnist_single.py:67-76: ModelCheckpoint(filepath=train_dir/ckpt_{epoch},
+# save_weights_only=True) every epoch, then load_weights(tf.train.latest_checkpoint(train_dir))
+# and evaluate (:88-92).
+def save_epoch_weights(model_sd: dict, train_dir: str, epoch: int) -> str:
+    os.makedirs(train_dir, exist_ok=True)
+    path = os.path.join(train_dir, f"ckpt_{epoch}.pth")
+    _atomic_save(_cpu(model_sd), path)
+    return path
+
+
+def latest_checkpoint(train_dir: str) -> str | None:
+    """Path of the highest-epoch ``ckpt_{epoch}.pth`` in train_dir (None if there is none)."""
+    best, best_ep = None, -1
+    if not os.path.isdir(train_dir):
+        return None
+    for f in os.listdir(train_dir):
+        if f.startswith("ckpt_") and f.endswith(".pth") and f[5:-4].isdigit() and int(f[5:-4]) > best_ep:
+            best, best_ep = os.path.join(train_dir, f), int(f[5:-4])
+    return best

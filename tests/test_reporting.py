@@ -86,6 +86,9 @@ def test_tf2_script_writes_tensorboard_and_summary(tmp_path):
     ev = tensorboard.read_events(str(tmp_path / "td" / files[0]))
     tags = {v["tag"] for e in ev for v in e["values"]}
     assert {"epoch_loss", "epoch_accuracy", "epoch_val_loss", "conv1.weight"} <= tags
+    assert (tmp_path / "td" / "ckpt_1.pth").exists() and "restored ckpt_1.pth" in out
+    sd = torch.load(tmp_path / "td" / "ckpt_1.pth", weights_only=True)
+    assert sum(v.numel() for v in sd.values()) == 93_322
 
 
 def test_chainer_script_writes_log_report_and_graph(tmp_path):
