@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--lr", type=float, default=0.01, help="SGD lr (momentum 0.9, wd 1e-4 as the reference)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
                     help="GEMM precision of the layers path (headline is fp32, >= the reference's precision)")
+    ap.add_argument("--cpu", action="store_true",
+                    help="BASELINE config 1: single process on the CPU (the reference's single_gpu.py CPU fallback)")
     ap.add_argument("--model", default="mnist_cnn",
                     help="headline: mnist_cnn (fused).  Others run the layers path: keras_cnn, mlp, pyramidnet110, resnet50")
     return ap.parse_args()
@@ -78,6 +80,8 @@ def main():
     from mxddp.parallel import comm as C
 
     ws_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.cpu:
+        return _cpu(a)
     if a.impl == "replica":
         if ws_env != 1:
             print("bench.py: --impl replica is single-process (do not launch it with torchrun)", file=sys.stderr)
@@ -261,6 +265,52 @@ def _replica_fused(a, devices, spec):
                    "image": "x".join(map(str, spec.input_shape)), "parallelism": f"replica{a.gpus}",
                    "impl": "replica-fused", "transport": "peer (in-process)" if len(devices) > 1 else "none",
                    "graph": True}}), flush=True)
+
+
+def _cpu(a):
+    """BASELINE config 1: the MNIST CNN (or --model) trained by ONE process on the CPU --
+    mxddp's CPU op path (PyTorch math, the same functions the GPU kernels are tested against),
+    flat SGD, synthetic class-conditional batches generated on the host."""
+    import torch
+
+    from mxddp import ops
+    from mxddp.models import build_model, get_spec
+    from mxddp.optim import SGD
+    from mxddp.parallel.flat import FlatParams
+
+    torch.manual_seed(a.seed)
+    spec = get_spec(a.model)
+    model = build_model(a.model)
+    flat = FlatParams(model, torch.device("cpu"))
+    opt = SGD(flat, lr=a.lr, momentum=0.9, weight_decay=1e-4)
+    g = torch.Generator().manual_seed(a.seed)
+    tmpl = torch.rand((spec.num_classes,) + tuple(spec.input_shape), generator=g)
+    B = a.batch
+
+    def batch():
+        y = torch.randint(0, spec.num_classes, (B,), generator=g)
+        return (tmpl[y] + 0.3 * torch.randn((B,) + tuple(spec.input_shape), generator=g)).clamp_(0, 1), y
+
+    def run(n):
+        for _ in range(n):
+            x, y = batch()
+            opt.zero_grad()
+            ops.cross_entropy(model(x), y).backward()
+            opt.step()
+
+    run(a.warmup)
+    t0 = time.perf_counter()
+    run(a.steps)
+    dt = time.perf_counter() - t0
+    value = B * a.steps / dt
+    print(json.dumps({
+        "metric": _metric(a.model) + " [CPU, single process]", "value": round(value, 1), "unit": "images/sec",
+        "n_gpus": 0, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (host class-conditional, random-init weights)",
+        "config": {"model": a.model, "global_batch": B, "per_rank_batch": B, "seq_len": None,
+                   "image": "x".join(map(str, spec.input_shape)), "parallelism": "cpu1", "impl": "cpu",
+                   "threads": torch.get_num_threads()}}), flush=True)
 
 
 def _data_desc(spec):
