@@ -99,3 +99,27 @@ def test_model_forward_backward_vs_torch(cuda, name):
     assert rel < max(2e-3, 3 * rel_torch), (rel, rel_torch)
     cos = torch.nn.functional.cosine_similarity(got, ref, dim=0).item()
     assert cos > 0.9995, cos
+
+
+@pytest.mark.parametrize("model,extra", [("mnist_cnn", ["--per-rank-batch", "64"]),
+                                         ("keras_cnn", ["--per-rank-batch", "32"])])
+def test_train_cli_two_ranks_share_gpu(cuda, tmp_path, model, extra):
+    """The reference DDP launch (one process per rank, reference flags) with two ranks on the one
+    GPU: RCCL cannot span them, so the DDP gradient exchange is the peer transport -- the fused
+    MNIST engine (autotuned step) and the layers-path bucket reducer (keras_cnn).  Both ranks'
+    reference-layout checkpoints must be identical."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    cmd = [sys.executable, "-m", "mxddp.train", "--model", model, "--nproc-per-node", "2", "-e", "1",
+           "--steps-per-epoch", "20", "--log-interval", "10", "-td", str(tmp_path), "-sm"] + extra
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    a = torch.load(tmp_path / "distributed_data_parallel_0.pth", weights_only=True)
+    b = torch.load(tmp_path / "distributed_data_parallel_1.pth", weights_only=True)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    assert "From Rank: 1, Training time" in p.stdout
