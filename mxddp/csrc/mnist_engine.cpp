@@ -96,6 +96,10 @@ void MnistEngine::uncapture() {
   if (graph_) hipGraphDestroy(graph_);
   exec_ = nullptr;
   graph_ = nullptr;
+  for (auto& e : rem_exec_) hipGraphExecDestroy(e.second);
+  for (auto g : rem_graph_) hipGraphDestroy(g);
+  rem_exec_.clear();
+  rem_graph_.clear();
   for (int k = 0; k < 3; ++k) {
     if (seg_exec_[k]) hipGraphExecDestroy(seg_exec_[k]);
     if (seg_graph_[k]) hipGraphDestroy(seg_graph_[k]);
@@ -234,6 +238,16 @@ void MnistEngine::capture(int mode, int steps_per_graph) {
     exec_ = capture_fn([this] {
       for (int i = 0; i < steps_per_graph_; ++i) launch_step();
     }, &graph_);
+    int k = 1;
+    while (2 * k < steps_per_graph_) k *= 2;
+    for (; k >= 1 && steps_per_graph_ > 1; k /= 2) {
+      hipGraph_t g = nullptr;
+      hipGraphExec_t e = capture_fn([this, k] {
+        for (int i = 0; i < k; ++i) launch_step();
+      }, &g);
+      rem_graph_.push_back(g);
+      rem_exec_.emplace_back(k, e);
+    }
   } else if (mode == 2) {  // three compute graphs; the two collectives are issued eagerly between them
     for (int k = 0; k < 3; ++k) seg_exec_[k] = capture_fn([this, k] { segment(k); }, &seg_graph_[k]);
   }
@@ -242,7 +256,12 @@ void MnistEngine::capture(int mode, int steps_per_graph) {
 void MnistEngine::replay(int n) {
   if (graph_mode_ == 1 && exec_ && steps_per_graph_ > 1) {
     for (; n >= steps_per_graph_; n -= steps_per_graph_) MX_HIP_CHECK(hipGraphLaunch(exec_, s_));
-    for (; n > 0; --n) launch_step();  // remainder: same kernels, launched eagerly
+    for (const auto& e : rem_exec_)  // remainder from the 2^k-step graphs, largest first
+      if (n >= e.first) {
+        MX_HIP_CHECK(hipGraphLaunch(e.second, s_));
+        n -= e.first;
+      }
+    for (; n > 0; --n) launch_step();
     return;
   }
   for (int i = 0; i < n; ++i) {

@@ -17,6 +17,8 @@
 
 #include <functional>
 #include <memory>
+#include <utility>
+#include <vector>
 
 #include "comm.h"
 #include "mnist_kernels.h"
@@ -110,6 +112,11 @@ class MnistEngine {
   hipStream_t s_ = nullptr;
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t exec_ = nullptr;
+  // mode 1, steps_per_graph > 1: graphs of 2^k < steps_per_graph steps for the remainder of a
+  // replay(n) (largest first), so a step count that is not a multiple of the group size still
+  // runs entirely from graphs
+  std::vector<std::pair<int, hipGraphExec_t>> rem_exec_;
+  std::vector<hipGraph_t> rem_graph_;
 };
 
 }  // namespace mx

@@ -102,13 +102,15 @@ def test_fused_engine_rccl_collectives_ws1(cuda, graph):
 
 
 def test_fused_engine_multi_step_graph(cuda):
-    """8 steps unrolled per graph == 8 single steps (same device-side data stream)."""
+    """8 steps unrolled per graph (+ 4/2/1-step remainder graphs) == single steps (same
+    device-side data stream)."""
     from mxddp.engine import FusedMnistTrainer
 
     a = FusedMnistTrainer(batch=64, device=cuda, lr=0.01, steps_per_graph=8)
     b = FusedMnistTrainer(batch=64, device=cuda, lr=0.01, steps_per_graph=1)
-    a.step(17)
-    b.step(17)
+    for n in (1, 13, 3, 7):  # remainders run from the 4 / 2 / 1-step graphs
+        a.step(n)
+        b.step(n)
     la, ca = a.read_metrics()
     lb, cb = b.read_metrics()
     assert abs(la - lb) < 1e-3 * abs(lb) and ca == cb
