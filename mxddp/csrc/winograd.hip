@@ -222,13 +222,18 @@ __device__ __forceinline__ unsigned window_mask(int h0, int w0) {
 
 // Block: 32 output channels x 32 output tiles; wave (wm, wn) owns 16 x 16 of it for all 16 xi
 // (16 accumulators = 64 registers) -> ~120 VGPRs, 3 blocks (12 waves) per CU.
-template <int W, int kOcc>
-__global__ __launch_bounds__(256, kOcc) void wino_fwd_kernel(WinoArgs a) {
+// KS = 2 (small images, where 32 x 32 blocks leave ~1 wave per SIMD): 8 waves per block in two
+// K groups; group k handles the chunks of parity k with its own U / V buffers, so every barrier
+// interval carries twice the MFMAs per SIMD, and the groups' partial outputs are summed through
+// LDS after the output transform (deterministic, no atomics).
+template <int W, int kOcc, int KS = 1>
+__global__ __launch_bounds__(256 * KS, kOcc) void wino_fwd_kernel(WinoArgs a) {
   constexpr int TW = W / 2, TPI = TW * TW, HW = W * W;
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* As = sm;                   // U slice [16][8 ci][kP] (32 co)
-  float* Bs = sm + 16 * kCC * kP;   // V slice [16][8 ci][kP] (32 tiles)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int grp = KS > 1 ? (int)(threadIdx.x >> 8) : 0;
+  float* As = sm + grp * (2 * 16 * kCC * kP);  // U slice [16][8 ci][kP] (32 co) of this K group
+  float* Bs = As + 16 * kCC * kP;              // V slice [16][8 ci][kP] (32 tiles)
+  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
   const int g = lane >> 4, l16 = lane & 15;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int kt = bid % a.ktiles, r1 = bid / a.ktiles;
@@ -279,16 +284,53 @@ __global__ __launch_bounds__(256, kOcc) void wino_fwd_kernel(WinoArgs a) {
 
   const float* ap = As + g * kP + 16 * wm + l16;
   const float* bp = Bs + g * kP + 16 * wn + l16;
-  if (ch_beg < ch_end) gload(ch_beg);
-  for (int ch = ch_beg; ch < ch_end; ++ch) {
-    if (ch != ch_beg) __syncthreads();  // previous chunk's LDS reads are done
-    sstore();
+  // K group grp takes chunks ch_beg + grp, + KS, ...; every group runs the same number of
+  // iterations (barriers are block-wide), a group past the end just waits them out
+  const int npass = (ch_end - ch_beg + KS - 1) / KS;
+  if (ch_beg + grp < ch_end) gload(ch_beg + grp);
+  for (int it = 0; it < npass; ++it) {
+    const int ch = ch_beg + it * KS + grp;
+    if (it != 0) __syncthreads();  // previous chunk's LDS reads are done
+    if (ch < ch_end) sstore();
     __syncthreads();
-    if (ch + 1 < ch_end) gload(ch + 1);
-    mfma_chunk<true>(ap, bp, acc);
+    if (ch + KS < ch_end) gload(ch + KS);
+    if (ch < ch_end) mfma_chunk<true>(ap, bp, acc);
   }
 
   // epilogue: row = output channel, column = output tile; Y = A^T M A, A^T = [[1,1,1,0],[0,1,-1,-1]]
+  float yt[4][2][2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float t0[4], t1[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      t0[c] = acc[0 + c][r] + acc[4 + c][r] + acc[8 + c][r];
+      t1[c] = acc[4 + c][r] - acc[8 + c][r] - acc[12 + c][r];
+    }
+    yt[r][0][0] = t0[0] + t0[1] + t0[2];
+    yt[r][0][1] = t0[1] - t0[2] - t0[3];
+    yt[r][1][0] = t1[0] + t1[1] + t1[2];
+    yt[r][1][1] = t1[1] - t1[2] - t1[3];
+  }
+  if constexpr (KS > 1) {  // group 1's partial outputs -> LDS -> added by group 0 (fixed order)
+    float* red = sm + (wave * 64 + lane) * 16;  // 16 KB, over group 0's (finished) U / V buffers
+    __syncthreads();
+    if (grp == 1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<float4*>(red + 4 * r) = make_float4(yt[r][0][0], yt[r][0][1], yt[r][1][0], yt[r][1][1]);
+    }
+    __syncthreads();
+    if (grp == 1) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float4 o = *reinterpret_cast<const float4*>(red + 4 * r);
+      yt[r][0][0] += o.x;
+      yt[r][0][1] += o.y;
+      yt[r][1][0] += o.z;
+      yt[r][1][1] += o.w;
+    }
+  }
   const int T = tb * 32 + 16 * wn + l16;
   if (T >= ntiles) return;
   const int n = T / TPI, rem = T - n * TPI, oh = 2 * (rem / TW), ow = 2 * (rem % TW);
@@ -296,14 +338,7 @@ __global__ __launch_bounds__(256, kOcc) void wino_fwd_kernel(WinoArgs a) {
   for (int r = 0; r < 4; ++r) {
     const int co = co0 + 16 * wm + 4 * g + r;
     if (co >= a.Co) continue;
-    float t0[4], t1[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      t0[c] = acc[0 + c][r] + acc[4 + c][r] + acc[8 + c][r];
-      t1[c] = acc[4 + c][r] - acc[8 + c][r] - acc[12 + c][r];
-    }
-    const float y[2][2] = {{t0[0] + t0[1] + t0[2], t0[1] - t0[2] - t0[3]},
-                           {t1[0] + t1[1] + t1[2], t1[1] - t1[2] - t1[3]}};
+    const float (&y)[2][2] = yt[r];
     const float bv = (a.bias && sp == 0) ? a.bias[co] : 0.f;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
@@ -708,13 +743,18 @@ void launch_fwd(const float* x, const float* w, const float* bias, const float* 
   a.Cop = Cop;
   // 3 = patch-staged 32 x 64 blocks (fastest on 32x32 images), 2 = per-window 32 x 32 blocks
   // (fastest on 16x16 / 8x8, where the larger block leaves too few blocks to fill the chip);
-  // measured per shape by scripts/bench_conv.py.  MXDDP_WINO_FWD=2|3 forces one.
+  // measured per shape by scripts/bench_conv.py.  MXDDP_WINO_FWD=2|3|4 forces one.
   static const int forced = [] {
     const char* e = std::getenv("MXDDP_WINO_FWD");
     return e ? std::atoi(e) : 0;
   }();
-  const int variant = forced ? forced : (Wd == 32 ? 3 : 2);
   const int tpi = (Wd / 2) * (Wd / 2);
+  // 4 = two K groups per 32 x 32 block: where the 32 x 32 grid fits in one wave of blocks (one
+  // block per CU, e.g. the 8x8 layers up to 256 channels), doubling the MFMAs per barrier
+  // interval wins (45 -> 39 us at C = 191, 57 -> 49 us at C = 231); with more blocks than CUs it
+  // loses (89 -> 99 us at C = 266: two waves of 98 KB-LDS blocks), as on 16x16 / 32x32
+  const int blocks32 = cdiv(N * tpi, 32) * (Cop / 32);
+  const int variant = forced ? forced : (Wd == 32 ? 3 : (blocks32 <= device_cu_count() ? 4 : 2));
   const int tile_blk = variant == 3 ? 64 : 32;
   a.tblocks = cdiv(N * tpi, tile_blk);
   a.ktiles = Cop / 32;
@@ -747,6 +787,23 @@ void launch_fwd(const float* x, const float* w, const float* bias, const float* 
       case 8: MX_LAUNCH(wino_fwd_patch_kernel<8>, grid, dim3(256), 0, st, a); break;
       case 16: MX_LAUNCH(wino_fwd_patch_kernel<16>, grid, dim3(256), 0, st, a); break;
       case 32: MX_LAUNCH(wino_fwd_patch_kernel<32>, grid, dim3(256), 0, st, a); break;
+      default: MX_CHECK(false, "winograd: unsupported width");
+    }
+    return;
+  }
+  if (variant == 4) {  // two K groups of 4 waves per block (see wino_fwd_kernel)
+    static bool attr = false;
+    if (!attr) {
+      for (const void* fn : {reinterpret_cast<const void*>(wino_fwd_kernel<8, 1, 2>),
+                             reinterpret_cast<const void*>(wino_fwd_kernel<16, 1, 2>),
+                             reinterpret_cast<const void*>(wino_fwd_kernel<32, 1, 2>)})
+        MX_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(2 * kLds)));
+      attr = true;
+    }
+    switch (Wd) {
+      case 8: MX_LAUNCH((wino_fwd_kernel<8, 1, 2>), grid, dim3(512), 2 * kLds, st, a); break;
+      case 16: MX_LAUNCH((wino_fwd_kernel<16, 1, 2>), grid, dim3(512), 2 * kLds, st, a); break;
+      case 32: MX_LAUNCH((wino_fwd_kernel<32, 1, 2>), grid, dim3(512), 2 * kLds, st, a); break;
       default: MX_CHECK(false, "winograd: unsupported width");
     }
     return;

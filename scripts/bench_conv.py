@@ -29,6 +29,8 @@ def timeit(fn, iters=30):
     return e0.elapsed_time(e1) / iters * 1e3  # us
 
 
+ONLY_WINO = "--only-wino" in sys.argv  # compare forward variants (MXDDP_WINO_FWD) quickly
+
 for (C, K, W) in SHAPES:
     x = torch.randn(N, C, W, W, device=dev)
     w = torch.randn(K, C, 3, 3, device=dev) * 0.05
@@ -38,7 +40,7 @@ for (C, K, W) in SHAPES:
     dw = torch.empty_like(w)
     geo = (N, C, W, W, K, 3, 3, 1, 1, 1, 1, 1, 1)
     res = {"C": C, "K": K, "W": W, "gflop_direct_each": round(2 * 9 * C * K * W * W * N / 1e9, 3)}
-    for algo, name in ((0, "wino"), (1, "direct")):
+    for algo, name in ((0, "wino"),) if ONLY_WINO else ((0, "wino"), (1, "direct")):
         C_.set_conv_algo(algo)
         scr = torch.empty(max(1, C_.conv_scratch_floats(*geo)), device=dev)
         ws = torch.empty(max(1, C_.conv_wgrad_scratch_floats(*geo)), device=dev)
@@ -46,6 +48,9 @@ for (C, K, W) in SHAPES:
         res[name + "_dgrad"] = round(timeit(lambda: C_.conv2d_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), *geo, 0, False, st, scr.data_ptr())), 1)
         res[name + "_wgrad"] = round(timeit(lambda: C_.conv2d_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), *geo, False, st, ws.data_ptr())), 1)
     C_.set_conv_algo(0)
+    if ONLY_WINO:
+        print(json.dumps(res), flush=True)
+        continue
     res["miopen_fwd"] = round(timeit(lambda: F.conv2d(x, w, None, 1, 1)), 1)
     res["miopen_dgrad"] = round(timeit(lambda: torch.nn.grad.conv2d_input(x.shape, w, dy, 1, 1)), 1)
     res["miopen_wgrad"] = round(timeit(lambda: torch.nn.grad.conv2d_weight(x, w.shape, dy, 1, 1)), 1)
