@@ -191,12 +191,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_splits", &bn_splits);
   m.def("bn_fwd_train", [](uintptr_t x, uintptr_t g, uintptr_t b, uintptr_t y, uintptr_t mean, uintptr_t invstd,
                            uintptr_t rm, uintptr_t rv, int N, int C, int HW, float mom, float eps, bool relu,
-                           uintptr_t part, uintptr_t st, uintptr_t nbt) {
+                           uintptr_t part, uintptr_t st, uintptr_t nbt, uintptr_t res, int res_C) {
     bn_fwd_train(P<const float>(x), P<const float>(g), P<const float>(b), P<float>(y), P<float>(mean), P<float>(invstd),
-                 P<float>(rm), P<float>(rv), N, C, HW, mom, eps, relu, P<float>(part), S(st), P<int64_t>(nbt));
+                 P<float>(rm), P<float>(rv), N, C, HW, mom, eps, relu, P<float>(part), S(st), P<int64_t>(nbt),
+                 P<const float>(res), res_C);
   }, py::arg("x"), py::arg("g"), py::arg("b"), py::arg("y"), py::arg("mean"), py::arg("invstd"), py::arg("rm"),
      py::arg("rv"), py::arg("N"), py::arg("C"), py::arg("HW"), py::arg("mom"), py::arg("eps"), py::arg("relu"),
-     py::arg("part"), py::arg("st"), py::arg("num_batches") = 0);
+     py::arg("part"), py::arg("st"), py::arg("num_batches") = 0, py::arg("residual") = 0, py::arg("residual_C") = 0);
   m.def("bn_partial_floats", &bn_partial_floats);
   m.def("bn_fwd_eval", [](uintptr_t x, uintptr_t g, uintptr_t b, uintptr_t y, uintptr_t rm, uintptr_t rv, int N, int C,
                           int HW, float eps, bool relu, uintptr_t st) {
@@ -205,10 +206,13 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("bn_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t yr, uintptr_t g, uintptr_t mean, uintptr_t invstd,
                      uintptr_t dx, uintptr_t dg, uintptr_t db, int N, int C, int HW, bool acc, uintptr_t part,
-                     uintptr_t st) {
+                     uintptr_t st, uintptr_t extra, int extra_C) {
     bn_bwd(P<const float>(dy), P<const float>(x), P<const float>(yr), P<const float>(g), P<const float>(mean),
-           P<const float>(invstd), P<float>(dx), P<float>(dg), P<float>(db), N, C, HW, acc, P<float>(part), S(st));
-  });
+           P<const float>(invstd), P<float>(dx), P<float>(dg), P<float>(db), N, C, HW, acc, P<float>(part), S(st),
+           P<const float>(extra), extra_C);
+  }, py::arg("dy"), py::arg("x"), py::arg("yr"), py::arg("g"), py::arg("mean"), py::arg("invstd"), py::arg("dx"),
+     py::arg("dg"), py::arg("db"), py::arg("N"), py::arg("C"), py::arg("HW"), py::arg("acc"), py::arg("part"),
+     py::arg("st"), py::arg("extra") = 0, py::arg("extra_C") = 0);
   m.def("shortcut_pad_add", [](uintptr_t x, uintptr_t y, int N, int Cin, int H, int W, int Cout, int P_, int Q,
                                int stride, uintptr_t st) {
     shortcut_pad_add(P<const float>(x), P<float>(y), N, Cin, H, W, Cout, P_, Q, stride, S(st));

@@ -118,13 +118,15 @@ size_t bn_partial_floats(int N, int C, int HW);
 void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* y, float* mean,
                   float* invstd, float* run_mean, float* run_var, int N, int C, int HW,
                   float momentum, float eps, bool relu, float* part, hipStream_t st,
-                  int64_t* num_batches = nullptr);  // num_batches: += 1 on device
+                  int64_t* num_batches = nullptr,  // num_batches: += 1 on device
+                  const float* residual = nullptr, int residual_C = 0);  // y[:, :Cr] += residual
 void bn_fwd_eval(const float* x, const float* gamma, const float* beta, float* y,
                  const float* run_mean, const float* run_var, int N, int C, int HW, float eps,
                  bool relu, hipStream_t st);
 void bn_bwd(const float* dy, const float* x, const float* y_relu, const float* gamma,
             const float* mean, const float* invstd, float* dx, float* dgamma, float* dbeta, int N,
-            int C, int HW, bool accumulate_params, float* part, hipStream_t st);
+            int C, int HW, bool accumulate_params, float* part, hipStream_t st,
+            const float* extra = nullptr, int extra_C = 0);  // dx += extra[:, :C] ([N][extra_C][HW])
 
 // PyramidNet shortcut: y[n,c,:,:] += (c < Cin ? pool(x)[n,c] : 0); pool = 2x2 avg, ceil.
 void shortcut_pad_add(const float* x, float* y, int N, int Cin, int H, int W, int Cout, int P, int Q,

@@ -154,7 +154,8 @@ __global__ __launch_bounds__(kBnTB) void bn_apply_slice_k(const float* __restric
                                                           float* __restrict__ run_mean, float* __restrict__ run_var,
                                                           float* __restrict__ y, int N, int C, int HW, int S, FastDiv dv,
                                                           float cnt, float eps, float momentum, int relu,
-                                                          int64_t* __restrict__ num_batches) {
+                                                          int64_t* __restrict__ num_batches,
+                                                          const float* __restrict__ res, int Cr) {
   __shared__ float red[2 * kBnTB / 64];
   const int s = blockIdx.x, c = blockIdx.y;
   if (s == 0 && c == 0 && num_batches && threadIdx.x == 0) *num_batches += 1;
@@ -172,6 +173,8 @@ __global__ __launch_bounds__(kBnTB) void bn_apply_slice_k(const float* __restric
     if (run_var) run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
   }
   const Slice sl = slice_of(s, S, N);
+  // residual (PyramidNet identity shortcut, channels zero-padded): channel c < Cr adds res[n][c]
+  const float* rc = (res && c < Cr) ? res + (size_t)c * HW : nullptr;  // uniform per block
   if (VEC) {
     const int hw4 = HW >> 2;
     const int total = (sl.n1 - sl.n0) * hw4;
@@ -189,6 +192,13 @@ __global__ __launch_bounds__(kBnTB) void bn_apply_slice_k(const float* __restric
         v.z = fmaxf(v.z, 0.f);
         v.w = fmaxf(v.w, 0.f);
       }
+      if (rc) {
+        const float4 r = reinterpret_cast<const float4*>(rc + (size_t)n * Cr * HW)[j];
+        v.x += r.x;
+        v.y += r.y;
+        v.z += r.z;
+        v.w += r.w;
+      }
       reinterpret_cast<float4*>(y)[o] = v;
     }
   } else {
@@ -196,8 +206,10 @@ __global__ __launch_bounds__(kBnTB) void bn_apply_slice_k(const float* __restric
     for (int i = threadIdx.x; i < total; i += kBnTB) {
       const int n = sl.n0 + (int)dv.div(i), j = i - (n - sl.n0) * HW;
       const size_t o = ((size_t)n * C + c) * HW + j;
-      const float r = fmaf(x[o], sc, sh);
-      y[o] = relu ? fmaxf(r, 0.f) : r;
+      float r = fmaf(x[o], sc, sh);
+      if (relu) r = fmaxf(r, 0.f);
+      if (rc) r += rc[(size_t)n * Cr * HW + j];
+      y[o] = r;
     }
   }
 }
@@ -207,7 +219,7 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_apply_slice_k(
     const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ yr,
     const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ part, float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dx, int N,
-    int C, int HW, int S, FastDiv dv, float cnt, int acc_params) {
+    int C, int HW, int S, FastDiv dv, float cnt, int acc_params, const float* __restrict__ extra, int extC) {
   __shared__ float red[2 * kBnTB / 64];
   const int s = blockIdx.x, c = blockIdx.y;
   const float inv = invstd[c], mu = mean[c];
@@ -220,6 +232,9 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_apply_slice_k(
     if (dbeta) dbeta[c] = acc_params ? dbeta[c] + db : db;
   }
   const Slice sl = slice_of(s, S, N);
+  // extra: a second gradient of x added to dx (the residual branch's, read in place from the
+  // block output gradient [N][extC][HW], channels 0..C-1), instead of a separate add launch
+  const float* ec = extra ? extra + (size_t)c * HW : nullptr;
   if (VEC) {
     const int hw4 = HW >> 2;
     const int total = (sl.n1 - sl.n0) * hw4;
@@ -240,6 +255,13 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_apply_slice_k(
       out.y = fmaf(A, g.y, fmaf(D, v.y, Bc));
       out.z = fmaf(A, g.z, fmaf(D, v.z, Bc));
       out.w = fmaf(A, g.w, fmaf(D, v.w, Bc));
+      if (ec) {
+        const float4 e = reinterpret_cast<const float4*>(ec + (size_t)n * extC * HW)[j];
+        out.x += e.x;
+        out.y += e.y;
+        out.z += e.z;
+        out.w += e.w;
+      }
       reinterpret_cast<float4*>(dx)[o] = out;
     }
   } else {
@@ -249,7 +271,7 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_apply_slice_k(
       const size_t o = ((size_t)n * C + c) * HW + j;
       float g = dy[o];
       if (yr && !(yr[o] > 0.f)) g = 0.f;
-      dx[o] = fmaf(A, g, fmaf(D, x[o], Bc));
+      dx[o] = fmaf(A, g, fmaf(D, x[o], Bc)) + (ec ? ec[(size_t)n * extC * HW + j] : 0.f);
     }
   }
 }
@@ -272,41 +294,43 @@ size_t bn_partial_floats(int N, int C, int HW) { return 2 * (size_t)bn_splits(N,
 
 void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* invstd,
                   float* run_mean, float* run_var, int N, int C, int HW, float momentum, float eps, bool relu,
-                  float* part, hipStream_t st, int64_t* num_batches) {
+                  float* part, hipStream_t st, int64_t* num_batches, const float* res, int Cr) {
   MX_CHECK((int64_t)N * C * HW < (1ll << 31), "bn: tensor too large for 32-bit index math");
   const int S = bn_splits(N, C, HW);
   MX_CHECK(S <= 4 * kBnTB, "bn: too many splits");
+  MX_CHECK(!res || (Cr > 0 && Cr <= C), "bn: residual channels must be in 1..C");
   const bool vec = HW % 4 == 0;
   const FastDiv dv(vec ? HW / 4 : HW);
   const float cnt = (float)N * (float)HW;
   if (vec) {
     MX_LAUNCH(bn_stats_k<true>, dim3(S, C), dim3(kBnTB), 0, st, x, N, C, HW, S, dv, part);
     MX_LAUNCH(bn_apply_slice_k<true>, dim3(S, C), dim3(kBnTB), 0, st, x, gamma, beta, part, mean, invstd, run_mean,
-              run_var, y, N, C, HW, S, dv, cnt, eps, momentum, relu ? 1 : 0, num_batches);
+              run_var, y, N, C, HW, S, dv, cnt, eps, momentum, relu ? 1 : 0, num_batches, res, Cr);
   } else {
     MX_LAUNCH(bn_stats_k<false>, dim3(S, C), dim3(kBnTB), 0, st, x, N, C, HW, S, dv, part);
     MX_LAUNCH(bn_apply_slice_k<false>, dim3(S, C), dim3(kBnTB), 0, st, x, gamma, beta, part, mean, invstd, run_mean,
-              run_var, y, N, C, HW, S, dv, cnt, eps, momentum, relu ? 1 : 0, num_batches);
+              run_var, y, N, C, HW, S, dv, cnt, eps, momentum, relu ? 1 : 0, num_batches, res, Cr);
   }
 }
 
 void bn_bwd(const float* dy, const float* x, const float* y_relu, const float* gamma, const float* mean,
             const float* invstd, float* dx, float* dgamma, float* dbeta, int N, int C, int HW, bool accp, float* part,
-            hipStream_t st) {
+            hipStream_t st, const float* extra, int extC) {
   MX_CHECK((int64_t)N * C * HW < (1ll << 31), "bn: tensor too large for 32-bit index math");
   const int S = bn_splits(N, C, HW);
   MX_CHECK(S <= 4 * kBnTB, "bn: too many splits");
+  MX_CHECK(!extra || extC >= C, "bn: extra gradient must have >= C channels");
   const bool vec = HW % 4 == 0;
   const FastDiv dv(vec ? HW / 4 : HW);
   const float cnt = (float)N * (float)HW;
   if (vec) {
     MX_LAUNCH(bn_bwd_reduce_k<true>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, mean, N, C, HW, S, dv, part);
     MX_LAUNCH(bn_bwd_apply_slice_k<true>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, gamma, mean, invstd, part,
-              dgamma, dbeta, dx, N, C, HW, S, dv, cnt, accp ? 1 : 0);
+              dgamma, dbeta, dx, N, C, HW, S, dv, cnt, accp ? 1 : 0, extra, extC);
   } else {
     MX_LAUNCH(bn_bwd_reduce_k<false>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, mean, N, C, HW, S, dv, part);
     MX_LAUNCH(bn_bwd_apply_slice_k<false>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, gamma, mean, invstd, part,
-              dgamma, dbeta, dx, N, C, HW, S, dv, cnt, accp ? 1 : 0);
+              dgamma, dbeta, dx, N, C, HW, S, dv, cnt, accp ? 1 : 0, extra, extC);
   }
 }
 

@@ -753,8 +753,11 @@ void launch_fwd(const float* x, const float* w, const float* bias, const float* 
   // block per CU, e.g. the 8x8 layers up to 256 channels), doubling the MFMAs per barrier
   // interval wins (45 -> 39 us at C = 191, 57 -> 49 us at C = 231); with more blocks than CUs it
   // loses (89 -> 99 us at C = 266: two waves of 98 KB-LDS blocks), as on 16x16 / 32x32
-  const int blocks32 = cdiv(N * tpi, 32) * (Cop / 32);
-  const int variant = forced ? forced : (Wd == 32 ? 3 : (blocks32 <= device_cu_count() ? 4 : 2));
+  // 32x32 images with one 32-channel output tile (the first stage-1 layers): the 32 x 64 patch
+  // blocks leave one block per CU and the 32 x 32 blocks win (11.7 vs 14.5 us at C = 16)
+  const int blocks32 = cdiv(N * tpi, 32) * (Cop / 32), cus = device_cu_count();
+  const int variant = forced ? forced
+                             : (Wd == 32 ? (blocks32 / 2 >= 2 * cus ? 3 : 2) : (blocks32 <= cus ? 4 : 2));
   const int tile_blk = variant == 3 ? 64 : 32;
   a.tblocks = cdiv(N * tpi, tile_blk);
   a.ktiles = Cop / 32;
@@ -831,7 +834,14 @@ WgradPlan wgrad_plan(const ConvShape& s) {
   // gain 1 ms of reduction time.
   const int tiles = p.ktiles * p.ctiles;
   const int cap = std::max(16, (int)std::min<int64_t>(1024, (8ll << 20) / ((int64_t)s.K * s.C * 9)));
-  int nblk = std::max(1, std::min(cdiv(768, tiles), cap));
+  // The grid must not exceed the 3 x 256 resident slots: a few blocks over (e.g. 25 tiles x 31
+  // ranges = 775) run as a second round and nearly double the kernel time.
+  static const int slots = [] {
+    const char* e = std::getenv("MXDDP_WGRAD_SLOTS");
+    return e ? std::atoi(e) : 3 * device_cu_count();
+  }();
+  static const bool ceil_mode = std::getenv("MXDDP_WGRAD_CEIL") != nullptr;  // old rounding, A/B only
+  int nblk = std::max(1, std::min(ceil_mode ? cdiv(slots, tiles) : slots / tiles, cap));
   nblk = std::min(nblk, std::max(1, p.nchunks / 8));
   p.cpb = cdiv(p.nchunks, nblk);
   p.nblk = cdiv(p.nchunks, p.cpb);

@@ -54,14 +54,16 @@ class BatchNorm2d(nn.BatchNorm2d):
         super().__init__(*a, **k)
         self.fuse_relu = fuse_relu
 
-    def forward(self, x):
+    def forward(self, x, residual=None, tap=False):
+        """``residual`` / ``tap``: the PyramidNet shortcut fusions of ops.batch_norm."""
         training = self.training or not self.track_running_stats
         nbt = self.num_batches_tracked if (self.training and self.track_running_stats) else None
         mom = self.momentum if self.momentum is not None else 0.1
         return ops.batch_norm(x, self.weight, self.bias,
                               self.running_mean if self.track_running_stats else None,
                               self.running_var if self.track_running_stats else None,
-                              training, mom, self.eps, relu=self.fuse_relu, num_batches=nbt)
+                              training, mom, self.eps, relu=self.fuse_relu, num_batches=nbt,
+                              residual=residual, tap=tap)
 
 
 def count_params(model: nn.Module) -> int:

@@ -7,8 +7,9 @@ Block = BN -> conv3x3(stride) -> BN -> ReLU -> conv3x3 -> BN, plus a parameter-f
 shortcut that zero-pads channels and 2x2-avg-pools (ceil) on stride 2 (model.py:17-21).
 No ReLU after the residual add.  Module / parameter names match the reference exactly,
 so ``state_dict`` has the same 880 keys (24,253,410 parameters) and checkpoints are
-interchangeable.  In the mxddp version the BN->ReLU pair and the pad+pool+add shortcut
-are single fused kernels.
+interchangeable.  In the mxddp version the BN->ReLU pair is one kernel, the identity
+shortcut (stride 1) is fused into bn3's normalise pass and bn1's backward, and the stride-2
+pad+pool+add shortcut is one kernel.
 """
 from __future__ import annotations
 
@@ -41,6 +42,11 @@ class ResidualBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        if self.stride == 1:
+            # identity shortcut fused into the BNs: bn3 adds x (zero-padded channels) while it
+            # normalises, and bn1's backward adds the shortcut's gradient to its dx
+            h, xs = self.bn1(x, tap=True)
+            return self.bn3(self.conv2(self.bn2(self.conv1(h))), residual=xs)
         out = self.bn3(self.conv2(self.bn2(self.conv1(self.bn1(x)))))
         return ops.shortcut_pad_add(out, x, self.stride)
 

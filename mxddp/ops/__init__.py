@@ -334,8 +334,19 @@ def avg_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False):
 
 # --------------------------------------------------------------------------- batch norm
 class _BatchNorm(torch.autograd.Function):
+    """Train / eval BN (+ fused ReLU).  Two PyramidNet fusions (pytorch/model.py:40-50):
+
+    * ``residual`` (tensor [N, Cr, H, W], Cr <= C): the block's identity shortcut with zero
+      channel padding is added inside the normalise pass, y[:, :Cr] += residual; its gradient
+      is handed back as a view of dy (no copy kernel).
+    * ``tap``: a second output aliasing the input x for the shortcut branch; the gradient that
+      branch sends back is added inside the dx pass, so the block input's two gradients are
+      never summed by a separate launch (read in place from the next block's output gradient).
+    """
+
     @staticmethod
-    def forward(ctx, x, gamma, beta, running_mean, running_var, training, momentum, eps, relu, num_batches=None):
+    def forward(ctx, x, gamma, beta, running_mean, running_var, training, momentum, eps, relu, num_batches=None,
+                residual=None, tap=False):
         C = native()
         x = x.contiguous()
         _check(x, "input")
@@ -343,26 +354,39 @@ class _BatchNorm(torch.autograd.Function):
         HW = x.numel() // (N * Cc)
         y = torch.empty_like(x)
         st = stream_of(x)
+        res_c = 0
+        if residual is not None:
+            residual = residual.contiguous()
+            _check(residual, "residual")
+            res_c = residual.shape[1]
+            if residual.shape[0] != N or residual.shape[2:] != x.shape[2:] or not 0 < res_c <= Cc or relu:
+                raise ValueError("batch_norm residual: [N, Cr <= C, H, W] of the input's size, no fused ReLU")
         if training:
             mean = torch.empty((Cc,), device=x.device, dtype=torch.float32)
             invstd = torch.empty_like(mean)
             part = _bn_part(x.device, C.bn_partial_floats(N, Cc, HW))
             C.bn_fwd_train(x.data_ptr(), _p(gamma), _p(beta), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
                            _p(running_mean), _p(running_var), N, Cc, HW, float(momentum), float(eps), bool(relu),
-                           part.data_ptr(), st, _p(num_batches))
+                           part.data_ptr(), st, _p(num_batches), _p(residual), res_c)
         else:
             mean = running_mean
             invstd = (running_var + eps).rsqrt()
             C.bn_fwd_eval(x.data_ptr(), _p(gamma), _p(beta), y.data_ptr(), running_mean.data_ptr(),
                           running_var.data_ptr(), N, Cc, HW, float(eps), bool(relu), st)
+            if residual is not None:
+                y[:, :res_c] += residual
         ctx.save_for_backward(x, gamma, mean, invstd, y if relu else None)
         ctx.dims = (N, Cc, HW)
         ctx.has_affine = gamma is not None
         ctx.affine_refs = (gamma, beta)
+        ctx.res_c = res_c
+        ctx.tap = tap
+        if tap:
+            return y, x
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dtap=None):
         x, gamma, mean, invstd, y = ctx.saved_tensors
         N, Cc, HW = ctx.dims
         dy = dy.contiguous()
@@ -375,14 +399,25 @@ class _BatchNorm(torch.autograd.Function):
         else:
             dg = torch.empty((Cc,), device=x.device) if ctx.has_affine else None
             db = torch.empty((Cc,), device=x.device) if ctx.has_affine else None
+        ext, ext_c = None, 0
+        if dtap is not None:
+            # usually a channel slice of the next block's output gradient: read it in place
+            s_ = dtap.stride()
+            W = x.shape[-1] if x.dim() >= 3 else 1
+            in_place = (dtap.dim() == 4 and s_[3] == 1 and s_[2] == W and s_[1] == HW and s_[0] % HW == 0
+                        and s_[0] // HW >= Cc and dtap.dtype == torch.float32)
+            ext = dtap if in_place else dtap.contiguous()
+            ext_c = s_[0] // HW if in_place else Cc
         part = _bn_part(x.device, native().bn_partial_floats(N, Cc, HW))
         native().bn_bwd(dy.data_ptr(), x.data_ptr(), _p(y), _p(gamma), mean.data_ptr(), invstd.data_ptr(),
-                        dx.data_ptr(), _p(dg), _p(db), N, Cc, HW, direct, part.data_ptr(), stream_of(dy))
+                        dx.data_ptr(), _p(dg), _p(db), N, Cc, HW, direct, part.data_ptr(), stream_of(dy),
+                        _p(ext), ext_c)
         if direct:
             _grad_done(g_ref)
             _grad_done(b_ref)
             dg = db = None
-        return dx, dg, db, None, None, None, None, None, None, None
+        dres = dy.narrow(1, 0, ctx.res_c) if ctx.res_c and ctx.needs_input_grad[10] else None
+        return dx, dg, db, None, None, None, None, None, None, None, dres, None
 
 
 _BN_PART: dict = {}
@@ -401,16 +436,21 @@ def _bn_part(device, n):
 
 
 def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum=0.1, eps=1e-5, relu=False,
-               num_batches=None):
+               num_batches=None, residual=None, tap=False):
     """``num_batches`` (int64 tensor, GPU path): incremented on device by the BN kernel
-    (BatchNorm2d.num_batches_tracked) instead of a separate launch per layer."""
+    (BatchNorm2d.num_batches_tracked) instead of a separate launch per layer.
+    ``residual``: y[:, :Cr] += residual (identity shortcut, zero channel padding; no ReLU).
+    ``tap``: return (y, x_alias); the gradient of x_alias is summed into dx by the BN kernel."""
     if _native(x):
         return _BatchNorm.apply(x, gamma, beta, running_mean, running_var, training, momentum, eps, relu,
-                                num_batches if training else None)
+                                num_batches if training else None, residual, tap)
     if num_batches is not None and training:
         num_batches.add_(1)
     y = F.batch_norm(x, running_mean, running_var, gamma, beta, training, momentum, eps)
-    return F.relu(y) if relu else y
+    y = F.relu(y) if relu else y
+    if residual is not None:
+        y = y + F.pad(residual, (0, 0, 0, 0, 0, y.shape[1] - residual.shape[1]))
+    return (y, x) if tap else y
 
 
 # --------------------------------------------------------------------------- loss

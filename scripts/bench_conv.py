@@ -10,8 +10,11 @@ sys.path.insert(0, ".")
 import mxddp  # noqa: E402
 
 C_ = mxddp.native()
-SHAPES = [(16, 21, 32), (56, 61, 32), (96, 101, 32), (106, 111, 16), (146, 151, 16), (181, 186, 16),
-          (191, 196, 8), (231, 236, 8), (266, 271, 8)]
+SHAPES = [(16, 21, 32), (56, 61, 32), (66, 71, 32), (96, 101, 32), (106, 111, 16), (126, 131, 16),
+          (146, 151, 16), (161, 166, 16), (181, 186, 16), (191, 196, 8), (211, 216, 8), (231, 236, 8),
+          (251, 256, 8), (266, 271, 8)]
+if "--shapes" in sys.argv:  # e.g. --shapes 146,151,16:266,271,8
+    SHAPES = [tuple(int(v) for v in t.split(",")) for t in sys.argv[sys.argv.index("--shapes") + 1].split(":")]
 N = 64
 dev = torch.device("cuda", 0)
 st = torch.cuda.current_stream().cuda_stream

@@ -209,6 +209,37 @@ def test_shortcut(cuda, stride):
     assert _rel(og.grad.cpu(), orr.grad) < 1e-5
 
 
+@pytest.mark.parametrize("shape", [(4, 21, 26, 16, 16), (8, 186, 186, 8, 8), (2, 5, 9, 7, 7)])
+def test_batchnorm_residual_tap(cuda, shape):
+    """PyramidNet identity-shortcut fusion: bn1 with a tap output (its gradient is summed into dx
+    by the BN kernel, read in place from the channel slice of the block-output gradient) and bn3
+    with the zero-padded residual added in its normalise pass, vs plain torch fp32."""
+    torch.manual_seed(7)
+    N, Cin, C, H, W = shape
+    x = torch.randn(N, Cin, H, W) * 1.5 + 0.3
+    z = torch.randn(N, C, H, W) - 0.7
+    g1, b1, g3, b3 = torch.rand(Cin) + 0.5, torch.randn(Cin), torch.rand(C) + 0.5, torch.randn(C)
+    gh, go = torch.randn(N, Cin, H, W), torch.randn(N, C, H, W)
+    leaves = [x, z, g1, b1, g3, b3]
+    ref = [t.clone().requires_grad_() for t in leaves]
+    xr, zr, g1r, b1r, g3r, b3r = ref
+    hr = F.batch_norm(xr, torch.zeros(Cin), torch.ones(Cin), g1r, b1r, True, 0.1, 1e-5)
+    outr = F.batch_norm(zr, torch.zeros(C), torch.ones(C), g3r, b3r, True, 0.1, 1e-5) + F.pad(
+        xr, (0, 0, 0, 0, 0, C - Cin))
+    ((hr * gh).sum() + (outr * go).sum()).backward()
+    dev = [t.to(cuda).requires_grad_() for t in leaves]
+    xg, zg, g1g, b1g, g3g, b3g = dev
+    h, xs = ops.batch_norm(xg, g1g, b1g, torch.zeros(Cin, device=cuda), torch.ones(Cin, device=cuda), True,
+                           tap=True)
+    out = ops.batch_norm(zg, g3g, b3g, torch.zeros(C, device=cuda), torch.ones(C, device=cuda), True, residual=xs)
+    ((h * gh.to(cuda)).sum() + (out * go.to(cuda)).sum()).backward()
+    torch.cuda.synchronize()
+    assert _rel(h.detach().cpu(), hr.detach()) < 1e-4
+    assert _rel(out.detach().cpu(), outr.detach()) < 1e-4
+    for a, b in zip(dev, ref):
+        assert _rel(a.grad.cpu(), b.grad) < 2e-4
+
+
 def test_sgd_adam_flat(cuda):
     import torch.nn as nn
 

@@ -75,3 +75,32 @@ def test_state_dict_loads_into_plain_torch_module():
 def test_registry_specs():
     assert set(MODELS) == set(GOLDEN_PARAMS)
     assert MODELS["keras_cnn"].optimizer == "adam" and MODELS["pyramidnet110"].optimizer == "sgd"
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_pyramidnet_block_matches_reference_formula(stride):
+    """ResidualBlock (the shortcut fused into the BNs on stride 1) computes the reference block
+    (pytorch/model.py:40-50): bn1 -> conv(s) -> bn2 -> ReLU -> conv -> bn3, + pad/pool shortcut."""
+    import torch.nn.functional as F
+
+    from mxddp.models.pyramidnet import ResidualBlock
+
+    torch.manual_seed(3)
+    blk = ResidualBlock(6, 11, stride)
+    x = torch.randn(3, 6, 8, 8, requires_grad=True)
+    out = blk(x)
+
+    def bn(m, t):
+        return F.batch_norm(t, None, None, m.weight, m.bias, True, 0.1, m.eps)
+
+    xr = x.detach().clone().requires_grad_()
+    h = bn(blk.bn3, blk.conv2(F.relu(bn(blk.bn2, F.conv2d(bn(blk.bn1, xr), blk.conv1.weight, None, stride, 1)))))
+    sc = F.pad(xr, (0, 0, 0, 0, 0, 5))
+    if stride == 2:
+        sc = F.avg_pool2d(sc, 2, 2, ceil_mode=True)
+    ref = h + sc
+    assert torch.allclose(out, ref, atol=1e-5)
+    g = torch.randn_like(ref)
+    out.backward(g)
+    ref.backward(g)
+    assert torch.allclose(x.grad, xr.grad, atol=1e-5)
