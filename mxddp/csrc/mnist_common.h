@@ -29,20 +29,34 @@ __device__ __forceinline__ float sel4(const float4& v, int j) {
 struct Scratch {  // carve of MnistFused::scratch (floats)
   float* wf;      // conv2 fwd B-fragments   [18 q][4 w][64 lane][4 j]
   float* wd;      // conv2 dgrad B-fragments [9 r][4 s][2 nt][64 lane][4 j]
-  float* wacc;    // conv2 wgrad accumulator [9 r][64 co][32 ci]
+  float* wacc;    // conv2 wgrad accumulator slabs [kWaccSlabs][9 r][64 co][32 ci], slab = image & (kWaccSlabs - 1)
   float* wu;      // conv2 dgrad Winograd filters G w' G^T (w' = w flipped) as F7W B-fragments
                   // [16 k-step][2 ci-half][64 lane][16 xi]
-  float* g1;      // conv1 grad partial slabs [kG1Slabs][320] (w[32][9] then b[32]), slab = image & 7
+  float* g1;      // conv1 grad partial slabs [kG1Slabs][320] (w[32][9] then b[32]), slab = image & (kWaccSlabs - 1)
   float* wv;      // conv2 forward Winograd filters G w G^T as F2W B-fragments
                   // [4 w][16 xi][2 s4][64 lane][4 j]
 };
 constexpr int kWinoPack = 16 * 2048;  // 16 Winograd-domain values per (co, ci)
 constexpr int kG1Slabs = 8;           // conv1-grad atomics spread over 8 slabs (image & 7)
-inline Scratch carve(float* s) {
-  float* g1 = s + 3 * kPack + kWinoPack;
-  return Scratch{s, s + kPack, s + 2 * kPack, s + 3 * kPack, g1, g1 + kG1Slabs * 320};
+// conv2-wgrad atomics spread over 2 slabs (image & 1): the 64 images' blocks finish together and
+// same-address float atomics serialise, so one accumulator cost F6W a 3.5 us epilogue; the
+// finalize (in the SGD launch at world size 1) sums the slabs in a fixed order.  Measured at
+// B = 64: 1 slab 837k, 2 slabs 843k, 4 slabs 835k, 8 slabs 821k img/s (the finalize's serial
+// tail grows with the slab count faster than the epilogue shrinks: 3.5 / 2.8 / - / 2.4 us).
+constexpr int kWaccSlabs = 2;
+__host__ __device__ inline Scratch carve(float* s) {
+  Scratch c;
+  c.wf = s;
+  c.wd = c.wf + kPack;
+  c.wu = c.wd + kPack;
+  c.g1 = c.wu + kWinoPack;
+  c.wv = c.g1 + kG1Slabs * 320;
+  c.wacc = c.wv + kWinoPack;
+  return c;
 }
-inline size_t scratch_floats(int) { return 3 * (size_t)kPack + 2 * (size_t)kWinoPack + (size_t)kG1Slabs * 320; }
+inline size_t scratch_floats(int) {
+  return 2 * (size_t)kPack + 2 * (size_t)kWinoPack + (size_t)kG1Slabs * 320 + (size_t)kWaccSlabs * kPack;
+}
 
 }  // namespace mnist
 }  // namespace mx

@@ -148,7 +148,7 @@ __device__ __forceinline__ void f6_body(const MnistFused& f, const Scratch& sc, 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int co = 16 * w + 4 * g + j, ci = 16 * c + m;
-      atomicAdd(sc.wacc + (r * 64 + co) * 32 + ci, acc[c][j]);
+      atomicAdd(sc.wacc + (b & (kWaccSlabs - 1)) * kPack + (r * 64 + co) * 32 + ci, acc[c][j]);
     }
   MX_TRACE_B(f, 3, 3, braw);
 }
@@ -293,6 +293,7 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
   // dw = G^T dU G, G^T = [1 .5 .5 0; 0 .5 -.5 0; 0 .5 .5 1]; acc[4i + j'][j] = dU[i][j'] of
   // (co = 16w + 4g + j, ci = 16h + m)
   const int ci = 16 * h + m;
+  float* wa = sc.wacc + (b & (kWaccSlabs - 1)) * kPack;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int cj = 16 * w + 4 * g + j;
@@ -309,9 +310,9 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
       const float o0 = t[ky][0] + 0.5f * (t[ky][1] + t[ky][2]);
       const float o1 = 0.5f * (t[ky][1] - t[ky][2]);
       const float o2 = 0.5f * (t[ky][1] + t[ky][2]) + t[ky][3];
-      atomicAdd(sc.wacc + ((ky * 3 + 0) * 64 + cj) * 32 + ci, o0);
-      atomicAdd(sc.wacc + ((ky * 3 + 1) * 64 + cj) * 32 + ci, o1);
-      atomicAdd(sc.wacc + ((ky * 3 + 2) * 64 + cj) * 32 + ci, o2);
+      atomicAdd(wa + ((ky * 3 + 0) * 64 + cj) * 32 + ci, o0);
+      atomicAdd(wa + ((ky * 3 + 1) * 64 + cj) * 32 + ci, o1);
+      atomicAdd(wa + ((ky * 3 + 2) * 64 + cj) * 32 + ci, o2);
     }
   }
   MX_TRACE_B(f, 3, 3, braw);
@@ -708,8 +709,8 @@ __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scr
 // ------------------------------------------------------------------------------------------
 // F8: finalize bucket 1: conv2.weight grad = transpose of the [r][co][ci] accumulator into
 // the canonical [co][ci][ky][kx] layout; conv1 weight/bias grads = sum over the per-image
-// partial slabs.  Every accumulator it consumes (wacc, g1) and the fc1 split-K accumulator h
-// are reset here for the next step, so the step needs no memset launches.
+// partial slabs (and the conv2 accumulator slabs).  The accumulators g1 and the fc1 split-K h are reset here for the next step
+// (the wacc slabs by the next F3), so the step needs no memset launches.
 // Blocks 0..71: wacc transpose (256 outputs each).  Blocks 72..73: the 8-slab sum, one output
 // per thread.  Blocks 74..: zero h.
 constexpr int kF8Wacc = kPack / 256, kF8G1 = 2;
@@ -719,8 +720,13 @@ __global__ __launch_bounds__(256) void f8_finalize_kernel(MnistFused f, Scratch 
     const int i = blk * 256 + tid;
     const int co = i / 288, rem = i - co * 288, ci = rem / 9, rr = rem - ci * 9;
     float* a = sc.wacc + (rr * 64 + co) * 32 + ci;
-    f.g[L::w2 + i] = *a;
-    *a = 0.f;
+    float v[kWaccSlabs];
+#pragma unroll
+    for (int k = 0; k < kWaccSlabs; ++k) v[k] = a[k * kPack];
+    float s = v[0];
+#pragma unroll
+    for (int k = 1; k < kWaccSlabs; ++k) s += v[k];
+    f.g[L::w2 + i] = s;  // (F3 of the next step zeroes the slabs)
   } else if (blk < kF8Wacc + kF8G1) {
     const int j = (blk - kF8Wacc) * 256 + tid;  // conv1 w/b grads: fixed-order sum of the slabs
     if (j < 320) {

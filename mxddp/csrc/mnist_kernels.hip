@@ -117,7 +117,7 @@ __device__ __forceinline__ void conv2_pack_pair(const Scratch& sc, int pair, con
 // K0 (once, and after any external weight load): pack conv2 weights, zero accumulators.
 __global__ __launch_bounds__(256) void k_init(MnistFused f, Scratch sc) {
   const int gtid = blockIdx.x * 256 + threadIdx.x, gsz = gridDim.x * 256;
-  for (int i = gtid; i < kPack; i += gsz) sc.wacc[i] = 0.f;
+  for (int i = gtid; i < kWaccSlabs * kPack; i += gsz) sc.wacc[i] = 0.f;
   for (int i = gtid; i < 2048; i += gsz) {
     float w[9];
 #pragma unroll
@@ -380,6 +380,7 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
 // wave w = batch rows 16w..16w+15 (loops over further M-tiles when B > 64).  Operands go
 // straight to registers as float4 along K (64-byte row segments).
 constexpr int kF3Chunk = 144, kF3Groups = kF3Chunk / 16;
+static_assert(kWaccSlabs * kPack / 4 <= (9216 / kF3Chunk) * 4 * 256, "F3 grid must cover the wacc slabs");
 __global__ __launch_bounds__(256) void f3_fc1_kernel(MnistFused f) {
   MX_TRACE(f, 1, 0);
   const int kc = blockIdx.x >> 2, nq = blockIdx.x & 3;
@@ -413,6 +414,13 @@ __global__ __launch_bounds__(256) void f3_fc1_kernel(MnistFused f) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         atomicAdd(f.h + (16 * mt + 4 * g + j) * 128 + 32 * nq + 16 * nt + m, acc[nt][j]);
+  }
+  // side job: zero the conv2-wgrad accumulator slabs for this step's F67 (last step's finalize
+  // has read them; one float4 per thread, so the finalize's serial tail carries no stores)
+  {
+    float4* wa = reinterpret_cast<float4*>(carve(f.scratch).wacc);
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < kWaccSlabs * kPack / 4) wa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   MX_TRACE(f, 1, 1);
 }
@@ -735,16 +743,29 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
     if (i >= kW2b && i < kW2b + 16) g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);  // conv2 bias grad reset
   }
   // conv2 weights: one thread per (co, ci) pair updates its 9 taps and writes every packed form
-  // (kFin: the gradient is read -- and reset -- straight from the [tap][co][ci] accumulator).
+  // (kFin: the gradient is summed straight from the [slab][tap][co][ci] accumulator).
   // The pairs go to wave 0 of the grid's last 32 blocks (one main-loop pass each: 32 CUs share
   // the scattered stores); all 27 loads are issued before any store.
   const int pair = ((int)blockIdx.x - ((int)gridDim.x - 32)) * 64 + (int)threadIdx.x;
   if (blockIdx.x + 32 >= gridDim.x && threadIdx.x < 64 && pair >= 0 && pair < 2048) {
     const int co = pair >> 5, ci = pair & 31, e0 = (int)L::w2 + pair * 9;
     float gg[9], pe[9], bb[9];
+    if (kFin) {  // fixed-order sum of the accumulator slabs
+      float sl[kWaccSlabs][9];
+#pragma unroll
+      for (int k = 0; k < kWaccSlabs; ++k)
+#pragma unroll
+        for (int r = 0; r < 9; ++r) sl[k][r] = sc.wacc[k * kPack + (r * 64 + co) * 32 + ci];
+#pragma unroll
+      for (int r = 0; r < 9; ++r) {
+        gg[r] = sl[0][r];
+#pragma unroll
+        for (int k = 1; k < kWaccSlabs; ++k) gg[r] += sl[k][r];
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 9; ++r) {
-      gg[r] = kFin ? sc.wacc[(r * 64 + co) * 32 + ci] : f.g[e0 + r];
+      if (!kFin) gg[r] = f.g[e0 + r];
       pe[r] = f.p[e0 + r];
       bb[r] = buf[e0 + r];
     }
@@ -753,8 +774,7 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
       bb[r] = mom * bb[r] + (gg[r] * gscale + wd * pe[r]);
       pe[r] -= lr * bb[r];
       if (kFin) {
-        sc.wacc[(r * 64 + co) * 32 + ci] = 0.f;
-        f.g[e0 + r] = gg[r];
+        f.g[e0 + r] = gg[r];  // (F3 of the next step zeroes the slabs)
       }
       buf[e0 + r] = bb[r];
       f.p[e0 + r] = pe[r];
