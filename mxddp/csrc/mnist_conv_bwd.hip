@@ -205,8 +205,11 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
 #pragma unroll
   for (int ks = 0; ks < 3; ++ks) w1b[ks] = 4 * ks + g < 9 ? w1s[m * 9 + 4 * ks + g] : 0.f;
   const float b1v = w1s[144 + m];
+  uint32_t tA = 0, tB = 0, tC = 0, tq = 0;  // phase-time sums (trace only)
+  const bool trc = f.trace && threadIdx.x == 0 && braw < 1024;
 #pragma unroll 1
   for (int c = c0; c < c0 + 6 / kF6WSplit; ++c) {
+    if (trc) tq = (uint32_t)__builtin_amdgcn_s_memrealtime();
     // (A) a1 rows 4c .. 4c+5 (x rows 4c .. 4c+7 <= 27) for the 16 ci on MFMA: M = 156 positions
     // (10 tiles of 16, wave w takes tiles w, w+4, w+8), N = 16 ci, K = 9 taps padded to 12
     for (int mt = w; mt < 10; mt += 4) {
@@ -226,6 +229,11 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
       }
     }
     __syncthreads();
+    if (trc) {
+      const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime();
+      tA += t - tq;
+      tq = t;
+    }
     // (B) V = B^T d B of 24 tiles x 16 ci; tile tl: a1 rows 2(tl/12).., cols 2(tl%12)..
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -270,6 +278,11 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
       }
     }
     __syncthreads();
+    if (trc) {
+      const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime();
+      tB += t - tq;
+      tq = t;
+    }
     // (C) k-step s: tile t = 6g + s of the chunk
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
@@ -288,6 +301,7 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
         acc[4 * i + 3] = mfma4(w3, bb[i].w, acc[4 * i + 3]);
       }
     }
+    if (trc) tC += (uint32_t)__builtin_amdgcn_s_memrealtime() - tq;  // issue time of (C)
   }
   MX_TRACE_B(f, 3, 2, braw);
   // dw = G^T dU G, G^T = [1 .5 .5 0; 0 .5 -.5 0; 0 .5 .5 1]; acc[4i + j'][j] = dU[i][j'] of
@@ -316,6 +330,12 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
     }
   }
   MX_TRACE_B(f, 3, 3, braw);
+  if (trc) {  // phase-time sums as "time after block start" in trace slots 4..6 (A, B, C)
+    const uint32_t t0 = f.trace[(3 * 1024 + braw) * 8];
+    f.trace[(3 * 1024 + braw) * 8 + 4] = t0 + tA;
+    f.trace[(3 * 1024 + braw) * 8 + 5] = t0 + tB;
+    f.trace[(3 * 1024 + braw) * 8 + 6] = t0 + tC;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
