@@ -654,10 +654,11 @@ __global__ __launch_bounds__(256, 3) void wino_wgrad_kernel(WinoWArgs a) {
 }
 
 // dw (+)= sum over nblk partial planes (fixed order -> deterministic).  Block = (256 / G) float4
-// quads x G plane groups: thread (q, g) sums planes g, g + G, ... of its quad (two independent
-// partial sums), the G group sums are combined in LDS in a fixed order.  Small PyramidNet layers
-// have ~200 planes: spreading them over G groups replaces one thread's ~50 dependent memory
-// round trips by a few.
+// quads x G plane groups: thread (q, g) sums planes g, g + G, g + 2G, g + 3G, ... of its quad with
+// four loads in flight per iteration, then the G group sums are combined by a fixed-shape LDS
+// tree.  G is picked so a thread sums at most ~4 planes: the small stage-1 PyramidNet layers
+// have 256 planes of only ~4 K floats, and a thread walking 16 of them as a dependent chain made
+// those reductions latency-bound (22-43 us for ~4 MB).
 __global__ __launch_bounds__(256) void wino_wgrad_reduce_k(const float* __restrict__ part, float* __restrict__ dw,
                                                             int64_t plane, int64_t pstride, int nblk, int accumulate,
                                                             int G) {
@@ -667,27 +668,33 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_k(const float* __restri
   const int QB = 256 / G, q = threadIdx.x % QB, g = threadIdx.x / QB;
   const int64_t i = (int64_t)blockIdx.x * QB + q;
   const float4* p4 = reinterpret_cast<const float4*>(part);
-  float4 t0 = make_float4(0.f, 0.f, 0.f, 0.f), t1 = t0;
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i < n4) {
-    int b = g;
-    for (; b + G < nblk; b += 2 * G) {
-      const float4 u = p4[b * s4 + i], v = p4[(b + G) * s4 + i];
-      t0.x += u.x; t0.y += u.y; t0.z += u.z; t0.w += u.w;
-      t1.x += v.x; t1.y += v.y; t1.z += v.z; t1.w += v.w;
-    }
-    if (b < nblk) {
-      const float4 u = p4[b * s4 + i];
-      t0.x += u.x; t0.y += u.y; t0.z += u.z; t0.w += u.w;
+    for (int b = g; b < nblk; b += 4 * G) {
+      float4 u[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int bb = b + k * G;
+        u[k] = bb < nblk ? p4[bb * s4 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        t.x += u[k].x; t.y += u[k].y; t.z += u[k].z; t.w += u[k].w;
+      }
     }
   }
-  red[threadIdx.x] = make_float4(t0.x + t1.x, t0.y + t1.y, t0.z + t1.z, t0.w + t1.w);
+  red[threadIdx.x] = t;
   __syncthreads();
-  if (g == 0 && i < n4) {
-    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int k = 0; k < G; ++k) {
-      const float4 v = red[k * QB + q];
+  for (int st = G >> 1; st > 0; st >>= 1) {
+    if (g < st) {
+      const float4 v = red[threadIdx.x + st * QB];
+      float4& r = red[threadIdx.x];
       r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
     }
+    __syncthreads();
+  }
+  if (g == 0 && i < n4) {
+    float4 r = red[threadIdx.x];
     float4* d4 = reinterpret_cast<float4*>(dw);
     if (accumulate) {
       const float4 o = d4[i];
@@ -695,13 +702,17 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_k(const float* __restri
     }
     d4[i] = r;
   }
-  // tail (plane % 4), one thread
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    for (int64_t k = n4 << 2; k < plane; ++k) {
-      float t = accumulate ? dw[k] : 0.f;
-      for (int b = 0; b < nblk; ++b) t += part[b * pstride + k];
-      dw[k] = t;
-    }
+  // tail (plane % 4 <= 3 floats): one wave per float in the last block, lanes stride over the
+  // planes, fixed-shape wave sum (a single thread walking 256 planes took tens of us)
+  const int tail = (int)(plane - (n4 << 2));
+  if (tail > 0 && blockIdx.x == gridDim.x - 1 && (int)(threadIdx.x >> 6) < tail) {
+    const int lane = threadIdx.x & 63;
+    const int64_t k = (n4 << 2) + (threadIdx.x >> 6);
+    float v = 0.f;
+    for (int b = lane; b < nblk; b += 64) v += part[b * pstride + k];
+    v = wave_sum(v);
+    if (lane == 0) dw[k] = (accumulate ? dw[k] : 0.f) + v;
+  }
 }
 
 // same reduction for a destination that is not 16-byte aligned
@@ -909,8 +920,8 @@ void wino_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, 
                 st, scratch, dw, plane, pstride, p.nblk, accumulate ? 1 : 0);
       return;
     }
-    int G = 1;  // plane groups per reduce block: each thread sums <= ~8 planes
-    while (G < 16 && G * 8 < p.nblk) G *= 2;
+    int G = 1;  // plane groups per reduce block: each thread sums <= ~4 planes
+    while (G < 64 && G * 4 < p.nblk) G *= 2;
     const int64_t blocks = std::max<int64_t>(1, (plane / 4 + 256 / G - 1) / (256 / G));
     MX_CHECK(blocks < (1ll << 31), "winograd wgrad: reduce grid too large");
     MX_LAUNCH(wino_wgrad_reduce_k, dim3((unsigned)blocks), dim3(256), 0, st, scratch, dw, plane, pstride, p.nblk,

@@ -267,3 +267,29 @@ def test_sgd_adam_flat(cuda):
         torch.cuda.synchronize()
         for p, q in zip(m.parameters(), m_ref.parameters()):
             assert _rel(p.detach().cpu(), q.detach()) < 1e-5, Opt.__name__
+
+
+@pytest.mark.parametrize("shape", [(64, 21, 32, 21), (64, 61, 32, 66), (64, 191, 8, 196), (4, 13, 16, 7)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_winograd_wgrad_partial_planes(cuda, shape, accumulate):
+    """Winograd weight gradient with its split reduction: up to 256 partial planes summed by the
+    grouped reduce (plane groups + LDS tree), odd plane sizes (the float tail), accumulate mode;
+    vs an fp64 CPU reference."""
+    import mxddp
+
+    C_ = mxddp.native()
+    N, C, W, K = shape
+    torch.manual_seed(11)
+    x = torch.randn(N, C, W, W)
+    dy = torch.randn(N, K, W, W)
+    ref = torch.nn.grad.conv2d_weight(x.double(), (K, C, 3, 3), dy.double(), 1, 1)
+    base = torch.randn(K, C, 3, 3) if accumulate else torch.zeros(K, C, 3, 3)
+    geo = (N, C, W, W, K, 3, 3, 1, 1, 1, 1, 1, 1)
+    xg, dyg, dw = x.to(cuda), dy.to(cuda), base.to(cuda)
+    ws = torch.empty(max(1, C_.conv_wgrad_scratch_floats(*geo)), device=cuda)
+    C_.conv2d_wgrad(dyg.data_ptr(), xg.data_ptr(), dw.data_ptr(), *geo, accumulate,
+                    torch.cuda.current_stream().cuda_stream, ws.data_ptr())
+    torch.cuda.synchronize()
+    want = ref + base.double()
+    err = ((dw.cpu().double() - want).abs().max() / want.abs().max()).item()
+    assert err < 2e-5, err
