@@ -31,14 +31,26 @@ PYBIND11_MODULE(_C, m) {
   // ---------------------------------------------------------------- GEMM-shaped ops
   m.def("conv2d_fwd", [](uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y, int N, int C, int H, int W, int K, int R,
                          int S_, int sh, int sw, int ph, int pw, int dh, int dw, bool relu, uintptr_t st,
-                         uintptr_t scratch, uintptr_t dgrad_filters) {
+                         uintptr_t scratch, uintptr_t dgrad_filters, bool pretransformed) {
     conv2d_fwd(P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y),
                CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw), relu, S(st), P<float>(scratch),
-               P<float>(dgrad_filters));
+               P<float>(dgrad_filters), pretransformed);
   }, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("y"), py::arg("N"), py::arg("C"), py::arg("H"), py::arg("W"),
      py::arg("K"), py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
      py::arg("dh"), py::arg("dw"), py::arg("relu"), py::arg("st"), py::arg("scratch") = 0,
-     py::arg("dgrad_filters") = 0);
+     py::arg("dgrad_filters") = 0, py::arg("pretransformed") = false);
+  m.def("conv_fwd_filter_floats", [](int N, int C, int H, int W, int K, int R, int S_, int sh, int sw, int ph,
+                                     int pw, int dh, int dw) {
+    return conv_fwd_filter_floats(CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw));
+  });
+  py::class_<WinoFilterBank>(m, "WinoFilterBank", "persistent Winograd filters of many convs, one refresh launch")
+      .def(py::init<>())
+      .def("add", [](WinoFilterBank& b, uintptr_t w, uintptr_t uf, uintptr_t ud, int K, int C) {
+        b.add(P<const float>(w), P<float>(uf), P<float>(ud), K, C);
+      })
+      .def("clear", &WinoFilterBank::clear)
+      .def("size", &WinoFilterBank::size)
+      .def("refresh", [](const WinoFilterBank& b, uintptr_t st) { b.refresh(S(st)); });
   m.def("conv_dgrad_filter_floats", [](int N, int C, int H, int W, int K, int R, int S_, int sh, int sw, int ph,
                                        int pw, int dh, int dw) {
     return conv_dgrad_filter_floats(CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw));

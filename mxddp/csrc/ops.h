@@ -2,6 +2,7 @@
 // All pointers are device pointers; all launches are asynchronous on `st` and
 // graph-capturable (no allocation, no synchronisation inside).
 #pragma once
+#include <vector>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -27,8 +28,11 @@ struct ConvShape {
 // also prepares the filters the Winograd data gradient will use (pass them to conv2d_dgrad with
 // pretransformed = true)
 void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s,
-                bool relu, hipStream_t st, float* scratch = nullptr, float* dgrad_filters = nullptr);
+                bool relu, hipStream_t st, float* scratch = nullptr, float* dgrad_filters = nullptr,
+                bool pretransformed = false);
 size_t conv_dgrad_filter_floats(const ConvShape& s);
+// forward Winograd filter floats (0 = this conv does not run the Winograd path)
+size_t conv_fwd_filter_floats(const ConvShape& s);
 // dx = conv_transpose(dy, w) [* (mask > 0)], stored (=) or accumulated (+=).  `wt_scratch`
 // (conv_scratch_floats(s) floats, optional) enables the Winograd / direct 3x3 paths.
 void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s,
@@ -47,9 +51,29 @@ void conv3x3_wgrad(const float* dy, const float* x, float* dw, const ConvShape& 
 bool wino_eligible(const ConvShape& s);
 size_t wino_scratch_floats(const ConvShape& s);
 // U_dgrad_out (optional, wino_dgrad_filter_floats(s)): also write the data-gradient filters
+// pretransformed: `scratch` already holds the forward filters (WinoFilterBank / an earlier call)
 void wino_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s, bool relu,
-              float* scratch, hipStream_t st, float* U_dgrad_out = nullptr);
+              float* scratch, hipStream_t st, float* U_dgrad_out = nullptr, bool pretransformed = false);
 size_t wino_dgrad_filter_floats(const ConvShape& s);
+size_t wino_fwd_filter_floats(const ConvShape& s);
+// Persistent Winograd filters of many 3x3 convs, re-transformed by ONE launch per <= 64 convs
+// after each optimizer step (the layer path's per-conv forward transform launches disappear).
+class WinoFilterBank {
+ public:
+  void add(const float* w, float* U_fwd, float* U_dgrad, int K, int C);  // U_dgrad may be null
+  void clear() { jobs_.clear(); }
+  size_t size() const { return jobs_.size(); }
+  void refresh(hipStream_t st) const;
+
+ private:
+  struct Job {
+    const float* w;
+    float* Uf;
+    float* Ud;
+    int K, C;
+  };
+  std::vector<Job> jobs_;
+};
 // pretransformed: `scratch` already holds the filters written by wino_fwd(..., U_dgrad_out)
 void wino_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s, const float* relu_mask,
                 bool accumulate, float* scratch, hipStream_t st, bool pretransformed = false);

@@ -376,10 +376,12 @@ size_t conv_scratch_floats(const ConvShape& s) {
 }
 
 size_t conv_dgrad_filter_floats(const ConvShape& s) { return use_wino(s) ? wino_dgrad_filter_floats(s) : 0; }
+size_t conv_fwd_filter_floats(const ConvShape& s) { return use_wino(s) ? wino_fwd_filter_floats(s) : 0; }
 
 void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s,
-                bool relu, hipStream_t st, float* scratch, float* dgrad_filters) {
-  if (scratch && use_wino(s)) return wino_fwd(x, w, bias, y, s, relu, scratch, st, dgrad_filters);
+                bool relu, hipStream_t st, float* scratch, float* dgrad_filters, bool pretransformed) {
+  MX_CHECK(!pretransformed || (scratch && use_wino(s)), "conv2d_fwd: pretransformed filters need the Winograd path");
+  if (scratch && use_wino(s)) return wino_fwd(x, w, bias, y, s, relu, scratch, st, dgrad_filters, pretransformed);
   if (g_gemm_precision == 0 && conv3x3_eligible(s)) return conv3x3_fwd(x, w, bias, y, s, relu, st);
   if (is_1x1_s1(s)) {
     Conv1x1FwdOp op{s.N * s.H * s.W, s.K, s.C, s.H * s.W, FastDiv(s.H * s.W), x, w, bias, y, relu};

@@ -149,6 +149,48 @@ __global__ void wino_wtrans2_k(const float* __restrict__ w, float* __restrict__ 
   }
 }
 
+// Filter bank refresh: the forward / data-gradient Winograd filters of MANY convolutions in one
+// launch (after the optimizer step), instead of one transform launch per conv per forward.  The
+// job table travels by value in the kernel arguments (graph-capturable, no upload); block b
+// belongs to the job with the largest blk0 <= b (uniform scalar scan).
+struct WFJob {
+  const float* w;
+  float* Uf;  // [16][Cipf][Copf]
+  float* Ud;  // [16][Cipd][Copd] or null
+  int K, C, Cipf, Copf, Cipd, Copd, blk0;
+};
+constexpr int kWFMaxJobs = 64;
+struct WFBatch {
+  WFJob j[kWFMaxJobs];
+  int n;
+};
+__global__ __launch_bounds__(256) void wino_wtrans_batch_k(WFBatch b) {
+  int q = 0;
+  while (q + 1 < b.n && b.j[q + 1].blk0 <= (int)blockIdx.x) ++q;
+  const WFJob& J = b.j[q];
+  const int tf = J.Cipf * J.Copf, td = J.Ud ? J.Cipd * J.Copd : 0;
+  const int i = ((int)blockIdx.x - J.blk0) * 256 + (int)threadIdx.x;
+  if (i >= tf + td) return;
+  const bool dg = i >= tf;
+  const int j = dg ? i - tf : i, Cop = dg ? J.Copd : J.Copf;
+  const size_t plane = dg ? (size_t)td : (size_t)tf;
+  float* U = dg ? J.Ud : J.Uf;
+  const int ci = j / Cop, co = j - ci * Cop;
+  const int k = dg ? ci : co, c = dg ? co : ci;
+  float g[9], u[16];
+  if (k < J.K && c < J.C) {
+    const float* src = J.w + ((size_t)k * J.C + c) * 9;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) g[t] = dg ? src[8 - t] : src[t];
+  } else {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) g[t] = 0.f;
+  }
+  filter_transform(g, u);
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi) U[xi * plane + j] = u[xi];
+}
+
 // One chunk (8 reduction rows) of the 16 Winograd-domain GEMMs: 32 MFMAs, each fed by one A and
 // one B operand read from LDS.  The schedule is pinned to a software pipeline (8 operand reads
 // ahead, then {1 MFMA, 2 reads}): left alone the scheduler hoists all 64 reads above the first
@@ -878,8 +920,40 @@ size_t wino_wgrad_scratch_floats(const ConvShape& s) {
 }
 
 void wino_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s, bool relu,
-              float* scratch, hipStream_t st, float* U_dgrad_out) {
-  launch_fwd(x, w, bias, nullptr, y, s.N, s.C, s.K, s.W, relu, false, false, scratch, s.K, s.C, st, U_dgrad_out);
+              float* scratch, hipStream_t st, float* U_dgrad_out, bool pretransformed) {
+  launch_fwd(x, w, bias, nullptr, y, s.N, s.C, s.K, s.W, relu, false, false, scratch, s.K, s.C, st,
+             pretransformed ? nullptr : U_dgrad_out, pretransformed);
+}
+
+size_t wino_fwd_filter_floats(const ConvShape& s) { return 16 * (size_t)pad_to(s.C, kCC) * pad_to(s.K, 32); }
+
+void WinoFilterBank::add(const float* w, float* U_fwd, float* U_dgrad, int K, int C) {
+  MX_CHECK(w && U_fwd, "filter bank: weight and forward filter buffer required");
+  jobs_.push_back(Job{w, U_fwd, U_dgrad, K, C});
+}
+
+void WinoFilterBank::refresh(hipStream_t st) const {
+  for (size_t b0 = 0; b0 < jobs_.size(); b0 += kWFMaxJobs) {
+    WFBatch bt{};
+    int blocks = 0;
+    bt.n = (int)std::min<size_t>(kWFMaxJobs, jobs_.size() - b0);
+    for (int q = 0; q < bt.n; ++q) {
+      const Job& j = jobs_[b0 + q];
+      WFJob& J = bt.j[q];
+      J.w = j.w;
+      J.Uf = j.Uf;
+      J.Ud = j.Ud;
+      J.K = j.K;
+      J.C = j.C;
+      J.Cipf = pad_to(j.C, kCC);
+      J.Copf = pad_to(j.K, 32);
+      J.Cipd = pad_to(j.K, kCC);
+      J.Copd = pad_to(j.C, 32);
+      J.blk0 = blocks;
+      blocks += cdiv(J.Cipf * J.Copf + (j.Ud ? J.Cipd * J.Copd : 0), 256);
+    }
+    MX_LAUNCH(wino_wtrans_batch_k, dim3(blocks), dim3(256), 0, st, bt);
+  }
 }
 
 size_t wino_dgrad_filter_floats(const ConvShape& s) { return 16 * (size_t)pad_to(s.K, kCC) * pad_to(s.C, 32); }

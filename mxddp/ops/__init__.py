@@ -13,6 +13,9 @@ conv / BN / pool / linear in ``pytorch/model.py:28-33,62-77``, CrossEntropyLoss 
 """
 from __future__ import annotations
 
+import os
+import weakref
+
 import torch
 import torch.nn.functional as F
 
@@ -20,7 +23,7 @@ from .. import native
 
 __all__ = [
     "conv2d", "linear", "relu", "max_pool2d", "avg_pool2d", "batch_norm", "cross_entropy",
-    "shortcut_pad_add", "stream_of",
+    "shortcut_pad_add", "stream_of", "refresh_filters", "invalidate_filters",
 ]
 
 
@@ -87,6 +90,95 @@ def _grad_done(p):
     return None
 
 
+# ------------------------------------------------------------- persistent Winograd filters
+# A 3x3 stride-1 conv on the Winograd path needs its filters transformed (forward: G w G^T,
+# data gradient: of the flipped / transposed w) once per weight update.  Instead of one
+# transform launch per conv per forward, every such conv registers persistent filter buffers in
+# a per-device native bank (csrc WinoFilterBank) and the optimizer re-transforms ALL of them in
+# one launch per 64 convs right after its step (refresh_filters).  A forward uses the banked
+# filters only while they are provably current: same bank generation (no unreported raw write
+# since the last refresh) and same tensor version (no torch in-place write, e.g. a checkpoint
+# load); otherwise it transforms as before, into the bank's buffers.
+class _Bank:
+    def __init__(self):
+        self.native = native().WinoFilterBank()
+        self.entries = {}  # (weight data_ptr, K, C) -> entry
+        self.gen = 0
+
+
+_BANKS: dict = {}
+
+
+class _FilterEntry:
+    __slots__ = ("ref", "w", "U", "Ud", "version", "gen")
+
+    def __init__(self, param, U, Ud):
+        # the native bank keeps raw pointers: the entry holds the weight storage (a detached
+        # alias, same version counter) and both buffers; `ref` lets a dead model's entries go
+        self.ref, self.w, self.U, self.Ud = weakref.ref(param), param.detach(), U, Ud
+        self.version, self.gen = -1, -1
+
+
+def _rebuild(bank) -> None:
+    dead = [k for k, e in bank.entries.items() if e.ref() is None]
+    for k in dead:
+        del bank.entries[k]
+    bank.native.clear()
+    for e in bank.entries.values():
+        bank.native.add(e.w.data_ptr(), e.U.data_ptr(), _p(e.Ud), e.w.shape[0], e.w.shape[1])
+
+
+_BANK_ON = os.environ.get("MXDDP_FILTER_BANK", "1") != "0"  # 0: per-conv transforms (A/B, tests)
+
+
+def _filter_entry(w, geom, needs_dgrad):
+    """This conv's banked filters (created and registered on first use), or None if the shape
+    does not run the Winograd path or the weight is not a leaf parameter."""
+    if not (_BANK_ON and w.is_leaf):
+        return None
+    C = native()
+    nf = C.conv_fwd_filter_floats(*geom)
+    if not nf:
+        return None
+    bank = _BANKS.get(w.device)
+    if bank is None:
+        bank = _BANKS[w.device] = _Bank()
+    key = (w.data_ptr(), w.shape[0], w.shape[1])
+    ent = bank.entries.get(key)
+    if ent is not None and ent.ref() is not w:  # storage reused by another tensor
+        ent = None
+    if ent is None or (needs_dgrad and ent.Ud is None):
+        nd = C.conv_dgrad_filter_floats(*geom) if needs_dgrad else 0
+        U = torch.empty((nf,), device=w.device, dtype=torch.float32)
+        Ud = torch.empty((nd,), device=w.device, dtype=torch.float32) if nd else None
+        ent = _FilterEntry(w, U, Ud)
+        bank.entries[key] = ent
+        _rebuild(bank)
+    return ent, bank
+
+
+def refresh_filters(device=None) -> None:
+    """Re-transform every banked Winograd filter (one launch per 64 convs, on the current stream).
+    Called by the mxddp optimizers right after their (raw-pointer) weight update."""
+    for dev, bank in _BANKS.items():
+        if device is not None and dev != device:
+            continue
+        bank.gen += 1
+        if any(e.ref() is None for e in bank.entries.values()):
+            _rebuild(bank)
+        if bank.entries:
+            bank.native.refresh(torch.cuda.current_stream(dev).cuda_stream)
+            for e in bank.entries.values():
+                e.version, e.gen = e.w._version, bank.gen
+
+
+def invalidate_filters(device=None) -> None:
+    """Weights changed behind torch's back without a refresh: banked filters are stale."""
+    for dev, bank in _BANKS.items():
+        if device is None or dev == device:
+            bank.gen += 1
+
+
 # --------------------------------------------------------------------------- conv2d
 class _Conv2d(torch.autograd.Function):
     @staticmethod
@@ -103,14 +195,22 @@ class _Conv2d(torch.autograd.Function):
         Q = (W + 2 * pw - dw * (S - 1) - 1) // sw + 1
         y = torch.empty((N, K, P, Q), device=x.device, dtype=x.dtype)
         st = stream_of(x)
-        ns = C.conv_scratch_floats(N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw)
-        scr = torch.empty((ns,), device=x.device, dtype=x.dtype) if ns else None
-        # Winograd layers: the forward's filter-transform launch also writes the backward's
-        # data-gradient filters (one launch per conv per step instead of two)
-        nd = C.conv_dgrad_filter_floats(N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw) if ctx.needs_input_grad[0] else 0
-        wd = torch.empty((nd,), device=x.device, dtype=x.dtype) if nd else None
-        C.conv2d_fwd(x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph, pw,
-                     dh, dw, bool(relu), st, _p(scr), _p(wd))
+        geom = (N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw)
+        fe = _filter_entry(w, geom, ctx.needs_input_grad[0])
+        if fe is not None:  # Winograd layer: banked filters (see refresh_filters)
+            ent, bank = fe
+            fresh = ent.gen == bank.gen and ent.version == w._version
+            C.conv2d_fwd(x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), *geom, bool(relu), st, ent.U.data_ptr(),
+                         _p(ent.Ud), fresh)
+            if not fresh:  # transformed just now, into the bank's buffers
+                ent.version, ent.gen = w._version, bank.gen
+            wd = ent.Ud if ctx.needs_input_grad[0] else None
+        else:
+            ns = C.conv_scratch_floats(*geom)
+            scr = torch.empty((ns,), device=x.device, dtype=x.dtype) if ns else None
+            nd = C.conv_dgrad_filter_floats(*geom) if ctx.needs_input_grad[0] else 0
+            wd = torch.empty((nd,), device=x.device, dtype=x.dtype) if nd else None
+            C.conv2d_fwd(x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), *geom, bool(relu), st, _p(scr), _p(wd))
         ctx.dgrad_filters = wd
         ctx.geom = (N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw, P, Q)
         ctx.relu = relu

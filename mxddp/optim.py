@@ -8,13 +8,15 @@ of epsilon (tensorflow2/mnist_single.py:78, chainer/train_mnist.py:69).
 The learning rate lives in a 1-element device tensor so schedulers (StepLR,
 pytorch/distributed_data_parallel.py:97) keep working under hipGraph replay.
 ``grad_scale`` folds DDP's 1/world_size average into the update when the reducer
-sums instead of averaging.
+sums instead of averaging.  After a GPU step the banked Winograd filters of the model's 3x3
+convs are re-transformed in one launch (ops.refresh_filters).
 """
 from __future__ import annotations
 
 import torch
 
 from . import native
+from . import ops as _ops
 from .parallel.flat import FlatParams
 
 
@@ -56,6 +58,7 @@ class SGD(_FlatOptimizer):
             native().sgd_step(f.data.data_ptr(), f.grad.data_ptr(), self.buf.data_ptr(), self._lr_dev.data_ptr(),
                               float(self.grad_scale), float(self.momentum), float(self.weight_decay), f.numel,
                               False, torch.cuda.current_stream(f.data.device).cuda_stream)
+            _ops.refresh_filters(f.data.device)
         else:
             g = f.grad * self.grad_scale + self.weight_decay * f.data
             if self.momentum:
@@ -98,6 +101,7 @@ class Adam(_FlatOptimizer):
                                self._lr_dev.data_ptr(), self._step_dev.data_ptr(), float(self.grad_scale),
                                self.b1, self.b2, float(eps), float(self.weight_decay), f.numel,
                                torch.cuda.current_stream(f.data.device).cuda_stream)
+            _ops.refresh_filters(f.data.device)
         else:
             g = f.grad * self.grad_scale + self.weight_decay * f.data
             self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)

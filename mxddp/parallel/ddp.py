@@ -132,6 +132,10 @@ class DistributedDataParallel(nn.Module):
     def _sync_params(self):
         with torch.no_grad():
             self._broadcast(self.flat.data)
+            if self.flat.data.is_cuda:
+                from .. import ops
+
+                ops.invalidate_filters(self.flat.data.device)  # raw write: banked filters stale
             if self.flat_buffers is not None:
                 self._broadcast(self.flat_buffers)
 

@@ -293,3 +293,41 @@ def test_winograd_wgrad_partial_planes(cuda, shape, accumulate):
     want = ref + base.double()
     err = ((dw.cpu().double() - want).abs().max() / want.abs().max()).item()
     assert err < 2e-5, err
+
+
+def test_winograd_filter_bank_matches_per_conv_transforms(cuda):
+    """Banked Winograd filters (one refresh launch after each optimizer step) give bit-identical
+    training to per-conv transforms, and a torch-level weight write (load_state_dict) is
+    detected as stale."""
+    import torch.nn as nn
+
+    from mxddp import ops as O
+    from mxddp.models.layers import BatchNorm2d, Conv2d
+    from mxddp.optim import SGD
+    from mxddp.parallel.flat import FlatParams
+
+    def run(bank_on):
+        prev, O._BANK_ON = O._BANK_ON, bank_on
+        try:
+            torch.manual_seed(21)
+            m = nn.Sequential(Conv2d(8, 12, 3, 1, 1, bias=False), BatchNorm2d(12, fuse_relu=True),
+                              Conv2d(12, 13, 3, 1, 1, bias=False), BatchNorm2d(13)).to(cuda)
+            flat = FlatParams(m)
+            opt = SGD(flat, lr=0.05, momentum=0.9, weight_decay=1e-4)
+            x = torch.randn(6, 8, 16, 16, device=cuda)
+            for _ in range(3):
+                opt.zero_grad()
+                m(x).square().mean().backward()
+                opt.step()
+            y = m(x).detach().clone()
+            # torch-level write: the banked filters must be recomputed, not reused
+            sd = {k: v * 0.5 if v.is_floating_point() else v for k, v in m.state_dict().items()}
+            m.load_state_dict(sd)
+            y2 = m(x).detach().clone()
+            return flat.data.clone(), y, y2
+        finally:
+            O._BANK_ON = prev
+
+    a, b = run(True), run(False)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
