@@ -32,12 +32,12 @@ struct Scratch {  // carve of MnistFused::scratch (floats)
   float* wacc;    // conv2 wgrad accumulator slabs [kWaccSlabs][9 r][64 co][32 ci], slab = image & (kWaccSlabs - 1)
   float* wu;      // conv2 dgrad Winograd filters G w' G^T (w' = w flipped) as F7W B-fragments
                   // [16 k-step][2 ci-half][64 lane][16 xi]
-  float* g1;      // conv1 grad partial slabs [kG1Slabs][320] (w[32][9] then b[32]), slab = image & (kWaccSlabs - 1)
+  float* g1;      // conv1 grad partial slabs [kG1Slabs][320] (w[32][9] then b[32]), slab = image & (kG1Slabs - 1)
   float* wv;      // conv2 forward Winograd filters G w G^T as F2W B-fragments
                   // [4 w][16 xi][2 s4][64 lane][4 j]
 };
 constexpr int kWinoPack = 16 * 2048;  // 16 Winograd-domain values per (co, ci)
-constexpr int kG1Slabs = 8;           // conv1-grad atomics spread over 8 slabs (image & 7)
+constexpr int kG1Slabs = 16;          // conv1-grad atomics spread over 16 slabs (image & 15)
 // conv2-wgrad atomics spread over 2 slabs (image & 1): the 64 images' blocks finish together and
 // same-address float atomics serialise, so one accumulator cost F6W a 3.5 us epilogue; the
 // finalize (in the SGD launch at world size 1) sums the slabs in a fixed order.  Measured at

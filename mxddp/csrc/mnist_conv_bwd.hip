@@ -167,20 +167,41 @@ __device__ __forceinline__ void f6_body(const MnistFused& f, const Scratch& sc, 
 // ds_read_b128 of the 16 xi), (C) 6 k-steps of 16 MFMAs; K inside a chunk is ordered
 // t = 6g + s (lane group g) so a lane's dp / q operands are 6 contiguous windows (float2 / u16
 // loads, prefetched one chunk ahead).
-constexpr int kF6WA1P = 157, kF6WVP = 20;
-constexpr size_t kF6WLds = sizeof(float) * (784 + 160 + 16 * kF6WA1P + 24 * 16 * kF6WVP);
+// kA1 (default): phase A loads the chunk's a1 rows that F2 published (one chunk ahead, 3 float4
+// per thread in registers) instead of recomputing conv1: phase A was 5.4 of F6W's 25 us.  The a1
+// tile pitch is then 164 (16-byte rows for the float4 stores; 36 ci mod 64 banks keeps phase B's
+// reads conflict-free).
+constexpr int kF6WA1P = 157, kF6WA1PL = 164, kF6WVP = 20;
+constexpr size_t kF6WLds = sizeof(float) * (784 + 160 + 16 * kF6WA1PL + 24 * 16 * kF6WVP);
 // kF6WSplit = blocks per (image, ci half), each 6 / kF6WSplit chunks
-template <int kF6WSplit>
+template <int kF6WSplit, bool kA1>
 __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc, float* sm, int braw, int nblk) {
   MX_TRACE_B(f, 3, 0, braw);
+  constexpr int kA1P = kA1 ? kF6WA1PL : kF6WA1P;
   float* xs = sm;             // [784]
   float* w1s = xs + 784;      // conv1 w [16][9] then b [16] of this ci half
-  float* a1s = w1s + 160;     // [16 ci][157]: 6 a1 rows x 26
-  float* vs = a1s + 16 * kF6WA1P;  // [24 t][16 ci][20]
+  float* a1s = w1s + 160;     // [16 ci][kA1P]: 6 a1 rows x 26
+  float* vs = a1s + 16 * kA1P;  // [24 t][16 ci][20]
   const int bid = xcd_remap(braw, nblk);
   const int b = bid / (2 * kF6WSplit), h = bid & 1, c0 = ((bid >> 1) % kF6WSplit) * (6 / kF6WSplit);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
-  {
+  // kA1: a1 rows 4c .. 4c+5 of the block's 16 ci = 16 x 39 float4 (624 of the 768 slots)
+  // (three named registers, not an array: an array here was placed in scratch memory)
+  const float* a1b = f.a1 + ((size_t)b * 32 + 16 * h) * 676;
+  int a1src[3], a1dst[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int i = min(tid + 256 * k, 623), ci = i / 39, f4 = i - 39 * ci;
+    a1src[k] = ci * 676 + 4 * f4;
+    a1dst[k] = tid + 256 * k < 624 ? ci * kA1P + 4 * f4 : -1;
+  }
+  float4 pa0, pa1, pa2;
+  if constexpr (kA1) {
+    pa0 = *reinterpret_cast<const float4*>(a1b + a1src[0] + 104 * c0);
+    pa1 = *reinterpret_cast<const float4*>(a1b + a1src[1] + 104 * c0);
+    pa2 = *reinterpret_cast<const float4*>(a1b + a1src[2] + 104 * c0);
+  }
+  if constexpr (!kA1) {
     const float4 xv = reinterpret_cast<const float4*>(f.x + b * 784)[min(tid, 195)];
     const float wv = tid < 144 ? f.p[L::w1 + 144 * h + tid] : f.p[L::b1 + 16 * h + min(tid - 144, 15)];
     if (tid < 196) *reinterpret_cast<float4*>(xs + 4 * tid) = xv;
@@ -210,8 +231,20 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
 #pragma unroll 1
   for (int c = c0; c < c0 + 6 / kF6WSplit; ++c) {
     if (trc) tq = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    if constexpr (kA1) {  // (A) published a1 rows -> LDS; next chunk's rows in flight
+      *reinterpret_cast<float4*>(a1s + a1dst[0]) = pa0;
+      *reinterpret_cast<float4*>(a1s + a1dst[1]) = pa1;
+      if (a1dst[2] >= 0) *reinterpret_cast<float4*>(a1s + a1dst[2]) = pa2;
+      if (c + 1 < c0 + 6 / kF6WSplit) {
+        const float* nb = a1b + 104 * (c + 1);
+        pa0 = *reinterpret_cast<const float4*>(nb + a1src[0]);
+        pa1 = *reinterpret_cast<const float4*>(nb + a1src[1]);
+        pa2 = *reinterpret_cast<const float4*>(nb + a1src[2]);
+      }
+    }
     // (A) a1 rows 4c .. 4c+5 (x rows 4c .. 4c+7 <= 27) for the 16 ci on MFMA: M = 156 positions
     // (10 tiles of 16, wave w takes tiles w, w+4, w+8), N = 16 ci, K = 9 taps padded to 12
+    if constexpr (!kA1)
     for (int mt = w; mt < 10; mt += 4) {
       const int p = min(16 * mt + m, 155), r = p / 26, col = p - 26 * r;
       const float* xp = xs + (4 * c + r) * 28 + col;
@@ -225,7 +258,7 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int q = 16 * mt + 4 * g + j;
-        if (q < 156) a1s[m * kF6WA1P + q] = fmaxf(a[j] + b1v, 0.f);
+        if (q < 156) a1s[m * kA1P + q] = fmaxf(a[j] + b1v, 0.f);
       }
     }
     __syncthreads();
@@ -240,7 +273,7 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
       const int i = tid + 256 * k;
       if (i < 384) {
         const int ci = i & 15, tl = i >> 4, tyl = tl / 12, tx = tl - 12 * tyl;
-        const float* ap = a1s + ci * kF6WA1P + 2 * tyl * 26 + 2 * tx;
+        const float* ap = a1s + ci * kA1P + 2 * tyl * 26 + 2 * tx;
         float d[4][4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -587,6 +620,7 @@ __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc,
     const float4* wu = reinterpret_cast<const float4*>(sc.wu) + (half * 64 + lane) * 4;
     // fully unrolled; B fragments prefetched kF7WPf k-steps ahead (indices fold to registers)
     constexpr int kF7WPf = 2;
+    constexpr bool kF7WPin = true;
     float4 bq[16][4];
 #pragma unroll
     for (int s = 0; s < kF7WPf; ++s)
@@ -598,6 +632,9 @@ __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc,
 #pragma unroll
         for (int k = 0; k < 4; ++k) bq[s + kF7WPf][k] = wu[(s + kF7WPf) * 512 + k];
       }
+      // keep the prefetch at the top of the step: left alone the scheduler sinks these loads
+      // next to their use and every k-step then waits for L2 (vmcnt(0)) before its MFMAs
+      if (kF7WPin) __builtin_amdgcn_sched_barrier(0);
       const float4* bc = bq[s];
       const int off = 4 * s * kF7WCoP;  // co = 4s + g
       float v[4];
@@ -710,13 +747,13 @@ __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc,
 // (576 + 704 blocks over 256 CUs at 3 per CU), so one kernel's prologue/epilogue latency and
 // the 2-vs-3-blocks-per-CU imbalance of each kernel alone are covered by the other's MFMA work.
 // 9B is a multiple of 8, so the F7 part keeps its XCD-aware block mapping.
-template <bool kWino, int kF6WSplit = 1>
+template <bool kWino, int kF6WSplit = 1, bool kA1 = false>
 __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scratch sc) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int n6 = (kWino ? 2 * kF6WSplit : 9) * f.B;
   if ((int)blockIdx.x < n6) {
     if (kWino)
-      f6w_body<kF6WSplit>(f, sc, sm, blockIdx.x, n6);
+      f6w_body<kF6WSplit, kA1>(f, sc, sm, blockIdx.x, n6);
     else
       f6_body(f, sc, sm, blockIdx.x, n6);
   } else if (kWino) {
@@ -729,8 +766,8 @@ __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scr
 // ------------------------------------------------------------------------------------------
 // F8: finalize bucket 1: conv2.weight grad = transpose of the [r][co][ci] accumulator into
 // the canonical [co][ci][ky][kx] layout; conv1 weight/bias grads = sum over the per-image
-// partial slabs (and the conv2 accumulator slabs).  The accumulators g1 and the fc1 split-K h are reset here for the next step
-// (the wacc slabs by the next F3), so the step needs no memset launches.
+// partial slabs (and the conv2 accumulator slabs).  The accumulators g1 and the fc1 split-K h
+// are reset here for the next step (the wacc slabs by the next F3): no memset launches.
 // Blocks 0..71: wacc transpose (256 outputs each).  Blocks 72..73: the 8-slab sum, one output
 // per thread.  Blocks 74..: zero h.
 constexpr int kF8Wacc = kPack / 256, kF8G1 = 2;
@@ -773,6 +810,13 @@ using namespace mnist;
 // F7 variant: Winograd (default) or direct implicit GEMM (MXDDP_MNIST_F7=direct); Winograd
 // weight-gradient blocks per (image, ci half): MXDDP_F6W_SPLIT = 1 (default: 748k img/s; 2: 725k,
 // 3: 695k -- more blocks double the weight-gradient atomics and slow the F7W blocks).
+bool mnist_a1_publish() {
+  static const int v = [] {
+    const char* e = std::getenv("MXDDP_MNIST_A1");
+    return (e && std::string(e) == "recompute") ? 0 : 1;
+  }();
+  return v == 1;
+}
 bool mnist_f7_wino() {
   static const int v = [] {
     const char* e = std::getenv("MXDDP_MNIST_F7");
@@ -792,13 +836,18 @@ static int f6w_split() {
 template <int kSplit>
 static void launch_f67_wino(const MnistFused& f, const Scratch& sc, hipStream_t st) {
   constexpr size_t lds = kF6WLds > kF7WLds ? kF6WLds : kF7WLds;
-  MX_LAUNCH((f67_conv2_bwd_kernel<true, kSplit>), dim3(2 * kSplit * f.B + kF7WChunks * f.B), dim3(256), lds, st, f, sc);
+  const dim3 grid(2 * kSplit * f.B + kF7WChunks * f.B);
+  if (kSplit == 1 && f.a1_pub)
+    MX_LAUNCH((f67_conv2_bwd_kernel<true, 1, true>), grid, dim3(256), lds, st, f, sc);
+  else
+    MX_LAUNCH((f67_conv2_bwd_kernel<true, kSplit>), grid, dim3(256), lds, st, f, sc);
 }
 
 void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_sgd) {
   static bool attr = false;
   if (!attr) {
     for (const void* fn : {reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 1>),
+                           reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 1, true>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 2>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 3>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<false>)})

@@ -137,6 +137,7 @@ MnistFused MnistEngine::fused_args() const {
   f.p = p_;
   f.g = g_;
   f.a1 = a1_;
+  f.a1_pub = mnist_a1_publish() ? 1 : 0;
   f.pool = pool_;
   f.idx = idx_;
   f.h = h_;

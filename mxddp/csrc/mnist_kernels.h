@@ -25,7 +25,9 @@ struct MnistFused {
   uint64_t seed;         // per-rank generator seed
   uint32_t* trace;       // optional per-phase timestamps (s_memrealtime, 100 MHz) for profiling, or null
   int synth;             // 1: F2 generates the batch on device; 0: x/y provided by the caller
+  int a1_pub;            // 1: F2 publishes conv1's output to a1 and F6W loads it (else F6W recomputes)
 };
+bool mnist_a1_publish();  // default on; MXDDP_MNIST_A1=recompute turns it off
 
 size_t mnist_fused_scratch_floats(int B);
 bool mnist_f7_wino();  // conv2 data gradient as Winograd (default) vs direct (MXDDP_MNIST_F7=direct)

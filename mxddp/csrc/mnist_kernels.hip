@@ -333,6 +333,14 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
   }
   __syncthreads();
   MX_TRACE(f, 0, 2);
+  if (f.a1_pub) {  // publish the a1 rows this block owns (2, or 4 for the last row) for F6W
+    const int nr = py == 11 ? 4 : 2, per = nr * 26;
+    float* dst = f.a1 + (size_t)b * 21632 + row0 * 26;
+    for (int i = tid; i < 32 * per; i += 256) {
+      const int ci = i / per, rem = i - ci * per, qr = rem / 26, qc = rem - 26 * qr;
+      dst[ci * 676 + qr * 26 + qc] = tile[ci * kF2ChP + qr * kF2RowP + qc];
+    }
+  }
   MX_TRACE(f, 0, 3);
   if constexpr (kWino) {
     f2_stage2_wino(f, sc, tile, b, py, w, lane, *reinterpret_cast<const float4(*)[4]>(bq));
