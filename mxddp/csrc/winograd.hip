@@ -634,6 +634,12 @@ __global__ __launch_bounds__(256, 3) void wino_wgrad_kernel(WinoWArgs a) {
     xmask = c_ok ? window_mask<W>(2 * th - 1, 2 * tw - 1) : 0u;
     load_window<W>(a.x, xc + (uint32_t)n * a.C * HW, (2 * th - 1) * W + 2 * tw - 1, xmask, rx);
   };
+  // LDS column swizzle: col ^ 4 * ((row >> 1) & 3).  The transform stores put 8 tile rows x 4
+  // columns in each 32-lane group; with the plain pitch-48 layout rows 0, 2, 4, 6 hit the same
+  // 32-bank column (4-way conflicts on every store, more conflict cycles than LDS-active cycles
+  // in the r1 counters).  The MFMA operand reads stay conflict-free: the XOR only permutes
+  // columns inside each 16-aligned group.
+  const int cs = cl ^ (4 * ((tt >> 1) & 3));
   auto sstore = [&]() {
     float v[16];
 #pragma unroll
@@ -641,25 +647,35 @@ __global__ __launch_bounds__(256, 3) void wino_wgrad_kernel(WinoWArgs a) {
     zero_outside(rx, xmask);
     dy_transform(rdy, v);
 #pragma unroll
-    for (int xi = 0; xi < 16; ++xi) As[(xi * kCC + tt) * kP + cl] = v[xi];
+    for (int xi = 0; xi < 16; ++xi) As[(xi * kCC + tt) * kP + cs] = v[xi];
     in_transform(rx, v);
 #pragma unroll
-    for (int xi = 0; xi < 16; ++xi) Bs[(xi * kCC + tt) * kP + cl] = v[xi];
+    for (int xi = 0; xi < 16; ++xi) Bs[(xi * kCC + tt) * kP + cs] = v[xi];
   };
 
   f32x4 acc[16];
 #pragma unroll
   for (int xi = 0; xi < 16; ++xi) acc[xi] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const float* ap = As + g * kP + 16 * wm + l16;
-  const float* bp = Bs + g * kP + 16 * wn + l16;
+  // operand rows 4s + g of every xi block: swizzle 4 * ((2s + (g >> 1)) & 3) per k-step s
+  const int sw0 = 4 * ((g >> 1) & 3), sw1 = 4 * ((2 + (g >> 1)) & 3);
+  const float* ap0 = As + g * kP + ((16 * wm + l16) ^ sw0);
+  const float* ap1 = As + g * kP + ((16 * wm + l16) ^ sw1);
+  const float* bp0 = Bs + g * kP + ((16 * wn + l16) ^ sw0);
+  const float* bp1 = Bs + g * kP + ((16 * wn + l16) ^ sw1);
   if (ch_beg < ch_end) gload(ch_beg);
   for (int ch = ch_beg; ch < ch_end; ++ch) {
     if (ch != ch_beg) __syncthreads();
     sstore();
     __syncthreads();
     if (ch + 1 < ch_end) gload(ch + 1);
-    mfma_chunk<false>(ap, bp, acc);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) {
+        const int ro = (xi * kCC + 4 * s) * kP;
+        acc[xi] = __builtin_amdgcn_mfma_f32_16x16x4f32(s ? ap1[ro] : ap0[ro], s ? bp1[ro] : bp0[ro], acc[xi], 0, 0, 0);
+      }
   }
 
   // epilogue: row = co, column = ci; dW = A'^T M A', A'^T = [[1,1,1,0],[0,1,-1,0],[0,1,1,-1]]
