@@ -193,6 +193,9 @@ __device__ __forceinline__ void f2_stage2_wino(const MnistFused& f, const Scratc
 #pragma unroll
       for (int q = 0; q < 4; ++q) bn[q] = up[(2 * xp + 2 + (q >> 1)) * 128 + 64 * (q & 1)];
     }
+    // keep the next pair's loads here: the scheduler otherwise sinks them into this pair's MFMAs
+    // and waits for L2 (vmcnt) inside the pair
+    __builtin_amdgcn_sched_barrier(0);
     acc[2 * xp] = f32x4{0.f, 0.f, 0.f, 0.f};
     acc[2 * xp + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
     const float* a = tile + 2 * xp * 512 + g * 16 + m;
@@ -333,12 +336,19 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
   }
   __syncthreads();
   MX_TRACE(f, 0, 2);
-  if (f.a1_pub) {  // publish the a1 rows this block owns (2, or 4 for the last row) for F6W
-    const int nr = py == 11 ? 4 : 2, per = nr * 26;
+  if (f.a1_pub) {  // publish the a1 rows this block owns (2, or 4 for the last row) for F6W:
+    // per channel they are 52 (104) contiguous, 16-byte aligned floats of a1 -> float4 stores
+    const int n4 = py == 11 ? 26 : 13;
     float* dst = f.a1 + (size_t)b * 21632 + row0 * 26;
-    for (int i = tid; i < 32 * per; i += 256) {
-      const int ci = i / per, rem = i - ci * per, qr = rem / 26, qc = rem - 26 * qr;
-      dst[ci * 676 + qr * 26 + qc] = tile[ci * kF2ChP + qr * kF2RowP + qc];
+    for (int i = tid; i < 32 * n4; i += 256) {
+      const int ci = i / n4, k = i - ci * n4;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int p = 4 * k + e, qr = p / 26, qc = p - 26 * qr;
+        v[e] = tile[ci * kF2ChP + qr * kF2RowP + qc];
+      }
+      *reinterpret_cast<float4*>(dst + ci * 676 + 4 * k) = make_float4(v[0], v[1], v[2], v[3]);
     }
   }
   MX_TRACE(f, 0, 3);
