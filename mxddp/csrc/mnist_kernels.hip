@@ -129,7 +129,12 @@ __global__ __launch_bounds__(256) void k_init(MnistFused f, Scratch sc) {
   if (gtid < 64) f.g[L::b2 + gtid] = 0.f;
 }
 
-constexpr int kF2RowP = 40, kF2ChP = 176;  // F2 a1 tile pitches (see f2_fwd_kernel)
+// F2 a1 tile pitches (row 38, channel 141): picked by an exhaustive bank model (32-lane groups,
+// bank = dword mod 32) over the two access patterns that dominate F2W's LDS time -- the conv1
+// MFMA stores (16 channels x 2 position groups per 32 lanes) and the stage-2 input-transform
+// reads (3 channels x 12 tiles): 1,472 -> 576 LDS cycles per block (40 / 176 had 8-way store
+// conflicts).  The direct-GEMM variant (MXDDP_MNIST_F2=direct) shares them.
+constexpr int kF2RowP = 38, kF2ChP = 141;
 
 // F2W stage 2 (see f2_fwd_kernel): a1 tile [32 ci][4 rows][26] (pitches kF2ChP / kF2RowP) in
 // `tile` -> pooled conv2 outputs of pooled row py of image b.
@@ -247,8 +252,7 @@ __device__ __forceinline__ void f2_stage2_wino(const MnistFused& f, const Scratc
 // (m = 4*window + 2*dy + dx), so a lane's 4 accumulator registers are exactly one 2x2 pooling
 // window: max-pool + argmax happen in registers.  K = 288 ordered k = r*32 + ci (r = ky*3+kx)
 // so the im2col LDS offset splits into a per-lane base + a compile-time immediate.  The tile
-// [32 ci][4 rows][26] has row pitch 40 and channel pitch 176 (= 8, 16 mod 32 banks): the 32
-// lanes of each ds_read_b32 half-wave hit 32 distinct banks.  B fragments for all 72 k-steps
+// [32 ci][4 rows][26] has row pitch kF2RowP and channel pitch kF2ChP (see their definition).  B fragments for all 72 k-steps
 // (18 float4 per lane, pre-packed by the previous SGD) are loaded once into registers.
 //
 // kWino (default; MXDDP_MNIST_F2=direct selects the above): stage 2 as Winograd F(2x2,3x3).  The
