@@ -9,7 +9,11 @@
 // Block = 256 threads = 4 waves in a WM x WN grid; block tile BM x BN, k-tile BK.
 // Operand tiles are staged global -> registers -> LDS (k-major, rows padded so the
 // two 16-lane groups of a ds_read_b32 half-wave hit disjoint banks), double-buffered
-// with one barrier per k-tile.  Each wave owns (BM/WM) x (BN/WN) outputs as
+// with one barrier per k-tile.  Columns are XOR-swizzled by (k & 14): an operand gathered
+// k-fast (weights along K, dy along pixels) stores 16 k-rows x 2 columns per 32-lane group,
+// and with the 16-mod-32 row pitch the even rows shared one bank (8-way conflicts: the
+// counters showed 2-4x more conflict cycles than LDS-active cycles); the XOR only permutes
+// columns inside each 16-aligned group, so the MFMA operand reads stay conflict-free.  Each wave owns (BM/WM) x (BN/WN) outputs as
 // TM x TN MFMA 16x16 accumulators.  fp32 in, fp32 accumulate: exact fp32 numerics
 // (gfx950 has no xf32), at the f32 matrix rate.
 //
@@ -74,11 +78,12 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(Op op, int k_split_len) 
       rb[i] = (k < kend) ? op.b_load(bpre[i], k) : 0.f;
     }
   };
+  static_assert(BK <= 16, "column swizzle assumes k-tile rows < 16");
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < EA; ++i) As[buf][a_kl[i] * LDA + a_ml[i]] = ra[i];
+    for (int i = 0; i < EA; ++i) As[buf][a_kl[i] * LDA + (a_ml[i] ^ (a_kl[i] & 14))] = ra[i];
 #pragma unroll
-    for (int i = 0; i < EB; ++i) Bs[buf][b_kl[i] * LDB + b_nl[i]] = rb[i];
+    for (int i = 0; i < EB; ++i) Bs[buf][b_kl[i] * LDB + (b_nl[i] ^ (b_kl[i] & 14))] = rb[i];
   };
 
   f32x4 acc[TM][TN];
@@ -91,8 +96,9 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(Op op, int k_split_len) 
   gload(kbeg);
   sstore(0);
   __syncthreads();
-  const int a_off = (lane >> 4) * LDA + wm * (BM / WM) + (lane & 15);
-  const int b_off = (lane >> 4) * LDB + wn * (BN / WN) + (lane & 15);
+  const int g = lane >> 4, l16 = lane & 15;
+  const int a_off = g * LDA + wm * (BM / WM);
+  const int b_off = g * LDB + wn * (BN / WN);
   for (int t = 0; t < nt; ++t) {
     const int cur = t & 1;
     if (t + 1 < nt) gload(kbeg + (t + 1) * BK);
@@ -100,11 +106,12 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(Op op, int k_split_len) 
     const float* bs = &Bs[cur][b_off];
 #pragma unroll
     for (int kk = 0; kk < BK / 4; ++kk) {
+      const int lx = l16 ^ ((4 * kk + (g & 2)) & 14);  // swizzled column of k-row 4kk + g
       float a[TM], b[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = as[kk * 4 * LDA + i * 16];
+      for (int i = 0; i < TM; ++i) a[i] = as[kk * 4 * LDA + i * 16 + lx];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = bs[kk * 4 * LDB + j * 16];
+      for (int j = 0; j < TN; ++j) b[j] = bs[kk * 4 * LDB + j * 16 + lx];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
