@@ -71,6 +71,7 @@ class DistributedDataParallel(nn.Module):
                                                          first_bucket_cap_mb)
         self.average = average
         self._comm = _comm.rccl_comm() if self.device.type == "cuda" else None
+        self.transport = "rccl" if self.device.type == "cuda" else "gloo"
         self._sync_params()
         if self.device.type == "cuda":
             C = native()
@@ -122,7 +123,18 @@ class DistributedDataParallel(nn.Module):
             C = native()
             self._comm.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), C.DType.f32, 0,
                                  torch.cuda.current_stream(self.device).cuda_stream)
-        elif t.is_cuda:  # ranks sharing a GPU: no RCCL, broadcast through the gloo control plane
+        elif t.is_cuda and self.transport == "peer":
+            # ranks sharing a GPU (no RCCL): broadcast = peer all-reduce of (rank 0 ? t : 0), exact
+            # in fp32 and, unlike a host round trip, capturable into a hipGraph
+            from . import peer as _peer
+
+            pc = _peer.peer_comm()
+            if self.rank != 0:
+                t.zero_()
+            C = native()
+            pc.all_reduce(t.data_ptr(), t.numel(), C.DType.f32, torch.cuda.current_stream(self.device).cuda_stream,
+                          C.RedOp.sum)
+        elif t.is_cuda:  # before the transport is chosen (wrap time): through the gloo control plane
             h = t.cpu()
             dist.broadcast(h, 0)
             t.copy_(h)
