@@ -43,6 +43,10 @@ class ReplicaGroup:
                 raise ValueError("replica mode across several devices needs GPUs")
             self.comms = native().Comm.init_all([d.index for d in self.devices])
         self._sync(self.flats[0].data, [f.data for f in self.flats])
+        if self.n > 1:  # raw-pointer write to the replicas' weights: banked conv filters are stale
+            from .. import ops
+
+            ops.invalidate_filters()
         if self.buffers and self.buffers[0] is not None:
             self._sync(self.buffers[0], self.buffers)
 
