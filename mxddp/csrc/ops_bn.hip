@@ -16,6 +16,8 @@
 //
 // Replaces (reference): cuDNN BatchNorm fwd-training / bwd reached from pytorch/model.py:27,30,
 // 33,64,74 (PyramidNet) -- SURVEY §2.4.
+#include <cstdlib>
+
 #include "common.h"
 #include "ops.h"
 
@@ -277,6 +279,172 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_apply_slice_k(
 }
 
 
+// ------------------------------------------------------------------ one block per channel
+// For small per-channel counts the split design's two launches (statistics, then the
+// elementwise pass) cost more than the work: one block of kBnF threads owns a whole channel,
+// reduces it (pass 1), derives the coefficients and applies them (pass 2, the channel's bytes
+// are still in L2).  No partials, no second launch; the block reduction is a fixed-shape tree
+// (deterministic).  Used for the PyramidNet stage-2 / stage-3 BNs (up to 16 K values per
+// channel), where the grid still has one block per channel (106..271 channels).
+constexpr int kBnF = 512;
+
+__device__ __forceinline__ float2 block_sum2_f(float a, float b, float* red) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[2 * w] = a;
+    red[2 * w + 1] = b;
+  }
+  __syncthreads();
+  float2 t = make_float2(0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < kBnF / 64; ++k) {
+    t.x += red[2 * k];
+    t.y += red[2 * k + 1];
+  }
+  __syncthreads();
+  return t;
+}
+
+// HW % 4 == 0 (float4 path only); element e of the channel: image e / HW4, float4 e % HW4
+__global__ __launch_bounds__(kBnF) void bn_fwd_fused_k(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, float* __restrict__ y,
+                                                      float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                                                      float* __restrict__ run_mean, float* __restrict__ run_var, int N,
+                                                      int C, int HW, FastDiv dv, float eps, float momentum, int relu,
+                                                      int64_t* __restrict__ num_batches, const float* __restrict__ res,
+                                                      int Cr) {
+  __shared__ float red[2 * kBnF / 64];
+  const int c = blockIdx.x, hw4 = HW >> 2, total = N * hw4;
+  if (c == 0 && num_batches && threadIdx.x == 0) *num_batches += 1;
+  const float K = x[(size_t)c * HW];  // shift: x[0, c, 0, 0]
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  float s1 = 0.f, s2 = 0.f;
+  for (int i = threadIdx.x; i < total; i += kBnF) {
+    const int n = (int)dv.div(i), j = i - n * hw4;
+    const float4 v = x4[((size_t)n * C + c) * hw4 + j];
+    const float p = v.x - K, q = v.y - K, r = v.z - K, t = v.w - K;
+    s1 += (p + q) + (r + t);
+    s2 = fmaf(p, p, fmaf(q, q, fmaf(r, r, fmaf(t, t, s2))));
+  }
+  const float2 st = block_sum2_f(s1, s2, red);
+  const float cnt = (float)N * (float)HW;
+  const float m1 = st.x / cnt;
+  const float var = fmaxf(st.y / cnt - m1 * m1, 0.f);
+  const float mu = K + m1, inv = rsqrtf(var + eps);
+  const float sc = inv * (gamma ? gamma[c] : 1.f);
+  const float sh = (beta ? beta[c] : 0.f) - mu * sc;
+  if (threadIdx.x == 0) {
+    mean_out[c] = mu;
+    invstd_out[c] = inv;
+    if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
+    if (run_var) run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
+  }
+  const float4* r4 = (res && c < Cr) ? reinterpret_cast<const float4*>(res + (size_t)c * HW) : nullptr;
+  float4* y4 = reinterpret_cast<float4*>(y);
+  for (int i = threadIdx.x; i < total; i += kBnF) {
+    const int n = (int)dv.div(i), j = i - n * hw4;
+    const size_t o = ((size_t)n * C + c) * hw4 + j;
+    float4 v = x4[o];
+    v.x = fmaf(v.x, sc, sh);
+    v.y = fmaf(v.y, sc, sh);
+    v.z = fmaf(v.z, sc, sh);
+    v.w = fmaf(v.w, sc, sh);
+    if (relu) {
+      v.x = fmaxf(v.x, 0.f);
+      v.y = fmaxf(v.y, 0.f);
+      v.z = fmaxf(v.z, 0.f);
+      v.w = fmaxf(v.w, 0.f);
+    }
+    if (r4) {
+      const float4 rr = r4[(size_t)n * Cr * hw4 + j];
+      v.x += rr.x;
+      v.y += rr.y;
+      v.z += rr.z;
+      v.w += rr.w;
+    }
+    y4[o] = v;
+  }
+}
+
+__global__ __launch_bounds__(kBnF) void bn_bwd_fused_k(const float* __restrict__ dy, const float* __restrict__ x,
+                                                      const float* __restrict__ yr, const float* __restrict__ gamma,
+                                                      const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                      float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                      float* __restrict__ dx, int N, int C, int HW, FastDiv dv,
+                                                      int acc_params, const float* __restrict__ extra, int extC) {
+  __shared__ float red[2 * kBnF / 64];
+  const int c = blockIdx.x, hw4 = HW >> 2, total = N * hw4;
+  const float mu = mean[c], inv = invstd[c];
+  const float4* g4 = reinterpret_cast<const float4*>(dy);
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  const float4* y4 = reinterpret_cast<const float4*>(yr);
+  float s1 = 0.f, s2 = 0.f;
+  for (int i = threadIdx.x; i < total; i += kBnF) {
+    const int n = (int)dv.div(i), j = i - n * hw4;
+    const size_t o = ((size_t)n * C + c) * hw4 + j;
+    float4 g = g4[o];
+    const float4 v = x4[o];
+    if (yr) {
+      const float4 r = y4[o];
+      g.x = r.x > 0.f ? g.x : 0.f;
+      g.y = r.y > 0.f ? g.y : 0.f;
+      g.z = r.z > 0.f ? g.z : 0.f;
+      g.w = r.w > 0.f ? g.w : 0.f;
+    }
+    s1 += (g.x + g.y) + (g.z + g.w);
+    s2 = fmaf(g.x, v.x - mu, fmaf(g.y, v.y - mu, fmaf(g.z, v.z - mu, fmaf(g.w, v.w - mu, s2))));
+  }
+  const float2 t = block_sum2_f(s1, s2, red);
+  const float cnt = (float)N * (float)HW;
+  const float db = t.x, dg = t.y * inv;
+  const float k = (gamma ? gamma[c] : 1.f) * inv / cnt;
+  const float A = k * cnt, D = -k * dg * inv, Bc = -k * db + k * dg * inv * mu;
+  if (threadIdx.x == 0) {
+    if (dgamma) dgamma[c] = acc_params ? dgamma[c] + dg : dg;
+    if (dbeta) dbeta[c] = acc_params ? dbeta[c] + db : db;
+  }
+  const float4* e4 = extra ? reinterpret_cast<const float4*>(extra + (size_t)c * HW) : nullptr;
+  float4* d4 = reinterpret_cast<float4*>(dx);
+  for (int i = threadIdx.x; i < total; i += kBnF) {
+    const int n = (int)dv.div(i), j = i - n * hw4;
+    const size_t o = ((size_t)n * C + c) * hw4 + j;
+    float4 g = g4[o];
+    const float4 v = x4[o];
+    if (yr) {
+      const float4 r = y4[o];
+      g.x = r.x > 0.f ? g.x : 0.f;
+      g.y = r.y > 0.f ? g.y : 0.f;
+      g.z = r.z > 0.f ? g.z : 0.f;
+      g.w = r.w > 0.f ? g.w : 0.f;
+    }
+    float4 out;
+    out.x = fmaf(A, g.x, fmaf(D, v.x, Bc));
+    out.y = fmaf(A, g.y, fmaf(D, v.y, Bc));
+    out.z = fmaf(A, g.z, fmaf(D, v.z, Bc));
+    out.w = fmaf(A, g.w, fmaf(D, v.w, Bc));
+    if (e4) {
+      const float4 e = e4[(size_t)n * extC * hw4 + j];
+      out.x += e.x;
+      out.y += e.y;
+      out.z += e.z;
+      out.w += e.w;
+    }
+    d4[o] = out;
+  }
+}
+
+// per-channel blocks when the channel is small enough for one block and there are enough
+// channels to occupy the chip; MXDDP_BN_FUSED_MAX = per-channel value limit (0 disables)
+bool bn_use_fused(int N, int C, int HW) {
+  static const int64_t lim = [] {
+    const char* e = std::getenv("MXDDP_BN_FUSED_MAX");
+    return e ? (int64_t)std::atoll(e) : (int64_t)16384;
+  }();
+  return HW % 4 == 0 && (int64_t)N * HW <= lim && C >= 64;
+}
+
 }  // namespace
 
 int bn_splits(int N, int C, int HW) {
@@ -299,6 +467,11 @@ void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* 
   const int S = bn_splits(N, C, HW);
   MX_CHECK(S <= 4 * kBnTB, "bn: too many splits");
   MX_CHECK(!res || (Cr > 0 && Cr <= C), "bn: residual channels must be in 1..C");
+  if (bn_use_fused(N, C, HW)) {
+    MX_LAUNCH(bn_fwd_fused_k, dim3(C), dim3(kBnF), 0, st, x, gamma, beta, y, mean, invstd, run_mean, run_var, N, C,
+              HW, FastDiv(HW / 4), eps, momentum, relu ? 1 : 0, num_batches, res, Cr);
+    return;
+  }
   const bool vec = HW % 4 == 0;
   const FastDiv dv(vec ? HW / 4 : HW);
   const float cnt = (float)N * (float)HW;
@@ -320,6 +493,11 @@ void bn_bwd(const float* dy, const float* x, const float* y_relu, const float* g
   const int S = bn_splits(N, C, HW);
   MX_CHECK(S <= 4 * kBnTB, "bn: too many splits");
   MX_CHECK(!extra || extC >= C, "bn: extra gradient must have >= C channels");
+  if (bn_use_fused(N, C, HW)) {
+    MX_LAUNCH(bn_bwd_fused_k, dim3(C), dim3(kBnF), 0, st, dy, x, y_relu, gamma, mean, invstd, dgamma, dbeta, dx, N,
+              C, HW, FastDiv(HW / 4), accp ? 1 : 0, extra, extC);
+    return;
+  }
   const bool vec = HW % 4 == 0;
   const FastDiv dv(vec ? HW / 4 : HW);
   const float cnt = (float)N * (float)HW;
