@@ -1,0 +1,9 @@
+#!/bin/bash
+# MNIST A/B: current default vs an env override ($AB_ENV), engine tests, phases, bench.
+source "$(dirname "$0")/../gpu_check.sh"
+rm -f gpurun_out/steps.log
+run engine_tests 300 python -u -m pytest tests/test_gpu_engine.py -x -q --timeout 120 --timeout-method thread
+run phases 300 python scripts/phase_profile.py
+run bench 300 python bench.py --steps 2000 --warmup 100
+run bench_b 300 env $AB_ENV python bench.py --steps 2000 --warmup 100
+run bench2 300 python bench.py --steps 2000 --warmup 100

@@ -1,0 +1,8 @@
+#!/bin/bash
+source "$(dirname "$0")/../gpu_check.sh"
+rm -f gpurun_out/steps.log
+run pytest_nhwc 300 python -u -m pytest tests/test_gpu_nhwc.py -m gpu -v --timeout 120 --timeout-method thread
+run bench_rn 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3
+run bench_rn2 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3
+run prof_rn 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_rn -o run --output-format csv -- python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 4 --warmup 2
+run layers_rn 300 python scripts/bench_nhwc_layers.py 32 20
