@@ -2,7 +2,7 @@
 # Rank-count rehearsal on the one-GPU box: 4 and 8 ranks SHARE the GPU (peer transport only,
 # RCCL refuses duplicate GPUs) -- exercises the ws=4/8 code paths of bench.py (fused engine
 # autotune, layer-path DDP), not a scaling measurement.  Then the full GPU suite.
-source "$(dirname "$0")/../gpu_check.sh"
+source "$(dirname "$0")/gpu_check.sh"
 rm -f gpurun_out/steps.log
 TR="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
 run ws4_fused 300 $TR --nproc-per-node 4 --master-port 29561 bench.py --gpus 4 --steps 200 --warmup 20
