@@ -817,6 +817,13 @@ bool mnist_a1_publish() {
   }();
   return v == 1;
 }
+bool mnist_f5_sgd() {
+  static const int v = [] {
+    const char* e = std::getenv("MXDDP_F5_SGD");
+    return (e && std::string(e) == "0") ? 0 : 1;
+  }();
+  return v == 1;
+}
 bool mnist_f7_wino() {
   static const int v = [] {
     const char* e = std::getenv("MXDDP_MNIST_F7");

@@ -150,6 +150,13 @@ MnistFused MnistEngine::fused_args() const {
   f.seed = data_seed;
   f.trace = trace_;
   f.synth = external_batch_ ? 0 : 1;
+  // without gradient collectives F5 applies the fc1 weight update itself (no all-reduce has to
+  // come between the gradient and the update)
+  f.fc1_sgd = (variant_ == 1 && !reducer_->active() && mnist_f5_sgd()) ? 1 : 0;
+  f.mom = m_;
+  f.lr = lr_;
+  f.sgd_mom = momentum_;
+  f.sgd_wd = wd_;
   return f;
 }
 

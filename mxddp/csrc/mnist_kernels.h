@@ -26,8 +26,16 @@ struct MnistFused {
   uint32_t* trace;       // optional per-phase timestamps (s_memrealtime, 100 MHz) for profiling, or null
   int synth;             // 1: F2 generates the batch on device; 0: x/y provided by the caller
   int a1_pub;            // 1: F2 publishes conv1's output to a1 and F6W loads it (else F6W recomputes)
+  // fc1-weight SGD folded into F5 (no gradient collectives in the step): each F5 block updates
+  // the weight columns whose gradient it just produced (the gradient is not written to g), and
+  // the SGD launch skips them
+  int fc1_sgd;
+  float* mom;            // flat momentum buffer
+  const float* lr;       // device learning rate
+  float sgd_mom, sgd_wd;
 };
 bool mnist_a1_publish();  // default on; MXDDP_MNIST_A1=recompute turns it off
+bool mnist_f5_sgd();      // default on; MXDDP_F5_SGD=0 keeps the fc1 update in the SGD launch
 
 size_t mnist_fused_scratch_floats(int B);
 bool mnist_f7_wino();  // conv2 data gradient as Winograd (default) vs direct (MXDDP_MNIST_F7=direct)

@@ -477,6 +477,18 @@ __global__ __launch_bounds__(256) void f5_head_fc1_bwd_kernel(MnistFused f) {
   uint8_t* qs = reinterpret_cast<uint8_t*>(misc + 4);  // [B][48] argmax codes of this column slice
   const int c0 = blockIdx.x * kF5Cols;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  // folded fc1 SGD: this block owns weight columns c0..c0+47 of every row (old values in wsm);
+  // the momentum of this thread's dW1 elements is loaded with the prologue's loads
+  float mb[2][kF5NT][4];
+  if (f.fc1_sgd) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < kF5NT; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          mb[a][c][j] = f.mom[L::fw1 + (size_t)(32 * w + 16 * a + 4 * g + j) * 9216 + c0 + 16 * c + m];
+  }
   {  // all global loads in flight at once, then LDS stores
     constexpr int ND = B * 32 / 256, NP = (B * kF5C4 + 255) / 256, NW = (128 * kF5C4 + 255) / 256, N2 = 5;
     float4 vd[ND], vp[NP], vw[NW];
@@ -654,15 +666,33 @@ __global__ __launch_bounds__(256) void f5_head_fc1_bwd_kernel(MnistFused f) {
         }
       }
     }
+    if (!f.fc1_sgd) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+      for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int c = 0; c < kF5NT; ++c)
+        for (int c = 0; c < kF5NT; ++c)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int n = 32 * w + 16 * a + 4 * g + j;
-          f.g[L::fw1 + (size_t)n * 9216 + c0 + 16 * c + m] = acc[a][c][j];
-        }
+          for (int j = 0; j < 4; ++j) {
+            const int n = 32 * w + 16 * a + 4 * g + j;
+            f.g[L::fw1 + (size_t)n * 9216 + c0 + 16 * c + m] = acc[a][c][j];
+          }
+    } else {  // the gradient is consumed here (not materialised in g)  // the SGD kernel's update, same operation order (gscale = 1: world size 1)
+      const float lr = *f.lr;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < kF5NT; ++c)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int n = 32 * w + 16 * a + 4 * g + j;
+            const size_t e = L::fw1 + (size_t)n * 9216 + c0 + 16 * c + m;
+            float pv = wsm[n * kF5P + 16 * c + m];
+            const float bv = f.sgd_mom * mb[a][c][j] + (acc[a][c][j] + f.sgd_wd * pv);
+            pv -= lr * bv;
+            f.mom[e] = bv;
+            f.p[e] = pv;
+          }
+    }
   }
   MX_TRACE(f, 2, 5);
   // ---- dp tiles: rows b (M-tiles of 16, wave-strided), cols kF5NT N-tiles, K = 128.  The 48
@@ -729,7 +759,11 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
       h4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   constexpr int kW2a = (int)L::w2 / 4, kW2b = ((int)L::w2 + kPack) / 4;  // conv2 weights (float4 range)
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
+  constexpr int kF1a = (int)L::fw1 / 4, kF1n = ((int)L::fb1 - (int)L::fw1) / 4;  // fc1 weights (float4 range)
+  static_assert(L::fw1 % 4 == 0 && L::fb1 % 4 == 0, "fc1 weights must be float4-aligned");
+  const int skip = f.fc1_sgd ? kF1n : 0;  // fc1 updated by F5: iterate around it
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < n4 - skip; t += gridDim.x * 256) {
+    const int i = t >= kF1a ? t + skip : t;
     if (i >= kW2a && i < kW2b) continue;  // per (co, ci) pair below
     float4 pv = p4[i];
     float4 gv = g4[i];
@@ -886,11 +920,14 @@ void mnist_fused_fc1_bwd(const MnistFused& f, hipStream_t st) {
 
 void mnist_fused_sgd(const MnistFused& f, float* mom_buf, const float* lr, float gscale, float momentum, float wd,
                      hipStream_t st, bool finalize) {
+  MX_CHECK(!f.fc1_sgd || (finalize && gscale == 1.f && f.mom == mom_buf),
+           "fc1 SGD is folded into F5 only without gradient collectives");
+  const dim3 grid(f.fc1_sgd ? 128 : 1024);  // folded: ~20 K elements left (+ the 32 pair blocks)
   if (finalize)
-    MX_LAUNCH(sgd_pack_kernel<true>, dim3(1024), dim3(256), 0, st, f, carve(f.scratch), mom_buf, lr, gscale,
+    MX_LAUNCH(sgd_pack_kernel<true>, grid, dim3(256), 0, st, f, carve(f.scratch), mom_buf, lr, gscale,
               momentum, wd, !(f2_wino() && mnist_f7_wino()));
   else
-    MX_LAUNCH(sgd_pack_kernel<false>, dim3(1024), dim3(256), 0, st, f, carve(f.scratch), mom_buf, lr, gscale,
+    MX_LAUNCH(sgd_pack_kernel<false>, grid, dim3(256), 0, st, f, carve(f.scratch), mom_buf, lr, gscale,
               momentum, wd, !(f2_wino() && mnist_f7_wino()));
   MX_HIP_CHECK(hipGetLastError());
 }

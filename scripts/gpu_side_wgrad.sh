@@ -2,7 +2,7 @@
 # Conv weight gradients on a side stream (eager steps; operands held until the join): the
 # PyramidNet eager step first (it faulted with record_stream lifetimes), then numerics and A/B.
 source "$(dirname "$0")/gpu_check.sh"
-rm -f gpurun_out/steps.log
+
 run pyr_eager_side 300 python bench.py --model pyramidnet110 --impl layers --steps 20 --warmup 3 --no-graph
 run pyr_eager_side_long 300 python bench.py --model pyramidnet110 --impl layers --steps 100 --warmup 3 --no-graph
 run t_side 300 python -u -m pytest tests/test_gpu_parallel.py -m gpu -x -q --timeout 120 --timeout-method thread
