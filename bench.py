@@ -167,7 +167,7 @@ def main():
                        "image": "x".join(map(str, spec.input_shape)), "parallelism": f"dp{a.gpus}", "impl": a.impl,
                        # how the timed steps were actually launched (autotune may pick eager mode 0)
                        "graph": (a.impl == "fused" and tr.eng.graph_mode != 0) or getattr(a, "layers_graph", False),
-                       **({"graph_mode": tr.eng.graph_mode, "overlap": tr.eng.overlap,
+                       **({"graph_mode": tr.eng.graph_mode, "overlap": tr.eng.overlap, "merged_bucket": tr.eng.merged,
                            "transport": tr.active_transport, "force_collectives": a.force_collectives, "autotune": tr.tuned}
                           if a.impl == "fused" else {})},
             **extra,

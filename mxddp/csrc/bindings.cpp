@@ -372,6 +372,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_force_collectives", &MnistEngine::set_force_collectives)
       .def_property_readonly("graph_mode", &MnistEngine::graph_mode)
       .def("set_overlap", &MnistEngine::set_overlap)
+      .def("set_merged", &MnistEngine::set_merged)
+      .def_property_readonly("merged", &MnistEngine::merged)
       .def("set_peer", &MnistEngine::set_peer, py::arg("peer").none(true), py::keep_alive<1, 2>())
       .def_property_readonly("peer_active", &MnistEngine::peer_active)
       .def_property_readonly("overlap", &MnistEngine::overlap)

@@ -82,6 +82,10 @@ MnistEngine::MnistEngine(int batch, uintptr_t params, uintptr_t grads, uintptr_t
   };
   reducer_ = std::make_unique<Reducer>(comm_, reinterpret_cast<uintptr_t>(g_), DType::kF32, buckets,
                                        std::vector<int>{1, 1, 1, 1, 0, 0, 0, 0}, RedOp::kSum, false);
+  merged_reducer_ = std::make_unique<Reducer>(
+      comm_, reinterpret_cast<uintptr_t>(g_), DType::kF32, std::vector<Reducer::BucketSpec>{{0, MnistLayout::total}},
+      std::vector<int>(8, 0), RedOp::kSum, false);
+  merged_reducer_->set_overlap(false);  // issued at the end of the backward: nothing to overlap
   repack();
   MX_HIP_CHECK(hipStreamSynchronize(s_));
 }
@@ -112,6 +116,7 @@ void MnistEngine::uncapture() {
 MnistEngine::~MnistEngine() {
   uncapture();
   reducer_.reset();
+  merged_reducer_.reset();
   if (s_) hipStreamDestroy(s_);
 }
 
@@ -205,12 +210,13 @@ void MnistEngine::segment(int k) {
 }
 
 void MnistEngine::launch_step() {
-  reducer_->prepare();
+  Reducer& r = red();
+  r.prepare();
   segment(0);
-  reducer_->mark_bucket_ready(0, s_);  // fc grads all-reduce on the side stream ...
-  segment(1);                          // ... overlapped with the whole conv backward
-  reducer_->mark_bucket_ready(1, s_);
-  reducer_->finalize(s_);              // compute stream waits for the comm stream
+  if (!merged_) r.mark_bucket_ready(0, s_);  // fc grads all-reduce on the side stream ...
+  segment(1);                                // ... overlapped with the whole conv backward
+  r.mark_bucket_ready(merged_ ? 0 : 1, s_);
+  r.finalize(s_);                            // compute stream waits for the comm stream
   segment(2);
 }
 
@@ -276,12 +282,13 @@ void MnistEngine::replay(int n) {
     if (graph_mode_ == 1 && exec_) {
       MX_HIP_CHECK(hipGraphLaunch(exec_, s_));
     } else if (graph_mode_ == 2 && seg_exec_[0]) {
-      reducer_->prepare();
+      Reducer& r = red();
+      r.prepare();
       MX_HIP_CHECK(hipGraphLaunch(seg_exec_[0], s_));
-      reducer_->mark_bucket_ready(0, s_);
+      if (!merged_) r.mark_bucket_ready(0, s_);
       MX_HIP_CHECK(hipGraphLaunch(seg_exec_[1], s_));
-      reducer_->mark_bucket_ready(1, s_);
-      reducer_->finalize(s_);
+      r.mark_bucket_ready(merged_ ? 0 : 1, s_);
+      r.finalize(s_);
       MX_HIP_CHECK(hipGraphLaunch(seg_exec_[2], s_));
     } else {
       launch_step();

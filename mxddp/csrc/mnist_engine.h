@@ -55,6 +55,7 @@ class MnistEngine {
   void set_force_collectives(bool on) {
     if (on != reducer_->forced()) uncapture();
     reducer_->set_force_collectives(on);
+    merged_reducer_->set_force_collectives(on);
   }
   void set_overlap(bool on) { reducer_->set_overlap(on); }  // see Reducer::set_overlap
   // gradient transport: nullptr = RCCL, else the direct xGMI peer all-reduce (peer.h); drops
@@ -62,14 +63,23 @@ class MnistEngine {
   void set_peer(PeerComm* p) {
     if (p != reducer_->peer()) uncapture();
     reducer_->set_peer(p);
+    merged_reducer_->set_peer(p);
   }
+  // merged = true: ONE all-reduce over the whole gradient after the conv backward instead of
+  // the fc bucket (overlappable) + the conv bucket: one collective latency per step instead of
+  // two, no overlap.  Drops captured graphs.
+  void set_merged(bool on) {
+    if (on != merged_) uncapture();
+    merged_ = on;
+  }
+  bool merged() const { return merged_; }
   bool peer_active() const { return reducer_->peer() != nullptr; }
   // data-parallel degree: the RCCL communicator's, else the peer transport's (a peer-only job,
   // e.g. several ranks sharing one GPU in tests)
   int world_size() const {
     return comm_ ? comm_->world_size() : (reducer_->peer() ? reducer_->peer()->world_size() : 1);
   }
-  bool overlap() const { return reducer_->overlap(); }
+  bool overlap() const { return !merged_ && reducer_->overlap(); }
   bool reducer_active() const { return reducer_->active(); }
   void uncapture();  // drop captured graphs (back to eager; capture() may be called again)
   void forward_only(uintptr_t x, uintptr_t logits, int B);  // eval helper (no grads)
@@ -84,10 +94,11 @@ class MnistEngine {
   // in-kernel phase timestamps (MnistFused::trace); 0 = off.  Eager steps only: a captured
   // graph keeps the arguments it was captured with.
   void set_trace(uintptr_t buf) { trace_ = reinterpret_cast<uint32_t*>(buf); }
-  float last_comm_ms() { return reducer_ ? reducer_->last_comm_ms() : 0.f; }
+  float last_comm_ms() { return reducer_ ? red().last_comm_ms() : 0.f; }
   bool captured() const { return exec_ != nullptr || seg_exec_[0] != nullptr; }
 
  private:
+  Reducer& red() const { return merged_ ? *merged_reducer_ : *reducer_; }
   void launch_step();
   void segment(int k);
   MnistFused fused_args() const;
@@ -104,7 +115,9 @@ class MnistEngine {
   int32_t *y_, *idx_, *counter_;
   float *lr_, *metrics_;
   Comm* comm_;
-  std::unique_ptr<Reducer> reducer_;
+  std::unique_ptr<Reducer> reducer_;         // buckets [fc1.w .. fc2.b], [conv1.w .. conv2.b]
+  std::unique_ptr<Reducer> merged_reducer_;  // one bucket: the whole flat gradient
+  bool merged_ = false;
   uint64_t seed_;
   float momentum_, wd_;
   int variant_;

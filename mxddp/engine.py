@@ -128,9 +128,11 @@ class FusedMnistTrainer:
     def autotune(self, trial_steps: int = 24, include_graphs: bool | None = None) -> dict:
         """Pick the fastest launch strategy for the DDP step on THIS machine by timing a few real
         training steps of each (they count as warm-up).  Candidates: gradient transport (RCCL
-        ring, or the direct xGMI peer all-reduce when it validated) x (fc-bucket all-reduce
-        overlapped on the side stream, or in order on the compute stream) x (eager launches, or
-        the whole step captured in one hipGraph).  Peer-transport graphs are always tried (the
+        ring, or the direct xGMI peer all-reduce when it validated) x bucket strategy (fc-bucket
+        all-reduce overlapped on the side stream "ovl", the two buckets in order on the compute
+        stream "inl", or ONE all-reduce over the whole gradient after the conv backward "one":
+        one collective latency instead of two) x (eager launches, or the whole step captured in
+        one hipGraph).  Peer-transport graphs are always tried (the
         peer kernel is an ordinary kernel); RCCL-in-graph only with MXDDP_AUTOTUNE_GRAPHS=1.
         The slowest rank's time decides, so every rank picks the same strategy.  Returns
         {candidate: ms/step}."""
@@ -145,14 +147,14 @@ class FusedMnistTrainer:
             transports = [self.transport] if self.transport in transports else ["rccl"]
         cands = []
         for tr in transports:
-            cands += [(tr, 0, True), (tr, 0, False)]
+            cands += [(tr, 0, "ovl"), (tr, 0, "inl"), (tr, 0, "one")]
             if self.use_graph and (include_graphs or tr == "peer"):
-                cands += [(tr, 1, True), (tr, 1, False)]
+                cands += [(tr, 1, "ovl"), (tr, 1, "inl"), (tr, 1, "one")]
         results = {}
-        for tr, mode, ov in cands:
+        for tr, mode, strat in cands:
             self.eng.uncapture()
             self.eng.set_peer(self.peer if tr == "peer" else None)
-            self.eng.set_overlap(ov)
+            self._set_buckets(strat)
             failed = 0.0
             try:  # capture issues no collective, so a local failure here is safe to agree on
                 if mode:
@@ -163,7 +165,7 @@ class FusedMnistTrainer:
             # candidate that failed to capture on ANY rank is skipped by ALL ranks together
             if pc.all_reduce_max(failed) > 0:
                 self.eng.uncapture()
-                results[(tr, mode, ov)] = float("inf")
+                results[(tr, mode, strat)] = float("inf")
                 continue
             # replay errors are not swallowed: peers may already be inside the collectives
             self.eng.replay(2)
@@ -175,19 +177,24 @@ class FusedMnistTrainer:
             dt = pc.all_reduce_max(time.perf_counter() - t0)
             self._check_peer()
             self.steps += 2 + trial_steps
-            results[(tr, mode, ov)] = dt / trial_steps * 1e3
+            results[(tr, mode, strat)] = dt / trial_steps * 1e3
         best = min(results, key=results.get)
         self.eng.uncapture()
         self.eng.set_peer(self.peer if best[0] == "peer" else None)
-        self.eng.set_overlap(best[2])
+        self._set_buckets(best[2])
         if best[1]:
             self._capture(best[1])
         self._capture_done = True
         self.read_metrics(reset=True)
-        self.tuned = {"transport": best[0], "graph_mode": best[1], "overlap": best[2],
-                      "trials_ms": {f"{t}/{m}/{'ovl' if o else 'inl'}": round(v, 4)
-                                    for (t, m, o), v in results.items()}}
+        self.tuned = {"transport": best[0], "graph_mode": best[1], "buckets": best[2],
+                      "trials_ms": {f"{t}/{m}/{s}": round(v, 4) for (t, m, s), v in results.items()}}
         return results
+
+    def _set_buckets(self, strat: str):
+        """ovl: fc bucket overlapped on the side stream; inl: both buckets in order; one: a
+        single all-reduce of the whole gradient after the conv backward."""
+        self.eng.set_merged(strat == "one")
+        self.eng.set_overlap(strat == "ovl")
 
     def _check_peer(self):
         if self.peer is not None and self.peer.error():

@@ -74,10 +74,12 @@ def test_fused_engine_batch_sizes_match_reference(cuda, B):
         assert err < 1e-4, (B, k, err)
 
 
+@pytest.mark.parametrize("merged", [False, True])
 @pytest.mark.parametrize("graph", [0, 1, 2])
-def test_fused_engine_rccl_collectives_ws1(cuda, graph):
+def test_fused_engine_rccl_collectives_ws1(cuda, graph, merged):
     """The DDP path with REAL RCCL all-reduces (1-rank communicator, collectives forced):
-    eager, captured inside the step graph (mode 1) and issued between compute graphs (mode 2)."""
+    eager, captured inside the step graph (mode 1) and issued between compute graphs (mode 2);
+    two buckets, or one all-reduce over the whole gradient (merged)."""
     from mxddp import native
     from mxddp.engine import FusedMnistTrainer
     from mxddp.models import MnistCNN
@@ -89,6 +91,8 @@ def test_fused_engine_rccl_collectives_ws1(cuda, graph):
     B, steps = 32, 5
     tr = FusedMnistTrainer(batch=B, device=cuda, comm=comm, init_model=ref, use_graph=graph > 0,
                            graph_mode=graph if graph else None, force_collectives=True)
+    tr.eng.set_merged(merged)
+    assert tr.eng.merged == merged
     xs = [torch.rand(B, 1, 28, 28) for _ in range(steps)]
     ys = [torch.randint(0, 10, (B,)) for _ in range(steps)]
     losses = []
@@ -144,9 +148,9 @@ def test_fused_engine_autotune_keeps_training_exact(cuda):
     b = FusedMnistTrainer(batch=64, device=cuda, lr=0.01)
     a.step(1)
     res = a.autotune(trial_steps=4, include_graphs=True)
-    assert len(res) == 4 and a.tuned is not None
+    assert len(res) == 6 and a.tuned is not None  # {eager, graph} x {ovl, inl, one}
     a.step(10)
-    b.step(1 + 4 * (2 + 4) + 10)
+    b.step(1 + 6 * (2 + 4) + 10)
     assert a.steps == b.steps
     # same device-side data stream and update rule; only the (nondeterministic) order of the
     # fp32 split-K atomics differs between two engines, so allow rounding-level drift
