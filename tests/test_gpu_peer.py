@@ -94,6 +94,7 @@ def _ddp_layers_worker(rank, ws, port, q):
             ropt.step()
         torch.cuda.synchronize()
         d = (flat.data.cpu() - mine).abs().max().item()
+        print(f"ddp_layers: max |ddp - global batch| = {d:.3g}", flush=True)
         if not d < 1e-5:
             bad.append(("ddp != global batch", d, len(ddp.buckets)))
     q.put((rank, bad, ddp.transport))
