@@ -76,26 +76,38 @@ def validate(pc, rccl, dtype: str = "f32", numel: int = 1_181_066, iters: int = 
     dev = inf.device
     tdt = torch.float32 if dtype == "f32" else torch.bfloat16
     cdt = C.DType.f32 if dtype == "f32" else C.DType.bf16
-    ok = True
     st = torch.cuda.current_stream(dev).cuda_stream
     g = torch.Generator(device="cpu").manual_seed(1234 + inf.rank)
+    # a transport that does not work on this machine (flags never seen across the links) must
+    # not stall the job for the full 30 s training timeout per call: 2 s while validating
+    pc.set_timeout_ms(float(os.environ.get("MXDDP_PEER_VALIDATE_TIMEOUT_MS", "2000")))
+    try:
+        ok = _validate_iters(pc, rccl, C, dev, tdt, cdt, numel, iters, st, g, inf)
+    finally:
+        pc.set_timeout_ms(float(os.environ.get("MXDDP_PEER_TIMEOUT_MS", "30000")))
+    return _agree_ok(ok)
+
+
+def _validate_iters(pc, rccl, C, dev, tdt, cdt, numel, iters, st, g, inf) -> bool:
+    # every rank runs every iteration (no early exit): the RCCL calls must stay matched across
+    # ranks even when the peer transport fails on some of them
+    ok = True
     for _ in range(iters):
         x = torch.randn(numel, generator=g).to(dev, tdt)
         a, b = x.clone(), x.clone()
         pc.reset_error()
         pc.all_reduce(a.data_ptr(), numel, cdt, st)
         rccl.all_reduce(b.data_ptr(), b.data_ptr(), numel, cdt, C.RedOp.sum, st)
-        torch.cuda.synchronize(dev)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
         if pc.error():
             ok = False
-            break
-        tol = 1e-5 * inf.world_size if dtype == "f32" else 2e-2
+            continue
+        tol = 1e-5 * inf.world_size if tdt == torch.float32 else 2e-2
         err = (a.float() - b.float()).abs().max().item()
         scale = b.float().abs().max().item() + 1e-6
-        if not (err <= tol * scale):
-            ok = False
-            break
-    return _agree_ok(ok)
+        ok = ok and err <= tol * scale
+    return ok
 
 
 def pick_transport(pc, rccl, numels: list[int], dtype: str = "f32", iters: int = 10) -> tuple[str, dict]:
