@@ -1,6 +1,6 @@
 #!/bin/bash
 # F5 slice width 36 (256 blocks) vs 48 (192 blocks): engine numerics, interleaved A/B, trace.
-source "$(dirname "$0")/gpu_check.sh"
+source "$(dirname "$0")/../gpu_check.sh"
 rm -f gpurun_out/steps.log
 run eng 300 python -u -m pytest tests/test_gpu_engine.py -m gpu -x -q --timeout 120 --timeout-method thread
 run c36 300 python bench.py --steps 2000 --warmup 100

@@ -1,6 +1,6 @@
 #!/bin/bash
 # fc1 SGD folded into F5 (world size 1): engine numerics + interleaved A/B + kernel trace.
-source "$(dirname "$0")/gpu_check.sh"
+source "$(dirname "$0")/../gpu_check.sh"
 rm -f gpurun_out/steps.log
 run eng 300 python -u -m pytest tests/test_gpu_engine.py -m gpu -x -q --timeout 120 --timeout-method thread
 run m_fold 300 python bench.py --steps 2000 --warmup 100

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Conv weight gradients on a side stream (eager steps; operands held until the join): the
 # PyramidNet eager step first (it faulted with record_stream lifetimes), then numerics and A/B.
-source "$(dirname "$0")/gpu_check.sh"
+source "$(dirname "$0")/../gpu_check.sh"
 
 run pyr_eager_side 300 python bench.py --model pyramidnet110 --impl layers --steps 20 --warmup 3 --no-graph
 run pyr_eager_side_long 300 python bench.py --model pyramidnet110 --impl layers --steps 100 --warmup 3 --no-graph
