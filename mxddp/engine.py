@@ -119,7 +119,7 @@ class FusedMnistTrainer:
         if spg is None:
             spg = self.steps_per_graph
         if spg is None:
-            spg = int(os.environ.get("MXDDP_STEPS_PER_GRAPH", "8"))
+            spg = int(os.environ.get("MXDDP_STEPS_PER_GRAPH", "32"))
         if self._external:
             spg = 1  # a caller-provided batch is copied in before EVERY step
         self.eng.capture(mode, spg)
