@@ -39,24 +39,63 @@ __global__ void fill_k(float* __restrict__ y, float v, int64_t n) {
     y[i] = v;
 }
 
-// one block per channel; reduce over outer x inner
-__global__ void bias_grad_k(const float* __restrict__ dy, float* __restrict__ db, int outer, int C, int inner,
-                            int accumulate) {
+// Bias gradient db[c] = sum over (outer, inner) of dy[outer][C][inner], fixed summation order
+// (deterministic).  inner > 1 (conv): one 1024-thread block per channel, the flattened
+// (outer, inner) index split with a 32-bit magic division (a 64-bit divide per element made this
+// 17 us per call for the Keras CNN's conv1), eight loads in flight per thread.  inner == 1
+// (linear): a block covers 64 channels with its 4 waves taking every 4th row, partials combined
+// through LDS in a fixed order.
+constexpr int kBgTB = 1024, kBgU = 8;
+__global__ __launch_bounds__(kBgTB) void bias_grad_k(const float* __restrict__ dy, float* __restrict__ db, int outer,
+                                                     int C, int inner, FastDiv dv, int accumulate) {
   const int c = blockIdx.x;
-  float s = 0.f;
-  const int64_t total = (int64_t)outer * inner;
-  for (int64_t i = threadIdx.x; i < total; i += blockDim.x) {
-    const int64_t o = i / inner, in = i - o * inner;
-    s += dy[(o * C + c) * inner + in];
+  const int total = outer * inner;
+  float s[kBgU];
+#pragma unroll
+  for (int k = 0; k < kBgU; ++k) s[k] = 0.f;
+  int i = threadIdx.x;
+  for (; i + (kBgU - 1) * kBgTB < total; i += kBgU * kBgTB) {
+#pragma unroll
+    for (int k = 0; k < kBgU; ++k) {
+      const int j = i + k * kBgTB, o = (int)dv.div((uint32_t)j), in = j - o * inner;
+      s[k] += dy[((size_t)o * C + c) * inner + in];
+    }
   }
-  __shared__ float red[kTB / 64];
-  s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  for (; i < total; i += kBgTB) {
+    const int o = (int)dv.div((uint32_t)i), in = i - o * inner;
+    s[0] += dy[((size_t)o * C + c) * inner + in];
+  }
+  float t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  t = wave_sum(t);
+  __shared__ float red[kBgTB / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
   __syncthreads();
   if (threadIdx.x == 0) {
-    float t = 0.f;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
-    db[c] = accumulate ? db[c] + t : t;
+    float u = 0.f;
+#pragma unroll
+    for (int w = 0; w < kBgTB / 64; ++w) u += red[w];
+    db[c] = accumulate ? db[c] + u : u;
+  }
+}
+
+__global__ __launch_bounds__(256) void bias_grad_rows_k(const float* __restrict__ dy, float* __restrict__ db, int rows,
+                                                        int C, int accumulate) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = blockIdx.x * 64 + lane;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    int r = w;
+    for (; r + 12 < rows; r += 16) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s[k] += dy[(size_t)(r + 4 * k) * C + c];
+    }
+    for (; r < rows; r += 4) s[0] += dy[(size_t)r * C + c];
+  }
+  red[w][lane] = (s[0] + s[1]) + (s[2] + s[3]);
+  __syncthreads();
+  if (w == 0 && c < C) {
+    const float u = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    db[c] = accumulate ? db[c] + u : u;
   }
 }
 
@@ -265,7 +304,13 @@ void fill(float* y, float v, int64_t n, hipStream_t st) {
   MX_LAUNCH(fill_k, dim3(grid_for(n)), dim3(kTB), 0, st, y, v, n);
 }
 void bias_grad(const float* dy, float* db, int outer, int C, int inner, bool accumulate, hipStream_t st) {
-  MX_LAUNCH(bias_grad_k, dim3(C), dim3(kTB), 0, st, dy, db, outer, C, inner, accumulate ? 1 : 0);
+  MX_CHECK((int64_t)outer * inner < (1ll << 31), "bias_grad: reduction too large");
+  if (inner == 1) {
+    MX_LAUNCH(bias_grad_rows_k, dim3((C + 63) / 64), dim3(256), 0, st, dy, db, outer, C, accumulate ? 1 : 0);
+    return;
+  }
+  MX_LAUNCH(bias_grad_k, dim3(C), dim3(kBgTB), 0, st, dy, db, outer, C, inner, FastDiv((uint32_t)inner),
+            accumulate ? 1 : 0);
 }
 void maxpool2d_fwd(const float* x, float* y, int32_t* idx, int N, int C, int H, int W, int kh, int kw, int sh,
                    int sw, int ph, int pw, int P, int Q, hipStream_t st) {
