@@ -9,7 +9,7 @@
 // Block = 256 threads = 4 waves in a WM x WN grid; block tile BM x BN, k-tile BK.
 // Operand tiles are staged global -> registers -> LDS (k-major, rows padded so the
 // two 16-lane groups of a ds_read_b32 half-wave hit disjoint banks), double-buffered
-// with one barrier per k-tile.  Columns are XOR-swizzled by (k & 14): an operand gathered
+// with one barrier per k-tile; global loads run two k-tiles ahead (two register sets).  Columns are XOR-swizzled by (k & 14): an operand gathered
 // k-fast (weights along K, dy along pixels) stores 16 k-rows x 2 columns per 32-lane group,
 // and with the 16-mod-32 row pitch the even rows shared one bank (8-way conflicts: the
 // counters showed 2-4x more conflict cycles than LDS-active cycles); the XOR only permutes
@@ -65,8 +65,11 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(Op op, int k_split_len) 
     bpre[i] = op.b_pre(n0 + b_nl[i]);
   }
 
-  float ra[EA], rb[EB];
-  auto gload = [&](int k0) {
+  // two register sets of prefetched k-tiles: a tile's global loads are issued two k-tiles
+  // before it is stored to LDS (one k-tile of MFMAs was too little to cover the load latency
+  // on the long-K, few-block shapes: ~1 us per k-tile)
+  float ra0[EA], rb0[EB], ra1[EA], rb1[EB];
+  auto gload = [&](float (&ra)[EA], float (&rb)[EB], int k0) {
 #pragma unroll
     for (int i = 0; i < EA; ++i) {
       const int k = k0 + a_kl[i];
@@ -79,7 +82,7 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(Op op, int k_split_len) 
     }
   };
   static_assert(BK <= 16, "column swizzle assumes k-tile rows < 16");
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, const float (&ra)[EA], const float (&rb)[EB]) {
 #pragma unroll
     for (int i = 0; i < EA; ++i) As[buf][a_kl[i] * LDA + (a_ml[i] ^ (a_kl[i] & 14))] = ra[i];
 #pragma unroll
@@ -93,15 +96,10 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(Op op, int k_split_len) 
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nt = (kend - kbeg + BK - 1) / BK;
-  gload(kbeg);
-  sstore(0);
-  __syncthreads();
   const int g = lane >> 4, l16 = lane & 15;
   const int a_off = g * LDA + wm * (BM / WM);
   const int b_off = g * LDB + wn * (BN / WN);
-  for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nt) gload(kbeg + (t + 1) * BK);
+  auto mfma_tile = [&](int cur) {
     const float* as = &As[cur][a_off];
     const float* bs = &Bs[cur][b_off];
 #pragma unroll
@@ -118,8 +116,23 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(Op op, int k_split_len) 
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    if (t + 1 < nt) sstore(cur ^ 1);
+  };
+  gload(ra0, rb0, kbeg);
+  sstore(0, ra0, rb0);
+  __syncthreads();
+  if (nt > 1) gload(ra0, rb0, kbeg + BK);      // k-tile 1 -> set 0
+  if (nt > 2) gload(ra1, rb1, kbeg + 2 * BK);  // k-tile 2 -> set 1
+  // invariant at even t: LDS buffer 0 holds k-tile t, set 0 k-tile t + 1, set 1 k-tile t + 2
+  for (int t = 0; t < nt; t += 2) {
+    mfma_tile(0);
+    if (t + 1 < nt) sstore(1, ra0, rb0);
     __syncthreads();
+    if (t + 3 < nt) gload(ra0, rb0, kbeg + (t + 3) * BK);
+    if (t + 1 >= nt) break;
+    mfma_tile(1);
+    if (t + 2 < nt) sstore(0, ra1, rb1);
+    __syncthreads();
+    if (t + 4 < nt) gload(ra1, rb1, kbeg + (t + 4) * BK);
   }
 
   // C/D map of 16x16x4 f32: col = lane & 15, row = (lane >> 4) * 4 + reg.
