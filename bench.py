@@ -124,6 +124,8 @@ def main():
         if a.graph_mode is None and not a.no_autotune and tr.eng.reducer_active:
             tr.step(1)
             tr.autotune()  # untimed: a few real steps per candidate strategy, before the warm-up
+        if os.environ.get("MXDDP_WARM_GRAPHS", "1") == "1":
+            tr.warm_graphs()  # untimed: first launch of every captured graph (real steps)
     else:
         run = _layers_or_torch(a, torch, inf, dev, comm, B)
 
@@ -140,7 +142,7 @@ def main():
 
     if a.impl == "fused":
         loss_sum, correct = tr.read_metrics()
-        seen = (a.warmup + a.steps) * B
+        seen = max(1, (tr.steps - tr.steps_at_reset) * B)
         extra = {"train_loss_avg": loss_sum / seen, "train_acc": correct / seen}
     else:
         extra = {}

@@ -131,23 +131,25 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_wgrad_scratch_floats", &nhwc_wgrad_scratch_floats);
   m.def("nhwc_bn_fwd", [](uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t g, uintptr_t b, uintptr_t mean,
                           uintptr_t invstd, uintptr_t rm, uintptr_t rv, uintptr_t nbt, int Npix, int C, float mom,
-                          float eps, bool relu, uintptr_t scratch, uintptr_t st, uintptr_t coef_out) {
+                          float eps, bool relu, uintptr_t scratch, uintptr_t st, uintptr_t coef_out,
+                          uintptr_t mask_out) {
     nhwc_bn_fwd(P<const uint16_t>(x), P<const uint16_t>(res), P<uint16_t>(y), P<const float>(g), P<const float>(b),
                 P<float>(mean), P<float>(invstd), P<float>(rm), P<float>(rv), P<int64_t>(nbt), Npix, C, mom, eps, relu,
-                P<float>(scratch), S(st), P<float>(coef_out));
+                P<float>(scratch), S(st), P<float>(coef_out), P<uint8_t>(mask_out));
   }, py::arg("x"), py::arg("res"), py::arg("y"), py::arg("g"), py::arg("b"), py::arg("mean"), py::arg("invstd"),
      py::arg("rm"), py::arg("rv"), py::arg("nbt"), py::arg("Npix"), py::arg("C"), py::arg("mom"), py::arg("eps"),
-     py::arg("relu"), py::arg("scratch"), py::arg("st"), py::arg("coef_out") = 0);
+     py::arg("relu"), py::arg("scratch"), py::arg("st"), py::arg("coef_out") = 0, py::arg("mask_out") = 0);
   m.def("nhwc_bn_scratch_floats", &nhwc_bn_scratch_floats);
   m.def("nhwc_bn_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t y, uintptr_t g, uintptr_t mean, uintptr_t invstd,
                           uintptr_t dx, uintptr_t dres, uintptr_t dg, uintptr_t db, int Npix, int C, bool relu,
-                          bool accp, uintptr_t scratch, uintptr_t st, uintptr_t fcoef) {
+                          bool accp, uintptr_t scratch, uintptr_t st, uintptr_t fcoef, uintptr_t mask) {
     nhwc_bn_bwd(P<const uint16_t>(dy), P<const uint16_t>(x), P<const uint16_t>(y), P<const float>(g),
                 P<const float>(mean), P<const float>(invstd), P<uint16_t>(dx), P<uint16_t>(dres), P<float>(dg),
-                P<float>(db), Npix, C, relu, accp, P<float>(scratch), S(st), P<const float>(fcoef));
+                P<float>(db), Npix, C, relu, accp, P<float>(scratch), S(st), P<const float>(fcoef),
+                P<const uint8_t>(mask));
   }, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("g"), py::arg("mean"), py::arg("invstd"), py::arg("dx"),
      py::arg("dres"), py::arg("dg"), py::arg("db"), py::arg("Npix"), py::arg("C"), py::arg("relu"), py::arg("accp"),
-     py::arg("scratch"), py::arg("st"), py::arg("fcoef") = 0);
+     py::arg("scratch"), py::arg("st"), py::arg("fcoef") = 0, py::arg("mask") = 0);
   m.def("nhwc_maxpool_fwd", [](uintptr_t x, uintptr_t y, uintptr_t arg, int N, int H, int W, int C, int P_, int Q,
                                int k, int s, int p, uintptr_t st) {
     nhwc_maxpool_fwd(P<const uint16_t>(x), P<uint16_t>(y), P<uint8_t>(arg), N, H, W, C, P_, Q, k, s, p, S(st));
@@ -380,6 +382,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("reducer_active", &MnistEngine::reducer_active)
       .def("uncapture", &MnistEngine::uncapture)
       .def("replay", &MnistEngine::replay)
+      .def("warm_graphs", &MnistEngine::warm_graphs)
+      .def("set_small_first", &MnistEngine::set_small_first)
       .def("forward_only", &MnistEngine::forward_only)
       .def("repack", &MnistEngine::repack)
       .def("sync", &MnistEngine::sync, py::call_guard<py::gil_scoped_release>())

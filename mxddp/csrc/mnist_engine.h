@@ -49,6 +49,12 @@ class MnistEngine {
   // device memory, so every unrolled step is a distinct, correct training step).
   void capture(int mode = -1, int steps_per_graph = 1);
   void replay(int n);        // n steps via the captured graph(s) (eager if not captured)
+  // launch every captured graph once (real training steps; returns how many): untimed warm-up
+  // of graph execs that a replay would otherwise run for the first time
+  int warm_graphs();
+  // replay order of a step count that needs several graphs: full groups first, then the
+  // remainder graphs largest first (default), or the remainder smallest first (measured: no gain)
+  void set_small_first(bool on) { small_first_ = on; }
   int graph_mode() const { return graph_mode_; }
   // captured graphs bake in whether collectives run (and whether F8 folds into the SGD launch):
   // changing it drops them (eager until capture() is called again)
@@ -108,6 +114,7 @@ class MnistEngine {
   int graph_mode_ = 0;
   uint32_t* trace_ = nullptr;
   int steps_per_graph_ = 1;
+  bool small_first_ = false;
   void fwd(const float* x, float* logits_out, int B);
   int B_;
   float *p_, *g_, *m_;

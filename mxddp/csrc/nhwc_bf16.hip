@@ -58,6 +58,18 @@ __device__ __forceinline__ void unpack8(const uint4& u, float* f) {
 __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }
+// bit e set <=> bf16 element e of the packed vector is > 0 (unpack8 order): the ReLU mask of a
+// stored activation, 1/16 of its bytes
+__device__ __forceinline__ uint32_t pos_bits8(const uint4& u) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+  uint32_t b = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    b |= (uint32_t)((int16_t)(w[i] & 0xffffu) > 0) << (2 * i);
+    b |= (uint32_t)((int16_t)(w[i] >> 16) > 0) << (2 * i + 1);
+  }
+  return b;
+}
 // 8 bf16 c + 8 bf16 d, summed in fp32 and rounded once
 __device__ __forceinline__ u32x4 add8(u32x4 c, u32x4 d) {
   float x[8], y[8];
@@ -824,6 +836,8 @@ struct BnNArgs {
   int Npix, C, relu, gx, acc_params;
   const float* fcoef;  // bwd, ReLU without residual: the forward's [C][2] (scale, shift); the mask
                        // is then (x * scale + shift > 0) and y is not read (one tensor less)
+  uint8_t* mask;       // ReLU mask bits [Npix * C / 8] (bit e of byte i: element e of vector i > 0):
+                       // written by the forward apply, read by the backward instead of y
   float momentum, eps;
 };
 
@@ -850,13 +864,15 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
       }
     }
   }
-  const bool ymask = BWD && a.relu && !a.fcoef;
+  const bool ymask = BWD && a.relu && !a.fcoef && !a.mask;
+  const bool bmask = BWD && a.relu && !a.fcoef && a.mask;
   // UNR pixel rows per iteration with all their loads issued before any use: one 16-byte load
   // in flight per thread cannot cover HBM latency with ~256 blocks
   constexpr int UNR = BWD ? 2 : 4;
   const int pstep = gridDim.x * ppi;
   for (int p0 = blockIdx.x * ppi + pr; p0 < a.Npix; p0 += UNR * pstep) {
     uint4 xr[UNR], gr[UNR], yr[UNR];
+    uint32_t mb[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int p = p0 + u * pstep;
@@ -866,6 +882,7 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
       if (BWD) {
         gr[u] = ok ? *reinterpret_cast<const uint4*>(a.dy + o) : make_uint4(0u, 0u, 0u, 0u);
         if (ymask) yr[u] = ok ? *reinterpret_cast<const uint4*>(a.y + o) : make_uint4(0u, 0u, 0u, 0u);
+        if (bmask) mb[u] = ok ? a.mask[o >> 3] : 0u;
       }
     }
 #pragma unroll
@@ -883,7 +900,10 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
       } else {
         float g[8];
         unpack8(gr[u], g);
-        if (ymask) {
+        if (bmask) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) g[e] = (mb[u] >> e) & 1u ? g[e] : 0.f;
+        } else if (ymask) {
           float yv[8];
           unpack8(yr[u], yv);
 #pragma unroll
@@ -1054,7 +1074,9 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
         if (a.res) o += rv[e];
         xv[e] = a.relu ? fmaxf(o, 0.f) : o;
       }
-      reinterpret_cast<uint4*>(a.y)[i] = pack8(xv);
+      const uint4 yo = pack8(xv);
+      reinterpret_cast<uint4*>(a.y)[i] = yo;
+      if (a.mask) a.mask[i] = (uint8_t)pos_bits8(yo);
     }
   }
 }
@@ -1088,15 +1110,18 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv f
       mc[4 * j + 3] = q.w;
     }
   }
+  const bool bmask = !XM && a.relu && a.mask;
   for (int i0 = i00; i0 < total; i0 += 2 * step) {
     uint4 gr[2], xr[2], yr[2];
+    uint32_t mb[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int i = i0 + u * step;
       const bool ok = i < total;
       gr[u] = ok ? reinterpret_cast<const uint4*>(a.dy)[i] : z;
       xr[u] = ok ? reinterpret_cast<const uint4*>(a.x)[i] : z;
-      if (!XM && a.relu) yr[u] = ok ? reinterpret_cast<const uint4*>(a.y)[i] : z;
+      if (bmask) mb[u] = ok ? a.mask[i] : 0u;
+      else if (!XM && a.relu) yr[u] = ok ? reinterpret_cast<const uint4*>(a.y)[i] : z;
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -1108,6 +1133,9 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv f
       if (XM) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) g[e] = fmaf(xv[e], mc[2 * e], mc[2 * e + 1]) > 0.f ? g[e] : 0.f;
+      } else if (bmask) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = (mb[u] >> e) & 1u ? g[e] : 0.f;
       } else if (a.relu) {
         float yv[8];
         unpack8(yr[u], yv);
@@ -1539,7 +1567,8 @@ size_t nhwc_bn_scratch_floats(int Npix, int C) {
 
 void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* gamma, const float* beta,
                  float* mean, float* invstd, float* run_mean, float* run_var, int64_t* num_batches, int Npix, int C,
-                 float momentum, float eps, bool relu, float* scratch, hipStream_t st, float* coef_out) {
+                 float momentum, float eps, bool relu, float* scratch, hipStream_t st, float* coef_out,
+                 uint8_t* mask_out) {
   const int V = C / 8;
   MX_CHECK(C % 8 == 0 && C <= 2048 && (V >= kBnT ? V % kBnT == 0 : kBnT % V == 0),
            "nhwc bn: unsupported channel count");
@@ -1561,6 +1590,7 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
   a.gx = g.x;
   a.num_batches = num_batches;
   a.relu = relu;
+  a.mask = relu ? mask_out : nullptr;
   a.momentum = momentum;
   a.eps = eps;
   MX_LAUNCH(bn_nhwc_partial_k<false>, g, dim3(kBnT), 0, st, a);
@@ -1571,7 +1601,8 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
 
 void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma, const float* mean,
                  const float* invstd, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, int Npix, int C,
-                 bool relu, bool accumulate_params, float* scratch, hipStream_t st, const float* fcoef) {
+                 bool relu, bool accumulate_params, float* scratch, hipStream_t st, const float* fcoef,
+                 const uint8_t* mask) {
   const int V = C / 8;
   MX_CHECK(C % 8 == 0 && C <= 2048 && (V >= kBnT ? V % kBnT == 0 : kBnT % V == 0),
            "nhwc bn: unsupported channel count");
@@ -1595,6 +1626,8 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
   a.relu = relu;
   a.acc_params = accumulate_params;
   a.fcoef = (relu && fcoef && C <= 512) ? fcoef : nullptr;
+  a.mask = (relu && !a.fcoef) ? const_cast<uint8_t*>(mask) : nullptr;
+  MX_CHECK(!relu || a.fcoef || a.mask || y, "nhwc bn bwd: ReLU needs y, the forward's mask or its coefficients");
   MX_LAUNCH(bn_nhwc_partial_k<true>, g, dim3(kBnT), 0, st, a);
   MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");

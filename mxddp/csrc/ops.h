@@ -193,11 +193,12 @@ size_t nhwc_bn_scratch_floats(int Npix, int C);
 void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* gamma, const float* beta,
                  float* mean, float* invstd, float* run_mean, float* run_var, int64_t* num_batches, int Npix, int C,
                  float momentum, float eps, bool relu, float* scratch, hipStream_t st,
-                 float* coef_out = nullptr);  // coef_out: [C][2] (scale, shift) kept for nhwc_bn_bwd
+                 float* coef_out = nullptr,  // coef_out: [C][2] (scale, shift) kept for nhwc_bn_bwd
+                 uint8_t* mask_out = nullptr);  // ReLU mask bits [Npix * C / 8] for nhwc_bn_bwd
 void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma, const float* mean,
                  const float* invstd, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, int Npix, int C,
                  bool relu, bool accumulate_params, float* scratch, hipStream_t st,
-                 const float* fcoef = nullptr);  // fcoef: the forward's coef_out (ReLU, no residual,
+                 const float* fcoef = nullptr, const uint8_t* mask = nullptr);  // fcoef: the forward's coef_out (ReLU, no residual,
                                                  // C <= 512): mask from x, y not read
 void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, int k,
                       int s, int p, hipStream_t st);

@@ -1,6 +1,10 @@
 // Conv2d / Linear forward + backward as Ops of the MFMA implicit-GEMM engine.
 // NCHW fp32, arbitrary stride / padding / dilation and non-tile-multiple channel
 // counts (PyramidNet-110 has 103 distinct (C_in, C_out) pairs).
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
 #include "igemm.h"
 #include "igemm_bf16.h"
 #include "ops.h"
@@ -47,6 +51,8 @@ struct ConvFwdOp {
   const float* bias;
   float* y;
   bool relu;
+  float* part = nullptr;  // split-K: raw partial sums part[split][y index] (finished by splitk_finish_k)
+  int64_t ptotal = 0;
   struct APre { int64_t base; int h0, w0; bool ok; };
   struct BPre { int64_t base; bool ok; };
   __device__ APre a_pre(int m) const {
@@ -69,11 +75,16 @@ struct ConvFwdOp {
   }
   __device__ BPre b_pre(int n) const { return BPre{(int64_t)(n < N ? n : 0) * K, n < N}; }
   __device__ float b_load(const BPre& b, int k) const { return b.ok ? w[b.base + k] : 0.f; }
-  __device__ void store(int m, int n, float v, int) const {
+  __device__ void store(int m, int n, float v, int split) const {
     const int nb = g.fPQ.div(m), pq = m - nb * g.PQ;
+    const int64_t idx = ((int64_t)nb * g.K + n) * g.PQ + pq;
+    if (part) {
+      part[split * ptotal + idx] = v;
+      return;
+    }
     if (bias) v += bias[n];
     if (relu) v = fmaxf(v, 0.f);
-    y[((int64_t)nb * g.K + n) * g.PQ + pq] = v;
+    y[idx] = v;
   }
 };
 
@@ -240,6 +251,8 @@ struct LinFwdOp {  // y[M,N] = x[M,K] w[N,K]^T + b
   float* y;
   bool relu;
   int mode;
+  float* part = nullptr;  // split-K partials (see ConvFwdOp)
+  int64_t ptotal = 0;
   struct Pre { int64_t base; bool ok; };
   using APre = Pre;
   using BPre = Pre;
@@ -248,6 +261,10 @@ struct LinFwdOp {  // y[M,N] = x[M,K] w[N,K]^T + b
   __device__ Pre b_pre(int n) const { return Pre{(int64_t)(n < N ? n : 0) * K, n < N}; }
   __device__ float b_load(const Pre& p, int k) const { return p.ok ? w[p.base + k] : 0.f; }
   __device__ void store(int m, int n, float v, int split) const {
+    if (part) {
+      part[split * ptotal + (int64_t)m * N + n] = v;
+      return;
+    }
     if (b && split == 0) v += b[n];
     if (relu) v = fmaxf(v, 0.f);
     emit(y, (int64_t)m * N + n, v, mode);
@@ -263,14 +280,20 @@ struct LinDgradOp {  // dx[M,Kin] = dy[M,Nout] w[Nout,Kin]; GEMM N=Kin, K=Nout
   float* dx;
   const float* mask;
   int mode;
+  float* part = nullptr;  // split-K partials (see ConvFwdOp)
+  int64_t ptotal = 0;
   struct APre { int64_t base; bool ok; };
   struct BPre { int n; bool ok; };
   __device__ APre a_pre(int m) const { return APre{(int64_t)(m < M ? m : 0) * K, m < M}; }
   __device__ float a_load(const APre& a, int k) const { return a.ok ? dy[a.base + k] : 0.f; }
   __device__ BPre b_pre(int n) const { return BPre{n, n < N}; }
   __device__ float b_load(const BPre& b, int k) const { return b.ok ? w[(int64_t)k * N + b.n] : 0.f; }
-  __device__ void store(int m, int n, float v, int) const {
+  __device__ void store(int m, int n, float v, int split) const {
     const int64_t idx = (int64_t)m * N + n;
+    if (part) {
+      part[split * ptotal + idx] = v;
+      return;
+    }
     if (mask && !(mask[idx] > 0.f)) v = 0.f;
     emit(dx, idx, v, mode);
   }
@@ -299,6 +322,108 @@ template <class Op>
 void run(Op& op, int splits, hipStream_t st) {
   if (g_gemm_precision == 1) igemm_bf16_launch<Op, 64, 64, 32, 2, 2>(op, splits, st);
   else igemm_launch<Op, 64, 64, 16, 2, 2>(op, splits, st);
+}
+
+// ---------------------------------------------------------------- split-K with partial planes
+// Few output tiles over a long reduction (the Keras / MLP layers at batch 64: 9-25 tiles x
+// 36-63 k-tiles) leave most CUs idle and serialise the k-loop's load latency (~1 us per k-tile).
+// Such GEMMs run split-K: every split stores its raw partial sums to plane part[split][out
+// index], and splitk_finish_k sums the planes in a fixed order (deterministic) and applies the
+// epilogue (bias, ReLU, ReLU mask, accumulate).  The planes live in a grow-only per-device
+// buffer that only grows outside stream capture (a capture that would need more runs unsplit).
+int effective_splits(int K, int splits) {  // what igemm_*_launch will run (every split non-empty)
+  const int BK = g_gemm_precision == 1 ? 32 : 16;
+  if (splits <= 1) return 1;
+  const int klen = cdiv(cdiv(K, splits), BK) * BK;
+  return cdiv(K, klen);
+}
+
+float* splitk_planes(size_t floats, hipStream_t st) {
+  static std::mutex mu;
+  static std::vector<std::pair<float*, size_t>> bufs;
+  int dev = 0;
+  MX_HIP_CHECK(hipStreamGetDevice(st, &dev));
+  std::lock_guard<std::mutex> lk(mu);
+  if ((int)bufs.size() <= dev) bufs.resize(dev + 1, {nullptr, 0});
+  auto& b = bufs[dev];
+  if (b.second >= floats) return b.first;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  MX_HIP_CHECK(hipStreamIsCapturing(st, &cs));
+  if (cs != hipStreamCaptureStatusNone) return nullptr;
+  int cur = 0;
+  MX_HIP_CHECK(hipGetDevice(&cur));
+  MX_HIP_CHECK(hipSetDevice(dev));
+  if (b.first) {  // earlier launches may still read the old planes
+    MX_HIP_CHECK(hipDeviceSynchronize());
+    MX_HIP_CHECK(hipFree(b.first));
+  }
+  const size_t n = std::max(floats, 2 * b.second);
+  MX_HIP_CHECK(hipMalloc(&b.first, n * sizeof(float)));
+  b.second = n;
+  MX_HIP_CHECK(hipSetDevice(cur));
+  return b.first;
+}
+
+// out[i] = epilogue(sum_s part[s][i]); bias channel of i = (i / inner) % C
+__global__ void splitk_finish_k(const float* __restrict__ part, int splits, int total, float* __restrict__ out,
+                                const float* __restrict__ bias, int C, int inner, int relu,
+                                const float* __restrict__ mask, int accumulate) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    // four independent partial sums (loads in flight together), combined in a fixed order
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int sp = 0;
+    for (; sp + 4 <= splits; sp += 4) {
+      a0 += part[(int64_t)sp * total + i];
+      a1 += part[(int64_t)(sp + 1) * total + i];
+      a2 += part[(int64_t)(sp + 2) * total + i];
+      a3 += part[(int64_t)(sp + 3) * total + i];
+    }
+    for (; sp < splits; ++sp) a0 += part[(int64_t)sp * total + i];
+    float v = (a0 + a1) + (a2 + a3);
+    if (bias) v += bias[(i / inner) % C];
+    if (relu) v = fmaxf(v, 0.f);
+    if (mask && !(mask[i] > 0.f)) v = 0.f;
+    if (accumulate) v += out[i];
+    out[i] = v;
+  }
+}
+
+// Split factor for a GEMM of `tiles` output tiles over K: only when the tiles alone leave the
+// chip mostly idle and each split keeps >= 64 reduction elements (4 f32 k-tiles).
+bool partial_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("MXDDP_SPLITK_PARTIAL");
+    return !(e && std::string(e) == "0");
+  }();
+  return on;
+}
+
+int partial_splits(int tiles, int K) {
+  if (tiles >= 192 || K < 128 || !partial_enabled()) return 1;
+  return pick_splits(tiles, K, 64, 512);
+}
+
+// Runs `op` split-K into partial planes and finishes into `out` (total outputs); false if no
+// split applies or no planes are available (the caller then runs it unsplit).
+template <class Op>
+bool run_partial(Op& op, int64_t total, float* out, const float* bias, int C, int inner, bool relu,
+                 const float* mask, bool accumulate, hipStream_t st) {
+  const int tiles = cdiv(op.M, 64) * cdiv(op.N, 64);
+  // <= ~1 M partial floats (a plane per split is written and read once more by the finish
+  // pass) and <= max(16, total / 256) planes (each finish thread sums the planes of one output:
+  // MNIST fc1's 8 K outputs over 128 planes left the finish 32 blocks with long loops, 13 us)
+  const int cap = (int)std::max<int64_t>(
+      2, std::min<int64_t>((1 << 20) / std::max<int64_t>(total, 1), std::max<int64_t>(16, total / 256)));
+  const int splits = effective_splits(op.K, std::min(cap, partial_splits(tiles, op.K)));
+  if (splits <= 1 || total >= (1ll << 31) || total * splits > (1ll << 28)) return false;
+  float* part = splitk_planes((size_t)total * splits, st);
+  if (!part) return false;
+  op.part = part;
+  op.ptotal = total;
+  run(op, splits, st);
+  MX_LAUNCH(splitk_finish_k, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 1024)), dim3(256), 0, st,
+            part, splits, (int)total, out, bias, C, inner, relu ? 1 : 0, mask, accumulate ? 1 : 0);
+  return true;
 }
 
 }  // namespace
@@ -388,6 +513,8 @@ void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, con
     return run(op, 1, st);
   }
   ConvFwdOp op{s.N * s.P * s.Q, s.K, s.C * s.R * s.S, ConvG(s), x, w, bias, y, relu};
+  if (run_partial(op, (int64_t)s.N * s.K * s.P * s.Q, y, bias, s.K, s.P * s.Q, relu, nullptr, false, st)) return;
+  op.part = nullptr;
   run(op, 1, st);
 }
 
@@ -411,6 +538,8 @@ void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s
               wt_scratch, s.K, s.C, s.R * s.S);
     const ConvShape t = ConvShape::make(s.N, s.K, s.P, s.Q, s.C, s.R, s.S, 1, 1, s.R - 1 - s.pad_h, s.S - 1 - s.pad_w);
     ConvFwdOp op{t.N * t.P * t.Q, t.K, t.C * t.R * t.S, ConvG(t), dy, wt_scratch, nullptr, dx, false};
+    if (run_partial(op, (int64_t)t.N * t.K * t.P * t.Q, dx, nullptr, 1, 1, false, nullptr, false, st)) return;
+    op.part = nullptr;
     return run(op, 1, st);
   }
   if (is_1x1_s1(s)) {
@@ -432,7 +561,7 @@ void conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s
   if (g_gemm_precision == 0 && conv3x3_wgrad_eligible(s)) return conv3x3_wgrad(dy, x, dw, s, accumulate, st);
   ConvWgradOp op{s.K, s.C * s.R * s.S, s.N * s.P * s.Q, ConvG(s), dy, x, dw, kAtomic};
   const int tiles = cdiv(op.M, 64) * cdiv(op.N, 64);
-  const int splits = pick_splits(tiles, op.K, 512, 768);
+  const int splits = pick_splits(tiles, op.K, tiles < 64 ? 128 : 512, 768);
   if (splits == 1) {
     op.mode = accumulate ? kAccum : kStore;
   } else if (!accumulate) {
@@ -444,6 +573,8 @@ void conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s
 void linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int N, int K,
                 bool relu, hipStream_t st) {
   LinFwdOp op{M, N, K, x, w, b, y, relu, kStore};
+  if (run_partial(op, (int64_t)M * N, y, b, N, 1, relu, nullptr, false, st)) return;
+  op.part = nullptr;
   const int tiles = cdiv(M, 64) * cdiv(N, 64);
   int splits = relu ? 1 : pick_splits(tiles, K, 256, 256);
   if (splits > 1) {
@@ -457,6 +588,8 @@ void linear_dgrad(const float* dy, const float* w, float* dx, int M, int N, int 
                   const float* relu_mask, bool accumulate, hipStream_t st) {
   // GEMM view: M x K(out=Kin) reduction over N(out features)
   LinDgradOp op{M, K, N, dy, w, dx, relu_mask, accumulate ? kAccum : kStore};
+  if (run_partial(op, (int64_t)M * K, dx, nullptr, 1, 1, false, relu_mask, accumulate, st)) return;
+  op.part = nullptr;
   run(op, 1, st);
 }
 

@@ -74,6 +74,8 @@ class FusedMnistTrainer:
             self.eng.set_force_collectives(True)
         self.stream = torch.cuda.ExternalStream(self.eng.stream, device=self.device)
         self.steps = 0
+        self.steps_at_reset = 0  # self.steps when the device metrics were last zeroed
+        self.eng.set_small_first(os.environ.get("MXDDP_SMALL_FIRST", "0") == "1")
         self.world_size = comm.world_size if comm is not None else (peer.world_size if peer is not None else 1)
         # gradient transport (world size > 1): RCCL, or the direct xGMI peer all-reduce
         # (parallel/peer.py) -- validated against RCCL on every rank before it may be used;
@@ -106,6 +108,16 @@ class FusedMnistTrainer:
         if n > 0:
             self.eng.replay(n)
             self.steps += n
+
+    def warm_graphs(self) -> int:
+        """Launch every captured multi-step graph once (untimed warm-up; they are real training
+        steps, counted in self.steps): a replay whose step count needs a graph never launched
+        before would otherwise pay that graph's first-launch cost.  Returns the steps run."""
+        if self.use_graph and not self._capture_done:
+            self.step(1)
+        n = self.eng.warm_graphs()
+        self.steps += n
+        return n
 
     def _default_mode(self) -> int:
         # MXDDP_GRAPH_MODE: 0 = eager launches, 1 = whole step(s) incl. RCCL collectives in one
@@ -248,6 +260,7 @@ class FusedMnistTrainer:
             with torch.cuda.stream(self.stream):
                 self.metrics.zero_()
             self.eng.sync()
+            self.steps_at_reset = self.steps
         return m[0], m[1]
 
     def phase_profile(self, steps: int = 20) -> dict:

@@ -280,9 +280,8 @@ class _Linear(torch.autograd.Function):
         N = w.shape[0]
         y = torch.empty((M, N), device=x.device, dtype=x.dtype)
         st = stream_of(x)
-        C.linear_fwd(x2.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), M, N, K, False, st)
-        if relu:
-            C.relu_fwd(y.data_ptr(), y.data_ptr(), y.numel(), st)
+        # ReLU in the GEMM epilogue (or in the split-K finish pass)
+        C.linear_fwd(x2.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), M, N, K, bool(relu), st)
         ctx.relu = relu
         ctx.has_bias = b is not None
         ctx.bias_ref = b

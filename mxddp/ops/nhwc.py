@@ -216,11 +216,15 @@ class _BN(torch.autograd.Function):
         # ReLU without residual: keep the affine coefficients, the backward rebuilds the mask from x
         fcoef = torch.empty((2 * C,), device=x.device, dtype=torch.float32) if (relu and res is None and C <= 512) \
             else None
+        # any other ReLU: the forward stores its mask as bits (1/16 of y's bytes), read by the
+        # backward's two passes instead of y
+        mask = torch.empty((npix * C // 8,), device=x.device, dtype=torch.uint8) if (relu and fcoef is None) else None
         Cn.nhwc_bn_fwd(x.data_ptr(), _p(res), y.data_ptr(), _p(gamma), _p(beta), mean.data_ptr(), invstd.data_ptr(),
                        _p(rm), _p(rv), _p(nbt), npix, C, float(momentum), float(eps), bool(relu), scr.data_ptr(),
-                       stream_of(x), _p(fcoef))
+                       stream_of(x), _p(fcoef), _p(mask))
         ctx.fcoef = fcoef
-        ctx.save_for_backward(x, y, gamma, mean, invstd)
+        ctx.mask = mask
+        ctx.save_for_backward(x, gamma, mean, invstd)
         ctx.relu, ctx.has_res = bool(relu), res is not None
         ctx.join = join
         ctx.refs = (gamma, beta)
@@ -229,7 +233,7 @@ class _BN(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         Cn = native()
-        x, y, gamma, mean, invstd = ctx.saved_tensors
+        x, gamma, mean, invstd = ctx.saved_tensors
         N, H, W, C = x.shape
         dy = dy.contiguous()
         dx = torch.empty_like(x)
@@ -239,9 +243,9 @@ class _BN(torch.autograd.Function):
         direct = gs is not None and bs is not None
         dg, db = (gs, bs) if direct else (torch.empty((C,), device=x.device), torch.empty((C,), device=x.device))
         scr = torch.empty((Cn.nhwc_bn_scratch_floats(N * H * W, C),), device=x.device, dtype=torch.float32)
-        Cn.nhwc_bn_bwd(dy.data_ptr(), x.data_ptr(), y.data_ptr(), _p(gamma), mean.data_ptr(), invstd.data_ptr(),
+        Cn.nhwc_bn_bwd(dy.data_ptr(), x.data_ptr(), 0, _p(gamma), mean.data_ptr(), invstd.data_ptr(),
                        dx.data_ptr(), _p(dres), dg.data_ptr(), db.data_ptr(), N * H * W, C, ctx.relu, direct,
-                       scr.data_ptr(), stream_of(dy), _p(ctx.fcoef))
+                       scr.data_ptr(), stream_of(dy), _p(ctx.fcoef), _p(ctx.mask))
         if direct:
             dg = db = None
         if ctx.join is not None and dres is not None:

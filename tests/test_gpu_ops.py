@@ -32,6 +32,10 @@ CONV_CASES = [
     # Winograd F(2x2,3x3) path (winograd.hip): split-C grid (8x8, many channels), partial tile blocks
     (16, 191, 8, 8, 196, 3, 3, 1, 1),
     (4, 101, 16, 16, 106, 3, 3, 1, 1),
+    # few output tiles over a long reduction: split-K into partial planes + finish pass
+    # (forward and the flipped-filter data gradient), small-tile weight-gradient splits
+    (64, 64, 5, 5, 64, 3, 3, 1, 0),      # keras conv3
+    (16, 32, 13, 13, 64, 3, 3, 1, 0),    # keras conv2
 ]
 
 
@@ -47,14 +51,17 @@ def test_conv2d_fwd_bwd(cuda, case, relu):
     x = torch.randn(N, C, H, W)
     w = torch.randn(K, C, R, S) * 0.1
     b = torch.randn(K)
+    xg, wg, bg = (t.to(cuda).requires_grad_() for t in (x, w, b))
+    y = ops.conv2d(xg, wg, bg, st, pd, relu=relu)
     xr, wr, br = (t.clone().requires_grad_() for t in (x, w, b))
     yr = F.conv2d(xr, wr, br, st, pd)
     if relu:
-        yr = F.relu(yr)
+        # the reference takes the kernel's ReLU mask: an output within rounding of 0 may go either
+        # way, and a flipped mask element would move dx / dw by a whole gradient term
+        assert _rel(y.detach().cpu(), F.relu(yr.detach())) < 1e-4
+        yr = yr * (y.detach().cpu() > 0)
     gy = torch.randn_like(yr)
     yr.backward(gy)
-    xg, wg, bg = (t.to(cuda).requires_grad_() for t in (x, w, b))
-    y = ops.conv2d(xg, wg, bg, st, pd, relu=relu)
     y.backward(gy.to(cuda))
     torch.cuda.synchronize()
     assert _rel(y.cpu(), yr.detach()) < 1e-4
@@ -105,7 +112,8 @@ def test_winograd_vs_direct_fp64(cuda, case):
         assert e_w < 2e-5 and e_w < 8 * e_d + 1e-6, errs
 
 
-@pytest.mark.parametrize("M,N,K", [(64, 128, 9216), (64, 10, 128), (100, 1000, 784), (7, 33, 65)])
+@pytest.mark.parametrize("M,N,K", [(64, 128, 9216), (64, 10, 128), (100, 1000, 784), (7, 33, 65), (64, 64, 576),
+                                   (64, 1000, 1000)])
 def test_linear_fwd_bwd(cuda, M, N, K):
     torch.manual_seed(1)
     x, w, b = torch.randn(M, K), torch.randn(N, K) * 0.05, torch.randn(N)
@@ -121,6 +129,25 @@ def test_linear_fwd_bwd(cuda, M, N, K):
     assert _rel(xg.grad.cpu(), xr.grad) < 1e-4
     assert _rel(wg.grad.cpu(), wr.grad) < 1e-4
     assert _rel(bg.grad.cpu(), br.grad) < 1e-4
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 1000, 1000), (64, 128, 9216), (5, 70, 300)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_linear_dgrad_mask_accumulate(cuda, M, N, K, accumulate):
+    """dx (+)= (dy @ w) * (mask > 0): split-K partial planes finish with mask and accumulate."""
+    from mxddp import native
+
+    torch.manual_seed(3)
+    dy, w = torch.randn(M, N), torch.randn(N, K) * 0.05
+    mask = torch.randn(M, K).clamp_min(0)  # ~half the entries masked
+    dx0 = torch.randn(M, K)
+    ref = (dy @ w) * (mask > 0) + (dx0 if accumulate else 0)
+    dyg, wg, mg = dy.to(cuda), w.to(cuda), mask.to(cuda)
+    dx = dx0.to(cuda) if accumulate else torch.full((M, K), float("nan"), device=cuda)
+    st = torch.cuda.current_stream(cuda).cuda_stream
+    native().linear_dgrad(dyg.data_ptr(), wg.data_ptr(), dx.data_ptr(), M, N, K, mg.data_ptr(), accumulate, st)
+    torch.cuda.synchronize()
+    assert _rel(dx.cpu(), ref) < 1e-4
 
 
 @pytest.mark.parametrize("k,s,p,ceil", [(2, 2, 0, False), (3, 2, 1, False), (2, 2, 0, True)])

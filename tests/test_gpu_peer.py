@@ -95,7 +95,11 @@ def _ddp_layers_worker(rank, ws, port, q):
         torch.cuda.synchronize()
         d = (flat.data.cpu() - mine).abs().max().item()
         print(f"ddp_layers: max |ddp - global batch| = {d:.3g}", flush=True)
-        if not d < 1e-5:
+        # 3 SGD steps of a ReLU + max-pool net from two different summation orders (per-rank
+        # batches averaged vs one global batch): an activation within rounding of a ReLU / pool
+        # decision may go either way and move a weight by ~1e-4; a real reducer error (a bucket
+        # missed, wrong averaging) moves them by lr * grad ~ 1e-2
+        if not d < 5e-4:
             bad.append(("ddp != global batch", d, len(ddp.buckets)))
     q.put((rank, bad, ddp.transport))
     PC.shutdown()
