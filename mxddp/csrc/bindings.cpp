@@ -198,10 +198,11 @@ PYBIND11_MODULE(_C, m) {
     avgpool2d_bwd(P<const float>(dy), P<float>(dx), N, C, H, W, kh, kw, sh, sw, ph, pw, P_, Q, S(st));
   });
   m.def("xent_fwd_bwd", [](uintptr_t logits, uintptr_t y, uintptr_t logp, uintptr_t dlogits, uintptr_t loss_sum,
-                           uintptr_t correct, int B, int C, float scale, uintptr_t st) {
+                           uintptr_t correct, int B, int C, float scale, uintptr_t st, float loss_scale) {
     xent_fwd_bwd(P<const float>(logits), P<const int32_t>(y), P<float>(logp), P<float>(dlogits), P<float>(loss_sum),
-                 P<float>(correct), B, C, scale, S(st));
-  });
+                 P<float>(correct), B, C, scale, S(st), loss_scale);
+  }, py::arg("logits"), py::arg("y"), py::arg("logp"), py::arg("dlogits"), py::arg("loss_sum"), py::arg("correct"),
+     py::arg("B"), py::arg("C"), py::arg("scale"), py::arg("st"), py::arg("loss_scale") = 1.f);
   m.def("bn_splits", &bn_splits);
   m.def("bn_fwd_train", [](uintptr_t x, uintptr_t g, uintptr_t b, uintptr_t y, uintptr_t mean, uintptr_t invstd,
                            uintptr_t rm, uintptr_t rv, int N, int C, int HW, float mom, float eps, bool relu,

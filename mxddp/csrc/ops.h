@@ -130,8 +130,10 @@ void avgpool2d_bwd(const float* dy, float* dx, int N, int C, int H, int W, int k
 //  logits [B,C] -> loss_sum (atomic += sum of -logp[y]), correct (atomic += #argmax==y),
 //  dlogits = (softmax - onehot) * grad_scale  (if dlogits != nullptr), logp (optional).
 // `probs_input`=true treats logits as already-softmaxed probabilities (Keras softmax head).
+// loss_scale multiplies each row's loss before the sum (1 / B: loss_sum is the mean).
 void xent_fwd_bwd(const float* logits, const int32_t* y, float* logp, float* dlogits,
-                  float* loss_sum, float* correct, int B, int C, float grad_scale, hipStream_t st);
+                  float* loss_sum, float* correct, int B, int C, float grad_scale, hipStream_t st,
+                  float loss_scale = 1.f);
 
 // BatchNorm2d (training): batch stats, running-stat update, normalise (+ optional ReLU).
 // Split reduction (ops_bn.hip): S x C workgroups write partial sums to `part`

@@ -184,7 +184,7 @@ __global__ void avgpool_bwd_k(const float* __restrict__ dy, float* __restrict__ 
 // One wave per row.
 __global__ void xent_k(const float* __restrict__ logits, const int32_t* __restrict__ y, float* __restrict__ logp,
                        float* __restrict__ dlogits, float* __restrict__ loss_sum, float* __restrict__ correct,
-                       int B, int C, float scale) {
+                       int B, int C, float scale, float loss_scale) {
   const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= B) return;
@@ -215,7 +215,7 @@ __global__ void xent_k(const float* __restrict__ logits, const int32_t* __restri
       dlogits[(int64_t)row * C + c] = (pr - (c == label ? 1.f : 0.f)) * scale;
     }
   if (lane == 0) {
-    if (loss_sum) atomicAdd(loss_sum, lse - lr[label]);
+    if (loss_sum) atomicAdd(loss_sum, (lse - lr[label]) * loss_scale);
     if (correct) atomicAdd(correct, am == label ? 1.f : 0.f);
   }
 }
@@ -335,10 +335,10 @@ void avgpool2d_bwd(const float* dy, float* dx, int N, int C, int H, int W, int k
                      kh, kw, sh, sw, ph, pw, P, Q);
 }
 void xent_fwd_bwd(const float* logits, const int32_t* y, float* logp, float* dlogits, float* loss_sum,
-                  float* correct, int B, int C, float grad_scale, hipStream_t st) {
+                  float* correct, int B, int C, float grad_scale, hipStream_t st, float loss_scale) {
   const int rows_per_block = 4;
   MX_LAUNCH(xent_k, dim3(cdiv(B, rows_per_block)), dim3(64 * rows_per_block), 0, st, logits, y, logp,
-                     dlogits, loss_sum, correct, B, C, grad_scale);
+                     dlogits, loss_sum, correct, B, C, grad_scale, loss_scale);
 }
 void bn_fwd_eval(const float* x, const float* gamma, const float* beta, float* y, const float* rm, const float* rv,
                  int N, int C, int HW, float eps, bool relu, hipStream_t st) {

@@ -47,18 +47,21 @@ class Bottleneck(nn.Module):
     def forward_nhwc(self, x, pack=None):
         from ..ops import nhwc as N
 
-        join = None
-        if self.downsample is None:
-            # identity shortcut: its gradient is added inside conv1's data-gradient epilogue
-            join = N.GradJoin()
-            x, idt = N.fork(x, join)
-        else:
-            dc, dbn = self.downsample[0], self.downsample[1]
-            idt = N.batch_norm(N.conv2d(x, dc.weight, dc.stride, dc.padding, pack), dbn)
+        # the shortcut's input gradient is added inside conv1's data-gradient epilogue: the
+        # identity gradient left by bn3's backward, or the projection conv's data gradient.  The
+        # projection branch is built AFTER the main branch so its backward nodes carry the higher
+        # sequence numbers and autograd runs them first (its dx exists when conv1's dgrad runs).
+        join = N.GradJoin()
+        x, xs = N.fork(x, join)
         out = N.batch_norm(N.conv2d(x, self.conv1.weight, pack=pack, join=join), self.bn1, relu=True)
         out = N.batch_norm(N.conv2d(out, self.conv2.weight, self.conv2.stride, self.conv2.padding, pack), self.bn2,
                            relu=True)
-        return N.batch_norm(N.conv2d(out, self.conv3.weight, pack=pack), self.bn3, relu=True, res=idt, join=join)
+        out = N.conv2d(out, self.conv3.weight, pack=pack)
+        if self.downsample is None:
+            return N.batch_norm(out, self.bn3, relu=True, res=xs, join=join)
+        dc, dbn = self.downsample[0], self.downsample[1]
+        idt = N.batch_norm(N.conv2d(xs, dc.weight, dc.stride, dc.padding, pack, deposit=join), dbn)
+        return N.batch_norm(out, self.bn3, relu=True, res=idt)
 
 
 class ResNet(nn.Module):

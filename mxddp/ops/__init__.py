@@ -562,14 +562,16 @@ class _CrossEntropy(torch.autograd.Function):
         logits = logits.contiguous()
         _check(logits, "logits")
         B, K = logits.shape
-        tgt = target.to(torch.int32).contiguous()
+        # int32 targets are used as they are (no cast launch); the kernel sums loss / B, so the
+        # mean needs no division launch
+        tgt = (target if target.dtype == torch.int32 else target.to(torch.int32)).contiguous()
         acc = torch.zeros(2, device=logits.device, dtype=torch.float32)
         dl = torch.empty_like(logits)
         C.xent_fwd_bwd(logits.data_ptr(), tgt.data_ptr(), 0, dl.data_ptr(), acc.data_ptr(), acc.data_ptr() + 4,
-                       B, K, 1.0 / B, stream_of(logits))
+                       B, K, 1.0 / B, stream_of(logits), 1.0 / B)
         ctx.save_for_backward(dl)
         ctx.mark_non_differentiable(acc)
-        return acc[0] / B, acc[1]
+        return acc[0], acc[1]
 
     @staticmethod
     def backward(ctx, dloss, _dcorrect):

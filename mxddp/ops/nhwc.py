@@ -97,9 +97,11 @@ class WeightPack:
 
 class GradJoin:
     """Joins the two input-gradient branches of a residual block without a separate add: the
-    block's last batch norm (whose ``res`` is the identity shortcut) leaves its shortcut gradient
-    here, and the block's first convolution adds it in its data-gradient epilogue
-    (``nhwc_conv_dgrad(..., addend)``).  ``fork`` then passes that sum through unchanged."""
+    shortcut branch leaves its input gradient here -- the block's last batch norm (whose ``res``
+    is the identity shortcut), or the projection shortcut's convolution (``conv2d(..., deposit=)``)
+    -- and the block's first convolution adds it in its data-gradient epilogue
+    (``nhwc_conv_dgrad(..., addend)``).  ``fork`` then passes that sum through unchanged.  If the
+    first convolution's backward runs before the shortcut's, nothing is joined and ``fork`` adds."""
 
     def __init__(self):
         self.dres = None
@@ -133,7 +135,7 @@ def fork(x, join: GradJoin):
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad, packed=None, join=None):
+    def forward(ctx, x, w, stride, pad, packed=None, join=None, deposit=None):
         Cn = native()
         N, H, W, Cp = x.shape
         K, C, R, S = w.shape
@@ -155,6 +157,7 @@ class _Conv(torch.autograd.Function):
                          _p(scr), st)
         ctx.wtd = wtd
         ctx.join = join
+        ctx.deposit = deposit
         ctx.save_for_backward(x, w)
         ctx.geom = (N, H, W, Cp, K, C, R, S, sh, sw, ph, pw, P, Q)
         return y
@@ -183,6 +186,8 @@ class _Conv(torch.autograd.Function):
                                _p(scr), st, _p(add))
             if add is not None:
                 j.consumed = True
+            if ctx.deposit is not None:
+                ctx.deposit.dres = dx  # picked up by the block's first conv (see GradJoin)
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(w)
             dw = sink if sink is not None else torch.empty_like(w)
@@ -192,15 +197,17 @@ class _Conv(torch.autograd.Function):
                                P, Q, sink is not None, part.data_ptr(), st)
             if sink is not None:
                 dw = None
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
-def conv2d(x, w, stride=1, padding=0, pack: WeightPack | None = None, join: GradJoin | None = None):
+def conv2d(x, w, stride=1, padding=0, pack: WeightPack | None = None, join: GradJoin | None = None,
+           deposit: GradJoin | None = None):
     """bf16 NHWC convolution; ``pack`` supplies weights already repacked by WeightPack.refresh(),
-    ``join`` (see ``fork``) adds a residual block's shortcut gradient to this conv's input gradient."""
+    ``join`` (see ``fork``) adds a residual block's shortcut gradient to this conv's input gradient,
+    ``deposit`` leaves this conv's input gradient in that join (a projection shortcut)."""
     s = (stride, stride) if isinstance(stride, int) else tuple(stride)
     p = (padding, padding) if isinstance(padding, int) else tuple(padding)
-    return _Conv.apply(x, w, s, p, pack.get(w) if pack is not None else None, join)
+    return _Conv.apply(x, w, s, p, pack.get(w) if pack is not None else None, join, deposit)
 
 
 class _BN(torch.autograd.Function):
