@@ -109,10 +109,13 @@ PYBIND11_MODULE(_C, m) {
     nhwc_repack_many(P<const int64_t>(desc), n, total_blocks, S(st));
   });
   m.def("nhwc_conv_fwd", [](uintptr_t x, uintptr_t wt, uintptr_t y, int N, int H, int W, int Cp, int K, int R, int S_,
-                            int sh, int sw, int ph, int pw, int P_, int Q, uintptr_t scratch, uintptr_t st) {
-    nhwc_conv_fwd(P<const uint16_t>(x), P<const uint16_t>(wt), P<uint16_t>(y), N, H, W, Cp, K, R, S_, sh, sw, ph, pw,
-                  P_, Q, P<float>(scratch), S(st));
-  });
+                            int sh, int sw, int ph, int pw, int P_, int Q, uintptr_t scratch, uintptr_t st,
+                            uintptr_t bnpart, uintptr_t bnshift) {
+    return nhwc_conv_fwd(P<const uint16_t>(x), P<const uint16_t>(wt), P<uint16_t>(y), N, H, W, Cp, K, R, S_, sh, sw,
+                         ph, pw, P_, Q, P<float>(scratch), S(st), P<float>(bnpart), P<const float>(bnshift));
+  }, py::arg("x"), py::arg("wt"), py::arg("y"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cp"), py::arg("K"),
+     py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("P"), py::arg("Q"),
+     py::arg("scratch"), py::arg("st"), py::arg("bnpart") = 0, py::arg("bnshift") = 0);
   m.def("nhwc_conv_scratch_floats", &nhwc_conv_scratch_floats);
   m.def("nhwc_conv_dgrad", [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int N, int H, int W, int C, int K, int R,
                               int S_, int sh, int sw, int ph, int pw, int P_, int Q, uintptr_t scratch,
@@ -132,13 +135,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_bn_fwd", [](uintptr_t x, uintptr_t res, uintptr_t y, uintptr_t g, uintptr_t b, uintptr_t mean,
                           uintptr_t invstd, uintptr_t rm, uintptr_t rv, uintptr_t nbt, int Npix, int C, float mom,
                           float eps, bool relu, uintptr_t scratch, uintptr_t st, uintptr_t coef_out,
-                          uintptr_t mask_out) {
+                          uintptr_t mask_out, uintptr_t pre_part, int pre_gx, uintptr_t kshift) {
     nhwc_bn_fwd(P<const uint16_t>(x), P<const uint16_t>(res), P<uint16_t>(y), P<const float>(g), P<const float>(b),
                 P<float>(mean), P<float>(invstd), P<float>(rm), P<float>(rv), P<int64_t>(nbt), Npix, C, mom, eps, relu,
-                P<float>(scratch), S(st), P<float>(coef_out), P<uint8_t>(mask_out));
+                P<float>(scratch), S(st), P<float>(coef_out), P<uint8_t>(mask_out), P<const float>(pre_part), pre_gx,
+                P<const float>(kshift));
   }, py::arg("x"), py::arg("res"), py::arg("y"), py::arg("g"), py::arg("b"), py::arg("mean"), py::arg("invstd"),
      py::arg("rm"), py::arg("rv"), py::arg("nbt"), py::arg("Npix"), py::arg("C"), py::arg("mom"), py::arg("eps"),
-     py::arg("relu"), py::arg("scratch"), py::arg("st"), py::arg("coef_out") = 0, py::arg("mask_out") = 0);
+     py::arg("relu"), py::arg("scratch"), py::arg("st"), py::arg("coef_out") = 0, py::arg("mask_out") = 0,
+     py::arg("pre_part") = 0, py::arg("pre_gx") = 0, py::arg("kshift") = 0);
   m.def("nhwc_bn_scratch_floats", &nhwc_bn_scratch_floats);
   m.def("nhwc_bn_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t y, uintptr_t g, uintptr_t mean, uintptr_t invstd,
                           uintptr_t dx, uintptr_t dres, uintptr_t dg, uintptr_t db, int Npix, int C, bool relu,

@@ -100,6 +100,11 @@ struct ConvNArgs {
   int par, Hc, Wc;
   const bf16* addend;  // data gradient: added to the result in the epilogue ([M][Ng], or null) -- a
                        // residual block's two input-gradient branches joined without another pass
+  // forward feeding a training BatchNorm (LDS-DMA kernel, no split): the epilogue writes the BN's
+  // per-channel partial sums of (y - shift[c]) and its square over each 256-pixel tile to
+  // bnpart[tile][2 Ng] (the layout bn_nhwc_partial_k writes), so the BN skips its statistics pass
+  float* bnpart;
+  const float* bnshift;  // per-channel shift (the BN's running mean: well conditioned), or null = 0
   FastDiv fOW, fOHW, fCa, fS, fWc, fHWc;
 };
 
@@ -385,7 +390,7 @@ __device__ __forceinline__ void glds16(const void* src, void* lds) {
   __builtin_amdgcn_global_load_lds(src, (lds_void_t*)lds, 16, 0, 0);
 }
 
-template <int TM>
+template <int TM, bool STATS = false>
 __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
   constexpr int TN = 256, BK = 64, NS = 3;
   constexpr int AB = TM * 128, SB = AB + TN * 128;   // bytes: A image, whole stage
@@ -526,6 +531,57 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
       u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
       if (a.addend) v = add8(v, *reinterpret_cast<const u32x4*>(a.addend + o));
       *reinterpret_cast<u32x4*>(a.out + o) = v;
+    }
+  }
+  if constexpr (STATS) {  // BN statistics of the stored (bf16) tile: 512 / TM threads per channel
+    constexpr int TPC = 512 / TM, RPT = TN / TPC, U = 8;
+    static_assert(RPT % U == 0, "rows per thread");
+    // reduction slots after the C tile in the (idle) stage buffers
+    float* bred = reinterpret_cast<float*>(smem + ((TN * CP * 2 + 255) & ~255));
+    static_assert(((TN * CP * 2 + 255) & ~255) + 2 * 512 * 4 <= NS * SB, "BN reduction slots must fit");
+    const int c = tid % TM, q = tid / TM, ch = ch0 + c;
+    const float K = (a.bnshift && ch < a.Ng) ? a.bnshift[ch] : 0.f;
+    const int rows = min(TN, a.M - px0);
+    const uint16_t* col = reinterpret_cast<const uint16_t*>(Cs) + c;
+    float s1[U], s2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) s1[u] = s2[u] = 0.f;
+    if (rows == TN) {  // full tile: U independent rows per iteration (loads in flight together)
+      for (int r0 = q * RPT; r0 < (q + 1) * RPT; r0 += U) {
+        uint16_t h[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) h[u] = col[(r0 + u) * CP];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float d = bf2f(h[u]) - K;
+          s1[u] += d;
+          s2[u] = fmaf(d, d, s2[u]);
+        }
+      }
+    } else {
+      for (int r = q * RPT; r < min(rows, (q + 1) * RPT); ++r) {
+        const float d = bf2f(col[r * CP]) - K;
+        s1[0] += d;
+        s2[0] = fmaf(d, d, s2[0]);
+      }
+    }
+#pragma unroll
+    for (int u = 1; u < U; ++u) {
+      s1[0] += s1[u];
+      s2[0] += s2[u];
+    }
+    bred[tid] = s1[0];
+    bred[512 + tid] = s2[0];
+    __syncthreads();
+    if (q == 0 && ch < a.Ng) {
+      float t1 = s1[0], t2 = s2[0];
+      for (int k = 1; k < TPC; ++k) {
+        t1 += bred[tid + k * TM];
+        t2 += bred[512 + tid + k * TM];
+      }
+      float* dst = a.bnpart + (size_t)(px0 / TN) * 2 * a.Ng + 2 * ch;
+      dst[0] = t1;
+      dst[1] = t2;
     }
   }
 }
@@ -838,6 +894,8 @@ struct BnNArgs {
                        // is then (x * scale + shift > 0) and y is not read (one tensor less)
   uint8_t* mask;       // ReLU mask bits [Npix * C / 8] (bit e of byte i: element e of vector i > 0):
                        // written by the forward apply, read by the backward instead of y
+  const float* kshift;  // fwd, partials precomputed by the conv epilogue: their per-channel shift
+  int pre;              // fwd: part already holds gx partial rows (no statistics pass)
   float momentum, eps;
 };
 
@@ -960,11 +1018,13 @@ __global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
   const bool cok = c < a.C;
   const size_t pitch = 2 * (size_t)a.C;
   float s1 = 0.f, s2 = 0.f;
-  if (cok) {
+  // passes of RG * MAXR rows (one unless the partials came from a conv epilogue: one row per
+  // 256-pixel tile, up to ~12 K rows)
+  for (int base = 0; cok && base < a.gx; base += RG * MAXR) {
     float t1[MAXR], t2[MAXR];
 #pragma unroll
     for (int u = 0; u < MAXR; ++u) {
-      const int b = rg + RG * u;
+      const int b = base + rg + RG * u;
       const bool ok = b < a.gx;
       const float* q = a.part + (size_t)(ok ? b : 0) * pitch + 2 * c;
       t1[u] = ok ? q[0] : 0.f;
@@ -984,7 +1044,7 @@ __global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
       bt = a.beta ? a.beta[c] : 0.f;
       rm = a.run_mean ? a.run_mean[c] : 0.f;
       rv = a.run_var ? a.run_var[c] : 0.f;
-      K0 = bf2f(a.x[c]);
+      K0 = a.pre ? (a.kshift ? a.kshift[c] : 0.f) : bf2f(a.x[c]);
     } else {
       mu = a.mean[c];
       inv = a.invstd[c];
@@ -1359,7 +1419,9 @@ size_t nhwc_conv_scratch_floats(int M, int Ng, int Kg) {
   return n;
 }
 
-static void launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
+// returns the number of BN partial rows the epilogue wrote to a.bnpart (0: none, the BN runs its
+// own statistics pass)
+static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   MX_CHECK(a.Kg % 8 == 0 && a.Ca % 8 == 0 && a.Ng % 8 == 0, "nhwc conv: channels must be multiples of 8");
   a.fOW = FastDiv(a.OW);
   a.fOHW = FastDiv(a.OH * a.OW);
@@ -1373,16 +1435,24 @@ static void launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     a.par = 0;
     a.kt_per_split = gp.kt_per_split;
     a.part = gp.splits > 1 ? scratch : nullptr;
+    const int gx = cdiv(a.M, 256);
+    if (!(a.bnpart && !a.dgrad && gp.splits == 1 && gx <= 16384)) a.bnpart = nullptr;
     const dim3 grid(cdiv(a.Ng, gp.tm) * cdiv(a.M, 256), gp.splits);
-    if (gp.tm == 128) MX_LAUNCH((conv_nhwc_glds_kernel<128>), grid, dim3(512), 0, st, a);
-    else MX_LAUNCH((conv_nhwc_glds_kernel<64>), grid, dim3(512), 0, st, a);
+    if (a.bnpart) {
+      if (gp.tm == 128) MX_LAUNCH((conv_nhwc_glds_kernel<128, true>), grid, dim3(512), 0, st, a);
+      else MX_LAUNCH((conv_nhwc_glds_kernel<64, true>), grid, dim3(512), 0, st, a);
+    } else {
+      if (gp.tm == 128) MX_LAUNCH((conv_nhwc_glds_kernel<128>), grid, dim3(512), 0, st, a);
+      else MX_LAUNCH((conv_nhwc_glds_kernel<64>), grid, dim3(512), 0, st, a);
+    }
     if (gp.splits > 1) {
       const int64_t n4 = (int64_t)a.M * a.Ng / 4;
       MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, gp.splits,
                 a.addend);
     }
-    return;
+    return a.bnpart ? gx : 0;
   }
+  a.bnpart = nullptr;
   a.par = cs.par ? 1 : 0;
   if (cs.par) {
     a.Hc = a.OH / 2;
@@ -1412,10 +1482,12 @@ static void launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, p.splits,
               a.addend);
   }
+  return 0;
 }
 
-void nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int H, int W, int Cp, int K, int R,
-                   int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st) {
+int nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int H, int W, int Cp, int K, int R,
+                  int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st, float* bnpart,
+                  const float* bnshift) {
   ConvNArgs a{};
   a.act = x;
   a.wt = wt;
@@ -1435,7 +1507,9 @@ void nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, in
   a.ph = ph;
   a.pw = pw;
   a.dgrad = 0;
-  launch_conv(a, scratch, st);
+  a.bnpart = bnpart;
+  a.bnshift = bnshift;
+  return launch_conv(a, scratch, st);
 }
 
 static ConvNArgs dgrad_args(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K,
@@ -1568,7 +1642,7 @@ size_t nhwc_bn_scratch_floats(int Npix, int C) {
 void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const float* gamma, const float* beta,
                  float* mean, float* invstd, float* run_mean, float* run_var, int64_t* num_batches, int Npix, int C,
                  float momentum, float eps, bool relu, float* scratch, hipStream_t st, float* coef_out,
-                 uint8_t* mask_out) {
+                 uint8_t* mask_out, const float* pre_part, int pre_gx, const float* kshift) {
   const int V = C / 8;
   MX_CHECK(C % 8 == 0 && C <= 2048 && (V >= kBnT ? V % kBnT == 0 : kBnT % V == 0),
            "nhwc bn: unsupported channel count");
@@ -1593,7 +1667,15 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
   a.mask = relu ? mask_out : nullptr;
   a.momentum = momentum;
   a.eps = eps;
-  MX_LAUNCH(bn_nhwc_partial_k<false>, g, dim3(kBnT), 0, st, a);
+  if (pre_part) {  // the producing conv's epilogue already wrote the partial sums
+    MX_CHECK(pre_gx >= 1 && pre_gx <= 16384, "nhwc bn: precomputed partial rows out of range");
+    a.part = const_cast<float*>(pre_part);
+    a.gx = pre_gx;
+    a.pre = 1;
+    a.kshift = kshift;
+  } else {
+    MX_LAUNCH(bn_nhwc_partial_k<false>, g, dim3(kBnT), 0, st, a);
+  }
   MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
   MX_LAUNCH(bn_nhwc_apply_k, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));

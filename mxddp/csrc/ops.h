@@ -172,8 +172,12 @@ void nhwc_repack_many(const int64_t* desc, int n, int total_blocks, hipStream_t 
 // scratch (or null = no split-K): nhwc_conv_scratch_floats(M = output pixels, Ng = output
 // channels, Kg = R*S*input channels) floats of fp32 split-K partials
 size_t nhwc_conv_scratch_floats(int M, int Ng, int Kg);
-void nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int H, int W, int Cp, int K, int R,
-                   int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st);
+// bnpart (optional, [cdiv(M, 256)][2K] floats): the output feeds a training BatchNorm; when the
+// LDS-DMA kernel runs unsplit its epilogue writes the BN partial sums of (y - bnshift[c]) there
+// and the call returns the number of rows written (pass them to nhwc_bn_fwd), else 0
+int nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int H, int W, int Cp, int K, int R,
+                  int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st,
+                  float* bnpart = nullptr, const float* bnshift = nullptr);
 // large-layer LDS-DMA conv kernel: 0 = off, 1 = large layers (default, env MXDDP_CONV_GLDS), 2 = always
 void nhwc_conv_set_glds(int mode);
 // split-K scratch of nhwc_conv_dgrad (floats; 0 = none needed)
@@ -196,7 +200,9 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
                  float* mean, float* invstd, float* run_mean, float* run_var, int64_t* num_batches, int Npix, int C,
                  float momentum, float eps, bool relu, float* scratch, hipStream_t st,
                  float* coef_out = nullptr,  // coef_out: [C][2] (scale, shift) kept for nhwc_bn_bwd
-                 uint8_t* mask_out = nullptr);  // ReLU mask bits [Npix * C / 8] for nhwc_bn_bwd
+                 uint8_t* mask_out = nullptr,  // ReLU mask bits [Npix * C / 8] for nhwc_bn_bwd
+                 // partial sums already written by the producing conv (nhwc_conv_fwd's bnpart)
+                 const float* pre_part = nullptr, int pre_gx = 0, const float* kshift = nullptr);
 void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma, const float* mean,
                  const float* invstd, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, int Npix, int C,
                  bool relu, bool accumulate_params, float* scratch, hipStream_t st,

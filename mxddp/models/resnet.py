@@ -53,14 +53,15 @@ class Bottleneck(nn.Module):
         # sequence numbers and autograd runs them first (its dx exists when conv1's dgrad runs).
         join = N.GradJoin()
         x, xs = N.fork(x, join)
-        out = N.batch_norm(N.conv2d(x, self.conv1.weight, pack=pack, join=join), self.bn1, relu=True)
-        out = N.batch_norm(N.conv2d(out, self.conv2.weight, self.conv2.stride, self.conv2.padding, pack), self.bn2,
-                           relu=True)
-        out = N.conv2d(out, self.conv3.weight, pack=pack)
+        # bn=: each conv's epilogue computes its BN's partial statistics where its kernel allows
+        out = N.batch_norm(N.conv2d(x, self.conv1.weight, pack=pack, join=join, bn=self.bn1), self.bn1, relu=True)
+        out = N.batch_norm(N.conv2d(out, self.conv2.weight, self.conv2.stride, self.conv2.padding, pack, bn=self.bn2),
+                           self.bn2, relu=True)
+        out = N.conv2d(out, self.conv3.weight, pack=pack, bn=self.bn3)
         if self.downsample is None:
             return N.batch_norm(out, self.bn3, relu=True, res=xs, join=join)
         dc, dbn = self.downsample[0], self.downsample[1]
-        idt = N.batch_norm(N.conv2d(xs, dc.weight, dc.stride, dc.padding, pack, deposit=join), dbn)
+        idt = N.batch_norm(N.conv2d(xs, dc.weight, dc.stride, dc.padding, pack, deposit=join, bn=dbn), dbn)
         return N.batch_norm(out, self.bn3, relu=True, res=idt)
 
 

@@ -13,6 +13,8 @@ model in ``mxddp.models.resnet``, which is also the oracle of ``tests/test_gpu_n
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import native
@@ -135,7 +137,7 @@ def fork(x, join: GradJoin):
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad, packed=None, join=None, deposit=None):
+    def forward(ctx, x, w, stride, pad, packed=None, join=None, deposit=None, bnstat=None):
         Cn = native()
         N, H, W, Cp = x.shape
         K, C, R, S = w.shape
@@ -153,8 +155,10 @@ class _Conv(torch.autograd.Function):
             Cn.nhwc_repack_weight(w.data_ptr(), wt.data_ptr(), _p(wtd), K, C, R, S, Cp, st)
         y = torch.empty((N, P, Q, K), device=x.device, dtype=BF16)
         scr = _splitk_scratch(N * P * Q, K, R * S * Cp, x.device)
-        Cn.nhwc_conv_fwd(x.data_ptr(), wt.data_ptr(), y.data_ptr(), N, H, W, Cp, K, R, S, sh, sw, ph, pw, P, Q,
-                         _p(scr), st)
+        gx = Cn.nhwc_conv_fwd(x.data_ptr(), wt.data_ptr(), y.data_ptr(), N, H, W, Cp, K, R, S, sh, sw, ph, pw, P, Q,
+                              _p(scr), st, _p(bnstat[0]) if bnstat else 0, _p(bnstat[1]) if bnstat else 0)
+        if bnstat:
+            bnstat[2] = gx
         ctx.wtd = wtd
         ctx.join = join
         ctx.deposit = deposit
@@ -197,22 +201,41 @@ class _Conv(torch.autograd.Function):
                                P, Q, sink is not None, part.data_ptr(), st)
             if sink is not None:
                 dw = None
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None
 
 
 def conv2d(x, w, stride=1, padding=0, pack: WeightPack | None = None, join: GradJoin | None = None,
-           deposit: GradJoin | None = None):
+           deposit: GradJoin | None = None, bn: torch.nn.BatchNorm2d | None = None):
     """bf16 NHWC convolution; ``pack`` supplies weights already repacked by WeightPack.refresh(),
     ``join`` (see ``fork``) adds a residual block's shortcut gradient to this conv's input gradient,
-    ``deposit`` leaves this conv's input gradient in that join (a projection shortcut)."""
+    ``deposit`` leaves this conv's input gradient in that join (a projection shortcut).  ``bn``: the
+    training BatchNorm that consumes the output; the conv's epilogue then computes that BN's
+    partial statistics where the kernel allows it (``batch_norm`` picks them up and skips its
+    statistics pass)."""
     s = (stride, stride) if isinstance(stride, int) else tuple(stride)
     p = (padding, padding) if isinstance(padding, int) else tuple(padding)
-    return _Conv.apply(x, w, s, p, pack.get(w) if pack is not None else None, join, deposit)
+    bnstat = None
+    if bn is not None and bn.training and _BN_STATS_IN_CONV:
+        N_, H_, W_, _ = x.shape
+        K, _, R, S = w.shape
+        P, Q = _out(H_, R, s[0], p[0]), _out(W_, S, s[1], p[1])
+        rows = -(-(N_ * P * Q) // 256)
+        if rows <= 16384:
+            shift = bn.running_mean if bn.track_running_stats else None
+            bnstat = [torch.empty((rows * 2 * K,), device=x.device, dtype=torch.float32), shift, 0]
+    y = _Conv.apply(x, w, s, p, pack.get(w) if pack is not None else None, join, deposit, bnstat)
+    if bnstat and bnstat[2] > 0:
+        y._mx_bnpre = (bnstat[0], bnstat[2], bnstat[1])  # (partials, rows, shift) for batch_norm
+    return y
+
+
+# MXDDP_BN_STATS_IN_CONV=0: every BN runs its own statistics pass (A/B switch)
+_BN_STATS_IN_CONV = os.environ.get("MXDDP_BN_STATS_IN_CONV", "1") == "1"
 
 
 class _BN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, rm, rv, nbt, res, relu, momentum, eps, join=None):
+    def forward(ctx, x, gamma, beta, rm, rv, nbt, res, relu, momentum, eps, join=None, pre=None):
         Cn = native()
         N, H, W, C = x.shape
         npix = N * H * W
@@ -226,9 +249,10 @@ class _BN(torch.autograd.Function):
         # any other ReLU: the forward stores its mask as bits (1/16 of y's bytes), read by the
         # backward's two passes instead of y
         mask = torch.empty((npix * C // 8,), device=x.device, dtype=torch.uint8) if (relu and fcoef is None) else None
+        part, rows, shift = pre if pre is not None else (None, 0, None)
         Cn.nhwc_bn_fwd(x.data_ptr(), _p(res), y.data_ptr(), _p(gamma), _p(beta), mean.data_ptr(), invstd.data_ptr(),
                        _p(rm), _p(rv), _p(nbt), npix, C, float(momentum), float(eps), bool(relu), scr.data_ptr(),
-                       stream_of(x), _p(fcoef), _p(mask))
+                       stream_of(x), _p(fcoef), _p(mask), _p(part), rows, _p(shift))
         ctx.fcoef = fcoef
         ctx.mask = mask
         ctx.save_for_backward(x, gamma, mean, invstd)
@@ -257,7 +281,7 @@ class _BN(torch.autograd.Function):
             dg = db = None
         if ctx.join is not None and dres is not None:
             ctx.join.dres = dres  # picked up by the block's first conv (data-gradient epilogue)
-        return dx, dg, db, None, None, None, dres, None, None, None, None
+        return dx, dg, db, None, None, None, dres, None, None, None, None, None
 
 
 def batch_norm(x, bn: torch.nn.BatchNorm2d, relu: bool = False, res: torch.Tensor | None = None,
@@ -268,7 +292,14 @@ def batch_norm(x, bn: torch.nn.BatchNorm2d, relu: bool = False, res: torch.Tenso
     if bn.training or not bn.track_running_stats:
         mom = bn.momentum if bn.momentum is not None else 0.1
         nbt = bn.num_batches_tracked if (bn.training and bn.track_running_stats) else None
-        return _BN.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, res, relu, mom, bn.eps, join)
+        # partial statistics from the producing conv's epilogue (conv2d(..., bn=bn)), valid only
+        # for this exact tensor and shifted by this BN's running mean
+        pre = getattr(x, "_mx_bnpre", None)
+        if pre is not None and (pre[2] is not (bn.running_mean if bn.track_running_stats else None)
+                                or pre[0].numel() != pre[1] * 2 * x.shape[-1]):
+            pre = None
+        return _BN.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, res, relu, mom, bn.eps, join,
+                         pre)
     y = (x.float() - bn.running_mean) * torch.rsqrt(bn.running_var + bn.eps) * bn.weight + bn.bias
     if res is not None:
         y = y + res.float()

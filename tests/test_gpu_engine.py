@@ -122,6 +122,29 @@ def test_fused_engine_multi_step_graph(cuda):
         assert torch.allclose(v, b.state_dict()[k], rtol=1e-4, atol=1e-6), k
 
 
+def test_fused_engine_warm_graphs_are_training_steps(cuda):
+    """warm_graphs() launches every captured graph once (8 + 4 + 2 + 1 steps) and counts them:
+    the same state and metrics as that many single steps, and small-first replay ordering runs
+    the same steps."""
+    from mxddp.engine import FusedMnistTrainer
+
+    a = FusedMnistTrainer(batch=64, device=cuda, lr=0.01, steps_per_graph=8)
+    b = FusedMnistTrainer(batch=64, device=cuda, lr=0.01, steps_per_graph=1)
+    a.step(1)
+    n = a.warm_graphs()
+    assert n == 8 + 4 + 2 + 1 and a.steps == 1 + n
+    b.step(1 + n)
+    a.eng.set_small_first(True)
+    a.step(13)  # 8 + 4 + 1, remainders first
+    b.step(13)
+    la, ca = a.read_metrics()
+    lb, cb = b.read_metrics()
+    assert a.steps_at_reset == a.steps == b.steps
+    assert abs(la - lb) < 1e-3 * abs(lb) and ca == cb
+    for k, v in a.state_dict().items():
+        assert torch.allclose(v, b.state_dict()[k], rtol=1e-4, atol=1e-6), k
+
+
 def test_fused_engine_trains(cuda):
     from mxddp.engine import FusedMnistTrainer
 

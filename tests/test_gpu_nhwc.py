@@ -176,6 +176,38 @@ def test_bn_nhwc(cuda, C, relu, res):
     assert int(bn.num_batches_tracked) == 1
 
 
+@pytest.mark.parametrize("shape,offset", [((16, 64, 56, 56, 128, 3, 1), 0.0), ((32, 64, 28, 28, 256, 1, 0), 4.0),
+                                          ((14, 64, 61, 59, 128, 3, 1), -2.0), ((96, 64, 56, 56, 64, 1, 0), 1.0)])
+def test_bn_statistics_from_conv_epilogue(cuda, shape, offset):
+    """conv2d(..., bn=bn) -> batch_norm: the LDS-DMA conv's epilogue computes the BN partial sums
+    (shifted by the running mean) and the BN skips its statistics pass; same output, running
+    statistics and gradients as the separate pass (incl. a partial last pixel tile and outputs
+    with a large mean)."""
+    N, C, H, W, K, R, pad = shape
+    torch.manual_seed(5)
+    x = (torch.randn(N, H, W, C) + offset).to(torch.bfloat16).to(cuda)
+    w = (torch.randn(K, C, R, R) * 0.05).to(cuda)
+    gamma = torch.rand(K) + 0.5
+    outs = []
+    for fused in (False, True):
+        bn = nn.BatchNorm2d(K).to(cuda)
+        with torch.no_grad():
+            bn.running_mean.fill_(0.7 * offset)  # a stale shift, as after some steps
+            bn.weight.copy_(gamma)
+        xg = x.clone().requires_grad_()
+        wg = w.clone().requires_grad_()
+        c = nhwc.conv2d(xg, wg, 1, pad, bn=bn if fused else None)
+        assert (getattr(c, "_mx_bnpre", None) is not None) == fused  # the glds kernel ran
+        y = nhwc.batch_norm(c, bn, relu=True)
+        gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(9)).to(torch.bfloat16).to(cuda)
+        y.backward(gy)
+        torch.cuda.synchronize()
+        outs.append((y.float().cpu(), bn.running_mean.cpu(), bn.running_var.cpu(), xg.grad.float().cpu(),
+                     wg.grad.cpu(), bn.weight.grad.cpu()))
+    for a, b in zip(*outs):
+        assert _rel(b, a) < 2e-2
+
+
 def test_weight_pack_matches_per_conv_repack(cuda):
     """One-launch repack of many convolutions == the per-convolution repack (both layouts, padded
     stem channels, a conv without the data-gradient layout)."""
