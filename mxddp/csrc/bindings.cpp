@@ -87,12 +87,16 @@ PYBIND11_MODULE(_C, m) {
     linear_fwd(P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), M, N, K, relu, S(st));
   });
   m.def("linear_dgrad", [](uintptr_t dy, uintptr_t w, uintptr_t dx, int M, int N, int K, uintptr_t mask, bool acc,
-                           uintptr_t st) {
-    linear_dgrad(P<const float>(dy), P<const float>(w), P<float>(dx), M, N, K, P<const float>(mask), acc, S(st));
-  });
-  m.def("linear_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, int M, int N, int K, bool acc, uintptr_t st) {
-    linear_wgrad(P<const float>(dy), P<const float>(x), P<float>(dw), M, N, K, acc, S(st));
-  });
+                           uintptr_t st, uintptr_t dy_mask) {
+    linear_dgrad(P<const float>(dy), P<const float>(w), P<float>(dx), M, N, K, P<const float>(mask), acc, S(st),
+                 P<const float>(dy_mask));
+  }, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("mask"),
+     py::arg("acc"), py::arg("st"), py::arg("dy_mask") = 0);
+  m.def("linear_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, int M, int N, int K, bool acc, uintptr_t st,
+                           uintptr_t dy_mask) {
+    linear_wgrad(P<const float>(dy), P<const float>(x), P<float>(dw), M, N, K, acc, S(st), P<const float>(dy_mask));
+  }, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("acc"),
+     py::arg("st"), py::arg("dy_mask") = 0);
 
   // ---------------------------------------------------------------- channels-last bf16 (nhwc_bf16.hip)
   m.def("nhwc_from_nchw", [](uintptr_t x, uintptr_t y, int N, int C, int H, int W, int Cp, uintptr_t st) {
@@ -180,9 +184,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("relu_bwd", [](uintptr_t dy, uintptr_t y, uintptr_t dx, int64_t n, uintptr_t st) {
     relu_bwd(P<const float>(dy), P<const float>(y), P<float>(dx), n, S(st));
   });
-  m.def("bias_grad", [](uintptr_t dy, uintptr_t db, int outer, int C, int inner, bool acc, uintptr_t st) {
-    bias_grad(P<const float>(dy), P<float>(db), outer, C, inner, acc, S(st));
-  });
+  m.def("bias_grad", [](uintptr_t dy, uintptr_t db, int outer, int C, int inner, bool acc, uintptr_t st,
+                        uintptr_t dy_mask) {
+    bias_grad(P<const float>(dy), P<float>(db), outer, C, inner, acc, S(st), P<const float>(dy_mask));
+  }, py::arg("dy"), py::arg("db"), py::arg("outer"), py::arg("C"), py::arg("inner"), py::arg("acc"), py::arg("st"),
+     py::arg("dy_mask") = 0);
   m.def("add_inplace", [](uintptr_t y, uintptr_t x, int64_t n, uintptr_t st) { add_inplace(P<float>(y), P<const float>(x), n, S(st)); });
   m.def("scale_inplace", [](uintptr_t y, float a, int64_t n, uintptr_t st) { scale_inplace(P<float>(y), a, n, S(st)); });
   m.def("fill", [](uintptr_t y, float v, int64_t n, uintptr_t st) { fill(P<float>(y), v, n, S(st)); });

@@ -94,11 +94,13 @@ size_t conv_wgrad_scratch_floats(const ConvShape& s);
 void linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int N, int K,
                 bool relu, hipStream_t st);
 // dx[M,K] (+)= dy[M,N] @ w[N,K]  [* (mask > 0)]
+// dy_mask (optional, [M,N]): dy is used as dy * (dy_mask > 0) -- the layer's own fused ReLU,
+// applied on load instead of a separate relu_bwd pass (also for linear_wgrad / bias_grad)
 void linear_dgrad(const float* dy, const float* w, float* dx, int M, int N, int K,
-                  const float* relu_mask, bool accumulate, hipStream_t st);
+                  const float* relu_mask, bool accumulate, hipStream_t st, const float* dy_mask = nullptr);
 // dw[N,K] (+)= dy[M,N]^T @ x[M,K]
 void linear_wgrad(const float* dy, const float* x, float* dw, int M, int N, int K, bool accumulate,
-                  hipStream_t st);
+                  hipStream_t st, const float* dy_mask = nullptr);
 
 // GEMM operand precision for every op above: 0 = fp32 MFMA (exact fp32, default),
 // 1 = bf16 operands with fp32 accumulation (mixed precision; fp32 tensors in memory).
@@ -110,7 +112,7 @@ void relu_fwd(const float* x, float* y, int64_t n, hipStream_t st);
 void relu_bwd(const float* dy, const float* y, float* dx, int64_t n, hipStream_t st);
 // db[c] (+)= sum over (outer, inner) of dy[outer][c][inner]
 void bias_grad(const float* dy, float* db, int outer, int C, int inner, bool accumulate,
-               hipStream_t st);
+               hipStream_t st, const float* dy_mask = nullptr);
 void add_inplace(float* y, const float* x, int64_t n, hipStream_t st);
 void scale_inplace(float* y, float a, int64_t n, hipStream_t st);
 void fill(float* y, float v, int64_t n, hipStream_t st);

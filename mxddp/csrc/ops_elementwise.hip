@@ -79,17 +79,19 @@ __global__ __launch_bounds__(kBgTB) void bias_grad_k(const float* __restrict__ d
 }
 
 __global__ __launch_bounds__(256) void bias_grad_rows_k(const float* __restrict__ dy, float* __restrict__ db, int rows,
-                                                        int C, int accumulate) {
+                                                        int C, int accumulate, const float* __restrict__ mask) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = blockIdx.x * 64 + lane;
   float s[4] = {0.f, 0.f, 0.f, 0.f};
+  // dy masked by (mask > 0) when given: the layer's fused ReLU, no separate relu_bwd pass
+  auto ld = [&](size_t i) { return (mask && !(mask[i] > 0.f)) ? 0.f : dy[i]; };
   if (c < C) {
     int r = w;
     for (; r + 12 < rows; r += 16) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) s[k] += dy[(size_t)(r + 4 * k) * C + c];
+      for (int k = 0; k < 4; ++k) s[k] += ld((size_t)(r + 4 * k) * C + c);
     }
-    for (; r < rows; r += 4) s[0] += dy[(size_t)r * C + c];
+    for (; r < rows; r += 4) s[0] += ld((size_t)r * C + c);
   }
   red[w][lane] = (s[0] + s[1]) + (s[2] + s[3]);
   __syncthreads();
@@ -303,12 +305,14 @@ void scale_inplace(float* y, float a, int64_t n, hipStream_t st) {
 void fill(float* y, float v, int64_t n, hipStream_t st) {
   MX_LAUNCH(fill_k, dim3(grid_for(n)), dim3(kTB), 0, st, y, v, n);
 }
-void bias_grad(const float* dy, float* db, int outer, int C, int inner, bool accumulate, hipStream_t st) {
+void bias_grad(const float* dy, float* db, int outer, int C, int inner, bool accumulate, hipStream_t st,
+               const float* dy_mask) {
   MX_CHECK((int64_t)outer * inner < (1ll << 31), "bias_grad: reduction too large");
   if (inner == 1) {
-    MX_LAUNCH(bias_grad_rows_k, dim3((C + 63) / 64), dim3(256), 0, st, dy, db, outer, C, accumulate ? 1 : 0);
+    MX_LAUNCH(bias_grad_rows_k, dim3((C + 63) / 64), dim3(256), 0, st, dy, db, outer, C, accumulate ? 1 : 0, dy_mask);
     return;
   }
+  MX_CHECK(!dy_mask, "bias_grad: a dy mask is supported for [rows][C] gradients only");
   MX_LAUNCH(bias_grad_k, dim3(C), dim3(kBgTB), 0, st, dy, db, outer, C, inner, FastDiv((uint32_t)inner),
             accumulate ? 1 : 0);
 }

@@ -282,10 +282,15 @@ struct LinDgradOp {  // dx[M,Kin] = dy[M,Nout] w[Nout,Kin]; GEMM N=Kin, K=Nout
   int mode;
   float* part = nullptr;  // split-K partials (see ConvFwdOp)
   int64_t ptotal = 0;
+  const float* amask = nullptr;  // dy masked on load by (amask > 0): the layer's own fused ReLU
   struct APre { int64_t base; bool ok; };
   struct BPre { int n; bool ok; };
   __device__ APre a_pre(int m) const { return APre{(int64_t)(m < M ? m : 0) * K, m < M}; }
-  __device__ float a_load(const APre& a, int k) const { return a.ok ? dy[a.base + k] : 0.f; }
+  __device__ float a_load(const APre& a, int k) const {
+    if (!a.ok) return 0.f;
+    const float v = dy[a.base + k];
+    return (amask && !(amask[a.base + k] > 0.f)) ? 0.f : v;
+  }
   __device__ BPre b_pre(int n) const { return BPre{n, n < N}; }
   __device__ float b_load(const BPre& b, int k) const { return b.ok ? w[(int64_t)k * N + b.n] : 0.f; }
   __device__ void store(int m, int n, float v, int split) const {
@@ -307,10 +312,15 @@ struct LinWgradOp {  // dw[Nout,Kin] = dy[B,Nout]^T x[B,Kin]; GEMM M=Nout, N=Kin
   const float* x;
   float* dw;
   int mode;
+  const float* amask = nullptr;  // dy masked on load by (amask > 0) (see LinDgradOp)
   struct APre { int m; bool ok; };
   struct BPre { int n; bool ok; };
   __device__ APre a_pre(int m) const { return APre{m, m < M}; }
-  __device__ float a_load(const APre& a, int k) const { return a.ok ? dy[(int64_t)k * M + a.m] : 0.f; }
+  __device__ float a_load(const APre& a, int k) const {
+    if (!a.ok) return 0.f;
+    const float v = dy[(int64_t)k * M + a.m];
+    return (amask && !(amask[(int64_t)k * M + a.m] > 0.f)) ? 0.f : v;
+  }
   __device__ BPre b_pre(int n) const { return BPre{n, n < N}; }
   __device__ float b_load(const BPre& b, int k) const { return b.ok ? x[(int64_t)k * N + b.n] : 0.f; }
   __device__ void store(int m, int n, float v, int) const { emit(dw, (int64_t)m * N + n, v, mode); }
@@ -585,17 +595,19 @@ void linear_fwd(const float* x, const float* w, const float* b, float* y, int M,
 }
 
 void linear_dgrad(const float* dy, const float* w, float* dx, int M, int N, int K,
-                  const float* relu_mask, bool accumulate, hipStream_t st) {
+                  const float* relu_mask, bool accumulate, hipStream_t st, const float* dy_mask) {
   // GEMM view: M x K(out=Kin) reduction over N(out features)
   LinDgradOp op{M, K, N, dy, w, dx, relu_mask, accumulate ? kAccum : kStore};
+  op.amask = dy_mask;
   if (run_partial(op, (int64_t)M * K, dx, nullptr, 1, 1, false, relu_mask, accumulate, st)) return;
   op.part = nullptr;
   run(op, 1, st);
 }
 
 void linear_wgrad(const float* dy, const float* x, float* dw, int M, int N, int K, bool accumulate,
-                  hipStream_t st) {
+                  hipStream_t st, const float* dy_mask) {
   LinWgradOp op{N, K, M, dy, x, dw, kStore};
+  op.amask = dy_mask;
   const int tiles = cdiv(N, 64) * cdiv(K, 64);
   const int splits = pick_splits(tiles, M, 256, 512);
   if (splits == 1) {

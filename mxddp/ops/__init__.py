@@ -297,19 +297,23 @@ class _Linear(torch.autograd.Function):
         N = w.shape[0]
         dy = dy.reshape(M, N).contiguous()
         st = stream_of(dy)
-        if ctx.relu:
+        # MXDDP_RELU_ON_LOAD=1: the fused ReLU's mask (y > 0) is applied as the three GEMM /
+        # reduction kernels load dy instead of a relu_bwd pass (measured: no gain inside a
+        # captured step, MLP 468-470k vs 471-480k img/s, so off by default)
+        dm = y.data_ptr() if ctx.relu else 0
+        if ctx.relu and not _RELU_ON_LOAD:
             g = torch.empty_like(dy)
             C.relu_bwd(dy.data_ptr(), y.data_ptr(), g.data_ptr(), dy.numel(), st)
-            dy = g
+            dy, dm = g, 0
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty((M, K), device=dy.device, dtype=dy.dtype)
-            C.linear_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), M, N, K, 0, False, st)
+            C.linear_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), M, N, K, 0, False, st, dm)
             dx = dx.reshape(ctx.in_shape)
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(w)
             dw = sink if sink is not None else torch.empty_like(w)
-            C.linear_wgrad(dy.data_ptr(), x2.data_ptr(), dw.data_ptr(), M, N, K, sink is not None, st)
+            C.linear_wgrad(dy.data_ptr(), x2.data_ptr(), dw.data_ptr(), M, N, K, sink is not None, st, dm)
             if sink is not None:
                 _grad_done(w)
                 dw = None
@@ -317,11 +321,14 @@ class _Linear(torch.autograd.Function):
             b = ctx.bias_ref
             sink = _grad_sink(b)
             db = sink if sink is not None else torch.empty((N,), device=dy.device, dtype=dy.dtype)
-            C.bias_grad(dy.data_ptr(), db.data_ptr(), M, N, 1, sink is not None, st)
+            C.bias_grad(dy.data_ptr(), db.data_ptr(), M, N, 1, sink is not None, st, dm)
             if sink is not None:
                 _grad_done(b)
                 db = None
         return dx, dw, db, None
+
+
+_RELU_ON_LOAD = os.environ.get("MXDDP_RELU_ON_LOAD", "0") == "1"
 
 
 def linear(x, w, b=None, relu=False):

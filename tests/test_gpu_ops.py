@@ -150,6 +150,31 @@ def test_linear_dgrad_mask_accumulate(cuda, M, N, K, accumulate):
     assert _rel(dx.cpu(), ref) < 1e-4
 
 
+@pytest.mark.parametrize("M,N,K", [(64, 1000, 1000), (100, 130, 70)])
+def test_linear_backward_dy_mask(cuda, M, N, K):
+    """linear_dgrad / linear_wgrad / bias_grad with dy masked on load == the same kernels on the
+    masked copy of dy."""
+    from mxddp import native
+
+    C_ = native()
+    torch.manual_seed(4)
+    dy, w, x = torch.randn(M, N), torch.randn(N, K) * 0.05, torch.randn(M, K)
+    y = torch.randn(M, N).clamp_min(0)
+    g = dy * (y > 0)
+    dyg, wg, xg, yg = (t.to(cuda) for t in (dy, w, x, y))
+    dx = torch.empty(M, K, device=cuda)
+    dw = torch.empty(N, K, device=cuda)
+    db = torch.empty(N, device=cuda)
+    st = torch.cuda.current_stream(cuda).cuda_stream
+    C_.linear_dgrad(dyg.data_ptr(), wg.data_ptr(), dx.data_ptr(), M, N, K, 0, False, st, yg.data_ptr())
+    C_.linear_wgrad(dyg.data_ptr(), xg.data_ptr(), dw.data_ptr(), M, N, K, False, st, yg.data_ptr())
+    C_.bias_grad(dyg.data_ptr(), db.data_ptr(), M, N, 1, False, st, yg.data_ptr())
+    torch.cuda.synchronize()
+    assert _rel(dx.cpu(), g @ w) < 1e-4
+    assert _rel(dw.cpu(), g.t() @ x) < 1e-4
+    assert _rel(db.cpu(), g.sum(0)) < 1e-4
+
+
 @pytest.mark.parametrize("k,s,p,ceil", [(2, 2, 0, False), (3, 2, 1, False), (2, 2, 0, True)])
 def test_pools(cuda, k, s, p, ceil):
     torch.manual_seed(2)
