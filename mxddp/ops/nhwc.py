@@ -225,7 +225,7 @@ def conv2d(x, w, stride=1, padding=0, pack: WeightPack | None = None, join: Grad
             bnstat = [torch.empty((rows * 2 * K,), device=x.device, dtype=torch.float32), shift, 0]
     y = _Conv.apply(x, w, s, p, pack.get(w) if pack is not None else None, join, deposit, bnstat)
     if bnstat and bnstat[2] > 0:
-        y._mx_bnpre = (bnstat[0], bnstat[2], bnstat[1])  # (partials, rows, shift) for batch_norm
+        y._mx_bnpre = (bnstat[0], bnstat[2], bnstat[1], y._version)  # (partials, rows, shift, version)
     return y
 
 
@@ -294,10 +294,13 @@ def batch_norm(x, bn: torch.nn.BatchNorm2d, relu: bool = False, res: torch.Tenso
         nbt = bn.num_batches_tracked if (bn.training and bn.track_running_stats) else None
         # partial statistics from the producing conv's epilogue (conv2d(..., bn=bn)), valid only
         # for this exact tensor and shifted by this BN's running mean
+        # (an in-place change of x since the conv bumped its version: the partials are stale)
         pre = getattr(x, "_mx_bnpre", None)
         if pre is not None and (pre[2] is not (bn.running_mean if bn.track_running_stats else None)
-                                or pre[0].numel() != pre[1] * 2 * x.shape[-1]):
+                                or pre[0].numel() != pre[1] * 2 * x.shape[-1] or pre[3] != x._version):
             pre = None
+        if pre is not None:
+            pre = pre[:3]
         return _BN.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, res, relu, mom, bn.eps, join,
                          pre)
     y = (x.float() - bn.running_mean) * torch.rsqrt(bn.running_var + bn.eps) * bn.weight + bn.bias
