@@ -203,7 +203,7 @@ def _replica(a):
             return Adam(flat, lr=spec.lr, eps=1e-7, eps_hat=True)
         return SGD(flat, lr=a.lr, momentum=0.9, weight_decay=1e-4)
 
-    grp = ReplicaGroup(build_model(a.model), devices, make_opt)
+    grp = ReplicaGroup(build_model(a.model), devices, make_opt, use_graph=not a.no_graph)
     B = a.batch * a.gpus
     D = 1
     for s_ in spec.input_shape:
@@ -240,7 +240,7 @@ def _replica(a):
         "vs_baseline": None, "dtype": a.dtype, "data": _data_desc(spec),
         "config": {"model": a.model, "global_batch": B, "per_rank_batch": a.batch, "seq_len": None,
                    "image": "x".join(map(str, spec.input_shape)), "parallelism": f"replica{a.gpus}",
-                   "impl": "replica"}}), flush=True)
+                   "impl": "replica", "graph": grp._graphs is not None}}), flush=True)
 
 
 def _replica_fused(a, devices, spec):
