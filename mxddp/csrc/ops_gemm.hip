@@ -339,8 +339,10 @@ void run(Op& op, int splits, hipStream_t st) {
 // 36-63 k-tiles) leave most CUs idle and serialise the k-loop's load latency (~1 us per k-tile).
 // Such GEMMs run split-K: every split stores its raw partial sums to plane part[split][out
 // index], and splitk_finish_k sums the planes in a fixed order (deterministic) and applies the
-// epilogue (bias, ReLU, ReLU mask, accumulate).  The planes live in a grow-only per-device
-// buffer that only grows outside stream capture (a capture that would need more runs unsplit).
+// epilogue (bias, ReLU, ReLU mask, accumulate).  The planes live in ONE fixed per-device
+// buffer allocated on first use and never freed or moved: captured hipGraphs bake its address
+// into their kernel arguments (a grow-and-free buffer left replays of an earlier capture
+// reading freed memory).  A GEMM whose planes would not fit runs unsplit.
 int effective_splits(int K, int splits) {  // what igemm_*_launch will run (every split non-empty)
   const int BK = g_gemm_precision == 1 ? 32 : 16;
   if (splits <= 1) return 1;
@@ -348,30 +350,27 @@ int effective_splits(int K, int splits) {  // what igemm_*_launch will run (ever
   return cdiv(K, klen);
 }
 
+constexpr size_t kPlaneFloats = size_t(3) << 20;  // 12 MB per device
+
 float* splitk_planes(size_t floats, hipStream_t st) {
   static std::mutex mu;
-  static std::vector<std::pair<float*, size_t>> bufs;
+  static std::vector<float*> bufs;
+  if (floats > kPlaneFloats) return nullptr;
   int dev = 0;
   MX_HIP_CHECK(hipStreamGetDevice(st, &dev));
   std::lock_guard<std::mutex> lk(mu);
-  if ((int)bufs.size() <= dev) bufs.resize(dev + 1, {nullptr, 0});
-  auto& b = bufs[dev];
-  if (b.second >= floats) return b.first;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  MX_HIP_CHECK(hipStreamIsCapturing(st, &cs));
-  if (cs != hipStreamCaptureStatusNone) return nullptr;
-  int cur = 0;
-  MX_HIP_CHECK(hipGetDevice(&cur));
-  MX_HIP_CHECK(hipSetDevice(dev));
-  if (b.first) {  // earlier launches may still read the old planes
-    MX_HIP_CHECK(hipDeviceSynchronize());
-    MX_HIP_CHECK(hipFree(b.first));
+  if ((int)bufs.size() <= dev) bufs.resize(dev + 1, nullptr);
+  if (!bufs[dev]) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    MX_HIP_CHECK(hipStreamIsCapturing(st, &cs));
+    if (cs != hipStreamCaptureStatusNone) return nullptr;  // no allocation inside a capture
+    int cur = 0;
+    MX_HIP_CHECK(hipGetDevice(&cur));
+    MX_HIP_CHECK(hipSetDevice(dev));
+    MX_HIP_CHECK(hipMalloc(&bufs[dev], kPlaneFloats * sizeof(float)));
+    MX_HIP_CHECK(hipSetDevice(cur));
   }
-  const size_t n = std::max(floats, 2 * b.second);
-  MX_HIP_CHECK(hipMalloc(&b.first, n * sizeof(float)));
-  b.second = n;
-  MX_HIP_CHECK(hipSetDevice(cur));
-  return b.first;
+  return bufs[dev];
 }
 
 // out[i] = epilogue(sum_s part[s][i]); bias channel of i = (i / inner) % C

@@ -191,10 +191,15 @@ class SyntheticLoader:
     """Class-conditional synthetic images of the real dataset's shape, generated on the
     device each step (GPU: Philox kernel; CPU: torch generator).  ``steps`` batches/epoch."""
 
-    def __init__(self, shape, num_classes: int, batch_size: int, steps: int, device, seed: int = 1, rank: int = 0):
+    def __init__(self, shape, num_classes: int, batch_size: int, steps: int, device, seed: int = 1, rank: int = 0,
+                 template_seed: int | None = None):
+        """``template_seed`` (default ``seed``) fixes the class templates: a held-out set drawn with
+        another ``seed`` but the training run's template seed comes from the same distribution."""
         self.shape, self.nc, self.batch_size, self.steps = tuple(shape), num_classes, batch_size, steps
         self.device = torch.device(device)
         self.seed = seed + 7919 * rank
+        if template_seed is not None:
+            seed = template_seed
         D = int(np.prod(shape))
         self.D = D
         if self.device.type == "cuda":
@@ -230,7 +235,8 @@ DATASET_SIZES = {"mnist": 60000, "cifar10": 50000, "imagenet": 1281167}
 
 
 def build_loader(dataset: str, data: str, root: str, batch_size: int, device, world_size: int, rank: int,
-                 seed: int, shape, num_classes: int, train: bool = True, steps: int | None = None):
+                 seed: int, shape, num_classes: int, train: bool = True, steps: int | None = None,
+                 template_seed: int | None = None):
     """data: 'synthetic' | 'real' | 'auto' (real if files exist, else synthetic)."""
     if data in ("real", "auto"):
         try:
@@ -250,4 +256,4 @@ def build_loader(dataset: str, data: str, root: str, batch_size: int, device, wo
     n = DATASET_SIZES.get(dataset, 50000)
     if steps is None:
         steps = math.ceil(math.ceil(n / world_size) / batch_size)
-    return SyntheticLoader(shape, num_classes, batch_size, steps, device, seed, rank), "synthetic"
+    return SyntheticLoader(shape, num_classes, batch_size, steps, device, seed, rank, template_seed), "synthetic"

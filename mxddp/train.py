@@ -67,7 +67,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--per-rank-batch", type=int, default=None, help="override: batch per process")
     p.add_argument("--nproc-per-node", type=int, default=1, help="spawn this many ranks on this node")
     p.add_argument("--cpu", action="store_true", help="force the CPU path (gloo)")
-    p.add_argument("--no-graph", action="store_true", help="fused engine: launch eagerly instead of hipGraph replay")
+    p.add_argument("--no-graph", action="store_true",
+                   help="fused engine / replica mode: launch eagerly instead of hipGraph replay")
     p.add_argument("--debug-sync", action="store_true",
                    help="synchronise and check for faults after every kernel launch (implies --no-graph)")
     p.add_argument("--bucket-cap-mb", type=float, default=25.0)
@@ -283,7 +284,7 @@ def _maybe_eval(args, inf, spec, model, bs, mw, epoch=None, force=False):
     tb = max(1, min(args.test_batch_size, math.ceil(10000 / ws)))
     loader, kind = build_loader(spec.dataset, args.data, args.dataset_dir, tb, inf.device, ws, rank,
                                 args.seed + 99, spec.input_shape, spec.num_classes, train=False,
-                                steps=max(1, math.ceil(10000 / ws / tb)))
+                                steps=max(1, math.ceil(10000 / ws / tb)), template_seed=args.seed)
     loss, acc = evaluate(model, loader, inf.device)
     if ws > 1:
         loss, acc = [v / ws for v in C.all_reduce_sum([loss, acc])]
@@ -442,7 +443,13 @@ def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
         return _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw)
     torch.manual_seed(args.seed)
     model = build_model(spec.name, **_model_kwargs(args, spec))
-    group = ReplicaGroup(model, devices, lambda f: _make_opt(opt_name, f, lr, mom, wd, spec))
+    # per-device step graphs are opt-in here (MXDDP_REPLICA_GRAPH=1): with per-epoch evaluation +
+    # TensorBoard histograms, 3 of 6 graph-mode runs diverged in epoch 2 while every eager run
+    # and every graph run without those extensions trained normally (cause not found yet,
+    # profiles/r2_replica_graph/); bench.py's replica mode uses them
+    group = ReplicaGroup(model, devices, lambda f: _make_opt(opt_name, f, lr, mom, wd, spec),
+                         use_graph=(devices[0].type == "cuda" and not args.no_graph
+                                    and os.environ.get("MXDDP_REPLICA_GRAPH", "0") == "1"))
     scheds = [StepLR(o, args.lr_step_size, args.lr_gamma) for o in group.optimizers] if args.lr_step_size else []
     loader, kind = build_loader(spec.dataset, args.data, args.dataset_dir, bs, devices[0], 1, 0, args.seed,
                                 spec.input_shape, spec.num_classes, train=True, steps=args.steps_per_epoch)

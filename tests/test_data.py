@@ -88,6 +88,18 @@ def test_synthetic_loader_cpu_learnable_shape():
     assert float(xs[0][0].min()) >= 0.0 and float(xs[0][0].max()) <= 1.0
 
 
+def test_synthetic_heldout_set_shares_training_templates():
+    """The held-out synthetic set (another sample seed) keeps the training run's class templates:
+    a nearest-template classifier fit on the train templates labels it correctly."""
+    train = SyntheticLoader((1, 28, 28), 10, 64, 1, "cpu", seed=1)
+    test = SyntheticLoader((1, 28, 28), 10, 64, 1, "cpu", seed=100, template_seed=1)
+    other = SyntheticLoader((1, 28, 28), 10, 64, 1, "cpu", seed=100)
+    assert torch.equal(train.tmpl, test.tmpl) and not torch.equal(train.tmpl, other.tmpl)
+    x, y = next(iter(test))
+    pred = torch.cdist(x.flatten(1), train.tmpl).argmin(1)
+    assert (pred == y).float().mean() > 0.9
+
+
 def test_build_loader_auto_falls_back_to_synthetic(tmp_path):
     ld, kind = build_loader("mnist", "auto", str(tmp_path), 16, "cpu", 2, 0, 1, (1, 28, 28), 10)
     assert kind == "synthetic" and len(ld) == 30000 // 16 + 1 - (1 if 30000 % 16 == 0 else 0)
