@@ -443,10 +443,10 @@ def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
         return _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw)
     torch.manual_seed(args.seed)
     model = build_model(spec.name, **_model_kwargs(args, spec))
-    # per-device step graphs are opt-in here (MXDDP_REPLICA_GRAPH=1): with per-epoch evaluation +
-    # TensorBoard histograms, 3 of 6 graph-mode runs diverged in epoch 2 while every eager run
-    # and every graph run without those extensions trained normally (cause not found yet,
-    # profiles/r2_replica_graph/); bench.py's replica mode uses them
+    # per-device step graphs are opt-in here (MXDDP_REPLICA_GRAPH=1): graph-mode runs with
+    # TensorBoard weight histograms diverged in epoch 2 while every eager run and graph runs
+    # with evaluation only trained normally (cause not found yet, profiles/r2_replica_graph/);
+    # bench.py's replica mode uses them
     group = ReplicaGroup(model, devices, lambda f: _make_opt(opt_name, f, lr, mom, wd, spec),
                          use_graph=(devices[0].type == "cuda" and not args.no_graph
                                     and os.environ.get("MXDDP_REPLICA_GRAPH", "0") == "1"))
