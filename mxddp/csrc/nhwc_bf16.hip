@@ -1212,62 +1212,92 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv f
 }
 
 // ------------------------------------------------------------------------------------------
-// max pool (k x k, stride, pad) with uint8 argmax tap; backward gathers over covering windows
+// max pool (k x k, stride, pad) with uint8 argmax tap; backward gathers over covering windows.
+// 32-bit indices through FastDiv (sizes checked on the host), the 8 taps of a channel vector
+// loaded / stored as one 8-byte word, and the window loops unrolled for the ResNet stem pool
+// (KS = 3; KS = 0: runtime k).
+template <int KS>
 __global__ void maxpool_nhwc_k(const bf16* __restrict__ x, bf16* __restrict__ y, uint8_t* __restrict__ arg, int N,
-                               int H, int W, int C, int P, int Q, int k, int st, int pd) {
+                               int H, int W, int C, int P, int Q, int kr, int st, int pd, FastDiv fV, FastDiv fQ,
+                               FastDiv fP) {
+  const int k = KS ? KS : kr;
   const int V = C >> 3;
-  const int64_t total = (int64_t)N * P * Q * V;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int v = (int)(i % V);
-    const int64_t pix = i / V;
-    const int q = (int)(pix % Q), p = (int)((pix / Q) % P), n = (int)(pix / ((int64_t)P * Q));
+  const int total = N * P * Q * V;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int pix = (int)fV.div((uint32_t)i), v = i - pix * V;
+    const int pq = (int)fQ.div((uint32_t)pix), q = pix - pq * Q;
+    const int n = (int)fP.div((uint32_t)pq), p = pq - n * P;
     float best[8];
-    uint8_t bi[8];
+    uint32_t b0 = 0, b1 = 0;  // argmax taps, 4 per word
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
-    for (int r = 0; r < k; ++r)
-      for (int s = 0; s < k; ++s) {
-        const int h = p * st - pd + r, w = q * st - pd + s;
-        if ((unsigned)h >= (unsigned)H || (unsigned)w >= (unsigned)W) continue;
-        float xv[8];
-        unpack8(*reinterpret_cast<const uint4*>(x + (((size_t)n * H + h) * W + w) * C + 8 * v), xv);
+    for (int e = 0; e < 8; ++e) best[e] = -INFINITY;
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (xv[e] > best[e]) { best[e] = xv[e]; bi[e] = (uint8_t)(r * k + s); }
+    for (int r = 0; r < (KS ? KS : 1); ++r) {
+      for (int rr = (KS ? r : 0); rr < (KS ? r + 1 : k); ++rr) {
+#pragma unroll
+        for (int s = 0; s < (KS ? KS : 1); ++s) {
+          for (int ss = (KS ? s : 0); ss < (KS ? s + 1 : k); ++ss) {
+            const int h = p * st - pd + rr, w = q * st - pd + ss;
+            if ((unsigned)h >= (unsigned)H || (unsigned)w >= (unsigned)W) continue;
+            float xv[8];
+            unpack8(*reinterpret_cast<const uint4*>(x + ((size_t)(n * H + h) * W + w) * C + 8 * v), xv);
+            const uint32_t tap = (uint32_t)(rr * k + ss);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (xv[e] > best[e]) {
+                best[e] = xv[e];
+                if (e < 4) b0 = (b0 & ~(0xffu << (8 * e))) | (tap << (8 * e));
+                else b1 = (b1 & ~(0xffu << (8 * (e - 4)))) | (tap << (8 * (e - 4)));
+              }
+          }
+        }
       }
+    }
     reinterpret_cast<uint4*>(y)[i] = pack8(best);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) arg[i * 8 + e] = bi[e];
+    reinterpret_cast<uint2*>(arg)[i] = make_uint2(b0, b1);
   }
 }
 
+template <int KS>
 __global__ void maxpool_nhwc_bwd_k(const bf16* __restrict__ dy, const uint8_t* __restrict__ arg, bf16* __restrict__ dx,
-                                   int N, int H, int W, int C, int P, int Q, int k, int st, int pd) {
+                                   int N, int H, int W, int C, int P, int Q, int kr, int st, int pd, FastDiv fV,
+                                   FastDiv fW, FastDiv fH, FastDiv fS) {
+  const int k = KS ? KS : kr;
   const int V = C >> 3;
-  const int64_t total = (int64_t)N * H * W * V;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int v = (int)(i % V);
-    const int64_t pix = i / V;
-    const int w = (int)(pix % W), h = (int)((pix / W) % H), n = (int)(pix / ((int64_t)H * W));
+  const int total = N * H * W * V;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int pix = (int)fV.div((uint32_t)i), v = i - pix * V;
+    const int hw = (int)fW.div((uint32_t)pix), w = pix - hw * W;
+    const int n = (int)fH.div((uint32_t)hw), h = hw - n * H;
     float g[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) g[e] = 0.f;
-    for (int r = 0; r < k; ++r) {
-      const int tp = h + pd - r;
-      if (tp < 0 || tp % st) continue;
-      const int p = tp / st;
-      if (p >= P) continue;
-      for (int s = 0; s < k; ++s) {
-        const int tq = w + pd - s;
-        if (tq < 0 || tq % st) continue;
-        const int q = tq / st;
-        if (q >= Q) continue;
-        const int64_t o = (((int64_t)n * P + p) * Q + q) * V + v;
-        float dv[8];
-        unpack8(reinterpret_cast<const uint4*>(dy)[o], dv);
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (arg[o * 8 + e] == (uint8_t)(r * k + s)) g[e] += dv[e];
+    for (int r = 0; r < (KS ? KS : 1); ++r) {
+      for (int rr = (KS ? r : 0); rr < (KS ? r + 1 : k); ++rr) {
+        const int tp = h + pd - rr;
+        if (tp < 0) continue;
+        const int p = (int)fS.div((uint32_t)tp);
+        if (p * st != tp || p >= P) continue;
+#pragma unroll
+        for (int s = 0; s < (KS ? KS : 1); ++s) {
+          for (int ss = (KS ? s : 0); ss < (KS ? s + 1 : k); ++ss) {
+            const int tq = w + pd - ss;
+            if (tq < 0) continue;
+            const int q = (int)fS.div((uint32_t)tq);
+            if (q * st != tq || q >= Q) continue;
+            const int o = ((n * P + p) * Q + q) * V + v;
+            float dv[8];
+            unpack8(reinterpret_cast<const uint4*>(dy)[o], dv);
+            const uint2 a2 = reinterpret_cast<const uint2*>(arg)[o];
+            const uint32_t tap = (uint32_t)(rr * k + ss);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t t = ((e < 4 ? a2.x : a2.y) >> (8 * (e & 3))) & 0xffu;
+              if (t == tap) g[e] += dv[e];
+            }
+          }
+        }
       }
     }
     reinterpret_cast<uint4*>(dx)[i] = pack8(g);
@@ -1719,14 +1749,20 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
 
 void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, int k,
                       int s, int p, hipStream_t st) {
-  MX_LAUNCH(maxpool_nhwc_k, dim3(grid_for((int64_t)N * P * Q * (C / 8))), dim3(256), 0, st, x, y, arg, N, H, W, C, P,
-            Q, k, s, p);
+  MX_CHECK(C % 8 == 0 && (int64_t)N * H * W * C / 8 < (1ll << 31), "nhwc maxpool: C % 8 and 32-bit indices");
+  const dim3 g(grid_for((int64_t)N * P * Q * (C / 8))), b(256);
+  const FastDiv fV(C / 8), fQ(Q), fP(P);
+  if (k == 3) MX_LAUNCH(maxpool_nhwc_k<3>, g, b, 0, st, x, y, arg, N, H, W, C, P, Q, k, s, p, fV, fQ, fP);
+  else MX_LAUNCH(maxpool_nhwc_k<0>, g, b, 0, st, x, y, arg, N, H, W, C, P, Q, k, s, p, fV, fQ, fP);
 }
 
 void nhwc_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int P, int Q,
                       int k, int s, int p, hipStream_t st) {
-  MX_LAUNCH(maxpool_nhwc_bwd_k, dim3(grid_for((int64_t)N * H * W * (C / 8))), dim3(256), 0, st, dy, arg, dx, N, H, W,
-            C, P, Q, k, s, p);
+  MX_CHECK(C % 8 == 0 && (int64_t)N * H * W * C / 8 < (1ll << 31), "nhwc maxpool: C % 8 and 32-bit indices");
+  const dim3 g(grid_for((int64_t)N * H * W * (C / 8))), b(256);
+  const FastDiv fV(C / 8), fW(W), fH(H), fS(s);
+  if (k == 3) MX_LAUNCH(maxpool_nhwc_bwd_k<3>, g, b, 0, st, dy, arg, dx, N, H, W, C, P, Q, k, s, p, fV, fW, fH, fS);
+  else MX_LAUNCH(maxpool_nhwc_bwd_k<0>, g, b, 0, st, dy, arg, dx, N, H, W, C, P, Q, k, s, p, fV, fW, fH, fS);
 }
 
 void nhwc_gap_fwd(const uint16_t* x, float* y, int N, int HW, int C, hipStream_t st) {

@@ -233,15 +233,16 @@ def test_weight_pack_matches_per_conv_repack(cuda):
     assert pack.matches(specs) and not pack.matches(specs[:2])
 
 
-def test_pools_nhwc(cuda):
+@pytest.mark.parametrize("k,s,p", [(3, 2, 1), (2, 2, 0), (3, 1, 1)])
+def test_pools_nhwc(cuda, k, s, p):
     torch.manual_seed(3)
     x = torch.randn(2, 13, 11, 16).to(torch.bfloat16)
     xr = _nchw(x).requires_grad_()
-    yr = F.max_pool2d(xr, 3, 2, 1)
+    yr = F.max_pool2d(xr, k, s, p)
     gy = torch.randn_like(yr).to(torch.bfloat16).float()
     yr.backward(gy)
     xg = x.to(cuda).requires_grad_()
-    y = nhwc.max_pool2d(xg, 3, 2, 1)
+    y = nhwc.max_pool2d(xg, k, s, p)
     y.backward(gy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(cuda))
     assert torch.equal(_nchw(y), yr.detach())
     assert _rel(_nchw(xg.grad), xr.grad) < 1e-2
