@@ -791,13 +791,21 @@ __global__ __launch_bounds__(256) void wgrad_nhwc_reduce_k(const float* __restri
 // ------------------------------------------------------------------------------------------
 // layout / weight conversion
 // x fp32 [N][C][H][W] -> bf16 [N][H][W][Cp] (zeros for c >= C)
-__global__ void nchw_to_nhwc_k(const float* __restrict__ x, bf16* __restrict__ y, int N, int C, int HW, int Cp) {
-  const int64_t total = (int64_t)N * HW * Cp;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int c = (int)(i % Cp);
-    const int64_t nhw = i / Cp;
-    const int n = (int)(nhw / HW), hw = (int)(nhw - (int64_t)n * HW);
-    y[i] = c < C ? f2bf(x[((int64_t)n * C + c) * HW + hw]) : (bf16)0;
+// one thread per (pixel, 8-channel group): 8 coalesced fp32 plane reads, one 16-byte store,
+// 32-bit FastDiv indexing (the per-element 64-bit divisions and 2-byte stores ran at ~1.7 TB/s)
+__global__ void nchw_to_nhwc_k(const float* __restrict__ x, uint4* __restrict__ y, int N, int C, int HW, int G,
+                               FastDiv fG, FastDiv fHW) {
+  const int total = N * HW * G;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int pix = (int)fG.div((uint32_t)i), g = i - pix * G;
+    const int n = (int)fHW.div((uint32_t)pix), hw = pix - n * HW;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = 8 * g + e;
+      v[e] = c < C ? x[((size_t)n * C + c) * HW + hw] : 0.f;
+    }
+    y[i] = pack8(v);
   }
 }
 
@@ -1333,7 +1341,10 @@ int grid_for(int64_t n, int cap = 4096) {
 
 // ------------------------------------------------------------------------------------------
 void nhwc_from_nchw(const float* x, uint16_t* y, int N, int C, int H, int W, int Cp, hipStream_t st) {
-  MX_LAUNCH(nchw_to_nhwc_k, dim3(grid_for((int64_t)N * H * W * Cp)), dim3(256), 0, st, x, y, N, C, H * W, Cp);
+  MX_CHECK(Cp % 8 == 0 && C <= Cp && (int64_t)N * H * W * Cp / 8 < (1ll << 31), "nhwc_from_nchw: Cp % 8, 32-bit indices");
+  const int G = Cp / 8;
+  MX_LAUNCH(nchw_to_nhwc_k, dim3(grid_for((int64_t)N * H * W * G)), dim3(256), 0, st, x, reinterpret_cast<uint4*>(y), N,
+            C, H * W, G, FastDiv(G), FastDiv(H * W));
 }
 
 void nhwc_repack_weight(const float* w, uint16_t* wt, uint16_t* wtd, int K, int C, int R, int S, int Cp,

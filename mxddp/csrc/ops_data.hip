@@ -24,17 +24,27 @@ __global__ void synth_batch_k(float* __restrict__ x, int32_t* __restrict__ y, co
                               int D, int C, uint64_t seed, int32_t* counter) {
   const uint32_t ctr = (uint32_t)*counter;
   const uint2 key = synth_key(seed);
+  // blockIdx.y splits an image over several blocks (a 224x224x3 image per block left the
+  // ImageNet-shape batch on one block per CU); values depend only on (counter, b, d), so the
+  // mapping does not change the data
+  const bool vec = (D & 3) == 0;  // rows 16-byte aligned: float4 template loads / stores
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
     const int label = synth_label(ctr, b, C, key);
-    if (threadIdx.x == 0) y[b] = label;
+    if (threadIdx.x == 0 && blockIdx.y == 0) y[b] = label;
     const float* tp = tmpl + (int64_t)label * D;
     float* xp = x + (int64_t)b * D;
-    for (int d = threadIdx.x * 4; d < D; d += blockDim.x * 4) {
+    for (int d = (blockIdx.y * blockDim.x + threadIdx.x) * 4; d < D; d += gridDim.y * blockDim.x * 4) {
       const uint4 r = synth_noise4(ctr, b, d, key);
-      const uint32_t rv[4] = {r.x, r.y, r.z, r.w};
+      if (vec) {
+        const float4 t = *reinterpret_cast<const float4*>(tp + d);
+        *reinterpret_cast<float4*>(xp + d) = make_float4(0.5f * t.x + 0.5f * u01(r.x), 0.5f * t.y + 0.5f * u01(r.y),
+                                                         0.5f * t.z + 0.5f * u01(r.z), 0.5f * t.w + 0.5f * u01(r.w));
+      } else {
+        const uint32_t rv[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (d + j < D) xp[d + j] = 0.5f * tp[d + j] + 0.5f * u01(rv[j]);
+        for (int j = 0; j < 4; ++j)
+          if (d + j < D) xp[d + j] = 0.5f * tp[d + j] + 0.5f * u01(rv[j]);
+      }
     }
   }
 }
@@ -91,7 +101,8 @@ void synth_templates(float* templates, int C, int D, uint64_t seed, hipStream_t 
 
 void synth_batch(float* x, int32_t* y, const float* templates, int B, int D, int C, uint64_t seed, int32_t* counter,
                  hipStream_t st, bool bump) {
-  MX_LAUNCH(synth_batch_k, dim3(B < 1024 ? B : 1024), dim3(256), 0, st, x, y, templates, B, D, C, seed,
+  const int gy = std::max(1, std::min(64, (D + 256 * 4 * 8 - 1) / (256 * 4 * 8)));  // >= 8 float4 per thread
+  MX_LAUNCH(synth_batch_k, dim3(B < 1024 ? B : 1024, gy), dim3(256), 0, st, x, y, templates, B, D, C, seed,
                      counter);
   if (bump) MX_LAUNCH(bump_counter_k, dim3(1), dim3(1), 0, st, counter);
 }

@@ -233,6 +233,17 @@ def test_weight_pack_matches_per_conv_repack(cuda):
     assert pack.matches(specs) and not pack.matches(specs[:2])
 
 
+@pytest.mark.parametrize("C,cp", [(3, 8), (13, 16), (16, None)])
+def test_to_nhwc_exact(cuda, C, cp):
+    """fp32 NCHW -> bf16 NHWC with zero channel padding: exactly the rounded permute."""
+    torch.manual_seed(1)
+    x = torch.randn(3, C, 9, 7)
+    y = nhwc.to_nhwc(x.to(cuda), cp).cpu()
+    ref = x.permute(0, 2, 3, 1).to(torch.bfloat16)
+    assert y.shape[-1] == (cp or C) and torch.equal(y[..., :C], ref)
+    assert not y[..., C:].any()
+
+
 @pytest.mark.parametrize("k,s,p", [(3, 2, 1), (2, 2, 0), (3, 1, 1)])
 def test_pools_nhwc(cuda, k, s, p):
     torch.manual_seed(3)
