@@ -32,6 +32,9 @@ from .. import native
 from .flat import FlatParams, flatten_buffers
 
 
+_REPLAY_SIDE = __import__("os").environ.get("MXDDP_REPLICA_REPLAY_SIDE", "0") == "1"
+
+
 class ReplicaGroup:
     def __init__(self, model: nn.Module, devices: list[torch.device], make_optimizer, broadcast_buffers: bool = True,
                  use_graph: bool = False):
@@ -124,7 +127,7 @@ class ReplicaGroup:
     def _capture(self, xs, ys, loss_fn):
         self._xs = [t.to(d).clone() for t, d in zip(xs, self.devices)]
         self._ys = [t.to(d).clone() for t, d in zip(ys, self.devices)]
-        self._outs, graphs = [], []
+        self._outs, graphs, self._sides = [], [], []
         for i, (m, d) in enumerate(zip(self.replicas, self.devices)):
             with torch.cuda.device(d):
                 cur = torch.cuda.current_stream(d)
@@ -137,6 +140,7 @@ class ReplicaGroup:
                     loss.backward()
                 cur.wait_stream(side)
             graphs.append(g)
+            self._sides.append(side)
             self._outs.append((loss, correct))
         self._graphs = graphs
 
@@ -145,7 +149,14 @@ class ReplicaGroup:
             with torch.cuda.device(d):
                 self._xs[i].copy_(xs[i], non_blocking=True)
                 self._ys[i].copy_(ys[i], non_blocking=True)
-                self._graphs[i].replay()
+                if _REPLAY_SIDE:  # replay on the capture stream, fenced both ways (diagnostic)
+                    cur, side = torch.cuda.current_stream(d), self._sides[i]
+                    side.wait_stream(cur)
+                    with torch.cuda.stream(side):
+                        self._graphs[i].replay()
+                    cur.wait_stream(side)
+                else:
+                    self._graphs[i].replay()
         self._all_reduce_grads()
         for opt in self.optimizers:
             opt.step()
