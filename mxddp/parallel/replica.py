@@ -33,6 +33,7 @@ from .flat import FlatParams, flatten_buffers
 
 
 _REPLAY_SIDE = __import__("os").environ.get("MXDDP_REPLICA_REPLAY_SIDE", "0") == "1"
+_REPLAY_SYNC = __import__("os").environ.get("MXDDP_REPLICA_SYNC", "")
 
 
 class ReplicaGroup:
@@ -149,6 +150,8 @@ class ReplicaGroup:
             with torch.cuda.device(d):
                 self._xs[i].copy_(xs[i], non_blocking=True)
                 self._ys[i].copy_(ys[i], non_blocking=True)
+                if _REPLAY_SYNC == "before":  # diagnostic: prior eager work finished on the host
+                    torch.cuda.current_stream(d).synchronize()
                 if _REPLAY_SIDE:  # replay on the capture stream, fenced both ways (diagnostic)
                     cur, side = torch.cuda.current_stream(d), self._sides[i]
                     side.wait_stream(cur)
@@ -157,6 +160,8 @@ class ReplicaGroup:
                     cur.wait_stream(side)
                 else:
                     self._graphs[i].replay()
+                if _REPLAY_SYNC == "after":  # diagnostic: the graph finished before the optimizer
+                    torch.cuda.current_stream(d).synchronize()
         self._all_reduce_grads()
         for opt in self.optimizers:
             opt.step()

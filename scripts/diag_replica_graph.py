@@ -1,6 +1,7 @@
 """Replica-mode hipGraph divergence hunt: train the Keras CNN with ReplicaGroup(use_graph=True)
 for one 'epoch', do ACTION (none | cpu_read: copy every parameter to the host | sleep: idle the
 host 50 ms | sync: device synchronize), train another epoch; print the loss trajectory."""
+import os
 import sys
 import time
 
@@ -29,7 +30,7 @@ for epoch in range(epochs):
     for i, (x, y) in enumerate(loader):
         ls, _ = grp.step(x, y, loss_fn)
         acc += ls / 512
-        if 95 <= epoch * steps + i <= 135:
+        if os.environ.get("DIAG_PER_STEP") and 95 <= epoch * steps + i <= 135:
             per_step.append(round(ls.item() / 512, 3))
         if i % 20 == 19:
             traj.append(round(acc.item() / 20, 4))
