@@ -203,10 +203,9 @@ def _replica(a):
             return Adam(flat, lr=spec.lr, eps=1e-7, eps_hat=True)
         return SGD(flat, lr=a.lr, momentum=0.9, weight_decay=1e-4)
 
-    # per-device step graphs: opt-in (MXDDP_REPLICA_GRAPH=1) while the epoch-2 divergence seen in
-    # graph-mode training runs is open (docs/BENCHMARKS.md, replica mode)
+    # per-device step graphs (MXDDP_REPLICA_GRAPH=0: eager)
     grp = ReplicaGroup(build_model(a.model), devices, make_opt,
-                       use_graph=not a.no_graph and os.environ.get("MXDDP_REPLICA_GRAPH", "0") == "1")
+                       use_graph=not a.no_graph and os.environ.get("MXDDP_REPLICA_GRAPH", "1") == "1")
     B = a.batch * a.gpus
     D = 1
     for s_ in spec.input_shape:

@@ -352,7 +352,7 @@ bool conv3x3_wgrad_eligible(const ConvShape& s) {
 }
 
 void conv3x3_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate, hipStream_t st) {
-  if (!accumulate) MX_HIP_CHECK(hipMemsetAsync(dw, 0, sizeof(float) * (size_t)s.K * s.C * 9, st));
+  if (!accumulate) zero_fill(dw, (int64_t)s.K * s.C * 9, st);
   C3WArgs a{};
   a.dy = dy;
   a.x = x;

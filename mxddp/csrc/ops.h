@@ -114,6 +114,8 @@ void relu_bwd(const float* dy, const float* y, float* dx, int64_t n, hipStream_t
 void bias_grad(const float* dy, float* db, int outer, int C, int inner, bool accumulate,
                hipStream_t st, const float* dy_mask = nullptr);
 void add_inplace(float* y, const float* x, int64_t n, hipStream_t st);
+// p[0..n) = 0 by a kernel (not a memset node inside captured graphs)
+void zero_fill(float* p, int64_t n, hipStream_t st);
 void scale_inplace(float* y, float a, int64_t n, hipStream_t st);
 void fill(float* y, float v, int64_t n, hipStream_t st);
 

@@ -127,6 +127,16 @@ __global__ void maxpool_fwd_k(const float* __restrict__ x, float* __restrict__ y
   }
 }
 
+// zero fill as a compute kernel: inside a captured hipGraph a memset becomes a separate memset
+// node (a copy-engine operation on ROCm); kernels keep every node of a step on the compute queue
+__global__ void zero_fill_k(float* __restrict__ p, int64_t n, int vec) {
+  const int64_t n4 = vec ? n >> 2 : 0;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
+    p4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t i = 4 * n4 + blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0.f;
+}
+
 __global__ void maxpool_bwd_k(const float* __restrict__ dy, const int32_t* __restrict__ idx, float* __restrict__ dx,
                               int NC, int H, int W, int P, int Q) {
   const int64_t total = (int64_t)NC * P * Q;
@@ -316,6 +326,12 @@ void bias_grad(const float* dy, float* db, int outer, int C, int inner, bool acc
   MX_LAUNCH(bias_grad_k, dim3(C), dim3(kBgTB), 0, st, dy, db, outer, C, inner, FastDiv((uint32_t)inner),
             accumulate ? 1 : 0);
 }
+void zero_fill(float* p, int64_t n, hipStream_t st) {
+  if (n <= 0) return;
+  const int vec = (reinterpret_cast<uintptr_t>(p) & 15) == 0;  // float4 body only when aligned
+  MX_LAUNCH(zero_fill_k, dim3((unsigned)std::min<int64_t>((n / 4 + 255) / 256 + 1, 2048)), dim3(256), 0, st, p, n,
+            vec);
+}
 void maxpool2d_fwd(const float* x, float* y, int32_t* idx, int N, int C, int H, int W, int kh, int kw, int sh,
                    int sw, int ph, int pw, int P, int Q, hipStream_t st) {
   MX_LAUNCH(maxpool_fwd_k, dim3(grid_for((int64_t)N * C * P * Q)), dim3(kTB), 0, st, x, y, idx, N * C, H,
@@ -323,7 +339,7 @@ void maxpool2d_fwd(const float* x, float* y, int32_t* idx, int N, int C, int H, 
 }
 void maxpool2d_bwd(const float* dy, const int32_t* idx, float* dx, int N, int C, int H, int W, int P, int Q,
                    hipStream_t st) {
-  MX_HIP_CHECK(hipMemsetAsync(dx, 0, sizeof(float) * (size_t)N * C * H * W, st));
+  zero_fill(dx, (int64_t)N * C * H * W, st);
   MX_LAUNCH(maxpool_bwd_k, dim3(grid_for((int64_t)N * C * P * Q)), dim3(kTB), 0, st, dy, idx, dx, N * C,
                      H, W, P, Q);
 }
@@ -334,7 +350,7 @@ void avgpool2d_fwd(const float* x, float* y, int N, int C, int H, int W, int kh,
 }
 void avgpool2d_bwd(const float* dy, float* dx, int N, int C, int H, int W, int kh, int kw, int sh, int sw, int ph,
                    int pw, int P, int Q, hipStream_t st) {
-  MX_HIP_CHECK(hipMemsetAsync(dx, 0, sizeof(float) * (size_t)N * C * H * W, st));
+  zero_fill(dx, (int64_t)N * C * H * W, st);
   MX_LAUNCH(avgpool_bwd_k, dim3(grid_for((int64_t)N * C * P * Q)), dim3(kTB), 0, st, dy, dx, N * C, H, W,
                      kh, kw, sh, sw, ph, pw, P, Q);
 }

@@ -574,7 +574,7 @@ void conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s
   if (splits == 1) {
     op.mode = accumulate ? kAccum : kStore;
   } else if (!accumulate) {
-    MX_HIP_CHECK(hipMemsetAsync(dw, 0, sizeof(float) * (size_t)op.M * op.N, st));
+    zero_fill(dw, (int64_t)op.M * op.N, st);
   }
   run(op, splits, st);
 }
@@ -588,7 +588,7 @@ void linear_fwd(const float* x, const float* w, const float* b, float* y, int M,
   int splits = relu ? 1 : pick_splits(tiles, K, 256, 256);
   if (splits > 1) {
     op.mode = kAtomic;
-    MX_HIP_CHECK(hipMemsetAsync(y, 0, sizeof(float) * (size_t)M * N, st));
+    zero_fill(y, (int64_t)M * N, st);
   }
   run(op, splits, st);
 }
@@ -613,7 +613,7 @@ void linear_wgrad(const float* dy, const float* x, float* dw, int M, int N, int 
     op.mode = accumulate ? kAccum : kStore;
   } else {
     op.mode = kAtomic;
-    if (!accumulate) MX_HIP_CHECK(hipMemsetAsync(dw, 0, sizeof(float) * (size_t)N * K, st));
+    if (!accumulate) zero_fill(dw, (int64_t)N * K, st);
   }
   run(op, splits, st);
 }

@@ -848,7 +848,7 @@ void launch_fwd(const float* x, const float* w, const float* bias, const float* 
   a.splits = cdiv(nch, a.chunks_per_split);
   a.relu = relu;
   if (a.splits > 1) {
-    if (!accumulate) MX_HIP_CHECK(hipMemsetAsync(y, 0, sizeof(float) * (size_t)N * Co * Wd * Wd, st));
+    if (!accumulate) zero_fill(y, (int64_t)N * Co * Wd * Wd, st);
     a.accumulate = 2;
   } else {
     a.accumulate = accumulate ? 1 : 0;

@@ -443,13 +443,10 @@ def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
         return _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw)
     torch.manual_seed(args.seed)
     model = build_model(spec.name, **_model_kwargs(args, spec))
-    # per-device step graphs are opt-in here (MXDDP_REPLICA_GRAPH=1): graph-mode runs with
-    # TensorBoard weight histograms diverged in epoch 2 while every eager run and graph runs
-    # with evaluation only trained normally (cause not found yet, profiles/r2_replica_graph/);
-    # bench.py's replica mode uses them
+    # per-device step graphs (MXDDP_REPLICA_GRAPH=0 or --no-graph: eager)
     group = ReplicaGroup(model, devices, lambda f: _make_opt(opt_name, f, lr, mom, wd, spec),
                          use_graph=(devices[0].type == "cuda" and not args.no_graph
-                                    and os.environ.get("MXDDP_REPLICA_GRAPH", "0") == "1"))
+                                    and os.environ.get("MXDDP_REPLICA_GRAPH", "1") == "1"))
     scheds = [StepLR(o, args.lr_step_size, args.lr_gamma) for o in group.optimizers] if args.lr_step_size else []
     loader, kind = build_loader(spec.dataset, args.data, args.dataset_dir, bs, devices[0], 1, 0, args.seed,
                                 spec.input_shape, spec.num_classes, train=True, steps=args.steps_per_epoch)

@@ -25,8 +25,10 @@ loader = SyntheticLoader(spec.input_shape, 10, 512, steps, dev, seed=1)
 loss_fn = lambda o, t: ops.cross_entropy(o, t, return_correct=True)  # noqa: E731
 traj = []
 per_step = []
+acc = torch.zeros((), device=dev)
 for epoch in range(epochs):
-    acc = torch.zeros((), device=dev)
+    if action != "noalloc":
+        acc = torch.zeros((), device=dev)
     for i, (x, y) in enumerate(loader):
         ls, _ = grp.step(x, y, loss_fn)
         acc += ls / 512
