@@ -32,10 +32,6 @@ from .. import native
 from .flat import FlatParams, flatten_buffers
 
 
-_REPLAY_SIDE = __import__("os").environ.get("MXDDP_REPLICA_REPLAY_SIDE", "0") == "1"
-_REPLAY_SYNC = __import__("os").environ.get("MXDDP_REPLICA_SYNC", "")
-
-
 class ReplicaGroup:
     def __init__(self, model: nn.Module, devices: list[torch.device], make_optimizer, broadcast_buffers: bool = True,
                  use_graph: bool = False):
@@ -128,7 +124,7 @@ class ReplicaGroup:
     def _capture(self, xs, ys, loss_fn):
         self._xs = [t.to(d).clone() for t, d in zip(xs, self.devices)]
         self._ys = [t.to(d).clone() for t, d in zip(ys, self.devices)]
-        self._outs, graphs, self._sides = [], [], []
+        self._outs, graphs = [], []
         for i, (m, d) in enumerate(zip(self.replicas, self.devices)):
             with torch.cuda.device(d):
                 cur = torch.cuda.current_stream(d)
@@ -141,7 +137,6 @@ class ReplicaGroup:
                     loss.backward()
                 cur.wait_stream(side)
             graphs.append(g)
-            self._sides.append(side)
             self._outs.append((loss, correct))
         self._graphs = graphs
 
@@ -150,18 +145,7 @@ class ReplicaGroup:
             with torch.cuda.device(d):
                 self._xs[i].copy_(xs[i], non_blocking=True)
                 self._ys[i].copy_(ys[i], non_blocking=True)
-                if _REPLAY_SYNC == "before":  # diagnostic: prior eager work finished on the host
-                    torch.cuda.current_stream(d).synchronize()
-                if _REPLAY_SIDE:  # replay on the capture stream, fenced both ways (diagnostic)
-                    cur, side = torch.cuda.current_stream(d), self._sides[i]
-                    side.wait_stream(cur)
-                    with torch.cuda.stream(side):
-                        self._graphs[i].replay()
-                    cur.wait_stream(side)
-                else:
-                    self._graphs[i].replay()
-                if _REPLAY_SYNC == "after":  # diagnostic: the graph finished before the optimizer
-                    torch.cuda.current_stream(d).synchronize()
+                self._graphs[i].replay()
         self._all_reduce_grads()
         for opt in self.optimizers:
             opt.step()
