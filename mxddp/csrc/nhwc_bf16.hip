@@ -849,6 +849,29 @@ __global__ __launch_bounds__(256) void wrepack_many_k(const int64_t* __restrict_
   const int K = (int)d[3], C = (int)d[4], RS = (int)d[5], Cp = (int)d[6], b0 = (int)d[7];
   const int nb = (lo + 1 < n ? (int)desc[(lo + 1) * 8 + 7] : (int)gridDim.x) - b0;
   const int tf = wt ? K * RS * Cp : 0, td = wtd ? C * RS * K : 0;
+  if ((K & 7) == 0) {
+    // 8 consecutive outputs per thread (8 channels of one fwd (k, tap) row, or 8 output channels
+    // of one dgrad (c, tap) row): one 16-byte store instead of eight 2-byte ones (WeightPack
+    // places every layout at a 64-element boundary, so the stores are aligned)
+    for (int e = (((int)blockIdx.x - b0) * 256 + threadIdx.x) * 8; e < tf + td; e += nb * 256 * 8) {
+      float v[8];
+      if (e < tf) {
+        const int krs = e / Cp, c0 = e - krs * Cp;
+        const int k = krs / RS, rs = krs - k * RS;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = c0 + u < C ? w[(k * C + c0 + u) * RS + rs] : 0.f;
+        *reinterpret_cast<uint4*>(wt + e) = pack8(v);
+      } else {
+        const int j = e - tf;
+        const int crs = j / K, k0 = j - crs * K;
+        const int c = crs / RS, rs = crs - c * RS;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = w[((k0 + u) * C + c) * RS + rs];
+        *reinterpret_cast<uint4*>(wtd + j) = pack8(v);
+      }
+    }
+    return;
+  }
   for (int i = ((int)blockIdx.x - b0) * 256 + threadIdx.x; i < tf + td; i += nb * 256) {
     if (i < tf) {
       const int c = i % Cp, krs = i / Cp;

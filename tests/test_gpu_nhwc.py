@@ -216,7 +216,8 @@ def test_weight_pack_matches_per_conv_repack(cuda):
     Cn = native()
     torch.manual_seed(8)
     specs = [(torch.randn(64, 3, 7, 7, device=cuda), 8, False), (torch.randn(40, 64, 3, 3, device=cuda), 64, True),
-             (torch.randn(256, 64, 1, 1, device=cuda), 64, True), (torch.randn(24, 16, 3, 3, device=cuda), 16, False)]
+             (torch.randn(256, 64, 1, 1, device=cuda), 64, True), (torch.randn(24, 16, 3, 3, device=cuda), 16, False),
+             (torch.randn(20, 16, 3, 3, device=cuda), 16, True)]  # K % 8 != 0: the scalar repack path
     pack = nhwc.WeightPack(specs)
     pack.refresh()
     st = torch.cuda.current_stream().cuda_stream
