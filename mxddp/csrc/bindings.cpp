@@ -197,9 +197,10 @@ PYBIND11_MODULE(_C, m) {
     maxpool2d_fwd(P<const float>(x), P<float>(y), P<int32_t>(idx), N, C, H, W, kh, kw, sh, sw, ph, pw, P_, Q, S(st));
   });
   m.def("maxpool2d_bwd", [](uintptr_t dy, uintptr_t idx, uintptr_t dx, int N, int C, int H, int W, int P_, int Q,
-                            uintptr_t st) {
-    maxpool2d_bwd(P<const float>(dy), P<const int32_t>(idx), P<float>(dx), N, C, H, W, P_, Q, S(st));
-  });
+                            uintptr_t st, int sh, int sw) {
+    maxpool2d_bwd(P<const float>(dy), P<const int32_t>(idx), P<float>(dx), N, C, H, W, P_, Q, S(st), sh, sw);
+  }, py::arg("dy"), py::arg("idx"), py::arg("dx"), py::arg("N"), py::arg("C"), py::arg("H"), py::arg("W"),
+     py::arg("P"), py::arg("Q"), py::arg("st"), py::arg("sh") = 0, py::arg("sw") = 0);
   m.def("avgpool2d_fwd", [](uintptr_t x, uintptr_t y, int N, int C, int H, int W, int kh, int kw, int sh, int sw, int ph,
                             int pw, int P_, int Q, uintptr_t st) {
     avgpool2d_fwd(P<const float>(x), P<float>(y), N, C, H, W, kh, kw, sh, sw, ph, pw, P_, Q, S(st));

@@ -122,8 +122,9 @@ void fill(float* y, float v, int64_t n, hipStream_t st);
 // maxpool 2D (NCHW); idx stores the flat argmax offset inside the input plane.
 void maxpool2d_fwd(const float* x, float* y, int32_t* idx, int N, int C, int H, int W, int kh, int kw,
                    int sh, int sw, int ph, int pw, int P, int Q, hipStream_t st);
+// sh, sw > 0: the windows do not overlap (kernel == stride, no padding) -> gather, no zero fill
 void maxpool2d_bwd(const float* dy, const int32_t* idx, float* dx, int N, int C, int H, int W, int P,
-                   int Q, hipStream_t st);
+                   int Q, hipStream_t st, int sh = 0, int sw = 0);
 // avgpool 2D (count_include_pad=True semantics of nn.AvgPool2d, ceil_mode clipping)
 void avgpool2d_fwd(const float* x, float* y, int N, int C, int H, int W, int kh, int kw, int sh, int sw,
                    int ph, int pw, int P, int Q, hipStream_t st);

@@ -137,6 +137,24 @@ __global__ void zero_fill_k(float* __restrict__ p, int64_t n, int vec) {
   for (int64_t i = 4 * n4 + blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0.f;
 }
 
+// non-overlapping windows (kernel == stride, no padding): every input element has at most one
+// window, so dx is a gather -- every element written once, no zero fill, no atomics
+__global__ void maxpool_bwd_gather_k(const float* __restrict__ dy, const int32_t* __restrict__ idx,
+                                     float* __restrict__ dx, int total, int H, int W, int P, int Q, FastDiv fW,
+                                     FastDiv fH, FastDiv fsh, FastDiv fsw) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int r = (int)fW.div((uint32_t)i), w = i - r * W;
+    const int nc = (int)fH.div((uint32_t)r), h = r - nc * H;
+    const int p = (int)fsh.div((uint32_t)h), q = (int)fsw.div((uint32_t)w);
+    float v = 0.f;
+    if (p < P && q < Q) {
+      const int o = (nc * P + p) * Q + q;
+      if (idx[o] == h * W + w) v = dy[o];
+    }
+    dx[i] = v;
+  }
+}
+
 __global__ void maxpool_bwd_k(const float* __restrict__ dy, const int32_t* __restrict__ idx, float* __restrict__ dx,
                               int NC, int H, int W, int P, int Q) {
   const int64_t total = (int64_t)NC * P * Q;
@@ -338,7 +356,13 @@ void maxpool2d_fwd(const float* x, float* y, int32_t* idx, int N, int C, int H, 
                      W, kh, kw, sh, sw, ph, pw, P, Q);
 }
 void maxpool2d_bwd(const float* dy, const int32_t* idx, float* dx, int N, int C, int H, int W, int P, int Q,
-                   hipStream_t st) {
+                   hipStream_t st, int sh, int sw) {
+  if (sh > 0 && sw > 0 && (int64_t)N * C * H * W < (1ll << 31)) {
+    const int total = N * C * H * W;
+    MX_LAUNCH(maxpool_bwd_gather_k, dim3(grid_for(total)), dim3(kTB), 0, st, dy, idx, dx, total, H, W, P, Q,
+              FastDiv(W), FastDiv(H), FastDiv(sh), FastDiv(sw));
+    return;
+  }
   zero_fill(dx, (int64_t)N * C * H * W, st);
   MX_LAUNCH(maxpool_bwd_k, dim3(grid_for((int64_t)N * C * P * Q)), dim3(kTB), 0, st, dy, idx, dx, N * C,
                      H, W, P, Q);

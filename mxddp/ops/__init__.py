@@ -385,6 +385,8 @@ class _MaxPool2d(torch.autograd.Function):
                                p[0], p[1], P, Q, stream_of(x))
         ctx.save_for_backward(idx)
         ctx.shape = (N, Cc, H, W, P, Q)
+        # non-overlapping windows: the backward is a gather (no zero fill, no atomics)
+        ctx.gather = (s[0], s[1]) if (tuple(k) == tuple(s) and tuple(p) == (0, 0)) else (0, 0)
         return y
 
     @staticmethod
@@ -393,7 +395,8 @@ class _MaxPool2d(torch.autograd.Function):
         N, Cc, H, W, P, Q = ctx.shape
         dy = dy.contiguous()
         dx = torch.empty((N, Cc, H, W), device=dy.device, dtype=dy.dtype)
-        native().maxpool2d_bwd(dy.data_ptr(), idx.data_ptr(), dx.data_ptr(), N, Cc, H, W, P, Q, stream_of(dy))
+        native().maxpool2d_bwd(dy.data_ptr(), idx.data_ptr(), dx.data_ptr(), N, Cc, H, W, P, Q, stream_of(dy),
+                               *ctx.gather)
         return dx, None, None, None, None
 
 
