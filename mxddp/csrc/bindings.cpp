@@ -72,12 +72,12 @@ PYBIND11_MODULE(_C, m) {
      py::arg("pretransformed") = false);
   m.def("conv2d_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw_, int N, int C, int H, int W, int K, int R, int S_,
                            int sh, int sw, int ph, int pw, int dh, int dw, bool acc, uintptr_t st,
-                           uintptr_t scratch) {
-    conv2d_wgrad(P<const float>(dy), P<const float>(x), P<float>(dw_), CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw),
-                 acc, S(st), P<float>(scratch));
+                           uintptr_t scratch, uintptr_t db) {
+    return conv2d_wgrad(P<const float>(dy), P<const float>(x), P<float>(dw_),
+                        CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw), acc, S(st), P<float>(scratch), P<float>(db));
   }, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("N"), py::arg("C"), py::arg("H"), py::arg("W"), py::arg("K"),
      py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"),
-     py::arg("dwd"), py::arg("acc"), py::arg("st"), py::arg("scratch") = 0);
+     py::arg("dwd"), py::arg("acc"), py::arg("st"), py::arg("scratch") = 0, py::arg("db") = 0);
   m.def("conv_wgrad_scratch_floats", [](int N, int C, int H, int W, int K, int R, int S_, int sh, int sw, int ph,
                                         int pw, int dh, int dw) {
     return conv_wgrad_scratch_floats(CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw));

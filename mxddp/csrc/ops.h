@@ -87,8 +87,10 @@ int conv_algo();
 // floats of scratch conv2d_fwd / conv2d_dgrad can use for this shape (0 = none needed)
 size_t conv_scratch_floats(const ConvShape& s);
 // dw (+)= sum_{n,p,q} dy * im2col(x)
-void conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate,
-                  hipStream_t st, float* scratch = nullptr);
+// db (optional): the bias gradient sum_{n,p,q} dy is produced by the same GEMM (an extra column of
+// ones) where the generic path runs; returns whether it did (else the caller runs bias_grad)
+bool conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate,
+                  hipStream_t st, float* scratch = nullptr, float* db = nullptr);
 size_t conv_wgrad_scratch_floats(const ConvShape& s);
 // y[M,N] = x[M,K] @ w[N,K]^T + b  (optional ReLU)
 void linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int N, int K,

@@ -147,8 +147,12 @@ struct ConvWgradOp {
   const float* x;
   float* dw;
   int mode;
+  // db != null: GEMM column nw (= C*R*S) is a column of ones, so the same reduction over the
+  // B*P*Q pixels also produces the bias gradient (no separate bias_grad launch); N = nw + 1
+  float* db = nullptr;
+  int nw = 0;
   struct APre { int m; bool ok; };
-  struct BPre { int64_t coff; int r, s; bool ok; };
+  struct BPre { int64_t coff; int r, s; bool ok, one; };
   __device__ APre a_pre(int m) const { return APre{m, m < M}; }
   __device__ float a_load(const APre& a, int k) const {
     if (!a.ok) return 0.f;
@@ -157,7 +161,8 @@ struct ConvWgradOp {
   }
   __device__ BPre b_pre(int n) const {
     BPre b;
-    b.ok = n < N;
+    b.one = db != nullptr && n == nw;
+    b.ok = n < nw;
     const int nn = b.ok ? n : 0;
     const int c = g.fRS.div(nn), rs = nn - c * g.RS;
     b.r = g.fS.div(rs);
@@ -168,13 +173,17 @@ struct ConvWgradOp {
     return b;
   }
   __device__ float b_load(const BPre& b, int k) const {
+    if (b.one) return 1.f;
     const int nb = g.fPQ.div(k), pq = k - nb * g.PQ;
     const int p = g.fQ.div(pq), q = pq - p * g.Q;
     const int h = p * g.sh - g.ph + b.r, ww = q * g.sw - g.pw + b.s;
     if (!b.ok || (unsigned)h >= (unsigned)g.H || (unsigned)ww >= (unsigned)g.W) return 0.f;
     return x[(int64_t)nb * g.C * g.HW + b.coff + h * g.W + ww];
   }
-  __device__ void store(int m, int n, float v, int) const { emit(dw, (int64_t)m * N + n, v, mode); }
+  __device__ void store(int m, int n, float v, int) const {
+    if (n == nw) emit(db, m, v, mode);  // only reached when db is set (n < N = nw + 1)
+    else emit(dw, (int64_t)m * nw + n, v, mode);
+  }
 };
 
 // ------------------------------------------------------------------ 1x1 stride-1 convs
@@ -563,20 +572,32 @@ void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s
 
 size_t conv_wgrad_scratch_floats(const ConvShape& s) { return use_wino(s) ? wino_wgrad_scratch_floats(s) : 0; }
 
-void conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate,
-                  hipStream_t st, float* scratch) {
-  if (use_wino(s) && (scratch || wino_wgrad_scratch_floats(s) == 0))
-    return wino_wgrad(dy, x, dw, s, accumulate, scratch, st);
-  if (g_gemm_precision == 0 && conv3x3_wgrad_eligible(s)) return conv3x3_wgrad(dy, x, dw, s, accumulate, st);
+bool conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate,
+                  hipStream_t st, float* scratch, float* db) {
+  if (use_wino(s) && (scratch || wino_wgrad_scratch_floats(s) == 0)) {
+    wino_wgrad(dy, x, dw, s, accumulate, scratch, st);
+    return false;
+  }
+  if (g_gemm_precision == 0 && conv3x3_wgrad_eligible(s)) {
+    conv3x3_wgrad(dy, x, dw, s, accumulate, st);
+    return false;
+  }
   ConvWgradOp op{s.K, s.C * s.R * s.S, s.N * s.P * s.Q, ConvG(s), dy, x, dw, kAtomic};
+  op.nw = op.N;
+  if (db) {  // bias gradient as the extra column of ones
+    op.db = db;
+    op.N = op.nw + 1;
+  }
   const int tiles = cdiv(op.M, 64) * cdiv(op.N, 64);
   const int splits = pick_splits(tiles, op.K, tiles < 64 ? 128 : 512, 768);
   if (splits == 1) {
     op.mode = accumulate ? kAccum : kStore;
   } else if (!accumulate) {
-    zero_fill(dw, (int64_t)op.M * op.N, st);
+    zero_fill(dw, (int64_t)op.M * op.nw, st);
+    if (db) zero_fill(db, op.M, st);
   }
   run(op, splits, st);
+  return db != nullptr;
 }
 
 void linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int N, int K,

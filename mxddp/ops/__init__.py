@@ -241,17 +241,31 @@ class _Conv2d(torch.autograd.Function):
             C.conv2d_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph, pw,
                            dh, dw, 0, False, st, 0 if wt is None else wt.data_ptr(), pre)
         b = ctx.bias_ref
+        bias_done = False
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(w)
             dw_ = sink if sink is not None else torch.empty_like(w)
             ns = C.conv_wgrad_scratch_floats(N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw)
             ws = torch.empty((ns,), device=dy.device, dtype=dy.dtype) if ns else None
-            C.conv2d_wgrad(dy.data_ptr(), x.data_ptr(), dw_.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph, pw,
-                           dh, dw, sink is not None, st, _p(ws))
+            # the bias gradient rides along as an extra GEMM column when both gradients go to the
+            # same kind of destination (both flat-buffer sinks, or both fresh tensors)
+            db_t = None
+            if ctx.has_bias and ctx.needs_input_grad[2]:
+                bsink = _grad_sink(b)
+                if (bsink is None) == (sink is None):
+                    db_t = bsink if bsink is not None else torch.empty((K,), device=dy.device, dtype=dy.dtype)
+            bias_done = C.conv2d_wgrad(dy.data_ptr(), x.data_ptr(), dw_.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph,
+                                       pw, dh, dw, sink is not None, st, _p(ws), _p(db_t))
             if sink is not None:
                 _grad_done(w)
                 dw_ = None
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+            if bias_done:
+                if db_t is bsink:
+                    _grad_done(b)
+                    db = None
+                else:
+                    db = db_t
+        if ctx.has_bias and ctx.needs_input_grad[2] and not bias_done:
             sink = _grad_sink(b)
             db = sink if sink is not None else torch.empty((K,), device=dy.device, dtype=dy.dtype)
             C.bias_grad(dy.data_ptr(), db.data_ptr(), N, K, P * Q, sink is not None, st)
