@@ -141,9 +141,13 @@ def main():
     dt = C.all_reduce_max(time.perf_counter() - t0)
 
     if a.impl == "fused":
-        loss_sum, correct = tr.read_metrics()
+        # per-image averages over every step since the device accumulators were last zeroed
+        # (autotune zeroes them; warm-up, graph pre-launch and timed steps all accumulate):
+        # count the steps BEFORE any reset
+        loss_sum, correct = tr.read_metrics(reset=False)
         seen = max(1, (tr.steps - tr.steps_at_reset) * B)
-        extra = {"train_loss_avg": loss_sum / seen, "train_acc": correct / seen}
+        extra = {"train_loss_avg": round(loss_sum / seen, 5), "train_acc": round(correct / seen, 5),
+                 "train_images": seen}
     else:
         extra = {}
     if inf.rank == 0:
@@ -388,18 +392,19 @@ def _layers_or_torch(a, torch, inf, dev, comm, B):
         for _ in range(n):
             step()
 
-    # Whole-step hipGraph for the single-GPU layer path: the ~700 (ResNet-50) to ~1,500
-    # (PyramidNet) kernel launches of a step are replayed without Python / autograd overhead.
-    # Every op of the step is graph-safe (no host sync; LR, step counters and the synthetic
-    # data counter live on the device).
-    if a.impl == "layers" and not a.no_graph and inf.world_size == 1:
+    # Whole-step hipGraph for the layer path at ANY world size: the ~700 (ResNet-50) to ~1,500
+    # (PyramidNet) kernel launches of a step -- with the DDP buffer broadcast and every bucket
+    # all-reduce (RCCL or the peer transport, on the reducer's side stream) -- are replayed
+    # without Python / autograd overhead.  Every op of the step is graph-safe (no host sync; LR,
+    # Adam / BN step counters and the synthetic data counter live on the device).
+    if a.impl == "layers" and not a.no_graph:
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             run_eager(2)  # allocator / autograd warm-up outside the capture
         torch.cuda.current_stream(dev).wait_stream(side)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             step()
 
         def run_graph(n):

@@ -254,10 +254,10 @@ PYBIND11_MODULE(_C, m) {
                        int64_t n, bool first, uintptr_t st) {
     sgd_step(P<float>(p), P<const float>(g), P<float>(buf), P<const float>(lr), gscale, mom, wd, n, first, S(st));
   });
-  m.def("adam_step", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t lr, uintptr_t step,
-                        float gscale, float b1, float b2, float eps, float wd, int64_t n, uintptr_t st) {
-    adam_step(P<float>(p), P<const float>(g), P<float>(mm), P<float>(v), P<const float>(lr), P<const int32_t>(step),
-              gscale, b1, b2, eps, wd, n, S(st));
+  m.def("adam_step", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t lr, uintptr_t state,
+                        float gscale, float b1, float b2, float eps, float wd, bool eps_hat, int64_t n, uintptr_t st) {
+    adam_step(P<float>(p), P<const float>(g), P<float>(mm), P<float>(v), P<const float>(lr), P<int32_t>(state),
+              gscale, b1, b2, eps, wd, eps_hat, n, S(st));
   });
   m.def("synth_templates", [](uintptr_t t, int C, int D, uint64_t seed, uintptr_t st) {
     synth_templates(P<float>(t), C, D, seed, S(st));
@@ -363,6 +363,8 @@ PYBIND11_MODULE(_C, m) {
       .def("finalize", [](Reducer& r, uintptr_t st) { r.finalize(S(st)); })
       .def("comm_stream", [](Reducer& r) { return reinterpret_cast<uintptr_t>(r.comm_stream()); })
       .def("last_comm_ms", &Reducer::last_comm_ms)
+      .def("set_timing", &Reducer::set_timing)
+      .def_property_readonly("timing", &Reducer::timing)
       .def_property_readonly("num_buckets", &Reducer::num_buckets)
       .def_property_readonly("launched", &Reducer::launched)
       .def("set_overlap", &Reducer::set_overlap)
@@ -406,5 +408,6 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("stream", &MnistEngine::stream)
       .def_property_readonly("x_ptr", &MnistEngine::x_ptr)
       .def_property_readonly("y_ptr", &MnistEngine::y_ptr)
+      .def_property_readonly("counter_ptr", &MnistEngine::counter_ptr)
       .def_property_readonly("captured", &MnistEngine::captured);
 }

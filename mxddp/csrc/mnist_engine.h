@@ -96,6 +96,8 @@ class MnistEngine {
   uintptr_t stream() const { return reinterpret_cast<uintptr_t>(s_); }
   uintptr_t x_ptr() const { return reinterpret_cast<uintptr_t>(x_); }
   uintptr_t y_ptr() const { return reinterpret_cast<uintptr_t>(y_); }
+  // synthetic-data stream position (4 x int32 Philox counter): saved in the resume state
+  uintptr_t counter_ptr() const { return reinterpret_cast<uintptr_t>(counter_); }
   void set_external_batch(bool on) { external_batch_ = on; }
   // in-kernel phase timestamps (MnistFused::trace); 0 = off.  Eager steps only: a captured
   // graph keeps the arguments it was captured with.

@@ -227,9 +227,11 @@ void nhwc_gap_bwd(const float* dy, uint16_t* dx, int N, int HW, int C, hipStream
 // `lr` is read from device memory so a captured graph follows LR schedules.
 void sgd_step(float* p, const float* g, float* buf, const float* lr, float gscale, float momentum,
               float wd, int64_t n, bool first_step, hipStream_t st);
-// Adam (PyTorch/Keras semantics, bias-corrected); step counter read from device memory.
-void adam_step(float* p, const float* g, float* m, float* v, const float* lr, const int32_t* step,
-               float gscale, float b1, float b2, float eps, float wd, int64_t n, hipStream_t st);
+// Adam (PyTorch semantics, or Keras / Chainer eps_hat), bias-corrected.  `state` = int32[2]
+// device words {completed steps, arrival ticket (0 between launches)}: the kernel advances the
+// step count itself, so a captured graph needs no host value per step.
+void adam_step(float* p, const float* g, float* m, float* v, const float* lr, int32_t* state,
+               float gscale, float b1, float b2, float eps, float wd, bool eps_hat, int64_t n, hipStream_t st);
 
 // ---- data (ops_data.hip) ----
 // Class-conditional synthetic images: x = 0.5*template[y] + 0.5*noise, y ~ U{0..C-1}.

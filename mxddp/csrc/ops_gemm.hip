@@ -348,10 +348,13 @@ void run(Op& op, int splits, hipStream_t st) {
 // 36-63 k-tiles) leave most CUs idle and serialise the k-loop's load latency (~1 us per k-tile).
 // Such GEMMs run split-K: every split stores its raw partial sums to plane part[split][out
 // index], and splitk_finish_k sums the planes in a fixed order (deterministic) and applies the
-// epilogue (bias, ReLU, ReLU mask, accumulate).  The planes live in ONE fixed per-device
-// buffer allocated on first use and never freed or moved: captured hipGraphs bake its address
+// epilogue (bias, ReLU, ReLU mask, accumulate).  The planes live in one fixed buffer per
+// STREAM, allocated on first use and never freed or moved: captured hipGraphs bake its address
 // into their kernel arguments (a grow-and-free buffer left replays of an earlier capture
-// reading freed memory).  A GEMM whose planes would not fit runs unsplit.
+// reading freed memory), and GEMMs issued on two streams at once must not share planes (the
+// round-2 side-stream weight-gradient experiment did exactly that with one buffer per device).
+// A GEMM whose planes would not fit, or a stream beyond the first kMaxPlaneStreams of a
+// device, runs unsplit.
 int effective_splits(int K, int splits) {  // what igemm_*_launch will run (every split non-empty)
   const int BK = g_gemm_precision == 1 ? 32 : 16;
   if (splits <= 1) return 1;
@@ -359,27 +362,38 @@ int effective_splits(int K, int splits) {  // what igemm_*_launch will run (ever
   return cdiv(K, klen);
 }
 
-constexpr size_t kPlaneFloats = size_t(3) << 20;  // 12 MB per device
+constexpr size_t kPlaneFloats = size_t(3) << 20;  // 12 MB per stream
+constexpr int kMaxPlaneStreams = 8;                // per device
 
 float* splitk_planes(size_t floats, hipStream_t st) {
   static std::mutex mu;
-  static std::vector<float*> bufs;
+  struct Planes {
+    hipStream_t st;
+    int dev;
+    float* p;
+  };
+  static std::vector<Planes> bufs;  // never freed (a handle reused by a new stream reuses them)
   if (floats > kPlaneFloats) return nullptr;
   int dev = 0;
   MX_HIP_CHECK(hipStreamGetDevice(st, &dev));
   std::lock_guard<std::mutex> lk(mu);
-  if ((int)bufs.size() <= dev) bufs.resize(dev + 1, nullptr);
-  if (!bufs[dev]) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    MX_HIP_CHECK(hipStreamIsCapturing(st, &cs));
-    if (cs != hipStreamCaptureStatusNone) return nullptr;  // no allocation inside a capture
-    int cur = 0;
-    MX_HIP_CHECK(hipGetDevice(&cur));
-    MX_HIP_CHECK(hipSetDevice(dev));
-    MX_HIP_CHECK(hipMalloc(&bufs[dev], kPlaneFloats * sizeof(float)));
-    MX_HIP_CHECK(hipSetDevice(cur));
+  int on_dev = 0;
+  for (const auto& b : bufs) {
+    if (b.st == st && b.dev == dev) return b.p;
+    on_dev += b.dev == dev;
   }
-  return bufs[dev];
+  if (on_dev >= kMaxPlaneStreams) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  MX_HIP_CHECK(hipStreamIsCapturing(st, &cs));
+  if (cs != hipStreamCaptureStatusNone) return nullptr;  // no allocation inside a capture
+  int cur = 0;
+  float* p = nullptr;
+  MX_HIP_CHECK(hipGetDevice(&cur));
+  MX_HIP_CHECK(hipSetDevice(dev));
+  MX_HIP_CHECK(hipMalloc(&p, kPlaneFloats * sizeof(float)));
+  MX_HIP_CHECK(hipSetDevice(cur));
+  bufs.push_back({st, dev, p});
+  return p;
 }
 
 // out[i] = epilogue(sum_s part[s][i]); bias channel of i = (i / inner) % C

@@ -48,21 +48,36 @@ __global__ void sgd_k(float* __restrict__ p, const float* __restrict__ g, float*
   }
 }
 
+// Adam with the step count on the device, so a captured hipGraph replays it exactly: every
+// block reads the count of completed steps, t = count + 1; the LAST block to finish (arrival
+// ticket, agent-scope atomics) publishes count = t and rewinds the ticket.  Every block has read
+// the count before it arrives, so the update never races the reads; the next launch sees it.
+// eps_hat (Keras / Chainer): m_hat / (sqrt(v_hat) + eps)  ==  m / bc1 / (sqrt(v) / sqrt(bc2) +
+// eps / sqrt(bc2)); otherwise torch.optim.Adam's m_hat / (sqrt(v_hat) + eps).
 __global__ void adam_k(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                       float* __restrict__ v, const float* __restrict__ lr_ptr, const int32_t* __restrict__ step_ptr,
-                       float gscale, float b1, float b2, float eps, float wd, int64_t n) {
+                       float* __restrict__ v, const float* __restrict__ lr_ptr, int32_t* __restrict__ state,
+                       float gscale, float b1, float b2, float eps, float wd, int eps_hat, int64_t n) {
   const float lr = *lr_ptr;
-  const int t = *step_ptr;  // 1-based step count of THIS update
+  const int t = __hip_atomic_load(state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   const float bc1 = 1.f - powf(b1, (float)t), bc2 = 1.f - powf(b2, (float)t);
   const float step_size = lr / bc1;
   const float bc2s = sqrtf(bc2);
+  const float e = eps_hat ? eps / bc2s : eps;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const float gg = g[i] * gscale + wd * p[i];
     const float mi = b1 * m[i] + (1.f - b1) * gg;
     const float vi = b2 * v[i] + (1.f - b2) * gg * gg;
     m[i] = mi;
     v[i] = vi;
-    p[i] -= step_size * mi / (sqrtf(vi) / bc2s + eps);
+    p[i] -= step_size * mi / (sqrtf(vi) / bc2s + e);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int arrived = __hip_atomic_fetch_add(state + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (arrived == (int)gridDim.x - 1) {
+      __hip_atomic_store(state, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(state + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -82,10 +97,10 @@ void sgd_step(float* p, const float* g, float* buf, const float* lr, float gscal
                      first_step ? 1 : 0);
 }
 
-void adam_step(float* p, const float* g, float* m, float* v, const float* lr, const int32_t* step, float gscale,
-               float b1, float b2, float eps, float wd, int64_t n, hipStream_t st) {
-  MX_LAUNCH(adam_k, dim3(grid_for(n * 4)), dim3(256), 0, st, p, g, m, v, lr, step, gscale, b1, b2, eps,
-                     wd, n);
+void adam_step(float* p, const float* g, float* m, float* v, const float* lr, int32_t* state, float gscale,
+               float b1, float b2, float eps, float wd, bool eps_hat, int64_t n, hipStream_t st) {
+  MX_LAUNCH(adam_k, dim3(grid_for(n * 4)), dim3(256), 0, st, p, g, m, v, lr, state, gscale, b1, b2, eps,
+                     wd, eps_hat ? 1 : 0, n);
 }
 
 }  // namespace mx

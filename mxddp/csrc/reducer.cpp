@@ -29,7 +29,21 @@ Reducer::~Reducer() {
   if (comm_stream_) hipStreamDestroy(comm_stream_);
 }
 
-void Reducer::prepare() { sched_.prepare(); }
+void Reducer::prepare() {
+  MX_CHECK(!side_used_, "reducer: a new backward started while the previous one's side-stream all-reduces were "
+                        "never joined (finalize() not called): the optimizer would race the comm stream");
+  sched_.prepare();
+  in_step_ = true;
+  step_compute_ = nullptr;
+}
+
+void Reducer::set_timing(bool on) {
+  if (on && !t0_) {
+    MX_HIP_CHECK(hipEventCreate(&t0_));
+    MX_HIP_CHECK(hipEventCreate(&t1_));
+  }
+  timing_ = on;
+}
 
 void Reducer::mark_ready(int p, hipStream_t compute) {
   if (sched_.mark(p)) launch_ready(compute);
@@ -46,6 +60,11 @@ bool Reducer::active() const {
 
 void Reducer::launch_ready(hipStream_t compute) {
   const bool act = active();
+  if (in_step_) {
+    if (!step_compute_) step_compute_ = compute;
+    MX_CHECK(step_compute_ == compute, "reducer: buckets of one backward marked ready from two different compute "
+                                       "streams (each bucket's fence must follow the stream that wrote it)");
+  }
   for (int bi = sched_.pop_ready(); bi >= 0; bi = sched_.pop_ready()) {
     const BucketSchedule::Bucket& b = sched_.bucket(bi);
     if (act) {  // no collectives -> no fences either (a fence alone costs a few us of GPU idle)
@@ -71,6 +90,8 @@ void Reducer::launch_ready(hipStream_t compute) {
 void Reducer::finalize(hipStream_t compute) {
   sched_.release_all();  // unused parameters: reduce whatever the bucket holds (zeros on this rank)
   launch_ready(compute);
+  in_step_ = false;
+  step_compute_ = nullptr;
   if (!active()) return;
   if (timing_) {
     MX_HIP_CHECK(hipEventRecord(t1_, side_used_ ? comm_stream_ : compute));

@@ -11,7 +11,10 @@
 //    overlaps the remaining backward;
 //  * finalize() makes the compute stream wait on the comm stream before the optimizer.
 //  * debug checks: a parameter marked twice in one backward, or a bucket launched
-//    before all of its parameters were marked, raises (race detection).
+//    before all of its parameters were marked, raises (race detection);
+//    so do buckets of one backward marked from two different compute streams (the event
+//    fence would order the all-reduce after the wrong stream's work) and a new backward
+//    started while the previous one's side-stream all-reduces were never joined.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -42,6 +45,10 @@ class Reducer {
   // milliseconds between first bucket launch and comm completion of the last step
   // (requires timing=true; synchronises on the comm stream's end event).
   float last_comm_ms();
+  // time the next steps' comm window (eager steps only: a graph captured while timing would
+  // bake the event records in)
+  void set_timing(bool on);
+  bool timing() const { return timing_; }
   void set_comm(Comm* c) { comm_ = c; }
   // issue the collectives even at world_size 1 (exercises the RCCL + graph-capture path on
   // a single GPU; an all-reduce over one rank is the identity)
@@ -72,6 +79,10 @@ class Reducer {
   hipStream_t comm_stream_ = nullptr;
   hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
   bool timing_ = false, timed_ = false, force_ = false, overlap_ = true, side_used_ = false;
+  // stream discipline: every bucket of one backward is fenced against ONE compute
+  // stream, and a backward's side-stream work must be joined (finalize) before the next begins
+  hipStream_t step_compute_ = nullptr;
+  bool in_step_ = false;
 };
 
 }  // namespace mx

@@ -153,6 +153,16 @@ class TensorLoader:
         n = len(self.sampler)
         return n // self.batch_size if self.drop_last else math.ceil(n / self.batch_size)
 
+    def state_dict(self) -> dict:
+        """Stream position for resume: the sampler epoch (the shuffle of an epoch is a function
+        of (seed, epoch)) and the augmentation Philox counter."""
+        return {"sampler_epoch": self.sampler.epoch, "aug_counter": self._ctr.cpu().clone()}
+
+    def load_state_dict(self, sd: dict):
+        self.sampler.set_epoch(int(sd.get("sampler_epoch", self.sampler.epoch)))
+        if "aug_counter" in sd:
+            self._ctr.copy_(sd["aug_counter"].to(self._ctr.device))
+
     def __iter__(self):
         idx = torch.from_numpy(self.sampler.indices()).to(self.device)
         for i in range(len(self)):
@@ -215,6 +225,18 @@ class SyntheticLoader:
 
     def __len__(self):
         return self.steps
+
+    def state_dict(self) -> dict:
+        """Stream position for resume (GPU: the Philox counter; CPU: the generator state)."""
+        if self.device.type == "cuda":
+            return {"counter": self.ctr.cpu().clone()}
+        return {"gen_state": self.gen.get_state()}
+
+    def load_state_dict(self, sd: dict):
+        if self.device.type == "cuda" and "counter" in sd:
+            self.ctr.copy_(sd["counter"].to(self.ctr.device))
+        elif "gen_state" in sd:
+            self.gen.set_state(sd["gen_state"])
 
     def __iter__(self):
         for _ in range(self.steps):

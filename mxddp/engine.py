@@ -137,7 +137,7 @@ class FusedMnistTrainer:
         self.eng.capture(mode, spg)
         self._capture_done = True
 
-    def autotune(self, trial_steps: int = 24, include_graphs: bool | None = None) -> dict:
+    def autotune(self, trial_steps: int = 24, include_graphs: bool | None = None, restore: bool = False) -> dict:
         """Pick the fastest launch strategy for the DDP step on THIS machine by timing a few real
         training steps of each (they count as warm-up).  Candidates: gradient transport (RCCL
         ring, or the direct xGMI peer all-reduce when it validated) x bucket strategy (fc-bucket
@@ -146,8 +146,10 @@ class FusedMnistTrainer:
         one collective latency instead of two) x (eager launches, or the whole step captured in
         one hipGraph).  Peer-transport graphs are always tried (the
         peer kernel is an ordinary kernel); RCCL-in-graph only with MXDDP_AUTOTUNE_GRAPHS=1.
-        The slowest rank's time decides, so every rank picks the same strategy.  Returns
-        {candidate: ms/step}."""
+        The slowest rank's time decides, so every rank picks the same strategy.  ``restore``:
+        the trial steps are scratch -- weights, momentum, data-stream position and metrics are
+        put back afterwards and the step count is unchanged (the trainer CLI, so that the trained
+        model and --max-steps still match epochs x batches).  Returns {candidate: ms/step}."""
         from .parallel import comm as pc
 
         if include_graphs is None:
@@ -157,6 +159,7 @@ class FusedMnistTrainer:
         transports = ["rccl", "peer"] if self.peer is not None else ["rccl"]
         if self.transport in ("rccl", "peer"):
             transports = [self.transport] if self.transport in transports else ["rccl"]
+        snap = self.snapshot() if restore else None
         cands = []
         for tr in transports:
             cands += [(tr, 0, "ovl"), (tr, 0, "inl"), (tr, 0, "one")]
@@ -197,7 +200,10 @@ class FusedMnistTrainer:
         if best[1]:
             self._capture(best[1])
         self._capture_done = True
-        self.read_metrics(reset=True)
+        if snap is not None:
+            self.restore(snap)
+        else:
+            self.read_metrics(reset=True)
         self.tuned = {"transport": best[0], "graph_mode": best[1], "buckets": best[2],
                       "trials_ms": {f"{t}/{m}/{s}": round(v, 4) for (t, m, s), v in results.items()}}
         return results
@@ -239,6 +245,40 @@ class FusedMnistTrainer:
     def _y_view(self):
         off = (self.eng.y_ptr - self.workspace.data_ptr()) // 4
         return self.workspace[off:off + self.batch].view(torch.int32)
+
+    def _counter_view(self):
+        off = (self.eng.counter_ptr - self.workspace.data_ptr()) // 4
+        return self.workspace[off:off + 4].view(torch.int32)
+
+    # --------------------------------------------------------------- snapshots
+    def data_state(self) -> torch.Tensor:
+        """Position of the on-device synthetic data stream (Philox counter), for resume state."""
+        self.eng.sync()
+        return self._counter_view().cpu().clone()
+
+    def load_data_state(self, ctr: torch.Tensor):
+        self.eng.sync()
+        self._counter_view().copy_(ctr.to(torch.int32).to(self.device))
+        torch.cuda.synchronize(self.device)
+
+    def snapshot(self) -> dict:
+        """Device copies of everything a training step changes (weights, momentum, data-stream
+        position, metric accumulators): restore() puts the trainer back exactly."""
+        self.eng.sync()
+        return {"params": self.params.clone(), "mom": self.mom.clone(), "ctr": self._counter_view().clone(),
+                "metrics": self.metrics.clone(), "steps": self.steps, "steps_at_reset": self.steps_at_reset}
+
+    def restore(self, snap: dict):
+        self.eng.sync()
+        with torch.cuda.stream(self.stream):
+            self.params.copy_(snap["params"])
+            self.mom.copy_(snap["mom"])
+            self._counter_view().copy_(snap["ctr"])
+            self.metrics.copy_(snap["metrics"])
+        self.eng.sync()
+        self.steps, self.steps_at_reset = snap["steps"], snap["steps_at_reset"]
+        self.eng.repack()  # conv2 weights pre-packed in MFMA fragment order + accumulator resets
+        self.eng.sync()
 
     def set_lr(self, lr: float):
         if lr != self._lr_host:

@@ -544,17 +544,26 @@ class _BatchNorm(torch.autograd.Function):
 
 
 _BN_PART: dict = {}
+_BN_PART_RETIRED: list = []
 
 
-def _bn_part(device, n):
-    """Partial-sum scratch of the split-reduction BN kernels (ops_bn.hip), one per device: every
-    call rewrites what it reads and BN calls are stream-ordered, so one buffer serves them all
-    (and a captured graph replays without any reset).  Grows only, so captured pointers stay
-    valid once the warm-up has seen the widest layer."""
-    buf = _BN_PART.get(device)
+def _bn_part(device, n, stream=None):
+    """Partial-sum scratch of the split-reduction BN kernels (ops_bn.hip), one per (device,
+    stream): every call rewrites what it reads and the BN calls of one stream are ordered, so one
+    buffer serves them all (and a captured graph replays without any reset); BNs issued on two
+    streams at once get two buffers (no cross-stream race on the partials).  When a wider layer
+    needs a bigger buffer the old one is RETIRED, never freed: a hipGraph captured earlier bakes
+    its address into its kernel arguments, and freeing it would leave those replays writing into
+    memory the caching allocator has handed to someone else."""
+    if stream is None:
+        stream = torch.cuda.current_stream(device).cuda_stream
+    key = (device, stream)
+    buf = _BN_PART.get(key)
     if buf is None or buf.numel() < n:
+        if buf is not None:
+            _BN_PART_RETIRED.append(buf)
         buf = torch.empty((max(n, 8192),), dtype=torch.float32, device=device)
-        _BN_PART[device] = buf
+        _BN_PART[key] = buf
     return buf
 
 

@@ -77,6 +77,10 @@ class SGD(_FlatOptimizer):
 
 
 class Adam(_FlatOptimizer):
+    """On a GPU the step count lives on the device (``_state``: completed steps, arrival ticket)
+    and the kernel advances it, so ``step()`` issues one launch and no host value: a captured
+    hipGraph replays Adam exactly (bias corrections and the eps_hat form included)."""
+
     def __init__(self, flat: FlatParams, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, eps_hat: bool = False):
         super().__init__(flat, lr)
@@ -84,30 +88,34 @@ class Adam(_FlatOptimizer):
         self.eps, self.weight_decay, self.eps_hat = eps, weight_decay, eps_hat
         self.m = torch.zeros_like(flat.data)
         self.v = torch.zeros_like(flat.data)
-        self.steps = 0
-        self._step_dev = torch.zeros(1, dtype=torch.int32, device=flat.data.device)
+        self._steps_host = 0  # CPU path / host mirror of the eager step count
+        self._state = torch.zeros(2, dtype=torch.int32, device=flat.data.device)
+
+    @property
+    def steps(self) -> int:
+        if self.flat.data.is_cuda:
+            return int(self._state[0].item())
+        return self._steps_host
 
     @torch.no_grad()
     def step(self):
         self._sync_lr()
-        self.steps += 1
         f = self.flat
-        eps = self.eps
-        if self.eps_hat:  # Keras/Chainer: m_hat / (sqrt(v_hat) + eps*sqrt(bc2)) form
-            eps = self.eps / (1.0 - self.b2 ** self.steps) ** 0.5
         if f.data.is_cuda:
-            self._step_dev.fill_(self.steps)
             native().adam_step(f.data.data_ptr(), f.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
-                               self._lr_dev.data_ptr(), self._step_dev.data_ptr(), float(self.grad_scale),
-                               self.b1, self.b2, float(eps), float(self.weight_decay), f.numel,
-                               torch.cuda.current_stream(f.data.device).cuda_stream)
+                               self._lr_dev.data_ptr(), self._state.data_ptr(), float(self.grad_scale),
+                               self.b1, self.b2, float(self.eps), float(self.weight_decay), bool(self.eps_hat),
+                               f.numel, torch.cuda.current_stream(f.data.device).cuda_stream)
             _ops.refresh_filters(f.data.device)
         else:
+            self._steps_host += 1
+            t = self._steps_host
+            eps = self.eps / (1.0 - self.b2 ** t) ** 0.5 if self.eps_hat else self.eps
             g = f.grad * self.grad_scale + self.weight_decay * f.data
             self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)
             self.v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
-            bc1 = 1 - self.b1 ** self.steps
-            bc2 = 1 - self.b2 ** self.steps
+            bc1 = 1 - self.b1 ** t
+            bc2 = 1 - self.b2 ** t
             denom = (self.v.sqrt() / bc2 ** 0.5).add_(eps)
             f.data.addcdiv_(self.m, denom, value=-self.lr / bc1)
 
@@ -118,7 +126,9 @@ class Adam(_FlatOptimizer):
         self.param_groups[0]["lr"] = sd["lr"]
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
-        self.steps = sd["steps"]
+        self._steps_host = int(sd["steps"])
+        self._state.fill_(0)
+        self._state[0] = int(sd["steps"])
 
 
 class StepLR:

@@ -58,7 +58,6 @@ def env_dist() -> dict:
         }
     if "SLURM_PROCID" in os.environ and "SLURM_NTASKS" in os.environ:
         ws = int(os.environ["SLURM_NTASKS"])
-        per_node = os.environ.get("SLURM_NTASKS_PER_NODE", str(ws)).split("(")[0].split(",")[0]
         if "MASTER_ADDR" not in os.environ and "SLURM_LAUNCH_NODE_IPADDR" in os.environ:
             os.environ["MASTER_ADDR"] = os.environ["SLURM_LAUNCH_NODE_IPADDR"]
         os.environ.setdefault("MASTER_PORT", str(29500 + int(os.environ.get("SLURM_JOB_ID", "0")) % 1000))
@@ -66,9 +65,24 @@ def env_dist() -> dict:
             "rank": int(os.environ["SLURM_PROCID"]),
             "world_size": ws,
             "local_rank": int(os.environ.get("SLURM_LOCALID", "0")),
-            "local_world_size": int(per_node) if per_node.isdigit() else ws,
+            "local_world_size": slurm_tasks_per_node(ws),
         }
     return {}
+
+
+def slurm_tasks_per_node(ws: int) -> int:
+    """Ranks on THIS node under srun.  SLURM_NTASKS_PER_NODE exists only with --ntasks-per-node;
+    SLURM_TASKS_PER_NODE is always set ("8(x2)" or "8,6" -- the first entry is this job's first
+    node; nodes are normally filled evenly); else SLURM_NTASKS / SLURM_NNODES.  Never silently
+    the global world size on a multi-node job (that would mark the ranks as sharing GPUs)."""
+    for key in ("SLURM_NTASKS_PER_NODE", "SLURM_TASKS_PER_NODE"):
+        v = os.environ.get(key, "").split("(")[0].split(",")[0].strip()
+        if v.isdigit() and int(v) > 0:
+            return int(v)
+    nn = os.environ.get("SLURM_NNODES", os.environ.get("SLURM_JOB_NUM_NODES", ""))
+    if nn.isdigit() and int(nn) > 0:
+        return max(1, -(-ws // int(nn)))
+    return ws
 
 
 def init_distributed(backend: str | None = None, init_method: str | None = None, rank: int | None = None,
@@ -87,6 +101,8 @@ def init_distributed(backend: str | None = None, init_method: str | None = None,
         use_gpu = torch.cuda.is_available()
     if backend is None:
         backend = "nccl" if use_gpu else "gloo"
+    if backend not in ("nccl", "gloo"):
+        raise RuntimeError(f"--dist-backend {backend!r}: nccl (= RCCL on MI355X) or gloo")
     if backend == "nccl" and not use_gpu:
         raise RuntimeError("--dist-backend nccl (RCCL) needs a GPU; use gloo for CPU runs")
     if use_gpu:
@@ -117,6 +133,8 @@ def rccl_comm(force: bool = False):
     inf = info()
     if (inf.world_size == 1 and not force) or inf.device.type != "cuda":
         return None
+    if inf.backend == "gloo" and not force:
+        return None  # --dist-backend gloo: gradients go over gloo (parallel/ddp.py), not RCCL
     if inf.world_size > 1 and shared_devices():
         return None  # RCCL refuses several ranks on one GPU; such jobs use the peer transport
     if _COMM is None and inf.world_size == 1:

@@ -70,18 +70,21 @@ class DistributedDataParallel(nn.Module):
         self.buckets, self.param_bucket = assign_buckets(numels, self.flat.offsets, self.flat.numel, bucket_cap_mb,
                                                          first_bucket_cap_mb)
         self.average = average
-        self._comm = _comm.rccl_comm() if self.device.type == "cuda" else None
-        self.transport = "rccl" if self.device.type == "cuda" else "gloo"
+        # --dist-backend gloo on a GPU (pytorch/distributed_data_parallel.py:46): honoured --
+        # the gradient buckets and broadcasts go over gloo (host-staged), not RCCL / peer
+        self.gloo_data = self.device.type == "cuda" and inf.backend == "gloo" and self.world_size > 1
+        native_reducer = self.device.type == "cuda" and not self.gloo_data
+        self._comm = _comm.rccl_comm() if native_reducer else None
         self._sync_params()
-        if self.device.type == "cuda":
+        if native_reducer:
             C = native()
             self.reducer = C.Reducer(self._comm, self.flat.grad.data_ptr(), C.DType.f32, self.buckets,
                                      self.param_bucket, C.RedOp.avg if average else C.RedOp.sum, timing)
         else:
             self.reducer = _GlooReducer(self.flat.grad, self.buckets, self.param_bucket, average, self.world_size)
-        self.transport = "rccl" if self.device.type == "cuda" else "gloo"
+        self.transport = "rccl" if native_reducer else "gloo"
         self.transport_ms = None
-        if self.device.type == "cuda" and self.world_size > 1:
+        if native_reducer and self.world_size > 1:
             self._select_transport(transport)
         self._queued = False
         # fires on both gradient paths: returned gradients and gradients the GPU kernels wrote
@@ -123,7 +126,9 @@ class DistributedDataParallel(nn.Module):
             C = native()
             self._comm.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), C.DType.f32, 0,
                                  torch.cuda.current_stream(self.device).cuda_stream)
-        elif t.is_cuda and self.transport == "peer":
+        elif self.gloo_data:
+            dist.broadcast(t, 0)  # gloo data plane: a GPU tensor is staged through the host
+        elif t.is_cuda and getattr(self, "transport", None) == "peer":
             # ranks sharing a GPU (no RCCL): broadcast = peer all-reduce of (rank 0 ? t : 0), exact
             # in fp32 and, unlike a host round trip, capturable into a hipGraph
             from . import peer as _peer

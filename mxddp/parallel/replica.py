@@ -16,10 +16,11 @@ DataParallel's replicate-every-step:
 * every replica runs its own flat optimizer step, so replicas never diverge;
 * all replicas' backward passes are issued by a single multi-root autograd call, which
   runs the per-device graphs concurrently on the autograd engine's device threads;
-* ``use_graph=True`` captures each replica's zero-grad + forward + backward into one hipGraph
-  per device after two eager warm-up steps (inputs copied into static per-device buffers), so
-  a step is n graph launches + one grouped all-reduce + the n optimizer launches, instead of
-  hundreds of Python-issued kernels per replica.
+* ``use_graph=True`` captures each replica's WHOLE step -- BN-buffer sync, zero-grad, forward,
+  backward, gradient average over the in-process peer transport, optimizer (SGD, or Adam with
+  its step count on the device), metric accumulation -- into one hipGraph per device after two
+  eager warm-up steps (inputs copied into static per-device buffers), so a step is n graph
+  launches and nothing else, instead of hundreds of Python-issued kernels per replica.
 """
 from __future__ import annotations
 
@@ -34,10 +35,10 @@ from .flat import FlatParams, flatten_buffers
 
 class ReplicaGroup:
     def __init__(self, model: nn.Module, devices: list[torch.device], make_optimizer, broadcast_buffers: bool = True,
-                 use_graph: bool = False):
+                 use_graph: bool = False, peer_blocks: int = 64):
         self.devices = [torch.device(d) for d in devices]
         self.use_graph = use_graph and all(torch.device(d).type == "cuda" for d in devices)
-        self._graphs = None  # per-device hipGraphs of zero-grad + forward + backward
+        self._graphs = None  # per-device hipGraphs of the WHOLE step
         self._eager_steps = 0
         base = model.to(self.devices[0])
         self.replicas = [base] + [copy.deepcopy(base).to(d) for d in self.devices[1:]]
@@ -45,11 +46,27 @@ class ReplicaGroup:
         self.buffers = [flatten_buffers(m, d) for m, d in zip(self.replicas, self.devices)] if broadcast_buffers else None
         self.optimizers = [make_optimizer(f) for f in self.flats]
         self.n = len(self.devices)
+        # per-device on-device metric accumulators (sum of per-image loss, correct count)
+        self._acc = [torch.zeros(2, device=d) for d in self.devices]
         self.comms = None
+        self.peers = None
         if self.n > 1:
             if any(d.type != "cuda" for d in self.devices):
                 raise ValueError("replica mode across several devices needs GPUs")
             self.comms = native().Comm.init_all([d.index for d in self.devices])
+            if self.use_graph:
+                # the in-graph gradient / buffer exchange: the peer transport opened in-process
+                # (device peer access, no IPC) -- an ordinary kernel per device, so each replica's
+                # whole step is one graph launch (RCCL's single-thread multi-device calls need a
+                # host-side group and stay on the eager path)
+                C = native()
+                self.peers = []
+                for i, d in enumerate(self.devices):
+                    with torch.cuda.device(d):
+                        self.peers.append(C.PeerComm(i, self.n, d.index, 32 << 20, peer_blocks))
+                for pc, d in zip(self.peers, self.devices):
+                    with torch.cuda.device(d):
+                        pc.open_local(self.peers)
         self._sync(self.flats[0].data, [f.data for f in self.flats])
         if self.n > 1:  # raw-pointer write to the replicas' weights: banked conv filters are stale
             from .. import ops
@@ -90,69 +107,99 @@ class ReplicaGroup:
             f.zero_grad()
 
     def step(self, x: torch.Tensor, y: torch.Tensor, loss_fn):
-        """One synchronous-replica step on a GLOBAL batch; returns (sum loss, #correct) tensors
-        on device 0 (no host sync)."""
+        """One synchronous-replica step on a GLOBAL batch.  Loss (per-image sum) and correct
+        count accumulate on the devices; read them with read_metrics() (no host sync here)."""
         xs, ys = x.chunk(self.n), y.chunk(self.n)
         if len(xs) != self.n:
             raise ValueError(f"global batch {x.shape[0]} smaller than the number of replicas {self.n}")
-        if self.buffers and self.buffers[0] is not None and self.n > 1:
-            self._sync(self.buffers[0], self.buffers)
         if self.use_graph:
             if self._graphs is None and self._eager_steps >= 2:  # allocator / autograd warmed up
                 self._capture(xs, ys, loss_fn)
             if self._graphs is not None and [t.shape for t in xs] == [t.shape for t in self._xs]:
                 return self._replay(xs, ys)
             self._eager_steps += 1
+        if self.buffers and self.buffers[0] is not None and self.n > 1:
+            self._sync(self.buffers[0], self.buffers)
         self.zero_grad()
-        losses, corrects, weights = [], [], []
+        losses, corrects = [], []
         for i, (m, d) in enumerate(zip(self.replicas, self.devices)):
             xi = xs[i].to(d, non_blocking=True)
             yi = ys[i].to(d, non_blocking=True)
             loss, correct = loss_fn(m(xi), yi)
             losses.append(loss)
             corrects.append(correct)
-            weights.append(xi.shape[0])
         torch.autograd.backward(losses)  # one multi-root call: per-device graphs run concurrently
         self._all_reduce_grads()
-        for opt in self.optimizers:
+        for i, opt in enumerate(self.optimizers):
             opt.step()
-        d0 = self.devices[0]
-        loss_sum = sum(l.detach().to(d0) * w for l, w in zip(losses, weights))
-        correct = sum(c.to(d0) for c in corrects)
-        return loss_sum, correct
+            self._accumulate(i, losses[i].detach(), corrects[i], xs[i].shape[0])
+
+    def _accumulate(self, i, loss, correct, n):
+        a = self._acc[i]
+        a[0].add_(loss * n)
+        a[1].add_(correct)
+
+    def read_metrics(self) -> tuple[float, float]:
+        """(sum of per-image losses, correct) over all replicas since the last read (host sync)."""
+        tot = [0.0, 0.0]
+        for i, d in enumerate(self.devices):
+            torch.cuda.synchronize(d) if d.type == "cuda" else None
+            v = self._acc[i].tolist()
+            tot[0] += v[0]
+            tot[1] += v[1]
+            self._acc[i].zero_()
+        self._check_peers()
+        return tot[0], tot[1]
+
+    def _check_peers(self):
+        for pc in self.peers or []:
+            if pc.error():
+                raise RuntimeError(f"replica all-reduce: replica {pc.error() - 1} never arrived (timeout)")
+
+    def _graph_step(self, i, loss_fn):
+        """Replica i's whole step, as captured: BN-buffer sync from replica 0, zero-grad,
+        forward, loss, backward, gradient average, optimizer, metric accumulation."""
+        C = native()
+        st = self._stream(i)
+        if self.n > 1 and self.buffers and self.buffers[i] is not None:
+            # broadcast from replica 0 = peer sum of (replica 0 ? buffers : 0): exact in fp32
+            if i != 0:
+                self.buffers[i].zero_()
+            self.peers[i].all_reduce(self.buffers[i].data_ptr(), self.buffers[i].numel(), C.DType.f32, st, C.RedOp.sum)
+        self.flats[i].zero_grad()
+        loss, correct = loss_fn(self.replicas[i](self._xs[i]), self._ys[i])
+        loss.backward()
+        if self.n > 1:
+            f = self.flats[i]
+            self.peers[i].all_reduce(f.grad.data_ptr(), f.numel, C.DType.f32, st, C.RedOp.avg)
+        self.optimizers[i].step()
+        self._accumulate(i, loss.detach(), correct, self._xs[i].shape[0])
 
     def _capture(self, xs, ys, loss_fn):
         self._xs = [t.to(d).clone() for t, d in zip(xs, self.devices)]
         self._ys = [t.to(d).clone() for t, d in zip(ys, self.devices)]
-        self._outs, graphs = [], []
-        for i, (m, d) in enumerate(zip(self.replicas, self.devices)):
+        graphs = []
+        for i, d in enumerate(self.devices):
             with torch.cuda.device(d):
                 cur = torch.cuda.current_stream(d)
                 side = torch.cuda.Stream(d)
                 side.wait_stream(cur)
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=side):
-                    self.flats[i].zero_grad()
-                    loss, correct = loss_fn(m(self._xs[i]), self._ys[i])
-                    loss.backward()
+                with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
+                    self._graph_step(i, loss_fn)
                 cur.wait_stream(side)
             graphs.append(g)
-            self._outs.append((loss, correct))
         self._graphs = graphs
 
     def _replay(self, xs, ys):
+        # EVERY replica's graph is launched before the host waits on any of them: each graph's
+        # gradient exchange waits on the GPUs for the other replicas
         for i, d in enumerate(self.devices):
             with torch.cuda.device(d):
                 self._xs[i].copy_(xs[i], non_blocking=True)
                 self._ys[i].copy_(ys[i], non_blocking=True)
+                self.optimizers[i]._sync_lr()
                 self._graphs[i].replay()
-        self._all_reduce_grads()
-        for opt in self.optimizers:
-            opt.step()
-        d0 = self.devices[0]
-        loss_sum = sum(l.detach().to(d0) * t.shape[0] for (l, _), t in zip(self._outs, self._xs))
-        correct = sum(c.to(d0) for _, c in self._outs)
-        return loss_sum, correct
 
     @property
     def module(self) -> nn.Module:

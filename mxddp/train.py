@@ -90,6 +90,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--chainer-out", type=str, default="",
                    help="Chainer trainer extensions: LogReport (<dir>/log), PrintReport, dump_graph (<dir>/cg.dot)")
     p.add_argument("--summary", action="store_true", help="print a Keras-style model summary")
+    p.add_argument("--profile-phases", action="store_true",
+                   help="layers path: eager steps; log steps write fwd / bwd / opt device times and the DDP comm "
+                        "window (ms) to the JSONL stream, with roctx ranges for rocprofv3 --marker-trace")
     p.add_argument("--epoch-checkpoints", action="store_true",
                    help="Keras ModelCheckpoint: weights-only <train-dir>/ckpt_<epoch>.pth every epoch (rank 0); "
                         "with --eval the final evaluation reloads the latest one first")
@@ -189,7 +192,11 @@ def main(argv=None) -> int:
     engine = args.engine
     if engine == "auto":
         engine = "fused" if (args.model == "mnist_cnn" and use_gpu and opt_name == "sgd" and mode != "replica"
-                             and bs % 16 == 0 and 16 <= bs <= 128 and args.dtype == "fp32") else "layers"
+                             and bs % 16 == 0 and 16 <= bs <= 128 and args.dtype == "fp32"
+                             and not (backend == "gloo" and inf.world_size > 1)) else "layers"
+    if engine == "fused" and use_gpu and backend == "gloo" and inf.world_size > 1:
+        raise SystemExit("--engine fused all-reduces over RCCL / the xGMI peer transport; with --dist-backend gloo "
+                         "use --engine layers (gradients over gloo) or --dist-backend nccl")
     if use_gpu:
         from . import native, ops
 
@@ -246,6 +253,14 @@ def _log_epoch(inf, mode, seconds):
         print(L.ddp_epoch_line(inf.rank, seconds), flush=True)
     elif inf.is_main:
         print(L.single_epoch_line(seconds), flush=True)
+
+
+class _null:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
 
 
 def _sync(dev):
@@ -312,6 +327,23 @@ def _reload_latest(args, inf, model):
         print(f"==> restored {os.path.basename(path)} for evaluation", flush=True)
 
 
+def _epoch_saves(args, inf, epoch, step, model_sd, opt_sd, sched_sd, loader=None, data_counters=None):
+    """End-of-epoch saves every training mode honours: the full resume state every
+    --save-every epochs (Chainer snapshot: chainer/train_mnist.py:91-93) and the Keras
+    ModelCheckpoint weights ckpt_<epoch>.pth (tensorflow2/mnist_mirror_strategy.py:64)."""
+    from .utils.checkpoint import save_epoch_weights, save_training_state
+
+    if args.save_every and epoch % args.save_every == 0:
+        extra = {}
+        if loader is not None and hasattr(loader, "state_dict"):
+            extra["data"] = loader.state_dict()
+        if data_counters is not None:
+            extra["data_counters"] = data_counters
+        save_training_state(args.train_dir, inf.rank, model_sd, opt_sd, sched_sd, epoch, step, extra=extra)
+    if args.epoch_checkpoints and inf.is_main:
+        save_epoch_weights(model_sd, args.train_dir, epoch)
+
+
 def _save_final(args, inf, mode, state_dict):
     if not args.save_model:
         return
@@ -333,7 +365,7 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
     from .optim import StepLR
     from .parallel.ddp import DistributedDataParallel as DDP
     from .parallel.flat import FlatParams
-    from .utils.checkpoint import load_training_state, save_training_state
+    from .utils.checkpoint import load_training_state
 
     dev = inf.device
     torch.manual_seed(args.seed)
@@ -346,6 +378,7 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
     opt = _make_opt(opt_name, flat, lr, mom, wd, spec)
     sched = StepLR(opt, args.lr_step_size, args.lr_gamma) if args.lr_step_size else None
     start_epoch = 1
+    st = {}
     if args.resume:
         st = load_training_state(args.resume)
         model.load_state_dict(st["model"])
@@ -359,6 +392,11 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
     loader, kind = build_loader(spec.dataset, args.data, args.dataset_dir, bs, dev, inf.world_size, inf.rank,
                                 args.seed, spec.input_shape, spec.num_classes, train=True,
                                 steps=args.steps_per_epoch)
+    step = 0
+    if args.resume:  # data-stream position (Chainer snapshot keeps the iterator position)
+        if "data" in st.get("extra", {}):
+            loader.load_state_dict(st["extra"]["data"])
+        step = int(st.get("step", 0))
     if inf.is_main:
         print(f"==> data: {kind}, {len(loader)} batches/epoch", flush=True)
         if args.summary:
@@ -366,37 +404,80 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
 
             print(model_summary(model, spec.input_shape, spec.name), flush=True)
     rep = _Reporter(args, inf)
-    step = 0
+    from .parallel.graphed import GraphedStep
+    from .utils.profiler import PhaseTimer
+    from .utils.profiler import range as roctx_range
+
+    cuda = dev.type == "cuda"
+    # --profile-phases: eager steps, and every log step is bracketed by device events per phase
+    # (fwd / bwd+comm / opt) with roctx ranges, plus the reducer's comm window (first bucket
+    # issued -> last bucket done); otherwise the whole step is ONE hipGraph at any world size
+    # (parallel/graphed.py) and log steps record the step's device time
+    profile = args.profile_phases and cuda
+    reducer = getattr(net, "reducer", None) if mode == "ddp" else None
+    loss_acc = torch.zeros((), device=dev)
+    corr_acc = torch.zeros((), device=dev)
+    pt = PhaseTimer(enabled=profile)
+    timing = {"on": False}
+
+    def train_step(x, y):
+        opt.zero_grad()
+        with pt.phase("fwd") if timing["on"] else _null(), roctx_range("fwd") if timing["on"] else _null():
+            out = net(x)
+            loss, corr = ops.cross_entropy(out, y, return_correct=True)
+        if rep.graph_path is not None:
+            rep.first_loss(loss, model)
+        with pt.phase("bwd") if timing["on"] else _null(), roctx_range("bwd") if timing["on"] else _null():
+            loss.backward()
+        with pt.phase("opt") if timing["on"] else _null(), roctx_range("opt") if timing["on"] else _null():
+            opt.step()
+        loss_acc.add_(loss.detach())
+        corr_acc.add_(corr)
+        return loss.detach(), corr
+
+    use_graph = cuda and not args.no_graph and not profile and not getattr(net, "gloo_data", False)
+    runner = GraphedStep(train_step, dev, warmup=2, before_replay=opt._sync_lr, enabled=use_graph)
     for epoch in range(start_epoch, args.epochs + 1):
         if hasattr(loader, "sampler"):
             loader.sampler.set_epoch(epoch)
         net.train()
-        loss_acc = torch.zeros((), device=dev)
-        corr_acc = torch.zeros((), device=dev)
+        loss_acc.zero_()
+        corr_acc.zero_()
         total = 0
         t_epoch = t_log = time.time()
         last_log = 0
         for bi, (x, y) in enumerate(loader):
-            opt.zero_grad()
-            out = net(x)
-            loss, corr = ops.cross_entropy(out, y, return_correct=True)
-            if step == 0:
-                rep.first_loss(loss, model)
-            loss.backward()
-            opt.step()
-            loss_acc += loss.detach()
-            corr_acc += corr
+            log = bi % args.log_interval == 0
+            timing["on"] = profile and log
+            if reducer is not None and profile and hasattr(reducer, "set_timing"):
+                reducer.set_timing(log)
+            ev = None
+            if cuda and log and not profile:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+            runner(x, y)
+            if ev is not None:
+                ev[1].record()
             total += x.shape[0]
             step += 1
-            if bi % args.log_interval == 0:
+            if log:
                 _sync(dev)
                 now = time.time()
                 bt = (now - t_log) / max(1, bi - last_log) if bi else now - t_log
                 t_log, last_log = now, bi
                 l_avg, acc = loss_acc.item() / (bi + 1), 100.0 * corr_acc.item() / total
                 _log_step(inf, mode, epoch, bi, len(loader), l_avg, acc, bt)
-                mw.write(kind="step", epoch=epoch, step=step, loss=l_avg, acc=acc, batch_time=bt,
-                         img_per_s=x.shape[0] * inf.world_size / max(bt, 1e-9))
+                rec = dict(kind="step", epoch=epoch, step=step, loss=l_avg, acc=acc, batch_time=bt,
+                           img_per_s=x.shape[0] * inf.world_size / max(bt, 1e-9), graph=runner.captured)
+                if ev is not None:
+                    rec["step_ms"] = ev[0].elapsed_time(ev[1])
+                if profile:
+                    rec.update({f"{k}_ms": v for k, v in pt.summary().items()})
+                    pt.totals.clear()
+                    pt.counts.clear()
+                    if reducer is not None and hasattr(reducer, "last_comm_ms") and getattr(reducer, "active", False):
+                        rec["comm_ms"] = reducer.last_comm_ms()
+                mw.write(**rec)
             if args.max_steps and step >= args.max_steps:
                 break
         _sync(dev)
@@ -406,13 +487,8 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
         val = _maybe_eval(args, inf, spec, model, bs, mw, epoch=epoch)
         nb_done = bi + 1
         rep.epoch_end(epoch, step, loss_acc.item() / max(1, nb_done), corr_acc.item() / max(1, total), val, model)
-        if args.save_every and epoch % args.save_every == 0:
-            save_training_state(args.train_dir, inf.rank, model.state_dict(), opt.state_dict(),
-                                sched.state_dict() if sched else None, epoch, step)
-        if args.epoch_checkpoints and inf.is_main:
-            from .utils.checkpoint import save_epoch_weights
-
-            save_epoch_weights(model.state_dict(), args.train_dir, epoch)
+        _epoch_saves(args, inf, epoch, step, model.state_dict(), opt.state_dict(),
+                     sched.state_dict() if sched else None, loader)
         if args.max_steps and step >= args.max_steps:
             break
     if args.epoch_checkpoints and args.eval:
@@ -443,6 +519,13 @@ def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
         return _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw)
     torch.manual_seed(args.seed)
     model = build_model(spec.name, **_model_kwargs(args, spec))
+    st, start_epoch = {}, 1
+    if args.resume:
+        from .utils.checkpoint import load_training_state
+
+        st = load_training_state(args.resume)
+        model.load_state_dict(st["model"])
+        start_epoch = st["epoch"] + 1
     # per-device step graphs (MXDDP_REPLICA_GRAPH=0 or --no-graph: eager)
     group = ReplicaGroup(model, devices, lambda f: _make_opt(opt_name, f, lr, mom, wd, spec),
                          use_graph=(devices[0].type == "cuda" and not args.no_graph
@@ -450,6 +533,16 @@ def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
     scheds = [StepLR(o, args.lr_step_size, args.lr_gamma) for o in group.optimizers] if args.lr_step_size else []
     loader, kind = build_loader(spec.dataset, args.data, args.dataset_dir, bs, devices[0], 1, 0, args.seed,
                                 spec.input_shape, spec.num_classes, train=True, steps=args.steps_per_epoch)
+    step = 0
+    if st:  # every replica's optimizer / scheduler from the one saved state (replicas are identical)
+        for o in group.optimizers:
+            o.load_state_dict(st["optimizer"])
+        for s_ in scheds:
+            if st.get("scheduler"):
+                s_.load_state_dict(st["scheduler"])
+        if "data" in st.get("extra", {}):
+            loader.load_state_dict(st["extra"]["data"])
+        step = int(st.get("step", 0))
     print(f"==> replica mode on {len(devices)} device(s), global batch {bs}, data {kind}", flush=True)
     if args.summary:
         from .utils.report import model_summary
@@ -462,39 +555,42 @@ def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
         rep.first_loss(loss_fn(group.module(x0[:max(1, x0.shape[0] // len(devices))].to(devices[0])),
                                y0[:max(1, x0.shape[0] // len(devices))].to(devices[0]))[0], group.module)
         group.zero_grad()
-    step = 0
-    for epoch in range(1, args.epochs + 1):
+    for epoch in range(start_epoch, args.epochs + 1):
         if hasattr(loader, "sampler"):
             loader.sampler.set_epoch(epoch)
-        loss_acc = torch.zeros((), device=devices[0])
-        corr_acc = torch.zeros((), device=devices[0])
+        loss_sum = corr_sum = 0.0
         total = 0
         t_epoch = t_log = time.time()
         last_log = 0
         for bi, (x, y) in enumerate(loader):
-            ls, c = group.step(x, y, loss_fn)
-            loss_acc += ls / x.shape[0]
-            corr_acc += c
+            group.step(x, y, loss_fn)
             total += x.shape[0]
             step += 1
             if bi % args.log_interval == 0:
-                _sync(devices[0])
+                ls, c = group.read_metrics()  # syncs every replica's device
+                loss_sum += ls
+                corr_sum += c
                 now = time.time()
                 bt = (now - t_log) / max(1, bi - last_log) if bi else now - t_log
                 t_log, last_log = now, bi
-                _log_step(inf, "single", epoch, bi, len(loader), loss_acc.item() / (bi + 1),
-                          100.0 * corr_acc.item() / total, bt)
+                _log_step(inf, "single", epoch, bi, len(loader), loss_sum / total, 100.0 * corr_sum / total, bt)
+                mw.write(kind="step", epoch=epoch, step=step, loss=loss_sum / total, acc=100.0 * corr_sum / total,
+                         batch_time=bt, img_per_s=x.shape[0] / max(bt, 1e-9), graph=group._graphs is not None)
             if args.max_steps and step >= args.max_steps:
                 break
-        _sync(devices[0])
+        ls, c = group.read_metrics()  # remainder since the last log line
+        loss_sum, corr_sum = loss_sum + ls, corr_sum + c
         _log_epoch(inf, "single", time.time() - t_epoch)
         for s in scheds:
             s.step()
         val = _maybe_eval(args, inf, spec, group.module, bs, mw, epoch=epoch)
-        rep.epoch_end(epoch, step, loss_acc.item() / max(1, bi + 1), corr_acc.item() / max(1, total), val,
-                      group.module)
+        rep.epoch_end(epoch, step, loss_sum / max(1, total), corr_sum / max(1, total), val, group.module)
+        _epoch_saves(args, inf, epoch, step, group.module.state_dict(), group.optimizers[0].state_dict(),
+                     scheds[0].state_dict() if scheds else None, loader)
         if args.max_steps and step >= args.max_steps:
             break
+    if args.epoch_checkpoints and args.eval:
+        _reload_latest(args, inf, group.module)
     _maybe_eval(args, inf, spec, group.module, bs, mw, force=True)
     rep.close()
     _save_final(args, inf, "replica", group.module.state_dict())
@@ -508,14 +604,31 @@ def _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw):
     from .parallel.replica import FusedMnistReplicas
 
     torch.manual_seed(args.seed)
+    init = build_model("mnist_cnn")
+    st, start_epoch = {}, 1
+    if args.resume:
+        from .utils.checkpoint import load_training_state
+
+        st = load_training_state(args.resume)
+        init.load_state_dict(st["model"])
+        start_epoch = st["epoch"] + 1
     rep = FusedMnistReplicas(devices, batch=bs // len(devices), lr=lr, momentum=mom, weight_decay=wd, seed=args.seed,
-                             init_model=build_model("mnist_cnn"), use_graph=not args.no_graph)
+                             init_model=init, use_graph=not args.no_graph)
+    step = 0
+    if st:
+        ctrs = st.get("extra", {}).get("data_counters")
+        for i, t in enumerate(rep.trainers):
+            if "momentum" in st.get("optimizer", {}):
+                t.mom.copy_(st["optimizer"]["momentum"].to(t.device))
+            if ctrs is not None and i < len(ctrs):
+                t.load_data_state(ctrs[i])
+        step = int(st.get("step", 0))
     loader, kind = build_loader("mnist", args.data, args.dataset_dir, bs, devices[0], 1, 0, args.seed,
                                 spec.input_shape, 10, train=True, steps=args.steps_per_epoch)
     print(f"==> replica mode (fused engine) on {len(devices)} device(s), global batch {bs}, data {kind}", flush=True)
     rep_ = _Reporter(args, inf)
-    step, base_lr = 0, lr
-    for epoch in range(1, args.epochs + 1):
+    base_lr = lr
+    for epoch in range(start_epoch, args.epochs + 1):
         if args.lr_step_size:
             for t in rep.trainers:
                 t.set_lr(base_lr * args.lr_gamma ** ((epoch - 1) // args.lr_step_size))
@@ -553,9 +666,14 @@ def _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw):
         model = rep.to_module().to(devices[0])
         val = _maybe_eval(args, inf, spec, model, bs, mw, epoch=epoch)
         rep_.epoch_end(epoch, step, loss_tot / max(1, bi * bs), corr_tot / max(1, bi * bs), val, model)
+        t0_ = rep.trainers[0]
+        _epoch_saves(args, inf, epoch, step, rep.state_dict(), {"momentum": t0_.mom.cpu(), "lr": t0_._lr_host},
+                     {"base_lr": base_lr}, None, data_counters=[t.data_state() for t in rep.trainers])
         if args.max_steps and step >= args.max_steps:
             break
     model = rep.to_module().to(devices[0])
+    if args.epoch_checkpoints and args.eval:
+        _reload_latest(args, inf, model)
     _maybe_eval(args, inf, spec, model, bs, mw, force=True)
     rep_.close()
     _save_final(args, inf, "replica", rep.state_dict())  # save_model adds the module. prefix
@@ -573,6 +691,7 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
     torch.manual_seed(args.seed)
     init = build_model("mnist_cnn")
     start_epoch = 1
+    st = {}
     if args.resume:
         st = load_training_state(args.resume)
         init.load_state_dict(st["model"])
@@ -593,6 +712,14 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
     loader, kind = build_loader("mnist", args.data, args.dataset_dir, bs, dev, inf.world_size, inf.rank, args.seed,
                                 spec.input_shape, 10, train=True, steps=args.steps_per_epoch)
     synthetic = kind == "synthetic"
+    step = 0
+    if args.resume:
+        # data-stream position (Chainer snapshot keeps the iterator: chainer/train_mnist.py:91-93):
+        # the on-device synthetic counter; a real-data sampler is re-seeded per epoch by set_epoch
+        ex = st.get("extra", {})
+        if "data_counter" in ex:
+            tr.load_data_state(ex["data_counter"])
+        step = int(st.get("step", 0))
     if inf.is_main:
         print("From Rank: {}, The number of parameters of model is {}".format(inf.rank, 1199882), flush=True)
         print(f"==> data: {kind}, {len(loader)} batches/epoch, fused hipGraph step={'off' if args.no_graph else 'on'}",
@@ -607,14 +734,15 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
 
             print(model_summary(probe, spec.input_shape, spec.name), flush=True)
         rep.first_loss(_ops.cross_entropy(probe(torch.zeros(2, 1, 28, 28)), torch.zeros(2, dtype=torch.long)), probe)
-    step = 0
     base_lr = lr
     if tr.eng.reducer_active and synthetic and not args.no_graph:
-        # pick transport / overlap / graph mode on this machine (a few real training steps, counted)
+        # pick transport / overlap / graph mode on this machine by timing real steps; they are
+        # scratch: weights, momentum, data-stream position and metrics are restored afterwards,
+        # so the trained model and --max-steps still match epochs x batches
+        snap = tr.snapshot()
         tr.step(1)
         tr.autotune()
-        tr.read_metrics(reset=True)
-        step = tr.steps
+        tr.restore(snap)
         if inf.is_main:
             print(f"==> DDP step strategy: {tr.tuned}", flush=True)
     for epoch in range(start_epoch, args.epochs + 1):
@@ -674,10 +802,17 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
                           tr.to_module() if rep.tb is not None else None)
         if args.save_every and epoch % args.save_every == 0:
             save_training_state(args.train_dir, inf.rank, tr.state_dict(), {"momentum": tr.mom.cpu(), "lr": tr._lr_host},
-                                {"base_lr": base_lr}, epoch, step)
+                                {"base_lr": base_lr}, epoch, step,
+                                extra={"data_counter": tr.data_state(), "sampler_epoch": epoch})
+        if args.epoch_checkpoints and inf.is_main:
+            from .utils.checkpoint import save_epoch_weights
+
+            save_epoch_weights(tr.state_dict(), args.train_dir, epoch)
         if args.max_steps and step >= args.max_steps:
             break
     model = tr.to_module().to(dev)
+    if args.epoch_checkpoints and args.eval:
+        _reload_latest(args, inf, model)
     _maybe_eval(args, inf, spec, model, bs, mw, force=True)
     rep.close()
     _save_final(args, inf, mode, tr.state_dict())

@@ -92,14 +92,22 @@ _EDGES = np.asarray(_default_edges())
 
 def histogram_proto(values) -> bytes:
     v = np.asarray(values, dtype=np.float64).reshape(-1)
+    # a diverged run (exactly when the histograms matter) has NaN / inf weights: NaNs are
+    # dropped (TensorBoard has no bucket for them), +-inf land in the end buckets, and
+    # min / max / sum are over the finite values so the proto stays well formed
+    v = v[~np.isnan(v)]
     if v.size == 0:
         v = np.zeros(1)
-    idx = np.searchsorted(_EDGES, v, side="left")
+    idx = np.minimum(np.searchsorted(_EDGES, v, side="left"), len(_EDGES) - 1)
     counts = np.bincount(idx, minlength=len(_EDGES)).astype(np.float64)
+    fin = v[np.isfinite(v)]
+    if fin.size == 0:
+        fin = np.zeros(1)
+    v_stats = fin
     nz = np.nonzero(counts)[0]
     lo, hi = (int(nz[0]), int(nz[-1]) + 1) if nz.size else (0, 1)
-    return (_f_double(1, float(v.min())) + _f_double(2, float(v.max())) + _f_double(3, float(v.size)) +
-            _f_double(4, float(v.sum())) + _f_double(5, float((v * v).sum())) +
+    return (_f_double(1, float(v_stats.min())) + _f_double(2, float(v_stats.max())) + _f_double(3, float(v.size)) +
+            _f_double(4, float(v_stats.sum())) + _f_double(5, float((v_stats * v_stats).sum())) +
             _f_packed_doubles(6, _EDGES[lo:hi].tolist()) + _f_packed_doubles(7, counts[lo:hi].tolist()))
 
 

@@ -125,3 +125,24 @@ def test_slurm_env_contract(monkeypatch):
     import os
 
     assert os.environ["MASTER_ADDR"] == "10.0.0.7" and os.environ["MASTER_PORT"] == str(29500 + 242)
+
+
+def test_slurm_tasks_per_node_fallbacks(monkeypatch):
+    """srun -N2 -n16 without --ntasks-per-node: SLURM_NTASKS_PER_NODE is unset; the per-node
+    count must come from SLURM_TASKS_PER_NODE ("8(x2)") or SLURM_NTASKS / SLURM_NNODES, never
+    the global world size (which would mark the ranks as sharing GPUs)."""
+    from mxddp.parallel import comm
+
+    for k in ("RANK", "WORLD_SIZE", "SLURM_NTASKS_PER_NODE", "SLURM_TASKS_PER_NODE", "SLURM_NNODES",
+              "SLURM_JOB_NUM_NODES"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("SLURM_PROCID", "9")
+    monkeypatch.setenv("SLURM_NTASKS", "16")
+    monkeypatch.setenv("SLURM_LOCALID", "1")
+    monkeypatch.setenv("SLURM_TASKS_PER_NODE", "8(x2)")
+    assert comm.env_dist()["local_world_size"] == 8
+    monkeypatch.delenv("SLURM_TASKS_PER_NODE")
+    monkeypatch.setenv("SLURM_NNODES", "2")
+    assert comm.env_dist()["local_world_size"] == 8
+    monkeypatch.delenv("SLURM_NNODES")
+    assert comm.env_dist()["local_world_size"] == 16  # single node: every task is local

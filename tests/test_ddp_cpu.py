@@ -178,3 +178,102 @@ def test_rccl_uid_rendezvous_ws4():
         assert p.exitcode == 0
     for r, (rank, same_uid, rest) in enumerate(res):
         assert rank == r and same_uid and rest == (r, ws, r), res
+
+
+def _tiny_pyramidnet():
+    from mxddp.models.pyramidnet import PyramidNet
+
+    return PyramidNet(num_layers=3, alpha=24)  # 2 blocks per stage: BN, identity + stride-2 shortcuts
+
+
+def _bn_worker(rank, ws, port, steps, b, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from mxddp import ops
+    from mxddp.optim import SGD
+    from mxddp.parallel import comm
+    from mxddp.parallel.ddp import DistributedDataParallel as DDP
+
+    comm.init_distributed(rank=rank, world_size=ws, use_gpu=False, init_method=f"tcp://127.0.0.1:{port}")
+    torch.manual_seed(0)
+    model = _tiny_pyramidnet()
+    if rank == 1:  # rank-divergent weights AND buffers: the wrap-time broadcast must win
+        with torch.no_grad():
+            for p in model.parameters():
+                p.add_(0.5)
+            for n, bf in model.named_buffers():
+                if bf.is_floating_point():
+                    bf.add_(3.0)
+    ddp = DDP(model, bucket_cap_mb=0.02, first_bucket_cap_mb=0.01)  # several buckets
+    opt = SGD(ddp.flat, lr=0.05, momentum=0.9, weight_decay=1e-4)
+    for x, y in _batches(steps, ws * b, (3, 32, 32), seed=77):
+        opt.zero_grad()
+        ops.cross_entropy(ddp(x[rank * b:(rank + 1) * b]), y[rank * b:(rank + 1) * b]).backward()
+        opt.step()
+    q.put((rank, {k: v.detach().numpy().copy() for k, v in model.state_dict().items()}, len(ddp.buckets)))
+    comm.shutdown()
+
+
+def test_ddp_batchnorm_model_matches_simulated_ranks():
+    """DDP semantics for a BatchNorm model (PyramidNet blocks): every rank normalises with its OWN
+    shard's batch statistics, gradients are averaged, and rank 0's floating buffers (running
+    mean / var) are broadcast before every forward (broadcast_buffers=True,
+    pytorch/distributed_data_parallel.py:74).  Golden reference: one process, plain torch, one
+    model copy per rank -- copy rank 0's buffers to the others, forward / backward every copy on
+    its shard, average the gradients, identical torch.optim.SGD steps."""
+    import copy
+
+    import torch.nn.functional as F
+
+    ws, steps, b = 2, 3, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_bn_worker, args=(r, ws, port, steps, b, q)) for r in range(ws)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in range(ws):
+        r, sd, nb = q.get(timeout=240)
+        out[r] = {k: torch.from_numpy(v) for k, v in sd.items()}
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert nb >= 3
+
+    torch.manual_seed(0)
+    base = _tiny_pyramidnet()
+    copies = [copy.deepcopy(base) for _ in range(ws)]
+    params = [list(c.parameters()) for c in copies]
+    opts = [torch.optim.SGD(c.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4) for c in copies]
+    with torch.no_grad():
+        for x, y in _batches(steps, ws * b, (3, 32, 32), seed=77):
+            for c in copies[1:]:  # per-forward buffer broadcast from rank 0
+                for (n, dst), src in zip(c.named_buffers(), copies[0].buffers()):
+                    if dst.is_floating_point():
+                        dst.copy_(src)
+            grads = []
+            for r, c in enumerate(copies):
+                c.zero_grad()
+                with torch.enable_grad():
+                    F.cross_entropy(c(x[r * b:(r + 1) * b]), y[r * b:(r + 1) * b]).backward()
+                grads.append([p.grad.clone() for p in c.parameters()])
+            avg = [sum(gs) / ws for gs in zip(*grads)]
+            for r in range(ws):
+                for p, g in zip(params[r], avg):
+                    p.grad.copy_(g)
+                opts[r].step()
+    for r in range(ws):
+        ref = copies[r].state_dict()
+        for k, v in ref.items():
+            got = out[r][k]
+            if v.is_floating_point():
+                assert torch.allclose(got, v, rtol=1e-4, atol=1e-5), (r, k, (got - v).abs().max())
+            else:
+                assert torch.equal(got, v), (r, k, got, v)  # num_batches_tracked == steps
+    assert int(out[0]["bn1.num_batches_tracked"]) == steps
+    # parameters identical across ranks; running stats differ (each rank's own last shard)
+    for k in out[0]:
+        if k.endswith("weight") or k.endswith("bias"):
+            assert torch.equal(out[0][k], out[1][k]), k
+    assert not torch.equal(out[0]["bn1.running_mean"], out[1]["bn1.running_mean"])

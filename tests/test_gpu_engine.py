@@ -179,3 +179,22 @@ def test_fused_engine_autotune_keeps_training_exact(cuda):
     # fp32 split-K atomics differs between two engines, so allow rounding-level drift
     for k, v in a.state_dict().items():
         assert torch.allclose(v, b.state_dict()[k], rtol=1e-3, atol=2e-5), k
+
+
+def test_bench_json_reports_per_image_metrics(cuda):
+    """The driver-visible bench line: train_acc is a fraction in [0, 1] and train_loss_avg a
+    per-image average (round 2 divided the sums by 1 after a premature reset)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "20", "--warmup", "5"],
+                       capture_output=True, text=True, timeout=240, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    out = json.loads(line)
+    assert 0.0 <= out["train_acc"] <= 1.0, out
+    assert 0.0 < out["train_loss_avg"] < 3.0, out
+    assert out["train_images"] >= 25 * 64, out

@@ -384,3 +384,32 @@ def test_winograd_filter_bank_matches_per_conv_transforms(cuda):
     a, b = run(True), run(False)
     for u, v in zip(a, b):
         assert torch.equal(u, v)
+
+
+def test_scratch_is_stream_owned_two_streams(cuda):
+    """Split-K partial planes (linear forward / data gradient) and BN partial sums issued on two
+    streams AT ONCE: each stream owns its scratch, so neither result is corrupted by the other
+    (round 2 shared one per-device buffer across streams: the side-stream experiment's fault)."""
+    torch.manual_seed(11)
+    cases = []
+    for s in range(2):
+        x, w = torch.randn(64, 9216 - 7 * s), torch.randn(128 + s, 9216 - 7 * s) * 0.02
+        xb = torch.randn(32, 64 + 5 * s, 11, 11) + s
+        cases.append((x, w, xb, F.linear(x, w), F.batch_norm(xb, None, None, training=True)))
+    streams = [torch.cuda.Stream(cuda) for _ in range(2)]
+    dev_in = [(x.to(cuda), w.to(cuda), xb.to(cuda)) for x, w, xb, _, _ in cases]
+    torch.cuda.synchronize()
+    outs = [[], []]
+    for rep in range(12):  # interleave launches so both streams' kernels overlap on the device
+        for s in range(2):
+            with torch.cuda.stream(streams[s]):
+                x, w, xb = dev_in[s]
+                C = xb.shape[1]
+                y = ops.linear(x, w, None)
+                z = ops.batch_norm(xb, None, None, torch.zeros(C, device=cuda), torch.ones(C, device=cuda), True)
+                outs[s].append((y, z))
+    torch.cuda.synchronize()
+    for s in range(2):
+        for y, z in outs[s]:
+            assert _rel(y.cpu(), cases[s][3]) < 1e-4
+            assert _rel(z.cpu(), cases[s][4]) < 1e-4

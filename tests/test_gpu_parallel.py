@@ -48,16 +48,19 @@ def test_replica_group_single_device(cuda):
     grp = ReplicaGroup(build_model("keras_cnn"), [cuda], lambda f: Adam(f, lr=1e-3, eps=1e-7, eps_hat=True))
     x = torch.rand(16, 1, 28, 28, device=cuda)
     y = torch.randint(0, 10, (16,), device=cuda)
-    l0, _ = grp.step(x, y, lambda o, t: ops.cross_entropy(o, t, return_correct=True))
+    grp.step(x, y, lambda o, t: ops.cross_entropy(o, t, return_correct=True))
+    l0, _ = grp.read_metrics()
     for _ in range(20):
-        ls, _ = grp.step(x, y, lambda o, t: ops.cross_entropy(o, t, return_correct=True))
-    assert ls.item() < l0.item()
+        grp.step(x, y, lambda o, t: ops.cross_entropy(o, t, return_correct=True))
+        ls, c = grp.read_metrics()
+    assert ls < l0 and 0 <= c <= 16
 
 
 @pytest.mark.parametrize("model", ["keras_cnn", "mlp"])
 def test_replica_group_graph_matches_eager(cuda, model):
-    """use_graph=True (per-device hipGraph of zero-grad + forward + backward after two eager
-    steps, fresh batches copied into static inputs) trains exactly like the eager replica step."""
+    """use_graph=True (per-device hipGraph of the whole step -- zero-grad, forward, backward,
+    Adam with its on-device step count, metric accumulation -- after two eager steps, fresh
+    batches copied into static inputs) trains exactly like the eager replica step."""
     from mxddp import ops
     from mxddp.models import build_model
     from mxddp.optim import Adam
@@ -73,13 +76,14 @@ def test_replica_group_graph_matches_eager(cuda, model):
                            use_graph=graph)
         losses = []
         for x, y in batches:
-            ls, corr = grp.step(x.to(cuda), y.to(cuda), loss_fn)
-            losses.append(ls.item())
+            grp.step(x.to(cuda), y.to(cuda), loss_fn)
+            losses.append(grp.read_metrics()[0])
         assert (grp._graphs is not None) == graph
         res.append((losses, grp.flats[0].data.cpu()))
     (la, pa), (lb, pb) = res
     assert max(abs(a - b) for a, b in zip(la, lb)) < 1e-4 * max(abs(a) for a in la)
     assert torch.allclose(pa, pb, rtol=1e-4, atol=1e-6)
+    assert grp.optimizers[0].steps == len(batches)  # the device step count advanced in the graph
 
 
 @pytest.mark.parametrize("name", ["pyramidnet110", "resnet50"])

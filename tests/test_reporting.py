@@ -99,3 +99,38 @@ def test_chainer_script_writes_log_report_and_graph(tmp_path):
     assert [e["epoch"] for e in log] == [1, 2] and "validation/main/accuracy" in log[0]
     assert (tmp_path / "result" / "cg.dot").exists()
     assert "main/loss" in out and "validation/main/accuracy" in out  # PrintReport header
+
+
+def test_histogram_proto_nonfinite_values():
+    """A diverged run's weights (NaN / inf) still give a well-formed HistogramProto: as many
+    bucket limits as counts, finite min / max / sum."""
+    import math
+    import struct
+
+    import numpy as np
+
+    from mxddp.utils.tensorboard import histogram_proto
+
+    raw = histogram_proto(np.array([1.0, float("nan"), -2.0, float("inf"), float("-inf"), 0.5]))
+    fields, i = {}, 0
+    while i < len(raw):  # minimal protobuf walk: field 1-5 doubles, 6-7 packed doubles
+        key = raw[i]
+        i += 1
+        f, wt = key >> 3, key & 7
+        if wt == 1:
+            fields[f] = struct.unpack("<d", raw[i:i + 8])[0]
+            i += 8
+        else:
+            n, shift = 0, 0
+            while True:
+                b = raw[i]
+                i += 1
+                n |= (b & 0x7F) << shift
+                shift += 7
+                if not b & 0x80:
+                    break
+            fields[f] = struct.unpack(f"<{n // 8}d", raw[i:i + n])
+            i += n
+    assert len(fields[6]) == len(fields[7])
+    assert fields[1] == -2.0 and fields[2] == 1.0 and math.isfinite(fields[4])
+    assert sum(fields[7]) == 5  # the NaN is dropped, both infinities counted
