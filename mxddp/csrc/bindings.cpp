@@ -283,7 +283,17 @@ PYBIND11_MODULE(_C, m) {
       .value("sum", RedOp::kSum).value("avg", RedOp::kAvg).value("max", RedOp::kMax)
       .value("min", RedOp::kMin).value("prod", RedOp::kProd);
   py::class_<Comm>(m, "Comm")
-      .def(py::init([](py::bytes uid, int rank, int ws, int dev) { return new Comm(std::string(uid), rank, ws, dev); }))
+      .def(py::init([](py::bytes uid, int rank, int ws, int dev, int ctas, const std::string& algo,
+                       const std::string& proto) {
+             CommConfig cfg;
+             cfg.ctas = ctas;
+             cfg.algo = algo;
+             cfg.proto = proto;
+             return new Comm(std::string(uid), rank, ws, dev, cfg);
+           }),
+           py::arg("uid"), py::arg("rank"), py::arg("world_size"), py::arg("device"), py::arg("ctas") = 0,
+           py::arg("algo") = "", py::arg("proto") = "")
+      .def_property_readonly("variant", [](const Comm& c) { return c.config().name(); })
       .def_static("new_unique_id", []() { return py::bytes(Comm::new_unique_id()); })
       .def_static("init_all", [](const std::vector<int>& devs) {
         auto v = Comm::init_all(devs);
@@ -364,6 +374,9 @@ PYBIND11_MODULE(_C, m) {
       .def("comm_stream", [](Reducer& r) { return reinterpret_cast<uintptr_t>(r.comm_stream()); })
       .def("last_comm_ms", &Reducer::last_comm_ms)
       .def("set_timing", &Reducer::set_timing)
+      .def("set_padding", &Reducer::set_padding)
+      .def("padded_count", &Reducer::padded_count)
+      .def("set_comm", &Reducer::set_comm, py::keep_alive<1, 2>())
       .def_property_readonly("timing", &Reducer::timing)
       .def_property_readonly("num_buckets", &Reducer::num_buckets)
       .def_property_readonly("launched", &Reducer::launched)
@@ -392,6 +405,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_merged", &MnistEngine::set_merged)
       .def_property_readonly("merged", &MnistEngine::merged)
       .def("set_peer", &MnistEngine::set_peer, py::arg("peer").none(true), py::keep_alive<1, 2>())
+      .def("set_comm", &MnistEngine::set_comm, py::arg("comm").none(true), py::keep_alive<1, 2>())
+      .def("set_bucket_padding", &MnistEngine::set_bucket_padding)
       .def_property_readonly("peer_active", &MnistEngine::peer_active)
       .def_property_readonly("overlap", &MnistEngine::overlap)
       .def_property_readonly("reducer_active", &MnistEngine::reducer_active)

@@ -1,5 +1,8 @@
 #include "comm.h"
 
+#include <cstdlib>
+#include <cstring>
+
 #include "common.h"
 
 namespace mx {
@@ -51,13 +54,65 @@ std::string Comm::new_unique_id() {
   return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
 }
 
-Comm::Comm(const std::string& uid, int rank, int world_size, int device)
-    : rank_(rank), ws_(world_size), device_(device) {
+std::string CommConfig::name() const {
+  if (ctas <= 0 && algo.empty() && proto.empty()) return "default";
+  std::string n = algo.empty() ? "auto" : algo;
+  if (!proto.empty()) n += "/" + proto;
+  if (ctas > 0) n += ":c" + std::to_string(ctas);
+  return n;
+}
+
+namespace {
+// The communicator-config prefix that every RCCL >= 2.18 understands.  The headers here are
+// newer (2.27) than the RCCL inside the PyTorch wheel this module links (2.26): RCCL copies
+// `size` bytes of the caller's struct over its defaults, so handing it the 2.27 struct would
+// write past its own.  The fields after splitShare keep RCCL's defaults.
+struct CommConfigV218 {
+  size_t size;
+  unsigned int magic, version;
+  int blocking, cgaClusterSize, minCTAs, maxCTAs;
+  const char* netName;
+  int splitShare;
+};
+
+// NCCL_ALGO / NCCL_PROTO for the duration of one communicator init
+class ScopedEnv {
+ public:
+  ScopedEnv(const char* key, const std::string& val) : key_(key) {
+    if (val.empty()) return;
+    const char* old = std::getenv(key);
+    had_ = old != nullptr;
+    if (had_) old_ = old;
+    setenv(key, val.c_str(), 1);
+    set_ = true;
+  }
+  ~ScopedEnv() {
+    if (!set_) return;
+    if (had_) setenv(key_, old_.c_str(), 1);
+    else unsetenv(key_);
+  }
+
+ private:
+  const char* key_;
+  std::string old_;
+  bool had_ = false, set_ = false;
+};
+}  // namespace
+
+Comm::Comm(const std::string& uid, int rank, int world_size, int device, const CommConfig& cfg)
+    : rank_(rank), ws_(world_size), device_(device), cfg_(cfg) {
   MX_CHECK(uid.size() == sizeof(ncclUniqueId), "unique id has wrong size");
   ncclUniqueId id;
   std::memcpy(&id, uid.data(), sizeof(id));
   MX_HIP_CHECK(hipSetDevice(device));
-  MX_NCCL_CHECK(ncclCommInitRank(&comm_, world_size, id, rank));
+  ScopedEnv algo("NCCL_ALGO", cfg.algo), proto("NCCL_PROTO", cfg.proto);
+  if (cfg.ctas > 0) {
+    CommConfigV218 c{sizeof(CommConfigV218), 0xcafebeef, NCCL_VERSION(2, 18, 0), 1,
+                     NCCL_CONFIG_UNDEF_INT, cfg.ctas, cfg.ctas, nullptr, NCCL_CONFIG_UNDEF_INT};
+    MX_NCCL_CHECK(ncclCommInitRankConfig(&comm_, world_size, id, rank, reinterpret_cast<ncclConfig_t*>(&c)));
+  } else {
+    MX_NCCL_CHECK(ncclCommInitRank(&comm_, world_size, id, rank));
+  }
 }
 
 Comm::Comm(ncclComm_t c, int rank, int world_size, int device)

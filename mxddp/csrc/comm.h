@@ -20,9 +20,20 @@ ncclDataType_t to_nccl(DType t);
 ncclRedOp_t to_nccl(RedOp o);
 size_t dtype_size(DType t);
 
+// How a communicator is built for the 8x MI355X xGMI mesh (every GPU: 7 point-to-point links).
+// `ctas` pins RCCL's channel count (ncclConfig_t minCTAs = maxCTAs; each channel is one ring
+// permutation over the mesh, so 7 / 14 / 28 channels put 1 / 2 / 4 rings on every link);
+// `algo` / `proto` pin NCCL_ALGO / NCCL_PROTO for this communicator only (read by RCCL's tuner
+// at init; restored afterwards).  Defaults (0 / "") leave RCCL's own tuning.
+struct CommConfig {
+  int ctas = 0;
+  std::string algo, proto;
+  std::string name() const;
+};
+
 class Comm {
  public:
-  Comm(const std::string& unique_id, int rank, int world_size, int device);
+  Comm(const std::string& unique_id, int rank, int world_size, int device, const CommConfig& cfg = CommConfig());
   explicit Comm(ncclComm_t c, int rank, int world_size, int device);  // adopt (replica engine)
   ~Comm();
   Comm(const Comm&) = delete;
@@ -49,12 +60,14 @@ class Comm {
   int rank() const { return rank_; }
   int world_size() const { return ws_; }
   int device() const { return device_; }
+  const CommConfig& config() const { return cfg_; }
   ncclComm_t raw() const { return comm_; }
 
  private:
   ncclComm_t comm_ = nullptr;
   int rank_ = 0, ws_ = 1, device_ = 0;
   bool aborted_ = false;
+  CommConfig cfg_;
 };
 
 }  // namespace mx

@@ -90,6 +90,16 @@ MnistEngine::MnistEngine(int batch, uintptr_t params, uintptr_t grads, uintptr_t
   MX_HIP_CHECK(hipStreamSynchronize(s_));
 }
 
+void MnistEngine::set_comm(Comm* c) {
+  if (c == comm_) return;
+  MX_CHECK(!c || !comm_ || (c->rank() == comm_->rank() && c->world_size() == comm_->world_size()),
+           "set_comm: the communicator must have this engine's rank and world size");
+  uncapture();
+  comm_ = c;
+  reducer_->set_comm(c);
+  merged_reducer_->set_comm(c);
+}
+
 void MnistEngine::repack() {
   if (variant_ == 1) mnist_fused_init(fused_args(), s_);
 }

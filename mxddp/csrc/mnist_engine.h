@@ -71,6 +71,15 @@ class MnistEngine {
     reducer_->set_peer(p);
     merged_reducer_->set_peer(p);
   }
+  // RCCL communicator (same rank / world size; one of the configured variants of
+  // parallel/comm.py); drops captured graphs
+  void set_comm(Comm* c);
+  // pad the all-reduce of a bucket that ends at the end of the gradient buffer up to a multiple
+  // of `multiple` elements, into zeroed slack (capacity = elements the grads buffer really has)
+  void set_bucket_padding(size_t capacity, size_t multiple) {
+    reducer_->set_padding(MnistLayout::total, capacity, multiple);
+    merged_reducer_->set_padding(MnistLayout::total, capacity, multiple);
+  }
   // merged = true: ONE all-reduce over the whole gradient after the conv backward instead of
   // the fc bucket (overlappable) + the conv bucket: one collective latency per step instead of
   // two, no overlap.  Drops captured graphs.

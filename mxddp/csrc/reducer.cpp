@@ -81,7 +81,7 @@ void Reducer::launch_ready(hipStream_t compute) {
         peer_->all_reduce(p, b.numel, dtype_, st, op_);
       } else {
         MX_CHECK(comm_ != nullptr, "reducer: no RCCL communicator for this collective");
-        comm_->all_reduce(p, p, b.numel, dtype_, op_, st);
+        comm_->all_reduce(p, p, padded_count(b.offset, b.numel), dtype_, op_, st);
       }
     }
   }
@@ -102,6 +102,12 @@ void Reducer::finalize(hipStream_t compute) {
     MX_HIP_CHECK(hipStreamWaitEvent(compute, done_, 0));
     side_used_ = false;
   }
+}
+
+size_t Reducer::padded_count(size_t offset, size_t numel) const {
+  if (pad_mult_ <= 1 || offset + numel != pad_total_) return numel;
+  const size_t n = (numel + pad_mult_ - 1) / pad_mult_ * pad_mult_;
+  return offset + n <= pad_cap_ ? n : numel;
 }
 
 float Reducer::last_comm_ms() {

@@ -50,6 +50,16 @@ class Reducer {
   void set_timing(bool on);
   bool timing() const { return timing_; }
   void set_comm(Comm* c) { comm_ = c; }
+  // A bucket that ends where the gradients end ([offset, total)) is all-reduced over
+  // roundup(numel, multiple) elements when the buffer has that much zeroed slack (capacity):
+  // every rank's share of every channel then starts 16-byte aligned (xGMI sizing).
+  // Interior buckets are never padded (their tail is the next bucket's data).
+  void set_padding(size_t total, size_t capacity, size_t multiple) {
+    pad_total_ = total;
+    pad_cap_ = capacity;
+    pad_mult_ = multiple;
+  }
+  size_t padded_count(size_t offset, size_t numel) const;
   // issue the collectives even at world_size 1 (exercises the RCCL + graph-capture path on
   // a single GPU; an all-reduce over one rank is the identity)
   void set_force_collectives(bool on) { force_ = on; }
@@ -82,6 +92,7 @@ class Reducer {
   // stream discipline: every bucket of one backward is fenced against ONE compute
   // stream, and a backward's side-stream work must be joined (finalize) before the next begins
   hipStream_t step_compute_ = nullptr;
+  size_t pad_total_ = 0, pad_cap_ = 0, pad_mult_ = 1;
   bool in_step_ = false;
 };
 

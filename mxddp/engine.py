@@ -33,7 +33,7 @@ class FusedMnistTrainer:
                  momentum: float = 0.9, weight_decay: float = 1e-4, variant: int = 1, use_graph: bool = True,
                  init_model: MnistCNN | None = None, graph_mode: int | None = None,
                  steps_per_graph: int | None = None, force_collectives: bool = False, transport: str = "auto",
-                 peer=None):
+                 peer=None, rccl_variants=None):
         C = native()
         self.C = C
         self.graph_mode = graph_mode
@@ -53,7 +53,11 @@ class FusedMnistTrainer:
         flat = torch.cat([sd[k].detach().reshape(-1).float().cpu() for k, _ in _LAYOUT])
         assert flat.numel() == n
         self.params = flat.to(self.device)
-        self.grads = torch.zeros(n, device=self.device)
+        # + zeroed slack: the all-reduce of the bucket that ends at the end of the gradient is
+        # padded to a multiple of world_size x channels x 16 B (Reducer::set_padding)
+        self._grad_slack = 1024
+        self._grad_store = torch.zeros(n + self._grad_slack, device=self.device)
+        self.grads = self._grad_store[:n]
         self.mom = torch.zeros(n, device=self.device)
         self.lr = torch.full((1,), lr, device=self.device)
         self._lr_host = lr
@@ -70,13 +74,16 @@ class FusedMnistTrainer:
         self.eng = C.MnistEngine(batch, self.params.data_ptr(), self.grads.data_ptr(), self.mom.data_ptr(),
                                  self.workspace.data_ptr(), wsb, comm, seed, momentum, weight_decay,
                                  self.lr.data_ptr(), self.metrics.data_ptr(), variant)
+        self.eng_comm = comm
         if force_collectives:
             self.eng.set_force_collectives(True)
+        self.rccl_variants = rccl_variants  # [(name, Comm)] timed by autotune(); None = comm.py's list
         self.stream = torch.cuda.ExternalStream(self.eng.stream, device=self.device)
         self.steps = 0
         self.steps_at_reset = 0  # self.steps when the device metrics were last zeroed
         self.eng.set_small_first(os.environ.get("MXDDP_SMALL_FIRST", "0") == "1")
         self.world_size = comm.world_size if comm is not None else (peer.world_size if peer is not None else 1)
+        self._set_padding(comm)
         # gradient transport (world size > 1): RCCL, or the direct xGMI peer all-reduce
         # (parallel/peer.py) -- validated against RCCL on every rank before it may be used;
         # "auto" lets autotune() time both
@@ -156,9 +163,13 @@ class FusedMnistTrainer:
             include_graphs = os.environ.get("MXDDP_AUTOTUNE_GRAPHS", "0") == "1"
         if not self.eng.reducer_active or self._external:
             return {}
-        transports = ["rccl", "peer"] if self.peer is not None else ["rccl"]
-        if self.transport in ("rccl", "peer"):
-            transports = [self.transport] if self.transport in transports else ["rccl"]
+        comms = self._rccl_candidates()
+        rccl_names = [f"rccl:{v}" if len(comms) > 1 else "rccl" for v in comms]
+        transports = rccl_names + (["peer"] if self.peer is not None else [])
+        if self.transport == "peer" and self.peer is not None:
+            transports = ["peer"]
+        elif self.transport == "rccl":
+            transports = rccl_names
         snap = self.snapshot() if restore else None
         cands = []
         for tr in transports:
@@ -168,7 +179,7 @@ class FusedMnistTrainer:
         results = {}
         for tr, mode, strat in cands:
             self.eng.uncapture()
-            self.eng.set_peer(self.peer if tr == "peer" else None)
+            self._use_transport(tr, comms)
             self._set_buckets(strat)
             failed = 0.0
             try:  # capture issues no collective, so a local failure here is safe to agree on
@@ -195,7 +206,7 @@ class FusedMnistTrainer:
             results[(tr, mode, strat)] = dt / trial_steps * 1e3
         best = min(results, key=results.get)
         self.eng.uncapture()
-        self.eng.set_peer(self.peer if best[0] == "peer" else None)
+        self._use_transport(best[0], comms)
         self._set_buckets(best[2])
         if best[1]:
             self._capture(best[1])
@@ -207,6 +218,47 @@ class FusedMnistTrainer:
         self.tuned = {"transport": best[0], "graph_mode": best[1], "buckets": best[2],
                       "trials_ms": {f"{t}/{m}/{s}": round(v, 4) for (t, m, s), v in results.items()}}
         return results
+
+    def _rccl_candidates(self) -> dict:
+        """{variant name: Comm} the autotune times: the caller's list, else (world size > 1, or
+        MXDDP_RCCL_VARIANTS set) comm.py's xGMI-sized variants over the same ranks, else just
+        the trainer's own communicator."""
+        if self.rccl_variants is not None:
+            return dict(self.rccl_variants)
+        if self.comm is None:
+            return {}
+        from .parallel import comm as pc
+
+        if self.world_size > 1 or "MXDDP_RCCL_VARIANTS" in os.environ:
+            out = {}
+            for v in pc.rccl_variants():
+                c = self.comm if v == "default" else pc.rccl_comm(force=True, variant=v)
+                if c is not None:
+                    out[v] = c
+            if out:
+                return out
+        return {"default": self.comm}
+
+    def _set_padding(self, comm):
+        ctas = 0
+        if comm is not None:
+            from .parallel import comm as pc
+
+            ctas = pc.parse_variant(comm.variant)["ctas"]
+        mult = max(1, self.world_size) * max(ctas, 32) * 4  # elements of 4 B: 16-B chunks per channel
+        self.eng.set_bucket_padding(self.params.numel() + self._grad_slack, mult)
+
+    def _use_transport(self, tr: str, comms: dict):
+        if tr == "peer":
+            self.eng.set_peer(self.peer)
+            return
+        self.eng.set_peer(None)
+        name = tr.split(":", 1)[1] if ":" in tr else next(iter(comms), "default")
+        c = comms.get(name, self.comm)
+        if c is not None and c is not self.eng_comm:
+            self.eng.set_comm(c)
+            self.eng_comm = c
+        self._set_padding(c)
 
     def _set_buckets(self, strat: str):
         """ovl: fc bucket overlapped on the side stream; inl: both buckets in order; one: a
@@ -222,7 +274,9 @@ class FusedMnistTrainer:
     def active_transport(self) -> str:
         if self.world_size == 1 and not self.eng.reducer_active:
             return "none"
-        return "peer" if self.eng.peer_active else "rccl"
+        if self.eng.peer_active:
+            return "peer"
+        return "rccl" if self.eng_comm is None else f"rccl:{self.eng_comm.variant}"
 
     def set_batch(self, x: torch.Tensor, y: torch.Tensor):
         """Use a caller-provided batch instead of the on-device generator (real MNIST)."""

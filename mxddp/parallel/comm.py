@@ -41,6 +41,33 @@ class DistInfo:
 
 _INFO: DistInfo | None = None
 _COMM = None
+_VARIANT_COMMS: dict = {}
+
+# RCCL communicator variants sized for the 8x MI355X xGMI mesh: RCCL's own
+# tuning, and the ring algorithm pinned with 7 / 14 / 28 channels (1 / 2 / 4 ring permutations
+# per point-to-point link).  The autotuners time them against each other and against the direct
+# peer transport on the machine they run on.  MXDDP_RCCL_VARIANTS overrides the list.
+DEFAULT_RCCL_VARIANTS = "default,Ring:c7,Ring:c14,Ring:c28"
+
+
+def parse_variant(name: str) -> dict:
+    """'default' | '<algo>[/<proto>][:c<channels>]' -> Comm kwargs (ctas, algo, proto)."""
+    if name in ("", "default"):
+        return {"ctas": 0, "algo": "", "proto": ""}
+    head, _, tail = name.partition(":")
+    algo, _, proto = head.partition("/")
+    ctas = 0
+    if tail:
+        if not (tail.startswith("c") and tail[1:].isdigit()):
+            raise ValueError(f"RCCL variant {name!r}: channel spec must be c<N>")
+        ctas = int(tail[1:])
+    if algo.lower() in ("", "auto"):
+        algo = ""
+    return {"ctas": ctas, "algo": algo, "proto": proto}
+
+
+def rccl_variants() -> list[str]:
+    return [v.strip() for v in os.environ.get("MXDDP_RCCL_VARIANTS", DEFAULT_RCCL_VARIANTS).split(",") if v.strip()]
 
 
 def env_dist() -> dict:
@@ -126,10 +153,31 @@ def info() -> DistInfo:
     return _INFO if _INFO is not None else DistInfo()
 
 
-def rccl_comm(force: bool = False):
+def rccl_comm(force: bool = False, variant: str = "default"):
     """This rank's RCCL communicator (created on first use; None when world_size == 1 unless
-    ``force``: a 1-rank communicator exercises the full RCCL path for tests/benchmarks)."""
+    ``force``: a 1-rank communicator exercises the full RCCL path for tests/benchmarks).
+    ``variant`` (see parse_variant): another communicator over the same ranks built with a
+    pinned algorithm / channel count; collective over all ranks, so every rank must ask for the
+    same variants in the same order."""
     global _COMM
+    if variant not in ("", "default"):
+        base = rccl_comm(force)
+        if base is None:
+            return None
+        if variant not in _VARIANT_COMMS:
+            inf = info()
+            C = native()
+            kw = parse_variant(variant)
+            if inf.world_size == 1:
+                uid = C.Comm.new_unique_id()
+            else:
+                store = dist.distributed_c10d._get_default_store()
+                key = f"mxddp/rccl_uid/{variant}"
+                if inf.rank == 0:
+                    store.set(key, C.Comm.new_unique_id())
+                uid = store.get(key)
+            _VARIANT_COMMS[variant] = C.Comm(uid, inf.rank, inf.world_size, inf.device.index, **kw)
+        return _VARIANT_COMMS[variant]
     inf = info()
     if (inf.world_size == 1 and not force) or inf.device.type != "cuda":
         return None
@@ -187,6 +235,7 @@ def shutdown():
 
     _peer.shutdown()
     _COMM = None
+    _VARIANT_COMMS.clear()
     if dist.is_initialized():
         dist.destroy_process_group()
     _INFO = None

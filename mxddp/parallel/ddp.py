@@ -86,6 +86,8 @@ class DistributedDataParallel(nn.Module):
         self.transport_ms = None
         if native_reducer and self.world_size > 1:
             self._select_transport(transport)
+        if native_reducer and self.transport == "rccl":
+            self._set_padding()
         self._queued = False
         # fires on both gradient paths: returned gradients and gradients the GPU kernels wrote
         # straight into the flat buffer (mxddp.ops._grad_sink; AccumulateGrad still runs)
@@ -97,26 +99,47 @@ class DistributedDataParallel(nn.Module):
         this model's buckets; ranks sharing one GPU (no RCCL) must use the peer transport."""
         from . import peer as _peer
 
-        if transport == "rccl" and self._comm is not None:
-            return
-        pc = _peer.peer_comm()
+        pc = _peer.peer_comm() if transport != "rccl" or self._comm is None else None
         if self._comm is None:
             if pc is None:
                 raise RuntimeError("DDP: no RCCL communicator (ranks share a GPU) and no peer transport")
             self.reducer.set_peer(pc)
             self.transport = "peer"
             return
-        if pc is None or not _peer.validate(pc, self._comm):
+        if pc is not None and not _peer.validate(pc, self._comm):
             if transport == "peer":
                 raise RuntimeError("DDP: peer transport requested but unavailable / failed validation")
+            pc = None
+        if transport == "peer":
+            if pc is None:
+                raise RuntimeError("DDP: peer transport requested but unavailable")
+            self.reducer.set_peer(pc)
+            self.transport = "peer"
             return
-        if transport == "auto":
-            choice, self.transport_ms = _peer.pick_transport(pc, self._comm, [n for _, n in self.buckets])
-        else:
-            choice = "peer"
+        # time the xGMI-sized RCCL variants (and the validated peer transport) on this model's
+        # buckets; every rank gets the same verdict
+        variants = {}
+        for v in _comm.rccl_variants():
+            c = self._comm if v == "default" else _comm.rccl_comm(variant=v)
+            if c is not None:
+                variants[v] = c
+        choice, self.transport_ms = _peer.pick_transport(pc, variants, [n for _, n in self.buckets])
         if choice == "peer":
             self.reducer.set_peer(pc)
             self.transport = "peer"
+            return
+        name = choice.split(":", 1)[1]
+        self._comm = variants[name]
+        self.reducer.set_comm(self._comm)
+        self.transport = choice
+        self._set_padding()
+
+    def _set_padding(self):
+        """Pad the last bucket's all-reduce into the flat buffer's zeroed slack (xGMI sizing)."""
+        if self._comm is None or not hasattr(self.reducer, "set_padding"):
+            return
+        ctas = _comm.parse_variant(self._comm.variant)["ctas"]
+        self.reducer.set_padding(self.flat.numel, self.flat.capacity, self.world_size * max(ctas, 32) * 4)
 
     # ------------------------------------------------------------------ sync helpers
     def _broadcast(self, t: torch.Tensor):

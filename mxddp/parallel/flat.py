@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 
 _ALIGN = 16  # elements (64 bytes)
+_GRAD_SLACK = 1024  # elements >= 8 ranks x 32 channels x 4
 
 
 def _al(n: int) -> int:
@@ -37,7 +38,11 @@ class FlatParams:
             off += _al(p.numel())
         self.numel = max(off, _ALIGN)
         self.data = torch.zeros(self.numel, dtype=torch.float32, device=device)
-        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=device)
+        # zeroed slack after the gradients: the DDP reducer pads the all-reduce of the bucket that
+        # ends there to a multiple of world_size x channels x 16 B (Reducer::set_padding)
+        self.capacity = self.numel + _GRAD_SLACK
+        self._grad_store = torch.zeros(self.capacity, dtype=torch.float32, device=device)
+        self.grad = self._grad_store[:self.numel]
         with torch.no_grad():
             for p, o in zip(self.params, self.offsets):
                 self.data[o:o + p.numel()].copy_(p.detach().reshape(-1))
@@ -56,7 +61,7 @@ class FlatParams:
                 p.grad = g
 
     def zero_grad(self) -> None:
-        self.grad.zero_()
+        self.grad.zero_()  # the slack stays zero: only all-reduces of zeros ever touch it
         self.attach_grads()
 
     def span(self, i: int) -> tuple[int, int]:

@@ -112,7 +112,9 @@ def _validate_iters(pc, rccl, C, dev, tdt, cdt, numel, iters, st, g, inf) -> boo
 
 def pick_transport(pc, rccl, numels: list[int], dtype: str = "f32", iters: int = 10) -> tuple[str, dict]:
     """Time one pass of all-reduces over buckets of `numels` elements with each transport (the
-    DDP reducer's buckets), slowest rank decides; every rank returns the same choice."""
+    DDP reducer's buckets), slowest rank decides; every rank returns the same choice.  ``rccl``
+    is one communicator (name "rccl") or {variant: Comm} (names "rccl:<variant>", the xGMI-sized
+    variants of comm.py); ``pc`` may be None (RCCL variants only)."""
     import time
 
     inf = _comm.info()
@@ -122,14 +124,16 @@ def pick_transport(pc, rccl, numels: list[int], dtype: str = "f32", iters: int =
     cdt = C.DType.f32 if dtype == "f32" else C.DType.bf16
     bufs = [torch.zeros(n, dtype=tdt, device=dev) for n in numels]
     st = torch.cuda.current_stream(dev).cuda_stream
+    comms = {"rccl": rccl} if not isinstance(rccl, dict) else {f"rccl:{k}": v for k, v in rccl.items()}
+    cands = list(comms) + (["peer"] if pc is not None else [])
     res = {}
-    for name in ("rccl", "peer"):
+    for name in cands:
         def one_pass():
             for b in bufs:
                 if name == "peer":
                     pc.all_reduce(b.data_ptr(), b.numel(), cdt, st)
                 else:
-                    rccl.all_reduce(b.data_ptr(), b.data_ptr(), b.numel(), cdt, C.RedOp.sum, st)
+                    comms[name].all_reduce(b.data_ptr(), b.data_ptr(), b.numel(), cdt, C.RedOp.sum, st)
         one_pass()
         torch.cuda.synchronize(dev)
         _comm.barrier()
@@ -138,9 +142,10 @@ def pick_transport(pc, rccl, numels: list[int], dtype: str = "f32", iters: int =
             one_pass()
         torch.cuda.synchronize(dev)
         res[name] = _comm.all_reduce_max(time.perf_counter() - t0) / iters * 1e3
-    if pc.error():
-        res["peer"] = float("inf")
-    res["peer"] = _comm.all_reduce_max(res["peer"])
+    if pc is not None:
+        if pc.error():
+            res["peer"] = float("inf")
+        res["peer"] = _comm.all_reduce_max(res["peer"])
     return min(res, key=res.get), res
 
 

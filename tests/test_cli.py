@@ -146,3 +146,17 @@ def test_slurm_tasks_per_node_fallbacks(monkeypatch):
     assert comm.env_dist()["local_world_size"] == 8
     monkeypatch.delenv("SLURM_NNODES")
     assert comm.env_dist()["local_world_size"] == 16  # single node: every task is local
+
+
+def test_rccl_variant_names():
+    from mxddp.parallel.comm import parse_variant, rccl_variants
+
+    assert parse_variant("default") == {"ctas": 0, "algo": "", "proto": ""}
+    assert parse_variant("Ring:c14") == {"ctas": 14, "algo": "Ring", "proto": ""}
+    assert parse_variant("Ring/LL128:c28") == {"ctas": 28, "algo": "Ring", "proto": "LL128"}
+    assert parse_variant("auto:c7") == {"ctas": 7, "algo": "", "proto": ""}
+    assert "default" in rccl_variants() and "Ring:c7" in rccl_variants()
+    import pytest
+
+    with pytest.raises(ValueError):
+        parse_variant("Ring:7")

@@ -198,3 +198,57 @@ def test_bench_json_reports_per_image_metrics(cuda):
     assert 0.0 <= out["train_acc"] <= 1.0, out
     assert 0.0 < out["train_loss_avg"] < 3.0, out
     assert out["train_images"] >= 25 * 64, out
+
+
+@pytest.mark.parametrize("variant", ["default", "Ring:c7", "Ring:c28", "Ring/Simple:c14"])
+def test_fused_engine_rccl_variants_ws1(cuda, variant):
+    """Every xGMI-sized RCCL communicator variant (ncclCommInitRankConfig with pinned CTA counts,
+    NCCL_ALGO / NCCL_PROTO pinned for its init) carries the forced DDP all-reduces of the fused
+    step -- the padded fc bucket included -- and trains exactly like the reference."""
+    from mxddp import native
+    from mxddp.engine import FusedMnistTrainer
+    from mxddp.models import MnistCNN
+    from mxddp.parallel.comm import parse_variant
+
+    C = native()
+    comm = C.Comm(C.Comm.new_unique_id(), 0, 1, cuda.index or 0, **parse_variant(variant))
+    assert comm.variant == variant
+    torch.manual_seed(0)
+    ref = MnistCNN()
+    B, steps = 32, 4
+    tr = FusedMnistTrainer(batch=B, device=cuda, comm=comm, init_model=ref, use_graph=False, force_collectives=True)
+    assert tr.active_transport == f"rccl:{variant}"
+    xs = [torch.rand(B, 1, 28, 28) for _ in range(steps)]
+    ys = [torch.randint(0, 10, (B,)) for _ in range(steps)]
+    losses = []
+    for i in range(steps):
+        tr.set_batch(xs[i].to(cuda), ys[i].to(cuda))
+        tr.step(1)
+        losses.append(tr.read_metrics()[0] / B)
+    ref_losses = _ref_steps(ref, xs, ys, steps)
+    for a, b in zip(losses, ref_losses):
+        assert abs(a - b) < 1e-4 * max(1.0, abs(b)), (losses, ref_losses)
+    assert tr._grad_store[tr.params.numel():].abs().max().item() == 0.0  # padding slack stays zero
+
+
+def test_fused_autotune_lists_rccl_variants(cuda, monkeypatch):
+    """autotune() times every configured RCCL variant (here at world size 1, collectives
+    forced) and reports them in its JSON; the trained weights stay exact under restore=True."""
+    from mxddp.engine import FusedMnistTrainer
+    from mxddp.parallel import comm as pc
+
+    monkeypatch.setenv("MXDDP_RCCL_VARIANTS", "default,Ring:c7,Ring:c28")
+    pc.init_distributed(use_gpu=True)
+    comm = pc.rccl_comm(force=True)
+    a = FusedMnistTrainer(batch=64, device=cuda, lr=0.01, comm=comm, force_collectives=True)
+    b = FusedMnistTrainer(batch=64, device=cuda, lr=0.01)
+    a.step(1)
+    b.step(1)
+    res = a.autotune(trial_steps=3, restore=True)
+    names = {k.split("/")[0] for k in a.tuned["trials_ms"]}
+    assert names == {"rccl:default", "rccl:Ring:c7", "rccl:Ring:c28"}, a.tuned
+    assert len(res) == 9 and a.steps == 1
+    a.step(10)
+    b.step(10)
+    for k, v in a.state_dict().items():
+        assert torch.allclose(v, b.state_dict()[k], rtol=1e-3, atol=2e-5), k
