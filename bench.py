@@ -398,13 +398,15 @@ def _layers_or_torch(a, torch, inf, dev, comm, B):
     # without Python / autograd overhead.  Every op of the step is graph-safe (no host sync; LR,
     # Adam / BN step counters and the synthetic data counter live on the device).
     if a.impl == "layers" and not a.no_graph:
-        side = torch.cuda.Stream(dev)
+        from mxddp.parallel.graphed import capture_stream
+
+        side = capture_stream(dev)  # its split-K planes are reserved before the capture
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             run_eager(2)  # allocator / autograd warm-up outside the capture
         torch.cuda.current_stream(dev).wait_stream(side)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+        with torch.cuda.graph(graph, stream=side, capture_error_mode="thread_local"):
             step()
 
         def run_graph(n):

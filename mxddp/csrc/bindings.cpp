@@ -249,6 +249,8 @@ PYBIND11_MODULE(_C, m) {
     shortcut_pad_add_bwd(P<const float>(dy), P<float>(dx), N, Cin, H, W, Cout, P_, Q, stride, acc, S(st));
   });
 
+  m.def("reserve_splitk_planes", [](uintptr_t st) { reserve_splitk_planes(S(st)); });
+
   // ---------------------------------------------------------------- optim / data
   m.def("sgd_step", [](uintptr_t p, uintptr_t g, uintptr_t buf, uintptr_t lr, float gscale, float mom, float wd,
                        int64_t n, bool first, uintptr_t st) {

@@ -222,6 +222,9 @@ void nhwc_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int 
 void nhwc_gap_fwd(const uint16_t* x, float* y, int N, int HW, int C, hipStream_t st);
 void nhwc_gap_bwd(const float* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st);
 
+// split-K partial planes of a stream, allocated ahead of a graph capture on it (ops_gemm.hip)
+void reserve_splitk_planes(hipStream_t st);
+
 // ---- optimizers (ops_optim.hip): flat multi-tensor, fp32 master ----
 // SGD (PyTorch semantics): g' = g*gscale + wd*p; buf = mom*buf + g' (buf=g' at first step); p -= lr*buf
 // `lr` is read from device memory so a captured graph follows LR schedules.

@@ -460,6 +460,10 @@ bool run_partial(Op& op, int64_t total, float* out, const float* bias, int C, in
 
 }  // namespace
 
+// Allocate the split-K partial planes of `st` now (outside any capture): a stream that will
+// capture a hipGraph gets its planes before the capture, so the captured GEMMs run split.
+void reserve_splitk_planes(hipStream_t st) { (void)splitk_planes(kPlaneFloats, st); }
+
 namespace {
 int init_conv_algo() {
   const char* e = std::getenv("MXDDP_CONV_ALGO");

@@ -203,6 +203,19 @@ class DistributedDataParallel(nn.Module):
             self.reducer.prepare()
         return self.module(*args, **kwargs)
 
+    def check(self):
+        """Raise if the gradient transport reported a failure (a peer that never arrived in the
+        xGMI peer all-reduce, an RCCL async error): a collective that silently gave up would
+        leave the ranks training on different gradients."""
+        if self.transport == "peer":
+            from . import peer as _peer
+
+            pc = _peer.peer_comm()
+            if pc is not None and pc.error():
+                raise RuntimeError(f"DDP peer all-reduce: rank {pc.error() - 1} never arrived (timeout)")
+        elif self._comm is not None and self.world_size > 1:
+            self._comm.check_async_error()
+
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero_grad()
 

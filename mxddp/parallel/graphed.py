@@ -25,6 +25,23 @@ from __future__ import annotations
 
 import torch
 
+from .. import native
+
+_CAPTURE_STREAMS: dict = {}
+
+
+def capture_stream(device: torch.device) -> torch.cuda.Stream:
+    """One stream per device on which every mxddp hipGraph is captured.  Stream-owned scratch
+    (the split-K partial planes of ops_gemm.hip) is reserved for it here, outside any capture:
+    a GEMM captured on a stream without planes would have to run unsplit."""
+    device = torch.device(device)
+    s = _CAPTURE_STREAMS.get(device)
+    if s is None:
+        s = torch.cuda.Stream(device)
+        native().reserve_splitk_planes(s.cuda_stream)
+        _CAPTURE_STREAMS[device] = s
+    return s
+
 
 class GraphedStep:
     def __init__(self, step_fn, device: torch.device, warmup: int = 2, before_replay=None, enabled: bool = True):
@@ -65,7 +82,7 @@ class GraphedStep:
         cur = torch.cuda.current_stream(self.device)
         self._x = x.detach().clone()
         self._y = y.detach().clone()
-        side = torch.cuda.Stream(self.device)
+        side = capture_stream(self.device)
         side.wait_stream(cur)
         g = torch.cuda.CUDAGraph()
         # thread-local capture mode: the communicator and reducer issue their own stream work

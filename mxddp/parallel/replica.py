@@ -181,8 +181,10 @@ class ReplicaGroup:
         graphs = []
         for i, d in enumerate(self.devices):
             with torch.cuda.device(d):
+                from .graphed import capture_stream
+
                 cur = torch.cuda.current_stream(d)
-                side = torch.cuda.Stream(d)
+                side = capture_stream(d)
                 side.wait_stream(cur)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):

@@ -462,6 +462,8 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
             step += 1
             if log:
                 _sync(dev)
+                if hasattr(net, "check"):
+                    net.check()  # a gradient collective that gave up must not go unnoticed
                 now = time.time()
                 bt = (now - t_log) / max(1, bi - last_log) if bi else now - t_log
                 t_log, last_log = now, bi

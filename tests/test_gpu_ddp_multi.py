@@ -62,7 +62,7 @@ def _graph_worker(rank, ws, port, model_name, b, optname, q):
     spec = get_spec(model_name)
     batches = _batches(5, ws * b, spec.input_shape, seed=21)
     res, bad = [], []
-    for use_graph in (False, True):
+    for use_graph in (False, False, True):  # eager twice: the run-to-run noise floor
         torch.manual_seed(0)
         ddp = DDP(build_model(model_name).to(dev))
         if ddp.transport != "peer":
@@ -86,13 +86,22 @@ def _graph_worker(rank, ws, port, model_name, b, optname, q):
             bad.append(("graph use", use_graph, run.captured, run.replays))
         fb = ddp.flat_buffers.cpu() if ddp.flat_buffers is not None else torch.zeros(1)
         res.append((ddp.flat.data.cpu(), fb, acc.item(), len(ddp.buckets)))
-    (pa, ba, la, nb), (pg, bg, lg, _) = res
-    rel = ((pa - pg).abs().max() / pa.abs().max()).item()
-    relb = ((ba - bg).abs().max() / (ba.abs().max() + 1e-12)).item()
-    moved = None
-    if not rel <= 1e-6 or not relb <= 1e-6 or not abs(la - lg) <= 1e-6 * abs(la):
-        bad.append(("graph != eager", rel, relb, la, lg))
-    q.put((rank, bad, {"rel": rel, "relb": relb, "buckets": nb, "moved": moved}))
+    (pa, ba, la, nb), (pe, be, le, _), (pg, bg, lg, _) = res
+
+    def rel(a, b):
+        return ((a - b).abs().max() / (a.abs().max() + 1e-12)).item()
+
+    # kernels with float atomics (Winograd split reductions, split-K) make two EAGER runs differ
+    # by rounding, which BN at batch 8 amplifies; the graph must be as close as that floor
+    floor = max(rel(pa, pe), rel(ba, be))
+    r_p, r_b = rel(pa, pg), rel(ba, bg)
+    if not r_p <= max(1e-6, 4 * floor) or not r_b <= max(1e-6, 4 * floor):
+        bad.append(("graph != eager", r_p, r_b, "noise floor", floor, la, le, lg))
+    allp = [None] * ws
+    torch.distributed.all_gather_object(allp, pg)
+    if any(not torch.equal(allp[0], t) for t in allp):
+        bad.append("ranks' graph-step parameters diverged")
+    q.put((rank, bad, {"rel": r_p, "relb": r_b, "floor": floor, "buckets": nb}))
     PC.shutdown()
 
 
@@ -155,20 +164,36 @@ def _bn_worker(rank, ws, port, model_name, b, dtype, q):
                 flats[r].grad.copy_(avg)
                 opts[r].step()
         torch.cuda.synchronize()
+        # weights: relative to their scale; BN shift (beta) and running mean: relative to the
+        # feature's spread sqrt(running_var) -- their values sit near 0, and float-atomic
+        # rounding amplified by BN at batch 4 moves them by a tiny fraction of that spread,
+        # whereas a semantic error (no buffer broadcast, no per-rank statistics, wrong average)
+        # moves them by a sizeable part of it
         tol = 1e-4 if dtype == "fp32" else 2e-2
+        tol_spread = 1e-2 if dtype == "fp32" else 5e-2
         worst = {}
         for r in range(ws):
             ref = sims[r].state_dict()
             for k, v in ref.items():
                 got = allsd[r][k]
                 v = v.detach().cpu()
-                if v.is_floating_point():
+                if not v.is_floating_point():
+                    if not torch.equal(got, v):
+                        bad.append((r, k, "int buffer", got.tolist(), v.tolist()))
+                    continue
+                mod = k.rsplit(".", 1)[0]
+                is_bn_shift = (k.endswith("running_mean") or
+                               (k.endswith("bias") and f"{mod}.running_var" in ref))
+                if is_bn_shift:
+                    spread = ref[f"{mod}.running_var"].detach().cpu().clamp_min(1e-12).sqrt().max().item()
+                    e = ((got - v).abs().max() / spread).item()
+                    lim = tol_spread
+                else:
                     e = ((got - v).abs().max() / (v.abs().max() + 1e-6)).item()
-                    worst[k] = max(worst.get(k, 0.0), e)
-                    if not e <= tol:
-                        bad.append((r, k, e))
-                elif not torch.equal(got, v):
-                    bad.append((r, k, "int buffer", got.tolist(), v.tolist()))
+                    lim = tol
+                worst[k] = max(worst.get(k, 0.0), e)
+                if not e <= lim:
+                    bad.append((r, k, e))
         info["worst_rel"] = max(worst.values())
         # running stats differ between ranks (each rank's own last shard) while weights agree
         k_rm = [k for k in allsd[0] if k.endswith("running_mean")][0]
