@@ -7,6 +7,7 @@
 
 #include "comm.h"
 #include "common.h"
+#include "keras_engine.h"
 #include "mnist_engine.h"
 #include "ops.h"
 #include "peer.h"
@@ -386,6 +387,38 @@ PYBIND11_MODULE(_C, m) {
       .def("set_peer", &Reducer::set_peer, py::arg("peer").none(true), py::keep_alive<1, 2>())
       .def("set_force_collectives", &Reducer::set_force_collectives)
       .def_property_readonly("active", &Reducer::active);
+
+  // ---------------------------------------------------------------- fused Keras-CNN engine
+  m.def("keras_workspace_bytes", &KerasEngine::workspace_bytes);
+  m.attr("KERAS_NUM_PARAMS") = KerasLayout::total;
+  py::class_<KerasEngine>(m, "KerasEngine")
+      .def(py::init([](int B, uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t st, uintptr_t ws,
+                       size_t wsb, Comm* comm, uint64_t seed, uintptr_t lr, uintptr_t metrics, float b1, float b2,
+                       float eps, float wd, bool eps_hat) {
+             return new KerasEngine(B, p, g, mm, v, st, ws, wsb, comm, seed, lr, metrics, b1, b2, eps, wd, eps_hat);
+           }),
+           py::arg("batch"), py::arg("params"), py::arg("grads"), py::arg("m"), py::arg("v"), py::arg("adam_state"),
+           py::arg("workspace"), py::arg("workspace_bytes"), py::arg("comm").none(true), py::arg("seed"),
+           py::arg("lr_dev"), py::arg("metrics_dev"), py::arg("b1"), py::arg("b2"), py::arg("eps"),
+           py::arg("weight_decay"), py::arg("eps_hat"), py::keep_alive<1, 10>())
+      .def("step", &KerasEngine::step)
+      .def("capture", &KerasEngine::capture, py::arg("steps_per_graph") = 1)
+      .def("replay", &KerasEngine::replay)
+      .def("uncapture", &KerasEngine::uncapture)
+      .def("warm_graphs", &KerasEngine::warm_graphs)
+      .def("repack", &KerasEngine::repack)
+      .def("sync", &KerasEngine::sync, py::call_guard<py::gil_scoped_release>())
+      .def("set_peer", &KerasEngine::set_peer, py::arg("peer").none(true), py::keep_alive<1, 2>())
+      .def("set_force_collectives", &KerasEngine::set_force_collectives)
+      .def("set_external_batch", &KerasEngine::set_external_batch)
+      .def_property_readonly("world_size", &KerasEngine::world_size)
+      .def_property_readonly("reducer_active", &KerasEngine::reducer_active)
+      .def_property_readonly("peer_active", &KerasEngine::peer_active)
+      .def_property_readonly("captured", &KerasEngine::captured)
+      .def_property_readonly("stream", &KerasEngine::stream)
+      .def_property_readonly("x_ptr", &KerasEngine::x_ptr)
+      .def_property_readonly("y_ptr", &KerasEngine::y_ptr)
+      .def_property_readonly("counter_ptr", &KerasEngine::counter_ptr);
 
   // ---------------------------------------------------------------- fused MNIST engine
   m.def("mnist_workspace_bytes", &MnistLayout::workspace_bytes);

@@ -1,0 +1,653 @@
+// Fused gfx950 training step of the reference's TF2 Keras CNN (tensorflow2/mnist_single.py:16-26,
+// trained with Keras Adam: :78) -- the model of the MirroredStrategy config (BASELINE config 4).
+//
+// Four launches per step (five with gradient collectives), every one over the whole batch:
+//   KF1  on-device batch + conv1 + ReLU + max-pool (VALU, one 28x28 image per block) + conv2 as
+//        an MFMA implicit GEMM whose M order puts each 2x2 pool window in one lane's four
+//        accumulators, so bias, ReLU, max-pool and argmax happen in registers
+//        (block = image x 16 output channels; 4B blocks)
+//   KF2  conv3 + ReLU + fc1 + ReLU + fc2 + softmax-CE + accuracy, and the whole activation
+//        backward of that head down to the pooled conv2 output (conv3 data gradient, ReLU mask):
+//        everything per image lives in LDS (block = image)
+//   KB1  the rest of the backward in ONE heterogeneous launch:
+//          A  conv2 data gradient on MFMA (dY2 expanded on the fly from its compact pooled form
+//             [co][window] + argmax code: 1 compare + 1 select per operand element) -> pool1 /
+//             ReLU1 backward -> conv1 weight / bias gradient (block = image x 16 ci x M quarter)
+//          B  conv2 weight gradient on MFMA (block = image x 16 co)
+//          C  conv3 + fc1 weight gradients (block = 8 images x N quarter)
+//          E  fc2 weight gradient
+//        weight gradients go to per-image / per-group partial planes with plain stores: no
+//        float atomics, deterministic
+//   KO   finalize (each gradient = its planes summed in a fixed order) + Adam + repack of the
+//        conv2 weights into the MFMA fragment orders of KF1 / KB1 for the next step
+//        (with gradient collectives: finalize -> bucket all-reduce -> Adam)
+//
+// MFMA = v_mfma_f32_16x16x4_f32 (exact fp32): lane l supplies A[l&15][k=l>>4] and
+// B[k=l>>4][l&15]; the C tile has col = l&15, row = 4*(l>>4) + reg.
+//
+// Replaces (reference): the TF2 / Keras graph of Conv2D / MaxPooling2D / Dense /
+// sparse_categorical_crossentropy / Adam kernels run per replica by MirroredStrategy
+// (tensorflow2/mnist_mirror_strategy.py:12,68-79).
+#include "common.h"
+#include "keras_kernels.h"
+#include "rng.h"
+
+namespace mx {
+namespace keras {
+
+using L = KerasLayout;
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+constexpr int kP1 = 169;          // 13 x 13 pooled conv1 positions
+constexpr int kP1Img = 32 * kP1;  // 5408 floats per image
+constexpr int kP2Img = 64 * 25;   // 1600
+constexpr int kPl2 = 64 * 288;    // conv2 weights
+constexpr int kPl3 = 64 * 576;    // conv3 / fc1 weights
+
+// ------------------------------------------------------------------------------------------
+// KF1: block = (image n, conv2 output channels 16*c4 .. 16*c4+15).
+// conv2 GEMM: M = the 100 conv2 outputs that feed pool2 (rows / cols 0..9; MaxPool2D drops the
+// 11th), window-major: m = 4*window + 2*dy + dx (7 M-tiles, rows 100..111 dummy); N = 16 co;
+// K = 288 ordered k = r*32 + ci so the im2col LDS offset = per-lane base + compile-time
+// immediate.  The 72 B fragments (pre-packed w2f) sit in registers.
+__global__ __launch_bounds__(256) void kf1_kernel(KerasFused f) {
+  const int n = blockIdx.x >> 2, c4 = blockIdx.x & 3;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  __shared__ float xs[784];
+  __shared__ float w1s[320];
+  __shared__ float p1s[kP1Img];
+  if (f.synth) {
+    const uint32_t ctr = (uint32_t)*f.counter;
+    const uint2 key = synth_key(f.seed);
+    const int label = synth_label(ctr, n, 10, key);
+    if (tid < 196) {
+      const int d = 4 * tid;
+      const uint4 r = synth_noise4(ctr, n, d, key);
+      const float4 t = *reinterpret_cast<const float4*>(f.tmpl + label * 784 + d);
+      const float4 v = make_float4(0.5f * t.x + 0.5f * u01(r.x), 0.5f * t.y + 0.5f * u01(r.y),
+                                   0.5f * t.z + 0.5f * u01(r.z), 0.5f * t.w + 0.5f * u01(r.w));
+      *reinterpret_cast<float4*>(xs + d) = v;
+      if (c4 == 0) *reinterpret_cast<float4*>(f.x + (size_t)n * 784 + d) = v;
+    }
+    if (c4 == 0 && tid == 0) f.y[n] = label;
+  } else if (tid < 196) {
+    *reinterpret_cast<float4*>(xs + 4 * tid) = *reinterpret_cast<const float4*>(f.x + (size_t)n * 784 + 4 * tid);
+  }
+  for (int i = tid; i < 320; i += 256) w1s[i] = f.p[L::w1 + i];  // w1 [32][9] then b1 [32]
+  __syncthreads();
+
+  // conv1 + ReLU + 2x2 max-pool (+ argmax): 32 x 169 pooled outputs, one 4x4 input patch each
+  for (int o = tid; o < kP1Img; o += 256) {
+    const int ci = o / kP1, pp = o - ci * kP1, py = pp / 13, px = pp - py * 13;
+    const float* xp = xs + (2 * py) * 28 + 2 * px;
+    float pt[16];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) pt[a * 4 + b] = xp[a * 28 + b];
+    const float* wc = w1s + ci * 9;
+    float wr[9];
+#pragma unroll
+    for (int r = 0; r < 9; ++r) wr[r] = wc[r];
+    const float bias = w1s[288 + ci];
+    float bz = 0.f;
+    int best = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int dy = j >> 1, dx = j & 1;
+      float z = bias;
+#pragma unroll
+      for (int r = 0; r < 9; ++r) z += wr[r] * pt[(dy + r / 3) * 4 + dx + r % 3];
+      if (j == 0 || z > bz) {
+        bz = z;
+        best = j;
+      }
+    }
+    const float v = fmaxf(bz, 0.f);
+    p1s[o] = v;
+    if (c4 == 0) {
+      f.p1[(size_t)n * kP1Img + o] = v;
+      f.q1[(size_t)n * kP1Img + o] = (uint8_t)best;
+    }
+  }
+  __syncthreads();
+
+  // conv2 (16 co of this block) on MFMA
+  float breg[72];
+  const float* wf = f.w2f + (size_t)c4 * 72 * 64;
+#pragma unroll
+  for (int s = 0; s < 72; ++s) breg[s] = wf[s * 64 + lane];
+  const int co = 16 * c4 + (lane & 15);
+  const float bias2 = f.p[L::b2 + co];
+  for (int mt = w; mt < 7; mt += 4) {
+    const int ml = lane & 15, win = 4 * mt + (ml >> 2);
+    int base = 0;
+    if (win < 25) {
+      const int wy = win / 5, wx = win - wy * 5;
+      base = (2 * wy + ((ml >> 1) & 1)) * 13 + 2 * wx + (ml & 1);
+    }
+    const float* ap = p1s + base + g * kP1;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 72; ++s) {
+      const int r = s >> 3;
+      acc = mfma4(ap[(4 * (s & 7)) * kP1 + (r / 3) * 13 + (r % 3)], breg[s], acc);
+    }
+    const int wo = 4 * mt + g;  // this lane's accumulators = the 4 outputs of window wo, channel co
+    if (wo < 25) {
+      int best = 0;
+      float bz = acc[0];
+#pragma unroll
+      for (int j = 1; j < 4; ++j)
+        if (acc[j] > bz) {
+          bz = acc[j];
+          best = j;
+        }
+      const size_t o = ((size_t)n * 64 + co) * 25 + wo;
+      f.p2[o] = fmaxf(bz + bias2, 0.f);
+      f.q2[o] = (uint8_t)best;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// KF2: block = image.  Head forward + backward to the pooled conv2 output; VALU, LDS-resident.
+__global__ __launch_bounds__(256) void kf2_kernel(KerasFused f) {
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  __shared__ float p2s[kP2Img];
+  __shared__ float x3s[576];
+  __shared__ float dx3s[576];
+  __shared__ float hs[64];
+  __shared__ float dh1s[64];
+  __shared__ float dls[16];
+  for (int i = tid; i < kP2Img; i += 256) p2s[i] = f.p2[(size_t)n * kP2Img + i];
+  if (f.synth && n == 0 && tid == 0) *f.counter += 1;  // KF1 consumed this batch index
+  __syncthreads();
+
+  // conv3 + bias + ReLU: thread (co = tid/4, ci quarter q) -> all 9 outputs of co over 16 ci
+  {
+    const int co = tid >> 2, q = tid & 3;
+    float acc[9];
+#pragma unroll
+    for (int pos = 0; pos < 9; ++pos) acc[pos] = 0.f;
+    const float* wp = f.p + L::w3 + ((size_t)co * 64 + 16 * q) * 9;
+    for (int c = 0; c < 16; ++c) {
+      const float* pc = p2s + (16 * q + c) * 25;
+      float pt[25];
+#pragma unroll
+      for (int k = 0; k < 25; ++k) pt[k] = pc[k];
+      float wr[9];
+#pragma unroll
+      for (int r = 0; r < 9; ++r) wr[r] = wp[c * 9 + r];
+#pragma unroll
+      for (int pos = 0; pos < 9; ++pos)
+#pragma unroll
+        for (int r = 0; r < 9; ++r) acc[pos] += wr[r] * pt[(pos / 3 + r / 3) * 5 + pos % 3 + r % 3];
+    }
+#pragma unroll
+    for (int pos = 0; pos < 9; ++pos) {
+      acc[pos] += __shfl_xor(acc[pos], 1, 64);
+      acc[pos] += __shfl_xor(acc[pos], 2, 64);
+    }
+    if (q == 0) {
+      const float b = f.p[L::b3 + co];
+#pragma unroll
+      for (int pos = 0; pos < 9; ++pos) x3s[co * 9 + pos] = fmaxf(acc[pos] + b, 0.f);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < 576; i += 256) f.x3[(size_t)n * 576 + i] = x3s[i];
+
+  // fc1 + bias + ReLU: thread (j = tid/4, quarter q of the 576 inputs)
+  {
+    const int j = tid >> 2, q = tid & 3;
+    const float4* wr = reinterpret_cast<const float4*>(f.p + L::fw1 + (size_t)j * 576 + 144 * q);
+    const float4* xr = reinterpret_cast<const float4*>(x3s + 144 * q);
+    float a = 0.f;
+#pragma unroll 4
+    for (int k = 0; k < 36; ++k) {
+      const float4 wv4 = wr[k], xv = xr[k];
+      a += wv4.x * xv.x + wv4.y * xv.y + wv4.z * xv.z + wv4.w * xv.w;
+    }
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    if (q == 0) hs[j] = fmaxf(a + f.p[L::fb1 + j], 0.f);
+  }
+  __syncthreads();
+
+  // fc2 + softmax + cross entropy + accuracy + dlogits (wave 0)
+  if (wv == 0) {
+    float a = 0.f;
+    if (lane < 40) {
+      const int c = lane >> 2, q = lane & 3;
+      const float* wr = f.p + L::fw2 + c * 64 + 16 * q;
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) a += wr[jj] * hs[16 * q + jj];
+    }
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    const float lg0 = __shfl(a, 4 * (lane < 10 ? lane : 0), 64);
+    const float lg = lane < 10 ? lg0 + f.p[L::fb2 + lane] : -INFINITY;
+    const float mx = wave_max(lg);
+    const float ex = lane < 10 ? __expf(lg - mx) : 0.f;
+    const float se = wave_sum(ex);
+    const int label = f.y[n];
+    const float lbl = __shfl(lg, label, 64);
+    const unsigned long long ball = __ballot(lane < 10 && lg == mx);
+    const int first = __ffsll((long long)ball) - 1;
+    if (lane < 10) {
+      const float d = (ex / se - (lane == label ? 1.f : 0.f)) / (float)f.B;
+      dls[lane] = d;
+      f.dl[(size_t)n * 16 + lane] = d;
+      f.sv[(size_t)n * 256 + 192 + lane] = d;
+    }
+    if (lane == 0) {
+      atomicAdd(f.metrics, mx + __logf(se) - lbl);
+      atomicAdd(f.metrics + 1, first == label ? 1.f : 0.f);
+    }
+  }
+  __syncthreads();
+  // dh1 = (fw2^T dl) * (h > 0)
+  if (tid < 64) {
+    float a = 0.f;
+#pragma unroll
+    for (int c = 0; c < 10; ++c) a += f.p[L::fw2 + c * 64 + tid] * dls[c];
+    const float d = hs[tid] > 0.f ? a : 0.f;
+    dh1s[tid] = d;
+    f.dh1[(size_t)n * 64 + tid] = d;
+    f.h1[(size_t)n * 64 + tid] = hs[tid];
+    f.sv[(size_t)n * 256 + 128 + tid] = d;
+  }
+  __syncthreads();
+  // dx3 = (fw1^T dh1) * (x3 > 0)
+  for (int i = tid; i < 576; i += 256) {
+    const float* wc = f.p + L::fw1 + i;
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll 8
+    for (int j = 0; j < 64; j += 2) {
+      a0 += wc[(size_t)j * 576] * dh1s[j];
+      a1 += wc[(size_t)(j + 1) * 576] * dh1s[j + 1];
+    }
+    const float d = x3s[i] > 0.f ? a0 + a1 : 0.f;
+    dx3s[i] = d;
+    f.dx3[(size_t)n * 576 + i] = d;
+  }
+  __syncthreads();
+  if (tid < 64) {  // conv3 bias grad of this image
+    float s = 0.f;
+#pragma unroll
+    for (int pos = 0; pos < 9; ++pos) s += dx3s[tid * 9 + pos];
+    f.sv[(size_t)n * 256 + 64 + tid] = s;
+  }
+  // conv3 data gradient -> dp2 (ReLU-masked with p2 > 0), conv2 bias grad:
+  // thread (ci = tid/4, co quarter q) scatters its 16 co's contributions into 25 registers
+  {
+    const int ci = tid >> 2, q = tid & 3;
+    float acc[25];
+#pragma unroll
+    for (int k = 0; k < 25; ++k) acc[k] = 0.f;
+    for (int c = 0; c < 16; ++c) {
+      const int co = 16 * q + c;
+      float d[9], wr[9];
+#pragma unroll
+      for (int pos = 0; pos < 9; ++pos) d[pos] = dx3s[co * 9 + pos];
+      const float* wp = f.p + L::w3 + ((size_t)co * 64 + ci) * 9;
+#pragma unroll
+      for (int r = 0; r < 9; ++r) wr[r] = wp[r];
+#pragma unroll
+      for (int pos = 0; pos < 9; ++pos)
+#pragma unroll
+        for (int r = 0; r < 9; ++r) acc[(pos / 3 + r / 3) * 5 + pos % 3 + r % 3] += d[pos] * wr[r];
+    }
+#pragma unroll
+    for (int k = 0; k < 25; ++k) {
+      acc[k] += __shfl_xor(acc[k], 1, 64);
+      acc[k] += __shfl_xor(acc[k], 2, 64);
+    }
+    if (q == 0) {
+      float sb = 0.f;
+#pragma unroll
+      for (int k = 0; k < 25; ++k) {
+        const float v = p2s[ci * 25 + k] > 0.f ? acc[k] : 0.f;
+        f.dp2[((size_t)n * 64 + ci) * 25 + k] = v;
+        sb += v;
+      }
+      f.sv[(size_t)n * 256 + ci] = sb;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// KB1 role A: conv2 data gradient dP1[ci][y][x] = sum_{co,ky,kx} dY2[co][y-ky][x-kx] w2[co][ci][ky][kx]
+// on MFMA: M = the 169 pooled conv1 positions (11 tiles; this block: M quarter mq = 3 tiles, the
+// last 2), N = 16 ci (ci half nh), K = 576 = (tap r, co) split over the 4 waves by co (wave w:
+// co 16w..16w+15, 36 k-steps: r = s/4, co = 16w + 4(s%4) + lane group).  dY2 lives compact in LDS
+// as [co][8][8] pool windows (a dead ring of windows around the 5x5, so no bounds checks) + the
+// argmax code; an operand element is (code == its parity) ? value : 0.  The 4 waves' partial
+// tiles are summed in LDS, then each lane masks with pool1 / ReLU1 (argmax code, p1 > 0) and
+// contracts with the 3x3 input patch at the argmax position: conv1 weight / bias grads, reduced
+// over lanes and tiles into this block's partial plane.
+struct SmemA {
+  float dps[64 * 64];
+  uint8_t qs[64 * 64];
+  float xs[784];
+  float red[4][3][4][64];
+  float c1[3][16][10];
+};
+struct SmemB {
+  float p1s[kP1Img];
+};
+struct SmemC {
+  float dx3[8][576];
+  float p2[8][16][25];
+  float dh1[8][64];
+  float x3[8][144];
+};
+union SmemKB1 {
+  SmemA a;
+  SmemB b;
+  SmemC c;
+};
+
+__device__ void kb1_role_a(const KerasFused& f, SmemA& sm, int bid) {
+  const int n = bid >> 3, nh = (bid >> 2) & 1, mq = bid & 3;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  for (int i = tid; i < 64 * 64; i += 256) {
+    sm.dps[i] = 0.f;
+    sm.qs[i] = 0;
+  }
+  for (int i = tid; i < 784; i += 256) sm.xs[i] = f.x[(size_t)n * 784 + i];
+  __syncthreads();
+  for (int e = tid; e < kP2Img; e += 256) {
+    const int co = e / 25, wi = e - co * 25, wy = wi / 5, wx = wi - wy * 5;
+    const int idx = co * 64 + (wy + 1) * 8 + wx + 1;
+    sm.dps[idx] = f.dp2[(size_t)n * kP2Img + e];
+    sm.qs[idx] = f.q2[(size_t)n * kP2Img + e];
+  }
+  // B fragments of this wave's 36 k-steps (pre-packed w2d)
+  float breg[36];
+  const float* wd = f.w2d + ((size_t)(nh * 4 + w) * 36) * 64;
+#pragma unroll
+  for (int s = 0; s < 36; ++s) breg[s] = wd[s * 64 + lane];
+  const int t0 = 3 * mq, nt = mq == 3 ? 2 : 3;
+  // per tile, per tap: window offset [8x8 grid] and the argmax code dY2's position must match
+  int off[3][9], code[3][9];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    int m = 16 * (t0 + t) + (lane & 15);
+    if (t >= nt || m >= kP1) m = 0;
+    const int y = m / 13, x = m - y * 13;
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      const int oy = y - r / 3, ox = x - r % 3;
+      off[t][r] = ((oy + 2) >> 1) * 8 + ((ox + 2) >> 1);
+      code[t][r] = (oy & 1) * 2 + (ox & 1);
+    }
+  }
+  __syncthreads();
+  const int lbase = (16 * w + g) * 64;
+  f32x4 acc[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int s = 0; s < 36; ++s) {
+    const int r = s >> 2, cofs = 4 * (s & 3) * 64;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int idx = lbase + cofs + off[t][r];
+      const float a = (int)sm.qs[idx] == code[t][r] ? sm.dps[idx] : 0.f;
+      acc[t] = mfma4(a, breg[s], acc[t]);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sm.red[w][t][j][lane] = acc[t][j];
+  __syncthreads();
+  if (w < nt) {  // wave w finishes tile t0 + w
+    const int t = w, ci_l = lane & 15, ci = 16 * nh + ci_l;
+    float cw[9], cb = 0.f;
+#pragma unroll
+    for (int r = 0; r < 9; ++r) cw[r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = 16 * (t0 + t) + 4 * g + j;
+      if (m < kP1) {
+        const float d = sm.red[0][t][j][lane] + sm.red[1][t][j][lane] + sm.red[2][t][j][lane] + sm.red[3][t][j][lane];
+        const size_t pi = ((size_t)n * 32 + ci) * kP1 + m;
+        if (f.p1[pi] > 0.f) {
+          const int cd = f.q1[pi];
+          const int y1 = 2 * (m / 13) + (cd >> 1), x1 = 2 * (m % 13) + (cd & 1);
+#pragma unroll
+          for (int r = 0; r < 9; ++r) cw[r] += d * sm.xs[(y1 + r / 3) * 28 + x1 + r % 3];
+          cb += d;
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      cw[r] += __shfl_xor(cw[r], 16, 64);
+      cw[r] += __shfl_xor(cw[r], 32, 64);
+    }
+    cb += __shfl_xor(cb, 16, 64);
+    cb += __shfl_xor(cb, 32, 64);
+    if (g == 0) {
+#pragma unroll
+      for (int r = 0; r < 9; ++r) sm.c1[t][ci_l][r] = cw[r];
+      sm.c1[t][ci_l][9] = cb;
+    }
+  }
+  __syncthreads();
+  if (tid < 160) {
+    const int ci_l = tid / 10, k = tid - ci_l * 10, ci = 16 * nh + ci_l;
+    float s = 0.f;
+    for (int t = 0; t < nt; ++t) s += sm.c1[t][ci_l][k];
+    float* plane = f.pl1 + ((size_t)n * 4 + mq) * 320;
+    if (k < 9) plane[ci * 9 + k] = s;
+    else plane[288 + ci] = s;
+  }
+}
+
+// role B: conv2 weight gradient of image n for co 16cq..16cq+15: M = 16 co, N = 288 (ci, tap) in
+// 18 tiles (wave w: tiles w, w+4, ...), K = the 100 conv2 outputs that feed pool2 (25 k-steps).
+// The A operand (expanded dY2) of a lane is the same for every N tile: 25 registers built once.
+__device__ void kb1_role_b(const KerasFused& f, SmemB& sm, int bid) {
+  const int n = bid >> 2, cq = bid & 3;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  for (int i = tid; i < kP1Img / 4; i += 256)
+    reinterpret_cast<float4*>(sm.p1s)[i] = reinterpret_cast<const float4*>(f.p1 + (size_t)n * kP1Img)[i];
+  const int co_a = 16 * cq + (lane & 15);
+  float av[25];
+  int poff[25];
+#pragma unroll
+  for (int s = 0; s < 25; ++s) {
+    const int pos = 4 * s + g, oy = pos / 10, ox = pos - oy * 10;
+    const size_t e = ((size_t)n * 64 + co_a) * 25 + (oy >> 1) * 5 + (ox >> 1);
+    av[s] = (int)f.q2[e] == (oy & 1) * 2 + (ox & 1) ? f.dp2[e] : 0.f;
+    poff[s] = oy * 13 + ox;
+  }
+  __syncthreads();
+  for (int nt = w; nt < 18; nt += 4) {
+    const int c = 16 * nt + (lane & 15), ci = c / 9, r = c - ci * 9;
+    const float* bp = sm.p1s + ci * kP1 + (r / 3) * 13 + r % 3;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 25; ++s) acc = mfma4(av[s], bp[poff[s]], acc);
+    float* plane = f.pl2 + (size_t)n * kPl2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) plane[(16 * cq + 4 * g + j) * 288 + c] = acc[j];
+  }
+}
+
+// role C: conv3 + fc1 weight gradients of an 8-image group gi, quarter nq of the input columns
+__device__ void kb1_role_c(const KerasFused& f, SmemC& sm, int bid) {
+  const int gi = bid >> 2, nq = bid & 3, tid = threadIdx.x;
+  const int n0 = 8 * gi;
+  for (int i = tid; i < 8 * 576; i += 256) sm.dx3[i / 576][i % 576] = f.dx3[(size_t)n0 * 576 + i];
+  for (int i = tid; i < 8 * 16 * 25; i += 256) {
+    const int im = i / 400, rem = i - im * 400;
+    sm.p2[im][rem / 25][rem % 25] = f.p2[((size_t)(n0 + im) * 64 + 16 * nq) * 25 + rem];
+  }
+  for (int i = tid; i < 8 * 64; i += 256) sm.dh1[i / 64][i % 64] = f.dh1[(size_t)n0 * 64 + i];
+  for (int i = tid; i < 8 * 144; i += 256)
+    sm.x3[i / 144][i % 144] = f.x3[(size_t)(n0 + i / 144) * 576 + 144 * nq + i % 144];
+  __syncthreads();
+  {  // conv3: thread (co, 4 ci of the block's 16) -> 36 weights
+    const int co = tid >> 2, cq = tid & 3;
+    float acc[4][9];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 9; ++r) acc[c][r] = 0.f;
+    for (int im = 0; im < 8; ++im) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float pt[25];
+#pragma unroll
+        for (int k = 0; k < 25; ++k) pt[k] = sm.p2[im][4 * cq + c][k];
+#pragma unroll
+        for (int pos = 0; pos < 9; ++pos) {
+          const float d = sm.dx3[im][co * 9 + pos];
+#pragma unroll
+          for (int r = 0; r < 9; ++r) acc[c][r] += d * pt[(pos / 3 + r / 3) * 5 + pos % 3 + r % 3];
+        }
+      }
+    }
+    float* plane = f.pl3 + (size_t)gi * kPl3 + (size_t)co * 576 + (16 * nq + 4 * cq) * 9;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 9; ++r) plane[c * 9 + r] = acc[c][r];
+  }
+  {  // fc1: thread (j, 36 of the block's 144 inputs)
+    const int j = tid >> 2, q = tid & 3;
+    float acc[36];
+#pragma unroll
+    for (int i = 0; i < 36; ++i) acc[i] = 0.f;
+    for (int im = 0; im < 8; ++im) {
+      const float h = sm.dh1[im][j];
+#pragma unroll
+      for (int i = 0; i < 36; ++i) acc[i] += h * sm.x3[im][36 * q + i];
+    }
+    float* plane = f.pf1 + (size_t)gi * kPl3 + (size_t)j * 576 + 144 * nq + 36 * q;
+#pragma unroll
+    for (int i = 0; i < 36; ++i) plane[i] = acc[i];
+  }
+}
+
+__device__ void kb1_role_e(const KerasFused& f) {
+  for (int o = threadIdx.x; o < 640; o += 256) {
+    const int c = o >> 6, j = o & 63;
+    float a = 0.f;
+    for (int nn = 0; nn < f.B; ++nn) a += f.dl[(size_t)nn * 16 + c] * f.h1[(size_t)nn * 64 + j];
+    f.gf2[o] = a;
+  }
+}
+
+__global__ __launch_bounds__(256) void kb1_kernel(KerasFused f) {
+  __shared__ SmemKB1 sm;
+  const int b = blockIdx.x, B = f.B;
+  if (b < 8 * B) kb1_role_a(f, sm.a, b);
+  else if (b < 12 * B) kb1_role_b(f, sm.b, b - 8 * B);
+  else if (b < 12 * B + B / 2) kb1_role_c(f, sm.c, b - 12 * B);
+  else kb1_role_e(f);
+}
+
+// ------------------------------------------------------------------------------------------
+// KO: one thread per parameter.  Gradient = its partial planes summed in a fixed order; Adam
+// (device step count advanced by the last block to finish, as ops_optim.hip); then the updated
+// conv2 weight is written into both MFMA fragment orders.
+__device__ __forceinline__ float sum_planes(const float* p, size_t stride, int n) {
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int i = 0;
+  for (; i + 4 <= n; i += 4) {
+    a0 += p[(size_t)i * stride];
+    a1 += p[(size_t)(i + 1) * stride];
+    a2 += p[(size_t)(i + 2) * stride];
+    a3 += p[(size_t)(i + 3) * stride];
+  }
+  for (; i < n; ++i) a0 += p[(size_t)i * stride];
+  return (a0 + a1) + (a2 + a3);
+}
+
+__device__ __forceinline__ float finalize_grad(const KerasFused& f, int i) {
+  const int B = f.B;
+  if (i < (int)L::w2) return sum_planes(f.pl1 + i, 320, 4 * B);
+  if (i < (int)L::b2) return sum_planes(f.pl2 + (i - L::w2), kPl2, B);
+  if (i < (int)L::w3) return sum_planes(f.sv + (i - L::b2), 256, B);
+  if (i < (int)L::b3) return sum_planes(f.pl3 + (i - L::w3), kPl3, B / 8);
+  if (i < (int)L::fw1) return sum_planes(f.sv + 64 + (i - L::b3), 256, B);
+  if (i < (int)L::fb1) return sum_planes(f.pf1 + (i - L::fw1), kPl3, B / 8);
+  if (i < (int)L::fw2) return sum_planes(f.sv + 128 + (i - L::fb1), 256, B);
+  if (i < (int)L::fb2) return f.gf2[i - L::fw2];
+  return sum_planes(f.sv + 192 + (i - L::fb2), 256, B);
+}
+
+__device__ __forceinline__ void pack_w2(const KerasFused& f, int i, float val) {
+  // i in [w2, b2): co, ci, tap r of conv2.weight[co][ci][ky][kx]
+  const int j = i - L::w2, co = j / 288, rem = j - co * 288, ci = rem / 9, r = rem - ci * 9;
+  // KF1 B: (c4, s, lane): co = 16 c4 + (lane & 15), k = 4s + (lane >> 4) = r*32 + ci
+  const int k = r * 32 + ci;
+  f.w2f[((co >> 4) * 72 + (k >> 2)) * 64 + (co & 15) + 16 * (k & 3)] = val;
+  // KB1-A B: (nh, wave, s, lane): ci = 16 nh + (lane & 15), co = 16 wave + 4 (s%4) + (lane >> 4), r = s/4
+  const int cl = co & 15;
+  f.w2d[(((ci >> 4) * 4 + (co >> 4)) * 36 + r * 4 + (cl >> 2)) * 64 + (ci & 15) + 16 * (cl & 3)] = val;
+}
+
+__global__ __launch_bounds__(256) void ko_kernel(KerasFused f, int mode, float gscale) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const bool live = i < (int)L::total;
+  int t = 0;
+  if (mode == 0 || mode == 2) t = __hip_atomic_load(f.adam_state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  if (live) {
+    float pv = f.p[i];
+    if (mode == 0 || mode == 1 || mode == 2) {
+      float gr = mode == 2 ? f.g[i] * gscale : finalize_grad(f, i);
+      if (mode == 1) {
+        f.g[i] = gr;
+      } else {
+        gr += f.wd * pv;
+        const float bc1 = 1.f - powf(f.b1, (float)t), bc2 = 1.f - powf(f.b2, (float)t);
+        const float bc2s = sqrtf(bc2);
+        const float e = f.eps_hat ? f.eps / bc2s : f.eps;
+        const float mi = f.b1 * f.m[i] + (1.f - f.b1) * gr;
+        const float vi = f.b2 * f.v[i] + (1.f - f.b2) * gr * gr;
+        f.m[i] = mi;
+        f.v[i] = vi;
+        pv -= (*f.lr / bc1) * mi / (sqrtf(vi) / bc2s + e);
+        f.p[i] = pv;
+      }
+    }
+    if (mode != 1 && i >= (int)L::w2 && i < (int)L::b2) pack_w2(f, i, pv);
+  }
+  if (mode == 0 || mode == 2) {  // the last block to finish publishes the step count
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int arrived = __hip_atomic_fetch_add(f.adam_state + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (arrived == (int)gridDim.x - 1) {
+        __hip_atomic_store(f.adam_state, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(f.adam_state + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+}  // namespace keras
+
+void keras_fused_forward(const KerasFused& f, hipStream_t st) {
+  MX_CHECK(f.B > 0 && f.B % 8 == 0 && f.B <= 1024, "keras engine: batch must be a multiple of 8 (<= 1024)");
+  MX_LAUNCH(keras::kf1_kernel, dim3(4 * f.B), dim3(256), 0, st, f);
+  MX_LAUNCH(keras::kf2_kernel, dim3(f.B), dim3(256), 0, st, f);
+}
+
+void keras_fused_backward(const KerasFused& f, hipStream_t st) {
+  MX_LAUNCH(keras::kb1_kernel, dim3(12 * f.B + f.B / 2 + 1), dim3(256), 0, st, f);
+}
+
+void keras_fused_update(const KerasFused& f, int mode, float gscale, hipStream_t st) {
+  MX_CHECK(mode >= 0 && mode <= 3, "keras engine: update mode 0..3");
+  MX_LAUNCH(keras::ko_kernel, dim3((unsigned)((KerasLayout::total + 255) / 256)), dim3(256), 0, st, f, mode, gscale);
+}
+
+}  // namespace mx

@@ -255,6 +255,21 @@ def _log_epoch(inf, mode, seconds):
         print(L.single_epoch_line(seconds), flush=True)
 
 
+_DEBUG_RANKSUM = os.environ.get("MXDDP_DEBUG_RANKSUM", "0") == "1"
+
+
+def _print_rank_sums(inf, step, flat, runner):
+    """MXDDP_DEBUG_RANKSUM=1: every rank's parameter checksum at each log step (rank 0 prints)."""
+    import torch.distributed as dist
+
+    cs = (flat.data.double().sum().item(), flat.grad.double().sum().item(), runner.captured)
+    allcs = [None] * inf.world_size
+    dist.all_gather_object(allcs, cs)
+    if inf.is_main:
+        print(f"[ranksum] step {step}: " + " | ".join(f"r{r} p={a:.9f} g={b:.9f} graph={c}"
+                                                     for r, (a, b, c) in enumerate(allcs)), flush=True)
+
+
 class _null:
     def __enter__(self):
         return None
@@ -464,6 +479,8 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
                 _sync(dev)
                 if hasattr(net, "check"):
                     net.check()  # a gradient collective that gave up must not go unnoticed
+                if _DEBUG_RANKSUM and inf.world_size > 1:
+                    _print_rank_sums(inf, step, flat, runner)
                 now = time.time()
                 bt = (now - t_log) / max(1, bi - last_log) if bi else now - t_log
                 t_log, last_log = now, bi

@@ -169,7 +169,7 @@ def _bn_worker(rank, ws, port, model_name, b, dtype, q):
         # rounding amplified by BN at batch 4 moves them by a tiny fraction of that spread,
         # whereas a semantic error (no buffer broadcast, no per-rank statistics, wrong average)
         # moves them by a sizeable part of it
-        tol = 1e-4 if dtype == "fp32" else 2e-2
+        tol = 1e-3 if dtype == "fp32" else 2e-2  # BN at batch 4 amplifies atomic-order rounding
         tol_spread = 1e-2 if dtype == "fp32" else 5e-2
         worst = {}
         for r in range(ws):
