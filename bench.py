@@ -28,7 +28,7 @@ BASELINE_VALUE = None  # BASELINE.json "published": {} -- no MNIST number exists
 MODEL_METRIC = {
     "resnet50": "images/sec (whole node) ResNet-50 synthetic-ImageNet DDP (BASELINE config 5)",
     "pyramidnet110": "images/sec (whole node) PyramidNet-110 CIFAR-10 DDP (reference pytorch/README.md benchmark)",
-    "keras_cnn": "images/sec (whole node) Keras MNIST CNN (reference tensorflow2/) on the mxddp layers path",
+    "keras_cnn": "images/sec (whole node) Keras MNIST CNN (reference tensorflow2/, Adam)",
     "mlp": "images/sec (whole node) Chainer MNIST MLP (reference chainer/) on the mxddp layers path",
 }
 
@@ -57,6 +57,10 @@ def parse():
     ap.add_argument("--steps-per-graph", type=int, default=None, help="fused engine, graph mode 1: steps unrolled per graph")
     ap.add_argument("--force-collectives", action="store_true",
                     help="fused engine: issue the RCCL bucket all-reduces even at world size 1 (measures the DDP path)")
+    ap.add_argument("--buckets", default=None, choices=["ovl", "inl", "one", "co"],
+                    help="fused MNIST engine: pin the bucket strategy instead of autotuning it (ovl: fc bucket "
+                         "all-reduce on the side stream overlapping the conv backward; inl: both buckets in order; "
+                         "one: one all-reduce of the whole gradient)")
     ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "peer"],
                     help="fused engine, world size > 1: gradient all-reduce over RCCL's ring, the direct xGMI "
                          "peer all-reduce, or auto (validated + timed during the untimed warm-up)")
@@ -102,9 +106,25 @@ def main():
     comm = C.rccl_comm(force=a.force_collectives)
     B = a.batch
 
-    if a.model != "mnist_cnn" and a.impl == "fused":
+    if a.model not in ("mnist_cnn", "keras_cnn") and a.impl == "fused":
         a.impl = "layers"
-    if a.impl == "fused":
+    if a.impl == "fused" and a.model == "keras_cnn":
+        # native fused Keras-CNN step (csrc/keras_kernels.hip) with the reference's Keras Adam
+        from mxddp.keras_engine import FusedKerasTrainer
+
+        peer = None
+        if comm is None and inf.world_size > 1:
+            from mxddp.parallel import peer as P
+
+            peer = P.peer_comm()
+            if peer is None:
+                raise SystemExit("bench.py: ranks share a GPU and the peer transport is unavailable")
+        tr = FusedKerasTrainer(batch=B, device=dev, comm=comm, seed=a.seed, use_graph=not a.no_graph,
+                               steps_per_graph=a.steps_per_graph, peer=peer, force_collectives=a.force_collectives)
+        run = tr.step
+        if os.environ.get("MXDDP_WARM_GRAPHS", "1") == "1":
+            tr.warm_graphs()
+    elif a.impl == "fused":
         from mxddp.engine import FusedMnistTrainer
 
         peer = None
@@ -121,6 +141,9 @@ def main():
                                use_graph=not a.no_graph, graph_mode=a.graph_mode, steps_per_graph=a.steps_per_graph,
                                force_collectives=a.force_collectives, transport=a.transport, peer=peer)
         run = tr.step
+        if a.buckets is not None:
+            tr._set_buckets(a.buckets)
+            a.no_autotune = True
         if a.graph_mode is None and not a.no_autotune and tr.eng.reducer_active:
             tr.step(1)
             tr.autotune()  # untimed: a few real steps per candidate strategy, before the warm-up
@@ -172,16 +195,33 @@ def main():
             "config": {"model": a.model, "global_batch": B * a.gpus, "per_rank_batch": B, "seq_len": None,
                        "image": "x".join(map(str, spec.input_shape)), "parallelism": f"dp{a.gpus}", "impl": a.impl,
                        # how the timed steps were actually launched (autotune may pick eager mode 0)
-                       "graph": (a.impl == "fused" and tr.eng.graph_mode != 0) or getattr(a, "layers_graph", False),
-                       **({"graph_mode": tr.eng.graph_mode, "overlap": tr.eng.overlap, "merged_bucket": tr.eng.merged,
-                           "transport": tr.active_transport, "force_collectives": a.force_collectives, "autotune": tr.tuned}
-                          if a.impl == "fused" else {})},
+                       "graph": _fused_graph(a, tr) or getattr(a, "layers_graph", False),
+                       **_fused_config(a, tr)},
             **extra,
         }
         if C.shared_devices():
             out["shared_gpu_rehearsal"] = True  # several ranks on one GPU: not a scaling number
         print(json.dumps(out), flush=True)
     C.shutdown()
+
+
+def _fused_graph(a, tr) -> bool:
+    if a.impl != "fused":
+        return False
+    if a.model == "keras_cnn":
+        return bool(tr.eng.captured)
+    return tr.eng.graph_mode != 0
+
+
+def _fused_config(a, tr) -> dict:
+    if a.impl != "fused":
+        return {}
+    if a.model == "keras_cnn":
+        return {"optimizer": "adam (Keras eps-hat, lr 1e-3)",
+                "transport": ("peer" if tr.eng.peer_active else "rccl") if tr.eng.reducer_active else "none"}
+    return {"graph_mode": tr.eng.graph_mode, "overlap": tr.eng.overlap, "merged_bucket": tr.eng.merged,
+            "coscheduled_exchange": tr.eng.coscheduled,
+            "transport": tr.active_transport, "force_collectives": a.force_collectives, "autotune": tr.tuned}
 
 
 def _replica(a):
@@ -199,7 +239,7 @@ def _replica(a):
     devices = [torch.device("cuda", i) for i in range(a.gpus)]
     spec = get_spec(a.model)
     torch.manual_seed(a.seed)
-    if a.model == "mnist_cnn" and a.dtype == "fp32" and not a.no_graph:
+    if a.model in ("mnist_cnn", "keras_cnn") and a.dtype == "fp32" and not a.no_graph:
         return _replica_fused(a, devices, spec)
 
     def make_opt(flat):
@@ -254,9 +294,14 @@ def _replica_fused(a, devices, spec):
     every replica's step one hipGraph launch): MirroredStrategy / DataParallel semantics."""
     import torch
 
-    from mxddp.parallel.replica import FusedMnistReplicas
+    if a.model == "keras_cnn":
+        from mxddp.keras_engine import FusedKerasReplicas
 
-    rep = FusedMnistReplicas(devices, batch=a.batch, lr=a.lr, seed=a.seed, steps_per_graph=a.steps_per_graph)
+        rep = FusedKerasReplicas(devices, batch=a.batch, seed=a.seed, steps_per_graph=a.steps_per_graph)
+    else:
+        from mxddp.parallel.replica import FusedMnistReplicas
+
+        rep = FusedMnistReplicas(devices, batch=a.batch, lr=a.lr, seed=a.seed, steps_per_graph=a.steps_per_graph)
     rep.step(a.warmup)
     rep.synchronize()
     t0 = time.perf_counter()

@@ -439,6 +439,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_overlap", &MnistEngine::set_overlap)
       .def("set_merged", &MnistEngine::set_merged)
       .def_property_readonly("merged", &MnistEngine::merged)
+      .def("set_coscheduled", &MnistEngine::set_coscheduled)
+      .def_property_readonly("coscheduled", &MnistEngine::coscheduled)
       .def("set_peer", &MnistEngine::set_peer, py::arg("peer").none(true), py::keep_alive<1, 2>())
       .def("set_comm", &MnistEngine::set_comm, py::arg("comm").none(true), py::keep_alive<1, 2>())
       .def("set_bucket_padding", &MnistEngine::set_bucket_padding)

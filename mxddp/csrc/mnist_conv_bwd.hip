@@ -12,6 +12,7 @@
 #include <string>
 
 #include "mnist_common.h"
+#include "peer_device.h"
 
 namespace mx {
 namespace mnist {
@@ -747,19 +748,30 @@ __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc,
 // (576 + 704 blocks over 256 CUs at 3 per CU), so one kernel's prologue/epilogue latency and
 // the 2-vs-3-blocks-per-CU imbalance of each kernel alone are covered by the other's MFMA work.
 // 9B is a multiple of 8, so the F7 part keeps its XCD-aware block mapping.
+//
+// Co-scheduled gradient exchange (f.co_blocks > 0): the first co_blocks blocks run the two-shot
+// peer all-reduce of the fc bucket (complete since F5) instead -- dispatched first, they wait on
+// the peers' matching blocks while the remaining blocks do the conv backward, so the 4.7 MB
+// exchange overlaps it inside ONE launch (no side stream, no cross-queue fence).  co_blocks is
+// a multiple of 8, so the conv part keeps its XCD-aware block mapping.
 template <bool kWino, int kF6WSplit = 1, bool kA1 = false>
 __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scratch sc) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  if ((int)blockIdx.x < f.co_blocks) {
+    peer_two_shot_f32_block(f.co_args, f.co_part, blockIdx.x);
+    return;
+  }
+  const int bid = (int)blockIdx.x - f.co_blocks;
   const int n6 = (kWino ? 2 * kF6WSplit : 9) * f.B;
-  if ((int)blockIdx.x < n6) {
+  if (bid < n6) {
     if (kWino)
-      f6w_body<kF6WSplit, kA1>(f, sc, sm, blockIdx.x, n6);
+      f6w_body<kF6WSplit, kA1>(f, sc, sm, bid, n6);
     else
-      f6_body(f, sc, sm, blockIdx.x, n6);
+      f6_body(f, sc, sm, bid, n6);
   } else if (kWino) {
-    f7w_body(f, sc, sm, blockIdx.x - n6, kF7WChunks * f.B);
+    f7w_body(f, sc, sm, bid - n6, kF7WChunks * f.B);
   } else {
-    f7_body(f, sc, sm, blockIdx.x - n6, 11 * f.B);
+    f7_body(f, sc, sm, bid - n6, 11 * f.B);
   }
 }
 
@@ -843,7 +855,7 @@ static int f6w_split() {
 template <int kSplit>
 static void launch_f67_wino(const MnistFused& f, const Scratch& sc, hipStream_t st) {
   constexpr size_t lds = kF6WLds > kF7WLds ? kF6WLds : kF7WLds;
-  const dim3 grid(2 * kSplit * f.B + kF7WChunks * f.B);
+  const dim3 grid(f.co_blocks + 2 * kSplit * f.B + kF7WChunks * f.B);
   if (kSplit == 1 && f.a1_pub)
     MX_LAUNCH((f67_conv2_bwd_kernel<true, 1, true>), grid, dim3(256), lds, st, f, sc);
   else
@@ -870,7 +882,7 @@ void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_
     }
   } else {
     constexpr size_t lds = kF6Lds > kF7Lds ? kF6Lds : kF7Lds;
-    MX_LAUNCH(f67_conv2_bwd_kernel<false>, dim3(9 * f.B + 11 * f.B), dim3(256), lds, st, f, sc);
+    MX_LAUNCH(f67_conv2_bwd_kernel<false>, dim3(f.co_blocks + 9 * f.B + 11 * f.B), dim3(256), lds, st, f, sc);
   }
   if (!finalize_in_sgd) MX_LAUNCH(f8_finalize_kernel, dim3(kF8Wacc + kF8G1 + 8), dim3(256), 0, st, f, sc);
   MX_HIP_CHECK(hipGetLastError());

@@ -86,6 +86,10 @@ MnistEngine::MnistEngine(int batch, uintptr_t params, uintptr_t grads, uintptr_t
       comm_, reinterpret_cast<uintptr_t>(g_), DType::kF32, std::vector<Reducer::BucketSpec>{{0, MnistLayout::total}},
       std::vector<int>(8, 0), RedOp::kSum, false);
   merged_reducer_->set_overlap(false);  // issued at the end of the backward: nothing to overlap
+  co_reducer_ = std::make_unique<Reducer>(
+      comm_, reinterpret_cast<uintptr_t>(g_), DType::kF32, std::vector<Reducer::BucketSpec>{{0, MnistLayout::fw1}},
+      std::vector<int>(8, 0), RedOp::kSum, false);
+  co_reducer_->set_overlap(false);
   repack();
   MX_HIP_CHECK(hipStreamSynchronize(s_));
 }
@@ -98,6 +102,21 @@ void MnistEngine::set_comm(Comm* c) {
   comm_ = c;
   reducer_->set_comm(c);
   merged_reducer_->set_comm(c);
+  co_reducer_->set_comm(c);
+}
+
+bool MnistEngine::set_coscheduled(bool on) {
+  if (on) {
+    PeerComm* pc = reducer_->peer();
+    if (!pc || variant_ != 1 ||
+        !pc->coschedule_args(g_ + MnistLayout::fw1, MnistLayout::total - MnistLayout::fw1, RedOp::kSum, &co_args_,
+                             &co_part_) ||
+        pc->blocks() % 8 != 0)
+      on = false;
+  }
+  if (on != coscheduled_) uncapture();
+  coscheduled_ = on;
+  return on;
 }
 
 void MnistEngine::repack() {
@@ -127,6 +146,7 @@ MnistEngine::~MnistEngine() {
   uncapture();
   reducer_.reset();
   merged_reducer_.reset();
+  co_reducer_.reset();
   if (s_) hipStreamDestroy(s_);
 }
 
@@ -172,6 +192,11 @@ MnistFused MnistEngine::fused_args() const {
   f.lr = lr_;
   f.sgd_mom = momentum_;
   f.sgd_wd = wd_;
+  if (co_active()) {
+    f.co_blocks = reducer_->peer()->blocks();
+    f.co_args = co_args_;
+    f.co_part = co_part_;
+  }
   return f;
 }
 
@@ -220,6 +245,16 @@ void MnistEngine::segment(int k) {
 }
 
 void MnistEngine::launch_step() {
+  if (co_active()) {
+    Reducer& rc = *co_reducer_;
+    rc.prepare();
+    segment(0);                   // ... F5: the fc bucket is complete
+    segment(1);                   // F67 (its first blocks all-reduce the fc bucket) + F8
+    rc.mark_bucket_ready(0, s_);  // the 75 KB conv bucket
+    rc.finalize(s_);
+    segment(2);
+    return;
+  }
   Reducer& r = red();
   r.prepare();
   segment(0);
@@ -255,6 +290,7 @@ void MnistEngine::capture(int mode, int steps_per_graph) {
   // default: one graph at world size 1; eager launches (mode 0) when real collectives run --
   // the caller (FusedMnistTrainer.autotune) may pick a graph mode after timing the options.
   if (mode < 0) mode = multi ? 0 : 1;
+  if (mode == 2 && co_active()) mode = 1;  // the fc exchange lives inside segment 1's launch
   MX_HIP_CHECK(hipStreamSynchronize(s_));
   graph_mode_ = mode;
   if (mode == 1) {  // whole step(s), RCCL collectives included (one launch per group of steps)

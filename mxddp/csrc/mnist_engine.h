@@ -62,6 +62,7 @@ class MnistEngine {
     if (on != reducer_->forced()) uncapture();
     reducer_->set_force_collectives(on);
     merged_reducer_->set_force_collectives(on);
+    co_reducer_->set_force_collectives(on);
   }
   void set_overlap(bool on) { reducer_->set_overlap(on); }  // see Reducer::set_overlap
   // gradient transport: nullptr = RCCL, else the direct xGMI peer all-reduce (peer.h); drops
@@ -70,6 +71,8 @@ class MnistEngine {
     if (p != reducer_->peer()) uncapture();
     reducer_->set_peer(p);
     merged_reducer_->set_peer(p);
+    co_reducer_->set_peer(p);
+    if (coscheduled_) set_coscheduled(true);  // re-derive the exchange arguments (or drop it)
   }
   // RCCL communicator (same rank / world size; one of the configured variants of
   // parallel/comm.py); drops captured graphs
@@ -88,6 +91,11 @@ class MnistEngine {
     merged_ = on;
   }
   bool merged() const { return merged_; }
+  // co-scheduled = true (peer transport only): the fc bucket's two-shot exchange runs in the
+  // first blocks of the conv-backward launch itself (overlapping it without a second stream);
+  // the conv bucket follows after F8.  Drops captured graphs.  False if the transport cannot.
+  bool set_coscheduled(bool on);
+  bool coscheduled() const { return co_active(); }
   bool peer_active() const { return reducer_->peer() != nullptr; }
   // data-parallel degree: the RCCL communicator's, else the peer transport's (a peer-only job,
   // e.g. several ranks sharing one GPU in tests)
@@ -132,6 +140,13 @@ class MnistEngine {
   float *x_, *a1_, *c2_, *pool_, *h_, *logits_, *dlogits_, *dh_, *dp_, *dc2_, *da1_, *tmpl_, *scratch_;
   int32_t *y_, *idx_, *counter_;
   float *lr_, *metrics_;
+  bool co_active() const {
+    return coscheduled_ && variant_ == 1 && reducer_->peer() != nullptr && reducer_->active();
+  }
+  bool coscheduled_ = false;
+  PeerArgs co_args_{};
+  PeerPartition co_part_{};
+  std::unique_ptr<Reducer> co_reducer_;  // the conv bucket alone (the fc bucket rides F67)
   Comm* comm_;
   std::unique_ptr<Reducer> reducer_;         // buckets [fc1.w .. fc2.b], [conv1.w .. conv2.b]
   std::unique_ptr<Reducer> merged_reducer_;  // one bucket: the whole flat gradient

@@ -4,6 +4,8 @@
 
 #include <cstdint>
 
+#include "peer.h"
+
 namespace mx {
 
 struct MnistFused {
@@ -33,6 +35,11 @@ struct MnistFused {
   float* mom;            // flat momentum buffer
   const float* lr;       // device learning rate
   float sgd_mom, sgd_wd;
+  // co-scheduled fc-bucket exchange: blocks [0, co_blocks) of the conv-backward launch run the
+  // two-shot peer all-reduce of the fc gradients (ready since F5), the rest the conv work
+  int co_blocks;
+  PeerArgs co_args;
+  PeerPartition co_part;
 };
 bool mnist_a1_publish();  // default on; MXDDP_MNIST_A1=recompute turns it off
 bool mnist_f5_sgd();      // default on; MXDDP_F5_SGD=0 keeps the fc1 update in the SGD launch

@@ -142,6 +142,28 @@ void PeerComm::set_blocks(int b) {
 int PeerComm::error() const { return __atomic_load_n(err_host_, __ATOMIC_ACQUIRE); }
 void PeerComm::reset_error() { __atomic_store_n(err_host_, 0, __ATOMIC_RELEASE); }
 
+bool PeerComm::coschedule_args(void* data, size_t count, RedOp op, PeerArgs* a, PeerPartition* part) const {
+  if (ws_ == 1 || count == 0 || !opened_ || count * 4 > cap_) return false;
+  if (reinterpret_cast<uintptr_t>(data) % 16) return false;
+  *a = PeerArgs{};
+  for (int p = 0; p < ws_; ++p) {
+    a->xbuf[p] = peer_x_[p];
+    a->sig[p] = peer_sig_[p];
+  }
+  a->epoch = epoch_;
+  a->err = err_dev_;
+  a->slot_bytes = static_cast<long long>(slot_bytes_);
+  a->timeout = timeout_;
+  a->rank = rank_;
+  a->ws = ws_;
+  a->fence = fence_;
+  a->scale = op == RedOp::kAvg ? 1.f / static_cast<float>(ws_) : 1.f;
+  a->data = data;
+  a->count = static_cast<long long>(count);
+  *part = PeerPartition::make(a->count, ws_, blocks_, 4);
+  return part->chunk * 4 <= a->slot_bytes;
+}
+
 void PeerComm::all_reduce(void* data, size_t count, DType t, hipStream_t st, RedOp op) {
   if (ws_ == 1 || count == 0) return;
   MX_CHECK(op == RedOp::kSum || op == RedOp::kAvg, "peer transport: sum or average only");

@@ -79,6 +79,10 @@ class PeerComm {
   // in-place all-reduce of `count` elements (f32 or bf16) on `st`: sum, or average
   // (RedOp::kAvg, the sum times 1/world_size); graph-capturable
   void all_reduce(void* data, size_t count, DType t, hipStream_t st, RedOp op = RedOp::kSum);
+  // kernel arguments of ONE two-shot f32 exchange of `count` elements run by blocks() blocks of
+  // another kernel (peer_device.h: peer_two_shot_f32_block); false if it does not fit one
+  // launch (bucket above the exchange capacity) or world size 1
+  bool coschedule_args(void* data, size_t count, RedOp op, PeerArgs* a, PeerPartition* part) const;
   int error() const;                                 // 0 = ok; else 1 + (peer that timed out)
   void reset_error();
   void set_blocks(int b);

@@ -17,14 +17,13 @@
 // order) before it released p's block b into call k+1 (flag set 1 of call k).
 #include "common.h"
 #include "peer.h"
+#include "peer_device.h"
 
 namespace mx {
 
 namespace {
 
-constexpr int kThreads = 256;
-
-__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+constexpr int kThreads = kPeerThreads;
 
 // 16-byte register vector (a native vector type: HIP's uint4 is a union-based struct that
 // keeps arrays of it out of registers)
@@ -88,46 +87,6 @@ template <class T>
 __device__ __forceinline__ void st_elem(T* p, float f) {
   if constexpr (sizeof(T) == 4) *reinterpret_cast<float*>(p) = f;
   else *reinterpret_cast<uint16_t*>(p) = static_cast<uint16_t>(f_to_bf16(f));
-}
-
-__device__ __forceinline__ uint32_t* flag_at(uint32_t* sig, int set, int b, int p) {
-  return sig + ((size_t)set * kPeerMaxBlocks + b) * kPeerMaxRanks + p;
-}
-
-// lanes 0..ws-1 (except `rank`) of wave 0 each wait for one peer's flag; bounded.
-__device__ __forceinline__ void wait_peers(const PeerArgs& a, int set, int b, uint32_t ep) {
-  const int t = threadIdx.x;
-  if (t < a.ws && t != a.rank) {
-    uint32_t* f = flag_at(a.sig[a.rank], set, b, t);
-    const long long t0 = wall_clock64();
-    while (static_cast<int32_t>(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - ep) < 0) {
-      __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() - t0 > a.timeout) {
-        __hip_atomic_store(a.err, 1 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-    }
-  }
-  if ((a.fence & 2) && t < kWave) {  // acquire (only needed when the exchange memory is cached)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    vm_drain();
-  }
-  __syncthreads();
-}
-
-// every wave's stores drained, then one lane per peer publishes `ep` in that peer's flag
-__device__ __forceinline__ void signal_peers(const PeerArgs& a, int set, int b, uint32_t ep) {
-  vm_drain();
-  __syncthreads();
-  const int t = threadIdx.x;
-  if (t < kWave) {
-    if (a.fence & 1) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      vm_drain();
-    }
-    if (t < a.ws && t != a.rank)
-      __hip_atomic_store(flag_at(a.sig[t], set, b, a.rank), ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
 }
 
 template <class T, int W>

@@ -173,9 +173,10 @@ class FusedMnistTrainer:
         snap = self.snapshot() if restore else None
         cands = []
         for tr in transports:
-            cands += [(tr, 0, "ovl"), (tr, 0, "inl"), (tr, 0, "one")]
+            strats = ["ovl", "inl", "one"] + (["co"] if tr == "peer" else [])
+            cands += [(tr, 0, st) for st in strats]
             if self.use_graph and (include_graphs or tr == "peer"):
-                cands += [(tr, 1, "ovl"), (tr, 1, "inl"), (tr, 1, "one")]
+                cands += [(tr, 1, st) for st in strats]
         results = {}
         for tr, mode, strat in cands:
             self.eng.uncapture()
@@ -262,9 +263,14 @@ class FusedMnistTrainer:
 
     def _set_buckets(self, strat: str):
         """ovl: fc bucket overlapped on the side stream; inl: both buckets in order; one: a
-        single all-reduce of the whole gradient after the conv backward."""
+        single all-reduce of the whole gradient after the conv backward; co (peer transport): the
+        fc bucket's exchange co-scheduled in the first blocks of the conv-backward launch."""
+        co = strat == "co" and self.eng.set_coscheduled(True)
+        if not co:
+            self.eng.set_coscheduled(False)
         self.eng.set_merged(strat == "one")
         self.eng.set_overlap(strat == "ovl")
+        self.bucket_strategy = "co" if co else ("inl" if strat == "co" else strat)
 
     def _check_peer(self):
         if self.peer is not None and self.peer.error():

@@ -191,8 +191,9 @@ def main(argv=None) -> int:
         raise SystemExit("--mode single cannot run with world_size > 1")
     engine = args.engine
     if engine == "auto":
-        engine = "fused" if (args.model == "mnist_cnn" and use_gpu and opt_name == "sgd" and mode != "replica"
-                             and bs % 16 == 0 and 16 <= bs <= 128 and args.dtype == "fp32"
+        fusable = ((args.model == "mnist_cnn" and opt_name == "sgd" and bs % 16 == 0 and 16 <= bs <= 128) or
+                   (args.model == "keras_cnn" and opt_name == "adam" and bs % 8 == 0 and bs <= 1024))
+        engine = "fused" if (fusable and use_gpu and mode != "replica" and args.dtype == "fp32"
                              and not (backend == "gloo" and inf.world_size > 1)) else "layers"
     if engine == "fused" and use_gpu and backend == "gloo" and inf.world_size > 1:
         raise SystemExit("--engine fused all-reduces over RCCL / the xGMI peer transport; with --dist-backend gloo "
@@ -532,9 +533,10 @@ def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
         devices = [torch.device("cuda", i) for i in range(n)]
     else:
         devices = [torch.device("cpu")]
-    if (spec.name == "mnist_cnn" and opt_name == "sgd" and devices[0].type == "cuda" and args.dtype == "fp32"
-            and args.engine != "layers" and bs % len(devices) == 0 and (bs // len(devices)) % 16 == 0
-            and 16 <= bs // len(devices) <= 128):
+    per = bs // len(devices) if bs % len(devices) == 0 else 0
+    if devices[0].type == "cuda" and args.dtype == "fp32" and args.engine != "layers" and per and (
+            (spec.name == "mnist_cnn" and opt_name == "sgd" and per % 16 == 0 and 16 <= per <= 128) or
+            (spec.name == "keras_cnn" and opt_name == "adam" and per % 8 == 0 and wd == 0.0)):
         return _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw)
     torch.manual_seed(args.seed)
     model = build_model(spec.name, **_model_kwargs(args, spec))
@@ -622,8 +624,9 @@ def _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw):
     from .models import build_model
     from .parallel.replica import FusedMnistReplicas
 
+    keras = spec.name == "keras_cnn"
     torch.manual_seed(args.seed)
-    init = build_model("mnist_cnn")
+    init = build_model(spec.name)
     st, start_epoch = {}, 1
     if args.resume:
         from .utils.checkpoint import load_training_state
@@ -631,20 +634,29 @@ def _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw):
         st = load_training_state(args.resume)
         init.load_state_dict(st["model"])
         start_epoch = st["epoch"] + 1
-    rep = FusedMnistReplicas(devices, batch=bs // len(devices), lr=lr, momentum=mom, weight_decay=wd, seed=args.seed,
-                             init_model=init, use_graph=not args.no_graph)
+    if keras:
+        from .keras_engine import FusedKerasReplicas
+
+        rep = FusedKerasReplicas(devices, batch=bs // len(devices), lr=lr, seed=args.seed, init_model=init,
+                                 use_graph=not args.no_graph)
+    else:
+        rep = FusedMnistReplicas(devices, batch=bs // len(devices), lr=lr, momentum=mom, weight_decay=wd,
+                                 seed=args.seed, init_model=init, use_graph=not args.no_graph)
     step = 0
     if st:
         ctrs = st.get("extra", {}).get("data_counters")
         for i, t in enumerate(rep.trainers):
             if "momentum" in st.get("optimizer", {}):
                 t.mom.copy_(st["optimizer"]["momentum"].to(t.device))
+            if "m" in st.get("optimizer", {}):
+                t.load_optimizer_state(st["optimizer"])
             if ctrs is not None and i < len(ctrs):
                 t.load_data_state(ctrs[i])
         step = int(st.get("step", 0))
     loader, kind = build_loader("mnist", args.data, args.dataset_dir, bs, devices[0], 1, 0, args.seed,
                                 spec.input_shape, 10, train=True, steps=args.steps_per_epoch)
-    print(f"==> replica mode (fused engine) on {len(devices)} device(s), global batch {bs}, data {kind}", flush=True)
+    print(f"==> replica mode (fused {spec.name} engine) on {len(devices)} device(s), global batch {bs}, data {kind}",
+          flush=True)
     rep_ = _Reporter(args, inf)
     base_lr = lr
     for epoch in range(start_epoch, args.epochs + 1):
@@ -686,7 +698,8 @@ def _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw):
         val = _maybe_eval(args, inf, spec, model, bs, mw, epoch=epoch)
         rep_.epoch_end(epoch, step, loss_tot / max(1, bi * bs), corr_tot / max(1, bi * bs), val, model)
         t0_ = rep.trainers[0]
-        _epoch_saves(args, inf, epoch, step, rep.state_dict(), {"momentum": t0_.mom.cpu(), "lr": t0_._lr_host},
+        opt_sd = t0_.optimizer_state() if keras else {"momentum": t0_.mom.cpu(), "lr": t0_._lr_host}
+        _epoch_saves(args, inf, epoch, step, rep.state_dict(), opt_sd,
                      {"base_lr": base_lr}, None, data_counters=[t.data_state() for t in rep.trainers])
         if args.max_steps and step >= args.max_steps:
             break
@@ -700,15 +713,17 @@ def _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw):
 
 # ====================================================================================== fused
 def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
+    """The native fused engines: MNIST CNN + SGD (engine.py) and the reference's Keras CNN + Keras
+    Adam (keras_engine.py); one hipGraph launch per step (or group of steps)."""
     from .data import build_loader
-    from .engine import FusedMnistTrainer
     from .models import build_model
     from .parallel import comm as C
     from .utils.checkpoint import load_training_state, save_training_state
 
     dev = inf.device
+    keras = spec.name == "keras_cnn"
     torch.manual_seed(args.seed)
-    init = build_model("mnist_cnn")
+    init = build_model(spec.name)
     start_epoch = 1
     st = {}
     if args.resume:
@@ -723,11 +738,21 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
         peer = _peer.peer_comm()
         if peer is None:
             raise SystemExit("ranks share a GPU and the peer transport is unavailable")
-    tr = FusedMnistTrainer(batch=bs, device=dev, comm=comm, seed=args.seed, lr=lr, momentum=mom,
-                           weight_decay=wd, use_graph=not args.no_graph, init_model=init, transport=args.transport,
-                           peer=peer)
-    if args.resume and "momentum" in st.get("optimizer", {}):
-        tr.mom.copy_(st["optimizer"]["momentum"].to(dev))
+    if keras:
+        from .keras_engine import FusedKerasTrainer
+
+        tr = FusedKerasTrainer(batch=bs, device=dev, comm=comm, seed=args.seed, lr=lr, eps=1e-7, weight_decay=wd,
+                               eps_hat=True, use_graph=not args.no_graph, init_model=init, peer=peer)
+        if args.resume and "m" in st.get("optimizer", {}):
+            tr.load_optimizer_state(st["optimizer"])
+    else:
+        from .engine import FusedMnistTrainer
+
+        tr = FusedMnistTrainer(batch=bs, device=dev, comm=comm, seed=args.seed, lr=lr, momentum=mom,
+                               weight_decay=wd, use_graph=not args.no_graph, init_model=init, transport=args.transport,
+                               peer=peer)
+        if args.resume and "momentum" in st.get("optimizer", {}):
+            tr.mom.copy_(st["optimizer"]["momentum"].to(dev))
     loader, kind = build_loader("mnist", args.data, args.dataset_dir, bs, dev, inf.world_size, inf.rank, args.seed,
                                 spec.input_shape, 10, train=True, steps=args.steps_per_epoch)
     synthetic = kind == "synthetic"
@@ -740,7 +765,8 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
             tr.load_data_state(ex["data_counter"])
         step = int(st.get("step", 0))
     if inf.is_main:
-        print("From Rank: {}, The number of parameters of model is {}".format(inf.rank, 1199882), flush=True)
+        print("From Rank: {}, The number of parameters of model is {}".format(
+            inf.rank, sum(p.numel() for p in init.parameters())), flush=True)
         print(f"==> data: {kind}, {len(loader)} batches/epoch, fused hipGraph step={'off' if args.no_graph else 'on'}",
               flush=True)
     rep = _Reporter(args, inf)
@@ -754,7 +780,7 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
             print(model_summary(probe, spec.input_shape, spec.name), flush=True)
         rep.first_loss(_ops.cross_entropy(probe(torch.zeros(2, 1, 28, 28)), torch.zeros(2, dtype=torch.long)), probe)
     base_lr = lr
-    if tr.eng.reducer_active and synthetic and not args.no_graph:
+    if not keras and tr.eng.reducer_active and synthetic and not args.no_graph:
         # pick transport / overlap / graph mode on this machine by timing real steps; they are
         # scratch: weights, momentum, data-stream position and metrics are restored afterwards,
         # so the trained model and --max-steps still match epochs x batches
@@ -820,8 +846,8 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
             rep.epoch_end(epoch, step, loss_tot / seen, corr_tot / seen, None,
                           tr.to_module() if rep.tb is not None else None)
         if args.save_every and epoch % args.save_every == 0:
-            save_training_state(args.train_dir, inf.rank, tr.state_dict(), {"momentum": tr.mom.cpu(), "lr": tr._lr_host},
-                                {"base_lr": base_lr}, epoch, step,
+            opt_sd = tr.optimizer_state() if keras else {"momentum": tr.mom.cpu(), "lr": tr._lr_host}
+            save_training_state(args.train_dir, inf.rank, tr.state_dict(), opt_sd, {"base_lr": base_lr}, epoch, step,
                                 extra={"data_counter": tr.data_state(), "sampler_epoch": epoch})
         if args.epoch_checkpoints and inf.is_main:
             from .utils.checkpoint import save_epoch_weights

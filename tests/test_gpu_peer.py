@@ -178,7 +178,7 @@ def _worker(rank, ws, port, mode, q):
                 torch.cuda.synchronize()
                 if pc.error() or not torch.equal(buf.cpu(), _expected(ws, count, rep, torch.float32)):
                     bad.append(("graph", rep, pc.error()))
-        elif mode in ("trainer", "trainer_graph"):
+        elif mode in ("trainer", "trainer_graph", "trainer_co", "trainer_co_graph"):
             # fused MNIST DDP step over the peer transport == one process on the global batch
             from mxddp.engine import FusedMnistTrainer
             from mxddp.models import MnistCNN
@@ -190,7 +190,11 @@ def _worker(rank, ws, port, mode, q):
             batches = [(torch.rand(ws * b, 1, 28, 28, generator=g), torch.randint(0, 10, (ws * b,), generator=g))
                        for _ in range(steps)]
             tr = FusedMnistTrainer(batch=b, device=0, comm=None, peer=pc, lr=0.05, init_model=init,
-                                   use_graph=mode == "trainer_graph", graph_mode=1)
+                                   use_graph=mode.endswith("graph"), graph_mode=1)
+            if "co" in mode:  # fc-bucket exchange co-scheduled inside the conv-backward launch
+                tr._set_buckets("co")
+                if not tr.eng.coscheduled:
+                    bad.append("co-scheduling refused")
             for x, y in batches:
                 tr.set_batch(x[rank * b:(rank + 1) * b].cuda(), y[rank * b:(rank + 1) * b].cuda())
                 tr.step(1)
@@ -269,9 +273,9 @@ def test_peer_all_reduce_graph_replay(cuda):
     _run(4, "graph")
 
 
-@pytest.mark.parametrize("mode", ["trainer", "trainer_graph"])
+@pytest.mark.parametrize("mode", ["trainer", "trainer_graph", "trainer_co", "trainer_co_graph"])
 def test_fused_trainer_peer_ddp_matches_global_batch(cuda, mode):
-    _run(2 if mode == "trainer" else 4, mode)
+    _run(4 if mode.endswith("graph") else 2, mode)
 
 
 def test_ddp_layers_peer_transport_matches_global_batch(cuda):
