@@ -30,6 +30,8 @@
 // (tensorflow2/mnist_mirror_strategy.py:12,68-79).
 #include "common.h"
 #include "keras_kernels.h"
+
+#include <cstdlib>
 #include "rng.h"
 
 namespace mx {
@@ -41,6 +43,13 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// element k of a float4 register array (k compile-time after unrolling: no address taken, so
+// the array stays in registers)
+__device__ __forceinline__ float f4_at(const float4* a, int k) {
+  const float4 v = a[k >> 2];
+  return (k & 3) == 0 ? v.x : (k & 3) == 1 ? v.y : (k & 3) == 2 ? v.z : v.w;
+}
+
 constexpr int kP1 = 169;          // 13 x 13 pooled conv1 positions
 constexpr int kP1Img = 32 * kP1;  // 5408 floats per image
 constexpr int kP2Img = 64 * 25;   // 1600
@@ -48,12 +57,12 @@ constexpr int kPl2 = 64 * 288;    // conv2 weights
 constexpr int kPl3 = 64 * 576;    // conv3 / fc1 weights
 
 // ------------------------------------------------------------------------------------------
-// KF1: block = (image n, conv2 output channels 16*c4 .. 16*c4+15).
+// KF1: block = (image n, conv2 output channels 16*c4 .. 16*c4+15), 8 waves.
 // conv2 GEMM: M = the 100 conv2 outputs that feed pool2 (rows / cols 0..9; MaxPool2D drops the
 // 11th), window-major: m = 4*window + 2*dy + dx (7 M-tiles, rows 100..111 dummy); N = 16 co;
 // K = 288 ordered k = r*32 + ci so the im2col LDS offset = per-lane base + compile-time
 // immediate.  The 72 B fragments (pre-packed w2f) sit in registers.
-__global__ __launch_bounds__(256) void kf1_kernel(KerasFused f) {
+__global__ __launch_bounds__(512) void kf1_kernel(KerasFused f) {
   const int n = blockIdx.x >> 2, c4 = blockIdx.x & 3;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   __shared__ float xs[784];
@@ -76,11 +85,11 @@ __global__ __launch_bounds__(256) void kf1_kernel(KerasFused f) {
   } else if (tid < 196) {
     *reinterpret_cast<float4*>(xs + 4 * tid) = *reinterpret_cast<const float4*>(f.x + (size_t)n * 784 + 4 * tid);
   }
-  for (int i = tid; i < 320; i += 256) w1s[i] = f.p[L::w1 + i];  // w1 [32][9] then b1 [32]
+  for (int i = tid; i < 320; i += 512) w1s[i] = f.p[L::w1 + i];  // w1 [32][9] then b1 [32]
   __syncthreads();
 
   // conv1 + ReLU + 2x2 max-pool (+ argmax): 32 x 169 pooled outputs, one 4x4 input patch each
-  for (int o = tid; o < kP1Img; o += 256) {
+  for (int o = tid; o < kP1Img; o += 512) {
     const int ci = o / kP1, pp = o - ci * kP1, py = pp / 13, px = pp - py * 13;
     const float* xp = xs + (2 * py) * 28 + 2 * px;
     float pt[16];
@@ -122,7 +131,7 @@ __global__ __launch_bounds__(256) void kf1_kernel(KerasFused f) {
   for (int s = 0; s < 72; ++s) breg[s] = wf[s * 64 + lane];
   const int co = 16 * c4 + (lane & 15);
   const float bias2 = f.p[L::b2 + co];
-  for (int mt = w; mt < 7; mt += 4) {
+  for (int mt = w; mt < 7; mt += 8) {  // 7 M-tiles over 8 waves
     const int ml = lane & 15, win = 4 * mt + (ml >> 2);
     int base = 0;
     if (win < 25) {
@@ -154,8 +163,11 @@ __global__ __launch_bounds__(256) void kf1_kernel(KerasFused f) {
 }
 
 // ------------------------------------------------------------------------------------------
-// KF2: block = image.  Head forward + backward to the pooled conv2 output; VALU, LDS-resident.
-__global__ __launch_bounds__(256) void kf2_kernel(KerasFused f) {
+// KF2: block = image, 8 waves.  Head forward + backward to the pooled conv2 output; VALU,
+// LDS-resident.  The phases are a dependent chain, so each thread issues the global loads of its
+// weight slices ahead of use (conv3 + fc1 slices at entry, the fc1-transpose column during the
+// loss): the chain does not wait on L2 once per phase.
+__global__ __launch_bounds__(512) void kf2_kernel(KerasFused f) {
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   __shared__ float p2s[kP2Img];
   __shared__ float x3s[576];
@@ -163,69 +175,79 @@ __global__ __launch_bounds__(256) void kf2_kernel(KerasFused f) {
   __shared__ float hs[64];
   __shared__ float dh1s[64];
   __shared__ float dls[16];
-  for (int i = tid; i < kP2Img; i += 256) p2s[i] = f.p2[(size_t)n * kP2Img + i];
+  const int hi = tid >> 3, q = tid & 7;  // (output channel / feature, eighth of the reduction)
+  // conv3 slice w3[hi][8q .. 8q+7][9] and fc1 slice fw1[hi][72q .. 72q+71]: 18 float4 each
+  float4 wc[18], wf[18];
+  {
+    const float4* a = reinterpret_cast<const float4*>(f.p + L::w3 + ((size_t)hi * 64 + 8 * q) * 9);
+    const float4* b = reinterpret_cast<const float4*>(f.p + L::fw1 + (size_t)hi * 576 + 72 * q);
+#pragma unroll
+    for (int k = 0; k < 18; ++k) {
+      wc[k] = a[k];
+      wf[k] = b[k];
+    }
+  }
+  for (int i = tid; i < kP2Img; i += 512) p2s[i] = f.p2[(size_t)n * kP2Img + i];
   if (f.synth && n == 0 && tid == 0) *f.counter += 1;  // KF1 consumed this batch index
   __syncthreads();
 
-  // conv3 + bias + ReLU: thread (co = tid/4, ci quarter q) -> all 9 outputs of co over 16 ci
+  // conv3 + bias + ReLU: thread (co = hi, ci 8q..8q+7) -> all 9 outputs of co, xor-tree over q
   {
-    const int co = tid >> 2, q = tid & 3;
     float acc[9];
 #pragma unroll
     for (int pos = 0; pos < 9; ++pos) acc[pos] = 0.f;
-    const float* wp = f.p + L::w3 + ((size_t)co * 64 + 16 * q) * 9;
-    for (int c = 0; c < 16; ++c) {
-      const float* pc = p2s + (16 * q + c) * 25;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float* pc = p2s + (8 * q + c) * 25;
       float pt[25];
 #pragma unroll
       for (int k = 0; k < 25; ++k) pt[k] = pc[k];
-      float wr[9];
-#pragma unroll
-      for (int r = 0; r < 9; ++r) wr[r] = wp[c * 9 + r];
 #pragma unroll
       for (int pos = 0; pos < 9; ++pos)
 #pragma unroll
-        for (int r = 0; r < 9; ++r) acc[pos] += wr[r] * pt[(pos / 3 + r / 3) * 5 + pos % 3 + r % 3];
+        for (int r = 0; r < 9; ++r) acc[pos] += f4_at(wc, c * 9 + r) * pt[(pos / 3 + r / 3) * 5 + pos % 3 + r % 3];
     }
 #pragma unroll
-    for (int pos = 0; pos < 9; ++pos) {
-      acc[pos] += __shfl_xor(acc[pos], 1, 64);
-      acc[pos] += __shfl_xor(acc[pos], 2, 64);
-    }
+    for (int pos = 0; pos < 9; ++pos)
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) acc[pos] += __shfl_xor(acc[pos], o, 64);
     if (q == 0) {
-      const float b = f.p[L::b3 + co];
+      const float b = f.p[L::b3 + hi];
 #pragma unroll
-      for (int pos = 0; pos < 9; ++pos) x3s[co * 9 + pos] = fmaxf(acc[pos] + b, 0.f);
+      for (int pos = 0; pos < 9; ++pos) x3s[hi * 9 + pos] = fmaxf(acc[pos] + b, 0.f);
     }
   }
   __syncthreads();
-  for (int i = tid; i < 576; i += 256) f.x3[(size_t)n * 576 + i] = x3s[i];
 
-  // fc1 + bias + ReLU: thread (j = tid/4, quarter q of the 576 inputs)
+  for (int i = tid; i < 576; i += 512) f.x3[(size_t)n * 576 + i] = x3s[i];
+
+  // fc1 + bias + ReLU: thread (j = hi, inputs 72q .. 72q+71)
   {
-    const int j = tid >> 2, q = tid & 3;
-    const float4* wr = reinterpret_cast<const float4*>(f.p + L::fw1 + (size_t)j * 576 + 144 * q);
-    const float4* xr = reinterpret_cast<const float4*>(x3s + 144 * q);
+    const float4* xr = reinterpret_cast<const float4*>(x3s + 72 * q);
     float a = 0.f;
-#pragma unroll 4
-    for (int k = 0; k < 36; ++k) {
-      const float4 wv4 = wr[k], xv = xr[k];
-      a += wv4.x * xv.x + wv4.y * xv.y + wv4.z * xv.z + wv4.w * xv.w;
+#pragma unroll
+    for (int k = 0; k < 18; ++k) {
+      const float4 xv = xr[k];
+      a += wf[k].x * xv.x + wf[k].y * xv.y + wf[k].z * xv.z + wf[k].w * xv.w;
     }
-    a += __shfl_xor(a, 1, 64);
-    a += __shfl_xor(a, 2, 64);
-    if (q == 0) hs[j] = fmaxf(a + f.p[L::fb1 + j], 0.f);
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) a += __shfl_xor(a, o, 64);
+    if (q == 0) hs[hi] = fmaxf(a + f.p[L::fb1 + hi], 0.f);
   }
   __syncthreads();
+  // fc1-transpose column fw1[:, tid] for dx3 (issued now, used after the loss)
+  float wx[64];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) wx[j] = f.p[L::fw1 + (size_t)j * 576 + tid];
 
   // fc2 + softmax + cross entropy + accuracy + dlogits (wave 0)
   if (wv == 0) {
     float a = 0.f;
     if (lane < 40) {
-      const int c = lane >> 2, q = lane & 3;
-      const float* wr = f.p + L::fw2 + c * 64 + 16 * q;
+      const int c = lane >> 2, qq = lane & 3;
+      const float* wr = f.p + L::fw2 + c * 64 + 16 * qq;
 #pragma unroll
-      for (int jj = 0; jj < 16; ++jj) a += wr[jj] * hs[16 * q + jj];
+      for (int jj = 0; jj < 16; ++jj) a += wr[jj] * hs[16 * qq + jj];
     }
     a += __shfl_xor(a, 1, 64);
     a += __shfl_xor(a, 2, 64);
@@ -262,60 +284,66 @@ __global__ __launch_bounds__(256) void kf2_kernel(KerasFused f) {
     f.sv[(size_t)n * 256 + 128 + tid] = d;
   }
   __syncthreads();
-  // dx3 = (fw1^T dh1) * (x3 > 0)
-  for (int i = tid; i < 576; i += 256) {
-    const float* wc = f.p + L::fw1 + i;
+  // dx3 = (fw1^T dh1) * (x3 > 0): inputs tid (and 512 + tid for the first wave)
+  {
     float a0 = 0.f, a1 = 0.f;
-#pragma unroll 8
+#pragma unroll
     for (int j = 0; j < 64; j += 2) {
-      a0 += wc[(size_t)j * 576] * dh1s[j];
-      a1 += wc[(size_t)(j + 1) * 576] * dh1s[j + 1];
+      a0 += wx[j] * dh1s[j];
+      a1 += wx[j + 1] * dh1s[j + 1];
     }
-    const float d = x3s[i] > 0.f ? a0 + a1 : 0.f;
-    dx3s[i] = d;
-    f.dx3[(size_t)n * 576 + i] = d;
+    const float d = x3s[tid] > 0.f ? a0 + a1 : 0.f;
+    dx3s[tid] = d;
+    f.dx3[(size_t)n * 576 + tid] = d;
+    if (tid < 64) {
+      const int i2 = 512 + tid;
+      float b0 = 0.f;
+#pragma unroll 16
+      for (int j = 0; j < 64; ++j) b0 += f.p[L::fw1 + (size_t)j * 576 + i2] * dh1s[j];
+      const float d2 = x3s[i2] > 0.f ? b0 : 0.f;
+      dx3s[i2] = d2;
+      f.dx3[(size_t)n * 576 + i2] = d2;
+    }
   }
   __syncthreads();
   if (tid < 64) {  // conv3 bias grad of this image
-    float s = 0.f;
+    float sb = 0.f;
 #pragma unroll
-    for (int pos = 0; pos < 9; ++pos) s += dx3s[tid * 9 + pos];
-    f.sv[(size_t)n * 256 + 64 + tid] = s;
+    for (int pos = 0; pos < 9; ++pos) sb += dx3s[tid * 9 + pos];
+    f.sv[(size_t)n * 256 + 64 + tid] = sb;
   }
-  // conv3 data gradient -> dp2 (ReLU-masked with p2 > 0), conv2 bias grad:
-  // thread (ci = tid/4, co quarter q) scatters its 16 co's contributions into 25 registers
+  // conv3 data gradient -> dp2 (ReLU-masked with p2 > 0) + conv2 bias grad:
+  // thread (ci = hi, co 8q .. 8q+7) scatters into 25 registers, xor-tree over q
   {
-    const int ci = tid >> 2, q = tid & 3;
     float acc[25];
 #pragma unroll
     for (int k = 0; k < 25; ++k) acc[k] = 0.f;
-    for (int c = 0; c < 16; ++c) {
-      const int co = 16 * q + c;
-      float d[9], wr[9];
+#pragma unroll 2
+    for (int c = 0; c < 8; ++c) {
+      const int co = 8 * q + c;
+      float d[9], w[9];
 #pragma unroll
       for (int pos = 0; pos < 9; ++pos) d[pos] = dx3s[co * 9 + pos];
-      const float* wp = f.p + L::w3 + ((size_t)co * 64 + ci) * 9;
 #pragma unroll
-      for (int r = 0; r < 9; ++r) wr[r] = wp[r];
+      for (int r = 0; r < 9; ++r) w[r] = f.p[L::w3 + ((size_t)co * 64 + hi) * 9 + r];
 #pragma unroll
       for (int pos = 0; pos < 9; ++pos)
 #pragma unroll
-        for (int r = 0; r < 9; ++r) acc[(pos / 3 + r / 3) * 5 + pos % 3 + r % 3] += d[pos] * wr[r];
+        for (int r = 0; r < 9; ++r) acc[(pos / 3 + r / 3) * 5 + pos % 3 + r % 3] += d[pos] * w[r];
     }
 #pragma unroll
-    for (int k = 0; k < 25; ++k) {
-      acc[k] += __shfl_xor(acc[k], 1, 64);
-      acc[k] += __shfl_xor(acc[k], 2, 64);
-    }
+    for (int k = 0; k < 25; ++k)
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) acc[k] += __shfl_xor(acc[k], o, 64);
     if (q == 0) {
       float sb = 0.f;
 #pragma unroll
       for (int k = 0; k < 25; ++k) {
-        const float v = p2s[ci * 25 + k] > 0.f ? acc[k] : 0.f;
-        f.dp2[((size_t)n * 64 + ci) * 25 + k] = v;
+        const float v = p2s[hi * 25 + k] > 0.f ? acc[k] : 0.f;
+        f.dp2[((size_t)n * 64 + hi) * 25 + k] = v;
         sb += v;
       }
-      f.sv[(size_t)n * 256 + ci] = sb;
+      f.sv[(size_t)n * 256 + hi] = sb;
     }
   }
 }
@@ -346,10 +374,15 @@ struct SmemC {
   float dh1[8][64];
   float x3[8][144];
 };
+struct SmemE {
+  float dl[64 * 16];
+  float h1[64 * 64];
+};
 union SmemKB1 {
   SmemA a;
   SmemB b;
   SmemC c;
+  SmemE e;
 };
 
 __device__ void kb1_role_a(const KerasFused& f, SmemA& sm, int bid) {
@@ -536,54 +569,69 @@ __device__ void kb1_role_c(const KerasFused& f, SmemC& sm, int bid) {
   }
 }
 
-__device__ void kb1_role_e(const KerasFused& f) {
-  for (int o = threadIdx.x; o < 640; o += 256) {
-    const int c = o >> 6, j = o & 63;
-    float a = 0.f;
-    for (int nn = 0; nn < f.B; ++nn) a += f.dl[(size_t)nn * 16 + c] * f.h1[(size_t)nn * 64 + j];
-    f.gf2[o] = a;
+// role E: fc2 weight gradient = sum over the batch of dl (x) h1, staged through LDS 64 images at a
+// time (coalesced loads; the products then come from LDS, not from dependent global loads)
+__device__ void kb1_role_e(const KerasFused& f, SmemE& sm) {
+  const int tid = threadIdx.x;
+  float acc[3] = {0.f, 0.f, 0.f};  // outputs tid, tid + 256, tid + 512 (< 640)
+  for (int n0 = 0; n0 < f.B; n0 += 64) {
+    const int nb = f.B - n0 < 64 ? f.B - n0 : 64;
+    __syncthreads();
+    for (int i = tid; i < nb * 16; i += 256) sm.dl[i] = f.dl[(size_t)n0 * 16 + i];
+    for (int i = tid; i < nb * 64; i += 256) sm.h1[i] = f.h1[(size_t)n0 * 64 + i];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int o = tid + 256 * k;
+      if (o < 640) {
+        const int c = o >> 6, j = o & 63;
+        float a = 0.f;
+        for (int nn = 0; nn < nb; ++nn) a += sm.dl[nn * 16 + c] * sm.h1[nn * 64 + j];
+        acc[k] += a;
+      }
+    }
   }
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    if (tid + 256 * k < 640) f.gf2[tid + 256 * k] = acc[k];
 }
 
-__global__ __launch_bounds__(256) void kb1_kernel(KerasFused f) {
+// roles: bit mask of the roles to run (15 = all; fewer only for per-role timing, MXDDP_KB1_ROLES)
+__global__ __launch_bounds__(256) void kb1_kernel(KerasFused f, int roles) {
   __shared__ SmemKB1 sm;
   const int b = blockIdx.x, B = f.B;
-  if (b < 8 * B) kb1_role_a(f, sm.a, b);
-  else if (b < 12 * B) kb1_role_b(f, sm.b, b - 8 * B);
-  else if (b < 12 * B + B / 2) kb1_role_c(f, sm.c, b - 12 * B);
-  else kb1_role_e(f);
+  if (b < 8 * B) {
+    if (roles & 1) kb1_role_a(f, sm.a, b);
+  } else if (b < 12 * B) {
+    if (roles & 2) kb1_role_b(f, sm.b, b - 8 * B);
+  } else if (b < 12 * B + B / 2) {
+    if (roles & 4) kb1_role_c(f, sm.c, b - 12 * B);
+  } else if (roles & 8) {
+    kb1_role_e(f, sm.e);
+  }
 }
+
+struct KoRegion {
+  int blk0;          // first block of the region
+  int p0, np;        // parameter range
+  int T;             // 1: one thread per parameter; 4: the block's 4 waves split the planes
+  int nplanes;
+  long long stride;  // floats between planes
+  const float* src;  // plane 0 of the region's first parameter
+};
+constexpr int kKoMaxRegions = 10;
+struct KoPlan {
+  int nreg, nblocks;
+  KoRegion r[kKoMaxRegions];
+};
 
 // ------------------------------------------------------------------------------------------
-// KO: one thread per parameter.  Gradient = its partial planes summed in a fixed order; Adam
-// (device step count advanced by the last block to finish, as ops_optim.hip); then the updated
-// conv2 weight is written into both MFMA fragment orders.
-__device__ __forceinline__ float sum_planes(const float* p, size_t stride, int n) {
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  int i = 0;
-  for (; i + 4 <= n; i += 4) {
-    a0 += p[(size_t)i * stride];
-    a1 += p[(size_t)(i + 1) * stride];
-    a2 += p[(size_t)(i + 2) * stride];
-    a3 += p[(size_t)(i + 3) * stride];
-  }
-  for (; i < n; ++i) a0 += p[(size_t)i * stride];
-  return (a0 + a1) + (a2 + a3);
-}
-
-__device__ __forceinline__ float finalize_grad(const KerasFused& f, int i) {
-  const int B = f.B;
-  if (i < (int)L::w2) return sum_planes(f.pl1 + i, 320, 4 * B);
-  if (i < (int)L::b2) return sum_planes(f.pl2 + (i - L::w2), kPl2, B);
-  if (i < (int)L::w3) return sum_planes(f.sv + (i - L::b2), 256, B);
-  if (i < (int)L::b3) return sum_planes(f.pl3 + (i - L::w3), kPl3, B / 8);
-  if (i < (int)L::fw1) return sum_planes(f.sv + 64 + (i - L::b3), 256, B);
-  if (i < (int)L::fb1) return sum_planes(f.pf1 + (i - L::fw1), kPl3, B / 8);
-  if (i < (int)L::fw2) return sum_planes(f.sv + 128 + (i - L::fb1), 256, B);
-  if (i < (int)L::fb2) return f.gf2[i - L::fw2];
-  return sum_planes(f.sv + 192 + (i - L::fb2), 256, B);
-}
-
+// KO: finalize + Adam + repack.  The parameters are split into regions by gradient source (the
+// partial planes of each weight, the per-image bias vectors).  A plane-summing region (T = 4)
+// gives each block 64 consecutive parameters: wave w sums planes w, w + 4, ... with four
+// independent accumulators (each plane read is one coalesced 256-byte row per wave), the four
+// wave sums meet in LDS in a fixed order (deterministic), and wave 0 finishes the parameters.
+// T = 1 (the all-reduced g, the single fc2 plane): one thread per parameter.
 __device__ __forceinline__ void pack_w2(const KerasFused& f, int i, float val) {
   // i in [w2, b2): co, ci, tap r of conv2.weight[co][ci][ky][kx]
   const int j = i - L::w2, co = j / 288, rem = j - co * 288, ci = rem / 9, r = rem - ci * 9;
@@ -595,33 +643,63 @@ __device__ __forceinline__ void pack_w2(const KerasFused& f, int i, float val) {
   f.w2d[(((ci >> 4) * 4 + (co >> 4)) * 36 + r * 4 + (cl >> 2)) * 64 + (ci & 15) + 16 * (cl & 3)] = val;
 }
 
-__global__ __launch_bounds__(256) void ko_kernel(KerasFused f, int mode, float gscale) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  const bool live = i < (int)L::total;
+__global__ __launch_bounds__(256) void ko_kernel(KerasFused f, KoPlan plan, int mode, float gscale) {
+  __shared__ float red[4][64];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int ri = 0;
+#pragma unroll
+  for (int k = 1; k < kKoMaxRegions; ++k)
+    if (k < plan.nreg && b >= plan.r[k].blk0) ri = k;
+  const KoRegion& R = plan.r[ri];
+  const int T = R.T;
+  const int q = T == 1 ? 0 : w;
+  const int li = T == 1 ? (b - R.blk0) * 256 + tid : (b - R.blk0) * 64 + lane;  // index inside the region
+  const bool live = li < R.np;
+  const int i = R.p0 + li;
+  const bool adam = mode == 0 || mode == 2;
   int t = 0;
-  if (mode == 0 || mode == 2) t = __hip_atomic_load(f.adam_state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  if (live) {
-    float pv = f.p[i];
-    if (mode == 0 || mode == 1 || mode == 2) {
-      float gr = mode == 2 ? f.g[i] * gscale : finalize_grad(f, i);
-      if (mode == 1) {
-        f.g[i] = gr;
-      } else {
-        gr += f.wd * pv;
-        const float bc1 = 1.f - powf(f.b1, (float)t), bc2 = 1.f - powf(f.b2, (float)t);
-        const float bc2s = sqrtf(bc2);
-        const float e = f.eps_hat ? f.eps / bc2s : f.eps;
-        const float mi = f.b1 * f.m[i] + (1.f - f.b1) * gr;
-        const float vi = f.b2 * f.v[i] + (1.f - f.b2) * gr * gr;
-        f.m[i] = mi;
-        f.v[i] = vi;
-        pv -= (*f.lr / bc1) * mi / (sqrtf(vi) / bc2s + e);
-        f.p[i] = pv;
+  if (adam) t = __hip_atomic_load(f.adam_state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  float gr = 0.f;
+  if (mode != 3) {
+    if (live) {
+      const float* src = R.src + li;
+      const long long st = R.stride;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      int k = q;
+      for (; k + 3 * T < R.nplanes; k += 4 * T) {
+        a0 += src[(size_t)k * st];
+        a1 += src[(size_t)(k + T) * st];
+        a2 += src[(size_t)(k + 2 * T) * st];
+        a3 += src[(size_t)(k + 3 * T) * st];
       }
+      for (; k < R.nplanes; k += T) a0 += src[(size_t)k * st];
+      gr = (a0 + a1) + (a2 + a3);
+    }
+    if (T > 1) {  // block-uniform branch
+      red[w][lane] = gr;
+      __syncthreads();
+      gr = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    }
+  }
+  if (live && q == 0) {
+    float pv = f.p[i];
+    if (mode == 1) {
+      f.g[i] = gr;
+    } else if (adam) {
+      gr = gr * gscale + f.wd * pv;
+      const float bc1 = 1.f - powf(f.b1, (float)t), bc2 = 1.f - powf(f.b2, (float)t);
+      const float bc2s = sqrtf(bc2);
+      const float e = f.eps_hat ? f.eps / bc2s : f.eps;
+      const float mi = f.b1 * f.m[i] + (1.f - f.b1) * gr;
+      const float vi = f.b2 * f.v[i] + (1.f - f.b2) * gr * gr;
+      f.m[i] = mi;
+      f.v[i] = vi;
+      pv -= (*f.lr / bc1) * mi / (sqrtf(vi) / bc2s + e);
+      f.p[i] = pv;
     }
     if (mode != 1 && i >= (int)L::w2 && i < (int)L::b2) pack_w2(f, i, pv);
   }
-  if (mode == 0 || mode == 2) {  // the last block to finish publishes the step count
+  if (adam) {  // the last block to finish publishes the step count (ops_optim.hip)
     __syncthreads();
     if (threadIdx.x == 0) {
       const int arrived = __hip_atomic_fetch_add(f.adam_state + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
@@ -637,17 +715,58 @@ __global__ __launch_bounds__(256) void ko_kernel(KerasFused f, int mode, float g
 
 void keras_fused_forward(const KerasFused& f, hipStream_t st) {
   MX_CHECK(f.B > 0 && f.B % 8 == 0 && f.B <= 1024, "keras engine: batch must be a multiple of 8 (<= 1024)");
-  MX_LAUNCH(keras::kf1_kernel, dim3(4 * f.B), dim3(256), 0, st, f);
-  MX_LAUNCH(keras::kf2_kernel, dim3(f.B), dim3(256), 0, st, f);
+  MX_LAUNCH(keras::kf1_kernel, dim3(4 * f.B), dim3(512), 0, st, f);
+  MX_LAUNCH(keras::kf2_kernel, dim3(f.B), dim3(512), 0, st, f);
 }
 
 void keras_fused_backward(const KerasFused& f, hipStream_t st) {
-  MX_LAUNCH(keras::kb1_kernel, dim3(12 * f.B + f.B / 2 + 1), dim3(256), 0, st, f);
+  static const int roles = [] {
+    const char* e = std::getenv("MXDDP_KB1_ROLES");  // timing experiments only: breaks training
+    return e ? std::atoi(e) : 15;
+  }();
+  MX_LAUNCH(keras::kb1_kernel, dim3(12 * f.B + f.B / 2 + 1), dim3(256), 0, st, f, roles);
+}
+
+// Regions of the update (mode 0 / 1: the finalize reads the partial planes; mode 2: Adam from
+// the all-reduced g, one thread per parameter; mode 3: only the conv2 repack)
+static keras::KoPlan ko_plan(const KerasFused& f, int mode) {
+  using L = KerasLayout;
+  keras::KoPlan p{};
+  int blk = 0;
+  auto add = [&](size_t p0, size_t np, int T, int nplanes, long long stride, const float* src) {
+    keras::KoRegion& r = p.r[p.nreg++];
+    r.blk0 = blk;
+    r.p0 = (int)p0;
+    r.np = (int)np;
+    r.T = T;
+    r.nplanes = nplanes;
+    r.stride = stride;
+    r.src = src;
+    const size_t per = T == 1 ? 256 : 64;
+    blk += (int)((np + per - 1) / per);
+  };
+  const int B = f.B;
+  if (mode == 2 || mode == 3) {
+    add(0, L::total, 1, mode == 3 ? 0 : 1, 0, f.g);
+  } else {
+    add(L::w1, 320, 4, 4 * B, 320, f.pl1);
+    add(L::w2, L::b2 - L::w2, 4, B, 18432, f.pl2);
+    add(L::b2, 64, 4, B, 256, f.sv);
+    add(L::w3, L::b3 - L::w3, 4, B / 8, 36864, f.pl3);
+    add(L::b3, 64, 4, B, 256, f.sv + 64);
+    add(L::fw1, L::fb1 - L::fw1, 4, B / 8, 36864, f.pf1);
+    add(L::fb1, 64, 4, B, 256, f.sv + 128);
+    add(L::fw2, 640, 1, 1, 0, f.gf2);
+    add(L::fb2, 10, 4, B, 256, f.sv + 192);
+  }
+  p.nblocks = blk;
+  return p;
 }
 
 void keras_fused_update(const KerasFused& f, int mode, float gscale, hipStream_t st) {
   MX_CHECK(mode >= 0 && mode <= 3, "keras engine: update mode 0..3");
-  MX_LAUNCH(keras::ko_kernel, dim3((unsigned)((KerasLayout::total + 255) / 256)), dim3(256), 0, st, f, mode, gscale);
+  const keras::KoPlan plan = ko_plan(f, mode);
+  MX_LAUNCH(keras::ko_kernel, dim3((unsigned)plan.nblocks), dim3(256), 0, st, f, plan, mode, gscale);
 }
 
 }  // namespace mx

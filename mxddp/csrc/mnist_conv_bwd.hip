@@ -758,7 +758,7 @@ template <bool kWino, int kF6WSplit = 1, bool kA1 = false>
 __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scratch sc) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   if ((int)blockIdx.x < f.co_blocks) {
-    peer_two_shot_f32_block(f.co_args, f.co_part, blockIdx.x);
+    peer_two_shot_f32_block(f.co_args, f.co_part, blockIdx.x, reinterpret_cast<uint32_t*>(sm));
     return;
   }
   const int bid = (int)blockIdx.x - f.co_blocks;

@@ -447,6 +447,91 @@ __global__ __launch_bounds__(256) void f3_fc1_kernel(MnistFused f) {
   MX_TRACE(f, 1, 1);
 }
 
+// F3 with a deeper K chunk per block (kKC = 256 .. 576) split over the block's 4 waves: each wave
+// runs its kKC/4 slice for every batch M-tile, the 4 slices are summed through LDS, and ONE atomic
+// per output per block remains -- 9216 / kKC blocks per output (16-way at kKC = 576) instead of
+// 64-way: the same-address atomic chains that bound the 144-chunk kernel get 2.25-4x shorter.
+// Block = (K chunk, kNF output features).
+template <int kKC, int kNF>
+__global__ __launch_bounds__(256) void f3k_fc1_kernel(MnistFused f) {
+  MX_TRACE(f, 1, 0);
+  constexpr int kG = kKC / 64, kNT = kNF / 16, kNq = 128 / kNF;
+  static_assert(kKC % 64 == 0 && 9216 % kKC == 0 && kNF % 16 == 0, "F3 tiling");
+  __shared__ float red[4][16][kNF + 1];
+  const int kc = blockIdx.x / kNq, nq = blockIdx.x - kc * kNq;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  if (f.synth && blockIdx.x == 0 && tid == 0) *f.counter += 1;  // F2 consumed it
+  const int k0 = kc * kKC + w * (kKC / 4) + 4 * g;
+  const float* W = f.p + L::fw1;
+  float4 bw[kNT][kG];
+#pragma unroll
+  for (int nt = 0; nt < kNT; ++nt)
+#pragma unroll
+    for (int s = 0; s < kG; ++s)
+      bw[nt][s] = *reinterpret_cast<const float4*>(W + (size_t)(kNF * nq + 16 * nt + m) * 9216 + k0 + 16 * s);
+  for (int mt = 0; mt < f.B / 16; ++mt) {
+    float4 av[kG];
+    const float* A = f.pool + (size_t)(16 * mt + m) * 9216 + k0;
+#pragma unroll
+    for (int s = 0; s < kG; ++s) av[s] = *reinterpret_cast<const float4*>(A + 16 * s);
+    f32x4 acc[kNT];
+#pragma unroll
+    for (int nt = 0; nt < kNT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < kG; ++s)
+#pragma unroll
+      for (int nt = 0; nt < kNT; ++nt) {
+        acc[nt] = mfma4(av[s].x, bw[nt][s].x, acc[nt]);
+        acc[nt] = mfma4(av[s].y, bw[nt][s].y, acc[nt]);
+        acc[nt] = mfma4(av[s].z, bw[nt][s].z, acc[nt]);
+        acc[nt] = mfma4(av[s].w, bw[nt][s].w, acc[nt]);
+      }
+    if (mt > 0) __syncthreads();  // the previous M-tile's sums have been read
+#pragma unroll
+    for (int nt = 0; nt < kNT; ++nt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[w][4 * g + j][16 * nt + m] = acc[nt][j];
+    __syncthreads();
+    for (int i = tid; i < 16 * kNF; i += 256) {
+      const int row = i / kNF, col = i - row * kNF;
+      const float v = (red[0][row][col] + red[1][row][col]) + (red[2][row][col] + red[3][row][col]);
+      atomicAdd(f.h + (16 * mt + row) * 128 + kNF * nq + col, v);
+    }
+  }
+  // side job: zero the conv2-wgrad accumulator slabs for this step's F67 (see f3_fc1_kernel)
+  {
+    float4* wa = reinterpret_cast<float4*>(carve(f.scratch).wacc);
+    for (int i = blockIdx.x * 256 + tid; i < kWaccSlabs * kPack / 4; i += gridDim.x * 256)
+      wa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  MX_TRACE(f, 1, 1);
+}
+
+// fc1-forward tiling (MXDDP_F3 = 144 | 576x32 | 576x16 | 384x16 | 256x16)
+static int f3_variant() {
+  static const int v = [] {
+    const char* e = std::getenv("MXDDP_F3");
+    const std::string s = e ? e : "";
+    if (s == "144") return 0;
+    if (s == "576x32") return 1;
+    if (s == "576x16") return 2;
+    if (s == "384x16") return 3;
+    if (s == "256x16") return 4;
+    return 0;
+  }();
+  return v;
+}
+
+static void launch_f3(const MnistFused& f, hipStream_t st) {
+  switch (f3_variant()) {
+    case 1: MX_LAUNCH((f3k_fc1_kernel<576, 32>), dim3(16 * 4), dim3(256), 0, st, f); break;
+    case 2: MX_LAUNCH((f3k_fc1_kernel<576, 16>), dim3(16 * 8), dim3(256), 0, st, f); break;
+    case 3: MX_LAUNCH((f3k_fc1_kernel<384, 16>), dim3(24 * 8), dim3(256), 0, st, f); break;
+    case 4: MX_LAUNCH((f3k_fc1_kernel<256, 16>), dim3(36 * 8), dim3(256), 0, st, f); break;
+    default: MX_LAUNCH(f3_fc1_kernel, dim3((9216 / kF3Chunk) * 4), dim3(256), 0, st, f); break;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // F5: head + fc1 backward for a 48-column slice of the 9216 fc1 inputs (192 blocks: at most one
 // per CU, so no CU runs two of these latency-bound blocks back to back).
@@ -896,7 +981,7 @@ void mnist_fused_forward(const MnistFused& f, hipStream_t st) {
     MX_LAUNCH(f2_fwd_kernel<true>, dim3(f.B * 12), dim3(256), 0, st, f, sc);
   else
     MX_LAUNCH(f2_fwd_kernel<false>, dim3(f.B * 12), dim3(256), 0, st, f, sc);
-  MX_LAUNCH(f3_fc1_kernel, dim3((9216 / kF3Chunk) * 4), dim3(256), 0, st, f);
+  launch_f3(f, st);
   MX_HIP_CHECK(hipGetLastError());
 }
 

@@ -56,14 +56,16 @@ __device__ __forceinline__ void signal_peers(const PeerArgs& a, int set, int b, 
 // One block's share (slice b) of the two-shot float all-reduce, world size at run time (the
 // standalone kernel's per-W template, for a caller that cannot be instantiated per W).  Same
 // slots, flags, epochs and partition as peer_all_reduce_kernel<float, W> with the same block
-// count, so the two can alternate call by call.
-__device__ __forceinline__ void peer_two_shot_f32_block(const PeerArgs& a, const PeerPartition& part, int b) {
+// count, so the two can alternate call by call.  `s_ep` is one word of the caller's LDS (a
+// static __shared__ here would add to the host kernel's static LDS and make its 160 KB dynamic
+// allocation fail).
+__device__ __forceinline__ void peer_two_shot_f32_block(const PeerArgs& a, const PeerPartition& part, int b,
+                                                        uint32_t* s_ep) {
   typedef uint32_t v4u __attribute__((ext_vector_type(4)));
   const int r = a.rank, t = threadIdx.x, W = a.ws;
-  __shared__ uint32_t s_ep;
-  if (t == 0) s_ep = a.epoch[b] + 1;
+  if (t == 0) *s_ep = a.epoch[b] + 1;
   __syncthreads();
-  const uint32_t ep = s_ep;
+  const uint32_t ep = *s_ep;
   float* data = static_cast<float*>(a.data);
   const long long c = part.chunk, lo = (long long)b * part.slice;
   const long long slot = a.slot_bytes / 4;

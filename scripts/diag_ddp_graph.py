@@ -31,6 +31,7 @@ ap.add_argument("--graph", action="store_true")
 ap.add_argument("--overlap", type=int, default=1)
 ap.add_argument("--opt", default="adam")
 ap.add_argument("--loader", default="synthetic", choices=["synthetic", "fixed"])
+ap.add_argument("--mimic", action="store_true", help="step body as in mxddp.train (correct count, events, check)")
 a = ap.parse_args()
 
 inf = PC.init_distributed(use_gpu=True)
@@ -43,12 +44,20 @@ opt = Adam(ddp.flat, lr=1e-3, eps=1e-7, eps_hat=True) if a.opt == "adam" else SG
 acc = torch.zeros((), device=dev)
 
 
+corr_acc = torch.zeros((), device=dev)
+
+
 def step(x, y):
     opt.zero_grad()
-    loss = ops.cross_entropy(ddp(x), y)
+    if a.mimic:
+        loss, corr = ops.cross_entropy(ddp(x), y, return_correct=True)
+    else:
+        loss, corr = ops.cross_entropy(ddp(x), y), None
     loss.backward()
     opt.step()
     acc.add_(loss.detach())
+    if corr is not None:
+        corr_acc.add_(corr)
     return (loss.detach(),)
 
 
@@ -61,8 +70,15 @@ pc = PP.peer_comm()
 it = iter(loader) if a.loader == "synthetic" else iter(fixed)
 for i in range(a.steps):
     x, y = next(it)
+    if a.mimic:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
     run(x, y)
+    if a.mimic:
+        ev[1].record()
     torch.cuda.synchronize()
+    if a.mimic:
+        ddp.check()
     cs = ddp.flat.data.double().sum().item()
     allcs = [None] * inf.world_size
     dist.all_gather_object(allcs, (cs, pc.error() if pc is not None else -1, run.captured))
