@@ -175,7 +175,12 @@ __device__ __forceinline__ void f6_body(const MnistFused& f, const Scratch& sc, 
 constexpr int kF6WA1P = 157, kF6WA1PL = 164, kF6WVP = 20;
 constexpr size_t kF6WLds = sizeof(float) * (784 + 160 + 16 * kF6WA1PL + 24 * 16 * kF6WVP);
 // kF6WSplit = blocks per (image, ci half), each 6 / kF6WSplit chunks
-template <int kF6WSplit, bool kA1>
+// kCoS = 2 (co-split): block = (image, ci half, co half) -- 2x the blocks, each wave owns one co
+// tile and HALF the Winograd points (ky-side rows i = 2xh, 2xh+1: 8 accumulators, half the MFMAs);
+// the wave pair sharing a co tile sums its partial G^T dU G outputs through LDS and each wave
+// issues the atomics of two of its four co rows, so the atomic count per image is unchanged while
+// the per-wave MFMA chain (the F67 long pole) halves and the weight gradient spreads over 2x the CUs.
+template <int kF6WSplit, bool kA1, int kCoS = 1>
 __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc, float* sm, int braw, int nblk) {
   MX_TRACE_B(f, 3, 0, braw);
   constexpr int kA1P = kA1 ? kF6WA1PL : kF6WA1P;
@@ -184,8 +189,12 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
   float* a1s = w1s + 160;     // [16 ci][kA1P]: 6 a1 rows x 26
   float* vs = a1s + 16 * kA1P;  // [24 t][16 ci][20]
   const int bid = xcd_remap(braw, nblk);
-  const int b = bid / (2 * kF6WSplit), h = bid & 1, c0 = ((bid >> 1) % kF6WSplit) * (6 / kF6WSplit);
+  static_assert(kCoS == 1 || kF6WSplit == 1, "co-split only with unsplit chunks");
+  const int b = bid / (2 * kF6WSplit * kCoS), h = bid & 1, c0 = ((bid >> 1) % kF6WSplit) * (6 / kF6WSplit);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  // co tile of this wave and (kCoS = 2) its Winograd-row half
+  const int ct = kCoS == 1 ? w : 2 * ((bid >> 1) & 1) + (w & 1), xh = kCoS == 1 ? 0 : w >> 1;
+  constexpr int kNI = 4 / kCoS;  // Winograd rows i per wave
   // kA1: a1 rows 4c .. 4c+5 of the block's 16 ci = 16 x 39 float4 (624 of the 768 slots)
   // (three named registers, not an array: an array here was placed in scratch memory)
   const float* a1b = f.a1 + ((size_t)b * 32 + 16 * h) * 676;
@@ -208,7 +217,7 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
     if (tid < 196) *reinterpret_cast<float4*>(xs + 4 * tid) = xv;
     if (tid < 160) w1s[tid] = wv;
   }
-  const int co = 16 * w + m;  // A row of this lane
+  const int co = 16 * ct + m;  // A row of this lane
   const float* dpl = f.dp + (size_t)b * 9216 + co * 144 + 6 * g;
   const uint16_t* qpl = reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(f.idx) + (size_t)b * 9216 + co * 144 + 6 * g);
   float2 dn[3];
@@ -218,9 +227,9 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
     dn[k] = *reinterpret_cast<const float2*>(dpl + 24 * c0 + 2 * k);
     qn[k] = qpl[12 * c0 + k];
   }
-  f32x4 acc[16];
+  f32x4 acc[4 * kNI];
 #pragma unroll
-  for (int x = 0; x < 16; ++x) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int x = 0; x < 4 * kNI; ++x) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
   MX_TRACE_B(f, 3, 1, braw);
   float w1b[3];  // conv1 B fragments: tap 4ks + g of channel m (taps 9..11 are padding)
@@ -320,14 +329,18 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
     // (C) k-step s: tile t = 6g + s of the chunk
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
-      const float4* vp = reinterpret_cast<const float4*>(vs + ((6 * g + s) * 16 + m) * kF6WVP);
-      const float4 b0 = vp[0], b1 = vp[1], b2 = vp[2], b3 = vp[3];
+      const float4* vp = reinterpret_cast<const float4*>(vs + ((6 * g + s) * 16 + m) * kF6WVP) + kNI * xh;
+      float4 bb[kNI];
+#pragma unroll
+      for (int i = 0; i < kNI; ++i) bb[i] = vp[i];
       const float v = dv[s];
       const bool qy = (qv[s] >> 1) & 1, qx = qv[s] & 1;
-      const float vy[4] = {qy ? 0.f : v, v, qy ? -v : v, qy ? -v : 0.f};
-      const float4 bb[4] = {b0, b1, b2, b3};
+      const float vy4[4] = {qy ? 0.f : v, v, qy ? -v : v, qy ? -v : 0.f};
+      float vy[kNI];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < kNI; ++i) vy[i] = kCoS == 1 ? vy4[i] : (xh ? vy4[2 + i] : vy4[i]);
+#pragma unroll
+      for (int i = 0; i < kNI; ++i) {
         const float w0 = qx ? 0.f : vy[i], w2 = qx ? -vy[i] : vy[i], w3 = qx ? -vy[i] : 0.f;
         acc[4 * i + 0] = mfma4(w0, bb[i].x, acc[4 * i + 0]);
         acc[4 * i + 1] = mfma4(vy[i], bb[i].y, acc[4 * i + 1]);
@@ -342,6 +355,51 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
   // (co = 16w + 4g + j, ci = 16h + m)
   const int ci = 16 * h + m;
   float* wa = sc.wacc + (b & (kWaccSlabs - 1)) * kPack;
+  if constexpr (kCoS == 2) {
+    // partial G^T dU G of this wave's two Winograd rows: t[ky][jj] over rows (m0, m1) = i 0, 1 or
+    // (m2, m3) = i 2, 3 of G^T = [1 .5 .5 0; 0 .5 -.5 0; 0 .5 .5 1]
+    float o[4][9];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float t[3][4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const float ma = acc[jj][j], mb = acc[4 + jj][j];
+        if (xh == 0) {
+          t[0][jj] = ma + 0.5f * mb;
+          t[1][jj] = 0.5f * mb;
+          t[2][jj] = 0.5f * mb;
+        } else {
+          t[0][jj] = 0.5f * ma;
+          t[1][jj] = -0.5f * ma;
+          t[2][jj] = 0.5f * ma + mb;
+        }
+      }
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        o[j][ky * 3 + 0] = t[ky][0] + 0.5f * (t[ky][1] + t[ky][2]);
+        o[j][ky * 3 + 1] = 0.5f * (t[ky][1] - t[ky][2]);
+        o[j][ky * 3 + 2] = 0.5f * (t[ky][1] + t[ky][2]) + t[ky][3];
+      }
+    }
+    // wave xh finalises co rows j = 2xh, 2xh+1 of its lanes; hands the other two to its partner
+    // (wave w ^ 2, same co tile) through LDS over vs: [4 w][2 jl][9 tap][64 lane]
+    __syncthreads();  // every wave's phase-C reads of vs are done
+    float* xch = vs;
+#pragma unroll
+    for (int jl = 0; jl < 2; ++jl)
+#pragma unroll
+      for (int k = 0; k < 9; ++k) xch[((w * 2 + jl) * 9 + k) * 64 + lane] = o[xh ? jl : 2 + jl][k];
+    __syncthreads();
+    const int pw = w ^ 2;
+#pragma unroll
+    for (int jl = 0; jl < 2; ++jl) {
+      const int j = 2 * xh + jl, cj = 16 * ct + 4 * g + j;
+#pragma unroll
+      for (int k = 0; k < 9; ++k)
+        atomicAdd(wa + (k * 64 + cj) * 32 + ci, o[j][k] + xch[((pw * 2 + jl) * 9 + k) * 64 + lane]);
+    }
+  } else {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int cj = 16 * w + 4 * g + j;
@@ -362,6 +420,7 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
       atomicAdd(wa + ((ky * 3 + 1) * 64 + cj) * 32 + ci, o1);
       atomicAdd(wa + ((ky * 3 + 2) * 64 + cj) * 32 + ci, o2);
     }
+  }
   }
   MX_TRACE_B(f, 3, 3, braw);
   if (trc) {  // phase-time sums as "time after block start" in trace slots 4..6 (A, B, C)
@@ -754,7 +813,7 @@ __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc,
 // the peers' matching blocks while the remaining blocks do the conv backward, so the 4.7 MB
 // exchange overlaps it inside ONE launch (no side stream, no cross-queue fence).  co_blocks is
 // a multiple of 8, so the conv part keeps its XCD-aware block mapping.
-template <bool kWino, int kF6WSplit = 1, bool kA1 = false>
+template <bool kWino, int kF6WSplit = 1, bool kA1 = false, int kCoS = 1>
 __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scratch sc) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   if ((int)blockIdx.x < f.co_blocks) {
@@ -762,10 +821,10 @@ __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scr
     return;
   }
   const int bid = (int)blockIdx.x - f.co_blocks;
-  const int n6 = (kWino ? 2 * kF6WSplit : 9) * f.B;
+  const int n6 = (kWino ? 2 * kF6WSplit * kCoS : 9) * f.B;
   if (bid < n6) {
     if (kWino)
-      f6w_body<kF6WSplit, kA1>(f, sc, sm, bid, n6);
+      f6w_body<kF6WSplit, kA1, kCoS>(f, sc, sm, bid, n6);
     else
       f6_body(f, sc, sm, bid, n6);
   } else if (kWino) {
@@ -851,12 +910,23 @@ static int f6w_split() {
   }();
   return v;
 }
+// weight-gradient blocks split over output channels (MXDDP_F6W_COS = 1 | 2)
+static int f6w_cos() {
+  static const int v = [] {
+    const char* e = std::getenv("MXDDP_F6W_COS");
+    return (e && std::atoi(e) == 2) ? 2 : 1;
+  }();
+  return v;
+}
 
 template <int kSplit>
 static void launch_f67_wino(const MnistFused& f, const Scratch& sc, hipStream_t st) {
   constexpr size_t lds = kF6WLds > kF7WLds ? kF6WLds : kF7WLds;
-  const dim3 grid(f.co_blocks + 2 * kSplit * f.B + kF7WChunks * f.B);
-  if (kSplit == 1 && f.a1_pub)
+  const int cos = kSplit == 1 && f.a1_pub ? f6w_cos() : 1;
+  const dim3 grid(f.co_blocks + 2 * kSplit * cos * f.B + kF7WChunks * f.B);
+  if (kSplit == 1 && f.a1_pub && cos == 2)
+    MX_LAUNCH((f67_conv2_bwd_kernel<true, 1, true, 2>), grid, dim3(256), lds, st, f, sc);
+  else if (kSplit == 1 && f.a1_pub)
     MX_LAUNCH((f67_conv2_bwd_kernel<true, 1, true>), grid, dim3(256), lds, st, f, sc);
   else
     MX_LAUNCH((f67_conv2_bwd_kernel<true, kSplit>), grid, dim3(256), lds, st, f, sc);
@@ -867,6 +937,7 @@ void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_
   if (!attr) {
     for (const void* fn : {reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 1>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 1, true>),
+                           reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 1, true, 2>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 2>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 3>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<false>)})

@@ -603,11 +603,20 @@ class _CrossEntropy(torch.autograd.Function):
         C.xent_fwd_bwd(logits.data_ptr(), tgt.data_ptr(), 0, dl.data_ptr(), acc.data_ptr(), acc.data_ptr() + 4,
                        B, K, 1.0 / B, stream_of(logits), 1.0 / B)
         ctx.save_for_backward(dl)
-        ctx.mark_non_differentiable(acc)
-        return acc[0], acc[1]
+        correct = acc[1]
+        # the correct count must carry no autograd history: a caller accumulating it across steps
+        # (corr_acc.add_(corr)) would otherwise chain every step's graph to the next and keep the
+        # parameters' grad accumulators of the FIRST step alive -- with the stream they were
+        # created on, so a later hipGraph capture ran the DDP hooks (and their bucket all-reduce)
+        # outside the capture (ranks then trained on un-reduced gradients)
+        ctx.mark_non_differentiable(correct)
+        ctx.set_materialize_grads(False)
+        return acc[0], correct
 
     @staticmethod
     def backward(ctx, dloss, _dcorrect):
+        if dloss is None:
+            return None, None
         (dl,) = ctx.saved_tensors
         return dl * dloss, None
 

@@ -142,6 +142,11 @@ def init_distributed(backend: str | None = None, init_method: str | None = None,
     if world_size > 1 and not dist.is_initialized():
         if init_method is None and "MASTER_ADDR" in os.environ:
             init_method = "env://"
+        if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True" and init_method and init_method != "env://":
+            # under torchrun every worker's tcp:// rendezvous becomes a CLIENT of the agent's store
+            # at that address: a tcp:// URL other than the agent's (e.g. the reference default
+            # tcp://127.0.0.1:13456) has no server and hangs; the agent's env contract is the truth
+            init_method = "env://"
         # control plane always gloo (TCPStore + CPU collectives); RCCL data plane is ours.
         dist.init_process_group("gloo", init_method=init_method, world_size=world_size, rank=rank,
                                 timeout=datetime.timedelta(seconds=timeout_s))

@@ -24,6 +24,7 @@ import torch.nn as nn
 
 from .. import native
 from . import comm as _comm
+from . import graphed as _graphed
 from .flat import FlatParams, flatten_buffers
 
 
@@ -182,6 +183,12 @@ class DistributedDataParallel(nn.Module):
     # ------------------------------------------------------------------ hooks
     def _make_hook(self, i: int):
         def hook(p):
+            if self.device.type == "cuda" and _graphed.capturing() and not torch.cuda.is_current_stream_capturing():
+                # the grad accumulator runs on the stream it was created on: one kept alive from an
+                # eager step (an autograd graph held across steps) puts this bucket's all-reduce
+                # outside the captured step, and every replay would skip it
+                raise RuntimeError("DDP: gradient hook ran outside the hipGraph capture (an autograd graph from an "
+                                   "earlier step is still alive: detach step outputs accumulated across steps)")
             if not self._queued:
                 self._queued = True
                 torch.autograd.Variable._execution_engine.queue_callback(self._finalize)

@@ -28,6 +28,12 @@ import torch
 from .. import native
 
 _CAPTURE_STREAMS: dict = {}
+_CAPTURING = [0]
+
+
+def capturing() -> bool:
+    """True while a GraphedStep records its step (hooks use it to check they run inside it)."""
+    return _CAPTURING[0] > 0
 
 
 def capture_stream(device: torch.device) -> torch.cuda.Stream:
@@ -87,8 +93,12 @@ class GraphedStep:
         g = torch.cuda.CUDAGraph()
         # thread-local capture mode: the communicator and reducer issue their own stream work
         # (side comm stream, RCCL kernels) from this thread inside the capture
-        with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
-            self._out = self.step_fn(self._x, self._y)
+        _CAPTURING[0] += 1
+        try:
+            with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
+                self._out = self.step_fn(self._x, self._y)
+        finally:
+            _CAPTURING[0] -= 1
         cur.wait_stream(side)
         self.graph = g
         # the capture only RECORDED the step: run it once so this call trains like any other

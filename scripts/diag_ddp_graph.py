@@ -32,7 +32,9 @@ ap.add_argument("--overlap", type=int, default=1)
 ap.add_argument("--opt", default="adam")
 ap.add_argument("--loader", default="synthetic", choices=["synthetic", "fixed"])
 ap.add_argument("--mimic", action="store_true", help="step body as in mxddp.train (correct count, events, check)")
+ap.add_argument("--parts", default="corr,ev,check", help="--mimic parts: corr (return_correct), ev (events), check")
 a = ap.parse_args()
+parts = set(a.parts.split(",")) if a.mimic else set()
 
 inf = PC.init_distributed(use_gpu=True)
 dev = inf.device
@@ -49,7 +51,7 @@ corr_acc = torch.zeros((), device=dev)
 
 def step(x, y):
     opt.zero_grad()
-    if a.mimic:
+    if "corr" in parts:
         loss, corr = ops.cross_entropy(ddp(x), y, return_correct=True)
     else:
         loss, corr = ops.cross_entropy(ddp(x), y), None
@@ -70,14 +72,14 @@ pc = PP.peer_comm()
 it = iter(loader) if a.loader == "synthetic" else iter(fixed)
 for i in range(a.steps):
     x, y = next(it)
-    if a.mimic:
+    if "ev" in parts:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
     run(x, y)
-    if a.mimic:
+    if "ev" in parts:
         ev[1].record()
     torch.cuda.synchronize()
-    if a.mimic:
+    if "check" in parts:
         ddp.check()
     cs = ddp.flat.data.double().sum().item()
     allcs = [None] * inf.world_size

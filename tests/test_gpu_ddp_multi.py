@@ -69,13 +69,15 @@ def _graph_worker(rank, ws, port, model_name, b, optname, q):
             bad.append(("transport", ddp.transport))
         opt = _make_opt(optname, ddp.flat)
         acc = torch.zeros((), device=dev)
+        corr_acc = torch.zeros((), device=dev)
 
-        def step(x, y):
+        def step(x, y):  # the step body of mxddp.train (the correct count accumulates across steps)
             opt.zero_grad()
-            loss = ops.cross_entropy(ddp(x), y)
+            loss, corr = ops.cross_entropy(ddp(x), y, return_correct=True)
             loss.backward()
             opt.step()
             acc.add_(loss.detach())
+            corr_acc.add_(corr)
             return (loss.detach(),)
 
         run = GraphedStep(step, dev, warmup=2, before_replay=opt._sync_lr, enabled=use_graph)
