@@ -507,7 +507,57 @@ __global__ __launch_bounds__(256) void f3k_fc1_kernel(MnistFused f) {
   MX_TRACE(f, 1, 1);
 }
 
-// fc1-forward tiling (MXDDP_F3 = 144 | 576x32 | 576x16 | 384x16 | 256x16)
+// F3, output-tiled split-K: block = (K chunk of 1152, 16 x 16 output tile) -- 8 chunks x B/2 tiles
+// (256 blocks at B = 64).  Every block loads only its 16 pool rows and 16 W1 rows of the chunk
+// (147 KB), and the tiles of one chunk sit on one XCD (xcd_remap), so that XCD's L2 holds the
+// chunk's pool / W1 columns once.  Wave w reduces K slice w of the chunk (288 deep, all 36 float4
+// operands issued up front, two accumulator chains), the 4 wave partials are summed in LDS, and
+// one atomic per output per block remains: 8-way per output instead of 64-way (65 K atomics per
+// step instead of 524 K -- the 144-chunk kernel's time was mostly its atomics draining).
+constexpr int kF3TChunks = 8, kF3TK = 9216 / kF3TChunks, kF3TW = kF3TK / 4, kF3TS = kF3TW / 16;
+__global__ __launch_bounds__(256) void f3t_fc1_kernel(MnistFused f) {
+  MX_TRACE(f, 1, 0);
+  __shared__ float red[4][16][17];
+  const int tiles = f.B / 2;  // (B / 16) row tiles x 8 column tiles
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kc = bid / tiles, tile = bid - kc * tiles, mt = tile >> 3, nt = tile & 7;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  if (f.synth && blockIdx.x == 0 && tid == 0) *f.counter += 1;  // F2 consumed it
+  const int k0 = kc * kF3TK + w * kF3TW + 4 * g;
+  const float4* A = reinterpret_cast<const float4*>(f.pool + (size_t)(16 * mt + m) * 9216 + k0);
+  const float4* W = reinterpret_cast<const float4*>(f.p + L::fw1 + (size_t)(16 * nt + m) * 9216 + k0);
+  float4 av[kF3TS], bv[kF3TS];
+#pragma unroll
+  for (int s = 0; s < kF3TS; ++s) {
+    av[s] = A[4 * s];
+    bv[s] = W[4 * s];
+  }
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int s = 0; s < kF3TS; ++s) {
+    acc[0] = mfma4(av[s].x, bv[s].x, acc[0]);
+    acc[1] = mfma4(av[s].y, bv[s].y, acc[1]);
+    acc[0] = mfma4(av[s].z, bv[s].z, acc[0]);
+    acc[1] = mfma4(av[s].w, bv[s].w, acc[1]);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[w][4 * g + j][m] = acc[0][j] + acc[1][j];
+  __syncthreads();
+  {
+    const int row = tid >> 4, col = tid & 15;
+    const float v = (red[0][row][col] + red[1][row][col]) + (red[2][row][col] + red[3][row][col]);
+    atomicAdd(f.h + (16 * mt + row) * 128 + 16 * nt + col, v);
+  }
+  // side job: zero the conv2-wgrad accumulator slabs for this step's F67 (see f3_fc1_kernel)
+  {
+    float4* wa = reinterpret_cast<float4*>(carve(f.scratch).wacc);
+    for (int i = blockIdx.x * 256 + tid; i < kWaccSlabs * kPack / 4; i += gridDim.x * 256)
+      wa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  MX_TRACE(f, 1, 1);
+}
+
+// fc1-forward tiling (MXDDP_F3 = tile (default) | 144 | 576x32 | 576x16 | 384x16 | 256x16)
 static int f3_variant() {
   static const int v = [] {
     const char* e = std::getenv("MXDDP_F3");
@@ -517,7 +567,7 @@ static int f3_variant() {
     if (s == "576x16") return 2;
     if (s == "384x16") return 3;
     if (s == "256x16") return 4;
-    return 0;
+    return 5;
   }();
   return v;
 }
@@ -528,6 +578,7 @@ static void launch_f3(const MnistFused& f, hipStream_t st) {
     case 2: MX_LAUNCH((f3k_fc1_kernel<576, 16>), dim3(16 * 8), dim3(256), 0, st, f); break;
     case 3: MX_LAUNCH((f3k_fc1_kernel<384, 16>), dim3(24 * 8), dim3(256), 0, st, f); break;
     case 4: MX_LAUNCH((f3k_fc1_kernel<256, 16>), dim3(36 * 8), dim3(256), 0, st, f); break;
+    case 5: MX_LAUNCH(f3t_fc1_kernel, dim3(kF3TChunks * (f.B / 2)), dim3(256), 0, st, f); break;
     default: MX_LAUNCH(f3_fc1_kernel, dim3((9216 / kF3Chunk) * 4), dim3(256), 0, st, f); break;
   }
 }
