@@ -87,6 +87,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--tensorboard-dir", type=str, default="",
                    help="write TensorBoard event files here (TF2 TensorBoard callback; rank 0 only)")
     p.add_argument("--histogram-freq", type=int, default=1, help="TensorBoard weight histograms every N epochs (0 = off)")
+    p.add_argument("--profile-batch", type=int, default=2,
+                   help="TensorBoard profile_batch: host + device trace of this batch of the first epoch into "
+                        "<tensorboard-dir>/plugins/profile (0 = off; only with --tensorboard-dir)")
     p.add_argument("--chainer-out", type=str, default="",
                    help="Chainer trainer extensions: LogReport (<dir>/log), PrintReport, dump_graph (<dir>/cg.dot)")
     p.add_argument("--summary", action="store_true", help="print a Keras-style model summary")
@@ -109,11 +112,21 @@ class _Reporter:
 
         main = inf.is_main
         self.tb = SummaryWriter(args.tensorboard_dir, enabled=main) if args.tensorboard_dir else None
+        from .utils.tensorboard import DeviceTrace
+
+        self.trace = DeviceTrace(args.tensorboard_dir, getattr(args, "profile_batch", 0), enabled=main)
+        self.first_epoch = None
         self.hist_freq = args.histogram_freq
         self.log = LogReport(args.chainer_out, enabled=main) if args.chainer_out else None
         self.pr = PrintReport(enabled=main, out=lambda s: print(s, flush=True)) if args.chainer_out else None
         self.graph_path = os.path.join(args.chainer_out, "cg.dot") if (args.chainer_out and main) else None
         self.t0 = time.time()
+
+    def around(self, epoch: int, bi: int, n: int = 1):
+        """Wrap a step call covering batches [bi, bi + n) of `epoch` (TensorBoard profile_batch)."""
+        if self.first_epoch is None:
+            self.first_epoch = epoch
+        return self.trace.around(epoch == self.first_epoch, bi, n)
 
     def first_loss(self, loss, model):
         if self.graph_path is not None and loss.grad_fn is not None:
@@ -471,7 +484,8 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
             if cuda and log and not profile:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
-            runner(x, y)
+            with rep.around(epoch, bi):
+                runner(x, y)
             if ev is not None:
                 ev[1].record()
             total += x.shape[0]
@@ -584,7 +598,8 @@ def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
         t_epoch = t_log = time.time()
         last_log = 0
         for bi, (x, y) in enumerate(loader):
-            group.step(x, y, loss_fn)
+            with rep.around(epoch, bi):
+                group.step(x, y, loss_fn)
             total += x.shape[0]
             step += 1
             if bi % args.log_interval == 0:
@@ -672,7 +687,8 @@ def _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw):
         while bi < nb:
             if it is None:
                 n = 1 if bi % args.log_interval == 0 else min(args.log_interval - bi % args.log_interval, nb - bi)
-                rep.step(n)
+                with rep_.around(epoch, bi, n):
+                    rep.step(n)
             else:
                 x, y = next(it)
                 if x.shape[0] != bs:
@@ -680,7 +696,8 @@ def _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw):
                     continue
                 n = 1
                 rep.set_batch(x, y)
-                rep.step(1)
+                with rep_.around(epoch, bi):
+                    rep.step(1)
             bi += n
             step += n
             if (bi - 1) % args.log_interval == 0 or bi == nb:
@@ -802,7 +819,8 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
         if synthetic:
             while bi < nb:
                 n = 1 if bi % args.log_interval == 0 else min(args.log_interval - bi % args.log_interval, nb - bi)
-                tr.step(n)
+                with rep.around(epoch, bi, n):
+                    tr.step(n)
                 bi += n
                 step += n
                 if (bi - 1) % args.log_interval == 0 or bi == nb:
@@ -823,7 +841,8 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
                 if x.shape[0] != bs:
                     continue  # the captured graph has a fixed batch (drop_last semantics)
                 tr.set_batch(x, y)
-                tr.step(1)
+                with rep.around(epoch, bi):
+                    tr.step(1)
                 step += 1
                 if bi % args.log_interval == 0:
                     ls, cs = tr.read_metrics()

@@ -165,6 +165,75 @@ class SummaryWriter:
             self._f = None
 
 
+class DeviceTrace:
+    """The TF2 TensorBoard callback's ``profile_batch`` (tensorflow2/mnist_single.py:73 with TF's
+    default profile_batch=2 [framework]): a host + device trace of one training batch, written where
+    TensorBoard's profile plugin looks for it, ``<logdir>/plugins/profile/<run>/<host>.trace.json.gz``
+    (Chrome trace format).  The device side comes from the ROCm tracer behind ``torch.profiler``:
+    every HIP kernel of the step -- ours, RCCL's, graph replays included -- with its stream and
+    duration.  ``batch`` counts from 1 in the first epoch, as in Keras; 0 = off."""
+
+    def __init__(self, logdir: str, batch: int, enabled: bool = True):
+        self.logdir, self.batch, self.enabled = logdir, int(batch), enabled and bool(logdir) and int(batch) > 0
+        self.path = None
+        self._prof = None
+        self._done = False
+
+    def wants(self, first_epoch: bool, bi_lo: int, n: int = 1) -> bool:
+        """True if the step call covering batch indices [bi_lo, bi_lo + n) holds the traced batch."""
+        return self.enabled and not self._done and first_epoch and bi_lo <= self.batch - 1 < bi_lo + n
+
+    def start(self):
+        import torch
+        from torch.profiler import ProfilerActivity, profile
+
+        acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if torch.cuda.is_available() else [])
+        self._prof = profile(activities=acts)
+        self._prof.__enter__()
+
+    def stop(self):
+        import gzip
+        import shutil
+        import tempfile
+
+        import torch
+
+        if self._prof is None:
+            return None
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        self._prof.__exit__(None, None, None)
+        run = time.strftime("%Y_%m_%d_%H_%M_%S")
+        d = os.path.join(self.logdir, "plugins", "profile", run)
+        os.makedirs(d, exist_ok=True)
+        with tempfile.TemporaryDirectory() as td:
+            raw = os.path.join(td, "trace.json")
+            self._prof.export_chrome_trace(raw)
+            self.path = os.path.join(d, f"{socket.gethostname()}.trace.json.gz")
+            with open(raw, "rb") as fi, gzip.open(self.path, "wb") as fo:
+                shutil.copyfileobj(fi, fo)
+        self._prof = None
+        self._done = True
+        return self.path
+
+    def around(self, first_epoch: bool, bi_lo: int, n: int = 1):
+        """Context manager for one step call: traces it if it holds the profiled batch."""
+        tr = self
+
+        class _Ctx:
+            def __enter__(self):
+                self.on = tr.wants(first_epoch, bi_lo, n)
+                if self.on:
+                    tr.start()
+
+            def __exit__(self, *exc):
+                if self.on:
+                    tr.stop()
+                return False
+
+        return _Ctx()
+
+
 # ----------------------------------------------------------------------------- reader (tests / tools)
 def _read_varint(b: bytes, i: int) -> tuple[int, int]:
     v, s = 0, 0

@@ -176,3 +176,26 @@ def test_fused_keras_replicas_match_global_batch(cuda, graph):
         if p.is_alive():
             p.kill()
     assert bad == [], bad
+
+
+def test_tensorboard_profile_batch_has_device_kernels(cuda, tmp_path):
+    """TF2 TensorBoard profile_batch parity on the GPU path: the trace of batch 2 holds the fused
+    engine's HIP kernels (device activity from the ROCm tracer), not only host events."""
+    import glob
+    import gzip
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    td = tmp_path / "tb"
+    r = subprocess.run([sys.executable, "-m", "mxddp.train", "--model", "keras_cnn", "-e", "1", "--steps-per-epoch", "6",
+                        "--log-interval", "1", "-b", "32", "--tensorboard-dir", str(td)],
+                       cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    traces = glob.glob(str(td / "plugins" / "profile" / "*" / "*.trace.json.gz"))
+    assert len(traces) == 1, traces
+    ev = json.loads(gzip.open(traces[0]).read())["traceEvents"]
+    kernels = [e.get("name", "") for e in ev if e.get("cat") == "kernel"]
+    assert any("keras" in k for k in kernels), sorted(set(kernels))[:20]

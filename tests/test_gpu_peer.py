@@ -352,3 +352,47 @@ def test_fused_replicas_in_process_match_global_batch(cuda, graph):
         if p.is_alive():
             p.kill()
     assert bad == [], bad
+
+
+def _replicas_timeout_worker(q):
+    try:
+        import torch
+
+        from mxddp.models import MnistCNN
+        from mxddp.parallel.replica import FusedMnistReplicas
+
+        cuda = torch.device("cuda", 0)
+        torch.manual_seed(0)
+        rep = FusedMnistReplicas([cuda, cuda], batch=16, lr=0.05, init_model=MnistCNN(), use_graph=False)
+        for pc in rep.peers:
+            pc.set_timeout_ms(300)
+        bad = []
+        rep.trainers[0].eng.step()  # replica 1 never launches its step: replica 0's exchange must give up
+        try:
+            rep.synchronize()
+            bad.append("no error raised for a replica that never arrived")
+        except RuntimeError as e:
+            if "replica 1 never arrived" not in str(e):
+                bad.append(("wrong error", str(e)))
+        if rep.peers[0].error() != 2:
+            bad.append(("error word", rep.peers[0].error()))
+        q.put((0, bad, ""))
+    except Exception:
+        q.put((0, ["exception: " + traceback.format_exc()], ""))
+
+
+def test_fused_replicas_stalled_replica_fails_fast(cuda):
+    """A replica whose partner never runs its step (a hung device, a crashed thread) must not
+    hang the in-process replica group: the exchange kernel gives up at the peer timeout (here
+    300 ms instead of 30 s) and synchronize() names the missing replica."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_replicas_timeout_worker, args=(q,))
+    p.start()
+    try:
+        _, bad, _ = q.get(timeout=200)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert bad == [], bad

@@ -89,6 +89,14 @@ def test_tf2_script_writes_tensorboard_and_summary(tmp_path):
     assert (tmp_path / "td" / "ckpt_1.pth").exists() and "restored ckpt_1.pth" in out
     sd = torch.load(tmp_path / "td" / "ckpt_1.pth", weights_only=True)
     assert sum(v.numel() for v in sd.values()) == 93_322
+    # TensorBoard profile_batch=2: one trace of batch 2 where the profile plugin looks for it
+    import glob
+    import gzip
+
+    traces = glob.glob(str(tmp_path / "td" / "plugins" / "profile" / "*" / "*.trace.json.gz"))
+    assert len(traces) == 1, traces
+    tr = json.loads(gzip.open(traces[0]).read())
+    assert len(tr["traceEvents"]) > 0
 
 
 def test_chainer_script_writes_log_report_and_graph(tmp_path):
