@@ -105,6 +105,7 @@ def main():
     dev = inf.device
     comm = C.rccl_comm(force=a.force_collectives)
     B = a.batch
+    tr = None  # the fused engine, when one runs
 
     if a.model not in ("mnist_cnn", "keras_cnn") and a.impl == "fused":
         a.impl = "layers"

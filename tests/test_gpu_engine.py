@@ -200,6 +200,25 @@ def test_bench_json_reports_per_image_metrics(cuda):
     assert out["train_images"] >= 25 * 64, out
 
 
+@pytest.mark.parametrize("args", [["--model", "resnet50", "--dtype", "bf16", "--batch", "8"],
+                                  ["--model", "mlp", "--impl", "layers"]])
+def test_bench_json_layer_path(cuda, args):
+    """bench.py on the layer path (no fused engine): one JSON line with the graph flag (round 3
+    broke this for every non-fused model)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3", "--warmup", "2", *args],
+                       capture_output=True, text=True, timeout=240, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["value"] > 0 and out["config"]["model"] == args[1], out
+    assert "graph" in out["config"], out
+
+
 @pytest.mark.parametrize("variant", ["default", "Ring:c7", "Ring:c28", "Ring/Simple:c14"])
 def test_fused_engine_rccl_variants_ws1(cuda, variant):
     """Every xGMI-sized RCCL communicator variant (ncclCommInitRankConfig with pinned CTA counts,
