@@ -72,6 +72,10 @@ def parse():
                     help="GEMM precision of the layers path (headline is fp32, >= the reference's precision)")
     ap.add_argument("--cpu", action="store_true",
                     help="BASELINE config 1: single process on the CPU (the reference's single_gpu.py CPU fallback)")
+    ap.add_argument("--phase-profile", type=int, default=0, metavar="STEPS",
+                    help="fused MNIST engine: instead of the benchmark, print the in-kernel phase timings of STEPS "
+                         "eager steps (every block stamps its phase boundaries; shows the co-scheduled exchange "
+                         "blocks against the conv-backward blocks of the same launch)")
     ap.add_argument("--model", default="mnist_cnn",
                     help="headline: mnist_cnn (fused).  Others run the layers path: keras_cnn, mlp, pyramidnet110, resnet50")
     return ap.parse_args()
@@ -148,6 +152,13 @@ def main():
         if a.graph_mode is None and not a.no_autotune and tr.eng.reducer_active:
             tr.step(1)
             tr.autotune()  # untimed: a few real steps per candidate strategy, before the warm-up
+        if a.phase_profile:
+            prof = tr.phase_profile(a.phase_profile)
+            if inf.rank == 0:
+                print(json.dumps({"phase_profile": prof, "world_size": inf.world_size,
+                                  "buckets": getattr(tr, "bucket_strategy", None), "transport": tr.active_transport}, indent=1))
+            C.shutdown()
+            return
         if os.environ.get("MXDDP_WARM_GRAPHS", "1") == "1":
             tr.warm_graphs()  # untimed: first launch of every captured graph (real steps)
     else:

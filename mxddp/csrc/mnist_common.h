@@ -16,6 +16,9 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 __device__ __forceinline__ float sel4(const float4& v, int j) {
   return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
 }
+__device__ __forceinline__ int g1_slab_mask(const MnistFused& f) {
+  return (f.g1_slabs >= 1 && f.g1_slabs <= 64 ? f.g1_slabs : 16) - 1;
+}
 
 // Phase timestamps for in-kernel profiling (MnistFused::trace, off = null): blocks 0..1023 of
 // kernel `kid` record the 100 MHz wall clock at phase `ph` (<8) from thread 0.
@@ -32,12 +35,12 @@ struct Scratch {  // carve of MnistFused::scratch (floats)
   float* wacc;    // conv2 wgrad accumulator slabs [kWaccSlabs][9 r][64 co][32 ci], slab = image & (kWaccSlabs - 1)
   float* wu;      // conv2 dgrad Winograd filters G w' G^T (w' = w flipped) as F7W B-fragments
                   // [16 k-step][2 ci-half][64 lane][16 xi]
-  float* g1;      // conv1 grad partial slabs [kG1Slabs][320] (w[32][9] then b[32]), slab = image & (kG1Slabs - 1)
+  float* g1;      // conv1 grad partial slabs [kG1Slabs][320] (w[32][9] then b[32]), slab = image & (g1_slabs - 1)
   float* wv;      // conv2 forward Winograd filters G w G^T as F2W B-fragments
                   // [4 w][16 xi][2 s4][64 lane][4 j]
 };
 constexpr int kWinoPack = 16 * 2048;  // 16 Winograd-domain values per (co, ci)
-constexpr int kG1Slabs = 16;          // conv1-grad atomics spread over 16 slabs (image & 15)
+constexpr int kG1Slabs = 64;          // conv1-grad atomic slabs allocated (MnistFused::g1_slabs used)
 // conv2-wgrad atomics spread over 2 slabs (image & 1): the 64 images' blocks finish together and
 // same-address float atomics serialise, so one accumulator cost F6W a 3.5 us epilogue; the
 // finalize (in the SGD launch at world size 1) sums the slabs in a fixed order.  Measured at

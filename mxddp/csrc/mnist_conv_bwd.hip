@@ -580,7 +580,7 @@ __device__ __forceinline__ void f7_body(const MnistFused& f, const Scratch& sc, 
   __syncthreads();
   // one of 8 partial slabs (image & 7: 88 blocks per address instead of all 704 hammering
   // the same 320 words: same-address float atomics serialise at the memory side)
-  float* g1 = sc.g1 + (b & (kG1Slabs - 1)) * 320;
+  float* g1 = sc.g1 + (b & g1_slab_mask(f)) * 320;
   for (int i = tid; i < 320; i += 256) {
     const float v = red[i] + red[320 + i] + red[640 + i] + red[960 + i];
     const int ci = i / 10, k = i - ci * 10;
@@ -791,7 +791,7 @@ __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc,
     for (int k = 0; k < 10; ++k) red[(mg * 32 + ci) * 10 + k] = part[k];
   }
   __syncthreads();
-  float* g1 = sc.g1 + (b & (kG1Slabs - 1)) * 320;
+  float* g1 = sc.g1 + (b & g1_slab_mask(f)) * 320;
   for (int i = tid; i < 320; i += 256) {
     const float v = red[i] + red[320 + i];
     const int c = i / 10, k = i - c * 10;
@@ -817,12 +817,20 @@ template <bool kWino, int kF6WSplit = 1, bool kA1 = false, int kCoS = 1>
 __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scratch sc) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   if ((int)blockIdx.x < f.co_blocks) {
+    MX_TRACE_B(f, 5, 0, (int)blockIdx.x);  // trace: exchange blocks vs conv blocks of this launch
     peer_two_shot_f32_block(f.co_args, f.co_part, blockIdx.x, reinterpret_cast<uint32_t*>(sm));
+    MX_TRACE_B(f, 5, 1, (int)blockIdx.x);
     return;
   }
   const int bid = (int)blockIdx.x - f.co_blocks;
   const int n6 = (kWino ? 2 * kF6WSplit * kCoS : 9) * f.B;
   if (bid < n6) {
+    switch (f.f6_prio) {  // s_setprio takes an immediate
+      case 1: __builtin_amdgcn_s_setprio(1); break;
+      case 2: __builtin_amdgcn_s_setprio(2); break;
+      case 3: __builtin_amdgcn_s_setprio(3); break;
+      default: break;
+    }
     if (kWino)
       f6w_body<kF6WSplit, kA1, kCoS>(f, sc, sm, bid, n6);
     else
@@ -858,13 +866,17 @@ __global__ __launch_bounds__(256) void f8_finalize_kernel(MnistFused f, Scratch 
   } else if (blk < kF8Wacc + kF8G1) {
     const int j = (blk - kF8Wacc) * 256 + tid;  // conv1 w/b grads: fixed-order sum of the slabs
     if (j < 320) {
-      float v[kG1Slabs], s = 0.f;
+      const int ns = g1_slab_mask(f) + 1;
+      float s = 0.f;
+      for (int k0 = 0; k0 < ns; k0 += 16) {  // 16 loads in flight, fixed order
+        float v[16];
 #pragma unroll
-      for (int k = 0; k < kG1Slabs; ++k) v[k] = sc.g1[k * 320 + j];
+        for (int k = 0; k < 16; ++k) v[k] = k0 + k < ns ? sc.g1[(k0 + k) * 320 + j] : 0.f;
 #pragma unroll
-      for (int k = 0; k < kG1Slabs; ++k) {
-        s += v[k];
-        sc.g1[k * 320 + j] = 0.f;
+        for (int k = 0; k < 16; ++k) {
+          s += v[k];
+          if (k0 + k < ns) sc.g1[(k0 + k) * 320 + j] = 0.f;
+        }
       }
       f.g[L::w1 + j] = s;
     }
@@ -901,6 +913,14 @@ bool mnist_f7_wino() {
     return (e && std::string(e) == "direct") ? 0 : 1;
   }();
   return v == 1;
+}
+int mnist_f6w_prio() {
+  static const int v = [] {
+    const char* e = std::getenv("MXDDP_F6W_PRIO");
+    const int s = e ? std::atoi(e) : 0;
+    return (s >= 0 && s <= 3) ? s : 0;
+  }();
+  return v;
 }
 static int f6w_split() {
   static const int v = [] {

@@ -188,6 +188,8 @@ MnistFused MnistEngine::fused_args() const {
   // without gradient collectives F5 applies the fc1 weight update itself (no all-reduce has to
   // come between the gradient and the update)
   f.fc1_sgd = (variant_ == 1 && !reducer_->active() && mnist_f5_sgd()) ? 1 : 0;
+  f.g1_slabs = mnist_g1_slabs();
+  f.f6_prio = mnist_f6w_prio();
   f.mom = m_;
   f.lr = lr_;
   f.sgd_mom = momentum_;

@@ -514,27 +514,30 @@ __global__ __launch_bounds__(256) void f3k_fc1_kernel(MnistFused f) {
 // operands issued up front, two accumulator chains), the 4 wave partials are summed in LDS, and
 // one atomic per output per block remains: 8-way per output instead of 64-way (65 K atomics per
 // step instead of 524 K -- the 144-chunk kernel's time was mostly its atomics draining).
-constexpr int kF3TChunks = 8, kF3TK = 9216 / kF3TChunks, kF3TW = kF3TK / 4, kF3TS = kF3TW / 16;
-__global__ __launch_bounds__(256) void f3t_fc1_kernel(MnistFused f) {
+constexpr int kF3TChunks = 8, kF3TK = 9216 / kF3TChunks;
+// kWv = waves per block (4: 288-deep K slices; 8: 144-deep slices, twice the loads in flight per CU)
+template <int kWv>
+__global__ __launch_bounds__(64 * kWv) void f3t_fc1_kernel(MnistFused f) {
   MX_TRACE(f, 1, 0);
-  __shared__ float red[4][16][17];
+  constexpr int kTW = kF3TK / kWv, kTS = kTW / 16;
+  __shared__ float red[kWv][16][17];
   const int tiles = f.B / 2;  // (B / 16) row tiles x 8 column tiles
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int kc = bid / tiles, tile = bid - kc * tiles, mt = tile >> 3, nt = tile & 7;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
   if (f.synth && blockIdx.x == 0 && tid == 0) *f.counter += 1;  // F2 consumed it
-  const int k0 = kc * kF3TK + w * kF3TW + 4 * g;
+  const int k0 = kc * kF3TK + w * kTW + 4 * g;
   const float4* A = reinterpret_cast<const float4*>(f.pool + (size_t)(16 * mt + m) * 9216 + k0);
   const float4* W = reinterpret_cast<const float4*>(f.p + L::fw1 + (size_t)(16 * nt + m) * 9216 + k0);
-  float4 av[kF3TS], bv[kF3TS];
+  float4 av[kTS], bv[kTS];
 #pragma unroll
-  for (int s = 0; s < kF3TS; ++s) {
+  for (int s = 0; s < kTS; ++s) {
     av[s] = A[4 * s];
     bv[s] = W[4 * s];
   }
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-  for (int s = 0; s < kF3TS; ++s) {
+  for (int s = 0; s < kTS; ++s) {
     acc[0] = mfma4(av[s].x, bv[s].x, acc[0]);
     acc[1] = mfma4(av[s].y, bv[s].y, acc[1]);
     acc[0] = mfma4(av[s].z, bv[s].z, acc[0]);
@@ -543,21 +546,22 @@ __global__ __launch_bounds__(256) void f3t_fc1_kernel(MnistFused f) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) red[w][4 * g + j][m] = acc[0][j] + acc[1][j];
   __syncthreads();
-  {
+  if (tid < 256) {
     const int row = tid >> 4, col = tid & 15;
-    const float v = (red[0][row][col] + red[1][row][col]) + (red[2][row][col] + red[3][row][col]);
+    float v = (red[0][row][col] + red[1][row][col]) + (red[2][row][col] + red[3][row][col]);
+    if constexpr (kWv == 8) v += (red[4][row][col] + red[5][row][col]) + (red[6][row][col] + red[7][row][col]);
     atomicAdd(f.h + (16 * mt + row) * 128 + 16 * nt + col, v);
   }
   // side job: zero the conv2-wgrad accumulator slabs for this step's F67 (see f3_fc1_kernel)
   {
     float4* wa = reinterpret_cast<float4*>(carve(f.scratch).wacc);
-    for (int i = blockIdx.x * 256 + tid; i < kWaccSlabs * kPack / 4; i += gridDim.x * 256)
+    for (int i = blockIdx.x * 64 * kWv + tid; i < kWaccSlabs * kPack / 4; i += gridDim.x * 64 * kWv)
       wa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   MX_TRACE(f, 1, 1);
 }
 
-// fc1-forward tiling (MXDDP_F3 = tile (default) | 144 | 576x32 | 576x16 | 384x16 | 256x16)
+// fc1-forward tiling (MXDDP_F3 = tile (default) | tile8 | 144 | 576x32 | 576x16 | 384x16 | 256x16)
 static int f3_variant() {
   static const int v = [] {
     const char* e = std::getenv("MXDDP_F3");
@@ -567,6 +571,7 @@ static int f3_variant() {
     if (s == "576x16") return 2;
     if (s == "384x16") return 3;
     if (s == "256x16") return 4;
+    if (s == "tile8") return 6;
     return 5;
   }();
   return v;
@@ -578,7 +583,8 @@ static void launch_f3(const MnistFused& f, hipStream_t st) {
     case 2: MX_LAUNCH((f3k_fc1_kernel<576, 16>), dim3(16 * 8), dim3(256), 0, st, f); break;
     case 3: MX_LAUNCH((f3k_fc1_kernel<384, 16>), dim3(24 * 8), dim3(256), 0, st, f); break;
     case 4: MX_LAUNCH((f3k_fc1_kernel<256, 16>), dim3(36 * 8), dim3(256), 0, st, f); break;
-    case 5: MX_LAUNCH(f3t_fc1_kernel, dim3(kF3TChunks * (f.B / 2)), dim3(256), 0, st, f); break;
+    case 5: MX_LAUNCH(f3t_fc1_kernel<4>, dim3(kF3TChunks * (f.B / 2)), dim3(256), 0, st, f); break;
+    case 6: MX_LAUNCH(f3t_fc1_kernel<8>, dim3(kF3TChunks * (f.B / 2)), dim3(512), 0, st, f); break;
     default: MX_LAUNCH(f3_fc1_kernel, dim3((9216 / kF3Chunk) * 4), dim3(256), 0, st, f); break;
   }
 }
@@ -905,19 +911,23 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
     float4 gv = g4[i];
     if (kFin && i < kW2a) {  // conv1 w/b: fixed-order sum of the 8 slabs
       float4* sl = reinterpret_cast<float4*>(sc.g1) + i;
-      float4 v[kG1Slabs];
+      const int ns = g1_slab_mask(f) + 1;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int k0 = 0; k0 < ns; k0 += 16) {  // 16 loads in flight, fixed order
+        float4 v[16];
 #pragma unroll
-      for (int k = 0; k < kG1Slabs; ++k) v[k] = sl[k * 80];
-      float4 a = v[0];
+        for (int k = 0; k < 16; ++k) v[k] = k0 + k < ns ? sl[(k0 + k) * 80] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int k = 1; k < kG1Slabs; ++k) {
-        a.x += v[k].x;
-        a.y += v[k].y;
-        a.z += v[k].z;
-        a.w += v[k].w;
+        for (int k = 0; k < 16; ++k) {
+          a.x += v[k].x;
+          a.y += v[k].y;
+          a.z += v[k].z;
+          a.w += v[k].w;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if (k0 + k < ns) sl[(k0 + k) * 80] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
-#pragma unroll
-      for (int k = 0; k < kG1Slabs; ++k) sl[k * 80] = make_float4(0.f, 0.f, 0.f, 0.f);
       gv = a;
       g4[i] = gv;
     }
@@ -987,6 +997,15 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
 using namespace mnist;
 
 size_t mnist_fused_scratch_floats(int B) { return scratch_floats(B); }
+
+int mnist_g1_slabs() {
+  static const int v = [] {
+    const char* e = std::getenv("MXDDP_G1_SLABS");
+    const int s = e ? std::atoi(e) : 16;
+    return (s == 8 || s == 16 || s == 32 || s == 64) ? s : 16;
+  }();
+  return v;
+}
 
 static void check(const MnistFused& f) {
   MX_CHECK(f.B % 16 == 0 && f.B >= 16 && f.B <= 128, "fused MNIST engine needs batch % 16 == 0 and 16 <= B <= 128");

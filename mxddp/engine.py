@@ -369,7 +369,7 @@ class FusedMnistTrainer:
         boundaries.  Returns per kernel: block start spread (us after the first block started;
         median / max), block duration (median / max) and the median time from block start to
         each phase mark."""
-        names = ["F2_fwd", "F3_fc1", "F5_head_fc1bwd", "F6_wgrad", "F7_dgrad"]
+        names = ["F2_fwd", "F3_fc1", "F5_head_fc1bwd", "F6_wgrad", "F7_dgrad", "CO_exchange"]
         buf = torch.zeros(7 * 1024 * 8, dtype=torch.int32, device=self.device)
         self.eng.set_trace(buf.data_ptr())
         acc = {n: [] for n in names}
@@ -380,6 +380,21 @@ class FusedMnistTrainer:
                 self.eng.step()
                 self.eng.sync()
                 t = buf.view(7, 1024, 8).cpu().to(torch.int64) & 0xFFFFFFFF
+                # one time base for the conv-backward launch (F6 / F7 blocks and the co-scheduled
+                # exchange blocks share it): [first start, median end, last end] per block kind
+                t67 = t[3:6]
+                live67 = t67[:, :, 0] != 0
+                if live67[2].any():
+                    o = t67[:, :, 0][live67].min()
+                    win = {}
+                    for k, n in ((3, "F6_wgrad"), (4, "F7_dgrad"), (5, "CO_exchange")):
+                        lv = t[k, :, 0] != 0
+                        if lv.any():
+                            end = t[k][lv].max(dim=1).values
+                            win[n] = [round((t[k, :, 0][lv].min() - o).item() * 0.01, 2),
+                                      round((end.double().median() - o).item() * 0.01, 2),
+                                      round((end.max() - o).item() * 0.01, 2)]
+                    acc.setdefault("_f67_window", []).append(win)
                 for k, n in enumerate(names):
                     t0 = t[k, :, 0]
                     live = t0 != 0
@@ -404,6 +419,10 @@ class FusedMnistTrainer:
         finally:
             self.eng.set_trace(0)
         out = {}
+        wins = acc.pop("_f67_window", [])[1:]
+        if wins:  # [start, median end, last end] us after the conv-backward launch's first block
+            out["F67_launch_window"] = {n: [round(sum(w[n][i] for w in wins) / len(wins), 2) for i in range(3)]
+                                        for n in wins[0] if all(n in w for w in wins)}
         for n, runs in acc.items():
             runs = runs[1:]  # drop the first (cold) step
             if not runs:
