@@ -38,6 +38,8 @@ struct Scratch {  // carve of MnistFused::scratch (floats)
   float* g1;      // conv1 grad partial slabs [kG1Slabs][320] (w[32][9] then b[32]), slab = image & (g1_slabs - 1)
   float* wv;      // conv2 forward Winograd filters G w G^T as F2W B-fragments
                   // [4 w][16 xi][2 s4][64 lane][4 j]
+  float* wslab;   // conv2 wgrad per-image slabs [B][64 co][32 ci][9 tap] (canonical order), written
+                  // with plain stores by F6W (MnistFused::wslab), summed by the finalize
 };
 constexpr int kWinoPack = 16 * 2048;  // 16 Winograd-domain values per (co, ci)
 constexpr int kG1Slabs = 64;          // conv1-grad atomic slabs allocated (MnistFused::g1_slabs used)
@@ -55,10 +57,49 @@ __host__ __device__ inline Scratch carve(float* s) {
   c.g1 = c.wu + kWinoPack;
   c.wv = c.g1 + kG1Slabs * 320;
   c.wacc = c.wv + kWinoPack;
+  c.wslab = c.wacc + kWaccSlabs * kPack;
   return c;
 }
-inline size_t scratch_floats(int) {
-  return 2 * (size_t)kPack + 2 * (size_t)kWinoPack + (size_t)kG1Slabs * 320 + (size_t)kWaccSlabs * kPack;
+inline size_t scratch_floats(int B) {
+  return 2 * (size_t)kPack + 2 * (size_t)kWinoPack + (size_t)kG1Slabs * 320 + (size_t)kWaccSlabs * kPack +
+         (size_t)B * kPack;
+}
+
+// conv2 weight gradient of pairs 4 grp .. 4 grp + 3 (36 consecutive floats of the canonical
+// [co][ci][ky][kx] layout) summed over the B per-image slabs in a fixed order -> gs[36] (LDS).
+// Threads t < 144: float4 q = t % 9 of the group, image subgroup sg = t / 9 sums images sg,
+// sg + 16, ... (4 loads in flight per round, clamped + masked: no load behind a branch); the 16
+// subgroup partials are added in order.  red: 576 floats of LDS.
+constexpr int kWslabGroups = 512;  // 2048 pairs / 4
+__device__ __forceinline__ void wslab_group_sum(const MnistFused& f, const Scratch& sc, int grp, float* red, float* gs) {
+  const int t = threadIdx.x;
+  if (t < 144) {
+    const int q = t % 9, sg = t / 9, nb = f.B / 16;
+    const float4* src = reinterpret_cast<const float4*>(sc.wslab) + grp * 9 + q;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i0 = 0; i0 < nb; i0 += 4) {
+      float4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = src[(size_t)min(sg + 16 * (i0 + i), f.B - 1) * (kPack / 4)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool in = i0 + i < nb;
+        a.x += in ? v[i].x : 0.f;
+        a.y += in ? v[i].y : 0.f;
+        a.z += in ? v[i].z : 0.f;
+        a.w += in ? v[i].w : 0.f;
+      }
+    }
+    reinterpret_cast<float4*>(red)[sg * 9 + q] = a;
+  }
+  __syncthreads();
+  if (t < 36) {
+    float s = red[t];
+#pragma unroll
+    for (int sg = 1; sg < 16; ++sg) s += red[sg * 36 + t];
+    gs[t] = s;
+  }
+  __syncthreads();
 }
 
 }  // namespace mnist

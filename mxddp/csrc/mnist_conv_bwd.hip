@@ -400,6 +400,13 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
         atomicAdd(wa + (k * 64 + cj) * 32 + ci, o[j][k] + xch[((pw * 2 + jl) * 9 + k) * 64 + lane]);
     }
   } else {
+  // f.wslab (kF6WSplit == 1): this block's [64 co][16 ci][9] result is staged in LDS (over the
+  // idle operand tiles) and written to the image's slab in canonical [co][ci][ky][kx] order with
+  // coalesced 16-byte stores -- no atomics (the atomic epilogue was ~3 us and delayed the F7
+  // blocks' own atomics behind it); the finalize sums the B slabs in a fixed order
+  const bool slab = kF6WSplit == 1 && f.wslab;
+  float* st = sm;  // [64 co][16 ci][9]
+  if (slab) __syncthreads();  // every wave's phase-C reads of the operand tiles are done
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int cj = 16 * w + 4 * g + j;
@@ -416,9 +423,27 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
       const float o0 = t[ky][0] + 0.5f * (t[ky][1] + t[ky][2]);
       const float o1 = 0.5f * (t[ky][1] - t[ky][2]);
       const float o2 = 0.5f * (t[ky][1] + t[ky][2]) + t[ky][3];
-      atomicAdd(wa + ((ky * 3 + 0) * 64 + cj) * 32 + ci, o0);
-      atomicAdd(wa + ((ky * 3 + 1) * 64 + cj) * 32 + ci, o1);
-      atomicAdd(wa + ((ky * 3 + 2) * 64 + cj) * 32 + ci, o2);
+      if (slab) {
+        float* sp = st + (cj * 16 + m) * 9 + 3 * ky;
+        sp[0] = o0;
+        sp[1] = o1;
+        sp[2] = o2;
+      } else {
+        atomicAdd(wa + ((ky * 3 + 0) * 64 + cj) * 32 + ci, o0);
+        atomicAdd(wa + ((ky * 3 + 1) * 64 + cj) * 32 + ci, o1);
+        atomicAdd(wa + ((ky * 3 + 2) * 64 + cj) * 32 + ci, o2);
+      }
+    }
+  }
+  if (slab) {
+    __syncthreads();
+    // per co: 16 ci x 9 taps = 144 contiguous floats (36 float4) at (co * 32 + 16 h) * 9
+    const float4* s4 = reinterpret_cast<const float4*>(st);
+    float4* d4 = reinterpret_cast<float4*>(sc.wslab + (size_t)b * kPack + 144 * h);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int i = tid + 256 * k, co = i / 36, q = i - 36 * co;
+      d4[co * 72 + q] = s4[i];
     }
   }
   }
@@ -825,12 +850,6 @@ __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scr
   const int bid = (int)blockIdx.x - f.co_blocks;
   const int n6 = (kWino ? 2 * kF6WSplit * kCoS : 9) * f.B;
   if (bid < n6) {
-    switch (f.f6_prio) {  // s_setprio takes an immediate
-      case 1: __builtin_amdgcn_s_setprio(1); break;
-      case 2: __builtin_amdgcn_s_setprio(2); break;
-      case 3: __builtin_amdgcn_s_setprio(3); break;
-      default: break;
-    }
     if (kWino)
       f6w_body<kF6WSplit, kA1, kCoS>(f, sc, sm, bid, n6);
     else
@@ -851,7 +870,17 @@ __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scr
 // per thread.  Blocks 74..: zero h.
 constexpr int kF8Wacc = kPack / 256, kF8G1 = 2;
 __global__ __launch_bounds__(256) void f8_finalize_kernel(MnistFused f, Scratch sc) {
-  const int blk = blockIdx.x, tid = threadIdx.x;
+  __shared__ float red[576 + 36];
+  const int tid = threadIdx.x;
+  int blk = blockIdx.x;
+  if (f.wslab) {  // blocks 0 .. 511: the fixed-order slab sum, 4 (co, ci) pairs each
+    if (blk < kWslabGroups) {
+      wslab_group_sum(f, sc, blk, red, red + 576);
+      if (tid < 36) f.g[L::w2 + 36 * blk + tid] = red[576 + tid];
+      return;
+    }
+    blk += kF8Wacc - kWslabGroups;  // the remaining blocks as in the atomic layout
+  }
   if (blk < kF8Wacc) {
     const int i = blk * 256 + tid;
     const int co = i / 288, rem = i - co * 288, ci = rem / 9, rr = rem - ci * 9;
@@ -869,14 +898,14 @@ __global__ __launch_bounds__(256) void f8_finalize_kernel(MnistFused f, Scratch 
       const int ns = g1_slab_mask(f) + 1;
       float s = 0.f;
       for (int k0 = 0; k0 < ns; k0 += 16) {  // 16 loads in flight, fixed order
-        float v[16];
+        float v[16];  // clamped loads, masked adds: no load behind a branch
 #pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = k0 + k < ns ? sc.g1[(k0 + k) * 320 + j] : 0.f;
+        for (int k = 0; k < 16; ++k) v[k] = sc.g1[min(k0 + k, ns - 1) * 320 + j];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          s += v[k];
+        for (int k = 0; k < 16; ++k) s += k0 + k < ns ? v[k] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
           if (k0 + k < ns) sc.g1[(k0 + k) * 320 + j] = 0.f;
-        }
       }
       f.g[L::w1 + j] = s;
     }
@@ -914,13 +943,15 @@ bool mnist_f7_wino() {
   }();
   return v == 1;
 }
-int mnist_f6w_prio() {
+static int f6w_split();
+static int f6w_cos();
+bool mnist_wslab() {
   static const int v = [] {
-    const char* e = std::getenv("MXDDP_F6W_PRIO");
-    const int s = e ? std::atoi(e) : 0;
-    return (s >= 0 && s <= 3) ? s : 0;
+    const char* e = std::getenv("MXDDP_WSLAB");
+    return (e && std::string(e) == "0") ? 0 : 1;
   }();
-  return v;
+  // the slab epilogue exists in the unsplit, non-co-split Winograd weight-gradient blocks only
+  return v == 1 && mnist_f7_wino() && f6w_split() == 1 && f6w_cos() == 1;
 }
 static int f6w_split() {
   static const int v = [] {
@@ -975,7 +1006,8 @@ void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_
     constexpr size_t lds = kF6Lds > kF7Lds ? kF6Lds : kF7Lds;
     MX_LAUNCH(f67_conv2_bwd_kernel<false>, dim3(f.co_blocks + 9 * f.B + 11 * f.B), dim3(256), lds, st, f, sc);
   }
-  if (!finalize_in_sgd) MX_LAUNCH(f8_finalize_kernel, dim3(kF8Wacc + kF8G1 + 8), dim3(256), 0, st, f, sc);
+  if (!finalize_in_sgd)
+    MX_LAUNCH(f8_finalize_kernel, dim3((f.wslab ? kWslabGroups : kF8Wacc) + kF8G1 + 8), dim3(256), 0, st, f, sc);
   MX_HIP_CHECK(hipGetLastError());
 }
 

@@ -43,12 +43,12 @@ struct MnistFused {
   // conv1-grad atomic slabs in use (power of two <= kG1SlabsMax; MXDDP_G1_SLABS): F7 blocks of
   // image b add into slab b & (g1_slabs - 1), the finalize sums them in a fixed order
   int g1_slabs;
-  // wave priority of the conv2 weight-gradient blocks in the shared conv-backward launch
-  // (MXDDP_F6W_PRIO, 0..3): they are its long pole, the data-gradient blocks have slack
-  int f6_prio;
+  // 1: F6W writes its conv2 weight gradient as per-image slabs with plain stores (no atomics)
+  // and the finalize (F8 / the folded SGD) sums them in a fixed order; 0: slab atomics (wacc)
+  int wslab;
 };
 int mnist_g1_slabs();
-int mnist_f6w_prio();
+bool mnist_wslab();  // default on; MXDDP_WSLAB=0 (and the split / co-split / direct F6 variants) use atomics
 bool mnist_a1_publish();  // default on; MXDDP_MNIST_A1=recompute turns it off
 bool mnist_f5_sgd();      // default on; MXDDP_F5_SGD=0 keeps the fc1 update in the SGD launch
 

@@ -439,7 +439,7 @@ __global__ __launch_bounds__(256) void f3_fc1_kernel(MnistFused f) {
   }
   // side job: zero the conv2-wgrad accumulator slabs for this step's F67 (last step's finalize
   // has read them; one float4 per thread, so the finalize's serial tail carries no stores)
-  {
+  if (!f.wslab) {
     float4* wa = reinterpret_cast<float4*>(carve(f.scratch).wacc);
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < kWaccSlabs * kPack / 4) wa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -499,7 +499,7 @@ __global__ __launch_bounds__(256) void f3k_fc1_kernel(MnistFused f) {
     }
   }
   // side job: zero the conv2-wgrad accumulator slabs for this step's F67 (see f3_fc1_kernel)
-  {
+  if (!f.wslab) {
     float4* wa = reinterpret_cast<float4*>(carve(f.scratch).wacc);
     for (int i = blockIdx.x * 256 + tid; i < kWaccSlabs * kPack / 4; i += gridDim.x * 256)
       wa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -553,7 +553,7 @@ __global__ __launch_bounds__(64 * kWv) void f3t_fc1_kernel(MnistFused f) {
     atomicAdd(f.h + (16 * mt + row) * 128 + 16 * nt + col, v);
   }
   // side job: zero the conv2-wgrad accumulator slabs for this step's F67 (see f3_fc1_kernel)
-  {
+  if (!f.wslab) {
     float4* wa = reinterpret_cast<float4*>(carve(f.scratch).wacc);
     for (int i = blockIdx.x * 64 * kWv + tid; i < kWaccSlabs * kPack / 4; i += gridDim.x * 64 * kWv)
       wa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -561,7 +561,7 @@ __global__ __launch_bounds__(64 * kWv) void f3t_fc1_kernel(MnistFused f) {
   MX_TRACE(f, 1, 1);
 }
 
-// fc1-forward tiling (MXDDP_F3 = tile (default) | tile8 | 144 | 576x32 | 576x16 | 384x16 | 256x16)
+// fc1-forward tiling (MXDDP_F3 = tile8 (default) | tile | 144 | 576x32 | 576x16 | 384x16 | 256x16)
 static int f3_variant() {
   static const int v = [] {
     const char* e = std::getenv("MXDDP_F3");
@@ -571,8 +571,8 @@ static int f3_variant() {
     if (s == "576x16") return 2;
     if (s == "384x16") return 3;
     if (s == "256x16") return 4;
-    if (s == "tile8") return 6;
-    return 5;
+    if (s == "tile") return 5;
+    return 6;  // tile8 (measured: 6.7 vs 7.9 us, 902k vs 884k img/s, profiles/r3_mnist_knobs)
   }();
   return v;
 }
@@ -891,20 +891,48 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
                                                        const float* __restrict__ lr_ptr, float gscale, float mom,
                                                        float wd, bool pack_direct) {
   const float lr = *lr_ptr;
+  // kFin + f.wslab: the last kWslabGroups blocks sum the conv2 weight-gradient slabs (4 (co, ci)
+  // pairs each, fixed order) and update + repack those pairs; the other nflat blocks do the rest
+  const int ngrp = (kFin && f.wslab) ? kWslabGroups : 0, nflat = (int)gridDim.x - ngrp;
+  if ((int)blockIdx.x >= nflat) {
+    __shared__ float red[576 + 36];
+    const int grp = (int)blockIdx.x - nflat;
+    wslab_group_sum(f, sc, grp, red, red + 576);
+    if (threadIdx.x < 4) {
+      const int pair = 4 * grp + (int)threadIdx.x, e0 = (int)L::w2 + pair * 9;
+      float pe[9], bb[9];
+#pragma unroll
+      for (int r = 0; r < 9; ++r) {
+        pe[r] = f.p[e0 + r];
+        bb[r] = buf[e0 + r];
+      }
+#pragma unroll
+      for (int r = 0; r < 9; ++r) {
+        const float gg = red[576 + 9 * threadIdx.x + r];
+        bb[r] = mom * bb[r] + (gg * gscale + wd * pe[r]);
+        pe[r] -= lr * bb[r];
+        f.g[e0 + r] = gg;
+        buf[e0 + r] = bb[r];
+        f.p[e0 + r] = pe[r];
+      }
+      conv2_pack_pair(sc, pair, pe, pack_direct);
+    }
+    return;
+  }
   float4* p4 = reinterpret_cast<float4*>(f.p);
   float4* g4 = reinterpret_cast<float4*>(f.g);
   float4* b4 = reinterpret_cast<float4*>(buf);
   constexpr int n4 = (int)(L::total / 4);  // 299970 float4 (total = 1199882 = 4*299970 + 2)
   if (kFin) {
     float4* h4 = reinterpret_cast<float4*>(f.h);
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < f.B * 32; i += gridDim.x * 256)
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < f.B * 32; i += nflat * 256)
       h4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   constexpr int kW2a = (int)L::w2 / 4, kW2b = ((int)L::w2 + kPack) / 4;  // conv2 weights (float4 range)
   constexpr int kF1a = (int)L::fw1 / 4, kF1n = ((int)L::fb1 - (int)L::fw1) / 4;  // fc1 weights (float4 range)
   static_assert(L::fw1 % 4 == 0 && L::fb1 % 4 == 0, "fc1 weights must be float4-aligned");
   const int skip = f.fc1_sgd ? kF1n : 0;  // fc1 updated by F5: iterate around it
-  for (int t = blockIdx.x * 256 + threadIdx.x; t < n4 - skip; t += gridDim.x * 256) {
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < n4 - skip; t += nflat * 256) {
     const int i = t >= kF1a ? t + skip : t;
     if (i >= kW2a && i < kW2b) continue;  // per (co, ci) pair below
     float4 pv = p4[i];
@@ -914,15 +942,16 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
       const int ns = g1_slab_mask(f) + 1;
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
       for (int k0 = 0; k0 < ns; k0 += 16) {  // 16 loads in flight, fixed order
-        float4 v[16];
+        float4 v[16];  // clamped loads, masked adds: no load behind a branch
 #pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = k0 + k < ns ? sl[(k0 + k) * 80] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = 0; k < 16; ++k) v[k] = sl[min(k0 + k, ns - 1) * 80];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-          a.x += v[k].x;
-          a.y += v[k].y;
-          a.z += v[k].z;
-          a.w += v[k].w;
+          const bool in = k0 + k < ns;
+          a.x += in ? v[k].x : 0.f;
+          a.y += in ? v[k].y : 0.f;
+          a.z += in ? v[k].z : 0.f;
+          a.w += in ? v[k].w : 0.f;
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k)
@@ -948,8 +977,8 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
   // (kFin: the gradient is summed straight from the [slab][tap][co][ci] accumulator).
   // The pairs go to wave 0 of the grid's last 32 blocks (one main-loop pass each: 32 CUs share
   // the scattered stores); all 27 loads are issued before any store.
-  const int pair = ((int)blockIdx.x - ((int)gridDim.x - 32)) * 64 + (int)threadIdx.x;
-  if (blockIdx.x + 32 >= gridDim.x && threadIdx.x < 64 && pair >= 0 && pair < 2048) {
+  const int pair = ((int)blockIdx.x - (nflat - 32)) * 64 + (int)threadIdx.x;
+  if (ngrp == 0 && (int)blockIdx.x + 32 >= nflat && threadIdx.x < 64 && pair >= 0 && pair < 2048) {
     const int co = pair >> 5, ci = pair & 31, e0 = (int)L::w2 + pair * 9;
     float gg[9], pe[9], bb[9];
     if (kFin) {  // fixed-order sum of the accumulator slabs
@@ -1077,7 +1106,8 @@ void mnist_fused_sgd(const MnistFused& f, float* mom_buf, const float* lr, float
                      hipStream_t st, bool finalize) {
   MX_CHECK(!f.fc1_sgd || (finalize && gscale == 1.f && f.mom == mom_buf),
            "fc1 SGD is folded into F5 only without gradient collectives");
-  const dim3 grid(f.fc1_sgd ? 128 : 1024);  // folded: ~20 K elements left (+ the 32 pair blocks)
+  // folded: ~20 K elements left (+ the 32 pair blocks, or the 512 slab-sum pair-group blocks)
+  const dim3 grid((f.fc1_sgd ? 128 : 1024) + (finalize && f.wslab ? kWslabGroups : 0));
   if (finalize)
     MX_LAUNCH(sgd_pack_kernel<true>, grid, dim3(256), 0, st, f, carve(f.scratch), mom_buf, lr, gscale,
               momentum, wd, !(f2_wino() && mnist_f7_wino()));
