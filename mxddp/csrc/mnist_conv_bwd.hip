@@ -629,6 +629,9 @@ __device__ __forceinline__ void f7_body(const MnistFused& f, const Scratch& sc, 
 // reduced in registers -> lanes -> LDS -> slab atomics (slab = image & 7).
 constexpr int kF7WChunks = 6, kF7WRows = 5, kF7WCols = 14, kF7WCoP = 80;
 constexpr size_t kF7WLds = sizeof(float) * (64 * kF7WCoP + 784 + 320 + 640) + 64 * kF7WCoP;
+// kVq: the (value, code) LDS operands of k-step s + 1 are loaded during k-step s (the step's
+// scheduling barrier otherwise keeps every step waiting for its own LDS reads)
+template <bool kVq = false>
 __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc, float* sm, int braw, int nblk) {
   MX_TRACE_B(f, 4, 0, braw);
   float* dps = sm;                                      // [64 co][80]: 5 window rows x 14 cols
@@ -711,24 +714,51 @@ __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc,
     for (int s = 0; s < kF7WPf; ++s)
 #pragma unroll
       for (int k = 0; k < 4; ++k) bq[s][k] = wu[s * 512 + k];
+    float vn[4];
+    uint32_t qn[4];
+    if constexpr (kVq) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int o = (k >> 1) * kF7WCols + (k & 1);
+        vn[k] = dpp[o];
+        qn[k] = qp[o];
+      }
+    }
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       if (s + kF7WPf < 16) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) bq[s + kF7WPf][k] = wu[(s + kF7WPf) * 512 + k];
       }
+      float v[4];
+      uint32_t q[4];
+      if constexpr (kVq) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[k] = vn[k];
+          q[k] = qn[k];
+        }
+        if (s + 1 < 16) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int o = 4 * (s + 1) * kF7WCoP + (k >> 1) * kF7WCols + (k & 1);
+            vn[k] = dpp[o];
+            qn[k] = qp[o];
+          }
+        }
+      }
       // keep the prefetch at the top of the step: left alone the scheduler sinks these loads
       // next to their use and every k-step then waits for L2 (vmcnt(0)) before its MFMAs
       if (kF7WPin) __builtin_amdgcn_sched_barrier(0);
       const float4* bc = bq[s];
       const int off = 4 * s * kF7WCoP;  // co = 4s + g
-      float v[4];
-      uint32_t q[4];
+      if constexpr (!kVq) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {  // windows (a, c) = (k>>1, k&1) at +a*14 + c
-        const int o = off + (k >> 1) * kF7WCols + (k & 1);
-        v[k] = dpp[o];
-        q[k] = qp[o];
+        for (int k = 0; k < 4; ++k) {  // windows (a, c) = (k>>1, k&1) at +a*14 + c
+          const int o = off + (k >> 1) * kF7WCols + (k & 1);
+          v[k] = dpp[o];
+          q[k] = qp[o];
+        }
       }
       // d[r][c] = nonzero of window (r>>1, c>>1) if its argmax code is 2*(r&1) + (c&1)
       float d[4][4];
@@ -838,7 +868,7 @@ __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc,
 // the peers' matching blocks while the remaining blocks do the conv backward, so the 4.7 MB
 // exchange overlaps it inside ONE launch (no side stream, no cross-queue fence).  co_blocks is
 // a multiple of 8, so the conv part keeps its XCD-aware block mapping.
-template <bool kWino, int kF6WSplit = 1, bool kA1 = false, int kCoS = 1>
+template <bool kWino, int kF6WSplit = 1, bool kA1 = false, int kCoS = 1, bool kVq = false>
 __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scratch sc) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   if ((int)blockIdx.x < f.co_blocks) {
@@ -855,7 +885,7 @@ __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scr
     else
       f6_body(f, sc, sm, bid, n6);
   } else if (kWino) {
-    f7w_body(f, sc, sm, bid - n6, kF7WChunks * f.B);
+    f7w_body<kVq>(f, sc, sm, bid - n6, kF7WChunks * f.B);
   } else {
     f7_body(f, sc, sm, bid - n6, 11 * f.B);
   }
@@ -970,6 +1000,15 @@ static int f6w_cos() {
   return v;
 }
 
+// F7W operand prefetch one k-step ahead (MXDDP_F7W_VQ=1)
+static bool f7w_vq() {
+  static const int v = [] {
+    const char* e = std::getenv("MXDDP_F7W_VQ");
+    return (e && std::string(e) == "1") ? 1 : 0;
+  }();
+  return v == 1;
+}
+
 template <int kSplit>
 static void launch_f67_wino(const MnistFused& f, const Scratch& sc, hipStream_t st) {
   constexpr size_t lds = kF6WLds > kF7WLds ? kF6WLds : kF7WLds;
@@ -977,6 +1016,8 @@ static void launch_f67_wino(const MnistFused& f, const Scratch& sc, hipStream_t 
   const dim3 grid(f.co_blocks + 2 * kSplit * cos * f.B + kF7WChunks * f.B);
   if (kSplit == 1 && f.a1_pub && cos == 2)
     MX_LAUNCH((f67_conv2_bwd_kernel<true, 1, true, 2>), grid, dim3(256), lds, st, f, sc);
+  else if (kSplit == 1 && f.a1_pub && f7w_vq())
+    MX_LAUNCH((f67_conv2_bwd_kernel<true, 1, true, 1, true>), grid, dim3(256), lds, st, f, sc);
   else if (kSplit == 1 && f.a1_pub)
     MX_LAUNCH((f67_conv2_bwd_kernel<true, 1, true>), grid, dim3(256), lds, st, f, sc);
   else
@@ -988,6 +1029,7 @@ void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_
   if (!attr) {
     for (const void* fn : {reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 1>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 1, true>),
+                           reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 1, true, 1, true>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 1, true, 2>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 2>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 3>),

@@ -1,7 +1,7 @@
 #!/bin/bash
 # mxddp vs stock PyTorch-ROCm on the same GPU, same run: every model of the framework.
 source "$(dirname "$0")/gpu_check.sh"
-rm -f gpurun_out/steps.log
+[ -n "${KEEP_STEPS:-}" ] || rm -f gpurun_out/steps.log
 run cmp_mnist_mx 300 python bench.py --steps 2000 --warmup 100
 run cmp_mnist_torch 300 python bench.py --impl torch --steps 500 --warmup 50
 run cmp_keras_mx 300 python bench.py --model keras_cnn --steps 500 --warmup 50
