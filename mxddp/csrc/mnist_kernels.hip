@@ -273,6 +273,25 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int row0 = 2 * py;  // first input row of this block's conv1 rows
   float4 bq[kWino ? 4 : 18];
+  // ---- stage 1a: input rows row0 .. row0+5 (+ publish the rows this block owns).  Every global
+  // operand of stage 1 is requested in ONE round trip: the batch counter, conv1's weights and --
+  // synthetic data -- the 6 template rows of ALL 10 classes (the label, a function of the counter,
+  // then selects one in registers), instead of counter -> label -> template -> weights as four
+  // dependent trips.  Loads use clamped lanes (no per-lane branches) and the B fragments of stage 2 are
+  // issued after them, so waiting for stage 1 never drains the fragments (vmcnt counts in order).
+  const int own_lo = row0, own_hi = py == 11 ? 28 : row0 + 2;  // x rows written by this block
+  const int t42 = min(tid, 41), d = row0 * 28 + t42 * 4;
+  float w1v[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) w1v[k] = f.p[L::w1 + min(tid + 256 * k, 319)];
+  // (both data sources are requested whatever f.synth says -- counter, templates and x always
+  // exist -- so no load sits behind a branch whose join would make the waitcnt pass drain the
+  // B fragments too)
+  const uint32_t ctr = (uint32_t)*f.counter;
+  float4 tv[10];
+#pragma unroll
+  for (int c = 0; c < 10; ++c) tv[c] = *reinterpret_cast<const float4*>(f.tmpl + c * 784 + d);
+  const float4 xv = *reinterpret_cast<const float4*>(f.x + b * 784 + d);
   if constexpr (kWino) {  // F2W: first B fragments (points 0, 1) in flight during stage 1
     const float4* up = reinterpret_cast<const float4*>(sc.wv) + (size_t)w * 16 * 2 * 64 + lane;
 #pragma unroll
@@ -282,27 +301,36 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
 #pragma unroll
     for (int q = 0; q < 18; ++q) bq[q] = wf[q * 256];
   }
-  // ---- stage 1a: input rows row0 .. row0+5 (+ publish the rows this block owns)
-  const int own_lo = row0, own_hi = py == 11 ? 28 : row0 + 2;  // x rows written by this block
-  if (f.synth) {
-    const uint32_t ctr = (uint32_t)*f.counter;
+  __builtin_amdgcn_sched_barrier(0);  // every stage-1 load issued before the counter is consumed
+  {  // branch-free in f.synth (a branch would let the compiler sink the template loads behind
+     // the counter's round trip): both sources are formed, one is kept
     const uint2 key = synth_key(f.seed);
     const int label = synth_label(ctr, b, 10, key);
+    // masked sum, not `label == c ? tv[c] : t` (hipcc turns that select chain into tv[label]:
+    // a dynamically indexed array in scratch memory)
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int c = 0; c < 10; ++c) {
+      const float mk = (float)(label == c);
+      t.x = fmaf(mk, tv[c].x, t.x);
+      t.y = fmaf(mk, tv[c].y, t.y);
+      t.z = fmaf(mk, tv[c].z, t.z);
+      t.w = fmaf(mk, tv[c].w, t.w);
+    }
+    const uint4 r = synth_noise4(ctr, b, d, key);
+    const float4 sv = make_float4(0.5f * t.x + 0.5f * u01(r.x), 0.5f * t.y + 0.5f * u01(r.y),
+                                  0.5f * t.z + 0.5f * u01(r.z), 0.5f * t.w + 0.5f * u01(r.w));
+    const float4 v = f.synth ? sv : xv;
     if (tid < 42) {  // 6 rows x 28 = 168 pixels = 42 groups of 4
-      const int d = row0 * 28 + tid * 4;
-      const uint4 r = synth_noise4(ctr, b, d, key);
-      const float4 t = *reinterpret_cast<const float4*>(f.tmpl + label * 784 + d);
-      const float4 v = make_float4(0.5f * t.x + 0.5f * u01(r.x), 0.5f * t.y + 0.5f * u01(r.y),
-                                   0.5f * t.z + 0.5f * u01(r.z), 0.5f * t.w + 0.5f * u01(r.w));
       *reinterpret_cast<float4*>(xs + tid * 4) = v;
       const int row = d / 28;
-      if (row >= own_lo && row < own_hi) *reinterpret_cast<float4*>(f.x + b * 784 + d) = v;
+      if (f.synth && row >= own_lo && row < own_hi) *reinterpret_cast<float4*>(f.x + b * 784 + d) = v;
     }
-    if (py == 0 && tid == 0) f.y[b] = label;
-  } else if (tid < 42) {
-    *reinterpret_cast<float4*>(xs + tid * 4) = *reinterpret_cast<const float4*>(f.x + b * 784 + row0 * 28 + tid * 4);
+    if (f.synth && py == 0 && tid == 0) f.y[b] = label;
   }
-  for (int i = tid; i < 320; i += 256) w1s[i] = f.p[L::w1 + i];  // conv1 w [32][9] then b [32]
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+    if (tid + 256 * k < 320) w1s[tid + 256 * k] = w1v[k];  // conv1 w [32][9] then b [32]
   __syncthreads();
   MX_TRACE(f, 0, 1);
   // ---- stage 1b: conv1 + ReLU for 32 ci x 4 rows x 26 cols -> LDS tile, on MFMA: M = 104
@@ -604,10 +632,38 @@ static void launch_f3(const MnistFused& f, hipStream_t st) {
 // (dead windows -> 0) and db2 accumulated.  dh lives in LDS as [B][132] (row pitch = 4 mod 32
 // words: float4 row reads and 4-row-strided scalar reads are both bank-conflict free).
 // LDS at B = 64: 92 KB (one block per CU by design).
+// Up to 6 values held in NAMED registers across a long stretch of code: a plain array here
+// (F5's prefetched fc1 operands, live across the head) was placed in scratch memory and re-read
+// with dynamic offsets.  Accessed with compile-time k (inside fully unrolled loops).
+template <typename T>
+struct Reg6 {
+  T r0, r1, r2, r3, r4, r5;
+  __device__ __forceinline__ void set(int k, const T& x) {
+    switch (k) {
+      case 0: r0 = x; break;
+      case 1: r1 = x; break;
+      case 2: r2 = x; break;
+      case 3: r3 = x; break;
+      case 4: r4 = x; break;
+      default: r5 = x; break;
+    }
+  }
+  __device__ __forceinline__ T get(int k) const {
+    switch (k) {
+      case 0: return r0;
+      case 1: return r1;
+      case 2: return r2;
+      case 3: return r3;
+      case 4: return r4;
+      default: return r5;
+    }
+  }
+};
+
 constexpr int kF5Cols = 48, kF5NT = kF5Cols / 16, kF5C4 = kF5Cols / 4;
 constexpr int kF5DhP = 132, kF5P = 52, kF5W2P = 20, kF5LgP = 20;  // kF5P = 4 mod 8: 4-row groups 16 banks apart
 template <int B>
-__global__ __launch_bounds__(256) void f5_head_fc1_bwd_kernel(MnistFused f) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void f5_head_fc1_bwd_kernel(MnistFused f) {
   MX_TRACE(f, 2, 0);
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* dhs = sm;                       // [B][132]: h (post-ReLU), then dh in place
@@ -621,68 +677,69 @@ __global__ __launch_bounds__(256) void f5_head_fc1_bwd_kernel(MnistFused f) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
   // folded fc1 SGD: this block owns weight columns c0..c0+47 of every row (old values in wsm);
   // the momentum of this thread's dW1 elements is loaded with the prologue's loads
+  // Prologue in two groups so the head overlaps the fc1 operand loads: (1) the head's operands
+  // (h, b1, W2, b2, labels) are loaded, staged and consumed first; (2) this slice's pool / argmax
+  // / W1 (/ momentum) loads are issued right after group (1) and stay in flight (registers) while
+  // the head runs -- the head has no global loads of its own, so its waits never drain them --
+  // and are staged into LDS only after dh.  (Before: every load, then the head: ~3 us more.)
+  constexpr int ND = B * 32 / 256, NP = (B * kF5C4 + 255) / 256, NW = (128 * kF5C4 + 255) / 256, N2 = 5;
+  static_assert(NP <= 6 && NW <= 6, "F5 prefetch registers");
+  float4 vd[ND], vb1[ND];
+  Reg6<float4> vp, vw;
+  float v2[N2];
+  Reg6<uint32_t> vq;  // argmax codes, 4 per uint32
+#pragma unroll
+  for (int k = 0; k < ND; ++k) {
+    const int i = tid + 256 * k;
+    vd[k] = *reinterpret_cast<const float4*>(f.h + (i >> 5) * 128 + (i & 31) * 4);
+    vb1[k] = *reinterpret_cast<const float4*>(f.p + L::fb1 + (i & 31) * 4);
+  }
+#pragma unroll
+  for (int k = 0; k < N2; ++k) v2[k] = f.p[L::fw2 + tid + 256 * k];  // 1280 = 5 x 256
+  const int yv = f.y[tid < B ? tid : 0];
+  const float b2v = f.p[L::fb2 + (m < 10 ? m : 0)];
+  // group (2) strictly after group (1) in issue order: vmcnt counts in order, so a group-2 load
+  // scheduled in front of a head operand would be waited for before the head
+  __builtin_amdgcn_sched_barrier(0);
+  // (2) fc1 operands: in flight during the head
+  // folded fc1 SGD: this block owns weight columns c0..c0+47 of every row (old values in wsm);
+  // the momentum of this thread's dW1 elements
+  // (loaded unconditionally -- f.mom always exists: a load behind the fc1_sgd branch made the
+  // waitcnt pass merge both paths and drain most of group 2 before the head)
   float mb[2][kF5NT][4];
-  if (f.fc1_sgd) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int c = 0; c < kF5NT; ++c)
+    for (int c = 0; c < kF5NT; ++c)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          mb[a][c][j] = f.mom[L::fw1 + (size_t)(32 * w + 16 * a + 4 * g + j) * 9216 + c0 + 16 * c + m];
+      for (int j = 0; j < 4; ++j)
+        mb[a][c][j] = f.mom[L::fw1 + (size_t)(32 * w + 16 * a + 4 * g + j) * 9216 + c0 + 16 * c + m];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int i = min(tid + 256 * k, B * kF5C4 - 1), r = i / kF5C4, c4 = i - r * kF5C4;
+    vp.set(k, *reinterpret_cast<const float4*>(f.pool + (size_t)r * 9216 + c0 + c4 * 4));
+    vq.set(k, *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(f.idx) + (size_t)r * 9216 + c0 +
+                                                 c4 * 4));
   }
-  {  // all global loads in flight at once, then LDS stores
-    constexpr int ND = B * 32 / 256, NP = (B * kF5C4 + 255) / 256, NW = (128 * kF5C4 + 255) / 256, N2 = 5;
-    float4 vd[ND], vp[NP], vw[NW];
-    float v2[N2];
-    uint32_t vq[NP];  // argmax codes, 4 per uint32 (prefetched: the dp epilogue needs them last)
 #pragma unroll
-    for (int k = 0; k < ND; ++k) {
-      const int i = tid + 256 * k;
-      vd[k] = *reinterpret_cast<const float4*>(f.h + (i >> 5) * 128 + (i & 31) * 4);
-    }
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      const int i = min(tid + 256 * k, B * kF5C4 - 1), r = i / kF5C4, c4 = i - r * kF5C4;
-      vp[k] = *reinterpret_cast<const float4*>(f.pool + (size_t)r * 9216 + c0 + c4 * 4);
-      vq[k] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(f.idx) + (size_t)r * 9216 + c0 +
-                                                 c4 * 4);
-    }
-#pragma unroll
-    for (int k = 0; k < NW; ++k) {
-      const int i = min(tid + 256 * k, 128 * kF5C4 - 1), r = i / kF5C4, c4 = i - r * kF5C4;
-      vw[k] = *reinterpret_cast<const float4*>(f.p + L::fw1 + (size_t)r * 9216 + c0 + c4 * 4);
-    }
-#pragma unroll
-    for (int k = 0; k < N2; ++k) v2[k] = f.p[L::fw2 + tid + 256 * k];  // 1280 = 5 x 256
-#pragma unroll
-    for (int k = 0; k < ND; ++k) {
-      const int i = tid + 256 * k, c4 = (i & 31) * 4;
-      const float4 b1 = *reinterpret_cast<const float4*>(f.p + L::fb1 + c4);
-      const float4 hv = vd[k];
-      *reinterpret_cast<float4*>(dhs + (i >> 5) * kF5DhP + c4) =
-          make_float4(fmaxf(hv.x + b1.x, 0.f), fmaxf(hv.y + b1.y, 0.f), fmaxf(hv.z + b1.z, 0.f), fmaxf(hv.w + b1.w, 0.f));
-    }
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      const int i = tid + 256 * k, r = i / kF5C4, c4 = i - r * kF5C4;
-      if (i < B * kF5C4) {
-        *reinterpret_cast<float4*>(ps + r * kF5P + c4 * 4) = vp[k];
-        *reinterpret_cast<uint32_t*>(qs + r * kF5Cols + c4 * 4) = vq[k];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < NW; ++k) {
-      const int i = tid + 256 * k, r = i / kF5C4, c4 = i - r * kF5C4;
-      if (i < 128 * kF5C4) *reinterpret_cast<float4*>(wsm + r * kF5P + c4 * 4) = vw[k];
-    }
-#pragma unroll
-    for (int k = 0; k < N2; ++k) {
-      const int i = tid + 256 * k;
-      w2t[(i & 127) * kF5W2P + (i >> 7)] = v2[k];
-    }
-    for (int i = tid; i < 128 * 6; i += 256) w2t[(i / 6) * kF5W2P + 10 + i % 6] = 0.f;
+  for (int k = 0; k < NW; ++k) {
+    const int i = min(tid + 256 * k, 128 * kF5C4 - 1), r = i / kF5C4, c4 = i - r * kF5C4;
+    vw.set(k, *reinterpret_cast<const float4*>(f.p + L::fw1 + (size_t)r * 9216 + c0 + c4 * 4));
   }
+  // (1) stage the head operands
+#pragma unroll
+  for (int k = 0; k < ND; ++k) {
+    const int i = tid + 256 * k, c4 = (i & 31) * 4;
+    const float4 b1 = vb1[k], hv = vd[k];
+    *reinterpret_cast<float4*>(dhs + (i >> 5) * kF5DhP + c4) =
+        make_float4(fmaxf(hv.x + b1.x, 0.f), fmaxf(hv.y + b1.y, 0.f), fmaxf(hv.z + b1.z, 0.f), fmaxf(hv.w + b1.w, 0.f));
+  }
+#pragma unroll
+  for (int k = 0; k < N2; ++k) {
+    const int i = tid + 256 * k;
+    w2t[(i & 127) * kF5W2P + (i >> 7)] = v2[k];
+  }
+  for (int i = tid; i < 128 * 6; i += 256) w2t[(i / 6) * kF5W2P + 10 + i % 6] = 0.f;
   if (tid < 4) misc[tid] = 0.f;
   __syncthreads();
   MX_TRACE(f, 2, 1);
@@ -697,9 +754,8 @@ __global__ __launch_bounds__(256) void f5_head_fc1_bwd_kernel(MnistFused f) {
       for (int j = 0; j < 4; ++j) acc = mfma4(sel4(av, j), w2t[(16 * s + 4 * g + j) * kF5W2P + m], acc);
     }
     if (m < 10) {
-      const float bias = f.p[L::fb2 + m];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) lg[(16 * mt + 4 * g + j) * kF5LgP + m] = acc[j] + bias;
+      for (int j = 0; j < 4; ++j) lg[(16 * mt + 4 * g + j) * kF5LgP + m] = acc[j] + b2v;
     }
   }
   __syncthreads();
@@ -717,7 +773,7 @@ __global__ __launch_bounds__(256) void f5_head_fc1_bwd_kernel(MnistFused f) {
 #pragma unroll
     for (int c = 0; c < 10; ++c) se += __expf(l[c] - mx);
     const float lse = mx + __logf(se);
-    const int y = f.y[tid];
+    const int y = yv;
     float ly = 0.f;
 #pragma unroll
     for (int c = 0; c < 10; ++c) ly = c == y ? l[c] : ly;
@@ -777,6 +833,20 @@ __global__ __launch_bounds__(256) void f5_head_fc1_bwd_kernel(MnistFused f) {
         *d = *d > 0.f ? acc[j] : 0.f;
       }
     }
+  }
+  // (2) stage the fc1 operands (their loads have been in flight since the prologue)
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int i = tid + 256 * k, r = i / kF5C4, c4 = i - r * kF5C4;
+    if (i < B * kF5C4) {
+      *reinterpret_cast<float4*>(ps + r * kF5P + c4 * 4) = vp.get(k);
+      *reinterpret_cast<uint32_t*>(qs + r * kF5Cols + c4 * 4) = vq.get(k);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const int i = tid + 256 * k, r = i / kF5C4, c4 = i - r * kF5C4;
+    if (i < 128 * kF5C4) *reinterpret_cast<float4*>(wsm + r * kF5P + c4 * 4) = vw.get(k);
   }
   __syncthreads();
   MX_TRACE(f, 2, 4);
