@@ -967,15 +967,16 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
   if ((int)blockIdx.x >= nflat) {
     __shared__ float red[576 + 36];
     const int grp = (int)blockIdx.x - nflat;
+    // the pair's weights / momentum are requested before the slab sum (one round trip for both)
+    const int pair = 4 * grp + min((int)threadIdx.x, 3), e0 = (int)L::w2 + pair * 9;
+    float pe[9], bb[9];
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      pe[r] = f.p[e0 + r];
+      bb[r] = buf[e0 + r];
+    }
     wslab_group_sum(f, sc, grp, red, red + 576);
     if (threadIdx.x < 4) {
-      const int pair = 4 * grp + (int)threadIdx.x, e0 = (int)L::w2 + pair * 9;
-      float pe[9], bb[9];
-#pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        pe[r] = f.p[e0 + r];
-        bb[r] = buf[e0 + r];
-      }
 #pragma unroll
       for (int r = 0; r < 9; ++r) {
         const float gg = red[576 + 9 * threadIdx.x + r];
