@@ -139,8 +139,15 @@ constexpr int kF2RowP = 38, kF2ChP = 141;
 // F2W stage 2 (see f2_fwd_kernel): a1 tile [32 ci][4 rows][26] (pitches kF2ChP / kF2RowP) in
 // `tile` -> pooled conv2 outputs of pooled row py of image b.
 __device__ __forceinline__ void f2_stage2_wino(const MnistFused& f, const Scratch& sc, float* tile, int b, int py,
-                                               int w, int lane, const float4 (&bp)[4]) {
+                                               int w, int lane) {
   const int tid = threadIdx.x;
+  // B fragments of points 0, 1: requested here, in flight during the input transform (issued at
+  // kernel start they stayed live through stage 1 and the register shuffles around them waited
+  // for the loads: vmcnt(0) in the middle of the transform)
+  const float4* up = reinterpret_cast<const float4*>(sc.wv) + (size_t)w * 16 * 2 * 64 + lane;
+  float4 bc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) bc[q] = up[(q >> 1) * 128 + 64 * (q & 1)];
   // (a) input transform: items (ci, t) = it / 12, it % 12, two per thread (384 items)
   float v[2][16];
 #pragma unroll
@@ -171,7 +178,7 @@ __device__ __forceinline__ void f2_stage2_wino(const MnistFused& f, const Scratc
       }
     }
   }
-  __syncthreads();  // every a1 read done: V overwrites the tile
+  lds_barrier();  // every a1 read done: V overwrites the tile
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int it = tid + 256 * k;
@@ -181,16 +188,14 @@ __device__ __forceinline__ void f2_stage2_wino(const MnistFused& f, const Scratc
       for (int xi = 0; xi < 16; ++xi) tile[xi * 512 + ci * 16 + t] = v[k][xi];
     }
   }
-  __syncthreads();
+  lds_barrier();
   MX_TRACE(f, 0, 3);
   // (b) 16 GEMMs; lane: A row = tile m, k = ci 4s + g; B col = co 16w + m
   const int m = lane & 15, g = lane >> 4;
-  const float4* up = reinterpret_cast<const float4*>(sc.wv) + (size_t)w * 16 * 2 * 64 + lane;
   // Points are processed in pairs: two independent accumulator chains interleave, so a
   // dependent MFMA never waits on its predecessor's latency; the next pair's B fragments are
   // in flight during the current pair's MFMAs.
   f32x4 acc[16];
-  float4 bc[4] = {bp[0], bp[1], bp[2], bp[3]};  // xi = 0, 1 fragments, loaded at kernel start
 #pragma unroll
   for (int xp = 0; xp < 8; ++xp) {
     float4 bn[4] = {bc[0], bc[1], bc[2], bc[3]};
@@ -272,7 +277,7 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
   const int b = bid / 12, py = bid - b * 12;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int row0 = 2 * py;  // first input row of this block's conv1 rows
-  float4 bq[kWino ? 4 : 18];
+  float4 bq[kWino ? 1 : 18];  // direct path: conv2 B fragments for all 72 k-steps
   // ---- stage 1a: input rows row0 .. row0+5 (+ publish the rows this block owns).  Every global
   // operand of stage 1 is requested in ONE round trip: the batch counter, conv1's weights and --
   // synthetic data -- the 6 template rows of ALL 10 classes (the label, a function of the counter,
@@ -292,11 +297,7 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
 #pragma unroll
   for (int c = 0; c < 10; ++c) tv[c] = *reinterpret_cast<const float4*>(f.tmpl + c * 784 + d);
   const float4 xv = *reinterpret_cast<const float4*>(f.x + b * 784 + d);
-  if constexpr (kWino) {  // F2W: first B fragments (points 0, 1) in flight during stage 1
-    const float4* up = reinterpret_cast<const float4*>(sc.wv) + (size_t)w * 16 * 2 * 64 + lane;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) bq[q] = up[(q >> 1) * 128 + 64 * (q & 1)];
-  } else {
+  if constexpr (!kWino) {
     const float4* wf = reinterpret_cast<const float4*>(sc.wf) + w * 64 + lane;
 #pragma unroll
     for (int q = 0; q < 18; ++q) bq[q] = wf[q * 256];
@@ -331,8 +332,12 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
 #pragma unroll
   for (int k = 0; k < 2; ++k)
     if (tid + 256 * k < 320) w1s[tid + 256 * k] = w1v[k];  // conv1 w [32][9] then b [32]
-  __syncthreads();
+  lds_barrier();  // (the x rows / label just stored are read by later kernels only)
   MX_TRACE(f, 0, 1);
+  // conv1's short dependent MFMA chains run at raised wave priority: a CU's later-dispatched
+  // blocks reach this stage while the earlier ones issue their long stage-2 MFMA sequences, and
+  // without priority the chains starved (slowest blocks 6 us here instead of 2.3)
+  if (f.f2_prio) __builtin_amdgcn_s_setprio(2);
   // ---- stage 1b: conv1 + ReLU for 32 ci x 4 rows x 26 cols -> LDS tile, on MFMA: M = 104
   // positions (7 tiles of 16), N = 32 channels (2 tiles), K = 9 taps padded to 12 (3 k-steps).
   // Wave w owns N-tile (w & 1) and M-tiles (w >> 1) * 4 .. +3 (the last wave pair gets 3).
@@ -356,36 +361,30 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
       }
       // C: row = position 16 mt + 4g + j, column = channel 16 nt + l16
       const float bias = w1s[288 + ci_b];
+      float o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int q = 16 * mt + 4 * g + j;
+        o[j] = fmaxf(c[j] + bias, 0.f);
         if (q < 104) {
           const int qr = q / 26, qc = q - qr * 26;
-          tile[ci_b * kF2ChP + qr * kF2RowP + qc] = fmaxf(c[j] + bias, 0.f);
+          tile[ci_b * kF2ChP + qr * kF2RowP + qc] = o[j];
         }
       }
+      // publish the a1 rows this block owns (2, or 4 for the last row) for F6W straight from the
+      // accumulators: the 4 rows of the strip are 104 contiguous floats of channel ci_b, so a
+      // lane's 4 consecutive positions are one aligned float4 (no LDS read-back pass)
+      const int q0 = 16 * mt + 4 * g;
+      if (f.a1_pub && q0 < (py == 11 ? 104 : 52))
+        *reinterpret_cast<float4*>(f.a1 + (size_t)b * 21632 + ci_b * 676 + row0 * 26 + q0) =
+            make_float4(o[0], o[1], o[2], o[3]);
     }
   }
-  __syncthreads();
+  lds_barrier();  // the published a1 rows are read by F6W, not by this block
+  if (f.f2_prio) __builtin_amdgcn_s_setprio(0);
   MX_TRACE(f, 0, 2);
-  if (f.a1_pub) {  // publish the a1 rows this block owns (2, or 4 for the last row) for F6W:
-    // per channel they are 52 (104) contiguous, 16-byte aligned floats of a1 -> float4 stores
-    const int n4 = py == 11 ? 26 : 13;
-    float* dst = f.a1 + (size_t)b * 21632 + row0 * 26;
-    for (int i = tid; i < 32 * n4; i += 256) {
-      const int ci = i / n4, k = i - ci * n4;
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int p = 4 * k + e, qr = p / 26, qc = p - 26 * qr;
-        v[e] = tile[ci * kF2ChP + qr * kF2RowP + qc];
-      }
-      *reinterpret_cast<float4*>(dst + ci * 676 + 4 * k) = make_float4(v[0], v[1], v[2], v[3]);
-    }
-  }
-  MX_TRACE(f, 0, 3);
   if constexpr (kWino) {
-    f2_stage2_wino(f, sc, tile, b, py, w, lane, *reinterpret_cast<const float4(*)[4]>(bq));
+    f2_stage2_wino(f, sc, tile, b, py, w, lane);
   } else {
   // ---- stage 2: conv2 implicit GEMM + pool
   const int m = lane & 15, g = lane >> 4;
@@ -1097,6 +1096,14 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
 using namespace mnist;
 
 size_t mnist_fused_scratch_floats(int B) { return scratch_floats(B); }
+
+int mnist_f2_prio() {
+  static const int v = [] {
+    const char* e = std::getenv("MXDDP_F2_PRIO");
+    return (e && std::string(e) == "1") ? 1 : 0;
+  }();
+  return v;
+}
 
 int mnist_g1_slabs() {
   static const int v = [] {
