@@ -65,6 +65,12 @@ constexpr int kPl3 = 64 * 576;    // conv3 / fc1 weights
 __global__ __launch_bounds__(512) void kf1_kernel(KerasFused f) {
   const int n = blockIdx.x >> 2, c4 = blockIdx.x & 3;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  // commit the previous update's Adam step count (see ko_kernel): no KO runs concurrently
+  if (blockIdx.x == 0 && tid == 0) {
+    const int s1 = __hip_atomic_load(f.adam_state + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (s1 > __hip_atomic_load(f.adam_state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      __hip_atomic_store(f.adam_state, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   __shared__ float xs[784];
   __shared__ float w1s[320];
   __shared__ float p1s[kP1Img];
@@ -657,24 +663,28 @@ __global__ __launch_bounds__(256) void ko_kernel(KerasFused f, KoPlan plan, int 
   const bool live = li < R.np;
   const int i = R.p0 + li;
   const bool adam = mode == 0 || mode == 2;
+  // Adam step count: state[0] = steps committed before this update (read by every block, not
+  // written here), state[1] = this update's count, published by block 0 and copied to state[0]
+  // by the next step's KF1.  (Each block arriving on one counter to find the last one serialised
+  // ~1,450 same-address atomics: most of this kernel's 41 us.)
   int t = 0;
   if (adam) t = __hip_atomic_load(f.adam_state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   float gr = 0.f;
   if (mode != 3) {
-    if (live) {
-      const float* src = R.src + li;
-      const long long st = R.stride;
-      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-      int k = q;
-      for (; k + 3 * T < R.nplanes; k += 4 * T) {
-        a0 += src[(size_t)k * st];
-        a1 += src[(size_t)(k + T) * st];
-        a2 += src[(size_t)(k + 2 * T) * st];
-        a3 += src[(size_t)(k + 3 * T) * st];
-      }
-      for (; k < R.nplanes; k += T) a0 += src[(size_t)k * st];
-      gr = (a0 + a1) + (a2 + a3);
+    // this thread's planes k = q, q + T, ... (fixed order), 8 loads in flight per round
+    // (clamped + masked: no load behind a branch); np_t = planes per thread
+    const float* src = R.src + (live ? li : 0);
+    const long long st = R.stride;
+    const int np_t = R.nplanes > q ? (R.nplanes - q + T - 1) / T : 0;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < np_t; k0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(q + T * min(k0 + u, np_t - 1)) * st];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += k0 + u < np_t ? v[u] : 0.f;
     }
+    gr = live ? ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7])) : 0.f;
     if (T > 1) {  // block-uniform branch
       red[w][lane] = gr;
       __syncthreads();
@@ -699,16 +709,7 @@ __global__ __launch_bounds__(256) void ko_kernel(KerasFused f, KoPlan plan, int 
     }
     if (mode != 1 && i >= (int)L::w2 && i < (int)L::b2) pack_w2(f, i, pv);
   }
-  if (adam) {  // the last block to finish publishes the step count (ops_optim.hip)
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int arrived = __hip_atomic_fetch_add(f.adam_state + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (arrived == (int)gridDim.x - 1) {
-        __hip_atomic_store(f.adam_state, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(f.adam_state + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
+  if (adam && b == 0 && tid == 0) __hip_atomic_store(f.adam_state + 1, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace keras

@@ -189,7 +189,6 @@ MnistFused MnistEngine::fused_args() const {
   // come between the gradient and the update)
   f.fc1_sgd = (variant_ == 1 && !reducer_->active() && mnist_f5_sgd()) ? 1 : 0;
   f.g1_slabs = mnist_g1_slabs();
-  f.f2_prio = mnist_f2_prio();
   f.wslab = (variant_ == 1 && mnist_wslab()) ? 1 : 0;
   f.mom = m_;
   f.lr = lr_;

@@ -46,9 +46,7 @@ struct MnistFused {
   // 1: F6W writes its conv2 weight gradient as per-image slabs with plain stores (no atomics)
   // and the finalize (F8 / the folded SGD) sums them in a fixed order; 0: slab atomics (wacc)
   int wslab;
-  int f2_prio;  // F2's conv1 stage at raised wave priority (MXDDP_F2_PRIO=1)
 };
-int mnist_f2_prio();
 int mnist_g1_slabs();
 bool mnist_wslab();  // default on; MXDDP_WSLAB=0 (and the split / co-split / direct F6 variants) use atomics
 bool mnist_a1_publish();  // default on; MXDDP_MNIST_A1=recompute turns it off

@@ -334,10 +334,6 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
     if (tid + 256 * k < 320) w1s[tid + 256 * k] = w1v[k];  // conv1 w [32][9] then b [32]
   lds_barrier();  // (the x rows / label just stored are read by later kernels only)
   MX_TRACE(f, 0, 1);
-  // conv1's short dependent MFMA chains run at raised wave priority: a CU's later-dispatched
-  // blocks reach this stage while the earlier ones issue their long stage-2 MFMA sequences, and
-  // without priority the chains starved (slowest blocks 6 us here instead of 2.3)
-  if (f.f2_prio) __builtin_amdgcn_s_setprio(2);
   // ---- stage 1b: conv1 + ReLU for 32 ci x 4 rows x 26 cols -> LDS tile, on MFMA: M = 104
   // positions (7 tiles of 16), N = 32 channels (2 tiles), K = 9 taps padded to 12 (3 k-steps).
   // Wave w owns N-tile (w & 1) and M-tiles (w >> 1) * 4 .. +3 (the last wave pair gets 3).
@@ -381,7 +377,6 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
     }
   }
   lds_barrier();  // the published a1 rows are read by F6W, not by this block
-  if (f.f2_prio) __builtin_amdgcn_s_setprio(0);
   MX_TRACE(f, 0, 2);
   if constexpr (kWino) {
     f2_stage2_wino(f, sc, tile, b, py, w, lane);
@@ -1096,14 +1091,6 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
 using namespace mnist;
 
 size_t mnist_fused_scratch_floats(int B) { return scratch_floats(B); }
-
-int mnist_f2_prio() {
-  static const int v = [] {
-    const char* e = std::getenv("MXDDP_F2_PRIO");
-    return (e && std::string(e) == "1") ? 1 : 0;
-  }();
-  return v;
-}
 
 int mnist_g1_slabs() {
   static const int v = [] {

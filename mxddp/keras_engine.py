@@ -152,8 +152,9 @@ class FusedKerasTrainer:
 
     @property
     def adam_steps(self) -> int:
+        # [0] committed by the next forward, [1] written by the last update (ko_kernel)
         self.eng.sync()
-        return int(self.adam_state[0].item())
+        return int(self.adam_state.max().item())
 
     def data_state(self) -> torch.Tensor:
         self.eng.sync()
@@ -178,14 +179,13 @@ class FusedKerasTrainer:
 
     def optimizer_state(self) -> dict:
         self.eng.sync()
-        return {"lr": self._lr_host, "m": self.m.cpu(), "v": self.v.cpu(), "steps": int(self.adam_state[0].item())}
+        return {"lr": self._lr_host, "m": self.m.cpu(), "v": self.v.cpu(), "steps": int(self.adam_state.max().item())}
 
     def load_optimizer_state(self, st: dict):
         self.eng.sync()
         self.m.copy_(st["m"].to(self.device))
         self.v.copy_(st["v"].to(self.device))
-        self.adam_state.zero_()
-        self.adam_state[0] = int(st["steps"])
+        self.adam_state.fill_(int(st["steps"]))
         self.set_lr(float(st["lr"]))
         torch.cuda.synchronize(self.device)
 
