@@ -68,6 +68,12 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return base + orig / kNumXcd;
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, NOT for its
+// outstanding global stores.  A __syncthreads() (workgroup release fence + s_barrier) emits
+// s_waitcnt vmcnt(0) whenever global stores precede it, so a block that publishes data and then
+// synchronises on LDS waits for the stores' write acknowledgements (measured in F2: the slowest
+// blocks spent ~7 us there).  Use only where no other wave reads the stored global data.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -16,12 +16,6 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 __device__ __forceinline__ float sel4(const float4& v, int j) {
   return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
 }
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, NOT for its
-// outstanding global stores.  A __syncthreads() (workgroup release fence + s_barrier) emits
-// s_waitcnt vmcnt(0) whenever global stores precede it, so a block that publishes data and then
-// synchronises on LDS waits for the stores' write acknowledgements (measured in F2: the slowest
-// blocks spent ~7 us there).  Use only where no other wave reads the stored global data.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ __forceinline__ int g1_slab_mask(const MnistFused& f) {
   return (f.g1_slabs >= 1 && f.g1_slabs <= 64 ? f.g1_slabs : 16) - 1;
 }

@@ -49,9 +49,11 @@ __global__ void sgd_k(float* __restrict__ p, const float* __restrict__ g, float*
 }
 
 // Adam with the step count on the device, so a captured hipGraph replays it exactly: every
-// block reads the count of completed steps, t = count + 1; the LAST block to finish (arrival
-// ticket, agent-scope atomics) publishes count = t and rewinds the ticket.  Every block has read
-// the count before it arrives, so the update never races the reads; the next launch sees it.
+// block reads the count of completed steps state[0], t = count + 1; block 0 records t in
+// state[1] and a one-block launch right after (adam_commit_k) publishes it as state[0] -- no
+// block ever writes what another block of the same launch reads.  (The previous form -- every
+// block arriving on a ticket so the last one publishes -- serialised up to 2,048 same-address
+// atomics per step; the Keras engine's update kernel lost ~30 us to the same pattern.)
 // eps_hat (Keras / Chainer): m_hat / (sqrt(v_hat) + eps)  ==  m / bc1 / (sqrt(v) / sqrt(bc2) +
 // eps / sqrt(bc2)); otherwise torch.optim.Adam's m_hat / (sqrt(v_hat) + eps).
 __global__ void adam_k(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
@@ -71,14 +73,11 @@ __global__ void adam_k(float* __restrict__ p, const float* __restrict__ g, float
     v[i] = vi;
     p[i] -= step_size * mi / (sqrtf(vi) / bc2s + e);
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int arrived = __hip_atomic_fetch_add(state + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (arrived == (int)gridDim.x - 1) {
-      __hip_atomic_store(state, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(state + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(state + 1, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void adam_commit_k(int32_t* __restrict__ state) {
+  if (threadIdx.x == 0) state[0] = state[1];
 }
 
 int grid_for(int64_t n) {
@@ -101,6 +100,7 @@ void adam_step(float* p, const float* g, float* m, float* v, const float* lr, in
                float b1, float b2, float eps, float wd, bool eps_hat, int64_t n, hipStream_t st) {
   MX_LAUNCH(adam_k, dim3(grid_for(n * 4)), dim3(256), 0, st, p, g, m, v, lr, state, gscale, b1, b2, eps,
                      wd, eps_hat ? 1 : 0, n);
+  MX_LAUNCH(adam_commit_k, dim3(1), dim3(64), 0, st, state);
 }
 
 }  // namespace mx

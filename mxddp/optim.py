@@ -77,9 +77,10 @@ class SGD(_FlatOptimizer):
 
 
 class Adam(_FlatOptimizer):
-    """On a GPU the step count lives on the device (``_state``: completed steps, arrival ticket)
-    and the kernel advances it, so ``step()`` issues one launch and no host value: a captured
-    hipGraph replays Adam exactly (bias corrections and the eps_hat form included)."""
+    """On a GPU the step count lives on the device (``_state``: completed steps, the count being
+    applied) and the kernels advance it, so ``step()`` issues two launches (update, one-block
+    commit) and no host value: a captured hipGraph replays Adam exactly (bias corrections and the
+    eps_hat form included)."""
 
     def __init__(self, flat: FlatParams, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, eps_hat: bool = False):
@@ -127,8 +128,7 @@ class Adam(_FlatOptimizer):
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
         self._steps_host = int(sd["steps"])
-        self._state.fill_(0)
-        self._state[0] = int(sd["steps"])
+        self._state.fill_(int(sd["steps"]))
 
 
 class StepLR:
