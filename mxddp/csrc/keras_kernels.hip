@@ -74,25 +74,47 @@ __global__ __launch_bounds__(512) void kf1_kernel(KerasFused f) {
   __shared__ float xs[784];
   __shared__ float w1s[320];
   __shared__ float p1s[kP1Img];
-  if (f.synth) {
-    const uint32_t ctr = (uint32_t)*f.counter;
+  // Stage-1 operands in ONE round trip (counter, conv1 weights, the image row-group of all 10
+  // class templates -- the label picks one arithmetically -- or the caller's x), then the 72 conv2
+  // B fragments, which stay in flight through conv1 (vmcnt counts in order: they are issued
+  // last so waiting for the stage-1 operands never waits for them).  Branch-free in f.synth.
+  const int t196 = min(tid, 195), d = 4 * t196;
+  const uint32_t ctr = (uint32_t)*f.counter;
+  float4 tv[10];
+#pragma unroll
+  for (int c = 0; c < 10; ++c) tv[c] = *reinterpret_cast<const float4*>(f.tmpl + c * 784 + d);
+  const float4 xv = *reinterpret_cast<const float4*>(f.x + (size_t)n * 784 + d);
+  const float w1v = f.p[L::w1 + min(tid, 319)];
+  __builtin_amdgcn_sched_barrier(0);  // issue order: stage-1 operands, then the fragments
+  float breg[72];
+  const float* wf = f.w2f + (size_t)c4 * 72 * 64;
+#pragma unroll
+  for (int s = 0; s < 72; ++s) breg[s] = wf[s * 64 + lane];
+  __builtin_amdgcn_sched_barrier(0);
+  {
     const uint2 key = synth_key(f.seed);
     const int label = synth_label(ctr, n, 10, key);
-    if (tid < 196) {
-      const int d = 4 * tid;
-      const uint4 r = synth_noise4(ctr, n, d, key);
-      const float4 t = *reinterpret_cast<const float4*>(f.tmpl + label * 784 + d);
-      const float4 v = make_float4(0.5f * t.x + 0.5f * u01(r.x), 0.5f * t.y + 0.5f * u01(r.y),
-                                   0.5f * t.z + 0.5f * u01(r.z), 0.5f * t.w + 0.5f * u01(r.w));
-      *reinterpret_cast<float4*>(xs + d) = v;
-      if (c4 == 0) *reinterpret_cast<float4*>(f.x + (size_t)n * 784 + d) = v;
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);  // masked sum (a select chain becomes tv[label])
+#pragma unroll
+    for (int c = 0; c < 10; ++c) {
+      const float mk = (float)(label == c);
+      t.x = fmaf(mk, tv[c].x, t.x);
+      t.y = fmaf(mk, tv[c].y, t.y);
+      t.z = fmaf(mk, tv[c].z, t.z);
+      t.w = fmaf(mk, tv[c].w, t.w);
     }
-    if (c4 == 0 && tid == 0) f.y[n] = label;
-  } else if (tid < 196) {
-    *reinterpret_cast<float4*>(xs + 4 * tid) = *reinterpret_cast<const float4*>(f.x + (size_t)n * 784 + 4 * tid);
+    const uint4 r = synth_noise4(ctr, n, d, key);
+    const float4 sv = make_float4(0.5f * t.x + 0.5f * u01(r.x), 0.5f * t.y + 0.5f * u01(r.y),
+                                  0.5f * t.z + 0.5f * u01(r.z), 0.5f * t.w + 0.5f * u01(r.w));
+    const float4 v = f.synth ? sv : xv;
+    if (tid < 196) {
+      *reinterpret_cast<float4*>(xs + d) = v;
+      if (f.synth && c4 == 0) *reinterpret_cast<float4*>(f.x + (size_t)n * 784 + d) = v;
+    }
+    if (f.synth && c4 == 0 && tid == 0) f.y[n] = label;
   }
-  for (int i = tid; i < 320; i += 512) w1s[i] = f.p[L::w1 + i];  // w1 [32][9] then b1 [32]
-  __syncthreads();
+  if (tid < 320) w1s[tid] = w1v;  // w1 [32][9] then b1 [32]
+  lds_barrier();  // (x / label stores are read by later kernels only)
 
   // conv1 + ReLU + 2x2 max-pool (+ argmax): 32 x 169 pooled outputs, one 4x4 input patch each
   for (int o = tid; o < kP1Img; o += 512) {
@@ -128,13 +150,9 @@ __global__ __launch_bounds__(512) void kf1_kernel(KerasFused f) {
       f.q1[(size_t)n * kP1Img + o] = (uint8_t)best;
     }
   }
-  __syncthreads();
+  lds_barrier();  // the published p1 / q1 are read by KB1, not by this block
 
-  // conv2 (16 co of this block) on MFMA
-  float breg[72];
-  const float* wf = f.w2f + (size_t)c4 * 72 * 64;
-#pragma unroll
-  for (int s = 0; s < 72; ++s) breg[s] = wf[s * 64 + lane];
+  // conv2 (16 co of this block) on MFMA (B fragments in flight since the start)
   const int co = 16 * c4 + (lane & 15);
   const float bias2 = f.p[L::b2 + co];
   for (int mt = w; mt < 7; mt += 8) {  // 7 M-tiles over 8 waves
@@ -170,9 +188,13 @@ __global__ __launch_bounds__(512) void kf1_kernel(KerasFused f) {
 
 // ------------------------------------------------------------------------------------------
 // KF2: block = image, 8 waves.  Head forward + backward to the pooled conv2 output; VALU,
-// LDS-resident.  The phases are a dependent chain, so each thread issues the global loads of its
-// weight slices ahead of use (conv3 + fc1 slices at entry, the fc1-transpose column during the
-// loss): the chain does not wait on L2 once per phase.
+// LDS-resident.  The phases are a dependent chain, so no phase waits on a global load of its own:
+// group 1 (entry) = conv3 / fc1 slices, the pooled input, biases, the fc2 operands of the loss
+// and dh1; group 2 (issued after fc1, in flight during the loss) = the fc1-transpose column(s)
+// for dx3; group 3 = the conv3 data-gradient slice, one tap row ahead of its use.  vmcnt counts in order, so a phase that needed a
+// group-1 value after group 2 was issued would wait for all of group 2 -- every group-1 operand
+// is therefore consumed or copied to registers before group 2 starts.  Barriers that follow
+// this block's global stores (x3, dl, dh1, dx3, ... for KB1) are LDS-only (no store drain).
 __global__ __launch_bounds__(512) void kf2_kernel(KerasFused f) {
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   __shared__ float p2s[kP2Img];
@@ -181,7 +203,11 @@ __global__ __launch_bounds__(512) void kf2_kernel(KerasFused f) {
   __shared__ float hs[64];
   __shared__ float dh1s[64];
   __shared__ float dls[16];
+  __shared__ float red2[8][64];  // dx3 inputs 512..575: partial sums over 8 feature groups
+  __shared__ float w2s[640];     // fc2 weights [10][64]
+  __shared__ float bss[138];     // conv3 bias, fc1 bias, fc2 bias
   const int hi = tid >> 3, q = tid & 7;  // (output channel / feature, eighth of the reduction)
+  // ---- group 1
   // conv3 slice w3[hi][8q .. 8q+7][9] and fc1 slice fw1[hi][72q .. 72q+71]: 18 float4 each
   float4 wc[18], wf[18];
   {
@@ -193,7 +219,20 @@ __global__ __launch_bounds__(512) void kf2_kernel(KerasFused f) {
       wf[k] = b[k];
     }
   }
-  for (int i = tid; i < kP2Img; i += 512) p2s[i] = f.p2[(size_t)n * kP2Img + i];
+  float p2v[4];  // 1600 floats = 3 x 512 + 64
+#pragma unroll
+  for (int k = 0; k < 4; ++k) p2v[k] = f.p2[(size_t)n * kP2Img + min(tid + 512 * k, kP2Img - 1)];
+  // the small operands of the later phases go to LDS with the input (registers are needed by the
+  // conv3 / fc1 slices): fc2 weights [10][64], biases b3 / fb1 / fb2, the label
+  const float w2v0 = f.p[L::fw2 + tid], w2v1 = f.p[L::fw2 + min(512 + tid, 639)];
+  const float bv = f.p[(tid < 64 ? L::b3 : tid < 128 ? L::fb1 : L::fb2) + min(tid & 63, tid < 128 ? 63 : 9)];
+  const int label = f.y[n];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (tid + 512 * k < kP2Img) p2s[tid + 512 * k] = p2v[k];
+  w2s[tid] = w2v0;
+  if (tid < 128) w2s[512 + tid] = w2v1;
+  if (tid < 138) bss[tid] = bv;  // b3 [0, 64), fb1 [64, 128), fb2 [128, 138)
   if (f.synth && n == 0 && tid == 0) *f.counter += 1;  // KF1 consumed this batch index
   __syncthreads();
 
@@ -218,9 +257,8 @@ __global__ __launch_bounds__(512) void kf2_kernel(KerasFused f) {
 #pragma unroll
       for (int o = 1; o < 8; o <<= 1) acc[pos] += __shfl_xor(acc[pos], o, 64);
     if (q == 0) {
-      const float b = f.p[L::b3 + hi];
 #pragma unroll
-      for (int pos = 0; pos < 9; ++pos) x3s[hi * 9 + pos] = fmaxf(acc[pos] + b, 0.f);
+      for (int pos = 0; pos < 9; ++pos) x3s[hi * 9 + pos] = fmaxf(acc[pos] + bss[hi], 0.f);
     }
   }
   __syncthreads();
@@ -238,31 +276,33 @@ __global__ __launch_bounds__(512) void kf2_kernel(KerasFused f) {
     }
 #pragma unroll
     for (int o = 1; o < 8; o <<= 1) a += __shfl_xor(a, o, 64);
-    if (q == 0) hs[hi] = fmaxf(a + f.p[L::fb1 + hi], 0.f);
+    if (q == 0) hs[hi] = fmaxf(a + bss[64 + hi], 0.f);
   }
-  __syncthreads();
-  // fc1-transpose column fw1[:, tid] for dx3 (issued now, used after the loss)
-  float wx[64];
+  lds_barrier();
+  // ---- group 2 (in flight during the loss): fc1-transpose column fw1[:, tid] for dx3 input
+  // tid; for inputs 512..575 thread t takes input 512 + (t & 63) over features 8 (t >> 6) .. +7
+  // (8 registers, not a second 64-entry column); conv3 data-gradient slice w3[8q + c][hi][9]
+  float wx[64], wx2[8];
 #pragma unroll
   for (int j = 0; j < 64; ++j) wx[j] = f.p[L::fw1 + (size_t)j * 576 + tid];
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) wx2[jj] = f.p[L::fw1 + (size_t)(8 * wv + jj) * 576 + 512 + lane];
 
   // fc2 + softmax + cross entropy + accuracy + dlogits (wave 0)
   if (wv == 0) {
     float a = 0.f;
     if (lane < 40) {
       const int c = lane >> 2, qq = lane & 3;
-      const float* wr = f.p + L::fw2 + c * 64 + 16 * qq;
 #pragma unroll
-      for (int jj = 0; jj < 16; ++jj) a += wr[jj] * hs[16 * qq + jj];
+      for (int jj = 0; jj < 16; ++jj) a += w2s[c * 64 + 16 * qq + jj] * hs[16 * qq + jj];
     }
     a += __shfl_xor(a, 1, 64);
     a += __shfl_xor(a, 2, 64);
     const float lg0 = __shfl(a, 4 * (lane < 10 ? lane : 0), 64);
-    const float lg = lane < 10 ? lg0 + f.p[L::fb2 + lane] : -INFINITY;
+    const float lg = lane < 10 ? lg0 + bss[128 + lane] : -INFINITY;
     const float mx = wave_max(lg);
     const float ex = lane < 10 ? __expf(lg - mx) : 0.f;
     const float se = wave_sum(ex);
-    const int label = f.y[n];
     const float lbl = __shfl(lg, label, 64);
     const unsigned long long ball = __ballot(lane < 10 && lg == mx);
     const int first = __ffsll((long long)ball) - 1;
@@ -277,19 +317,19 @@ __global__ __launch_bounds__(512) void kf2_kernel(KerasFused f) {
       atomicAdd(f.metrics + 1, first == label ? 1.f : 0.f);
     }
   }
-  __syncthreads();
+  lds_barrier();
   // dh1 = (fw2^T dl) * (h > 0)
   if (tid < 64) {
     float a = 0.f;
 #pragma unroll
-    for (int c = 0; c < 10; ++c) a += f.p[L::fw2 + c * 64 + tid] * dls[c];
+    for (int c = 0; c < 10; ++c) a += w2s[c * 64 + tid] * dls[c];
     const float d = hs[tid] > 0.f ? a : 0.f;
     dh1s[tid] = d;
     f.dh1[(size_t)n * 64 + tid] = d;
     f.h1[(size_t)n * 64 + tid] = hs[tid];
     f.sv[(size_t)n * 256 + 128 + tid] = d;
   }
-  __syncthreads();
+  lds_barrier();
   // dx3 = (fw1^T dh1) * (x3 > 0): inputs tid (and 512 + tid for the first wave)
   {
     float a0 = 0.f, a1 = 0.f;
@@ -301,17 +341,28 @@ __global__ __launch_bounds__(512) void kf2_kernel(KerasFused f) {
     const float d = x3s[tid] > 0.f ? a0 + a1 : 0.f;
     dx3s[tid] = d;
     f.dx3[(size_t)n * 576 + tid] = d;
-    if (tid < 64) {
-      const int i2 = 512 + tid;
-      float b0 = 0.f;
-#pragma unroll 16
-      for (int j = 0; j < 64; ++j) b0 += f.p[L::fw1 + (size_t)j * 576 + i2] * dh1s[j];
-      const float d2 = x3s[i2] > 0.f ? b0 : 0.f;
-      dx3s[i2] = d2;
-      f.dx3[(size_t)n * 576 + i2] = d2;
-    }
+    float b0 = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) b0 += wx2[jj] * dh1s[8 * wv + jj];
+    red2[wv][lane] = b0;
   }
-  __syncthreads();
+  // group 3 (the fc1 column is consumed): the first tap row of the conv3 data-gradient slice
+  // w3[8q][hi][9], in flight during the remaining dx3 / bias-gradient steps; the other 7 are
+  // prefetched one step ahead inside the loop (all 72 in registers spilled: 292 B/lane)
+  float wn[9];
+#pragma unroll
+  for (int r = 0; r < 9; ++r) wn[r] = f.p[L::w3 + ((size_t)(8 * q) * 64 + hi) * 9 + r];
+  lds_barrier();
+  if (tid < 64) {  // inputs 512..575: the 8 feature-group partials in a fixed order
+    float b0 = red2[0][tid];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) b0 += red2[k][tid];
+    const int i2 = 512 + tid;
+    const float d2 = x3s[i2] > 0.f ? b0 : 0.f;
+    dx3s[i2] = d2;
+    f.dx3[(size_t)n * 576 + i2] = d2;
+  }
+  lds_barrier();
   if (tid < 64) {  // conv3 bias grad of this image
     float sb = 0.f;
 #pragma unroll
@@ -324,14 +375,18 @@ __global__ __launch_bounds__(512) void kf2_kernel(KerasFused f) {
     float acc[25];
 #pragma unroll
     for (int k = 0; k < 25; ++k) acc[k] = 0.f;
-#pragma unroll 2
+#pragma unroll 1
     for (int c = 0; c < 8; ++c) {
       const int co = 8 * q + c;
-      float d[9], w[9];
+      float w[9], d[9];
+#pragma unroll
+      for (int r = 0; r < 9; ++r) w[r] = wn[r];
+      if (c + 1 < 8) {
+#pragma unroll
+        for (int r = 0; r < 9; ++r) wn[r] = f.p[L::w3 + ((size_t)(co + 1) * 64 + hi) * 9 + r];
+      }
 #pragma unroll
       for (int pos = 0; pos < 9; ++pos) d[pos] = dx3s[co * 9 + pos];
-#pragma unroll
-      for (int r = 0; r < 9; ++r) w[r] = f.p[L::w3 + ((size_t)co * 64 + hi) * 9 + r];
 #pragma unroll
       for (int pos = 0; pos < 9; ++pos)
 #pragma unroll
@@ -394,24 +449,59 @@ union SmemKB1 {
 __device__ void kb1_role_a(const KerasFused& f, SmemA& sm, int bid) {
   const int n = bid >> 3, nh = (bid >> 2) & 1, mq = bid & 3;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
-  for (int i = tid; i < 64 * 64; i += 256) {
-    sm.dps[i] = 0.f;
-    sm.qs[i] = 0;
-  }
-  for (int i = tid; i < 784; i += 256) sm.xs[i] = f.x[(size_t)n * 784 + i];
-  __syncthreads();
-  for (int e = tid; e < kP2Img; e += 256) {
-    const int co = e / 25, wi = e - co * 25, wy = wi / 5, wx = wi - wy * 5;
-    const int idx = co * 64 + (wy + 1) * 8 + wx + 1;
-    sm.dps[idx] = f.dp2[(size_t)n * kP2Img + e];
-    sm.qs[idx] = f.q2[(size_t)n * kP2Img + e];
-  }
-  // B fragments of this wave's 36 k-steps (pre-packed w2d)
+  // Every global operand of the block is requested up front, in one round trip: the B fragments
+  // of this wave's 36 k-steps (pre-packed w2d), the input image, the compact dY2 + argmax codes,
+  // and the pool1 / ReLU1 operands of the epilogue (clamped lanes, no loads behind branches).
   float breg[36];
   const float* wd = f.w2d + ((size_t)(nh * 4 + w) * 36) * 64;
 #pragma unroll
   for (int s = 0; s < 36; ++s) breg[s] = wd[s * 64 + lane];
+  float xv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) xv[k] = f.x[(size_t)n * 784 + min(tid + 256 * k, 783)];
+  float dv[7];
+  uint8_t qv[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const int e = min(tid + 256 * k, kP2Img - 1);
+    dv[k] = f.dp2[(size_t)n * kP2Img + e];
+    qv[k] = f.q2[(size_t)n * kP2Img + e];
+  }
   const int t0 = 3 * mq, nt = mq == 3 ? 2 : 3;
+  float p1v[4];
+  uint8_t q1v[4];
+  {
+    const int ci = 16 * nh + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = min(16 * (t0 + min(w, nt - 1)) + 4 * g + j, kP1 - 1);
+      const size_t pi = ((size_t)n * 32 + ci) * kP1 + m;
+      p1v[j] = f.p1[pi];
+      q1v[j] = f.q1[pi];
+    }
+  }
+  // dY2 windows [co][8][8] with a dead ring: the ring is zeroed, the 5 x 5 interior scattered
+  // (disjoint entries: one barrier)
+  for (int i = tid; i < 64 * 64; i += 256) {
+    const int wy = (i >> 3) & 7, wx = i & 7;
+    if (wy < 1 || wy > 5 || wx < 1 || wx > 5) {
+      sm.dps[i] = 0.f;
+      sm.qs[i] = 0;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (tid + 256 * k < 784) sm.xs[tid + 256 * k] = xv[k];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const int e = tid + 256 * k;
+    if (e < kP2Img) {
+      const int co = e / 25, wi = e - co * 25, wy = wi / 5, wx = wi - wy * 5;
+      const int idx = co * 64 + (wy + 1) * 8 + wx + 1;
+      sm.dps[idx] = dv[k];
+      sm.qs[idx] = qv[k];
+    }
+  }
   // per tile, per tap: window offset [8x8 grid] and the argmax code dY2's position must match
   int off[3][9], code[3][9];
 #pragma unroll
@@ -454,9 +544,8 @@ __device__ void kb1_role_a(const KerasFused& f, SmemA& sm, int bid) {
       const int m = 16 * (t0 + t) + 4 * g + j;
       if (m < kP1) {
         const float d = sm.red[0][t][j][lane] + sm.red[1][t][j][lane] + sm.red[2][t][j][lane] + sm.red[3][t][j][lane];
-        const size_t pi = ((size_t)n * 32 + ci) * kP1 + m;
-        if (f.p1[pi] > 0.f) {
-          const int cd = f.q1[pi];
+        if (p1v[j] > 0.f) {
+          const int cd = q1v[j];
           const int y1 = 2 * (m / 13) + (cd >> 1), x1 = 2 * (m % 13) + (cd & 1);
 #pragma unroll
           for (int r = 0; r < 9; ++r) cw[r] += d * sm.xs[(y1 + r / 3) * 28 + x1 + r % 3];
@@ -494,8 +583,13 @@ __device__ void kb1_role_a(const KerasFused& f, SmemA& sm, int bid) {
 __device__ void kb1_role_b(const KerasFused& f, SmemB& sm, int bid) {
   const int n = bid >> 2, cq = bid & 3;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
-  for (int i = tid; i < kP1Img / 4; i += 256)
-    reinterpret_cast<float4*>(sm.p1s)[i] = reinterpret_cast<const float4*>(f.p1 + (size_t)n * kP1Img)[i];
+  // the pooled conv1 tile (1352 float4: 6 per thread, clamped) and the A operands below are
+  // all requested before anything is stored (one round trip)
+  constexpr int kP1v = kP1Img / 4, kP1n = (kP1v + 255) / 256;
+  float4 pv[kP1n];
+#pragma unroll
+  for (int k = 0; k < kP1n; ++k)
+    pv[k] = reinterpret_cast<const float4*>(f.p1 + (size_t)n * kP1Img)[min(tid + 256 * k, kP1v - 1)];
   const int co_a = 16 * cq + (lane & 15);
   float av[25];
   int poff[25];
@@ -503,9 +597,13 @@ __device__ void kb1_role_b(const KerasFused& f, SmemB& sm, int bid) {
   for (int s = 0; s < 25; ++s) {
     const int pos = 4 * s + g, oy = pos / 10, ox = pos - oy * 10;
     const size_t e = ((size_t)n * 64 + co_a) * 25 + (oy >> 1) * 5 + (ox >> 1);
-    av[s] = (int)f.q2[e] == (oy & 1) * 2 + (ox & 1) ? f.dp2[e] : 0.f;
+    const float dv = f.dp2[e];
+    av[s] = (int)f.q2[e] == (oy & 1) * 2 + (ox & 1) ? dv : 0.f;
     poff[s] = oy * 13 + ox;
   }
+#pragma unroll
+  for (int k = 0; k < kP1n; ++k)
+    if (tid + 256 * k < kP1v) reinterpret_cast<float4*>(sm.p1s)[tid + 256 * k] = pv[k];
   __syncthreads();
   for (int nt = w; nt < 18; nt += 4) {
     const int c = 16 * nt + (lane & 15), ci = c / 9, r = c - ci * 9;
@@ -523,14 +621,42 @@ __device__ void kb1_role_b(const KerasFused& f, SmemB& sm, int bid) {
 __device__ void kb1_role_c(const KerasFused& f, SmemC& sm, int bid) {
   const int gi = bid >> 2, nq = bid & 3, tid = threadIdx.x;
   const int n0 = 8 * gi;
-  for (int i = tid; i < 8 * 576; i += 256) sm.dx3[i / 576][i % 576] = f.dx3[(size_t)n0 * 576 + i];
-  for (int i = tid; i < 8 * 16 * 25; i += 256) {
-    const int im = i / 400, rem = i - im * 400;
-    sm.p2[im][rem / 25][rem % 25] = f.p2[((size_t)(n0 + im) * 64 + 16 * nq) * 25 + rem];
+  // all four operand tiles requested before any LDS store (one round trip, clamped lanes)
+  float vdx[18], vp2[13], vdh[2], vx3[5];
+#pragma unroll
+  for (int k = 0; k < 18; ++k) vdx[k] = f.dx3[(size_t)n0 * 576 + tid + 256 * k];  // 4608 = 18 x 256
+#pragma unroll
+  for (int k = 0; k < 13; ++k) {
+    const int i = min(tid + 256 * k, 8 * 16 * 25 - 1), im = i / 400, rem = i - im * 400;
+    vp2[k] = f.p2[((size_t)(n0 + im) * 64 + 16 * nq) * 25 + rem];
   }
-  for (int i = tid; i < 8 * 64; i += 256) sm.dh1[i / 64][i % 64] = f.dh1[(size_t)n0 * 64 + i];
-  for (int i = tid; i < 8 * 144; i += 256)
-    sm.x3[i / 144][i % 144] = f.x3[(size_t)(n0 + i / 144) * 576 + 144 * nq + i % 144];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) vdh[k] = f.dh1[(size_t)n0 * 64 + tid + 256 * k];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int i = min(tid + 256 * k, 8 * 144 - 1);
+    vx3[k] = f.x3[(size_t)(n0 + i / 144) * 576 + 144 * nq + i % 144];
+  }
+#pragma unroll
+  for (int k = 0; k < 18; ++k) {
+    const int i = tid + 256 * k;
+    sm.dx3[i / 576][i % 576] = vdx[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 13; ++k) {
+    const int i = tid + 256 * k, im = i / 400, rem = i - im * 400;
+    if (i < 8 * 16 * 25) sm.p2[im][rem / 25][rem % 25] = vp2[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = tid + 256 * k;
+    sm.dh1[i / 64][i % 64] = vdh[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int i = tid + 256 * k;
+    if (i < 8 * 144) sm.x3[i / 144][i % 144] = vx3[k];
+  }
   __syncthreads();
   {  // conv3: thread (co, 4 ci of the block's 16) -> 36 weights
     const int co = tid >> 2, cq = tid & 3;
