@@ -25,6 +25,38 @@
 
 namespace mx {
 
+// Epilogue shared by the fp32 and bf16 engines.  Phase 1 requests every output's operands (bias,
+// mask, accumulate source: Op::spre, clamped indices) for all of the lane's TM x TN x 4 outputs;
+// phase 2 stores.  (store() loading its own operands was one dependent round trip per output.)
+// C/D map of the 16x16 MFMA tiles: col = lane & 15, row = (lane >> 4) * 4 + reg.
+template <class Op, int BM, int BN, int WM, int WN, int TM, int TN>
+__device__ __forceinline__ void igemm_epilogue(const Op& op, const f32x4 (&acc)[TM][TN], int m0, int n0, int wm,
+                                               int wn, int lane) {
+  typename Op::SP sp[TM][TN][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = min(n0 + wn * (BN / WN) + j * 16 + (lane & 15), op.N - 1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = min(m0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r, op.M - 1);
+        sp[i][j][r] = op.spre(m, n, blockIdx.z);
+      }
+    }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
+        if (m < op.M && n < op.N) op.store(m, n, acc[i][j][r], blockIdx.z, sp[i][j][r]);
+      }
+    }
+}
+
 template <class Op, int BM, int BN, int BK, int WM, int WN>
 __global__ __launch_bounds__(256) void igemm_f32_kernel(Op op, int k_split_len) {
   static_assert(WM * WN == 4, "4 waves per block");
@@ -68,25 +100,37 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(Op op, int k_split_len) 
   // two register sets of prefetched k-tiles: a tile's global loads are issued two k-tiles
   // before it is stored to LDS (one k-tile of MFMAs was too little to cover the load latency
   // on the long-K, few-block shapes: ~1 us per k-tile)
+  // Loads are branch-free: the op reads a clamped address and reports the element's validity
+  // (k, bounds, padding) as a bit; the zero is selected only at LDS-store time.  (A load behind a
+  // per-element test is a branch, and a select right after the load waits for it: either way the
+  // ISA showed s_waitcnt vmcnt(0) after every load, so the two prefetched register sets never
+  // actually overlapped the MFMAs.)
+  static_assert(EA <= 32 && EB <= 32, "validity bits");
   float ra0[EA], rb0[EB], ra1[EA], rb1[EB];
-  auto gload = [&](float (&ra)[EA], float (&rb)[EB], int k0) {
+  uint32_t va0 = 0, vb0 = 0, va1 = 0, vb1 = 0;
+  auto gload = [&](float (&ra)[EA], float (&rb)[EB], uint32_t& va, uint32_t& vb, int k0) {
+    va = vb = 0;
 #pragma unroll
     for (int i = 0; i < EA; ++i) {
       const int k = k0 + a_kl[i];
-      ra[i] = (k < kend) ? op.a_load(apre[i], k) : 0.f;
+      bool ok;
+      ra[i] = op.a_load(apre[i], min(k, kend - 1), ok);
+      va |= (ok && k < kend ? 1u : 0u) << i;
     }
 #pragma unroll
     for (int i = 0; i < EB; ++i) {
       const int k = k0 + b_kl[i];
-      rb[i] = (k < kend) ? op.b_load(bpre[i], k) : 0.f;
+      bool ok;
+      rb[i] = op.b_load(bpre[i], min(k, kend - 1), ok);
+      vb |= (ok && k < kend ? 1u : 0u) << i;
     }
   };
   static_assert(BK <= 16, "column swizzle assumes k-tile rows < 16");
-  auto sstore = [&](int buf, const float (&ra)[EA], const float (&rb)[EB]) {
+  auto sstore = [&](int buf, const float (&ra)[EA], const float (&rb)[EB], uint32_t va, uint32_t vb) {
 #pragma unroll
-    for (int i = 0; i < EA; ++i) As[buf][a_kl[i] * LDA + (a_ml[i] ^ (a_kl[i] & 14))] = ra[i];
+    for (int i = 0; i < EA; ++i) As[buf][a_kl[i] * LDA + (a_ml[i] ^ (a_kl[i] & 14))] = (va >> i) & 1u ? ra[i] : 0.f;
 #pragma unroll
-    for (int i = 0; i < EB; ++i) Bs[buf][b_kl[i] * LDB + (b_nl[i] ^ (b_kl[i] & 14))] = rb[i];
+    for (int i = 0; i < EB; ++i) Bs[buf][b_kl[i] * LDB + (b_nl[i] ^ (b_kl[i] & 14))] = (vb >> i) & 1u ? rb[i] : 0.f;
   };
 
   f32x4 acc[TM][TN];
@@ -117,36 +161,24 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(Op op, int k_split_len) 
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
     }
   };
-  gload(ra0, rb0, kbeg);
-  sstore(0, ra0, rb0);
+  gload(ra0, rb0, va0, vb0, kbeg);
+  sstore(0, ra0, rb0, va0, vb0);
   __syncthreads();
-  if (nt > 1) gload(ra0, rb0, kbeg + BK);      // k-tile 1 -> set 0
-  if (nt > 2) gload(ra1, rb1, kbeg + 2 * BK);  // k-tile 2 -> set 1
+  if (nt > 1) gload(ra0, rb0, va0, vb0, kbeg + BK);      // k-tile 1 -> set 0
+  if (nt > 2) gload(ra1, rb1, va1, vb1, kbeg + 2 * BK);  // k-tile 2 -> set 1
   // invariant at even t: LDS buffer 0 holds k-tile t, set 0 k-tile t + 1, set 1 k-tile t + 2
   for (int t = 0; t < nt; t += 2) {
     mfma_tile(0);
-    if (t + 1 < nt) sstore(1, ra0, rb0);
+    if (t + 1 < nt) sstore(1, ra0, rb0, va0, vb0);
     __syncthreads();
-    if (t + 3 < nt) gload(ra0, rb0, kbeg + (t + 3) * BK);
+    if (t + 3 < nt) gload(ra0, rb0, va0, vb0, kbeg + (t + 3) * BK);
     if (t + 1 >= nt) break;
     mfma_tile(1);
-    if (t + 2 < nt) sstore(0, ra1, rb1);
+    if (t + 2 < nt) sstore(0, ra1, rb1, va1, vb1);
     __syncthreads();
-    if (t + 4 < nt) gload(ra1, rb1, kbeg + (t + 4) * BK);
+    if (t + 4 < nt) gload(ra1, rb1, va1, vb1, kbeg + (t + 4) * BK);
   }
-
-  // C/D map of 16x16x4 f32: col = lane & 15, row = (lane >> 4) * 4 + reg.
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
-        if (m < op.M && n < op.N) op.store(m, n, acc[i][j][r], blockIdx.z);
-      }
-    }
+  igemm_epilogue<Op, BM, BN, WM, WN, TM, TN>(op, acc, m0, n0, wm, wn, lane);
 }
 
 // Host-side launcher.  `splits` > 1 splits the reduction dimension over gridDim.z;

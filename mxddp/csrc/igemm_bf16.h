@@ -56,24 +56,32 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(Op op, int k_split_len)
     else { b_kl[i] = e % BK; b_nl[i] = e / BK; }
     bpre[i] = op.b_pre(n0 + b_nl[i]);
   }
-  unsigned short ra[EA], rb[EB];
+  // raw values + validity bits, converted / zeroed at LDS-store time (see igemm.h)
+  static_assert(EA <= 32 && EB <= 32, "validity bits");
+  float ra[EA], rb[EB];
+  uint32_t va = 0, vb = 0;
   auto gload = [&](int k0) {
+    va = vb = 0;
 #pragma unroll
     for (int i = 0; i < EA; ++i) {
       const int k = k0 + a_kl[i];
-      ra[i] = f2bf((k < kend) ? op.a_load(apre[i], k) : 0.f);
+      bool ok;
+      ra[i] = op.a_load(apre[i], min(k, kend - 1), ok);
+      va |= (ok && k < kend ? 1u : 0u) << i;
     }
 #pragma unroll
     for (int i = 0; i < EB; ++i) {
       const int k = k0 + b_kl[i];
-      rb[i] = f2bf((k < kend) ? op.b_load(bpre[i], k) : 0.f);
+      bool ok;
+      rb[i] = op.b_load(bpre[i], min(k, kend - 1), ok);
+      vb |= (ok && k < kend ? 1u : 0u) << i;
     }
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < EA; ++i) As[buf][a_ml[i] * LD + a_kl[i]] = ra[i];
+    for (int i = 0; i < EA; ++i) As[buf][a_ml[i] * LD + a_kl[i]] = f2bf((va >> i) & 1u ? ra[i] : 0.f);
 #pragma unroll
-    for (int i = 0; i < EB; ++i) Bs[buf][b_nl[i] * LD + b_kl[i]] = rb[i];
+    for (int i = 0; i < EB; ++i) Bs[buf][b_nl[i] * LD + b_kl[i]] = f2bf((vb >> i) & 1u ? rb[i] : 0.f);
   };
 
   f32x4 acc[TM][TN];
@@ -109,17 +117,7 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(Op op, int k_split_len)
     if (t + 1 < nt) sstore(cur ^ 1);
     __syncthreads();
   }
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
-        if (m < op.M && n < op.N) op.store(m, n, acc[i][j][r], blockIdx.z);
-      }
-    }
+  igemm_epilogue<Op, BM, BN, WM, WN, TM, TN>(op, acc, m0, n0, wm, wn, lane);
 }
 
 template <class Op, int BM, int BN, int BK, int WM, int WN>

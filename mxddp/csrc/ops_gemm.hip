@@ -19,6 +19,17 @@ __device__ __forceinline__ void emit(float* out, int64_t idx, float v, int mode)
   else if (mode == kAccum) out[idx] += v;
   else atomicAdd(out + idx, v);
 }
+// Epilogue operands of one output, requested for ALL of a lane's outputs before any is stored
+// (igemm epilogue phase 1): bias, ReLU / mask source, accumulate source.  A load inside store()
+// was a branch + load + wait per output -- 16 to 32 dependent round trips per lane.
+struct SPre {
+  float b = 0.f, mk = 1.f, old = 0.f;
+};
+__device__ __forceinline__ void emit2(float* out, int64_t idx, float v, int mode, float old) {
+  if (mode == kStore) out[idx] = v;
+  else if (mode == kAccum) out[idx] = old + v;
+  else atomicAdd(out + idx, v);
+}
 
 // ------------------------------------------------------------------ conv geometry
 struct ConvG {
@@ -42,6 +53,7 @@ struct ConvG {
 
 // Forward: C[m=(n,p,q)][kout] = sum_{k=(c,r,s)} x[n,c,p*sh-ph+r*dh, q*sw-pw+s*dw] * w[kout,c,r,s]
 struct ConvFwdOp {
+  using SP = SPre;
   static constexpr bool A_MFAST = true;   // consecutive q -> coalesced input rows
   static constexpr bool B_NFAST = false;  // weights read along (c,r,s)
   int M, N, K;
@@ -66,23 +78,33 @@ struct ConvFwdOp {
     a.base = (int64_t)n * g.C * g.HW;
     return a;
   }
-  __device__ float a_load(const APre& a, int k) const {
+  __device__ float a_load(const APre& a, int k, bool& ok) const {
     const int c = g.fRS.div(k), rs = k - c * g.RS;
     const int r = g.fS.div(rs), s = rs - r * g.S;
     const int h = a.h0 + r * g.dh, ww = a.w0 + s * g.dw;
-    if (!a.ok || (unsigned)h >= (unsigned)g.H || (unsigned)ww >= (unsigned)g.W) return 0.f;
-    return x[a.base + (int64_t)c * g.HW + h * g.W + ww];
+    ok = a.ok && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
+    // clamped address, validity returned: the select happens at LDS-store time (a load behind the
+    // bounds test is a branch, and a select right after it waits for the load)
+    return x[a.base + (int64_t)c * g.HW + min(max(h, 0), g.H - 1) * g.W + min(max(ww, 0), g.W - 1)];
   }
   __device__ BPre b_pre(int n) const { return BPre{(int64_t)(n < N ? n : 0) * K, n < N}; }
-  __device__ float b_load(const BPre& b, int k) const { return b.ok ? w[b.base + k] : 0.f; }
-  __device__ void store(int m, int n, float v, int split) const {
+  __device__ float b_load(const BPre& b, int k, bool& ok) const {
+    ok = b.ok;
+    return w[b.base + k];
+  }
+  __device__ SPre spre(int, int n, int) const {
+    SPre p;
+    if (!part && bias) p.b = bias[n];
+    return p;
+  }
+  __device__ void store(int m, int n, float v, int split, const SPre& p) const {
     const int nb = g.fPQ.div(m), pq = m - nb * g.PQ;
     const int64_t idx = ((int64_t)nb * g.K + n) * g.PQ + pq;
     if (part) {
       part[split * ptotal + idx] = v;
       return;
     }
-    if (bias) v += bias[n];
+    v += p.b;
     if (relu) v = fmaxf(v, 0.f);
     y[idx] = v;
   }
@@ -91,6 +113,7 @@ struct ConvFwdOp {
 // Data gradient: C[m=(n,h,w)][c] = sum_{k=(kout,r,s)} dy[n,kout,p,q] * w[kout,c,r,s]
 //   with p = (h + ph - r*dh)/sh when divisible and in range.
 struct ConvDgradOp {
+  using SP = SPre;
   static constexpr bool A_MFAST = true;
   static constexpr bool B_NFAST = true;
   int M, N, K;
@@ -112,33 +135,40 @@ struct ConvDgradOp {
     a.base = (int64_t)n * g.K * g.PQ;
     return a;
   }
-  __device__ float a_load(const APre& a, int k) const {
+  __device__ float a_load(const APre& a, int k, bool& ok) const {
     const int ko = g.fRS.div(k), rs = k - ko * g.RS;
     const int r = g.fS.div(rs), s = rs - r * g.S;
-    int ph_ = a.h + g.ph - r * g.dh, pw_ = a.w + g.pw - s * g.dw;
-    if (!a.ok || ph_ < 0 || pw_ < 0) return 0.f;
-    int p = ph_, q = pw_;
-    if (g.sh != 1) { p = ph_ / g.sh; if (p * g.sh != ph_) return 0.f; }
-    if (g.sw != 1) { q = pw_ / g.sw; if (q * g.sw != pw_) return 0.f; }
-    if (p >= g.P || q >= g.Q) return 0.f;
-    return dy[a.base + (int64_t)ko * g.PQ + p * g.Q + q];
+    const int ph_ = a.h + g.ph - r * g.dh, pw_ = a.w + g.pw - s * g.dw;
+    const int p = ph_ >= 0 ? ph_ / g.sh : -1, q = pw_ >= 0 ? pw_ / g.sw : -1;
+    ok = a.ok && ph_ >= 0 && pw_ >= 0 && p * g.sh == ph_ && q * g.sw == pw_ && p < g.P && q < g.Q;
+    return dy[a.base + (int64_t)ko * g.PQ + min(max(p, 0), g.P - 1) * g.Q + min(max(q, 0), g.Q - 1)];
   }
   __device__ BPre b_pre(int n) const { return BPre{n, n < N}; }
-  __device__ float b_load(const BPre& b, int k) const {
-    if (!b.ok) return 0.f;
+  __device__ float b_load(const BPre& b, int k, bool& ok) const {
     const int ko = g.fRS.div(k), rs = k - ko * g.RS;
-    return w[((int64_t)ko * g.C + b.n) * g.RS + rs];
+    ok = b.ok;
+    return w[((int64_t)ko * g.C + (b.ok ? b.n : 0)) * g.RS + rs];
   }
-  __device__ void store(int m, int n, float v, int) const {
+  __device__ int64_t oidx(int m, int n) const {
     const int nb = g.fHW.div(m), hw = m - nb * g.HW;
-    const int64_t idx = ((int64_t)nb * g.C + n) * g.HW + hw;
-    if (mask && !(mask[idx] > 0.f)) v = 0.f;
-    emit(dx, idx, v, mode);
+    return ((int64_t)nb * g.C + n) * g.HW + hw;
+  }
+  __device__ SPre spre(int m, int n, int) const {
+    SPre p;
+    const int64_t idx = oidx(m, n);
+    if (mask) p.mk = mask[idx];
+    if (mode == kAccum) p.old = dx[idx];
+    return p;
+  }
+  __device__ void store(int m, int n, float v, int, const SPre& p) const {
+    if (mask && !(p.mk > 0.f)) v = 0.f;
+    emit2(dx, oidx(m, n), v, mode, p.old);
   }
 };
 
 // Weight gradient: C[kout][n=(c,r,s)] = sum_{k=(n,p,q)} dy[n,kout,p,q] * x[n,c,h,w]
 struct ConvWgradOp {
+  using SP = SPre;
   static constexpr bool A_MFAST = false;  // consecutive k = consecutive q: coalesced dy rows
   static constexpr bool B_NFAST = false;  // consecutive k: coalesced x rows
   int M, N, K;
@@ -154,10 +184,10 @@ struct ConvWgradOp {
   struct APre { int m; bool ok; };
   struct BPre { int64_t coff; int r, s; bool ok, one; };
   __device__ APre a_pre(int m) const { return APre{m, m < M}; }
-  __device__ float a_load(const APre& a, int k) const {
-    if (!a.ok) return 0.f;
+  __device__ float a_load(const APre& a, int k, bool& ok) const {
     const int nb = g.fPQ.div(k), pq = k - nb * g.PQ;
-    return dy[((int64_t)nb * g.K + a.m) * g.PQ + pq];
+    ok = a.ok;
+    return dy[((int64_t)nb * g.K + (a.ok ? a.m : 0)) * g.PQ + pq];
   }
   __device__ BPre b_pre(int n) const {
     BPre b;
@@ -172,17 +202,22 @@ struct ConvWgradOp {
     b.coff = (int64_t)c * g.HW;
     return b;
   }
-  __device__ float b_load(const BPre& b, int k) const {
-    if (b.one) return 1.f;
+  __device__ float b_load(const BPre& b, int k, bool& ok) const {
     const int nb = g.fPQ.div(k), pq = k - nb * g.PQ;
     const int p = g.fQ.div(pq), q = pq - p * g.Q;
     const int h = p * g.sh - g.ph + b.r, ww = q * g.sw - g.pw + b.s;
-    if (!b.ok || (unsigned)h >= (unsigned)g.H || (unsigned)ww >= (unsigned)g.W) return 0.f;
-    return x[(int64_t)nb * g.C * g.HW + b.coff + h * g.W + ww];
+    ok = b.one || (b.ok && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W);
+    const float v = x[(int64_t)nb * g.C * g.HW + b.coff + min(max(h, 0), g.H - 1) * g.W + min(max(ww, 0), g.W - 1)];
+    return b.one ? 1.f : v;
   }
-  __device__ void store(int m, int n, float v, int) const {
-    if (n == nw) emit(db, m, v, mode);  // only reached when db is set (n < N = nw + 1)
-    else emit(dw, (int64_t)m * nw + n, v, mode);
+  __device__ SPre spre(int m, int n, int) const {
+    SPre p;
+    if (mode == kAccum) p.old = (db != nullptr && n == nw) ? db[m] : dw[(int64_t)m * nw + min(n, nw - 1)];
+    return p;
+  }
+  __device__ void store(int m, int n, float v, int, const SPre& p) const {
+    if (n == nw) emit2(db, m, v, mode, p.old);  // only reached when db is set (n < N = nw + 1)
+    else emit2(dw, (int64_t)m * nw + n, v, mode, p.old);
   }
 };
 
@@ -190,6 +225,7 @@ struct ConvWgradOp {
 // (ResNet bottlenecks): plain batched GEMMs over (n, hw) with channel-strided operands; no
 // im2col index math per element.
 struct Conv1x1FwdOp {  // y[n,k,hw] = sum_c x[n,c,hw] w[k,c]
+  using SP = SPre;
   static constexpr bool A_MFAST = true;   // consecutive m = consecutive hw
   static constexpr bool B_NFAST = false;  // w rows contiguous along c
   int M, N, K;
@@ -206,18 +242,30 @@ struct Conv1x1FwdOp {  // y[n,k,hw] = sum_c x[n,c,hw] w[k,c]
     const int mm = m < M ? m : 0, nb = fHW.div(mm), hw = mm - nb * HW;
     return APre{(int64_t)nb * K * HW + hw, m < M};
   }
-  __device__ float a_load(const APre& a, int k) const { return a.ok ? x[a.base + (int64_t)k * HW] : 0.f; }
+  __device__ float a_load(const APre& a, int k, bool& ok) const {
+    ok = a.ok;
+    return x[a.base + (int64_t)k * HW];
+  }
   __device__ BPre b_pre(int n) const { return BPre{(int64_t)(n < N ? n : 0) * K, n < N}; }
-  __device__ float b_load(const BPre& b, int k) const { return b.ok ? w[b.base + k] : 0.f; }
-  __device__ void store(int m, int n, float v, int) const {
+  __device__ float b_load(const BPre& b, int k, bool& ok) const {
+    ok = b.ok;
+    return w[b.base + k];
+  }
+  __device__ SPre spre(int, int n, int) const {
+    SPre p;
+    if (bias) p.b = bias[n];
+    return p;
+  }
+  __device__ void store(int m, int n, float v, int, const SPre& p) const {
     const int nb = fHW.div(m), hw = m - nb * HW;
-    if (bias) v += bias[n];
+    v += p.b;
     if (relu) v = fmaxf(v, 0.f);
     y[((int64_t)nb * N + n) * HW + hw] = v;
   }
 };
 
 struct Conv1x1DgradOp {  // dx[n,c,hw] = sum_k dy[n,k,hw] w[k,c]
+  using SP = SPre;
   static constexpr bool A_MFAST = true;
   static constexpr bool B_NFAST = true;   // w[k, c]: consecutive c contiguous
   int M, N, K;
@@ -234,14 +282,29 @@ struct Conv1x1DgradOp {  // dx[n,c,hw] = sum_k dy[n,k,hw] w[k,c]
     const int mm = m < M ? m : 0, nb = fHW.div(mm), hw = mm - nb * HW;
     return APre{(int64_t)nb * K * HW + hw, m < M};
   }
-  __device__ float a_load(const APre& a, int k) const { return a.ok ? dy[a.base + (int64_t)k * HW] : 0.f; }
-  __device__ BPre b_pre(int n) const { return BPre{n, n < N}; }
-  __device__ float b_load(const BPre& b, int k) const { return b.ok ? w[(int64_t)k * N + b.n] : 0.f; }
-  __device__ void store(int m, int n, float v, int) const {
+  __device__ float a_load(const APre& a, int k, bool& ok) const {
+    ok = a.ok;
+    return dy[a.base + (int64_t)k * HW];
+  }
+  __device__ BPre b_pre(int n) const { return BPre{n < N ? n : 0, n < N}; }
+  __device__ float b_load(const BPre& b, int k, bool& ok) const {
+    ok = b.ok;
+    return w[(int64_t)k * N + b.n];
+  }
+  __device__ int64_t oidx(int m, int n) const {
     const int nb = fHW.div(m), hw = m - nb * HW;
-    const int64_t idx = ((int64_t)nb * N + n) * HW + hw;
-    if (mask && !(mask[idx] > 0.f)) v = 0.f;
-    emit(dx, idx, v, mode);
+    return ((int64_t)nb * N + n) * HW + hw;
+  }
+  __device__ SPre spre(int m, int n, int) const {
+    SPre p;
+    const int64_t idx = oidx(m, n);
+    if (mask) p.mk = mask[idx];
+    if (mode == kAccum) p.old = dx[idx];
+    return p;
+  }
+  __device__ void store(int m, int n, float v, int, const SPre& p) const {
+    if (mask && !(p.mk > 0.f)) v = 0.f;
+    emit2(dx, oidx(m, n), v, mode, p.old);
   }
 };
 
@@ -251,6 +314,7 @@ bool is_1x1_s1(const ConvShape& s) {
 
 // ------------------------------------------------------------------ linear
 struct LinFwdOp {  // y[M,N] = x[M,K] w[N,K]^T + b
+  using SP = SPre;
   static constexpr bool A_MFAST = false;
   static constexpr bool B_NFAST = false;
   int M, N, K;
@@ -266,21 +330,35 @@ struct LinFwdOp {  // y[M,N] = x[M,K] w[N,K]^T + b
   using APre = Pre;
   using BPre = Pre;
   __device__ Pre a_pre(int m) const { return Pre{(int64_t)(m < M ? m : 0) * K, m < M}; }
-  __device__ float a_load(const Pre& a, int k) const { return a.ok ? x[a.base + k] : 0.f; }
+  __device__ float a_load(const Pre& a, int k, bool& ok) const {
+    ok = a.ok;
+    return x[a.base + k];
+  }
   __device__ Pre b_pre(int n) const { return Pre{(int64_t)(n < N ? n : 0) * K, n < N}; }
-  __device__ float b_load(const Pre& p, int k) const { return p.ok ? w[p.base + k] : 0.f; }
-  __device__ void store(int m, int n, float v, int split) const {
+  __device__ float b_load(const Pre& p, int k, bool& ok) const {
+    ok = p.ok;
+    return w[p.base + k];
+  }
+  __device__ SPre spre(int m, int n, int split) const {
+    SPre p;
+    if (part) return p;
+    if (b && split == 0) p.b = b[n];
+    if (mode == kAccum) p.old = y[(int64_t)m * N + n];
+    return p;
+  }
+  __device__ void store(int m, int n, float v, int split, const SPre& p) const {
     if (part) {
       part[split * ptotal + (int64_t)m * N + n] = v;
       return;
     }
-    if (b && split == 0) v += b[n];
+    v += p.b;
     if (relu) v = fmaxf(v, 0.f);
-    emit(y, (int64_t)m * N + n, v, mode);
+    emit2(y, (int64_t)m * N + n, v, mode, p.old);
   }
 };
 
 struct LinDgradOp {  // dx[M,Kin] = dy[M,Nout] w[Nout,Kin]; GEMM N=Kin, K=Nout
+  using SP = SPre;
   static constexpr bool A_MFAST = false;
   static constexpr bool B_NFAST = true;
   int M, N, K;
@@ -295,25 +373,36 @@ struct LinDgradOp {  // dx[M,Kin] = dy[M,Nout] w[Nout,Kin]; GEMM N=Kin, K=Nout
   struct APre { int64_t base; bool ok; };
   struct BPre { int n; bool ok; };
   __device__ APre a_pre(int m) const { return APre{(int64_t)(m < M ? m : 0) * K, m < M}; }
-  __device__ float a_load(const APre& a, int k) const {
-    if (!a.ok) return 0.f;
-    const float v = dy[a.base + k];
-    return (amask && !(amask[a.base + k] > 0.f)) ? 0.f : v;
+  __device__ float a_load(const APre& a, int k, bool& ok) const {
+    ok = a.ok && (!amask || amask[a.base + k] > 0.f);  // (amask: off by default)
+    return dy[a.base + k];
   }
-  __device__ BPre b_pre(int n) const { return BPre{n, n < N}; }
-  __device__ float b_load(const BPre& b, int k) const { return b.ok ? w[(int64_t)k * N + b.n] : 0.f; }
-  __device__ void store(int m, int n, float v, int split) const {
+  __device__ BPre b_pre(int n) const { return BPre{n < N ? n : 0, n < N}; }
+  __device__ float b_load(const BPre& b, int k, bool& ok) const {
+    ok = b.ok;
+    return w[(int64_t)k * N + b.n];
+  }
+  __device__ SPre spre(int m, int n, int) const {
+    SPre p;
+    if (part) return p;
+    const int64_t idx = (int64_t)m * N + n;
+    if (mask) p.mk = mask[idx];
+    if (mode == kAccum) p.old = dx[idx];
+    return p;
+  }
+  __device__ void store(int m, int n, float v, int split, const SPre& p) const {
     const int64_t idx = (int64_t)m * N + n;
     if (part) {
       part[split * ptotal + idx] = v;
       return;
     }
-    if (mask && !(mask[idx] > 0.f)) v = 0.f;
-    emit(dx, idx, v, mode);
+    if (mask && !(p.mk > 0.f)) v = 0.f;
+    emit2(dx, idx, v, mode, p.old);
   }
 };
 
 struct LinWgradOp {  // dw[Nout,Kin] = dy[B,Nout]^T x[B,Kin]; GEMM M=Nout, N=Kin, K=B
+  using SP = SPre;
   static constexpr bool A_MFAST = true;
   static constexpr bool B_NFAST = true;
   int M, N, K;
@@ -324,15 +413,22 @@ struct LinWgradOp {  // dw[Nout,Kin] = dy[B,Nout]^T x[B,Kin]; GEMM M=Nout, N=Kin
   const float* amask = nullptr;  // dy masked on load by (amask > 0) (see LinDgradOp)
   struct APre { int m; bool ok; };
   struct BPre { int n; bool ok; };
-  __device__ APre a_pre(int m) const { return APre{m, m < M}; }
-  __device__ float a_load(const APre& a, int k) const {
-    if (!a.ok) return 0.f;
-    const float v = dy[(int64_t)k * M + a.m];
-    return (amask && !(amask[(int64_t)k * M + a.m] > 0.f)) ? 0.f : v;
+  __device__ APre a_pre(int m) const { return APre{m < M ? m : 0, m < M}; }
+  __device__ float a_load(const APre& a, int k, bool& ok) const {
+    ok = a.ok && (!amask || amask[(int64_t)k * M + a.m] > 0.f);  // (amask: off by default)
+    return dy[(int64_t)k * M + a.m];
   }
-  __device__ BPre b_pre(int n) const { return BPre{n, n < N}; }
-  __device__ float b_load(const BPre& b, int k) const { return b.ok ? x[(int64_t)k * N + b.n] : 0.f; }
-  __device__ void store(int m, int n, float v, int) const { emit(dw, (int64_t)m * N + n, v, mode); }
+  __device__ BPre b_pre(int n) const { return BPre{n < N ? n : 0, n < N}; }
+  __device__ float b_load(const BPre& b, int k, bool& ok) const {
+    ok = b.ok;
+    return x[(int64_t)k * N + b.n];
+  }
+  __device__ SPre spre(int m, int n, int) const {
+    SPre p;
+    if (mode == kAccum) p.old = dw[(int64_t)m * N + n];
+    return p;
+  }
+  __device__ void store(int m, int n, float v, int, const SPre& p) const { emit2(dw, (int64_t)m * N + n, v, mode, p.old); }
 };
 
 int g_gemm_precision = 0;  // 0 = fp32 MFMA (exact), 1 = bf16 operands / fp32 accumulate

@@ -262,6 +262,68 @@ __device__ __forceinline__ unsigned window_mask(int h0, int w0) {
   return m;
 }
 
+// Output of one lane: 4 output channels co4 .. co4 + 3 of output tile T (2 x 2 pixels each) with
+// bias / ReLU / mask / accumulate.  Every operand (bias, ReLU-mask source, accumulate source) is
+// requested before any is used, with clamped indices and only flag-level (uniform) branches:
+// the previous per-pixel form waited for each load in turn (~40 dependent round trips per lane in
+// the forward kernels' epilogues, visible as s_waitcnt vmcnt(0) before every use in the ISA).
+template <int W>
+__device__ __forceinline__ void wino_epilogue(const WinoArgs& a, const float (&yt)[4][2][2], int T, int ntiles,
+                                              int co4, int sp) {
+  constexpr int TW = W / 2, TPI = TW * TW, HW = W * W;
+  const bool tok = T < ntiles;
+  const int Tc = tok ? T : 0;
+  const int n = Tc / TPI, rem = Tc - n * TPI, oh = 2 * (rem / TW), ow = 2 * (rem % TW);
+  size_t o[4][2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      o[r][p] = ((size_t)n * a.Co + min(co4 + r, a.Co - 1)) * HW + (size_t)(oh + p) * W + ow;
+  float bv[4] = {0.f, 0.f, 0.f, 0.f};
+  float2 mk[4][2], old[4][2];
+  if (a.bias && sp == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = a.bias[min(co4 + r, a.Co - 1)];
+  }
+  if (a.mask) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) mk[r][p] = *reinterpret_cast<const float2*>(a.mask + o[r][p]);
+  }
+  if (a.accumulate == 1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) old[r][p] = *reinterpret_cast<const float2*>(a.y + o[r][p]);
+  }
+  if (!tok) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (co4 + r >= a.Co) continue;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      float2 v = make_float2(yt[r][p][0] + bv[r], yt[r][p][1] + bv[r]);
+      if (a.accumulate == 2) {
+        atomicAdd(a.y + o[r][p], v.x);
+        atomicAdd(a.y + o[r][p] + 1, v.y);
+        continue;
+      }
+      if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); }
+      if (a.mask) {
+        if (!(mk[r][p].x > 0.f)) v.x = 0.f;
+        if (!(mk[r][p].y > 0.f)) v.y = 0.f;
+      }
+      if (a.accumulate == 1) {
+        v.x += old[r][p].x;
+        v.y += old[r][p].y;
+      }
+      *reinterpret_cast<float2*>(a.y + o[r][p]) = v;
+    }
+  }
+}
+
 // Block: 32 output channels x 32 output tiles; wave (wm, wn) owns 16 x 16 of it for all 16 xi
 // (16 accumulators = 64 registers) -> ~120 VGPRs, 3 blocks (12 waves) per CU.
 // KS = 2 (small images, where 32 x 32 blocks leave ~1 wave per SIMD): 8 waves per block in two
@@ -373,38 +435,7 @@ __global__ __launch_bounds__(256 * KS, kOcc) void wino_fwd_kernel(WinoArgs a) {
       yt[r][1][1] += o.w;
     }
   }
-  const int T = tb * 32 + 16 * wn + l16;
-  if (T >= ntiles) return;
-  const int n = T / TPI, rem = T - n * TPI, oh = 2 * (rem / TW), ow = 2 * (rem % TW);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int co = co0 + 16 * wm + 4 * g + r;
-    if (co >= a.Co) continue;
-    const float (&y)[2][2] = yt[r];
-    const float bv = (a.bias && sp == 0) ? a.bias[co] : 0.f;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const size_t o = ((size_t)n * a.Co + co) * HW + (size_t)(oh + p) * W + ow;
-      float2 v = make_float2(y[p][0] + bv, y[p][1] + bv);
-      if (a.accumulate == 2) {
-        atomicAdd(a.y + o, v.x);
-        atomicAdd(a.y + o + 1, v.y);
-        continue;
-      }
-      if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); }
-      if (a.mask) {
-        const float2 mk = *reinterpret_cast<const float2*>(a.mask + o);
-        if (!(mk.x > 0.f)) v.x = 0.f;
-        if (!(mk.y > 0.f)) v.y = 0.f;
-      }
-      if (a.accumulate) {
-        const float2 old = *reinterpret_cast<const float2*>(a.y + o);
-        v.x += old.x;
-        v.y += old.y;
-      }
-      *reinterpret_cast<float2*>(a.y + o) = v;
-    }
-  }
+  wino_epilogue<W>(a, yt, tb * 32 + 16 * wn + l16, ntiles, co0 + 16 * wm + 4 * g, sp);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -550,44 +581,21 @@ __global__ __launch_bounds__(256, 2) void wino_fwd_patch_kernel(WinoArgs a) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int T = tb * 64 + 32 * wn + 16 * j + l16;
-    if (T >= ntiles) continue;
-    const int n = T / TPI, rem = T - n * TPI, oh = 2 * (rem / TW), ow = 2 * (rem % TW);
+    float yt[4][2][2];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int co = co0 + 16 * wm + 4 * g + r;
-      if (co >= a.Co) continue;
       float t0[4], t1[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         t0[c] = acc[0 + c][j][r] + acc[4 + c][j][r] + acc[8 + c][j][r];
         t1[c] = acc[4 + c][j][r] - acc[8 + c][j][r] - acc[12 + c][j][r];
       }
-      const float y[2][2] = {{t0[0] + t0[1] + t0[2], t0[1] - t0[2] - t0[3]},
-                             {t1[0] + t1[1] + t1[2], t1[1] - t1[2] - t1[3]}};
-      const float bv = (a.bias && sp == 0) ? a.bias[co] : 0.f;
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const size_t o = ((size_t)n * a.Co + co) * HW + (size_t)(oh + p) * W + ow;
-        float2 v = make_float2(y[p][0] + bv, y[p][1] + bv);
-        if (a.accumulate == 2) {
-          atomicAdd(a.y + o, v.x);
-          atomicAdd(a.y + o + 1, v.y);
-          continue;
-        }
-        if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); }
-        if (a.mask) {
-          const float2 mk = *reinterpret_cast<const float2*>(a.mask + o);
-          if (!(mk.x > 0.f)) v.x = 0.f;
-          if (!(mk.y > 0.f)) v.y = 0.f;
-        }
-        if (a.accumulate) {
-          const float2 old = *reinterpret_cast<const float2*>(a.y + o);
-          v.x += old.x;
-          v.y += old.y;
-        }
-        *reinterpret_cast<float2*>(a.y + o) = v;
-      }
+      yt[r][0][0] = t0[0] + t0[1] + t0[2];
+      yt[r][0][1] = t0[1] - t0[2] - t0[3];
+      yt[r][1][0] = t1[0] + t1[1] + t1[2];
+      yt[r][1][1] = t1[1] - t1[2] - t1[3];
     }
+    wino_epilogue<W>(a, yt, T, ntiles, co0 + 16 * wm + 4 * g, sp);
   }
 }
 
