@@ -586,6 +586,159 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Stem forward: 7x7 / stride 2 / pad 3 over an 8-channel (padded) image, 64 output channels,
+// output height and width multiples of 16 (ResNet-50's conv1 at any batch).  The generic gather
+// kernel re-fetches every input pixel from L2 for each of the 49 taps that read it (Kg = 392 in
+// 8-channel gathers with per-element tap arithmetic: 510 us at batch 256, 8x its byte floor).
+// Here a block owns a 16 x 16 output tile and stages its 37 x 38 input patch in LDS ONCE, plus
+// the whole filter bank in an MFMA-ready layout; the B fragments are then read straight out of
+// the patch with no im2col: with k ordered (r, s, c) and s padded to 8 (s = 7 has zero weights),
+// one 32-deep k-step is half a filter row, and lane group g's 8 consecutive k are the 8 channels
+// of tap s = 4h + g -- one 16-byte LDS read of patch pixel (2 oh + r, 2 ow + s).  For the 16
+// lanes of a group the reads are 32 bytes apart, which the ds_read_b128 lane groups
+// ({0-3,12-15,20-27}, ...) map onto 16 distinct 16-byte bank slots.
+//   8 waves: wave w computes output rows 2w, 2w + 1 (two 16-pixel column tiles) x 64 channels
+//   (4 row tiles), 14 k-steps of 8 MFMAs.  LDS: filters [64][456 bf16] (912 B pitch: the 16
+//   channels of a fragment read hit distinct bank slots), patch [37][38][16 B]: 79 KB, two blocks
+//   per CU.  Epilogue as the LDS-DMA kernel: C tile staged in LDS -> 16-byte stores, optional BN
+//   partial sums (one row per tile).
+constexpr int kStemWP = 456, kStemPW = 38, kStemPH = 37;
+constexpr int kStemA = 64 * kStemWP * 2, kStemP = kStemPH * kStemPW * 16;
+
+template <bool STATS>
+__global__ __launch_bounds__(512, 4) void conv_nhwc_stem_kernel(ConvNArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[kStemA + kStemP];
+  char* As = smem;
+  char* Ps = smem + kStemA;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  const int tw_n = a.OW >> 4, th_n = a.OH >> 4;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int n = bid / (th_n * tw_n), trem = bid - n * th_n * tw_n;
+  const int oh0 = (trem / tw_n) * 16, ow0 = (trem % tw_n) * 16;
+  const int ih0 = 2 * oh0 - 3, iw0 = 2 * ow0 - 3;
+
+  // stage: filters (64 ch x 7 r x 8 s 16-byte vectors, s = 7 zero) and the input patch; every
+  // load of the thread is issued before the first store
+  constexpr int NAV = 64 * 7 * 8 / 512, NPV = (kStemPH * kStemPW + 511) / 512;
+  u32x4 av[NAV], pv[NPV];
+  const u32x4 z4 = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int i = 0; i < NAV; ++i) {
+    const int v = tid + 512 * i, ch = v / 56, rs8 = v - ch * 56, r = rs8 >> 3, s = rs8 & 7;
+    av[i] = s < 7 ? *reinterpret_cast<const u32x4*>(a.wt + ((size_t)ch * 49 + r * 7 + s) * 8) : z4;
+  }
+  const bf16* xin = a.act + (size_t)n * a.IH * a.IW * 8;
+#pragma unroll
+  for (int i = 0; i < NPV; ++i) {
+    const int v = min(tid + 512 * i, kStemPH * kStemPW - 1), pr = v / kStemPW, pc = v - pr * kStemPW;
+    const int ih = ih0 + pr, iw = iw0 + pc;
+    const bool ok = (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW && pc < 37;
+    pv[i] = *reinterpret_cast<const u32x4*>(xin + (size_t)(ok ? ih * a.IW + iw : 0) * 8);
+    if (!ok) pv[i] = z4;
+  }
+#pragma unroll
+  for (int i = 0; i < NAV; ++i) {
+    const int v = tid + 512 * i, ch = v / 56, rs8 = v - ch * 56;
+    *reinterpret_cast<u32x4*>(As + ch * (kStemWP * 2) + rs8 * 16) = av[i];
+  }
+#pragma unroll
+  for (int i = 0; i < NPV; ++i) {
+    const int v = tid + 512 * i;
+    if (v < kStemPH * kStemPW) *reinterpret_cast<u32x4*>(Ps + v * 16) = pv[i];
+  }
+  __syncthreads();
+
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const char* arow = As + m * (kStemWP * 2) + g * 16;
+  const char* prow = Ps + ((4 * w) * kStemPW + 2 * m + g) * 16;  // output row 2w, tap (0, g)
+#pragma unroll 2
+  for (int r = 0; r < 7; ++r) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 fa[4], fb[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(arow + i * 16 * (kStemWP * 2) + (r * 64 + 32 * h) * 2);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)  // output row 2w + j reads patch row 2 (2w + j) + r
+        fb[j] = *reinterpret_cast<const bf16x8*>(prow + ((2 * j + r) * kStemPW + 4 * h) * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // every wave done with the filters and the patch
+
+  // C tile [256 pixels][64 channels] (pitch 72) over the filter region; pixel = 16 row + col
+  constexpr int CP = 72;
+  bf16* Cs = reinterpret_cast<bf16*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      *reinterpret_cast<uint2*>(Cs + ((2 * w + j) * 16 + m) * CP + 16 * i + 4 * g) =
+          make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int v = tid + 512 * k, px = v >> 3, cv = v & 7;
+    const size_t o = (((size_t)n * a.OH + oh0 + (px >> 4)) * a.OW + ow0 + (px & 15)) * 64 + 8 * cv;
+    *reinterpret_cast<u32x4*>(a.out + o) = *reinterpret_cast<const u32x4*>(Cs + px * CP + 8 * cv);
+  }
+  if constexpr (STATS) {  // BN partial sums of the stored (bf16) tile: 8 threads per channel
+    float* bred = reinterpret_cast<float*>(smem + 256 * CP * 2);
+    const int c = tid & 63, q = tid >> 6;
+    const float K = a.bnshift ? a.bnshift[c] : 0.f;
+    const uint16_t* col = reinterpret_cast<const uint16_t*>(Cs) + c;
+    float s1[8], s2[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s1[u] = s2[u] = 0.f;
+#pragma unroll
+    for (int r0 = 0; r0 < 32; r0 += 8) {
+      uint16_t hv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) hv[u] = col[(32 * q + r0 + u) * CP];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float d = bf2f(hv[u]) - K;
+        s1[u] += d;
+        s2[u] = fmaf(d, d, s2[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 1; u < 8; ++u) {
+      s1[0] += s1[u];
+      s2[0] += s2[u];
+    }
+    bred[tid] = s1[0];
+    bred[512 + tid] = s2[0];
+    __syncthreads();
+    if (q == 0) {
+      float t1 = s1[0], t2 = s2[0];
+      for (int k = 1; k < 8; ++k) {
+        t1 += bred[tid + 64 * k];
+        t2 += bred[512 + tid + 64 * k];
+      }
+      float* dst = a.bnpart + (size_t)blockIdx.x * 128 + 2 * c;
+      dst[0] = t1;
+      dst[1] = t2;
+    }
+  }
+}
+
+static bool stem_eligible(const ConvNArgs& a) {
+  return !a.dgrad && a.Ca == 8 && a.R == 7 && a.S == 7 && a.sh == 2 && a.sw == 2 && a.ph == 3 && a.pw == 3 &&
+         a.Ng == 64 && a.OH % 16 == 0 && a.OW % 16 == 0 && !a.addend && a.OH == (a.IH + 6 - 7) / 2 + 1 &&
+         a.OW == (a.IW + 6 - 7) / 2 + 1;
+}
+
 // split-K epilogue: out (bf16) = sum over splits of the fp32 partials (fixed order)
 __global__ void conv_nhwc_splitk_reduce_k(const float* __restrict__ part, bf16* __restrict__ out, int64_t n4,
                                           int splits, const bf16* __restrict__ addend) {
@@ -833,8 +986,16 @@ __global__ void wrepack_k(const float* __restrict__ w, bf16* __restrict__ wt, bf
 
 // Every convolution of a model in ONE launch (nhwc_repack_many): desc[i] = {w, wt, wtd, K, C,
 // R*S, Cp, first block}; block b finds its convolution by binary search over the first-block
-// column, then strides over that convolution's elements (32-bit indices, 8 per thread).
+// column.  K % 8 == 0: the convolution's first cdiv(K*RS*Cp, 2048) blocks write the forward
+// layout (8 outputs per thread, one 16-byte store), the rest are 64 x 64 tiles of the data-gradient
+// layout, which is the transpose of w viewed as [K][C*RS]: read as coalesced rows into LDS, written
+// as 16-byte vectors along k.  (A thread gathering 8 k straight from global read 8 cache lines
+// 4 bytes each, C*RS*4 bytes apart: the one-launch repack ran at ~1.2 TB/s, 174 us per ResNet-50
+// step.)  Otherwise every block strides over the convolution's elements (32-bit indices).
 constexpr int kRepackPerBlock = 256 * 8;
+constexpr int kRepackT = 64;  // data-gradient transpose tile (k x crs)
+
+__host__ __device__ inline int repack_fwd_blocks(int64_t nf) { return (int)((nf + kRepackPerBlock - 1) / kRepackPerBlock); }
 
 __global__ __launch_bounds__(256) void wrepack_many_k(const int64_t* __restrict__ desc, int n) {
   int lo = 0, hi = n - 1;
@@ -850,24 +1011,41 @@ __global__ __launch_bounds__(256) void wrepack_many_k(const int64_t* __restrict_
   const int nb = (lo + 1 < n ? (int)desc[(lo + 1) * 8 + 7] : (int)gridDim.x) - b0;
   const int tf = wt ? K * RS * Cp : 0, td = wtd ? C * RS * K : 0;
   if ((K & 7) == 0) {
-    // 8 consecutive outputs per thread (8 channels of one fwd (k, tap) row, or 8 output channels
-    // of one dgrad (c, tap) row): one 16-byte store instead of eight 2-byte ones (WeightPack
-    // places every layout at a 64-element boundary, so the stores are aligned)
-    for (int e = (((int)blockIdx.x - b0) * 256 + threadIdx.x) * 8; e < tf + td; e += nb * 256 * 8) {
-      float v[8];
+    // (WeightPack places every layout at a 64-element boundary, so the 16-byte stores are aligned)
+    const int lb = (int)blockIdx.x - b0, fb = repack_fwd_blocks(tf);
+    if (lb < fb) {  // forward layout: 8 channels of one (k, tap) row per thread
+      const int e = (lb * 256 + threadIdx.x) * 8;
       if (e < tf) {
+        float v[8];
         const int krs = e / Cp, c0 = e - krs * Cp;
         const int k = krs / RS, rs = krs - k * RS;
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = c0 + u < C ? w[(k * C + c0 + u) * RS + rs] : 0.f;
         *reinterpret_cast<uint4*>(wt + e) = pack8(v);
-      } else {
-        const int j = e - tf;
-        const int crs = j / K, k0 = j - crs * K;
-        const int c = crs / RS, rs = crs - c * RS;
+      }
+      return;
+    }
+    if (!wtd) return;
+    // data-gradient layout: tile (k0.., j0..) of W[K][CRS] -> wtd[CRS][K]
+    const int CRS = C * RS, tcols = (CRS + kRepackT - 1) / kRepackT;
+    const int t = lb - fb, k0 = (t / tcols) * kRepackT, j0 = (t % tcols) * kRepackT;
+    __shared__ float tile[kRepackT][kRepackT + 1];
+    const int col = threadIdx.x & 63, r0 = threadIdx.x >> 6;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = w[((k0 + u) * C + c) * RS + rs];
-        *reinterpret_cast<uint4*>(wtd + j) = pack8(v);
+    for (int i = 0; i < kRepackT / 4; ++i) {  // 16 independent coalesced row loads per thread
+      const int row = r0 + 4 * i, k = k0 + row, j = j0 + col;
+      tile[row][col] = (k < K && j < CRS) ? w[(size_t)k * CRS + j] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int v = threadIdx.x + 256 * h, row = v >> 3, kv = v & 7;
+      const int j = j0 + row, kk = k0 + 8 * kv;
+      if (j < CRS && kk < K) {
+        float f8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) f8[u] = tile[8 * kv + u][row];
+        *reinterpret_cast<uint4*>(wtd + (size_t)j * K + kk) = pack8(f8);
       }
     }
     return;
@@ -1377,9 +1555,11 @@ void nhwc_repack_weight(const float* w, uint16_t* wt, uint16_t* wtd, int K, int 
 }
 
 int nhwc_repack_blocks(int K, int C, int R, int S, int Cp, bool fwd, bool dgrad) {
-  const int64_t n = (fwd ? (int64_t)K * R * S * Cp : 0) + (dgrad ? (int64_t)K * C * R * S : 0);
-  MX_CHECK(n < (1ll << 31), "nhwc repack: weight too large for 32-bit indices");
-  return std::max(1, (int)((n + kRepackPerBlock - 1) / kRepackPerBlock));
+  const int64_t nf = fwd ? (int64_t)K * R * S * Cp : 0, nd = dgrad ? (int64_t)K * C * R * S : 0;
+  MX_CHECK(nf + nd < (1ll << 31), "nhwc repack: weight too large for 32-bit indices");
+  if (K % 8 == 0)  // forward blocks, then the data-gradient transpose tiles (wrepack_many_k)
+    return std::max(1, repack_fwd_blocks(nf) + (dgrad ? cdiv(K, kRepackT) * cdiv(C * R * S, kRepackT) : 0));
+  return std::max(1, (int)((nf + nd + kRepackPerBlock - 1) / kRepackPerBlock));
 }
 
 void nhwc_repack_many(const int64_t* desc, int n, int total_blocks, hipStream_t st) {
@@ -1483,6 +1663,15 @@ size_t nhwc_conv_scratch_floats(int M, int Ng, int Kg) {
   return n;
 }
 
+// MXDDP_STEM=0: the ResNet stem on the generic gather kernel (A/B switch for the stem kernel)
+static bool stem_mode() {
+  static const bool on = [] {
+    const char* e = std::getenv("MXDDP_STEM");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
 // returns the number of BN partial rows the epilogue wrote to a.bnpart (0: none, the BN runs its
 // own statistics pass)
 static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
@@ -1491,6 +1680,13 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   a.fOHW = FastDiv(a.OH * a.OW);
   a.fCa = FastDiv(a.Ca);
   a.fS = FastDiv(a.S);
+  if (stem_eligible(a) && stem_mode()) {  // 16 x 16 output tiles: M / 256 blocks
+    const int gx = a.M / 256;
+    if (!(a.bnpart && gx <= 16384)) a.bnpart = nullptr;
+    if (a.bnpart) MX_LAUNCH(conv_nhwc_stem_kernel<true>, dim3(gx), dim3(512), 0, st, a);
+    else MX_LAUNCH(conv_nhwc_stem_kernel<false>, dim3(gx), dim3(512), 0, st, a);
+    return a.bnpart ? gx : 0;
+  }
   const ConvSetup cs = conv_setup(a);
   ConvPlan p = cs.p;
   const bool wide = cs.wide;

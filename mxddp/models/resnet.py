@@ -130,8 +130,9 @@ class ResNet(nn.Module):
 
         pack = self._weight_pack()
         y = N.to_nhwc(x)
-        y = N.batch_norm(N.conv2d(y, self.conv1.weight, self.conv1.stride, self.conv1.padding, pack), self.bn1,
-                         relu=True)
+        # the stem kernel's epilogue computes bn1's statistics (csrc/nhwc_bf16.hip conv_nhwc_stem_kernel)
+        y = N.conv2d(y, self.conv1.weight, self.conv1.stride, self.conv1.padding, pack, bn=self.bn1)
+        y = N.batch_norm(y, self.bn1, relu=True)
         y = N.max_pool2d(y, 3, 2, 1)
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:

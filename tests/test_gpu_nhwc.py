@@ -28,6 +28,8 @@ CONV = [
     (2, 128, 14, 14, 256, 1, 2, 0),
     (1, 256, 7, 7, 512, 3, 1, 1),
     (2, 8, 30, 30, 64, 7, 2, 3),   # stem-like (channel-padded input)
+    (2, 8, 64, 96, 64, 7, 2, 3),   # the stem kernel (output 32 x 48: 16 x 16 tiles)
+    (1, 8, 31, 32, 64, 7, 2, 3),   # the stem kernel with odd input height (output 16 x 16)
     # stride-2 data gradients on the parity-class path (wide, even input), incl. split-K
     (2, 64, 14, 14, 128, 3, 2, 1),
     (2, 256, 8, 8, 512, 3, 2, 1),
@@ -208,6 +210,34 @@ def test_bn_statistics_from_conv_epilogue(cuda, shape, offset):
         assert _rel(b, a) < 2e-2
 
 
+@pytest.mark.parametrize("offset", [0.0, 3.0])
+def test_stem_kernel_bn_statistics(cuda, offset):
+    """The stem kernel (7x7 / 2, 8-channel input, 16 x 16 output tiles) writes the BN partial sums
+    in its epilogue: same output, running statistics and gradients as the same conv followed by the
+    BN's own statistics pass."""
+    torch.manual_seed(6)
+    x = (torch.randn(3, 64, 64, 8) + offset).to(torch.bfloat16).to(cuda)
+    w = (torch.randn(64, 8, 7, 7) * 0.05).to(cuda)
+    outs = []
+    for fused in (False, True):
+        bn = nn.BatchNorm2d(64).to(cuda)
+        with torch.no_grad():
+            bn.running_mean.fill_(0.5 * offset)
+        xg = x.clone().requires_grad_()
+        wg = w.clone().requires_grad_()
+        c = nhwc.conv2d(xg, wg, 2, 3, bn=bn if fused else None)
+        assert c.shape == (3, 32, 32, 64)
+        assert (getattr(c, "_mx_bnpre", None) is not None) == fused  # the stem kernel's epilogue ran
+        y = nhwc.batch_norm(c, bn, relu=True)
+        gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(3)).to(torch.bfloat16).to(cuda)
+        y.backward(gy)
+        torch.cuda.synchronize()
+        outs.append((y.float().cpu(), bn.running_mean.cpu(), bn.running_var.cpu(), wg.grad.cpu(),
+                     bn.weight.grad.cpu()))
+    for a, b in zip(*outs):
+        assert _rel(b, a) < 2e-2
+
+
 def test_weight_pack_matches_per_conv_repack(cuda):
     """One-launch repack of many convolutions == the per-convolution repack (both layouts, padded
     stem channels, a conv without the data-gradient layout)."""
@@ -217,7 +247,9 @@ def test_weight_pack_matches_per_conv_repack(cuda):
     torch.manual_seed(8)
     specs = [(torch.randn(64, 3, 7, 7, device=cuda), 8, False), (torch.randn(40, 64, 3, 3, device=cuda), 64, True),
              (torch.randn(256, 64, 1, 1, device=cuda), 64, True), (torch.randn(24, 16, 3, 3, device=cuda), 16, False),
-             (torch.randn(20, 16, 3, 3, device=cuda), 16, True)]  # K % 8 != 0: the scalar repack path
+             (torch.randn(20, 16, 3, 3, device=cuda), 16, True),  # K % 8 != 0: the scalar repack path
+             (torch.randn(72, 40, 3, 3, device=cuda), 40, True),  # partial 64 x 64 transpose tiles
+             (torch.randn(512, 1024, 1, 1, device=cuda), 1024, True)]
     pack = nhwc.WeightPack(specs)
     pack.refresh()
     st = torch.cuda.current_stream().cuda_stream
