@@ -392,12 +392,39 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
       for (int k = 0; k < 9; ++k) xch[((w * 2 + jl) * 9 + k) * 64 + lane] = o[xh ? jl : 2 + jl][k];
     __syncthreads();
     const int pw = w ^ 2;
+    if (f.wslab) {
+      // slab epilogue (as the unsplit blocks): this block's [32 co][16 ci][9] half of the image's
+      // slab staged in LDS over the exchange buffer, then coalesced 16-byte stores, no atomics
+      float fin[2][9];
 #pragma unroll
-    for (int jl = 0; jl < 2; ++jl) {
-      const int j = 2 * xh + jl, cj = 16 * ct + 4 * g + j;
+      for (int jl = 0; jl < 2; ++jl)
 #pragma unroll
-      for (int k = 0; k < 9; ++k)
-        atomicAdd(wa + (k * 64 + cj) * 32 + ci, o[j][k] + xch[((pw * 2 + jl) * 9 + k) * 64 + lane]);
+        for (int k = 0; k < 9; ++k) fin[jl][k] = o[2 * xh + jl][k] + xch[((pw * 2 + jl) * 9 + k) * 64 + lane];
+      __syncthreads();  // every partner read of the exchange buffer is done
+      float* st = sm;   // [32 co of this half][16 ci][9]
+#pragma unroll
+      for (int jl = 0; jl < 2; ++jl) {
+        const int cl = 16 * (w & 1) + 4 * g + 2 * xh + jl;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) st[(cl * 16 + m) * 9 + k] = fin[jl][k];
+      }
+      __syncthreads();
+      const int chalf = (bid >> 1) & 1;
+      const float4* s4 = reinterpret_cast<const float4*>(st);
+      float4* d4 = reinterpret_cast<float4*>(sc.wslab + (size_t)b * kPack + 144 * h);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const int i = tid + 256 * k, col = i / 36, q = i - 36 * col;
+        if (i < 32 * 36) d4[(32 * chalf + col) * 72 + q] = s4[i];
+      }
+    } else {
+#pragma unroll
+      for (int jl = 0; jl < 2; ++jl) {
+        const int j = 2 * xh + jl, cj = 16 * ct + 4 * g + j;
+#pragma unroll
+        for (int k = 0; k < 9; ++k)
+          atomicAdd(wa + (k * 64 + cj) * 32 + ci, o[j][k] + xch[((pw * 2 + jl) * 9 + k) * 64 + lane]);
+      }
     }
   } else {
   // f.wslab (kF6WSplit == 1): this block's [64 co][16 ci][9] result is staged in LDS (over the
@@ -980,8 +1007,8 @@ bool mnist_wslab() {
     const char* e = std::getenv("MXDDP_WSLAB");
     return (e && std::string(e) == "0") ? 0 : 1;
   }();
-  // the slab epilogue exists in the unsplit, non-co-split Winograd weight-gradient blocks only
-  return v == 1 && mnist_f7_wino() && f6w_split() == 1 && f6w_cos() == 1;
+  // the slab epilogue exists in the unsplit Winograd weight-gradient blocks (co-split or not)
+  return v == 1 && mnist_f7_wino() && f6w_split() == 1;
 }
 static int f6w_split() {
   static const int v = [] {
@@ -1015,7 +1042,9 @@ static void launch_f67_wino(const MnistFused& f, const Scratch& sc, hipStream_t 
   constexpr size_t lds = kF6WLds > kF7WLds ? kF6WLds : kF7WLds;
   const int cos = kSplit == 1 && f.a1_pub ? f6w_cos() : 1;
   const dim3 grid(f.co_blocks + 2 * kSplit * cos * f.B + kF7WChunks * f.B);
-  if (kSplit == 1 && f.a1_pub && cos == 2)
+  if (kSplit == 1 && f.a1_pub && cos == 2 && f7w_vq())
+    MX_LAUNCH((f67_conv2_bwd_kernel<true, 1, true, 2, true>), grid, dim3(256), lds, st, f, sc);
+  else if (kSplit == 1 && f.a1_pub && cos == 2)
     MX_LAUNCH((f67_conv2_bwd_kernel<true, 1, true, 2>), grid, dim3(256), lds, st, f, sc);
   else if (kSplit == 1 && f.a1_pub && f7w_vq())
     MX_LAUNCH((f67_conv2_bwd_kernel<true, 1, true, 1, true>), grid, dim3(256), lds, st, f, sc);
@@ -1032,6 +1061,7 @@ void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 1, true>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 1, true, 1, true>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 1, true, 2>),
+                           reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 1, true, 2, true>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 2>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true, 3>),
                            reinterpret_cast<const void*>(f67_conv2_bwd_kernel<false>)})
