@@ -897,6 +897,136 @@ __global__ __launch_bounds__(256) void wgrad_nhwc_kernel(WgNArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Stem weight gradient (the forward's conv_nhwc_stem_kernel shape): dW[co][(r, s, c)] = sum over
+// output pixels of dy[px][co] x[2 oh + r - 3][2 ow + s - 3][c].  The generic kernel gathers
+// every (pixel, tap) vector from L2 once per tap (49x per input pixel, 32-byte strided: 527 us
+// per step at batch 256).  Here a PERSISTENT block walks 16 x 16 output tiles: per tile the dy
+// tile [256 px][64 co] and the 37 x 38 input patch are staged in LDS once (the next tile's loads
+// in flight in registers during this tile's MFMAs), and per 32-pixel k-step the pixel-major
+// im2col rows [32 px][56 (r, s8) x 8 c] are expanded from the patch in LDS (16-byte copies) and
+// read with ds_read_b64_tr_b16 exactly like the generic kernel's tiles.  The 64 x 448 fp32
+// result stays in registers over all tiles of the block (wave w: 4 co tiles x n tiles w + 8 t);
+// one partial plane per block in the generic layout (s = 7 dropped), summed by
+// wgrad_nhwc_reduce_k.
+constexpr int kSwPA = 64 + 32, kSwPB = 448 + 32;  // LDS pitches (bf16), see wg_swz
+constexpr int kSwA = 256 * kSwPA * 2, kSwP = kStemPH * kStemPW * 16, kSwB = 32 * kSwPB * 2;
+
+__global__ __launch_bounds__(512) void wgrad_stem_kernel(WgNArgs a, int ntiles) {
+  __shared__ __attribute__((aligned(16))) char smem[kSwA + kSwP + 2 * kSwB];
+  bf16* As = reinterpret_cast<bf16*>(smem);                      // dy tile [256 px][kSwPA]
+  char* Ps = smem + kSwA;                                         // patch [37][38] x 16 B
+  bf16* Bs = reinterpret_cast<bf16*>(smem + kSwA + kSwP);         // im2col [2][32 px][kSwPB]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tw_n = a.Q >> 4, th_n = a.P >> 4;
+  constexpr int NDV = 256 * 8 / 512, NPV = (kStemPH * kStemPW + 511) / 512;
+  u32x4 dv[NDV], pv[NPV];
+  const u32x4 z4 = {0u, 0u, 0u, 0u};
+  auto gload = [&](int t) {
+    const int n = t / (th_n * tw_n), trem = t - n * th_n * tw_n;
+    const int oh0 = (trem / tw_n) * 16, ow0 = (trem % tw_n) * 16;
+#pragma unroll
+    for (int i = 0; i < NDV; ++i) {
+      const int v = tid + 512 * i, px = v >> 3, cv = v & 7;
+      dv[i] = *reinterpret_cast<const u32x4*>(
+          a.dy + (((size_t)n * a.P + oh0 + (px >> 4)) * a.Q + ow0 + (px & 15)) * 64 + 8 * cv);
+    }
+    const bf16* xin = a.x + (size_t)n * a.H * a.W * 8;
+#pragma unroll
+    for (int i = 0; i < NPV; ++i) {
+      const int v = min(tid + 512 * i, kStemPH * kStemPW - 1), pr = v / kStemPW, pc = v - pr * kStemPW;
+      const int ih = 2 * oh0 - 3 + pr, iw = 2 * ow0 - 3 + pc;
+      const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W && pc < 37;
+      pv[i] = *reinterpret_cast<const u32x4*>(xin + (size_t)(ok ? ih * a.W + iw : 0) * 8);
+      if (!ok) pv[i] = z4;
+    }
+  };
+  auto sstore = [&] {
+#pragma unroll
+    for (int i = 0; i < NDV; ++i) {
+      const int v = tid + 512 * i, px = v >> 3, cv = v & 7;
+      *reinterpret_cast<u32x4*>(As + px * kSwPA + 8 * (cv ^ wg_swz(px))) = dv[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NPV; ++i) {
+      const int v = tid + 512 * i;
+      if (v < kStemPH * kStemPW) *reinterpret_cast<u32x4*>(Ps + v * 16) = pv[i];
+    }
+  };
+  // im2col rows of k-step ks (tile pixel rows 2 ks, 2 ks + 1) -> buffer buf
+  auto build = [&](int ks, int buf) {
+    bf16* B = Bs + buf * 32 * kSwPB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int v = tid + 512 * i;
+      if (v < 32 * 56) {
+        const int pl = v / 56, rs8 = v - pl * 56, r = rs8 >> 3, s = rs8 & 7;
+        const int ohl = 2 * ks + (pl >> 4), owl = pl & 15;
+        const u32x4 val = *reinterpret_cast<const u32x4*>(Ps + ((2 * ohl + r) * kStemPW + 2 * owl + s) * 16);
+        *reinterpret_cast<u32x4*>(B + pl * kSwPB + 8 * (rs8 ^ wg_swz(pl))) = val;
+      }
+    }
+  };
+
+  const int nj = w < 4 ? 4 : 3;  // n tiles of this wave: w + 8 t (28 tiles of 16 columns)
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int t = blockIdx.x;
+  if (t < ntiles) {
+    gload(t);
+    sstore();
+  }
+  __syncthreads();
+  for (; t < ntiles; t += gridDim.x) {
+    const bool more = t + (int)gridDim.x < ntiles;
+    if (more) gload(t + gridDim.x);  // next tile in flight during this one
+    build(0, 0);
+    __syncthreads();
+    for (int ks = 0; ks < 8; ++ks) {
+      if (ks + 1 < 8) build(ks + 1, (ks + 1) & 1);
+      const bf16* B = Bs + (ks & 1) * 32 * kSwPB;
+      bf16x8 av[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) av[i] = tr_frag(As + 32 * ks * kSwPA, kSwPA, 16 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j < nj) {
+          const bf16x8 bv = tr_frag(B, kSwPB, 16 * (w + 8 * j), lane);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv, acc[i][j], 0, 0, 0);
+        }
+      }
+      __syncthreads();
+    }
+    if (more) sstore();
+    __syncthreads();
+  }
+  // partial plane of this block, generic layout [64 co][(r * 7 + s) * 8 + c] (s = 7 dropped)
+  float* pl = a.part + (size_t)blockIdx.x * 64 * 392;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j >= nj) continue;
+    const int n8 = 16 * (w + 8 * j) + (lane & 15), rs8 = n8 >> 3, c = n8 & 7, r = rs8 >> 3, s = rs8 & 7;
+    if (s == 7) continue;
+    const int col = (r * 7 + s) * 8 + c;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pl[(size_t)(16 * i + 4 * (lane >> 4) + q) * 392 + col] = acc[i][j][q];
+  }
+}
+
+static bool wgrad_stem_eligible(const WgNArgs& a) {
+  return a.Ca == 8 && a.R == 7 && a.S == 7 && a.sh == 2 && a.sw == 2 && a.ph == 3 && a.pw == 3 && a.Kout == 64 &&
+         a.P % 16 == 0 && a.Q % 16 == 0 && a.P == (a.H + 6 - 7) / 2 + 1 && a.Q == (a.W + 6 - 7) / 2 + 1;
+}
+constexpr int kSwBlocks = 256;  // persistent blocks (one per CU: 131 KB of LDS each)
+
 // dw[k][c][r][s] (+)= sum over splits of part[sp][k][(r, s, c)] (c < Cin; padded channels dropped).
 // Block = (256 / G) float4 column quads x G split groups: thread (q, g) sums splits g, g + G, ...
 // of its quad (float4 loads, 4 consecutive columns of one tap since Ca % 8 == 0), the G group
@@ -1837,7 +1967,10 @@ static int wgrad_splits(int Npix, int K, int Ng) {
 
 size_t nhwc_wgrad_scratch_floats(int N, int Cp, int K, int R, int S, int P, int Q) {
   const int Ng = R * S * Cp;
-  return (size_t)wgrad_splits(N * P * Q, K, Ng) * K * Ng;
+  size_t n = (size_t)wgrad_splits(N * P * Q, K, Ng) * K * Ng;
+  if (Cp == 8 && R == 7 && S == 7 && K == 64 && P % 16 == 0 && Q % 16 == 0)  // the stem kernel may run
+    n = std::max(n, (size_t)kSwBlocks * K * Ng);
+  return n;
 }
 
 void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, int H, int W, int Cin, int Cp, int K,
@@ -1867,6 +2000,14 @@ void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, in
   a.fPQ = FastDiv(P * Q);
   a.fCa = FastDiv(Cp);
   a.fS = FastDiv(S);
+  MX_CHECK((int64_t)K * a.Ng < (1ll << 31), "nhwc wgrad: weight too large for 32-bit indices");
+  if (wgrad_stem_eligible(a) && stem_mode()) {  // persistent LDS-patch kernel, one plane per block
+    MX_LAUNCH(wgrad_stem_kernel, dim3(kSwBlocks), dim3(512), 0, st, a, N * (P / 16) * (Q / 16));
+    const int plane4 = K * a.Ng / 4;
+    MX_LAUNCH(wgrad_nhwc_reduce_k, dim3(cdiv(plane4, 256 / 16)), dim3(256), 0, st, scratch, dw, kSwBlocks, K, a.Ng,
+              Cp, Cin, R * S, accumulate ? 1 : 0, 16);
+    return;
+  }
   int tm, tn;
   wgrad_tile(K, a.Ng, tm, tn);
   const int tiles = cdiv(K, tm) * cdiv(a.Ng, tn);
