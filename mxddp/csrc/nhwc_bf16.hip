@@ -1597,6 +1597,65 @@ __global__ void maxpool_nhwc_k(const bf16* __restrict__ x, bf16* __restrict__ y,
   }
 }
 
+// 3x3 / stride 2 / pad 1 (ResNet's stem pool): input row h is covered by window row h / 2 (tap 1)
+// when h is even, by rows (h + 1) / 2 (tap 0) and (h - 1) / 2 (tap 2) when odd; the same for
+// columns.  All four candidate windows' (dy, argmax) loads are issued unconditionally (clamped
+// indices, validity as a mask) -- the generic kernel's loads sat behind data-dependent branches,
+// one round trip each (250 us per step at batch 256).
+__global__ void maxpool_nhwc_bwd_s2_k(const bf16* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                      bf16* __restrict__ dx, int N, int H, int W, int C, int P, int Q, FastDiv fV,
+                                      FastDiv fW, FastDiv fH) {
+  const int V = C >> 3;
+  const int total = N * H * W * V;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int pix = (int)fV.div((uint32_t)i), v = i - pix * V;
+    const int hw = (int)fW.div((uint32_t)pix), w = pix - hw * W;
+    const int n = (int)fH.div((uint32_t)hw), h = hw - n * H;
+    int pr[2], tr[2], qc[2], tc[2];
+    bool okr[2], okc[2];
+    if (h & 1) {
+      pr[0] = (h + 1) >> 1; tr[0] = 0; okr[0] = pr[0] < P;
+      pr[1] = (h - 1) >> 1; tr[1] = 2; okr[1] = true;
+    } else {
+      pr[0] = h >> 1; tr[0] = 1; okr[0] = pr[0] < P;
+      pr[1] = 0; tr[1] = 0; okr[1] = false;
+    }
+    if (w & 1) {
+      qc[0] = (w + 1) >> 1; tc[0] = 0; okc[0] = qc[0] < Q;
+      qc[1] = (w - 1) >> 1; tc[1] = 2; okc[1] = true;
+    } else {
+      qc[0] = w >> 1; tc[0] = 1; okc[0] = qc[0] < Q;
+      qc[1] = 0; tc[1] = 0; okc[1] = false;
+    }
+    uint4 d4[4];
+    uint2 a4[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int a = c >> 1, b = c & 1;
+      const int o = ((n * P + min(pr[a], P - 1)) * Q + min(qc[b], Q - 1)) * V + v;
+      d4[c] = reinterpret_cast<const uint4*>(dy)[o];
+      a4[c] = reinterpret_cast<const uint2*>(arg)[o];
+    }
+    float g[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int a = c >> 1, b = c & 1;
+      const bool ok = okr[a] && okc[b];
+      const uint32_t tap = (uint32_t)(tr[a] * 3 + tc[b]);
+      float dv[8];
+      unpack8(d4[c], dv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t t = ((e < 4 ? a4[c].x : a4[c].y) >> (8 * (e & 3))) & 0xffu;
+        g[e] += (ok && t == tap) ? dv[e] : 0.f;
+      }
+    }
+    reinterpret_cast<uint4*>(dx)[i] = pack8(g);
+  }
+}
+
 template <int KS>
 __global__ void maxpool_nhwc_bwd_k(const bf16* __restrict__ dy, const uint8_t* __restrict__ arg, bf16* __restrict__ dx,
                                    int N, int H, int W, int C, int P, int Q, int kr, int st, int pd, FastDiv fV,
@@ -2132,7 +2191,9 @@ void nhwc_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int 
   MX_CHECK(C % 8 == 0 && (int64_t)N * H * W * C / 8 < (1ll << 31), "nhwc maxpool: C % 8 and 32-bit indices");
   const dim3 g(grid_for((int64_t)N * H * W * (C / 8))), b(256);
   const FastDiv fV(C / 8), fW(W), fH(H), fS(s);
-  if (k == 3) MX_LAUNCH(maxpool_nhwc_bwd_k<3>, g, b, 0, st, dy, arg, dx, N, H, W, C, P, Q, k, s, p, fV, fW, fH, fS);
+  if (k == 3 && s == 2 && p == 1)
+    MX_LAUNCH(maxpool_nhwc_bwd_s2_k, g, b, 0, st, dy, arg, dx, N, H, W, C, P, Q, fV, fW, fH);
+  else if (k == 3) MX_LAUNCH(maxpool_nhwc_bwd_k<3>, g, b, 0, st, dy, arg, dx, N, H, W, C, P, Q, k, s, p, fV, fW, fH, fS);
   else MX_LAUNCH(maxpool_nhwc_bwd_k<0>, g, b, 0, st, dy, arg, dx, N, H, W, C, P, Q, k, s, p, fV, fW, fH, fS);
 }
 

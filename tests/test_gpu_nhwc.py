@@ -277,10 +277,11 @@ def test_to_nhwc_exact(cuda, C, cp):
     assert not y[..., C:].any()
 
 
-@pytest.mark.parametrize("k,s,p", [(3, 2, 1), (2, 2, 0), (3, 1, 1)])
-def test_pools_nhwc(cuda, k, s, p):
+@pytest.mark.parametrize("k,s,p,hw", [(3, 2, 1, (13, 11)), (3, 2, 1, (12, 10)), (2, 2, 0, (13, 11)),
+                                       (3, 1, 1, (13, 11))])
+def test_pools_nhwc(cuda, k, s, p, hw):
     torch.manual_seed(3)
-    x = torch.randn(2, 13, 11, 16).to(torch.bfloat16)
+    x = torch.randn(2, hw[0], hw[1], 16).to(torch.bfloat16)
     xr = _nchw(x).requires_grad_()
     yr = F.max_pool2d(xr, k, s, p)
     gy = torch.randn_like(yr).to(torch.bfloat16).float()
