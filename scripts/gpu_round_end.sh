@@ -23,3 +23,5 @@ run bench_cpu 300 python bench.py --cpu --steps 30 --warmup 3
 run bench_replica 300 python bench.py --impl replica --steps 1000 --warmup 50
 run bench_coll 300 python bench.py --steps 2000 --warmup 100 --force-collectives
 run bench_ws2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29591 bench.py --gpus 2 --steps 1000 --warmup 50
+run bench_keras_replica 300 python bench.py --model keras_cnn --impl replica --steps 300 --warmup 30
+run bench_ws2_keras 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29592 bench.py --gpus 2 --model keras_cnn --steps 300 --warmup 30
