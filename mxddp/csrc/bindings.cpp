@@ -108,6 +108,7 @@ PYBIND11_MODULE(_C, m) {
     nhwc_repack_weight(P<const float>(w), P<uint16_t>(wt), P<uint16_t>(wtd), K, C, R, S_, Cp, S(st));
   });
   m.def("nhwc_repack_blocks", &nhwc_repack_blocks);
+  m.def("nhwc_conv_bn_rows", &nhwc_conv_bn_rows);
   m.def("nhwc_conv_dgrad_scratch_floats", &nhwc_conv_dgrad_scratch_floats);
   m.def("nhwc_conv_set_glds", &nhwc_conv_set_glds);
   m.def("nhwc_repack_many", [](uintptr_t desc, int n, int total_blocks, uintptr_t st) {

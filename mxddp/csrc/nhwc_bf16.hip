@@ -733,6 +733,162 @@ __global__ __launch_bounds__(512, 4) void conv_nhwc_stem_kernel(ConvNArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1, 64 -> 64 channels (ResNet-50 layer1's conv2: forward, and its data
+// gradient, which is the same correlation over dy with the taps flipped).  The LDS-DMA kernel
+// re-fetches each input vector from L2 for every one of the 9 taps through a 128-channel-row
+// tile; here PERSISTENT blocks keep the whole filter bank in LDS ([64][576 + 8] bf16, loaded once
+// per block) and walk bands of RT full-width output rows (RT x W <= 256 pixels, 56 x 56: 4 rows):
+// the (RT + 2) x (W + 2) x 64 input patch of a band is staged in LDS once (the next band's patch
+// in flight in registers during this band's MFMAs) and the B fragments are read straight out of
+// it -- k = (tap, channel), so a lane's 8 consecutive k are one 16-byte channel chunk of one patch
+// pixel.  Patch chunks are XOR-swizzled by (pixel >> 1) & 7 (the 16 lanes of a ds_read_b128 lane
+// group land on distinct bank slots for runs of consecutive pixels).  8 waves: wave w = pixel
+// groups 2w, 2w + 1 (16 band pixels each, row-major) x 64 channels, 18 k-steps.
+constexpr int kC3WP = 576 + 8, kC3A = 64 * kC3WP * 2, kC3PMax = 360, kC3C = 256 * 72 * 2;
+
+__host__ __device__ inline int c3_band_rows(int H, int W) {  // largest RT | H with RT * W <= 256
+  int rt = 0;
+  for (int r = 1; r <= 256 / W && r <= H; ++r)
+    if (H % r == 0 && (r + 2) * (W + 2) <= kC3PMax) rt = r;
+  return rt;
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(512) void conv3x3_s1_c64_kernel(ConvNArgs a, int rt, int ntiles) {
+  __shared__ __attribute__((aligned(16))) char smem[kC3A + kC3PMax * 128 + kC3C + 2 * 512 * 4];
+  char* As = smem;
+  char* Ps = smem + kC3A;
+  bf16* Cs = reinterpret_cast<bf16*>(smem + kC3A + kC3PMax * 128);
+  float* bred = reinterpret_cast<float*>(smem + kC3A + kC3PMax * 128 + kC3C);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  const int W = a.OW, PWd = W + 2, npx = rt * W, npp = (rt + 2) * PWd, bands = a.OH / rt;
+  const u32x4 z4 = {0u, 0u, 0u, 0u};
+  // filters once per block: LDS row co, k = tap * 64 + ci (data gradient: tap flipped, 8 - tap)
+  for (int v = tid; v < 64 * 72; v += 512) {
+    const int row = v / 72, kv = v - row * 72, tap = kv >> 3, ch = kv & 7;
+    *reinterpret_cast<u32x4*>(As + row * (kC3WP * 2) + kv * 16) =
+        *reinterpret_cast<const u32x4*>(a.wt + (size_t)row * 576 + (a.dgrad ? 8 - tap : tap) * 64 + 8 * ch);
+  }
+  // this lane's band pixels (groups 2w, 2w + 1): patch offset of tap (0, 0), validity
+  int poff[2];
+  bool pval[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int p = 16 * (2 * w + j) + m;
+    pval[j] = p < npx;
+    const int pp = pval[j] ? p : 0, pr = pp / W;
+    poff[j] = pr * PWd + (pp - pr * W);
+  }
+  constexpr int NPV = (kC3PMax * 8 + 511) / 512;
+  u32x4 pv[NPV];
+  auto gload = [&](int t) {
+    const int n = t / bands, ih0 = (t - n * bands) * rt - 1;
+    const bf16* xin = a.act + (size_t)n * a.IH * a.IW * 64;
+#pragma unroll
+    for (int i = 0; i < NPV; ++i) {
+      const int v = min(tid + 512 * i, npp * 8 - 1), pix = v >> 3, ch = v & 7;
+      const int pr = pix / PWd, pc = pix - pr * PWd, ih = ih0 + pr, iw = pc - 1;
+      const bool ok = (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
+      pv[i] = *reinterpret_cast<const u32x4*>(xin + (size_t)(ok ? ih * a.IW + iw : 0) * 64 + 8 * ch);
+      if (!ok) pv[i] = z4;
+    }
+  };
+  auto pstore = [&] {
+#pragma unroll
+    for (int i = 0; i < NPV; ++i) {
+      const int v = tid + 512 * i, pix = v >> 3, ch = v & 7;
+      if (v < npp * 8) *reinterpret_cast<u32x4*>(Ps + pix * 128 + 16 * (ch ^ ((pix >> 1) & 7))) = pv[i];
+    }
+  };
+  int t = blockIdx.x;
+  if (t < ntiles) {
+    gload(t);
+    pstore();
+  }
+  __syncthreads();
+  const char* arow = As + m * (kC3WP * 2) + g * 16;
+  constexpr int CP = 72;
+  for (; t < ntiles; t += gridDim.x) {
+    const bool more = t + (int)gridDim.x < ntiles;
+    if (more) gload(t + gridDim.x);
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+    for (int ks = 0; ks < 18; ++ks) {
+      const int tap = ks >> 1, r = tap / 3, s = tap - 3 * r, c = 4 * (ks & 1) + g;
+      bf16x8 fa[4], fb[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(arow + i * 16 * (kC3WP * 2) + ks * 64);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int pix = poff[j] + r * PWd + s;
+        fb[j] = *reinterpret_cast<const bf16x8*>(Ps + pix * 128 + 16 * (c ^ ((pix >> 1) & 7)));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        *reinterpret_cast<uint2*>(Cs + (16 * (2 * w + j) + m) * CP + 16 * i + 4 * g) =
+            make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
+    __syncthreads();  // C tile complete; every wave done with this band's patch
+    if (more) pstore();
+    const size_t obase = (size_t)t * npx * 64;  // bands are consecutive row ranges: pixel t * npx + px
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int v = tid + 512 * k, px = v >> 3, cv = v & 7;
+      if (px < npx) {
+        const size_t o = obase + (size_t)px * 64 + 8 * cv;
+        u32x4 val = *reinterpret_cast<const u32x4*>(Cs + px * CP + 8 * cv);
+        if (a.addend) val = add8(val, *reinterpret_cast<const u32x4*>(a.addend + o));
+        *reinterpret_cast<u32x4*>(a.out + o) = val;
+      }
+    }
+    if constexpr (STATS) {  // BN partial sums of the stored (bf16) band, one row per band
+      const int cc = tid & 63, q = tid >> 6;
+      const float K = a.bnshift ? a.bnshift[cc] : 0.f;
+      const uint16_t* col = reinterpret_cast<const uint16_t*>(Cs) + cc;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll 8
+      for (int rr = 0; rr < 32; ++rr) {
+        const int px = 32 * q + rr;
+        const float d = px < npx ? bf2f(col[px * CP]) - K : 0.f;
+        s1 += d;
+        s2 = fmaf(d, d, s2);
+      }
+      bred[tid] = s1;
+      bred[512 + tid] = s2;
+      __syncthreads();
+      if (q == 0) {
+        float t1 = s1, t2 = s2;
+        for (int k = 1; k < 8; ++k) {
+          t1 += bred[tid + 64 * k];
+          t2 += bred[512 + tid + 64 * k];
+        }
+        float* dst = a.bnpart + (size_t)t * 128 + 2 * cc;
+        dst[0] = t1;
+        dst[1] = t2;
+      }
+    }
+    __syncthreads();  // C tile / reduction slots read; the next patch stored
+  }
+}
+
+static bool c3_eligible(const ConvNArgs& a) {
+  return a.Ca == 64 && a.Ng == 64 && a.R == 3 && a.S == 3 && a.sh == 1 && a.sw == 1 && a.ph == 1 && a.pw == 1 &&
+         a.OH == a.IH && a.OW == a.IW && a.OW <= 64 && c3_band_rows(a.OH, a.OW) >= 2;
+}
+
 static bool stem_eligible(const ConvNArgs& a) {
   return !a.dgrad && a.Ca == 8 && a.R == 7 && a.S == 7 && a.sh == 2 && a.sw == 2 && a.ph == 3 && a.pw == 3 &&
          a.Ng == 64 && a.OH % 16 == 0 && a.OW % 16 == 0 && !a.addend && a.OH == (a.IH + 6 - 7) / 2 + 1 &&
@@ -1869,6 +2025,15 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   a.fOHW = FastDiv(a.OH * a.OW);
   a.fCa = FastDiv(a.Ca);
   a.fS = FastDiv(a.S);
+  if (c3_eligible(a) && stem_mode()) {  // persistent band kernel (forward or data gradient)
+    const int rt = c3_band_rows(a.OH, a.OW), nb = a.M / (rt * a.OW);
+    // BN rows: one per band (nhwc_conv_bn_rows sized the buffer for them)
+    if (!(a.bnpart && !a.dgrad && nb <= 16384)) a.bnpart = nullptr;
+    const int blocks = std::min(nb, 256);
+    if (a.bnpart) MX_LAUNCH(conv3x3_s1_c64_kernel<true>, dim3(blocks), dim3(512), 0, st, a, rt, nb);
+    else MX_LAUNCH(conv3x3_s1_c64_kernel<false>, dim3(blocks), dim3(512), 0, st, a, rt, nb);
+    return a.bnpart ? nb : 0;
+  }
   if (stem_eligible(a) && stem_mode()) {  // 16 x 16 output tiles: M / 256 blocks
     const int gx = a.M / 256;
     if (!(a.bnpart && gx <= 16384)) a.bnpart = nullptr;
@@ -1959,6 +2124,16 @@ int nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int
   a.bnpart = bnpart;
   a.bnshift = bnshift;
   return launch_conv(a, scratch, st);
+}
+
+int nhwc_conv_bn_rows(int N, int H, int W, int Cp, int K, int R, int S, int sh, int sw, int ph, int pw, int P, int Q) {
+  int rows = cdiv(N * P * Q, 256);  // one per 256-pixel tile (LDS-DMA kernel, stem kernel)
+  if (Cp == 64 && K == 64 && R == 3 && S == 3 && sh == 1 && sw == 1 && ph == 1 && pw == 1 && P == H && Q == W &&
+      W <= 64) {  // the band kernel writes one row per band
+    const int rt = c3_band_rows(P, Q);
+    if (rt >= 2) rows = std::max(rows, N * P / rt);
+  }
+  return rows;
 }
 
 static ConvNArgs dgrad_args(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K,

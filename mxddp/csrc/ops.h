@@ -175,6 +175,8 @@ void nhwc_repack_weight(const float* w, uint16_t* wt, uint16_t* wtd, int K, int 
 // all convolutions of a model in one launch: desc = device int64 [n][8] rows {w, wt, wtd (or 0), K,
 // C, R*S, Cp, first block}, first blocks = prefix sums of nhwc_repack_blocks(...)
 int nhwc_repack_blocks(int K, int C, int R, int S, int Cp, bool fwd, bool dgrad);
+// rows of BN partial sums a forward conv's epilogue may write (size of nhwc_conv_fwd's bnpart / 2K)
+int nhwc_conv_bn_rows(int N, int H, int W, int Cp, int K, int R, int S, int sh, int sw, int ph, int pw, int P, int Q);
 void nhwc_repack_many(const int64_t* desc, int n, int total_blocks, hipStream_t st);
 // scratch (or null = no split-K): nhwc_conv_scratch_floats(M = output pixels, Ng = output
 // channels, Kg = R*S*input channels) floats of fp32 split-K partials

@@ -219,7 +219,7 @@ def conv2d(x, w, stride=1, padding=0, pack: WeightPack | None = None, join: Grad
         N_, H_, W_, _ = x.shape
         K, _, R, S = w.shape
         P, Q = _out(H_, R, s[0], p[0]), _out(W_, S, s[1], p[1])
-        rows = -(-(N_ * P * Q) // 256)
+        rows = native().nhwc_conv_bn_rows(N_, H_, W_, x.shape[3], K, R, S, s[0], s[1], p[0], p[1], P, Q)
         if rows <= 16384:
             shift = bn.running_mean if bn.track_running_stats else None
             bnstat = [torch.empty((rows * 2 * K,), device=x.device, dtype=torch.float32), shift, 0]

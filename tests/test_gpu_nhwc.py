@@ -30,6 +30,8 @@ CONV = [
     (2, 8, 30, 30, 64, 7, 2, 3),   # stem-like (channel-padded input)
     (2, 8, 64, 96, 64, 7, 2, 3),   # the stem kernel (output 32 x 48: 16 x 16 tiles)
     (1, 8, 31, 32, 64, 7, 2, 3),   # the stem kernel with odd input height (output 16 x 16)
+    (3, 64, 32, 48, 64, 3, 1, 1),  # the persistent 3x3 / 64-channel kernel (forward + data gradient)
+    (2, 64, 56, 56, 64, 3, 1, 1),  # ... on ResNet-50 layer1's 56 x 56 (4-row bands)
     # stride-2 data gradients on the parity-class path (wide, even input), incl. split-K
     (2, 64, 14, 14, 128, 3, 2, 1),
     (2, 256, 8, 8, 512, 3, 2, 1),
@@ -93,7 +95,7 @@ def test_conv_glds_kernel(cuda, case):
     assert _rel(wg.grad.cpu(), wr.grad) < 1e-2
 
 
-@pytest.mark.parametrize("case", [(1, 256, 7, 7, 512, 3, 1, 1), (2, 64, 14, 14, 256, 1, 1, 0)])
+@pytest.mark.parametrize("case", [(1, 256, 7, 7, 512, 3, 1, 1), (2, 64, 14, 14, 256, 1, 1, 0), (2, 64, 16, 32, 64, 3, 1, 1)])
 def test_conv_dgrad_addend(cuda, case):
     """dx = conv_transpose(dy) + addend fused in the data-gradient epilogue (split-K reduction and
     direct epilogue) == the two computed separately."""
@@ -179,7 +181,9 @@ def test_bn_nhwc(cuda, C, relu, res):
 
 
 @pytest.mark.parametrize("shape,offset", [((16, 64, 56, 56, 128, 3, 1), 0.0), ((32, 64, 28, 28, 256, 1, 0), 4.0),
-                                          ((14, 64, 61, 59, 128, 3, 1), -2.0), ((96, 64, 56, 56, 64, 1, 0), 1.0)])
+                                          ((14, 64, 61, 59, 128, 3, 1), -2.0), ((96, 64, 56, 56, 64, 1, 0), 1.0),
+                                          ((5, 64, 48, 32, 64, 3, 1), 2.0),  # the 3x3 / 64-channel band kernel
+                                          ((2, 64, 56, 56, 64, 3, 1), 0.5)])  # (4-row bands: more rows than 256-px tiles)
 def test_bn_statistics_from_conv_epilogue(cuda, shape, offset):
     """conv2d(..., bn=bn) -> batch_norm: the LDS-DMA conv's epilogue computes the BN partial sums
     (shifted by the running mean) and the BN skips its statistics pass; same output, running
