@@ -1177,6 +1177,137 @@ __global__ __launch_bounds__(512) void wgrad_stem_kernel(WgNArgs a, int ntiles) 
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Weight gradient of the 3x3 / stride-1 / 64-channel convolution (conv3x3_s1_c64_kernel's shape):
+// persistent blocks walk the same full-width row bands; per band the dy rows [npx][64] and the
+// (rt + 2) x (W + 2) x 64 input patch are staged in LDS once (the next band's in registers during
+// this band's MFMAs).  dW[co][(tap, c)] = sum_px dy[px][co] x[px + tap][c]: the reduction runs
+// over band pixels, 8 consecutive ones per lane group, which (W % 8 == 0) are 8 consecutive patch
+// pixels of one row -- so the B operand is read with ds_read_b64_tr_b16 straight out of the
+// patch at the tap-shifted pixel, no im2col; A (dy^T) as in the generic kernel.  The 64 x 576
+// result stays in registers over all bands of a block (wave w: 4 co tiles x column tiles
+// w + 8 t); one partial plane per block, summed by wgrad_nhwc_reduce_k.
+__device__ __forceinline__ bf16x8 patch_tr_frag(const bf16* ps, int pix0, int c16, int lane) {
+  // rows = patch pixels pix0 + 8 (lane >> 4) + q (+ 4), columns = channels 8 c16 + (lane & 15)
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const int P0 = pix0 + 8 * g + q, P1 = P0 + 4, ch = c16 + (p >> 1);
+  const bf16* a0 = ps + P0 * 64 + 8 * (ch ^ ((P0 >> 1) & 7)) + 4 * (p & 1);
+  const bf16* a1 = ps + P1 * 64 + 8 * (ch ^ ((P1 >> 1) & 7)) + 4 * (p & 1);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+  bf16x8 res;
+  res[0] = lo[0]; res[1] = lo[1]; res[2] = lo[2]; res[3] = lo[3];
+  res[4] = hi[0]; res[5] = hi[1]; res[6] = hi[2]; res[7] = hi[3];
+  return res;
+}
+
+constexpr int kWc3PA = 64 + 32;
+__global__ __launch_bounds__(512) void wgrad_c3_kernel(WgNArgs a, int rt, int nbands) {
+  __shared__ __attribute__((aligned(16))) char smem[256 * kWc3PA * 2 + kC3PMax * 128];
+  bf16* Ds = reinterpret_cast<bf16*>(smem);                // dy band [px][kWc3PA]
+  char* Ps = smem + 256 * kWc3PA * 2;                       // patch, chunks XOR-swizzled
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int W = a.Q, PWd = W + 2, npx = rt * W, npp = (rt + 2) * PWd, bpi = a.P / rt;
+  const int nks = (npx + 31) >> 5;
+  const u32x4 z4 = {0u, 0u, 0u, 0u};
+  constexpr int NDV = 256 * 8 / 512, NPV = (kC3PMax * 8 + 511) / 512;
+  u32x4 dv[NDV], pv[NPV];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < NDV; ++i) {
+      const int v = tid + 512 * i, px = v >> 3, cv = v & 7;
+      const int pc = min(px, npx - 1);
+      dv[i] = *reinterpret_cast<const u32x4*>(a.dy + ((size_t)t * npx + pc) * 64 + 8 * cv);
+      if (px >= npx) dv[i] = z4;
+    }
+    const int n = t / bpi, ih0 = (t - n * bpi) * rt - 1;
+    const bf16* xin = a.x + (size_t)n * a.H * a.W * 64;
+#pragma unroll
+    for (int i = 0; i < NPV; ++i) {
+      const int v = min(tid + 512 * i, npp * 8 - 1), pix = v >> 3, ch = v & 7;
+      const int pr = pix / PWd, pc = pix - pr * PWd, ih = ih0 + pr, iw = pc - 1;
+      const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      pv[i] = *reinterpret_cast<const u32x4*>(xin + (size_t)(ok ? ih * a.W + iw : 0) * 64 + 8 * ch);
+      if (!ok) pv[i] = z4;
+    }
+  };
+  auto sstore = [&] {
+#pragma unroll
+    for (int i = 0; i < NDV; ++i) {
+      const int v = tid + 512 * i, px = v >> 3, cv = v & 7;
+      *reinterpret_cast<u32x4*>(Ds + px * kWc3PA + 8 * (cv ^ wg_swz(px))) = dv[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NPV; ++i) {
+      const int v = tid + 512 * i, pix = v >> 3, ch = v & 7;
+      if (v < npp * 8) *reinterpret_cast<u32x4*>(Ps + pix * 128 + 16 * (ch ^ ((pix >> 1) & 7))) = pv[i];
+    }
+  };
+  const int nj = w < 4 ? 5 : 4;  // column tiles w + 8 t of the 36
+  f32x4 acc[4][5];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int t = blockIdx.x;
+  if (t < nbands) {
+    gload(t);
+    sstore();
+  }
+  __syncthreads();
+  const bf16* ps = reinterpret_cast<const bf16*>(Ps);
+  for (; t < nbands; t += gridDim.x) {
+    const bool more = t + (int)gridDim.x < nbands;
+    if (more) gload(t + gridDim.x);
+    for (int ks = 0; ks < nks; ++ks) {
+      bf16x8 av[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) av[i] = tr_frag(Ds + 32 * ks * kWc3PA, kWc3PA, 16 * i, lane);
+      // first pixel of this k-step's lane groups: 8-pixel groups never straddle a band row (W % 8 == 0)
+      const int p0 = min(32 * ks + 8 * (lane >> 4), npx - 8), pr = p0 / W, base = pr * PWd + (p0 - pr * W);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        if (j < nj) {
+          const int nt = w + 8 * j, tap = nt >> 2, r = tap / 3, s = tap - 3 * r;
+          // patch_tr_frag adds 8 (lane >> 4) itself: pass the group-0 origin of this lane's group
+          const bf16x8 bv = patch_tr_frag(ps, base + r * PWd + s - 8 * (lane >> 4), 2 * (nt & 3), lane);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv, acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();  // every wave done with this band's tiles
+    if (more) sstore();
+    __syncthreads();
+  }
+  float* pl = a.part + (size_t)blockIdx.x * 64 * 576;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    if (j >= nj) continue;
+    const int col = 16 * (w + 8 * j) + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pl[(size_t)(16 * i + 4 * (lane >> 4) + q) * 576 + col] = acc[i][j][q];
+  }
+}
+
+// MXDDP_WGRAD_C3=1 selects wgrad_c3_kernel (default off until measured on the GPU)
+static bool wgrad_c3_mode() {
+  static const bool on = [] {
+    const char* e = std::getenv("MXDDP_WGRAD_C3");
+    return e && *e == '1';
+  }();
+  return on;
+}
+
+static bool wgrad_c3_eligible(const WgNArgs& a) {
+  return a.Ca == 64 && a.Kout == 64 && a.R == 3 && a.S == 3 && a.sh == 1 && a.sw == 1 && a.ph == 1 && a.pw == 1 &&
+         a.P == a.H && a.Q == a.W && a.Q <= 64 && a.Q % 8 == 0 && c3_band_rows(a.P, a.Q) >= 2;
+}
+
 static bool wgrad_stem_eligible(const WgNArgs& a) {
   return a.Ca == 8 && a.R == 7 && a.S == 7 && a.sh == 2 && a.sw == 2 && a.ph == 3 && a.pw == 3 && a.Kout == 64 &&
          a.P % 16 == 0 && a.Q % 16 == 0 && a.P == (a.H + 6 - 7) / 2 + 1 && a.Q == (a.W + 6 - 7) / 2 + 1;
@@ -2204,6 +2335,8 @@ size_t nhwc_wgrad_scratch_floats(int N, int Cp, int K, int R, int S, int P, int 
   size_t n = (size_t)wgrad_splits(N * P * Q, K, Ng) * K * Ng;
   if (Cp == 8 && R == 7 && S == 7 && K == 64 && P % 16 == 0 && Q % 16 == 0)  // the stem kernel may run
     n = std::max(n, (size_t)kSwBlocks * K * Ng);
+  if (Cp == 64 && K == 64 && R == 3 && S == 3 && Q <= 64 && Q % 8 == 0 && c3_band_rows(P, Q) >= 2)  // band kernel
+    n = std::max(n, (size_t)kSwBlocks * K * Ng);
   return n;
 }
 
@@ -2235,6 +2368,14 @@ void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, in
   a.fCa = FastDiv(Cp);
   a.fS = FastDiv(S);
   MX_CHECK((int64_t)K * a.Ng < (1ll << 31), "nhwc wgrad: weight too large for 32-bit indices");
+  if (wgrad_c3_eligible(a) && stem_mode() && wgrad_c3_mode()) {  // persistent band kernel, one plane per block
+    const int rt = c3_band_rows(P, Q);
+    MX_LAUNCH(wgrad_c3_kernel, dim3(kSwBlocks), dim3(512), 0, st, a, rt, N * (P / rt));
+    const int plane4 = K * a.Ng / 4;
+    MX_LAUNCH(wgrad_nhwc_reduce_k, dim3(cdiv(plane4, 256 / 16)), dim3(256), 0, st, scratch, dw, kSwBlocks, K, a.Ng,
+              Cp, Cin, R * S, accumulate ? 1 : 0, 16);
+    return;
+  }
   if (wgrad_stem_eligible(a) && stem_mode()) {  // persistent LDS-patch kernel, one plane per block
     MX_LAUNCH(wgrad_stem_kernel, dim3(kSwBlocks), dim3(512), 0, st, a, N * (P / 16) * (Q / 16));
     const int plane4 = K * a.Ng / 4;
