@@ -1294,11 +1294,12 @@ __global__ __launch_bounds__(512) void wgrad_c3_kernel(WgNArgs a, int rt, int nb
   }
 }
 
-// MXDDP_WGRAD_C3=1 selects wgrad_c3_kernel (default off until measured on the GPU)
+// MXDDP_WGRAD_C3=0: the generic weight-gradient kernel for this layer too (A/B switch; the band
+// kernel measured 90 vs ~243 us per call at batch 256, profiles/r3_wgrad_c3/)
 static bool wgrad_c3_mode() {
   static const bool on = [] {
     const char* e = std::getenv("MXDDP_WGRAD_C3");
-    return e && *e == '1';
+    return !(e && *e == '0');
   }();
   return on;
 }
