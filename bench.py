@@ -10,8 +10,11 @@ Each timed step is a full training step: forward, backward, bucketed RCCL all-re
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 bench.py --gpus 8 --steps 200 --warmup 20
 
-Timing: W untimed warm-up steps (the first also captures the hipGraph), then barrier +
-device sync, K timed steps, barrier + device sync; the time is the MAX over ranks.
+Timing: W untimed warm-up steps (the first also captures the hipGraph), then device sync +
+barrier + device sync, K timed steps, device sync; each rank stops its clock after its own
+sync, the closing barrier runs after the clock stops, and the time is the MAX over ranks.
+``warmup_steps_run`` in the JSON counts every untimed step that really ran (autotune trials,
+the capture step and the first launch of each captured graph included).
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -66,6 +69,9 @@ def parse():
                          "peer all-reduce, or auto (validated + timed during the untimed warm-up)")
     ap.add_argument("--channels-last", action="store_true",
                     help="--impl torch: channels_last memory format (stock PyTorch's NHWC convs, for a fair bf16 baseline)")
+    ap.add_argument("--min-warmup-ms", type=float, default=300.0,
+                    help="keep running untimed warm-up steps until this much wall time of warm-up ran (GPU "
+                         "clock ramp of a fresh process); counted in warmup_steps_run")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--lr", type=float, default=0.01, help="SGD lr (momentum 0.9, wd 1e-4 as the reference)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
@@ -165,15 +171,31 @@ def main():
         run = _layers_or_torch(a, torch, inf, dev, comm, B)
 
     run(a.warmup)
+    # clock ramp: a freshly started process's GPU runs its first ~100 ms of steps slower
+    # (profiles/r3_intercept): keep stepping, untimed, until --min-warmup-ms of warm-up ran
+    # (the slowest rank's elapsed time decides, so every rank runs the same number of steps)
+    extra = 0
+    torch.cuda.synchronize(dev)
+    t_w = time.perf_counter()
+    while C.all_reduce_max(time.perf_counter() - t_w) * 1e3 < a.min_warmup_ms:
+        n = max(1, min(32, a.steps))
+        run(n)
+        extra += n
+        torch.cuda.synchronize(dev)
+    # every untimed step that ran before the timed region: autotune trials, the capture step,
+    # the first launch of every captured graph, the requested warm-up and the clock-ramp steps
+    warmup_run = tr.steps if tr is not None else a.warmup + extra + getattr(a, "layers_eager_steps", 0)
     torch.cuda.synchronize(dev)
     C.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     run(a.steps)
     torch.cuda.synchronize(dev)
+    # each rank stops its own clock after its own device sync; the slowest rank decides (the
+    # closing barrier runs outside the timed region, so no host collective is inside it)
+    t_rank = time.perf_counter() - t0
     C.barrier()
-    torch.cuda.synchronize(dev)
-    dt = C.all_reduce_max(time.perf_counter() - t0)
+    dt = C.all_reduce_max(t_rank)
 
     if a.impl == "fused":
         # per-image averages over every step since the device accumulators were last zeroed
@@ -198,6 +220,7 @@ def main():
             "n_gpus": a.gpus,
             "steps": a.steps,
             "warmup": a.warmup,
+            "warmup_steps_run": warmup_run,
             "ms_per_step": round(dt / a.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
@@ -294,7 +317,8 @@ def _replica(a):
     value = B * a.steps / dt
     print(json.dumps({
         "metric": _metric(a.model), "value": round(value, 1), "unit": "images/sec", "n_gpus": a.gpus, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "warmup": a.warmup, "warmup_steps_run": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": a.dtype, "data": _data_desc(spec),
         "config": {"model": a.model, "global_batch": B, "per_rank_batch": a.batch, "seq_len": None,
                    "image": "x".join(map(str, spec.input_shape)), "parallelism": f"replica{a.gpus}",
@@ -324,7 +348,8 @@ def _replica_fused(a, devices, spec):
     value = B * a.steps / dt
     print(json.dumps({
         "metric": _metric(a.model), "value": round(value, 1), "unit": "images/sec", "n_gpus": a.gpus, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "warmup": a.warmup, "warmup_steps_run": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": a.dtype, "data": _data_desc(spec),
         "config": {"model": a.model, "global_batch": B, "per_rank_batch": a.batch, "seq_len": None,
                    "image": "x".join(map(str, spec.input_shape)), "parallelism": f"replica{a.gpus}",
@@ -461,6 +486,7 @@ def _layers_or_torch(a, torch, inf, dev, comm, B):
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             run_eager(2)  # allocator / autograd warm-up outside the capture
+        a.layers_eager_steps = 2
         torch.cuda.current_stream(dev).wait_stream(side)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=side, capture_error_mode="thread_local"):

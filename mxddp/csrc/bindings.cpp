@@ -372,6 +372,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("param_bucket"), py::arg("op") = RedOp::kSum, py::arg("timing") = false,
            py::keep_alive<1, 2>())
       .def("prepare", &Reducer::prepare)
+      .def("abort", &Reducer::abort)
       .def("mark_ready", [](Reducer& r, int p, uintptr_t st) { r.mark_ready(p, S(st)); })
       .def("mark_bucket_ready", [](Reducer& r, int b, uintptr_t st) { r.mark_bucket_ready(b, S(st)); })
       .def("finalize", [](Reducer& r, uintptr_t st) { r.finalize(S(st)); })

@@ -107,6 +107,14 @@ Comm::Comm(const std::string& uid, int rank, int world_size, int device, const C
   MX_HIP_CHECK(hipSetDevice(device));
   ScopedEnv algo("NCCL_ALGO", cfg.algo), proto("NCCL_PROTO", cfg.proto);
   if (cfg.ctas > 0) {
+    // the prefix struct is only valid for a linked RCCL that reads the >= 2.18 config layout (it
+    // copies `size` bytes and checks magic / version): refuse anything older with a clear error
+    // instead of handing it a struct it would misread
+    int v = 0;
+    MX_NCCL_CHECK(ncclGetVersion(&v));
+    MX_CHECK(v >= NCCL_VERSION(2, 18, 0),
+             "RCCL " + std::to_string(v) + " is older than 2.18: pinned-CTA communicator variants ('" + cfg.name() +
+                 "') need ncclCommInitRankConfig's 2.18 config layout; use the default variant");
     CommConfigV218 c{sizeof(CommConfigV218), 0xcafebeef, NCCL_VERSION(2, 18, 0), 1,
                      NCCL_CONFIG_UNDEF_INT, cfg.ctas, cfg.ctas, nullptr, NCCL_CONFIG_UNDEF_INT};
     MX_NCCL_CHECK(ncclCommInitRankConfig(&comm_, world_size, id, rank, reinterpret_cast<ncclConfig_t*>(&c)));

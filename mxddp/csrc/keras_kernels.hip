@@ -728,17 +728,16 @@ __device__ void kb1_role_e(const KerasFused& f, SmemE& sm) {
     if (tid + 256 * k < 640) f.gf2[tid + 256 * k] = acc[k];
 }
 
-// roles: bit mask of the roles to run (15 = all; fewer only for per-role timing, MXDDP_KB1_ROLES)
-__global__ __launch_bounds__(256) void kb1_kernel(KerasFused f, int roles) {
+__global__ __launch_bounds__(256) void kb1_kernel(KerasFused f) {
   __shared__ SmemKB1 sm;
   const int b = blockIdx.x, B = f.B;
   if (b < 8 * B) {
-    if (roles & 1) kb1_role_a(f, sm.a, b);
+    kb1_role_a(f, sm.a, b);
   } else if (b < 12 * B) {
-    if (roles & 2) kb1_role_b(f, sm.b, b - 8 * B);
+    kb1_role_b(f, sm.b, b - 8 * B);
   } else if (b < 12 * B + B / 2) {
-    if (roles & 4) kb1_role_c(f, sm.c, b - 12 * B);
-  } else if (roles & 8) {
+    kb1_role_c(f, sm.c, b - 12 * B);
+  } else {
     kb1_role_e(f, sm.e);
   }
 }
@@ -847,11 +846,7 @@ void keras_fused_forward(const KerasFused& f, hipStream_t st) {
 }
 
 void keras_fused_backward(const KerasFused& f, hipStream_t st) {
-  static const int roles = [] {
-    const char* e = std::getenv("MXDDP_KB1_ROLES");  // timing experiments only: breaks training
-    return e ? std::atoi(e) : 15;
-  }();
-  MX_LAUNCH(keras::kb1_kernel, dim3(12 * f.B + f.B / 2 + 1), dim3(256), 0, st, f, roles);
+  MX_LAUNCH(keras::kb1_kernel, dim3(12 * f.B + f.B / 2 + 1), dim3(256), 0, st, f);
 }
 
 // Regions of the update (mode 0 / 1: the finalize reads the partial planes; mode 2: Adam from

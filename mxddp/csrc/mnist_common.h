@@ -16,8 +16,21 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 __device__ __forceinline__ float sel4(const float4& v, int j) {
   return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
 }
-__device__ __forceinline__ int g1_slab_mask(const MnistFused& f) {
-  return (f.g1_slabs >= 1 && f.g1_slabs <= 64 ? f.g1_slabs : 16) - 1;
+
+// Deterministic cross-block sums: partial results are added as 64-bit fixed-point integers
+// (two's complement, wrapping adds are exact and associative), so the total does not depend on
+// the order in which blocks arrive.  kHScale for the fc1 pre-activation (|h| << 2^31),
+// kGScale for gradients (|g| << 2^23; 2^-40 absolute resolution).
+constexpr float kHScale = 4294967296.f, kHInv = 1.f / 4294967296.f;                   // 2^32
+constexpr float kGScale = 1099511627776.f, kGInv = 1.f / 1099511627776.f;             // 2^40
+__device__ __forceinline__ unsigned long long to_fix(float v, float scale) {
+  // saturate instead of wrapping if a diverged run overflows the range
+  const float s = fminf(fmaxf(v * scale, -9.2e18f), 9.2e18f);
+  return (unsigned long long)__float2ll_rn(s);
+}
+__device__ __forceinline__ float from_fix(long long v, float inv) { return (float)v * inv; }
+__device__ __forceinline__ void fix_add(long long* dst, float v, float scale) {
+  atomicAdd(reinterpret_cast<unsigned long long*>(dst), to_fix(v, scale));
 }
 
 // Phase timestamps for in-kernel profiling (MnistFused::trace, off = null): blocks 0..1023 of
@@ -30,39 +43,31 @@ __device__ __forceinline__ int g1_slab_mask(const MnistFused& f) {
 #define MX_TRACE(f, kid, ph) MX_TRACE_B(f, kid, ph, (int)blockIdx.x)
 
 struct Scratch {  // carve of MnistFused::scratch (floats)
-  float* wf;      // conv2 fwd B-fragments   [18 q][4 w][64 lane][4 j]
-  float* wd;      // conv2 dgrad B-fragments [9 r][4 s][2 nt][64 lane][4 j]
-  float* wacc;    // conv2 wgrad accumulator slabs [kWaccSlabs][9 r][64 co][32 ci], slab = image & (kWaccSlabs - 1)
   float* wu;      // conv2 dgrad Winograd filters G w' G^T (w' = w flipped) as F7W B-fragments
                   // [16 k-step][2 ci-half][64 lane][16 xi]
-  float* g1;      // conv1 grad partial slabs [kG1Slabs][320] (w[32][9] then b[32]), slab = image & (g1_slabs - 1)
+  long long* g1;  // conv1 grad slabs, int64 fixed point (kGScale) [kG1Slabs][320] (w[32][9] then
+                  // b[32]), slab = image & (kG1Slabs - 1)
+  long long* db2; // conv2 bias grad, int64 fixed point (kGScale) [64] (F5 blocks add, finalize reads)
   float* wv;      // conv2 forward Winograd filters G w G^T as F2W B-fragments
                   // [4 w][16 xi][2 s4][64 lane][4 j]
   float* wslab;   // conv2 wgrad per-image slabs [B][64 co][32 ci][9 tap] (canonical order), written
-                  // with plain stores by F6W (MnistFused::wslab), summed by the finalize
+                  // with plain stores by F6W, summed by the finalize in a fixed order
 };
 constexpr int kWinoPack = 16 * 2048;  // 16 Winograd-domain values per (co, ci)
-constexpr int kG1Slabs = 64;          // conv1-grad atomic slabs allocated (MnistFused::g1_slabs used)
-// conv2-wgrad atomics spread over 2 slabs (image & 1): the 64 images' blocks finish together and
-// same-address float atomics serialise, so one accumulator cost F6W a 3.5 us epilogue; the
-// finalize (in the SGD launch at world size 1) sums the slabs in a fixed order.  Measured at
-// B = 64: 1 slab 837k, 2 slabs 843k, 4 slabs 835k, 8 slabs 821k img/s (the finalize's serial
-// tail grows with the slab count faster than the epilogue shrinks: 3.5 / 2.8 / - / 2.4 us).
-constexpr int kWaccSlabs = 2;
+// conv1-grad slabs: the F7W blocks of image b add into slab b & 15 (integer adds, so the slab
+// count only spreads same-address contention; the sum is exact either way)
+constexpr int kG1Slabs = 16;
 __host__ __device__ inline Scratch carve(float* s) {
   Scratch c;
-  c.wf = s;
-  c.wd = c.wf + kPack;
-  c.wu = c.wd + kPack;
-  c.g1 = c.wu + kWinoPack;
-  c.wv = c.g1 + kG1Slabs * 320;
-  c.wacc = c.wv + kWinoPack;
-  c.wslab = c.wacc + kWaccSlabs * kPack;
+  c.wu = s;
+  c.g1 = reinterpret_cast<long long*>(c.wu + kWinoPack);
+  c.db2 = c.g1 + kG1Slabs * 320;
+  c.wv = reinterpret_cast<float*>(c.db2 + 64);
+  c.wslab = c.wv + kWinoPack;
   return c;
 }
 inline size_t scratch_floats(int B) {
-  return 2 * (size_t)kPack + 2 * (size_t)kWinoPack + (size_t)kG1Slabs * 320 + (size_t)kWaccSlabs * kPack +
-         (size_t)B * kPack;
+  return 2 * (size_t)kWinoPack + 2 * ((size_t)kG1Slabs * 320 + 64) + (size_t)B * kPack;
 }
 
 // conv2 weight gradient of pairs 4 grp .. 4 grp + 3 (36 consecutive floats of the canonical

@@ -29,7 +29,7 @@ size_t ws_floats(int B) {
   add((size_t)B * 36864);  // c2
   add((size_t)B * 9216);   // pool
   add((size_t)B * 9216);   // idx
-  add(B * 128);            // h
+  add(B * 256);            // h (int64 fixed point)
   add(B * 10);             // logits
   add(B * 10);             // dlogits
   add(B * 128);            // dh
@@ -60,7 +60,7 @@ MnistEngine::MnistEngine(int batch, uintptr_t params, uintptr_t grads, uintptr_t
   c2_ = c.take<float>((size_t)B_ * 36864);
   pool_ = c.take<float>((size_t)B_ * 9216);
   idx_ = c.take<int32_t>((size_t)B_ * 9216);
-  h_ = c.take<float>(B_ * 128);
+  h_ = c.take<float>(B_ * 256);  // int64 [B][128] on the fused path, float [B][128] on the generic one
   logits_ = c.take<float>(B_ * 10);
   dlogits_ = c.take<float>(B_ * 10);
   dh_ = c.take<float>(B_ * 128);
@@ -172,10 +172,9 @@ MnistFused MnistEngine::fused_args() const {
   f.p = p_;
   f.g = g_;
   f.a1 = a1_;
-  f.a1_pub = mnist_a1_publish() ? 1 : 0;
   f.pool = pool_;
   f.idx = idx_;
-  f.h = h_;
+  f.h = reinterpret_cast<long long*>(h_);
   f.dh = dh_;
   f.dp = dp_;
   f.scratch = scratch_;
@@ -187,9 +186,7 @@ MnistFused MnistEngine::fused_args() const {
   f.synth = external_batch_ ? 0 : 1;
   // without gradient collectives F5 applies the fc1 weight update itself (no all-reduce has to
   // come between the gradient and the update)
-  f.fc1_sgd = (variant_ == 1 && !reducer_->active() && mnist_f5_sgd()) ? 1 : 0;
-  f.g1_slabs = mnist_g1_slabs();
-  f.wslab = (variant_ == 1 && mnist_wslab()) ? 1 : 0;
+  f.fc1_sgd = (variant_ == 1 && !reducer_->active()) ? 1 : 0;
   f.mom = m_;
   f.lr = lr_;
   f.sgd_mom = momentum_;
@@ -374,7 +371,7 @@ void MnistEngine::forward_only(uintptr_t x, uintptr_t logits, int B) {
   MX_CHECK(B <= B_, "eval batch larger than engine batch");
   fwd(reinterpret_cast<const float*>(x), reinterpret_cast<float*>(logits), B);
   // the generic forward stores into h_, which the fused F3 uses as a zeroed split-K accumulator
-  if (variant_ == 1) MX_HIP_CHECK(hipMemsetAsync(h_, 0, sizeof(float) * B_ * 128, s_));
+  if (variant_ == 1) MX_HIP_CHECK(hipMemsetAsync(h_, 0, sizeof(long long) * B_ * 128, s_));
 }
 
 void MnistEngine::sync() { MX_HIP_CHECK(hipStreamSynchronize(s_)); }

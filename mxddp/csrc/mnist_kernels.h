@@ -17,7 +17,9 @@ struct MnistFused {
   float* a1;             // [B,32,26,26] post-ReLU conv1
   float* pool;           // [B,64,12,12] post-ReLU pooled conv2
   int32_t* idx;          // used as uint8 [B,64,12,12]: argmax 0..3 inside the 2x2 window, 4 = dead
-  float* h;              // [B,128] fc1 pre-activation accumulator
+  // [B,128] fc1 pre-activation as int64 fixed point (kHScale): F3's split-K partials are added
+  // with 64-bit integer atomics, so the sum is exact and independent of their order
+  long long* h;
   float* dh;             // [B,128] grad wrt fc1 pre-activation
   float* dp;             // [B,9216] grad wrt pooled activation (0 on dead windows)
   float* scratch;        // packed weights + accumulators
@@ -27,7 +29,6 @@ struct MnistFused {
   uint64_t seed;         // per-rank generator seed
   uint32_t* trace;       // optional per-phase timestamps (s_memrealtime, 100 MHz) for profiling, or null
   int synth;             // 1: F2 generates the batch on device; 0: x/y provided by the caller
-  int a1_pub;            // 1: F2 publishes conv1's output to a1 and F6W loads it (else F6W recomputes)
   // fc1-weight SGD folded into F5 (no gradient collectives in the step): each F5 block updates
   // the weight columns whose gradient it just produced (the gradient is not written to g), and
   // the SGD launch skips them
@@ -40,21 +41,9 @@ struct MnistFused {
   int co_blocks;
   PeerArgs co_args;
   PeerPartition co_part;
-  // conv1-grad atomic slabs in use (power of two <= kG1SlabsMax; MXDDP_G1_SLABS): F7 blocks of
-  // image b add into slab b & (g1_slabs - 1), the finalize sums them in a fixed order
-  int g1_slabs;
-  // 1: F6W writes its conv2 weight gradient as per-image slabs with plain stores (no atomics)
-  // and the finalize (F8 / the folded SGD) sums them in a fixed order; 0: slab atomics (wacc)
-  int wslab;
 };
-int mnist_g1_slabs();
-bool mnist_wslab();  // default on; MXDDP_WSLAB=0 (and the split / co-split / direct F6 variants) use atomics
-bool mnist_a1_publish();  // default on; MXDDP_MNIST_A1=recompute turns it off
-bool mnist_f5_sgd();      // default on; MXDDP_F5_SGD=0 keeps the fc1 update in the SGD launch
-
 size_t mnist_fused_scratch_floats(int B);
-bool mnist_f7_wino();  // conv2 data gradient as Winograd (default) vs direct (MXDDP_MNIST_F7=direct)
-// Pack conv2 weights into the F2/F7 fragment orders and zero the cross-step accumulators;
+// Pack conv2 weights into the F2 Winograd fragment order and zero the cross-step accumulators;
 // needed once and after any change of the parameters outside the fused SGD.
 void mnist_fused_init(const MnistFused& f, hipStream_t st);
 void mnist_fused_forward(const MnistFused& f, hipStream_t st);  // F2 + F3

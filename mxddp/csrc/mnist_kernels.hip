@@ -2,7 +2,7 @@
 //
 // One step = 7 launches:
 //   F2  on-device batch + conv1+ReLU + conv2+bias+ReLU+maxpool (MFMA)
-//   F3  fc1 forward, split-K (MFMA)
+//   F3  fc1 forward, split-K (MFMA), partials added as int64 fixed point (order-independent)
 //   F5  head (fc1 bias+ReLU, fc2, log_softmax+NLL, dlogits, fc2/fc1-bias grads, dh) recomputed in
 //       every block + fc1 dgrad/wgrad (MFMA) + ReLU/maxpool-masked dp          -> bucket 0 ready
 //   F6  conv2 wgrad (MFMA) | F7 conv2 dgrad (MFMA) + conv1 ReLU mask + conv1 wgrad
@@ -15,8 +15,10 @@
 // inside a 16-wide group is permuted (k = 16*s' + 4*g + j for k-step (s', j), lane group
 // g = l>>4) identically for A and B -- legal because K is a pure reduction.
 //
-// Every cross-step duty (weight packing, zeroing atomic accumulators) is folded into a kernel
-// that already exists (SGD, F8); the step has no helper launches.
+// Every cross-step duty (weight packing, zeroing accumulators) is folded into a kernel that
+// already exists (SGD, F8); the step has no helper launches.  Every cross-block sum is either a
+// fixed-order reduction or an int64 fixed-point atomic (mnist_common.h), so a step is bitwise
+// reproducible run to run.
 //
 // Replaces (reference): cuDNN conv/ReLU/pool + cuBLAS linear + log_softmax/NLL + per-tensor
 // SGD kernels reached through the PyTorch training loop of
@@ -27,20 +29,6 @@
 namespace mx {
 namespace mnist {
 namespace {
-
-// Inverse maps canonical conv2 weight (co, ci, r) -> packed fragment index.
-//  wf (F2 B-fragments): i = ((q*4 + w)*64 + l)*4 + j, k-step s = 4q + j, co = 16w + (l&15),
-//                       ci = 4*(s&7) + (l>>4), r = s>>3
-//  wd (F7 B-fragments): i = ((((r*4 + s)*2 + nt)*64 + l)*4 + j, co = 16s + 4*(l>>4) + j,
-//                       ci = 16nt + (l&15)
-__device__ __forceinline__ int wf_index(int co, int ci, int r) {
-  const int s = 8 * r + (ci >> 2), l = (co & 15) + 16 * (ci & 3);
-  return (((s >> 2) * 4 + (co >> 4)) * 64 + l) * 4 + (s & 3);
-}
-__device__ __forceinline__ int wd_index(int co, int ci, int r) {
-  const int s = co >> 4, rem = co & 15, l = (ci & 15) + 16 * (rem >> 2);
-  return ((((r * 4 + s) * 2 + (ci >> 4)) * 64 + l) * 4) + (rem & 3);
-}
 
 // F7W B operand for (co, ci) = pair i of 2048: U = G w' G^T, w'[a][b] = w[co][ci][2-a][2-b] (the
 // data gradient is the full correlation of dY2 with the flipped filter), G = [1 0 0; .5 .5 .5;
@@ -84,18 +72,9 @@ __device__ __forceinline__ int wv_index(int co, int ci, int xi) {
   const int s = ci >> 2, l = (co & 15) + 16 * (ci & 3);
   return ((((co >> 4) * 16 + xi) * 2 + (s >> 2)) * 64 + l) * 4 + (s & 3);
 }
-// Every packed form of conv2 weight pair (co, ci) (taps w[0..8] = w[co][ci][ky][kx]):
-// F2 / F7 direct fragments and the F2W Winograd filter.
-// (pack_direct = false: only the Winograd filter -- the direct F2 / F7 kernels are not in use)
-__device__ __forceinline__ void conv2_pack_pair(const Scratch& sc, int pair, const float w[9], bool pack_direct = true) {
+// The F2W Winograd filter of conv2 weight pair (co, ci) (taps w[0..8] = w[co][ci][ky][kx]).
+__device__ __forceinline__ void conv2_pack_pair(const Scratch& sc, int pair, const float w[9]) {
   const int co = pair >> 5, ci = pair & 31;
-  if (pack_direct) {
-#pragma unroll
-    for (int r = 0; r < 9; ++r) {
-      sc.wf[wf_index(co, ci, r)] = w[r];
-      sc.wd[wd_index(co, ci, r)] = w[r];
-    }
-  }
   float t[4][3];
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
@@ -117,23 +96,22 @@ __device__ __forceinline__ void conv2_pack_pair(const Scratch& sc, int pair, con
 // K0 (once, and after any external weight load): pack conv2 weights, zero accumulators.
 __global__ __launch_bounds__(256) void k_init(MnistFused f, Scratch sc) {
   const int gtid = blockIdx.x * 256 + threadIdx.x, gsz = gridDim.x * 256;
-  for (int i = gtid; i < kWaccSlabs * kPack; i += gsz) sc.wacc[i] = 0.f;
   for (int i = gtid; i < 2048; i += gsz) {
     float w[9];
 #pragma unroll
     for (int r = 0; r < 9; ++r) w[r] = f.p[L::w2 + i * 9 + r];
     conv2_pack_pair(sc, i, w);
   }
-  for (int i = gtid; i < f.B * 128; i += gsz) f.h[i] = 0.f;
-  for (int i = gtid; i < kG1Slabs * 320; i += gsz) sc.g1[i] = 0.f;
-  if (gtid < 64) f.g[L::b2 + gtid] = 0.f;
+  for (int i = gtid; i < f.B * 128; i += gsz) f.h[i] = 0;
+  for (int i = gtid; i < kG1Slabs * 320; i += gsz) sc.g1[i] = 0;
+  if (gtid < 64) sc.db2[gtid] = 0;
 }
 
 // F2 a1 tile pitches (row 38, channel 141): picked by an exhaustive bank model (32-lane groups,
 // bank = dword mod 32) over the two access patterns that dominate F2W's LDS time -- the conv1
 // MFMA stores (16 channels x 2 position groups per 32 lanes) and the stage-2 input-transform
 // reads (3 channels x 12 tiles): 1,472 -> 576 LDS cycles per block (40 / 176 had 8-way store
-// conflicts).  The direct-GEMM variant (MXDDP_MNIST_F2=direct) shares them.
+// conflicts).
 constexpr int kF2RowP = 38, kF2ChP = 141;
 
 // F2W stage 2 (see f2_fwd_kernel): a1 tile [32 ci][4 rows][26] (pitches kF2ChP / kF2RowP) in
@@ -251,33 +229,26 @@ __device__ __forceinline__ void f2_stage2_wino(const MnistFused& f, const Scratc
 // Block = (image b, pooled row py).  Stage 1 builds the 6 input rows it needs (generated by
 // the Philox stream of ops_data.hip synth_batch, or read from x) and recomputes the 4 conv1
 // rows feeding this pooled row straight into the LDS tile (a1 rows shared by neighbouring
-// blocks are recomputed, 25 MFLOP total).  a1 never goes to HBM: the backward (F6/F7)
-// recomputes it from x, which this kernel publishes (each block its own rows).  Stage 2 is the conv2 implicit GEMM: 2 output rows x 24 cols = 48 positions
-// (3 M-tiles of 16) x 64 channels (wave w owns N-tile w).  M is ordered window-major
-// (m = 4*window + 2*dy + dx), so a lane's 4 accumulator registers are exactly one 2x2 pooling
-// window: max-pool + argmax happen in registers.  K = 288 ordered k = r*32 + ci (r = ky*3+kx)
-// so the im2col LDS offset splits into a per-lane base + a compile-time immediate.  The tile
-// [32 ci][4 rows][26] has row pitch kF2RowP and channel pitch kF2ChP (see their definition).  B fragments for all 72 k-steps
-// (18 float4 per lane, pre-packed by the previous SGD) are loaded once into registers.
+// blocks are recomputed, 25 MFLOP total); the rows this block owns are published to a1 for the
+// weight gradient (F6W), and x for the data gradient's conv1 mask.  The tile [32 ci][4 rows][26]
+// has row pitch kF2RowP and channel pitch kF2ChP (see their definition).
 //
-// kWino (default; MXDDP_MNIST_F2=direct selects the above): stage 2 as Winograd F(2x2,3x3).  The
+// Stage 2 is conv2 as Winograd F(2x2,3x3).  The
 // block's 12 pooling windows are exactly 12 Winograd output tiles, so the per-tile inverse
 // transform ends in the 2x2 max-pool.  V = B^T d B of every (tile, ci) goes to LDS over the a1
 // tile ([16 xi][32 ci][16 tiles], tiles 12..15 unused rows), then 16 GEMMs (one per Winograd
 // point) M = 16 tiles x N = 64 co (wave w: 16 co) x K = 32 ci: 128 MFMAs per wave instead of
 // 216.  The 16 accumulators of a lane hold all 16 points of its (tile, co), so A^T M A, bias,
 // max-pool, argmax and ReLU happen in registers.
-template <bool kWino>
 __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
   MX_TRACE(f, 0, 0);
-  __shared__ float tile[kWino ? 16 * 32 * 16 : 32 * kF2ChP];
+  __shared__ float tile[16 * 32 * 16];
   __shared__ float xs[6 * 28];
   __shared__ float w1s[288 + 32];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);  // an image's 12 blocks share one XCD L2
   const int b = bid / 12, py = bid - b * 12;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int row0 = 2 * py;  // first input row of this block's conv1 rows
-  float4 bq[kWino ? 1 : 18];  // direct path: conv2 B fragments for all 72 k-steps
   // ---- stage 1a: input rows row0 .. row0+5 (+ publish the rows this block owns).  Every global
   // operand of stage 1 is requested in ONE round trip: the batch counter, conv1's weights and --
   // synthetic data -- the 6 template rows of ALL 10 classes (the label, a function of the counter,
@@ -297,11 +268,6 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
 #pragma unroll
   for (int c = 0; c < 10; ++c) tv[c] = *reinterpret_cast<const float4*>(f.tmpl + c * 784 + d);
   const float4 xv = *reinterpret_cast<const float4*>(f.x + b * 784 + d);
-  if constexpr (!kWino) {
-    const float4* wf = reinterpret_cast<const float4*>(sc.wf) + w * 64 + lane;
-#pragma unroll
-    for (int q = 0; q < 18; ++q) bq[q] = wf[q * 256];
-  }
   __builtin_amdgcn_sched_barrier(0);  // every stage-1 load issued before the counter is consumed
   {  // branch-free in f.synth (a branch would let the compiler sink the template loads behind
      // the counter's round trip): both sources are formed, one is kept
@@ -371,178 +337,36 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
       // accumulators: the 4 rows of the strip are 104 contiguous floats of channel ci_b, so a
       // lane's 4 consecutive positions are one aligned float4 (no LDS read-back pass)
       const int q0 = 16 * mt + 4 * g;
-      if (f.a1_pub && q0 < (py == 11 ? 104 : 52))
+      if (q0 < (py == 11 ? 104 : 52))
         *reinterpret_cast<float4*>(f.a1 + (size_t)b * 21632 + ci_b * 676 + row0 * 26 + q0) =
             make_float4(o[0], o[1], o[2], o[3]);
     }
   }
   lds_barrier();  // the published a1 rows are read by F6W, not by this block
   MX_TRACE(f, 0, 2);
-  if constexpr (kWino) {
-    f2_stage2_wino(f, sc, tile, b, py, w, lane);
-  } else {
-  // ---- stage 2: conv2 implicit GEMM + pool
-  const int m = lane & 15, g = lane >> 4;
-  const int base = g * kF2ChP + ((m >> 1) & 1) * kF2RowP + 2 * (m >> 2) + (m & 1);
-  f32x4 acc[3];
-#pragma unroll
-  for (int t = 0; t < 3; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int s = 0; s < 72; ++s) {
-    const int r = s >> 3, ky = r / 3, kx = r - 3 * (r / 3);
-    const int koff = 4 * (s & 7) * kF2ChP + ky * kF2RowP + kx;
-    const float bf = sel4(bq[s >> 2], s & 3);
-#pragma unroll
-    for (int t = 0; t < 3; ++t) acc[t] = mfma4(tile[base + 8 * t + koff], bf, acc[t]);
-  }
-  MX_TRACE(f, 0, 4);
-  // epilogue: lane holds window (4t + g) of channel co for the 4 positions j = 2*dy + dx
-  const int co = 16 * w + m;
-  const float bias = f.p[L::b2 + co];
-  uint8_t* idx = reinterpret_cast<uint8_t*>(f.idx);
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    float best = acc[t][0];
-    int q = 0;
-#pragma unroll
-    for (int j = 1; j < 4; ++j)
-      if (acc[t][j] > best) { best = acc[t][j]; q = j; }
-    const float v = best + bias;
-    const int o = ((b * 64 + co) * 12 + py) * 12 + 4 * t + g;
-    f.pool[o] = v > 0.f ? v : 0.f;
-    idx[o] = v > 0.f ? (uint8_t)q : (uint8_t)4;
-  }
-  }
+  f2_stage2_wino(f, sc, tile, b, py, w, lane);
   // side job of the first 8 blocks: this step's conv2 data-gradient Winograd filters for F7W
   if (blockIdx.x < 8) wino_dgrad_filter(f, sc, blockIdx.x * 256 + tid);
   MX_TRACE(f, 0, 5);
 }
 
 // ------------------------------------------------------------------------------------------
-// F3: fc1 forward h_pre[b][n] += pool[b][k-chunk] . W1[n][k-chunk] (split-K, MFMA, atomics into
-// h, which F8 of the previous step zeroed).  Block = (k-chunk of 144, 32 output features);
-// wave w = batch rows 16w..16w+15 (loops over further M-tiles when B > 64).  Operands go
-// straight to registers as float4 along K (64-byte row segments).
-constexpr int kF3Chunk = 144, kF3Groups = kF3Chunk / 16;
-static_assert(kWaccSlabs * kPack / 4 <= (9216 / kF3Chunk) * 4 * 256, "F3 grid must cover the wacc slabs");
-__global__ __launch_bounds__(256) void f3_fc1_kernel(MnistFused f) {
+// F3: fc1 forward h_pre[b][n] = pool[b][:] . W1[n][:], output-tiled split-K on MFMA.
+// Block = (K chunk of 1152, 16 x 16 output tile) -- 8 chunks x B/2 tiles (256 blocks at B = 64).
+// Every block loads only its 16 pool rows and 16 W1 rows of the chunk (147 KB), and the tiles of
+// one chunk sit on one XCD (xcd_remap), so that XCD's L2 holds the chunk's pool / W1 columns
+// once.  Wave w of the 8 reduces K slice w of the chunk (144 deep, all 18 float4 operands issued
+// up front, two accumulator chains), the 8 wave partials are summed in LDS in a fixed order, and
+// one 64-bit fixed-point atomic per output per block adds the chunk partial into h (8 per
+// output; integer adds, so h is exact and independent of the chunks' arrival order -- the float
+// atomics this replaces made every step's rounding depend on it).  h was zeroed by the previous
+// step's finalize.  (Measured alternatives, profiles/r3_mnist_knobs: 64-way split-K with 144-deep
+// chunks 8.85 us; 16-way 576-deep chunks; 4 waves of 288-deep slices 7.8 us; this one 6.7 us.)
+constexpr int kF3TChunks = 8, kF3TK = 9216 / kF3TChunks, kF3Wv = 8;
+__global__ __launch_bounds__(64 * kF3Wv) void f3t_fc1_kernel(MnistFused f) {
   MX_TRACE(f, 1, 0);
-  const int kc = blockIdx.x >> 2, nq = blockIdx.x & 3;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, m = lane & 15;
-  if (f.synth && blockIdx.x == 0 && threadIdx.x == 0) *f.counter += 1;  // F2 consumed it
-  const int k0 = kc * kF3Chunk + 4 * g;
-  const float* W = f.p + L::fw1;
-  float4 bw[2][kF3Groups];
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-    for (int s = 0; s < kF3Groups; ++s)
-      bw[nt][s] = *reinterpret_cast<const float4*>(W + (size_t)(32 * nq + 16 * nt + m) * 9216 + k0 + 16 * s);
-  for (int mt = w; mt < f.B / 16; mt += 4) {
-    float4 av[kF3Groups];
-    const float* A = f.pool + (size_t)(16 * mt + m) * 9216 + k0;
-#pragma unroll
-    for (int s = 0; s < kF3Groups; ++s) av[s] = *reinterpret_cast<const float4*>(A + 16 * s);
-    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-    for (int s = 0; s < kF3Groups; ++s)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        acc[nt] = mfma4(av[s].x, bw[nt][s].x, acc[nt]);
-        acc[nt] = mfma4(av[s].y, bw[nt][s].y, acc[nt]);
-        acc[nt] = mfma4(av[s].z, bw[nt][s].z, acc[nt]);
-        acc[nt] = mfma4(av[s].w, bw[nt][s].w, acc[nt]);
-      }
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        atomicAdd(f.h + (16 * mt + 4 * g + j) * 128 + 32 * nq + 16 * nt + m, acc[nt][j]);
-  }
-  // side job: zero the conv2-wgrad accumulator slabs for this step's F67 (last step's finalize
-  // has read them; one float4 per thread, so the finalize's serial tail carries no stores)
-  if (!f.wslab) {
-    float4* wa = reinterpret_cast<float4*>(carve(f.scratch).wacc);
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < kWaccSlabs * kPack / 4) wa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  MX_TRACE(f, 1, 1);
-}
-
-// F3 with a deeper K chunk per block (kKC = 256 .. 576) split over the block's 4 waves: each wave
-// runs its kKC/4 slice for every batch M-tile, the 4 slices are summed through LDS, and ONE atomic
-// per output per block remains -- 9216 / kKC blocks per output (16-way at kKC = 576) instead of
-// 64-way: the same-address atomic chains that bound the 144-chunk kernel get 2.25-4x shorter.
-// Block = (K chunk, kNF output features).
-template <int kKC, int kNF>
-__global__ __launch_bounds__(256) void f3k_fc1_kernel(MnistFused f) {
-  MX_TRACE(f, 1, 0);
-  constexpr int kG = kKC / 64, kNT = kNF / 16, kNq = 128 / kNF;
-  static_assert(kKC % 64 == 0 && 9216 % kKC == 0 && kNF % 16 == 0, "F3 tiling");
-  __shared__ float red[4][16][kNF + 1];
-  const int kc = blockIdx.x / kNq, nq = blockIdx.x - kc * kNq;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
-  if (f.synth && blockIdx.x == 0 && tid == 0) *f.counter += 1;  // F2 consumed it
-  const int k0 = kc * kKC + w * (kKC / 4) + 4 * g;
-  const float* W = f.p + L::fw1;
-  float4 bw[kNT][kG];
-#pragma unroll
-  for (int nt = 0; nt < kNT; ++nt)
-#pragma unroll
-    for (int s = 0; s < kG; ++s)
-      bw[nt][s] = *reinterpret_cast<const float4*>(W + (size_t)(kNF * nq + 16 * nt + m) * 9216 + k0 + 16 * s);
-  for (int mt = 0; mt < f.B / 16; ++mt) {
-    float4 av[kG];
-    const float* A = f.pool + (size_t)(16 * mt + m) * 9216 + k0;
-#pragma unroll
-    for (int s = 0; s < kG; ++s) av[s] = *reinterpret_cast<const float4*>(A + 16 * s);
-    f32x4 acc[kNT];
-#pragma unroll
-    for (int nt = 0; nt < kNT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < kG; ++s)
-#pragma unroll
-      for (int nt = 0; nt < kNT; ++nt) {
-        acc[nt] = mfma4(av[s].x, bw[nt][s].x, acc[nt]);
-        acc[nt] = mfma4(av[s].y, bw[nt][s].y, acc[nt]);
-        acc[nt] = mfma4(av[s].z, bw[nt][s].z, acc[nt]);
-        acc[nt] = mfma4(av[s].w, bw[nt][s].w, acc[nt]);
-      }
-    if (mt > 0) __syncthreads();  // the previous M-tile's sums have been read
-#pragma unroll
-    for (int nt = 0; nt < kNT; ++nt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) red[w][4 * g + j][16 * nt + m] = acc[nt][j];
-    __syncthreads();
-    for (int i = tid; i < 16 * kNF; i += 256) {
-      const int row = i / kNF, col = i - row * kNF;
-      const float v = (red[0][row][col] + red[1][row][col]) + (red[2][row][col] + red[3][row][col]);
-      atomicAdd(f.h + (16 * mt + row) * 128 + kNF * nq + col, v);
-    }
-  }
-  // side job: zero the conv2-wgrad accumulator slabs for this step's F67 (see f3_fc1_kernel)
-  if (!f.wslab) {
-    float4* wa = reinterpret_cast<float4*>(carve(f.scratch).wacc);
-    for (int i = blockIdx.x * 256 + tid; i < kWaccSlabs * kPack / 4; i += gridDim.x * 256)
-      wa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  MX_TRACE(f, 1, 1);
-}
-
-// F3, output-tiled split-K: block = (K chunk of 1152, 16 x 16 output tile) -- 8 chunks x B/2 tiles
-// (256 blocks at B = 64).  Every block loads only its 16 pool rows and 16 W1 rows of the chunk
-// (147 KB), and the tiles of one chunk sit on one XCD (xcd_remap), so that XCD's L2 holds the
-// chunk's pool / W1 columns once.  Wave w reduces K slice w of the chunk (288 deep, all 36 float4
-// operands issued up front, two accumulator chains), the 4 wave partials are summed in LDS, and
-// one atomic per output per block remains: 8-way per output instead of 64-way (65 K atomics per
-// step instead of 524 K -- the 144-chunk kernel's time was mostly its atomics draining).
-constexpr int kF3TChunks = 8, kF3TK = 9216 / kF3TChunks;
-// kWv = waves per block (4: 288-deep K slices; 8: 144-deep slices, twice the loads in flight per CU)
-template <int kWv>
-__global__ __launch_bounds__(64 * kWv) void f3t_fc1_kernel(MnistFused f) {
-  MX_TRACE(f, 1, 0);
-  constexpr int kTW = kF3TK / kWv, kTS = kTW / 16;
-  __shared__ float red[kWv][16][17];
+  constexpr int kTW = kF3TK / kF3Wv, kTS = kTW / 16;
+  __shared__ float red[kF3Wv][16][17];
   const int tiles = f.B / 2;  // (B / 16) row tiles x 8 column tiles
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int kc = bid / tiles, tile = bid - kc * tiles, mt = tile >> 3, nt = tile & 7;
@@ -570,45 +394,15 @@ __global__ __launch_bounds__(64 * kWv) void f3t_fc1_kernel(MnistFused f) {
   __syncthreads();
   if (tid < 256) {
     const int row = tid >> 4, col = tid & 15;
-    float v = (red[0][row][col] + red[1][row][col]) + (red[2][row][col] + red[3][row][col]);
-    if constexpr (kWv == 8) v += (red[4][row][col] + red[5][row][col]) + (red[6][row][col] + red[7][row][col]);
-    atomicAdd(f.h + (16 * mt + row) * 128 + 16 * nt + col, v);
-  }
-  // side job: zero the conv2-wgrad accumulator slabs for this step's F67 (see f3_fc1_kernel)
-  if (!f.wslab) {
-    float4* wa = reinterpret_cast<float4*>(carve(f.scratch).wacc);
-    for (int i = blockIdx.x * 64 * kWv + tid; i < kWaccSlabs * kPack / 4; i += gridDim.x * 64 * kWv)
-      wa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float v = ((red[0][row][col] + red[1][row][col]) + (red[2][row][col] + red[3][row][col])) +
+                    ((red[4][row][col] + red[5][row][col]) + (red[6][row][col] + red[7][row][col]));
+    fix_add(f.h + (16 * mt + row) * 128 + 16 * nt + col, v, kHScale);
   }
   MX_TRACE(f, 1, 1);
 }
 
-// fc1-forward tiling (MXDDP_F3 = tile8 (default) | tile | 144 | 576x32 | 576x16 | 384x16 | 256x16)
-static int f3_variant() {
-  static const int v = [] {
-    const char* e = std::getenv("MXDDP_F3");
-    const std::string s = e ? e : "";
-    if (s == "144") return 0;
-    if (s == "576x32") return 1;
-    if (s == "576x16") return 2;
-    if (s == "384x16") return 3;
-    if (s == "256x16") return 4;
-    if (s == "tile") return 5;
-    return 6;  // tile8 (measured: 6.7 vs 7.9 us, 902k vs 884k img/s, profiles/r3_mnist_knobs)
-  }();
-  return v;
-}
-
 static void launch_f3(const MnistFused& f, hipStream_t st) {
-  switch (f3_variant()) {
-    case 1: MX_LAUNCH((f3k_fc1_kernel<576, 32>), dim3(16 * 4), dim3(256), 0, st, f); break;
-    case 2: MX_LAUNCH((f3k_fc1_kernel<576, 16>), dim3(16 * 8), dim3(256), 0, st, f); break;
-    case 3: MX_LAUNCH((f3k_fc1_kernel<384, 16>), dim3(24 * 8), dim3(256), 0, st, f); break;
-    case 4: MX_LAUNCH((f3k_fc1_kernel<256, 16>), dim3(36 * 8), dim3(256), 0, st, f); break;
-    case 5: MX_LAUNCH(f3t_fc1_kernel<4>, dim3(kF3TChunks * (f.B / 2)), dim3(256), 0, st, f); break;
-    case 6: MX_LAUNCH(f3t_fc1_kernel<8>, dim3(kF3TChunks * (f.B / 2)), dim3(512), 0, st, f); break;
-    default: MX_LAUNCH(f3_fc1_kernel, dim3((9216 / kF3Chunk) * 4), dim3(256), 0, st, f); break;
-  }
+  MX_LAUNCH(f3t_fc1_kernel, dim3(kF3TChunks * (f.B / 2)), dim3(64 * kF3Wv), 0, st, f);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -623,7 +417,8 @@ static void launch_f3(const MnistFused& f, hipStream_t st) {
 // grad c), block 10 the fc1 bias grad, block 0 the metrics.
 // fc1: dW1[:, cols] = dh^T pool[:, cols] (M=128, K=B) and dp[:, cols] = dh W1[:, cols]
 // (M=B, K=128), both on MFMA from LDS; dp is masked with the max-pool argmax / ReLU liveness
-// (dead windows -> 0) and db2 accumulated.  dh lives in LDS as [B][132] (row pitch = 4 mod 32
+// (dead windows -> 0) and db2 accumulated (wave partials summed in order, one int64
+// fixed-point add per block into the channel's accumulator).  dh lives in LDS as [B][132] (row pitch = 4 mod 32
 // words: float4 row reads and 4-row-strided scalar reads are both bank-conflict free).
 // LDS at B = 64: 92 KB (one block per CU by design).
 // Up to 6 values held in NAMED registers across a long stretch of code: a plain array here
@@ -656,6 +451,7 @@ struct Reg6 {
 
 constexpr int kF5Cols = 48, kF5NT = kF5Cols / 16, kF5C4 = kF5Cols / 4;
 constexpr int kF5DhP = 132, kF5P = 52, kF5W2P = 20, kF5LgP = 20;  // kF5P = 4 mod 8: 4-row groups 16 banks apart
+constexpr int kF5Misc = 12;  // [0..3] db2, [4..7] loss, [8..11] correct: one slot per wave
 template <int B>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void f5_head_fc1_bwd_kernel(MnistFused f) {
   MX_TRACE(f, 2, 0);
@@ -665,8 +461,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   float* wsm = ps + B * kF5P;            // [128][52]: W1 columns of this slice
   float* w2t = wsm + 128 * kF5P;         // [128][20]: W2^T, cols 10..15 zero
   float* lg = w2t + 128 * kF5W2P;        // [B][20]: logits, then dlogits (cols 10..15 zero)
-  float* misc = lg + B * kF5LgP;         // [4]: db2 partials (2), loss, correct
-  uint8_t* qs = reinterpret_cast<uint8_t*>(misc + 4);  // [B][48] argmax codes of this column slice
+  float* misc = lg + B * kF5LgP;         // [kF5Misc]: db2 / loss / correct partials per wave
+  uint8_t* qs = reinterpret_cast<uint8_t*>(misc + kF5Misc);  // [B][48] argmax codes of this column slice
   const int c0 = blockIdx.x * kF5Cols;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
   // folded fc1 SGD: this block owns weight columns c0..c0+47 of every row (old values in wsm);
@@ -678,14 +474,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // and are staged into LDS only after dh.  (Before: every load, then the head: ~3 us more.)
   constexpr int ND = B * 32 / 256, NP = (B * kF5C4 + 255) / 256, NW = (128 * kF5C4 + 255) / 256, N2 = 5;
   static_assert(NP <= 6 && NW <= 6, "F5 prefetch registers");
-  float4 vd[ND], vb1[ND];
+  longlong2 vd[ND][2];  // h_pre as int64 fixed point
+  float4 vb1[ND];
   Reg6<float4> vp, vw;
   float v2[N2];
   Reg6<uint32_t> vq;  // argmax codes, 4 per uint32
 #pragma unroll
   for (int k = 0; k < ND; ++k) {
     const int i = tid + 256 * k;
-    vd[k] = *reinterpret_cast<const float4*>(f.h + (i >> 5) * 128 + (i & 31) * 4);
+    const longlong2* hp = reinterpret_cast<const longlong2*>(f.h + (i >> 5) * 128 + (i & 31) * 4);
+    vd[k][0] = hp[0];
+    vd[k][1] = hp[1];
     vb1[k] = *reinterpret_cast<const float4*>(f.p + L::fb1 + (i & 31) * 4);
   }
 #pragma unroll
@@ -724,7 +523,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
   for (int k = 0; k < ND; ++k) {
     const int i = tid + 256 * k, c4 = (i & 31) * 4;
-    const float4 b1 = vb1[k], hv = vd[k];
+    const float4 b1 = vb1[k];
+    const float4 hv = make_float4(from_fix(vd[k][0].x, kHInv), from_fix(vd[k][0].y, kHInv),
+                                  from_fix(vd[k][1].x, kHInv), from_fix(vd[k][1].y, kHInv));
     *reinterpret_cast<float4*>(dhs + (i >> 5) * kF5DhP + c4) =
         make_float4(fmaxf(hv.x + b1.x, 0.f), fmaxf(hv.y + b1.y, 0.f), fmaxf(hv.z + b1.z, 0.f), fmaxf(hv.w + b1.w, 0.f));
   }
@@ -734,7 +535,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     w2t[(i & 127) * kF5W2P + (i >> 7)] = v2[k];
   }
   for (int i = tid; i < 128 * 6; i += 256) w2t[(i / 6) * kF5W2P + 10 + i % 6] = 0.f;
-  if (tid < 4) misc[tid] = 0.f;
+  if (tid < kF5Misc) misc[tid] = 0.f;
   __syncthreads();
   MX_TRACE(f, 2, 1);
   // ---- head: logits (wave w: batch M-tiles w, w+4, ...; K = 128 permuted for float4 A reads)
@@ -779,11 +580,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int c = 10; c < 16; ++c) l[c] = 0.f;
   }
-  if (blockIdx.x == 0 && 64 * w < B) {  // batch loss / correct: one LDS atomic per wave
+  if (blockIdx.x == 0 && 64 * w < B) {  // batch loss / correct: one slot per wave
     const float ls = wave_sum(loss_v), cs = wave_sum(corr_v);
     if (lane == 0) {
-      atomicAdd(&misc[2], ls);
-      atomicAdd(&misc[3], cs);
+      misc[4 + w] = ls;
+      misc[8 + w] = cs;
     }
   }
   __syncthreads();
@@ -806,8 +607,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     f.g[tid < 128 ? L::fw2 + c * 128 + tid : L::fb2 + c] = sum;
   }
   if (blockIdx.x == 0 && tid == 0 && f.metrics) {
-    atomicAdd(f.metrics, misc[2]);
-    atomicAdd(f.metrics + 1, misc[3]);
+    atomicAdd(f.metrics, (misc[4] + misc[5]) + (misc[6] + misc[7]));
+    atomicAdd(f.metrics + 1, (misc[8] + misc[9]) + (misc[10] + misc[11]));
   }
   if (blockIdx.x < 10) __syncthreads();  // the fc2 grad read h before dh overwrites it
   // ---- head: dh = (dlogits W2) * (h > 0), in place over h (K = 16: c 10..15 are zero)
@@ -934,30 +735,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   {
     const float s = wave_sum(db2_part);
-    if (lane == 0 && s != 0.f) atomicAdd(&misc[0], s);
+    if (lane == 0) misc[w] = s;
   }
   __syncthreads();
   MX_TRACE(f, 2, 6);
-  if (tid == 0 && misc[0] != 0.f) atomicAdd(f.g + L::b2 + c0 / 144, misc[0]);
+  if (tid == 0) fix_add(carve(f.scratch).db2 + c0 / 144, (misc[0] + misc[1]) + (misc[2] + misc[3]), kGScale);
   MX_TRACE(f, 2, 7);
 }
 
 // ------------------------------------------------------------------------------------------
 // SGD over the flat parameter buffer (PyTorch semantics; DDP's 1/world_size folded into
-// gscale) + repack of the updated conv2 weights into the F2 / F7 fragment orders + reset of
-// the conv2 bias grad accumulator (F5 atomics) for the next step.
+// gscale) + repack of the updated conv2 weights into F2's Winograd fragment order.
 // kFin (no gradient collectives in the step, i.e. world size 1): F8's duties are folded in --
-// the conv2 weight grad is read straight from the [tap][co][ci] accumulator, the conv1 grads are
-// summed over the 8 slabs, both are reset (and written to g for inspection), and h is
-// zeroed -- one launch and one kernel boundary fewer per step.
+// the conv2 weight grad is summed from the per-image slabs, the conv1 and conv2-bias grads are
+// converted from their int64 fixed-point accumulators, all of them are reset (and written to g
+// for inspection), and h is zeroed -- one launch and one kernel boundary fewer per step.
 template <bool kFin>
 __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc, float* __restrict__ buf,
                                                        const float* __restrict__ lr_ptr, float gscale, float mom,
-                                                       float wd, bool pack_direct) {
+                                                       float wd) {
   const float lr = *lr_ptr;
-  // kFin + f.wslab: the last kWslabGroups blocks sum the conv2 weight-gradient slabs (4 (co, ci)
-  // pairs each, fixed order) and update + repack those pairs; the other nflat blocks do the rest
-  const int ngrp = (kFin && f.wslab) ? kWslabGroups : 0, nflat = (int)gridDim.x - ngrp;
+  // kFin: the last kWslabGroups blocks sum the conv2 weight-gradient slabs (4 (co, ci) pairs
+  // each, fixed order) and update + repack those pairs; the other nflat blocks do the rest
+  const int ngrp = kFin ? kWslabGroups : 0, nflat = (int)gridDim.x - ngrp;
   if ((int)blockIdx.x >= nflat) {
     __shared__ float red[576 + 36];
     const int grp = (int)blockIdx.x - nflat;
@@ -980,7 +780,7 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
         buf[e0 + r] = bb[r];
         f.p[e0 + r] = pe[r];
       }
-      conv2_pack_pair(sc, pair, pe, pack_direct);
+      conv2_pack_pair(sc, pair, pe);
     }
     return;
   }
@@ -989,40 +789,55 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
   float4* b4 = reinterpret_cast<float4*>(buf);
   constexpr int n4 = (int)(L::total / 4);  // 299970 float4 (total = 1199882 = 4*299970 + 2)
   if (kFin) {
-    float4* h4 = reinterpret_cast<float4*>(f.h);
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < f.B * 32; i += nflat * 256)
-      h4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    longlong2* h2 = reinterpret_cast<longlong2*>(f.h);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < f.B * 64; i += nflat * 256) h2[i] = make_longlong2(0, 0);
   }
   constexpr int kW2a = (int)L::w2 / 4, kW2b = ((int)L::w2 + kPack) / 4;  // conv2 weights (float4 range)
   constexpr int kF1a = (int)L::fw1 / 4, kF1n = ((int)L::fb1 - (int)L::fw1) / 4;  // fc1 weights (float4 range)
-  static_assert(L::fw1 % 4 == 0 && L::fb1 % 4 == 0, "fc1 weights must be float4-aligned");
+  static_assert(L::fw1 % 4 == 0 && L::fb1 % 4 == 0 && L::b2 % 4 == 0, "fc1 / conv2 bias must be float4-aligned");
   const int skip = f.fc1_sgd ? kF1n : 0;  // fc1 updated by F5: iterate around it
   for (int t = blockIdx.x * 256 + threadIdx.x; t < n4 - skip; t += nflat * 256) {
     const int i = t >= kF1a ? t + skip : t;
     if (i >= kW2a && i < kW2b) continue;  // per (co, ci) pair below
     float4 pv = p4[i];
     float4 gv = g4[i];
-    if (kFin && i < kW2a) {  // conv1 w/b: fixed-order sum of the 8 slabs
-      float4* sl = reinterpret_cast<float4*>(sc.g1) + i;
-      const int ns = g1_slab_mask(f) + 1;
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int k0 = 0; k0 < ns; k0 += 16) {  // 16 loads in flight, fixed order
-        float4 v[16];  // clamped loads, masked adds: no load behind a branch
+    if (kFin && (i < kW2a || (i >= kW2b && i < kW2b + 16))) {
+      // conv1 w/b: exact int64 sum of the slabs; conv2 bias: its accumulator.  Then reset them.
+      long long a[4] = {0, 0, 0, 0};
+      if (i < kW2a) {
+        longlong2* sl = reinterpret_cast<longlong2*>(sc.g1) + 2 * i;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = sl[min(k0 + k, ns - 1) * 80];
+        for (int k0 = 0; k0 < kG1Slabs; k0 += 8) {
+          longlong2 v[16];  // 8 slabs' loads in flight, then the adds
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const bool in = k0 + k < ns;
-          a.x += in ? v[k].x : 0.f;
-          a.y += in ? v[k].y : 0.f;
-          a.z += in ? v[k].z : 0.f;
-          a.w += in ? v[k].w : 0.f;
+          for (int k = 0; k < 8; ++k) {
+            v[2 * k] = sl[(k0 + k) * 160];
+            v[2 * k + 1] = sl[(k0 + k) * 160 + 1];
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            a[0] += v[2 * k].x;
+            a[1] += v[2 * k].y;
+            a[2] += v[2 * k + 1].x;
+            a[3] += v[2 * k + 1].y;
+          }
         }
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-          if (k0 + k < ns) sl[(k0 + k) * 80] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = 0; k < kG1Slabs; ++k) {
+          sl[k * 160] = make_longlong2(0, 0);
+          sl[k * 160 + 1] = make_longlong2(0, 0);
+        }
+      } else {
+        longlong2* d = reinterpret_cast<longlong2*>(sc.db2) + 2 * (i - kW2b);
+        const longlong2 v0 = d[0], v1 = d[1];
+        a[0] = v0.x;
+        a[1] = v0.y;
+        a[2] = v1.x;
+        a[3] = v1.y;
+        d[0] = make_longlong2(0, 0);
+        d[1] = make_longlong2(0, 0);
       }
-      gv = a;
+      gv = make_float4(from_fix(a[0], kGInv), from_fix(a[1], kGInv), from_fix(a[2], kGInv), from_fix(a[3], kGInv));
       g4[i] = gv;
     }
     float4 bv = b4[i];
@@ -1036,32 +851,18 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
     pv.w -= lr * bv.w;
     b4[i] = bv;
     p4[i] = pv;
-    if (i >= kW2b && i < kW2b + 16) g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);  // conv2 bias grad reset
   }
-  // conv2 weights: one thread per (co, ci) pair updates its 9 taps and writes every packed form
-  // (kFin: the gradient is summed straight from the [slab][tap][co][ci] accumulator).
-  // The pairs go to wave 0 of the grid's last 32 blocks (one main-loop pass each: 32 CUs share
-  // the scattered stores); all 27 loads are issued before any store.
+  // !kFin (the gradient was all-reduced, F8 wrote it to g): conv2 weights, one thread per
+  // (co, ci) pair updates its 9 taps and rewrites its Winograd filter.  The pairs go to wave 0
+  // of the grid's last 32 blocks (one main-loop pass each: 32 CUs share the scattered stores);
+  // all 27 loads are issued before any store.
   const int pair = ((int)blockIdx.x - (nflat - 32)) * 64 + (int)threadIdx.x;
-  if (ngrp == 0 && (int)blockIdx.x + 32 >= nflat && threadIdx.x < 64 && pair >= 0 && pair < 2048) {
-    const int co = pair >> 5, ci = pair & 31, e0 = (int)L::w2 + pair * 9;
+  if (!kFin && (int)blockIdx.x + 32 >= nflat && threadIdx.x < 64 && pair >= 0 && pair < 2048) {
+    const int e0 = (int)L::w2 + pair * 9;
     float gg[9], pe[9], bb[9];
-    if (kFin) {  // fixed-order sum of the accumulator slabs
-      float sl[kWaccSlabs][9];
-#pragma unroll
-      for (int k = 0; k < kWaccSlabs; ++k)
-#pragma unroll
-        for (int r = 0; r < 9; ++r) sl[k][r] = sc.wacc[k * kPack + (r * 64 + co) * 32 + ci];
-#pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        gg[r] = sl[0][r];
-#pragma unroll
-        for (int k = 1; k < kWaccSlabs; ++k) gg[r] += sl[k][r];
-      }
-    }
 #pragma unroll
     for (int r = 0; r < 9; ++r) {
-      if (!kFin) gg[r] = f.g[e0 + r];
+      gg[r] = f.g[e0 + r];
       pe[r] = f.p[e0 + r];
       bb[r] = buf[e0 + r];
     }
@@ -1069,13 +870,10 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
     for (int r = 0; r < 9; ++r) {
       bb[r] = mom * bb[r] + (gg[r] * gscale + wd * pe[r]);
       pe[r] -= lr * bb[r];
-      if (kFin) {
-        f.g[e0 + r] = gg[r];  // (F3 of the next step zeroes the slabs)
-      }
       buf[e0 + r] = bb[r];
       f.p[e0 + r] = pe[r];
     }
-    conv2_pack_pair(sc, pair, pe, pack_direct);
+    conv2_pack_pair(sc, pair, pe);
   }
   if (blockIdx.x == 0 && threadIdx.x < (int)(L::total - 4 * n4)) {  // 2-element tail (fc2.bias)
     const int e = 4 * n4 + threadIdx.x;
@@ -1091,15 +889,6 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
 using namespace mnist;
 
 size_t mnist_fused_scratch_floats(int B) { return scratch_floats(B); }
-
-int mnist_g1_slabs() {
-  static const int v = [] {
-    const char* e = std::getenv("MXDDP_G1_SLABS");
-    const int s = e ? std::atoi(e) : 16;
-    return (s == 8 || s == 16 || s == 32 || s == 64) ? s : 16;
-  }();
-  return v;
-}
 
 static void check(const MnistFused& f) {
   MX_CHECK(f.B % 16 == 0 && f.B >= 16 && f.B <= 128, "fused MNIST engine needs batch % 16 == 0 and 16 <= B <= 128");
@@ -1121,15 +910,6 @@ static void set_lds_limits() {
   done = true;
 }
 
-// F2 variant: Winograd conv2 (default) or direct implicit GEMM (MXDDP_MNIST_F2=direct).
-static bool f2_wino() {
-  static const int v = [] {
-    const char* e = std::getenv("MXDDP_MNIST_F2");
-    return (e && std::string(e) == "direct") ? 0 : 1;
-  }();
-  return v == 1;
-}
-
 void mnist_fused_init(const MnistFused& f, hipStream_t st) {
   check(f);
   set_lds_limits();
@@ -1141,16 +921,13 @@ void mnist_fused_forward(const MnistFused& f, hipStream_t st) {
   check(f);
   set_lds_limits();
   const Scratch sc = carve(f.scratch);
-  if (f2_wino())
-    MX_LAUNCH(f2_fwd_kernel<true>, dim3(f.B * 12), dim3(256), 0, st, f, sc);
-  else
-    MX_LAUNCH(f2_fwd_kernel<false>, dim3(f.B * 12), dim3(256), 0, st, f, sc);
+  MX_LAUNCH(f2_fwd_kernel, dim3(f.B * 12), dim3(256), 0, st, f, sc);
   launch_f3(f, st);
   MX_HIP_CHECK(hipGetLastError());
 }
 
 void mnist_fused_fc1_bwd(const MnistFused& f, hipStream_t st) {
-  const size_t lds = sizeof(float) * ((size_t)f.B * kF5DhP + f.B * kF5P + 128 * kF5P + 128 * kF5W2P + f.B * kF5LgP + 4) +
+  const size_t lds = sizeof(float) * ((size_t)f.B * kF5DhP + f.B * kF5P + 128 * kF5P + 128 * kF5W2P + f.B * kF5LgP + kF5Misc) +
                      (size_t)f.B * kF5Cols;
   const dim3 grid(9216 / kF5Cols), block(256);
   switch (f.B) {
@@ -1172,13 +949,11 @@ void mnist_fused_sgd(const MnistFused& f, float* mom_buf, const float* lr, float
   MX_CHECK(!f.fc1_sgd || (finalize && gscale == 1.f && f.mom == mom_buf),
            "fc1 SGD is folded into F5 only without gradient collectives");
   // folded: ~20 K elements left (+ the 32 pair blocks, or the 512 slab-sum pair-group blocks)
-  const dim3 grid((f.fc1_sgd ? 128 : 1024) + (finalize && f.wslab ? kWslabGroups : 0));
+  const dim3 grid((f.fc1_sgd ? 128 : 1024) + (finalize ? kWslabGroups : 0));
   if (finalize)
-    MX_LAUNCH(sgd_pack_kernel<true>, grid, dim3(256), 0, st, f, carve(f.scratch), mom_buf, lr, gscale,
-              momentum, wd, !(f2_wino() && mnist_f7_wino()));
+    MX_LAUNCH(sgd_pack_kernel<true>, grid, dim3(256), 0, st, f, carve(f.scratch), mom_buf, lr, gscale, momentum, wd);
   else
-    MX_LAUNCH(sgd_pack_kernel<false>, grid, dim3(256), 0, st, f, carve(f.scratch), mom_buf, lr, gscale,
-              momentum, wd, !(f2_wino() && mnist_f7_wino()));
+    MX_LAUNCH(sgd_pack_kernel<false>, grid, dim3(256), 0, st, f, carve(f.scratch), mom_buf, lr, gscale, momentum, wd);
   MX_HIP_CHECK(hipGetLastError());
 }
 

@@ -2095,8 +2095,7 @@ static int g_conv_glds = -1;
 void nhwc_conv_set_glds(int mode) { g_conv_glds = mode; }
 static int conv_glds_mode() {
   if (g_conv_glds < 0) {
-    const char* e = std::getenv("MXDDP_CONV_GLDS");
-    g_conv_glds = (e && *e) ? std::atoi(e) : 1;
+    g_conv_glds = 1;  // nhwc_conv_set_glds() overrides (tests, A/B runs)
   }
   return g_conv_glds;
 }
@@ -2149,6 +2148,16 @@ static bool stem_mode() {
   return on;
 }
 
+// MXDDP_CONV_C3=0: the 3x3 / 64-channel layers' forward and data gradient on the generic kernels
+// (A/B switch for the band kernel alone; MXDDP_STEM covers the stem kernels only)
+static bool conv_c3_mode() {
+  static const bool on = [] {
+    const char* e = std::getenv("MXDDP_CONV_C3");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
 // returns the number of BN partial rows the epilogue wrote to a.bnpart (0: none, the BN runs its
 // own statistics pass)
 static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
@@ -2157,7 +2166,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   a.fOHW = FastDiv(a.OH * a.OW);
   a.fCa = FastDiv(a.Ca);
   a.fS = FastDiv(a.S);
-  if (c3_eligible(a) && stem_mode()) {  // persistent band kernel (forward or data gradient)
+  if (c3_eligible(a) && conv_c3_mode()) {  // persistent band kernel (forward or data gradient)
     const int rt = c3_band_rows(a.OH, a.OW), nb = a.M / (rt * a.OW);
     // BN rows: one per band (nhwc_conv_bn_rows sized the buffer for them)
     if (!(a.bnpart && !a.dgrad && nb <= 16384)) a.bnpart = nullptr;
@@ -2320,10 +2329,7 @@ static int wgrad_splits(int Npix, int K, int Ng) {
   wgrad_tile(K, Ng, tm, tn);
   const int tiles = cdiv(K, tm) * cdiv(Ng, tn);
   // ~2 blocks per CU, >= 512 pixels (8 stages) per block, partial planes <= 32M floats
-  static const int target = [] {
-    const char* e = std::getenv("MXDDP_WGRAD_BLOCKS");
-    return (e && *e) ? std::max(1, std::atoi(e)) : 512;
-  }();
+  constexpr int target = 512;
   int splits = std::max(1, cdiv(target, tiles));
   splits = std::min(splits, std::max(1, Npix / 512));
   splits = std::min(splits, std::max(1, (int)((32ll << 20) / ((int64_t)K * Ng))));
@@ -2369,7 +2375,7 @@ void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, in
   a.fCa = FastDiv(Cp);
   a.fS = FastDiv(S);
   MX_CHECK((int64_t)K * a.Ng < (1ll << 31), "nhwc wgrad: weight too large for 32-bit indices");
-  if (wgrad_c3_eligible(a) && stem_mode() && wgrad_c3_mode()) {  // persistent band kernel, one plane per block
+  if (wgrad_c3_eligible(a) && wgrad_c3_mode()) {  // persistent band kernel, one plane per block
     const int rt = c3_band_rows(P, Q);
     MX_LAUNCH(wgrad_c3_kernel, dim3(kSwBlocks), dim3(512), 0, st, a, rt, N * (P / rt));
     const int plane4 = K * a.Ng / 4;

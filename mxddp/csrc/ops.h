@@ -187,7 +187,7 @@ size_t nhwc_conv_scratch_floats(int M, int Ng, int Kg);
 int nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int H, int W, int Cp, int K, int R,
                   int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st,
                   float* bnpart = nullptr, const float* bnshift = nullptr);
-// large-layer LDS-DMA conv kernel: 0 = off, 1 = large layers (default, env MXDDP_CONV_GLDS), 2 = always
+// large-layer LDS-DMA conv kernel: 0 = off, 1 = large layers (default), 2 = always
 void nhwc_conv_set_glds(int mode);
 // split-K scratch of nhwc_conv_dgrad (floats; 0 = none needed)
 size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,

@@ -436,13 +436,9 @@ __global__ __launch_bounds__(kBnF) void bn_bwd_fused_k(const float* __restrict__
 }
 
 // per-channel blocks when the channel is small enough for one block and there are enough
-// channels to occupy the chip; MXDDP_BN_FUSED_MAX = per-channel value limit (0 disables)
+// channels to occupy the chip: at most 16,384 values per channel
 bool bn_use_fused(int N, int C, int HW) {
-  static const int64_t lim = [] {
-    const char* e = std::getenv("MXDDP_BN_FUSED_MAX");
-    return e ? (int64_t)std::atoll(e) : (int64_t)16384;
-  }();
-  return HW % 4 == 0 && (int64_t)N * HW <= lim && C >= 64;
+  return HW % 4 == 0 && (int64_t)N * HW <= 16384 && C >= 64;
 }
 
 }  // namespace

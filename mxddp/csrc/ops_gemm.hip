@@ -518,16 +518,8 @@ __global__ void splitk_finish_k(const float* __restrict__ part, int splits, int 
 
 // Split factor for a GEMM of `tiles` output tiles over K: only when the tiles alone leave the
 // chip mostly idle and each split keeps >= 64 reduction elements (4 f32 k-tiles).
-bool partial_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("MXDDP_SPLITK_PARTIAL");
-    return !(e && std::string(e) == "0");
-  }();
-  return on;
-}
-
 int partial_splits(int tiles, int K) {
-  if (tiles >= 192 || K < 128 || !partial_enabled()) return 1;
+  if (tiles >= 192 || K < 128) return 1;
   return pick_splits(tiles, K, 64, 512);
 }
 
@@ -561,11 +553,7 @@ bool run_partial(Op& op, int64_t total, float* out, const float* bias, int C, in
 void reserve_splitk_planes(hipStream_t st) { (void)splitk_planes(kPlaneFloats, st); }
 
 namespace {
-int init_conv_algo() {
-  const char* e = std::getenv("MXDDP_CONV_ALGO");
-  return (e && std::string(e) == "direct") ? 1 : 0;
-}
-int g_conv_algo = init_conv_algo();
+int g_conv_algo = 0;  // set_conv_algo(): 0 = Winograd where eligible, 1 = direct
 bool use_wino(const ConvShape& s) { return g_gemm_precision == 0 && g_conv_algo == 0 && wino_eligible(s); }
 }  // namespace
 

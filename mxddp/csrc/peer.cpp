@@ -65,7 +65,6 @@ PeerComm::PeerComm(int rank, int world_size, int device, size_t cap_bytes, int b
   MX_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0));
   if (const char* t = std::getenv("MXDDP_PEER_TIMEOUT_MS")) set_timeout_ms(std::atof(t));
   else timeout_ = 3000000000ll;  // 30 s: a slow rank (checkpoint, evaluation) is not an error
-  if (const char* o = std::getenv("MXDDP_PEER_ONESHOT_BYTES")) oneshot_bytes_ = std::atoll(o);
   MX_HIP_CHECK(hipDeviceSynchronize());
   peer_x_[rank_] = xbuf_;
   peer_sig_[rank_] = sig_;

@@ -37,6 +37,16 @@ void Reducer::prepare() {
   step_compute_ = nullptr;
 }
 
+void Reducer::abort() {
+  // a backward that raised after some buckets were launched: wait for what the side stream
+  // already runs (nothing may still write the gradient), then forget the step
+  if (side_used_) MX_HIP_CHECK(hipStreamSynchronize(comm_stream_));
+  side_used_ = false;
+  in_step_ = false;
+  step_compute_ = nullptr;
+  sched_.prepare();
+}
+
 void Reducer::set_timing(bool on) {
   if (on && !t0_) {
     MX_HIP_CHECK(hipEventCreate(&t0_));

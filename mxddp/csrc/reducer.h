@@ -35,7 +35,10 @@ class Reducer {
           const std::vector<int>& param_bucket, RedOp op, bool timing);
   ~Reducer();
 
-  void prepare();                                   // start of a backward pass
+  void prepare();
+  // drop a step whose backward failed between prepare() and finalize() (joins the side stream)
+  void abort();
+  // start of a backward pass
   void mark_ready(int param_idx, hipStream_t compute);
   void mark_bucket_ready(int bucket, hipStream_t compute);  // fused engines: whole bucket at once
   void finalize(hipStream_t compute);               // launch stragglers; compute waits on comm

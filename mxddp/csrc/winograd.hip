@@ -820,11 +820,7 @@ void launch_fwd(const float* x, const float* w, const float* bias, const float* 
   a.Cop = Cop;
   // 3 = patch-staged 32 x 64 blocks (fastest on 32x32 images), 2 = per-window 32 x 32 blocks
   // (fastest on 16x16 / 8x8, where the larger block leaves too few blocks to fill the chip);
-  // measured per shape by scripts/bench_conv.py.  MXDDP_WINO_FWD=2|3|4 forces one.
-  static const int forced = [] {
-    const char* e = std::getenv("MXDDP_WINO_FWD");
-    return e ? std::atoi(e) : 0;
-  }();
+  // measured per shape by scripts/bench_conv.py.
   const int tpi = (Wd / 2) * (Wd / 2);
   // 4 = two K groups per 32 x 32 block: where the 32 x 32 grid fits in one wave of blocks (one
   // block per CU, e.g. the 8x8 layers up to 256 channels), doubling the MFMAs per barrier
@@ -833,34 +829,18 @@ void launch_fwd(const float* x, const float* w, const float* bias, const float* 
   // 32x32 images with one 32-channel output tile (the first stage-1 layers): the 32 x 64 patch
   // blocks leave one block per CU and the 32 x 32 blocks win (11.7 vs 14.5 us at C = 16)
   const int blocks32 = cdiv(N * tpi, 32) * (Cop / 32), cus = device_cu_count();
-  const int variant = forced ? forced
-                             : (Wd == 32 ? (blocks32 / 2 >= 2 * cus ? 3 : 2) : (blocks32 <= cus ? 4 : 2));
+  const int variant = Wd == 32 ? (blocks32 / 2 >= 2 * cus ? 3 : 2) : (blocks32 <= cus ? 4 : 2);
   const int tile_blk = variant == 3 ? 64 : 32;
   a.tblocks = cdiv(N * tpi, tile_blk);
   a.ktiles = Cop / 32;
-  const int nch = Cip / kCC;
-  // split the input channels when the grid would not fill the CUs (e.g. 8x8 images); only for
-  // plain outputs (no ReLU / mask), each split adds its partial result atomically
-  static const int slots_env = [] {
-    const char* e = std::getenv("MXDDP_WINO_SLOTS");
-    return e ? std::atoi(e) : -1;
-  }();
-  // Measured (scripts/bench_conv.py): splitting the input channels over blocks with atomic
-  // accumulation LOSES on every PyramidNet shape (8x8: 63 -> 45 us without it), the atomics
-  // and the output memset cost more than the extra blocks gain.  Off unless MXDDP_WINO_SLOTS.
-  const int slots = slots_env >= 0 ? slots_env : 0;
-  int splits = 1;
-  const int base = a.tblocks * a.ktiles;
-  if (!relu && !mask && base < slots) splits = std::max(1, std::min(cdiv(slots, base), nch / 4));
-  a.chunks_per_split = cdiv(nch, splits);
-  a.splits = cdiv(nch, a.chunks_per_split);
+  // One block per (tile group, output-channel tile) over all input channels.  (Measured with
+  // scripts/bench_conv.py: splitting the input channels over blocks with atomic accumulation
+  // LOSES on every PyramidNet shape -- 8x8: 63 vs 45 us -- the atomics and the output memset
+  // cost more than the extra blocks gain; removed.)
+  a.chunks_per_split = Cip / kCC;
+  a.splits = 1;
   a.relu = relu;
-  if (a.splits > 1) {
-    if (!accumulate) zero_fill(y, (int64_t)N * Co * Wd * Wd, st);
-    a.accumulate = 2;
-  } else {
-    a.accumulate = accumulate ? 1 : 0;
-  }
+  a.accumulate = accumulate ? 1 : 0;
   const dim3 grid(a.tblocks * a.ktiles * a.splits);
   if (variant == 3) {
     switch (Wd) {
@@ -913,12 +893,8 @@ WgradPlan wgrad_plan(const ConvShape& s) {
   const int cap = std::max(16, (int)std::min<int64_t>(1024, (8ll << 20) / ((int64_t)s.K * s.C * 9)));
   // The grid must not exceed the 3 x 256 resident slots: a few blocks over (e.g. 25 tiles x 31
   // ranges = 775) run as a second round and nearly double the kernel time.
-  static const int slots = [] {
-    const char* e = std::getenv("MXDDP_WGRAD_SLOTS");
-    return e ? std::atoi(e) : 3 * device_cu_count();
-  }();
-  static const bool ceil_mode = std::getenv("MXDDP_WGRAD_CEIL") != nullptr;  // old rounding, A/B only
-  int nblk = std::max(1, std::min(ceil_mode ? cdiv(slots, tiles) : slots / tiles, cap));
+  const int slots = 3 * device_cu_count();
+  int nblk = std::max(1, std::min(slots / tiles, cap));
   nblk = std::min(nblk, std::max(1, p.nchunks / 8));
   p.cpb = cdiv(p.nchunks, nblk);
   p.nblk = cdiv(p.nchunks, p.cpb);

@@ -81,7 +81,6 @@ class FusedMnistTrainer:
         self.stream = torch.cuda.ExternalStream(self.eng.stream, device=self.device)
         self.steps = 0
         self.steps_at_reset = 0  # self.steps when the device metrics were last zeroed
-        self.eng.set_small_first(os.environ.get("MXDDP_SMALL_FIRST", "0") == "1")
         self.world_size = comm.world_size if comm is not None else (peer.world_size if peer is not None else 1)
         self._set_padding(comm)
         # gradient transport (world size > 1): RCCL, or the direct xGMI peer all-reduce

@@ -311,14 +311,13 @@ class _Linear(torch.autograd.Function):
         N = w.shape[0]
         dy = dy.reshape(M, N).contiguous()
         st = stream_of(dy)
-        # MXDDP_RELU_ON_LOAD=1: the fused ReLU's mask (y > 0) is applied as the three GEMM /
-        # reduction kernels load dy instead of a relu_bwd pass (measured: no gain inside a
-        # captured step, MLP 468-470k vs 471-480k img/s, so off by default)
-        dm = y.data_ptr() if ctx.relu else 0
-        if ctx.relu and not _RELU_ON_LOAD:
+        # the fused ReLU's mask as one relu_bwd pass (applying it as the three GEMM / reduction
+        # kernels load dy measured no faster inside a captured step: MLP 468-470k vs 471-480k)
+        dm = 0
+        if ctx.relu:
             g = torch.empty_like(dy)
             C.relu_bwd(dy.data_ptr(), y.data_ptr(), g.data_ptr(), dy.numel(), st)
-            dy, dm = g, 0
+            dy = g
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty((M, K), device=dy.device, dtype=dy.dtype)
@@ -340,9 +339,6 @@ class _Linear(torch.autograd.Function):
                 _grad_done(b)
                 db = None
         return dx, dw, db, None
-
-
-_RELU_ON_LOAD = os.environ.get("MXDDP_RELU_ON_LOAD", "0") == "1"
 
 
 def linear(x, w, b=None, relu=False):

@@ -30,8 +30,15 @@ class _FlatOptimizer:
         self.grad_scale = 1.0
 
     def _sync_lr(self):
+        """Write a changed host learning rate to the device tensor the kernels read.  Never
+        inside a stream capture: the fill would be recorded into the graph and every replay
+        would write the capture-time lr back over the value ``before_replay`` set.  The sync is
+        left pending instead (``_lr_host`` unchanged), so the next eager step or
+        ``before_replay`` applies it."""
         lr = self.param_groups[0]["lr"]
         if lr != self._lr_host:
+            if self._lr_dev.is_cuda and torch.cuda.is_current_stream_capturing():
+                return
             self._lr_dev.fill_(lr)
             self._lr_host = lr
 
@@ -48,7 +55,22 @@ class SGD(_FlatOptimizer):
         super().__init__(flat, lr)
         self.momentum, self.weight_decay = momentum, weight_decay
         self.buf = torch.zeros_like(flat.data) if momentum else flat.data.new_zeros(16)
-        self.steps = 0
+        # completed steps: on a GPU a device counter advanced inside the step (graph replays
+        # count too), on the CPU a host int
+        self._steps_host = 0
+        self._steps_dev = torch.zeros(1, dtype=torch.int64, device=flat.data.device) if flat.data.is_cuda else None
+
+    @property
+    def steps(self) -> int:
+        if self._steps_dev is not None:
+            return int(self._steps_dev.item())
+        return self._steps_host
+
+    @steps.setter
+    def steps(self, n: int):
+        self._steps_host = int(n)
+        if self._steps_dev is not None:
+            self._steps_dev.fill_(int(n))
 
     @torch.no_grad()
     def step(self):
@@ -65,7 +87,10 @@ class SGD(_FlatOptimizer):
                 self.buf.mul_(self.momentum).add_(g)  # buf starts at 0 -> buf = g at step 1
                 g = self.buf
             f.data.sub_(self.lr * g)
-        self.steps += 1
+        if self._steps_dev is not None:
+            self._steps_dev.add_(1)
+        else:
+            self._steps_host += 1
 
     def state_dict(self):
         return {"lr": self.lr, "momentum_buffer": self.buf.detach().cpu().clone(), "steps": self.steps}

@@ -206,6 +206,11 @@ class DistributedDataParallel(nn.Module):
         if self.broadcast_buffers and self.world_size > 1 and self.module.training:
             with torch.no_grad():
                 self._broadcast(self.flat_buffers)
+        if self._queued:
+            # the previous backward raised after its first gradient hook: its finalize callback
+            # never ran, so drop that step's reducer state before starting a new one
+            self.reducer.abort()
+            self._queued = False
         if torch.is_grad_enabled():
             self.reducer.prepare()
         return self.module(*args, **kwargs)
@@ -249,6 +254,11 @@ class _GlooReducer:
         self.marked = set()
         self.next = 0
         self.works = []
+
+    def abort(self):
+        """Drop a step whose backward raised (its async all-reduces are abandoned, not joined:
+        the peers of a failed step may never post theirs)."""
+        self.prepare()
 
     def mark_ready(self, p, _stream=0):
         if p in self.marked:

@@ -1,0 +1,88 @@
+#!/bin/bash
+# One parameterised GPU-box runner (replaces the per-experiment gpu_r3*.sh one-offs):
+#
+#   scripts/gpu_run.sh <step> [<step> ...]
+#
+# Each step runs under its own timeout, logs to gpurun_out/<step>.log and appends to
+# gpurun_out/steps.log; the run stops at the first crash / timeout (gpu_check.sh).  Kernel-trace
+# summaries land in gpurun_out/summary_<step>.txt, counter passes in gpurun_out/pmc_<step>.txt.
+# Steps:
+#   suite        full GPU test suite           smoke        __graft_entry__.smoke()
+#   driver       bench at the driver's length  long         2,000-step bench
+#   prof_mnist   rocprofv3 kernel trace of the MNIST step
+#   pmc_mnist    counter passes of the MNIST step (eager launches, one pass per run)
+#   keras / keras_rep / keras_ws2 / prof_keras / pmc_keras   Keras CNN fused engine
+#   mlp / mlp_rep / prof_mlp / pmc_mlp                       Chainer MLP
+#   rn32 / rn256 / prof_rn / pmc_rn / rn_stock               ResNet-50 bf16
+#   pyr / prof_pyr / pyr_stock                               PyramidNet-110
+#   ws2 / ws4 / ws8 (MNIST), keras_ws8, pyr_ws8, rn_ws8      shared-GPU DDP rehearsals
+#   coll         MNIST with RCCL collectives forced at one rank
+#   cpu          BASELINE config 1
+source "$(dirname "$0")/gpu_check.sh"
+rm -f gpurun_out/steps.log
+
+SQ_A="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"
+SQ_B="SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_VALU"
+
+prof() {  # prof <name> <steps-for-per-step-numbers> <bench args...>
+  local name=$1 n=$2; shift 2
+  run "$name" 300 rocprofv3 --kernel-trace --stats -d "gpurun_out/$name" -o run --output-format csv -- python bench.py "$@"
+  python scripts/kstats.py "$(find "gpurun_out/$name" -name '*kernel_stats.csv' | head -1)" "$n" > "gpurun_out/summary_$name.txt" || true
+}
+pmc() {  # pmc <name> <bench args...>: 4 counter passes (SQ A, SQ B, FETCH_SIZE, WRITE_SIZE)
+  local name=$1; shift
+  local i=0
+  for set in "$SQ_A" "$SQ_B" "FETCH_SIZE" "WRITE_SIZE"; do
+    i=$((i + 1))
+    run "${name}_$i" 90 timeout -s KILL 80 rocprofv3 --pmc $set --kernel-trace --output-format csv \
+      -d "gpurun_out/${name}_$i" -o run -- python bench.py "$@"
+  done
+  python scripts/pmc_summary.py $(find gpurun_out/${name}_[1-4] -name '*counter_collection.csv') > "gpurun_out/$name.txt" || true
+}
+ws() {  # ws <name> <ranks> <bench args...>: ranks share the one GPU (functional rehearsal)
+  local name=$1 n=$2; shift 2
+  run "$name" 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
+    --master-port $((29500 + RANDOM % 400)) bench.py --gpus "$n" "$@"
+}
+
+for step in "$@"; do
+  case "$step" in
+    suite) run suite 1500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    driver) run driver 300 python bench.py --steps 20 --warmup 5 ;;
+    long) run long 300 python bench.py --steps 2000 --warmup 100 ;;
+    default) run default 300 python bench.py ;;
+    prof_mnist) prof prof_mnist 200 --steps 200 --warmup 20 --min-warmup-ms 0 ;;
+    pmc_mnist) pmc pmc_mnist --steps 20 --warmup 2 --no-graph --min-warmup-ms 0 ;;
+    phase_mnist) run phase_mnist 300 python bench.py --phase-profile 30 ;;
+    coll) run coll 300 python bench.py --steps 2000 --warmup 100 --force-collectives ;;
+    replica) run replica 300 python bench.py --impl replica --steps 1000 --warmup 50 ;;
+    layers) run layers 300 python bench.py --impl layers --steps 300 --warmup 30 ;;
+    cpu) run cpu 300 python bench.py --cpu --steps 30 --warmup 3 ;;
+    keras) run keras 300 python bench.py --model keras_cnn --steps 2000 --warmup 100 ;;
+    keras_rep) run keras_rep 300 python bench.py --model keras_cnn --impl replica --steps 1000 --warmup 50 ;;
+    prof_keras) prof prof_keras 200 --model keras_cnn --steps 200 --warmup 20 --min-warmup-ms 0 ;;
+    pmc_keras) pmc pmc_keras --model keras_cnn --steps 20 --warmup 2 --no-graph --min-warmup-ms 0 ;;
+    mlp) run mlp 300 python bench.py --model mlp --steps 2000 --warmup 100 ;;
+    mlp_layers) run mlp_layers 300 python bench.py --model mlp --impl layers --steps 300 --warmup 30 ;;
+    mlp_rep) run mlp_rep 300 python bench.py --model mlp --impl replica --steps 1000 --warmup 50 ;;
+    prof_mlp) prof prof_mlp 200 --model mlp --steps 200 --warmup 20 --min-warmup-ms 0 ;;
+    pmc_mlp) pmc pmc_mlp --model mlp --steps 20 --warmup 2 --no-graph --min-warmup-ms 0 ;;
+    rn32) run rn32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 ;;
+    rn256) run rn256 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 ;;
+    rn_stock) run rn_stock 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --impl torch --channels-last ;;
+    prof_rn) prof prof_rn 3 --model resnet50 --dtype bf16 --batch 256 --steps 3 --warmup 2 --min-warmup-ms 0 ;;
+    pmc_rn) pmc pmc_rn --model resnet50 --dtype bf16 --batch 256 --steps 1 --warmup 1 --no-graph --min-warmup-ms 0 ;;
+    pyr) run pyr 300 python bench.py --model pyramidnet110 --steps 20 --warmup 3 ;;
+    pyr_stock) run pyr_stock 300 python bench.py --model pyramidnet110 --steps 20 --warmup 3 --impl torch ;;
+    prof_pyr) prof prof_pyr 5 --model pyramidnet110 --steps 5 --warmup 2 --min-warmup-ms 0 ;;
+    ws2) ws ws2 2 --steps 1000 --warmup 50 ;;
+    ws4) ws ws4 4 --steps 500 --warmup 20 ;;
+    ws8) ws ws8 8 --steps 200 --warmup 20 ;;
+    keras_ws2) ws keras_ws2 2 --model keras_cnn --steps 300 --warmup 30 ;;
+    keras_ws8) ws keras_ws8 8 --model keras_cnn --steps 100 --warmup 10 ;;
+    pyr_ws8) ws pyr_ws8 8 --model pyramidnet110 --batch 8 --steps 5 --warmup 2 ;;
+    rn_ws8) ws rn_ws8 8 --model resnet50 --dtype bf16 --batch 8 --steps 5 --warmup 2 ;;
+    *) echo "gpu_run.sh: unknown step $step"; exit 2 ;;
+  esac
+done
