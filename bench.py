@@ -32,7 +32,7 @@ MODEL_METRIC = {
     "resnet50": "images/sec (whole node) ResNet-50 synthetic-ImageNet DDP (BASELINE config 5)",
     "pyramidnet110": "images/sec (whole node) PyramidNet-110 CIFAR-10 DDP (reference pytorch/README.md benchmark)",
     "keras_cnn": "images/sec (whole node) Keras MNIST CNN (reference tensorflow2/, Adam)",
-    "mlp": "images/sec (whole node) Chainer MNIST MLP (reference chainer/) on the mxddp layers path",
+    "mlp": "images/sec (whole node) Chainer MNIST MLP (reference chainer/, Adam)",
 }
 
 
@@ -83,7 +83,8 @@ def parse():
                          "eager steps (every block stamps its phase boundaries; shows the co-scheduled exchange "
                          "blocks against the conv-backward blocks of the same launch)")
     ap.add_argument("--model", default="mnist_cnn",
-                    help="headline: mnist_cnn (fused).  Others run the layers path: keras_cnn, mlp, pyramidnet110, resnet50")
+                    help="headline: mnist_cnn (fused).  keras_cnn and mlp have fused engines too; pyramidnet110 and "
+                         "resnet50 run the layers path")
     return ap.parse_args()
 
 
@@ -117,12 +118,11 @@ def main():
     B = a.batch
     tr = None  # the fused engine, when one runs
 
-    if a.model not in ("mnist_cnn", "keras_cnn") and a.impl == "fused":
+    if a.model not in ("mnist_cnn", "keras_cnn", "mlp") and a.impl == "fused":
         a.impl = "layers"
-    if a.impl == "fused" and a.model == "keras_cnn":
-        # native fused Keras-CNN step (csrc/keras_kernels.hip) with the reference's Keras Adam
-        from mxddp.keras_engine import FusedKerasTrainer
-
+    if a.impl == "fused" and a.model in ("keras_cnn", "mlp"):
+        # native fused Keras-CNN (csrc/keras_kernels.hip, Keras Adam) / Chainer-MLP step
+        # (csrc/mlp_kernels.hip, Chainer Adam)
         peer = None
         if comm is None and inf.world_size > 1:
             from mxddp.parallel import peer as P
@@ -130,9 +130,23 @@ def main():
             peer = P.peer_comm()
             if peer is None:
                 raise SystemExit("bench.py: ranks share a GPU and the peer transport is unavailable")
-        tr = FusedKerasTrainer(batch=B, device=dev, comm=comm, seed=a.seed, use_graph=not a.no_graph,
-                               steps_per_graph=a.steps_per_graph, peer=peer, force_collectives=a.force_collectives)
+        kw = dict(batch=B, device=dev, comm=comm, seed=a.seed, use_graph=not a.no_graph,
+                  steps_per_graph=a.steps_per_graph, peer=peer, force_collectives=a.force_collectives)
+        if a.model == "mlp":
+            from mxddp.mlp_engine import FusedMlpTrainer
+
+            tr = FusedMlpTrainer(graph_mode=a.graph_mode, transport=a.transport, **kw)
+        else:
+            from mxddp.keras_engine import FusedKerasTrainer
+
+            tr = FusedKerasTrainer(**kw)
         run = tr.step
+        if a.buckets is not None and hasattr(tr, "autotune"):
+            tr._set_buckets(a.buckets)
+            a.no_autotune = True
+        if hasattr(tr, "autotune") and a.graph_mode is None and not a.no_autotune and tr.eng.reducer_active:
+            tr.step(1)
+            tr.autotune()  # untimed: a few real steps per candidate strategy, before the warm-up
         if os.environ.get("MXDDP_WARM_GRAPHS", "1") == "1":
             tr.warm_graphs()
     elif a.impl == "fused":
@@ -254,6 +268,10 @@ def _fused_config(a, tr) -> dict:
     if a.model == "keras_cnn":
         return {"optimizer": "adam (Keras eps-hat, lr 1e-3)",
                 "transport": ("peer" if tr.eng.peer_active else "rccl") if tr.eng.reducer_active else "none"}
+    if a.model == "mlp":
+        return {"optimizer": "adam (Chainer eps-hat, lr 1e-3)", "graph_mode": tr.eng.graph_mode,
+                "buckets": tr.bucket_strategy if tr.eng.reducer_active else "none",
+                "transport": tr.active_transport, "autotune": tr.tuned}
     return {"graph_mode": tr.eng.graph_mode, "overlap": tr.eng.overlap, "merged_bucket": tr.eng.merged,
             "coscheduled_exchange": tr.eng.coscheduled,
             "transport": tr.active_transport, "force_collectives": a.force_collectives, "autotune": tr.tuned}
@@ -274,12 +292,13 @@ def _replica(a):
     devices = [torch.device("cuda", i) for i in range(a.gpus)]
     spec = get_spec(a.model)
     torch.manual_seed(a.seed)
-    if a.model in ("mnist_cnn", "keras_cnn") and a.dtype == "fp32" and not a.no_graph:
+    if a.model in ("mnist_cnn", "keras_cnn", "mlp") and a.dtype == "fp32" and not a.no_graph:
         return _replica_fused(a, devices, spec)
 
     def make_opt(flat):
         if spec.optimizer == "adam":
-            return Adam(flat, lr=spec.lr, eps=1e-7, eps_hat=True)
+            # Keras (1e-7) / Chainer (1e-8) epsilon-hat Adam
+            return Adam(flat, lr=spec.lr, eps=1e-7 if a.model == "keras_cnn" else 1e-8, eps_hat=True)
         return SGD(flat, lr=a.lr, momentum=0.9, weight_decay=1e-4)
 
     # per-device step graphs (MXDDP_REPLICA_GRAPH=0: eager)
@@ -334,6 +353,10 @@ def _replica_fused(a, devices, spec):
         from mxddp.keras_engine import FusedKerasReplicas
 
         rep = FusedKerasReplicas(devices, batch=a.batch, seed=a.seed, steps_per_graph=a.steps_per_graph)
+    elif a.model == "mlp":
+        from mxddp.mlp_engine import FusedMlpReplicas
+
+        rep = FusedMlpReplicas(devices, batch=a.batch, seed=a.seed, steps_per_graph=a.steps_per_graph)
     else:
         from mxddp.parallel.replica import FusedMnistReplicas
 

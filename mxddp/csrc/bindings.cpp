@@ -8,6 +8,7 @@
 #include "comm.h"
 #include "common.h"
 #include "keras_engine.h"
+#include "mlp_engine.h"
 #include "mnist_engine.h"
 #include "ops.h"
 #include "peer.h"
@@ -404,15 +405,22 @@ PYBIND11_MODULE(_C, m) {
            py::arg("lr_dev"), py::arg("metrics_dev"), py::arg("b1"), py::arg("b2"), py::arg("eps"),
            py::arg("weight_decay"), py::arg("eps_hat"), py::keep_alive<1, 10>())
       .def("step", &KerasEngine::step)
-      .def("capture", &KerasEngine::capture, py::arg("steps_per_graph") = 1)
+      .def("capture", &KerasEngine::capture, py::arg("mode") = 1, py::arg("steps_per_graph") = 1)
       .def("replay", &KerasEngine::replay)
       .def("uncapture", &KerasEngine::uncapture)
       .def("warm_graphs", &KerasEngine::warm_graphs)
       .def("repack", &KerasEngine::repack)
       .def("sync", &KerasEngine::sync, py::call_guard<py::gil_scoped_release>())
       .def("set_peer", &KerasEngine::set_peer, py::arg("peer").none(true), py::keep_alive<1, 2>())
+      .def("set_comm", &KerasEngine::set_comm, py::arg("comm").none(true), py::keep_alive<1, 2>())
       .def("set_force_collectives", &KerasEngine::set_force_collectives)
+      .def("set_merged", &KerasEngine::set_merged)
+      .def("set_overlap", &KerasEngine::set_overlap)
+      .def("set_bucket_padding", &KerasEngine::set_bucket_padding)
       .def("set_external_batch", &KerasEngine::set_external_batch)
+      .def_property_readonly("graph_mode", &KerasEngine::graph_mode)
+      .def_property_readonly("merged", &KerasEngine::merged)
+      .def_property_readonly("overlap", &KerasEngine::overlap)
       .def_property_readonly("world_size", &KerasEngine::world_size)
       .def_property_readonly("reducer_active", &KerasEngine::reducer_active)
       .def_property_readonly("peer_active", &KerasEngine::peer_active)
@@ -421,6 +429,44 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("x_ptr", &KerasEngine::x_ptr)
       .def_property_readonly("y_ptr", &KerasEngine::y_ptr)
       .def_property_readonly("counter_ptr", &KerasEngine::counter_ptr);
+
+  // ---------------------------------------------------------------- fused Chainer-MLP engine
+  m.def("mlp_workspace_bytes", &MlpEngine::workspace_bytes);
+  m.attr("MLP_NUM_PARAMS") = MlpLayout::total;
+  py::class_<MlpEngine>(m, "MlpEngine")
+      .def(py::init([](int B, uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t st, uintptr_t ws,
+                       size_t wsb, Comm* comm, uint64_t seed, uintptr_t lr, uintptr_t metrics, float b1, float b2,
+                       float eps, float wd, bool eps_hat) {
+             return new MlpEngine(B, p, g, mm, v, st, ws, wsb, comm, seed, lr, metrics, b1, b2, eps, wd, eps_hat);
+           }),
+           py::arg("batch"), py::arg("params"), py::arg("grads"), py::arg("m"), py::arg("v"), py::arg("adam_state"),
+           py::arg("workspace"), py::arg("workspace_bytes"), py::arg("comm").none(true), py::arg("seed"),
+           py::arg("lr_dev"), py::arg("metrics_dev"), py::arg("b1"), py::arg("b2"), py::arg("eps"),
+           py::arg("weight_decay"), py::arg("eps_hat"), py::keep_alive<1, 10>())
+      .def("step", &MlpEngine::step)
+      .def("capture", &MlpEngine::capture, py::arg("mode") = 1, py::arg("steps_per_graph") = 1)
+      .def("replay", &MlpEngine::replay)
+      .def("uncapture", &MlpEngine::uncapture)
+      .def("warm_graphs", &MlpEngine::warm_graphs)
+      .def("sync", &MlpEngine::sync, py::call_guard<py::gil_scoped_release>())
+      .def("set_peer", &MlpEngine::set_peer, py::arg("peer").none(true), py::keep_alive<1, 2>())
+      .def("set_comm", &MlpEngine::set_comm, py::arg("comm").none(true), py::keep_alive<1, 2>())
+      .def("set_force_collectives", &MlpEngine::set_force_collectives)
+      .def("set_merged", &MlpEngine::set_merged)
+      .def("set_overlap", &MlpEngine::set_overlap)
+      .def("set_bucket_padding", &MlpEngine::set_bucket_padding)
+      .def("set_external_batch", &MlpEngine::set_external_batch)
+      .def_property_readonly("graph_mode", &MlpEngine::graph_mode)
+      .def_property_readonly("merged", &MlpEngine::merged)
+      .def_property_readonly("overlap", &MlpEngine::overlap)
+      .def_property_readonly("world_size", &MlpEngine::world_size)
+      .def_property_readonly("reducer_active", &MlpEngine::reducer_active)
+      .def_property_readonly("peer_active", &MlpEngine::peer_active)
+      .def_property_readonly("captured", &MlpEngine::captured)
+      .def_property_readonly("stream", &MlpEngine::stream)
+      .def_property_readonly("x_ptr", &MlpEngine::x_ptr)
+      .def_property_readonly("y_ptr", &MlpEngine::y_ptr)
+      .def_property_readonly("counter_ptr", &MlpEngine::counter_ptr);
 
   // ---------------------------------------------------------------- fused MNIST engine
   m.def("mnist_workspace_bytes", &MnistLayout::workspace_bytes);

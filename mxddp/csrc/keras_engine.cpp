@@ -77,6 +77,7 @@ KerasEngine::KerasEngine(int batch, uintptr_t params, uintptr_t grads, uintptr_t
   f_.wd = weight_decay;
   f_.eps_hat = eps_hat ? 1 : 0;
   MX_HIP_CHECK(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
+  graphs_.set_stream(s_);
   MX_HIP_CHECK(hipMemsetAsync(f_.counter, 0, 16, s_));
   synth_templates(const_cast<float*>(f_.tmpl), 10, 784, seed_ ^ 0x5eedull, s_);  // identical on every rank
   // one bucket: the whole 373 KB gradient, all-reduced in order on the compute stream
@@ -125,75 +126,25 @@ void KerasEngine::launch_step() {
 
 void KerasEngine::step() { launch_step(); }
 
-hipGraphExec_t KerasEngine::capture_fn(int steps, hipGraph_t* g) {
-  MX_HIP_CHECK(hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal));
-  try {
-    for (int i = 0; i < steps; ++i) launch_step();
-  } catch (...) {
-    hipGraph_t tmp = nullptr;
-    hipStreamEndCapture(s_, &tmp);
-    if (tmp) hipGraphDestroy(tmp);
-    throw;
-  }
-  MX_HIP_CHECK(hipStreamEndCapture(s_, g));
-  hipGraphExec_t exec = nullptr;
-  MX_HIP_CHECK(hipGraphInstantiate(&exec, *g, nullptr, nullptr, 0));
-  MX_HIP_CHECK(hipGraphUpload(exec, s_));
-  return exec;
+void KerasEngine::capture(int mode, int steps_per_graph) {
+  if (mode == 0 || graphs_.captured()) return;
+  graphs_.capture([this] { launch_step(); }, steps_per_graph);
 }
 
-void KerasEngine::capture(int steps_per_graph) {
-  if (exec_) return;
-  MX_HIP_CHECK(hipStreamSynchronize(s_));
-  steps_per_graph_ = steps_per_graph < 1 ? 1 : steps_per_graph;
-  exec_ = capture_fn(steps_per_graph_, &graph_);
-  int k = 1;
-  while (2 * k < steps_per_graph_) k *= 2;
-  for (; k >= 1 && steps_per_graph_ > 1; k /= 2) {  // remainder graphs 2^k steps, largest first
-    hipGraph_t gr = nullptr;
-    rem_exec_.emplace_back(k, capture_fn(k, &gr));
-    rem_graph_.push_back(gr);
-  }
-}
+void KerasEngine::replay(int n) { graphs_.replay(n, [this] { launch_step(); }); }
 
 void KerasEngine::uncapture() {
   if (s_) MX_HIP_CHECK(hipStreamSynchronize(s_));
-  if (exec_) hipGraphExecDestroy(exec_);
-  if (graph_) hipGraphDestroy(graph_);
-  exec_ = nullptr;
-  graph_ = nullptr;
-  for (auto& e : rem_exec_) hipGraphExecDestroy(e.second);
-  for (auto gr : rem_graph_) hipGraphDestroy(gr);
-  rem_exec_.clear();
-  rem_graph_.clear();
+  graphs_.clear();
 }
 
-void KerasEngine::replay(int n) {
-  if (!exec_) {
-    for (int i = 0; i < n; ++i) launch_step();
-    return;
-  }
-  const int full = n / steps_per_graph_;
-  n -= full * steps_per_graph_;
-  for (int i = 0; i < full; ++i) MX_HIP_CHECK(hipGraphLaunch(exec_, s_));
-  for (const auto& e : rem_exec_)
-    if (n >= e.first) {
-      MX_HIP_CHECK(hipGraphLaunch(e.second, s_));
-      n -= e.first;
-    }
-  for (; n > 0; --n) launch_step();
-}
-
-int KerasEngine::warm_graphs() {
-  if (!exec_) return 0;
-  int steps = steps_per_graph_;
-  MX_HIP_CHECK(hipGraphLaunch(exec_, s_));
-  for (const auto& e : rem_exec_) {
-    MX_HIP_CHECK(hipGraphLaunch(e.second, s_));
-    steps += e.first;
-  }
-  MX_HIP_CHECK(hipStreamSynchronize(s_));
-  return steps;
+void KerasEngine::set_comm(Comm* c) {
+  if (c == comm_) return;
+  MX_CHECK(!c || !comm_ || (c->rank() == comm_->rank() && c->world_size() == comm_->world_size()),
+           "set_comm: the communicator must have this engine's rank and world size");
+  uncapture();
+  comm_ = c;
+  reducer_->set_comm(c);
 }
 
 void KerasEngine::set_peer(PeerComm* p) {

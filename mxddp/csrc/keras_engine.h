@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "comm.h"
+#include "graph_runner.h"
 #include "keras_kernels.h"
 #include "reducer.h"
 
@@ -29,20 +30,33 @@ class KerasEngine {
 
   static size_t workspace_bytes(int B);
   void step();                           // one eager step on stream()
-  void capture(int steps_per_graph);     // whole step(s), collectives included, in one graph
+  // mode 1: whole step(s), collectives included, in one graph per steps_per_graph steps;
+  // mode 0: eager launches
+  void capture(int mode, int steps_per_graph);
   void replay(int n);                    // n steps (graphs once captured)
   void uncapture();
-  int warm_graphs();
+  int warm_graphs() { return graphs_.warm(); }
   void repack();                         // after parameters changed outside the engine
   void sync();
   // gradient transport at world size > 1: RCCL (default) or the peer transport; drops graphs
   void set_peer(PeerComm* p);
+  void set_comm(Comm* c);  // another RCCL communicator over the same ranks (comm.py variants)
   void set_force_collectives(bool on);
+  // the step all-reduces its 373 KB gradient as ONE bucket between the finalize and Adam: the
+  // bucket strategies of the other engines ("one" is the only one) and the all-reduce padding
+  void set_merged(bool) {}
+  void set_overlap(bool) {}
+  bool merged() const { return true; }
+  bool overlap() const { return false; }
+  void set_bucket_padding(size_t capacity, size_t multiple) {
+    reducer_->set_padding(KerasLayout::total, capacity, multiple);
+  }
   void set_external_batch(bool on) { external_ = on; }
   int world_size() const;
   bool reducer_active() const { return reducer_->active(); }
   bool peer_active() const { return reducer_->peer() != nullptr; }
-  bool captured() const { return exec_ != nullptr; }
+  bool captured() const { return graphs_.captured(); }
+  int graph_mode() const { return graphs_.captured() ? 1 : 0; }
   uintptr_t stream() const { return reinterpret_cast<uintptr_t>(s_); }
   uintptr_t x_ptr() const { return reinterpret_cast<uintptr_t>(f_.x); }
   uintptr_t y_ptr() const { return reinterpret_cast<uintptr_t>(f_.y); }
@@ -51,7 +65,6 @@ class KerasEngine {
  private:
   void launch_step();
   KerasFused args() const;
-  hipGraphExec_t capture_fn(int steps, hipGraph_t* g);
   int B_;
   KerasFused f_{};
   Comm* comm_;
@@ -59,11 +72,7 @@ class KerasEngine {
   bool external_ = false;
   hipStream_t s_ = nullptr;
   std::unique_ptr<Reducer> reducer_;
-  int steps_per_graph_ = 1;
-  hipGraph_t graph_ = nullptr;
-  hipGraphExec_t exec_ = nullptr;
-  std::vector<std::pair<int, hipGraphExec_t>> rem_exec_;
-  std::vector<hipGraph_t> rem_graph_;
+  GraphRunner graphs_;
 };
 
 }  // namespace mx

@@ -1,0 +1,521 @@
+// Fused gfx950 kernels for the Chainer MLP training step (fp32 in / fp32 MFMA accumulate).
+//
+// Reference: chainer/train_mnist.py:13-26 (l1 784->1000, l2 1000->1000, l3 1000->10, ReLU),
+// :69 (Adam, alpha 1e-3, eps 1e-8 in Chainer's epsilon-hat form), L.Classifier softmax cross
+// entropy + accuracy; ParallelUpdater at chainer/train_mnist_gpu.py:87-93.
+//
+// One step = 5 launches (world size 1; with gradient collectives K4 / K5 write g and the flat
+// Adam of ops_optim.hip runs after the all-reduce):
+//   K1  [on-device batch] + l1 forward + bias + ReLU          (split-K over 4 waves, MFMA)
+//   K2  l2 forward + bias + ReLU
+//   K3  l3 forward (logits) + softmax CE + accuracy + dlogits + dh2 = (dlogits W3) * (h2 > 0)
+//   K4  per (256-row slice of W2, 16-column tile): dW2 tile (MFMA) + Adam of the tile, the l2
+//       data-gradient partial of the slice (MFMA, plain stores, 4 planes); db2; l3 grads + Adam
+//                                                                        -> bucket 0 ready
+//   K5  per (16 rows of W1, 112 columns): dh1 = sum of the 4 planes, ReLU-masked; dW1 tile
+//       (MFMA) + Adam; db1                                               -> bucket 1 ready
+// Every block owns the weights it updates, so old values (needed by K4's data gradient) are
+// read before the same block writes the new ones -- no cross-block hazard, no extra launch.
+// All cross-block sums are fixed-order (4 data-gradient planes, per-tile loss slots): a step is
+// bitwise reproducible.  The Adam step count lives on the device: K4 / K5 read state[0] + 1, K5
+// publishes it in state[1], the next step's K1 commits it to state[0] (ops_optim.hip adam_k).
+//
+// MFMA = v_mfma_f32_16x16x4_f32 (lane l: A[l&15][k=l>>4], B[k=l>>4][l&15]; C row = 4*(l>>4) +
+// reg, col = l&15).  Where operands are read as float4 along K, the K order inside a 16-wide
+// chunk is permuted (k = 16c + 4g + j for lane group g, register j) identically for A and B.
+#include "common.h"
+#include "mlp_kernels.h"
+#include "rng.h"
+
+namespace mx {
+namespace mlp {
+namespace {
+
+using L = MlpLayout;
+constexpr int kNT = (L::kH + 15) / 16;  // 63 column tiles of the hidden layers (the last half used)
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+struct AdamC {
+  float step_size, bc2s, e, b1, b2, wd;
+};
+// the constants of ops_optim.hip adam_k for step t = completed steps + 1
+__device__ __forceinline__ AdamC adam_consts(const MlpFused& f) {
+  const int t = __hip_atomic_load(f.adam_state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  const float bc1 = 1.f - powf(f.b1, (float)t), bc2 = 1.f - powf(f.b2, (float)t);
+  AdamC c;
+  c.step_size = *f.lr / bc1;
+  c.bc2s = sqrtf(bc2);
+  c.e = f.eps_hat ? f.eps / c.bc2s : f.eps;
+  c.b1 = f.b1;
+  c.b2 = f.b2;
+  c.wd = f.wd;
+  return c;
+}
+// adam_k's update of one parameter (same operation order: identical results)
+__device__ __forceinline__ void adam_upd(float& p, float& m, float& v, float grad, const AdamC& c) {
+  const float gg = grad + c.wd * p;
+  m = c.b1 * m + (1.f - c.b1) * gg;
+  v = c.b2 * v + (1.f - c.b2) * gg * gg;
+  p -= c.step_size * m / (sqrtf(v) / c.bc2s + c.e);
+}
+// one parameter's gradient: Adam in place (fused) or the gradient into g (all-reduced next)
+__device__ __forceinline__ void apply_grad(const MlpFused& f, size_t e, float p_old, float grad, const AdamC& c) {
+  if (f.fused_adam) {
+    float p = p_old, m = f.m[e], v = f.v[e];
+    adam_upd(p, m, v, grad, c);
+    f.m[e] = m;
+    f.v[e] = v;
+    f.p[e] = p;
+  } else {
+    f.g[e] = grad;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K1 / K2: out = ReLU(in W^T + b) for in [B][kIn] (x, pitch 784, or h1, pitch 1024) and W
+// [1000][kIn].  Block = (16-row M-tile, 16-column N-tile): (B/16) x 63 blocks; the 4 waves split
+// K into 16-wide chunks (chunk c -> wave c % 4), every operand float4 issued up front, two
+// accumulator chains per wave; the 4 partials are summed in LDS in a fixed order.  The N-tiles
+// of one M-tile are spread over the XCDs while the blocks sharing W rows sit on one (xcd_remap).
+// K1 (kSynth) forms its A operand from the on-device generator (ops_data.hip synth_batch's
+// recipe: template of the label + uniform noise) instead of loading x, and the blocks of
+// N-tile 0 publish x / y for the backward.  K2's h1 columns 1000.. are zero, so its last chunk
+// needs no bounds (the W2 values read past a row's end are finite parameters times zero).
+template <int kIn, bool kSynth>
+__global__ __launch_bounds__(256) void fwd_kernel(MlpFused f) {
+  constexpr int kCh = (kIn + 15) / 16, kPerW = (kCh + 3) / 4, kAP = kIn == L::kIn ? L::kIn : L::kHP;
+  static_assert(!kSynth || kIn == L::kIn, "the generator feeds l1");
+  __shared__ float red[4][16][17];
+  const float* W = f.p + (kIn == L::kIn ? L::w1 : L::w2);
+  const float* bias = f.p + (kIn == L::kIn ? L::b1 : L::b2);
+  float* out = kIn == L::kIn ? f.h1 : f.h2;
+  const int MT = f.B / 16;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int nt = bid / MT, mt = bid - nt * MT;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  if (blockIdx.x == 0 && tid == 0) {
+    if (kIn == L::kIn) f.adam_state[0] = f.adam_state[1];  // commit the previous step's Adam count
+    else if (f.synth) *f.counter += 1;                      // K1 consumed the batch counter
+  }
+  const int row = 16 * mt + m, n = min(16 * nt + m, L::kH - 1);
+  const float* Ap = (kIn == L::kIn ? f.x : f.h1) + (size_t)row * kAP + 4 * g;
+  const float* Bp = W + (size_t)n * kIn + 4 * g;
+  float4 av[kPerW], bv[kPerW];
+  uint2 key = make_uint2(0, 0);
+  uint32_t ctr = 0;
+  int label = 0;
+  if constexpr (kSynth) {
+    key = synth_key(f.seed);
+    ctr = (uint32_t)*f.counter;
+    label = synth_label(ctr, row, L::kNC, key);
+  }
+#pragma unroll
+  for (int i = 0; i < kPerW; ++i) {
+    const int c = min(w + 4 * i, kCh - 1);  // clamped: the chunk is masked below
+    bv[i] = *reinterpret_cast<const float4*>(Bp + 16 * c);
+    if constexpr (kSynth)
+      av[i] = *reinterpret_cast<const float4*>(f.tmpl + label * L::kIn + 16 * c + 4 * g);
+    else
+      av[i] = *reinterpret_cast<const float4*>(Ap + 16 * c);
+  }
+  if constexpr (kSynth) {
+#pragma unroll
+    for (int i = 0; i < kPerW; ++i) {
+      const int c = min(w + 4 * i, kCh - 1), d = 16 * c + 4 * g;
+      const uint4 r = synth_noise4(ctr, row, d, key);
+      const float4 t = av[i];
+      av[i] = make_float4(0.5f * t.x + 0.5f * u01(r.x), 0.5f * t.y + 0.5f * u01(r.y), 0.5f * t.z + 0.5f * u01(r.z),
+                          0.5f * t.w + 0.5f * u01(r.w));
+      if (nt == 0 && w + 4 * i < kCh) *reinterpret_cast<float4*>(f.x + (size_t)row * L::kIn + d) = av[i];
+    }
+    if (nt == 0 && w == 0 && g == 0) f.y[row] = label;
+  }
+  // every operand load issued before the first MFMA (left alone, the scheduler interleaves each
+  // load with its MFMAs and the wave waits on L2 once per chunk)
+  __builtin_amdgcn_sched_barrier(0);
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int i = 0; i < kPerW; ++i) {
+    const bool ok = w + 4 * i < kCh;
+    const float4 a = ok ? av[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    acc[0] = mfma4(a.x, bv[i].x, acc[0]);
+    acc[1] = mfma4(a.y, bv[i].y, acc[1]);
+    acc[0] = mfma4(a.z, bv[i].z, acc[0]);
+    acc[1] = mfma4(a.w, bv[i].w, acc[1]);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[w][4 * g + j][m] = acc[0][j] + acc[1][j];
+  __syncthreads();
+  const int r = tid >> 4, col = tid & 15, no = 16 * nt + col;
+  const float v = ((red[0][r][col] + red[1][r][col]) + (red[2][r][col] + red[3][r][col])) + bias[min(no, L::kH - 1)];
+  float* o = out + (size_t)(16 * mt + r) * L::kHP;
+  o[no] = no < L::kH ? fmaxf(v, 0.f) : 0.f;
+  if (nt == kNT - 1) o[16 * kNT + col] = 0.f;  // columns 1008 .. 1023 of the padded row
+}
+
+// ------------------------------------------------------------------------------------------
+// K3: head.  Block = (16-row M-tile, 128-column group of h2): (B/16) x 8 blocks.  Every block
+// computes the 16 rows' logits (K = 1000 split over the 4 waves, MFMA with W3's 10 rows padded to
+// 16), softmax cross entropy, accuracy and dlogits = (softmax - onehot) / B, then its slice of
+// dh2 = (dlogits W3) * (h2 > 0) (K = 10, VALU, W3 columns in LDS).  Column group 0 publishes
+// dlogits and the tile's loss / correct sums (fixed order) for K4.
+__global__ __launch_bounds__(256) void head_kernel(MlpFused f) {
+  constexpr int kCh = (L::kH + 15) / 16, kPerW = (kCh + 3) / 4;
+  __shared__ float red[4][16][17];
+  __shared__ float dls[16][17];
+  __shared__ float w3s[L::kNC][128];
+  __shared__ float lc[2][16];
+  const int mt = blockIdx.x >> 3, cg = blockIdx.x & 7;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  const int row = 16 * mt + m;
+  const float* Ap = f.h2 + (size_t)row * L::kHP + 4 * g;
+  const float* Bp = f.p + L::w3 + (size_t)min(m, L::kNC - 1) * L::kH + 4 * g;
+  const float bm = m < L::kNC ? 1.f : 0.f;
+  float4 av[kPerW], bv[kPerW];
+#pragma unroll
+  for (int i = 0; i < kPerW; ++i) {
+    const int c = min(w + 4 * i, kCh - 1);
+    av[i] = *reinterpret_cast<const float4*>(Ap + 16 * c);
+    bv[i] = *reinterpret_cast<const float4*>(Bp + 16 * c);
+  }
+  float w3v[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {  // W3 columns of this group: [10][128] = 1280 = 5 x 256
+    const int i = tid + 256 * k, c = i >> 7, j = 128 * cg + (i & 127);
+    w3v[k] = f.p[L::w3 + c * L::kH + min(j, L::kH - 1)] * (j < L::kH ? 1.f : 0.f);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // all operand loads in flight first (see fwd_kernel)
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int i = 0; i < kPerW; ++i) {
+    const float4 a = w + 4 * i < kCh ? av[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 b = bv[i];
+    acc[0] = mfma4(a.x, b.x * bm, acc[0]);
+    acc[1] = mfma4(a.y, b.y * bm, acc[1]);
+    acc[0] = mfma4(a.z, b.z * bm, acc[0]);
+    acc[1] = mfma4(a.w, b.w * bm, acc[1]);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[w][4 * g + j][m] = acc[0][j] + acc[1][j];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int i = tid + 256 * k;
+    w3s[i >> 7][i & 127] = w3v[k];
+  }
+  __syncthreads();
+  if (tid < 16) {  // softmax cross entropy of row tid of the tile
+    float l[L::kNC];
+#pragma unroll
+    for (int c = 0; c < L::kNC; ++c)
+      l[c] = ((red[0][tid][c] + red[1][tid][c]) + (red[2][tid][c] + red[3][tid][c])) + f.p[L::b3 + c];
+    const int y = f.y[16 * mt + tid];
+    float mx = l[0];
+    int am = 0;
+#pragma unroll
+    for (int c = 1; c < L::kNC; ++c)
+      if (l[c] > mx) { mx = l[c]; am = c; }
+    float se = 0.f;
+#pragma unroll
+    for (int c = 0; c < L::kNC; ++c) se += __expf(l[c] - mx);
+    const float lse = mx + __logf(se);
+    float ly = 0.f;
+#pragma unroll
+    for (int c = 0; c < L::kNC; ++c) ly = c == y ? l[c] : ly;
+    lc[0][tid] = lse - ly;
+    lc[1][tid] = am == y ? 1.f : 0.f;
+    const float inv = 1.f / (float)f.B;
+#pragma unroll
+    for (int c = 0; c < L::kNC; ++c) dls[tid][c] = (__expf(l[c] - lse) - (c == y ? 1.f : 0.f)) * inv;
+#pragma unroll
+    for (int c = L::kNC; c < 16; ++c) dls[tid][c] = 0.f;
+  }
+  __syncthreads();
+  if (cg == 0) {
+    f.dl[(size_t)(16 * mt + (tid >> 4)) * 16 + (tid & 15)] = dls[tid >> 4][tid & 15];
+    if (tid < 2) {
+      float s = 0.f;
+      for (int i = 0; i < 16; ++i) s += lc[tid][i];
+      f.lsum[2 * mt + tid] = s;
+    }
+  }
+  // dh2 of the 16 rows x 128 columns: thread = one column, 8 rows
+  const int jl = tid & 127, j = 128 * cg + jl, r0 = (tid >> 7) * 8;
+  float hv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) hv[k] = f.h2[(size_t)(16 * mt + r0 + k) * L::kHP + j];
+  float wc[L::kNC];
+#pragma unroll
+  for (int c = 0; c < L::kNC; ++c) wc[c] = w3s[c][jl];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < L::kNC; ++c) s = fmaf(dls[r0 + k][c], wc[c], s);
+    f.dh2[(size_t)(16 * mt + r0 + k) * L::kHP + j] = hv[k] > 0.f ? s : 0.f;  // h2 pad columns are 0
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K4: l2 / l3 backward.  Blocks [0, 252): (row slice ri of W2: rows 256 ri .. +255, column tile
+// jt: W2 columns 16 jt .. +15).  The slice's dh2 columns [B][256] (pitch 260: the data-gradient
+// A reads are bank-conflict free), the W2 tile [256][16] (OLD weights) and h1's 16 columns are
+// staged in LDS, then
+//   dh1 partial [B][16] = dh2[:, slice] . W2[slice, tile]  (MFMA, K = 256) -> plane ri (plain stores)
+//   dW2 tile [256][16]  = dh2[:, slice]^T . h1[:, tile]    (MFMA, K = B)   -> Adam / g
+//   db2 (tile 0 of each slice)                                              -> Adam / g
+// Blocks [252, 256): W3 columns 250 q .. +249 (VALU, K = B) and b3 + the step's metrics (q = 0).
+constexpr int kRS = 256, kDhP = 260, kK4A = 4 * kNT;
+__global__ __launch_bounds__(256) void bwd2_kernel(MlpFused f) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int B = f.B;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  const AdamC ac = adam_consts(f);
+  if ((int)blockIdx.x >= kK4A) {
+    const int q = blockIdx.x - kK4A;
+    float* dls = sm;  // [B][16]
+    for (int i = tid; i < B * 16; i += 256) dls[i] = f.dl[i];
+    __syncthreads();
+    if (tid < 250) {
+      const int j = 250 * q + tid;
+      float acc[L::kNC];
+#pragma unroll
+      for (int c = 0; c < L::kNC; ++c) acc[c] = 0.f;
+      for (int b0 = 0; b0 < B; b0 += 16) {
+        float hv[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) hv[k] = f.h2[(size_t)(b0 + k) * L::kHP + j];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+#pragma unroll
+          for (int c = 0; c < L::kNC; ++c) acc[c] = fmaf(dls[(b0 + k) * 16 + c], hv[k], acc[c]);
+      }
+#pragma unroll
+      for (int c = 0; c < L::kNC; ++c) {
+        const size_t e = L::w3 + (size_t)c * L::kH + j;
+        apply_grad(f, e, f.p[e], acc[c], ac);
+      }
+    }
+    if (q == 0 && tid < L::kNC) {
+      float s = 0.f;
+      for (int b = 0; b < B; ++b) s += dls[b * 16 + tid];
+      const size_t e = L::b3 + tid;
+      apply_grad(f, e, f.p[e], s, ac);
+    }
+    if (q == 0 && tid == 0 && f.metrics) {
+      float ls = 0.f, cs = 0.f;
+      for (int t = 0; t < B / 16; ++t) {
+        ls += f.lsum[2 * t];
+        cs += f.lsum[2 * t + 1];
+      }
+      atomicAdd(f.metrics, ls);
+      atomicAdd(f.metrics + 1, cs);
+    }
+    return;
+  }
+  const int bid = xcd_remap(blockIdx.x, kK4A);  // the tiles of one row slice share an XCD's L2
+  const int ri = bid / kNT, jt = bid - ri * kNT;
+  const int i0 = kRS * ri;
+  float* dh2s = sm;                 // [B][260]
+  float* w2s = dh2s + B * kDhP;     // [256][16]
+  float* h1s = w2s + kRS * 16;      // [B][16]
+  for (int k = tid; k < B * 64; k += 256) {  // dh2 columns i0 .. i0 + 255 (pad columns are 0)
+    const int b = k >> 6, c4 = k & 63;
+    *reinterpret_cast<float4*>(dh2s + b * kDhP + 4 * c4) =
+        *reinterpret_cast<const float4*>(f.dh2 + (size_t)b * L::kHP + i0 + 4 * c4);
+  }
+  {  // W2 tile: thread = row i0 + tid, 16 columns (zero outside the 1000 x 1000 matrix)
+    const int i = min(i0 + tid, L::kH - 1);
+    const float4* src = reinterpret_cast<const float4*>(f.p + L::w2 + (size_t)i * L::kH + 16 * jt);
+    float4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = src[q];
+    const bool rok = i0 + tid < L::kH;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool cok = rok && 16 * jt + 4 * q < L::kH;  // 1000 % 4 == 0: whole float4s
+      *reinterpret_cast<float4*>(w2s + tid * 16 + 4 * q) = cok ? v[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  for (int k = tid; k < B * 4; k += 256) {
+    const int b = k >> 2, c4 = k & 3;
+    *reinterpret_cast<float4*>(h1s + b * 16 + 4 * c4) =
+        *reinterpret_cast<const float4*>(f.h1 + (size_t)b * L::kHP + 16 * jt + 4 * c4);
+  }
+  __syncthreads();
+  // dh1 partial: M = batch (wave w: M-tiles w, w+4, ..), N = 16 columns, K = the 256 rows
+  for (int mt = w; mt < B / 16; mt += 4) {
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    const float* a = dh2s + (16 * mt + m) * kDhP + g;
+    const float* bb = w2s + g * 16 + m;
+#pragma unroll 16
+    for (int s = 0; s < kRS / 4; ++s) acc[s & 1] = mfma4(a[4 * s], bb[64 * s], acc[s & 1]);
+    float* dst = f.dh1p + ((size_t)ri * B + 16 * mt + 4 * g) * L::kHP + 16 * jt + m;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dst[(size_t)r * L::kHP] = acc[0][r] + acc[1][r];
+  }
+  // dW2 tile: M = the 256 rows (wave w: tiles w, w+4, w+8, w+12), N = 16 columns, K = batch
+  f32x4 dw[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dw[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < B / 4; ++s) {
+    const float bvv = h1s[(4 * s + g) * 16 + m];
+    const float* a = dh2s + (4 * s + g) * kDhP + m;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dw[q] = mfma4(a[16 * (w + 4 * q)], bvv, dw[q]);
+  }
+  const int j = 16 * jt + m;
+  if (j < L::kH) {
+    float mv[4][4], vv[4][4];
+    if (f.fused_adam) {  // every moment load in flight before the first update
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = min(i0 + 16 * (w + 4 * q) + 4 * g + r, L::kH - 1);
+          const size_t e = L::w2 + (size_t)i * L::kH + j;
+          mv[q][r] = f.m[e];
+          vv[q][r] = f.v[e];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int il = 16 * (w + 4 * q) + 4 * g + r, i = i0 + il;
+        if (i < L::kH) {
+          const size_t e = L::w2 + (size_t)i * L::kH + j;
+          if (f.fused_adam) {
+            float p = w2s[il * 16 + m];
+            adam_upd(p, mv[q][r], vv[q][r], dw[q][r], ac);
+            f.m[e] = mv[q][r];
+            f.v[e] = vv[q][r];
+            f.p[e] = p;
+          } else {
+            f.g[e] = dw[q][r];
+          }
+        }
+      }
+  }
+  if (jt == 0 && i0 + tid < L::kH) {  // db2 of the slice's rows: fixed-order column sums
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < B; b += 4)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s[k] += dh2s[(b + k) * kDhP + tid];
+    const size_t e = L::b2 + i0 + tid;
+    apply_grad(f, e, f.p[e], (s[0] + s[1]) + (s[2] + s[3]), ac);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K5: l1 backward.  Block = (16 rows of W1 = hidden units 16 nt .., 112 input columns 112 kg ..):
+// 63 x 7 blocks.  dh1 [B][16] = sum of K4's 4 planes (fixed order), masked by h1 > 0, and x's
+// 112 columns are staged in LDS (pitch 112: lane groups 16 banks apart); wave w computes the
+// 16 x 16 dW1 tiles kt = w, w + 4 (M = rows, N = columns, K = batch) and applies Adam to them;
+// db1 in the column-group-0 blocks.  Block 0 publishes the Adam step count.
+__global__ __launch_bounds__(256) void bwd1_kernel(MlpFused f) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int B = f.B;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  const AdamC ac = adam_consts(f);
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int nt = bid / 7, kg = bid - nt * 7;
+  float* dh1s = sm;            // [B][16]
+  float* xs = dh1s + B * 16;   // [B][112]
+  for (int k = tid; k < B * 16; k += 256) {
+    const int b = k >> 4, n = 16 * nt + (k & 15);
+    const size_t o = (size_t)b * L::kHP + n;
+    const size_t pl = (size_t)B * L::kHP;
+    const float s = (f.dh1p[o] + f.dh1p[pl + o]) + (f.dh1p[2 * pl + o] + f.dh1p[3 * pl + o]);
+    dh1s[k] = f.h1[o] > 0.f ? s : 0.f;  // h1 pad columns are 0: those planes' garbage is dropped
+  }
+  for (int k = tid; k < B * 28; k += 256) {
+    const int b = k / 28, c4 = k - 28 * b;
+    *reinterpret_cast<float4*>(xs + b * 112 + 4 * c4) =
+        *reinterpret_cast<const float4*>(f.x + (size_t)b * L::kIn + 112 * kg + 4 * c4);
+  }
+  if (blockIdx.x == 0 && tid == 0 && f.fused_adam)
+    __hip_atomic_store(f.adam_state + 1, __hip_atomic_load(f.adam_state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  for (int kt = w; kt < 7; kt += 4) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < B / 4; ++s) acc = mfma4(dh1s[(4 * s + g) * 16 + m], xs[(4 * s + g) * 112 + 16 * kt + m], acc);
+    const int k = 112 * kg + 16 * kt + m;
+    float pv[4], mv[4], vv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = min(16 * nt + 4 * g + r, L::kH - 1);
+      const size_t e = L::w1 + (size_t)n * L::kIn + k;
+      pv[r] = f.p[e];
+      if (f.fused_adam) {
+        mv[r] = f.m[e];
+        vv[r] = f.v[e];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = 16 * nt + 4 * g + r;
+      if (n < L::kH) {
+        const size_t e = L::w1 + (size_t)n * L::kIn + k;
+        if (f.fused_adam) {
+          adam_upd(pv[r], mv[r], vv[r], acc[r], ac);
+          f.m[e] = mv[r];
+          f.v[e] = vv[r];
+          f.p[e] = pv[r];
+        } else {
+          f.g[e] = acc[r];
+        }
+      }
+    }
+  }
+  if (kg == 0 && tid < 16 && 16 * nt + tid < L::kH) {
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < B; b += 4)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s[k] += dh1s[(b + k) * 16 + tid];
+    const size_t e = L::b1 + 16 * nt + tid;
+    apply_grad(f, e, f.p[e], (s[0] + s[1]) + (s[2] + s[3]), ac);
+  }
+}
+
+size_t bwd2_lds(int B) { return sizeof(float) * ((size_t)B * kDhP + kRS * 16 + (size_t)B * 16); }
+size_t bwd1_lds(int B) { return sizeof(float) * ((size_t)B * 16 + (size_t)B * 112); }
+
+}  // namespace
+}  // namespace mlp
+
+using namespace mlp;
+
+static void check(const MlpFused& f) {
+  MX_CHECK(f.B % 16 == 0 && f.B >= 16 && f.B <= 128, "fused MLP engine needs batch % 16 == 0 and 16 <= B <= 128");
+}
+
+void mlp_fused_forward(const MlpFused& f, hipStream_t st) {
+  check(f);
+  const dim3 grid((f.B / 16) * kNT);
+  if (f.synth)
+    MX_LAUNCH((fwd_kernel<MlpLayout::kIn, true>), grid, dim3(256), 0, st, f);
+  else
+    MX_LAUNCH((fwd_kernel<MlpLayout::kIn, false>), grid, dim3(256), 0, st, f);
+  MX_LAUNCH((fwd_kernel<MlpLayout::kH, false>), grid, dim3(256), 0, st, f);
+  MX_LAUNCH(head_kernel, dim3((f.B / 16) * 8), dim3(256), 0, st, f);
+}
+
+void mlp_fused_backward2(const MlpFused& f, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    MX_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(bwd2_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  MX_LAUNCH(bwd2_kernel, dim3(kK4A + 4), dim3(256), bwd2_lds(f.B), st, f);
+}
+
+void mlp_fused_backward1(const MlpFused& f, hipStream_t st) {
+  MX_LAUNCH(bwd1_kernel, dim3(kNT * 7), dim3(256), bwd1_lds(f.B), st, f);
+}
+
+}  // namespace mx

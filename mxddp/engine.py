@@ -13,11 +13,11 @@ The parameters are one flat fp32 buffer in MnistCNN ``state_dict`` order, so
 from __future__ import annotations
 
 import os
-import time
 
 import torch
 
 from . import native
+from .fused import FusedTrainerBase
 from .models.mnist_cnn import MnistCNN
 
 _LAYOUT = [  # (name, shape) in state_dict order == flat offsets of MnistLayout (mnist_engine.h)
@@ -28,7 +28,10 @@ _LAYOUT = [  # (name, shape) in state_dict order == flat offsets of MnistLayout 
 ]
 
 
-class FusedMnistTrainer:
+class FusedMnistTrainer(FusedTrainerBase):
+    LAYOUT = _LAYOUT
+    MODEL = MnistCNN
+
     def __init__(self, batch: int = 64, device: torch.device | int = 0, comm=None, seed: int = 1, lr: float = 0.1,
                  momentum: float = 0.9, weight_decay: float = 1e-4, variant: int = 1, use_graph: bool = True,
                  init_model: MnistCNN | None = None, graph_mode: int | None = None,
@@ -36,229 +39,32 @@ class FusedMnistTrainer:
                  peer=None, rccl_variants=None):
         C = native()
         self.C = C
-        self.graph_mode = graph_mode
-        self.steps_per_graph = steps_per_graph
-        self._external = False
-        self._capture_done = False
-        self.tuned = None
-        self.device = torch.device("cuda", device) if isinstance(device, int) else device
-        self.batch = batch
-        self.comm = comm
-        self.use_graph = use_graph
-        n = C.MNIST_NUM_PARAMS
-        if init_model is None:
-            torch.manual_seed(seed)
-            init_model = MnistCNN()
-        sd = init_model.state_dict()
-        flat = torch.cat([sd[k].detach().reshape(-1).float().cpu() for k, _ in _LAYOUT])
-        assert flat.numel() == n
-        self.params = flat.to(self.device)
-        # + zeroed slack: the all-reduce of the bucket that ends at the end of the gradient is
-        # padded to a multiple of world_size x channels x 16 B (Reducer::set_padding)
-        self._grad_slack = 1024
-        self._grad_store = torch.zeros(n + self._grad_slack, device=self.device)
-        self.grads = self._grad_store[:n]
+        n = self._init_flat(batch, device, comm, seed, init_model)
+        assert n == C.MNIST_NUM_PARAMS
         self.mom = torch.zeros(n, device=self.device)
         self.lr = torch.full((1,), lr, device=self.device)
         self._lr_host = lr
-        self.metrics = torch.zeros(4, device=self.device)
         wsb = C.mnist_workspace_bytes(batch)
         self.workspace = torch.empty(wsb // 4 + 64, dtype=torch.float32, device=self.device)
         if os.environ.get("MXDDP_POISON_WORKSPACE"):  # debug: NaN-fill to catch reads before writes
             self.workspace.fill_(float("nan"))
         torch.cuda.synchronize(self.device)
-        if comm is not None and comm.world_size > 1:  # DDP ctor semantics: rank 0's weights everywhere
-            st = torch.cuda.current_stream(self.device).cuda_stream
-            comm.broadcast(self.params.data_ptr(), self.params.data_ptr(), n, C.DType.f32, 0, st)
-            torch.cuda.synchronize(self.device)
         self.eng = C.MnistEngine(batch, self.params.data_ptr(), self.grads.data_ptr(), self.mom.data_ptr(),
                                  self.workspace.data_ptr(), wsb, comm, seed, momentum, weight_decay,
                                  self.lr.data_ptr(), self.metrics.data_ptr(), variant)
-        self.eng_comm = comm
-        if force_collectives:
-            self.eng.set_force_collectives(True)
-        self.rccl_variants = rccl_variants  # [(name, Comm)] timed by autotune(); None = comm.py's list
-        self.stream = torch.cuda.ExternalStream(self.eng.stream, device=self.device)
-        self.steps = 0
-        self.steps_at_reset = 0  # self.steps when the device metrics were last zeroed
-        self.world_size = comm.world_size if comm is not None else (peer.world_size if peer is not None else 1)
-        self._set_padding(comm)
-        # gradient transport (world size > 1): RCCL, or the direct xGMI peer all-reduce
-        # (parallel/peer.py) -- validated against RCCL on every rank before it may be used;
-        # "auto" lets autotune() time both
-        self.transport = transport
-        self.peer = None
-        if peer is not None:  # caller-provided peer transport (peer-only job: no RCCL communicator)
-            self.peer, self.transport = peer, "peer"
-            self.eng.set_peer(peer)
-        elif self.world_size > 1 and transport in ("auto", "peer"):
-            from .parallel import peer as _peer
-
-            pc = _peer.peer_comm()
-            if pc is not None and _peer.validate(pc, comm):
-                self.peer = pc
-            elif transport == "peer":
-                raise RuntimeError("peer transport requested but unavailable / failed validation")
-        if self.peer is not None and transport == "peer":
-            self.eng.set_peer(self.peer)
-
-    # --------------------------------------------------------------- stepping
-    def step(self, n: int = 1):
-        """Run n training steps (graph replays once captured; first call warms up + captures)."""
-        if self.use_graph and not self._capture_done:
-            self.eng.step()          # warm-up: lazy RCCL/kernel init outside the capture
-            self.eng.sync()
-            self._capture(self._default_mode())
-            n -= 1
-            self.steps += 1
-        if n > 0:
-            self.eng.replay(n)
-            self.steps += n
-
-    def warm_graphs(self) -> int:
-        """Launch every captured multi-step graph once (untimed warm-up; they are real training
-        steps, counted in self.steps): a replay whose step count needs a graph never launched
-        before would otherwise pay that graph's first-launch cost.  Returns the steps run."""
-        if self.use_graph and not self._capture_done:
-            self.step(1)
-        n = self.eng.warm_graphs()
-        self.steps += n
-        return n
+        self._init_runtime(comm, peer, transport, force_collectives, rccl_variants, use_graph, graph_mode,
+                           steps_per_graph)
 
     def _default_mode(self) -> int:
         # MXDDP_GRAPH_MODE: 0 = eager launches, 1 = whole step(s) incl. RCCL collectives in one
-        # graph, 2 = compute graphs with eager collectives in between.  Default (-1): 1 at
-        # world size 1, eager when real collectives run (see autotune()).
+        # graph, 2 = compute graphs with eager collectives in between.  Default (-1): the engine
+        # picks 1 at world size 1, eager when real collectives run (see autotune()).
         if self.graph_mode is not None:
             return self.graph_mode
         return int(os.environ.get("MXDDP_GRAPH_MODE", "-1"))
 
-    def _capture(self, mode: int, spg: int | None = None):
-        if spg is None:
-            spg = self.steps_per_graph
-        if spg is None:
-            spg = int(os.environ.get("MXDDP_STEPS_PER_GRAPH", "32"))
-        if self._external:
-            spg = 1  # a caller-provided batch is copied in before EVERY step
-        self.eng.capture(mode, spg)
-        self._capture_done = True
-
-    def autotune(self, trial_steps: int = 24, include_graphs: bool | None = None, restore: bool = False) -> dict:
-        """Pick the fastest launch strategy for the DDP step on THIS machine by timing a few real
-        training steps of each (they count as warm-up).  Candidates: gradient transport (RCCL
-        ring, or the direct xGMI peer all-reduce when it validated) x bucket strategy (fc-bucket
-        all-reduce overlapped on the side stream "ovl", the two buckets in order on the compute
-        stream "inl", or ONE all-reduce over the whole gradient after the conv backward "one":
-        one collective latency instead of two) x (eager launches, or the whole step captured in
-        one hipGraph).  Peer-transport graphs are always tried (the
-        peer kernel is an ordinary kernel); RCCL-in-graph only with MXDDP_AUTOTUNE_GRAPHS=1.
-        The slowest rank's time decides, so every rank picks the same strategy.  ``restore``:
-        the trial steps are scratch -- weights, momentum, data-stream position and metrics are
-        put back afterwards and the step count is unchanged (the trainer CLI, so that the trained
-        model and --max-steps still match epochs x batches).  Returns {candidate: ms/step}."""
-        from .parallel import comm as pc
-
-        if include_graphs is None:
-            include_graphs = os.environ.get("MXDDP_AUTOTUNE_GRAPHS", "0") == "1"
-        if not self.eng.reducer_active or self._external:
-            return {}
-        comms = self._rccl_candidates()
-        rccl_names = [f"rccl:{v}" if len(comms) > 1 else "rccl" for v in comms]
-        transports = rccl_names + (["peer"] if self.peer is not None else [])
-        if self.transport == "peer" and self.peer is not None:
-            transports = ["peer"]
-        elif self.transport == "rccl":
-            transports = rccl_names
-        snap = self.snapshot() if restore else None
-        cands = []
-        for tr in transports:
-            strats = ["ovl", "inl", "one"] + (["co"] if tr == "peer" else [])
-            cands += [(tr, 0, st) for st in strats]
-            if self.use_graph and (include_graphs or tr == "peer"):
-                cands += [(tr, 1, st) for st in strats]
-        results = {}
-        for tr, mode, strat in cands:
-            self.eng.uncapture()
-            self._use_transport(tr, comms)
-            self._set_buckets(strat)
-            failed = 0.0
-            try:  # capture issues no collective, so a local failure here is safe to agree on
-                if mode:
-                    self._capture(mode)
-            except RuntimeError:
-                failed = 1.0
-            # every rank reaches this all-reduce before any collective of the candidate, so a
-            # candidate that failed to capture on ANY rank is skipped by ALL ranks together
-            if pc.all_reduce_max(failed) > 0:
-                self.eng.uncapture()
-                results[(tr, mode, strat)] = float("inf")
-                continue
-            # replay errors are not swallowed: peers may already be inside the collectives
-            self.eng.replay(2)
-            self.eng.sync()
-            pc.barrier()
-            t0 = time.perf_counter()
-            self.eng.replay(trial_steps)
-            self.eng.sync()
-            dt = pc.all_reduce_max(time.perf_counter() - t0)
-            self._check_peer()
-            self.steps += 2 + trial_steps
-            results[(tr, mode, strat)] = dt / trial_steps * 1e3
-        best = min(results, key=results.get)
-        self.eng.uncapture()
-        self._use_transport(best[0], comms)
-        self._set_buckets(best[2])
-        if best[1]:
-            self._capture(best[1])
-        self._capture_done = True
-        if snap is not None:
-            self.restore(snap)
-        else:
-            self.read_metrics(reset=True)
-        self.tuned = {"transport": best[0], "graph_mode": best[1], "buckets": best[2],
-                      "trials_ms": {f"{t}/{m}/{s}": round(v, 4) for (t, m, s), v in results.items()}}
-        return results
-
-    def _rccl_candidates(self) -> dict:
-        """{variant name: Comm} the autotune times: the caller's list, else (world size > 1, or
-        MXDDP_RCCL_VARIANTS set) comm.py's xGMI-sized variants over the same ranks, else just
-        the trainer's own communicator."""
-        if self.rccl_variants is not None:
-            return dict(self.rccl_variants)
-        if self.comm is None:
-            return {}
-        from .parallel import comm as pc
-
-        if self.world_size > 1 or "MXDDP_RCCL_VARIANTS" in os.environ:
-            out = {}
-            for v in pc.rccl_variants():
-                c = self.comm if v == "default" else pc.rccl_comm(force=True, variant=v)
-                if c is not None:
-                    out[v] = c
-            if out:
-                return out
-        return {"default": self.comm}
-
-    def _set_padding(self, comm):
-        ctas = 0
-        if comm is not None:
-            from .parallel import comm as pc
-
-            ctas = pc.parse_variant(comm.variant)["ctas"]
-        mult = max(1, self.world_size) * max(ctas, 32) * 4  # elements of 4 B: 16-B chunks per channel
-        self.eng.set_bucket_padding(self.params.numel() + self._grad_slack, mult)
-
-    def _use_transport(self, tr: str, comms: dict):
-        if tr == "peer":
-            self.eng.set_peer(self.peer)
-            return
-        self.eng.set_peer(None)
-        name = tr.split(":", 1)[1] if ":" in tr else next(iter(comms), "default")
-        c = comms.get(name, self.comm)
-        if c is not None and c is not self.eng_comm:
-            self.eng.set_comm(c)
-            self.eng_comm = c
-        self._set_padding(c)
+    def _candidate_strategies(self, transport: str) -> list:
+        return ["ovl", "inl", "one"] + (["co"] if transport == "peer" else [])
 
     def _set_buckets(self, strat: str):
         """ovl: fc bucket overlapped on the side stream; inl: both buckets in order; one: a
@@ -271,96 +77,11 @@ class FusedMnistTrainer:
         self.eng.set_overlap(strat == "ovl")
         self.bucket_strategy = "co" if co else ("inl" if strat == "co" else strat)
 
-    def _check_peer(self):
-        if self.peer is not None and self.peer.error():
-            raise RuntimeError(f"peer all-reduce: rank {self.peer.error() - 1} never arrived (timeout)")
+    def _opt_tensors(self) -> dict:
+        return {"mom": self.mom}
 
-    @property
-    def active_transport(self) -> str:
-        if self.world_size == 1 and not self.eng.reducer_active:
-            return "none"
-        if self.eng.peer_active:
-            return "peer"
-        return "rccl" if self.eng_comm is None else f"rccl:{self.eng_comm.variant}"
-
-    def set_batch(self, x: torch.Tensor, y: torch.Tensor):
-        """Use a caller-provided batch instead of the on-device generator (real MNIST)."""
-        self.eng.set_external_batch(True)
-        self._external = True
-        # x / y were produced (and allocated) on the caller's stream: the engine stream waits for
-        # that work before copying, and the caller's stream waits for the copy -- otherwise the
-        # caller's next batch can reuse their memory before this step's copy has run
-        cur = torch.cuda.current_stream(self.device)
-        self.stream.wait_stream(cur)
-        with torch.cuda.stream(self.stream):
-            self._x_view().copy_(x.reshape(self.batch, 1, 28, 28), non_blocking=True)
-            self._y_view().copy_(y.to(torch.int32), non_blocking=True)
-        cur.wait_stream(self.stream)
-
-    def _x_view(self):
-        off = (self.eng.x_ptr - self.workspace.data_ptr()) // 4
-        return self.workspace[off:off + self.batch * 784].view(self.batch, 1, 28, 28)
-
-    def _y_view(self):
-        off = (self.eng.y_ptr - self.workspace.data_ptr()) // 4
-        return self.workspace[off:off + self.batch].view(torch.int32)
-
-    def _counter_view(self):
-        off = (self.eng.counter_ptr - self.workspace.data_ptr()) // 4
-        return self.workspace[off:off + 4].view(torch.int32)
-
-    # --------------------------------------------------------------- snapshots
-    def data_state(self) -> torch.Tensor:
-        """Position of the on-device synthetic data stream (Philox counter), for resume state."""
-        self.eng.sync()
-        return self._counter_view().cpu().clone()
-
-    def load_data_state(self, ctr: torch.Tensor):
-        self.eng.sync()
-        self._counter_view().copy_(ctr.to(torch.int32).to(self.device))
-        torch.cuda.synchronize(self.device)
-
-    def snapshot(self) -> dict:
-        """Device copies of everything a training step changes (weights, momentum, data-stream
-        position, metric accumulators): restore() puts the trainer back exactly."""
-        self.eng.sync()
-        return {"params": self.params.clone(), "mom": self.mom.clone(), "ctr": self._counter_view().clone(),
-                "metrics": self.metrics.clone(), "steps": self.steps, "steps_at_reset": self.steps_at_reset}
-
-    def restore(self, snap: dict):
-        self.eng.sync()
-        with torch.cuda.stream(self.stream):
-            self.params.copy_(snap["params"])
-            self.mom.copy_(snap["mom"])
-            self._counter_view().copy_(snap["ctr"])
-            self.metrics.copy_(snap["metrics"])
-        self.eng.sync()
-        self.steps, self.steps_at_reset = snap["steps"], snap["steps_at_reset"]
+    def _after_param_load(self):
         self.eng.repack()  # conv2 weights pre-packed in MFMA fragment order + accumulator resets
-        self.eng.sync()
-
-    def set_lr(self, lr: float):
-        if lr != self._lr_host:
-            with torch.cuda.stream(self.stream):
-                self.lr.fill_(lr)
-            self._lr_host = lr
-
-    def synchronize(self):
-        self.eng.sync()
-
-    def read_metrics(self, reset: bool = True):
-        """(loss_sum, correct) accumulated since the last reset (one host sync)."""
-        self.eng.sync()
-        if self.comm is not None:
-            self.comm.check_async_error()  # surface a failed/aborted peer at log boundaries
-        self._check_peer()
-        m = self.metrics[:2].tolist()
-        if reset:
-            with torch.cuda.stream(self.stream):
-                self.metrics.zero_()
-            self.eng.sync()
-            self.steps_at_reset = self.steps
-        return m[0], m[1]
 
     def phase_profile(self, steps: int = 20) -> dict:
         """In-kernel phase timings of the fused step (MnistFused::trace, s_memrealtime at 100 MHz).
@@ -432,28 +153,3 @@ class FusedMnistTrainer:
             avg["phases"] = [round(sum(r["phases"][i] for r in runs) / len(runs), 2) for i in range(m)]
             out[n] = avg
         return out
-
-    # --------------------------------------------------------------- state
-    def state_dict(self) -> dict:
-        self.eng.sync()
-        out, off = {}, 0
-        for name, shape in _LAYOUT:
-            k = 1
-            for s in shape:
-                k *= s
-            out[name] = self.params[off:off + k].view(shape).detach().cpu().clone()
-            off += k
-        return out
-
-    def load_state_dict(self, sd: dict):
-        flat = torch.cat([sd[k].detach().reshape(-1).float().cpu() for k, _ in _LAYOUT])
-        self.eng.sync()
-        self.params.copy_(flat.to(self.device))
-        torch.cuda.synchronize(self.device)
-        self.eng.repack()  # fused path keeps conv2 weights pre-packed in MFMA fragment order
-        self.eng.sync()
-
-    def to_module(self) -> MnistCNN:
-        m = MnistCNN()
-        m.load_state_dict(self.state_dict())
-        return m

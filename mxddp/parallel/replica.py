@@ -30,6 +30,7 @@ import torch
 import torch.nn as nn
 
 from .. import native
+from ..fused import FusedReplicas
 from .flat import FlatParams, flatten_buffers
 
 
@@ -208,7 +209,7 @@ class ReplicaGroup:
         return self.replicas[0]
 
 
-class FusedMnistReplicas:
+class FusedMnistReplicas(FusedReplicas):
     """In-process replica data parallelism for the MNIST CNN on the fused native engine: ONE
     process drives one ``FusedMnistTrainer`` per device (MirroredStrategy / DataParallel /
     ParallelUpdater semantics: the global batch = replicas x per-replica batch, gradients
@@ -219,7 +220,7 @@ class FusedMnistReplicas:
     all-reduce, SGD -- stays one hipGraph on its own stream and the host only issues one graph
     launch per replica per group of steps; the replicas synchronise with each other on the GPUs.
     Because a replica's all-reduce waits for every other replica, all replicas' work is always
-    LAUNCHED before the host waits on any of them.
+    LAUNCHED before the host waits on any of them (fused.FusedReplicas).
     """
 
     def __init__(self, devices, batch: int = 64, lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 1e-4,
@@ -228,75 +229,11 @@ class FusedMnistReplicas:
         from ..engine import FusedMnistTrainer
         from ..models.mnist_cnn import MnistCNN
 
-        self.devices = [torch.device(d) for d in devices]
-        n = len(self.devices)
-        C = native()
         if init_model is None:
             torch.manual_seed(seed)
             init_model = MnistCNN()
-        self.peers = [None] * n
-        if n > 1:
-            self.peers = []
-            for i, d in enumerate(self.devices):
-                with torch.cuda.device(d):
-                    self.peers.append(C.PeerComm(i, n, d.index, 32 << 20, blocks))
-            for pc, d in zip(self.peers, self.devices):
-                with torch.cuda.device(d):
-                    pc.open_local(self.peers)
-        self.trainers = []
-        for pc, d in zip(self.peers, self.devices):
-            with torch.cuda.device(d):
-                self.trainers.append(FusedMnistTrainer(batch=batch, device=d, comm=None, peer=pc, seed=seed, lr=lr,
-                                                       momentum=momentum, weight_decay=weight_decay,
-                                                       init_model=init_model, use_graph=use_graph, graph_mode=1,
-                                                       steps_per_graph=steps_per_graph))
-        self.use_graph = use_graph
-        self._captured = False
         self.batch = batch
-
-    def _each(self, fn):
-        for t, d in zip(self.trainers, self.devices):
-            with torch.cuda.device(d):
-                fn(t)
-
-    def step(self, n: int = 1):
-        """n training steps of every replica (launched on all devices before any host wait)."""
-        if self.use_graph and not self._captured:
-            self._each(lambda t: t.eng.step())  # warm-up step: every replica launched ...
-            self._each(lambda t: t.eng.sync())  # ... before waiting on any of them
-            self._each(lambda t: t._capture(1))
-            self._each(lambda t: setattr(t, "steps", t.steps + 1))
-            self._captured = True
-            n -= 1
-        if n > 0:
-            self._each(lambda t: t.eng.replay(n))
-            self._each(lambda t: setattr(t, "steps", t.steps + n))
-
-    def set_batch(self, x: torch.Tensor, y: torch.Tensor):
-        """Split a global batch across the replicas (len(x) == replicas x batch)."""
-        xs, ys = x.chunk(len(self.trainers)), y.chunk(len(self.trainers))
-        for t, d, xi, yi in zip(self.trainers, self.devices, xs, ys):
-            with torch.cuda.device(d):
-                t.set_batch(xi.to(d, non_blocking=True), yi.to(d, non_blocking=True))
-
-    def synchronize(self):
-        self._each(lambda t: t.eng.sync())
-        for pc in self.peers:
-            if pc is not None and pc.error():
-                raise RuntimeError(f"replica all-reduce: replica {pc.error() - 1} never arrived (timeout)")
-
-    def read_metrics(self):
-        """(loss_sum, correct) over all replicas since the last read."""
-        self.synchronize()
-        ls = cs = 0.0
-        for t, d in zip(self.trainers, self.devices):
-            with torch.cuda.device(d):
-                a, b = t.read_metrics()
-            ls, cs = ls + a, cs + b
-        return ls, cs
-
-    def state_dict(self) -> dict:
-        return self.trainers[0].state_dict()
-
-    def to_module(self):
-        return self.trainers[0].to_module()
+        super().__init__(devices, lambda d, pc: FusedMnistTrainer(
+            batch=batch, device=d, comm=None, peer=pc, seed=seed, lr=lr, momentum=momentum, weight_decay=weight_decay,
+            init_model=init_model, use_graph=use_graph, graph_mode=1, steps_per_graph=steps_per_graph),
+            blocks=blocks, peer_bytes=32 << 20)

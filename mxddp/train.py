@@ -205,7 +205,9 @@ def main(argv=None) -> int:
     engine = args.engine
     if engine == "auto":
         fusable = ((args.model == "mnist_cnn" and opt_name == "sgd" and bs % 16 == 0 and 16 <= bs <= 128) or
-                   (args.model == "keras_cnn" and opt_name == "adam" and bs % 8 == 0 and bs <= 1024))
+                   (args.model == "keras_cnn" and opt_name == "adam" and bs % 8 == 0 and bs <= 1024) or
+                   (args.model == "mlp" and opt_name == "adam" and args.mlp_units == 1000 and bs % 16 == 0
+                    and 16 <= bs <= 128))
         engine = "fused" if (fusable and use_gpu and mode != "replica" and args.dtype == "fp32"
                              and not (backend == "gloo" and inf.world_size > 1)) else "layers"
     if engine == "fused" and use_gpu and backend == "gloo" and inf.world_size > 1:
@@ -550,7 +552,9 @@ def _train_replica(args, inf, spec, opt_name, lr, mom, wd, bs, mw):
     per = bs // len(devices) if bs % len(devices) == 0 else 0
     if devices[0].type == "cuda" and args.dtype == "fp32" and args.engine != "layers" and per and (
             (spec.name == "mnist_cnn" and opt_name == "sgd" and per % 16 == 0 and 16 <= per <= 128) or
-            (spec.name == "keras_cnn" and opt_name == "adam" and per % 8 == 0 and wd == 0.0)):
+            (spec.name == "keras_cnn" and opt_name == "adam" and per % 8 == 0 and wd == 0.0) or
+            (spec.name == "mlp" and opt_name == "adam" and args.mlp_units == 1000 and per % 16 == 0
+             and 16 <= per <= 128 and wd == 0.0)):
         return _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw)
     torch.manual_seed(args.seed)
     model = build_model(spec.name, **_model_kwargs(args, spec))
@@ -640,6 +644,7 @@ def _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw):
     from .parallel.replica import FusedMnistReplicas
 
     keras = spec.name == "keras_cnn"
+    adam = spec.name in ("keras_cnn", "mlp")
     torch.manual_seed(args.seed)
     init = build_model(spec.name)
     st, start_epoch = {}, 1
@@ -654,6 +659,11 @@ def _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw):
 
         rep = FusedKerasReplicas(devices, batch=bs // len(devices), lr=lr, seed=args.seed, init_model=init,
                                  use_graph=not args.no_graph)
+    elif spec.name == "mlp":
+        from .mlp_engine import FusedMlpReplicas
+
+        rep = FusedMlpReplicas(devices, batch=bs // len(devices), lr=lr, seed=args.seed, init_model=init,
+                               use_graph=not args.no_graph)
     else:
         rep = FusedMnistReplicas(devices, batch=bs // len(devices), lr=lr, momentum=mom, weight_decay=wd,
                                  seed=args.seed, init_model=init, use_graph=not args.no_graph)
@@ -715,7 +725,7 @@ def _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw):
         val = _maybe_eval(args, inf, spec, model, bs, mw, epoch=epoch)
         rep_.epoch_end(epoch, step, loss_tot / max(1, bi * bs), corr_tot / max(1, bi * bs), val, model)
         t0_ = rep.trainers[0]
-        opt_sd = t0_.optimizer_state() if keras else {"momentum": t0_.mom.cpu(), "lr": t0_._lr_host}
+        opt_sd = t0_.optimizer_state() if adam else {"momentum": t0_.mom.cpu(), "lr": t0_._lr_host}
         _epoch_saves(args, inf, epoch, step, rep.state_dict(), opt_sd,
                      {"base_lr": base_lr}, None, data_counters=[t.data_state() for t in rep.trainers])
         if args.max_steps and step >= args.max_steps:
@@ -730,8 +740,9 @@ def _train_replica_fused(args, inf, spec, lr, mom, wd, bs, devices, mw):
 
 # ====================================================================================== fused
 def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
-    """The native fused engines: MNIST CNN + SGD (engine.py) and the reference's Keras CNN + Keras
-    Adam (keras_engine.py); one hipGraph launch per step (or group of steps)."""
+    """The native fused engines: MNIST CNN + SGD (engine.py), the reference's Keras CNN + Keras Adam
+    (keras_engine.py) and Chainer MLP + Chainer Adam (mlp_engine.py); one hipGraph launch per step
+    (or group of steps)."""
     from .data import build_loader
     from .models import build_model
     from .parallel import comm as C
@@ -739,6 +750,7 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
 
     dev = inf.device
     keras = spec.name == "keras_cnn"
+    adam = spec.name in ("keras_cnn", "mlp")
     torch.manual_seed(args.seed)
     init = build_model(spec.name)
     start_epoch = 1
@@ -760,6 +772,14 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
 
         tr = FusedKerasTrainer(batch=bs, device=dev, comm=comm, seed=args.seed, lr=lr, eps=1e-7, weight_decay=wd,
                                eps_hat=True, use_graph=not args.no_graph, init_model=init, peer=peer)
+        if args.resume and "m" in st.get("optimizer", {}):
+            tr.load_optimizer_state(st["optimizer"])
+    elif spec.name == "mlp":
+        from .mlp_engine import FusedMlpTrainer
+
+        tr = FusedMlpTrainer(batch=bs, device=dev, comm=comm, seed=args.seed, lr=lr, eps=1e-8, weight_decay=wd,
+                             eps_hat=True, use_graph=not args.no_graph, init_model=init, peer=peer,
+                             transport=args.transport)
         if args.resume and "m" in st.get("optimizer", {}):
             tr.load_optimizer_state(st["optimizer"])
     else:
@@ -797,7 +817,7 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
             print(model_summary(probe, spec.input_shape, spec.name), flush=True)
         rep.first_loss(_ops.cross_entropy(probe(torch.zeros(2, 1, 28, 28)), torch.zeros(2, dtype=torch.long)), probe)
     base_lr = lr
-    if not keras and tr.eng.reducer_active and synthetic and not args.no_graph:
+    if hasattr(tr, "autotune") and tr.eng.reducer_active and synthetic and not args.no_graph:
         # pick transport / overlap / graph mode on this machine by timing real steps; they are
         # scratch: weights, momentum, data-stream position and metrics are restored afterwards,
         # so the trained model and --max-steps still match epochs x batches
@@ -865,7 +885,7 @@ def _train_fused(args, inf, spec, lr, mom, wd, mode, bs, mw):
             rep.epoch_end(epoch, step, loss_tot / seen, corr_tot / seen, None,
                           tr.to_module() if rep.tb is not None else None)
         if args.save_every and epoch % args.save_every == 0:
-            opt_sd = tr.optimizer_state() if keras else {"momentum": tr.mom.cpu(), "lr": tr._lr_host}
+            opt_sd = tr.optimizer_state() if adam else {"momentum": tr.mom.cpu(), "lr": tr._lr_host}
             save_training_state(args.train_dir, inf.rank, tr.state_dict(), opt_sd, {"base_lr": base_lr}, epoch, step,
                                 extra={"data_counter": tr.data_state(), "sampler_epoch": epoch})
         if args.epoch_checkpoints and inf.is_main:

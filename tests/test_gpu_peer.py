@@ -278,6 +278,13 @@ def test_fused_trainer_peer_ddp_matches_global_batch(cuda, mode):
     _run(4 if mode.endswith("graph") else 2, mode)
 
 
+@pytest.mark.parametrize("mode", ["trainer_co", "trainer_co_graph"])
+def test_fused_trainer_peer_ddp_8_ranks(cuda, mode):
+    """The co-scheduled fc-bucket exchange (PeerPartition / coschedule_args) at the full node's
+    world size: 8 ranks (sharing the one GPU here) against one trainer on the global batch."""
+    _run(8, mode)
+
+
 def test_ddp_layers_peer_transport_matches_global_batch(cuda):
     _run(2, "ddp_layers")
 
