@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--min-warmup-ms", type=float, default=300.0,
                     help="keep running untimed warm-up steps until this much wall time of warm-up ran (GPU "
                          "clock ramp of a fresh process); counted in warmup_steps_run")
+    ap.add_argument("--grad-comm-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="layers path DDP: bf16 gradient all-reduce (opt-in; fp32 master gradients)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--lr", type=float, default=0.01, help="SGD lr (momentum 0.9, wd 1e-4 as the reference)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
@@ -240,6 +242,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 3),
             "dtype": a.dtype,
+            "grad_comm_dtype": a.grad_comm_dtype if a.impl == "layers" else "fp32",
             "data": _data_desc(spec),
             "config": {"model": a.model, "global_batch": B * a.gpus, "per_rank_batch": B, "seq_len": None,
                        "image": "x".join(map(str, spec.input_shape)), "parallelism": f"dp{a.gpus}", "impl": a.impl,
@@ -446,7 +449,7 @@ def _layers_or_torch(a, torch, inf, dev, comm, B):
         from mxddp.optim import SGD
         from mxddp.parallel.ddp import DistributedDataParallel as DDP
 
-        net = DDP(model)
+        net = DDP(model, grad_comm_dtype=a.grad_comm_dtype)
         opt = SGD(net.flat, lr=0.1, momentum=0.9, weight_decay=1e-4)
         loss_fn = ops.cross_entropy
     else:

@@ -389,6 +389,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_overlap", &Reducer::set_overlap)
       .def("set_peer", &Reducer::set_peer, py::arg("peer").none(true), py::keep_alive<1, 2>())
       .def("set_force_collectives", &Reducer::set_force_collectives)
+      .def("set_comm_dtype", &Reducer::set_comm_dtype, py::arg("dtype"), py::arg("shadow") = 0)
+      .def_property_readonly("comm_dtype", &Reducer::comm_dtype)
       .def_property_readonly("active", &Reducer::active);
 
   // ---------------------------------------------------------------- fused Keras-CNN engine

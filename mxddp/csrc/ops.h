@@ -110,6 +110,9 @@ void set_gemm_precision(int p);
 int gemm_precision();
 
 // ---- elementwise / reductions (ops_elementwise.hip) ----
+// fp32 <-> bf16 (round to nearest even) for bf16 gradient communication (grad_cast.hip)
+void cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st);
+void cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t st);
 void relu_fwd(const float* x, float* y, int64_t n, hipStream_t st);
 void relu_bwd(const float* dy, const float* y, float* dx, int64_t n, hipStream_t st);
 // db[c] (+)= sum over (outer, inner) of dy[outer][c][inner]

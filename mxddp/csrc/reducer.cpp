@@ -1,6 +1,7 @@
 #include "reducer.h"
 
 #include "common.h"
+#include "ops.h"
 
 namespace mx {
 
@@ -35,6 +36,13 @@ void Reducer::prepare() {
   sched_.prepare();
   in_step_ = true;
   step_compute_ = nullptr;
+}
+
+void Reducer::set_comm_dtype(DType t, uintptr_t shadow) {
+  MX_CHECK(t == dtype_ || (t == DType::kBF16 && dtype_ == DType::kF32 && shadow),
+           "reducer: bf16 communication of an fp32 gradient needs a bf16 shadow buffer");
+  MX_CHECK(!in_step_, "reducer: communication dtype changed inside a backward");
+  shadow_ = t == dtype_ ? nullptr : reinterpret_cast<uint16_t*>(shadow);
 }
 
 void Reducer::abort() {
@@ -87,12 +95,22 @@ void Reducer::launch_ready(hipStream_t compute) {
       }
       if (timing_ && bi == 0) MX_HIP_CHECK(hipEventRecord(t0_, st));
       char* p = flat_ + b.offset * dtype_size(dtype_);
-      if (peer_ && (op_ == RedOp::kSum || op_ == RedOp::kAvg) && peer_->world_size() > 1) {
-        peer_->all_reduce(p, b.numel, dtype_, st, op_);
+      const bool via_peer = peer_ && (op_ == RedOp::kSum || op_ == RedOp::kAvg) && peer_->world_size() > 1;
+      const size_t n = via_peer ? b.numel : padded_count(b.offset, b.numel);
+      void* buf = p;
+      DType t = dtype_;
+      if (shadow_) {  // bf16 on the wire: cast in, all-reduce, cast back (same stream)
+        buf = shadow_ + b.offset;
+        t = DType::kBF16;
+        cast_f32_bf16(reinterpret_cast<const float*>(p), shadow_ + b.offset, (int64_t)n, st);
+      }
+      if (via_peer) {
+        peer_->all_reduce(buf, n, t, st, op_);
       } else {
         MX_CHECK(comm_ != nullptr, "reducer: no RCCL communicator for this collective");
-        comm_->all_reduce(p, p, padded_count(b.offset, b.numel), dtype_, op_, st);
+        comm_->all_reduce(buf, buf, n, t, op_, st);
       }
+      if (shadow_) cast_bf16_f32(shadow_ + b.offset, reinterpret_cast<float*>(p), (int64_t)b.numel, st);
     }
   }
 }

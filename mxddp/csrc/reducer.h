@@ -79,6 +79,11 @@ class Reducer {
   // (peer.h).  Every rank must make the same choice.
   void set_peer(PeerComm* p) { peer_ = p; }
   PeerComm* peer() const { return peer_; }
+  // opt-in reduced-precision communication of an fp32 gradient: each bucket is cast to bf16 into
+  // `shadow` (a bf16 buffer as long as the gradient buffer's capacity), all-reduced in bf16 and
+  // cast back into the fp32 bucket (half the bytes over the links).  kF32 = off.
+  void set_comm_dtype(DType t, uintptr_t shadow);
+  DType comm_dtype() const { return shadow_ ? DType::kBF16 : dtype_; }
 
  private:
   void launch_ready(hipStream_t compute);
@@ -96,6 +101,7 @@ class Reducer {
   // stream, and a backward's side-stream work must be joined (finalize) before the next begins
   hipStream_t step_compute_ = nullptr;
   size_t pad_total_ = 0, pad_cap_ = 0, pad_mult_ = 1;
+  uint16_t* shadow_ = nullptr;  // bf16 communication buffer (set_comm_dtype), or null
   bool in_step_ = false;
 };
 

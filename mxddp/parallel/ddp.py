@@ -12,6 +12,11 @@ Same contract as ``torch.nn.parallel.DistributedDataParallel`` as the reference 
 4. ``.module`` is the wrapped model, so ``ddp.module.state_dict()`` has no ``module.``
    prefix (checkpoint layout, pytorch/distributed_data_parallel.py:109-113).
 
+``grad_comm_dtype="bf16"`` (opt-in, off by default): every bucket is cast to bf16 before its
+all-reduce and back to fp32 after it -- half the bytes on the links for large models (ResNet-50's
+102 MB fp32 gradient travels as 51 MB); the optimizer still updates fp32 weights
+from fp32 gradient buffers.
+
 GPU: gradients live in one flat buffer (mxddp.parallel.flat); each bucket is an in-place
 RCCL all-reduce on the reducer's side HIP stream (C++ ``mxddp._C.Reducer``), fenced by
 events.  CPU: the same bucketing over gloo with async work handles.
@@ -58,7 +63,7 @@ def assign_buckets(numels: list[int], offsets: list[int], total: int, bucket_cap
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers: bool = True,
                  bucket_cap_mb: float = 25.0, first_bucket_cap_mb: float = 1.0, average: bool = True,
-                 timing: bool = False, transport: str = "auto"):
+                 timing: bool = False, transport: str = "auto", grad_comm_dtype: str = "fp32"):
         super().__init__()
         self.module = module
         inf = _comm.info()
@@ -71,6 +76,9 @@ class DistributedDataParallel(nn.Module):
         self.buckets, self.param_bucket = assign_buckets(numels, self.flat.offsets, self.flat.numel, bucket_cap_mb,
                                                          first_bucket_cap_mb)
         self.average = average
+        if grad_comm_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"grad_comm_dtype {grad_comm_dtype!r}: fp32 or bf16")
+        self.grad_comm_dtype = grad_comm_dtype
         # --dist-backend gloo on a GPU (pytorch/distributed_data_parallel.py:46): honoured --
         # the gradient buckets and broadcasts go over gloo (host-staged), not RCCL / peer
         self.gloo_data = self.device.type == "cuda" and inf.backend == "gloo" and self.world_size > 1
@@ -81,8 +89,13 @@ class DistributedDataParallel(nn.Module):
             C = native()
             self.reducer = C.Reducer(self._comm, self.flat.grad.data_ptr(), C.DType.f32, self.buckets,
                                      self.param_bucket, C.RedOp.avg if average else C.RedOp.sum, timing)
+            if grad_comm_dtype == "bf16":
+                # bf16 twin of the whole gradient store (slack included: the padded last bucket)
+                self._comm_shadow = torch.zeros(self.flat.capacity, dtype=torch.bfloat16, device=self.device)
+                self.reducer.set_comm_dtype(C.DType.bf16, self._comm_shadow.data_ptr())
         else:
-            self.reducer = _GlooReducer(self.flat.grad, self.buckets, self.param_bucket, average, self.world_size)
+            self.reducer = _GlooReducer(self.flat.grad, self.buckets, self.param_bucket, average, self.world_size,
+                                        bf16=grad_comm_dtype == "bf16")
         self.transport = "rccl" if native_reducer else "gloo"
         self.transport_ms = None
         if native_reducer and self.world_size > 1:
@@ -240,9 +253,9 @@ class _GlooReducer:
     """CPU twin of mxddp._C.Reducer: contiguous flat-buffer buckets, async gloo all-reduce
     launched in bucket order as buckets fill, joined in finalize()."""
 
-    def __init__(self, flat_grad, buckets, param_bucket, average, world_size):
+    def __init__(self, flat_grad, buckets, param_bucket, average, world_size, bf16: bool = False):
         self.flat, self.buckets, self.param_bucket = flat_grad, buckets, param_bucket
-        self.average, self.ws = average, world_size
+        self.average, self.ws, self.bf16 = average, world_size, bf16
         self.total = [0] * len(buckets)
         for b in param_bucket:
             self.total[b] += 1
@@ -279,15 +292,18 @@ class _GlooReducer:
         while self.next < len(self.buckets) and self.ready[self.next]:
             off, n = self.buckets[self.next]
             if self.ws > 1:
-                self.works.append((off, n, dist.all_reduce(self.flat[off:off + n], async_op=True)))
+                t = self.flat[off:off + n].to(torch.bfloat16) if self.bf16 else self.flat[off:off + n]
+                self.works.append((off, n, t, dist.all_reduce(t, async_op=True)))
             self.next += 1
 
     def finalize(self, _stream=0):
         for i in range(len(self.buckets)):
             self.ready[i] = True
         self._launch()
-        for off, n, w in self.works:
+        for off, n, t, w in self.works:
             w.wait()
+            if self.bf16:
+                self.flat[off:off + n].copy_(t)
             if self.average:
                 self.flat[off:off + n].div_(self.ws)
         self.works = []

@@ -82,6 +82,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
                    help="GEMM compute precision: fp32 (exact, reference) or bf16 operands + fp32 accumulate")
     p.add_argument("--metrics-jsonl", type=str, default="", help="append JSONL metrics here")
+    p.add_argument("--grad-comm-dtype", default="fp32", choices=["fp32", "bf16"],
+                   help="layers path DDP: dtype of the gradient all-reduce (bf16: buckets cast to bf16 on the wire, "
+                        "fp32 master gradients / weights; opt-in)")
     p.add_argument("--max-steps", type=int, default=0, help="stop after this many steps (0 = full epochs)")
     p.add_argument("--sync-set-epoch", action="store_true", default=True)
     p.add_argument("--tensorboard-dir", type=str, default="",
@@ -402,7 +405,8 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
     torch.manual_seed(args.seed)
     model = build_model(spec.name, **_model_kwargs(args, spec)).to(dev)
     if mode == "ddp":
-        net = DDP(model, bucket_cap_mb=args.bucket_cap_mb, transport=args.transport if dev.type == "cuda" else "auto")
+        net = DDP(model, bucket_cap_mb=args.bucket_cap_mb, transport=args.transport if dev.type == "cuda" else "auto",
+                  grad_comm_dtype=args.grad_comm_dtype)
         flat = net.flat
     else:
         net, flat = model, FlatParams(model, dev)

@@ -205,9 +205,48 @@ def _bn_worker(rank, ws, port, model_name, b, dtype, q):
     PC.shutdown()
 
 
+def _commdtype_worker(rank, ws, port, model_name, b, q):
+    """The same DDP steps with fp32 and with bf16 gradient communication (--grad-comm-dtype):
+    the bf16 run keeps the ranks identical and stays within bf16 rounding of the fp32 run."""
+    _env(rank, ws, port)
+    from mxddp import ops
+    from mxddp.models import build_model
+    from mxddp.optim import SGD
+    from mxddp.parallel import comm as PC
+    from mxddp.parallel.ddp import DistributedDataParallel as DDP
+
+    PC.init_distributed(use_gpu=True)
+    ops.set_compute_dtype("bf16")
+    dev = torch.device("cuda", 0)
+    batches = _batches(3, ws * b, (3, 64, 64), seed=7)
+    res, bad = {}, []
+    for cd in ("fp32", "bf16"):
+        torch.manual_seed(0)
+        ddp = DDP(build_model(model_name).to(dev), grad_comm_dtype=cd)
+        if cd == "bf16" and str(ddp.reducer.comm_dtype) != "DType.bf16":
+            bad.append(("comm dtype", str(ddp.reducer.comm_dtype)))
+        opt = SGD(ddp.flat, lr=0.02, momentum=0.9, weight_decay=1e-4)
+        for x, y in batches:
+            opt.zero_grad()
+            ops.cross_entropy(ddp(x[rank * b:(rank + 1) * b].to(dev)), y[rank * b:(rank + 1) * b].to(dev)).backward()
+            opt.step()
+        torch.cuda.synchronize()
+        res[cd] = ddp.flat.data.cpu().clone()
+        allp = [None] * ws
+        torch.distributed.all_gather_object(allp, res[cd])
+        if any(not torch.equal(allp[0], t) for t in allp):
+            bad.append((cd, "ranks diverged"))
+    d = (res["bf16"] - res["fp32"]).abs().max().item()
+    scale = res["fp32"].abs().max().item()
+    if not d <= 2e-2 * scale or d == 0.0:
+        bad.append(("bf16 comm vs fp32 comm", d, scale))
+    q.put((rank, bad, {"max_abs_diff": d}))
+    PC.shutdown()
+
+
 def _worker(kind, rank, ws, port, args, q):
     try:
-        (_graph_worker if kind == "graph" else _bn_worker)(rank, ws, port, *args, q)
+        {"graph": _graph_worker, "bn": _bn_worker, "commdtype": _commdtype_worker}[kind](rank, ws, port, *args, q)
     except Exception:
         q.put((rank, ["exception: " + traceback.format_exc()], {}))
 
@@ -253,3 +292,9 @@ def test_ddp_pyramidnet_bn_semantics_two_ranks(cuda):
 
 def test_ddp_resnet50_nhwc_bf16_bn_semantics_two_ranks(cuda):
     _run("bn", 2, "resnet50", 4, "bf16")
+
+
+def test_ddp_resnet50_bf16_gradient_communication_two_ranks(cuda):
+    """--grad-comm-dtype bf16 on ResNet-50 (BASELINE config 5's bucket stress): 2 ranks over the
+    peer transport, bf16 buckets on the wire, within bf16 rounding of the fp32-communication run."""
+    _run("commdtype", 2, "resnet50", 4)
