@@ -381,6 +381,9 @@ __global__ __launch_bounds__(64 * kF3Wv) void f3t_fc1_kernel(MnistFused f) {
     av[s] = A[4 * s];
     bv[s] = W[4 * s];
   }
+  // all 18 operand loads in flight before the first MFMA (left alone, the scheduler interleaves
+  // each load with its MFMAs: 30 VGPRs, and the wave waits on memory once per k-step)
+  __builtin_amdgcn_sched_barrier(0);
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
   for (int s = 0; s < kTS; ++s) {
