@@ -71,6 +71,61 @@ def test_fused_keras_matches_reference(cuda, graph, eps_hat, B):
     assert moved > 1e-3
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_fused_keras_rccl_collectives_ws1(cuda, graph):
+    """The DDP path of the fused Keras step with REAL RCCL all-reduces (1-rank communicator,
+    collectives forced): finalize into g, the 373 KB bucket all-reduced, Adam from g -- eager and
+    captured in the step graph -- against the CPU Adam reference."""
+    from mxddp import native
+    from mxddp.keras_engine import FusedKerasTrainer
+    from mxddp.models import KerasCNN
+
+    C = native()
+    comm = C.Comm(C.Comm.new_unique_id(), 0, 1, cuda.index or 0)
+    torch.manual_seed(0)
+    ref = KerasCNN()
+    init = {k: v.clone() for k, v in ref.state_dict().items()}
+    steps, lr, B = 4, 2e-3, 32
+    batches = _batches(steps, B, seed=5)
+    m0 = KerasCNN()
+    m0.load_state_dict(init)
+    tr = FusedKerasTrainer(batch=B, device=cuda, lr=lr, eps=1e-7, comm=comm, force_collectives=True,
+                           use_graph=graph, graph_mode=1 if graph else 0, init_model=m0)
+    assert tr.eng.reducer_active and tr.active_transport == "rccl:default"
+    losses = []
+    for x, y in batches:
+        tr.set_batch(x.to(cuda), y.to(cuda))
+        tr.step(1)
+        losses.append(tr.read_metrics()[0] / B)
+    assert tr.eng.captured == graph
+    ref_losses = _ref_run(ref, batches, lr, True)
+    for a, b in zip(losses, ref_losses):
+        assert abs(a - b) < 1e-4 * max(1.0, abs(b)), (losses, ref_losses)
+    sd = tr.state_dict()
+    for k, v in ref.state_dict().items():
+        assert torch.allclose(sd[k], v, rtol=1e-3, atol=2e-5), (k, (sd[k] - v).abs().max())
+
+
+def test_fused_keras_autotune_ws1(cuda):
+    """autotune() of the Keras engine (RCCL variants x eager / graph, collectives forced at one
+    rank) only changes how the step is launched: the trained weights equal an untuned engine's."""
+    from mxddp import native
+    from mxddp.keras_engine import FusedKerasTrainer
+
+    C = native()
+    comm = C.Comm(C.Comm.new_unique_id(), 0, 1, cuda.index or 0)
+    a = FusedKerasTrainer(batch=64, device=cuda, lr=1e-3, comm=comm, force_collectives=True)
+    b = FusedKerasTrainer(batch=64, device=cuda, lr=1e-3)
+    a.step(1)
+    res = a.autotune(trial_steps=3, include_graphs=True)
+    assert len(res) == 2 and a.tuned["buckets"] == "one"  # {eager, graph} x {one}
+    a.step(5)
+    b.step(1 + 2 * (2 + 3) + 5)
+    assert a.steps == b.steps and a.adam_steps == b.adam_steps
+    for k, v in a.state_dict().items():
+        assert torch.equal(v, b.state_dict()[k]), k
+
+
 def test_fused_keras_trains_on_device_stream(cuda):
     from mxddp.keras_engine import FusedKerasTrainer
 

@@ -134,12 +134,14 @@ def test_model_forward_backward_vs_torch(cuda, name):
 
 
 @pytest.mark.parametrize("model,extra", [("mnist_cnn", ["--per-rank-batch", "64"]),
-                                         ("keras_cnn", ["--per-rank-batch", "32"])])
+                                         ("keras_cnn", ["--per-rank-batch", "32"]),
+                                         ("mlp", ["--per-rank-batch", "32"])])
 def test_train_cli_two_ranks_share_gpu(cuda, tmp_path, model, extra):
     """The reference DDP launch (one process per rank, reference flags) with two ranks on the one
-    GPU: RCCL cannot span them, so the DDP gradient exchange is the peer transport -- the fused
-    MNIST engine (autotuned step) and the layers-path bucket reducer (keras_cnn).  Both ranks'
-    reference-layout checkpoints must be identical."""
+    GPU: RCCL cannot span them, so the DDP gradient exchange is the peer transport -- each model
+    on its fused engine (train.py routes mnist_cnn, keras_cnn and mlp there) with the autotuned
+    DDP step.  Both ranks' reference-layout checkpoints must be identical (the global-batch
+    equivalence of the fused DDP steps is checked in test_gpu_peer.py / test_gpu_keras_engine.py)."""
     import os
     import subprocess
     import sys

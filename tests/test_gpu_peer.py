@@ -216,6 +216,46 @@ def _worker(rank, ws, port, mode, q):
                 moved = (ref.params.cpu() - torch.cat([v.reshape(-1) for v in init.state_dict().values()])).abs().max()
                 if not d < 2e-5 or not moved > 1e-3:
                     bad.append(("ddp != global batch", d, float(moved)))
+        elif mode in ("keras", "keras_graph", "mlp", "mlp_graph"):
+            # fused Keras-CNN / Chainer-MLP DDP step over the peer transport == one trainer on
+            # the global batch (MultiWorkerMirroredStrategy / ChainerMN parity)
+            if mode.startswith("keras"):
+                from mxddp.keras_engine import FusedKerasTrainer as T
+                from mxddp.models import KerasCNN as M
+            else:
+                from mxddp.mlp_engine import FusedMlpTrainer as T
+                from mxddp.models import MLP as M
+            graph = mode.endswith("graph")
+            b, steps = 16, 3
+            torch.manual_seed(0)
+            init = M()
+            g = torch.Generator().manual_seed(6)
+            batches = [(torch.rand(ws * b, 1, 28, 28, generator=g), torch.randint(0, 10, (ws * b,), generator=g))
+                       for _ in range(steps)]
+            tr = T(batch=b, device=0, comm=None, peer=pc, lr=2e-3, init_model=init, use_graph=graph,
+                   graph_mode=1 if graph else 0)
+            for x, y in batches:
+                tr.set_batch(x[rank * b:(rank + 1) * b].cuda(), y[rank * b:(rank + 1) * b].cuda())
+                tr.step(1)
+            tr.synchronize()
+            if pc.error():
+                bad.append(("peer error", pc.error()))
+            if tr.eng.captured != graph:
+                bad.append(("graph", tr.eng.captured))
+            mine = tr.params.cpu()
+            allp = [None] * ws
+            dist.all_gather_object(allp, mine)
+            if any(not torch.equal(allp[0], t) for t in allp):
+                bad.append("ranks diverged")
+            if rank == 0:
+                ref = T(batch=ws * b, device=0, comm=None, lr=2e-3, init_model=init, use_graph=False)
+                for x, y in batches:
+                    ref.set_batch(x.cuda(), y.cuda())
+                    ref.step(1)
+                ref.synchronize()
+                d = (ref.params.cpu() - mine).abs().max().item()
+                if not d < 5e-5:
+                    bad.append(("ddp != global batch", d))
         elif mode == "timeout":
             pc.set_timeout_ms(300)
             x = torch.ones(10_000, device="cuda")
@@ -403,3 +443,11 @@ def test_fused_replicas_stalled_replica_fails_fast(cuda):
         if p.is_alive():
             p.kill()
     assert bad == [], bad
+
+
+@pytest.mark.parametrize("ws,mode", [(2, "keras"), (2, "keras_graph"), (8, "keras_graph"),
+                                     (2, "mlp"), (2, "mlp_graph"), (8, "mlp_graph")])
+def test_fused_adam_engines_peer_ddp_match_global_batch(cuda, ws, mode):
+    """The fused Keras-CNN and Chainer-MLP DDP steps (finalize / gradient kernels, bucket
+    all-reduce over the peer transport, Adam) at 2 and 8 ranks == one trainer on the global batch."""
+    _run(ws, mode)
