@@ -126,12 +126,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_conv_scratch_floats", &nhwc_conv_scratch_floats);
   m.def("nhwc_conv_dgrad", [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int N, int H, int W, int C, int K, int R,
                               int S_, int sh, int sw, int ph, int pw, int P_, int Q, uintptr_t scratch,
-                              uintptr_t st, uintptr_t addend) {
-    nhwc_conv_dgrad(P<const uint16_t>(dy), P<const uint16_t>(wt), P<uint16_t>(dx), N, H, W, C, K, R, S_, sh, sw, ph,
-                    pw, P_, Q, P<float>(scratch), S(st), P<const uint16_t>(addend));
+                              uintptr_t st, uintptr_t addend, uintptr_t bnpart, uintptr_t bx, uintptr_t bmean,
+                              uintptr_t bfcoef, uintptr_t bmask, bool brelu) {
+    return nhwc_conv_dgrad(P<const uint16_t>(dy), P<const uint16_t>(wt), P<uint16_t>(dx), N, H, W, C, K, R, S_, sh, sw,
+                           ph, pw, P_, Q, P<float>(scratch), S(st), P<const uint16_t>(addend), P<float>(bnpart),
+                           P<const uint16_t>(bx), P<const float>(bmean), P<const float>(bfcoef),
+                           P<const uint8_t>(bmask), brelu);
   }, py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("K"),
      py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("P"), py::arg("Q"),
-     py::arg("scratch"), py::arg("st"), py::arg("addend") = 0);
+     py::arg("scratch"), py::arg("st"), py::arg("addend") = 0, py::arg("bnpart") = 0, py::arg("bx") = 0,
+     py::arg("bmean") = 0, py::arg("bfcoef") = 0, py::arg("bmask") = 0, py::arg("brelu") = false);
+  m.def("nhwc_conv_dgrad_bn_rows", &nhwc_conv_dgrad_bn_rows);
   m.def("nhwc_conv_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, int N, int H, int W, int Cin, int Cp, int K,
                               int R, int S_, int sh, int sw, int ph, int pw, int P_, int Q, bool acc, uintptr_t scratch,
                               uintptr_t st) {
@@ -154,14 +159,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_bn_scratch_floats", &nhwc_bn_scratch_floats);
   m.def("nhwc_bn_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t y, uintptr_t g, uintptr_t mean, uintptr_t invstd,
                           uintptr_t dx, uintptr_t dres, uintptr_t dg, uintptr_t db, int Npix, int C, bool relu,
-                          bool accp, uintptr_t scratch, uintptr_t st, uintptr_t fcoef, uintptr_t mask) {
+                          bool accp, uintptr_t scratch, uintptr_t st, uintptr_t fcoef, uintptr_t mask,
+                          uintptr_t pre_part, int pre_gx) {
     nhwc_bn_bwd(P<const uint16_t>(dy), P<const uint16_t>(x), P<const uint16_t>(y), P<const float>(g),
                 P<const float>(mean), P<const float>(invstd), P<uint16_t>(dx), P<uint16_t>(dres), P<float>(dg),
                 P<float>(db), Npix, C, relu, accp, P<float>(scratch), S(st), P<const float>(fcoef),
-                P<const uint8_t>(mask));
+                P<const uint8_t>(mask), P<const float>(pre_part), pre_gx);
   }, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("g"), py::arg("mean"), py::arg("invstd"), py::arg("dx"),
      py::arg("dres"), py::arg("dg"), py::arg("db"), py::arg("Npix"), py::arg("C"), py::arg("relu"), py::arg("accp"),
-     py::arg("scratch"), py::arg("st"), py::arg("fcoef") = 0, py::arg("mask") = 0);
+     py::arg("scratch"), py::arg("st"), py::arg("fcoef") = 0, py::arg("mask") = 0, py::arg("pre_part") = 0,
+     py::arg("pre_gx") = 0);
   m.def("nhwc_maxpool_fwd", [](uintptr_t x, uintptr_t y, uintptr_t arg, int N, int H, int W, int C, int P_, int Q,
                                int k, int s, int p, uintptr_t st) {
     nhwc_maxpool_fwd(P<const uint16_t>(x), P<uint16_t>(y), P<uint8_t>(arg), N, H, W, C, P_, Q, k, s, p, S(st));

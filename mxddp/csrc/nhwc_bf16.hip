@@ -105,8 +105,65 @@ struct ConvNArgs {
   // bnpart[tile][2 Ng] (the layout bn_nhwc_partial_k writes), so the BN skips its statistics pass
   float* bnpart;
   const float* bnshift;  // per-channel shift (the BN's running mean: well conditioned), or null = 0
+  // data gradient whose result is the output gradient of a training BatchNorm (the BN feeding
+  // this conv): the epilogue also writes that BN's backward partial sums -- sum(g) and
+  // sum(g (x - mean)), g = the stored gradient masked by the BN's fused ReLU -- per pixel tile to
+  // bnpart (same layout as bn_nhwc_partial_k<true>), so the BN backward skips its statistics
+  // pass over dy and x.  bx: the BN's input; bmean: its batch mean; the ReLU mask from the
+  // forward's (scale, shift) (bfcoef, ReLU without residual) or from its mask bits (bmask), or none.
+  const bf16* bx;
+  const float* bmean;
+  const float* bfcoef;
+  const uint8_t* bmask;
+  int brelu;
   FastDiv fOW, fOHW, fCa, fS, fWc, fHWc;
 };
+
+// Backward BN statistics of one 8-channel vector of the stored data gradient (see ConvNArgs::bx):
+// g = v masked, s1 += g, s2 += g (x - mean).  The loads of x / mask are issued by the caller.
+__device__ __forceinline__ void bn_bwd_acc8(const ConvNArgs& a, const u32x4& v, const uint4& xr, uint32_t mb,
+                                            const float* mean8, const float* sc8, const float* sh8, float* s1,
+                                            float* s2) {
+  float g[8], xv[8];
+  unpack8(make_uint4(v[0], v[1], v[2], v[3]), g);
+  unpack8(xr, xv);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    if (a.brelu) {
+      const bool live = a.bfcoef ? fmaf(xv[e], sc8[e], sh8[e]) > 0.f : ((mb >> e) & 1u) != 0u;
+      g[e] = live ? g[e] : 0.f;
+    }
+    s1[e] += g[e];
+    s2[e] = fmaf(g[e], xv[e] - mean8[e], s2[e]);
+  }
+}
+
+// The per-thread sums of a fixed 8-channel vector cv (threads tid = cv mod VPR) reduced in LDS
+// in a fixed order and written as partial row `row` (channels ch0 .. ch0 + 8 VPR - 1).
+template <int NT, int VPR>
+__device__ __forceinline__ void bn_bwd_flush(const ConvNArgs& a, float* red, const float* s1, const float* s2,
+                                             int row, int ch0) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[e * NT + tid] = s1[e];
+    red[(8 + e) * NT + tid] = s2[e];
+  }
+  __syncthreads();
+  if (tid < 8 * VPR) {
+    const int cv = tid >> 3, e = tid & 7, ch = ch0 + tid;
+    float t1 = 0.f, t2 = 0.f;
+    for (int k = 0; k < NT / VPR; ++k) {
+      t1 += red[e * NT + cv + k * VPR];
+      t2 += red[(8 + e) * NT + cv + k * VPR];
+    }
+    if (ch < a.Ng) {
+      float* dst = a.bnpart + (size_t)row * 2 * a.Ng + 2 * ch;
+      dst[0] = t1;
+      dst[1] = t2;
+    }
+  }
+}
 
 // __launch_bounds__(256, 2): at least two waves per SIMD (<= 256 VGPRs); the LDS tiles allow two
 // 256-thread blocks per CU anyway, so a larger register budget would only lose occupancy
@@ -354,6 +411,19 @@ __global__ __launch_bounds__(256, 2) void conv_nhwc_kernel(ConvNArgs a) {
   }
   __syncthreads();
   constexpr int VPR = TM / 8;  // 16-byte vectors per pixel row
+  // backward BN statistics (a.bx): this thread's channel vector is fixed (256 % VPR == 0)
+  const bool bst = a.bx != nullptr;
+  float s1[8], s2[8], mean8[8], sc8[8], sh8[8];
+  if (bst) {
+    const int ch = min(ch0 + 8 * (tid % VPR), a.Ng - 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] = s2[e] = 0.f;
+      mean8[e] = a.bmean[ch + e];
+      sc8[e] = a.bfcoef ? a.bfcoef[2 * (ch + e)] : 0.f;
+      sh8[e] = a.bfcoef ? a.bfcoef[2 * (ch + e) + 1] : 0.f;
+    }
+  }
 #pragma unroll
   for (int v = tid; v < TN * VPR; v += 256) {
     const int row = v / VPR, cv = v - row * VPR;
@@ -361,10 +431,23 @@ __global__ __launch_bounds__(256, 2) void conv_nhwc_kernel(ConvNArgs a) {
     if (px < Mc && ch < a.Ng)
     {
       const size_t o = (size_t)pfull(px) * a.Ng + ch;
+      uint4 xr = make_uint4(0u, 0u, 0u, 0u);
+      uint32_t mb = 0u;
+      if (bst) {  // issued before the addend / tile reads so their latencies overlap
+        xr = *reinterpret_cast<const uint4*>(a.bx + o);
+        if (a.bmask) mb = a.bmask[o >> 3];
+      }
       u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
       if (a.addend) v = add8(v, *reinterpret_cast<const u32x4*>(a.addend + o));
       *reinterpret_cast<u32x4*>(a.out + o) = v;
+      if (bst) bn_bwd_acc8(a, v, xr, mb, mean8, sc8, sh8, s1, s2);
     }
+  }
+  if (bst) {
+    __syncthreads();  // every read of the C tile is done: its LDS becomes the reduction buffer
+    // partial row = (parity class, pixel tile): rows_per_class = ceil(Mc / TN)
+    bn_bwd_flush<256, VPR>(a, reinterpret_cast<float*>(&As[0][0]), s1, s2,
+                           (int)blockIdx.z * ((Mc + TN - 1) / TN) + px0 / TN, ch0);
   }
 }
 
@@ -390,6 +473,8 @@ __device__ __forceinline__ void glds16(const void* src, void* lds) {
   __builtin_amdgcn_global_load_lds(src, (lds_void_t*)lds, 16, 0, 0);
 }
 
+// STATS: the forward BN-statistics epilogue (bnpart / bnshift); the backward BN-statistics
+// epilogue of a data gradient runs whenever a.bx is set (ConvNArgs::bx)
 template <int TM, bool STATS = false>
 __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
   constexpr int TN = 256, BK = 64, NS = 3;
@@ -521,6 +606,18 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
   }
   __syncthreads();
   constexpr int VPR = TM / 8;
+  const bool bst = !STATS && a.bx != nullptr;  // backward BN statistics (fixed vector per thread)
+  float s1[8], s2[8], mean8[8], sc8[8], sh8[8];
+  if (bst) {
+    const int ch = min(ch0 + 8 * (tid % VPR), a.Ng - 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] = s2[e] = 0.f;
+      mean8[e] = a.bmean[ch + e];
+      sc8[e] = a.bfcoef ? a.bfcoef[2 * (ch + e)] : 0.f;
+      sh8[e] = a.bfcoef ? a.bfcoef[2 * (ch + e) + 1] : 0.f;
+    }
+  }
 #pragma unroll
   for (int v = tid; v < TN * VPR; v += 512) {
     const int row = v / VPR, cv = v - row * VPR;
@@ -528,10 +625,23 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
     if (px < a.M && ch < a.Ng)
     {
       const size_t o = (size_t)px * a.Ng + ch;
+      uint4 xr = make_uint4(0u, 0u, 0u, 0u);
+      uint32_t mb = 0u;
+      if (bst) {
+        xr = *reinterpret_cast<const uint4*>(a.bx + o);
+        if (a.bmask) mb = a.bmask[o >> 3];
+      }
       u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
       if (a.addend) v = add8(v, *reinterpret_cast<const u32x4*>(a.addend + o));
       *reinterpret_cast<u32x4*>(a.out + o) = v;
+      if (bst) bn_bwd_acc8(a, v, xr, mb, mean8, sc8, sh8, s1, s2);
     }
+  }
+  if (bst) {
+    // reduction slots after the C tile in the (idle) stage buffers
+    float* bred = reinterpret_cast<float*>(smem + ((TN * CP * 2 + 255) & ~255));
+    static_assert(((TN * CP * 2 + 255) & ~255) + 16 * 512 * 4 <= NS * SB, "BN reduction slots must fit");
+    bn_bwd_flush<512, VPR>(a, bred, s1, s2, px0 / TN, ch0);
   }
   if constexpr (STATS) {  // BN statistics of the stored (bf16) tile: 512 / TM threads per channel
     constexpr int TPC = 512 / TM, RPT = TN / TPC, U = 8;
@@ -2168,8 +2278,9 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   a.fS = FastDiv(a.S);
   if (c3_eligible(a) && conv_c3_mode()) {  // persistent band kernel (forward or data gradient)
     const int rt = c3_band_rows(a.OH, a.OW), nb = a.M / (rt * a.OW);
-    // BN rows: one per band (nhwc_conv_bn_rows sized the buffer for them)
+    // BN rows: one per band (nhwc_conv_bn_rows sized the buffer for them); no backward statistics
     if (!(a.bnpart && !a.dgrad && nb <= 16384)) a.bnpart = nullptr;
+    a.bx = nullptr;
     const int blocks = std::min(nb, 256);
     if (a.bnpart) MX_LAUNCH(conv3x3_s1_c64_kernel<true>, dim3(blocks), dim3(512), 0, st, a, rt, nb);
     else MX_LAUNCH(conv3x3_s1_c64_kernel<false>, dim3(blocks), dim3(512), 0, st, a, rt, nb);
@@ -2191,9 +2302,13 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     a.kt_per_split = gp.kt_per_split;
     a.part = gp.splits > 1 ? scratch : nullptr;
     const int gx = cdiv(a.M, 256);
-    if (!(a.bnpart && !a.dgrad && gp.splits == 1 && gx <= 16384)) a.bnpart = nullptr;
+    // epilogue BN statistics (forward: bnpart / bnshift; data gradient: bx, see ConvNArgs) need
+    // the whole reduction in one block: no split-K
+    const bool bst = a.dgrad && a.bx && a.bnpart && gp.splits == 1 && gx <= 16384;
+    if (!bst) a.bx = nullptr;
+    if (!(a.bnpart && (bst || (!a.dgrad && gp.splits == 1)) && gx <= 16384)) a.bnpart = nullptr;
     const dim3 grid(cdiv(a.Ng, gp.tm) * cdiv(a.M, 256), gp.splits);
-    if (a.bnpart) {
+    if (a.bnpart && !bst) {
       if (gp.tm == 128) MX_LAUNCH((conv_nhwc_glds_kernel<128, true>), grid, dim3(512), 0, st, a);
       else MX_LAUNCH((conv_nhwc_glds_kernel<64, true>), grid, dim3(512), 0, st, a);
     } else {
@@ -2207,7 +2322,6 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     }
     return a.bnpart ? gx : 0;
   }
-  a.bnpart = nullptr;
   a.par = cs.par ? 1 : 0;
   if (cs.par) {
     a.Hc = a.OH / 2;
@@ -2221,6 +2335,13 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   }
   a.kt_per_split = p.kt_per_split;
   a.part = p.splits > 1 ? scratch : nullptr;
+  // backward BN statistics in the epilogue: one partial row per (parity class, pixel tile)
+  const int Mc = cs.par ? a.M / 4 : a.M, brows = (cs.par ? 4 : 1) * cdiv(Mc, p.tn);
+  const bool bst = a.dgrad && a.bx && a.bnpart && p.splits == 1 && brows <= 16384;
+  if (!bst) {
+    a.bx = nullptr;
+    a.bnpart = nullptr;
+  }
   const dim3 grid(p.blocks, p.splits, cs.par ? 4 : 1);
   if (p.tm == 128) {
     if (wide) MX_LAUNCH((conv_nhwc_kernel<128, 128, true>), grid, dim3(256), 0, st, a);
@@ -2237,7 +2358,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, p.splits,
               a.addend);
   }
-  return 0;
+  return bst ? brows : 0;
 }
 
 int nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int H, int W, int Cp, int K, int R,
@@ -2311,12 +2432,30 @@ size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, 
   return splits > 1 ? (size_t)splits * a.M * a.Ng : 0;
 }
 
-void nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
-                     int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st,
-                     const uint16_t* addend) {
+int nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
+                    int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st,
+                    const uint16_t* addend, float* bnpart, const uint16_t* bx, const float* bmean,
+                    const float* bfcoef, const uint8_t* bmask, bool brelu) {
   ConvNArgs a = dgrad_args(dy, wt_d, dx, N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q);
   a.addend = addend;
-  launch_conv(a, scratch, st);
+  if (bnpart && bx && bmean) {
+    MX_CHECK(!brelu || bfcoef || bmask, "nhwc dgrad BN statistics: a ReLU needs the forward's coefficients or mask");
+    a.bnpart = bnpart;
+    a.bx = reinterpret_cast<const bf16*>(bx);
+    a.bmean = bmean;
+    a.bfcoef = brelu ? bfcoef : nullptr;
+    a.bmask = (brelu && !bfcoef) ? bmask : nullptr;
+    a.brelu = brelu ? 1 : 0;
+  }
+  return launch_conv(a, scratch, st);
+}
+
+int nhwc_conv_dgrad_bn_rows(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int P,
+                            int Q) {
+  // upper bound of the partial rows the data gradient's epilogue writes (the LDS-DMA kernel: one
+  // per 256-pixel tile; the generic kernel: one per (parity class, pixel tile) of >= 64 pixels)
+  const int M = N * H * W;
+  return std::max(cdiv(M, 256), cdiv(M, 64) + 4);
 }
 
 static void wgrad_tile(int K, int Ng, int& tm, int& tn) {
@@ -2467,7 +2606,7 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
 void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma, const float* mean,
                  const float* invstd, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, int Npix, int C,
                  bool relu, bool accumulate_params, float* scratch, hipStream_t st, const float* fcoef,
-                 const uint8_t* mask) {
+                 const uint8_t* mask, const float* pre_part, int pre_gx) {
   const int V = C / 8;
   MX_CHECK(C % 8 == 0 && C <= 2048 && (V >= kBnT ? V % kBnT == 0 : kBnT % V == 0),
            "nhwc bn: unsupported channel count");
@@ -2493,7 +2632,13 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
   a.fcoef = (relu && fcoef && C <= 512) ? fcoef : nullptr;
   a.mask = (relu && !a.fcoef) ? const_cast<uint8_t*>(mask) : nullptr;
   MX_CHECK(!relu || a.fcoef || a.mask || y, "nhwc bn bwd: ReLU needs y, the forward's mask or its coefficients");
-  MX_LAUNCH(bn_nhwc_partial_k<true>, g, dim3(kBnT), 0, st, a);
+  if (pre_part) {  // the consuming conv's data-gradient epilogue wrote the partial sums
+    MX_CHECK(pre_gx >= 1 && pre_gx <= 16384, "nhwc bn bwd: precomputed partial rows out of range");
+    a.part = const_cast<float*>(pre_part);
+    a.gx = pre_gx;
+  } else {
+    MX_LAUNCH(bn_nhwc_partial_k<true>, g, dim3(kBnT), 0, st, a);
+  }
   MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
   if (a.fcoef) MX_LAUNCH(bn_nhwc_bwd_apply_k<true>, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));

@@ -195,10 +195,18 @@ void nhwc_conv_set_glds(int mode);
 // split-K scratch of nhwc_conv_dgrad (floats; 0 = none needed)
 size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
                                       int P, int Q);
-// addend (optional, bf16 [N][H][W][C]): dx = conv_transpose(dy) + addend, summed in the epilogue
-void nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
-                     int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st,
-                     const uint16_t* addend = nullptr);
+// addend (optional, bf16 [N][H][W][C]): dx = conv_transpose(dy) + addend, summed in the epilogue.
+// bnpart / bx / bmean (optional): dx is the output gradient of a training BatchNorm with input bx
+// and batch mean bmean (ReLU mask from bfcoef or bmask when brelu): the epilogue writes that BN's
+// backward partial sums to bnpart (at most nhwc_conv_dgrad_bn_rows rows of 2 C floats).  Returns
+// the rows written (0: the kernel chosen for this shape cannot, the BN runs its own pass).
+int nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
+                    int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st,
+                    const uint16_t* addend = nullptr, float* bnpart = nullptr, const uint16_t* bx = nullptr,
+                    const float* bmean = nullptr, const float* bfcoef = nullptr, const uint8_t* bmask = nullptr,
+                    bool brelu = false);
+int nhwc_conv_dgrad_bn_rows(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int P,
+                            int Q);
 // dw fp32 [K][Cin][R][S] (+)= ...; x has Cp >= Cin channels (padding ignored);
 // scratch: nhwc_wgrad_scratch_floats(...) floats of per-split partial sums
 size_t nhwc_wgrad_scratch_floats(int N, int Cp, int K, int R, int S, int P, int Q);
@@ -218,7 +226,10 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
 void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma, const float* mean,
                  const float* invstd, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, int Npix, int C,
                  bool relu, bool accumulate_params, float* scratch, hipStream_t st,
-                 const float* fcoef = nullptr, const uint8_t* mask = nullptr);  // fcoef: the forward's coef_out (ReLU, no residual,
+                 const float* fcoef = nullptr, const uint8_t* mask = nullptr,
+                 // backward partial sums already written by the consuming conv's data-gradient
+                 // epilogue (nhwc_conv_dgrad's bnpart): the statistics pass over dy and x is skipped
+                 const float* pre_part = nullptr, int pre_gx = 0);  // fcoef: the forward's coef_out (ReLU, no residual,
                                                  // C <= 512): mask from x, y not read
 void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, int k,
                       int s, int p, hipStream_t st);

@@ -97,6 +97,30 @@ class WeightPack:
         return self._views.get(id(w))
 
 
+class _BnLink:
+    """What the data gradient of a convolution needs to compute the backward statistics of the
+    training BatchNorm whose output it consumes (csrc/nhwc_bf16.hip ConvNArgs::bx): the BN's
+    input, batch mean and ReLU-mask source.  The BN forward attaches it to its output; the
+    consumer conv's backward fills ``pre`` (partials, rows, data pointer of the gradient it
+    wrote) and the BN backward uses it when that gradient is exactly its dy.  ``join``: the
+    output also feeds a residual shortcut (fork): the conv's gradient is the BN's whole output
+    gradient only when the shortcut's gradient was added in its epilogue."""
+
+    __slots__ = ("x", "mean", "fcoef", "mask", "relu", "join", "pre")
+
+    def __init__(self, x, mean, fcoef, mask, relu):
+        self.x, self.mean, self.fcoef, self.mask, self.relu = x, mean, fcoef, mask, relu
+        self.join = None
+        self.pre = None
+
+
+def _bn_link_of(x):
+    link = getattr(x, "_mx_bnlink", None)
+    if link is None or link[1] != x._version:  # written in place since the BN: not its output any more
+        return None
+    return link[0]
+
+
 class GradJoin:
     """Joins the two input-gradient branches of a residual block without a separate add: the
     shortcut branch leaves its input gradient here -- the block's last batch norm (whose ``res``
@@ -132,13 +156,20 @@ class _Fork(torch.autograd.Function):
 def fork(x, join: GradJoin):
     """(main, shortcut) aliases of a residual block's input; pass ``join`` to the block's first
     conv2d and last batch_norm so the two gradients are summed inside the conv's epilogue."""
-    return _Fork.apply(x, join)
+    link = _bn_link_of(x)
+    main, short = _Fork.apply(x, join)
+    if link is not None:  # only the main branch's conv may compute the producing BN's statistics
+        link.join = join
+        main._mx_bnlink = (link, main._version)
+    return main, short
 
 
 class _Conv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, pad, packed=None, join=None, deposit=None, bnstat=None):
         Cn = native()
+        # the BN that produced x (its backward statistics can ride this conv's data gradient)
+        ctx.bnlink = _bn_link_of(x) if (_BN_STATS_IN_DGRAD and ctx.needs_input_grad[0]) else None
         N, H, W, Cp = x.shape
         K, C, R, S = w.shape
         sh, sw = stride
@@ -186,8 +217,22 @@ class _Conv(torch.autograd.Function):
             scr = torch.empty((n,), device=dy.device, dtype=torch.float32) if n else None
             j = ctx.join
             add = j.dres if j is not None and j.dres is not None and j.dres.shape == dx.shape else None
-            Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx.data_ptr(), N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q,
-                               _p(scr), st, _p(add))
+            link = ctx.bnlink
+            if link is not None and link.join is not None and add is None:
+                link = None  # the shortcut's gradient is not in this sum: not the BN's whole dy
+            bpart = None
+            if link is not None and link.x.shape == dx.shape:
+                rows = Cn.nhwc_conv_dgrad_bn_rows(N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q)
+                bpart = torch.empty((rows * 2 * C,), device=dy.device, dtype=torch.float32)
+            rows = Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx.data_ptr(), N, H, W, C, K, R, S, sh, sw, ph, pw,
+                                      P, Q, _p(scr), st, _p(add), _p(bpart),
+                                      _p(link.x) if bpart is not None else 0,
+                                      _p(link.mean) if bpart is not None else 0,
+                                      _p(link.fcoef) if bpart is not None else 0,
+                                      _p(link.mask) if bpart is not None else 0,
+                                      bool(link.relu) if bpart is not None else False)
+            if bpart is not None and rows > 0:
+                link.pre = (bpart, rows, dx.data_ptr())
             if add is not None:
                 j.consumed = True
             if ctx.deposit is not None:
@@ -229,8 +274,12 @@ def conv2d(x, w, stride=1, padding=0, pack: WeightPack | None = None, join: Grad
     return y
 
 
-# MXDDP_BN_STATS_IN_CONV=0: every BN runs its own statistics pass (A/B switch)
+# MXDDP_BN_STATS_IN_CONV=0: every BN runs its own statistics passes, forward and backward (A/B
+# switch for the conv-epilogue statistics)
 _BN_STATS_IN_CONV = os.environ.get("MXDDP_BN_STATS_IN_CONV", "1") == "1"
+_BN_STATS_IN_DGRAD = _BN_STATS_IN_CONV
+# how many BN backward passes took their statistics from a conv epilogue / ran their own pass
+BN_BWD_STATS = {"epilogue": 0, "pass": 0}
 
 
 class _BN(torch.autograd.Function):
@@ -259,6 +308,9 @@ class _BN(torch.autograd.Function):
         ctx.relu, ctx.has_res = bool(relu), res is not None
         ctx.join = join
         ctx.refs = (gamma, beta)
+        # for the consuming conv's data gradient: its epilogue can compute this BN's backward
+        # statistics (the mask source must be the one this backward uses: fcoef, else the bits)
+        ctx.link = _BnLink(x, mean, fcoef, mask, bool(relu))
         return y
 
     @staticmethod
@@ -274,9 +326,17 @@ class _BN(torch.autograd.Function):
         direct = gs is not None and bs is not None
         dg, db = (gs, bs) if direct else (torch.empty((C,), device=x.device), torch.empty((C,), device=x.device))
         scr = torch.empty((Cn.nhwc_bn_scratch_floats(N * H * W, C),), device=x.device, dtype=torch.float32)
+        # backward statistics from the consuming conv's data-gradient epilogue, valid only for
+        # exactly the gradient tensor that conv wrote
+        pre = ctx.link.pre
+        ctx.link.pre = None
+        if pre is not None and pre[2] != dy.data_ptr():
+            pre = None
+        BN_BWD_STATS["epilogue" if pre is not None else "pass"] += 1
         Cn.nhwc_bn_bwd(dy.data_ptr(), x.data_ptr(), 0, _p(gamma), mean.data_ptr(), invstd.data_ptr(),
                        dx.data_ptr(), _p(dres), dg.data_ptr(), db.data_ptr(), N * H * W, C, ctx.relu, direct,
-                       scr.data_ptr(), stream_of(dy), _p(ctx.fcoef), _p(ctx.mask))
+                       scr.data_ptr(), stream_of(dy), _p(ctx.fcoef), _p(ctx.mask),
+                       _p(pre[0]) if pre is not None else 0, pre[1] if pre is not None else 0)
         if direct:
             dg = db = None
         if ctx.join is not None and dres is not None:
@@ -301,8 +361,11 @@ def batch_norm(x, bn: torch.nn.BatchNorm2d, relu: bool = False, res: torch.Tenso
             pre = None
         if pre is not None:
             pre = pre[:3]
-        return _BN.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, res, relu, mom, bn.eps, join,
-                         pre)
+        y = _BN.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, nbt, res, relu, mom, bn.eps, join, pre)
+        link = getattr(y.grad_fn, "link", None)  # the node is the Function's ctx
+        if link is not None:
+            y._mx_bnlink = (link, y._version)
+        return y
     y = (x.float() - bn.running_mean) * torch.rsqrt(bn.running_var + bn.eps) * bn.weight + bn.bias
     if res is not None:
         y = y + res.float()

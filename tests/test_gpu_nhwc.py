@@ -214,6 +214,78 @@ def test_bn_statistics_from_conv_epilogue(cuda, shape, offset):
         assert _rel(b, a) < 2e-2
 
 
+@pytest.mark.parametrize("glds,stride,relu", [(2, 1, True), (2, 1, False), (0, 1, True), (0, 2, True),
+                                              (0, 1, False)])
+def test_bn_backward_statistics_from_dgrad_epilogue(cuda, glds, stride, relu):
+    """BN -> conv: the conv's data-gradient epilogue computes the BN's backward partial sums
+    (sum g, sum g (x - mean), g masked by the BN's fused ReLU) and the BN backward skips its
+    statistics pass.  Same input / weight / BN-parameter gradients as the separate pass, on the
+    LDS-DMA kernel (glds 2: forced) and the generic kernel incl. the stride-2 parity classes (glds 0)."""
+    from mxddp import native
+
+    C = native()
+    N, Cin, H, W, K = 4, 64, 16, 16, 128
+    torch.manual_seed(11)
+    x = (torch.randn(N, H, W, Cin) + 0.5).to(torch.bfloat16).to(cuda)
+    w = (torch.randn(K, Cin, 3, 3) * 0.05).to(cuda)
+    outs, used = [], []
+    try:
+        C.nhwc_conv_set_glds(glds)
+        for fused in (False, True):
+            nhwc._BN_STATS_IN_DGRAD = fused
+            bn = nn.BatchNorm2d(Cin).to(cuda)
+            with torch.no_grad():
+                bn.weight.copy_(torch.rand(Cin) + 0.5)
+                bn.bias.copy_(torch.randn(Cin) * 0.2)
+            xg = x.clone().requires_grad_()
+            wg = w.clone().requires_grad_()
+            before = dict(nhwc.BN_BWD_STATS)
+            y = nhwc.batch_norm(xg, bn, relu=relu)
+            c = nhwc.conv2d(y, wg, stride, 1)
+            gy = torch.randn(c.shape, generator=torch.Generator().manual_seed(4)).to(torch.bfloat16).to(cuda)
+            c.backward(gy)
+            torch.cuda.synchronize()
+            used.append(nhwc.BN_BWD_STATS["epilogue"] - before["epilogue"])
+            outs.append((xg.grad.float().cpu(), wg.grad.cpu(), bn.weight.grad.cpu(), bn.bias.grad.cpu()))
+    finally:
+        nhwc._BN_STATS_IN_DGRAD = nhwc._BN_STATS_IN_CONV
+        C.nhwc_conv_set_glds(1)
+    assert used == [0, 1], used  # the fused run really took the epilogue's statistics
+    for a, b in zip(*outs):
+        assert _rel(b, a) < 2e-2
+
+
+def test_bn_backward_statistics_residual_join(cuda):
+    """A residual block's output BN (ReLU after the residual add, mask bits) feeding the next
+    block's first conv and its identity shortcut: the statistics come from the conv's epilogue only
+    when the shortcut's gradient was joined there; the block gradients match the separate pass."""
+    from mxddp.models.resnet import Bottleneck
+
+    torch.manual_seed(12)
+    blocks = [Bottleneck(256, 64).to(cuda) for _ in range(2)]
+    x = torch.randn(2, 14, 14, 256).to(torch.bfloat16).to(cuda)
+    outs, used = [], []
+    try:
+        for fused in (False, True):
+            nhwc._BN_STATS_IN_DGRAD = fused
+            for blk in blocks:
+                blk.zero_grad()
+            xg = x.clone().requires_grad_()
+            before = dict(nhwc.BN_BWD_STATS)
+            y = blocks[1].forward_nhwc(blocks[0].forward_nhwc(xg))
+            gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(8)).to(torch.bfloat16).to(cuda)
+            y.backward(gy)
+            torch.cuda.synchronize()
+            used.append(nhwc.BN_BWD_STATS["epilogue"] - before["epilogue"])
+            grads = [p.grad.cpu() for blk in blocks for p in blk.parameters()]
+            outs.append((xg.grad.float().cpu(), *grads))
+    finally:
+        nhwc._BN_STATS_IN_DGRAD = nhwc._BN_STATS_IN_CONV
+    assert used[0] == 0 and used[1] >= 4, used  # bn1 / bn2 of both blocks at least
+    for a, b in zip(*outs):
+        assert _rel(b, a) < 3e-2
+
+
 @pytest.mark.parametrize("offset", [0.0, 3.0])
 def test_stem_kernel_bn_statistics(cuda, offset):
     """The stem kernel (7x7 / 2, 8-channel input, 16 x 16 output tiles) writes the BN partial sums
