@@ -80,6 +80,19 @@ __device__ __forceinline__ u32x4 add8(u32x4 c, u32x4 d) {
   const uint4 r = pack8(x);
   return u32x4{r.x, r.y, r.z, r.w};
 }
+// the 8 bf16 of d with element e zeroed unless bit e of mb is set (ReLU mask bits)
+__device__ __forceinline__ u32x4 mask8(u32x4 d, uint32_t mb) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    d[j] &= ((mb >> (2 * j)) & 1u ? 0x0000ffffu : 0u) | ((mb >> (2 * j + 1)) & 1u ? 0xffff0000u : 0u);
+  return d;
+}
+// epilogue of a data gradient: the residual join's addend, optionally masked by its ReLU bits
+__device__ __forceinline__ u32x4 join8(u32x4 v, const bf16* addend, const uint8_t* amask, size_t o) {
+  u32x4 d = *reinterpret_cast<const u32x4*>(addend + o);
+  if (amask) d = mask8(d, amask[o >> 3]);
+  return add8(v, d);
+}
 
 // ------------------------------------------------------------------------------------------
 // forward / data-gradient implicit GEMM
@@ -100,6 +113,9 @@ struct ConvNArgs {
   int par, Hc, Wc;
   const bf16* addend;  // data gradient: added to the result in the epilogue ([M][Ng], or null) -- a
                        // residual block's two input-gradient branches joined without another pass
+  const uint8_t* amask;  // addend masked by these ReLU bits (bit e of byte o / 8), or null: the
+                         // identity shortcut's gradient taken straight from the block's output
+                         // gradient, never materialised by the last BN's backward
   // forward feeding a training BatchNorm (LDS-DMA kernel, no split): the epilogue writes the BN's
   // per-channel partial sums of (y - shift[c]) and its square over each 256-pixel tile to
   // bnpart[tile][2 Ng] (the layout bn_nhwc_partial_k writes), so the BN skips its statistics pass
@@ -438,7 +454,7 @@ __global__ __launch_bounds__(256, 2) void conv_nhwc_kernel(ConvNArgs a) {
         if (a.bmask) mb = a.bmask[o >> 3];
       }
       u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
-      if (a.addend) v = add8(v, *reinterpret_cast<const u32x4*>(a.addend + o));
+      if (a.addend) v = join8(v, a.addend, a.amask, o);
       *reinterpret_cast<u32x4*>(a.out + o) = v;
       if (bst) bn_bwd_acc8(a, v, xr, mb, mean8, sc8, sh8, s1, s2);
     }
@@ -632,7 +648,7 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
         if (a.bmask) mb = a.bmask[o >> 3];
       }
       u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
-      if (a.addend) v = add8(v, *reinterpret_cast<const u32x4*>(a.addend + o));
+      if (a.addend) v = join8(v, a.addend, a.amask, o);
       *reinterpret_cast<u32x4*>(a.out + o) = v;
       if (bst) bn_bwd_acc8(a, v, xr, mb, mean8, sc8, sh8, s1, s2);
     }
@@ -960,7 +976,7 @@ __global__ __launch_bounds__(512) void conv3x3_s1_c64_kernel(ConvNArgs a, int rt
       if (px < npx) {
         const size_t o = obase + (size_t)px * 64 + 8 * cv;
         u32x4 val = *reinterpret_cast<const u32x4*>(Cs + px * CP + 8 * cv);
-        if (a.addend) val = add8(val, *reinterpret_cast<const u32x4*>(a.addend + o));
+        if (a.addend) val = join8(val, a.addend, a.amask, o);
         *reinterpret_cast<u32x4*>(a.out + o) = val;
       }
     }
@@ -1007,7 +1023,8 @@ static bool stem_eligible(const ConvNArgs& a) {
 
 // split-K epilogue: out (bf16) = sum over splits of the fp32 partials (fixed order)
 __global__ void conv_nhwc_splitk_reduce_k(const float* __restrict__ part, bf16* __restrict__ out, int64_t n4,
-                                          int splits, const bf16* __restrict__ addend) {
+                                          int splits, const bf16* __restrict__ addend,
+                                          const uint8_t* __restrict__ amask) {
   const float4* p4 = reinterpret_cast<const float4*>(part);
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     float4 s = p4[i];
@@ -1016,7 +1033,12 @@ __global__ void conv_nhwc_splitk_reduce_k(const float* __restrict__ part, bf16* 
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
     if (addend) {
-      const uint2 d = reinterpret_cast<const uint2*>(addend)[i];
+      uint2 d = reinterpret_cast<const uint2*>(addend)[i];
+      if (amask) {  // 4 elements: bits 4 (i & 1) .. + 3 of byte i / 2
+        const uint32_t mb = (uint32_t)amask[i >> 1] >> (4 * (i & 1));
+        d.x &= (mb & 1u ? 0x0000ffffu : 0u) | (mb & 2u ? 0xffff0000u : 0u);
+        d.y &= (mb & 4u ? 0x0000ffffu : 0u) | (mb & 8u ? 0xffff0000u : 0u);
+      }
       s.x += bf2f(d.x & 0xffffu); s.y += bf2f(d.x >> 16); s.z += bf2f(d.y & 0xffffu); s.w += bf2f(d.y >> 16);
     }
     reinterpret_cast<uint2*>(out)[i] = make_uint2(pack2(s.x, s.y), pack2(s.z, s.w));
@@ -2318,7 +2340,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     if (gp.splits > 1) {
       const int64_t n4 = (int64_t)a.M * a.Ng / 4;
       MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, gp.splits,
-                a.addend);
+                a.addend, a.amask);
     }
     return a.bnpart ? gx : 0;
   }
@@ -2356,7 +2378,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   if (p.splits > 1) {
     const int64_t n4 = (int64_t)a.M * a.Ng / 4;
     MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, p.splits,
-              a.addend);
+              a.addend, a.amask);
   }
   return bst ? brows : 0;
 }
@@ -2435,9 +2457,10 @@ size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, 
 int nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
                     int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st,
                     const uint16_t* addend, float* bnpart, const uint16_t* bx, const float* bmean,
-                    const float* bfcoef, const uint8_t* bmask, bool brelu) {
+                    const float* bfcoef, const uint8_t* bmask, bool brelu, const uint8_t* amask) {
   ConvNArgs a = dgrad_args(dy, wt_d, dx, N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q);
   a.addend = addend;
+  a.amask = addend ? amask : nullptr;
   if (bnpart && bx && bmean) {
     MX_CHECK(!brelu || bfcoef || bmask, "nhwc dgrad BN statistics: a ReLU needs the forward's coefficients or mask");
     a.bnpart = bnpart;

@@ -200,11 +200,12 @@ size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, 
 // and batch mean bmean (ReLU mask from bfcoef or bmask when brelu): the epilogue writes that BN's
 // backward partial sums to bnpart (at most nhwc_conv_dgrad_bn_rows rows of 2 C floats).  Returns
 // the rows written (0: the kernel chosen for this shape cannot, the BN runs its own pass).
+// amask: the addend is masked by these ReLU bits (bit e of byte i / 8 for element i) before the add.
 int nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
                     int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st,
                     const uint16_t* addend = nullptr, float* bnpart = nullptr, const uint16_t* bx = nullptr,
                     const float* bmean = nullptr, const float* bfcoef = nullptr, const uint8_t* bmask = nullptr,
-                    bool brelu = false);
+                    bool brelu = false, const uint8_t* amask = nullptr);
 int nhwc_conv_dgrad_bn_rows(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int P,
                             int Q);
 // dw fp32 [K][Cin][R][S] (+)= ...; x has Cp >= Cin channels (padding ignored);

@@ -127,17 +127,27 @@ class GradJoin:
     is the identity shortcut), or the projection shortcut's convolution (``conv2d(..., deposit=)``)
     -- and the block's first convolution adds it in its data-gradient epilogue
     (``nhwc_conv_dgrad(..., addend)``).  ``fork`` then passes that sum through unchanged.  If the
-    first convolution's backward runs before the shortcut's, nothing is joined and ``fork`` adds."""
+    first convolution's backward runs before the shortcut's, nothing is joined and ``fork`` adds.
+    An identity shortcut's gradient is never materialised: the last BN leaves its own output
+    gradient and ReLU mask bits (``amask``), and the conv's epilogue masks while it adds."""
 
     def __init__(self):
         self.dres = None
+        self.amask = None
         self.consumed = False
+
+
+def _mask_bits(g, mask):
+    """g with element i zeroed unless bit i % 8 of mask[i // 8] is set (fallback of a lazy join)."""
+    bits = (mask.view(-1, 1) >> torch.arange(8, device=mask.device, dtype=torch.uint8)) & 1
+    return g * bits.view(g.shape).to(g.dtype)
 
 
 class _Fork(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, join):
         ctx.join = join
+        ctx.set_materialize_grads(False)  # a lazy identity join leaves g_short undefined
         return x.view_as(x), x.view_as(x)
 
     @staticmethod
@@ -145,11 +155,14 @@ class _Fork(torch.autograd.Function):
         j = ctx.join
         if j.consumed:  # g_main already includes g_short (added by the conv's epilogue)
             out = g_main
-        elif g_main is None or g_short is None:
-            out = g_main if g_short is None else g_short
         else:
-            out = g_main + g_short
-        j.dres, j.consumed = None, False
+            if g_short is None and j.dres is not None:  # lazy identity gradient, never joined
+                g_short = _mask_bits(j.dres, j.amask) if j.amask is not None else j.dres
+            if g_main is None or g_short is None:
+                out = g_main if g_short is None else g_short
+            else:
+                out = g_main + g_short
+        j.dres, j.amask, j.consumed = None, None, False
         return out, None
 
 
@@ -217,6 +230,7 @@ class _Conv(torch.autograd.Function):
             scr = torch.empty((n,), device=dy.device, dtype=torch.float32) if n else None
             j = ctx.join
             add = j.dres if j is not None and j.dres is not None and j.dres.shape == dx.shape else None
+            amask = j.amask if add is not None else None
             link = ctx.bnlink
             if link is not None and link.join is not None and add is None:
                 link = None  # the shortcut's gradient is not in this sum: not the BN's whole dy
@@ -230,13 +244,13 @@ class _Conv(torch.autograd.Function):
                                       _p(link.mean) if bpart is not None else 0,
                                       _p(link.fcoef) if bpart is not None else 0,
                                       _p(link.mask) if bpart is not None else 0,
-                                      bool(link.relu) if bpart is not None else False)
+                                      bool(link.relu) if bpart is not None else False, _p(amask))
             if bpart is not None and rows > 0:
                 link.pre = (bpart, rows, dx.data_ptr())
             if add is not None:
                 j.consumed = True
             if ctx.deposit is not None:
-                ctx.deposit.dres = dx  # picked up by the block's first conv (see GradJoin)
+                ctx.deposit.dres, ctx.deposit.amask = dx, None  # picked up by the block's first conv (GradJoin)
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(w)
             dw = sink if sink is not None else torch.empty_like(w)
@@ -278,6 +292,7 @@ def conv2d(x, w, stride=1, padding=0, pack: WeightPack | None = None, join: Grad
 # switch for the conv-epilogue statistics)
 _BN_STATS_IN_CONV = os.environ.get("MXDDP_BN_STATS_IN_CONV", "1") == "1"
 _BN_STATS_IN_DGRAD = _BN_STATS_IN_CONV
+_LAZY_JOIN = True  # identity-shortcut gradient masked in the joining conv's epilogue (tests flip it)
 # how many BN backward passes took their statistics from a conv epilogue / ran their own pass
 BN_BWD_STATS = {"epilogue": 0, "pass": 0}
 
@@ -320,7 +335,10 @@ class _BN(torch.autograd.Function):
         N, H, W, C = x.shape
         dy = dy.contiguous()
         dx = torch.empty_like(x)
-        dres = torch.empty_like(x) if ctx.has_res else None
+        # identity shortcut joined in the block's first conv: its gradient (dy masked by this BN's
+        # ReLU bits) is not written here, the conv's epilogue reads dy and the bits instead
+        lazy = ctx.has_res and ctx.join is not None and _LAZY_JOIN and (not ctx.relu or ctx.mask is not None)
+        dres = torch.empty_like(x) if (ctx.has_res and not lazy) else None
         g_ref, b_ref = ctx.refs
         gs, bs = _grad_sink(g_ref), _grad_sink(b_ref)
         direct = gs is not None and bs is not None
@@ -339,8 +357,10 @@ class _BN(torch.autograd.Function):
                        _p(pre[0]) if pre is not None else 0, pre[1] if pre is not None else 0)
         if direct:
             dg = db = None
-        if ctx.join is not None and dres is not None:
-            ctx.join.dres = dres  # picked up by the block's first conv (data-gradient epilogue)
+        if lazy:
+            ctx.join.dres, ctx.join.amask = dy, (ctx.mask if ctx.relu else None)
+        elif ctx.join is not None and dres is not None:
+            ctx.join.dres, ctx.join.amask = dres, None  # picked up by the block's first conv (epilogue)
         return dx, dg, db, None, None, None, dres, None, None, None, None, None
 
 

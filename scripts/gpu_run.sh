@@ -86,8 +86,8 @@ for step in "$@"; do
     keras_ws8) ws keras_ws8 8 --model keras_cnn --steps 100 --warmup 10 ;;
     pyr_ws8) ws pyr_ws8 8 --model pyramidnet110 --batch 8 --steps 5 --warmup 2 ;;
     rn_ws8) ws rn_ws8 8 --model resnet50 --dtype bf16 --batch 8 --steps 5 --warmup 2 ;;
-    copies_pyr) run copies_pyr 300 python scripts/diag_copies2.py pyramidnet110 fp32 ;;
-    copies_rn) run copies_rn 300 python scripts/diag_copies2.py resnet50 bf16 ;;
+    copies_pyr) run copies_pyr 300 python scripts/diag_copies.py pyramidnet110 fp32 64 ;;
+    copies_rn) run copies_rn 300 python scripts/diag_copies.py resnet50 bf16 32 ;;
     *) echo "gpu_run.sh: unknown step $step"; exit 2 ;;
   esac
 done

@@ -95,10 +95,12 @@ def test_conv_glds_kernel(cuda, case):
     assert _rel(wg.grad.cpu(), wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("masked", [False, True])
 @pytest.mark.parametrize("case", [(1, 256, 7, 7, 512, 3, 1, 1), (2, 64, 14, 14, 256, 1, 1, 0), (2, 64, 16, 32, 64, 3, 1, 1)])
-def test_conv_dgrad_addend(cuda, case):
+def test_conv_dgrad_addend(cuda, case, masked):
     """dx = conv_transpose(dy) + addend fused in the data-gradient epilogue (split-K reduction and
-    direct epilogue) == the two computed separately."""
+    direct epilogue) == the two computed separately; masked: the addend's elements are kept only
+    where their ReLU bit is set (the lazy identity-shortcut join)."""
     from mxddp import native
 
     Cn = native()
@@ -117,10 +119,11 @@ def test_conv_dgrad_addend(cuda, case):
     dx1 = torch.empty_like(dx0)
     Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx0.data_ptr(), N, H, W, C, K, R, R, st, st, pd, pd, P, Q,
                        scr.data_ptr() if n else 0, s)
+    bits = torch.randint(0, 256, (N * H * W * C // 8,), dtype=torch.uint8, device=cuda) if masked else None
     Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx1.data_ptr(), N, H, W, C, K, R, R, st, st, pd, pd, P, Q,
-                       scr.data_ptr() if n else 0, s, add.data_ptr())
+                       scr.data_ptr() if n else 0, s, add.data_ptr(), amask=bits.data_ptr() if masked else 0)
     torch.cuda.synchronize()
-    ref = dx0.float() + add.float()
+    ref = dx0.float() + (nhwc._mask_bits(add, bits) if masked else add).float()
     assert _rel(dx1, ref) < 1e-2
 
 
@@ -284,6 +287,34 @@ def test_bn_backward_statistics_residual_join(cuda):
     assert used[0] == 0 and used[1] >= 4, used  # bn1 / bn2 of both blocks at least
     for a, b in zip(*outs):
         assert _rel(b, a) < 3e-2
+
+
+def test_lazy_identity_join_equals_materialised(cuda):
+    """Identity residual blocks: the shortcut gradient masked inside the next conv's epilogue (bn3
+    writes no dres) == bn3 materialising dres, bit for bit (same bf16 values summed)."""
+    from mxddp.models.resnet import Bottleneck
+
+    torch.manual_seed(13)
+    blocks = [Bottleneck(256, 64).to(cuda) for _ in range(3)]
+    x = torch.randn(2, 14, 14, 256).to(torch.bfloat16).to(cuda)
+    outs = []
+    try:
+        for lazy in (False, True):
+            nhwc._LAZY_JOIN = lazy
+            for blk in blocks:
+                blk.zero_grad()
+            xg = x.clone().requires_grad_()
+            y = xg
+            for blk in blocks:
+                y = blk.forward_nhwc(y)
+            gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(3)).to(torch.bfloat16).to(cuda)
+            y.backward(gy)
+            torch.cuda.synchronize()
+            outs.append([xg.grad.float().cpu()] + [p.grad.cpu() for blk in blocks for p in blk.parameters()])
+    finally:
+        nhwc._LAZY_JOIN = True
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("offset", [0.0, 3.0])
