@@ -428,6 +428,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_overlap", &KerasEngine::set_overlap)
       .def("set_bucket_padding", &KerasEngine::set_bucket_padding)
       .def("set_external_batch", &KerasEngine::set_external_batch)
+      .def("set_coscheduled", &KerasEngine::set_coscheduled)
+      .def_property_readonly("coscheduled", &KerasEngine::coscheduled)
       .def_property_readonly("graph_mode", &KerasEngine::graph_mode)
       .def_property_readonly("merged", &KerasEngine::merged)
       .def_property_readonly("overlap", &KerasEngine::overlap)

@@ -118,6 +118,10 @@ void KerasEngine::launch_step() {
     return;
   }
   keras_fused_update(f, 1, 1.f, s_);  // finalize into g
+  if (coscheduled_) {
+    keras_fused_exchange_adam(f, co_args_, s_);  // exchange + average + Adam in one launch
+    return;
+  }
   reducer_->prepare();
   reducer_->mark_bucket_ready(0, s_);  // sum all-reduce of g
   reducer_->finalize(s_);
@@ -150,6 +154,18 @@ void KerasEngine::set_comm(Comm* c) {
 void KerasEngine::set_peer(PeerComm* p) {
   if (p != reducer_->peer()) uncapture();
   reducer_->set_peer(p);
+  if (coscheduled_) set_coscheduled(true);  // re-derive the arguments, or drop the mode
+}
+
+bool KerasEngine::set_coscheduled(bool on) {
+  if (on) {
+    PeerComm* pc = reducer_->peer();
+    on = pc && reducer_->active() && keras_exchange_blocks() <= kPeerMaxBlocks &&
+         pc->oneshot_args(f_.g, KerasLayout::total, RedOp::kAvg, &co_args_);
+  }
+  if (on != coscheduled_) uncapture();
+  coscheduled_ = on;
+  return on;
 }
 
 void KerasEngine::set_force_collectives(bool on) {

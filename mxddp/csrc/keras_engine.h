@@ -51,6 +51,10 @@ class KerasEngine {
   void set_bucket_padding(size_t capacity, size_t multiple) {
     reducer_->set_padding(KerasLayout::total, capacity, multiple);
   }
+  // peer transport: the exchange co-scheduled with Adam in one launch (keras_fused_exchange_adam)
+  // instead of a separate all-reduce; false (and off) when no opened peer transport can take it
+  bool set_coscheduled(bool on);
+  bool coscheduled() const { return coscheduled_; }
   void set_external_batch(bool on) { external_ = on; }
   int world_size() const;
   bool reducer_active() const { return reducer_->active(); }
@@ -70,6 +74,8 @@ class KerasEngine {
   Comm* comm_;
   uint64_t seed_;
   bool external_ = false;
+  bool coscheduled_ = false;
+  PeerArgs co_args_{};
   hipStream_t s_ = nullptr;
   std::unique_ptr<Reducer> reducer_;
   GraphRunner graphs_;

@@ -8,6 +8,8 @@
 
 #include <cstdint>
 
+#include "peer.h"
+
 namespace mx {
 
 // Flat parameter layout = KerasCNN state_dict order (models/keras_cnn.py).
@@ -61,5 +63,9 @@ struct KerasFused {
 void keras_fused_forward(const KerasFused& f, hipStream_t st);   // KF1 + KF2
 void keras_fused_backward(const KerasFused& f, hipStream_t st);  // KB1
 void keras_fused_update(const KerasFused& f, int mode, float gscale, hipStream_t st);  // KO
+// KX (DDP over the peer transport): the one-shot gradient exchange co-scheduled with Adam --
+// replaces the bucket all-reduce and mode 2 (a: PeerComm::oneshot_args of g)
+void keras_fused_exchange_adam(const KerasFused& f, const PeerArgs& a, hipStream_t st);
+int keras_exchange_blocks();
 
 }  // namespace mx

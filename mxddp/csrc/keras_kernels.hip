@@ -30,6 +30,7 @@
 // (tensorflow2/mnist_mirror_strategy.py:12,68-79).
 #include "common.h"
 #include "keras_kernels.h"
+#include "peer_device.h"
 
 #include <cstdlib>
 #include "rng.h"
@@ -774,6 +775,22 @@ __device__ __forceinline__ void pack_w2(const KerasFused& f, int i, float val) {
   f.w2d[(((ci >> 4) * 4 + (co >> 4)) * 36 + r * 4 + (cl >> 2)) * 64 + (ci & 15) + 16 * (cl & 3)] = val;
 }
 
+// Adam (gradient gr already summed / averaged by gscale) + conv2 repack of parameter i
+__device__ __forceinline__ void adam_one(const KerasFused& f, int i, float gr, int t, float gscale) {
+  float pv = f.p[i];
+  gr = gr * gscale + f.wd * pv;
+  const float bc1 = 1.f - powf(f.b1, (float)t), bc2 = 1.f - powf(f.b2, (float)t);
+  const float bc2s = sqrtf(bc2);
+  const float e = f.eps_hat ? f.eps / bc2s : f.eps;
+  const float mi = f.b1 * f.m[i] + (1.f - f.b1) * gr;
+  const float vi = f.b2 * f.v[i] + (1.f - f.b2) * gr * gr;
+  f.m[i] = mi;
+  f.v[i] = vi;
+  pv -= (*f.lr / bc1) * mi / (sqrtf(vi) / bc2s + e);
+  f.p[i] = pv;
+  if (i >= (int)L::w2 && i < (int)L::b2) pack_w2(f, i, pv);
+}
+
 __global__ __launch_bounds__(256) void ko_kernel(KerasFused f, KoPlan plan, int mode, float gscale) {
   __shared__ float red[4][64];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -817,24 +834,56 @@ __global__ __launch_bounds__(256) void ko_kernel(KerasFused f, KoPlan plan, int 
     }
   }
   if (live && q == 0) {
-    float pv = f.p[i];
-    if (mode == 1) {
-      f.g[i] = gr;
-    } else if (adam) {
-      gr = gr * gscale + f.wd * pv;
-      const float bc1 = 1.f - powf(f.b1, (float)t), bc2 = 1.f - powf(f.b2, (float)t);
-      const float bc2s = sqrtf(bc2);
-      const float e = f.eps_hat ? f.eps / bc2s : f.eps;
-      const float mi = f.b1 * f.m[i] + (1.f - f.b1) * gr;
-      const float vi = f.b2 * f.v[i] + (1.f - f.b2) * gr * gr;
-      f.m[i] = mi;
-      f.v[i] = vi;
-      pv -= (*f.lr / bc1) * mi / (sqrtf(vi) / bc2s + e);
-      f.p[i] = pv;
-    }
-    if (mode != 1 && i >= (int)L::w2 && i < (int)L::b2) pack_w2(f, i, pv);
+    if (mode == 1) f.g[i] = gr;
+    else if (adam) adam_one(f, i, gr, t, gscale);
+    else if (i >= (int)L::w2 && i < (int)L::b2) pack_w2(f, i, f.p[i]);  // mode 3
   }
   if (adam && b == 0 && tid == 0) __hip_atomic_store(f.adam_state + 1, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------------------------------
+// KX: the gradient exchange co-scheduled with Adam (peer transport, world size 2..8): one
+// launch replaces the bucket all-reduce kernel and the Adam launch.  Block b owns parameters
+// [512 b, 512 b + 512): it pushes its slice of the finalized g into every peer's exchange slot
+// `rank` (one-shot: W-1 remote stores per value, all links at once), publishes its per-block
+// flag, waits for the peers' flags of the same block (peer_device.h; bounded, no grid barrier),
+// sums the W copies in rank order 0..W-1 (bit-identical on every rank) and applies Adam to the
+// average.  Slots / flags / epochs are the PeerComm's, so this alternates freely with its other
+// kernels; 182 blocks fit the 256 flag sets.
+constexpr int kKxThreads = 512;
+
+__global__ __launch_bounds__(kKxThreads) void kx_kernel(KerasFused f, PeerArgs a) {
+  __shared__ uint32_t s_ep;
+  const int b = blockIdx.x, tid = threadIdx.x, r = a.rank, W = a.ws;
+  const int i = b * kKxThreads + tid;
+  const bool live = i < (int)L::total;
+  const int t = __hip_atomic_load(f.adam_state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  if (tid == 0) s_ep = a.epoch[b] + 1;
+  __syncthreads();
+  const uint32_t ep = s_ep;
+  const long long slot = a.slot_bytes / 4;
+  const long long half = (long long)(ep & 1u) * 2 * W * slot;
+  const float mine = live ? f.g[i] : 0.f;
+  if (live)
+    for (int j = 1; j < W; ++j) {
+      const int p = (r + j) % W;
+      reinterpret_cast<float*>(a.xbuf[p])[half + (long long)r * slot + i] = mine;
+    }
+  signal_peers(a, 0, b, ep);
+  wait_peers(a, 0, b, ep);
+  if (live) {
+    const float* scat = reinterpret_cast<const float*>(a.xbuf[r]) + half + i;
+    float acc = 0.f;
+    for (int p = 0; p < W; ++p) {
+      const float v = p == r ? mine : __builtin_nontemporal_load(scat + (long long)p * slot);
+      acc = p == 0 ? v : acc + v;
+    }
+    adam_one(f, i, acc, t, a.scale);
+  }
+  if (tid == 0) {
+    a.epoch[b] = ep;
+    if (b == 0) __hip_atomic_store(f.adam_state + 1, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 }  // namespace keras
@@ -883,6 +932,15 @@ static keras::KoPlan ko_plan(const KerasFused& f, int mode) {
   }
   p.nblocks = blk;
   return p;
+}
+
+int keras_exchange_blocks() { return (int)((KerasLayout::total + keras::kKxThreads - 1) / keras::kKxThreads); }
+
+void keras_fused_exchange_adam(const KerasFused& f, const PeerArgs& a, hipStream_t st) {
+  const int nb = keras_exchange_blocks();
+  MX_CHECK(nb <= kPeerMaxBlocks && a.ws >= 2 && a.ws <= kPeerMaxRanks, "keras exchange: flag sets / world size");
+  MX_CHECK(a.slot_bytes >= (long long)(KerasLayout::total * sizeof(float)), "keras exchange: slot too small");
+  MX_LAUNCH(keras::kx_kernel, dim3(nb), dim3(keras::kKxThreads), 0, st, f, a);
 }
 
 void keras_fused_update(const KerasFused& f, int mode, float gscale, hipStream_t st) {

@@ -163,6 +163,12 @@ bool PeerComm::coschedule_args(void* data, size_t count, RedOp op, PeerArgs* a, 
   return part->chunk * 4 <= a->slot_bytes;
 }
 
+bool PeerComm::oneshot_args(void* data, size_t count, RedOp op, PeerArgs* a) const {
+  PeerPartition part{};
+  if (!coschedule_args(data, count, op, a, &part)) return false;
+  return static_cast<long long>(count) * 4 <= a->slot_bytes;
+}
+
 void PeerComm::all_reduce(void* data, size_t count, DType t, hipStream_t st, RedOp op) {
   if (ws_ == 1 || count == 0) return;
   MX_CHECK(op == RedOp::kSum || op == RedOp::kAvg, "peer transport: sum or average only");

@@ -83,6 +83,9 @@ class PeerComm {
   // another kernel (peer_device.h: peer_two_shot_f32_block); false if it does not fit one
   // launch (bucket above the exchange capacity) or world size 1
   bool coschedule_args(void* data, size_t count, RedOp op, PeerArgs* a, PeerPartition* part) const;
+  // kernel arguments of ONE one-shot f32 exchange of `count` elements (every rank's whole bucket
+  // in each peer's slot) run by another kernel's blocks; false if it does not fit one slot
+  bool oneshot_args(void* data, size_t count, RedOp op, PeerArgs* a) const;
   int error() const;                                 // 0 = ok; else 1 + (peer that timed out)
   void reset_error();
   void set_blocks(int b);

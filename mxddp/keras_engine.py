@@ -32,10 +32,23 @@ _LAYOUT = [  # (name, shape) in state_dict order == flat offsets of KerasLayout 
 class FusedKerasTrainer(AdamTrainerBase):
     """The fused Keras-CNN step.  DDP (world size > 1, or collectives forced): finalize into g,
     ONE all-reduce of the 373 KB gradient, Adam -- over RCCL (any comm.py variant) or the xGMI
-    peer transport, eager launches or one hipGraph per group of steps, picked by autotune()."""
+    peer transport, eager launches or one hipGraph per group of steps, picked by autotune().
+    With the peer transport the exchange can also run inside the Adam launch ("co": one-shot
+    push of every rank's gradient, per-block flags, rank-ordered sum, Adam; one launch fewer)."""
     LAYOUT = _LAYOUT
     MODEL = KerasCNN
     STRATEGIES = ("one",)
+
+    def _candidate_strategies(self, transport: str) -> list:
+        return ["one"] + (["co"] if transport == "peer" else [])
+
+    def _set_buckets(self, strat: str):
+        """one: a separate all-reduce of the whole gradient between the finalize and Adam; co
+        (peer transport): the exchange co-scheduled with Adam in one launch."""
+        co = strat == "co" and self.eng.set_coscheduled(True)
+        if not co:
+            self.eng.set_coscheduled(False)
+        self.bucket_strategy = "co" if co else "one"
 
     def __init__(self, batch: int = 64, device: torch.device | int = 0, comm=None, seed: int = 1, lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-7, weight_decay: float = 0.0, eps_hat: bool = True,
@@ -71,12 +84,18 @@ class FusedKerasReplicas(FusedReplicas):
     replicas synchronise on the GPUs.  All replicas' work is launched before the host waits."""
 
     def __init__(self, devices, batch: int = 64, lr: float = 1e-3, seed: int = 1, init_model=None,
-                 use_graph: bool = True, steps_per_graph: int | None = None, blocks: int = 32):
+                 use_graph: bool = True, steps_per_graph: int | None = None, blocks: int = 32,
+                 strategy: str = "co"):
         if init_model is None:
             torch.manual_seed(seed)
             init_model = KerasCNN()
         self.batch = batch
-        super().__init__(devices, lambda d, pc: FusedKerasTrainer(batch=batch, device=d, peer=pc, seed=seed, lr=lr,
-                                                                  init_model=init_model, use_graph=use_graph,
-                                                                  steps_per_graph=steps_per_graph, graph_mode=1),
-                         blocks=blocks, peer_bytes=4 << 20)
+
+        def make(d, pc):
+            t = FusedKerasTrainer(batch=batch, device=d, peer=pc, seed=seed, lr=lr, init_model=init_model,
+                                  use_graph=use_graph, steps_per_graph=steps_per_graph, graph_mode=1)
+            if pc is not None:
+                t._set_buckets(strategy)  # "co": exchange inside the Adam launch; "one": separate
+            return t
+
+        super().__init__(devices, make, blocks=blocks, peer_bytes=4 << 20)

@@ -216,7 +216,7 @@ def _worker(rank, ws, port, mode, q):
                 moved = (ref.params.cpu() - torch.cat([v.reshape(-1) for v in init.state_dict().values()])).abs().max()
                 if not d < 2e-5 or not moved > 1e-3:
                     bad.append(("ddp != global batch", d, float(moved)))
-        elif mode in ("keras", "keras_graph", "mlp", "mlp_graph"):
+        elif mode in ("keras", "keras_graph", "mlp", "mlp_graph", "keras_co", "keras_co_graph"):
             # fused Keras-CNN / Chainer-MLP DDP step over the peer transport == one trainer on
             # the global batch (MultiWorkerMirroredStrategy / ChainerMN parity)
             if mode.startswith("keras"):
@@ -234,6 +234,10 @@ def _worker(rank, ws, port, mode, q):
                        for _ in range(steps)]
             tr = T(batch=b, device=0, comm=None, peer=pc, lr=2e-3, init_model=init, use_graph=graph,
                    graph_mode=1 if graph else 0)
+            if "_co" in mode:  # exchange co-scheduled with Adam (one launch)
+                tr._set_buckets("co")
+                if not tr.eng.coscheduled:
+                    bad.append("co-scheduling refused")
             for x, y in batches:
                 tr.set_batch(x[rank * b:(rank + 1) * b].cuda(), y[rank * b:(rank + 1) * b].cuda())
                 tr.step(1)
@@ -446,8 +450,10 @@ def test_fused_replicas_stalled_replica_fails_fast(cuda):
 
 
 @pytest.mark.parametrize("ws,mode", [(2, "keras"), (2, "keras_graph"), (8, "keras_graph"),
+                                     (2, "keras_co"), (2, "keras_co_graph"), (8, "keras_co_graph"),
                                      (2, "mlp"), (2, "mlp_graph"), (8, "mlp_graph")])
 def test_fused_adam_engines_peer_ddp_match_global_batch(cuda, ws, mode):
     """The fused Keras-CNN and Chainer-MLP DDP steps (finalize / gradient kernels, bucket
-    all-reduce over the peer transport, Adam) at 2 and 8 ranks == one trainer on the global batch."""
+    all-reduce over the peer transport, Adam; keras_co: the exchange inside the Adam launch) at 2
+    and 8 ranks == one trainer on the global batch."""
     _run(ws, mode)
