@@ -307,7 +307,28 @@ __device__ __forceinline__ float2 block_sum2_f(float a, float b, float* red) {
   return t;
 }
 
-// HW % 4 == 0 (float4 path only); element e of the channel: image e / HW4, float4 e % HW4
+// HW % 4 == 0 (float4 path only); element e of the channel: image e / HW4, float4 e % HW4.
+// U = float4s per thread (the channel's N * HW / 4 <= U * kBnF): every operand of the channel is
+// loaded ONCE, all U loads issued before the first is consumed, and kept in registers through
+// the block reduction for the apply -- one memory round trip per kernel instead of a serial
+// load chain per pass plus a second read of the channel (the loop form measured 7.8 / 9.4 us
+// for the PyramidNet stage-2 / 3 BNs, profiles/r3_final/summary_pyr.txt).  Same per-thread
+// summation order as the loop form (u ascending), so the results are unchanged.
+template <int U>
+__device__ __forceinline__ void bn_chan_offsets(int c, int C, int hw4, int total, const FastDiv& dv, int side_c,
+                                                size_t (&o)[U], bool (&ok)[U], size_t (&so)[U]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i0 = threadIdx.x + u * kBnF;
+    ok[u] = i0 < total;
+    const int i = ok[u] ? i0 : total - 1;  // clamped: every lane loads, masked after
+    const int n = (int)dv.div(i), j = i - n * hw4;
+    o[u] = ((size_t)n * C + c) * hw4 + j;
+    so[u] = ((size_t)n * side_c) * hw4 + j;  // the side operand (residual / shortcut gradient) of image n
+  }
+}
+
+template <int U>
 __global__ __launch_bounds__(kBnF) void bn_fwd_fused_k(const float* __restrict__ x, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, float* __restrict__ y,
                                                       float* __restrict__ mean_out, float* __restrict__ invstd_out,
@@ -318,13 +339,24 @@ __global__ __launch_bounds__(kBnF) void bn_fwd_fused_k(const float* __restrict__
   __shared__ float red[2 * kBnF / 64];
   const int c = blockIdx.x, hw4 = HW >> 2, total = N * hw4;
   if (c == 0 && num_batches && threadIdx.x == 0) *num_batches += 1;
-  const float K = x[(size_t)c * HW];  // shift: x[0, c, 0, 0]
+  size_t o[U], so[U];
+  bool ok[U];
+  bn_chan_offsets<U>(c, C, hw4, total, dv, Cr, o, ok, so);
   const float4* x4 = reinterpret_cast<const float4*>(x);
+  const float4* r4 = (res && c < Cr) ? reinterpret_cast<const float4*>(res + (size_t)c * HW) : nullptr;
+  const float K = x[(size_t)c * HW];  // shift: x[0, c, 0, 0]
+  float4 v[U], rr[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) v[u] = x4[o[u]];
+  if (r4) {  // residual channel c of image n
+#pragma unroll
+    for (int u = 0; u < U; ++u) rr[u] = r4[so[u]];
+  }
   float s1 = 0.f, s2 = 0.f;
-  for (int i = threadIdx.x; i < total; i += kBnF) {
-    const int n = (int)dv.div(i), j = i - n * hw4;
-    const float4 v = x4[((size_t)n * C + c) * hw4 + j];
-    const float p = v.x - K, q = v.y - K, r = v.z - K, t = v.w - K;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (!ok[u]) continue;
+    const float p = v[u].x - K, q = v[u].y - K, r = v[u].z - K, t = v[u].w - K;
     s1 += (p + q) + (r + t);
     s2 = fmaf(p, p, fmaf(q, q, fmaf(r, r, fmaf(t, t, s2))));
   }
@@ -341,33 +373,32 @@ __global__ __launch_bounds__(kBnF) void bn_fwd_fused_k(const float* __restrict__
     if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
     if (run_var) run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
   }
-  const float4* r4 = (res && c < Cr) ? reinterpret_cast<const float4*>(res + (size_t)c * HW) : nullptr;
   float4* y4 = reinterpret_cast<float4*>(y);
-  for (int i = threadIdx.x; i < total; i += kBnF) {
-    const int n = (int)dv.div(i), j = i - n * hw4;
-    const size_t o = ((size_t)n * C + c) * hw4 + j;
-    float4 v = x4[o];
-    v.x = fmaf(v.x, sc, sh);
-    v.y = fmaf(v.y, sc, sh);
-    v.z = fmaf(v.z, sc, sh);
-    v.w = fmaf(v.w, sc, sh);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (!ok[u]) continue;
+    float4 w = v[u];
+    w.x = fmaf(w.x, sc, sh);
+    w.y = fmaf(w.y, sc, sh);
+    w.z = fmaf(w.z, sc, sh);
+    w.w = fmaf(w.w, sc, sh);
     if (relu) {
-      v.x = fmaxf(v.x, 0.f);
-      v.y = fmaxf(v.y, 0.f);
-      v.z = fmaxf(v.z, 0.f);
-      v.w = fmaxf(v.w, 0.f);
+      w.x = fmaxf(w.x, 0.f);
+      w.y = fmaxf(w.y, 0.f);
+      w.z = fmaxf(w.z, 0.f);
+      w.w = fmaxf(w.w, 0.f);
     }
     if (r4) {
-      const float4 rr = r4[(size_t)n * Cr * hw4 + j];
-      v.x += rr.x;
-      v.y += rr.y;
-      v.z += rr.z;
-      v.w += rr.w;
+      w.x += rr[u].x;
+      w.y += rr[u].y;
+      w.z += rr[u].z;
+      w.w += rr[u].w;
     }
-    y4[o] = v;
+    y4[o[u]] = w;
   }
 }
 
+template <int U>
 __global__ __launch_bounds__(kBnF) void bn_bwd_fused_k(const float* __restrict__ dy, const float* __restrict__ x,
                                                       const float* __restrict__ yr, const float* __restrict__ gamma,
                                                       const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -376,25 +407,40 @@ __global__ __launch_bounds__(kBnF) void bn_bwd_fused_k(const float* __restrict__
                                                       int acc_params, const float* __restrict__ extra, int extC) {
   __shared__ float red[2 * kBnF / 64];
   const int c = blockIdx.x, hw4 = HW >> 2, total = N * hw4;
-  const float mu = mean[c], inv = invstd[c];
+  size_t o[U], so[U];
+  bool ok[U];
+  bn_chan_offsets<U>(c, C, hw4, total, dv, extC, o, ok, so);
   const float4* g4 = reinterpret_cast<const float4*>(dy);
   const float4* x4 = reinterpret_cast<const float4*>(x);
   const float4* y4 = reinterpret_cast<const float4*>(yr);
-  float s1 = 0.f, s2 = 0.f;
-  for (int i = threadIdx.x; i < total; i += kBnF) {
-    const int n = (int)dv.div(i), j = i - n * hw4;
-    const size_t o = ((size_t)n * C + c) * hw4 + j;
-    float4 g = g4[o];
-    const float4 v = x4[o];
-    if (yr) {
-      const float4 r = y4[o];
-      g.x = r.x > 0.f ? g.x : 0.f;
-      g.y = r.y > 0.f ? g.y : 0.f;
-      g.z = r.z > 0.f ? g.z : 0.f;
-      g.w = r.w > 0.f ? g.w : 0.f;
+  const float4* e4 = extra ? reinterpret_cast<const float4*>(extra + (size_t)c * HW) : nullptr;
+  float4 g[U], v[U], e[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    g[u] = g4[o[u]];
+    v[u] = x4[o[u]];
+  }
+  if (yr) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float4 r = y4[o[u]];
+      g[u].x = r.x > 0.f ? g[u].x : 0.f;
+      g[u].y = r.y > 0.f ? g[u].y : 0.f;
+      g[u].z = r.z > 0.f ? g[u].z : 0.f;
+      g[u].w = r.w > 0.f ? g[u].w : 0.f;
     }
-    s1 += (g.x + g.y) + (g.z + g.w);
-    s2 = fmaf(g.x, v.x - mu, fmaf(g.y, v.y - mu, fmaf(g.z, v.z - mu, fmaf(g.w, v.w - mu, s2))));
+  }
+  if (e4) {  // the shortcut's gradient (channel c of a wider tensor): issued before the reduction
+#pragma unroll
+    for (int u = 0; u < U; ++u) e[u] = e4[so[u]];
+  }
+  const float mu = mean[c], inv = invstd[c];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (!ok[u]) continue;
+    s1 += (g[u].x + g[u].y) + (g[u].z + g[u].w);
+    s2 = fmaf(g[u].x, v[u].x - mu, fmaf(g[u].y, v[u].y - mu, fmaf(g[u].z, v[u].z - mu, fmaf(g[u].w, v[u].w - mu, s2))));
   }
   const float2 t = block_sum2_f(s1, s2, red);
   const float cnt = (float)N * (float)HW;
@@ -405,34 +451,29 @@ __global__ __launch_bounds__(kBnF) void bn_bwd_fused_k(const float* __restrict__
     if (dgamma) dgamma[c] = acc_params ? dgamma[c] + dg : dg;
     if (dbeta) dbeta[c] = acc_params ? dbeta[c] + db : db;
   }
-  const float4* e4 = extra ? reinterpret_cast<const float4*>(extra + (size_t)c * HW) : nullptr;
   float4* d4 = reinterpret_cast<float4*>(dx);
-  for (int i = threadIdx.x; i < total; i += kBnF) {
-    const int n = (int)dv.div(i), j = i - n * hw4;
-    const size_t o = ((size_t)n * C + c) * hw4 + j;
-    float4 g = g4[o];
-    const float4 v = x4[o];
-    if (yr) {
-      const float4 r = y4[o];
-      g.x = r.x > 0.f ? g.x : 0.f;
-      g.y = r.y > 0.f ? g.y : 0.f;
-      g.z = r.z > 0.f ? g.z : 0.f;
-      g.w = r.w > 0.f ? g.w : 0.f;
-    }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (!ok[u]) continue;
     float4 out;
-    out.x = fmaf(A, g.x, fmaf(D, v.x, Bc));
-    out.y = fmaf(A, g.y, fmaf(D, v.y, Bc));
-    out.z = fmaf(A, g.z, fmaf(D, v.z, Bc));
-    out.w = fmaf(A, g.w, fmaf(D, v.w, Bc));
+    out.x = fmaf(A, g[u].x, fmaf(D, v[u].x, Bc));
+    out.y = fmaf(A, g[u].y, fmaf(D, v[u].y, Bc));
+    out.z = fmaf(A, g[u].z, fmaf(D, v[u].z, Bc));
+    out.w = fmaf(A, g[u].w, fmaf(D, v[u].w, Bc));
     if (e4) {
-      const float4 e = e4[(size_t)n * extC * hw4 + j];
-      out.x += e.x;
-      out.y += e.y;
-      out.z += e.z;
-      out.w += e.w;
+      out.x += e[u].x;
+      out.y += e[u].y;
+      out.z += e[u].z;
+      out.w += e[u].w;
     }
-    d4[o] = out;
+    d4[o[u]] = out;
   }
+}
+
+// float4s per thread of the one-block-per-channel kernels (a power of two, <= 8)
+int bn_fused_u(int N, int HW) {
+  const int per = (N * (HW / 4) + kBnF - 1) / kBnF;
+  return per <= 1 ? 1 : per <= 2 ? 2 : per <= 4 ? 4 : 8;
 }
 
 // per-channel blocks when the channel is small enough for one block and there are enough
@@ -464,8 +505,16 @@ void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* 
   MX_CHECK(S <= 4 * kBnTB, "bn: too many splits");
   MX_CHECK(!res || (Cr > 0 && Cr <= C), "bn: residual channels must be in 1..C");
   if (bn_use_fused(N, C, HW)) {
-    MX_LAUNCH(bn_fwd_fused_k, dim3(C), dim3(kBnF), 0, st, x, gamma, beta, y, mean, invstd, run_mean, run_var, N, C,
-              HW, FastDiv(HW / 4), eps, momentum, relu ? 1 : 0, num_batches, res, Cr);
+#define MX_BN_FWD(U_)                                                                                            \
+  MX_LAUNCH(bn_fwd_fused_k<U_>, dim3(C), dim3(kBnF), 0, st, x, gamma, beta, y, mean, invstd, run_mean, run_var, N, C, \
+            HW, FastDiv(HW / 4), eps, momentum, relu ? 1 : 0, num_batches, res, Cr)
+    switch (bn_fused_u(N, HW)) {
+      case 1: MX_BN_FWD(1); break;
+      case 2: MX_BN_FWD(2); break;
+      case 4: MX_BN_FWD(4); break;
+      default: MX_BN_FWD(8); break;
+    }
+#undef MX_BN_FWD
     return;
   }
   const bool vec = HW % 4 == 0;
@@ -490,8 +539,16 @@ void bn_bwd(const float* dy, const float* x, const float* y_relu, const float* g
   MX_CHECK(S <= 4 * kBnTB, "bn: too many splits");
   MX_CHECK(!extra || extC >= C, "bn: extra gradient must have >= C channels");
   if (bn_use_fused(N, C, HW)) {
-    MX_LAUNCH(bn_bwd_fused_k, dim3(C), dim3(kBnF), 0, st, dy, x, y_relu, gamma, mean, invstd, dgamma, dbeta, dx, N,
-              C, HW, FastDiv(HW / 4), accp ? 1 : 0, extra, extC);
+#define MX_BN_BWD(U_)                                                                                              \
+  MX_LAUNCH(bn_bwd_fused_k<U_>, dim3(C), dim3(kBnF), 0, st, dy, x, y_relu, gamma, mean, invstd, dgamma, dbeta, dx, N, \
+            C, HW, FastDiv(HW / 4), accp ? 1 : 0, extra, extC)
+    switch (bn_fused_u(N, HW)) {
+      case 1: MX_BN_BWD(1); break;
+      case 2: MX_BN_BWD(2); break;
+      case 4: MX_BN_BWD(4); break;
+      default: MX_BN_BWD(8); break;
+    }
+#undef MX_BN_BWD
     return;
   }
   const bool vec = HW % 4 == 0;

@@ -208,10 +208,13 @@ def test_cross_entropy(cuda):
 
 @pytest.mark.parametrize("shape,offset", [((8, 21, 9, 7), 0.5), ((64, 16, 32, 32), 3.0), ((64, 271, 8, 8), -20.0),
                                           ((3, 5, 7, 7), 0.0), ((32, 64, 56, 56), 1.0),
-                                          ((64, 106, 16, 16), 7.0), ((16, 64, 6, 6), 0.0)])
+                                          ((64, 106, 16, 16), 7.0), ((16, 64, 6, 6), 0.0),
+                                          ((32, 80, 16, 16), -3.0)])
 @pytest.mark.parametrize("relu", [False, True])
 def test_batchnorm(cuda, relu, shape, offset):
-    """Split-reduction BN (vector and scalar paths, 1..64 splits, large mean offset) vs torch fp32."""
+    """Split-reduction BN (vector and scalar paths, 1..64 splits, large mean offset) and the
+    register-resident one-block-per-channel kernels (1, 2, 4 and 8 float4s per thread) vs torch
+    fp32."""
     torch.manual_seed(4)
     C = shape[1]
     x = torch.randn(*shape) * 2 + offset
@@ -262,7 +265,7 @@ def test_shortcut(cuda, stride):
     assert _rel(og.grad.cpu(), orr.grad) < 1e-5
 
 
-@pytest.mark.parametrize("shape", [(4, 21, 26, 16, 16), (8, 186, 186, 8, 8), (2, 5, 9, 7, 7)])
+@pytest.mark.parametrize("shape", [(4, 21, 26, 16, 16), (8, 186, 186, 8, 8), (2, 5, 9, 7, 7), (32, 100, 105, 16, 16)])
 def test_batchnorm_residual_tap(cuda, shape):
     """PyramidNet identity-shortcut fusion: bn1 with a tap output (its gradient is summed into dx
     by the BN kernel, read in place from the channel slice of the block-output gradient) and bn3
