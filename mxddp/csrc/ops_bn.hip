@@ -66,6 +66,32 @@ __device__ __forceinline__ Slice slice_of(int s, int S, int N) {
   return Slice{min(s * per, N), min((s + 1) * per, N)};
 }
 
+// The split kernels' vector paths walk their slice in chunks of kBnU float4s per thread with
+// every load of a chunk issued before the first is used (a slice is 1..4 float4s per thread for
+// the PyramidNet stage-1 BNs: one memory round trip), and the elementwise passes request their
+// first chunk before reading the channel's partials, so the two round trips overlap.  Per-thread
+// summation order is unchanged (i ascending).
+constexpr int kBnU = 4;
+struct BnChunk {
+  size_t o[kBnU];  // float4 offset of (n, c, j) in an [N][C][HW / 4] tensor
+  size_t so[kBnU]; // float4 offset of (n, j) in a side tensor [N][side_c][HW / 4] at channel 0
+  bool ok[kBnU];
+};
+__device__ __forceinline__ BnChunk bn_chunk(int i0, int total, const Slice& sl, int hw4, int C, int c, int side_c,
+                                            const FastDiv& dv) {
+  BnChunk k;
+#pragma unroll
+  for (int u = 0; u < kBnU; ++u) {
+    const int iu = i0 + u * kBnTB;
+    k.ok[u] = iu < total;
+    const int i = k.ok[u] ? iu : i0;
+    const int n = sl.n0 + (int)dv.div(i), j = i - (n - sl.n0) * hw4;
+    k.o[u] = ((size_t)n * C + c) * hw4 + j;
+    k.so[u] = ((size_t)n * side_c) * hw4 + j;
+  }
+  return k;
+}
+
 // ------------------------------------------------------------------ forward statistics
 template <bool VEC>
 __global__ __launch_bounds__(kBnTB) void bn_stats_k(const float* __restrict__ x, int N, int C, int HW, int S, FastDiv dv,
@@ -78,12 +104,19 @@ __global__ __launch_bounds__(kBnTB) void bn_stats_k(const float* __restrict__ x,
   if (VEC) {
     const int hw4 = HW >> 2;
     const int total = (sl.n1 - sl.n0) * hw4;
-    for (int i = threadIdx.x; i < total; i += kBnTB) {
-      const int n = sl.n0 + (int)dv.div(i), j = i - (n - sl.n0) * hw4;
-      const float4 v = reinterpret_cast<const float4*>(x + ((size_t)n * C + c) * HW)[j];
-      const float a = v.x - K, b = v.y - K, d = v.z - K, e = v.w - K;
-      s1 += (a + b) + (d + e);
-      s2 = fmaf(a, a, fmaf(b, b, fmaf(d, d, fmaf(e, e, s2))));
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    for (int i0 = threadIdx.x; i0 < total; i0 += kBnU * kBnTB) {
+      const BnChunk k = bn_chunk(i0, total, sl, hw4, C, c, 0, dv);
+      float4 v[kBnU];
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) v[u] = x4[k.o[u]];
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) {
+        if (!k.ok[u]) continue;
+        const float a = v[u].x - K, b = v[u].y - K, d = v[u].z - K, e = v[u].w - K;
+        s1 += (a + b) + (d + e);
+        s2 = fmaf(a, a, fmaf(b, b, fmaf(d, d, fmaf(e, e, s2))));
+      }
     }
   } else {
     const int total = (sl.n1 - sl.n0) * HW;
@@ -113,20 +146,30 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_reduce_k(const float* __restrict
   if (VEC) {
     const int hw4 = HW >> 2;
     const int total = (sl.n1 - sl.n0) * hw4;
-    for (int i = threadIdx.x; i < total; i += kBnTB) {
-      const int n = sl.n0 + (int)dv.div(i), j = i - (n - sl.n0) * hw4;
-      const size_t base = ((size_t)n * C + c) * HW;
-      float4 g = reinterpret_cast<const float4*>(dy + base)[j];
-      const float4 v = reinterpret_cast<const float4*>(x + base)[j];
-      if (yr) {
-        const float4 r = reinterpret_cast<const float4*>(yr + base)[j];
-        g.x = r.x > 0.f ? g.x : 0.f;
-        g.y = r.y > 0.f ? g.y : 0.f;
-        g.z = r.z > 0.f ? g.z : 0.f;
-        g.w = r.w > 0.f ? g.w : 0.f;
+    const float4 *g4 = reinterpret_cast<const float4*>(dy), *x4 = reinterpret_cast<const float4*>(x),
+                 *y4 = reinterpret_cast<const float4*>(yr);
+    for (int i0 = threadIdx.x; i0 < total; i0 += kBnU * kBnTB) {
+      const BnChunk k = bn_chunk(i0, total, sl, hw4, C, c, 0, dv);
+      float4 g[kBnU], v[kBnU], r[kBnU];
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) {
+        g[u] = g4[k.o[u]];
+        v[u] = x4[k.o[u]];
+        if (yr) r[u] = y4[k.o[u]];
       }
-      s1 += (g.x + g.y) + (g.z + g.w);
-      s2 = fmaf(g.x, v.x - mu, fmaf(g.y, v.y - mu, fmaf(g.z, v.z - mu, fmaf(g.w, v.w - mu, s2))));
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) {
+        if (!k.ok[u]) continue;
+        if (yr) {
+          g[u].x = r[u].x > 0.f ? g[u].x : 0.f;
+          g[u].y = r[u].y > 0.f ? g[u].y : 0.f;
+          g[u].z = r[u].z > 0.f ? g[u].z : 0.f;
+          g[u].w = r[u].w > 0.f ? g[u].w : 0.f;
+        }
+        s1 += (g[u].x + g[u].y) + (g[u].z + g[u].w);
+        s2 = fmaf(g[u].x, v[u].x - mu,
+                  fmaf(g[u].y, v[u].y - mu, fmaf(g[u].z, v[u].z - mu, fmaf(g[u].w, v[u].w - mu, s2))));
+      }
     }
   } else {
     const int total = (sl.n1 - sl.n0) * HW;
@@ -161,6 +204,23 @@ __global__ __launch_bounds__(kBnTB) void bn_apply_slice_k(const float* __restric
   __shared__ float red[2 * kBnTB / 64];
   const int s = blockIdx.x, c = blockIdx.y;
   if (s == 0 && c == 0 && num_batches && threadIdx.x == 0) *num_batches += 1;
+  const Slice sl = slice_of(s, S, N);
+  // residual (PyramidNet identity shortcut, channels zero-padded): channel c < Cr adds res[n][c]
+  const float* rc = (res && c < Cr) ? res + (size_t)c * HW : nullptr;  // uniform per block
+  const int hw4 = HW >> 2, total4 = (sl.n1 - sl.n0) * hw4;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  const float4* r4 = reinterpret_cast<const float4*>(rc);
+  float4* y4 = reinterpret_cast<float4*>(y);
+  BnChunk k0{};
+  float4 v0[kBnU], q0[kBnU];
+  if (VEC && threadIdx.x < total4) {  // first chunk requested before the partials are read
+    k0 = bn_chunk(threadIdx.x, total4, sl, hw4, C, c, Cr, dv);
+#pragma unroll
+    for (int u = 0; u < kBnU; ++u) {
+      v0[u] = x4[k0.o[u]];
+      if (r4) q0[u] = r4[k0.so[u]];
+    }
+  }
   const float K = x[(size_t)c * HW];  // the statistics kernel's shift
   const float2 t = channel_sums(part, c, S, red);
   const float m1 = t.x / cnt;
@@ -174,34 +234,41 @@ __global__ __launch_bounds__(kBnTB) void bn_apply_slice_k(const float* __restric
     if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
     if (run_var) run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
   }
-  const Slice sl = slice_of(s, S, N);
-  // residual (PyramidNet identity shortcut, channels zero-padded): channel c < Cr adds res[n][c]
-  const float* rc = (res && c < Cr) ? res + (size_t)c * HW : nullptr;  // uniform per block
   if (VEC) {
-    const int hw4 = HW >> 2;
-    const int total = (sl.n1 - sl.n0) * hw4;
-    for (int i = threadIdx.x; i < total; i += kBnTB) {
-      const int n = sl.n0 + (int)dv.div(i), j = i - (n - sl.n0) * hw4;
-      const size_t o = ((size_t)n * C + c) * hw4 + j;
-      float4 v = reinterpret_cast<const float4*>(x)[o];
-      v.x = fmaf(v.x, sc, sh);
-      v.y = fmaf(v.y, sc, sh);
-      v.z = fmaf(v.z, sc, sh);
-      v.w = fmaf(v.w, sc, sh);
-      if (relu) {
-        v.x = fmaxf(v.x, 0.f);
-        v.y = fmaxf(v.y, 0.f);
-        v.z = fmaxf(v.z, 0.f);
-        v.w = fmaxf(v.w, 0.f);
+    auto apply = [&](const BnChunk& k, const float4 (&v)[kBnU], const float4 (&q)[kBnU]) {
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) {
+        if (!k.ok[u]) continue;
+        float4 w = v[u];
+        w.x = fmaf(w.x, sc, sh);
+        w.y = fmaf(w.y, sc, sh);
+        w.z = fmaf(w.z, sc, sh);
+        w.w = fmaf(w.w, sc, sh);
+        if (relu) {
+          w.x = fmaxf(w.x, 0.f);
+          w.y = fmaxf(w.y, 0.f);
+          w.z = fmaxf(w.z, 0.f);
+          w.w = fmaxf(w.w, 0.f);
+        }
+        if (r4) {
+          w.x += q[u].x;
+          w.y += q[u].y;
+          w.z += q[u].z;
+          w.w += q[u].w;
+        }
+        y4[k.o[u]] = w;
       }
-      if (rc) {
-        const float4 r = reinterpret_cast<const float4*>(rc + (size_t)n * Cr * HW)[j];
-        v.x += r.x;
-        v.y += r.y;
-        v.z += r.z;
-        v.w += r.w;
+    };
+    if (threadIdx.x < total4) apply(k0, v0, q0);
+    for (int i0 = threadIdx.x + kBnU * kBnTB; i0 < total4; i0 += kBnU * kBnTB) {
+      const BnChunk k = bn_chunk(i0, total4, sl, hw4, C, c, Cr, dv);
+      float4 v[kBnU], q[kBnU];
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) {
+        v[u] = x4[k.o[u]];
+        if (r4) q[u] = r4[k.so[u]];
       }
-      reinterpret_cast<float4*>(y)[o] = v;
+      apply(k, v, q);
     }
   } else {
     const int total = (sl.n1 - sl.n0) * HW;
@@ -224,6 +291,26 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_apply_slice_k(
     int C, int HW, int S, FastDiv dv, float cnt, int acc_params, const float* __restrict__ extra, int extC) {
   __shared__ float red[2 * kBnTB / 64];
   const int s = blockIdx.x, c = blockIdx.y;
+  const Slice sl = slice_of(s, S, N);
+  // extra: a second gradient of x added to dx (the residual branch's, read in place from the
+  // block output gradient [N][extC][HW], channels 0..C-1), instead of a separate add launch
+  const float* ec = extra ? extra + (size_t)c * HW : nullptr;
+  const int hw4 = HW >> 2, total4 = (sl.n1 - sl.n0) * hw4;
+  const float4 *g4 = reinterpret_cast<const float4*>(dy), *x4 = reinterpret_cast<const float4*>(x),
+               *y4 = reinterpret_cast<const float4*>(yr), *e4 = reinterpret_cast<const float4*>(ec);
+  float4* d4 = reinterpret_cast<float4*>(dx);
+  BnChunk k0{};
+  float4 g0[kBnU], v0[kBnU], r0[kBnU], e0[kBnU];
+  if (VEC && threadIdx.x < total4) {  // first chunk requested before the partials are read
+    k0 = bn_chunk(threadIdx.x, total4, sl, hw4, C, c, extC, dv);
+#pragma unroll
+    for (int u = 0; u < kBnU; ++u) {
+      g0[u] = g4[k0.o[u]];
+      v0[u] = x4[k0.o[u]];
+      if (yr) r0[u] = y4[k0.o[u]];
+      if (e4) e0[u] = e4[k0.so[u]];
+    }
+  }
   const float inv = invstd[c], mu = mean[c];
   const float2 t = channel_sums(part, c, S, red);
   const float db = t.x, dg = t.y * inv;
@@ -233,38 +320,45 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_apply_slice_k(
     if (dgamma) dgamma[c] = acc_params ? dgamma[c] + dg : dg;
     if (dbeta) dbeta[c] = acc_params ? dbeta[c] + db : db;
   }
-  const Slice sl = slice_of(s, S, N);
-  // extra: a second gradient of x added to dx (the residual branch's, read in place from the
-  // block output gradient [N][extC][HW], channels 0..C-1), instead of a separate add launch
-  const float* ec = extra ? extra + (size_t)c * HW : nullptr;
   if (VEC) {
-    const int hw4 = HW >> 2;
-    const int total = (sl.n1 - sl.n0) * hw4;
-    for (int i = threadIdx.x; i < total; i += kBnTB) {
-      const int n = sl.n0 + (int)dv.div(i), j = i - (n - sl.n0) * hw4;
-      const size_t o = ((size_t)n * C + c) * hw4 + j;
-      float4 g = reinterpret_cast<const float4*>(dy)[o];
-      const float4 v = reinterpret_cast<const float4*>(x)[o];
-      if (yr) {
-        const float4 r = reinterpret_cast<const float4*>(yr)[o];
-        g.x = r.x > 0.f ? g.x : 0.f;
-        g.y = r.y > 0.f ? g.y : 0.f;
-        g.z = r.z > 0.f ? g.z : 0.f;
-        g.w = r.w > 0.f ? g.w : 0.f;
+    auto apply = [&](const BnChunk& k, const float4 (&g)[kBnU], const float4 (&v)[kBnU], const float4 (&r)[kBnU],
+                     const float4 (&e)[kBnU]) {
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) {
+        if (!k.ok[u]) continue;
+        float4 gg = g[u];
+        if (yr) {
+          gg.x = r[u].x > 0.f ? gg.x : 0.f;
+          gg.y = r[u].y > 0.f ? gg.y : 0.f;
+          gg.z = r[u].z > 0.f ? gg.z : 0.f;
+          gg.w = r[u].w > 0.f ? gg.w : 0.f;
+        }
+        float4 out;
+        out.x = fmaf(A, gg.x, fmaf(D, v[u].x, Bc));
+        out.y = fmaf(A, gg.y, fmaf(D, v[u].y, Bc));
+        out.z = fmaf(A, gg.z, fmaf(D, v[u].z, Bc));
+        out.w = fmaf(A, gg.w, fmaf(D, v[u].w, Bc));
+        if (e4) {
+          out.x += e[u].x;
+          out.y += e[u].y;
+          out.z += e[u].z;
+          out.w += e[u].w;
+        }
+        d4[k.o[u]] = out;
       }
-      float4 out;
-      out.x = fmaf(A, g.x, fmaf(D, v.x, Bc));
-      out.y = fmaf(A, g.y, fmaf(D, v.y, Bc));
-      out.z = fmaf(A, g.z, fmaf(D, v.z, Bc));
-      out.w = fmaf(A, g.w, fmaf(D, v.w, Bc));
-      if (ec) {
-        const float4 e = reinterpret_cast<const float4*>(ec + (size_t)n * extC * HW)[j];
-        out.x += e.x;
-        out.y += e.y;
-        out.z += e.z;
-        out.w += e.w;
+    };
+    if (threadIdx.x < total4) apply(k0, g0, v0, r0, e0);
+    for (int i0 = threadIdx.x + kBnU * kBnTB; i0 < total4; i0 += kBnU * kBnTB) {
+      const BnChunk k = bn_chunk(i0, total4, sl, hw4, C, c, extC, dv);
+      float4 g[kBnU], v[kBnU], r[kBnU], e[kBnU];
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) {
+        g[u] = g4[k.o[u]];
+        v[u] = x4[k.o[u]];
+        if (yr) r[u] = y4[k.o[u]];
+        if (e4) e[u] = e4[k.so[u]];
       }
-      reinterpret_cast<float4*>(dx)[o] = out;
+      apply(k, g, v, r, e);
     }
   } else {
     const int total = (sl.n1 - sl.n0) * HW;

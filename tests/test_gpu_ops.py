@@ -209,7 +209,7 @@ def test_cross_entropy(cuda):
 @pytest.mark.parametrize("shape,offset", [((8, 21, 9, 7), 0.5), ((64, 16, 32, 32), 3.0), ((64, 271, 8, 8), -20.0),
                                           ((3, 5, 7, 7), 0.0), ((32, 64, 56, 56), 1.0),
                                           ((64, 106, 16, 16), 7.0), ((16, 64, 6, 6), 0.0),
-                                          ((32, 80, 16, 16), -3.0)])
+                                          ((32, 80, 16, 16), -3.0), ((2, 8, 128, 128), 2.0)])
 @pytest.mark.parametrize("relu", [False, True])
 def test_batchnorm(cuda, relu, shape, offset):
     """Split-reduction BN (vector and scalar paths, 1..64 splits, large mean offset) and the
