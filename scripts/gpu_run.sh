@@ -7,7 +7,8 @@
 # gpurun_out/steps.log; the run stops at the first crash / timeout (gpu_check.sh).  Kernel-trace
 # summaries land in gpurun_out/summary_<step>.txt, counter passes in gpurun_out/pmc_<step>.txt.
 # Steps:
-#   suite        full GPU test suite           smoke        __graft_entry__.smoke()
+#   suite        full GPU test suite (-x)      suite_all    the same, every failure reported
+#   smoke        __graft_entry__.smoke()
 #   t_<name>     one test file, tests/test_gpu_<name>.py
 #   driver       bench at the driver's length  long         2,000-step bench
 #   prof_mnist   rocprofv3 kernel trace of the MNIST step
@@ -50,6 +51,7 @@ ws() {  # ws <name> <ranks> <bench args...>: ranks share the one GPU (functional
 for step in "$@"; do
   case "$step" in
     suite) run suite 1500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    suite_all) run suite_all 1500 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
     t_*) run "$step" 900 python -u -m pytest "tests/test_gpu_${step#t_}.py" -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     driver) run driver 300 python bench.py --steps 20 --warmup 5 ;;
