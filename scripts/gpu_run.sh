@@ -15,7 +15,7 @@
 #   pmc_mnist    counter passes of the MNIST step (eager launches, one pass per run)
 #   keras / keras_rep / keras_ws2 / prof_keras / pmc_keras   Keras CNN fused engine
 #   mlp / mlp_rep / prof_mlp / pmc_mlp                       Chainer MLP
-#   rn32 / rn256 / prof_rn / pmc_rn / rn_stock               ResNet-50 bf16
+#   rn32 / rn256 / prof_rn / pmc_rn / rn_stock / rn_layers    ResNet-50 bf16 (rn_layers: per conv shape)
 #   pyr / prof_pyr / pyr_stock                               PyramidNet-110
 #   ws2 / ws4 / ws8 (MNIST), keras_ws8, pyr_ws8, rn_ws8      shared-GPU DDP rehearsals
 #   coll         MNIST with RCCL collectives forced at one rank
@@ -75,6 +75,7 @@ for step in "$@"; do
     pmc_mlp) pmc pmc_mlp --model mlp --steps 20 --warmup 2 --no-graph --min-warmup-ms 0 ;;
     rn32) run rn32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 ;;
     rn256) run rn256 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 ;;
+    rn_layers) run rn_layers 300 python scripts/bench_nhwc_layers.py 256 5 ;;
     rn_stock) run rn_stock 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --impl torch --channels-last ;;
     prof_rn) prof prof_rn 3 --model resnet50 --dtype bf16 --batch 256 --steps 3 --warmup 2 --min-warmup-ms 0 ;;
     pmc_rn) pmc pmc_rn --model resnet50 --dtype bf16 --batch 256 --steps 1 --warmup 1 --no-graph --min-warmup-ms 0 ;;
