@@ -713,6 +713,206 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// 256 x 256 tile of the LDS-DMA kernel, for layers with Ng % 256 == 0 and enough pixel tiles to
+// fill the chip: 256 output channels x 256 pixels per 512-thread block, wave tile 64 channels x
+// 128 pixels (4 x 8 MFMA fragments: 12 ds_read_b128 per 32 MFMAs, against 16 per 32 for the
+// 128-channel tile), TWO 64 KB stage buffers: wait for stage t, barrier (every wave is done with
+// stage t - 1, so its buffer is free), issue stage t + 1 into it, compute stage t -- one k-tile in
+// flight behind the MFMAs, the structure the CDNA4 guide measures as tying a register pipeline
+// on a 256 x 256 tile at one block per CU.  Same operand images, swizzle, zero-row handling and
+// epilogues as conv_nhwc_glds_kernel; the C tile is staged through LDS in two 128-pixel halves
+// (the waves of pixel column wn own half wn), so the BN reduction slots still fit.
+template <bool STATS>
+__global__ __launch_bounds__(512) void conv_nhwc_glds256_kernel(ConvNArgs a) {
+  constexpr int TM = 256, TN = 256, BK = 64, NS = 2;
+  constexpr int AB = TM * 128, SB = AB + TN * 128;   // bytes: A image, whole stage (64 KB)
+  constexpr int NA = TM / 64, NB = 4;                 // LDS-DMA instructions per wave per stage
+  constexpr int WN = 2, WPX = TN / WN, WMT = 4, WNT = WPX / 16;
+  constexpr int CP = TM + 8, HT = TN / 2, VPR = TM / 8;
+  constexpr int RED = (HT * CP * 2 + 255) & ~255;    // reduction slots after the C half tile
+  static_assert(RED + 16 * 512 * 4 <= NS * SB, "BN reduction slots must fit");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * SB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave / WN, wn = wave % WN;
+  const int tiles_m = a.Ng / TM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ch0 = (bid % tiles_m) * TM, px0 = (bid / tiles_m) * TN;
+  const char* zero = reinterpret_cast<const char*>(&g_zero16);
+
+  const int pch = lane & 7;  // physical 16-byte chunk this lane fills
+  uint32_t abase[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int row = ((wave * NA + j) * 64 + lane) >> 3;  // < 256 = TM, and ch0 + TM <= Ng
+    abase[j] = 2u * ((uint32_t)(ch0 + row) * a.Kg + 8 * (pch ^ (row & 7)));
+  }
+  uint32_t pbase[NB];
+  int ihb[NB], iwb[NB], lchb[NB];
+  bool pok[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int row = ((wave * NB + j) * 64 + lane) >> 3;
+    const int m = px0 + row;
+    pok[j] = m < a.M;
+    const int mm = pok[j] ? m : 0;
+    const int n = (int)a.fOHW.div((uint32_t)mm), rem = mm - n * a.OH * a.OW;
+    const int oh = (int)a.fOW.div((uint32_t)rem), ow = rem - oh * a.OW;
+    pbase[j] = 2u * ((uint32_t)n * a.IH * a.IW * a.Ca);
+    ihb[j] = a.dgrad ? oh + a.ph : oh * a.sh - a.ph;
+    iwb[j] = a.dgrad ? ow + a.pw : ow * a.sw - a.pw;
+    lchb[j] = 8 * (pch ^ (row & 7));
+  }
+  auto issue = [&](int t, int buf) {
+    const int k0 = t * BK;
+    const int rs = (int)a.fCa.div((uint32_t)k0), c0 = k0 - rs * a.Ca;  // uniform: one tap per stage
+    const int r = (int)a.fS.div((uint32_t)rs), s = rs - r * a.S;
+    char* st = smem + buf * SB;
+    const char* wb = reinterpret_cast<const char*>(a.wt) + 2u * (uint32_t)k0;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) glds16(wb + abase[j], st + (wave * NA + j) * 1024);
+    const char* xb = reinterpret_cast<const char*>(a.act) + 2u * (uint32_t)c0;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int ih = a.dgrad ? ihb[j] - r : ihb[j] + r, iw = a.dgrad ? iwb[j] - s : iwb[j] + s;
+      const bool ok = pok[j] && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
+      const char* src = xb + pbase[j] + 2u * (uint32_t)((ih * a.IW + iw) * a.Ca + lchb[j]);
+      glds16(ok ? (const void*)src : (const void*)zero, st + AB + (wave * NB + j) * 1024);
+    }
+  };
+
+  f32x4 acc[WMT][WNT];
+#pragma unroll
+  for (int i = 0; i < WMT; ++i)
+#pragma unroll
+    for (int j = 0; j < WNT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nt = a.Kg / BK;
+  issue(0, 0);
+  for (int t = 0; t < nt; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage t landed for every wave; stage t - 1's buffer is free
+    if (t + 1 < nt) issue(t + 1, (t + 1) & 1);
+    const char* sA = smem + (t & 1) * SB;
+    const char* sB = sA + AB;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int lch = 4 * ks + (lane >> 4);
+      bf16x8 av[WMT], bv[WNT];
+#pragma unroll
+      for (int i = 0; i < WMT; ++i) {
+        const int row = wm * 64 + 16 * i + (lane & 15);
+        av[i] = *reinterpret_cast<const bf16x8*>(sA + row * 128 + 16 * (lch ^ (row & 7)));
+      }
+#pragma unroll
+      for (int j = 0; j < WNT; ++j) {
+        const int row = wn * WPX + 16 * j + (lane & 15);
+        bv[j] = *reinterpret_cast<const bf16x8*>(sB + row * 128 + 16 * (lch ^ (row & 7)));
+      }
+#pragma unroll
+      for (int i = 0; i < WMT; ++i)
+#pragma unroll
+        for (int j = 0; j < WNT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // every wave done with the stage buffers (no LDS-DMA outstanding)
+
+  bf16* Cs = reinterpret_cast<bf16*>(smem);
+  float* bred = reinterpret_cast<float*>(smem + RED);
+  const bool bst = !STATS && a.bx != nullptr;  // backward BN statistics (fixed vector per thread)
+  float s1[8], s2[8], mean8[8], sc8[8], sh8[8];
+  if (bst) {
+    const int ch = ch0 + 8 * (tid % VPR);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] = s2[e] = 0.f;
+      mean8[e] = a.bmean[ch + e];
+      sc8[e] = a.bfcoef ? a.bfcoef[2 * (ch + e)] : 0.f;
+      sh8[e] = a.bfcoef ? a.bfcoef[2 * (ch + e) + 1] : 0.f;
+    }
+  }
+  // forward BN statistics: channel c = tid % TM, rows q * 64 .. + 63 of each half
+  const int sc_c = tid % TM, sc_q = tid / TM;
+  const float shiftK = (STATS && a.bnshift) ? a.bnshift[ch0 + sc_c] : 0.f;
+  float f1 = 0.f, f2 = 0.f;
+  const int rows = min(TN, a.M - px0);
+#pragma unroll 1
+  for (int h = 0; h < 2; ++h) {
+    if (wn == h) {  // this wave's accumulators are pixels h * 128 .. + 127
+#pragma unroll
+      for (int i = 0; i < WMT; ++i) {
+        const int cl = wm * 64 + 16 * i + 4 * (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < WNT; ++j) {
+          const int pl = 16 * j + (lane & 15);
+          *reinterpret_cast<uint2*>(Cs + pl * CP + cl) =
+              make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int v = tid; v < HT * VPR; v += 512) {
+      const int row = v / VPR, cv = v - row * VPR;
+      const int px = px0 + h * HT + row, ch = ch0 + 8 * cv;
+      if (px < a.M) {
+        const size_t o = (size_t)px * a.Ng + ch;
+        uint4 xr = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t mb = 0u;
+        if (bst) {
+          xr = *reinterpret_cast<const uint4*>(a.bx + o);
+          if (a.bmask) mb = a.bmask[o >> 3];
+        }
+        u32x4 val = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
+        if (a.addend) val = join8(val, a.addend, a.amask, o);
+        *reinterpret_cast<u32x4*>(a.out + o) = val;
+        if (bst) bn_bwd_acc8(a, val, xr, mb, mean8, sc8, sh8, s1, s2);
+      }
+    }
+    if constexpr (STATS) {  // column sums of the stored (bf16) half tile
+      const int hr = min(max(rows - h * HT, 0), HT);
+      const uint16_t* col = reinterpret_cast<const uint16_t*>(Cs) + sc_c;
+      const int r0 = sc_q * (HT / 2), r1 = min(r0 + HT / 2, hr);
+      float u1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, u2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (r1 - r0 == HT / 2) {  // full: 8 independent rows per iteration
+        for (int r = r0; r < r1; r += 8) {
+          uint16_t hv[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) hv[u] = col[(r + u) * CP];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const float d = bf2f(hv[u]) - shiftK;
+            u1[u] += d;
+            u2[u] = fmaf(d, d, u2[u]);
+          }
+        }
+      } else {
+        for (int r = r0; r < r1; ++r) {
+          const float d = bf2f(col[r * CP]) - shiftK;
+          u1[0] += d;
+          u2[0] = fmaf(d, d, u2[0]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        f1 += u1[u];
+        f2 += u2[u];
+      }
+    }
+    __syncthreads();  // the half tile is read: the next half (or the reduction slots) may overwrite it
+  }
+  if (bst) bn_bwd_flush<512, VPR>(a, bred, s1, s2, px0 / TN, ch0);
+  if constexpr (STATS) {
+    bred[tid] = f1;
+    bred[512 + tid] = f2;
+    __syncthreads();
+    if (sc_q == 0) {
+      float* dst = a.bnpart + (size_t)(px0 / TN) * 2 * a.Ng + 2 * (ch0 + sc_c);
+      dst[0] = f1 + bred[tid + TM];
+      dst[1] = f2 + bred[512 + tid + TM];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Stem forward: 7x7 / stride 2 / pad 3 over an 8-channel (padded) image, 64 output channels,
 // output height and width multiples of 16 (ResNet-50's conv1 at any batch).  The generic gather
 // kernel re-fetches every input pixel from L2 for each of the 49 taps that read it (Kg = 392 in
@@ -2260,6 +2460,16 @@ static GldsPlan glds_plan(const ConvNArgs& a, bool wide, bool par) {
   return glds_plan_mnk(a.M, a.Ng, a.Kg);
 }
 
+// the 256 x 256 tile (conv_nhwc_glds256_kernel): 0 = never (default until measured), 1 = where
+// it fills the chip (>= 256 tiles, no split-K needed), 2 = wherever Ng % 256 == 0 (tests)
+static int g_conv_glds256 = 0;
+void nhwc_conv_set_glds256(int mode) { g_conv_glds256 = mode; }
+static bool glds256_fits(const ConvNArgs& a) {
+  if (g_conv_glds256 == 0 || a.Ng % 256 != 0 || a.Kg % 64 != 0) return false;
+  const int64_t tiles = (int64_t)(a.Ng / 256) * cdiv(a.M, 256);
+  return g_conv_glds256 == 2 || tiles >= 256;
+}
+
 size_t nhwc_conv_scratch_floats(int M, int Ng, int Kg) {
   // either kernel may run (the LDS-DMA one needs a wide layer: Kg % 64 == 0 is necessary)
   const ConvPlan p = conv_plan(M, Ng, Kg);
@@ -2319,6 +2529,18 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   ConvPlan p = cs.p;
   const bool wide = cs.wide;
   const GldsPlan gp = glds_plan(a, wide, cs.par);
+  if (gp.tm && glds256_fits(a)) {  // 256 x 256 tiles, no split-K
+    a.par = 0;
+    a.part = nullptr;
+    const int gx = cdiv(a.M, 256);
+    const bool bst = a.dgrad && a.bx && a.bnpart && gx <= 16384;
+    if (!bst) a.bx = nullptr;
+    if (!(a.bnpart && (bst || !a.dgrad) && gx <= 16384)) a.bnpart = nullptr;
+    const dim3 grid((a.Ng / 256) * gx);
+    if (a.bnpart && !bst) MX_LAUNCH(conv_nhwc_glds256_kernel<true>, grid, dim3(512), 0, st, a);
+    else MX_LAUNCH(conv_nhwc_glds256_kernel<false>, grid, dim3(512), 0, st, a);
+    return a.bnpart ? gx : 0;
+  }
   if (gp.tm && (gp.splits == 1 || scratch)) {
     a.par = 0;
     a.kt_per_split = gp.kt_per_split;

@@ -95,9 +95,45 @@ def test_conv_glds_kernel(cuda, case):
     assert _rel(wg.grad.cpu(), wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("case", [(2, 64, 14, 14, 256, 1, 1, 0), (1, 256, 9, 9, 256, 3, 1, 1),
+                                  (2, 512, 7, 7, 256, 1, 1, 0), (3, 64, 20, 20, 512, 1, 2, 0),
+                                  (2, 256, 16, 16, 256, 3, 1, 1)])
+def test_conv_glds256_kernel(cuda, case):
+    """The 256 x 256-tile LDS-DMA kernel (two stage buffers, C staged in two halves), forced on
+    every layer with 256 | output channels -- forward (incl. stride 2) and stride-1 data gradient,
+    partial pixel tiles -- vs the fp32 reference."""
+    from mxddp import native
+
+    C_ = native()
+    N, C, H, W, K, R, st, pd = case
+    torch.manual_seed(21)
+    x = torch.randn(N, H, W, C).to(torch.bfloat16)
+    w = torch.randn(K, C, R, R) * (2.0 / (C * R * R)) ** 0.5
+    xr = _nchw(x).requires_grad_()
+    wr = w.to(torch.bfloat16).float().requires_grad_()
+    yr = F.conv2d(xr, wr, None, st, pd)
+    gy = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(gy)
+    C_.nhwc_conv_set_glds(2)
+    C_.nhwc_conv_set_glds256(2)
+    try:
+        xg = x.to(cuda).requires_grad_()
+        wg = w.to(cuda).requires_grad_()
+        y = nhwc.conv2d(xg, wg, st, pd)
+        y.backward(gy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(cuda))
+        torch.cuda.synchronize()
+    finally:
+        C_.nhwc_conv_set_glds256(0)
+        C_.nhwc_conv_set_glds(1)
+    assert _rel(_nchw(y), yr.detach()) < 1e-2
+    assert _rel(_nchw(xg.grad), xr.grad) < 1e-2
+    assert _rel(wg.grad.cpu(), wr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("glds256", [0, 2])
 @pytest.mark.parametrize("masked", [False, True])
 @pytest.mark.parametrize("case", [(1, 256, 7, 7, 512, 3, 1, 1), (2, 64, 14, 14, 256, 1, 1, 0), (2, 64, 16, 32, 64, 3, 1, 1)])
-def test_conv_dgrad_addend(cuda, case, masked):
+def test_conv_dgrad_addend(cuda, case, masked, glds256):
     """dx = conv_transpose(dy) + addend fused in the data-gradient epilogue (split-K reduction and
     direct epilogue) == the two computed separately; masked: the addend's elements are kept only
     where their ReLU bit is set (the lazy identity-shortcut join)."""
@@ -120,9 +156,16 @@ def test_conv_dgrad_addend(cuda, case, masked):
     Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx0.data_ptr(), N, H, W, C, K, R, R, st, st, pd, pd, P, Q,
                        scr.data_ptr() if n else 0, s)
     bits = torch.randint(0, 256, (N * H * W * C // 8,), dtype=torch.uint8, device=cuda) if masked else None
-    Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx1.data_ptr(), N, H, W, C, K, R, R, st, st, pd, pd, P, Q,
-                       scr.data_ptr() if n else 0, s, add.data_ptr(), amask=bits.data_ptr() if masked else 0)
-    torch.cuda.synchronize()
+    if glds256:
+        Cn.nhwc_conv_set_glds(2)
+        Cn.nhwc_conv_set_glds256(glds256)
+    try:
+        Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx1.data_ptr(), N, H, W, C, K, R, R, st, st, pd, pd, P, Q,
+                           scr.data_ptr() if n else 0, s, add.data_ptr(), amask=bits.data_ptr() if masked else 0)
+        torch.cuda.synchronize()
+    finally:
+        Cn.nhwc_conv_set_glds256(0)
+        Cn.nhwc_conv_set_glds(1)
     ref = dx0.float() + (nhwc._mask_bits(add, bits) if masked else add).float()
     assert _rel(dx1, ref) < 1e-2
 
@@ -188,6 +231,25 @@ def test_bn_nhwc(cuda, C, relu, res):
                                           ((5, 64, 48, 32, 64, 3, 1), 2.0),  # the 3x3 / 64-channel band kernel
                                           ((2, 64, 56, 56, 64, 3, 1), 0.5)])  # (4-row bands: more rows than 256-px tiles)
 def test_bn_statistics_from_conv_epilogue(cuda, shape, offset):
+    _bn_stats_from_conv_epilogue(cuda, shape, offset)
+
+
+@pytest.mark.parametrize("shape,offset", [((4, 64, 14, 14, 256, 1, 0), 2.0), ((3, 256, 9, 9, 256, 3, 1), -1.0)])
+def test_bn_statistics_from_glds256_epilogue(cuda, shape, offset):
+    """The same through the 256 x 256-tile kernel's half-tile epilogue (forward statistics)."""
+    from mxddp import native
+
+    C_ = native()
+    C_.nhwc_conv_set_glds(2)
+    C_.nhwc_conv_set_glds256(2)
+    try:
+        _bn_stats_from_conv_epilogue(cuda, shape, offset)
+    finally:
+        C_.nhwc_conv_set_glds256(0)
+        C_.nhwc_conv_set_glds(1)
+
+
+def _bn_stats_from_conv_epilogue(cuda, shape, offset):
     """conv2d(..., bn=bn) -> batch_norm: the LDS-DMA conv's epilogue computes the BN partial sums
     (shifted by the running mean) and the BN skips its statistics pass; same output, running
     statistics and gradients as the separate pass (incl. a partial last pixel tile and outputs
@@ -218,7 +280,7 @@ def test_bn_statistics_from_conv_epilogue(cuda, shape, offset):
 
 
 @pytest.mark.parametrize("glds,stride,relu", [(2, 1, True), (2, 1, False), (0, 1, True), (0, 2, True),
-                                              (0, 1, False)])
+                                              (0, 1, False), (256, 1, True), (256, 1, False)])
 def test_bn_backward_statistics_from_dgrad_epilogue(cuda, glds, stride, relu):
     """BN -> conv: the conv's data-gradient epilogue computes the BN's backward partial sums
     (sum g, sum g (x - mean), g masked by the BN's fused ReLU) and the BN backward skips its
@@ -227,13 +289,14 @@ def test_bn_backward_statistics_from_dgrad_epilogue(cuda, glds, stride, relu):
     from mxddp import native
 
     C = native()
-    N, Cin, H, W, K = 4, 64, 16, 16, 128
+    N, Cin, H, W, K = (4, 64, 16, 16, 128) if glds != 256 else (2, 256, 10, 10, 128)  # 256: Cin-wide dgrad tile
     torch.manual_seed(11)
     x = (torch.randn(N, H, W, Cin) + 0.5).to(torch.bfloat16).to(cuda)
     w = (torch.randn(K, Cin, 3, 3) * 0.05).to(cuda)
     outs, used = [], []
     try:
-        C.nhwc_conv_set_glds(glds)
+        C.nhwc_conv_set_glds(2 if glds == 256 else glds)
+        C.nhwc_conv_set_glds256(2 if glds == 256 else 0)
         for fused in (False, True):
             nhwc._BN_STATS_IN_DGRAD = fused
             bn = nn.BatchNorm2d(Cin).to(cuda)
@@ -252,6 +315,7 @@ def test_bn_backward_statistics_from_dgrad_epilogue(cuda, glds, stride, relu):
             outs.append((xg.grad.float().cpu(), wg.grad.cpu(), bn.weight.grad.cpu(), bn.bias.grad.cpu()))
     finally:
         nhwc._BN_STATS_IN_DGRAD = nhwc._BN_STATS_IN_CONV
+        C.nhwc_conv_set_glds256(0)
         C.nhwc_conv_set_glds(1)
     assert used == [0, 1], used  # the fused run really took the epilogue's statistics
     for a, b in zip(*outs):
