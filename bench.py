@@ -78,6 +78,8 @@ def parse():
     ap.add_argument("--lr", type=float, default=0.01, help="SGD lr (momentum 0.9, wd 1e-4 as the reference)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
                     help="GEMM precision of the layers path (headline is fp32, >= the reference's precision)")
+    ap.add_argument("--conv-tile256", type=int, default=0, choices=[0, 1],
+                    help="bf16 NHWC convs: the 256 x 256-tile LDS-DMA kernel on layers with >= 256 tiles (A/B)")
     ap.add_argument("--cpu", action="store_true",
                     help="BASELINE config 1: single process on the CPU (the reference's single_gpu.py CPU fallback)")
     ap.add_argument("--phase-profile", type=int, default=0, metavar="STEPS",
@@ -109,6 +111,10 @@ def main():
             print(f"bench.py: --gpus {a.gpus} needs a launcher (torch.distributed.run)", file=sys.stderr)
             sys.exit(2)
     inf = C.init_distributed(use_gpu=True)
+    if a.conv_tile256:
+        from mxddp import native as _native
+
+        _native().nhwc_conv_set_glds256(a.conv_tile256)
     if a.dtype != "fp32":
         if a.impl == "fused":
             a.impl = "layers"  # the fused MNIST engine is fp32-only
@@ -248,7 +254,7 @@ def main():
                        "image": "x".join(map(str, spec.input_shape)), "parallelism": f"dp{a.gpus}", "impl": a.impl,
                        # how the timed steps were actually launched (autotune may pick eager mode 0)
                        "graph": _fused_graph(a, tr) or getattr(a, "layers_graph", False),
-                       **_fused_config(a, tr)},
+                       **_fused_config(a, tr), **({"conv_tile256": 1} if a.conv_tile256 else {})},
             **extra,
         }
         if C.shared_devices():
@@ -269,8 +275,9 @@ def _fused_config(a, tr) -> dict:
     if a.impl != "fused":
         return {}
     if a.model == "keras_cnn":
-        return {"optimizer": "adam (Keras eps-hat, lr 1e-3)",
-                "transport": ("peer" if tr.eng.peer_active else "rccl") if tr.eng.reducer_active else "none"}
+        return {"optimizer": "adam (Keras eps-hat, lr 1e-3)", "graph_mode": tr.eng.graph_mode,
+                "buckets": tr.bucket_strategy if tr.eng.reducer_active else "none",
+                "transport": tr.active_transport, "autotune": tr.tuned}
     if a.model == "mlp":
         return {"optimizer": "adam (Chainer eps-hat, lr 1e-3)", "graph_mode": tr.eng.graph_mode,
                 "buckets": tr.bucket_strategy if tr.eng.reducer_active else "none",
