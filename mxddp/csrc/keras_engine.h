@@ -52,7 +52,9 @@ class KerasEngine {
     reducer_->set_padding(KerasLayout::total, capacity, multiple);
   }
   // peer transport: the exchange co-scheduled with Adam in one launch (keras_fused_exchange_adam)
-  // instead of a separate all-reduce; false (and off) when no opened peer transport can take it
+  // instead of a separate all-reduce; false (and off) when no opened peer transport can take it.
+  // The PeerComm's other exchanges may run before / after only across a synchronisation of every
+  // rank (see kx_kernel).
   bool set_coscheduled(bool on);
   bool coscheduled() const { return coscheduled_; }
   void set_external_batch(bool on) { external_ = on; }

@@ -848,8 +848,12 @@ __global__ __launch_bounds__(256) void ko_kernel(KerasFused f, KoPlan plan, int 
 // `rank` (one-shot: W-1 remote stores per value, all links at once), publishes its per-block
 // flag, waits for the peers' flags of the same block (peer_device.h; bounded, no grid barrier),
 // sums the W copies in rank order 0..W-1 (bit-identical on every rank) and applies Adam to the
-// average.  Slots / flags / epochs are the PeerComm's, so this alternates freely with its other
-// kernels; 182 blocks fit the 256 flag sets.
+// average.  Slots / flags / epochs are the PeerComm's (182 blocks fit its 256 flag sets), but the
+// block partition is this kernel's own: between KX calls and the PeerComm's other exchanges every
+// rank's stream must be synchronised (the trainers switch strategies only across a host sync and
+// barrier, FusedTrainerBase.autotune), or a block could push into a slot region another block
+// of a different partition is still reading.  Consecutive KX calls are ordered by the per-block
+// flags alone.
 constexpr int kKxThreads = 512;
 
 __global__ __launch_bounds__(kKxThreads) void kx_kernel(KerasFused f, PeerArgs a) {
