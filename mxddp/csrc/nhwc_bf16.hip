@@ -1971,28 +1971,28 @@ __global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
   // sums are tree-combined in LDS in a fixed order (deterministic).  The per-channel inputs of
   // the finalize (gamma, beta, running stats, x[0][c]) are loaded by the 8 owner threads before
   // the reduction so their latency overlaps it.
-  constexpr int RG = 128, MAXR = 8;
+  constexpr int RG = 128, MAXR = 16;
   __shared__ float red[2][RG][8];
   const int cl = threadIdx.x & 7, rg = threadIdx.x >> 3, c = blockIdx.x * 8 + cl;
   const bool cok = c < a.C;
   const size_t pitch = 2 * (size_t)a.C;
   float s1 = 0.f, s2 = 0.f;
-  // passes of RG * MAXR rows (one unless the partials came from a conv epilogue: one row per
-  // 256-pixel tile, up to ~12 K rows)
+  // passes of RG * MAXR = 2048 rows, every (s1, s2) pair of a pass one 8-byte load issued before
+  // the first is summed (one memory round trip per pass; two passes cover the conv-epilogue
+  // partials of a whole batch-256 ResNet-50 layer -- one row per 256-pixel tile)
   for (int base = 0; cok && base < a.gx; base += RG * MAXR) {
-    float t1[MAXR], t2[MAXR];
+    float2 t[MAXR];
 #pragma unroll
     for (int u = 0; u < MAXR; ++u) {
       const int b = base + rg + RG * u;
       const bool ok = b < a.gx;
-      const float* q = a.part + (size_t)(ok ? b : 0) * pitch + 2 * c;
-      t1[u] = ok ? q[0] : 0.f;
-      t2[u] = ok ? q[1] : 0.f;
+      const float2 v = *reinterpret_cast<const float2*>(a.part + (size_t)(ok ? b : 0) * pitch + 2 * c);
+      t[u] = ok ? v : make_float2(0.f, 0.f);
     }
 #pragma unroll
     for (int u = 0; u < MAXR; ++u) {
-      s1 += t1[u];
-      s2 += t2[u];
+      s1 += t[u].x;
+      s2 += t[u].y;
     }
   }
   // per-channel inputs of the finalize, fetched while the reduction runs
