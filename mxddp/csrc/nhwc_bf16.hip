@@ -2072,13 +2072,19 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
     sc[2 * j + 1] = q.z;
     sh[2 * j + 1] = q.w;
   }
+  // loads at clamped indices, issued unconditionally (a per-lane `i < total ? load : 0` makes
+  // hipcc branch around each load and split it into dwords with a vmcnt(0) per element); only
+  // the stores are masked
+  const uint4* x4 = reinterpret_cast<const uint4*>(a.x);
+  const uint4* r4 = reinterpret_cast<const uint4*>(a.res);
   for (int i0 = i00; i0 < total; i0 += 2 * step) {
-    uint4 xr[2], rr[2];
+    const int ic[2] = {i0, min(i0 + step, total - 1)};
+    uint4 xr[2], rr[2] = {z, z};
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int i = i0 + u * step;
-      xr[u] = i < total ? reinterpret_cast<const uint4*>(a.x)[i] : z;
-      if (a.res) rr[u] = i < total ? reinterpret_cast<const uint4*>(a.res)[i] : z;
+    for (int u = 0; u < 2; ++u) xr[u] = x4[ic[u]];
+    if (r4) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) rr[u] = r4[ic[u]];
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -2130,17 +2136,25 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv f
     }
   }
   const bool bmask = !XM && a.relu && a.mask;
+  const bool ymask = !XM && a.relu && !a.mask;
+  // clamped, unconditional loads (see bn_nhwc_apply_k); the mask source is a uniform branch
+  const uint4 *g4 = reinterpret_cast<const uint4*>(a.dy), *x4 = reinterpret_cast<const uint4*>(a.x),
+              *y4 = reinterpret_cast<const uint4*>(a.y);
   for (int i0 = i00; i0 < total; i0 += 2 * step) {
-    uint4 gr[2], xr[2], yr[2];
-    uint32_t mb[2];
+    const int ic[2] = {i0, min(i0 + step, total - 1)};
+    uint4 gr[2], xr[2], yr[2] = {z, z};
+    uint32_t mb[2] = {0u, 0u};
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int i = i0 + u * step;
-      const bool ok = i < total;
-      gr[u] = ok ? reinterpret_cast<const uint4*>(a.dy)[i] : z;
-      xr[u] = ok ? reinterpret_cast<const uint4*>(a.x)[i] : z;
-      if (bmask) mb[u] = ok ? a.mask[i] : 0u;
-      else if (!XM && a.relu) yr[u] = ok ? reinterpret_cast<const uint4*>(a.y)[i] : z;
+      gr[u] = g4[ic[u]];
+      xr[u] = x4[ic[u]];
+    }
+    if (bmask) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) mb[u] = a.mask[ic[u]];
+    } else if (ymask) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) yr[u] = y4[ic[u]];
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
