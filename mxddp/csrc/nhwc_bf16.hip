@@ -243,13 +243,22 @@ __global__ __launch_bounds__(256, 2) void conv_nhwc_kernel(ConvNArgs a) {
   // two register stages: the loads of k-tile t + 2 are issued while tile t is computed, so each
   // has a whole compute phase plus a barrier to land (one stage hid L2 latency only)
   u32x4 ra0[EA], rb0[EB], ra1[EA], rb1[EB];  // (set 1 unused by the one-stage 128 x 128 tile)
+  bool ma0[EA], mb0[EB], ma1[EA], mb1[EB];     // their validity: applied when staged into LDS
   const u32x4 z4 = {0u, 0u, 0u, 0u};
   // wide path: per-lane byte bases (loop invariant)
   uint32_t abase[EA], pbase[EB];
   int ihb[EB], iwb[EB];
+  bool aok[EA];
+#pragma unroll
+  for (int i = 0; i < EA; ++i) aok[i] = ch0 + row0 + 32 * i < a.Ng;
+  // every operand load below is issued unconditionally from a valid (clamped) address and its
+  // validity kept beside it; the mask is applied when the stage is written to LDS.  (A per-lane
+  // `ok ? load : 0` makes hipcc branch around each load, which it then cannot count, and a mask
+  // applied right after the load is scheduled there: either way the loads of the second register
+  // stage were waited for before the current stage's MFMAs.)
   if constexpr (kWide) {
 #pragma unroll
-    for (int i = 0; i < EA; ++i) abase[i] = 2u * ((uint32_t)(ch0 + row0 + 32 * i) * a.Kg + 8 * kv);
+    for (int i = 0; i < EA; ++i) abase[i] = 2u * ((uint32_t)(aok[i] ? ch0 + row0 + 32 * i : 0) * a.Kg + 8 * kv);
 #pragma unroll
     for (int i = 0; i < EB; ++i) {
       pbase[i] = 2u * ((uint32_t)pn[i] * a.IH * a.IW * a.Ca + 8 * kv);
@@ -257,7 +266,7 @@ __global__ __launch_bounds__(256, 2) void conv_nhwc_kernel(ConvNArgs a) {
       iwb[i] = a.dgrad ? pow_[i] + a.pw : pow_[i] * a.sw - a.pw;
     }
   }
-  auto gload = [&](int k0, u32x4 (&ra)[EA], u32x4 (&rb)[EB]) {
+  auto gload = [&](int k0, u32x4 (&ra)[EA], u32x4 (&rb)[EB], bool (&ma)[EA], bool (&mb)[EB]) {
     if constexpr (kWide) {
       const int rs = (int)a.fCa.div((uint32_t)k0), c0 = k0 - rs * a.Ca;  // uniform
       int r, s, kw = k0;
@@ -272,8 +281,10 @@ __global__ __launch_bounds__(256, 2) void conv_nhwc_kernel(ConvNArgs a) {
       }
       const char* wb = reinterpret_cast<const char*>(a.wt) + 2u * (uint32_t)kw;
 #pragma unroll
-      for (int i = 0; i < EA; ++i)
-        ra[i] = (ch0 + row0 + 32 * i < a.Ng) ? *reinterpret_cast<const u32x4*>(wb + abase[i]) : z4;
+      for (int i = 0; i < EA; ++i) {
+        ra[i] = *reinterpret_cast<const u32x4*>(wb + abase[i]);
+        ma[i] = aok[i];
+      }
       const char* xb = reinterpret_cast<const char*>(a.act) + 2u * (uint32_t)c0;
 #pragma unroll
       for (int i = 0; i < EB; ++i) {
@@ -289,8 +300,9 @@ __global__ __launch_bounds__(256, 2) void conv_nhwc_kernel(ConvNArgs a) {
           ok = ok && th >= 0 && tw >= 0 && ih * a.sh == th && iw * a.sw == tw;
         }
         ok = ok && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
-        const uint32_t off = pbase[i] + 2u * (uint32_t)((ih * a.IW + iw) * a.Ca);
-        rb[i] = ok ? *reinterpret_cast<const u32x4*>(xb + off) : z4;
+        const uint32_t off = ok ? pbase[i] + 2u * (uint32_t)((ih * a.IW + iw) * a.Ca) : 0u;
+        rb[i] = *reinterpret_cast<const u32x4*>(xb + off);
+        mb[i] = ok;
       }
       return;
     }
@@ -301,8 +313,9 @@ __global__ __launch_bounds__(256, 2) void conv_nhwc_kernel(ConvNArgs a) {
     const int r = (int)a.fS.div((uint32_t)rs), s = rs - r * a.S;
 #pragma unroll
     for (int i = 0; i < EA; ++i) {
-      const int row = ch0 + row0 + 32 * i;
-      ra[i] = (kok && row < a.Ng) ? *reinterpret_cast<const u32x4*>(a.wt + (size_t)row * a.Kg + k) : z4;
+      const int row = aok[i] ? ch0 + row0 + 32 * i : 0;
+      ra[i] = *reinterpret_cast<const u32x4*>(a.wt + (size_t)row * a.Kg + kk);
+      ma[i] = kok && aok[i];
     }
 #pragma unroll
     for (int i = 0; i < EB; ++i) {
@@ -318,15 +331,19 @@ __global__ __launch_bounds__(256, 2) void conv_nhwc_kernel(ConvNArgs a) {
         ok = ok && th >= 0 && tw >= 0 && ih * a.sh == th && iw * a.sw == tw;
       }
       ok = ok && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
-      rb[i] = ok ? *reinterpret_cast<const u32x4*>(a.act + (((size_t)pn[i] * a.IH + ih) * a.IW + iw) * a.Ca + c)
-                 : z4;
+      const size_t off = ok ? (((size_t)pn[i] * a.IH + ih) * a.IW + iw) * a.Ca + c : 0;
+      rb[i] = *reinterpret_cast<const u32x4*>(a.act + off);
+      mb[i] = ok;
     }
   };
-  auto sstore = [&](int buf, const u32x4 (&ra)[EA], const u32x4 (&rb)[EB]) {
+  auto sstore = [&](int buf, const u32x4 (&ra)[EA], const u32x4 (&rb)[EB], const bool (&ma)[EA],
+                    const bool (&mb)[EB]) {
 #pragma unroll
-    for (int i = 0; i < EA; ++i) *reinterpret_cast<u32x4*>(&As[buf][(row0 + 32 * i) * LD + 8 * kv]) = ra[i];
+    for (int i = 0; i < EA; ++i)
+      *reinterpret_cast<u32x4*>(&As[buf][(row0 + 32 * i) * LD + 8 * kv]) = ma[i] ? ra[i] : z4;
 #pragma unroll
-    for (int i = 0; i < EB; ++i) *reinterpret_cast<u32x4*>(&Bs[buf][(row0 + 32 * i) * LD + 8 * kv]) = rb[i];
+    for (int i = 0; i < EB; ++i)
+      *reinterpret_cast<u32x4*>(&Bs[buf][(row0 + 32 * i) * LD + 8 * kv]) = mb[i] ? rb[i] : z4;
   };
 
   f32x4 acc[WMT][WNT];
@@ -358,37 +375,37 @@ __global__ __launch_bounds__(256, 2) void conv_nhwc_kernel(ConvNArgs a) {
   };
   if constexpr (TM * TN <= 64 * 128) {
     if (nt > 0) {
-      gload(kt0 * BK, ra0, rb0);
-      if (nt > 1) gload((kt0 + 1) * BK, ra1, rb1);
-      sstore(0, ra0, rb0);
+      gload(kt0 * BK, ra0, rb0, ma0, mb0);
+      if (nt > 1) gload((kt0 + 1) * BK, ra1, rb1, ma1, mb1);
+      sstore(0, ra0, rb0, ma0, mb0);
     }
     __syncthreads();
     // unrolled by two so each register stage is a compile-time array (runtime-indexed register
     // arrays would go to scratch): even steps compute buffer 0 and hold stage set 1, odd steps
     // the reverse
     for (int t = 0; t < nt; t += 2) {
-      if (t + 2 < nt) gload((kt0 + t + 2) * BK, ra0, rb0);
+      if (t + 2 < nt) gload((kt0 + t + 2) * BK, ra0, rb0, ma0, mb0);
       compute(0);
-      if (t + 1 < nt) sstore(1, ra1, rb1);
+      if (t + 1 < nt) sstore(1, ra1, rb1, ma1, mb1);
       __syncthreads();
       if (t + 1 >= nt) break;
-      if (t + 3 < nt) gload((kt0 + t + 3) * BK, ra1, rb1);
+      if (t + 3 < nt) gload((kt0 + t + 3) * BK, ra1, rb1, ma1, mb1);
       compute(1);
-      if (t + 2 < nt) sstore(0, ra0, rb0);
+      if (t + 2 < nt) sstore(0, ra0, rb0, ma0, mb0);
       __syncthreads();
     }
   } else {
     // 128 x 128: one register stage (two would exceed 256 VGPRs and spill)
     if (nt > 0) {
-      gload(kt0 * BK, ra0, rb0);
-      sstore(0, ra0, rb0);
+      gload(kt0 * BK, ra0, rb0, ma0, mb0);
+      sstore(0, ra0, rb0, ma0, mb0);
     }
     __syncthreads();
     for (int t = 0; t < nt; ++t) {
       const int cur = t & 1;
-      if (t + 1 < nt) gload((kt0 + t + 1) * BK, ra0, rb0);
+      if (t + 1 < nt) gload((kt0 + t + 1) * BK, ra0, rb0, ma0, mb0);
       compute(cur);
-      if (t + 1 < nt) sstore(cur ^ 1, ra0, rb0);
+      if (t + 1 < nt) sstore(cur ^ 1, ra0, rb0, ma0, mb0);
       __syncthreads();
     }
   }
@@ -1310,9 +1327,11 @@ __global__ __launch_bounds__(256) void wgrad_nhwc_kernel(WgNArgs a) {
   const u32x4 z4 = {0u, 0u, 0u, 0u};
   auto gload = [&](int p0) {
 #pragma unroll
-    for (int i = 0; i < EA; ++i) {
+    for (int i = 0; i < EA; ++i) {  // unconditional loads from clamped addresses, masked after
       const int pix = p0 + rowa0 + (256 / VA) * i;
-      ra[i] = (pix < pend && k_ok) ? *reinterpret_cast<const u32x4*>(a.dy + (size_t)pix * a.Kout + m0 + 8 * cva) : z4;
+      const bool ok = pix < pend && k_ok;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(a.dy + (ok ? (size_t)pix * a.Kout + m0 + 8 * cva : 0));
+      ra[i] = ok ? v : z4;
     }
 #pragma unroll
     for (int i = 0; i < EB; ++i) {
@@ -1323,7 +1342,8 @@ __global__ __launch_bounds__(256) void wgrad_nhwc_kernel(WgNArgs a) {
       const int p = (int)a.fQ.div((uint32_t)rem), q = rem - p * a.Q;
       const int h = p * a.sh - a.ph + br, w = q * a.sw - a.pw + bs;
       const bool xok = ok && col_ok && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-      rb[i] = xok ? *reinterpret_cast<const u32x4*>(a.x + (((size_t)n * a.H + h) * a.W + w) * a.Ca + bc) : z4;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(a.x + (xok ? (((size_t)n * a.H + h) * a.W + w) * a.Ca + bc : 0));
+      rb[i] = xok ? v : z4;
     }
   };
   auto sstore = [&](int buf) {
