@@ -10,6 +10,16 @@ namespace mnist {
 using L = MnistLayout;
 constexpr int kPack = 18432;  // 64*32*9 conv2 weights
 
+// PyTorch SGD (momentum, weight decay; DDP's 1 / world size in gscale) with every rounding
+// spelled out: the fused fc1 update in F5 and the flat SGD kernel produce bit-identical results
+// whichever path a step takes (left to the compiler, the contraction of g * gscale + wd * p into an
+// fma differed between the two, one ulp apart).
+__device__ __forceinline__ void sgd_upd(float& p, float& buf, float g, float gscale, float mom, float wd, float lr) {
+  const float gg = __fmaf_rn(wd, p, __fmul_rn(g, gscale));
+  buf = __fmaf_rn(mom, buf, gg);
+  p = __fmaf_rn(-lr, buf, p);
+}
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }

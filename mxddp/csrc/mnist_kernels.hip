@@ -696,9 +696,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           for (int j = 0; j < 4; ++j) {
             const int n = 32 * w + 16 * a + 4 * g + j;
             const size_t e = L::fw1 + (size_t)n * 9216 + c0 + 16 * c + m;
-            float pv = wsm[n * kF5P + 16 * c + m];
-            const float bv = f.sgd_mom * mb[a][c][j] + (acc[a][c][j] + f.sgd_wd * pv);
-            pv -= lr * bv;
+            float pv = wsm[n * kF5P + 16 * c + m], bv = mb[a][c][j];
+            sgd_upd(pv, bv, acc[a][c][j], 1.f, f.sgd_mom, f.sgd_wd, lr);
             f.mom[e] = bv;
             f.p[e] = pv;
           }
@@ -777,8 +776,7 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
 #pragma unroll
       for (int r = 0; r < 9; ++r) {
         const float gg = red[576 + 9 * threadIdx.x + r];
-        bb[r] = mom * bb[r] + (gg * gscale + wd * pe[r]);
-        pe[r] -= lr * bb[r];
+        sgd_upd(pe[r], bb[r], gg, gscale, mom, wd, lr);
         f.g[e0 + r] = gg;
         buf[e0 + r] = bb[r];
         f.p[e0 + r] = pe[r];
@@ -844,14 +842,10 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
       g4[i] = gv;
     }
     float4 bv = b4[i];
-    bv.x = mom * bv.x + (gv.x * gscale + wd * pv.x);
-    bv.y = mom * bv.y + (gv.y * gscale + wd * pv.y);
-    bv.z = mom * bv.z + (gv.z * gscale + wd * pv.z);
-    bv.w = mom * bv.w + (gv.w * gscale + wd * pv.w);
-    pv.x -= lr * bv.x;
-    pv.y -= lr * bv.y;
-    pv.z -= lr * bv.z;
-    pv.w -= lr * bv.w;
+    sgd_upd(pv.x, bv.x, gv.x, gscale, mom, wd, lr);
+    sgd_upd(pv.y, bv.y, gv.y, gscale, mom, wd, lr);
+    sgd_upd(pv.z, bv.z, gv.z, gscale, mom, wd, lr);
+    sgd_upd(pv.w, bv.w, gv.w, gscale, mom, wd, lr);
     b4[i] = bv;
     p4[i] = pv;
   }
@@ -871,8 +865,7 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
     }
 #pragma unroll
     for (int r = 0; r < 9; ++r) {
-      bb[r] = mom * bb[r] + (gg[r] * gscale + wd * pe[r]);
-      pe[r] -= lr * bb[r];
+      sgd_upd(pe[r], bb[r], gg[r], gscale, mom, wd, lr);
       buf[e0 + r] = bb[r];
       f.p[e0 + r] = pe[r];
     }
@@ -880,9 +873,10 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
   }
   if (blockIdx.x == 0 && threadIdx.x < (int)(L::total - 4 * n4)) {  // 2-element tail (fc2.bias)
     const int e = 4 * n4 + threadIdx.x;
-    const float gg = f.g[e] * gscale + wd * f.p[e];
-    buf[e] = mom * buf[e] + gg;
-    f.p[e] -= lr * buf[e];
+    float pe = f.p[e], bb = buf[e];
+    sgd_upd(pe, bb, f.g[e], gscale, mom, wd, lr);
+    buf[e] = bb;
+    f.p[e] = pe;
   }
 }
 

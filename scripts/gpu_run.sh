@@ -21,6 +21,8 @@
 #   coll         MNIST with RCCL collectives forced at one rank
 #   cpu          BASELINE config 1
 #   copies_pyr / copies_rn   torch.profiler census of the device copies in a layer-path step
+#   trace_pyr    kernel + HIP API trace of the graphed PyramidNet step (where its copies come from)
+#   diag_bnstats backward BN statistics of the data-gradient epilogues vs torch
 source "$(dirname "$0")/gpu_check.sh"
 rm -f gpurun_out/steps.log
 
@@ -91,6 +93,8 @@ for step in "$@"; do
     keras_ws8) ws keras_ws8 8 --model keras_cnn --steps 100 --warmup 10 ;;
     pyr_ws8) ws pyr_ws8 8 --model pyramidnet110 --batch 8 --steps 5 --warmup 2 ;;
     rn_ws8) ws rn_ws8 8 --model resnet50 --dtype bf16 --batch 8 --steps 5 --warmup 2 ;;
+    trace_pyr) run trace_pyr 300 rocprofv3 --kernel-trace --hip-trace -d gpurun_out/trace_pyr -o run --output-format csv -- python bench.py --model pyramidnet110 --steps 3 --warmup 2 --min-warmup-ms 0 ;;
+    diag_bnstats) run diag_bnstats 300 python scripts/diag_bn_dgrad_stats.py ;;
     copies_pyr) run copies_pyr 300 python scripts/diag_copies.py pyramidnet110 fp32 64 ;;
     copies_rn) run copies_rn 300 python scripts/diag_copies.py resnet50 bf16 32 ;;
     *) echo "gpu_run.sh: unknown step $step"; exit 2 ;;

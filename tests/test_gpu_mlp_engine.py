@@ -60,8 +60,11 @@ def _check(tr, batches, lr, B, init):
         assert abs(a - b) < 1e-4 * max(1.0, abs(b)), (losses, ref_losses)
     assert tr.adam_steps == len(batches)
     sd = tr.state_dict()
+    # normwise 1e-4: Adam divides each update by its own sqrt(v), so a gradient element that is
+    # rounding noise in both implementations still moves its weight by ~lr -- elementwise rtol
+    # at fp32 precision would test the noise, not the step
     for k, v in ref_sd.items():
-        assert torch.allclose(sd[k], v, rtol=1e-4, atol=1e-6), (k, (sd[k] - v).abs().max())
+        assert (sd[k] - v).abs().max() <= 1e-4 * v.abs().max(), (k, (sd[k] - v).abs().max())
     moved = max((sd[k] - init[k]).abs().max().item() for k in init)
     assert moved > 1e-4
 
