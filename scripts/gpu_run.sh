@@ -9,7 +9,7 @@
 # Steps:
 #   suite        full GPU test suite (-x)      suite_all    the same, every failure reported
 #   smoke        __graft_entry__.smoke()
-#   t_<name>     one test file, tests/test_gpu_<name>.py
+#   t_<name>     one test file, tests/test_gpu_<name>.py      tsel   the pytest selection in $TSEL
 #   driver       bench at the driver's length  long         2,000-step bench
 #   prof_mnist   rocprofv3 kernel trace of the MNIST step
 #   pmc_mnist    counter passes of the MNIST step (eager launches, one pass per run)
@@ -54,6 +54,7 @@ for step in "$@"; do
   case "$step" in
     suite) run suite 1500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     suite_all) run suite_all 1500 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
+    tsel) run tsel 900 python -u -m pytest ${TSEL:?set TSEL to the pytest selection} -m gpu -v --timeout 120 --timeout-method thread ;;
     t_*) run "$step" 900 python -u -m pytest "tests/test_gpu_${step#t_}.py" -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     driver) run driver 300 python bench.py --steps 20 --warmup 5 ;;
