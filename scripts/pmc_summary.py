@@ -6,7 +6,8 @@ Each csv is one ``--pmc`` pass (scripts/gpu_run.sh ``pmc``: SQ set A, SQ set B, 
 WRITE_SIZE); the kernel-trace csv next to each one gives the dispatch durations.  Counters are
 averaged per kernel over its dispatches, then combined:
 
-  mfma%   SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 256 CUs x 4 SIMDs)
+  mfma%   SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 256 CUs x 4 SIMDs): GRBM_GUI_ACTIVE
+          reads ~8x the kernel cycles on MI355X (one count per XCD), the MFMA counter is per SIMD
   wait%   SQ_WAIT_ANY / SQ_WAVE_CYCLES          (waves waiting on anything)
   winst%  SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES     (waves waiting for an instruction's operands)
   ldsc%   SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS
@@ -21,7 +22,7 @@ import os
 import sys
 from collections import defaultdict
 
-CUS, SIMDS = 256, 4
+CUS, SIMDS, XCDS = 256, 4, 8
 
 
 def short(name: str) -> str:
@@ -65,7 +66,7 @@ def main(paths):
         return 100.0 * a / b if a is not None and b else float("nan")
 
     for tot, k, n, us, a in rows:
-        mfma = pct(a.get("SQ_VALU_MFMA_BUSY_CYCLES"), a.get("GRBM_GUI_ACTIVE", 0) * CUS * SIMDS)
+        mfma = pct(a.get("SQ_VALU_MFMA_BUSY_CYCLES"), a.get("GRBM_GUI_ACTIVE", 0) / XCDS * CUS * SIMDS)
         wait = pct(a.get("SQ_WAIT_ANY"), a.get("SQ_WAVE_CYCLES"))
         winst = pct(a.get("SQ_WAIT_INST_ANY"), a.get("SQ_WAVE_CYCLES"))
         ldsc = pct(a.get("SQ_LDS_BANK_CONFLICT"), a.get("SQ_ACTIVE_INST_LDS"))
