@@ -1910,16 +1910,17 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
   for (int p0 = blockIdx.x * ppi + pr; p0 < a.Npix; p0 += UNR * pstep) {
     uint4 xr[UNR], gr[UNR], yr[UNR];
     uint32_t mb[UNR];
+    // loads at clamped rows issued unconditionally (the rows past Npix are skipped below): a
+    // per-lane `ok ? load : 0` would branch around each load and drain with a vmcnt(0) per row
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const int p = p0 + u * pstep;
-      const bool ok = p < a.Npix;
-      const size_t o = (size_t)(ok ? p : 0) * a.C + 8 * v;
-      xr[u] = ok ? *reinterpret_cast<const uint4*>(a.x + o) : make_uint4(0u, 0u, 0u, 0u);
+      const int p = min(p0 + u * pstep, a.Npix - 1);
+      const size_t o = (size_t)p * a.C + 8 * v;
+      xr[u] = *reinterpret_cast<const uint4*>(a.x + o);
       if (BWD) {
-        gr[u] = ok ? *reinterpret_cast<const uint4*>(a.dy + o) : make_uint4(0u, 0u, 0u, 0u);
-        if (ymask) yr[u] = ok ? *reinterpret_cast<const uint4*>(a.y + o) : make_uint4(0u, 0u, 0u, 0u);
-        if (bmask) mb[u] = ok ? a.mask[o >> 3] : 0u;
+        gr[u] = *reinterpret_cast<const uint4*>(a.dy + o);
+        if (ymask) yr[u] = *reinterpret_cast<const uint4*>(a.y + o);
+        if (bmask) mb[u] = a.mask[o >> 3];
       }
     }
 #pragma unroll
