@@ -75,5 +75,42 @@ def main():
         run(*c)
 
 
+def bn_pre_path():
+    """nhwc_bn_bwd with precomputed partial rows (one row of torch sums) vs its own statistics pass."""
+    Cn = native()
+    dev = torch.device("cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    torch.manual_seed(2)
+    N, H, W, C = 2, 10, 10, 256
+    npix = N * H * W
+    x = (torch.randn(N, H, W, C, device=dev) + 0.3).to(torch.bfloat16)
+    dy = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+    gamma = torch.rand(C, device=dev) + 0.5
+    beta = torch.randn(C, device=dev) * 0.2
+    mean = torch.empty(C, device=dev)
+    invstd = torch.empty(C, device=dev)
+    y = torch.empty_like(x)
+    scr = torch.empty(Cn.nhwc_bn_scratch_floats(npix, C), device=dev)
+    Cn.nhwc_bn_fwd(x.data_ptr(), 0, y.data_ptr(), gamma.data_ptr(), beta.data_ptr(), mean.data_ptr(),
+                   invstd.data_ptr(), 0, 0, 0, npix, C, 0.1, 1e-5, False, scr.data_ptr(), st, 0, 0, 0, 0, 0)
+    outs = []
+    for use_pre in (False, True):
+        dx = torch.empty_like(x)
+        dg = torch.empty(C, device=dev)
+        db = torch.empty(C, device=dev)
+        pre = None
+        if use_pre:
+            g = dy.float().reshape(-1, C)
+            pre = torch.stack([g.sum(0), (g * (x.float().reshape(-1, C) - mean)).sum(0)], 1).reshape(-1).contiguous()
+        Cn.nhwc_bn_bwd(dy.data_ptr(), x.data_ptr(), 0, gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                       dx.data_ptr(), 0, dg.data_ptr(), db.data_ptr(), npix, C, False, False, scr.data_ptr(), st, 0, 0,
+                       pre.data_ptr() if use_pre else 0, 1 if use_pre else 0)
+        torch.cuda.synchronize()
+        outs.append((dx.float(), dg.clone(), db.clone()))
+    for name, a, b in zip(("dx", "dgamma", "dbeta"), *outs):
+        print(f"bn_bwd pre path {name:7s} rel err {((a - b).abs().max() / (b.abs().max() + 1e-6)).item():.2e}")
+
+
 if __name__ == "__main__":
     main()
+    bn_pre_path()

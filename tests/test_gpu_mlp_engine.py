@@ -60,11 +60,13 @@ def _check(tr, batches, lr, B, init):
         assert abs(a - b) < 1e-4 * max(1.0, abs(b)), (losses, ref_losses)
     assert tr.adam_steps == len(batches)
     sd = tr.state_dict()
-    # normwise 1e-4: Adam divides each update by its own sqrt(v), so a gradient element that is
-    # rounding noise in both implementations still moves its weight by ~lr -- elementwise rtol
-    # at fp32 precision would test the noise, not the step
+    # the parameters relative to how far the 5 steps moved them (the losses above match at 1e-4):
+    # Adam divides each update by its own sqrt(v), so a gradient element that is rounding noise in
+    # both implementations still moves its weight by ~lr -- an elementwise fp32 tolerance would
+    # test that noise, not the step
     for k, v in ref_sd.items():
-        assert (sd[k] - v).abs().max() <= 1e-4 * v.abs().max(), (k, (sd[k] - v).abs().max())
+        step = (v - init[k]).norm()
+        assert (sd[k] - v).norm() <= 1e-3 * step, (k, ((sd[k] - v).norm() / step).item())
     moved = max((sd[k] - init[k]).abs().max().item() for k in init)
     assert moved > 1e-4
 
