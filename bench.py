@@ -229,6 +229,12 @@ def main():
                  "train_images": seen}
     else:
         extra = {}
+        if a.impl == "layers" and a.dtype == "bf16":
+            from mxddp.ops import nhwc as _nhwc
+
+            # BN backward passes whose statistics came from the consuming conv's data-gradient
+            # epilogue vs their own statistics pass (counted while the step was traced / captured)
+            extra = {"bn_bwd_stats": dict(_nhwc.BN_BWD_STATS)}
     if inf.rank == 0:
         from mxddp.models import get_spec
 

@@ -2,7 +2,7 @@
 conv shape at batch 32 (forward, data gradient, weight gradient): microseconds and TFLOP/s per
 direction, so the conv-kernel work can be prioritised by where the step time goes.
 
-    python scripts/bench_nhwc_layers.py [batch] [iters]
+    python scripts/bench_nhwc_layers.py [batch] [iters] [tile256]
 """
 import os
 import sys
@@ -36,8 +36,10 @@ def shapes(batch):
 def main():
     batch = int(sys.argv[1]) if len(sys.argv) > 1 else 32
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    tile256 = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # 1: the 256 x 256-tile kernel where it fits
     dev = torch.device("cuda")
     Cn = native()
+    Cn.nhwc_conv_set_glds256(tile256)
     st = torch.cuda.current_stream().cuda_stream
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     # floor: max(HBM bytes at 8 TB/s, FLOPs at the 2.5 PF bf16 dense peak), the same for all three
