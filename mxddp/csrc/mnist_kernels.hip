@@ -371,7 +371,6 @@ __global__ __launch_bounds__(64 * kF3Wv) void f3t_fc1_kernel(MnistFused f) {
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int kc = bid / tiles, tile = bid - kc * tiles, mt = tile >> 3, nt = tile & 7;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
-  if (f.synth && blockIdx.x == 0 && tid == 0) *f.counter += 1;  // F2 consumed it
   const int k0 = kc * kF3TK + w * kTW + 4 * g;
   const float4* A = reinterpret_cast<const float4*>(f.pool + (size_t)(16 * mt + m) * 9216 + k0);
   const float4* W = reinterpret_cast<const float4*>(f.p + L::fw1 + (size_t)(16 * nt + m) * 9216 + k0);
@@ -401,6 +400,9 @@ __global__ __launch_bounds__(64 * kF3Wv) void f3t_fc1_kernel(MnistFused f) {
                     ((red[4][row][col] + red[5][row][col]) + (red[6][row][col] + red[7][row][col]));
     fix_add(f.h + (16 * mt + row) * 128 + 16 * nt + col, v, kHScale);
   }
+  // F2 consumed the counter; bumped last so its load / wait does not hold wave 0 of block 0
+  // in front of the operand loads
+  if (f.synth && blockIdx.x == 0 && tid == 0) *f.counter += 1;
   MX_TRACE(f, 1, 1);
 }
 
@@ -522,6 +524,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int i = min(tid + 256 * k, 128 * kF5C4 - 1), r = i / kF5C4, c4 = i - r * kF5C4;
     vw.set(k, *reinterpret_cast<const float4*>(f.p + L::fw1 + (size_t)r * 9216 + c0 + c4 * 4));
   }
+  // every group-2 load issued before the first head conversion: otherwise the scheduler hoists an
+  // h fixed-point conversion above them and its wait delays all of group 2 by one load latency
+  __builtin_amdgcn_sched_barrier(0);
   // (1) stage the head operands
 #pragma unroll
   for (int k = 0; k < ND; ++k) {
