@@ -80,6 +80,8 @@ def parse():
                     help="GEMM precision of the layers path (headline is fp32, >= the reference's precision)")
     ap.add_argument("--conv-tile256", type=int, default=0, choices=[0, 1],
                     help="bf16 NHWC convs: the 256 x 256-tile LDS-DMA kernel on layers with >= 256 tiles (A/B)")
+    ap.add_argument("--f6w-split", type=int, default=0, choices=[0, 1, 2],
+                    help="fused MNIST: conv2 weight-gradient blocks per (image, ci half) (0 = the build default; A/B)")
     ap.add_argument("--cpu", action="store_true",
                     help="BASELINE config 1: single process on the CPU (the reference's single_gpu.py CPU fallback)")
     ap.add_argument("--phase-profile", type=int, default=0, metavar="STEPS",
@@ -115,6 +117,10 @@ def main():
         from mxddp import native as _native
 
         _native().nhwc_conv_set_glds256(a.conv_tile256)
+    if a.f6w_split:
+        from mxddp import native as _native
+
+        _native().mnist_set_f6w_split(a.f6w_split)
     if a.dtype != "fp32":
         if a.impl == "fused":
             a.impl = "layers"  # the fused MNIST engine is fp32-only
@@ -290,7 +296,14 @@ def _fused_config(a, tr) -> dict:
                 "transport": tr.active_transport, "autotune": tr.tuned}
     return {"graph_mode": tr.eng.graph_mode, "overlap": tr.eng.overlap, "merged_bucket": tr.eng.merged,
             "coscheduled_exchange": tr.eng.coscheduled,
-            "transport": tr.active_transport, "force_collectives": a.force_collectives, "autotune": tr.tuned}
+            "transport": tr.active_transport, "force_collectives": a.force_collectives, "autotune": tr.tuned,
+            "f6w_split": _f6w_split()}
+
+
+def _f6w_split() -> int:
+    from mxddp import native
+
+    return native().mnist_f6w_split()
 
 
 def _replica(a):

@@ -892,6 +892,13 @@ using namespace mnist;
 
 size_t mnist_fused_scratch_floats(int B) { return scratch_floats(B); }
 
+static int g_f6w_split = 1;
+void mnist_set_f6w_split(int split) {
+  if (split != 1 && split != 2) throw std::runtime_error("mnist_set_f6w_split: 1 or 2");
+  g_f6w_split = split;
+}
+int mnist_f6w_split() { return g_f6w_split; }
+
 static void check(const MnistFused& f) {
   MX_CHECK(f.B % 16 == 0 && f.B >= 16 && f.B <= 128, "fused MNIST engine needs batch % 16 == 0 and 16 <= B <= 128");
 }

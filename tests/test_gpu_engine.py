@@ -74,6 +74,38 @@ def test_fused_engine_batch_sizes_match_reference(cuda, B):
         assert err < 1e-4, (B, k, err)
 
 
+@pytest.mark.parametrize("B", [16, 64])
+def test_fused_engine_f6w_split_matches_reference(cuda, B):
+    """conv2 weight gradient over 2 tile-row blocks per (image, ci half) (2B slabs) vs the reference."""
+    from mxddp import native
+    from mxddp.engine import FusedMnistTrainer
+    from mxddp.models import MnistCNN
+
+    torch.manual_seed(0)
+    ref = MnistCNN()
+    steps = 3
+    native().mnist_set_f6w_split(2)
+    try:
+        tr = FusedMnistTrainer(batch=B, device=cuda, comm=None, init_model=ref, use_graph=True)
+    finally:
+        native().mnist_set_f6w_split(1)
+    g = torch.Generator().manual_seed(B + 1)
+    xs = [torch.rand(B, 1, 28, 28, generator=g) for _ in range(steps)]
+    ys = [torch.randint(0, 10, (B,), generator=g) for _ in range(steps)]
+    losses = []
+    for i in range(steps):
+        tr.set_batch(xs[i].to(cuda), ys[i].to(cuda))
+        tr.step(1)
+        losses.append(tr.read_metrics()[0] / B)
+    ref_losses = _ref_steps(ref, xs, ys, steps)
+    for a, b in zip(losses, ref_losses):
+        assert abs(a - b) < 1e-4 * max(1.0, abs(b)), (B, losses, ref_losses)
+    sd = tr.state_dict()
+    for k, v in ref.state_dict().items():
+        err = (sd[k] - v).abs().max().item() / (v.abs().max().item() + 1e-6)
+        assert err < 1e-4, (B, k, err)
+
+
 @pytest.mark.parametrize("merged", [False, True])
 @pytest.mark.parametrize("graph", [0, 1, 2])
 def test_fused_engine_rccl_collectives_ws1(cuda, graph, merged):
