@@ -82,6 +82,8 @@ def parse():
                     help="bf16 NHWC convs: the 256 x 256-tile LDS-DMA kernel on layers with >= 256 tiles (A/B)")
     ap.add_argument("--f6w-split", type=int, default=0, choices=[0, 1, 2],
                     help="fused MNIST: conv2 weight-gradient blocks per (image, ci half) (0 = the build default; A/B)")
+    ap.add_argument("--f5-wt", type=int, default=-1, choices=[-1, 0, 1],
+                    help="fused MNIST: F5 bulk stores L2 write-through (agent scope) (-1 = the build default; A/B)")
     ap.add_argument("--cpu", action="store_true",
                     help="BASELINE config 1: single process on the CPU (the reference's single_gpu.py CPU fallback)")
     ap.add_argument("--phase-profile", type=int, default=0, metavar="STEPS",
@@ -121,6 +123,10 @@ def main():
         from mxddp import native as _native
 
         _native().mnist_set_f6w_split(a.f6w_split)
+    if a.f5_wt >= 0:
+        from mxddp import native as _native
+
+        _native().mnist_set_f5_wt(a.f5_wt)
     if a.dtype != "fp32":
         if a.impl == "fused":
             a.impl = "layers"  # the fused MNIST engine is fp32-only
@@ -297,7 +303,13 @@ def _fused_config(a, tr) -> dict:
     return {"graph_mode": tr.eng.graph_mode, "overlap": tr.eng.overlap, "merged_bucket": tr.eng.merged,
             "coscheduled_exchange": tr.eng.coscheduled,
             "transport": tr.active_transport, "force_collectives": a.force_collectives, "autotune": tr.tuned,
-            "f6w_split": _f6w_split()}
+            "f6w_split": _f6w_split(), "f5_wt": _f5_wt()}
+
+
+def _f5_wt() -> int:
+    from mxddp import native
+
+    return native().mnist_f5_wt()
 
 
 def _f6w_split() -> int:

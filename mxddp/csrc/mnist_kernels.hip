@@ -457,7 +457,17 @@ struct Reg6 {
 constexpr int kF5Cols = 48, kF5NT = kF5Cols / 16, kF5C4 = kF5Cols / 4;
 constexpr int kF5DhP = 132, kF5P = 52, kF5W2P = 20, kF5LgP = 20;  // kF5P = 4 mod 8: 4-row groups 16 banks apart
 constexpr int kF5Misc = 12;  // [0..3] db2, [4..7] loss, [8..11] correct: one slot per wave
-template <int B>
+// Store of F5's bulk outputs (fc1 weights / momentum / dp): WT = agent-scope relaxed store
+// (global_store ... sc1), which does not keep the line dirty in the XCD's L2, so the bytes drain
+// to memory while the kernel still runs instead of in the end-of-kernel L2 write-back.
+template <bool WT>
+__device__ __forceinline__ void f5_store(float* p, float v) {
+  if constexpr (WT)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+template <int B, bool WT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void f5_head_fc1_bwd_kernel(MnistFused f) {
   MX_TRACE(f, 2, 0);
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -689,7 +699,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int n = 32 * w + 16 * a + 4 * g + j;
-            f.g[L::fw1 + (size_t)n * 9216 + c0 + 16 * c + m] = acc[a][c][j];
+            f5_store<WT>(f.g + L::fw1 + (size_t)n * 9216 + c0 + 16 * c + m, acc[a][c][j]);
           }
     } else {  // the gradient is consumed here (not materialised in g)  // the SGD kernel's update, same operation order (gscale = 1: world size 1)
       const float lr = *f.lr;
@@ -703,8 +713,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             const size_t e = L::fw1 + (size_t)n * 9216 + c0 + 16 * c + m;
             float pv = wsm[n * kF5P + 16 * c + m], bv = mb[a][c][j];
             sgd_upd(pv, bv, acc[a][c][j], 1.f, f.sgd_mom, f.sgd_wd, lr);
-            f.mom[e] = bv;
-            f.p[e] = pv;
+            f5_store<WT>(f.mom + e, bv);
+            f5_store<WT>(f.p + e, pv);
           }
     }
   }
@@ -735,7 +745,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const int b = 16 * mt + 4 * g + j;
         const bool alive = qs[b * kF5Cols + 16 * c + m] < 4;
         const float v = alive ? acc[c][j] : 0.f;
-        f.dp[(size_t)b * 9216 + kk] = v;
+        f5_store<WT>(f.dp + (size_t)b * 9216 + kk, v);
         db2_part += v;
       }
     }
@@ -898,6 +908,9 @@ void mnist_set_f6w_split(int split) {
   g_f6w_split = split;
 }
 int mnist_f6w_split() { return g_f6w_split; }
+static int g_f5_wt = 0;
+void mnist_set_f5_wt(int on) { g_f5_wt = on ? 1 : 0; }
+int mnist_f5_wt() { return g_f5_wt; }
 
 static void check(const MnistFused& f) {
   MX_CHECK(f.B % 16 == 0 && f.B >= 16 && f.B <= 128, "fused MNIST engine needs batch % 16 == 0 and 16 <= B <= 128");
@@ -906,14 +919,10 @@ static void check(const MnistFused& f) {
 static void set_lds_limits() {
   static bool done = false;
   if (done) return;
-  const void* fns[] = {reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<16>),
-                       reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<32>),
-                       reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<48>),
-                       reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<64>),
-                       reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<80>),
-                       reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<96>),
-                       reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<112>),
-                       reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<128>)};
+#define F5_FN(b) reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<b, false>), \
+                reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<b, true>)
+  const void* fns[] = {F5_FN(16), F5_FN(32), F5_FN(48), F5_FN(64), F5_FN(80), F5_FN(96), F5_FN(112), F5_FN(128)};
+#undef F5_FN
   for (const void* fn : fns)
     MX_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   done = true;
@@ -939,17 +948,17 @@ void mnist_fused_fc1_bwd(const MnistFused& f, hipStream_t st) {
   const size_t lds = sizeof(float) * ((size_t)f.B * kF5DhP + f.B * kF5P + 128 * kF5P + 128 * kF5W2P + f.B * kF5LgP + kF5Misc) +
                      (size_t)f.B * kF5Cols;
   const dim3 grid(9216 / kF5Cols), block(256);
+  void (*kfn)(MnistFused) = nullptr;
+#define F5_CASE(b)                                                                             \
+  case b:                                                                                      \
+    kfn = f.f5_wt ? f5_head_fc1_bwd_kernel<b, true> : f5_head_fc1_bwd_kernel<b, false>; \
+    break;
   switch (f.B) {
-    case 16: MX_LAUNCH(f5_head_fc1_bwd_kernel<16>, grid, block, lds, st, f); break;
-    case 32: MX_LAUNCH(f5_head_fc1_bwd_kernel<32>, grid, block, lds, st, f); break;
-    case 48: MX_LAUNCH(f5_head_fc1_bwd_kernel<48>, grid, block, lds, st, f); break;
-    case 64: MX_LAUNCH(f5_head_fc1_bwd_kernel<64>, grid, block, lds, st, f); break;
-    case 80: MX_LAUNCH(f5_head_fc1_bwd_kernel<80>, grid, block, lds, st, f); break;
-    case 96: MX_LAUNCH(f5_head_fc1_bwd_kernel<96>, grid, block, lds, st, f); break;
-    case 112: MX_LAUNCH(f5_head_fc1_bwd_kernel<112>, grid, block, lds, st, f); break;
-    case 128: MX_LAUNCH(f5_head_fc1_bwd_kernel<128>, grid, block, lds, st, f); break;
+    F5_CASE(16) F5_CASE(32) F5_CASE(48) F5_CASE(64) F5_CASE(80) F5_CASE(96) F5_CASE(112) F5_CASE(128)
     default: MX_CHECK(false, "unsupported fused batch");
   }
+#undef F5_CASE
+  MX_LAUNCH(kfn, grid, block, lds, st, f);
   MX_HIP_CHECK(hipGetLastError());
 }
 

@@ -74,9 +74,10 @@ def test_fused_engine_batch_sizes_match_reference(cuda, B):
         assert err < 1e-4, (B, k, err)
 
 
-@pytest.mark.parametrize("B", [16, 64])
-def test_fused_engine_f6w_split_matches_reference(cuda, B):
-    """conv2 weight gradient over 2 tile-row blocks per (image, ci half) (2B slabs) vs the reference."""
+@pytest.mark.parametrize("B,split,wt", [(16, 2, 0), (64, 2, 0), (64, 1, 1), (32, 2, 1)])
+def test_fused_engine_f6w_split_matches_reference(cuda, B, split, wt):
+    """conv2 weight gradient over 2 tile-row blocks per (image, ci half) (2B slabs) and F5's
+    write-through stores vs the reference."""
     from mxddp import native
     from mxddp.engine import FusedMnistTrainer
     from mxddp.models import MnistCNN
@@ -84,19 +85,22 @@ def test_fused_engine_f6w_split_matches_reference(cuda, B):
     torch.manual_seed(0)
     ref = MnistCNN()
     steps = 3
-    native().mnist_set_f6w_split(2)
+    old = native().mnist_f5_wt()
+    native().mnist_set_f6w_split(split)
+    native().mnist_set_f5_wt(wt)
     try:
         tr = FusedMnistTrainer(batch=B, device=cuda, comm=None, init_model=ref, use_graph=True)
+        g = torch.Generator().manual_seed(B + 1)
+        xs = [torch.rand(B, 1, 28, 28, generator=g) for _ in range(steps)]
+        ys = [torch.randint(0, 10, (B,), generator=g) for _ in range(steps)]
+        losses = []
+        for i in range(steps):
+            tr.set_batch(xs[i].to(cuda), ys[i].to(cuda))
+            tr.step(1)
+            losses.append(tr.read_metrics()[0] / B)
     finally:
         native().mnist_set_f6w_split(1)
-    g = torch.Generator().manual_seed(B + 1)
-    xs = [torch.rand(B, 1, 28, 28, generator=g) for _ in range(steps)]
-    ys = [torch.randint(0, 10, (B,), generator=g) for _ in range(steps)]
-    losses = []
-    for i in range(steps):
-        tr.set_batch(xs[i].to(cuda), ys[i].to(cuda))
-        tr.step(1)
-        losses.append(tr.read_metrics()[0] / B)
+        native().mnist_set_f5_wt(old)
     ref_losses = _ref_steps(ref, xs, ys, steps)
     for a, b in zip(losses, ref_losses):
         assert abs(a - b) < 1e-4 * max(1.0, abs(b)), (B, losses, ref_losses)
