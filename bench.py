@@ -80,6 +80,8 @@ def parse():
                     help="GEMM precision of the layers path (headline is fp32, >= the reference's precision)")
     ap.add_argument("--conv-tile256", type=int, default=0, choices=[0, 1],
                     help="bf16 NHWC convs: the 256 x 256-tile LDS-DMA kernel on layers with >= 256 tiles (A/B)")
+    ap.add_argument("--bn-unroll", type=int, default=0, choices=[0, 2, 4],
+                    help="bf16 NHWC BN apply kernels: vectors in flight per thread (0 = the build default; A/B)")
     ap.add_argument("--f6w-split", type=int, default=0, choices=[0, 1, 2],
                     help="fused MNIST: conv2 weight-gradient blocks per (image, ci half) (0 = the build default; A/B)")
     ap.add_argument("--f5-wt", type=int, default=-1, choices=[-1, 0, 1],
@@ -119,6 +121,10 @@ def main():
         from mxddp import native as _native
 
         _native().nhwc_conv_set_glds256(a.conv_tile256)
+    if a.bn_unroll:
+        from mxddp import native as _native
+
+        _native().nhwc_bn_set_unroll(a.bn_unroll)
     if a.f6w_split:
         from mxddp import native as _native
 
@@ -272,7 +278,8 @@ def main():
                        "image": "x".join(map(str, spec.input_shape)), "parallelism": f"dp{a.gpus}", "impl": a.impl,
                        # how the timed steps were actually launched (autotune may pick eager mode 0)
                        "graph": _fused_graph(a, tr) or getattr(a, "layers_graph", False),
-                       **_fused_config(a, tr), **({"conv_tile256": 1} if a.conv_tile256 else {})},
+                       **_fused_config(a, tr), **({"conv_tile256": 1} if a.conv_tile256 else {}),
+                       **({"bn_unroll": a.bn_unroll} if a.bn_unroll else {})},
             **extra,
         }
         if C.shared_devices():

@@ -113,6 +113,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_conv_dgrad_scratch_floats", &nhwc_conv_dgrad_scratch_floats);
   m.def("nhwc_conv_set_glds", &nhwc_conv_set_glds);
   m.def("nhwc_conv_set_glds256", &nhwc_conv_set_glds256);
+  m.def("nhwc_bn_set_unroll", &nhwc_bn_set_unroll);
   m.def("mnist_set_f6w_split", &mnist_set_f6w_split,
         "conv2 weight-gradient blocks per (image, ci half) for MNIST engines built afterwards (1 or 2)");
   m.def("mnist_f6w_split", &mnist_f6w_split);

@@ -2074,10 +2074,12 @@ __global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
 }
 
 // forward apply: y = relu?(x * scale + shift (+ res)).  32-bit indices (checked on the host),
-// two vectors per iteration with their loads issued first.  The grid stride is a multiple of
+// U vectors per iteration with their loads issued first (U = 4: 64 B of each stream in flight per
+// thread, 128 KB per CU at 8 blocks).  The grid stride is a multiple of
 // 256 and V = C / 8 divides 256 for every channel count up to 2048, so a thread's channel vector
 // v never changes: its 16 coefficients are loaded once into registers (the LDS copy indexed per
 // element cost 16-way bank conflicts: 9x more conflict than LDS-active cycles).
+template <int U>
 __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
   const int V = a.C >> 3;
   const int total = a.Npix * V, step = gridDim.x * kBnT;
@@ -2098,17 +2100,22 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
   // the stores are masked
   const uint4* x4 = reinterpret_cast<const uint4*>(a.x);
   const uint4* r4 = reinterpret_cast<const uint4*>(a.res);
-  for (int i0 = i00; i0 < total; i0 += 2 * step) {
-    const int ic[2] = {i0, min(i0 + step, total - 1)};
-    uint4 xr[2], rr[2] = {z, z};
+  for (int i0 = i00; i0 < total; i0 += U * step) {
+    int ic[U];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) xr[u] = x4[ic[u]];
+    for (int u = 0; u < U; ++u) ic[u] = min(i0 + u * step, total - 1);
+    uint4 xr[U], rr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      xr[u] = x4[ic[u]];
+      rr[u] = z;
+    }
     if (r4) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) rr[u] = r4[ic[u]];
+      for (int u = 0; u < U; ++u) rr[u] = r4[ic[u]];
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int i = i0 + u * step;
       if (i >= total) break;
       float xv[8], rv[8];
@@ -2130,7 +2137,7 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
 // backward apply: dx = A g + D x + B; dres = g (the residual branch gradient).  XM: the ReLU mask
 // from x and the forward's (scale, shift) (no residual), else from y.  Coefficients in registers
 // as in the forward apply (fixed channel vector per thread).
-template <bool XM>
+template <bool XM, int U>
 __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv fV) {
   const int V = a.C >> 3;
   const int total = a.Npix * V, step = gridDim.x * kBnT;
@@ -2161,24 +2168,28 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv f
   // clamped, unconditional loads (see bn_nhwc_apply_k); the mask source is a uniform branch
   const uint4 *g4 = reinterpret_cast<const uint4*>(a.dy), *x4 = reinterpret_cast<const uint4*>(a.x),
               *y4 = reinterpret_cast<const uint4*>(a.y);
-  for (int i0 = i00; i0 < total; i0 += 2 * step) {
-    const int ic[2] = {i0, min(i0 + step, total - 1)};
-    uint4 gr[2], xr[2], yr[2] = {z, z};
-    uint32_t mb[2] = {0u, 0u};
+  for (int i0 = i00; i0 < total; i0 += U * step) {
+    int ic[U];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < U; ++u) ic[u] = min(i0 + u * step, total - 1);
+    uint4 gr[U], xr[U], yr[U];
+    uint32_t mb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
       gr[u] = g4[ic[u]];
       xr[u] = x4[ic[u]];
+      yr[u] = z;
+      mb[u] = 0u;
     }
     if (bmask) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) mb[u] = a.mask[ic[u]];
+      for (int u = 0; u < U; ++u) mb[u] = a.mask[ic[u]];
     } else if (ymask) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) yr[u] = y4[ic[u]];
+      for (int u = 0; u < U; ++u) yr[u] = y4[ic[u]];
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int i = i0 + u * step;
       if (i >= total) break;
       float g[8], xv[8];
@@ -2498,6 +2509,11 @@ static GldsPlan glds_plan(const ConvNArgs& a, bool wide, bool par) {
 // the 256 x 256 tile (conv_nhwc_glds256_kernel): 0 = never (default until measured), 1 = where
 // it fills the chip (>= 256 tiles, no split-K needed), 2 = wherever Ng % 256 == 0 (tests)
 static int g_conv_glds256 = 0;
+static int g_bn_unroll = 4;  // vectors per thread per iteration of the BN apply kernels (2 or 4)
+void nhwc_bn_set_unroll(int u) {
+  MX_CHECK(u == 2 || u == 4, "nhwc_bn_set_unroll: 2 or 4");
+  g_bn_unroll = u;
+}
 void nhwc_conv_set_glds256(int mode) { g_conv_glds256 = mode; }
 static bool glds256_fits(const ConvNArgs& a) {
   if (g_conv_glds256 == 0 || a.Ng % 256 != 0 || a.Kg % 64 != 0) return false;
@@ -2880,7 +2896,10 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
   }
   MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
-  MX_LAUNCH(bn_nhwc_apply_k, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));
+  if (g_bn_unroll == 4)
+    MX_LAUNCH(bn_nhwc_apply_k<4>, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));
+  else
+    MX_LAUNCH(bn_nhwc_apply_k<2>, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));
 }
 
 void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma, const float* mean,
@@ -2921,8 +2940,14 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
   }
   MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
-  if (a.fcoef) MX_LAUNCH(bn_nhwc_bwd_apply_k<true>, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));
-  else MX_LAUNCH(bn_nhwc_bwd_apply_k<false>, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));
+  const dim3 agrid(grid_for((int64_t)Npix * V, 2048));
+  if (g_bn_unroll == 4) {
+    if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 4>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
+    else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 4>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
+  } else {
+    if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 2>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
+    else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 2>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
+  }
 }
 
 void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, int k,

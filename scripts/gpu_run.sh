@@ -19,6 +19,7 @@
 #   keras / keras_rep / keras_ws2 / prof_keras / pmc_keras   Keras CNN fused engine
 #   mlp / mlp_rep / prof_mlp / pmc_mlp                       Chainer MLP
 #   rn32 / rn256 / prof_rn / pmc_rn / rn_stock / rn_layers    ResNet-50 bf16 (rn_layers: per conv shape)
+#   ab_bnu       ResNet-50 at batch 256, BN apply kernels with 2 vs 4 vectors in flight per thread
 #   pyr / prof_pyr / pyr_stock                               PyramidNet-110
 #   ws2 / ws4 / ws8 (MNIST), keras_ws8, pyr_ws8, rn_ws8      shared-GPU DDP rehearsals
 #   coll         MNIST with RCCL collectives forced at one rank
@@ -94,6 +95,11 @@ for step in "$@"; do
     rn32) run rn32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 ;;
     rn256) run rn256 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 ;;
     rn256_t256) run rn256_t256 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --conv-tile256 1 ;;
+    ab_bnu)  # BN apply unroll 2 vs 4 at batch 256, interleaved
+      for r in 1 2; do
+        run "ab_bnu2_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --bn-unroll 2 &&
+        run "ab_bnu4_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --bn-unroll 4 || exit 1
+      done ;;
     rn32_t256) run rn32_t256 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --conv-tile256 1 ;;
     rn_layers) run rn_layers 300 python scripts/bench_nhwc_layers.py 256 5 ;;
     rn_layers_t256) run rn_layers_t256 300 python scripts/bench_nhwc_layers.py 256 5 1 ;;
