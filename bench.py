@@ -84,8 +84,9 @@ def parse():
                     help="bf16 NHWC BN apply kernels: vectors in flight per thread (0 = the build default; A/B)")
     ap.add_argument("--f6w-split", type=int, default=0, choices=[0, 1, 2],
                     help="fused MNIST: conv2 weight-gradient blocks per (image, ci half) (0 = the build default; A/B)")
-    ap.add_argument("--f5-wt", type=int, default=-1, choices=[-1, 0, 1],
-                    help="fused MNIST: F5 bulk stores L2 write-through (agent scope) (-1 = the build default; A/B)")
+    ap.add_argument("--f5-wt", type=int, default=-1, choices=range(-1, 8), metavar="MASK",
+                    help="fused MNIST: bulk stores with agent scope (L2 write-through), 1 = F5, 2 = F2, 4 = F6W "
+                         "(-1 = the build default; A/B)")
     ap.add_argument("--cpu", action="store_true",
                     help="BASELINE config 1: single process on the CPU (the reference's single_gpu.py CPU fallback)")
     ap.add_argument("--phase-profile", type=int, default=0, metavar="STEPS",
@@ -310,7 +311,7 @@ def _fused_config(a, tr) -> dict:
     return {"graph_mode": tr.eng.graph_mode, "overlap": tr.eng.overlap, "merged_bucket": tr.eng.merged,
             "coscheduled_exchange": tr.eng.coscheduled,
             "transport": tr.active_transport, "force_collectives": a.force_collectives, "autotune": tr.tuned,
-            "f6w_split": _f6w_split(), "f5_wt": _f5_wt()}
+            "f6w_split": _f6w_split(), "wt_stores": _f5_wt()}
 
 
 def _f5_wt() -> int:

@@ -117,7 +117,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("mnist_set_f6w_split", &mnist_set_f6w_split,
         "conv2 weight-gradient blocks per (image, ci half) for MNIST engines built afterwards (1 or 2)");
   m.def("mnist_f6w_split", &mnist_f6w_split);
-  m.def("mnist_set_f5_wt", &mnist_set_f5_wt, "F5 bulk stores L2 write-through (agent scope) for MNIST steps launched afterwards");
+  m.def("mnist_set_f5_wt", &mnist_set_f5_wt,
+        "MNIST bulk stores with agent scope (L2 write-through) for steps launched afterwards: mask 1 = F5, 2 = F2, "
+        "4 = F6W");
   m.def("mnist_f5_wt", &mnist_f5_wt);
   m.def("nhwc_repack_many", [](uintptr_t desc, int n, int total_blocks, uintptr_t st) {
     nhwc_repack_many(P<const int64_t>(desc), n, total_blocks, S(st));

@@ -20,6 +20,25 @@ __device__ __forceinline__ void sgd_upd(float& p, float& buf, float g, float gsc
   p = __fmaf_rn(-lr, buf, p);
 }
 
+// 16-byte vector store with agent scope (sc1): the line is not kept dirty in this XCD's L2, the
+// bytes go to memory while the kernel runs (MnistFused::wt)
+__device__ __forceinline__ void st4_wt(float4* p, float4 v) {
+  const f32x4 q = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(q) : "memory");
+}
+__device__ __forceinline__ void st4(float4* p, float4 v, bool wt) {
+  if (wt)
+    st4_wt(p, v);
+  else
+    *p = v;
+}
+__device__ __forceinline__ void st1(float* p, float v, bool wt) {
+  if (wt)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }

@@ -199,7 +199,7 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
       const int i = tid + 256 * k, cq = i / 36, q = i - 36 * cq;
-      d4[cq * 72 + q] = s4[i];
+      st4(d4 + cq * 72 + q, s4[i], f.wt & 4);
     }
   }
   MX_TRACE_B(f, 3, 3, braw);

@@ -192,7 +192,7 @@ MnistFused MnistEngine::fused_args() const {
   f.sgd_mom = momentum_;
   f.sgd_wd = wd_;
   f.f6w_split = f6w_split_;
-  f.f5_wt = mnist_f5_wt();
+  f.wt = mnist_f5_wt();
   if (co_active()) {
     f.co_blocks = reducer_->peer()->blocks();
     f.co_args = co_args_;

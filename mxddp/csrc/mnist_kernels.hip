@@ -218,7 +218,7 @@ __device__ __forceinline__ void f2_stage2_wino(const MnistFused& f, const Scratc
         if (y[e] > best) { best = y[e]; q = e; }
       const float vv = best + bias;
       const int o = ((b * 64 + co) * 12 + py) * 12 + 4 * g + j;
-      f.pool[o] = vv > 0.f ? vv : 0.f;
+      st1(f.pool + o, vv > 0.f ? vv : 0.f, f.wt & 2);
       idx[o] = vv > 0.f ? (uint8_t)q : (uint8_t)4;
     }
   }
@@ -338,8 +338,8 @@ __global__ __launch_bounds__(256) void f2_fwd_kernel(MnistFused f, Scratch sc) {
       // lane's 4 consecutive positions are one aligned float4 (no LDS read-back pass)
       const int q0 = 16 * mt + 4 * g;
       if (q0 < (py == 11 ? 104 : 52))
-        *reinterpret_cast<float4*>(f.a1 + (size_t)b * 21632 + ci_b * 676 + row0 * 26 + q0) =
-            make_float4(o[0], o[1], o[2], o[3]);
+        st4(reinterpret_cast<float4*>(f.a1 + (size_t)b * 21632 + ci_b * 676 + row0 * 26 + q0),
+            make_float4(o[0], o[1], o[2], o[3]), f.wt & 2);
     }
   }
   lds_barrier();  // the published a1 rows are read by F6W, not by this block
@@ -909,7 +909,7 @@ void mnist_set_f6w_split(int split) {
 }
 int mnist_f6w_split() { return g_f6w_split; }
 static int g_f5_wt = 0;
-void mnist_set_f5_wt(int on) { g_f5_wt = on ? 1 : 0; }
+void mnist_set_f5_wt(int mask) { g_f5_wt = mask & 7; }
 int mnist_f5_wt() { return g_f5_wt; }
 
 static void check(const MnistFused& f) {
@@ -951,7 +951,7 @@ void mnist_fused_fc1_bwd(const MnistFused& f, hipStream_t st) {
   void (*kfn)(MnistFused) = nullptr;
 #define F5_CASE(b)                                                                             \
   case b:                                                                                      \
-    kfn = f.f5_wt ? f5_head_fc1_bwd_kernel<b, true> : f5_head_fc1_bwd_kernel<b, false>; \
+    kfn = (f.wt & 1) ? f5_head_fc1_bwd_kernel<b, true> : f5_head_fc1_bwd_kernel<b, false>; \
     break;
   switch (f.B) {
     F5_CASE(16) F5_CASE(32) F5_CASE(48) F5_CASE(64) F5_CASE(80) F5_CASE(96) F5_CASE(112) F5_CASE(128)

@@ -74,7 +74,7 @@ def test_fused_engine_batch_sizes_match_reference(cuda, B):
         assert err < 1e-4, (B, k, err)
 
 
-@pytest.mark.parametrize("B,split,wt", [(16, 2, 0), (64, 2, 0), (64, 1, 1), (32, 2, 1)])
+@pytest.mark.parametrize("B,split,wt", [(16, 2, 0), (64, 2, 0), (64, 1, 1), (32, 2, 7)])
 def test_fused_engine_f6w_split_matches_reference(cuda, B, split, wt):
     """conv2 weight gradient over 2 tile-row blocks per (image, ci half) (2B slabs) and F5's
     write-through stores vs the reference."""
