@@ -218,7 +218,9 @@ def _commdtype_worker(rank, ws, port, model_name, b, q):
     PC.init_distributed(use_gpu=True)
     ops.set_compute_dtype("bf16")
     dev = torch.device("cuda", 0)
-    batches = _batches(3, ws * b, (3, 64, 64), seed=7)
+    # ONE step: the comparison measures the communication's rounding, not how a chaotic random-init
+    # ResNet amplifies a 0.4 % gradient difference over several steps (3 steps: 36 % of the step)
+    batches = _batches(1, ws * b, (3, 64, 64), seed=7)
     res, bad = {}, []
     for cd in ("fp32", "bf16"):
         torch.manual_seed(0)
@@ -237,7 +239,7 @@ def _commdtype_worker(rank, ws, port, model_name, b, q):
         torch.distributed.all_gather_object(allp, res[cd])
         if any(not torch.equal(allp[0], t) for t in allp):
             bad.append((cd, "ranks diverged"))
-    # relative to how far the 3 steps moved the weights: at a random init with 4 images per rank
+    # relative to how far the step moved the weights: at a random init with 4 images per rank
     # the gradients reach O(100) (BN affine), where bf16's 0.4 % rounding is O(1) per element
     if not torch.equal(res["fp320"], res["bf160"]):
         bad.append("different initial weights")

@@ -290,8 +290,10 @@ def test_bn_backward_statistics_from_dgrad_epilogue(cuda, glds, stride, relu):
 
     C = native()
     # K = 64: a 576-deep data-gradient reduction, no split-K (a split dgrad cannot carry the
-    # statistics); glds 256: the 256-channel data-gradient tile
-    N, Cin, H, W, K = (4, 64, 16, 16, 64) if glds != 256 else (2, 256, 10, 10, 64)
+    # statistics); Cin = 128: not the 3x3 / 64 -> 64 band kernel (whose epilogue carries no
+    # statistics: with Cin = 64 every stride-1 case ran the band kernel and took the separate pass);
+    # glds 256: the 256-channel data-gradient tile
+    N, Cin, H, W, K = (4, 128, 16, 16, 64) if glds != 256 else (2, 256, 10, 10, 64)
     torch.manual_seed(11)
     x = (torch.randn(N, H, W, Cin) + 0.5).to(torch.bfloat16).to(cuda)
     w = (torch.randn(K, Cin, 3, 3) * 0.05).to(cuda)
