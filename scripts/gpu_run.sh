@@ -27,6 +27,7 @@
 #   copies_pyr / copies_rn   torch.profiler census of the device copies in a layer-path step
 #   trace_pyr    kernel + HIP API trace of the graphed PyramidNet step (where its copies come from)
 #   diag_bnstats backward BN statistics of the data-gradient epilogues vs torch
+#   diag_join    residual-join / BN-statistics variants of two Bottleneck blocks vs a baseline (and a repeat)
 source "$(dirname "$0")/gpu_check.sh"
 rm -f gpurun_out/steps.log
 
@@ -68,12 +69,13 @@ for step in "$@"; do
     pmc_mnist) pmc pmc_mnist --steps 20 --warmup 2 --no-graph --min-warmup-ms 0 ;;
     phase_mnist) run phase_mnist 300 python bench.py --phase-profile 30 ;;
     phase_split) run phase_split 300 python bench.py --phase-profile 30 --f6w-split 2 ;;
-    ab_wt)  # write-through store masks A/B (0 none, 1 F5, 7 F5 + F2 + F6W), interleaved long runs
+    ab_wt)  # write-through store masks A/B (0 none, 6 F2 + F6W, 7 F5 + F2 + F6W), interleaved long runs
       for r in 1 2; do
         run "ab_wt0_$r" 300 python bench.py --steps 2000 --warmup 100 --f5-wt 0 &&
-        run "ab_wt1_$r" 300 python bench.py --steps 2000 --warmup 100 --f5-wt 1 &&
+        run "ab_wt6_$r" 300 python bench.py --steps 2000 --warmup 100 --f5-wt 6 &&
         run "ab_wt7_$r" 300 python bench.py --steps 2000 --warmup 100 --f5-wt 7 || exit 1
       done ;;
+    diag_join) run diag_join 300 python scripts/diag_join.py ;;
     prof_wt) prof prof_wt 200 --steps 200 --warmup 20 --min-warmup-ms 0 --f5-wt 1 ;;
     ab_split)  # F6W tile-row split A/B, interleaved long runs
       for r in 1 2; do
