@@ -36,6 +36,41 @@ def run(blocks, x, stats, lazy, unroll):
     return dict(zip(names, vals)), y.float().cpu()
 
 
+def reference(blocks, x):
+    """fp32 CPU autograd of the same blocks (NCHW, torch ops, training-mode BN on batch
+    statistics), with the bf16 input and output gradient of the GPU runs."""
+    import torch.nn.functional as F
+
+    xr = x.float().cpu().permute(0, 3, 1, 2).contiguous().requires_grad_()
+    params = []
+    y = xr
+    for blk in blocks:
+        ws = [blk.conv1.weight, blk.conv2.weight, blk.conv3.weight]
+        bns = [blk.bn1, blk.bn2, blk.bn3]
+        w = [t.detach().float().cpu().requires_grad_() for t in ws]
+        gb = [(b.weight.detach().float().cpu().requires_grad_(), b.bias.detach().float().cpu().requires_grad_())
+              for b in bns]
+        params.append((w, gb))
+        h = F.conv2d(y, w[0])
+        h = F.relu(F.batch_norm(h, None, None, gb[0][0], gb[0][1], training=True, eps=bns[0].eps))
+        h = F.conv2d(h, w[1], stride=blk.conv2.stride, padding=blk.conv2.padding)
+        h = F.relu(F.batch_norm(h, None, None, gb[1][0], gb[1][1], training=True, eps=bns[1].eps))
+        h = F.conv2d(h, w[2])
+        h = F.batch_norm(h, None, None, gb[2][0], gb[2][1], training=True, eps=bns[2].eps)
+        y = F.relu(h + y)
+    gy = torch.randn(tuple(y.permute(0, 2, 3, 1).shape), generator=torch.Generator().manual_seed(8))
+    gy = gy.to(torch.bfloat16).float().permute(0, 3, 1, 2)
+    y.backward(gy)
+    out = {"x": xr.grad.permute(0, 2, 3, 1).contiguous()}
+    for i, (blk, (w, gb)) in enumerate(zip(blocks, params)):
+        grads = {"conv1.weight": w[0].grad, "conv2.weight": w[1].grad, "conv3.weight": w[2].grad,
+                 "bn1.weight": gb[0][0].grad, "bn1.bias": gb[0][1].grad, "bn2.weight": gb[1][0].grad,
+                 "bn2.bias": gb[1][1].grad, "bn3.weight": gb[2][0].grad, "bn3.bias": gb[2][1].grad}
+        for n, _ in blk.named_parameters():
+            out[f"b{i}.{n}"] = grads[n]
+    return out
+
+
 def compare(tag, ref, out):
     worst = []
     for k, a in ref.items():
@@ -62,7 +97,11 @@ def main():
         blocks = [Bottleneck(256, 64).to(dev) for _ in range(nblk)]
         x = torch.randn(*shape).to(torch.bfloat16).to(dev)
         print(f"== {nblk} blocks, input {shape}")
+        fp32 = reference(blocks, x)
         base, y0 = run(blocks, x, False, False, 2)
+        compare("baseline vs fp32 CPU reference", fp32, base)
+        compare("lazy join vs fp32 CPU reference", fp32, run(blocks, x, False, True, 2)[0])
+        compare("statistics + lazy join vs fp32 CPU reference", fp32, run(blocks, x, True, True, 2)[0])
         again, y1 = run(blocks, x, False, False, 2)
         print(f"forward output repeat: {((y0 - y1).abs().max()).item():.3e}")
         compare("repeat (no stats, materialised join, unroll 2)", base, again)
