@@ -114,9 +114,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_conv_set_glds", &nhwc_conv_set_glds);
   m.def("nhwc_conv_set_glds256", &nhwc_conv_set_glds256);
   m.def("nhwc_bn_set_unroll", &nhwc_bn_set_unroll);
-  m.def("mnist_set_f6w_split", &mnist_set_f6w_split,
-        "conv2 weight-gradient blocks per (image, ci half) for MNIST engines built afterwards (1 or 2)");
-  m.def("mnist_f6w_split", &mnist_f6w_split);
   m.def("mnist_set_f5_wt", &mnist_set_f5_wt,
         "MNIST bulk stores with agent scope (L2 write-through) for steps launched afterwards: mask 1 = F5, 2 = F2, "
         "4 = F6W");

@@ -79,9 +79,8 @@ struct Scratch {  // carve of MnistFused::scratch (floats)
   long long* db2; // conv2 bias grad, int64 fixed point (kGScale) [64] (F5 blocks add, finalize reads)
   float* wv;      // conv2 forward Winograd filters G w G^T as F2W B-fragments
                   // [4 w][16 xi][2 s4][64 lane][4 j]
-  float* wslab;   // conv2 wgrad slabs [f6w_split * B][64 co][32 ci][9 tap] (canonical order), one per
-                  // (tile-row half, image), written with plain stores by F6W, summed by the
-                  // finalize in a fixed order
+  float* wslab;   // conv2 wgrad per-image slabs [B][64 co][32 ci][9 tap] (canonical order), written
+                  // by F6W, summed by the finalize in a fixed order
 };
 constexpr int kWinoPack = 16 * 2048;  // 16 Winograd-domain values per (co, ci)
 // conv1-grad slabs: the F7W blocks of image b add into slab b & 15 (integer adds, so the slab
@@ -97,19 +96,19 @@ __host__ __device__ inline Scratch carve(float* s) {
   return c;
 }
 inline size_t scratch_floats(int B) {
-  return 2 * (size_t)kWinoPack + 2 * ((size_t)kG1Slabs * 320 + 64) + 2 * (size_t)B * kPack;
+  return 2 * (size_t)kWinoPack + 2 * ((size_t)kG1Slabs * 320 + 64) + (size_t)B * kPack;
 }
 
 // conv2 weight gradient of pairs 4 grp .. 4 grp + 3 (36 consecutive floats of the canonical
-// [co][ci][ky][kx] layout) summed over the f6w_split * B slabs in a fixed order -> gs[36] (LDS).
-// Threads t < 144: float4 q = t % 9 of the group, slab subgroup sg = t / 9 sums slabs sg,
+// [co][ci][ky][kx] layout) summed over the B per-image slabs in a fixed order -> gs[36] (LDS).
+// Threads t < 144: float4 q = t % 9 of the group, image subgroup sg = t / 9 sums images sg,
 // sg + 16, ... (4 loads in flight per round, clamped + masked: no load behind a branch); the 16
 // subgroup partials are added in order.  red: 576 floats of LDS.
 constexpr int kWslabGroups = 512;  // 2048 pairs / 4
 __device__ __forceinline__ void wslab_group_sum(const MnistFused& f, const Scratch& sc, int grp, float* red, float* gs) {
   const int t = threadIdx.x;
   if (t < 144) {
-    const int ns = f.B * f.f6w_split, q = t % 9, sg = t / 9, nb = ns / 16;
+    const int ns = f.B, q = t % 9, sg = t / 9, nb = ns / 16;
     const float4* src = reinterpret_cast<const float4*>(sc.wslab) + grp * 9 + q;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int i0 = 0; i0 < nb; i0 += 4) {

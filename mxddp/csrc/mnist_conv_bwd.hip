@@ -23,8 +23,7 @@ namespace {
 // K = 144 tiles: dU[xi][co][ci] = sum_t W[xi][co][t] V[xi][t][ci], V = B^T a1_t B; then
 // dw = G^T dU G lane-locally (all 16 xi of a (co, ci) sit in one lane), written as this image's
 // slab of the weight gradient with plain stores (the finalize sums the B slabs in a fixed order).
-// Block = (image, ci half[, tile-row half when f6w_split = 2]).  Wave w = co 16w..16w+15.  6 (3)
-// chunks of 2 tile rows:
+// Block = (image, ci half): all 144 tiles.  Wave w = co 16w..16w+15.  6 chunks of 2 tile rows:
 // (A) the chunk's 6 a1 rows that F2 published -> LDS (one chunk ahead, 3 float4 per thread in
 // registers; recomputing conv1 here was 5.4 of 25 us), (B) V of 24 tiles x 16 ci -> LDS
 // ([t][ci][20]: conflict-free ds_read_b128 of the 16 xi), (C) 6 k-steps of 16 MFMAs; K inside a
@@ -41,13 +40,11 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
   float* a1s = sm + 784 + 160;  // [16 ci][kA1P]: 6 a1 rows x 26
   float* vs = a1s + 16 * kA1P;  // [24 t][16 ci][20]
   const int bid = xcd_remap(braw, nblk);
-  const int split = f.f6w_split, h = bid & 1, kh = (bid >> 1) & (split - 1), b = bid / (2 * split);
-  const int cb = kh * (6 / split), ce = cb + 6 / split;  // this block's chunks [cb, ce)
+  const int b = bid / 2, h = bid & 1;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
   // a1 rows 4c .. 4c+5 of the block's 16 ci = 16 x 39 float4 (624 of the 768 slots)
   // (three named registers, not an array: an array here was placed in scratch memory)
   const float* a1b = f.a1 + ((size_t)b * 32 + 16 * h) * 676;
-  const float* a1c = a1b + 104 * cb;
   int a1src[3], a1dst[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -55,9 +52,9 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
     a1src[k] = ci * 676 + 4 * f4;
     a1dst[k] = tid + 256 * k < 624 ? ci * kA1P + 4 * f4 : -1;
   }
-  float4 pa0 = *reinterpret_cast<const float4*>(a1c + a1src[0]);
-  float4 pa1 = *reinterpret_cast<const float4*>(a1c + a1src[1]);
-  float4 pa2 = *reinterpret_cast<const float4*>(a1c + a1src[2]);
+  float4 pa0 = *reinterpret_cast<const float4*>(a1b + a1src[0]);
+  float4 pa1 = *reinterpret_cast<const float4*>(a1b + a1src[1]);
+  float4 pa2 = *reinterpret_cast<const float4*>(a1b + a1src[2]);
   const int co = 16 * w + m;  // A row of this lane
   const float* dpl = f.dp + (size_t)b * 9216 + co * 144 + 6 * g;
   const uint16_t* qpl = reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(f.idx) + (size_t)b * 9216 + co * 144 + 6 * g);
@@ -65,8 +62,8 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
   uint16_t qn[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    dn[k] = *reinterpret_cast<const float2*>(dpl + 24 * cb + 2 * k);
-    qn[k] = qpl[12 * cb + k];
+    dn[k] = *reinterpret_cast<const float2*>(dpl + 2 * k);
+    qn[k] = qpl[k];
   }
   f32x4 acc[16];
 #pragma unroll
@@ -75,14 +72,14 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
   uint32_t tA = 0, tB = 0, tC = 0, tq = 0;  // phase-time sums (trace only)
   const bool trc = f.trace && threadIdx.x == 0 && braw < 1024;
 #pragma unroll 1
-  for (int c = cb; c < ce; ++c) {
+  for (int c = 0; c < 6; ++c) {
     if (trc) tq = (uint32_t)__builtin_amdgcn_s_memrealtime();
     // (A) published a1 rows -> LDS (the previous chunk's phase-B reads of a1s finished before the
     // barrier ahead of its phase C); next chunk's rows in flight
     *reinterpret_cast<float4*>(a1s + a1dst[0]) = pa0;
     *reinterpret_cast<float4*>(a1s + a1dst[1]) = pa1;
     if (a1dst[2] >= 0) *reinterpret_cast<float4*>(a1s + a1dst[2]) = pa2;
-    if (c + 1 < ce) {
+    if (c + 1 < 6) {
       const float* nb = a1b + 104 * (c + 1);
       pa0 = *reinterpret_cast<const float4*>(nb + a1src[0]);
       pa1 = *reinterpret_cast<const float4*>(nb + a1src[1]);
@@ -130,7 +127,7 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
       qv[2 * k] = qn[k] & 0xffu;
       qv[2 * k + 1] = qn[k] >> 8;
     }
-    if (c + 1 < ce) {
+    if (c + 1 < 6) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         dn[k] = *reinterpret_cast<const float2*>(dpl + 24 * (c + 1) + 2 * k);
@@ -195,7 +192,7 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
   {
     // per co: 16 ci x 9 taps = 144 contiguous floats (36 float4) at (co * 32 + 16 h) * 9
     const float4* s4 = reinterpret_cast<const float4*>(st);
-    float4* d4 = reinterpret_cast<float4*>(sc.wslab + ((size_t)kh * f.B + b) * kPack + 144 * h);
+    float4* d4 = reinterpret_cast<float4*>(sc.wslab + (size_t)b * kPack + 144 * h);
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
       const int i = tid + 256 * k, cq = i / 36, q = i - 36 * cq;
@@ -458,7 +455,7 @@ __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scr
     return;
   }
   const int bid = (int)blockIdx.x - f.co_blocks;
-  const int n6 = 2 * f.f6w_split * f.B;
+  const int n6 = 2 * f.B;
   if (bid < n6)
     f6w_body(f, sc, sm, bid, n6);
   else
@@ -513,9 +510,7 @@ void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_
     attr = true;
   }
   const Scratch sc = carve(f.scratch);
-  if (f.f6w_split != 1 && f.f6w_split != 2) throw std::runtime_error("mnist: f6w_split must be 1 or 2");
-  MX_LAUNCH(f67_conv2_bwd_kernel, dim3(f.co_blocks + 2 * f.f6w_split * f.B + kF7WChunks * f.B), dim3(256), lds, st,
-            f, sc);
+  MX_LAUNCH(f67_conv2_bwd_kernel, dim3(f.co_blocks + 2 * f.B + kF7WChunks * f.B), dim3(256), lds, st, f, sc);
   if (!finalize_in_sgd) MX_LAUNCH(f8_finalize_kernel, dim3(kWslabGroups + 2 + 8), dim3(256), 0, st, f, sc);
   MX_HIP_CHECK(hipGetLastError());
 }

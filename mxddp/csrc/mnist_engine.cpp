@@ -191,7 +191,6 @@ MnistFused MnistEngine::fused_args() const {
   f.lr = lr_;
   f.sgd_mom = momentum_;
   f.sgd_wd = wd_;
-  f.f6w_split = f6w_split_;
   f.wt = mnist_f5_wt();
   if (co_active()) {
     f.co_blocks = reducer_->peer()->blocks();

@@ -154,7 +154,6 @@ class MnistEngine {
   uint64_t seed_;
   float momentum_, wd_;
   int variant_;
-  int f6w_split_ = mnist_f6w_split();  // MnistFused::f6w_split (the process default at construction)
   bool external_batch_ = false;
   hipStream_t s_ = nullptr;
   hipGraph_t graph_ = nullptr;

@@ -41,17 +41,11 @@ struct MnistFused {
   int co_blocks;
   PeerArgs co_args;
   PeerPartition co_part;
-  // conv2 weight-gradient blocks per (image, ci half): 1 = all 144 tiles in one block, 2 = the
-  // tile rows split in halves, each writing a slab of its own (2B slabs, the finalize sums them)
-  int f6w_split;
   // bulk outputs written with agent-scope (sc1: not kept dirty in the XCD's L2) stores, per
   // kernel: 1 = F5 (fc1 weights / momentum / dp), 2 = F2 (a1, pool), 4 = F6W (weight slabs)
   int wt;
 };
 size_t mnist_fused_scratch_floats(int B);
-// process-wide default of MnistFused::f6w_split for engines built afterwards (1 or 2)
-void mnist_set_f6w_split(int split);
-int mnist_f6w_split();
 void mnist_set_f5_wt(int mask);  // process-wide default of MnistFused::wt (A/B)
 int mnist_f5_wt();
 // Pack conv2 weights into the F2 Winograd fragment order and zero the cross-step accumulators;

@@ -902,12 +902,6 @@ using namespace mnist;
 
 size_t mnist_fused_scratch_floats(int B) { return scratch_floats(B); }
 
-static int g_f6w_split = 1;
-void mnist_set_f6w_split(int split) {
-  if (split != 1 && split != 2) throw std::runtime_error("mnist_set_f6w_split: 1 or 2");
-  g_f6w_split = split;
-}
-int mnist_f6w_split() { return g_f6w_split; }
 static int g_f5_wt = 0;
 void mnist_set_f5_wt(int mask) { g_f5_wt = mask & 7; }
 int mnist_f5_wt() { return g_f5_wt; }

@@ -13,9 +13,8 @@
 #   driver       bench at the driver's length  long         2,000-step bench
 #   prof_mnist   rocprofv3 kernel trace of the MNIST step
 #   pmc_mnist    counter passes of the MNIST step (eager launches, one pass per run)
-#   phase_mnist / phase_split   in-kernel phase timings (phase_split: F6W over 2 tile-row blocks)
-#   ab_split     MNIST 2,000-step bench, F6W split 1 vs 2, interleaved twice
-#   ab_wt / prof_wt   the same for F5's write-through stores; kernel trace with them
+#   phase_mnist  in-kernel phase timings of the MNIST step
+#   ab_wt / prof_wt   MNIST bench A/B of the write-through store masks; kernel trace with F5's
 #   keras / keras_rep / keras_ws2 / prof_keras / pmc_keras   Keras CNN fused engine
 #   mlp / mlp_rep / prof_mlp / pmc_mlp                       Chainer MLP
 #   rn32 / rn256 / prof_rn / pmc_rn / rn_stock / rn_layers    ResNet-50 bf16 (rn_layers: per conv shape)
@@ -68,7 +67,6 @@ for step in "$@"; do
     prof_mnist) prof prof_mnist 200 --steps 200 --warmup 20 --min-warmup-ms 0 ;;
     pmc_mnist) pmc pmc_mnist --steps 20 --warmup 2 --no-graph --min-warmup-ms 0 ;;
     phase_mnist) run phase_mnist 300 python bench.py --phase-profile 30 ;;
-    phase_split) run phase_split 300 python bench.py --phase-profile 30 --f6w-split 2 ;;
     ab_wt)  # write-through store masks A/B (0 none, 6 F2 + F6W, 7 F5 + F2 + F6W), interleaved long runs
       for r in 1 2; do
         run "ab_wt0_$r" 300 python bench.py --steps 2000 --warmup 100 --f5-wt 0 &&
@@ -77,11 +75,6 @@ for step in "$@"; do
       done ;;
     diag_join) run diag_join 300 python scripts/diag_join.py ;;
     prof_wt) prof prof_wt 200 --steps 200 --warmup 20 --min-warmup-ms 0 --f5-wt 1 ;;
-    ab_split)  # F6W tile-row split A/B, interleaved long runs
-      for r in 1 2; do
-        run "ab_split1_$r" 300 python bench.py --steps 2000 --warmup 100 --f6w-split 1 &&
-        run "ab_split2_$r" 300 python bench.py --steps 2000 --warmup 100 --f6w-split 2 || exit 1
-      done ;;
     coll) run coll 300 python bench.py --steps 2000 --warmup 100 --force-collectives ;;
     replica) run replica 300 python bench.py --impl replica --steps 1000 --warmup 50 ;;
     layers) run layers 300 python bench.py --impl layers --steps 300 --warmup 30 ;;
