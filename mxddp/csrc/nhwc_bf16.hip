@@ -181,6 +181,60 @@ __device__ __forceinline__ void bn_bwd_flush(const ConvNArgs& a, float* red, con
   }
 }
 
+// Epilogue of the implicit-GEMM kernels: NV 16-byte vectors per thread of the C tile staged in
+// LDS (rows = pixels from px0, VPR vectors per row) -> residual addend (masked by its ReLU bits)
+// -> 16-byte store -> backward BN statistics.  Every global operand of the NV vectors (the BN's
+// x and mask bits, the addend and its bits) is requested at a clamped address before the first
+// is used: behind the per-lane range check, hipcc branched around each load and waited for it
+// vector by vector (8 dependent round trips per tile in the LDS-DMA kernel's data gradient).
+template <int NT, int NV, int VPR, typename PF>
+__device__ __forceinline__ void epi_vectors(const ConvNArgs& a, const bf16* Cs, int CP, int px0, int ch0, int Mlim,
+                                            PF pfull, bool bst, const float* mean8, const float* sc8,
+                                            const float* sh8, float* s1, float* s2) {
+  const int tid = threadIdx.x;
+  size_t o[NV];
+  bool ok[NV];
+  uint4 xr[NV];
+  u32x4 ad[NV];
+  uint32_t mb[NV], am[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int v = tid + NT * k, row = v / VPR, cv = v - row * VPR;
+    const int px = px0 + row, ch = ch0 + 8 * cv;
+    ok[k] = px < Mlim && ch < a.Ng;
+    o[k] = ok[k] ? (size_t)pfull(px) * a.Ng + ch : 0;
+    xr[k] = make_uint4(0u, 0u, 0u, 0u);
+    ad[k] = u32x4{0u, 0u, 0u, 0u};
+    mb[k] = 0u;
+    am[k] = 0xffu;
+  }
+  if (bst) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) xr[k] = *reinterpret_cast<const uint4*>(a.bx + o[k]);
+    if (a.bmask) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) mb[k] = a.bmask[o[k] >> 3];
+    }
+  }
+  if (a.addend) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) ad[k] = *reinterpret_cast<const u32x4*>(a.addend + o[k]);
+    if (a.amask) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) am[k] = a.amask[o[k] >> 3];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    if (!ok[k]) continue;
+    const int v = tid + NT * k, row = v / VPR, cv = v - row * VPR;
+    u32x4 val = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
+    if (a.addend) val = add8(val, a.amask ? mask8(ad[k], am[k]) : ad[k]);
+    *reinterpret_cast<u32x4*>(a.out + o[k]) = val;
+    if (bst) bn_bwd_acc8(a, val, xr[k], mb[k], mean8, sc8, sh8, s1, s2);
+  }
+}
+
 // __launch_bounds__(256, 2): at least two waves per SIMD (<= 256 VGPRs); the LDS tiles allow two
 // 256-thread blocks per CU anyway, so a larger register budget would only lose occupancy
 template <int TM, int TN, bool kWide>
@@ -457,25 +511,7 @@ __global__ __launch_bounds__(256, 2) void conv_nhwc_kernel(ConvNArgs a) {
       sh8[e] = a.bfcoef ? a.bfcoef[2 * (ch + e) + 1] : 0.f;
     }
   }
-#pragma unroll
-  for (int v = tid; v < TN * VPR; v += 256) {
-    const int row = v / VPR, cv = v - row * VPR;
-    const int px = px0 + row, ch = ch0 + 8 * cv;
-    if (px < Mc && ch < a.Ng)
-    {
-      const size_t o = (size_t)pfull(px) * a.Ng + ch;
-      uint4 xr = make_uint4(0u, 0u, 0u, 0u);
-      uint32_t mb = 0u;
-      if (bst) {  // issued before the addend / tile reads so their latencies overlap
-        xr = *reinterpret_cast<const uint4*>(a.bx + o);
-        if (a.bmask) mb = a.bmask[o >> 3];
-      }
-      u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
-      if (a.addend) v = join8(v, a.addend, a.amask, o);
-      *reinterpret_cast<u32x4*>(a.out + o) = v;
-      if (bst) bn_bwd_acc8(a, v, xr, mb, mean8, sc8, sh8, s1, s2);
-    }
-  }
+  epi_vectors<256, TN * VPR / 256, VPR>(a, Cs, CP, px0, ch0, Mc, pfull, bst, mean8, sc8, sh8, s1, s2);
   if (bst) {
     __syncthreads();  // every read of the C tile is done: its LDS becomes the reduction buffer
     // partial row = (parity class, pixel tile): rows_per_class = ceil(Mc / TN)
@@ -651,25 +687,8 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
       sh8[e] = a.bfcoef ? a.bfcoef[2 * (ch + e) + 1] : 0.f;
     }
   }
-#pragma unroll
-  for (int v = tid; v < TN * VPR; v += 512) {
-    const int row = v / VPR, cv = v - row * VPR;
-    const int px = px0 + row, ch = ch0 + 8 * cv;
-    if (px < a.M && ch < a.Ng)
-    {
-      const size_t o = (size_t)px * a.Ng + ch;
-      uint4 xr = make_uint4(0u, 0u, 0u, 0u);
-      uint32_t mb = 0u;
-      if (bst) {
-        xr = *reinterpret_cast<const uint4*>(a.bx + o);
-        if (a.bmask) mb = a.bmask[o >> 3];
-      }
-      u32x4 v = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
-      if (a.addend) v = join8(v, a.addend, a.amask, o);
-      *reinterpret_cast<u32x4*>(a.out + o) = v;
-      if (bst) bn_bwd_acc8(a, v, xr, mb, mean8, sc8, sh8, s1, s2);
-    }
-  }
+  epi_vectors<512, TN * VPR / 512, VPR>(a, Cs, CP, px0, ch0, a.M, [](int px) { return px; }, bst, mean8, sc8, sh8,
+                                       s1, s2);
   if (bst) {
     // reduction slots after the C tile in the (idle) stage buffers
     float* bred = reinterpret_cast<float*>(smem + ((TN * CP * 2 + 255) & ~255));
@@ -866,24 +885,8 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds256_kernel(ConvNArgs a) {
       }
     }
     __syncthreads();
-#pragma unroll 2
-    for (int v = tid; v < HT * VPR; v += 512) {
-      const int row = v / VPR, cv = v - row * VPR;
-      const int px = px0 + h * HT + row, ch = ch0 + 8 * cv;
-      if (px < a.M) {
-        const size_t o = (size_t)px * a.Ng + ch;
-        uint4 xr = make_uint4(0u, 0u, 0u, 0u);
-        uint32_t mb = 0u;
-        if (bst) {
-          xr = *reinterpret_cast<const uint4*>(a.bx + o);
-          if (a.bmask) mb = a.bmask[o >> 3];
-        }
-        u32x4 val = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
-        if (a.addend) val = join8(val, a.addend, a.amask, o);
-        *reinterpret_cast<u32x4*>(a.out + o) = val;
-        if (bst) bn_bwd_acc8(a, val, xr, mb, mean8, sc8, sh8, s1, s2);
-      }
-    }
+    epi_vectors<512, HT * VPR / 512, VPR>(a, Cs, CP, px0 + h * HT, ch0, a.M, [](int px) { return px; }, bst, mean8,
+                                          sc8, sh8, s1, s2);
     if constexpr (STATS) {  // column sums of the stored (bf16) half tile
       const int hr = min(max(rows - h * HT, 0), HT);
       const uint16_t* col = reinterpret_cast<const uint16_t*>(Cs) + sc_c;
@@ -2074,8 +2077,7 @@ __global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
 }
 
 // forward apply: y = relu?(x * scale + shift (+ res)).  32-bit indices (checked on the host),
-// U vectors per iteration with their loads issued first (U = 4: 64 B of each stream in flight per
-// thread, 128 KB per CU at 8 blocks).  The grid stride is a multiple of
+// U vectors per iteration with their loads issued first (g_bn_unroll).  The grid stride is a multiple of
 // 256 and V = C / 8 divides 256 for every channel count up to 2048, so a thread's channel vector
 // v never changes: its 16 coefficients are loaded once into registers (the LDS copy indexed per
 // element cost 16-way bank conflicts: 9x more conflict than LDS-active cycles).
@@ -2509,7 +2511,9 @@ static GldsPlan glds_plan(const ConvNArgs& a, bool wide, bool par) {
 // the 256 x 256 tile (conv_nhwc_glds256_kernel): 0 = never (default until measured), 1 = where
 // it fills the chip (>= 256 tiles, no split-K needed), 2 = wherever Ng % 256 == 0 (tests)
 static int g_conv_glds256 = 0;
-static int g_bn_unroll = 4;  // vectors per thread per iteration of the BN apply kernels (2 or 4)
+// vectors per thread per iteration of the BN apply kernels (2 or 4; 4 measured ~1 % slower at
+// ResNet-50 batch 256, profiles/r4_ab)
+static int g_bn_unroll = 2;
 void nhwc_bn_set_unroll(int u) {
   MX_CHECK(u == 2 || u == 4, "nhwc_bn_set_unroll: 2 or 4");
   g_bn_unroll = u;

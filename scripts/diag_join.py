@@ -77,9 +77,12 @@ def compare(tag, ref, out):
         b = out[k]
         d = (a - b).abs()
         rel = (d.max() / (a.abs().max() + 1e-6)).item()
-        worst.append((rel, k, d))
+        nrm = ((a - b).norm() / (a.norm() + 1e-12)).item()
+        worst.append((rel, k, d, nrm))
     worst.sort(key=lambda t: -t[0])
-    print(f"{tag}: " + ", ".join(f"{k} {r:.2e}" for r, k, _ in worst[:4]))
+    print(f"{tag}: max-rel " + ", ".join(f"{k} {r:.2e}" for r, k, _, _ in worst[:4]) +
+          f" | norm-rel max {max(t[3] for t in worst):.2e} (" +
+          ", ".join(f"{t[1]} {t[3]:.2e}" for t in sorted(worst, key=lambda t: -t[3])[:3]) + ")")
     r, k, d = worst[0]
     if r > 1e-2 and d.dim() == 4:
         idx = (d == d.max()).nonzero()[0].tolist()
@@ -90,8 +93,41 @@ def compare(tag, ref, out):
         print(f"   {k}: max at {idx}, {n_bad} elements > 10% of max; channels {chans}; (n,h,w) {pix}")
 
 
+def forward_trace(blk, x):
+    """Every intermediate of one block's NHWC forward (training mode), for the determinism probe."""
+    N = nhwc
+    out = []
+    join = N.GradJoin()
+    a, xs = N.fork(x, join)
+    c1 = N.conv2d(a, blk.conv1.weight, join=join, bn=blk.bn1)
+    out.append(("conv1", c1))
+    h1 = N.batch_norm(c1, blk.bn1, relu=True)
+    out.append(("bn1", h1))
+    c2 = N.conv2d(h1, blk.conv2.weight, blk.conv2.stride, blk.conv2.padding, bn=blk.bn2)
+    out.append(("conv2", c2))
+    h2 = N.batch_norm(c2, blk.bn2, relu=True)
+    out.append(("bn2", h2))
+    c3 = N.conv2d(h2, blk.conv3.weight, bn=blk.bn3)
+    out.append(("conv3", c3))
+    y = N.batch_norm(c3, blk.bn3, relu=True, res=xs, join=join)
+    out.append(("bn3", y))
+    return [(n, t.detach().float().cpu()) for n, t in out]
+
+
+def determinism_probe(dev):
+    torch.manual_seed(21)
+    for shape in ((4, 8, 8, 256), (2, 14, 14, 256)):
+        blk = Bottleneck(256, 64).to(dev)
+        x = torch.randn(*shape).to(torch.bfloat16).to(dev)
+        runs = [forward_trace(blk, x) for _ in range(4)]
+        for i, (name, t0) in enumerate(runs[0]):
+            diffs = [(r[i][1] - t0).abs().max().item() for r in runs[1:]]
+            print(f"determinism {shape} {name}: max |run k - run 0| = {', '.join(f'{d:.3e}' for d in diffs)}")
+
+
 def main():
     dev = torch.device("cuda")
+    determinism_probe(dev)
     torch.manual_seed(12)
     for nblk, shape in ((2, (2, 14, 14, 256)), (3, (2, 14, 14, 256)), (2, (4, 8, 8, 256))):
         blocks = [Bottleneck(256, 64).to(dev) for _ in range(nblk)]
