@@ -41,11 +41,12 @@ def main():
     Cn = native()
     Cn.nhwc_conv_set_glds256(tile256)
     st = torch.cuda.current_stream().cuda_stream
-    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+    tot = {"fwd": 0.0, "dgrad": 0.0, "dgrad_st": 0.0, "wgrad": 0.0}
     # floor: max(HBM bytes at 8 TB/s, FLOPs at the 2.5 PF bf16 dense peak), the same for all three
     # directions to first order (each reads / writes one activation pair and the weights)
     print(f"{'count':>5} {'N':>3} {'H':>4} {'C':>5} {'K':>5} {'R':>2} {'s':>2} | "
-          f"{'fwd us':>8} {'TF':>5} | {'dgrad us':>8} {'TF':>5} | {'wgrad us':>8} {'TF':>5} | {'floor us':>8}")
+          f"{'fwd us':>8} {'TF':>5} | {'dgrad us':>8} {'TF':>5} | {'+bnst us':>8} | {'wgrad us':>8} {'TF':>5} | "
+          f"{'floor us':>8}")
     for cnt, N, H, W, C, K, R, s, p in shapes(batch):
         P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
         x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
@@ -61,6 +62,12 @@ def main():
         sd = Cn.nhwc_conv_dgrad_scratch_floats(N, H, W, C, K, R, R, s, s, p, p, P, Q)
         sw = Cn.nhwc_wgrad_scratch_floats(N, C, K, R, R, P, Q)
         scr = torch.empty(max(sf, sd, sw, 1), device=dev)
+        # the data gradient with the producing BN's backward statistics in its epilogue (ReLU mask
+        # from the forward's coefficients), as the training step runs it
+        bmean = torch.randn(C, device=dev)
+        bcoef = torch.randn(2 * C, device=dev)
+        brows = Cn.nhwc_conv_dgrad_bn_rows(N, H, W, C, K, R, R, s, s, p, p, P, Q)
+        bpart = torch.empty(brows * 2 * C, device=dev)
         flops = 2.0 * N * P * Q * K * C * R * R
         hbm_bytes = 2.0 * (N * H * W * C + N * P * Q * K) + 2.0 * K * C * R * R
         floor_us = max(hbm_bytes / 8e12, flops / 2.5e15) * 1e6
@@ -69,12 +76,15 @@ def main():
                                             P, Q, scr.data_ptr() if sf else 0, st),
             "dgrad": lambda: Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx.data_ptr(), N, H, W, C, K, R, R, s, s,
                                                 p, p, P, Q, scr.data_ptr() if sd else 0, st),
+            "dgrad_st": lambda: Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx.data_ptr(), N, H, W, C, K, R, R, s,
+                                                   s, p, p, P, Q, scr.data_ptr() if sd else 0, st, 0, bpart.data_ptr(),
+                                                   x.data_ptr(), bmean.data_ptr(), bcoef.data_ptr(), 0, True, 0),
             "wgrad": lambda: Cn.nhwc_conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), N, H, W, C, C, K, R, R, s,
                                                 s, p, p, P, Q, False, scr.data_ptr(), st),
         }
         res = {}
         for name, fn in runs.items():
-            if name == "dgrad" and C == 8:
+            if name.startswith("dgrad") and C == 8:
                 res[name] = (0.0, 0.0)
                 continue
             for _ in range(3):
@@ -90,9 +100,9 @@ def main():
             tot[name] += us * cnt
         print(f"{cnt:5d} {N:3d} {H:4d} {C:5d} {K:5d} {R:2d} {s:2d} | "
               f"{res['fwd'][0]:8.1f} {res['fwd'][1]:5.0f} | {res['dgrad'][0]:8.1f} {res['dgrad'][1]:5.0f} | "
-              f"{res['wgrad'][0]:8.1f} {res['wgrad'][1]:5.0f} | {floor_us:8.1f}", flush=True)
+              f"{res['dgrad_st'][0]:8.1f} | {res['wgrad'][0]:8.1f} {res['wgrad'][1]:5.0f} | {floor_us:8.1f}", flush=True)
     print("per-step totals (us): " + " ".join(f"{k}={v:.0f}" for k, v in tot.items()) +
-          f" all={sum(tot.values()):.0f}")
+          f" all (without dgrad_st)={sum(v for k, v in tot.items() if k != 'dgrad_st'):.0f}")
 
 
 if __name__ == "__main__":

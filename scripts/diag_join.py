@@ -83,7 +83,7 @@ def compare(tag, ref, out):
     print(f"{tag}: max-rel " + ", ".join(f"{k} {r:.2e}" for r, k, _, _ in worst[:4]) +
           f" | norm-rel max {max(t[3] for t in worst):.2e} (" +
           ", ".join(f"{t[1]} {t[3]:.2e}" for t in sorted(worst, key=lambda t: -t[3])[:3]) + ")")
-    r, k, d = worst[0]
+    r, k, d, _ = worst[0]
     if r > 1e-2 and d.dim() == 4:
         idx = (d == d.max()).nonzero()[0].tolist()
         n_bad = int((d > 0.1 * d.max()).sum())
