@@ -82,7 +82,7 @@ def parse():
                     help="bf16 NHWC convs: the 256 x 256-tile LDS-DMA kernel on layers with >= 256 tiles (A/B)")
     ap.add_argument("--bn-unroll", type=int, default=0, choices=[0, 2, 4],
                     help="bf16 NHWC BN apply kernels: vectors in flight per thread (0 = the build default; A/B)")
-    ap.add_argument("--f5-wt", type=int, default=-1, choices=range(-1, 8), metavar="MASK",
+    ap.add_argument("--wt-stores", type=int, default=-1, choices=range(-1, 8), metavar="MASK",
                     help="fused MNIST: bulk stores with agent scope (L2 write-through), 1 = F5, 2 = F2, 4 = F6W "
                          "(-1 = the build default; A/B)")
     ap.add_argument("--cpu", action="store_true",
@@ -124,10 +124,10 @@ def main():
         from mxddp import native as _native
 
         _native().nhwc_bn_set_unroll(a.bn_unroll)
-    if a.f5_wt >= 0:
+    if a.wt_stores >= 0:
         from mxddp import native as _native
 
-        _native().mnist_set_f5_wt(a.f5_wt)
+        _native().mnist_set_wt_stores(a.wt_stores)
     if a.dtype != "fp32":
         if a.impl == "fused":
             a.impl = "layers"  # the fused MNIST engine is fp32-only
@@ -305,13 +305,13 @@ def _fused_config(a, tr) -> dict:
     return {"graph_mode": tr.eng.graph_mode, "overlap": tr.eng.overlap, "merged_bucket": tr.eng.merged,
             "coscheduled_exchange": tr.eng.coscheduled,
             "transport": tr.active_transport, "force_collectives": a.force_collectives, "autotune": tr.tuned,
-            "wt_stores": _f5_wt()}
+            "wt_stores": _wt_stores()}
 
 
-def _f5_wt() -> int:
+def _wt_stores() -> int:
     from mxddp import native
 
-    return native().mnist_f5_wt()
+    return native().mnist_wt_stores()
 
 
 def _replica(a):

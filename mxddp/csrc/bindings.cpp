@@ -114,10 +114,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_conv_set_glds", &nhwc_conv_set_glds);
   m.def("nhwc_conv_set_glds256", &nhwc_conv_set_glds256);
   m.def("nhwc_bn_set_unroll", &nhwc_bn_set_unroll);
-  m.def("mnist_set_f5_wt", &mnist_set_f5_wt,
+  m.def("mnist_set_wt_stores", &mnist_set_wt_stores,
         "MNIST bulk stores with agent scope (L2 write-through) for steps launched afterwards: mask 1 = F5, 2 = F2, "
         "4 = F6W");
-  m.def("mnist_f5_wt", &mnist_f5_wt);
+  m.def("mnist_wt_stores", &mnist_wt_stores);
   m.def("nhwc_repack_many", [](uintptr_t desc, int n, int total_blocks, uintptr_t st) {
     nhwc_repack_many(P<const int64_t>(desc), n, total_blocks, S(st));
   });

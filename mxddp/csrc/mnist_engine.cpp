@@ -191,7 +191,7 @@ MnistFused MnistEngine::fused_args() const {
   f.lr = lr_;
   f.sgd_mom = momentum_;
   f.sgd_wd = wd_;
-  f.wt = mnist_f5_wt();
+  f.wt = mnist_wt_stores();
   if (co_active()) {
     f.co_blocks = reducer_->peer()->blocks();
     f.co_args = co_args_;

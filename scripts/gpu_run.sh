@@ -69,12 +69,12 @@ for step in "$@"; do
     phase_mnist) run phase_mnist 300 python bench.py --phase-profile 30 ;;
     ab_wt)  # write-through store masks A/B (0 none, 6 F2 + F6W, 7 F5 + F2 + F6W), interleaved long runs
       for r in 1 2; do
-        run "ab_wt0_$r" 300 python bench.py --steps 2000 --warmup 100 --f5-wt 0 &&
-        run "ab_wt6_$r" 300 python bench.py --steps 2000 --warmup 100 --f5-wt 6 &&
-        run "ab_wt7_$r" 300 python bench.py --steps 2000 --warmup 100 --f5-wt 7 || exit 1
+        run "ab_wt0_$r" 300 python bench.py --steps 2000 --warmup 100 --wt-stores 0 &&
+        run "ab_wt6_$r" 300 python bench.py --steps 2000 --warmup 100 --wt-stores 6 &&
+        run "ab_wt7_$r" 300 python bench.py --steps 2000 --warmup 100 --wt-stores 7 || exit 1
       done ;;
     diag_join) run diag_join 300 python scripts/diag_join.py ;;
-    prof_wt) prof prof_wt 200 --steps 200 --warmup 20 --min-warmup-ms 0 --f5-wt 1 ;;
+    prof_wt) prof prof_wt 200 --steps 200 --warmup 20 --min-warmup-ms 0 --wt-stores 1 ;;
     coll) run coll 300 python bench.py --steps 2000 --warmup 100 --force-collectives ;;
     replica) run replica 300 python bench.py --impl replica --steps 1000 --warmup 50 ;;
     layers) run layers 300 python bench.py --impl layers --steps 300 --warmup 30 ;;
