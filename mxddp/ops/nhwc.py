@@ -291,7 +291,12 @@ def conv2d(x, w, stride=1, padding=0, pack: WeightPack | None = None, join: Grad
 # MXDDP_BN_STATS_IN_CONV=0: every BN runs its own statistics passes, forward and backward (A/B
 # switch for the conv-epilogue statistics)
 _BN_STATS_IN_CONV = os.environ.get("MXDDP_BN_STATS_IN_CONV", "1") == "1"
-_BN_STATS_IN_DGRAD = _BN_STATS_IN_CONV
+# Backward BN statistics in the consuming conv's data-gradient epilogue: OFF by default.  Measured
+# per layer at batch 256 (scripts/bench_nhwc_layers.py, profiles/r4_d/rn_layers.log) the epilogue
+# adds 2.9 ms to the step's data gradients (the LDS-DMA kernel runs one block per CU, so the x
+# re-read and the reduction of every tile are fully exposed) against the 1.6 ms of separate
+# statistics passes it removes.  Tests switch it on to keep the path exact.
+_BN_STATS_IN_DGRAD = False
 _LAZY_JOIN = True  # identity-shortcut gradient masked in the joining conv's epilogue (tests flip it)
 # how many BN backward passes took their statistics from a conv epilogue / ran their own pass
 BN_BWD_STATS = {"epilogue": 0, "pass": 0}

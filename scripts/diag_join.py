@@ -145,7 +145,7 @@ def main():
         compare("lazy join", base, run(blocks, x, False, True, 2)[0])
         compare("dgrad statistics, materialised join", base, run(blocks, x, True, False, 2)[0])
         compare("dgrad statistics + lazy join", base, run(blocks, x, True, True, 2)[0])
-    nhwc._BN_STATS_IN_DGRAD = nhwc._BN_STATS_IN_CONV
+    nhwc._BN_STATS_IN_DGRAD = False
     nhwc._LAZY_JOIN = True
     native().nhwc_bn_set_unroll(4)
 

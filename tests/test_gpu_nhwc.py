@@ -336,7 +336,7 @@ def test_bn_backward_statistics_from_dgrad_epilogue(cuda, glds, stride, relu):
             used.append(nhwc.BN_BWD_STATS["epilogue"] - before["epilogue"])
             outs.append((xg.grad.float().cpu(), wg.grad.cpu(), bn.weight.grad.cpu(), bn.bias.grad.cpu()))
     finally:
-        nhwc._BN_STATS_IN_DGRAD = nhwc._BN_STATS_IN_CONV
+        nhwc._BN_STATS_IN_DGRAD = False
         C.nhwc_conv_set_glds256(0)
         C.nhwc_conv_set_glds(1)
     assert used == [0, 1], used  # the fused run really took the epilogue's statistics
@@ -371,7 +371,7 @@ def test_bn_backward_statistics_residual_join(cuda):
             grads = [p.grad.cpu() for blk in blocks for p in blk.parameters()]
             outs.append((xg.grad.float().cpu(), *grads))
     finally:
-        nhwc._BN_STATS_IN_DGRAD = nhwc._BN_STATS_IN_CONV
+        nhwc._BN_STATS_IN_DGRAD = False
     # bn2 of both blocks (conv3's data gradient) and block 0's bn3 (block 1's conv1, joined); bn1
     # feeds the 3x3 / 64-channel band kernel, whose epilogue carries no statistics
     assert used[0] == 0 and used[1] >= 3, used
@@ -412,7 +412,7 @@ def test_lazy_identity_join_equals_materialised(cuda):
             outs.append([xg.grad.float().cpu()] + [p.grad.cpu() for blk in blocks for p in blk.parameters()])
     finally:
         nhwc._LAZY_JOIN = True
-        nhwc._BN_STATS_IN_DGRAD = nhwc._BN_STATS_IN_CONV
+        nhwc._BN_STATS_IN_DGRAD = False
     # the same bf16 values are added in the same epilogue: equal up to run-to-run bf16 flips
     for a, b in zip(*outs):
         assert _nrel(b, a) < 1e-2
