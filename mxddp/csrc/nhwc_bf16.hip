@@ -543,12 +543,17 @@ __device__ __forceinline__ void glds16(const void* src, void* lds) {
 }
 
 // STATS: the forward BN-statistics epilogue (bnpart / bnshift); the backward BN-statistics
-// epilogue of a data gradient runs whenever a.bx is set (ConvNArgs::bx)
-template <int TM, bool STATS = false>
-__global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
-  constexpr int TN = 256, BK = 64, NS = 3;
-  constexpr int AB = TM * 128, SB = AB + TN * 128;   // bytes: A image, whole stage
-  constexpr int NA = TM / 64, NB = 4, NPW = NA + NB;  // LDS-DMA instructions per wave per stage
+// epilogue of a data gradient runs whenever a.bx is set (ConvNArgs::bx).
+// TN = 128, NS = 2 (the short-reduction variant, 1x1 layers with <= 2 k-tiles): 64 KB of LDS
+// (TM = 128), two blocks per CU, so one block's loads and MFMAs run under the other's epilogue;
+// with one 144 KB block per CU every tile's load -> MFMA -> store chain was serial (the 56 x 56
+// 1x1 layers ran at 2-2.3x their HBM floor).
+template <int TM, bool STATS = false, int TN = 256, int NS = 3>
+__global__ __launch_bounds__(512, TN == 128 ? 2 : 1) void conv_nhwc_glds_kernel(ConvNArgs a) {
+  constexpr int BK = 64;
+  static_assert((TN == 256 && NS == 3) || (TN == 128 && NS == 2), "glds kernel variants");
+  constexpr int AB = TM * 128, SB = AB + TN * 128;        // bytes: A image, whole stage
+  constexpr int NA = TM / 64, NB = TN / 64, NPW = NA + NB;  // LDS-DMA instructions per wave per stage
   constexpr int WM = TM / 64, WN = 8 / WM, WPX = TN / WN, WMT = 4, WNT = WPX / 16;
   __shared__ __attribute__((aligned(1024))) char smem[NS * SB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave / WN, wn = wave % WN;
@@ -613,13 +618,14 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
 
   // split-K over blockIdx.y (fp32 partials, summed by conv_nhwc_splitk_reduce_k)
   const int nt = min(a.Kg / BK - kt0, a.kt_per_split);
+  // NS - 1 stages in flight ahead of the one computed
   if (nt > 0) issue(0, 0);
-  if (nt > 1) issue(1, 1);
+  if (NS == 3 && nt > 1) issue(1, 1);
   for (int t = 0; t < nt; ++t) {
-    if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+    if (NS == 3 && t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // stage t landed for every wave; stage t-1's buffer is free
-    if (t + 2 < nt) issue(t + 2, (t + 2) % NS);
+    if (t + NS - 1 < nt) issue(t + NS - 1, (t + NS - 1) % NS);
     const char* sA = smem + (t % NS) * SB;
     const char* sB = sA + AB;
 #pragma unroll
@@ -675,7 +681,10 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
   }
   __syncthreads();
   constexpr int VPR = TM / 8;
-  const bool bst = !STATS && a.bx != nullptr;  // backward BN statistics (fixed vector per thread)
+  // backward BN statistics (fixed vector per thread): only where the reduction slots fit after
+  // the C tile (not the two-stage variant; the host does not select it for them)
+  constexpr bool kBst = ((TN * CP * 2 + 255) & ~255) + 16 * 512 * 4 <= NS * SB;
+  const bool bst = kBst && !STATS && a.bx != nullptr;
   float s1[8], s2[8], mean8[8], sc8[8], sh8[8];
   if (bst) {
     const int ch = min(ch0 + 8 * (tid % VPR), a.Ng - 8);
@@ -689,11 +698,12 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds_kernel(ConvNArgs a) {
   }
   epi_vectors<512, TN * VPR / 512, VPR>(a, Cs, CP, px0, ch0, a.M, [](int px) { return px; }, bst, mean8, sc8, sh8,
                                        s1, s2);
-  if (bst) {
-    // reduction slots after the C tile in the (idle) stage buffers
-    float* bred = reinterpret_cast<float*>(smem + ((TN * CP * 2 + 255) & ~255));
-    static_assert(((TN * CP * 2 + 255) & ~255) + 16 * 512 * 4 <= NS * SB, "BN reduction slots must fit");
-    bn_bwd_flush<512, VPR>(a, bred, s1, s2, px0 / TN, ch0);
+  if constexpr (kBst) {
+    if (bst) {
+      // reduction slots after the C tile in the (idle) stage buffers
+      float* bred = reinterpret_cast<float*>(smem + ((TN * CP * 2 + 255) & ~255));
+      bn_bwd_flush<512, VPR>(a, bred, s1, s2, px0 / TN, ch0);
+    }
   }
   if constexpr (STATS) {  // BN statistics of the stored (bf16) tile: 512 / TM threads per channel
     constexpr int TPC = 512 / TM, RPT = TN / TPC, U = 8;
@@ -2511,6 +2521,10 @@ static GldsPlan glds_plan(const ConvNArgs& a, bool wide, bool par) {
 // the 256 x 256 tile (conv_nhwc_glds256_kernel): 0 = never (default until measured), 1 = where
 // it fills the chip (>= 256 tiles, no split-K needed), 2 = wherever Ng % 256 == 0 (tests)
 static int g_conv_glds256 = 0;
+// the two-stage 128-pixel variant of the LDS-DMA kernel (conv_nhwc_glds_kernel<TM, STATS, 128, 2>)
+// for layers of <= 2 k-tiles with >= 512 tiles: 0 = never, 1 = there (default)
+static int g_conv_glds_short = 1;
+void nhwc_conv_set_glds_short(int mode) { g_conv_glds_short = mode; }
 // vectors per thread per iteration of the BN apply kernels (2 or 4; 4 measured ~1 % slower at
 // ResNet-50 batch 256, profiles/r4_ab)
 static int g_bn_unroll = 2;
@@ -2600,14 +2614,26 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     a.par = 0;
     a.kt_per_split = gp.kt_per_split;
     a.part = gp.splits > 1 ? scratch : nullptr;
-    const int gx = cdiv(a.M, 256);
+    // short reductions (<= 2 k-tiles) with enough tiles for two blocks per CU: 128-pixel tiles,
+    // two stages (no backward statistics epilogue there)
+    const bool shrt = g_conv_glds_short && gp.splits == 1 && a.Kg <= 128 && !(a.dgrad && a.bx && a.bnpart) &&
+                      (int64_t)cdiv(a.Ng, gp.tm) * cdiv(a.M, 128) >= 512;
+    const int tn = shrt ? 128 : 256, gx = cdiv(a.M, tn);
     // epilogue BN statistics (forward: bnpart / bnshift; data gradient: bx, see ConvNArgs) need
     // the whole reduction in one block: no split-K
     const bool bst = a.dgrad && a.bx && a.bnpart && gp.splits == 1 && gx <= 16384;
     if (!bst) a.bx = nullptr;
     if (!(a.bnpart && (bst || (!a.dgrad && gp.splits == 1)) && gx <= 16384)) a.bnpart = nullptr;
-    const dim3 grid(cdiv(a.Ng, gp.tm) * cdiv(a.M, 256), gp.splits);
-    if (a.bnpart && !bst) {
+    const dim3 grid(cdiv(a.Ng, gp.tm) * gx, gp.splits);
+    if (shrt) {
+      if (a.bnpart) {
+        if (gp.tm == 128) MX_LAUNCH((conv_nhwc_glds_kernel<128, true, 128, 2>), grid, dim3(512), 0, st, a);
+        else MX_LAUNCH((conv_nhwc_glds_kernel<64, true, 128, 2>), grid, dim3(512), 0, st, a);
+      } else {
+        if (gp.tm == 128) MX_LAUNCH((conv_nhwc_glds_kernel<128, false, 128, 2>), grid, dim3(512), 0, st, a);
+        else MX_LAUNCH((conv_nhwc_glds_kernel<64, false, 128, 2>), grid, dim3(512), 0, st, a);
+      }
+    } else if (a.bnpart && !bst) {
       if (gp.tm == 128) MX_LAUNCH((conv_nhwc_glds_kernel<128, true>), grid, dim3(512), 0, st, a);
       else MX_LAUNCH((conv_nhwc_glds_kernel<64, true>), grid, dim3(512), 0, st, a);
     } else {
@@ -2688,7 +2714,9 @@ int nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int
 }
 
 int nhwc_conv_bn_rows(int N, int H, int W, int Cp, int K, int R, int S, int sh, int sw, int ph, int pw, int P, int Q) {
-  int rows = cdiv(N * P * Q, 256);  // one per 256-pixel tile (LDS-DMA kernel, stem kernel)
+  // upper bound: one per 128-pixel tile (the LDS-DMA kernel's two-stage variant; 256-pixel tiles
+  // elsewhere -- the launch returns the rows it wrote)
+  int rows = cdiv(N * P * Q, 128);
   if (Cp == 64 && K == 64 && R == 3 && S == 3 && sh == 1 && sw == 1 && ph == 1 && pw == 1 && P == H && Q == W &&
       W <= 64) {  // the band kernel writes one row per band
     const int rt = c3_band_rows(P, Q);

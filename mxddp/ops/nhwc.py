@@ -382,7 +382,7 @@ def batch_norm(x, bn: torch.nn.BatchNorm2d, relu: bool = False, res: torch.Tenso
         # (an in-place change of x since the conv bumped its version: the partials are stale)
         pre = getattr(x, "_mx_bnpre", None)
         if pre is not None and (pre[2] is not (bn.running_mean if bn.track_running_stats else None)
-                                or pre[0].numel() != pre[1] * 2 * x.shape[-1] or pre[3] != x._version):
+                                or pre[0].numel() < pre[1] * 2 * x.shape[-1] or pre[3] != x._version):
             pre = None
         if pre is not None:
             pre = pre[:3]

@@ -96,6 +96,14 @@ for step in "$@"; do
         run "ab_bnu2_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --bn-unroll 2 &&
         run "ab_bnu4_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --bn-unroll 4 || exit 1
       done ;;
+    ab_short)  # ResNet-50 batch 256 / 32: two-stage 128-pixel LDS-DMA variant off vs on, interleaved
+      for r in 1 2; do
+        run "ab_short0_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --glds-short 0 &&
+        run "ab_short1_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --glds-short 1 || exit 1
+      done
+      run ab_short0_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --glds-short 0 &&
+      run ab_short1_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --glds-short 1 || exit 1 ;;
+    rn_layers_short0) run rn_layers_short0 300 python scripts/bench_nhwc_layers.py 256 5 0 0 ;;
     rn32_t256) run rn32_t256 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --conv-tile256 1 ;;
     rn_layers) run rn_layers 300 python scripts/bench_nhwc_layers.py 256 5 ;;
     rn_layers_t256) run rn_layers_t256 300 python scripts/bench_nhwc_layers.py 256 5 1 ;;

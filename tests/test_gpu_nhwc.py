@@ -82,10 +82,14 @@ def test_conv_nhwc(cuda, case):
 
 @pytest.mark.parametrize("case", [(2, 64, 14, 14, 192, 3, 1, 1), (3, 128, 13, 11, 64, 1, 1, 0),
                                   (2, 64, 15, 15, 128, 3, 2, 1), (1, 128, 9, 9, 256, 3, 1, 1),
-                                  (1, 256, 7, 7, 128, 3, 1, 1)])  # long reduction: split-K partials
+                                  (1, 256, 7, 7, 128, 3, 1, 1),  # long reduction: split-K partials
+                                  # the two-stage 128-pixel variant (<= 2 k-tiles, >= 512 tiles): forward
+                                  # with a partial last pixel tile; the 256 -> 64 layer's data gradient
+                                  (10, 128, 61, 59, 256, 1, 1, 0), (10, 256, 61, 59, 64, 1, 1, 0)])
 def test_conv_glds_kernel(cuda, case):
-    """The LDS-DMA three-stage kernel, forced on every eligible layer (forward and stride-1 data
-    gradient; partial channel / pixel tiles, stride-2 forward) vs the fp32 reference."""
+    """The LDS-DMA kernel, forced on every eligible layer (forward and stride-1 data gradient;
+    partial channel / pixel tiles, stride-2 forward, the short-reduction two-stage variant) vs the
+    fp32 reference."""
     from mxddp import native
 
     C_ = native()
@@ -244,7 +248,9 @@ def test_bn_nhwc(cuda, C, relu, res):
 
 
 @pytest.mark.parametrize("shape,offset", [((16, 64, 56, 56, 128, 3, 1), 0.0), ((32, 64, 28, 28, 256, 1, 0), 4.0),
-                                          ((14, 64, 61, 59, 128, 3, 1), -2.0), ((96, 64, 56, 56, 64, 1, 0), 1.0),
+                                          ((14, 64, 61, 59, 128, 3, 1), -2.0),
+                                          ((96, 64, 56, 56, 64, 1, 0), 1.0),  # two-stage 128-pixel variant
+                                          ((23, 64, 57, 55, 256, 1, 0), -1.5),  # ... partial last tile
                                           ((5, 64, 48, 32, 64, 3, 1), 2.0),  # the 3x3 / 64-channel band kernel
                                           ((2, 64, 56, 56, 64, 3, 1), 0.5)])  # (4-row bands: more rows than 256-px tiles)
 def test_bn_statistics_from_conv_epilogue(cuda, shape, offset):
