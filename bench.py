@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--glds-short", type=int, default=-1, choices=[-1, 0, 1],
                     help="bf16 NHWC convs: the two-stage 128-pixel LDS-DMA variant on short-reduction layers "
                          "(-1 = the build default; A/B)")
+    ap.add_argument("--bn-pipe", type=int, default=-1, choices=[-1, 0, 1],
+                    help="bf16 NHWC BN apply kernels: software-pipelined loads (-1 = the build default; A/B)")
     ap.add_argument("--bn-unroll", type=int, default=0, choices=[0, 2, 4],
                     help="bf16 NHWC BN apply kernels: vectors in flight per thread (0 = the build default; A/B)")
     ap.add_argument("--wt-stores", type=int, default=-1, choices=range(-1, 8), metavar="MASK",
@@ -127,6 +129,10 @@ def main():
         from mxddp import native as _native
 
         _native().nhwc_conv_set_glds_short(a.glds_short)
+    if a.bn_pipe >= 0:
+        from mxddp import native as _native
+
+        _native().nhwc_bn_set_pipe(a.bn_pipe)
     if a.bn_unroll:
         from mxddp import native as _native
 
@@ -282,7 +288,8 @@ def main():
                        "graph": _fused_graph(a, tr) or getattr(a, "layers_graph", False),
                        **_fused_config(a, tr), **({"conv_tile256": 1} if a.conv_tile256 else {}),
                        **({"bn_unroll": a.bn_unroll} if a.bn_unroll else {}),
-                       **({"glds_short": a.glds_short} if a.glds_short >= 0 else {})},
+                       **({"glds_short": a.glds_short} if a.glds_short >= 0 else {}),
+                       **({"bn_pipe": a.bn_pipe} if a.bn_pipe >= 0 else {})},
             **extra,
         }
         if C.shared_devices():

@@ -2091,7 +2091,12 @@ __global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
 // 256 and V = C / 8 divides 256 for every channel count up to 2048, so a thread's channel vector
 // v never changes: its 16 coefficients are loaded once into registers (the LDS copy indexed per
 // element cost 16-way bank conflicts: 9x more conflict than LDS-active cycles).
-template <int U>
+// PIPE: the next iteration's loads are issued before this iteration's stores, into the other
+// of two register buffers.  Without it the loop head waited (vmcnt) for the previous
+// iteration's stores to be acknowledged before issuing its loads -- the loaded registers were the
+// stores' data registers -- so every iteration paid a store round trip plus a load round trip
+// (the apply kernels streamed at ~3.4 TB/s, profiles/r4_pmc/pmc_rn.txt).
+template <int U, bool PIPE>
 __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
   const int V = a.C >> 3;
   const int total = a.Npix * V, step = gridDim.x * kBnT;
@@ -2112,11 +2117,10 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
   // the stores are masked
   const uint4* x4 = reinterpret_cast<const uint4*>(a.x);
   const uint4* r4 = reinterpret_cast<const uint4*>(a.res);
-  for (int i0 = i00; i0 < total; i0 += U * step) {
+  auto load = [&](int i0, uint4 (&xr)[U], uint4 (&rr)[U]) {
     int ic[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) ic[u] = min(i0 + u * step, total - 1);
-    uint4 xr[U], rr[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       xr[u] = x4[ic[u]];
@@ -2126,6 +2130,8 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
 #pragma unroll
       for (int u = 0; u < U; ++u) rr[u] = r4[ic[u]];
     }
+  };
+  auto apply = [&](int i0, const uint4 (&xr)[U], const uint4 (&rr)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = i0 + u * step;
@@ -2143,13 +2149,36 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
       reinterpret_cast<uint4*>(a.y)[i] = yo;
       if (a.mask) a.mask[i] = (uint8_t)pos_bits8(yo);
     }
+  };
+  if constexpr (!PIPE) {
+    for (int i0 = i00; i0 < total; i0 += U * step) {
+      uint4 xr[U], rr[U];
+      load(i0, xr, rr);
+      apply(i0, xr, rr);
+    }
+  } else {
+    // ping-pong: (xa, ra) hold iteration i0, (xb, rb) the next one; the prefetch past the end
+    // re-reads the last valid vectors (clamped) and is not used
+    uint4 xa[U], ra[U], xb[U], rb[U];
+    int i0 = i00;
+    if (i0 < total) load(i0, xa, ra);
+    while (i0 < total) {
+      const int i1 = i0 + U * step;
+      load(i1, xb, rb);
+      apply(i0, xa, ra);
+      if (i1 >= total) break;
+      const int i2 = i1 + U * step;
+      load(i2, xa, ra);
+      apply(i1, xb, rb);
+      i0 = i2;
+    }
   }
 }
 
 // backward apply: dx = A g + D x + B; dres = g (the residual branch gradient).  XM: the ReLU mask
 // from x and the forward's (scale, shift) (no residual), else from y.  Coefficients in registers
 // as in the forward apply (fixed channel vector per thread).
-template <bool XM, int U>
+template <bool XM, int U, bool PIPE>
 __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv fV) {
   const int V = a.C >> 3;
   const int total = a.Npix * V, step = gridDim.x * kBnT;
@@ -2180,42 +2209,46 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv f
   // clamped, unconditional loads (see bn_nhwc_apply_k); the mask source is a uniform branch
   const uint4 *g4 = reinterpret_cast<const uint4*>(a.dy), *x4 = reinterpret_cast<const uint4*>(a.x),
               *y4 = reinterpret_cast<const uint4*>(a.y);
-  for (int i0 = i00; i0 < total; i0 += U * step) {
+  struct Buf {
+    uint4 g[U], x[U], y[U];
+    uint32_t m[U];
+  };
+  auto load = [&](int i0, Buf& b) {
     int ic[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) ic[u] = min(i0 + u * step, total - 1);
-    uint4 gr[U], xr[U], yr[U];
-    uint32_t mb[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      gr[u] = g4[ic[u]];
-      xr[u] = x4[ic[u]];
-      yr[u] = z;
-      mb[u] = 0u;
+      b.g[u] = g4[ic[u]];
+      b.x[u] = x4[ic[u]];
+      b.y[u] = z;
+      b.m[u] = 0u;
     }
     if (bmask) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) mb[u] = a.mask[ic[u]];
+      for (int u = 0; u < U; ++u) b.m[u] = a.mask[ic[u]];
     } else if (ymask) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) yr[u] = y4[ic[u]];
+      for (int u = 0; u < U; ++u) b.y[u] = y4[ic[u]];
     }
+  };
+  auto apply = [&](int i0, const Buf& b) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = i0 + u * step;
       if (i >= total) break;
       float g[8], xv[8];
-      unpack8(gr[u], g);
-      unpack8(xr[u], xv);
+      unpack8(b.g[u], g);
+      unpack8(b.x[u], xv);
       if (XM) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) g[e] = fmaf(xv[e], mc[2 * e], mc[2 * e + 1]) > 0.f ? g[e] : 0.f;
       } else if (bmask) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) g[e] = (mb[u] >> e) & 1u ? g[e] : 0.f;
+        for (int e = 0; e < 8; ++e) g[e] = (b.m[u] >> e) & 1u ? g[e] : 0.f;
       } else if (a.relu) {
         float yv[8];
-        unpack8(yr[u], yv);
+        unpack8(b.y[u], yv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) g[e] = yv[e] > 0.f ? g[e] : 0.f;
       }
@@ -2224,6 +2257,27 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv f
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = fmaf(kc[3 * e], g[e], fmaf(kc[3 * e + 1], xv[e], kc[3 * e + 2]));
       reinterpret_cast<uint4*>(a.dx)[i] = pack8(o);
+    }
+  };
+  if constexpr (!PIPE) {
+    for (int i0 = i00; i0 < total; i0 += U * step) {
+      Buf b;
+      load(i0, b);
+      apply(i0, b);
+    }
+  } else {  // ping-pong as in bn_nhwc_apply_k
+    Buf ba, bb;
+    int i0 = i00;
+    if (i0 < total) load(i0, ba);
+    while (i0 < total) {
+      const int i1 = i0 + U * step;
+      load(i1, bb);
+      apply(i0, ba);
+      if (i1 >= total) break;
+      const int i2 = i1 + U * step;
+      load(i2, ba);
+      apply(i1, bb);
+      i0 = i2;
     }
   }
 }
@@ -2532,6 +2586,9 @@ void nhwc_bn_set_unroll(int u) {
   MX_CHECK(u == 2 || u == 4, "nhwc_bn_set_unroll: 2 or 4");
   g_bn_unroll = u;
 }
+// software-pipelined BN apply kernels (next loads before this iteration's stores): 1 = on
+static int g_bn_pipe = 1;
+void nhwc_bn_set_pipe(int on) { g_bn_pipe = on ? 1 : 0; }
 void nhwc_conv_set_glds256(int mode) { g_conv_glds256 = mode; }
 static bool glds256_fits(const ConvNArgs& a) {
   if (g_conv_glds256 == 0 || a.Ng % 256 != 0 || a.Kg % 64 != 0) return false;
@@ -2928,10 +2985,13 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
   }
   MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
-  if (g_bn_unroll == 4)
-    MX_LAUNCH(bn_nhwc_apply_k<4>, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));
+  const dim3 agrid(grid_for((int64_t)Npix * V, 2048));
+  if (g_bn_pipe)
+    MX_LAUNCH((bn_nhwc_apply_k<2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
+  else if (g_bn_unroll == 4)
+    MX_LAUNCH((bn_nhwc_apply_k<4, false>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
   else
-    MX_LAUNCH(bn_nhwc_apply_k<2>, dim3(grid_for((int64_t)Npix * V, 2048)), dim3(kBnT), 0, st, a, FastDiv(V));
+    MX_LAUNCH((bn_nhwc_apply_k<2, false>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
 }
 
 void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma, const float* mean,
@@ -2973,12 +3033,15 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
   MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
   const dim3 agrid(grid_for((int64_t)Npix * V, 2048));
-  if (g_bn_unroll == 4) {
-    if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 4>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
-    else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 4>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
+  if (g_bn_pipe) {
+    if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
+    else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
+  } else if (g_bn_unroll == 4) {
+    if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 4, false>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
+    else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 4, false>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
   } else {
-    if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 2>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
-    else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 2>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
+    if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 2, false>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
+    else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 2, false>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
   }
 }
 

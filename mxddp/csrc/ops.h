@@ -195,7 +195,8 @@ void nhwc_conv_set_glds(int mode);
 // the 256 x 256-tile LDS-DMA kernel: 0 = off (default), 1 = layers with >= 256 tiles, 2 = wherever Ng % 256 == 0
 void nhwc_conv_set_glds256(int mode);
 void nhwc_conv_set_glds_short(int mode);  // two-stage 128-pixel LDS-DMA variant for short reductions
-void nhwc_bn_set_unroll(int u);  // NHWC BN apply kernels: vectors in flight per thread (2 or 4)
+void nhwc_bn_set_unroll(int u);
+void nhwc_bn_set_pipe(int on);  // software-pipelined NHWC BN apply kernels (default on)  // NHWC BN apply kernels: vectors in flight per thread (2 or 4)
 // split-K scratch of nhwc_conv_dgrad (floats; 0 = none needed)
 size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
                                       int P, int Q);
