@@ -1920,25 +1920,33 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
   // in flight per thread cannot cover HBM latency with ~256 blocks
   constexpr int UNR = BWD ? 2 : 4;
   const int pstep = gridDim.x * ppi;
-  for (int p0 = blockIdx.x * ppi + pr; p0 < a.Npix; p0 += UNR * pstep) {
-    uint4 xr[UNR], gr[UNR], yr[UNR];
-    uint32_t mb[UNR];
-    // loads at clamped rows issued unconditionally (the rows past Npix are skipped below): a
-    // per-lane `ok ? load : 0` would branch around each load and drain with a vmcnt(0) per row
+  struct Buf {
+    uint4 x[UNR], g[UNR], y[UNR];
+    uint32_t m[UNR];
+  };
+  // loads at clamped rows issued unconditionally (the rows past Npix are skipped below): a
+  // per-lane `ok ? load : 0` would branch around each load and drain with a vmcnt(0) per row
+  auto load = [&](int p0, Buf& b) {
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int p = min(p0 + u * pstep, a.Npix - 1);
       const size_t o = (size_t)p * a.C + 8 * v;
-      xr[u] = *reinterpret_cast<const uint4*>(a.x + o);
+      b.x[u] = *reinterpret_cast<const uint4*>(a.x + o);
       if (BWD) {
-        gr[u] = *reinterpret_cast<const uint4*>(a.dy + o);
-        if (ymask) yr[u] = *reinterpret_cast<const uint4*>(a.y + o);
-        if (bmask) mb[u] = a.mask[o >> 3];
+        b.g[u] = *reinterpret_cast<const uint4*>(a.dy + o);
+        if (ymask) b.y[u] = *reinterpret_cast<const uint4*>(a.y + o);
+        if (bmask) b.m[u] = a.mask[o >> 3];
       }
     }
+  };
+  auto accumulate = [&](int p0, const Buf& b) {
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       if (p0 + u * pstep >= a.Npix) break;
+      const uint4* xr = b.x;
+      const uint4* gr = b.g;
+      const uint4* yr = b.y;
+      const uint32_t* mb = b.m;
       float xv[8];
       unpack8(xr[u], xv);
       if (!BWD) {
@@ -1970,6 +1978,21 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
         }
       }
     }
+  };
+  // the next rows' loads are in flight while this iteration's are summed (ping-pong buffers);
+  // unpipelined, every iteration paid a full load round trip (2.4 TB/s, profiles/r4_pmc)
+  Buf ba, bb;
+  int p0 = blockIdx.x * ppi + pr;
+  if (p0 < a.Npix) load(p0, ba);
+  while (p0 < a.Npix) {
+    const int p1 = p0 + UNR * pstep;
+    load(p1, bb);
+    accumulate(p0, ba);
+    if (p1 >= a.Npix) break;
+    const int p2 = p1 + UNR * pstep;
+    load(p2, ba);
+    accumulate(p1, bb);
+    p0 = p2;
   }
   // planar [16][kBnT] (thread-fastest): a thread-major [kBnT][16] layout put 16 threads on one
   // bank for every store and read (counters: 3.5x more conflict than LDS-active cycles)
