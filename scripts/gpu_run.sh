@@ -26,6 +26,7 @@
 #   copies_pyr / copies_rn   torch.profiler census of the device copies in a layer-path step
 #   trace_pyr    kernel + HIP API trace of the graphed PyramidNet step (where its copies come from)
 #   diag_bnstats backward BN statistics of the data-gradient epilogues vs torch
+#   bench_bn     effective bandwidth of the NHWC BN kernel variants vs a copy
 #   diag_join    residual-join / BN-statistics variants of two Bottleneck blocks vs a baseline (and a repeat)
 source "$(dirname "$0")/gpu_check.sh"
 rm -f gpurun_out/steps.log
@@ -74,6 +75,7 @@ for step in "$@"; do
         run "ab_wt7_$r" 300 python bench.py --steps 2000 --warmup 100 --wt-stores 7 || exit 1
       done ;;
     diag_join) run diag_join 300 python scripts/diag_join.py ;;
+    bench_bn) run bench_bn 300 python scripts/bench_bn.py ;;
     prof_wt) prof prof_wt 200 --steps 200 --warmup 20 --min-warmup-ms 0 --wt-stores 1 ;;
     coll) run coll 300 python bench.py --steps 2000 --warmup 100 --force-collectives ;;
     replica) run replica 300 python bench.py --impl replica --steps 1000 --warmup 50 ;;
