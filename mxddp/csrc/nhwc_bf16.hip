@@ -2612,6 +2612,13 @@ void nhwc_bn_set_unroll(int u) {
 // software-pipelined BN apply kernels (next loads before this iteration's stores): 1 = on
 static int g_bn_pipe = 1;
 void nhwc_bn_set_pipe(int on) { g_bn_pipe = on ? 1 : 0; }
+// most blocks of the BN apply kernels (grid-stride loops; any multiple of 256 threads keeps each
+// thread's channel vector fixed)
+static int g_bn_grid_cap = 2048;
+void nhwc_bn_set_grid_cap(int cap) {
+  MX_CHECK(cap >= 256, "nhwc_bn_set_grid_cap: >= 256");
+  g_bn_grid_cap = cap;
+}
 void nhwc_conv_set_glds256(int mode) { g_conv_glds256 = mode; }
 static bool glds256_fits(const ConvNArgs& a) {
   if (g_conv_glds256 == 0 || a.Ng % 256 != 0 || a.Kg % 64 != 0) return false;
@@ -3008,7 +3015,7 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
   }
   MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
-  const dim3 agrid(grid_for((int64_t)Npix * V, 2048));
+  const dim3 agrid(grid_for((int64_t)Npix * V, g_bn_grid_cap));
   if (g_bn_pipe)
     MX_LAUNCH((bn_nhwc_apply_k<2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
   else if (g_bn_unroll == 4)
@@ -3055,7 +3062,7 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
   }
   MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
-  const dim3 agrid(grid_for((int64_t)Npix * V, 2048));
+  const dim3 agrid(grid_for((int64_t)Npix * V, g_bn_grid_cap));
   if (g_bn_pipe) {
     if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
     else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));

@@ -87,6 +87,17 @@ def main():
         us = timed(fn, iters)
         rows.append((name, us, byts / us / 1e6))
         print(f"{name:42s} {us:8.1f} us  {byts / us / 1e6:6.2f} TB/s (nominal bytes)", flush=True)
+    # apply-kernel grid cap and software pipelining
+    for pipe in (0, 1):
+        for cap in (1024, 2048, 4096, 8192, 32768):
+            Cn.nhwc_bn_set_pipe(pipe)
+            Cn.nhwc_bn_set_grid_cap(cap)
+            f_us = timed(fwd(True, None, False), iters)
+            b_us = timed(bwd(True, True, False, False), iters)
+            print(f"pipe {pipe} grid cap {cap:6d}: fwd apply ReLU {f_us:7.1f} us ({2 * nbytes / f_us / 1e6:5.2f} TB/s), "
+                  f"bwd {b_us:7.1f} us ({5 * nbytes / b_us / 1e6:5.2f} TB/s)", flush=True)
+    Cn.nhwc_bn_set_pipe(1)
+    Cn.nhwc_bn_set_grid_cap(2048)
 
 
 if __name__ == "__main__":
