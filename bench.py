@@ -78,8 +78,8 @@ def parse():
     ap.add_argument("--lr", type=float, default=0.01, help="SGD lr (momentum 0.9, wd 1e-4 as the reference)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
                     help="GEMM precision of the layers path (headline is fp32, >= the reference's precision)")
-    ap.add_argument("--conv-tile256", type=int, default=0, choices=[0, 1],
-                    help="bf16 NHWC convs: the 256 x 256-tile LDS-DMA kernel on layers with >= 256 tiles (A/B)")
+    ap.add_argument("--conv-tile256", type=int, default=-1, choices=[-1, 0, 1],
+                    help="bf16 NHWC convs: the 256 x 256-tile LDS-DMA kernel on layers with >= 256 tiles and >= 4 k-tiles (-1 = the build default: on; A/B)")
     ap.add_argument("--glds-short", type=int, default=-1, choices=[-1, 0, 1],
                     help="bf16 NHWC convs: the two-stage 128-pixel LDS-DMA variant on short-reduction layers "
                          "(-1 = the build default; A/B)")
@@ -121,7 +121,7 @@ def main():
             print(f"bench.py: --gpus {a.gpus} needs a launcher (torch.distributed.run)", file=sys.stderr)
             sys.exit(2)
     inf = C.init_distributed(use_gpu=True)
-    if a.conv_tile256:
+    if a.conv_tile256 >= 0:
         from mxddp import native as _native
 
         _native().nhwc_conv_set_glds256(a.conv_tile256)
@@ -286,7 +286,7 @@ def main():
                        "image": "x".join(map(str, spec.input_shape)), "parallelism": f"dp{a.gpus}", "impl": a.impl,
                        # how the timed steps were actually launched (autotune may pick eager mode 0)
                        "graph": _fused_graph(a, tr) or getattr(a, "layers_graph", False),
-                       **_fused_config(a, tr), **({"conv_tile256": 1} if a.conv_tile256 else {}),
+                       **_fused_config(a, tr), **({"conv_tile256": a.conv_tile256} if a.conv_tile256 >= 0 else {}),
                        **({"bn_unroll": a.bn_unroll} if a.bn_unroll else {}),
                        **({"glds_short": a.glds_short} if a.glds_short >= 0 else {}),
                        **({"bn_pipe": a.bn_pipe} if a.bn_pipe >= 0 else {})},

@@ -2595,9 +2595,9 @@ static GldsPlan glds_plan(const ConvNArgs& a, bool wide, bool par) {
   return glds_plan_mnk(a.M, a.Ng, a.Kg);
 }
 
-// the 256 x 256 tile (conv_nhwc_glds256_kernel): 0 = never (default until measured), 1 = where
-// it fills the chip (>= 256 tiles, no split-K needed), 2 = wherever Ng % 256 == 0 (tests)
-static int g_conv_glds256 = 0;
+// the 256 x 256 tile (conv_nhwc_glds256_kernel): 0 = never, 1 = where it fills the chip with a
+// reduction of >= 4 k-tiles (default), 2 = wherever Ng % 256 == 0 (tests)
+static int g_conv_glds256 = 1;
 // the two-stage 128-pixel variant of the LDS-DMA kernel (conv_nhwc_glds_kernel<TM, STATS, 128, 2>)
 // for layers of <= 2 k-tiles with >= 512 tiles: 0 = never, 1 = there (default)
 static int g_conv_glds_short = 1;
@@ -2623,7 +2623,11 @@ void nhwc_conv_set_glds256(int mode) { g_conv_glds256 = mode; }
 static bool glds256_fits(const ConvNArgs& a) {
   if (g_conv_glds256 == 0 || a.Ng % 256 != 0 || a.Kg % 64 != 0) return false;
   const int64_t tiles = (int64_t)(a.Ng / 256) * cdiv(a.M, 256);
-  return g_conv_glds256 == 2 || tiles >= 256;
+  // mode 1: enough tiles to fill the chip and a reduction of >= 4 k-tiles -- measured per layer at
+  // batch 256 (profiles/r4_i/rn_layers_t256.log): a win on every such layer (e.g. 512 -> 2048
+  // forward 51.8 -> 43.4 us, 1024 -> 512 84.1 -> 68.4 us), a loss on the 1-2 k-tile layers, which
+  // the two-stage 128-pixel variant serves better
+  return g_conv_glds256 == 2 || (tiles >= 256 && a.Kg >= 256);
 }
 
 size_t nhwc_conv_scratch_floats(int M, int Ng, int Kg) {

@@ -111,6 +111,13 @@ for step in "$@"; do
         run "ab_bnpipe1_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --bn-pipe 1 || exit 1
       done ;;
     prof_rn_pipe0) prof prof_rn_pipe0 3 --model resnet50 --dtype bf16 --batch 256 --steps 3 --warmup 2 --min-warmup-ms 0 --bn-pipe 0 ;;
+    ab_t256)  # ResNet-50: 256 x 256 tile on the long-reduction layers off vs on, interleaved
+      for r in 1 2; do
+        run "ab_t256_0_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --conv-tile256 0 &&
+        run "ab_t256_1_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --conv-tile256 1 || exit 1
+      done
+      run ab_t256_0_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --conv-tile256 0 &&
+      run ab_t256_1_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --conv-tile256 1 || exit 1 ;;
     rn_layers_short0) run rn_layers_short0 300 python scripts/bench_nhwc_layers.py 256 5 0 0 ;;
     rn32_t256) run rn32_t256 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --conv-tile256 1 ;;
     rn_layers) run rn_layers 300 python scripts/bench_nhwc_layers.py 256 5 ;;
