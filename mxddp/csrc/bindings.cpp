@@ -117,6 +117,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_bn_set_unroll", &nhwc_bn_set_unroll);
   m.def("nhwc_bn_set_pipe", &nhwc_bn_set_pipe);
   m.def("nhwc_bn_set_grid_cap", &nhwc_bn_set_grid_cap);
+  m.def("nhwc_bn_set_stat_blocks", &nhwc_bn_set_stat_blocks);
   m.def("mnist_set_wt_stores", &mnist_set_wt_stores,
         "MNIST bulk stores with agent scope (L2 write-through) for steps launched afterwards: mask 1 = F5, 2 = F2, "
         "4 = F6W");

@@ -2613,8 +2613,10 @@ void nhwc_bn_set_unroll(int u) {
 static int g_bn_pipe = 1;
 void nhwc_bn_set_pipe(int on) { g_bn_pipe = on ? 1 : 0; }
 // most blocks of the BN apply kernels (grid-stride loops; any multiple of 256 threads keeps each
-// thread's channel vector fixed)
-static int g_bn_grid_cap = 2048;
+// thread's channel vector fixed).  scripts/bench_bn.py on a 411 MB tensor: forward apply 171 us
+// (4.8 TB/s) at 2048 blocks, 147 us (5.6 TB/s, above a torch copy's 5.2) at 32768; backward 448
+// -> 391 us (profiles/r4_j/bench_bn.log)
+static int g_bn_grid_cap = 65536;
 void nhwc_bn_set_grid_cap(int cap) {
   MX_CHECK(cap >= 256, "nhwc_bn_set_grid_cap: >= 256");
   g_bn_grid_cap = cap;
@@ -2966,12 +2968,17 @@ void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, in
             R * S, accumulate ? 1 : 0, G);
 }
 
+// blocks of the statistics pass (one partial row each; the finalize sums them in passes of 2048)
+static int g_bn_stat_blocks = 1024;
+void nhwc_bn_set_stat_blocks(int n) {
+  MX_CHECK(n >= 256 && n <= 8192, "nhwc_bn_set_stat_blocks: 256 .. 8192");
+  g_bn_stat_blocks = n;
+}
 static dim3 bn_grid(int Npix, int C) {
   const int V = C / 8, vv = V >= kBnT ? kBnT : V, ppi = kBnT / vv;
   const int gy = V >= kBnT ? V / kBnT : 1;
-  // ~1024 blocks in total (4 per CU), at least 8 pixel rows per thread
-  // (<= 1024 partial rows: the finalize reads at most 8 per thread x 128 row groups)
-  const int gx = std::max(1, std::min(cdiv(Npix, ppi * 8), std::max(1, 1024 / gy)));
+  // g_bn_stat_blocks blocks in total, at least 8 pixel rows per thread
+  const int gx = std::max(1, std::min(cdiv(Npix, ppi * 8), std::max(1, g_bn_stat_blocks / gy)));
   return dim3(gx, gy);
 }
 

@@ -197,7 +197,8 @@ void nhwc_conv_set_glds256(int mode);
 void nhwc_conv_set_glds_short(int mode);  // two-stage 128-pixel LDS-DMA variant for short reductions
 void nhwc_bn_set_unroll(int u);
 void nhwc_bn_set_pipe(int on);
-void nhwc_bn_set_grid_cap(int cap);  // most blocks of the NHWC BN apply kernels  // software-pipelined NHWC BN apply kernels (default on)  // NHWC BN apply kernels: vectors in flight per thread (2 or 4)
+void nhwc_bn_set_grid_cap(int cap);  // most blocks of the NHWC BN apply kernels
+void nhwc_bn_set_stat_blocks(int n);  // blocks of the NHWC BN statistics pass  // software-pipelined NHWC BN apply kernels (default on)  // NHWC BN apply kernels: vectors in flight per thread (2 or 4)
 // split-K scratch of nhwc_conv_dgrad (floats; 0 = none needed)
 size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
                                       int P, int Q);

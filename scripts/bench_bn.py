@@ -97,7 +97,15 @@ def main():
             print(f"pipe {pipe} grid cap {cap:6d}: fwd apply ReLU {f_us:7.1f} us ({2 * nbytes / f_us / 1e6:5.2f} TB/s), "
                   f"bwd {b_us:7.1f} us ({5 * nbytes / b_us / 1e6:5.2f} TB/s)", flush=True)
     Cn.nhwc_bn_set_pipe(1)
-    Cn.nhwc_bn_set_grid_cap(2048)
+    Cn.nhwc_bn_set_grid_cap(65536)
+    # statistics-pass blocks (one partial row each)
+    for nb in (1024, 2048, 4096, 8192):
+        Cn.nhwc_bn_set_stat_blocks(nb)
+        s_us = timed(fwd(True, None, False, pre=False), iters)
+        b_us = timed(bwd(True, True, False, False), iters)
+        print(f"stat blocks {nb:5d}: fwd with statistics {s_us:7.1f} us ({3 * nbytes / s_us / 1e6:5.2f} TB/s), "
+              f"bwd {b_us:7.1f} us ({5 * nbytes / b_us / 1e6:5.2f} TB/s)", flush=True)
+    Cn.nhwc_bn_set_stat_blocks(1024)
 
 
 if __name__ == "__main__":
