@@ -2735,7 +2735,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     }
     if (gp.splits > 1) {
       const int64_t n4 = (int64_t)a.M * a.Ng / 4;
-      MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, gp.splits,
+      MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 65536)), dim3(256), 0, st, scratch, a.out, n4, gp.splits,
                 a.addend, a.amask);
     }
     return a.bnpart ? gx : 0;
@@ -2773,7 +2773,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   }
   if (p.splits > 1) {
     const int64_t n4 = (int64_t)a.M * a.Ng / 4;
-    MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, p.splits,
+    MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 65536)), dim3(256), 0, st, scratch, a.out, n4, p.splits,
               a.addend, a.amask);
   }
   return bst ? brows : 0;
@@ -3089,7 +3089,8 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
 void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, int k,
                       int s, int p, hipStream_t st) {
   MX_CHECK(C % 8 == 0 && (int64_t)N * H * W * C / 8 < (1ll << 31), "nhwc maxpool: C % 8 and 32-bit indices");
-  const dim3 g(grid_for((int64_t)N * P * Q * (C / 8))), b(256);
+  // grid-stride loops: a large grid streams faster than a 4,096-block one (scripts/bench_bn.py)
+  const dim3 g(grid_for((int64_t)N * P * Q * (C / 8), 65536)), b(256);
   const FastDiv fV(C / 8), fQ(Q), fP(P);
   if (k == 3) MX_LAUNCH(maxpool_nhwc_k<3>, g, b, 0, st, x, y, arg, N, H, W, C, P, Q, k, s, p, fV, fQ, fP);
   else MX_LAUNCH(maxpool_nhwc_k<0>, g, b, 0, st, x, y, arg, N, H, W, C, P, Q, k, s, p, fV, fQ, fP);
@@ -3098,7 +3099,7 @@ void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H
 void nhwc_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int P, int Q,
                       int k, int s, int p, hipStream_t st) {
   MX_CHECK(C % 8 == 0 && (int64_t)N * H * W * C / 8 < (1ll << 31), "nhwc maxpool: C % 8 and 32-bit indices");
-  const dim3 g(grid_for((int64_t)N * H * W * (C / 8))), b(256);
+  const dim3 g(grid_for((int64_t)N * H * W * (C / 8), 65536)), b(256);
   const FastDiv fV(C / 8), fW(W), fH(H), fS(s);
   if (k == 3 && s == 2 && p == 1)
     MX_LAUNCH(maxpool_nhwc_bwd_s2_k, g, b, 0, st, dy, arg, dx, N, H, W, C, P, Q, fV, fW, fH);
