@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--glds-short", type=int, default=-1, choices=[-1, 0, 1],
                     help="bf16 NHWC convs: the two-stage 128-pixel LDS-DMA variant on short-reduction layers "
                          "(-1 = the build default; A/B)")
+    ap.add_argument("--bn-grid-cap", type=int, default=0,
+                    help="bf16 NHWC BN apply kernels: most blocks (0 = the build default; 2048 = round-3 grids; A/B)")
     ap.add_argument("--bn-pipe", type=int, default=-1, choices=[-1, 0, 1],
                     help="bf16 NHWC BN apply kernels: software-pipelined loads (-1 = the build default; A/B)")
     ap.add_argument("--bn-unroll", type=int, default=0, choices=[0, 2, 4],
@@ -129,6 +131,10 @@ def main():
         from mxddp import native as _native
 
         _native().nhwc_conv_set_glds_short(a.glds_short)
+    if a.bn_grid_cap:
+        from mxddp import native as _native
+
+        _native().nhwc_bn_set_grid_cap(a.bn_grid_cap)
     if a.bn_pipe >= 0:
         from mxddp import native as _native
 
@@ -289,7 +295,8 @@ def main():
                        **_fused_config(a, tr), **({"conv_tile256": a.conv_tile256} if a.conv_tile256 >= 0 else {}),
                        **({"bn_unroll": a.bn_unroll} if a.bn_unroll else {}),
                        **({"glds_short": a.glds_short} if a.glds_short >= 0 else {}),
-                       **({"bn_pipe": a.bn_pipe} if a.bn_pipe >= 0 else {})},
+                       **({"bn_pipe": a.bn_pipe} if a.bn_pipe >= 0 else {}),
+                       **({"bn_grid_cap": a.bn_grid_cap} if a.bn_grid_cap else {})},
             **extra,
         }
         if C.shared_devices():

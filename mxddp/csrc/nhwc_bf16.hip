@@ -2612,11 +2612,17 @@ void nhwc_bn_set_unroll(int u) {
 // software-pipelined BN apply kernels (next loads before this iteration's stores): 1 = on
 static int g_bn_pipe = 1;
 void nhwc_bn_set_pipe(int on) { g_bn_pipe = on ? 1 : 0; }
-// most blocks of the BN apply kernels (grid-stride loops; any multiple of 256 threads keeps each
-// thread's channel vector fixed).  scripts/bench_bn.py on a 411 MB tensor: forward apply 171 us
-// (4.8 TB/s) at 2048 blocks, 147 us (5.6 TB/s, above a torch copy's 5.2) at 32768; backward 448
-// -> 391 us (profiles/r4_j/bench_bn.log)
-static int g_bn_grid_cap = 65536;
+// blocks of the BN apply kernels (grid-stride loops; any multiple of 256 threads keeps each
+// thread's channel vector fixed): ~6 vectors per thread, at least 2,048 blocks (or one vector per
+// thread), at most g_bn_grid_cap.  scripts/bench_bn.py on a 411 MB tensor: forward apply 171 us
+// (4.8 TB/s) at 2,048 blocks, 139-147 us (5.6-5.9 TB/s, above a torch copy's 5.2) at 8-32 k
+// (profiles/r4_j/); a flat 65,536-block cap made the mid-sized layers of the real step slower
+// (dispatch-bound, ResNet-50 9,683 img/s, profiles/r4_k/)
+static int g_bn_grid_cap = 32768;
+static int bn_apply_blocks(int64_t total) {
+  int64_t nb = std::max<int64_t>(cdiv(total, (int64_t)256 * 6), std::min<int64_t>(2048, cdiv(total, 256)));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(nb, g_bn_grid_cap));
+}
 void nhwc_bn_set_grid_cap(int cap) {
   MX_CHECK(cap >= 256, "nhwc_bn_set_grid_cap: >= 256");
   g_bn_grid_cap = cap;
@@ -2735,7 +2741,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     }
     if (gp.splits > 1) {
       const int64_t n4 = (int64_t)a.M * a.Ng / 4;
-      MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 65536)), dim3(256), 0, st, scratch, a.out, n4, gp.splits,
+      MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, gp.splits,
                 a.addend, a.amask);
     }
     return a.bnpart ? gx : 0;
@@ -2773,7 +2779,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   }
   if (p.splits > 1) {
     const int64_t n4 = (int64_t)a.M * a.Ng / 4;
-    MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 65536)), dim3(256), 0, st, scratch, a.out, n4, p.splits,
+    MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, p.splits,
               a.addend, a.amask);
   }
   return bst ? brows : 0;
@@ -3026,7 +3032,7 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
   }
   MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
-  const dim3 agrid(grid_for((int64_t)Npix * V, g_bn_grid_cap));
+  const dim3 agrid(bn_apply_blocks((int64_t)Npix * V));
   if (g_bn_pipe)
     MX_LAUNCH((bn_nhwc_apply_k<2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
   else if (g_bn_unroll == 4)
@@ -3073,7 +3079,7 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
   }
   MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
-  const dim3 agrid(grid_for((int64_t)Npix * V, g_bn_grid_cap));
+  const dim3 agrid(bn_apply_blocks((int64_t)Npix * V));
   if (g_bn_pipe) {
     if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
     else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
@@ -3089,8 +3095,7 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
 void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, int k,
                       int s, int p, hipStream_t st) {
   MX_CHECK(C % 8 == 0 && (int64_t)N * H * W * C / 8 < (1ll << 31), "nhwc maxpool: C % 8 and 32-bit indices");
-  // grid-stride loops: a large grid streams faster than a 4,096-block one (scripts/bench_bn.py)
-  const dim3 g(grid_for((int64_t)N * P * Q * (C / 8), 65536)), b(256);
+  const dim3 g(grid_for((int64_t)N * P * Q * (C / 8))), b(256);
   const FastDiv fV(C / 8), fQ(Q), fP(P);
   if (k == 3) MX_LAUNCH(maxpool_nhwc_k<3>, g, b, 0, st, x, y, arg, N, H, W, C, P, Q, k, s, p, fV, fQ, fP);
   else MX_LAUNCH(maxpool_nhwc_k<0>, g, b, 0, st, x, y, arg, N, H, W, C, P, Q, k, s, p, fV, fQ, fP);
@@ -3099,7 +3104,7 @@ void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H
 void nhwc_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int P, int Q,
                       int k, int s, int p, hipStream_t st) {
   MX_CHECK(C % 8 == 0 && (int64_t)N * H * W * C / 8 < (1ll << 31), "nhwc maxpool: C % 8 and 32-bit indices");
-  const dim3 g(grid_for((int64_t)N * H * W * (C / 8), 65536)), b(256);
+  const dim3 g(grid_for((int64_t)N * H * W * (C / 8))), b(256);
   const FastDiv fV(C / 8), fW(W), fH(H), fS(s);
   if (k == 3 && s == 2 && p == 1)
     MX_LAUNCH(maxpool_nhwc_bwd_s2_k, g, b, 0, st, dy, arg, dx, N, H, W, C, P, Q, fV, fW, fH);

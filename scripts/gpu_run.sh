@@ -110,6 +110,13 @@ for step in "$@"; do
         run "ab_bnpipe0_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --bn-pipe 0 &&
         run "ab_bnpipe1_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --bn-pipe 1 || exit 1
       done ;;
+    ab_bngrid)  # ResNet-50 batch 256 / 32: BN apply grids of round 3 (2,048 blocks) vs size-aware
+      for r in 1 2; do
+        run "ab_bngrid2k_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --bn-grid-cap 2048 &&
+        run "ab_bngrid_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 || exit 1
+      done
+      run ab_bngrid2k_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --bn-grid-cap 2048 &&
+      run ab_bngrid_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 || exit 1 ;;
     prof_rn_pipe0) prof prof_rn_pipe0 3 --model resnet50 --dtype bf16 --batch 256 --steps 3 --warmup 2 --min-warmup-ms 0 --bn-pipe 0 ;;
     ab_t256)  # ResNet-50: 256 x 256 tile on the long-reduction layers off vs on, interleaved
       for r in 1 2; do
