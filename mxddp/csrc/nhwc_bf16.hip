@@ -2482,6 +2482,16 @@ int grid_for(int64_t n, int cap = 4096) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
 }
 
+// grid of a streaming grid-stride kernel over n items (256-thread blocks): ~6 items per thread,
+// at least 2,048 blocks (or one item per thread), at most `cap`.  Measured on the BN apply kernels
+// (scripts/bench_bn.py, profiles/r4_j..l): 2,048-block grids capped a 411 MB stream at 4.8 TB/s,
+// 8-32 k blocks reach 5.6-5.9; a flat 65,536 made the mid-sized layers dispatch-bound.
+static int g_stream_cap = 32768;
+static int stream_blocks(int64_t n) {
+  const int64_t nb = std::max<int64_t>((n + 256 * 6 - 1) / (256 * 6), std::min<int64_t>(2048, (n + 255) / 256));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(nb, g_stream_cap));
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
@@ -2612,20 +2622,12 @@ void nhwc_bn_set_unroll(int u) {
 // software-pipelined BN apply kernels (next loads before this iteration's stores): 1 = on
 static int g_bn_pipe = 1;
 void nhwc_bn_set_pipe(int on) { g_bn_pipe = on ? 1 : 0; }
-// blocks of the BN apply kernels (grid-stride loops; any multiple of 256 threads keeps each
-// thread's channel vector fixed): ~6 vectors per thread, at least 2,048 blocks (or one vector per
-// thread), at most g_bn_grid_cap.  scripts/bench_bn.py on a 411 MB tensor: forward apply 171 us
-// (4.8 TB/s) at 2,048 blocks, 139-147 us (5.6-5.9 TB/s, above a torch copy's 5.2) at 8-32 k
-// (profiles/r4_j/); a flat 65,536-block cap made the mid-sized layers of the real step slower
-// (dispatch-bound, ResNet-50 9,683 img/s, profiles/r4_k/)
-static int g_bn_grid_cap = 32768;
-static int bn_apply_blocks(int64_t total) {
-  int64_t nb = std::max<int64_t>(cdiv(total, (int64_t)256 * 6), std::min<int64_t>(2048, cdiv(total, 256)));
-  return (int)std::max<int64_t>(1, std::min<int64_t>(nb, g_bn_grid_cap));
-}
-void nhwc_bn_set_grid_cap(int cap) {
+// blocks of the BN apply kernels (any multiple of 256 threads keeps each thread's channel vector
+// fixed): stream_blocks; ResNet-50 9,981 -> 10,218 img/s against the old 2,048-block cap
+// (profiles/r4_l/)
+void nhwc_bn_set_grid_cap(int cap) {  // cap of stream_blocks (2048 = the round-3 grids)
   MX_CHECK(cap >= 256, "nhwc_bn_set_grid_cap: >= 256");
-  g_bn_grid_cap = cap;
+  g_stream_cap = cap;
 }
 void nhwc_conv_set_glds256(int mode) { g_conv_glds256 = mode; }
 static bool glds256_fits(const ConvNArgs& a) {
@@ -2741,7 +2743,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     }
     if (gp.splits > 1) {
       const int64_t n4 = (int64_t)a.M * a.Ng / 4;
-      MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, gp.splits,
+      MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(stream_blocks(n4)), dim3(256), 0, st, scratch, a.out, n4, gp.splits,
                 a.addend, a.amask);
     }
     return a.bnpart ? gx : 0;
@@ -2779,7 +2781,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   }
   if (p.splits > 1) {
     const int64_t n4 = (int64_t)a.M * a.Ng / 4;
-    MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, p.splits,
+    MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(stream_blocks(n4)), dim3(256), 0, st, scratch, a.out, n4, p.splits,
               a.addend, a.amask);
   }
   return bst ? brows : 0;
@@ -3032,7 +3034,7 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
   }
   MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
-  const dim3 agrid(bn_apply_blocks((int64_t)Npix * V));
+  const dim3 agrid(stream_blocks((int64_t)Npix * V));
   if (g_bn_pipe)
     MX_LAUNCH((bn_nhwc_apply_k<2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
   else if (g_bn_unroll == 4)
@@ -3079,7 +3081,7 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
   }
   MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
-  const dim3 agrid(bn_apply_blocks((int64_t)Npix * V));
+  const dim3 agrid(stream_blocks((int64_t)Npix * V));
   if (g_bn_pipe) {
     if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
     else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
@@ -3095,7 +3097,7 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
 void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, int k,
                       int s, int p, hipStream_t st) {
   MX_CHECK(C % 8 == 0 && (int64_t)N * H * W * C / 8 < (1ll << 31), "nhwc maxpool: C % 8 and 32-bit indices");
-  const dim3 g(grid_for((int64_t)N * P * Q * (C / 8))), b(256);
+  const dim3 g(stream_blocks((int64_t)N * P * Q * (C / 8))), b(256);
   const FastDiv fV(C / 8), fQ(Q), fP(P);
   if (k == 3) MX_LAUNCH(maxpool_nhwc_k<3>, g, b, 0, st, x, y, arg, N, H, W, C, P, Q, k, s, p, fV, fQ, fP);
   else MX_LAUNCH(maxpool_nhwc_k<0>, g, b, 0, st, x, y, arg, N, H, W, C, P, Q, k, s, p, fV, fQ, fP);
@@ -3104,7 +3106,7 @@ void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H
 void nhwc_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int P, int Q,
                       int k, int s, int p, hipStream_t st) {
   MX_CHECK(C % 8 == 0 && (int64_t)N * H * W * C / 8 < (1ll << 31), "nhwc maxpool: C % 8 and 32-bit indices");
-  const dim3 g(grid_for((int64_t)N * H * W * (C / 8))), b(256);
+  const dim3 g(stream_blocks((int64_t)N * H * W * (C / 8))), b(256);
   const FastDiv fV(C / 8), fW(W), fH(H), fS(s);
   if (k == 3 && s == 2 && p == 1)
     MX_LAUNCH(maxpool_nhwc_bwd_s2_k, g, b, 0, st, dy, arg, dx, N, H, W, C, P, Q, fV, fW, fH);
@@ -3117,7 +3119,7 @@ void nhwc_gap_fwd(const uint16_t* x, float* y, int N, int HW, int C, hipStream_t
 }
 
 void nhwc_gap_bwd(const float* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st) {
-  MX_LAUNCH(gap_nhwc_bwd_k, dim3(grid_for((int64_t)N * HW * C)), dim3(256), 0, st, dy, dx, N, HW, C);
+  MX_LAUNCH(gap_nhwc_bwd_k, dim3(stream_blocks((int64_t)N * HW * C)), dim3(256), 0, st, dy, dx, N, HW, C);
 }
 
 }  // namespace mx
