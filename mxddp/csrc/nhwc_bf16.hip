@@ -2743,7 +2743,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     }
     if (gp.splits > 1) {
       const int64_t n4 = (int64_t)a.M * a.Ng / 4;
-      MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(stream_blocks(n4)), dim3(256), 0, st, scratch, a.out, n4, gp.splits,
+      MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, gp.splits,
                 a.addend, a.amask);
     }
     return a.bnpart ? gx : 0;
@@ -2781,7 +2781,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   }
   if (p.splits > 1) {
     const int64_t n4 = (int64_t)a.M * a.Ng / 4;
-    MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(stream_blocks(n4)), dim3(256), 0, st, scratch, a.out, n4, p.splits,
+    MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, p.splits,
               a.addend, a.amask);
   }
   return bst ? brows : 0;
@@ -3097,7 +3097,7 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
 void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, int k,
                       int s, int p, hipStream_t st) {
   MX_CHECK(C % 8 == 0 && (int64_t)N * H * W * C / 8 < (1ll << 31), "nhwc maxpool: C % 8 and 32-bit indices");
-  const dim3 g(stream_blocks((int64_t)N * P * Q * (C / 8))), b(256);
+  const dim3 g(grid_for((int64_t)N * P * Q * (C / 8))), b(256);  // (stream_blocks: 133 -> 147 us)
   const FastDiv fV(C / 8), fQ(Q), fP(P);
   if (k == 3) MX_LAUNCH(maxpool_nhwc_k<3>, g, b, 0, st, x, y, arg, N, H, W, C, P, Q, k, s, p, fV, fQ, fP);
   else MX_LAUNCH(maxpool_nhwc_k<0>, g, b, 0, st, x, y, arg, N, H, W, C, P, Q, k, s, p, fV, fQ, fP);
@@ -3106,7 +3106,7 @@ void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H
 void nhwc_maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int P, int Q,
                       int k, int s, int p, hipStream_t st) {
   MX_CHECK(C % 8 == 0 && (int64_t)N * H * W * C / 8 < (1ll << 31), "nhwc maxpool: C % 8 and 32-bit indices");
-  const dim3 g(stream_blocks((int64_t)N * H * W * (C / 8))), b(256);
+  const dim3 g(grid_for((int64_t)N * H * W * (C / 8))), b(256);  // (stream_blocks: no change)
   const FastDiv fV(C / 8), fW(W), fH(H), fS(s);
   if (k == 3 && s == 2 && p == 1)
     MX_LAUNCH(maxpool_nhwc_bwd_s2_k, g, b, 0, st, dy, arg, dx, N, H, W, C, P, Q, fV, fW, fH);
@@ -3119,7 +3119,7 @@ void nhwc_gap_fwd(const uint16_t* x, float* y, int N, int HW, int C, hipStream_t
 }
 
 void nhwc_gap_bwd(const float* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st) {
-  MX_LAUNCH(gap_nhwc_bwd_k, dim3(stream_blocks((int64_t)N * HW * C)), dim3(256), 0, st, dy, dx, N, HW, C);
+  MX_LAUNCH(gap_nhwc_bwd_k, dim3(grid_for((int64_t)N * HW * C)), dim3(256), 0, st, dy, dx, N, HW, C);
 }
 
 }  // namespace mx
