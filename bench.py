@@ -85,10 +85,6 @@ def parse():
                          "(-1 = the build default; A/B)")
     ap.add_argument("--bn-grid-cap", type=int, default=0,
                     help="bf16 NHWC BN apply kernels: most blocks (0 = the build default; 2048 = round-3 grids; A/B)")
-    ap.add_argument("--bn-pipe", type=int, default=-1, choices=[-1, 0, 1],
-                    help="bf16 NHWC BN apply kernels: software-pipelined loads (-1 = the build default; A/B)")
-    ap.add_argument("--bn-unroll", type=int, default=0, choices=[0, 2, 4],
-                    help="bf16 NHWC BN apply kernels: vectors in flight per thread (0 = the build default; A/B)")
     ap.add_argument("--wt-stores", type=int, default=-1, choices=range(-1, 8), metavar="MASK",
                     help="fused MNIST: bulk stores with agent scope (L2 write-through), 1 = F5, 2 = F2, 4 = F6W "
                          "(-1 = the build default; A/B)")
@@ -135,14 +131,6 @@ def main():
         from mxddp import native as _native
 
         _native().nhwc_bn_set_grid_cap(a.bn_grid_cap)
-    if a.bn_pipe >= 0:
-        from mxddp import native as _native
-
-        _native().nhwc_bn_set_pipe(a.bn_pipe)
-    if a.bn_unroll:
-        from mxddp import native as _native
-
-        _native().nhwc_bn_set_unroll(a.bn_unroll)
     if a.wt_stores >= 0:
         from mxddp import native as _native
 
@@ -293,9 +281,7 @@ def main():
                        # how the timed steps were actually launched (autotune may pick eager mode 0)
                        "graph": _fused_graph(a, tr) or getattr(a, "layers_graph", False),
                        **_fused_config(a, tr), **({"conv_tile256": a.conv_tile256} if a.conv_tile256 >= 0 else {}),
-                       **({"bn_unroll": a.bn_unroll} if a.bn_unroll else {}),
                        **({"glds_short": a.glds_short} if a.glds_short >= 0 else {}),
-                       **({"bn_pipe": a.bn_pipe} if a.bn_pipe >= 0 else {}),
                        **({"bn_grid_cap": a.bn_grid_cap} if a.bn_grid_cap else {})},
             **extra,
         }

@@ -2612,16 +2612,8 @@ static int g_conv_glds256 = 1;
 // for layers of <= 2 k-tiles with >= 512 tiles: 0 = never, 1 = there (default)
 static int g_conv_glds_short = 1;
 void nhwc_conv_set_glds_short(int mode) { g_conv_glds_short = mode; }
-// vectors per thread per iteration of the BN apply kernels (2 or 4; 4 measured ~1 % slower at
-// ResNet-50 batch 256, profiles/r4_ab)
-static int g_bn_unroll = 2;
-void nhwc_bn_set_unroll(int u) {
-  MX_CHECK(u == 2 || u == 4, "nhwc_bn_set_unroll: 2 or 4");
-  g_bn_unroll = u;
-}
-// software-pipelined BN apply kernels (next loads before this iteration's stores): 1 = on
-static int g_bn_pipe = 1;
-void nhwc_bn_set_pipe(int on) { g_bn_pipe = on ? 1 : 0; }
+// The BN apply kernels run U = 2 vectors per iteration, software-pipelined (4 vectors measured
+// ~1 % slower, the unpipelined loop equal: profiles/r4_ab2, r4_g).
 // blocks of the BN apply kernels (any multiple of 256 threads keeps each thread's channel vector
 // fixed): stream_blocks; ResNet-50 9,981 -> 10,218 img/s against the old 2,048-block cap
 // (profiles/r4_l/)
@@ -2976,17 +2968,12 @@ void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, in
             R * S, accumulate ? 1 : 0, G);
 }
 
-// blocks of the statistics pass (one partial row each; the finalize sums them in passes of 2048)
-static int g_bn_stat_blocks = 1024;
-void nhwc_bn_set_stat_blocks(int n) {
-  MX_CHECK(n >= 256 && n <= 8192, "nhwc_bn_set_stat_blocks: 256 .. 8192");
-  g_bn_stat_blocks = n;
-}
 static dim3 bn_grid(int Npix, int C) {
   const int V = C / 8, vv = V >= kBnT ? kBnT : V, ppi = kBnT / vv;
   const int gy = V >= kBnT ? V / kBnT : 1;
-  // g_bn_stat_blocks blocks in total, at least 8 pixel rows per thread
-  const int gx = std::max(1, std::min(cdiv(Npix, ppi * 8), std::max(1, g_bn_stat_blocks / gy)));
+  // ~1024 blocks in total (one partial row each; 2,048 - 8,192 measured slower on a 411 MB
+  // tensor, profiles/r4_k/bench_bn.log), at least 8 pixel rows per thread
+  const int gx = std::max(1, std::min(cdiv(Npix, ppi * 8), std::max(1, 1024 / gy)));
   return dim3(gx, gy);
 }
 
@@ -3035,12 +3022,7 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
   MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
   const dim3 agrid(stream_blocks((int64_t)Npix * V));
-  if (g_bn_pipe)
-    MX_LAUNCH((bn_nhwc_apply_k<2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
-  else if (g_bn_unroll == 4)
-    MX_LAUNCH((bn_nhwc_apply_k<4, false>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
-  else
-    MX_LAUNCH((bn_nhwc_apply_k<2, false>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
+  MX_LAUNCH((bn_nhwc_apply_k<2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
 }
 
 void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma, const float* mean,
@@ -3082,16 +3064,8 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
   MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
   const dim3 agrid(stream_blocks((int64_t)Npix * V));
-  if (g_bn_pipe) {
-    if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
-    else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
-  } else if (g_bn_unroll == 4) {
-    if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 4, false>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
-    else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 4, false>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
-  } else {
-    if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 2, false>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
-    else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 2, false>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
-  }
+  if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
+  else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
 }
 
 void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, int k,

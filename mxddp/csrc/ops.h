@@ -192,13 +192,10 @@ int nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int
                   float* bnpart = nullptr, const float* bnshift = nullptr);
 // large-layer LDS-DMA conv kernel: 0 = off, 1 = large layers (default), 2 = always
 void nhwc_conv_set_glds(int mode);
-// the 256 x 256-tile LDS-DMA kernel: 0 = off (default), 1 = layers with >= 256 tiles, 2 = wherever Ng % 256 == 0
+// the 256 x 256-tile LDS-DMA kernel: 0 = off, 1 = layers with >= 256 tiles and >= 4 k-tiles (default), 2 = wherever Ng % 256 == 0
 void nhwc_conv_set_glds256(int mode);
 void nhwc_conv_set_glds_short(int mode);  // two-stage 128-pixel LDS-DMA variant for short reductions
-void nhwc_bn_set_unroll(int u);
-void nhwc_bn_set_pipe(int on);
-void nhwc_bn_set_grid_cap(int cap);  // most blocks of the NHWC BN apply kernels
-void nhwc_bn_set_stat_blocks(int n);  // blocks of the NHWC BN statistics pass  // software-pipelined NHWC BN apply kernels (default on)  // NHWC BN apply kernels: vectors in flight per thread (2 or 4)
+void nhwc_bn_set_grid_cap(int cap);  // most blocks of the NHWC BN apply kernels (A/B; 2048 = round-3 grids)
 // split-K scratch of nhwc_conv_dgrad (floats; 0 = none needed)
 size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
                                       int P, int Q);

@@ -87,26 +87,14 @@ def main():
         us = timed(fn, iters)
         rows.append((name, us, byts / us / 1e6))
         print(f"{name:42s} {us:8.1f} us  {byts / us / 1e6:6.2f} TB/s (nominal bytes)", flush=True)
-    # apply-kernel grid cap and software pipelining
-    for pipe in (0, 1):
-        for cap in (1024, 2048, 4096, 8192, 32768):
-            Cn.nhwc_bn_set_pipe(pipe)
-            Cn.nhwc_bn_set_grid_cap(cap)
-            f_us = timed(fwd(True, None, False), iters)
-            b_us = timed(bwd(True, True, False, False), iters)
-            print(f"pipe {pipe} grid cap {cap:6d}: fwd apply ReLU {f_us:7.1f} us ({2 * nbytes / f_us / 1e6:5.2f} TB/s), "
-                  f"bwd {b_us:7.1f} us ({5 * nbytes / b_us / 1e6:5.2f} TB/s)", flush=True)
-    Cn.nhwc_bn_set_pipe(1)
-    Cn.nhwc_bn_set_grid_cap(65536)
-    # statistics-pass blocks (one partial row each)
-    for nb in (1024, 2048, 4096, 8192):
-        Cn.nhwc_bn_set_stat_blocks(nb)
-        s_us = timed(fwd(True, None, False, pre=False), iters)
+    # apply-kernel grid cap (2048 = the round-3 grids; 0 = the default, tensor-sized)
+    for cap in (2048, 8192, 32768):
+        Cn.nhwc_bn_set_grid_cap(cap)
+        f_us = timed(fwd(True, None, False), iters)
         b_us = timed(bwd(True, True, False, False), iters)
-        print(f"stat blocks {nb:5d}: fwd with statistics {s_us:7.1f} us ({3 * nbytes / s_us / 1e6:5.2f} TB/s), "
+        print(f"grid cap {cap:6d}: fwd apply ReLU {f_us:7.1f} us ({2 * nbytes / f_us / 1e6:5.2f} TB/s), "
               f"bwd {b_us:7.1f} us ({5 * nbytes / b_us / 1e6:5.2f} TB/s)", flush=True)
-    Cn.nhwc_bn_set_stat_blocks(1024)
-
+    Cn.nhwc_bn_set_grid_cap(32768)
 
 if __name__ == "__main__":
     main()

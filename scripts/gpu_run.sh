@@ -18,7 +18,6 @@
 #   keras / keras_rep / keras_ws2 / prof_keras / pmc_keras   Keras CNN fused engine
 #   mlp / mlp_rep / prof_mlp / pmc_mlp                       Chainer MLP
 #   rn32 / rn256 / prof_rn / pmc_rn / rn_stock / rn_layers    ResNet-50 bf16 (rn_layers: per conv shape)
-#   ab_bnu       ResNet-50 at batch 256, BN apply kernels with 2 vs 4 vectors in flight per thread
 #   pyr / prof_pyr / pyr_stock                               PyramidNet-110
 #   ws2 / ws4 / ws8 (MNIST), keras_ws8, pyr_ws8, rn_ws8      shared-GPU DDP rehearsals
 #   coll         MNIST with RCCL collectives forced at one rank
@@ -93,11 +92,6 @@ for step in "$@"; do
     rn32) run rn32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 ;;
     rn256) run rn256 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 ;;
     rn256_t256) run rn256_t256 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --conv-tile256 1 ;;
-    ab_bnu)  # BN apply unroll 2 vs 4 at batch 256, interleaved
-      for r in 1 2; do
-        run "ab_bnu2_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --bn-unroll 2 &&
-        run "ab_bnu4_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --bn-unroll 4 || exit 1
-      done ;;
     ab_short)  # ResNet-50 batch 256 / 32: two-stage 128-pixel LDS-DMA variant off vs on, interleaved
       for r in 1 2; do
         run "ab_short0_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --glds-short 0 &&
@@ -105,11 +99,6 @@ for step in "$@"; do
       done
       run ab_short0_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --glds-short 0 &&
       run ab_short1_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --glds-short 1 || exit 1 ;;
-    ab_bnpipe)  # ResNet-50 batch 256: software-pipelined BN apply kernels off vs on, interleaved
-      for r in 1 2; do
-        run "ab_bnpipe0_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --bn-pipe 0 &&
-        run "ab_bnpipe1_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --bn-pipe 1 || exit 1
-      done ;;
     ab_bngrid)  # ResNet-50 batch 256 / 32: BN apply grids of round 3 (2,048 blocks) vs size-aware
       for r in 1 2; do
         run "ab_bngrid2k_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --bn-grid-cap 2048 &&
@@ -117,7 +106,6 @@ for step in "$@"; do
       done
       run ab_bngrid2k_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --bn-grid-cap 2048 &&
       run ab_bngrid_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 || exit 1 ;;
-    prof_rn_pipe0) prof prof_rn_pipe0 3 --model resnet50 --dtype bf16 --batch 256 --steps 3 --warmup 2 --min-warmup-ms 0 --bn-pipe 0 ;;
     ab_t256)  # ResNet-50: 256 x 256 tile on the long-reduction layers off vs on, interleaved
       for r in 1 2; do
         run "ab_t256_0_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --conv-tile256 0 &&
