@@ -2023,38 +2023,42 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
 
 template <bool BWD>
 __global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
-  // block = 8 channels x 128 row groups: each thread sums <= gx / 128 (<= 8) partial rows with
-  // every load issued up front (one memory round trip, not a dependent chain), the 128 group
-  // sums are tree-combined in LDS in a fixed order (deterministic).  The per-channel inputs of
-  // the finalize (gamma, beta, running stats, x[0][c]) are loaded by the 8 owner threads before
-  // the reduction so their latency overlaps it.
-  constexpr int RG = 128, MAXR = 16;
+  // block = 8 channels as 4 pairs (one 16-byte (s1, s2, s1', s2') load per thread per row) x 256
+  // row groups: each thread sums <= 16 rows per pass of 4,096 with every load issued up front (one
+  // memory round trip per pass; the 128-pixel conv tiles give a batch-256 56 x 56 layer 6,272
+  // rows: 2 passes, 4 with the former 8-byte / 128-group layout), the 256 group sums are
+  // tree-combined in LDS in a fixed order (deterministic).  The per-channel inputs of the
+  // finalize (gamma, beta, running stats, x[0][c]) are loaded by 8 owner threads before the
+  // reduction so their latency overlaps it.
+  constexpr int RG = 256, MAXR = 16;
   __shared__ float red[2][RG][8];
-  const int cl = threadIdx.x & 7, rg = threadIdx.x >> 3, c = blockIdx.x * 8 + cl;
-  const bool cok = c < a.C;
+  const int cp = threadIdx.x & 3, rg = threadIdx.x >> 2, c2 = blockIdx.x * 8 + 2 * cp;
+  const bool pok = c2 + 1 < a.C;  // C % 8 == 0 (checked on the host): always true
   const size_t pitch = 2 * (size_t)a.C;
-  float s1 = 0.f, s2 = 0.f;
-  // passes of RG * MAXR = 2048 rows, every (s1, s2) pair of a pass one 8-byte load issued before
-  // the first is summed (one memory round trip per pass; two passes cover the conv-epilogue
-  // partials of a whole batch-256 ResNet-50 layer -- one row per 256-pixel tile)
-  for (int base = 0; cok && base < a.gx; base += RG * MAXR) {
-    float2 t[MAXR];
+  float s1a = 0.f, s2a = 0.f, s1b = 0.f, s2b = 0.f;
+  for (int base = 0; pok && base < a.gx; base += RG * MAXR) {
+    float4 t[MAXR];
 #pragma unroll
     for (int u = 0; u < MAXR; ++u) {
       const int b = base + rg + RG * u;
       const bool ok = b < a.gx;
-      const float2 v = *reinterpret_cast<const float2*>(a.part + (size_t)(ok ? b : 0) * pitch + 2 * c);
-      t[u] = ok ? v : make_float2(0.f, 0.f);
+      const float4 v = *reinterpret_cast<const float4*>(a.part + (size_t)(ok ? b : 0) * pitch + 2 * c2);
+      t[u] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int u = 0; u < MAXR; ++u) {
-      s1 += t[u].x;
-      s2 += t[u].y;
+      s1a += t[u].x;
+      s2a += t[u].y;
+      s1b += t[u].z;
+      s2b += t[u].w;
     }
   }
-  // per-channel inputs of the finalize, fetched while the reduction runs
+  // per-channel inputs of the finalize (threads 0..7 own channels blockIdx.x * 8 + tid), fetched
+  // while the reduction runs
+  const int cl = threadIdx.x, c = blockIdx.x * 8 + cl;
+  const bool own = cl < 8 && c < a.C;
   float gm = 1.f, bt = 0.f, rm = 0.f, rv = 0.f, K0 = 0.f, mu = 0.f, inv = 0.f, dg0 = 0.f, db0 = 0.f;
-  if (rg == 0 && cok) {
+  if (own) {
     gm = a.gamma ? a.gamma[c] : 1.f;
     if (!BWD) {
       bt = a.beta ? a.beta[c] : 0.f;
@@ -2070,20 +2074,23 @@ __global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
       }
     }
   }
-  red[0][rg][cl] = s1;
-  red[1][rg][cl] = s2;
+  red[0][rg][2 * cp] = s1a;
+  red[0][rg][2 * cp + 1] = s1b;
+  red[1][rg][2 * cp] = s2a;
+  red[1][rg][2 * cp + 1] = s2b;
 #pragma unroll
   for (int h = RG / 2; h > 0; h >>= 1) {
     __syncthreads();
     if (rg < h) {
-      red[0][rg][cl] += red[0][rg + h][cl];
-      red[1][rg][cl] += red[1][rg + h][cl];
+      red[0][rg][2 * cp] += red[0][rg + h][2 * cp];
+      red[0][rg][2 * cp + 1] += red[0][rg + h][2 * cp + 1];
+      red[1][rg][2 * cp] += red[1][rg + h][2 * cp];
+      red[1][rg][2 * cp + 1] += red[1][rg + h][2 * cp + 1];
     }
   }
   __syncthreads();
-  if (rg != 0 || !cok) return;
-  s1 = red[0][0][cl];
-  s2 = red[1][0][cl];
+  if (!own) return;
+  const float s1 = red[0][0][cl], s2 = red[1][0][cl];
   const float cnt = (float)a.Npix;
   if (!BWD) {
     if (a.num_batches && c == 0) *a.num_batches += 1;
