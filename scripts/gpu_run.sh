@@ -67,6 +67,11 @@ for step in "$@"; do
     prof_mnist) prof prof_mnist 200 --steps 200 --warmup 20 --min-warmup-ms 0 ;;
     pmc_mnist) pmc pmc_mnist --steps 20 --warmup 2 --no-graph --min-warmup-ms 0 ;;
     phase_mnist) run phase_mnist 300 python bench.py --phase-profile 30 ;;
+    ab_spg)  # driver-length MNIST: 32 steps per graph (16 + 4 launches) vs one 20-step graph, interleaved
+      for r in 1 2 3; do
+        run "ab_spg32_$r" 300 python bench.py --steps 20 --warmup 5 &&
+        run "ab_spg20_$r" 300 python bench.py --steps 20 --warmup 5 --steps-per-graph 20 || exit 1
+      done ;;
     ab_wt)  # write-through store masks A/B (0 none, 6 F2 + F6W, 7 F5 + F2 + F6W), interleaved long runs
       for r in 1 2; do
         run "ab_wt0_$r" 300 python bench.py --steps 2000 --warmup 100 --wt-stores 0 &&
