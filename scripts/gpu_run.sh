@@ -123,6 +123,7 @@ for step in "$@"; do
     rn_layers) run rn_layers 300 python scripts/bench_nhwc_layers.py 256 5 ;;
     rn_layers_t256) run rn_layers_t256 300 python scripts/bench_nhwc_layers.py 256 5 1 ;;
     rn_stock) run rn_stock 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --impl torch --channels-last ;;
+    prof_rn32) prof prof_rn32 10 --model resnet50 --dtype bf16 --batch 32 --steps 10 --warmup 2 --min-warmup-ms 0 ;;
     prof_rn) prof prof_rn 3 --model resnet50 --dtype bf16 --batch 256 --steps 3 --warmup 2 --min-warmup-ms 0 ;;
     pmc_rn) pmc pmc_rn --model resnet50 --dtype bf16 --batch 256 --steps 1 --warmup 1 --no-graph --min-warmup-ms 0 ;;
     pyr) run pyr 300 python bench.py --model pyramidnet110 --steps 20 --warmup 3 ;;
