@@ -62,6 +62,11 @@ for step in "$@"; do
     t_*) run "$step" 900 python -u -m pytest "tests/test_gpu_${step#t_}.py" -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     driver) run driver 300 python bench.py --steps 20 --warmup 5 ;;
+    driver_all)  # every fused model at the driver's length, and the 2-rank rehearsal
+      run driver_mnist 300 python bench.py --steps 20 --warmup 5 &&
+      run driver_keras 300 python bench.py --model keras_cnn --steps 20 --warmup 5 &&
+      run driver_mlp 300 python bench.py --model mlp --steps 20 --warmup 5 || exit 1
+      ws driver_ws2 2 --steps 20 --warmup 5 ;;
     long) run long 300 python bench.py --steps 2000 --warmup 100 ;;
     default) run default 300 python bench.py ;;
     prof_mnist) prof prof_mnist 200 --steps 200 --warmup 20 --min-warmup-ms 0 ;;
