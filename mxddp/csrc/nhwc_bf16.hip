@@ -1693,20 +1693,29 @@ __global__ __launch_bounds__(256) void wgrad_nhwc_reduce_k(const float* __restri
   const int q = threadIdx.x % QB, g = threadIdx.x / QB;
   const int i = blockIdx.x * QB + q;
   const float4* p4 = reinterpret_cast<const float4*>(part);
-  float4 t0 = make_float4(0.f, 0.f, 0.f, 0.f), t1 = t0;
-  if (i < plane4) {
-    int sp = g;
-    for (; sp + G < splits; sp += 2 * G) {
-      const float4 u = p4[(size_t)sp * plane4 + i], v = p4[(size_t)(sp + G) * plane4 + i];
-      t0.x += u.x; t0.y += u.y; t0.z += u.z; t0.w += u.w;
-      t1.x += v.x; t1.y += v.y; t1.z += v.z; t1.w += v.w;
-    }
-    if (sp < splits) {
-      const float4 u = p4[(size_t)sp * plane4 + i];
-      t0.x += u.x; t0.y += u.y; t0.z += u.z; t0.w += u.w;
+  // 8 partial planes per round with every load issued before the first add, at clamped indices
+  // (a plane past `splits` or a lane past the plane loads a valid element and discards it): the
+  // former loop, behind a per-lane range check, waited for each pair of loads in turn -- at batch
+  // 32 (~200 splits) that was ~6 dependent round trips per launch
+  const int ic = min(i, plane4 - 1);
+  float4 acc[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int sp0 = g; sp0 < splits; sp0 += 8 * G) {
+    float4 u[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) u[k] = p4[(size_t)min(sp0 + k * G, splits - 1) * plane4 + ic];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const bool in = sp0 + k * G < splits;
+      acc[k & 3].x += in ? u[k].x : 0.f;
+      acc[k & 3].y += in ? u[k].y : 0.f;
+      acc[k & 3].z += in ? u[k].z : 0.f;
+      acc[k & 3].w += in ? u[k].w : 0.f;
     }
   }
-  red[threadIdx.x] = make_float4(t0.x + t1.x, t0.y + t1.y, t0.z + t1.z, t0.w + t1.w);
+  red[threadIdx.x] = make_float4((acc[0].x + acc[1].x) + (acc[2].x + acc[3].x), (acc[0].y + acc[1].y) + (acc[2].y + acc[3].y),
+                                 (acc[0].z + acc[1].z) + (acc[2].z + acc[3].z), (acc[0].w + acc[1].w) + (acc[2].w + acc[3].w));
   __syncthreads();
   if (g != 0 || i >= plane4) return;
   float v[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1717,11 +1726,16 @@ __global__ __launch_bounds__(256) void wgrad_nhwc_reduce_k(const float* __restri
   const int e = 4 * i, k = e / Ng, n = e - k * Ng;
   const int rs = n / Ca, c = n - rs * Ca;
   float* d = dw + ((size_t)k * Cin + c) * RS + rs;
+  // the 4 old values (accumulate) requested together at clamped channels, then the masked stores
+  // (the per-element `break` made each read-add-write wait for its own load)
+  float old[4] = {0.f, 0.f, 0.f, 0.f};
+  if (accumulate) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (c + j >= Cin) break;
-    d[(size_t)j * RS] = accumulate ? d[(size_t)j * RS] + v[j] : v[j];
+    for (int j = 0; j < 4; ++j) old[j] = d[(size_t)min(j, Cin - 1 - c) * RS];
   }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (c + j < Cin) d[(size_t)j * RS] = old[j] + v[j];
 }
 
 // ------------------------------------------------------------------------------------------
