@@ -2041,11 +2041,11 @@ __global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
   // row groups: each thread sums <= 16 rows per pass of 4,096 with every load issued up front (one
   // memory round trip per pass; the 128-pixel conv tiles give a batch-256 56 x 56 layer 6,272
   // rows: 2 passes, 4 with the former 8-byte / 128-group layout), the 256 group sums are
-  // tree-combined in LDS in a fixed order (deterministic).  The per-channel inputs of the
+  // combined in a fixed order (deterministic): lane shuffles, then one LDS step.  The per-channel inputs of the
   // finalize (gamma, beta, running stats, x[0][c]) are loaded by 8 owner threads before the
   // reduction so their latency overlaps it.
-  constexpr int RG = 256, MAXR = 16;
-  __shared__ float red[2][RG][8];
+  constexpr int RG = 256, MAXR = 16, NW = 1024 / 64;
+  __shared__ float red[NW][4][4];
   const int cp = threadIdx.x & 3, rg = threadIdx.x >> 2, c2 = blockIdx.x * 8 + 2 * cp;
   const bool pok = c2 + 1 < a.C;  // C % 8 == 0 (checked on the host): always true
   const size_t pitch = 2 * (size_t)a.C;
@@ -2088,23 +2088,30 @@ __global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
       }
     }
   }
-  red[0][rg][2 * cp] = s1a;
-  red[0][rg][2 * cp + 1] = s1b;
-  red[1][rg][2 * cp] = s2a;
-  red[1][rg][2 * cp + 1] = s2b;
+  // the 16 row groups of a wave are combined with lane shuffles (xor 4..32 keeps cp), then the 16
+  // wave sums through LDS behind ONE barrier (the former 8-level LDS tree paid 9 barriers)
 #pragma unroll
-  for (int h = RG / 2; h > 0; h >>= 1) {
-    __syncthreads();
-    if (rg < h) {
-      red[0][rg][2 * cp] += red[0][rg + h][2 * cp];
-      red[0][rg][2 * cp + 1] += red[0][rg + h][2 * cp + 1];
-      red[1][rg][2 * cp] += red[1][rg + h][2 * cp];
-      red[1][rg][2 * cp + 1] += red[1][rg + h][2 * cp + 1];
-    }
+  for (int m = 4; m < 64; m <<= 1) {
+    s1a += __shfl_xor(s1a, m);
+    s2a += __shfl_xor(s2a, m);
+    s1b += __shfl_xor(s1b, m);
+    s2b += __shfl_xor(s2b, m);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane < 4) {
+    red[wv][lane][0] = s1a;
+    red[wv][lane][1] = s2a;
+    red[wv][lane][2] = s1b;
+    red[wv][lane][3] = s2b;
   }
   __syncthreads();
   if (!own) return;
-  const float s1 = red[0][0][cl], s2 = red[1][0][cl];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {  // fixed order: deterministic
+    s1 += red[w][cl >> 1][2 * (cl & 1)];
+    s2 += red[w][cl >> 1][2 * (cl & 1) + 1];
+  }
   const float cnt = (float)a.Npix;
   if (!BWD) {
     if (a.num_batches && c == 0) *a.num_batches += 1;

@@ -182,7 +182,8 @@ class _Conv(torch.autograd.Function):
     def forward(ctx, x, w, stride, pad, packed=None, join=None, deposit=None, bnstat=None):
         Cn = native()
         # the BN that produced x (its backward statistics can ride this conv's data gradient)
-        ctx.bnlink = _bn_link_of(x) if (_BN_STATS_IN_DGRAD and ctx.needs_input_grad[0]) else None
+        dstats = _BN_STATS_IN_DGRAD or x.numel() <= _BN_DGRAD_STATS_MAX
+        ctx.bnlink = _bn_link_of(x) if (dstats and ctx.needs_input_grad[0]) else None
         N, H, W, Cp = x.shape
         K, C, R, S = w.shape
         sh, sw = stride
@@ -297,6 +298,9 @@ _BN_STATS_IN_CONV = os.environ.get("MXDDP_BN_STATS_IN_CONV", "1") == "1"
 # re-read and the reduction of every tile are fully exposed) against the 1.6 ms of separate
 # statistics passes it removes.  Tests switch it on to keep the path exact.
 _BN_STATS_IN_DGRAD = False
+# ... except on tensors of at most this many elements (MXDDP_BN_DGRAD_STATS_MAX; 0 = never), where
+# the separate statistics pass is mostly its fixed per-kernel cost
+_BN_DGRAD_STATS_MAX = int(os.environ.get("MXDDP_BN_DGRAD_STATS_MAX", "0"))
 _LAZY_JOIN = True  # identity-shortcut gradient masked in the joining conv's epilogue (tests flip it)
 # how many BN backward passes took their statistics from a conv epilogue / ran their own pass
 BN_BWD_STATS = {"epilogue": 0, "pass": 0}
