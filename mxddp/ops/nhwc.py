@@ -299,8 +299,10 @@ _BN_STATS_IN_CONV = os.environ.get("MXDDP_BN_STATS_IN_CONV", "1") == "1"
 # statistics passes it removes.  Tests switch it on to keep the path exact.
 _BN_STATS_IN_DGRAD = False
 # ... except on tensors of at most this many elements (MXDDP_BN_DGRAD_STATS_MAX; 0 = never), where
-# the separate statistics pass is mostly its fixed per-kernel cost
-_BN_DGRAD_STATS_MAX = int(os.environ.get("MXDDP_BN_DGRAD_STATS_MAX", "0"))
+# the separate statistics pass is mostly its fixed per-kernel cost (~5 us a launch at batch 32).
+# ResNet-50 (profiles/r4_r/, two runs each): batch 32 5,332 img/s at 0, 5,352 at 4M (layers 2-4),
+# 5,266 at every size; batch 256 unchanged (its smallest BN tensor has 6.4M elements)
+_BN_DGRAD_STATS_MAX = int(os.environ.get("MXDDP_BN_DGRAD_STATS_MAX", "4000000"))
 _LAZY_JOIN = True  # identity-shortcut gradient masked in the joining conv's epilogue (tests flip it)
 # how many BN backward passes took their statistics from a conv epilogue / ran their own pass
 BN_BWD_STATS = {"epilogue": 0, "pass": 0}

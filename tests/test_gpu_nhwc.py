@@ -12,6 +12,8 @@ from mxddp import ops  # noqa: E402
 from mxddp.ops import nhwc  # noqa: E402
 
 
+_DSTATS_MAX = nhwc._BN_DGRAD_STATS_MAX
+
 def _rel(a, b):
     return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-6)).item()
 
@@ -327,6 +329,7 @@ def test_bn_backward_statistics_from_dgrad_epilogue(cuda, glds, stride, relu):
         gamma, beta = torch.rand(Cin) + 0.5, torch.randn(Cin) * 0.2  # the same BN in both runs
         for fused in (False, True):
             nhwc._BN_STATS_IN_DGRAD = fused
+            nhwc._BN_DGRAD_STATS_MAX = 0  # the size rule would switch the unfused run on too
             bn = nn.BatchNorm2d(Cin).to(cuda)
             with torch.no_grad():
                 bn.weight.copy_(gamma)
@@ -343,6 +346,7 @@ def test_bn_backward_statistics_from_dgrad_epilogue(cuda, glds, stride, relu):
             outs.append((xg.grad.float().cpu(), wg.grad.cpu(), bn.weight.grad.cpu(), bn.bias.grad.cpu()))
     finally:
         nhwc._BN_STATS_IN_DGRAD = False
+        nhwc._BN_DGRAD_STATS_MAX = _DSTATS_MAX
         C.nhwc_conv_set_glds256(0)
         C.nhwc_conv_set_glds(1)
     assert used == [0, 1], used  # the fused run really took the epilogue's statistics
@@ -364,6 +368,7 @@ def test_bn_backward_statistics_residual_join(cuda):
     try:
         for fused in (False, True):
             nhwc._BN_STATS_IN_DGRAD = fused
+            nhwc._BN_DGRAD_STATS_MAX = 0  # the size rule would switch the unfused run on too
             _restore(state)
             for blk in blocks:
                 blk.zero_grad()
@@ -378,6 +383,7 @@ def test_bn_backward_statistics_residual_join(cuda):
             outs.append((xg.grad.float().cpu(), *grads))
     finally:
         nhwc._BN_STATS_IN_DGRAD = False
+        nhwc._BN_DGRAD_STATS_MAX = _DSTATS_MAX
     # bn2 of both blocks (conv3's data gradient) and block 0's bn3 (block 1's conv1, joined); bn1
     # feeds the 3x3 / 64-channel band kernel, whose epilogue carries no statistics
     assert used[0] == 0 and used[1] >= 3, used
@@ -403,6 +409,7 @@ def test_lazy_identity_join_equals_materialised(cuda):
     outs = []
     try:
         nhwc._BN_STATS_IN_DGRAD = False  # the join alone (statistics are covered by their own tests)
+        nhwc._BN_DGRAD_STATS_MAX = 0
         for lazy in (False, True):
             nhwc._LAZY_JOIN = lazy
             _restore(state)  # same running-mean shift of the forward statistics in both runs
@@ -419,6 +426,7 @@ def test_lazy_identity_join_equals_materialised(cuda):
     finally:
         nhwc._LAZY_JOIN = True
         nhwc._BN_STATS_IN_DGRAD = False
+        nhwc._BN_DGRAD_STATS_MAX = _DSTATS_MAX
     # the same bf16 values are added in the same epilogue: equal up to run-to-run bf16 flips
     for a, b in zip(*outs):
         assert _nrel(b, a) < 1e-2
