@@ -1251,16 +1251,37 @@ static bool stem_eligible(const ConvNArgs& a) {
          a.OW == (a.IW + 6 - 7) / 2 + 1;
 }
 
-// split-K epilogue: out (bf16) = sum over splits of the fp32 partials (fixed order)
-__global__ void conv_nhwc_splitk_reduce_k(const float* __restrict__ part, bf16* __restrict__ out, int64_t n4,
-                                          int splits, const bf16* __restrict__ addend,
-                                          const uint8_t* __restrict__ amask) {
+// split-K epilogue: out (bf16) = sum over splits of the fp32 partials (fixed order).  8 partial
+// planes per round with every load issued before the first add, at clamped indices (one load per
+// iteration of a runtime-length loop waited for each in turn).
+// STATS (forward, the output feeds a training BatchNorm): the BN's partial sums of (y - shift[c])
+// and its square over the STORED bf16 values, one row of bnpart (layout of bn_nhwc_partial_k) per
+// `bpr` blocks.  The host guarantees a grid stride that is a multiple of Ng / 4 (each thread's
+// channel quad is fixed) and blocks that start on a row boundary (splitk_bn_ok).
+template <bool STATS>
+__global__ __launch_bounds__(256) void conv_nhwc_splitk_reduce_k(const float* __restrict__ part, bf16* __restrict__ out,
+                                                                 int64_t n4, int splits, const bf16* __restrict__ addend,
+                                                                 const uint8_t* __restrict__ amask, float* __restrict__ bnpart,
+                                                                 const float* __restrict__ bnshift, int Ng) {
   const float4* p4 = reinterpret_cast<const float4*>(part);
+  const int q4 = Ng >> 2;
+  const int cq = STATS ? (int)((blockIdx.x * 256ll + threadIdx.x) % q4) : 0;
+  float K[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (STATS && bnshift) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) K[j] = bnshift[4 * cq + j];
+  }
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    float4 s = p4[i];
-    for (int sp = 1; sp < splits; ++sp) {
-      const float4 v = p4[sp * n4 + i];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int sp0 = 0; sp0 < splits; sp0 += 8) {
+      float4 u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = p4[(int64_t)min(sp0 + k, splits - 1) * n4 + i];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {  // in split order (fixed)
+        const bool in = sp0 + k < splits;
+        s.x += in ? u[k].x : 0.f; s.y += in ? u[k].y : 0.f; s.z += in ? u[k].z : 0.f; s.w += in ? u[k].w : 0.f;
+      }
     }
     if (addend) {
       uint2 d = reinterpret_cast<const uint2*>(addend)[i];
@@ -1271,7 +1292,39 @@ __global__ void conv_nhwc_splitk_reduce_k(const float* __restrict__ part, bf16* 
       }
       s.x += bf2f(d.x & 0xffffu); s.y += bf2f(d.x >> 16); s.z += bf2f(d.y & 0xffffu); s.w += bf2f(d.y >> 16);
     }
-    reinterpret_cast<uint2*>(out)[i] = make_uint2(pack2(s.x, s.y), pack2(s.z, s.w));
+    const uint2 o = make_uint2(pack2(s.x, s.y), pack2(s.z, s.w));
+    reinterpret_cast<uint2*>(out)[i] = o;
+    if (STATS) {
+      const float y[4] = {bf2f(o.x & 0xffffu), bf2f(o.x >> 16), bf2f(o.y & 0xffffu), bf2f(o.y >> 16)};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = y[j] - K[j];
+        s1[j] += d;
+        s2[j] = fmaf(d, d, s2[j]);
+      }
+    }
+  }
+  if constexpr (STATS) {
+    // the threads of one channel quad (256 / q4 of them when q4 < 256) summed in a fixed order
+    __shared__ float red[8][256];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[j][threadIdx.x] = s1[j];
+      red[4 + j][threadIdx.x] = s2[j];
+    }
+    __syncthreads();
+    const int qb = q4 < 256 ? q4 : 256, bpr = q4 < 256 ? 1 : q4 / 256;
+    if ((int)threadIdx.x >= qb) return;
+    for (int g = 1; g < 256 / qb; ++g) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s1[j] += red[j][threadIdx.x + g * qb];
+        s2[j] += red[4 + j][threadIdx.x + g * qb];
+      }
+    }
+    float4* dst = reinterpret_cast<float4*>(bnpart + (size_t)(blockIdx.x / bpr) * 2 * Ng + 8 * cq);
+    dst[0] = make_float4(s1[0], s2[0], s1[1], s2[1]);
+    dst[1] = make_float4(s1[2], s2[2], s1[3], s2[3]);
   }
 }
 
@@ -2690,6 +2743,30 @@ static bool conv_c3_mode() {
   return on;
 }
 
+// forward BN statistics in the split-K reduce: one row per `bpr` blocks (>= 8 pixels per row,
+// <= 2,048 blocks); the channel quads must tile the grid stride (ResNet's power-of-two widths)
+static int splitk_bn_bpr(int Ng) { return std::max(1, Ng / 1024); }
+static int splitk_bn_rows(int M, int Ng) { return std::min(cdiv(M, 8), 2048 / splitk_bn_bpr(Ng)); }
+static bool splitk_bn_ok(int Ng) {
+  const int q4 = Ng / 4;
+  return Ng % 4 == 0 && q4 > 0 && (q4 <= 256 ? 256 % q4 == 0 : q4 % 256 == 0);
+}
+
+// sums the split-K partials into a.out; fpart (forward only): the consuming BN's partial rows are
+// written there too.  Returns their count (0: none)
+static int launch_splitk_reduce(const ConvNArgs& a, float* scratch, int splits, float* fpart, hipStream_t st) {
+  const int64_t n4 = (int64_t)a.M * a.Ng / 4;
+  if (fpart && !a.dgrad && !a.addend && splitk_bn_ok(a.Ng)) {
+    const int rows = splitk_bn_rows(a.M, a.Ng);
+    MX_LAUNCH(conv_nhwc_splitk_reduce_k<true>, dim3(rows * splitk_bn_bpr(a.Ng)), dim3(256), 0, st, scratch, a.out, n4,
+              splits, a.addend, a.amask, fpart, a.bnshift, a.Ng);
+    return rows;
+  }
+  MX_LAUNCH(conv_nhwc_splitk_reduce_k<false>, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, splits,
+            a.addend, a.amask, nullptr, nullptr, a.Ng);
+  return 0;
+}
+
 // returns the number of BN partial rows the epilogue wrote to a.bnpart (0: none, the BN runs its
 // own statistics pass)
 static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
@@ -2743,6 +2820,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     // epilogue BN statistics (forward: bnpart / bnshift; data gradient: bx, see ConvNArgs) need
     // the whole reduction in one block: no split-K
     const bool bst = a.dgrad && a.bx && a.bnpart && gp.splits == 1 && gx <= 16384;
+    float* const fpart = (!a.dgrad && gp.splits > 1) ? a.bnpart : nullptr;  // statistics in the reduce
     if (!bst) a.bx = nullptr;
     if (!(a.bnpart && (bst || (!a.dgrad && gp.splits == 1)) && gx <= 16384)) a.bnpart = nullptr;
     const dim3 grid(cdiv(a.Ng, gp.tm) * gx, gp.splits);
@@ -2761,11 +2839,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
       if (gp.tm == 128) MX_LAUNCH((conv_nhwc_glds_kernel<128>), grid, dim3(512), 0, st, a);
       else MX_LAUNCH((conv_nhwc_glds_kernel<64>), grid, dim3(512), 0, st, a);
     }
-    if (gp.splits > 1) {
-      const int64_t n4 = (int64_t)a.M * a.Ng / 4;
-      MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, gp.splits,
-                a.addend, a.amask);
-    }
+    if (gp.splits > 1) return launch_splitk_reduce(a, scratch, gp.splits, fpart, st);
     return a.bnpart ? gx : 0;
   }
   a.par = cs.par ? 1 : 0;
@@ -2784,6 +2858,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   // backward BN statistics in the epilogue: one partial row per (parity class, pixel tile)
   const int Mc = cs.par ? a.M / 4 : a.M, brows = (cs.par ? 4 : 1) * cdiv(Mc, p.tn);
   const bool bst = a.dgrad && a.bx && a.bnpart && p.splits == 1 && brows <= 16384;
+  float* const fpart = (!a.dgrad && p.splits > 1) ? a.bnpart : nullptr;  // statistics in the reduce
   if (!bst) {
     a.bx = nullptr;
     a.bnpart = nullptr;
@@ -2799,11 +2874,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     if (wide) MX_LAUNCH((conv_nhwc_kernel<64, 64, true>), grid, dim3(256), 0, st, a);
     else MX_LAUNCH((conv_nhwc_kernel<64, 64, false>), grid, dim3(256), 0, st, a);
   }
-  if (p.splits > 1) {
-    const int64_t n4 = (int64_t)a.M * a.Ng / 4;
-    MX_LAUNCH(conv_nhwc_splitk_reduce_k, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, p.splits,
-              a.addend, a.amask);
-  }
+  if (p.splits > 1) return launch_splitk_reduce(a, scratch, p.splits, fpart, st);
   return bst ? brows : 0;
 }
 
@@ -2836,8 +2907,8 @@ int nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int
 
 int nhwc_conv_bn_rows(int N, int H, int W, int Cp, int K, int R, int S, int sh, int sw, int ph, int pw, int P, int Q) {
   // upper bound: one per 128-pixel tile (the LDS-DMA kernel's two-stage variant; 256-pixel tiles
-  // elsewhere -- the launch returns the rows it wrote)
-  int rows = cdiv(N * P * Q, 128);
+  // elsewhere -- the launch returns the rows it wrote), or the split-K reduce's rows
+  int rows = std::max(cdiv(N * P * Q, 128), splitk_bn_rows(N * P * Q, K));  // or the split-K reduce's
   if (Cp == 64 && K == 64 && R == 3 && S == 3 && sh == 1 && sw == 1 && ph == 1 && pw == 1 && P == H && Q == W &&
       W <= 64) {  // the band kernel writes one row per band
     const int rt = c3_band_rows(P, Q);

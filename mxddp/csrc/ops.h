@@ -184,9 +184,10 @@ void nhwc_repack_many(const int64_t* desc, int n, int total_blocks, hipStream_t 
 // scratch (or null = no split-K): nhwc_conv_scratch_floats(M = output pixels, Ng = output
 // channels, Kg = R*S*input channels) floats of fp32 split-K partials
 size_t nhwc_conv_scratch_floats(int M, int Ng, int Kg);
-// bnpart (optional, [cdiv(M, 256)][2K] floats): the output feeds a training BatchNorm; when the
-// LDS-DMA kernel runs unsplit its epilogue writes the BN partial sums of (y - bnshift[c]) there
-// and the call returns the number of rows written (pass them to nhwc_bn_fwd), else 0
+// bnpart (optional, [nhwc_conv_bn_rows][2K] floats): the output feeds a training BatchNorm; the
+// epilogue (LDS-DMA / band / stem kernels, unsplit) or the split-K reduce writes the BN partial
+// sums of (y - bnshift[c]) there and the call returns the number of rows written (pass them to
+// nhwc_bn_fwd), else 0
 int nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int H, int W, int Cp, int K, int R,
                   int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st,
                   float* bnpart = nullptr, const float* bnshift = nullptr);

@@ -274,6 +274,23 @@ def test_bn_statistics_from_glds256_epilogue(cuda, shape, offset):
         C_.nhwc_conv_set_glds(1)
 
 
+@pytest.mark.parametrize("shape,offset,glds", [((4, 1024, 7, 7, 256, 1, 0), 1.0, 1),  # generic kernel, 2 splits
+                                               ((2, 1024, 7, 7, 2048, 1, 0), -0.5, 1),  # 2 blocks per row
+                                               ((4, 256, 14, 14, 256, 3, 1), 3.0, 1),  # 4 splits, 3x3
+                                               ((3, 512, 9, 11, 128, 3, 1), 0.0, 2)])  # LDS-DMA kernel, split
+def test_bn_statistics_from_splitk_reduce(cuda, shape, offset, glds):
+    """The same when the convolution splits its reduction: the split-K reduce computes the BN
+    partial sums of the bf16 output it stores."""
+    from mxddp import native
+
+    C_ = native()
+    C_.nhwc_conv_set_glds(glds)
+    try:
+        _bn_stats_from_conv_epilogue(cuda, shape, offset)
+    finally:
+        C_.nhwc_conv_set_glds(1)
+
+
 def _bn_stats_from_conv_epilogue(cuda, shape, offset):
     """conv2d(..., bn=bn) -> batch_norm: the LDS-DMA conv's epilogue computes the BN partial sums
     (shifted by the running mean) and the BN skips its statistics pass; same output, running
