@@ -33,6 +33,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace mx {
 
@@ -1273,16 +1274,20 @@ __global__ __launch_bounds__(256) void conv_nhwc_splitk_reduce_k(const float* __
   }
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int sp0 = 0; sp0 < splits; sp0 += 8) {
-      float4 u[8];
+    auto round = [&](auto nb, int sp0) {  // nb planes, loads first, then the adds in split order
+      constexpr int NB = decltype(nb)::value;
+      float4 u[NB];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) u[k] = p4[(int64_t)min(sp0 + k, splits - 1) * n4 + i];
+      for (int k = 0; k < NB; ++k) u[k] = p4[(int64_t)min(sp0 + k, splits - 1) * n4 + i];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {  // in split order (fixed)
+      for (int k = 0; k < NB; ++k) {
         const bool in = sp0 + k < splits;
         s.x += in ? u[k].x : 0.f; s.y += in ? u[k].y : 0.f; s.z += in ? u[k].z : 0.f; s.w += in ? u[k].w : 0.f;
       }
-    }
+    };
+    if (splits <= 4) round(std::integral_constant<int, 4>{}, 0);  // most splits: 2-4, no redundant loads
+    else
+      for (int sp0 = 0; sp0 < splits; sp0 += 8) round(std::integral_constant<int, 8>{}, sp0);
     if (addend) {
       uint2 d = reinterpret_cast<const uint2*>(addend)[i];
       if (amask) {  // 4 elements: bits 4 (i & 1) .. + 3 of byte i / 2
