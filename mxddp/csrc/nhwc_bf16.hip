@@ -2102,7 +2102,15 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
   }
 }
 
-template <bool BWD, int NT, int MAXR>
+// COH (fused finalize): the coefficients are stored device-coherent (agent-scope atomic stores write
+// through the XCD's L2), for the other blocks of the same launch
+template <bool COH>
+__device__ __forceinline__ void coef_store(float* p, float v) {
+  if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
+template <bool BWD, int NT, int MAXR, bool COH = false>
 __device__ __forceinline__ void bn_finalize_group(const BnNArgs& a, const int grp) {
   // block = 8 channels as 4 pairs (one 16-byte (s1, s2, s1', s2') load per thread per row) x 256
   // row groups: each thread sums <= 16 rows per pass of 4,096 with every load issued up front (one
@@ -2190,17 +2198,17 @@ __device__ __forceinline__ void bn_finalize_group(const BnNArgs& a, const int gr
     if (a.run_mean) a.run_mean[c] = (1.f - a.momentum) * rm + a.momentum * mean;
     if (a.run_var) a.run_var[c] = (1.f - a.momentum) * rv + a.momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
     const float sc = iv * gm;
-    a.coef[2 * c] = sc;
-    a.coef[2 * c + 1] = bt - mean * sc;
+    coef_store<COH>(a.coef + 2 * c, sc);
+    coef_store<COH>(a.coef + 2 * c + 1, bt - mean * sc);
   } else {
     const float db = s1, dg = s2 * inv;
     if (a.dgamma) a.dgamma[c] = dg0 + dg;
     if (a.dbeta) a.dbeta[c] = db0 + db;
     // dx = k (cnt g - db - (x - mu) inv dg), k = gamma inv / cnt
     const float k = gm * inv / cnt;
-    a.coef[3 * c] = k * cnt;
-    a.coef[3 * c + 1] = -k * inv * dg;
-    a.coef[3 * c + 2] = -k * db + k * inv * dg * mu;
+    coef_store<COH>(a.coef + 3 * c, k * cnt);
+    coef_store<COH>(a.coef + 3 * c + 1, -k * inv * dg);
+    coef_store<COH>(a.coef + 3 * c + 2, -k * db + k * inv * dg * mu);
   }
 }
 
@@ -2212,16 +2220,19 @@ __global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
 // Fused finalize: the apply kernel's blocks 0 .. nfin - 1 (dispatched first, so resident before
 // any block that waits on them) each finalize one 8-channel group and count it in sync->done;
 // every block issues its first loads, then waits until done reaches base + nfin and reads the
-// coefficients.  One launch less per BN pass (at batch 32 every launch costs ~5 us).  Release /
-// acquire at agent scope (the XCDs' L2s are not coherent).  The wait is bounded: a count that
-// never arrives sets sync->err and lets the kernel finish instead of hanging the device.
+// coefficients.  One launch less per BN pass (at batch 32 every launch costs ~5 us).  The XCDs'
+// L2s are not coherent, but agent-scope FENCES write back / invalidate a whole L2: with one per
+// block the step ran 2.5x slower (profiles/r4_u/).  So only the coefficients travel coherently:
+// written with agent-scope atomic stores (drained before the count), read with agent-scope atomic
+// loads.  The wait is bounded: a count that never arrives sets sync->err and lets the kernel
+// finish instead of hanging the device.
 __device__ __forceinline__ unsigned bn_fin_target(const BnNArgs& a) {
   return __hip_atomic_load(&a.sync->base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (unsigned)a.nfin;
 }
 template <bool BWD>
 __device__ __forceinline__ void bn_fin_publish(const BnNArgs& a) {
-  bn_finalize_group<BWD, kBnT, 8>(a, blockIdx.x);  // <= 1,024 rows (host): two passes
-  __threadfence();
+  bn_finalize_group<BWD, kBnT, 8, true>(a, blockIdx.x);  // <= 1,024 rows (host): two passes
+  __builtin_amdgcn_s_waitcnt(0);  // this thread's coefficient stores performed
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_fetch_add(&a.sync->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -2229,15 +2240,17 @@ __device__ __forceinline__ void bn_fin_wait(const BnNArgs& a, unsigned target) {
   if (threadIdx.x == 0) {
     int it = 0;
     while ((int)(__hip_atomic_load(&a.sync->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-      __builtin_amdgcn_s_sleep(4);
-      if (++it > (1 << 22)) {
+      __builtin_amdgcn_s_sleep(8);
+      if (++it > (1 << 21)) {
         __hip_atomic_fetch_or(&a.sync->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+__device__ __forceinline__ float coh_load(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void bn_fin_exit(const BnNArgs& a, unsigned target) {
   __syncthreads();
@@ -2273,7 +2286,15 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
   if (FUSE && (int)blockIdx.x < a.nfin) bn_fin_publish<false>(a);
   float sc[8], sh[8];
   auto load_coef = [&] {
-    if (FUSE) bn_fin_wait(a, target);
+    if constexpr (FUSE) {
+      bn_fin_wait(a, target);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sc[e] = coh_load(a.coef + 16 * v + 2 * e);
+        sh[e] = coh_load(a.coef + 16 * v + 2 * e + 1);
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float4 q = reinterpret_cast<const float4*>(a.coef + 16 * v)[j];
@@ -2364,7 +2385,12 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv f
   if (FUSE && (int)blockIdx.x < a.nfin) bn_fin_publish<true>(a);
   float kc[24], mc[16];
   auto load_coef = [&] {
-    if (FUSE) bn_fin_wait(a, target);
+    if constexpr (FUSE) {
+      bn_fin_wait(a, target);
+#pragma unroll
+      for (int e = 0; e < 24; ++e) kc[e] = coh_load(a.coef + 24 * v + e);
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const float4 q = reinterpret_cast<const float4*>(a.coef + 24 * v)[j];
