@@ -1935,13 +1935,6 @@ __global__ __launch_bounds__(256) void wrepack_many_k(const int64_t* __restrict_
 // fused ReLU.  Thread (in a 256-thread block) owns vector v = tid % V of pixels tid / V + k * PPI.
 constexpr int kBnT = 256;
 
-// per-device counters of the fused BN finalize (bn_fin_*): `done` counts finalized channel groups
-// (monotonic), `base` is its value at the start of the current apply launch (advanced by that
-// launch's last block to exit), `exited` counts the exits, `err` is set when a wait timed out
-struct BnSync {
-  unsigned done, base, exited, err;
-};
-
 struct BnNArgs {
   const bf16* x;      // BN input
   const bf16* res;    // residual added after the affine map (or null)
@@ -1968,8 +1961,6 @@ struct BnNArgs {
   const float* kshift;  // fwd, partials precomputed by the conv epilogue: their per-channel shift
   int pre;              // fwd: part already holds gx partial rows (no statistics pass)
   float momentum, eps;
-  BnSync* sync;         // fused finalize (nfin > 0): the device's launch counters, see bn_fin_*
-  int nfin;             // blocks 0 .. nfin - 1 of the apply kernel finalize one 8-channel group each
 };
 
 template <bool BWD>
@@ -2102,16 +2093,8 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_partial_k(BnNArgs a) {
   }
 }
 
-// COH (fused finalize): the coefficients are stored device-coherent (agent-scope atomic stores write
-// through the XCD's L2), for the other blocks of the same launch
-template <bool COH>
-__device__ __forceinline__ void coef_store(float* p, float v) {
-  if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
-
-template <bool BWD, int NT, int MAXR, bool COH = false>
-__device__ __forceinline__ void bn_finalize_group(const BnNArgs& a, const int grp) {
+template <bool BWD>
+__global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
   // block = 8 channels as 4 pairs (one 16-byte (s1, s2, s1', s2') load per thread per row) x 256
   // row groups: each thread sums <= 16 rows per pass of 4,096 with every load issued up front (one
   // memory round trip per pass; the 128-pixel conv tiles give a batch-256 56 x 56 layer 6,272
@@ -2119,9 +2102,9 @@ __device__ __forceinline__ void bn_finalize_group(const BnNArgs& a, const int gr
   // combined in a fixed order (deterministic): lane shuffles, then one LDS step.  The per-channel inputs of the
   // finalize (gamma, beta, running stats, x[0][c]) are loaded by 8 owner threads before the
   // reduction so their latency overlaps it.
-  constexpr int RG = NT / 4, NW = NT / 64;
+  constexpr int RG = 256, MAXR = 16, NW = 1024 / 64;
   __shared__ float red[NW][4][4];
-  const int cp = threadIdx.x & 3, rg = threadIdx.x >> 2, c2 = grp * 8 + 2 * cp;
+  const int cp = threadIdx.x & 3, rg = threadIdx.x >> 2, c2 = blockIdx.x * 8 + 2 * cp;
   const bool pok = c2 + 1 < a.C;  // C % 8 == 0 (checked on the host): always true
   const size_t pitch = 2 * (size_t)a.C;
   float s1a = 0.f, s2a = 0.f, s1b = 0.f, s2b = 0.f;
@@ -2142,9 +2125,9 @@ __device__ __forceinline__ void bn_finalize_group(const BnNArgs& a, const int gr
       s2b += t[u].w;
     }
   }
-  // per-channel inputs of the finalize (threads 0..7 own channels grp * 8 + tid), fetched
+  // per-channel inputs of the finalize (threads 0..7 own channels blockIdx.x * 8 + tid), fetched
   // while the reduction runs
-  const int cl = threadIdx.x, c = grp * 8 + cl;
+  const int cl = threadIdx.x, c = blockIdx.x * 8 + cl;
   const bool own = cl < 8 && c < a.C;
   float gm = 1.f, bt = 0.f, rm = 0.f, rv = 0.f, K0 = 0.f, mu = 0.f, inv = 0.f, dg0 = 0.f, db0 = 0.f;
   if (own) {
@@ -2163,7 +2146,7 @@ __device__ __forceinline__ void bn_finalize_group(const BnNArgs& a, const int gr
       }
     }
   }
-  // the 16 row groups of a wave are combined with lane shuffles (xor 4..32 keeps cp), then the NW
+  // the 16 row groups of a wave are combined with lane shuffles (xor 4..32 keeps cp), then the 16
   // wave sums through LDS behind ONE barrier (the former 8-level LDS tree paid 9 barriers)
 #pragma unroll
   for (int m = 4; m < 64; m <<= 1) {
@@ -2198,68 +2181,17 @@ __device__ __forceinline__ void bn_finalize_group(const BnNArgs& a, const int gr
     if (a.run_mean) a.run_mean[c] = (1.f - a.momentum) * rm + a.momentum * mean;
     if (a.run_var) a.run_var[c] = (1.f - a.momentum) * rv + a.momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
     const float sc = iv * gm;
-    coef_store<COH>(a.coef + 2 * c, sc);
-    coef_store<COH>(a.coef + 2 * c + 1, bt - mean * sc);
+    a.coef[2 * c] = sc;
+    a.coef[2 * c + 1] = bt - mean * sc;
   } else {
     const float db = s1, dg = s2 * inv;
     if (a.dgamma) a.dgamma[c] = dg0 + dg;
     if (a.dbeta) a.dbeta[c] = db0 + db;
     // dx = k (cnt g - db - (x - mu) inv dg), k = gamma inv / cnt
     const float k = gm * inv / cnt;
-    coef_store<COH>(a.coef + 3 * c, k * cnt);
-    coef_store<COH>(a.coef + 3 * c + 1, -k * inv * dg);
-    coef_store<COH>(a.coef + 3 * c + 2, -k * db + k * inv * dg * mu);
-  }
-}
-
-template <bool BWD>
-__global__ __launch_bounds__(1024) void bn_nhwc_finalize_k(BnNArgs a) {
-  bn_finalize_group<BWD, 1024, 16>(a, blockIdx.x);
-}
-
-// Fused finalize: the apply kernel's blocks 0 .. nfin - 1 (dispatched first, so resident before
-// any block that waits on them) each finalize one 8-channel group and count it in sync->done;
-// every block issues its first loads, then waits until done reaches base + nfin and reads the
-// coefficients.  One launch less per BN pass (at batch 32 every launch costs ~5 us).  The XCDs'
-// L2s are not coherent, but agent-scope FENCES write back / invalidate a whole L2: with one per
-// block the step ran 2.5x slower (profiles/r4_u/).  So only the coefficients travel coherently:
-// written with agent-scope atomic stores (drained before the count), read with agent-scope atomic
-// loads.  The wait is bounded: a count that never arrives sets sync->err and lets the kernel
-// finish instead of hanging the device.
-__device__ __forceinline__ unsigned bn_fin_target(const BnNArgs& a) {
-  return __hip_atomic_load(&a.sync->base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (unsigned)a.nfin;
-}
-template <bool BWD>
-__device__ __forceinline__ void bn_fin_publish(const BnNArgs& a) {
-  bn_finalize_group<BWD, kBnT, 8, true>(a, blockIdx.x);  // <= 1,024 rows (host): two passes
-  __builtin_amdgcn_s_waitcnt(0);  // this thread's coefficient stores performed
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(&a.sync->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void bn_fin_wait(const BnNArgs& a, unsigned target) {
-  if (threadIdx.x == 0) {
-    int it = 0;
-    while ((int)(__hip_atomic_load(&a.sync->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-      __builtin_amdgcn_s_sleep(8);
-      if (++it > (1 << 21)) {
-        __hip_atomic_fetch_or(&a.sync->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-}
-__device__ __forceinline__ float coh_load(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void bn_fin_exit(const BnNArgs& a, unsigned target) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(&a.sync->exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {  // every block has read base and passed its wait
-      __hip_atomic_store(&a.sync->exited, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&a.sync->base, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    a.coef[3 * c] = k * cnt;
+    a.coef[3 * c + 1] = -k * inv * dg;
+    a.coef[3 * c + 2] = -k * db + k * inv * dg * mu;
   }
 }
 
@@ -2273,38 +2205,22 @@ __device__ __forceinline__ void bn_fin_exit(const BnNArgs& a, unsigned target) {
 // iteration's stores to be acknowledged before issuing its loads -- the loaded registers were the
 // stores' data registers -- so every iteration paid a store round trip plus a load round trip
 // (the apply kernels streamed at ~3.4 TB/s, profiles/r4_pmc/pmc_rn.txt).
-// FUSE: the finalize runs in this launch (bn_fin_*); a separate instantiation because the fused
-// kernel needs 122 VGPRs (4 waves per SIMD) against the plain one's 78 (6)
-template <int U, bool PIPE, bool FUSE>
+template <int U, bool PIPE>
 __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
   const int V = a.C >> 3;
   const int total = a.Npix * V, step = gridDim.x * kBnT;
   const uint4 z = make_uint4(0u, 0u, 0u, 0u);
   const int i00 = blockIdx.x * kBnT + threadIdx.x;
   const int v = i00 - (int)fV.div((uint32_t)i00) * V;  // fixed for this thread (step % V == 0)
-  const unsigned target = FUSE ? bn_fin_target(a) : 0u;
-  if (FUSE && (int)blockIdx.x < a.nfin) bn_fin_publish<false>(a);
   float sc[8], sh[8];
-  auto load_coef = [&] {
-    if constexpr (FUSE) {
-      bn_fin_wait(a, target);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        sc[e] = coh_load(a.coef + 16 * v + 2 * e);
-        sh[e] = coh_load(a.coef + 16 * v + 2 * e + 1);
-      }
-      return;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float4 q = reinterpret_cast<const float4*>(a.coef + 16 * v)[j];
-      sc[2 * j] = q.x;
-      sh[2 * j] = q.y;
-      sc[2 * j + 1] = q.z;
-      sh[2 * j + 1] = q.w;
-    }
-  };
-  if constexpr (!FUSE) load_coef();  // (unfused: before anything else, as before the fused variant)
+  for (int j = 0; j < 4; ++j) {
+    const float4 q = reinterpret_cast<const float4*>(a.coef + 16 * v)[j];
+    sc[2 * j] = q.x;
+    sh[2 * j] = q.y;
+    sc[2 * j + 1] = q.z;
+    sh[2 * j + 1] = q.w;
+  }
   // loads at clamped indices, issued unconditionally (a per-lane `i < total ? load : 0` makes
   // hipcc branch around each load and split it into dwords with a vmcnt(0) per element); only
   // the stores are masked
@@ -2344,7 +2260,6 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
     }
   };
   if constexpr (!PIPE) {
-    if constexpr (FUSE) load_coef();
     for (int i0 = i00; i0 < total; i0 += U * step) {
       uint4 xr[U], rr[U];
       load(i0, xr, rr);
@@ -2356,7 +2271,6 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
     uint4 xa[U], ra[U], xb[U], rb[U];
     int i0 = i00;
     if (i0 < total) load(i0, xa, ra);
-    if constexpr (FUSE) load_coef();  // the first loads are in flight during the wait
     while (i0 < total) {
       const int i1 = i0 + U * step;
       load(i1, xb, rb);
@@ -2368,39 +2282,27 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
       i0 = i2;
     }
   }
-  if (FUSE) bn_fin_exit(a, target);
 }
 
 // backward apply: dx = A g + D x + B; dres = g (the residual branch gradient).  XM: the ReLU mask
 // from x and the forward's (scale, shift) (no residual), else from y.  Coefficients in registers
 // as in the forward apply (fixed channel vector per thread).
-template <bool XM, int U, bool PIPE, bool FUSE>
+template <bool XM, int U, bool PIPE>
 __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv fV) {
   const int V = a.C >> 3;
   const int total = a.Npix * V, step = gridDim.x * kBnT;
   const uint4 z = make_uint4(0u, 0u, 0u, 0u);
   const int i00 = blockIdx.x * kBnT + threadIdx.x;
   const int v = i00 - (int)fV.div((uint32_t)i00) * V;
-  const unsigned target = FUSE ? bn_fin_target(a) : 0u;
-  if (FUSE && (int)blockIdx.x < a.nfin) bn_fin_publish<true>(a);
   float kc[24], mc[16];
-  auto load_coef = [&] {
-    if constexpr (FUSE) {
-      bn_fin_wait(a, target);
 #pragma unroll
-      for (int e = 0; e < 24; ++e) kc[e] = coh_load(a.coef + 24 * v + e);
-      return;
-    }
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const float4 q = reinterpret_cast<const float4*>(a.coef + 24 * v)[j];
-      kc[4 * j] = q.x;
-      kc[4 * j + 1] = q.y;
-      kc[4 * j + 2] = q.z;
-      kc[4 * j + 3] = q.w;
-    }
-  };
-  if constexpr (!FUSE) load_coef();
+  for (int j = 0; j < 6; ++j) {
+    const float4 q = reinterpret_cast<const float4*>(a.coef + 24 * v)[j];
+    kc[4 * j] = q.x;
+    kc[4 * j + 1] = q.y;
+    kc[4 * j + 2] = q.z;
+    kc[4 * j + 3] = q.w;
+  }
   if (XM) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -2467,7 +2369,6 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv f
     }
   };
   if constexpr (!PIPE) {
-    if constexpr (FUSE) load_coef();
     for (int i0 = i00; i0 < total; i0 += U * step) {
       Buf b;
       load(i0, b);
@@ -2477,7 +2378,6 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv f
     Buf ba, bb;
     int i0 = i00;
     if (i0 < total) load(i0, ba);
-    if constexpr (FUSE) load_coef();
     while (i0 < total) {
       const int i1 = i0 + U * step;
       load(i1, bb);
@@ -2489,7 +2389,6 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv f
       i0 = i2;
     }
   }
-  if (FUSE) bn_fin_exit(a, target);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3182,48 +3081,6 @@ static dim3 bn_grid(int Npix, int C) {
   return dim3(gx, gy);
 }
 
-// fused BN finalize (BnSync) on tensors of at most this many elements whose partial rows fit two
-// passes of the finalize (0 = never: the separate finalize launch)
-static int64_t g_bn_fuse_max = 16ll << 20;
-void nhwc_bn_set_fused_finalize(int64_t max_elems) { g_bn_fuse_max = max_elems; }
-static BnSync* g_bn_sync[64] = {};
-// the device's counters (allocated and zeroed on first use; never during a stream capture, where
-// the call falls back to the separate finalize)
-static BnSync* bn_sync(hipStream_t st) {
-  int dev = 0;
-  MX_HIP_CHECK(hipGetDevice(&dev));
-  MX_CHECK(dev >= 0 && dev < 64, "nhwc bn: device index");
-  if (!g_bn_sync[dev]) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    MX_HIP_CHECK(hipStreamIsCapturing(st, &cs));
-    if (cs != hipStreamCaptureStatusNone) return nullptr;
-    BnSync* p = nullptr;
-    MX_HIP_CHECK(hipMalloc(&p, sizeof(BnSync)));
-    MX_HIP_CHECK(hipMemset(p, 0, sizeof(BnSync)));
-    MX_HIP_CHECK(hipDeviceSynchronize());
-    g_bn_sync[dev] = p;
-  }
-  return g_bn_sync[dev];
-}
-int nhwc_bn_sync_errors() {  // timed-out waits of the fused finalize since the last call (tests)
-  int dev = 0;
-  MX_HIP_CHECK(hipGetDevice(&dev));
-  if (dev < 0 || dev >= 64 || !g_bn_sync[dev]) return 0;
-  BnSync h{};
-  MX_HIP_CHECK(hipDeviceSynchronize());
-  MX_HIP_CHECK(hipMemcpy(&h, g_bn_sync[dev], sizeof(BnSync), hipMemcpyDeviceToHost));
-  if (h.err) MX_HIP_CHECK(hipMemset(&g_bn_sync[dev]->err, 0, sizeof(unsigned)));
-  return (int)h.err;
-}
-// finalize fused into the apply launch: nfin = C / 8 blocks finalize (<= 1,024 partial rows)
-static void bn_fuse(BnNArgs& a, hipStream_t st) {
-  a.nfin = 0;
-  a.sync = nullptr;
-  if ((int64_t)a.Npix * a.C > g_bn_fuse_max || a.gx > 1024) return;
-  a.sync = bn_sync(st);
-  if (a.sync) a.nfin = a.C / 8;
-}
-
 size_t nhwc_bn_scratch_floats(int Npix, int C) {
   const dim3 g = bn_grid(Npix, C);
   return (size_t)g.x * 2 * C + 3 * (size_t)C;  // partials + coefficients
@@ -3266,12 +3123,10 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
   } else {
     MX_LAUNCH(bn_nhwc_partial_k<false>, g, dim3(kBnT), 0, st, a);
   }
-  bn_fuse(a, st);
-  if (!a.nfin) MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
+  MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
-  const dim3 agrid(std::max(stream_blocks((int64_t)Npix * V), a.nfin));
-  if (a.nfin) MX_LAUNCH((bn_nhwc_apply_k<2, true, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
-  else MX_LAUNCH((bn_nhwc_apply_k<2, true, false>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
+  const dim3 agrid(stream_blocks((int64_t)Npix * V));
+  MX_LAUNCH((bn_nhwc_apply_k<2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
 }
 
 void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma, const float* mean,
@@ -3310,17 +3165,11 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
   } else {
     MX_LAUNCH(bn_nhwc_partial_k<true>, g, dim3(kBnT), 0, st, a);
   }
-  bn_fuse(a, st);
-  if (!a.nfin) MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
+  MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
-  const dim3 agrid(std::max(stream_blocks((int64_t)Npix * V), a.nfin));
-  if (a.nfin) {
-    if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 2, true, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
-    else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 2, true, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
-  } else {
-    if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 2, true, false>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
-    else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 2, true, false>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
-  }
+  const dim3 agrid(stream_blocks((int64_t)Npix * V));
+  if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
+  else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
 }
 
 void nhwc_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, int k,

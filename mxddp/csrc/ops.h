@@ -197,10 +197,6 @@ void nhwc_conv_set_glds(int mode);
 void nhwc_conv_set_glds256(int mode);
 void nhwc_conv_set_glds_short(int mode);  // two-stage 128-pixel LDS-DMA variant for short reductions
 void nhwc_bn_set_grid_cap(int cap);  // most blocks of the NHWC BN apply kernels (A/B; 2048 = round-3 grids)
-// BN finalize fused into the apply launch on tensors of <= max_elems elements with <= 1,024 partial
-// rows (0 = never) and the number of its timed-out waits since the last call (tests; 0 = healthy)
-void nhwc_bn_set_fused_finalize(int64_t max_elems);
-int nhwc_bn_sync_errors();
 // split-K scratch of nhwc_conv_dgrad (floats; 0 = none needed)
 size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
                                       int P, int Q);

@@ -135,17 +135,6 @@ for step in "$@"; do
       for m in 0 2000000 7000000; do
         run "ab_dst_b256_${m}" 300 env MXDDP_BN_DGRAD_STATS_MAX=$m $B256 || exit 1
       done ;;
-    ab_fuse)  # ResNet-50 batch 32 / 256: BN finalize fused into the apply launch, by tensor size
-      B32="python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3"
-      B256="python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3"
-      for r in 1 2; do
-        for m in 0 4194304 16777216 1099511627776; do
-          run "ab_fuse_b32_${m}_$r" 300 $B32 --bn-fuse-max $m || exit 1
-        done
-      done
-      for m in 0 16777216 1099511627776; do
-        run "ab_fuse_b256_${m}" 300 $B256 --bn-fuse-max $m || exit 1
-      done ;;
     rn32_t256) run rn32_t256 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --conv-tile256 1 ;;
     rn_layers) run rn_layers 300 python scripts/bench_nhwc_layers.py 256 5 ;;
     rn_layers_t256) run rn_layers_t256 300 python scripts/bench_nhwc_layers.py 256 5 1 ;;

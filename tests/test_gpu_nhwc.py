@@ -249,45 +249,6 @@ def test_bn_nhwc(cuda, C, relu, res):
     assert int(bn.num_batches_tracked) == 1
 
 
-@pytest.mark.parametrize("N,H,W,C,relu,res", [(4, 7, 9, 64, True, False), (2, 14, 14, 256, False, True),
-                                               (3, 7, 7, 2048, True, True), (8, 28, 28, 128, True, False),
-                                               (1, 3, 5, 512, False, False)])
-def test_bn_fused_finalize_matches_separate(cuda, N, H, W, C, relu, res):
-    """The BN finalize folded into the apply launch (its first C / 8 blocks finalize, the others wait
-    on the device counters): forward output, running statistics and every gradient match the
-    separate finalize launch (a different fixed summation order: 64 row groups instead of 256), two
-    fused runs agree bit for bit (the counters carry over from one launch to the next), and no wait
-    timed out."""
-    from mxddp import native
-
-    C_ = native()
-    torch.manual_seed(21)
-    x = (torch.randn(N, H, W, C) * 2 + 0.5).to(torch.bfloat16).to(cuda)
-    r = torch.randn(N, H, W, C).to(torch.bfloat16).to(cuda) if res else None
-    gy = torch.randn(N, H, W, C, generator=torch.Generator().manual_seed(5)).to(torch.bfloat16).to(cuda)
-    outs = []
-    try:
-        for fuse in (0, 1 << 40, 1 << 40):
-            C_.nhwc_bn_set_fused_finalize(fuse)
-            bn = nn.BatchNorm2d(C).to(cuda)
-            with torch.no_grad():
-                bn.weight.uniform_(0.5, 1.5, generator=torch.Generator(device=cuda).manual_seed(3))
-            xg = x.clone().requires_grad_()
-            rg = r.clone().requires_grad_() if res else None
-            y = nhwc.batch_norm(xg, bn, relu=relu, res=rg)
-            y.backward(gy)
-            torch.cuda.synchronize()
-            outs.append([y.float().cpu(), bn.running_mean.cpu(), bn.running_var.cpu(), xg.grad.float().cpu(),
-                         bn.weight.grad.cpu(), bn.bias.grad.cpu()] + ([rg.grad.float().cpu()] if res else []))
-    finally:
-        C_.nhwc_bn_set_fused_finalize(16 << 20)
-    assert C_.nhwc_bn_sync_errors() == 0
-    for a, b in zip(outs[1], outs[2]):
-        assert torch.equal(a, b)
-    for a, b in zip(outs[0], outs[1]):
-        assert _nrel(b, a) < 2e-2
-
-
 @pytest.mark.parametrize("shape,offset", [((16, 64, 56, 56, 128, 3, 1), 0.0), ((32, 64, 28, 28, 256, 1, 0), 4.0),
                                           ((14, 64, 61, 59, 128, 3, 1), -2.0),
                                           ((96, 64, 56, 56, 64, 1, 0), 1.0),  # two-stage 128-pixel variant
