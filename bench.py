@@ -85,6 +85,9 @@ def parse():
                          "(-1 = the build default; A/B)")
     ap.add_argument("--bn-grid-cap", type=int, default=0,
                     help="bf16 NHWC BN apply kernels: most blocks (0 = the build default; 2048 = round-3 grids; A/B)")
+    ap.add_argument("--split-blocks", type=int, default=0,
+                    help="bf16 NHWC generic conv kernel: split-K only below this many blocks (0 = the build "
+                         "default; A/B)")
     ap.add_argument("--wt-stores", type=int, default=-1, choices=range(-1, 8), metavar="MASK",
                     help="fused MNIST: bulk stores with agent scope (L2 write-through), 1 = F5, 2 = F2, 4 = F6W "
                          "(-1 = the build default; A/B)")
@@ -131,6 +134,10 @@ def main():
         from mxddp import native as _native
 
         _native().nhwc_bn_set_grid_cap(a.bn_grid_cap)
+    if a.split_blocks:
+        from mxddp import native as _native
+
+        _native().nhwc_conv_set_split_blocks(a.split_blocks)
     if a.wt_stores >= 0:
         from mxddp import native as _native
 
@@ -287,7 +294,8 @@ def main():
                        "graph": _fused_graph(a, tr) or getattr(a, "layers_graph", False),
                        **_fused_config(a, tr), **({"conv_tile256": a.conv_tile256} if a.conv_tile256 >= 0 else {}),
                        **({"glds_short": a.glds_short} if a.glds_short >= 0 else {}),
-                       **({"bn_grid_cap": a.bn_grid_cap} if a.bn_grid_cap else {})},
+                       **({"bn_grid_cap": a.bn_grid_cap} if a.bn_grid_cap else {}),
+                       **({"split_blocks": a.split_blocks} if a.split_blocks else {})},
             **extra,
         }
         if C.shared_devices():

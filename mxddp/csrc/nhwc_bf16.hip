@@ -2615,6 +2615,10 @@ struct ConvPlan {
 // 1.5k-6k output pixels at batch 32): 128 x 128, then 64 x 128, then 64 x 64; when even 64 x 64
 // leaves the chip under-filled, split the reduction (k-tiles) over blockIdx.y with fp32
 // partials (>= 8 k-tiles per split)
+// split-K only below this many blocks (A/B: nhwc_conv_set_split_blocks; each split adds a reduce
+// launch, ~5-6 us at batch 32)
+static int g_split_blocks = 512;
+void nhwc_conv_set_split_blocks(int n) { g_split_blocks = n; }
 static ConvPlan conv_plan(int M, int Ng, int Kg) {
   ConvPlan p{};
   const int b128 = cdiv(Ng, 128) * cdiv(M, 128), b64 = cdiv(Ng, 64) * cdiv(M, 128);
@@ -2627,7 +2631,7 @@ static ConvPlan conv_plan(int M, int Ng, int Kg) {
   }
   const int nkt = cdiv(Kg, 64);
   p.splits = 1;
-  if (p.blocks < 512) p.splits = std::max(1, std::min(cdiv(512, p.blocks), nkt / 8));
+  if (p.blocks < g_split_blocks) p.splits = std::max(1, std::min(cdiv(512, p.blocks), nkt / 8));
   p.kt_per_split = cdiv(nkt, p.splits);
   p.splits = cdiv(nkt, p.kt_per_split);
   return p;
