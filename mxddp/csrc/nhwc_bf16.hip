@@ -2616,8 +2616,9 @@ struct ConvPlan {
 // leaves the chip under-filled, split the reduction (k-tiles) over blockIdx.y with fp32
 // partials (>= 8 k-tiles per split)
 // split-K only below this many blocks (A/B: nhwc_conv_set_split_blocks; each split adds a reduce
-// launch, ~5-6 us at batch 32)
-static int g_split_blocks = 512;
+// launch, ~5-6 us at batch 32).  ResNet-50 (profiles/r4_w/, two runs each): batch 32 5,368 / 5,370
+// img/s at 512, 5,400 / 5,405 at 256, 5,399 / 5,410 at 384, 5,390 / 5,387 at 128; batch 256 equal
+static int g_split_blocks = 256;
 void nhwc_conv_set_split_blocks(int n) { g_split_blocks = n; }
 static ConvPlan conv_plan(int M, int Ng, int Kg) {
   ConvPlan p{};
