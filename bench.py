@@ -88,6 +88,9 @@ def parse():
     ap.add_argument("--split-blocks", type=int, default=0,
                     help="bf16 NHWC generic conv kernel: split-K only below this many blocks (0 = the build "
                          "default; A/B)")
+    ap.add_argument("--wgrad-target", type=int, default=0,
+                    help="bf16 NHWC weight gradient: blocks aimed at when splitting the pixels (0 = the build "
+                         "default; A/B)")
     ap.add_argument("--wt-stores", type=int, default=-1, choices=range(-1, 8), metavar="MASK",
                     help="fused MNIST: bulk stores with agent scope (L2 write-through), 1 = F5, 2 = F2, 4 = F6W "
                          "(-1 = the build default; A/B)")
@@ -138,6 +141,10 @@ def main():
         from mxddp import native as _native
 
         _native().nhwc_conv_set_split_blocks(a.split_blocks)
+    if a.wgrad_target:
+        from mxddp import native as _native
+
+        _native().nhwc_wgrad_set_target(a.wgrad_target)
     if a.wt_stores >= 0:
         from mxddp import native as _native
 
@@ -295,7 +302,8 @@ def main():
                        **_fused_config(a, tr), **({"conv_tile256": a.conv_tile256} if a.conv_tile256 >= 0 else {}),
                        **({"glds_short": a.glds_short} if a.glds_short >= 0 else {}),
                        **({"bn_grid_cap": a.bn_grid_cap} if a.bn_grid_cap else {}),
-                       **({"split_blocks": a.split_blocks} if a.split_blocks else {})},
+                       **({"split_blocks": a.split_blocks} if a.split_blocks else {}),
+                       **({"wgrad_target": a.wgrad_target} if a.wgrad_target else {})},
             **extra,
         }
         if C.shared_devices():

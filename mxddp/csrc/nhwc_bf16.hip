@@ -2993,12 +2993,15 @@ static void wgrad_tile(int K, int Ng, int& tm, int& tn) {
   tn = Ng <= 64 ? 64 : 128;
 }
 
+// weight-gradient blocks aimed at (A/B: nhwc_wgrad_set_target)
+static int g_wgrad_target = 512;
+void nhwc_wgrad_set_target(int n) { g_wgrad_target = n; }
 static int wgrad_splits(int Npix, int K, int Ng) {
   int tm, tn;
   wgrad_tile(K, Ng, tm, tn);
   const int tiles = cdiv(K, tm) * cdiv(Ng, tn);
   // ~2 blocks per CU, >= 512 pixels (8 stages) per block, partial planes <= 32M floats
-  constexpr int target = 512;
+  const int target = g_wgrad_target;
   int splits = std::max(1, cdiv(target, tiles));
   splits = std::min(splits, std::max(1, Npix / 512));
   splits = std::min(splits, std::max(1, (int)((32ll << 20) / ((int64_t)K * Ng))));

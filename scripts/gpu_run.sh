@@ -146,6 +146,17 @@ for step in "$@"; do
       for m in 512 256; do
         run "ab_split_b256_${m}" 300 $B256 --split-blocks $m || exit 1
       done ;;
+    ab_wgt)  # ResNet-50 batch 32 / 256: weight-gradient block target (pixel splits)
+      B32="python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3"
+      B256="python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3"
+      for r in 1 2; do
+        for m in 512 256 1024; do
+          run "ab_wgt_b32_${m}_$r" 300 $B32 --wgrad-target $m || exit 1
+        done
+      done
+      for m in 512 256 1024; do
+        run "ab_wgt_b256_${m}" 300 $B256 --wgrad-target $m || exit 1
+      done ;;
     rn32_t256) run rn32_t256 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --conv-tile256 1 ;;
     rn_layers) run rn_layers 300 python scripts/bench_nhwc_layers.py 256 5 ;;
     rn_layers_t256) run rn_layers_t256 300 python scripts/bench_nhwc_layers.py 256 5 1 ;;
