@@ -2993,7 +2993,8 @@ static void wgrad_tile(int K, int Ng, int& tm, int& tn) {
   tn = Ng <= 64 ? 64 : 128;
 }
 
-// weight-gradient blocks aimed at (A/B: nhwc_wgrad_set_target)
+// weight-gradient blocks aimed at (A/B: nhwc_wgrad_set_target; 256 and 1,024 measured no better,
+// profiles/r4_y/)
 static int g_wgrad_target = 512;
 void nhwc_wgrad_set_target(int n) { g_wgrad_target = n; }
 static int wgrad_splits(int Npix, int K, int Ng) {
