@@ -11,8 +11,9 @@ Each timed step is a full training step: forward, backward, bucketed RCCL all-re
         --master-port 29500 bench.py --gpus 8 --steps 200 --warmup 20
 
 Timing: W untimed warm-up steps (the first also captures the hipGraph), then device sync +
-barrier + device sync, K timed steps, device sync; each rank stops its clock after its own
-sync, the closing barrier runs after the clock stops, and the time is the MAX over ranks.
+barrier + device sync, one tiny alignment all-reduce on the step stream (world size > 1), a
+start event, K timed steps, an end event, device sync; the time is the MAX over ranks of the
+event-timed K steps (the host clock of the same region is reported as host_ms_per_step).
 ``warmup_steps_run`` in the JSON counts every untimed step that really ran (autotune trials,
 the capture step and the first launch of each captured graph included).
 Rank 0 prints one JSON line.
@@ -34,6 +35,32 @@ MODEL_METRIC = {
     "keras_cnn": "images/sec (whole node) Keras MNIST CNN (reference tensorflow2/, Adam)",
     "mlp": "images/sec (whole node) Chainer MNIST MLP (reference chainer/, Adam)",
 }
+
+
+# --ab KEY=VALUE: measured-once kernel choices kept switchable for A/B runs (docs/BENCHMARKS.md)
+AB_SWITCHES = {
+    "conv_tile256": ("nhwc_conv_set_glds256", "bf16 NHWC convs, 256x256-tile LDS-DMA kernel on big layers (0/1)"),
+    "glds_short": ("nhwc_conv_set_glds_short", "bf16 NHWC convs, two-stage 128-pixel variant on short reductions (0/1)"),
+    "bn_grid_cap": ("nhwc_bn_set_grid_cap", "bf16 NHWC BN apply kernels, most blocks"),
+    "split_blocks": ("nhwc_conv_set_split_blocks", "bf16 NHWC generic conv, split-K only below this many blocks"),
+    "wgrad_target": ("nhwc_wgrad_set_target", "bf16 NHWC weight gradient, blocks aimed at when splitting pixels"),
+    "wt_stores": ("mnist_set_wt_stores", "fused MNIST, L2 write-through bulk stores mask (1 F5, 2 F2, 4 F6W)"),
+}
+
+
+def _apply_ab(items) -> dict:
+    out = {}
+    if not items:
+        return out
+    from mxddp import native
+
+    for it in items:
+        k, sep, v = it.partition("=")
+        if not sep or k not in AB_SWITCHES:
+            raise SystemExit(f"bench.py: --ab {it!r}: expected KEY=VALUE with KEY in {sorted(AB_SWITCHES)}")
+        getattr(native(), AB_SWITCHES[k][0])(int(v))
+        out[k] = int(v)
+    return out
 
 
 def _metric(model: str) -> str:
@@ -78,22 +105,9 @@ def parse():
     ap.add_argument("--lr", type=float, default=0.01, help="SGD lr (momentum 0.9, wd 1e-4 as the reference)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
                     help="GEMM precision of the layers path (headline is fp32, >= the reference's precision)")
-    ap.add_argument("--conv-tile256", type=int, default=-1, choices=[-1, 0, 1],
-                    help="bf16 NHWC convs: the 256 x 256-tile LDS-DMA kernel on layers with >= 256 tiles and >= 4 k-tiles (-1 = the build default: on; A/B)")
-    ap.add_argument("--glds-short", type=int, default=-1, choices=[-1, 0, 1],
-                    help="bf16 NHWC convs: the two-stage 128-pixel LDS-DMA variant on short-reduction layers "
-                         "(-1 = the build default; A/B)")
-    ap.add_argument("--bn-grid-cap", type=int, default=0,
-                    help="bf16 NHWC BN apply kernels: most blocks (0 = the build default; 2048 = round-3 grids; A/B)")
-    ap.add_argument("--split-blocks", type=int, default=0,
-                    help="bf16 NHWC generic conv kernel: split-K only below this many blocks (0 = the build "
-                         "default; A/B)")
-    ap.add_argument("--wgrad-target", type=int, default=0,
-                    help="bf16 NHWC weight gradient: blocks aimed at when splitting the pixels (0 = the build "
-                         "default; A/B)")
-    ap.add_argument("--wt-stores", type=int, default=-1, choices=range(-1, 8), metavar="MASK",
-                    help="fused MNIST: bulk stores with agent scope (L2 write-through), 1 = F5, 2 = F2, 4 = F6W "
-                         "(-1 = the build default; A/B)")
+    ap.add_argument("--ab", action="append", default=[], metavar="KEY=VALUE",
+                    help="A/B switch of a native kernel choice (repeatable; the build default when absent): "
+                         + "; ".join(f"{k}: {h}" for k, (_, h) in AB_SWITCHES.items()))
     ap.add_argument("--cpu", action="store_true",
                     help="BASELINE config 1: single process on the CPU (the reference's single_gpu.py CPU fallback)")
     ap.add_argument("--phase-profile", type=int, default=0, metavar="STEPS",
@@ -125,30 +139,7 @@ def main():
             print(f"bench.py: --gpus {a.gpus} needs a launcher (torch.distributed.run)", file=sys.stderr)
             sys.exit(2)
     inf = C.init_distributed(use_gpu=True)
-    if a.conv_tile256 >= 0:
-        from mxddp import native as _native
-
-        _native().nhwc_conv_set_glds256(a.conv_tile256)
-    if a.glds_short >= 0:
-        from mxddp import native as _native
-
-        _native().nhwc_conv_set_glds_short(a.glds_short)
-    if a.bn_grid_cap:
-        from mxddp import native as _native
-
-        _native().nhwc_bn_set_grid_cap(a.bn_grid_cap)
-    if a.split_blocks:
-        from mxddp import native as _native
-
-        _native().nhwc_conv_set_split_blocks(a.split_blocks)
-    if a.wgrad_target:
-        from mxddp import native as _native
-
-        _native().nhwc_wgrad_set_target(a.wgrad_target)
-    if a.wt_stores >= 0:
-        from mxddp import native as _native
-
-        _native().mnist_set_wt_stores(a.wt_stores)
+    ab = _apply_ab(a.ab)
     if a.dtype != "fp32":
         if a.impl == "fused":
             a.impl = "layers"  # the fused MNIST engine is fp32-only
@@ -245,18 +236,33 @@ def main():
         torch.cuda.synchronize(dev)
     # every untimed step that ran before the timed region: autotune trials, the capture step,
     # the first launch of every captured graph, the requested warm-up and the clock-ramp steps
-    warmup_run = tr.steps if tr is not None else a.warmup + extra + getattr(a, "layers_eager_steps", 0)
+    warmup_run = (tr.steps + getattr(tr, "discarded_steps", 0) if tr is not None
+                  else a.warmup + extra + getattr(a, "layers_eager_steps", 0))
+    # Timed region, device-aligned: after the host barrier, ONE tiny all-reduce on the stream the
+    # steps run on (the job's RCCL communicator, or the peer transport when ranks share a GPU)
+    # lines the ranks' devices up whatever the skew with which their hosts left the barrier; a
+    # start event right after it and an end event after the K steps give each rank's device
+    # time of exactly those K steps, and the slowest rank decides.  The host clock around the
+    # same region (barrier exit -> own device sync) is reported next to it.
+    st = tr.stream if tr is not None else torch.cuda.current_stream(dev)
+    align_comm, align_peer = (tr.comm, tr.peer) if tr is not None else (comm, _layers_peer(inf, comm))
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     C.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    aligned = C.device_align(st, align_comm, align_peer)
+    ev0.record(st)
     run(a.steps)
+    ev1.record(st)
     torch.cuda.synchronize(dev)
-    # each rank stops its own clock after its own device sync; the slowest rank decides (the
-    # closing barrier runs outside the timed region, so no host collective is inside it)
+    # each rank stops its own host clock after its own device sync; the closing barrier runs
+    # outside the timed region, so no host collective is inside it
     t_rank = time.perf_counter() - t0
+    dev_rank = ev0.elapsed_time(ev1) * 1e-3
     C.barrier()
-    dt = C.all_reduce_max(t_rank)
+    dt = C.all_reduce_max(dev_rank)
+    dt_host = C.all_reduce_max(t_rank)
 
     if a.impl == "fused":
         # per-image averages over every step since the device accumulators were last zeroed
@@ -289,6 +295,9 @@ def main():
             "warmup": a.warmup,
             "warmup_steps_run": warmup_run,
             "ms_per_step": round(dt / a.steps * 1e3, 4),
+            # the same region on each rank's host clock (barrier exit -> own device sync, max)
+            "host_ms_per_step": round(dt_host / a.steps * 1e3, 4),
+            "timing": f"device events after a {aligned} alignment all-reduce" if aligned != "none" else "device events",
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 3),
@@ -299,17 +308,23 @@ def main():
                        "image": "x".join(map(str, spec.input_shape)), "parallelism": f"dp{a.gpus}", "impl": a.impl,
                        # how the timed steps were actually launched (autotune may pick eager mode 0)
                        "graph": _fused_graph(a, tr) or getattr(a, "layers_graph", False),
-                       **_fused_config(a, tr), **({"conv_tile256": a.conv_tile256} if a.conv_tile256 >= 0 else {}),
-                       **({"glds_short": a.glds_short} if a.glds_short >= 0 else {}),
-                       **({"bn_grid_cap": a.bn_grid_cap} if a.bn_grid_cap else {}),
-                       **({"split_blocks": a.split_blocks} if a.split_blocks else {}),
-                       **({"wgrad_target": a.wgrad_target} if a.wgrad_target else {})},
+                       **_fused_config(a, tr), **({"ab": ab} if ab else {})},
             **extra,
         }
         if C.shared_devices():
             out["shared_gpu_rehearsal"] = True  # several ranks on one GPU: not a scaling number
         print(json.dumps(out), flush=True)
     C.shutdown()
+
+
+def _layers_peer(inf, comm):
+    """The layer path's peer transport when the job has no RCCL communicator (ranks sharing a
+    GPU: the DDP reducer exchanges over it), for the timed region's alignment all-reduce."""
+    if comm is not None or inf.world_size == 1:
+        return None
+    from mxddp.parallel import peer as P
+
+    return P.peer_comm()
 
 
 def _fused_graph(a, tr) -> bool:
@@ -430,14 +445,15 @@ def _replica_fused(a, devices, spec):
     rep.step(a.warmup)
     rep.synchronize()
     t0 = time.perf_counter()
-    rep.step(a.steps)
-    rep.synchronize()
-    dt = time.perf_counter() - t0
+    dt = rep.timed_steps(a.steps)  # device events after an alignment exchange, slowest replica
+    dt_host = time.perf_counter() - t0
     B = a.batch * len(devices)
     value = B * a.steps / dt
     print(json.dumps({
         "metric": _metric(a.model), "value": round(value, 1), "unit": "images/sec", "n_gpus": a.gpus, "steps": a.steps,
         "warmup": a.warmup, "warmup_steps_run": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4),
+        "host_ms_per_step": round(dt_host / a.steps * 1e3, 4),
+        "timing": "device events after a peer alignment exchange" if len(devices) > 1 else "device events",
         "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": a.dtype, "data": _data_desc(spec),
         "config": {"model": a.model, "global_batch": B, "per_rank_batch": a.batch, "seq_len": None,

@@ -365,6 +365,8 @@ PYBIND11_MODULE(_C, m) {
       .def("reset_error", &PeerComm::reset_error)
       .def("set_blocks", &PeerComm::set_blocks)
       .def("set_fence", &PeerComm::set_fence)
+      .def("set_withhold", &PeerComm::set_withhold)
+      .def("reset_state", &PeerComm::reset_state, py::call_guard<py::gil_scoped_release>())
       .def("set_timeout_ms", &PeerComm::set_timeout_ms)
       .def("set_oneshot_bytes", &PeerComm::set_oneshot_bytes)
       .def_property_readonly("oneshot_bytes", &PeerComm::oneshot_bytes)
@@ -454,6 +456,7 @@ PYBIND11_MODULE(_C, m) {
   // ---------------------------------------------------------------- fused Chainer-MLP engine
   m.def("mlp_workspace_bytes", &MlpEngine::workspace_bytes);
   m.attr("MLP_NUM_PARAMS") = MlpLayout::total;
+  m.attr("MLP_MAX_BATCH") = kMlpMaxBatch;
   py::class_<MlpEngine>(m, "MlpEngine")
       .def(py::init([](int B, uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t st, uintptr_t ws,
                        size_t wsb, Comm* comm, uint64_t seed, uintptr_t lr, uintptr_t metrics, float b1, float b2,

@@ -40,7 +40,7 @@ void carve_all(Carve& c, MlpFused& f, int B) {
 size_t MlpEngine::workspace_bytes(int B) {
   MlpFused f{};
   Carve c{nullptr, 0, 0};
-  carve_all(c, f, B);
+  carve_all(c, f, (B + 15) / 16 * 16);  // every [B] buffer has the padded tile count of rows
   return c.off * 4;
 }
 
@@ -49,10 +49,12 @@ MlpEngine::MlpEngine(int batch, uintptr_t params, uintptr_t grads, uintptr_t m, 
                      uintptr_t metrics_dev, float b1, float b2, float eps, float weight_decay, bool eps_hat)
     : B_(batch), comm_(comm), seed_(seed) {
   using L = MlpLayout;
-  MX_CHECK(B_ % 16 == 0 && B_ >= 16 && B_ <= 128, "mlp engine: batch must be a multiple of 16 in [16, 128]");
+  MX_CHECK(B_ >= 1 && B_ <= kMlpMaxBatch, "mlp engine: batch must be in [1, 512]");
+  const int Bp = (B_ + 15) / 16 * 16;  // MFMA row tiles; rows B.. are masked out of every sum
   Carve c{reinterpret_cast<char*>(workspace), 0, workspace_bytes};
-  carve_all(c, f_, B_);
+  carve_all(c, f_, Bp);
   f_.B = B_;
+  f_.Bp = Bp;
   f_.p = reinterpret_cast<float*>(params);
   f_.g = reinterpret_cast<float*>(grads);
   f_.m = reinterpret_cast<float*>(m);
@@ -69,8 +71,11 @@ MlpEngine::MlpEngine(int batch, uintptr_t params, uintptr_t grads, uintptr_t m, 
   graphs_.set_stream(s_);
   MX_HIP_CHECK(hipMemsetAsync(f_.counter, 0, 16, s_));
   // h1 / h2 / dh2 pad columns must read as zero before the first step writes them
-  MX_HIP_CHECK(hipMemsetAsync(f_.h1, 0, sizeof(float) * B_ * L::kHP, s_));
-  MX_HIP_CHECK(hipMemsetAsync(f_.h2, 0, sizeof(float) * B_ * L::kHP, s_));
+  MX_HIP_CHECK(hipMemsetAsync(f_.h1, 0, sizeof(float) * Bp * L::kHP, s_));
+  MX_HIP_CHECK(hipMemsetAsync(f_.h2, 0, sizeof(float) * Bp * L::kHP, s_));
+  // a caller's batch fills rows 0..B-1 only: the tail rows of the last tile stay finite zeros
+  MX_HIP_CHECK(hipMemsetAsync(f_.x, 0, sizeof(float) * Bp * L::kIn, s_));
+  MX_HIP_CHECK(hipMemsetAsync(f_.y, 0, sizeof(int32_t) * Bp, s_));
   synth_templates(const_cast<float*>(f_.tmpl), 10, L::kIn, seed_ ^ 0x5eedull, s_);  // identical on every rank
   // bucket 0: [l2.w .. l3.b] (complete after K4, overlappable with K5); bucket 1: [l1.w, l1.b]
   std::vector<Reducer::BucketSpec> buckets = {{L::w2, L::total - L::w2}, {0, L::w2}};

@@ -8,6 +8,8 @@
 
 namespace mx {
 
+constexpr int kMlpMaxBatch = 512;  // per device; batches need not be multiples of the 16-row tile
+
 // Flat parameter layout = MLP state_dict order (models/mlp.py: l1, l2, l3 weight / bias).
 struct MlpLayout {
   static constexpr int kIn = 784, kH = 1000, kHP = 1024, kNC = 10;
@@ -16,7 +18,9 @@ struct MlpLayout {
 };
 
 struct MlpFused {
-  int B;
+  int B;             // batch (rows that count: loss, accuracy, 1/B)
+  int Bp;            // B rounded up to the 16-row MFMA tile: every [B]-shaped buffer below has Bp
+                     // rows; rows B.. carry zero loss gradient, so they add nothing to any sum
   float* x;          // [B][784]
   int32_t* y;        // [B]
   float* p;          // flat params (MlpLayout)

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void fwd_kernel(MlpFused f) {
   const float* W = f.p + (kIn == L::kIn ? L::w1 : L::w2);
   const float* bias = f.p + (kIn == L::kIn ? L::b1 : L::b2);
   float* out = kIn == L::kIn ? f.h1 : f.h2;
-  const int MT = f.B / 16;
+  const int MT = f.Bp / 16;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int nt = bid / MT, mt = bid - nt * MT;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
@@ -224,9 +224,11 @@ __global__ __launch_bounds__(256) void head_kernel(MlpFused f) {
     float ly = 0.f;
 #pragma unroll
     for (int c = 0; c < L::kNC; ++c) ly = c == y ? l[c] : ly;
-    lc[0][tid] = lse - ly;
-    lc[1][tid] = am == y ? 1.f : 0.f;
-    const float inv = 1.f / (float)f.B;
+    // rows B.. of the last tile (batch not a multiple of 16): no loss, no accuracy, no gradient
+    const float live = 16 * mt + tid < f.B ? 1.f : 0.f;
+    lc[0][tid] = (lse - ly) * live;
+    lc[1][tid] = am == y ? live : 0.f;
+    const float inv = live / (float)f.B;
 #pragma unroll
     for (int c = 0; c < L::kNC; ++c) dls[tid][c] = (__expf(l[c] - lse) - (c == y ? 1.f : 0.f)) * inv;
 #pragma unroll
@@ -268,9 +270,10 @@ __global__ __launch_bounds__(256) void head_kernel(MlpFused f) {
 //   db2 (tile 0 of each slice)                                              -> Adam / g
 // Blocks [252, 256): W3 columns 250 q .. +249 (VALU, K = B) and b3 + the step's metrics (q = 0).
 constexpr int kRS = 256, kDhP = 260, kK4A = 4 * kNT;
+constexpr int kBC2 = 128;  // batch rows per LDS pass of K4 (dh2 [128][260] + W2 tile + h1: 157 KB)
 __global__ __launch_bounds__(256) void bwd2_kernel(MlpFused f) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int B = f.B;
+  const int B = f.Bp;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
   const AdamC ac = adam_consts(f);
   if ((int)blockIdx.x >= kK4A) {
@@ -318,14 +321,9 @@ __global__ __launch_bounds__(256) void bwd2_kernel(MlpFused f) {
   const int bid = xcd_remap(blockIdx.x, kK4A);  // the tiles of one row slice share an XCD's L2
   const int ri = bid / kNT, jt = bid - ri * kNT;
   const int i0 = kRS * ri;
-  float* dh2s = sm;                 // [B][260]
-  float* w2s = dh2s + B * kDhP;     // [256][16]
-  float* h1s = w2s + kRS * 16;      // [B][16]
-  for (int k = tid; k < B * 64; k += 256) {  // dh2 columns i0 .. i0 + 255 (pad columns are 0)
-    const int b = k >> 6, c4 = k & 63;
-    *reinterpret_cast<float4*>(dh2s + b * kDhP + 4 * c4) =
-        *reinterpret_cast<const float4*>(f.dh2 + (size_t)b * L::kHP + i0 + 4 * c4);
-  }
+  float* dh2s = sm;                 // [kBC2][260]
+  float* w2s = dh2s + kBC2 * kDhP;  // [256][16]
+  float* h1s = w2s + kRS * 16;      // [kBC2][16]
   {  // W2 tile: thread = row i0 + tid, 16 columns (zero outside the 1000 x 1000 matrix)
     const int i = min(i0 + tid, L::kH - 1);
     const float4* src = reinterpret_cast<const float4*>(f.p + L::w2 + (size_t)i * L::kH + 16 * jt);
@@ -339,32 +337,48 @@ __global__ __launch_bounds__(256) void bwd2_kernel(MlpFused f) {
       *reinterpret_cast<float4*>(w2s + tid * 16 + 4 * q) = cok ? v[q] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  for (int k = tid; k < B * 4; k += 256) {
-    const int b = k >> 2, c4 = k & 3;
-    *reinterpret_cast<float4*>(h1s + b * 16 + 4 * c4) =
-        *reinterpret_cast<const float4*>(f.h1 + (size_t)b * L::kHP + 16 * jt + 4 * c4);
-  }
-  __syncthreads();
-  // dh1 partial: M = batch (wave w: M-tiles w, w+4, ..), N = 16 columns, K = the 256 rows
-  for (int mt = w; mt < B / 16; mt += 4) {
-    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    const float* a = dh2s + (16 * mt + m) * kDhP + g;
-    const float* bb = w2s + g * 16 + m;
-#pragma unroll 16
-    for (int s = 0; s < kRS / 4; ++s) acc[s & 1] = mfma4(a[4 * s], bb[64 * s], acc[s & 1]);
-    float* dst = f.dh1p + ((size_t)ri * B + 16 * mt + 4 * g) * L::kHP + 16 * jt + m;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) dst[(size_t)r * L::kHP] = acc[0][r] + acc[1][r];
-  }
-  // dW2 tile: M = the 256 rows (wave w: tiles w, w+4, w+8, w+12), N = 16 columns, K = batch
+  // the batch in passes of kBC2 rows (one pass for B <= 128): the dW2 tile and the db2 sums
+  // accumulate across passes in registers, in a fixed order (deterministic)
   f32x4 dw[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) dw[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < B / 4; ++s) {
-    const float bvv = h1s[(4 * s + g) * 16 + m];
-    const float* a = dh2s + (4 * s + g) * kDhP + m;
+  float s2[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < B; c0 += kBC2) {
+    const int bc = min(kBC2, B - c0);
+    if (c0) __syncthreads();  // the previous pass's LDS reads are done
+    for (int k = tid; k < bc * 64; k += 256) {  // dh2 columns i0 .. i0 + 255 (pad columns are 0)
+      const int b = k >> 6, c4 = k & 63;
+      *reinterpret_cast<float4*>(dh2s + b * kDhP + 4 * c4) =
+          *reinterpret_cast<const float4*>(f.dh2 + (size_t)(c0 + b) * L::kHP + i0 + 4 * c4);
+    }
+    for (int k = tid; k < bc * 4; k += 256) {
+      const int b = k >> 2, c4 = k & 3;
+      *reinterpret_cast<float4*>(h1s + b * 16 + 4 * c4) =
+          *reinterpret_cast<const float4*>(f.h1 + (size_t)(c0 + b) * L::kHP + 16 * jt + 4 * c4);
+    }
+    __syncthreads();
+    // dh1 partial: M = batch (wave w: M-tiles w, w+4, ..), N = 16 columns, K = the 256 rows
+    for (int mt = w; mt < bc / 16; mt += 4) {
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      const float* a = dh2s + (16 * mt + m) * kDhP + g;
+      const float* bb = w2s + g * 16 + m;
+#pragma unroll 16
+      for (int s = 0; s < kRS / 4; ++s) acc[s & 1] = mfma4(a[4 * s], bb[64 * s], acc[s & 1]);
+      float* dst = f.dh1p + ((size_t)ri * B + c0 + 16 * mt + 4 * g) * L::kHP + 16 * jt + m;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dw[q] = mfma4(a[16 * (w + 4 * q)], bvv, dw[q]);
+      for (int r = 0; r < 4; ++r) dst[(size_t)r * L::kHP] = acc[0][r] + acc[1][r];
+    }
+    // dW2 tile: M = the 256 rows (wave w: tiles w, w+4, w+8, w+12), N = 16 columns, K = batch
+    for (int s = 0; s < bc / 4; ++s) {
+      const float bvv = h1s[(4 * s + g) * 16 + m];
+      const float* a = dh2s + (4 * s + g) * kDhP + m;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dw[q] = mfma4(a[16 * (w + 4 * q)], bvv, dw[q]);
+    }
+    if (jt == 0)  // db2 of the slice's rows: fixed-order column sums
+      for (int b = 0; b < bc; b += 4)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s2[k] += dh2s[(b + k) * kDhP + tid];
   }
   const int j = 16 * jt + m;
   if (j < L::kH) {
@@ -399,13 +413,9 @@ __global__ __launch_bounds__(256) void bwd2_kernel(MlpFused f) {
         }
       }
   }
-  if (jt == 0 && i0 + tid < L::kH) {  // db2 of the slice's rows: fixed-order column sums
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int b = 0; b < B; b += 4)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) s[k] += dh2s[(b + k) * kDhP + tid];
+  if (jt == 0 && i0 + tid < L::kH) {
     const size_t e = L::b2 + i0 + tid;
-    apply_grad(f, e, f.p[e], (s[0] + s[1]) + (s[2] + s[3]), ac);
+    apply_grad(f, e, f.p[e], (s2[0] + s2[1]) + (s2[2] + s2[3]), ac);
   }
 }
 
@@ -415,34 +425,53 @@ __global__ __launch_bounds__(256) void bwd2_kernel(MlpFused f) {
 // 112 columns are staged in LDS (pitch 112: lane groups 16 banks apart); wave w computes the
 // 16 x 16 dW1 tiles kt = w, w + 4 (M = rows, N = columns, K = batch) and applies Adam to them;
 // db1 in the column-group-0 blocks.  Block 0 publishes the Adam step count.
+constexpr int kBC1 = 256;  // batch rows per LDS pass of K5 (dh1 [256][16] + x [256][112]: 128 KB)
 __global__ __launch_bounds__(256) void bwd1_kernel(MlpFused f) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int B = f.B;
+  const int B = f.Bp;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
   const AdamC ac = adam_consts(f);
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int nt = bid / 7, kg = bid - nt * 7;
-  float* dh1s = sm;            // [B][16]
-  float* xs = dh1s + B * 16;   // [B][112]
-  for (int k = tid; k < B * 16; k += 256) {
-    const int b = k >> 4, n = 16 * nt + (k & 15);
-    const size_t o = (size_t)b * L::kHP + n;
-    const size_t pl = (size_t)B * L::kHP;
-    const float s = (f.dh1p[o] + f.dh1p[pl + o]) + (f.dh1p[2 * pl + o] + f.dh1p[3 * pl + o]);
-    dh1s[k] = f.h1[o] > 0.f ? s : 0.f;  // h1 pad columns are 0: those planes' garbage is dropped
-  }
-  for (int k = tid; k < B * 28; k += 256) {
-    const int b = k / 28, c4 = k - 28 * b;
-    *reinterpret_cast<float4*>(xs + b * 112 + 4 * c4) =
-        *reinterpret_cast<const float4*>(f.x + (size_t)b * L::kIn + 112 * kg + 4 * c4);
-  }
+  float* dh1s = sm;              // [kBC1][16]
+  float* xs = dh1s + kBC1 * 16;  // [kBC1][112]
   if (blockIdx.x == 0 && tid == 0 && f.fused_adam)
     __hip_atomic_store(f.adam_state + 1, __hip_atomic_load(f.adam_state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1,
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  for (int kt = w; kt < 7; kt += 4) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < B / 4; ++s) acc = mfma4(dh1s[(4 * s + g) * 16 + m], xs[(4 * s + g) * 112 + 16 * kt + m], acc);
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  float s1[4] = {0.f, 0.f, 0.f, 0.f};
+  const size_t pl = (size_t)B * L::kHP;
+  for (int c0 = 0; c0 < B; c0 += kBC1) {  // one pass for B <= 256; fixed accumulation order
+    const int bc = min(kBC1, B - c0);
+    if (c0) __syncthreads();
+    for (int k = tid; k < bc * 16; k += 256) {
+      const int b = k >> 4, n = 16 * nt + (k & 15);
+      const size_t o = (size_t)(c0 + b) * L::kHP + n;
+      const float s = (f.dh1p[o] + f.dh1p[pl + o]) + (f.dh1p[2 * pl + o] + f.dh1p[3 * pl + o]);
+      dh1s[k] = f.h1[o] > 0.f ? s : 0.f;  // h1 pad columns are 0: those planes' garbage is dropped
+    }
+    for (int k = tid; k < bc * 28; k += 256) {
+      const int b = k / 28, c4 = k - 28 * b;
+      *reinterpret_cast<float4*>(xs + b * 112 + 4 * c4) =
+          *reinterpret_cast<const float4*>(f.x + (size_t)(c0 + b) * L::kIn + 112 * kg + 4 * c4);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int kt = w + 4 * u;
+      if (kt < 7)
+        for (int s = 0; s < bc / 4; ++s)
+          acc[u] = mfma4(dh1s[(4 * s + g) * 16 + m], xs[(4 * s + g) * 112 + 16 * kt + m], acc[u]);
+    }
+    if (kg == 0 && tid < 16)
+      for (int b = 0; b < bc; b += 4)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s1[k] += dh1s[(b + k) * 16 + tid];
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int kt = w + 4 * u;
+    if (kt >= 7) continue;
     const int k = 112 * kg + 16 * kt + m;
     float pv[4], mv[4], vv[4];
 #pragma unroll
@@ -461,28 +490,31 @@ __global__ __launch_bounds__(256) void bwd1_kernel(MlpFused f) {
       if (n < L::kH) {
         const size_t e = L::w1 + (size_t)n * L::kIn + k;
         if (f.fused_adam) {
-          adam_upd(pv[r], mv[r], vv[r], acc[r], ac);
+          adam_upd(pv[r], mv[r], vv[r], acc[u][r], ac);
           f.m[e] = mv[r];
           f.v[e] = vv[r];
           f.p[e] = pv[r];
         } else {
-          f.g[e] = acc[r];
+          f.g[e] = acc[u][r];
         }
       }
     }
   }
   if (kg == 0 && tid < 16 && 16 * nt + tid < L::kH) {
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int b = 0; b < B; b += 4)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) s[k] += dh1s[(b + k) * 16 + tid];
     const size_t e = L::b1 + 16 * nt + tid;
-    apply_grad(f, e, f.p[e], (s[0] + s[1]) + (s[2] + s[3]), ac);
+    apply_grad(f, e, f.p[e], (s1[0] + s1[1]) + (s1[2] + s1[3]), ac);
   }
 }
 
-size_t bwd2_lds(int B) { return sizeof(float) * ((size_t)B * kDhP + kRS * 16 + (size_t)B * 16); }
-size_t bwd1_lds(int B) { return sizeof(float) * ((size_t)B * 16 + (size_t)B * 112); }
+size_t bwd2_lds(int Bp) {
+  const size_t bc = Bp < kBC2 ? Bp : kBC2;
+  const size_t main = bc * kDhP + kRS * 16 + bc * 16, aux = (size_t)Bp * 16;  // aux: the W3 blocks' dlogits
+  return sizeof(float) * (main > aux ? main : aux);
+}
+size_t bwd1_lds(int Bp) {
+  const size_t bc = Bp < kBC1 ? Bp : kBC1;
+  return sizeof(float) * (bc * 16 + bc * 112);
+}
 
 }  // namespace
 }  // namespace mlp
@@ -490,18 +522,19 @@ size_t bwd1_lds(int B) { return sizeof(float) * ((size_t)B * 16 + (size_t)B * 11
 using namespace mlp;
 
 static void check(const MlpFused& f) {
-  MX_CHECK(f.B % 16 == 0 && f.B >= 16 && f.B <= 128, "fused MLP engine needs batch % 16 == 0 and 16 <= B <= 128");
+  MX_CHECK(f.B >= 1 && f.B <= kMlpMaxBatch && f.Bp == (f.B + 15) / 16 * 16,
+           "fused MLP engine: 1 <= batch <= 512, Bp = batch rounded up to 16");
 }
 
 void mlp_fused_forward(const MlpFused& f, hipStream_t st) {
   check(f);
-  const dim3 grid((f.B / 16) * kNT);
+  const dim3 grid((f.Bp / 16) * kNT);
   if (f.synth)
     MX_LAUNCH((fwd_kernel<MlpLayout::kIn, true>), grid, dim3(256), 0, st, f);
   else
     MX_LAUNCH((fwd_kernel<MlpLayout::kIn, false>), grid, dim3(256), 0, st, f);
   MX_LAUNCH((fwd_kernel<MlpLayout::kH, false>), grid, dim3(256), 0, st, f);
-  MX_LAUNCH(head_kernel, dim3((f.B / 16) * 8), dim3(256), 0, st, f);
+  MX_LAUNCH(head_kernel, dim3((f.Bp / 16) * 8), dim3(256), 0, st, f);
 }
 
 void mlp_fused_backward2(const MlpFused& f, hipStream_t st) {
@@ -511,11 +544,11 @@ void mlp_fused_backward2(const MlpFused& f, hipStream_t st) {
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  MX_LAUNCH(bwd2_kernel, dim3(kK4A + 4), dim3(256), bwd2_lds(f.B), st, f);
+  MX_LAUNCH(bwd2_kernel, dim3(kK4A + 4), dim3(256), bwd2_lds(f.Bp), st, f);
 }
 
 void mlp_fused_backward1(const MlpFused& f, hipStream_t st) {
-  MX_LAUNCH(bwd1_kernel, dim3(kNT * 7), dim3(256), bwd1_lds(f.B), st, f);
+  MX_LAUNCH(bwd1_kernel, dim3(kNT * 7), dim3(256), bwd1_lds(f.Bp), st, f);
 }
 
 }  // namespace mx

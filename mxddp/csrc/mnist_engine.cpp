@@ -43,7 +43,8 @@ size_t ws_floats(int B) {
 }
 }  // namespace
 
-size_t MnistLayout::workspace_bytes(int B) { return ws_floats(B) * 4; }
+// every [B] buffer has the padded row count of the fused kernels (16-row MFMA tiles)
+size_t MnistLayout::workspace_bytes(int B) { return ws_floats(MnistLayout::padded(B)) * 4; }
 
 MnistEngine::MnistEngine(int batch, uintptr_t params, uintptr_t grads, uintptr_t mom, uintptr_t workspace,
                          size_t workspace_bytes, Comm* comm, uint64_t seed, float momentum, float weight_decay,
@@ -53,25 +54,31 @@ MnistEngine::MnistEngine(int batch, uintptr_t params, uintptr_t grads, uintptr_t
       metrics_(reinterpret_cast<float*>(metrics_dev)), comm_(comm), seed_(seed), momentum_(momentum),
       wd_(weight_decay), variant_(kernel_variant) {
   MX_CHECK(B_ > 0, "batch must be positive");
+  // the fused kernels run whole 16-row tiles: a partial last tile is padded with rows that carry
+  // no loss (F5 masks them); the generic variant runs the exact batch
+  Bp_ = variant_ == 1 ? MnistLayout::padded(B_) : B_;
   Carve c{reinterpret_cast<char*>(workspace), 0, workspace_bytes};
-  x_ = c.take<float>(B_ * 784);
-  y_ = c.take<int32_t>(B_);
-  a1_ = c.take<float>((size_t)B_ * 21632);
-  c2_ = c.take<float>((size_t)B_ * 36864);
-  pool_ = c.take<float>((size_t)B_ * 9216);
-  idx_ = c.take<int32_t>((size_t)B_ * 9216);
-  h_ = c.take<float>(B_ * 256);  // int64 [B][128] on the fused path, float [B][128] on the generic one
-  logits_ = c.take<float>(B_ * 10);
-  dlogits_ = c.take<float>(B_ * 10);
-  dh_ = c.take<float>(B_ * 128);
-  dp_ = c.take<float>((size_t)B_ * 9216);
-  dc2_ = c.take<float>((size_t)B_ * 36864);
-  da1_ = c.take<float>((size_t)B_ * 21632);
+  x_ = c.take<float>(Bp_ * 784);
+  y_ = c.take<int32_t>(Bp_);
+  a1_ = c.take<float>((size_t)Bp_ * 21632);
+  c2_ = c.take<float>((size_t)Bp_ * 36864);
+  pool_ = c.take<float>((size_t)Bp_ * 9216);
+  idx_ = c.take<int32_t>((size_t)Bp_ * 9216);
+  h_ = c.take<float>(Bp_ * 256);  // int64 [B][128] on the fused path, float [B][128] on the generic one
+  logits_ = c.take<float>(Bp_ * 10);
+  dlogits_ = c.take<float>(Bp_ * 10);
+  dh_ = c.take<float>(Bp_ * 128);
+  dp_ = c.take<float>((size_t)Bp_ * 9216);
+  dc2_ = c.take<float>((size_t)Bp_ * 36864);
+  da1_ = c.take<float>((size_t)Bp_ * 21632);
   tmpl_ = c.take<float>(10 * 784);
   counter_ = c.take<int32_t>(4);
-  scratch_ = c.take<float>(mnist_fused_scratch_floats(B_));
+  scratch_ = c.take<float>(mnist_fused_scratch_floats(Bp_));
   MX_HIP_CHECK(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
   MX_HIP_CHECK(hipMemsetAsync(counter_, 0, 16, s_));
+  // a caller's batch fills rows 0..B-1 only: the pad rows stay finite zeros (0 * NaN would not)
+  MX_HIP_CHECK(hipMemsetAsync(x_, 0, sizeof(float) * Bp_ * 784, s_));
+  MX_HIP_CHECK(hipMemsetAsync(y_, 0, sizeof(int32_t) * Bp_, s_));
   synth_templates(tmpl_, 10, 784, seed_ ^ 0x5eedull, s_);  // identical on every rank
   // Two buckets in backward order: [fc1.w .. fc2.b] (4.72 MB, ready right after the fc
   // backward) and [conv1.w .. conv2.b] (75 KB, ready at the end).  The big bucket's
@@ -166,7 +173,8 @@ MnistFused MnistEngine::fused_args() const {
   const int rank = comm_ ? comm_->rank() : (reducer_ && reducer_->peer() ? reducer_->peer()->rank() : 0);
   const uint64_t data_seed = seed_ + rank * 7919ull;  // per-rank data shard
   MnistFused f{};
-  f.B = B_;
+  f.B = Bp_;
+  f.nB = B_;
   f.x = x_;
   f.y = y_;
   f.p = p_;
@@ -372,7 +380,7 @@ void MnistEngine::forward_only(uintptr_t x, uintptr_t logits, int B) {
   MX_CHECK(B <= B_, "eval batch larger than engine batch");
   fwd(reinterpret_cast<const float*>(x), reinterpret_cast<float*>(logits), B);
   // the generic forward stores into h_, which the fused F3 uses as a zeroed split-K accumulator
-  if (variant_ == 1) MX_HIP_CHECK(hipMemsetAsync(h_, 0, sizeof(long long) * B_ * 128, s_));
+  if (variant_ == 1) MX_HIP_CHECK(hipMemsetAsync(h_, 0, sizeof(long long) * Bp_ * 128, s_));
 }
 
 void MnistEngine::sync() { MX_HIP_CHECK(hipStreamSynchronize(s_)); }

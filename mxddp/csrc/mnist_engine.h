@@ -31,6 +31,7 @@ struct MnistLayout {
   static constexpr size_t w1 = 0, b1 = 288, w2 = 320, b2 = 18752, fw1 = 18816, fb1 = 1198464, fw2 = 1198592,
                           fb2 = 1199872, total = 1199882;
   static size_t workspace_bytes(int B);
+  static int padded(int B) { return (B + 15) / 16 * 16; }  // rows of the fused kernels' buffers
 };
 
 class MnistEngine {
@@ -135,7 +136,8 @@ class MnistEngine {
   int steps_per_graph_ = 1;
   bool small_first_ = false;
   void fwd(const float* x, float* logits_out, int B);
-  int B_;
+  int B_;   // batch
+  int Bp_;  // rows of the workspace buffers (fused variant: B_ rounded up to 16)
   float *p_, *g_, *m_;
   float *x_, *a1_, *c2_, *pool_, *h_, *logits_, *dlogits_, *dh_, *dp_, *dc2_, *da1_, *tmpl_, *scratch_;
   int32_t *y_, *idx_, *counter_;

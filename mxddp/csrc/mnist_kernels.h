@@ -9,7 +9,8 @@
 namespace mx {
 
 struct MnistFused {
-  int B;
+  int B;                 // rows of every [B] buffer: the batch rounded up to the 16-row MFMA tile
+  int nB;                // the real batch (loss / accuracy / 1/B); rows nB.. get zero loss gradient
   float* x;              // [B,1,28,28]
   int32_t* y;            // [B]
   float* p;              // flat params (MnistLayout offsets)

@@ -576,6 +576,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // ---- head: softmax / NLL / accuracy / dlogits (one thread per row)
   float loss_v = 0.f, corr_v = 0.f;
   if (tid < B) {
+    // rows f.nB.. pad the last 16-row tile (batch not a multiple of 16): no loss, no accuracy,
+    // zero dlogits -- so they add nothing to any gradient downstream
+    const float live = tid < f.nB ? 1.f : 0.f;
     float* l = lg + tid * kF5LgP;
     float mx = l[0];
     int am = 0;
@@ -590,9 +593,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     float ly = 0.f;
 #pragma unroll
     for (int c = 0; c < 10; ++c) ly = c == y ? l[c] : ly;
-    loss_v = lse - ly;
-    corr_v = am == y ? 1.f : 0.f;
-    const float inv = 1.f / (float)B;
+    loss_v = (lse - ly) * live;
+    corr_v = am == y ? live : 0.f;
+    const float inv = live / (float)f.nB;
 #pragma unroll
     for (int c = 0; c < 10; ++c) l[c] = (__expf(l[c] - lse) - (c == y ? 1.f : 0.f)) * inv;
 #pragma unroll
@@ -908,7 +911,8 @@ void mnist_set_wt_stores(int mask) { g_wt_stores = mask & 7; }
 int mnist_wt_stores() { return g_wt_stores; }
 
 static void check(const MnistFused& f) {
-  MX_CHECK(f.B % 16 == 0 && f.B >= 16 && f.B <= 128, "fused MNIST engine needs batch % 16 == 0 and 16 <= B <= 128");
+  MX_CHECK(f.B % 16 == 0 && f.B >= 16 && f.B <= 128 && f.nB >= 1 && f.nB <= f.B && f.B - f.nB < 16,
+           "fused MNIST engine: 1 <= batch <= 128, buffers padded to the next multiple of 16");
 }
 
 static void set_lds_limits() {

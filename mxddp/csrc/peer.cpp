@@ -138,6 +138,15 @@ void PeerComm::set_blocks(int b) {
   blocks_ = b;  // every rank must use the same value (flag sets are per block)
 }
 
+void PeerComm::reset_state() {
+  MX_HIP_CHECK(hipSetDevice(dev_));
+  MX_HIP_CHECK(hipDeviceSynchronize());
+  MX_HIP_CHECK(hipMemset(sig_, 0, sbytes_));
+  MX_HIP_CHECK(hipMemset(epoch_, 0, kPeerMaxBlocks * sizeof(uint32_t)));
+  MX_HIP_CHECK(hipDeviceSynchronize());
+  reset_error();
+}
+
 int PeerComm::error() const { return __atomic_load_n(err_host_, __ATOMIC_ACQUIRE); }
 void PeerComm::reset_error() { __atomic_store_n(err_host_, 0, __ATOMIC_RELEASE); }
 
@@ -155,7 +164,7 @@ bool PeerComm::coschedule_args(void* data, size_t count, RedOp op, PeerArgs* a, 
   a->timeout = timeout_;
   a->rank = rank_;
   a->ws = ws_;
-  a->fence = fence_;
+  a->fence = fence_ | ((withhold_ & 2) ? 4 : 0);
   a->scale = op == RedOp::kAvg ? 1.f / static_cast<float>(ws_) : 1.f;
   a->data = data;
   a->count = static_cast<long long>(count);
@@ -186,7 +195,7 @@ void PeerComm::all_reduce(void* data, size_t count, DType t, hipStream_t st, Red
   a.timeout = timeout_;
   a.rank = rank_;
   a.ws = ws_;
-  a.fence = fence_;
+  a.fence = fence_ | ((withhold_ & 1) ? 4 : 0);
   a.scale = op == RedOp::kAvg ? 1.f / static_cast<float>(ws_) : 1.f;
   for (size_t off = 0; off < count; off += per) {
     a.data = static_cast<char*>(data) + off * esz;

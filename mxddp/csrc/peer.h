@@ -52,7 +52,8 @@ struct PeerArgs {
   long long timeout;              // s_memrealtime ticks (100 MHz)
   float scale;                    // applied to the sum (1 = sum, 1/ws = average)
   int rank, ws;
-  int fence;                      // bit 0: system release before flag stores; bit 1: acquire after waits
+  int fence;                      // bit 0: system release before flag stores; bit 1: acquire after waits;
+                                  // bit 2: withhold this rank's flags (PeerComm::set_withhold, tests)
 };
 
 // host-side partition shared by the kernel and the tests: chunk (elements) per rank and
@@ -89,7 +90,17 @@ class PeerComm {
   int error() const;                                 // 0 = ok; else 1 + (peer that timed out)
   void reset_error();
   void set_blocks(int b);
-  void set_fence(int f) { fence_ = f; }
+  void set_fence(int f) { fence_ = f & 3; }
+  // tests only: this rank stops publishing its flags (a peer that never arrives), so the
+  // fail-fast / autotune-drop paths can be exercised on one box.  mask bit 0: the standalone
+  // all-reduce kernels; bit 1: exchanges co-scheduled inside another kernel (coschedule_args /
+  // oneshot_args, taken when that kernel's launch or graph is built)
+  void set_withhold(int mask) { withhold_ = mask; }
+  // every rank, device idle and host-synchronised with its peers (parallel/peer.py: resync):
+  // zero this rank's flags, per-block epochs and error word, so the next exchange starts a
+  // fresh epoch sequence on every rank -- after a timed-out exchange left the ranks' epochs
+  // apart, or before another kernel family with its own block partition takes the buffers
+  void reset_state();
   void set_timeout_ms(double ms) { timeout_ = static_cast<long long>(ms * 1e5); }
   // buckets up to this size take the one-shot kernel (every rank must use the same value)
   void set_oneshot_bytes(long long b) { oneshot_bytes_ = b; }
@@ -114,6 +125,7 @@ class PeerComm {
   uint32_t* peer_sig_[kPeerMaxRanks] = {};
   bool opened_ = false, local_ = false;
   int fence_ = 1;
+  int withhold_ = 0;
   long long timeout_ = 3000000000ll;  // 30 s
   long long oneshot_bytes_ = 256 << 10;
   std::string mem_kind_;

@@ -16,18 +16,24 @@ __device__ __forceinline__ uint32_t* flag_at(uint32_t* sig, int set, int b, int 
   return sig + ((size_t)set * kPeerMaxBlocks + b) * kPeerMaxRanks + p;
 }
 
-// lanes 0..ws-1 (except `rank`) of wave 0 each wait for one peer's flag; bounded.
+// lanes 0..ws-1 (except `rank`) of wave 0 each wait for one peer's flag; bounded.  Fail fast:
+// once the error word is set (a peer timed out in this or an earlier launch) no lane waits
+// again -- the bucket is garbage either way and the host raises at its next check -- so a
+// broken transport costs ONE timeout, not one per block per later launch.
 __device__ __forceinline__ void wait_peers(const PeerArgs& a, int set, int b, uint32_t ep) {
   const int t = threadIdx.x;
-  if (t < a.ws && t != a.rank) {
+  if (t < a.ws && t != a.rank && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
     uint32_t* f = flag_at(a.sig[a.rank], set, b, t);
     const long long t0 = wall_clock64();
+    unsigned spins = 0;
     while (static_cast<int32_t>(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - ep) < 0) {
       __builtin_amdgcn_s_sleep(1);
       if (wall_clock64() - t0 > a.timeout) {
         __hip_atomic_store(a.err, 1 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
+      // another block / lane already timed out: stop waiting (host-mapped word, polled rarely)
+      if ((++spins & 255u) == 0 && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
     }
   }
   if ((a.fence & 2) && t < kWave) {  // acquire (only needed when the exchange memory is cached)
@@ -47,7 +53,9 @@ __device__ __forceinline__ void signal_peers(const PeerArgs& a, int set, int b, 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       vm_drain();
     }
-    if (t < a.ws && t != a.rank)
+    // fence bit 2 (PeerComm::set_withhold, tests only): this rank never publishes its flags,
+    // i.e. it behaves like a peer that stopped arriving
+    if (t < a.ws && t != a.rank && !(a.fence & 4))
       __hip_atomic_store(flag_at(a.sig[t], set, b, a.rank), ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }

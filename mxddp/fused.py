@@ -162,12 +162,19 @@ class FusedTrainerBase:
         each configured communicator variant, or the direct xGMI peer all-reduce when it
         validated) x bucket strategy (``STRATEGIES``: "ovl" first bucket all-reduced on the side
         stream overlapping the rest of the backward, "inl" the buckets in order on the compute
-        stream, "one" a single all-reduce of the whole gradient, "co" (MNIST, peer transport) the
-        exchange co-scheduled inside the conv-backward launch) x (eager launches, or the step
-        captured in one hipGraph; peer-transport graphs always, RCCL-in-graph with
-        MXDDP_AUTOTUNE_GRAPHS=1).  The slowest rank's time decides, so every rank picks the same
-        strategy.  ``restore``: the trial steps are scratch -- the training state and step count
-        are put back afterwards.  Returns {candidate: ms/step}."""
+        stream, "one" a single all-reduce of the whole gradient, "co" the exchange co-scheduled
+        inside another launch of the step) x (eager launches, or the step captured in one
+        hipGraph; peer-transport graphs always, RCCL-in-graph with MXDDP_AUTOTUNE_GRAPHS=1).  The
+        slowest rank's time decides, so every rank picks the same strategy.
+
+        Fail fast, never raise for a peer candidate: before a peer-transport strategy is timed,
+        two steps of it run from a snapshot with the 2 s validate timeout and are compared with
+        the same two steps over RCCL (or over the standalone peer kernel when the job has no
+        RCCL); a strategy that times out or disagrees on ANY rank is marked ``inf`` on every
+        rank, the transport is re-synchronised (peer.resync) and the training state restored.  A
+        standalone-kernel failure, or a failure while timing, drops the peer transport for the
+        rest of the autotune.  ``restore``: the trial steps are scratch -- the training state and
+        step count are put back afterwards.  Returns {candidate: ms/step}."""
         from .parallel import comm as pc
 
         if include_graphs is None:
@@ -181,7 +188,7 @@ class FusedTrainerBase:
             transports = ["peer"]
         elif self.transport == "rccl":
             transports = rccl_names
-        snap = self.snapshot() if restore else None
+        snap0 = self.snapshot()
         cands = []
         for tr in transports:
             strats = self._candidate_strategies(tr)
@@ -189,47 +196,151 @@ class FusedTrainerBase:
             if self.use_graph and (include_graphs or tr == "peer"):
                 cands += [(tr, 1, st) for st in strats]
         results = {}
-        for tr, mode, strat in cands:
-            self.eng.uncapture()
-            self._use_transport(tr, comms)
-            self._set_buckets(strat)
-            failed = 0.0
-            try:  # capture issues no collective, so a local failure here is safe to agree on
-                if mode:
-                    self._capture(mode)
-            except RuntimeError:
-                failed = 1.0
-            # every rank reaches this all-reduce before any collective of the candidate, so a
-            # candidate that failed to capture on ANY rank is skipped by ALL ranks together
-            if pc.all_reduce_max(failed) > 0:
+        self._peer_ok = {}   # strategy -> agreed validation verdict (peer transport)
+        self._peer_ref = None
+        peer_dead = False
+        if self.peer is not None:
+            self.peer.set_timeout_ms(float(os.environ.get("MXDDP_PEER_VALIDATE_TIMEOUT_MS", "2000")))
+        try:
+            for tr, mode, strat in cands:
+                key = (tr, mode, strat)
+                if tr == "peer":
+                    if peer_dead:
+                        results[key] = float("inf")
+                        continue
+                    if strat not in self._peer_ok:
+                        self._peer_ok[strat] = self._validate_peer_strategy(strat, comms, rccl_names, snap0)
+                        if not self._peer_ok[strat] and strat != "co":
+                            peer_dead = True  # the standalone kernels themselves fail: no peer candidate can work
+                    if not self._peer_ok[strat]:
+                        results[key] = float("inf")
+                        continue
+                    self._peer_resync()
                 self.eng.uncapture()
-                results[(tr, mode, strat)] = float("inf")
-                continue
-            # replay errors are not swallowed: peers may already be inside the collectives
-            self.eng.replay(2)
-            self.eng.sync()
-            pc.barrier()
-            t0 = time.perf_counter()
-            self.eng.replay(trial_steps)
-            self.eng.sync()
-            dt = pc.all_reduce_max(time.perf_counter() - t0)
-            self._check_peer()
-            self.steps += 2 + trial_steps
-            results[(tr, mode, strat)] = dt / trial_steps * 1e3
-        best = min(results, key=results.get)
+                self._use_transport(tr, comms)
+                self._set_buckets(strat)
+                failed = 0.0
+                try:  # capture issues no collective, so a local failure here is safe to agree on
+                    if mode:
+                        self._capture(mode)
+                except RuntimeError:
+                    failed = 1.0
+                # every rank reaches this all-reduce before any collective of the candidate, so a
+                # candidate that failed to capture on ANY rank is skipped by ALL ranks together
+                if pc.all_reduce_max(failed) > 0:
+                    self.eng.uncapture()
+                    results[key] = float("inf")
+                    continue
+                # HIP errors of a replay are not swallowed (peers may be inside the collectives);
+                # a peer exchange that timed out is: its error word is agreed on below
+                self.eng.replay(2)
+                self.eng.sync()
+                pc.barrier()
+                t0 = time.perf_counter()
+                self.eng.replay(trial_steps)
+                self.eng.sync()
+                dt = pc.all_reduce_max(time.perf_counter() - t0)
+                self.steps += 2 + trial_steps
+                bad = 1.0 if (tr == "peer" and self.peer.error()) else 0.0
+                if pc.all_reduce_max(bad) > 0:
+                    results[key] = float("inf")
+                    peer_dead = True
+                    self.eng.uncapture()
+                    self._use_transport(rccl_names[0] if rccl_names else "peer", comms)
+                    self._peer_resync()
+                    self.restore(snap0)  # the failed trial's steps trained on garbage gradients
+                    continue
+                results[key] = dt / trial_steps * 1e3
+        finally:
+            if self.peer is not None:
+                self.peer.set_timeout_ms(float(os.environ.get("MXDDP_PEER_TIMEOUT_MS", "30000")))
+        best = min(results, key=results.get) if results else None
+        if best is None or results[best] == float("inf"):
+            raise RuntimeError(f"autotune: no launch strategy works on this machine ({results})")
         self.eng.uncapture()
+        if best[0] == "peer":
+            self._peer_resync()
         self._use_transport(best[0], comms)
         self._set_buckets(best[2])
         if best[1]:
             self._capture(best[1])
         self._capture_done = True
-        if snap is not None:
-            self.restore(snap)
+        if restore:
+            self.restore(snap0)
         else:
             self.read_metrics(reset=True)
         self.tuned = {"transport": best[0], "graph_mode": best[1], "buckets": best[2],
                       "trials_ms": {f"{t}/{m}/{s}": round(v, 4) for (t, m, s), v in results.items()}}
+        if self._peer_ok:
+            self.tuned["peer_validated"] = dict(self._peer_ok)
         return results
+
+    # ------------------------------------------------------------ candidate validation
+    def _peer_resync(self):
+        from .parallel import peer as _peer
+
+        if self.peer is not None:
+            _peer.resync(self.peer)
+
+    def _state_delta(self, snap: dict) -> torch.Tensor:
+        """What a step changed: parameters and the float optimizer state, minus the snapshot."""
+        parts = [(self.params - snap["params"]).flatten()]
+        for k, t in self._opt_tensors().items():
+            if t.dtype == torch.float32 and t.numel() == self.params.numel():
+                parts.append((t - snap["opt"][k]).flatten())
+        return torch.cat(parts)
+
+    def _run_from(self, snap: dict, steps: int = 2) -> torch.Tensor:
+        """`steps` eager steps from `snap` with the current strategy; returns their state delta
+        and puts the trainer back to `snap` (scratch steps, counted in discarded_steps)."""
+        self.restore(snap)
+        self.eng.replay(steps)
+        self.eng.sync()
+        d = self._state_delta(snap)
+        self.restore(snap)
+        self.discarded_steps = getattr(self, "discarded_steps", 0) + steps
+        return d
+
+    def _validate_peer_strategy(self, strat: str, comms: dict, rccl_names: list, snap0: dict) -> bool:
+        """Collective: two steps of the peer transport with bucket strategy `strat` against the
+        same two steps of the reference (RCCL's first variant with its first strategy, or the
+        standalone peer kernel with the first strategy when the job has no RCCL).  The verdict is
+        agreed over the ranks; a failed candidate leaves the transport re-synchronised."""
+        from .parallel import comm as pc
+
+        if self._peer_ref is None:
+            ref_tr = rccl_names[0] if rccl_names else "peer"
+            ref_strat = self._candidate_strategies(ref_tr)[0]
+            self.eng.uncapture()
+            if ref_tr == "peer":
+                self._peer_resync()
+            self._use_transport(ref_tr, comms)
+            self._set_buckets(ref_strat)
+            ref = self._run_from(snap0)
+            ok = not (ref_tr == "peer" and self.peer.error())
+            if pc.all_reduce_max(0.0 if ok else 1.0) > 0:
+                self._peer_resync()
+                if ref_tr == "peer":
+                    self._peer_ok[ref_strat] = False
+                    return False
+                raise RuntimeError("autotune: the RCCL reference step failed")
+            self._peer_ref = ref
+            if ref_tr == "peer" and strat == ref_strat:
+                return True
+        self.eng.uncapture()
+        self._peer_resync()
+        self._use_transport("peer", comms)
+        self._set_buckets(strat)
+        d = self._run_from(snap0)
+        ok = not self.peer.error()
+        if ok:
+            ref = self._peer_ref
+            rel = ((d - ref).norm() / ref.norm().clamp_min(1e-30)).item()
+            ok = rel <= float(os.environ.get("MXDDP_VALIDATE_RTOL", "1e-3"))
+        ok = pc.all_reduce_max(0.0 if ok else 1.0) == 0.0
+        if not ok:
+            self._peer_resync()
+        return ok
 
     def _rccl_candidates(self) -> dict:
         """{variant name: Comm} the autotune times: the caller's list, else (world size > 1, or
@@ -492,6 +603,30 @@ class FusedReplicas:
         if n > 0:
             self._each(lambda t: t.eng.replay(n))
             self._each(lambda t: setattr(t, "steps", t.steps + n))
+
+    def timed_steps(self, n: int) -> float:
+        """Run n steps; returns the slowest replica's DEVICE time of them in seconds.  Every
+        replica first runs one tiny peer all-reduce on its own stream, so the replicas' start
+        events fire together however far apart the host launched them (bench.py)."""
+        C = native()
+        self.synchronize()
+        evs = []
+        for t, d, pc in zip(self.trainers, self.devices, self.peers):
+            with torch.cuda.device(d):
+                if pc is not None:
+                    buf = torch.zeros(64, device=d)
+                    t.stream.wait_stream(torch.cuda.current_stream(d))
+                    pc.all_reduce(buf.data_ptr(), buf.numel(), C.DType.f32, t.eng.stream, C.RedOp.sum)
+                    buf.record_stream(t.stream)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(t.stream)
+                evs.append((e0, e1))
+        self.step(n)
+        for t, d, (_, e1) in zip(self.trainers, self.devices, evs):
+            with torch.cuda.device(d):
+                e1.record(t.stream)
+        self.synchronize()
+        return max(e0.elapsed_time(e1) for e0, e1 in evs) * 1e-3
 
     def set_batch(self, x: torch.Tensor, y: torch.Tensor):
         xs, ys = x.chunk(len(self.trainers)), y.chunk(len(self.trainers))

@@ -36,8 +36,8 @@ class FusedMlpTrainer(AdamTrainerBase):
                  graph_mode: int | None = None, peer=None, force_collectives: bool = False, transport: str = "auto",
                  rccl_variants=None):
         C = native()
-        if batch % 16 or not 16 <= batch <= 128:
-            raise ValueError("FusedMlpTrainer: batch must be a multiple of 16 in [16, 128]")
+        if not 1 <= batch <= C.MLP_MAX_BATCH:
+            raise ValueError(f"FusedMlpTrainer: batch must be in [1, {C.MLP_MAX_BATCH}]")
         if init_model is not None and tuple(init_model.l1.weight.shape) != (1000, 784):
             raise ValueError("FusedMlpTrainer: the native step is built for the reference's 1000 units")
         n = self._init_flat(batch, device, comm, seed, init_model)

@@ -247,7 +247,10 @@ class _Conv(torch.autograd.Function):
                                       _p(link.mask) if bpart is not None else 0,
                                       bool(link.relu) if bpart is not None else False, _p(amask))
             if bpart is not None and rows > 0:
-                link.pre = (bpart, rows, dx.data_ptr())
+                # (partials, rows, the gradient tensor's address and version): autograd may sum
+                # another consumer's gradient INTO dx in place (var.add_(old_var)) before the BN
+                # sees it -- same address, bumped version -- and then these partials are stale
+                link.pre = (bpart, rows, dx.data_ptr(), dx._version)
             if add is not None:
                 j.consumed = True
             if ctx.deposit is not None:
@@ -356,10 +359,11 @@ class _BN(torch.autograd.Function):
         dg, db = (gs, bs) if direct else (torch.empty((C,), device=x.device), torch.empty((C,), device=x.device))
         scr = torch.empty((Cn.nhwc_bn_scratch_floats(N * H * W, C),), device=x.device, dtype=torch.float32)
         # backward statistics from the consuming conv's data-gradient epilogue, valid only for
-        # exactly the gradient tensor that conv wrote
+        # exactly the gradient tensor that conv wrote, unmodified since (a second consumer's
+        # gradient accumulated into it in place bumps its version)
         pre = ctx.link.pre
         ctx.link.pre = None
-        if pre is not None and pre[2] != dy.data_ptr():
+        if pre is not None and (pre[2] != dy.data_ptr() or pre[3] != dy._version):
             pre = None
         BN_BWD_STATS["epilogue" if pre is not None else "pass"] += 1
         Cn.nhwc_bn_bwd(dy.data_ptr(), x.data_ptr(), 0, _p(gamma), mean.data_ptr(), invstd.data_ptr(),

@@ -226,6 +226,32 @@ def all_reduce_max(value: float) -> float:
     return float(t.item())
 
 
+_ALIGN_BUF: dict = {}
+
+
+def device_align(stream, comm=None, peer=None) -> str:
+    """Device-side start line of a timed region (bench.py): one tiny all-reduce enqueued on
+    `stream` -- over `comm` (RCCL) when given, else over the peer transport -- so every rank's
+    device leaves it at (nearly) the same moment, whatever the skew with which the ranks' hosts
+    left the preceding host barrier.  A start event recorded on `stream` right after it is then
+    a common start for all ranks.  Returns the transport used ("none" at world size 1)."""
+    inf = info()
+    if inf.world_size == 1 or inf.device.type != "cuda":
+        return "none"
+    buf = _ALIGN_BUF.get(inf.device)
+    if buf is None:
+        buf = _ALIGN_BUF[inf.device] = torch.zeros(64, dtype=torch.float32, device=inf.device)
+    C = native()
+    h = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+    if comm is not None:
+        comm.all_reduce(buf.data_ptr(), buf.data_ptr(), buf.numel(), C.DType.f32, C.RedOp.sum, h)
+        return "rccl"
+    if peer is not None:
+        peer.all_reduce(buf.data_ptr(), buf.numel(), C.DType.f32, h, C.RedOp.sum)
+        return "peer"
+    return "none"
+
+
 def all_reduce_sum(values):
     if not dist.is_initialized():
         return list(values)

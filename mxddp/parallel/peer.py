@@ -149,6 +149,30 @@ def pick_transport(pc, rccl, numels: list[int], dtype: str = "f32", iters: int =
     return min(res, key=res.get), res
 
 
+def resync(pc) -> None:
+    """Collective over all ranks: put the peer transport back at a fresh epoch sequence on
+    every rank (after an exchange timed out and left the ranks' per-block epochs apart, or when
+    an exchange with another block partition -- the Keras co-scheduled KX kernel -- takes over
+    the buffers).  Every rank's device is idle before any rank zeroes its flags, and no rank
+    exchanges again before every rank has zeroed them."""
+    inf = _comm.info()
+    if inf.device.type == "cuda":
+        torch.cuda.synchronize(inf.device)
+    _comm.barrier()
+    pc.reset_state()
+    _comm.barrier()
+
+
+def resync_local(pcs, devices) -> None:
+    """resync() for in-process replicas (FusedReplicas): one process owns every PeerComm, so
+    synchronising every device before any reset is the barrier."""
+    for d in devices:
+        torch.cuda.synchronize(d)
+    for pc in pcs:
+        if pc is not None:
+            pc.reset_state()
+
+
 def shutdown():
     global _PEER
     _PEER = None

@@ -14,7 +14,6 @@
 #   prof_mnist   rocprofv3 kernel trace of the MNIST step
 #   pmc_mnist    counter passes of the MNIST step (eager launches, one pass per run)
 #   phase_mnist  in-kernel phase timings of the MNIST step
-#   ab_wt / prof_wt   MNIST bench A/B of the write-through store masks; kernel trace with F5's
 #   keras / keras_rep / keras_ws2 / prof_keras / pmc_keras   Keras CNN fused engine
 #   mlp / mlp_rep / prof_mlp / pmc_mlp                       Chainer MLP
 #   rn32 / rn256 / prof_rn / pmc_rn / rn_stock / rn_layers    ResNet-50 bf16 (rn_layers: per conv shape)
@@ -72,20 +71,8 @@ for step in "$@"; do
     prof_mnist) prof prof_mnist 200 --steps 200 --warmup 20 --min-warmup-ms 0 ;;
     pmc_mnist) pmc pmc_mnist --steps 20 --warmup 2 --no-graph --min-warmup-ms 0 ;;
     phase_mnist) run phase_mnist 300 python bench.py --phase-profile 30 ;;
-    ab_spg)  # driver-length MNIST: 32 steps per graph (16 + 4 launches) vs one 20-step graph, interleaved
-      for r in 1 2 3; do
-        run "ab_spg32_$r" 300 python bench.py --steps 20 --warmup 5 &&
-        run "ab_spg20_$r" 300 python bench.py --steps 20 --warmup 5 --steps-per-graph 20 || exit 1
-      done ;;
-    ab_wt)  # write-through store masks A/B (0 none, 6 F2 + F6W, 7 F5 + F2 + F6W), interleaved long runs
-      for r in 1 2; do
-        run "ab_wt0_$r" 300 python bench.py --steps 2000 --warmup 100 --wt-stores 0 &&
-        run "ab_wt6_$r" 300 python bench.py --steps 2000 --warmup 100 --wt-stores 6 &&
-        run "ab_wt7_$r" 300 python bench.py --steps 2000 --warmup 100 --wt-stores 7 || exit 1
-      done ;;
     diag_join) run diag_join 300 python scripts/diag_join.py ;;
     bench_bn) run bench_bn 300 python scripts/bench_bn.py ;;
-    prof_wt) prof prof_wt 200 --steps 200 --warmup 20 --min-warmup-ms 0 --wt-stores 1 ;;
     coll) run coll 300 python bench.py --steps 2000 --warmup 100 --force-collectives ;;
     replica) run replica 300 python bench.py --impl replica --steps 1000 --warmup 50 ;;
     layers) run layers 300 python bench.py --impl layers --steps 300 --warmup 30 ;;
@@ -101,65 +88,7 @@ for step in "$@"; do
     pmc_mlp) pmc pmc_mlp --model mlp --steps 20 --warmup 2 --no-graph --min-warmup-ms 0 ;;
     rn32) run rn32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 ;;
     rn256) run rn256 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 ;;
-    rn256_t256) run rn256_t256 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --conv-tile256 1 ;;
-    ab_short)  # ResNet-50 batch 256 / 32: two-stage 128-pixel LDS-DMA variant off vs on, interleaved
-      for r in 1 2; do
-        run "ab_short0_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --glds-short 0 &&
-        run "ab_short1_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --glds-short 1 || exit 1
-      done
-      run ab_short0_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --glds-short 0 &&
-      run ab_short1_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --glds-short 1 || exit 1 ;;
-    ab_bngrid)  # ResNet-50 batch 256 / 32: BN apply grids of round 3 (2,048 blocks) vs size-aware
-      for r in 1 2; do
-        run "ab_bngrid2k_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --bn-grid-cap 2048 &&
-        run "ab_bngrid_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 || exit 1
-      done
-      run ab_bngrid2k_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --bn-grid-cap 2048 &&
-      run ab_bngrid_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 || exit 1 ;;
-    ab_t256)  # ResNet-50: 256 x 256 tile on the long-reduction layers off vs on, interleaved
-      for r in 1 2; do
-        run "ab_t256_0_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --conv-tile256 0 &&
-        run "ab_t256_1_$r" 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --conv-tile256 1 || exit 1
-      done
-      run ab_t256_0_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --conv-tile256 0 &&
-      run ab_t256_1_b32 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --conv-tile256 1 || exit 1 ;;
-    rn_layers_short0) run rn_layers_short0 300 python scripts/bench_nhwc_layers.py 256 5 0 0 ;;
-    ab_dst)  # ResNet-50 batch 32 / 256: backward BN statistics in the dgrad epilogue up to a tensor size
-      B32="python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3"
-      B256="python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3"
-      for r in 1 2; do
-        for m in 0 2000000 4000000 1073741824; do
-          run "ab_dst_b32_${m}_$r" 300 env MXDDP_BN_DGRAD_STATS_MAX=$m $B32 || exit 1
-        done
-      done
-      for m in 0 2000000 7000000; do
-        run "ab_dst_b256_${m}" 300 env MXDDP_BN_DGRAD_STATS_MAX=$m $B256 || exit 1
-      done ;;
-    ab_split)  # ResNet-50 batch 32 / 256: generic-kernel split-K threshold (blocks)
-      B32="python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3"
-      B256="python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3"
-      for r in 1 2; do
-        for m in 512 384 256 128; do
-          run "ab_split_b32_${m}_$r" 300 $B32 --split-blocks $m || exit 1
-        done
-      done
-      for m in 512 256; do
-        run "ab_split_b256_${m}" 300 $B256 --split-blocks $m || exit 1
-      done ;;
-    ab_wgt)  # ResNet-50 batch 32 / 256: weight-gradient block target (pixel splits)
-      B32="python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3"
-      B256="python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3"
-      for r in 1 2; do
-        for m in 512 256 1024; do
-          run "ab_wgt_b32_${m}_$r" 300 $B32 --wgrad-target $m || exit 1
-        done
-      done
-      for m in 512 256 1024; do
-        run "ab_wgt_b256_${m}" 300 $B256 --wgrad-target $m || exit 1
-      done ;;
-    rn32_t256) run rn32_t256 300 python bench.py --model resnet50 --dtype bf16 --batch 32 --steps 20 --warmup 3 --conv-tile256 1 ;;
     rn_layers) run rn_layers 300 python scripts/bench_nhwc_layers.py 256 5 ;;
-    rn_layers_t256) run rn_layers_t256 300 python scripts/bench_nhwc_layers.py 256 5 1 ;;
     rn_stock) run rn_stock 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --impl torch --channels-last ;;
     prof_rn32) prof prof_rn32 10 --model resnet50 --dtype bf16 --batch 32 --steps 10 --warmup 2 --min-warmup-ms 0 ;;
     prof_rn) prof prof_rn 3 --model resnet50 --dtype bf16 --batch 256 --steps 3 --warmup 2 --min-warmup-ms 0 ;;
@@ -170,6 +99,9 @@ for step in "$@"; do
     ws2) ws ws2 2 --steps 1000 --warmup 50 ;;
     ws4) ws ws4 4 --steps 500 --warmup 20 ;;
     ws8) ws ws8 8 --steps 200 --warmup 20 ;;
+    ws8_driver) ws ws8_driver 8 --steps 20 --warmup 5 ;;   # the driver's exact 8-rank command
+    ab)  # one A/B pass: AB="bench args" (e.g. AB="--model resnet50 --dtype bf16 --batch 32 --ab wgrad_target=256")
+      run ab 300 python bench.py ${AB:?set AB to the bench arguments} ;;
     keras_ws2) ws keras_ws2 2 --model keras_cnn --steps 300 --warmup 30 ;;
     keras_ws8) ws keras_ws8 8 --model keras_cnn --steps 100 --warmup 10 ;;
     pyr_ws8) ws pyr_ws8 8 --model pyramidnet110 --batch 8 --steps 5 --warmup 2 ;;

@@ -371,6 +371,50 @@ def test_bn_backward_statistics_from_dgrad_epilogue(cuda, glds, stride, relu):
         assert _rel(b, a) < 2e-2
 
 
+@pytest.mark.parametrize("order", ["conv_first", "conv_second"])
+def test_bn_output_read_by_two_convs(cuda, order):
+    """One BN output consumed by TWO convolutions without ``fork``: autograd sums their input
+    gradients, possibly in place into one conv's dx (same address).  The BN backward must then
+    NOT use the statistics that conv's epilogue computed from its own gradient alone: the result
+    equals the separate statistics pass."""
+    from mxddp import native
+
+    C = native()
+    N, Cin, H, W, K = 4, 128, 16, 16, 64
+    torch.manual_seed(12)
+    x = (torch.randn(N, H, W, Cin) + 0.5).to(torch.bfloat16).to(cuda)
+    w1 = (torch.randn(K, Cin, 3, 3) * 0.05).to(cuda)
+    w2 = (torch.randn(K, Cin, 1, 1) * 0.05).to(cuda)
+    gamma, beta = torch.rand(Cin) + 0.5, torch.randn(Cin) * 0.2
+    outs = []
+    try:
+        for fused in (False, True):
+            nhwc._BN_STATS_IN_DGRAD = fused
+            nhwc._BN_DGRAD_STATS_MAX = 0
+            bn = nn.BatchNorm2d(Cin).to(cuda)
+            with torch.no_grad():
+                bn.weight.copy_(gamma)
+                bn.bias.copy_(beta)
+            xg = x.clone().requires_grad_()
+            a, b = w1.clone().requires_grad_(), w2.clone().requires_grad_()
+            y = nhwc.batch_norm(xg, bn, relu=True)
+            if order == "conv_first":
+                c1, c2 = nhwc.conv2d(y, a, 1, 1), nhwc.conv2d(y, b, 1, 0)
+            else:
+                c2, c1 = nhwc.conv2d(y, b, 1, 0), nhwc.conv2d(y, a, 1, 1)
+            g = torch.Generator().manual_seed(5)
+            loss = (c1.float() * torch.randn(c1.shape, generator=g).to(cuda)).sum() + \
+                (c2.float() * torch.randn(c2.shape, generator=g).to(cuda)).sum()
+            loss.backward()
+            torch.cuda.synchronize()
+            outs.append((xg.grad.float().cpu(), bn.weight.grad.cpu(), bn.bias.grad.cpu()))
+    finally:
+        nhwc._BN_STATS_IN_DGRAD = False
+        nhwc._BN_DGRAD_STATS_MAX = _DSTATS_MAX
+    for u, f in zip(*outs):
+        assert _rel(f, u) < 2e-2
+
+
 def test_bn_backward_statistics_residual_join(cuda):
     """A residual block's output BN (ReLU after the residual add, mask bits) feeding the next
     block's first conv and its identity shortcut: the statistics come from the conv's epilogue only

@@ -263,6 +263,46 @@ def _worker(rank, ws, port, mode, q):
                 d = ((ref.params.cpu() - mine).norm() / (ref.params.cpu() - p0).norm()).item()
                 if not d < 1e-3:
                     bad.append(("ddp != global batch", d))
+        elif mode in ("autotune_withhold", "keras_autotune_withhold"):
+            # one rank stops publishing the flags of its CO-SCHEDULED exchanges (the standalone
+            # kernels still work): autotune must validate the co strategy with the short timeout,
+            # drop it on every rank, keep the working peer strategies and finish in seconds
+            import time as _time
+
+            if mode.startswith("keras"):
+                from mxddp.keras_engine import FusedKerasTrainer as T
+            else:
+                from mxddp.engine import FusedMnistTrainer as T
+            from mxddp.parallel import comm as PC
+
+            PC._INFO = PC.DistInfo(rank, ws, rank, ws, "gloo", torch.device("cuda", 0))
+            tr = T(batch=16, device=0, comm=None, peer=pc, seed=3, use_graph=True)
+            if rank == 1:
+                pc.set_withhold(2)
+            tr.step(1)
+            t0 = _time.perf_counter()
+            res = tr.autotune(trial_steps=4)
+            dt = _time.perf_counter() - t0
+            co = {k: v for k, v in res.items() if k[2] == "co"}
+            if not co or any(v != float("inf") for v in co.values()):
+                bad.append(("co not dropped", co))
+            if tr.tuned["buckets"] == "co" or tr.tuned["transport"] != "peer":
+                bad.append(("picked", tr.tuned))
+            if tr.tuned.get("peer_validated", {}).get("co") is not False:
+                bad.append(("validation verdict", tr.tuned.get("peer_validated")))
+            if not dt < 30:
+                bad.append(("autotune took", dt))
+            tr.step(3)
+            tr.synchronize()
+            if pc.error():
+                bad.append(("peer error after autotune", pc.error()))
+            allp = [None] * ws
+            dist.all_gather_object(allp, tr.params.cpu())
+            if any(not torch.equal(allp[0], t) for t in allp):
+                bad.append("ranks diverged after autotune")
+            if rank == 0:
+                print(f"{mode}: autotune {dt:.1f} s, picked {tr.tuned}", flush=True)
+            PC._INFO = None
         elif mode == "timeout":
             pc.set_timeout_ms(300)
             x = torch.ones(10_000, device="cuda")
@@ -338,6 +378,14 @@ def test_ddp_layers_peer_transport_matches_global_batch(cuda):
 
 def test_peer_all_reduce_timeout_reports_missing_peer(cuda):
     _run(2, "timeout")
+
+
+@pytest.mark.parametrize("mode", ["autotune_withhold", "keras_autotune_withhold"])
+def test_autotune_drops_failing_coscheduled_exchange(cuda, mode):
+    """A co-scheduled exchange that fails on one rank (here: rank 1 withholds its flags) is
+    validated with the 2 s timeout before it is timed, marked inf on every rank and dropped;
+    autotune picks a working peer strategy within seconds and the ranks keep training in step."""
+    _run(2, mode)
 
 
 def _replicas_worker(graph, q):
