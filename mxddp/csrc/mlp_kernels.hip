@@ -321,9 +321,10 @@ __global__ __launch_bounds__(256) void bwd2_kernel(MlpFused f) {
   const int bid = xcd_remap(blockIdx.x, kK4A);  // the tiles of one row slice share an XCD's L2
   const int ri = bid / kNT, jt = bid - ri * kNT;
   const int i0 = kRS * ri;
-  float* dh2s = sm;                 // [kBC2][260]
-  float* w2s = dh2s + kBC2 * kDhP;  // [256][16]
-  float* h1s = w2s + kRS * 16;      // [kBC2][16]
+  const int BC = min(B, kBC2);      // rows per pass (the dynamic LDS is sized for BC, bwd2_lds)
+  float* dh2s = sm;                 // [BC][260]
+  float* w2s = dh2s + BC * kDhP;    // [256][16]
+  float* h1s = w2s + kRS * 16;      // [BC][16]
   {  // W2 tile: thread = row i0 + tid, 16 columns (zero outside the 1000 x 1000 matrix)
     const int i = min(i0 + tid, L::kH - 1);
     const float4* src = reinterpret_cast<const float4*>(f.p + L::w2 + (size_t)i * L::kH + 16 * jt);
@@ -343,8 +344,8 @@ __global__ __launch_bounds__(256) void bwd2_kernel(MlpFused f) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) dw[q] = f32x4{0.f, 0.f, 0.f, 0.f};
   float s2[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int c0 = 0; c0 < B; c0 += kBC2) {
-    const int bc = min(kBC2, B - c0);
+  for (int c0 = 0; c0 < B; c0 += BC) {
+    const int bc = min(BC, B - c0);
     if (c0) __syncthreads();  // the previous pass's LDS reads are done
     for (int k = tid; k < bc * 64; k += 256) {  // dh2 columns i0 .. i0 + 255 (pad columns are 0)
       const int b = k >> 6, c4 = k & 63;
@@ -433,16 +434,17 @@ __global__ __launch_bounds__(256) void bwd1_kernel(MlpFused f) {
   const AdamC ac = adam_consts(f);
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int nt = bid / 7, kg = bid - nt * 7;
-  float* dh1s = sm;              // [kBC1][16]
-  float* xs = dh1s + kBC1 * 16;  // [kBC1][112]
+  const int BC = min(B, kBC1);   // rows per pass (the dynamic LDS is sized for BC, bwd1_lds)
+  float* dh1s = sm;              // [BC][16]
+  float* xs = dh1s + BC * 16;    // [BC][112]
   if (blockIdx.x == 0 && tid == 0 && f.fused_adam)
     __hip_atomic_store(f.adam_state + 1, __hip_atomic_load(f.adam_state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1,
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   float s1[4] = {0.f, 0.f, 0.f, 0.f};
   const size_t pl = (size_t)B * L::kHP;
-  for (int c0 = 0; c0 < B; c0 += kBC1) {  // one pass for B <= 256; fixed accumulation order
-    const int bc = min(kBC1, B - c0);
+  for (int c0 = 0; c0 < B; c0 += BC) {  // one pass for B <= 256; fixed accumulation order
+    const int bc = min(BC, B - c0);
     if (c0) __syncthreads();
     for (int k = tid; k < bc * 16; k += 256) {
       const int b = k >> 4, n = 16 * nt + (k & 15);

@@ -39,6 +39,9 @@ __device__ __forceinline__ void st1(float* p, float v, bool wt) {
     *p = v;
 }
 
+// ReLU that keeps NaN (fmaxf(NaN, 0) is 0: a diverged value would vanish into a finite 0)
+__device__ __forceinline__ float relu_nan(float x) { return x <= 0.f ? 0.f : x; }
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -58,8 +61,15 @@ __device__ __forceinline__ unsigned long long to_fix(float v, float scale) {
   return (unsigned long long)__float2ll_rn(s);
 }
 __device__ __forceinline__ float from_fix(long long v, float inv) { return (float)v * inv; }
-__device__ __forceinline__ void fix_add(long long* dst, float v, float scale) {
+// A non-finite partial (a diverged step) cannot be represented in the integer sum -- to_fix would
+// turn NaN into a saturated finite value -- so it raises the sticky `bad` word instead, and every
+// conversion back (from_fix_chk) then yields NaN: divergence stays visible in the loss and weights.
+__device__ __forceinline__ void fix_add(long long* dst, float v, float scale, int* bad) {
+  if (!__builtin_isfinite(v)) atomicOr(bad, 1);
   atomicAdd(reinterpret_cast<unsigned long long*>(dst), to_fix(v, scale));
+}
+__device__ __forceinline__ float from_fix_chk(long long v, float inv, int bad) {
+  return bad ? __builtin_nanf("") : (float)v * inv;
 }
 
 // Phase timestamps for in-kernel profiling (MnistFused::trace, off = null): blocks 0..1023 of
@@ -81,23 +91,26 @@ struct Scratch {  // carve of MnistFused::scratch (floats)
                   // [4 w][16 xi][2 s4][64 lane][4 j]
   float* wslab;   // conv2 wgrad per-image slabs [B][64 co][32 ci][9 tap] (canonical order), written
                   // by F6W, summed by the finalize in a fixed order
+  int* bad;       // sticky: a non-finite value reached a fixed-point sum (fix_add); zeroed by k_init
 };
 constexpr int kWinoPack = 16 * 2048;  // 16 Winograd-domain values per (co, ci)
 // conv1-grad slabs: the F7W blocks of image b add into slab b & 15 (integer adds, so the slab
 // count only spreads same-address contention; the sum is exact either way)
 constexpr int kG1Slabs = 16;
-__host__ __device__ inline Scratch carve(float* s) {
+__host__ __device__ inline Scratch carve(float* s, int B) {
   Scratch c;
   c.wu = s;
   c.g1 = reinterpret_cast<long long*>(c.wu + kWinoPack);
   c.db2 = c.g1 + kG1Slabs * 320;
   c.wv = reinterpret_cast<float*>(c.db2 + 64);
   c.wslab = c.wv + kWinoPack;
+  c.bad = reinterpret_cast<int*>(c.wslab + (size_t)B * kPack);  // after the slabs
   return c;
 }
 inline size_t scratch_floats(int B) {
-  return 2 * (size_t)kWinoPack + 2 * ((size_t)kG1Slabs * 320 + 64) + (size_t)B * kPack;
+  return 2 * (size_t)kWinoPack + 2 * ((size_t)kG1Slabs * 320 + 64) + (size_t)B * kPack + 64;
 }
+
 
 // conv2 weight gradient of pairs 4 grp .. 4 grp + 3 (36 consecutive floats of the canonical
 // [co][ci][ky][kx] layout) summed over the B per-image slabs in a fixed order -> gs[36] (LDS).

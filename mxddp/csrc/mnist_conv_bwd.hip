@@ -31,7 +31,9 @@ namespace {
 // (float2 / u16 loads, prefetched one chunk ahead).  The a1 tile pitch 164: 16-byte rows for the
 // float4 stores, 36 ci mod 64 banks keeps phase B's reads conflict-free.
 // (Measured and removed, profiles/r3_cos2 and r2: 2-3 blocks per (image, ci half): 725k / 695k vs
-// 748k img/s; blocks split over co halves: 917k vs 951k.)
+// 748k img/s; blocks split over co halves: 917k vs 951k; round 5, profiles/r5_f6split: blocks split
+// over the Winograd rows (2 x 8 of the 16 GEMMs, partial slabs): F6W 24 -> 18 us but F7W 19 -> 23 us
+// beside the extra blocks, 903k vs 929k.)
 constexpr int kF6WA1P = 164, kF6WVP = 20;
 constexpr size_t kF6WLds = sizeof(float) * (784 + 160 + 16 * kF6WA1P + 24 * 16 * kF6WVP);
 __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc, float* sm, int braw, int nblk) {
@@ -225,6 +227,7 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
 // image & 15 (order-independent sums).
 constexpr int kF7WChunks = 6, kF7WRows = 5, kF7WCols = 14, kF7WCoP = 80;
 constexpr size_t kF7WLds = sizeof(float) * (64 * kF7WCoP + 784 + 320 + 640) + 64 * kF7WCoP;
+template <int kF7WPf>
 __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc, float* sm, int braw, int nblk) {
   MX_TRACE_B(f, 4, 0, braw);
   float* dps = sm;                                      // [64 co][80]: 5 window rows x 14 cols
@@ -299,8 +302,8 @@ __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc,
     const float* dpp = dps + (ty - tyf) * kF7WCols + tx + g * kF7WCoP;
     const uint8_t* qp = qs + (ty - tyf) * kF7WCols + tx + g * kF7WCoP;
     const float4* wu = reinterpret_cast<const float4*>(sc.wu) + (half * 64 + lane) * 4;
-    // fully unrolled; B fragments prefetched kF7WPf k-steps ahead (indices fold to registers)
-    constexpr int kF7WPf = 2;
+    // fully unrolled; B fragments prefetched kF7WPf k-steps ahead (indices fold to registers;
+    // 3 ahead measured equal to 2, profiles/r5_tune: 930 / 933k vs 932 / 928k img/s)
     float4 bq[16][4];
 #pragma unroll
     for (int s = 0; s < kF7WPf; ++s)
@@ -429,7 +432,7 @@ __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc,
   for (int i = tid; i < 320; i += 256) {
     const float v = red[i] + red[320 + i];
     const int c = i / 10, k = i - c * 10;
-    fix_add(g1 + (k < 9 ? c * 9 + k : 288 + c), v, kGScale);  // conv1.weight [32][9], conv1.bias [32]
+    fix_add(g1 + (k < 9 ? c * 9 + k : 288 + c), v, kGScale, sc.bad);  // conv1.weight [32][9], conv1.bias [32]
   }
   MX_TRACE_B(f, 4, 3, braw);
 }
@@ -459,7 +462,7 @@ __global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scr
   if (bid < n6)
     f6w_body(f, sc, sm, bid, n6);
   else
-    f7w_body(f, sc, sm, bid - n6, kF7WChunks * f.B);
+    f7w_body<2>(f, sc, sm, bid - n6, kF7WChunks * f.B);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -485,9 +488,9 @@ __global__ __launch_bounds__(256) void f8_finalize_kernel(MnistFused f, Scratch 
       for (int k = 0; k < kG1Slabs; ++k) s += v[k];
 #pragma unroll
       for (int k = 0; k < kG1Slabs; ++k) sc.g1[k * 320 + j] = 0;
-      f.g[L::w1 + j] = from_fix(s, kGInv);
+      f.g[L::w1 + j] = from_fix_chk(s, kGInv, *sc.bad);
     } else if (j < 384) {  // conv2 bias
-      f.g[L::b2 + j - 320] = from_fix(sc.db2[j - 320], kGInv);
+      f.g[L::b2 + j - 320] = from_fix_chk(sc.db2[j - 320], kGInv, *sc.bad);
       sc.db2[j - 320] = 0;
     }
   } else {
@@ -509,7 +512,7 @@ void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  const Scratch sc = carve(f.scratch);
+  const Scratch sc = carve(f.scratch, f.B);
   MX_LAUNCH(f67_conv2_bwd_kernel, dim3(f.co_blocks + 2 * f.B + kF7WChunks * f.B), dim3(256), lds, st, f, sc);
   if (!finalize_in_sgd) MX_LAUNCH(f8_finalize_kernel, dim3(kWslabGroups + 2 + 8), dim3(256), 0, st, f, sc);
   MX_HIP_CHECK(hipGetLastError());

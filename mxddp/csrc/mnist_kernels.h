@@ -49,6 +49,7 @@ struct MnistFused {
 size_t mnist_fused_scratch_floats(int B);
 void mnist_set_wt_stores(int mask);  // process-wide default of MnistFused::wt
 int mnist_wt_stores();
+
 // Pack conv2 weights into the F2 Winograd fragment order and zero the cross-step accumulators;
 // needed once and after any change of the parameters outside the fused SGD.
 void mnist_fused_init(const MnistFused& f, hipStream_t st);

@@ -105,6 +105,7 @@ __global__ __launch_bounds__(256) void k_init(MnistFused f, Scratch sc) {
   for (int i = gtid; i < f.B * 128; i += gsz) f.h[i] = 0;
   for (int i = gtid; i < kG1Slabs * 320; i += gsz) sc.g1[i] = 0;
   if (gtid < 64) sc.db2[gtid] = 0;
+  if (gtid == 0) *sc.bad = 0;
 }
 
 // F2 a1 tile pitches (row 38, channel 141): picked by an exhaustive bank model (32-lane groups,
@@ -366,7 +367,9 @@ constexpr int kF3TChunks = 8, kF3TK = 9216 / kF3TChunks, kF3Wv = 8;
 __global__ __launch_bounds__(64 * kF3Wv) void f3t_fc1_kernel(MnistFused f) {
   MX_TRACE(f, 1, 0);
   constexpr int kTW = kF3TK / kF3Wv, kTS = kTW / 16;
-  __shared__ float red[kF3Wv][16][17];
+  // wave partials as [wave][j][64 lanes]: the stores (lane-linear) and the reads (thread = flat
+  // index) are both bank-conflict free (the [16][17] row layout took 2-4 cycles per access)
+  __shared__ float red[kF3Wv][4][64];
   const int tiles = f.B / 2;  // (B / 16) row tiles x 8 column tiles
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int kc = bid / tiles, tile = bid - kc * tiles, mt = tile >> 3, nt = tile & 7;
@@ -392,13 +395,14 @@ __global__ __launch_bounds__(64 * kF3Wv) void f3t_fc1_kernel(MnistFused f) {
     acc[1] = mfma4(av[s].w, bv[s].w, acc[1]);
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) red[w][4 * g + j][m] = acc[0][j] + acc[1][j];
+  for (int j = 0; j < 4; ++j) red[w][j][lane] = acc[0][j] + acc[1][j];
   __syncthreads();
   if (tid < 256) {
-    const int row = tid >> 4, col = tid & 15;
-    const float v = ((red[0][row][col] + red[1][row][col]) + (red[2][row][col] + red[3][row][col])) +
-                    ((red[4][row][col] + red[5][row][col]) + (red[6][row][col] + red[7][row][col]));
-    fix_add(f.h + (16 * mt + row) * 128 + 16 * nt + col, v, kHScale);
+    // flat index tid = (j, g, m): output row 4g + j, column m
+    const int j = tid >> 6, l = tid & 63, row = 4 * (l >> 4) + j, col = l & 15;
+    const float v = ((red[0][j][l] + red[1][j][l]) + (red[2][j][l] + red[3][j][l])) +
+                    ((red[4][j][l] + red[5][j][l]) + (red[6][j][l] + red[7][j][l]));
+    fix_add(f.h + (16 * mt + row) * 128 + 16 * nt + col, v, kHScale, carve(f.scratch, f.B).bad);
   }
   // F2 consumed the counter; bumped last so its load / wait does not hold wave 0 of block 0
   // in front of the operand loads
@@ -506,6 +510,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   for (int k = 0; k < N2; ++k) v2[k] = f.p[L::fw2 + tid + 256 * k];  // 1280 = 5 x 256
   const int yv = f.y[tid < B ? tid : 0];
   const float b2v = f.p[L::fb2 + (m < 10 ? m : 0)];
+  const int bad = *carve(f.scratch, f.B).bad;  // F3 saw a non-finite partial: h (and the loss) become NaN
   // group (2) strictly after group (1) in issue order: vmcnt counts in order, so a group-2 load
   // scheduled in front of a head operand would be waited for before the head
   __builtin_amdgcn_sched_barrier(0);
@@ -542,10 +547,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   for (int k = 0; k < ND; ++k) {
     const int i = tid + 256 * k, c4 = (i & 31) * 4;
     const float4 b1 = vb1[k];
-    const float4 hv = make_float4(from_fix(vd[k][0].x, kHInv), from_fix(vd[k][0].y, kHInv),
-                                  from_fix(vd[k][1].x, kHInv), from_fix(vd[k][1].y, kHInv));
+    const float4 hv = make_float4(from_fix_chk(vd[k][0].x, kHInv, bad), from_fix_chk(vd[k][0].y, kHInv, bad),
+                                  from_fix_chk(vd[k][1].x, kHInv, bad), from_fix_chk(vd[k][1].y, kHInv, bad));
     *reinterpret_cast<float4*>(dhs + (i >> 5) * kF5DhP + c4) =
-        make_float4(fmaxf(hv.x + b1.x, 0.f), fmaxf(hv.y + b1.y, 0.f), fmaxf(hv.z + b1.z, 0.f), fmaxf(hv.w + b1.w, 0.f));
+        make_float4(relu_nan(hv.x + b1.x), relu_nan(hv.y + b1.y), relu_nan(hv.z + b1.z), relu_nan(hv.w + b1.w));
   }
 #pragma unroll
   for (int k = 0; k < N2; ++k) {
@@ -759,7 +764,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   __syncthreads();
   MX_TRACE(f, 2, 6);
-  if (tid == 0) fix_add(carve(f.scratch).db2 + c0 / 144, (misc[0] + misc[1]) + (misc[2] + misc[3]), kGScale);
+  if (tid == 0) {
+    const Scratch sc = carve(f.scratch, f.B);
+    fix_add(sc.db2 + c0 / 144, (misc[0] + misc[1]) + (misc[2] + misc[3]), kGScale, sc.bad);
+  }
   MX_TRACE(f, 2, 7);
 }
 
@@ -856,7 +864,9 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(MnistFused f, Scratch sc,
         d[0] = make_longlong2(0, 0);
         d[1] = make_longlong2(0, 0);
       }
-      gv = make_float4(from_fix(a[0], kGInv), from_fix(a[1], kGInv), from_fix(a[2], kGInv), from_fix(a[3], kGInv));
+      const int bad = *sc.bad;
+      gv = make_float4(from_fix_chk(a[0], kGInv, bad), from_fix_chk(a[1], kGInv, bad), from_fix_chk(a[2], kGInv, bad),
+                       from_fix_chk(a[3], kGInv, bad));
       g4[i] = gv;
     }
     float4 bv = b4[i];
@@ -910,6 +920,7 @@ static int g_wt_stores = 6;
 void mnist_set_wt_stores(int mask) { g_wt_stores = mask & 7; }
 int mnist_wt_stores() { return g_wt_stores; }
 
+
 static void check(const MnistFused& f) {
   MX_CHECK(f.B % 16 == 0 && f.B >= 16 && f.B <= 128 && f.nB >= 1 && f.nB <= f.B && f.B - f.nB < 16,
            "fused MNIST engine: 1 <= batch <= 128, buffers padded to the next multiple of 16");
@@ -930,14 +941,14 @@ static void set_lds_limits() {
 void mnist_fused_init(const MnistFused& f, hipStream_t st) {
   check(f);
   set_lds_limits();
-  MX_LAUNCH(k_init, dim3(128), dim3(256), 0, st, f, carve(f.scratch));
+  MX_LAUNCH(k_init, dim3(128), dim3(256), 0, st, f, carve(f.scratch, f.B));
   MX_HIP_CHECK(hipGetLastError());
 }
 
 void mnist_fused_forward(const MnistFused& f, hipStream_t st) {
   check(f);
   set_lds_limits();
-  const Scratch sc = carve(f.scratch);
+  const Scratch sc = carve(f.scratch, f.B);
   MX_LAUNCH(f2_fwd_kernel, dim3(f.B * 12), dim3(256), 0, st, f, sc);
   launch_f3(f, st);
   MX_HIP_CHECK(hipGetLastError());
@@ -968,9 +979,9 @@ void mnist_fused_sgd(const MnistFused& f, float* mom_buf, const float* lr, float
   // folded: ~20 K elements left (+ the 32 pair blocks, or the 512 slab-sum pair-group blocks)
   const dim3 grid((f.fc1_sgd ? 128 : 1024) + (finalize ? kWslabGroups : 0));
   if (finalize)
-    MX_LAUNCH(sgd_pack_kernel<true>, grid, dim3(256), 0, st, f, carve(f.scratch), mom_buf, lr, gscale, momentum, wd);
+    MX_LAUNCH(sgd_pack_kernel<true>, grid, dim3(256), 0, st, f, carve(f.scratch, f.B), mom_buf, lr, gscale, momentum, wd);
   else
-    MX_LAUNCH(sgd_pack_kernel<false>, grid, dim3(256), 0, st, f, carve(f.scratch), mom_buf, lr, gscale, momentum, wd);
+    MX_LAUNCH(sgd_pack_kernel<false>, grid, dim3(256), 0, st, f, carve(f.scratch, f.B), mom_buf, lr, gscale, momentum, wd);
   MX_HIP_CHECK(hipGetLastError());
 }
 

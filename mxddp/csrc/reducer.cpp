@@ -13,7 +13,9 @@ Reducer::Reducer(Comm* comm, uintptr_t flat_grad, DType dtype, const std::vector
   sched_ = BucketSchedule(spans, param_bucket);
   ev_.assign(buckets.size(), nullptr);
   for (auto& e : ev_) MX_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  MX_HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
+  // the side stream is created on first use (side()): reducers that never overlap -- a merged
+  // bucket, the co-scheduled engines' -- then hold no stream, i.e. no extra hardware queue
+  MX_HIP_CHECK(hipGetDevice(&dev_));
   MX_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
   if (timing_) {
     MX_HIP_CHECK(hipEventCreate(&t0_));
@@ -76,6 +78,17 @@ bool Reducer::active() const {
   return (comm_ && (comm_->world_size() > 1 || force_)) || (peer_ && peer_->world_size() > 1);
 }
 
+hipStream_t Reducer::side() {
+  if (!comm_stream_) {
+    int cur = 0;
+    MX_HIP_CHECK(hipGetDevice(&cur));
+    if (cur != dev_) MX_HIP_CHECK(hipSetDevice(dev_));
+    MX_HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
+    if (cur != dev_) MX_HIP_CHECK(hipSetDevice(cur));
+  }
+  return comm_stream_;
+}
+
 void Reducer::launch_ready(hipStream_t compute) {
   const bool act = active();
   if (in_step_) {
@@ -89,8 +102,8 @@ void Reducer::launch_ready(hipStream_t compute) {
       hipStream_t st = compute;
       if (overlap_) {
         MX_HIP_CHECK(hipEventRecord(ev_[bi], compute));
-        MX_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_[bi], 0));
-        st = comm_stream_;
+        st = side();
+        MX_HIP_CHECK(hipStreamWaitEvent(st, ev_[bi], 0));
         side_used_ = true;
       }
       if (timing_ && bi == 0) MX_HIP_CHECK(hipEventRecord(t0_, st));

@@ -42,7 +42,7 @@ class Reducer {
   void mark_ready(int param_idx, hipStream_t compute);
   void mark_bucket_ready(int bucket, hipStream_t compute);  // fused engines: whole bucket at once
   void finalize(hipStream_t compute);               // launch stragglers; compute waits on comm
-  hipStream_t comm_stream() const { return comm_stream_; }
+  hipStream_t comm_stream() { return side(); }
   int num_buckets() const { return sched_.size(); }
   int launched() const { return sched_.launched(); }
   // milliseconds between first bucket launch and comm completion of the last step
@@ -94,7 +94,9 @@ class Reducer {
   RedOp op_;
   BucketSchedule sched_;          // host state machine (bucket_schedule.h)
   std::vector<hipEvent_t> ev_;    // per-bucket compute -> comm fence
-  hipStream_t comm_stream_ = nullptr;
+  hipStream_t comm_stream_ = nullptr;  // side stream, created on first use (side())
+  int dev_ = 0;
+  hipStream_t side();
   hipEvent_t done_ = nullptr, t0_ = nullptr, t1_ = nullptr;
   bool timing_ = false, timed_ = false, force_ = false, overlap_ = true, side_used_ = false;
   // stream discipline: every bucket of one backward is fenced against ONE compute

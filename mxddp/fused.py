@@ -164,7 +164,8 @@ class FusedTrainerBase:
         stream overlapping the rest of the backward, "inl" the buckets in order on the compute
         stream, "one" a single all-reduce of the whole gradient, "co" the exchange co-scheduled
         inside another launch of the step) x (eager launches, or the step captured in one
-        hipGraph; peer-transport graphs always, RCCL-in-graph with MXDDP_AUTOTUNE_GRAPHS=1).  The
+        hipGraph -- RCCL included, MXDDP_AUTOTUNE_GRAPHS=0 keeps RCCL eager: at 8 GPUs an eager
+        step is ~7 host launches per ~70 us of device work, a graph is one).  The
         slowest rank's time decides, so every rank picks the same strategy.
 
         Fail fast, never raise for a peer candidate: before a peer-transport strategy is timed,
@@ -178,7 +179,7 @@ class FusedTrainerBase:
         from .parallel import comm as pc
 
         if include_graphs is None:
-            include_graphs = os.environ.get("MXDDP_AUTOTUNE_GRAPHS", "0") == "1"
+            include_graphs = os.environ.get("MXDDP_AUTOTUNE_GRAPHS", "1") == "1"
         if not self.eng.reducer_active or self._external:
             return {}
         comms = self._rccl_candidates()

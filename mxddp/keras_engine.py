@@ -90,6 +90,13 @@ class FusedKerasReplicas(FusedReplicas):
             torch.manual_seed(seed)
             init_model = KerasCNN()
         self.batch = batch
+        n = len(devices)
+        if strategy == "co" and n > 2 and len({torch.device(d) for d in devices}) < n:
+            # replicas sharing one GPU (a rehearsal of an n-GPU node): the co-scheduled exchange is
+            # n x 182 blocks of 512 threads that must ALL be resident at once (each block waits on
+            # the peers' matching block), more than one GPU holds at n = 8 -- the separate
+            # exchange kernel (32 blocks per replica) is used instead
+            strategy = "one"
 
         def make(d, pc):
             t = FusedKerasTrainer(batch=batch, device=d, peer=pc, seed=seed, lr=lr, init_model=init_model,

@@ -36,16 +36,18 @@ def capturing() -> bool:
     return _CAPTURING[0] > 0
 
 
-def capture_stream(device: torch.device) -> torch.cuda.Stream:
+def capture_stream(device: torch.device, slot: int = 0) -> torch.cuda.Stream:
     """One stream per device on which every mxddp hipGraph is captured.  Stream-owned scratch
     (the split-K partial planes of ops_gemm.hip) is reserved for it here, outside any capture:
-    a GEMM captured on a stream without planes would have to run unsplit."""
+    a GEMM captured on a stream without planes would have to run unsplit.  ``slot``: graphs that
+    REPLAY CONCURRENTLY on one device (replicas sharing a GPU) need capture streams of their own,
+    or their captured GEMMs would share one set of partial planes."""
     device = torch.device(device)
-    s = _CAPTURE_STREAMS.get(device)
+    s = _CAPTURE_STREAMS.get((device, slot))
     if s is None:
         s = torch.cuda.Stream(device)
         native().reserve_splitk_planes(s.cuda_stream)
-        _CAPTURE_STREAMS[device] = s
+        _CAPTURE_STREAMS[(device, slot)] = s
     return s
 
 

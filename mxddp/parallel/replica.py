@@ -36,7 +36,7 @@ from .flat import FlatParams, flatten_buffers
 
 class ReplicaGroup:
     def __init__(self, model: nn.Module, devices: list[torch.device], make_optimizer, broadcast_buffers: bool = True,
-                 use_graph: bool = False, peer_blocks: int = 64):
+                 use_graph: bool = False, peer_blocks: int = 64, bucket_cap_mb: float = 25.0):
         self.devices = [torch.device(d) for d in devices]
         self.use_graph = use_graph and all(torch.device(d).type == "cuda" for d in devices)
         self._graphs = None  # per-device hipGraphs of the WHOLE step
@@ -51,11 +51,20 @@ class ReplicaGroup:
         self._acc = [torch.zeros(2, device=d) for d in self.devices]
         self.comms = None
         self.peers = None
+        self.reducers = None
+        self._capturing = None  # replica whose step is being captured (its gradient hooks are live)
+        # several replicas on ONE device (a rehearsal of an N-GPU node on one GPU): RCCL cannot
+        # span them, so every exchange is the in-process peer transport
+        self.shared = len(set(self.devices)) < self.n
         if self.n > 1:
             if any(d.type != "cuda" for d in self.devices):
                 raise ValueError("replica mode across several devices needs GPUs")
-            self.comms = native().Comm.init_all([d.index for d in self.devices])
-            if self.use_graph:
+            if not self.shared:
+                self.comms = native().Comm.init_all([d.index for d in self.devices])
+            # every replica's exchange kernels run on a stream of its own: a replica's all-reduce
+            # waits on the GPU for the others', which must not be queued behind it
+            self._rs = [torch.cuda.Stream(d) for d in self.devices]
+            if self.use_graph or self.shared:
                 # the in-graph gradient / buffer exchange: the peer transport opened in-process
                 # (device peer access, no IPC) -- an ordinary kernel per device, so each replica's
                 # whole step is one graph launch (RCCL's single-thread multi-device calls need a
@@ -68,6 +77,8 @@ class ReplicaGroup:
                 for pc, d in zip(self.peers, self.devices):
                     with torch.cuda.device(d):
                         pc.open_local(self.peers)
+            if self.use_graph:
+                self._make_reducers(bucket_cap_mb)
         self._sync(self.flats[0].data, [f.data for f in self.flats])
         if self.n > 1:  # raw-pointer write to the replicas' weights: banked conv filters are stale
             from .. import ops
@@ -76,14 +87,61 @@ class ReplicaGroup:
         if self.buffers and self.buffers[0] is not None:
             self._sync(self.buffers[0], self.buffers)
 
+    def _make_reducers(self, bucket_cap_mb: float):
+        """Graph mode: per replica, the DDP bucket reducer (csrc/reducer.cpp) over the peer
+        transport -- reverse-order buckets (1 MB first, then bucket_cap_mb) all-reduced on the
+        reducer's side stream as the backward fills them, so the exchange overlaps the rest of the
+        backward (PyramidNet's 97 MB gradient leaves in 5 buckets instead of one exchange after
+        the backward).  The hooks only act while a replica's step is being captured."""
+        from .ddp import assign_buckets
+
+        C = native()
+        f0 = self.flats[0]
+        self.buckets, pb = assign_buckets([p.numel() for p in f0.params], f0.offsets, f0.numel, bucket_cap_mb,
+                                          min(1.0, bucket_cap_mb))
+        self.reducers = []
+        for i, (f, d) in enumerate(zip(self.flats, self.devices)):
+            with torch.cuda.device(d):
+                r = C.Reducer(None, f.grad.data_ptr(), C.DType.f32, self.buckets, pb, C.RedOp.avg, False)
+                r.set_peer(self.peers[i])
+                r.comm_stream()  # its side stream exists before the capture that first uses it
+            self.reducers.append(r)
+            for j, p in enumerate(f.params):
+                p.register_post_accumulate_grad_hook(self._hook(i, j))
+
+    def _hook(self, i: int, j: int):
+        def hook(p):
+            if self._capturing == i:
+                # fenced against the capture stream the step's backward kernels run on (the hook
+                # runs on an autograd device thread, whose current stream need not be that one)
+                self.reducers[i].mark_ready(j, self._cap_stream)
+        return hook
+
     # ------------------------------------------------------------------ collectives
     def _stream(self, i):
         return torch.cuda.current_stream(self.devices[i]).cuda_stream
+
+    def _peer_each(self, tensors, op, zero_others: bool = False):
+        """One peer all-reduce per replica, each on its replica's own stream (ordered after the
+        device's current stream, and the current stream after it)."""
+        C = native()
+        for i, (t, d) in enumerate(zip(tensors, self.devices)):
+            rs = self._rs[i]
+            rs.wait_stream(torch.cuda.current_stream(d))
+            with torch.cuda.stream(rs):
+                if zero_others and i != 0:
+                    t.zero_()
+                self.peers[i].all_reduce(t.data_ptr(), t.numel(), C.DType.f32, rs.cuda_stream, op)
+        for rs, d in zip(self._rs, self.devices):
+            torch.cuda.current_stream(d).wait_stream(rs)
 
     def _sync(self, src, dsts):
         if self.n == 1:
             return
         C = native()
+        if self.comms is None:  # broadcast from replica 0 = peer sum of (replica 0 ? t : 0), exact
+            self._peer_each(dsts, C.RedOp.sum, zero_others=True)
+            return
         C.Comm.group_start()
         for i, (c, t) in enumerate(zip(self.comms, dsts)):
             c.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), C.DType.f32, 0, self._stream(i))
@@ -93,6 +151,9 @@ class ReplicaGroup:
         if self.n == 1:
             return
         C = native()
+        if self.comms is None:
+            self._peer_each([f.grad for f in self.flats], C.RedOp.avg)
+            return
         C.Comm.group_start()
         for i, (c, f) in enumerate(zip(self.comms, self.flats)):
             c.all_reduce(f.grad.data_ptr(), f.grad.data_ptr(), f.numel, C.DType.f32, C.RedOp.avg, self._stream(i))
@@ -169,10 +230,20 @@ class ReplicaGroup:
             self.peers[i].all_reduce(self.buffers[i].data_ptr(), self.buffers[i].numel(), C.DType.f32, st, C.RedOp.sum)
         self.flats[i].zero_grad()
         loss, correct = loss_fn(self.replicas[i](self._xs[i]), self._ys[i])
-        loss.backward()
-        if self.n > 1:
-            f = self.flats[i]
-            self.peers[i].all_reduce(f.grad.data_ptr(), f.numel, C.DType.f32, st, C.RedOp.avg)
+        if self.reducers is not None:
+            # bucketed: each bucket's average leaves on the reducer's side stream as soon as the
+            # backward has filled it; finalize joins them before the optimizer
+            r = self.reducers[i]
+            r.prepare()
+            self._cap_stream = st
+            self._capturing = i
+            try:
+                loss.backward()
+            finally:
+                self._capturing = None
+            r.finalize(st)
+        else:
+            loss.backward()
         self.optimizers[i].step()
         self._accumulate(i, loss.detach(), correct, self._xs[i].shape[0])
 
@@ -185,7 +256,9 @@ class ReplicaGroup:
                 from .graphed import capture_stream
 
                 cur = torch.cuda.current_stream(d)
-                side = capture_stream(d)
+                # replicas sharing a device replay concurrently: a capture stream (and its split-K
+                # planes) each
+                side = capture_stream(d, i if self.shared else 0)
                 side.wait_stream(cur)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
@@ -195,14 +268,25 @@ class ReplicaGroup:
         self._graphs = graphs
 
     def _replay(self, xs, ys):
-        # EVERY replica's graph is launched before the host waits on any of them: each graph's
-        # gradient exchange waits on the GPUs for the other replicas
+        # EVERY replica's graph is launched before the host waits on any of them, each on its
+        # replica's own stream: each graph's gradient exchange waits on the GPUs for the others
+        if self.n == 1:
+            self._xs[0].copy_(xs[0], non_blocking=True)
+            self._ys[0].copy_(ys[0], non_blocking=True)
+            self.optimizers[0]._sync_lr()
+            self._graphs[0].replay()
+            return
         for i, d in enumerate(self.devices):
+            rs = self._rs[i]
             with torch.cuda.device(d):
-                self._xs[i].copy_(xs[i], non_blocking=True)
-                self._ys[i].copy_(ys[i], non_blocking=True)
-                self.optimizers[i]._sync_lr()
-                self._graphs[i].replay()
+                rs.wait_stream(torch.cuda.current_stream(d))
+                with torch.cuda.stream(rs):
+                    self._xs[i].copy_(xs[i], non_blocking=True)
+                    self._ys[i].copy_(ys[i], non_blocking=True)
+                    self.optimizers[i]._sync_lr()
+                    self._graphs[i].replay()
+        for rs, d in zip(self._rs, self.devices):
+            torch.cuda.current_stream(d).wait_stream(rs)
 
     @property
     def module(self) -> nn.Module:

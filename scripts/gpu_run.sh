@@ -25,7 +25,7 @@
 #   trace_pyr    kernel + HIP API trace of the graphed PyramidNet step (where its copies come from)
 #   diag_bnstats backward BN statistics of the data-gradient epilogues vs torch
 #   bench_bn     effective bandwidth of the NHWC BN kernel variants vs a copy
-#   diag_join    residual-join / BN-statistics variants of two Bottleneck blocks vs a baseline (and a repeat)
+
 source "$(dirname "$0")/gpu_check.sh"
 rm -f gpurun_out/steps.log
 
@@ -71,7 +71,6 @@ for step in "$@"; do
     prof_mnist) prof prof_mnist 200 --steps 200 --warmup 20 --min-warmup-ms 0 ;;
     pmc_mnist) pmc pmc_mnist --steps 20 --warmup 2 --no-graph --min-warmup-ms 0 ;;
     phase_mnist) run phase_mnist 300 python bench.py --phase-profile 30 ;;
-    diag_join) run diag_join 300 python scripts/diag_join.py ;;
     bench_bn) run bench_bn 300 python scripts/bench_bn.py ;;
     coll) run coll 300 python bench.py --steps 2000 --warmup 100 --force-collectives ;;
     replica) run replica 300 python bench.py --impl replica --steps 1000 --warmup 50 ;;

@@ -160,3 +160,16 @@ def test_rccl_variant_names():
 
     with pytest.raises(ValueError):
         parse_variant("Ring:7")
+
+
+def test_fused_engines_take_reference_batch_sizes():
+    """The reference's own per-device batches route to the native fused engines: Chainer's 100 /
+    200 / 400 (chainer/train_mnist.py:31, train_mnist_gpu.py:33) and the DDP CLI's -b 64 over 8
+    local ranks = 8 per rank (pytorch/distributed_data_parallel.py:71)."""
+    from mxddp.train import fused_batch_ok
+
+    assert all(fused_batch_ok("mlp", b) for b in (100, 200, 400, 1, 512))
+    assert not fused_batch_ok("mlp", 513)
+    assert all(fused_batch_ok("mnist_cnn", b) for b in (8, 64, 1, 100, 128))
+    assert not fused_batch_ok("mnist_cnn", 129)
+    assert fused_batch_ok("keras_cnn", 64) and not fused_batch_ok("keras_cnn", 12)

@@ -47,9 +47,11 @@ def test_fused_engine_matches_reference(cuda, variant, graph):
         assert err < 1e-4, (k, err)
 
 
-@pytest.mark.parametrize("B", [16, 48, 64, 128])
+@pytest.mark.parametrize("B", [16, 48, 64, 128, 8, 1, 100, 37])
 def test_fused_engine_batch_sizes_match_reference(cuda, B):
-    """Every batch the fused engine accepts (16..128, multiples of 16) against the fp32 reference."""
+    """Batches the fused engine accepts (1..128) against the fp32 reference: whole 16-row tiles,
+    and partial last tiles whose pad rows must add nothing (8 = the reference DDP CLI's -b 64
+    over 8 local ranks, pytorch/distributed_data_parallel.py:71)."""
     from mxddp.engine import FusedMnistTrainer
     from mxddp.models import MnistCNN
 
@@ -296,7 +298,7 @@ def test_fused_autotune_lists_rccl_variants(cuda, monkeypatch):
     b = FusedMnistTrainer(batch=64, device=cuda, lr=0.01)
     a.step(1)
     b.step(1)
-    res = a.autotune(trial_steps=3, restore=True)
+    res = a.autotune(trial_steps=3, restore=True, include_graphs=False)
     names = {k.split("/")[0] for k in a.tuned["trials_ms"]}
     assert names == {"rccl:default", "rccl:Ring:c7", "rccl:Ring:c28"}, a.tuned
     assert len(res) == 9 and a.steps == 1
@@ -321,3 +323,22 @@ def test_fused_engine_is_deterministic(cuda):
     assert ma == mb == mc
     for k in sa:
         assert torch.equal(sa[k], sb[k]) and torch.equal(sa[k], sc[k]), k
+
+
+def test_fused_engine_divergence_stays_visible(cuda):
+    """A NaN reaching one of the step's int64 fixed-point sums (F3's fc1 pre-activation, the conv
+    gradient slabs) must not be saturated into finite garbage: the loss and the updated weights
+    come out NaN (the sticky flag of mnist_common.h fix_add)."""
+    from mxddp.engine import FusedMnistTrainer
+    from mxddp.models import MnistCNN
+
+    torch.manual_seed(0)
+    m = MnistCNN()
+    with torch.no_grad():
+        m.fc1.weight[7, 100] = float("nan")  # F3's fc1 partial of output column 7 becomes NaN
+    tr = FusedMnistTrainer(batch=16, device=cuda, comm=None, init_model=m, use_graph=False)
+    tr.step(1)
+    loss, _ = tr.read_metrics()
+    assert loss != loss, loss
+    sd = tr.state_dict()
+    assert torch.isnan(sd["fc2.weight"]).any() and torch.isnan(sd["conv1.weight"]).any()

@@ -72,8 +72,11 @@ def _check(tr, batches, lr, B, init):
 
 
 @pytest.mark.parametrize("graph", [False, True])
-@pytest.mark.parametrize("B", [64, 16, 128])
+@pytest.mark.parametrize("B", [64, 16, 128, 100, 200, 4, 512])
 def test_fused_mlp_matches_reference(cuda, graph, B):
+    """Whole 16-row tiles and the reference's own batches: 100 (chainer/train_mnist.py:31) and 200
+    per device (ParallelUpdater's 400 over 2 GPUs, chainer/train_mnist_gpu.py:33); 200 and 512 run
+    the backward kernels' batch in several LDS passes."""
     from mxddp.mlp_engine import FusedMlpTrainer
     from mxddp.models import MLP
 

@@ -157,3 +157,23 @@ def test_train_cli_two_ranks_share_gpu(cuda, tmp_path, model, extra):
     for k in a:
         assert torch.equal(a[k], b[k]), k
     assert "From Rank: 1, Training time" in p.stdout
+
+
+@pytest.mark.parametrize("script,argv,expect", [
+    ("chainer/train_mnist.py", ["--gpu", "0", "-e", "1"], "engine fused"),
+    ("chainer/train_mnist_gpu.py", ["--gpu", "-e", "1"], "replica mode (fused mlp engine)"),
+])
+def test_chainer_examples_run_fused_engine_at_reference_batch(cuda, tmp_path, script, argv, expect):
+    """The reference's Chainer launch lines with their DEFAULT batch sizes (100 for
+    train_mnist.py, 400 on --gpu_number 1 for train_mnist_gpu.py) run the native fused MLP step,
+    not the generic layer path (the engine pads the partial last 16-row tile)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    cmd = [sys.executable, os.path.join(root, "examples", script)] + argv + ["-o", str(tmp_path / "out")]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=tmp_path)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert expect in p.stdout, p.stdout[-3000:]
