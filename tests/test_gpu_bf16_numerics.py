@@ -10,7 +10,10 @@ the same GPU; mxddp's normwise error must stay within 1.5x stock's for EVERY gra
 
 Plus a 200-step ResNet-50 run on class-conditional synthetic data whose loss must fall.
 """
+import math
+
 import pytest
+
 import torch
 import torch.nn.functional as F
 
@@ -86,19 +89,20 @@ def test_bottlenecks_bf16_error_within_stock_bf16(cuda):
 
 
 def test_resnet50_bf16_loss_decreases_over_200_steps(cuda):
-    """ResNet-50 on the bf16 channels-last path, SGD (lr 0.1, momentum 0.9, wd 1e-4) on
-    class-conditional synthetic data (the bench's generator) for 200 steps: training must work,
-    i.e. the loss of the last 20 steps is well below that of the first 20."""
+    """ResNet-50 on the bf16 channels-last path, SGD (lr 0.02, momentum 0.9, wd 1e-4) on
+    class-conditional synthetic data (the bench's generator, 10 classes) for 200 steps: training
+    must work -- the loss of the last 20 steps is well below chance level (ln 10) and below half
+    that of the first 20 (a run that diverges and falls back to chance fails both)."""
     from mxddp import native, ops
     from mxddp.models import resnet50
     from mxddp.optim import SGD
     from mxddp.parallel.flat import FlatParams
 
     torch.manual_seed(2)
-    nc, B, hw = 100, 32, 128
+    nc, B, hw = 10, 32, 128
     m = resnet50(num_classes=nc).to(cuda)
     flat = FlatParams(m, cuda)
-    opt = SGD(flat, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    opt = SGD(flat, lr=0.02, momentum=0.9, weight_decay=1e-4)
     Cn = native()
     D = 3 * hw * hw
     tmpl = torch.empty(nc * D, device=cuda)
@@ -125,4 +129,5 @@ def test_resnet50_bf16_loss_decreases_over_200_steps(cuda):
     first, last = ls[:20].mean().item(), ls[-20:].mean().item()
     print(f"resnet50 bf16: loss first 20 steps {first:.3f}, last 20 {last:.3f}")
     assert torch.isfinite(ls).all()
-    assert last < 0.5 * first, (first, last)
+    assert first < 2.0 * math.log(nc), (first, last)  # no early blow-up
+    assert last < 0.5 * math.log(nc) and last < 0.5 * first, (first, last)
