@@ -117,6 +117,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_bn_set_grid_cap", &nhwc_bn_set_grid_cap);
   m.def("nhwc_conv_set_split_blocks", &nhwc_conv_set_split_blocks);
   m.def("nhwc_wgrad_set_target", &nhwc_wgrad_set_target);
+  m.def("nhwc_wgrad_set_tile256", &nhwc_wgrad_set_tile256);
   m.def("mnist_set_wt_stores", &mnist_set_wt_stores,
         "MNIST bulk stores with agent scope (L2 write-through) for steps launched afterwards: mask 1 = F5, 2 = F2, "
         "4 = F6W");

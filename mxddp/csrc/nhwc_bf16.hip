@@ -1366,26 +1366,34 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* tile, int pitch, int col0,
   return res;
 }
 
-// TM x TN output tile (output channels x (r, s, c) columns), TM, TN in {64, 128}: 64-wide tiles
-// for the 64-channel layers (a 128-wide tile over a 64-channel operand computes 50-75 % zeros)
-template <int TM, int TN>
-__global__ __launch_bounds__(256) void wgrad_nhwc_kernel(WgNArgs a) {
+// TM x TN output tile (output channels x (r, s, c) columns) over WGM x WGN waves, TM, TN in
+// {64, 128, 256}: 64-wide tiles for the 64-channel layers (a 128-wide tile over a 64-channel
+// operand computes 50-75 % zeros).  The 256 x 256 tile (8 waves of 128 x 64, one 147 KB block per
+// CU) stages 1 KB per pixel for 128 K FLOP (128 FLOP per staged byte, vs 64 for 128 x 128: at
+// 64 FLOP/B a CU's 64 B/clk from L2 only just feeds its MFMAs, so the 128-tile kernel ran at
+// 17 % MFMA busy, profiles/r4_pmc/pmc_rn.txt).  The LDS pitch rule (width + 32, wg_swz) keeps the
+// row stride at 16 banks for every width, so the same swizzle stays conflict-free.
+template <int TM, int TN, int WGM = 2, int WGN = 2>
+__global__ __launch_bounds__(64 * WGM * WGN) void wgrad_nhwc_kernel(WgNArgs a) {
+  constexpr int NT = 64 * WGM * WGN;       // threads
   constexpr int BK = 64;                   // pixels per stage (two MFMA k-steps)
   constexpr int PA = TM + 32, PB = TN + 32;  // LDS pitches (see wg_swz)
   constexpr int VA = TM / 8, VB = TN / 8;  // 16-byte vectors per pixel row
-  constexpr int EA = BK * VA / 256, EB = BK * VB / 256;
-  constexpr int WMT = TM / 32, WNT = TN / 32;
+  static_assert(NT % VA == 0 && NT % VB == 0, "load roles: a thread keeps its vector column");
+  constexpr int EA = BK * VA / NT, EB = BK * VB / NT;
+  constexpr int WTM = TM / WGM, WTN = TN / WGN;  // wave tile
+  constexpr int WMT = WTM / 16, WNT = WTN / 16;
   __shared__ __attribute__((aligned(16))) bf16 As[2][BK * PA];  // dy tile  [pixel][k]
   __shared__ __attribute__((aligned(16))) bf16 Bs[2][BK * PB];  // x gather [pixel][(r,s,c)]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave / WGN, wn = wave % WGN;
   const int tiles_m = (a.Kout + TM - 1) / TM, tiles_n = (a.Ng + TN - 1) / TN;
   const int bid = blockIdx.x;
   const int tm = bid % tiles_m, r1 = bid / tiles_m, tn = r1 % tiles_n, sp = r1 / tiles_n;
   const int m0 = tm * TM, n0 = tn * TN;
   const int pbeg = sp * a.chunk, pend = min(a.Npix, pbeg + a.chunk);
   if (pbeg >= pend) return;
-  // load roles (fixed per thread: 256 is a multiple of VA and VB): A vector cva of pixel rows
-  // rowa0 + (256 / VA) i, B vector cvb of rows rowb0 + (256 / VB) i
+  // load roles (fixed per thread: NT is a multiple of VA and VB): A vector cva of pixel rows
+  // rowa0 + (NT / VA) i, B vector cvb of rows rowb0 + (NT / VB) i
   const int cva = tid % VA, rowa0 = tid / VA, cvb = tid % VB, rowb0 = tid / VB;
   // B column decomposition (fixed per thread): column n0 + 8 cvb -> (r, s, c)
   const int col = n0 + 8 * cvb;
@@ -1399,14 +1407,14 @@ __global__ __launch_bounds__(256) void wgrad_nhwc_kernel(WgNArgs a) {
   auto gload = [&](int p0) {
 #pragma unroll
     for (int i = 0; i < EA; ++i) {  // unconditional loads from clamped addresses, masked after
-      const int pix = p0 + rowa0 + (256 / VA) * i;
+      const int pix = p0 + rowa0 + (NT / VA) * i;
       const bool ok = pix < pend && k_ok;
       const u32x4 v = *reinterpret_cast<const u32x4*>(a.dy + (ok ? (size_t)pix * a.Kout + m0 + 8 * cva : 0));
       ra[i] = ok ? v : z4;
     }
 #pragma unroll
     for (int i = 0; i < EB; ++i) {
-      const int pix = p0 + rowb0 + (256 / VB) * i;
+      const int pix = p0 + rowb0 + (NT / VB) * i;
       const bool ok = pix < pend;
       const int pp = ok ? pix : 0;
       const int n = (int)a.fPQ.div((uint32_t)pp), rem = pp - n * a.P * a.Q;
@@ -1420,12 +1428,12 @@ __global__ __launch_bounds__(256) void wgrad_nhwc_kernel(WgNArgs a) {
   auto sstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < EA; ++i) {
-      const int r = rowa0 + (256 / VA) * i;
+      const int r = rowa0 + (NT / VA) * i;
       *reinterpret_cast<u32x4*>(&As[buf][r * PA + 8 * (cva ^ wg_swz(r))]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < EB; ++i) {
-      const int r = rowb0 + (256 / VB) * i;
+      const int r = rowb0 + (NT / VB) * i;
       *reinterpret_cast<u32x4*>(&Bs[buf][r * PB + 8 * (cvb ^ wg_swz(r))]) = rb[i];
     }
   };
@@ -1447,9 +1455,9 @@ __global__ __launch_bounds__(256) void wgrad_nhwc_kernel(WgNArgs a) {
     for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8 av[WMT], bv[WNT];
 #pragma unroll
-      for (int i = 0; i < WMT; ++i) av[i] = tr_frag(As[cur] + 32 * ks * PA, PA, wm * (TM / 2) + 16 * i, lane);
+      for (int i = 0; i < WMT; ++i) av[i] = tr_frag(As[cur] + 32 * ks * PA, PA, wm * WTM + 16 * i, lane);
 #pragma unroll
-      for (int j = 0; j < WNT; ++j) bv[j] = tr_frag(Bs[cur] + 32 * ks * PB, PB, wn * (TN / 2) + 16 * j, lane);
+      for (int j = 0; j < WNT; ++j) bv[j] = tr_frag(Bs[cur] + 32 * ks * PB, PB, wn * WTN + 16 * j, lane);
 #pragma unroll
       for (int i = 0; i < WMT; ++i)
 #pragma unroll
@@ -1463,13 +1471,13 @@ __global__ __launch_bounds__(256) void wgrad_nhwc_kernel(WgNArgs a) {
   float* pl = a.part + (size_t)sp * a.Kout * a.Ng;
 #pragma unroll
   for (int j = 0; j < WNT; ++j) {
-    const int cn = n0 + wn * (TN / 2) + 16 * j + (lane & 15);
+    const int cn = n0 + wn * WTN + 16 * j + (lane & 15);
     if (cn >= a.Ng) continue;
 #pragma unroll
     for (int i = 0; i < WMT; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int k = m0 + wm * (TM / 2) + 16 * i + 4 * (lane >> 4) + r;
+        const int k = m0 + wm * WTM + 16 * i + 4 * (lane >> 4) + r;
         if (k < a.Kout) pl[(size_t)k * a.Ng + cn] = acc[i][j][r];
       }
     }
@@ -2988,21 +2996,33 @@ int nhwc_conv_dgrad_bn_rows(int N, int H, int W, int C, int K, int R, int S, int
   return std::max(cdiv(M, 256), cdiv(M, 64) + 4);
 }
 
-static void wgrad_tile(int K, int Ng, int& tm, int& tn) {
+// 256 x 256 weight-gradient tiles where both GEMM dimensions reach 256 and the layer is a 3x3 or
+// has >= 96 K pixels (A/B: nhwc_wgrad_set_tile256).  Per layer at batch 256 (profiles/r5_wgrad/):
+// the 3x3 layers 395 -> 585, 402 -> 585 TF/s, 28 x 28 1x1 412 -> 482; the 1x1 layers of 14 x 14
+// and 7 x 7 (<= 50 K pixels, one block per CU with few stages each) 3-14 % slower, so they keep
+// the 128 x 128 tile.
+static int g_wgrad_tile256 = 1;
+void nhwc_wgrad_set_tile256(int on) { g_wgrad_tile256 = on; }
+static void wgrad_tile(int K, int Ng, int Npix, int RS, int& tm, int& tn) {
+  if (g_wgrad_tile256 && K >= 256 && Ng >= 256 && (RS > 1 || Npix >= 96 * 1024)) {
+    tm = tn = 256;
+    return;
+  }
   tm = K <= 64 ? 64 : 128;
   tn = Ng <= 64 ? 64 : 128;
 }
 
 // weight-gradient blocks aimed at (A/B: nhwc_wgrad_set_target; 256 and 1,024 measured no better,
-// profiles/r4_y/)
+// profiles/r4_y/); half that for the one-block-per-CU 256 x 256 tile
 static int g_wgrad_target = 512;
 void nhwc_wgrad_set_target(int n) { g_wgrad_target = n; }
-static int wgrad_splits(int Npix, int K, int Ng) {
+static int wgrad_splits(int Npix, int K, int Ng, int RS) {
   int tm, tn;
-  wgrad_tile(K, Ng, tm, tn);
+  wgrad_tile(K, Ng, Npix, RS, tm, tn);
   const int tiles = cdiv(K, tm) * cdiv(Ng, tn);
-  // ~2 blocks per CU, >= 512 pixels (8 stages) per block, partial planes <= 32M floats
-  const int target = g_wgrad_target;
+  // ~2 blocks per CU (1 for the 256 tile), >= 512 pixels (8 stages) per block, partial planes
+  // <= 32M floats
+  const int target = tm == 256 ? g_wgrad_target / 2 : g_wgrad_target;
   int splits = std::max(1, cdiv(target, tiles));
   splits = std::min(splits, std::max(1, Npix / 512));
   splits = std::min(splits, std::max(1, (int)((32ll << 20) / ((int64_t)K * Ng))));
@@ -3012,7 +3032,7 @@ static int wgrad_splits(int Npix, int K, int Ng) {
 
 size_t nhwc_wgrad_scratch_floats(int N, int Cp, int K, int R, int S, int P, int Q) {
   const int Ng = R * S * Cp;
-  size_t n = (size_t)wgrad_splits(N * P * Q, K, Ng) * K * Ng;
+  size_t n = (size_t)wgrad_splits(N * P * Q, K, Ng, R * S) * K * Ng;
   if (Cp == 8 && R == 7 && S == 7 && K == 64 && P % 16 == 0 && Q % 16 == 0)  // the stem kernel may run
     n = std::max(n, (size_t)kSwBlocks * K * Ng);
   if (Cp == 64 && K == 64 && R == 3 && S == 3 && Q <= 64 && Q % 8 == 0 && c3_band_rows(P, Q) >= 2)  // band kernel
@@ -3064,12 +3084,13 @@ void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, in
     return;
   }
   int tm, tn;
-  wgrad_tile(K, a.Ng, tm, tn);
+  wgrad_tile(K, a.Ng, a.Npix, R * S, tm, tn);
   const int tiles = cdiv(K, tm) * cdiv(a.Ng, tn);
-  const int splits = wgrad_splits(a.Npix, K, a.Ng);
+  const int splits = wgrad_splits(a.Npix, K, a.Ng, R * S);
   a.chunk = cdiv(cdiv(a.Npix, splits), 64) * 64;
   const dim3 grid(tiles * splits);
-  if (tm == 128 && tn == 128) MX_LAUNCH((wgrad_nhwc_kernel<128, 128>), grid, dim3(256), 0, st, a);
+  if (tm == 256) MX_LAUNCH((wgrad_nhwc_kernel<256, 256, 2, 4>), grid, dim3(512), 0, st, a);
+  else if (tm == 128 && tn == 128) MX_LAUNCH((wgrad_nhwc_kernel<128, 128>), grid, dim3(256), 0, st, a);
   else if (tm == 128) MX_LAUNCH((wgrad_nhwc_kernel<128, 64>), grid, dim3(256), 0, st, a);
   else if (tn == 128) MX_LAUNCH((wgrad_nhwc_kernel<64, 128>), grid, dim3(256), 0, st, a);
   else MX_LAUNCH((wgrad_nhwc_kernel<64, 64>), grid, dim3(256), 0, st, a);

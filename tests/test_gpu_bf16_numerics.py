@@ -8,7 +8,8 @@ Bottleneck blocks at a realistic shape (batch 32, 28 x 28, 256 channels) is comp
 CPU autograd of the same blocks, and so is stock ``torch.autocast(bfloat16)`` channels_last on
 the same GPU; mxddp's normwise error must stay within 1.5x stock's for EVERY gradient.
 
-Plus a 200-step ResNet-50 run on class-conditional synthetic data whose loss must fall.
+Plus a 100-step ResNet-50 run on class-conditional synthetic data next to stock autocast bf16:
+both must learn, and mxddp must end where stock ends.
 """
 import math
 
@@ -88,46 +89,86 @@ def test_bottlenecks_bf16_error_within_stock_bf16(cuda):
     assert not bad, "\n".join(r for r in rows if r.split()[0] in bad)
 
 
-def test_resnet50_bf16_loss_decreases_over_200_steps(cuda):
-    """ResNet-50 on the bf16 channels-last path, SGD (lr 0.02, momentum 0.9, wd 1e-4) on
-    class-conditional synthetic data (the bench's generator, 10 classes) for 200 steps: training
-    must work -- the loss of the last 20 steps is well below chance level (ln 10) and below half
-    that of the first 20 (a run that diverges and falls back to chance fails both)."""
+def _bn_fn(x, bn):
+    return F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias, training=True, momentum=0.1,
+                        eps=bn.eps)
+
+
+def _stock_resnet(m, x):
+    """mxddp's ResNet-50 module parameters through plain torch ops (stock MIOpen / hipBLASLt)."""
+    y = F.max_pool2d(F.relu(_bn_fn(F.conv2d(x, m.conv1.weight, stride=2, padding=3), m.bn1)), 3, 2, 1)
+    for layer in (m.layer1, m.layer2, m.layer3, m.layer4):
+        for b in layer:
+            h = F.relu(_bn_fn(F.conv2d(y, b.conv1.weight), b.bn1))
+            h = F.relu(_bn_fn(F.conv2d(h, b.conv2.weight, stride=b.conv2.stride, padding=1), b.bn2))
+            h = _bn_fn(F.conv2d(h, b.conv3.weight), b.bn3)
+            sc = y if b.downsample is None else _bn_fn(
+                F.conv2d(y, b.downsample[0].weight, stride=b.downsample[0].stride), b.downsample[1])
+            y = F.relu(h + sc)
+    return F.linear(y.float().mean((2, 3)), m.fc.weight, m.fc.bias)
+
+
+def test_resnet50_bf16_trains_like_stock_bf16(cuda):
+    """ResNet-50 on the bf16 channels-last path vs stock ``torch.autocast(bfloat16)`` channels_last
+    on the same init and the same 100 class-conditional synthetic batches (the bench's generator,
+    10 classes, batch 32, 128 px), SGD lr 0.005 / momentum 0.9 / wd 1e-4 (at lr >= 0.02 every path,
+    stock included, spikes to loss 30-40 in the first steps: scripts/diag_resnet_train.py,
+    profiles/r5_bf16/).  Training must work -- the last 10 steps' loss far below chance (ln 10) --
+    and end where stock ends (within 2x, or both near zero)."""
+    import copy
+
     from mxddp import native, ops
     from mxddp.models import resnet50
     from mxddp.optim import SGD
     from mxddp.parallel.flat import FlatParams
 
     torch.manual_seed(2)
-    nc, B, hw = 10, 32, 128
-    m = resnet50(num_classes=nc).to(cuda)
-    flat = FlatParams(m, cuda)
-    opt = SGD(flat, lr=0.02, momentum=0.9, weight_decay=1e-4)
+    nc, B, hw, steps, lr = 10, 32, 128, 100, 0.005
+    m0 = resnet50(num_classes=nc).to(cuda)
     Cn = native()
     D = 3 * hw * hw
     tmpl = torch.empty(nc * D, device=cuda)
     ctr = torch.zeros(4, dtype=torch.int32, device=cuda)
-    x = torch.empty((B, 3, hw, hw), device=cuda)
-    y = torch.empty(B, dtype=torch.int32, device=cuda)
     st = torch.cuda.current_stream(cuda).cuda_stream
     Cn.synth_templates(tmpl.data_ptr(), nc, D, 5, st)
-    losses = []
+    batches = []
+    for _ in range(steps):
+        x = torch.empty((B, 3, hw, hw), device=cuda)
+        y = torch.empty(B, dtype=torch.int32, device=cuda)
+        Cn.synth_batch(x.data_ptr(), y.data_ptr(), tmpl.data_ptr(), B, D, nc, 5, ctr.data_ptr(), st)
+        batches.append((x, y))
+
+    m = copy.deepcopy(m0)
+    opt = torch.optim.SGD(m.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4)
+    stock = []
+    for x, y in batches:
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = _stock_resnet(m, x.contiguous(memory_format=torch.channels_last))
+        loss = F.cross_entropy(out.float(), y.long())
+        loss.backward()
+        opt.step()
+        stock.append(loss.detach())
+
+    m = copy.deepcopy(m0)
+    flat = FlatParams(m, cuda)
+    opt = SGD(flat, lr=lr, momentum=0.9, weight_decay=1e-4)
+    mine = []
     ops.set_compute_dtype("bf16")
     try:
-        for _ in range(200):
-            Cn.synth_batch(x.data_ptr(), y.data_ptr(), tmpl.data_ptr(), B, D, nc, 5, ctr.data_ptr(), st)
+        for x, y in batches:
             opt.zero_grad()
             flat.attach_grads()
             loss = ops.cross_entropy(m(x), y)
             loss.backward()
             opt.step()
-            losses.append(loss.detach())
+            mine.append(loss.detach())
         torch.cuda.synchronize()
     finally:
         ops.set_compute_dtype("fp32")
-    ls = torch.stack(losses).float().cpu()
-    first, last = ls[:20].mean().item(), ls[-20:].mean().item()
-    print(f"resnet50 bf16: loss first 20 steps {first:.3f}, last 20 {last:.3f}")
+    ls, lst = torch.stack(mine).float().cpu(), torch.stack(stock).float().cpu()
+    first, last, slast = ls[:10].mean().item(), ls[-10:].mean().item(), lst[-10:].mean().item()
+    print(f"resnet50 bf16: mxddp loss first 10 steps {first:.3f}, last 10 {last:.3f}; stock last 10 {slast:.3f}")
     assert torch.isfinite(ls).all()
-    assert first < 2.0 * math.log(nc), (first, last)  # no early blow-up
-    assert last < 0.5 * math.log(nc) and last < 0.5 * first, (first, last)
+    assert last < 0.25 * math.log(nc), (first, last, slast)
+    assert last <= max(2.0 * slast, 0.3), (first, last, slast)

@@ -82,6 +82,38 @@ def test_conv_nhwc(cuda, case):
     assert _rel(wg.grad.cpu(), wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("case", [(2, 40, 9, 11, 320, 3, 1, 1),      # partial 256-tiles both ways
+                                  (32, 256, 56, 56, 256, 1, 1, 0),   # 1x1 with >= 96 K pixels
+                                  (2, 512, 7, 7, 512, 3, 2, 1)])     # stride 2, odd pixel count
+def test_wgrad_tile256(cuda, case):
+    """The 256 x 256 weight-gradient tile (8 waves) vs the 128 x 128 kernel and the fp32 reference."""
+    from mxddp import native
+
+    N, C, H, W, K, R, st, pd = case
+    Cn = native()
+    torch.manual_seed(3)
+    x = torch.randn(N, H, W, C).to(torch.bfloat16)
+    w = torch.randn(K, C, R, R) * (2.0 / (C * R * R)) ** 0.5
+    xr = _nchw(x)
+    wr = w.to(torch.bfloat16).float().requires_grad_()
+    yr = F.conv2d(xr, wr, None, st, pd)
+    gy = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(gy)
+    gyn = gy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(cuda)
+    grads = []
+    try:
+        for big in (1, 0):
+            Cn.nhwc_wgrad_set_tile256(big)
+            wg = w.to(cuda).requires_grad_()
+            nhwc.conv2d(x.to(cuda), wg, st, pd).backward(gyn)
+            torch.cuda.synchronize()
+            grads.append(wg.grad.cpu())
+    finally:
+        Cn.nhwc_wgrad_set_tile256(1)
+    assert _rel(grads[0], wr.grad) < 1e-2
+    assert _rel(grads[0], grads[1]) < 1e-5  # same fp32 products, different summation order only
+
+
 @pytest.mark.parametrize("case", [(2, 64, 14, 14, 192, 3, 1, 1), (3, 128, 13, 11, 64, 1, 1, 0),
                                   (2, 64, 15, 15, 128, 3, 2, 1), (1, 128, 9, 9, 256, 3, 1, 1),
                                   (1, 256, 7, 7, 128, 3, 1, 1),  # long reduction: split-K partials
