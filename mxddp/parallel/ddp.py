@@ -268,9 +268,22 @@ class _GlooReducer:
         self.next = 0
         self.works = []
 
-    def abort(self):
-        """Drop a step whose backward raised (its async all-reduces are abandoned, not joined:
-        the peers of a failed step may never post theirs)."""
+    def abort(self, timeout_s: float = 30.0):
+        """Drop a step whose backward raised.  Its launched all-reduces are joined first: they
+        write into the gradient buffer in place, and one finishing after the next step's
+        zero_grad() would corrupt that step.  When every rank raised at the same point (the same
+        buckets launched everywhere: a deterministic error) they complete at once; a rank whose
+        peers never posted them is out of step for good, and that is raised after `timeout_s`
+        instead of hanging (as with torch DDP, an error on one rank only is fatal to the job)."""
+        import datetime
+
+        for _off, _n, _t, w in self.works:
+            try:
+                w.wait(timeout=datetime.timedelta(seconds=timeout_s))
+            except Exception as e:  # gloo raises on timeout
+                self.prepare()
+                raise RuntimeError("DDP abort: the peers did not post the failed step's bucket all-reduces -- "
+                                   "the backward raised on this rank only and the ranks are out of step") from e
         self.prepare()
 
     def mark_ready(self, p, _stream=0):

@@ -293,3 +293,79 @@ def test_ddp_batchnorm_model_matches_simulated_ranks():
         if k.endswith("weight") or k.endswith("bias"):
             assert torch.equal(out[0][k], out[1][k]), k
     assert not torch.equal(out[0]["bn1.running_mean"], out[1]["bn1.running_mean"])
+
+
+def _abort_worker(rank, ws, port, fail, q):
+    """Three DDP steps of the MNIST CNN; with `fail`, an extra step in the middle whose backward
+    raises on every rank after the fc bucket's all-reduce was launched (a hook on conv2's output
+    gradient runs after fc1 / fc2 have their gradients)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from mxddp import ops
+    from mxddp.optim import SGD
+    from mxddp.parallel import comm
+    from mxddp.parallel.ddp import DistributedDataParallel as DDP
+
+    comm.init_distributed(rank=rank, world_size=ws, use_gpu=False, init_method=f"tcp://127.0.0.1:{port}")
+    torch.manual_seed(0)
+    model = build_model("mnist_cnn")
+    ddp = DDP(model)
+    opt = SGD(ddp.flat, lr=0.05, momentum=0.9, weight_decay=1e-4)
+    b = 4
+    batches = _batches(3, ws * b, model.input_shape)
+    armed = {"on": False}
+
+    def boom(g):
+        if armed["on"]:
+            raise RuntimeError("injected backward failure")
+        return g
+
+    def attach(_m, _i, o):  # (returns None: a forward hook's return value would replace the output)
+        if o.requires_grad:
+            o.register_hook(boom)
+
+    handle = model.conv2.register_forward_hook(attach)
+    launched = None
+    for i, (x, y) in enumerate(batches):
+        if fail and i == 1:
+            armed["on"] = True
+            opt.zero_grad()
+            try:
+                ops.cross_entropy(ddp(x[rank * b:(rank + 1) * b]), y[rank * b:(rank + 1) * b]).backward()
+            except RuntimeError as e:
+                assert "injected" in str(e)
+                launched = len(ddp.reducer.works)
+            armed["on"] = False
+        opt.zero_grad()
+        ops.cross_entropy(ddp(x[rank * b:(rank + 1) * b]), y[rank * b:(rank + 1) * b]).backward()
+        opt.step()
+    handle.remove()
+    q.put((rank, launched, {k: v.detach().numpy().copy() for k, v in model.state_dict().items()}))
+    comm.shutdown()
+
+
+def test_ddp_recovers_from_backward_that_raised_on_every_rank():
+    """Reducer.abort (ddp.py forward): a backward that raised after its first bucket's all-reduce
+    was launched leaves that step's reducer state behind; the next forward joins the launched
+    all-reduces (they write the gradient buffer in place) and drops the step, so training goes on
+    exactly as if the failed step had never run -- on every rank."""
+    ctx = mp.get_context("spawn")
+    res = {}
+    for fail in (False, True):
+        q = ctx.Queue()
+        port = _free_port()
+        ps = [ctx.Process(target=_abort_worker, args=(r, 2, port, fail, q)) for r in range(2)]
+        for p in ps:
+            p.start()
+        out = {}
+        for _ in range(2):
+            r, launched, sd = q.get(timeout=240)
+            out[r] = (launched, sd)
+        for p in ps:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        res[fail] = out
+    for r in range(2):
+        assert res[True][r][0] == 1  # the fc bucket's all-reduce was in flight when it raised
+        for k, v in res[False][r][1].items():
+            assert (res[True][r][1][k] == v).all(), (r, k)

@@ -224,9 +224,12 @@ def _commdtype_worker(rank, ws, port, model_name, b, q):
     res, bad = {}, []
     for cd in ("fp32", "bf16"):
         torch.manual_seed(0)
-        ddp = DDP(build_model(model_name).to(dev), grad_comm_dtype=cd)
+        # transport pinned: the bf16 shadow path through PeerComm::all_reduce (reducer.cpp via_peer)
+        ddp = DDP(build_model(model_name).to(dev), grad_comm_dtype=cd, transport="peer")
         if cd == "bf16" and str(ddp.reducer.comm_dtype) != "DType.bf16":
             bad.append(("comm dtype", str(ddp.reducer.comm_dtype)))
+        if ddp.transport != "peer":
+            bad.append(("transport", ddp.transport))
         opt = SGD(ddp.flat, lr=0.02, momentum=0.9, weight_decay=1e-4)
         res[cd + "0"] = ddp.flat.data.cpu().clone()
         for x, y in batches:
