@@ -18,7 +18,9 @@ from .layers import BatchNorm2d, Conv2d, Linear, MaxPool2d
 
 
 def _nhwc_mode(x) -> bool:
-    return x.is_cuda and ops.compute_dtype() == "bf16"
+    # not under ops.torch_reference_mode (bench.py --impl torch): the stock baseline must run
+    # PyTorch's own kernels end to end, never mxddp's NHWC ones
+    return x.is_cuda and ops.compute_dtype() == "bf16" and not ops.torch_reference_active()
 
 
 class Bottleneck(nn.Module):

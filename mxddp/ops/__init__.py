@@ -44,6 +44,11 @@ class torch_reference_mode:
         _TORCH_REFERENCE = self._prev
 
 
+def torch_reference_active() -> bool:
+    """True inside ``torch_reference_mode``: models must not take a native-only path."""
+    return _TORCH_REFERENCE
+
+
 def _native(t: torch.Tensor) -> bool:
     return t.is_cuda and not _TORCH_REFERENCE
 

@@ -91,6 +91,7 @@ for step in "$@"; do
     rn_stock) run rn_stock 300 python bench.py --model resnet50 --dtype bf16 --batch 256 --steps 10 --warmup 3 --impl torch --channels-last ;;
     prof_rn32) prof prof_rn32 10 --model resnet50 --dtype bf16 --batch 32 --steps 10 --warmup 2 --min-warmup-ms 0 ;;
     prof_rn) prof prof_rn 3 --model resnet50 --dtype bf16 --batch 256 --steps 3 --warmup 2 --min-warmup-ms 0 ;;
+    prof_rn_stock) prof prof_rn_stock 3 --model resnet50 --dtype bf16 --batch 256 --steps 3 --warmup 2 --min-warmup-ms 0 --impl torch --channels-last ;;
     pmc_rn) pmc pmc_rn --model resnet50 --dtype bf16 --batch 256 --steps 1 --warmup 1 --no-graph --min-warmup-ms 0 ;;
     pyr) run pyr 300 python bench.py --model pyramidnet110 --steps 20 --warmup 3 ;;
     pyr_stock) run pyr_stock 300 python bench.py --model pyramidnet110 --steps 20 --warmup 3 --impl torch ;;

@@ -104,3 +104,20 @@ def test_pyramidnet_block_matches_reference_formula(stride):
     out.backward(g)
     ref.backward(g)
     assert torch.allclose(x.grad, xr.grad, atol=1e-5)
+
+
+def test_resnet_stock_baseline_never_takes_the_native_nhwc_path(monkeypatch):
+    """bench.py --impl torch (the stock PyTorch-ROCm baseline) runs under ops.torch_reference_mode
+    with the compute dtype set to bf16: ResNet must then take its torch-op path, not mxddp's NHWC
+    kernels (which made the round-3/4 "stock" ResNet-50 numbers mxddp's own)."""
+    from types import SimpleNamespace
+
+    from mxddp import ops
+    from mxddp.models import resnet as R
+
+    monkeypatch.setattr(ops, "compute_dtype", lambda: "bf16")
+    x = SimpleNamespace(is_cuda=True)
+    assert R._nhwc_mode(x)
+    with ops.torch_reference_mode():
+        assert not R._nhwc_mode(x)
+    assert R._nhwc_mode(x)
