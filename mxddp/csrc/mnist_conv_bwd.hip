@@ -142,13 +142,22 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
       tB += t - tq;
       tq = t;
     }
-    // (C) k-step s: tile t = 6g + s of the chunk
+    // (C) k-step s: tile t = 6g + s of the chunk.  The next k-step's B fragments are read from LDS
+    // before this step's MFMAs (kept there by the scheduling barrier): loaded at their use, each
+    // group of 8 MFMAs waited for an LDS round trip (lgkmcnt(0) in the ISA, ~30 % of phase C)
+    const float4* vp0 = reinterpret_cast<const float4*>(vs + ((6 * g) * 16 + m) * kF6WVP);
+    float4 bb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bb[i] = vp0[i];
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
-      const float4* vp = reinterpret_cast<const float4*>(vs + ((6 * g + s) * 16 + m) * kF6WVP);
-      float4 bb[4];
+      float4 bn[4];
+      if (s + 1 < 6) {
+        const float4* vp = reinterpret_cast<const float4*>(vs + ((6 * g + s + 1) * 16 + m) * kF6WVP);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) bb[i] = vp[i];
+        for (int i = 0; i < 4; ++i) bn[i] = vp[i];
+      }
+      __builtin_amdgcn_sched_barrier(0);
       const float v = dv[s];
       const bool qy = (qv[s] >> 1) & 1, qx = qv[s] & 1;
       const float vy[4] = {qy ? 0.f : v, v, qy ? -v : v, qy ? -v : 0.f};
@@ -159,6 +168,10 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
         acc[4 * i + 1] = mfma4(vy[i], bb[i].y, acc[4 * i + 1]);
         acc[4 * i + 2] = mfma4(w2, bb[i].z, acc[4 * i + 2]);
         acc[4 * i + 3] = mfma4(w3, bb[i].w, acc[4 * i + 3]);
+      }
+      if (s + 1 < 6) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bb[i] = bn[i];
       }
     }
     if (trc) tC += (uint32_t)__builtin_amdgcn_s_memrealtime() - tq;  // issue time of (C)
