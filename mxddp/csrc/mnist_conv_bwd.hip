@@ -34,13 +34,13 @@ namespace {
 // 748k img/s; blocks split over co halves: 917k vs 951k; round 5, profiles/r5_f6split: blocks split
 // over the Winograd rows (2 x 8 of the 16 GEMMs, partial slabs): F6W 24 -> 18 us but F7W 19 -> 23 us
 // beside the extra blocks, 903k vs 929k.)
-constexpr int kF6WA1P = 164, kF6WVP = 20;
-constexpr size_t kF6WLds = sizeof(float) * (784 + 160 + 16 * kF6WA1P + 24 * 16 * kF6WVP);
+constexpr int kF6WA1P = 164, kF6WVP = 20, kF6WV = 24 * 16 * kF6WVP;
+constexpr size_t kF6WLds = sizeof(float) * (784 + 160 + 16 * kF6WA1P + 2 * kF6WV);
 __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc, float* sm, int braw, int nblk) {
   MX_TRACE_B(f, 3, 0, braw);
   constexpr int kA1P = kF6WA1P;
   float* a1s = sm + 784 + 160;  // [16 ci][kA1P]: 6 a1 rows x 26
-  float* vs = a1s + 16 * kA1P;  // [24 t][16 ci][20]
+  float* vs = a1s + 16 * kA1P;  // 2 x [24 t][16 ci][20]: chunk c's V in buffer c & 1
   const int bid = xcd_remap(braw, nblk);
   const int b = bid / 2, h = bid & 1;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
@@ -70,53 +70,79 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
   f32x4 acc[16];
 #pragma unroll
   for (int x = 0; x < 16; ++x) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // (B) item i (< 384) of a chunk: V = B^T d B of tile tl = i / 16, channel ci = i % 16 (a1 rows
+  // 2(tl/12).., cols 2(tl%12)..) -- its 16 LDS reads, then the transform into V buffer vb
+  auto b_load = [&](int i, float (&d)[16]) {
+    const int ci = i & 15, tl = i >> 4, tyl = tl / 12, tx = tl - 12 * tyl;
+    const float* ap = a1s + ci * kA1P + 2 * tyl * 26 + 2 * tx;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) d[4 * r + cc] = ap[r * 26 + cc];
+  };
+  auto b_store = [&](int i, const float (&d)[16], float* vb) {
+    float e[4][4];
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      e[0][cc] = d[cc] - d[8 + cc];
+      e[1][cc] = d[4 + cc] + d[8 + cc];
+      e[2][cc] = d[8 + cc] - d[4 + cc];
+      e[3][cc] = d[4 + cc] - d[12 + cc];
+    }
+    float4* vp = reinterpret_cast<float4*>(vb + ((i >> 4) * 16 + (i & 15)) * kF6WVP);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      vp[r] = make_float4(e[r][0] - e[r][2], e[r][1] + e[r][2], e[r][2] - e[r][1], e[r][1] - e[r][3]);
+  };
   MX_TRACE_B(f, 3, 1, braw);
   uint32_t tA = 0, tB = 0, tC = 0, tq = 0;  // phase-time sums (trace only)
   const bool trc = f.trace && threadIdx.x == 0 && braw < 1024;
+  if (trc) tq = (uint32_t)__builtin_amdgcn_s_memrealtime();
+  // prologue: chunk 0's a1 rows -> LDS, its V (the only (B) not hidden under MFMAs)
+  *reinterpret_cast<float4*>(a1s + a1dst[0]) = pa0;
+  *reinterpret_cast<float4*>(a1s + a1dst[1]) = pa1;
+  if (a1dst[2] >= 0) *reinterpret_cast<float4*>(a1s + a1dst[2]) = pa2;
+  {
+    const float* nb = a1b + 104;
+    pa0 = *reinterpret_cast<const float4*>(nb + a1src[0]);
+    pa1 = *reinterpret_cast<const float4*>(nb + a1src[1]);
+    pa2 = *reinterpret_cast<const float4*>(nb + a1src[2]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = tid + 256 * k;
+    if (i < 384) {
+      float d[16];
+      b_load(i, d);
+      b_store(i, d, vs);
+    }
+  }
+  __syncthreads();
+  if (trc) {
+    const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    tB += t - tq;
+  }
+  // Chunk c: (A) chunk c + 1's a1 rows -> LDS (chunk c's were consumed by its (B) before the
+  // barrier closing the previous chunk), then (C) -- chunk c's 36 k-steps of MFMAs on V buffer
+  // c & 1 -- with chunk c + 1's (B) into the other buffer interleaved between the k-steps: the
+  // transform's LDS reads, VALU and LDS writes issue while the MFMAs run (as two separate phases
+  // with a barrier between them, the block's MFMAs idled through 3.7 us of (B), r5_f6pf).
 #pragma unroll 1
   for (int c = 0; c < 6; ++c) {
     if (trc) tq = (uint32_t)__builtin_amdgcn_s_memrealtime();
-    // (A) published a1 rows -> LDS (the previous chunk's phase-B reads of a1s finished before the
-    // barrier ahead of its phase C); next chunk's rows in flight
-    *reinterpret_cast<float4*>(a1s + a1dst[0]) = pa0;
-    *reinterpret_cast<float4*>(a1s + a1dst[1]) = pa1;
-    if (a1dst[2] >= 0) *reinterpret_cast<float4*>(a1s + a1dst[2]) = pa2;
-    if (c + 1 < 6) {
-      const float* nb = a1b + 104 * (c + 1);
-      pa0 = *reinterpret_cast<const float4*>(nb + a1src[0]);
-      pa1 = *reinterpret_cast<const float4*>(nb + a1src[1]);
-      pa2 = *reinterpret_cast<const float4*>(nb + a1src[2]);
-    }
-    __syncthreads();
-    if (trc) {
-      const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime();
-      tA += t - tq;
-      tq = t;
-    }
-    // (B) V = B^T d B of 24 tiles x 16 ci; tile tl: a1 rows 2(tl/12).., cols 2(tl%12)..
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int i = tid + 256 * k;
-      if (i < 384) {
-        const int ci = i & 15, tl = i >> 4, tyl = tl / 12, tx = tl - 12 * tyl;
-        const float* ap = a1s + ci * kA1P + 2 * tyl * 26 + 2 * tx;
-        float d[4][4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int cc = 0; cc < 4; ++cc) d[r][cc] = ap[r * 26 + cc];
-        float e[4][4];
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-          e[0][cc] = d[0][cc] - d[2][cc];
-          e[1][cc] = d[1][cc] + d[2][cc];
-          e[2][cc] = d[2][cc] - d[1][cc];
-          e[3][cc] = d[1][cc] - d[3][cc];
-        }
-        float4* vp = reinterpret_cast<float4*>(vs + (tl * 16 + ci) * kF6WVP);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          vp[r] = make_float4(e[r][0] - e[r][2], e[r][1] + e[r][2], e[r][2] - e[r][1], e[r][1] - e[r][3]);
+    const bool nxt = c + 1 < 6;
+    float* vcur = vs + (c & 1) * kF6WV;
+    float* vnext = vs + ((c + 1) & 1) * kF6WV;
+    if (nxt) {
+      *reinterpret_cast<float4*>(a1s + a1dst[0]) = pa0;
+      *reinterpret_cast<float4*>(a1s + a1dst[1]) = pa1;
+      if (a1dst[2] >= 0) *reinterpret_cast<float4*>(a1s + a1dst[2]) = pa2;
+      if (c + 2 < 6) {
+        const float* nb = a1b + 104 * (c + 2);
+        pa0 = *reinterpret_cast<const float4*>(nb + a1src[0]);
+        pa1 = *reinterpret_cast<const float4*>(nb + a1src[1]);
+        pa2 = *reinterpret_cast<const float4*>(nb + a1src[2]);
       }
     }
     // this chunk's dp / q operands; prefetch the next chunk's
@@ -129,34 +155,39 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
       qv[2 * k] = qn[k] & 0xffu;
       qv[2 * k + 1] = qn[k] >> 8;
     }
-    if (c + 1 < 6) {
+    if (nxt) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         dn[k] = *reinterpret_cast<const float2*>(dpl + 24 * (c + 1) + 2 * k);
         qn[k] = qpl[12 * (c + 1) + k];
       }
     }
-    __syncthreads();
+    __syncthreads();  // chunk c + 1's a1 rows are in LDS
     if (trc) {
       const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime();
-      tB += t - tq;
+      tA += t - tq;
       tq = t;
     }
     // (C) k-step s: tile t = 6g + s of the chunk.  The next k-step's B fragments are read from LDS
     // before this step's MFMAs (kept there by the scheduling barrier): loaded at their use, each
-    // group of 8 MFMAs waited for an LDS round trip (lgkmcnt(0) in the ISA, ~30 % of phase C)
-    const float4* vp0 = reinterpret_cast<const float4*>(vs + ((6 * g) * 16 + m) * kF6WVP);
+    // group of 8 MFMAs waited for an LDS round trip (lgkmcnt(0) in the ISA, ~30 % of phase C).
+    // Chunk c + 1's (B) items: item 0 read at k-step 0 and transformed + stored at k-step 1, item 1
+    // (threads < 128) at k-steps 2 and 3.
+    const float4* vp0 = reinterpret_cast<const float4*>(vcur + ((6 * g) * 16 + m) * kF6WVP);
     float4 bb[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) bb[i] = vp0[i];
+    float db[16];
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
       float4 bn[4];
       if (s + 1 < 6) {
-        const float4* vp = reinterpret_cast<const float4*>(vs + ((6 * g + s + 1) * 16 + m) * kF6WVP);
+        const float4* vp = reinterpret_cast<const float4*>(vcur + ((6 * g + s + 1) * 16 + m) * kF6WVP);
 #pragma unroll
         for (int i = 0; i < 4; ++i) bn[i] = vp[i];
       }
+      if (nxt && s == 0) b_load(tid, db);
+      if (nxt && s == 2 && tid < 128) b_load(tid + 256, db);
       __builtin_amdgcn_sched_barrier(0);
       const float v = dv[s];
       const bool qy = (qv[s] >> 1) & 1, qx = qv[s] & 1;
@@ -169,12 +200,15 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
         acc[4 * i + 2] = mfma4(w2, bb[i].z, acc[4 * i + 2]);
         acc[4 * i + 3] = mfma4(w3, bb[i].w, acc[4 * i + 3]);
       }
+      if (nxt && s == 1) b_store(tid, db, vnext);
+      if (nxt && s == 3 && tid < 128) b_store(tid + 256, db, vnext);
       if (s + 1 < 6) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) bb[i] = bn[i];
       }
     }
-    if (trc) tC += (uint32_t)__builtin_amdgcn_s_memrealtime() - tq;  // issue time of (C)
+    __syncthreads();  // chunk c + 1's V complete; every read of chunk c's V done
+    if (trc) tC += (uint32_t)__builtin_amdgcn_s_memrealtime() - tq;  // (C) with the next (B)
   }
   MX_TRACE_B(f, 3, 2, braw);
   // dw = G^T dU G, G^T = [1 .5 .5 0; 0 .5 -.5 0; 0 .5 .5 1]; acc[4i + j'][j] = dU[i][j'] of
@@ -462,7 +496,7 @@ __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc,
 // the peers' matching blocks while the remaining blocks do the conv backward, so the 4.7 MB
 // exchange overlaps it inside ONE launch (no side stream, no cross-queue fence).  co_blocks is
 // a multiple of 8, so the conv part keeps its XCD-aware block mapping.
-__global__ __launch_bounds__(256, 3) void f67_conv2_bwd_kernel(MnistFused f, Scratch sc) {
+__global__ __launch_bounds__(256, 2) void f67_conv2_bwd_kernel(MnistFused f, Scratch sc) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   if ((int)blockIdx.x < f.co_blocks) {
     MX_TRACE_B(f, 5, 0, (int)blockIdx.x);  // trace: exchange blocks vs conv blocks of this launch
