@@ -96,6 +96,7 @@ for step in "$@"; do
     pyr) run pyr 300 python bench.py --model pyramidnet110 --steps 20 --warmup 3 ;;
     pyr_stock) run pyr_stock 300 python bench.py --model pyramidnet110 --steps 20 --warmup 3 --impl torch ;;
     prof_pyr) prof prof_pyr 5 --model pyramidnet110 --steps 5 --warmup 2 --min-warmup-ms 0 ;;
+    prof_pyr_stock) prof prof_pyr_stock 5 --model pyramidnet110 --steps 5 --warmup 2 --min-warmup-ms 0 --impl torch ;;
     ws2) ws ws2 2 --steps 1000 --warmup 50 ;;
     ws4) ws ws4 4 --steps 500 --warmup 20 ;;
     ws8) ws ws8 8 --steps 200 --warmup 20 ;;
