@@ -186,8 +186,7 @@ def main():
         if hasattr(tr, "autotune") and a.graph_mode is None and not a.no_autotune and tr.eng.reducer_active:
             tr.step(1)
             tr.autotune()  # untimed: a few real steps per candidate strategy, before the warm-up
-        if os.environ.get("MXDDP_WARM_GRAPHS", "1") == "1":
-            tr.warm_graphs()
+        tr.warm_graphs()
     elif a.impl == "fused":
         from mxddp.engine import FusedMnistTrainer
 
@@ -218,8 +217,7 @@ def main():
                                   "buckets": getattr(tr, "bucket_strategy", None), "transport": tr.active_transport}, indent=1))
             C.shutdown()
             return
-        if os.environ.get("MXDDP_WARM_GRAPHS", "1") == "1":
-            tr.warm_graphs()  # untimed: first launch of every captured graph (real steps)
+        tr.warm_graphs()  # untimed: first launch of every captured graph (real steps)
     else:
         run = _layers_or_torch(a, torch, inf, dev, comm, B)
 

@@ -1725,16 +1725,6 @@ __global__ __launch_bounds__(512) void wgrad_c3_kernel(WgNArgs a, int rt, int nb
   }
 }
 
-// MXDDP_WGRAD_C3=0: the generic weight-gradient kernel for this layer too (A/B switch; the band
-// kernel measured 90 vs ~243 us per call at batch 256, profiles/r3_wgrad_c3/)
-static bool wgrad_c3_mode() {
-  static const bool on = [] {
-    const char* e = std::getenv("MXDDP_WGRAD_C3");
-    return !(e && *e == '0');
-  }();
-  return on;
-}
-
 static bool wgrad_c3_eligible(const WgNArgs& a) {
   return a.Ca == 64 && a.Kout == 64 && a.R == 3 && a.S == 3 && a.sh == 1 && a.sw == 1 && a.ph == 1 && a.pw == 1 &&
          a.P == a.H && a.Q == a.W && a.Q <= 64 && a.Q % 8 == 0 && c3_band_rows(a.P, a.Q) >= 2;
@@ -2742,25 +2732,6 @@ size_t nhwc_conv_scratch_floats(int M, int Ng, int Kg) {
   return n;
 }
 
-// MXDDP_STEM=0: the ResNet stem on the generic gather kernel (A/B switch for the stem kernel)
-static bool stem_mode() {
-  static const bool on = [] {
-    const char* e = std::getenv("MXDDP_STEM");
-    return !(e && *e == '0');
-  }();
-  return on;
-}
-
-// MXDDP_CONV_C3=0: the 3x3 / 64-channel layers' forward and data gradient on the generic kernels
-// (A/B switch for the band kernel alone; MXDDP_STEM covers the stem kernels only)
-static bool conv_c3_mode() {
-  static const bool on = [] {
-    const char* e = std::getenv("MXDDP_CONV_C3");
-    return !(e && *e == '0');
-  }();
-  return on;
-}
-
 // forward BN statistics in the split-K reduce: one row per `bpr` blocks (>= 8 pixels per row,
 // <= 2,048 blocks); the channel quads must tile the grid stride (ResNet's power-of-two widths)
 static int splitk_bn_bpr(int Ng) { return std::max(1, Ng / 1024); }
@@ -2793,7 +2764,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   a.fOHW = FastDiv(a.OH * a.OW);
   a.fCa = FastDiv(a.Ca);
   a.fS = FastDiv(a.S);
-  if (c3_eligible(a) && conv_c3_mode()) {  // persistent band kernel (forward or data gradient)
+  if (c3_eligible(a)) {  // persistent band kernel (forward or data gradient)
     const int rt = c3_band_rows(a.OH, a.OW), nb = a.M / (rt * a.OW);
     // BN rows: one per band (nhwc_conv_bn_rows sized the buffer for them); no backward statistics
     if (!(a.bnpart && !a.dgrad && nb <= 16384)) a.bnpart = nullptr;
@@ -2803,7 +2774,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     else MX_LAUNCH(conv3x3_s1_c64_kernel<false>, dim3(blocks), dim3(512), 0, st, a, rt, nb);
     return a.bnpart ? nb : 0;
   }
-  if (stem_eligible(a) && stem_mode()) {  // 16 x 16 output tiles: M / 256 blocks
+  if (stem_eligible(a)) {  // 16 x 16 output tiles: M / 256 blocks
     const int gx = a.M / 256;
     if (!(a.bnpart && gx <= 16384)) a.bnpart = nullptr;
     if (a.bnpart) MX_LAUNCH(conv_nhwc_stem_kernel<true>, dim3(gx), dim3(512), 0, st, a);
@@ -3069,7 +3040,7 @@ void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, in
   a.fCa = FastDiv(Cp);
   a.fS = FastDiv(S);
   MX_CHECK((int64_t)K * a.Ng < (1ll << 31), "nhwc wgrad: weight too large for 32-bit indices");
-  if (wgrad_c3_eligible(a) && wgrad_c3_mode()) {  // persistent band kernel, one plane per block
+  if (wgrad_c3_eligible(a)) {  // persistent band kernel, one plane per block
     const int rt = c3_band_rows(P, Q);
     MX_LAUNCH(wgrad_c3_kernel, dim3(kSwBlocks), dim3(512), 0, st, a, rt, N * (P / rt));
     const int plane4 = K * a.Ng / 4;
@@ -3077,7 +3048,7 @@ void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, in
               Cp, Cin, R * S, accumulate ? 1 : 0, 16);
     return;
   }
-  if (wgrad_stem_eligible(a) && stem_mode()) {  // persistent LDS-patch kernel, one plane per block
+  if (wgrad_stem_eligible(a)) {  // persistent LDS-patch kernel, one plane per block
     MX_LAUNCH(wgrad_stem_kernel, dim3(kSwBlocks), dim3(512), 0, st, a, N * (P / 16) * (Q / 16));
     const int plane4 = K * a.Ng / 4;
     MX_LAUNCH(wgrad_nhwc_reduce_k, dim3(cdiv(plane4, 256 / 16)), dim3(256), 0, st, scratch, dw, kSwBlocks, K, a.Ng,

@@ -133,7 +133,7 @@ def _rebuild(bank) -> None:
         bank.native.add(e.w.data_ptr(), e.U.data_ptr(), _p(e.Ud), e.w.shape[0], e.w.shape[1])
 
 
-_BANK_ON = os.environ.get("MXDDP_FILTER_BANK", "1") != "0"  # 0: per-conv transforms (A/B, tests)
+_BANK_ON = True  # False: per-conv transforms (tests compare the two)
 
 
 def _filter_entry(w, geom, needs_dgrad):

@@ -292,9 +292,9 @@ def conv2d(x, w, stride=1, padding=0, pack: WeightPack | None = None, join: Grad
     return y
 
 
-# MXDDP_BN_STATS_IN_CONV=0: every BN runs its own statistics passes, forward and backward (A/B
-# switch for the conv-epilogue statistics)
-_BN_STATS_IN_CONV = os.environ.get("MXDDP_BN_STATS_IN_CONV", "1") == "1"
+# False: every BN runs its own statistics passes, forward and backward (the conv-epilogue
+# statistics measured a win on every ResNet-50 layer, docs/BENCHMARKS.md; tests may flip it)
+_BN_STATS_IN_CONV = True
 # Backward BN statistics in the consuming conv's data-gradient epilogue: OFF by default.  Measured
 # per layer at batch 256 (scripts/bench_nhwc_layers.py, profiles/r4_d/rn_layers.log) the epilogue
 # adds 2.9 ms to the step's data gradients (the LDS-DMA kernel runs one block per CU, so the x

@@ -44,7 +44,7 @@ def peer_comm(cap_bytes: int = 32 << 20, blocks: int | None = None):
         return None
     C = native()
     if blocks is None:
-        blocks = int(os.environ.get("MXDDP_PEER_BLOCKS", "64"))
+        blocks = 64
     pc, err = None, ""
     try:
         pc = C.PeerComm(inf.rank, inf.world_size, inf.device.index, cap_bytes, blocks)
