@@ -35,7 +35,207 @@ namespace {
 // over the Winograd rows (2 x 8 of the 16 GEMMs, partial slabs): F6W 24 -> 18 us but F7W 19 -> 23 us
 // beside the extra blocks, 903k vs 929k.)
 constexpr int kF6WA1P = 164, kF6WVP = 20, kF6WV = 24 * 16 * kF6WVP;
-constexpr size_t kF6WLds = sizeof(float) * (784 + 160 + 16 * kF6WA1P + 2 * kF6WV);
+// f6w_body: two V buffers (75 KB, two blocks per CU -- the grid without exchange blocks is exactly
+// two per CU); f6w_body_serial: one (45 KB, three per CU)
+constexpr size_t kF6WLdsPipe = sizeof(float) * (784 + 160 + 16 * kF6WA1P + 2 * kF6WV);
+constexpr size_t kF6WLdsSerial = sizeof(float) * (784 + 160 + 16 * kF6WA1P + kF6WV);
+// F6W epilogue (both variants): dw = G^T dU G of the block's accumulators -> the image's slab.
+__device__ __forceinline__ void f6w_epilogue(const MnistFused& f, const Scratch& sc, float* sm, const f32x4 (&acc)[16],
+                                             int b, int h, int braw, bool trc, uint32_t tA, uint32_t tB, uint32_t tC) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  MX_TRACE_B(f, 3, 2, braw);
+  // dw = G^T dU G, G^T = [1 .5 .5 0; 0 .5 -.5 0; 0 .5 .5 1]; acc[4i + j'][j] = dU[i][j'] of
+  // (co = 16w + 4g + j, ci = 16h + m).  This block's [64 co][16 ci][9] result is staged in LDS
+  // (over the idle operand tiles) and written to the image's slab in canonical [co][ci][ky][kx]
+  // order with coalesced 16-byte stores -- no atomics (the atomic epilogue was ~3 us and delayed
+  // the F7W blocks' own atomics behind it); the finalize sums the B slabs in a fixed order.
+  float* st = sm;  // [64 co][16 ci][9]
+  __syncthreads();  // every wave's phase-C reads of the operand tiles are done
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int cj = 16 * w + 4 * g + j;
+    float t[3][4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const float m0 = acc[jj][j], m1 = acc[4 + jj][j], m2 = acc[8 + jj][j], m3 = acc[12 + jj][j];
+      t[0][jj] = m0 + 0.5f * (m1 + m2);
+      t[1][jj] = 0.5f * (m1 - m2);
+      t[2][jj] = 0.5f * (m1 + m2) + m3;
+    }
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      float* sp = st + (cj * 16 + m) * 9 + 3 * ky;
+      sp[0] = t[ky][0] + 0.5f * (t[ky][1] + t[ky][2]);
+      sp[1] = 0.5f * (t[ky][1] - t[ky][2]);
+      sp[2] = 0.5f * (t[ky][1] + t[ky][2]) + t[ky][3];
+    }
+  }
+  __syncthreads();
+  {
+    // per co: 16 ci x 9 taps = 144 contiguous floats (36 float4) at (co * 32 + 16 h) * 9
+    const float4* s4 = reinterpret_cast<const float4*>(st);
+    float4* d4 = reinterpret_cast<float4*>(sc.wslab + (size_t)b * kPack + 144 * h);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int i = tid + 256 * k, cq = i / 36, q = i - 36 * cq;
+      st4(d4 + cq * 72 + q, s4[i], f.wt & 4);
+    }
+  }
+  MX_TRACE_B(f, 3, 3, braw);
+  if (trc) {  // phase-time sums as "time after block start" in trace slots 4..6 (A, B, C)
+    const uint32_t t0 = f.trace[(3 * 1024 + braw) * 8];
+    f.trace[(3 * 1024 + braw) * 8 + 4] = t0 + tA;
+    f.trace[(3 * 1024 + braw) * 8 + 5] = t0 + tB;
+    f.trace[(3 * 1024 + braw) * 8 + 6] = t0 + tC;
+  }
+}
+
+// F6W with ONE V buffer and (B) as its own phase per chunk (45 KB, three blocks per CU): the
+// variant for launches that also hold co-scheduled exchange blocks, which need CU slots beside
+// the 512 conv blocks.
+__device__ __forceinline__ void f6w_body_serial(const MnistFused& f, const Scratch& sc, float* sm, int braw, int nblk) {
+  MX_TRACE_B(f, 3, 0, braw);
+  constexpr int kA1P = kF6WA1P;
+  float* a1s = sm + 784 + 160;  // [16 ci][kA1P]: 6 a1 rows x 26
+  float* vs = a1s + 16 * kA1P;  // [24 t][16 ci][20]
+  const int bid = xcd_remap(braw, nblk);
+  const int b = bid / 2, h = bid & 1;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  // a1 rows 4c .. 4c+5 of the block's 16 ci = 16 x 39 float4 (624 of the 768 slots)
+  // (three named registers, not an array: an array here was placed in scratch memory)
+  const float* a1b = f.a1 + ((size_t)b * 32 + 16 * h) * 676;
+  int a1src[3], a1dst[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int i = min(tid + 256 * k, 623), ci = i / 39, f4 = i - 39 * ci;
+    a1src[k] = ci * 676 + 4 * f4;
+    a1dst[k] = tid + 256 * k < 624 ? ci * kA1P + 4 * f4 : -1;
+  }
+  float4 pa0 = *reinterpret_cast<const float4*>(a1b + a1src[0]);
+  float4 pa1 = *reinterpret_cast<const float4*>(a1b + a1src[1]);
+  float4 pa2 = *reinterpret_cast<const float4*>(a1b + a1src[2]);
+  const int co = 16 * w + m;  // A row of this lane
+  const float* dpl = f.dp + (size_t)b * 9216 + co * 144 + 6 * g;
+  const uint16_t* qpl = reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(f.idx) + (size_t)b * 9216 + co * 144 + 6 * g);
+  float2 dn[3];
+  uint16_t qn[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    dn[k] = *reinterpret_cast<const float2*>(dpl + 2 * k);
+    qn[k] = qpl[k];
+  }
+  f32x4 acc[16];
+#pragma unroll
+  for (int x = 0; x < 16; ++x) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
+  MX_TRACE_B(f, 3, 1, braw);
+  uint32_t tA = 0, tB = 0, tC = 0, tq = 0;  // phase-time sums (trace only)
+  const bool trc = f.trace && threadIdx.x == 0 && braw < 1024;
+#pragma unroll 1
+  for (int c = 0; c < 6; ++c) {
+    if (trc) tq = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    // (A) published a1 rows -> LDS (the previous chunk's phase-B reads of a1s finished before the
+    // barrier ahead of its phase C); next chunk's rows in flight
+    *reinterpret_cast<float4*>(a1s + a1dst[0]) = pa0;
+    *reinterpret_cast<float4*>(a1s + a1dst[1]) = pa1;
+    if (a1dst[2] >= 0) *reinterpret_cast<float4*>(a1s + a1dst[2]) = pa2;
+    if (c + 1 < 6) {
+      const float* nb = a1b + 104 * (c + 1);
+      pa0 = *reinterpret_cast<const float4*>(nb + a1src[0]);
+      pa1 = *reinterpret_cast<const float4*>(nb + a1src[1]);
+      pa2 = *reinterpret_cast<const float4*>(nb + a1src[2]);
+    }
+    __syncthreads();
+    if (trc) {
+      const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime();
+      tA += t - tq;
+      tq = t;
+    }
+    // (B) V = B^T d B of 24 tiles x 16 ci; tile tl: a1 rows 2(tl/12).., cols 2(tl%12)..
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = tid + 256 * k;
+      if (i < 384) {
+        const int ci = i & 15, tl = i >> 4, tyl = tl / 12, tx = tl - 12 * tyl;
+        const float* ap = a1s + ci * kA1P + 2 * tyl * 26 + 2 * tx;
+        float d[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) d[r][cc] = ap[r * 26 + cc];
+        float e[4][4];
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+          e[0][cc] = d[0][cc] - d[2][cc];
+          e[1][cc] = d[1][cc] + d[2][cc];
+          e[2][cc] = d[2][cc] - d[1][cc];
+          e[3][cc] = d[1][cc] - d[3][cc];
+        }
+        float4* vp = reinterpret_cast<float4*>(vs + (tl * 16 + ci) * kF6WVP);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          vp[r] = make_float4(e[r][0] - e[r][2], e[r][1] + e[r][2], e[r][2] - e[r][1], e[r][1] - e[r][3]);
+      }
+    }
+    // this chunk's dp / q operands; prefetch the next chunk's
+    float dv[6];
+    uint32_t qv[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      dv[2 * k] = dn[k].x;
+      dv[2 * k + 1] = dn[k].y;
+      qv[2 * k] = qn[k] & 0xffu;
+      qv[2 * k + 1] = qn[k] >> 8;
+    }
+    if (c + 1 < 6) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        dn[k] = *reinterpret_cast<const float2*>(dpl + 24 * (c + 1) + 2 * k);
+        qn[k] = qpl[12 * (c + 1) + k];
+      }
+    }
+    __syncthreads();
+    if (trc) {
+      const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime();
+      tB += t - tq;
+      tq = t;
+    }
+    // (C) k-step s: tile t = 6g + s of the chunk.  The next k-step's B fragments are read from LDS
+    // before this step's MFMAs (kept there by the scheduling barrier): loaded at their use, each
+    // group of 8 MFMAs waited for an LDS round trip (lgkmcnt(0) in the ISA, ~30 % of phase C)
+    const float4* vp0 = reinterpret_cast<const float4*>(vs + ((6 * g) * 16 + m) * kF6WVP);
+    float4 bb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bb[i] = vp0[i];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      float4 bn[4];
+      if (s + 1 < 6) {
+        const float4* vp = reinterpret_cast<const float4*>(vs + ((6 * g + s + 1) * 16 + m) * kF6WVP);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bn[i] = vp[i];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const float v = dv[s];
+      const bool qy = (qv[s] >> 1) & 1, qx = qv[s] & 1;
+      const float vy[4] = {qy ? 0.f : v, v, qy ? -v : v, qy ? -v : 0.f};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float w0 = qx ? 0.f : vy[i], w2 = qx ? -vy[i] : vy[i], w3 = qx ? -vy[i] : 0.f;
+        acc[4 * i + 0] = mfma4(w0, bb[i].x, acc[4 * i + 0]);
+        acc[4 * i + 1] = mfma4(vy[i], bb[i].y, acc[4 * i + 1]);
+        acc[4 * i + 2] = mfma4(w2, bb[i].z, acc[4 * i + 2]);
+        acc[4 * i + 3] = mfma4(w3, bb[i].w, acc[4 * i + 3]);
+      }
+      if (s + 1 < 6) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bb[i] = bn[i];
+      }
+    }
+    if (trc) tC += (uint32_t)__builtin_amdgcn_s_memrealtime() - tq;  // issue time of (C)
+  }
+  f6w_epilogue(f, sc, sm, acc, b, h, braw, trc, tA, tB, tC);
+}
+
 __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc, float* sm, int braw, int nblk) {
   MX_TRACE_B(f, 3, 0, braw);
   constexpr int kA1P = kF6WA1P;
@@ -210,51 +410,7 @@ __device__ __forceinline__ void f6w_body(const MnistFused& f, const Scratch& sc,
     __syncthreads();  // chunk c + 1's V complete; every read of chunk c's V done
     if (trc) tC += (uint32_t)__builtin_amdgcn_s_memrealtime() - tq;  // (C) with the next (B)
   }
-  MX_TRACE_B(f, 3, 2, braw);
-  // dw = G^T dU G, G^T = [1 .5 .5 0; 0 .5 -.5 0; 0 .5 .5 1]; acc[4i + j'][j] = dU[i][j'] of
-  // (co = 16w + 4g + j, ci = 16h + m).  This block's [64 co][16 ci][9] result is staged in LDS
-  // (over the idle operand tiles) and written to the image's slab in canonical [co][ci][ky][kx]
-  // order with coalesced 16-byte stores -- no atomics (the atomic epilogue was ~3 us and delayed
-  // the F7W blocks' own atomics behind it); the finalize sums the B slabs in a fixed order.
-  float* st = sm;  // [64 co][16 ci][9]
-  __syncthreads();  // every wave's phase-C reads of the operand tiles are done
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int cj = 16 * w + 4 * g + j;
-    float t[3][4];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const float m0 = acc[jj][j], m1 = acc[4 + jj][j], m2 = acc[8 + jj][j], m3 = acc[12 + jj][j];
-      t[0][jj] = m0 + 0.5f * (m1 + m2);
-      t[1][jj] = 0.5f * (m1 - m2);
-      t[2][jj] = 0.5f * (m1 + m2) + m3;
-    }
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      float* sp = st + (cj * 16 + m) * 9 + 3 * ky;
-      sp[0] = t[ky][0] + 0.5f * (t[ky][1] + t[ky][2]);
-      sp[1] = 0.5f * (t[ky][1] - t[ky][2]);
-      sp[2] = 0.5f * (t[ky][1] + t[ky][2]) + t[ky][3];
-    }
-  }
-  __syncthreads();
-  {
-    // per co: 16 ci x 9 taps = 144 contiguous floats (36 float4) at (co * 32 + 16 h) * 9
-    const float4* s4 = reinterpret_cast<const float4*>(st);
-    float4* d4 = reinterpret_cast<float4*>(sc.wslab + (size_t)b * kPack + 144 * h);
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-      const int i = tid + 256 * k, cq = i / 36, q = i - 36 * cq;
-      st4(d4 + cq * 72 + q, s4[i], f.wt & 4);
-    }
-  }
-  MX_TRACE_B(f, 3, 3, braw);
-  if (trc) {  // phase-time sums as "time after block start" in trace slots 4..6 (A, B, C)
-    const uint32_t t0 = f.trace[(3 * 1024 + braw) * 8];
-    f.trace[(3 * 1024 + braw) * 8 + 4] = t0 + tA;
-    f.trace[(3 * 1024 + braw) * 8 + 5] = t0 + tB;
-    f.trace[(3 * 1024 + braw) * 8 + 6] = t0 + tC;
-  }
+  f6w_epilogue(f, sc, sm, acc, b, h, braw, trc, tA, tB, tC);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -496,7 +652,8 @@ __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc,
 // the peers' matching blocks while the remaining blocks do the conv backward, so the 4.7 MB
 // exchange overlaps it inside ONE launch (no side stream, no cross-queue fence).  co_blocks is
 // a multiple of 8, so the conv part keeps its XCD-aware block mapping.
-__global__ __launch_bounds__(256, 2) void f67_conv2_bwd_kernel(MnistFused f, Scratch sc) {
+template <bool kPipe>
+__global__ __launch_bounds__(256, kPipe ? 2 : 3) void f67_conv2_bwd_kernel(MnistFused f, Scratch sc) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   if ((int)blockIdx.x < f.co_blocks) {
     MX_TRACE_B(f, 5, 0, (int)blockIdx.x);  // trace: exchange blocks vs conv blocks of this launch
@@ -507,7 +664,8 @@ __global__ __launch_bounds__(256, 2) void f67_conv2_bwd_kernel(MnistFused f, Scr
   const int bid = (int)blockIdx.x - f.co_blocks;
   const int n6 = 2 * f.B;
   if (bid < n6)
-    f6w_body(f, sc, sm, bid, n6);
+    if constexpr (kPipe) f6w_body(f, sc, sm, bid, n6);
+    else f6w_body_serial(f, sc, sm, bid, n6);
   else
     f7w_body<2>(f, sc, sm, bid - n6, kF7WChunks * f.B);
 }
@@ -552,15 +710,22 @@ __global__ __launch_bounds__(256) void f8_finalize_kernel(MnistFused f, Scratch 
 using namespace mnist;
 
 void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_sgd) {
-  constexpr size_t lds = kF6WLds > kF7WLds ? kF6WLds : kF7WLds;
   static bool attr = false;
   if (!attr) {
-    MX_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f67_conv2_bwd_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    for (const void* fn : {reinterpret_cast<const void*>(f67_conv2_bwd_kernel<true>),
+                           reinterpret_cast<const void*>(f67_conv2_bwd_kernel<false>)})
+      MX_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
   const Scratch sc = carve(f.scratch, f.B);
-  MX_LAUNCH(f67_conv2_bwd_kernel, dim3(f.co_blocks + 2 * f.B + kF7WChunks * f.B), dim3(256), lds, st, f, sc);
+  const dim3 grid(f.co_blocks + 2 * f.B + kF7WChunks * f.B);
+  if (f.co_blocks == 0) {
+    constexpr size_t lds = kF6WLdsPipe > kF7WLds ? kF6WLdsPipe : kF7WLds;
+    MX_LAUNCH(f67_conv2_bwd_kernel<true>, grid, dim3(256), lds, st, f, sc);
+  } else {  // the exchange blocks need CU slots beside the conv blocks: three per CU
+    constexpr size_t lds = kF6WLdsSerial > kF7WLds ? kF6WLdsSerial : kF7WLds;
+    MX_LAUNCH(f67_conv2_bwd_kernel<false>, grid, dim3(256), lds, st, f, sc);
+  }
   if (!finalize_in_sgd) MX_LAUNCH(f8_finalize_kernel, dim3(kWslabGroups + 2 + 8), dim3(256), 0, st, f, sc);
   MX_HIP_CHECK(hipGetLastError());
 }

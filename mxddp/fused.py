@@ -22,6 +22,7 @@ by ``_opt_tensors()``.
 from __future__ import annotations
 
 import os
+import sys
 import time
 
 import torch
@@ -333,11 +334,16 @@ class FusedTrainerBase:
         self._use_transport("peer", comms)
         self._set_buckets(strat)
         d = self._run_from(snap0)
-        ok = not self.peer.error()
+        err = self.peer.error()
+        ok, why = not err, f"peer timeout (rank {err - 1} never arrived)" if err else ""
         if ok:
             ref = self._peer_ref
             rel = ((d - ref).norm() / ref.norm().clamp_min(1e-30)).item()
             ok = rel <= float(os.environ.get("MXDDP_VALIDATE_RTOL", "1e-3"))
+            why = "" if ok else f"disagrees with the reference steps (relative {rel:.3g})"
+        if not ok:  # the driver's logs say why a candidate was dropped
+            print(f"mxddp autotune: rank {pc.info().rank}: peer strategy {strat!r} rejected: {why}",
+                  file=sys.stderr, flush=True)
         ok = pc.all_reduce_max(0.0 if ok else 1.0) == 0.0
         if not ok:
             self._peer_resync()
