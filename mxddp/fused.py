@@ -362,7 +362,16 @@ class FusedTrainerBase:
         if self.world_size > 1 or "MXDDP_RCCL_VARIANTS" in os.environ:
             out = {}
             for v in pc.rccl_variants():
-                c = self.comm if v == "default" else pc.rccl_comm(force=True, variant=v)
+                c, why = None, ""
+                try:  # a variant RCCL refuses (config field, version) is dropped, not fatal
+                    c = self.comm if v == "default" else pc.rccl_comm(force=True, variant=v)
+                except Exception as e:  # noqa: BLE001 - any init failure
+                    why = str(e).splitlines()[0] if str(e) else type(e).__name__
+                # every rank must agree (a communicator some ranks lack cannot run collectives)
+                if pc.all_reduce_max(0.0 if c is not None or v == "default" else 1.0) > 0:
+                    if why:
+                        print(f"mxddp autotune: RCCL variant {v!r} dropped: {why}", file=sys.stderr, flush=True)
+                    continue
                 if c is not None:
                     out[v] = c
             if out:

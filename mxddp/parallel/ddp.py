@@ -23,6 +23,8 @@ events.  CPU: the same bucketing over gloo with async work handles.
 """
 from __future__ import annotations
 
+import sys
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -134,9 +136,16 @@ class DistributedDataParallel(nn.Module):
         # buckets; every rank gets the same verdict
         variants = {}
         for v in _comm.rccl_variants():
-            c = self._comm if v == "default" else _comm.rccl_comm(variant=v)
-            if c is not None:
-                variants[v] = c
+            c, why = None, ""
+            try:  # a variant RCCL refuses (config field, version) is dropped, not fatal
+                c = self._comm if v == "default" else _comm.rccl_comm(variant=v)
+            except Exception as e:  # noqa: BLE001 - any init failure
+                why = str(e).splitlines()[0] if str(e) else type(e).__name__
+            if _comm.all_reduce_max(0.0 if c is not None else 1.0) > 0:  # every rank must have it
+                if why:
+                    print(f"mxddp DDP: RCCL variant {v!r} dropped: {why}", file=sys.stderr, flush=True)
+                continue
+            variants[v] = c
         choice, self.transport_ms = _peer.pick_transport(pc, variants, [n for _, n in self.buckets])
         if choice == "peer":
             self.reducer.set_peer(pc)
