@@ -187,3 +187,26 @@ def test_no_working_candidate_raises(monkeypatch):
     tr.transport = "peer"  # peer-only job (ranks share a GPU): nothing else to fall back to
     with pytest.raises(RuntimeError, match="no launch strategy"):
         tr.autotune(trial_steps=2)
+
+
+def test_rccl_variant_that_fails_to_initialise_is_dropped(monkeypatch, capsys):
+    """An RCCL communicator variant the library refuses (ncclCommInitRankConfig error) is dropped
+    from the candidates on every rank (the verdict is agreed), with the reason logged -- not an
+    exception that kills the bench."""
+    from mxddp.parallel import comm as pc
+
+    _pc_stub(monkeypatch)
+    tr = _make()
+    tr.rccl_variants = None
+    good = types.SimpleNamespace(world_size=2, variant="Ring:c28")
+
+    def fake_rccl_comm(force=False, variant="default"):
+        if variant == "Ring:c7":
+            raise RuntimeError("ncclCommInitRankConfig: invalid argument")
+        return good
+
+    monkeypatch.setattr(pc, "rccl_variants", lambda: ["default", "Ring:c7", "Ring:c28"])
+    monkeypatch.setattr(pc, "rccl_comm", fake_rccl_comm)
+    cands = tr._rccl_candidates()
+    assert list(cands) == ["default", "Ring:c28"] and cands["Ring:c28"] is good
+    assert "RCCL variant 'Ring:c7' dropped" in capsys.readouterr().err
