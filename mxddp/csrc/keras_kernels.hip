@@ -520,15 +520,40 @@ __device__ void kb1_role_a(const KerasFused& f, SmemA& sm, int bid) {
   __syncthreads();
   const int lbase = (16 * w + g) * 64;
   f32x4 acc[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  // The (value, code) pairs of k-step s + 1 are read while k-step s's MFMAs run, both loads
+  // unconditional: written as `code == c ? dps[idx] : 0` the value load sat behind the code
+  // load's wait, and every MFMA behind two dependent LDS round trips (the ISA: ds_read_u8,
+  // lgkmcnt(0), ds_read_b32, lgkmcnt(0), v_mfma).
+  float dn[3];
+  int qn[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int idx = lbase + off[t][0];
+    dn[t] = sm.dps[idx];
+    qn[t] = sm.qs[idx];
+  }
 #pragma unroll
   for (int s = 0; s < 36; ++s) {
-    const int r = s >> 2, cofs = 4 * (s & 3) * 64;
+    const int r = s >> 2;
+    float dc[3];
+    int qc[3];
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
-      const int idx = lbase + cofs + off[t][r];
-      const float a = (int)sm.qs[idx] == code[t][r] ? sm.dps[idx] : 0.f;
-      acc[t] = mfma4(a, breg[s], acc[t]);
+      dc[t] = dn[t];
+      qc[t] = qn[t];
     }
+    if (s + 1 < 36) {
+      const int r1 = (s + 1) >> 2, cofs1 = 4 * ((s + 1) & 3) * 64;
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int idx = lbase + cofs1 + off[t][r1];
+        dn[t] = sm.dps[idx];
+        qn[t] = sm.qs[idx];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) acc[t] = mfma4(qc[t] == code[t][r] ? dc[t] : 0.f, breg[s], acc[t]);
   }
 #pragma unroll
   for (int t = 0; t < 3; ++t)
