@@ -164,12 +164,16 @@ __global__ __launch_bounds__(512) void kf1_kernel(KerasFused f) {
       base = (2 * wy + ((ml >> 1) & 1)) * 13 + 2 * wx + (ml & 1);
     }
     const float* ap = p1s + base + g * kP1;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // two accumulator chains (even / odd k-steps): one chain made each MFMA wait for the last
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < 72; ++s) {
       const int r = s >> 3;
-      acc = mfma4(ap[(4 * (s & 7)) * kP1 + (r / 3) * 13 + (r % 3)], breg[s], acc);
+      const float a = ap[(4 * (s & 7)) * kP1 + (r / 3) * 13 + (r % 3)];
+      if (s & 1) acc1 = mfma4(a, breg[s], acc1);
+      else acc0 = mfma4(a, breg[s], acc0);
     }
+    const f32x4 acc = acc0 + acc1;
     const int wo = 4 * mt + g;  // this lane's accumulators = the 4 outputs of window wo, channel co
     if (wo < 25) {
       int best = 0;
@@ -634,12 +638,16 @@ __device__ void kb1_role_b(const KerasFused& f, SmemB& sm, int bid) {
   for (int nt = w; nt < 18; nt += 4) {
     const int c = 16 * nt + (lane & 15), ci = c / 9, r = c - ci * 9;
     const float* bp = sm.p1s + ci * kP1 + (r / 3) * 13 + r % 3;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // two accumulator chains (even / odd k-steps): one chain made each MFMA wait for the last
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < 25; ++s) acc = mfma4(av[s], bp[poff[s]], acc);
+    for (int s = 0; s < 25; ++s) {
+      if (s & 1) acc1 = mfma4(av[s], bp[poff[s]], acc1);
+      else acc0 = mfma4(av[s], bp[poff[s]], acc0);
+    }
     float* plane = f.pl2 + (size_t)n * kPl2;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) plane[(16 * cq + 4 * g + j) * 288 + c] = acc[j];
+    for (int j = 0; j < 4; ++j) plane[(16 * cq + 4 * g + j) * 288 + c] = acc0[j] + acc1[j];
   }
 }
 
