@@ -114,6 +114,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_conv_set_glds", &nhwc_conv_set_glds);
   m.def("nhwc_conv_set_glds256", &nhwc_conv_set_glds256);
   m.def("nhwc_conv_set_glds_short", &nhwc_conv_set_glds_short);
+  m.def("nhwc_conv_set_glds_deep", &nhwc_conv_set_glds_deep);
   m.def("nhwc_bn_set_grid_cap", &nhwc_bn_set_grid_cap);
   m.def("nhwc_conv_set_split_blocks", &nhwc_conv_set_split_blocks);
   m.def("nhwc_wgrad_set_target", &nhwc_wgrad_set_target);

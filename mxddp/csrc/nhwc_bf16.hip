@@ -2701,6 +2701,17 @@ static int g_conv_glds256 = 1;
 // for layers of <= 2 k-tiles with >= 512 tiles: 0 = never, 1 = there (default)
 static int g_conv_glds_short = 1;
 void nhwc_conv_set_glds_short(int mode) { g_conv_glds_short = mode; }
+// deep reductions on too few 256-pixel tiles to fill the chip (e.g. the 7 x 7 stage at batch 256:
+// 4 x 49 tiles of 128 channels): 128 x 128 tiles of the two-stage variant, two blocks per CU,
+// the whole reduction per block -- instead of split-K or the generic kernel.  0 = never, 1 = there
+static int g_conv_glds_deep = 1;
+void nhwc_conv_set_glds_deep(int mode) { g_conv_glds_deep = mode; }
+static bool glds_deep_fits(const ConvNArgs& a, bool wide, bool par) {
+  if (!g_conv_glds_deep || conv_glds_mode() == 0 || !wide || par || (a.dgrad && (a.sh != 1 || a.sw != 1))) return false;
+  if (a.Kg % 64 != 0 || a.Kg < 256 || a.Ng < 128 || (a.dgrad && a.bx && a.bnpart)) return false;
+  const int64_t t256 = (int64_t)cdiv(a.Ng, 128) * cdiv(a.M, 256), t128 = (int64_t)cdiv(a.Ng, 128) * cdiv(a.M, 128);
+  return t256 < 256 && t128 >= 256;
+}
 // The BN apply kernels run U = 2 vectors per iteration, software-pipelined (4 vectors measured
 // ~1 % slower, the unpipelined loop equal: profiles/r4_ab2, r4_g).
 // blocks of the BN apply kernels (any multiple of 256 threads keeps each thread's channel vector
@@ -2785,6 +2796,18 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   ConvPlan p = cs.p;
   const bool wide = cs.wide;
   const GldsPlan gp = glds_plan(a, wide, cs.par);
+  if (glds_deep_fits(a, wide, cs.par)) {  // 128 x 128 tiles, two blocks per CU, no split-K
+    a.par = 0;
+    a.part = nullptr;
+    a.bx = nullptr;
+    a.kt_per_split = a.Kg / 64;
+    const int gx = cdiv(a.M, 128);
+    if (!(a.bnpart && !a.dgrad && gx <= 16384)) a.bnpart = nullptr;
+    const dim3 grid(cdiv(a.Ng, 128) * gx, 1);
+    if (a.bnpart) MX_LAUNCH((conv_nhwc_glds_kernel<128, true, 128, 2>), grid, dim3(512), 0, st, a);
+    else MX_LAUNCH((conv_nhwc_glds_kernel<128, false, 128, 2>), grid, dim3(512), 0, st, a);
+    return a.bnpart ? gx : 0;
+  }
   if (gp.tm && glds256_fits(a)) {  // 256 x 256 tiles, no split-K
     a.par = 0;
     a.part = nullptr;

@@ -2,7 +2,7 @@
 conv shape at batch 32 (forward, data gradient, weight gradient): microseconds and TFLOP/s per
 direction, so the conv-kernel work can be prioritised by where the step time goes.
 
-    python scripts/bench_nhwc_layers.py [batch] [iters] [tile256] [glds_short] [wgrad_tile256]
+    python scripts/bench_nhwc_layers.py [batch] [iters] [tile256] [glds_short] [wgrad_tile256] [glds_deep]
 """
 import os
 import sys
@@ -44,6 +44,8 @@ def main():
         Cn.nhwc_conv_set_glds_short(int(sys.argv[4]))
     if len(sys.argv) > 5:  # 256 x 256 weight-gradient tiles (default 1)
         Cn.nhwc_wgrad_set_tile256(int(sys.argv[5]))
+    if len(sys.argv) > 6:  # 128 x 128 LDS-DMA tiles for deep reductions on few tiles (default 1)
+        Cn.nhwc_conv_set_glds_deep(int(sys.argv[6]))
     st = torch.cuda.current_stream().cuda_stream
     tot = {"fwd": 0.0, "dgrad": 0.0, "dgrad_st": 0.0, "wgrad": 0.0}
     # floor: max(HBM bytes at 8 TB/s, FLOPs at the 2.5 PF bf16 dense peak), the same for all three

@@ -150,6 +150,41 @@ def test_conv_glds_kernel(cuda, case):
     assert _rel(wg.grad.cpu(), wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("case", [(16, 512, 28, 28, 512, 3, 1, 1),   # forward + data gradient, K = 4,608
+                                  (13, 512, 28, 28, 512, 1, 1, 0),   # partial last 128-pixel tile
+                                  (16, 256, 28, 28, 512, 1, 1, 0)])  # forward only (dgrad: 196 blocks)
+def test_conv_glds_deep_tiles(cuda, case):
+    """Deep reductions on too few 256-pixel tiles run 128 x 128 tiles of the two-stage LDS-DMA
+    kernel (glds_deep_fits): same result as the former route and the fp32 reference."""
+    from mxddp import native
+
+    Cn = native()
+    N, C, H, W, K, R, st, pd = case
+    torch.manual_seed(5)
+    x = torch.randn(N, H, W, C).to(torch.bfloat16)
+    w = torch.randn(K, C, R, R) * (2.0 / (C * R * R)) ** 0.5
+    xr = _nchw(x).requires_grad_()
+    wr = w.to(torch.bfloat16).float().requires_grad_()
+    yr = F.conv2d(xr, wr, None, st, pd)
+    gy = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(gy)
+    gyn = gy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(cuda)
+    outs = []
+    try:
+        for deep in (1, 0):
+            Cn.nhwc_conv_set_glds_deep(deep)
+            xg = x.to(cuda).requires_grad_()
+            y = nhwc.conv2d(xg, w.to(cuda), st, pd)
+            y.backward(gyn)
+            torch.cuda.synchronize()
+            outs.append((_nchw(y), _nchw(xg.grad)))
+    finally:
+        Cn.nhwc_conv_set_glds_deep(1)
+    assert _rel(outs[0][0], yr.detach()) < 1e-2
+    assert _rel(outs[0][1], xr.grad) < 1e-2
+    assert _rel(outs[0][0], outs[1][0]) < 1e-2 and _rel(outs[0][1], outs[1][1]) < 1e-2
+
+
 @pytest.mark.parametrize("case", [(2, 64, 14, 14, 256, 1, 1, 0), (1, 256, 9, 9, 256, 3, 1, 1),
                                   (2, 512, 7, 7, 256, 1, 1, 0), (3, 64, 20, 20, 512, 1, 2, 0),
                                   (2, 256, 16, 16, 256, 3, 1, 1)])
@@ -286,7 +321,8 @@ def test_bn_nhwc(cuda, C, relu, res):
                                           ((96, 64, 56, 56, 64, 1, 0), 1.0),  # two-stage 128-pixel variant
                                           ((23, 64, 57, 55, 256, 1, 0), -1.5),  # ... partial last tile
                                           ((5, 64, 48, 32, 64, 3, 1), 2.0),  # the 3x3 / 64-channel band kernel
-                                          ((2, 64, 56, 56, 64, 3, 1), 0.5)])  # (4-row bands: more rows than 256-px tiles)
+                                          ((2, 64, 56, 56, 64, 3, 1), 0.5),  # (4-row bands: more rows than 256-px tiles)
+                                          ((13, 512, 28, 28, 512, 1, 0), 1.0)])  # 128 x 128 deep-reduction tiles
 def test_bn_statistics_from_conv_epilogue(cuda, shape, offset):
     _bn_stats_from_conv_epilogue(cuda, shape, offset)
 
