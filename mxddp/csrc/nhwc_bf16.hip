@@ -2701,16 +2701,25 @@ static int g_conv_glds256 = 1;
 // for layers of <= 2 k-tiles with >= 512 tiles: 0 = never, 1 = there (default)
 static int g_conv_glds_short = 1;
 void nhwc_conv_set_glds_short(int mode) { g_conv_glds_short = mode; }
-// deep reductions on too few 256-pixel tiles to fill the chip (e.g. the 7 x 7 stage at batch 256:
-// 4 x 49 tiles of 128 channels): 128 x 128 tiles of the two-stage variant, two blocks per CU,
-// the whole reduction per block -- instead of split-K or the generic kernel.  0 = never, 1 = there
+// 128 x 128 tiles of the two-stage LDS-DMA variant (two blocks per CU, the whole reduction per
+// block) for reductions of >= 4 k-tiles.  Measured per layer (profiles/r5_deep/): on the layers
+// whose 256-pixel tiles under-fill the chip (the 7 x 7 stage at batch 256: 4 x 49 tiles) they
+// replace split-K / the generic kernel (3x3 512 -> 512 150 -> 66 us); with >= ~200 such tiles they
+// also beat the three-stage 256-pixel and the 256 x 256 tiles on most layers (28 x 28 3x3 97 -> 72
+// us, 14 x 14 1024 -> 256 data gradient 58 -> 43 us), and lose below ~100 tiles (batch 32's
+// 7 x 7 stage: 24 -> 47 us at 52 tiles).  0 = never, 1 = >= 192 tiles (default), 2 = every
+// eligible layer, 3 = only where the 256-pixel tiles would under-fill the chip (the first rule)
 static int g_conv_glds_deep = 1;
 void nhwc_conv_set_glds_deep(int mode) { g_conv_glds_deep = mode; }
 static bool glds_deep_fits(const ConvNArgs& a, bool wide, bool par) {
   if (!g_conv_glds_deep || conv_glds_mode() == 0 || !wide || par || (a.dgrad && (a.sh != 1 || a.sw != 1))) return false;
   if (a.Kg % 64 != 0 || a.Kg < 256 || a.Ng < 128 || (a.dgrad && a.bx && a.bnpart)) return false;
   const int64_t t256 = (int64_t)cdiv(a.Ng, 128) * cdiv(a.M, 256), t128 = (int64_t)cdiv(a.Ng, 128) * cdiv(a.M, 128);
-  return t256 < 256 && t128 >= 256;
+  switch (g_conv_glds_deep) {
+    case 2: return true;
+    case 3: return t256 < 256 && t128 >= 256;
+    default: return t128 >= 192;
+  }
 }
 // The BN apply kernels run U = 2 vectors per iteration, software-pipelined (4 vectors measured
 // ~1 % slower, the unpipelined loop equal: profiles/r4_ab2, r4_g).
