@@ -556,7 +556,12 @@ __global__ __launch_bounds__(512, TN == 128 ? 2 : 1) void conv_nhwc_glds_kernel(
   constexpr int AB = TM * 128, SB = AB + TN * 128;        // bytes: A image, whole stage
   constexpr int NA = TM / 64, NB = TN / 64, NPW = NA + NB;  // LDS-DMA instructions per wave per stage
   constexpr int WM = TM / 64, WN = 8 / WM, WPX = TN / WN, WMT = 4, WNT = WPX / 16;
-  __shared__ __attribute__((aligned(1024))) char smem[NS * SB];
+  // after the k loop the stage buffers hold the bf16 C tile ([TN][TM + 8]) and, for the backward
+  // BN statistics, 16 reduction floats per thread; the two-stage variant's 64 KB of stages are
+  // topped up to fit them (67.6 KB at TM = 128: still two blocks per CU)
+  constexpr int kCB = ((TN * (TM + 8) * 2 + 255) & ~255), kBstB = kCB + 16 * 512 * 4;
+  constexpr int kSmem = (TN == 128 && kBstB > NS * SB) ? kBstB : NS * SB;
+  __shared__ __attribute__((aligned(1024))) char smem[kSmem];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave / WN, wn = wave % WN;
   const int tiles_m = (a.Ng + TM - 1) / TM;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -668,7 +673,7 @@ __global__ __launch_bounds__(512, TN == 128 ? 2 : 1) void conv_nhwc_glds_kernel(
   __syncthreads();  // every wave done with the stage buffers (no LDS-DMA outstanding)
   // bf16 output staged through LDS ([TN pixels][TM channels], pitch TM + 8) -> 16-byte stores
   constexpr int CP = TM + 8;
-  static_assert(TN * CP * 2 <= NS * SB, "C tile must fit in the stage buffers");
+  static_assert(TN * CP * 2 <= kSmem, "C tile must fit in the stage buffers");
   bf16* Cs = reinterpret_cast<bf16*>(smem);
 #pragma unroll
   for (int i = 0; i < WMT; ++i) {
@@ -684,7 +689,7 @@ __global__ __launch_bounds__(512, TN == 128 ? 2 : 1) void conv_nhwc_glds_kernel(
   constexpr int VPR = TM / 8;
   // backward BN statistics (fixed vector per thread): only where the reduction slots fit after
   // the C tile (not the two-stage variant; the host does not select it for them)
-  constexpr bool kBst = ((TN * CP * 2 + 255) & ~255) + 16 * 512 * 4 <= NS * SB;
+  constexpr bool kBst = kBstB <= kSmem;
   const bool bst = kBst && !STATS && a.bx != nullptr;
   float s1[8], s2[8], mean8[8], sc8[8], sh8[8];
   if (bst) {
@@ -711,7 +716,7 @@ __global__ __launch_bounds__(512, TN == 128 ? 2 : 1) void conv_nhwc_glds_kernel(
     static_assert(RPT % U == 0, "rows per thread");
     // reduction slots after the C tile in the (idle) stage buffers
     float* bred = reinterpret_cast<float*>(smem + ((TN * CP * 2 + 255) & ~255));
-    static_assert(((TN * CP * 2 + 255) & ~255) + 2 * 512 * 4 <= NS * SB, "BN reduction slots must fit");
+    static_assert(((TN * CP * 2 + 255) & ~255) + 2 * 512 * 4 <= kSmem, "BN reduction slots must fit");
     const int c = tid % TM, q = tid / TM, ch = ch0 + c;
     const float K = (a.bnshift && ch < a.Ng) ? a.bnshift[ch] : 0.f;
     const int rows = min(TN, a.M - px0);
@@ -2713,7 +2718,7 @@ static int g_conv_glds_deep = 1;
 void nhwc_conv_set_glds_deep(int mode) { g_conv_glds_deep = mode; }
 static bool glds_deep_fits(const ConvNArgs& a, bool wide, bool par) {
   if (!g_conv_glds_deep || conv_glds_mode() == 0 || !wide || par || (a.dgrad && (a.sh != 1 || a.sw != 1))) return false;
-  if (a.Kg % 64 != 0 || a.Kg < 256 || a.Ng < 128 || (a.dgrad && a.bx && a.bnpart)) return false;
+  if (a.Kg % 64 != 0 || a.Kg < 256 || a.Ng < 128) return false;
   const int64_t t256 = (int64_t)cdiv(a.Ng, 128) * cdiv(a.M, 256), t128 = (int64_t)cdiv(a.Ng, 128) * cdiv(a.M, 128);
   switch (g_conv_glds_deep) {
     case 2: return true;
@@ -2808,12 +2813,13 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   if (glds_deep_fits(a, wide, cs.par)) {  // 128 x 128 tiles, two blocks per CU, no split-K
     a.par = 0;
     a.part = nullptr;
-    a.bx = nullptr;
     a.kt_per_split = a.Kg / 64;
     const int gx = cdiv(a.M, 128);
-    if (!(a.bnpart && !a.dgrad && gx <= 16384)) a.bnpart = nullptr;
+    const bool bst = a.dgrad && a.bx && a.bnpart && gx <= 16384;  // backward BN statistics epilogue
+    if (!bst) a.bx = nullptr;
+    if (!(a.bnpart && (bst || !a.dgrad) && gx <= 16384)) a.bnpart = nullptr;
     const dim3 grid(cdiv(a.Ng, 128) * gx, 1);
-    if (a.bnpart) MX_LAUNCH((conv_nhwc_glds_kernel<128, true, 128, 2>), grid, dim3(512), 0, st, a);
+    if (a.bnpart && !bst) MX_LAUNCH((conv_nhwc_glds_kernel<128, true, 128, 2>), grid, dim3(512), 0, st, a);
     else MX_LAUNCH((conv_nhwc_glds_kernel<128, false, 128, 2>), grid, dim3(512), 0, st, a);
     return a.bnpart ? gx : 0;
   }
@@ -2834,8 +2840,8 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     a.kt_per_split = gp.kt_per_split;
     a.part = gp.splits > 1 ? scratch : nullptr;
     // short reductions (<= 2 k-tiles) with enough tiles for two blocks per CU: 128-pixel tiles,
-    // two stages (no backward statistics epilogue there)
-    const bool shrt = g_conv_glds_short && gp.splits == 1 && a.Kg <= 128 && !(a.dgrad && a.bx && a.bnpart) &&
+    // two stages
+    const bool shrt = g_conv_glds_short && gp.splits == 1 && a.Kg <= 128 &&
                       (int64_t)cdiv(a.Ng, gp.tm) * cdiv(a.M, 128) >= 512;
     const int tn = shrt ? 128 : 256, gx = cdiv(a.M, tn);
     // epilogue BN statistics (forward: bnpart / bnshift; data gradient: bx, see ConvNArgs) need
@@ -2846,7 +2852,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     if (!(a.bnpart && (bst || (!a.dgrad && gp.splits == 1)) && gx <= 16384)) a.bnpart = nullptr;
     const dim3 grid(cdiv(a.Ng, gp.tm) * gx, gp.splits);
     if (shrt) {
-      if (a.bnpart) {
+      if (a.bnpart && !bst) {
         if (gp.tm == 128) MX_LAUNCH((conv_nhwc_glds_kernel<128, true, 128, 2>), grid, dim3(512), 0, st, a);
         else MX_LAUNCH((conv_nhwc_glds_kernel<64, true, 128, 2>), grid, dim3(512), 0, st, a);
       } else {

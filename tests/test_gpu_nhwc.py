@@ -390,7 +390,8 @@ def _bn_stats_from_conv_epilogue(cuda, shape, offset):
 
 
 @pytest.mark.parametrize("glds,stride,relu", [(2, 1, True), (2, 1, False), (0, 1, True), (0, 2, True),
-                                              (0, 1, False), (256, 1, True), (256, 1, False)])
+                                              (0, 1, False), (256, 1, True), (256, 1, False),
+                                              ("deep", 1, True), ("short", 1, True), ("short", 1, False)])
 def test_bn_backward_statistics_from_dgrad_epilogue(cuda, glds, stride, relu):
     """BN -> conv: the conv's data-gradient epilogue computes the BN's backward partial sums
     (sum g, sum g (x - mean), g masked by the BN's fused ReLU) and the BN backward skips its
@@ -402,14 +403,16 @@ def test_bn_backward_statistics_from_dgrad_epilogue(cuda, glds, stride, relu):
     # K = 64: a 576-deep data-gradient reduction, no split-K (a split dgrad cannot carry the
     # statistics); Cin = 128: not the 3x3 / 64 -> 64 band kernel (whose epilogue carries no
     # statistics: with Cin = 64 every stride-1 case ran the band kernel and took the separate pass);
-    # glds 256: the 256-channel data-gradient tile
-    N, Cin, H, W, K = (4, 128, 16, 16, 64) if glds != 256 else (2, 256, 10, 10, 64)
+    # glds 256: the 256-channel data-gradient tile; "deep" / "short": the two-stage 128 x 128 tiles
+    # (>= 192 of them, a 576-deep reduction; a 1x1 with >= 512 tiles and a 128-deep reduction)
+    N, Cin, H, W, K, R = {256: (2, 256, 10, 10, 64, 3), "deep": (8, 128, 56, 56, 64, 3),
+                          "short": (8, 128, 96, 96, 128, 1)}.get(glds, (4, 128, 16, 16, 64, 3))
     torch.manual_seed(11)
     x = (torch.randn(N, H, W, Cin) + 0.5).to(torch.bfloat16).to(cuda)
-    w = (torch.randn(K, Cin, 3, 3) * 0.05).to(cuda)
+    w = (torch.randn(K, Cin, R, R) * 0.05).to(cuda)
     outs, used = [], []
     try:
-        C.nhwc_conv_set_glds(2 if glds == 256 else glds)
+        C.nhwc_conv_set_glds(2 if glds == 256 else (1 if isinstance(glds, str) else glds))
         C.nhwc_conv_set_glds256(2 if glds == 256 else 0)
         gamma, beta = torch.rand(Cin) + 0.5, torch.randn(Cin) * 0.2  # the same BN in both runs
         for fused in (False, True):
@@ -423,7 +426,7 @@ def test_bn_backward_statistics_from_dgrad_epilogue(cuda, glds, stride, relu):
             wg = w.clone().requires_grad_()
             before = dict(nhwc.BN_BWD_STATS)
             y = nhwc.batch_norm(xg, bn, relu=relu)
-            c = nhwc.conv2d(y, wg, stride, 1)
+            c = nhwc.conv2d(y, wg, stride, R // 2)
             gy = torch.randn(c.shape, generator=torch.Generator().manual_seed(4)).to(torch.bfloat16).to(cuda)
             c.backward(gy)
             torch.cuda.synchronize()
