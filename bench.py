@@ -45,6 +45,7 @@ AB_SWITCHES = {
     "bn_grid_cap": ("nhwc_bn_set_grid_cap", "bf16 NHWC BN apply kernels, most blocks"),
     "split_blocks": ("nhwc_conv_set_split_blocks", "bf16 NHWC generic conv, split-K only below this many blocks"),
     "wgrad_target": ("nhwc_wgrad_set_target", "bf16 NHWC weight gradient, blocks aimed at when splitting pixels"),
+    "wgrad_w8": ("nhwc_wgrad_set_waves8", "bf16 NHWC weight gradient, 128-row tiles over 8 waves (1) or 4 (0)"),
     "wgrad_tile256": ("nhwc_wgrad_set_tile256", "bf16 NHWC weight gradient, 256 x 256 tiles (1) or 128 x 128 (0)"),
     "wt_stores": ("mnist_set_wt_stores", "fused MNIST, L2 write-through bulk stores mask (1 F5, 2 F2, 4 F6W)"),
 }

@@ -115,6 +115,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_conv_set_glds256", &nhwc_conv_set_glds256);
   m.def("nhwc_conv_set_glds_short", &nhwc_conv_set_glds_short);
   m.def("nhwc_conv_set_glds_deep", &nhwc_conv_set_glds_deep);
+  m.def("nhwc_wgrad_set_waves8", &nhwc_wgrad_set_waves8);
   m.def("nhwc_bn_set_grid_cap", &nhwc_bn_set_grid_cap);
   m.def("nhwc_conv_set_split_blocks", &nhwc_conv_set_split_blocks);
   m.def("nhwc_wgrad_set_target", &nhwc_wgrad_set_target);
@@ -138,16 +139,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_conv_dgrad", [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int N, int H, int W, int C, int K, int R,
                               int S_, int sh, int sw, int ph, int pw, int P_, int Q, uintptr_t scratch,
                               uintptr_t st, uintptr_t addend, uintptr_t bnpart, uintptr_t bx, uintptr_t bmean,
-                              uintptr_t bfcoef, uintptr_t bmask, bool brelu, uintptr_t amask) {
+                              uintptr_t bfcoef, uintptr_t bmask, bool brelu, uintptr_t amask, bool addend_sub) {
     return nhwc_conv_dgrad(P<const uint16_t>(dy), P<const uint16_t>(wt), P<uint16_t>(dx), N, H, W, C, K, R, S_, sh, sw,
                            ph, pw, P_, Q, P<float>(scratch), S(st), P<const uint16_t>(addend), P<float>(bnpart),
                            P<const uint16_t>(bx), P<const float>(bmean), P<const float>(bfcoef),
-                           P<const uint8_t>(bmask), brelu, P<const uint8_t>(amask));
+                           P<const uint8_t>(bmask), brelu, P<const uint8_t>(amask), addend_sub);
   }, py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("K"),
      py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("P"), py::arg("Q"),
      py::arg("scratch"), py::arg("st"), py::arg("addend") = 0, py::arg("bnpart") = 0, py::arg("bx") = 0,
      py::arg("bmean") = 0, py::arg("bfcoef") = 0, py::arg("bmask") = 0, py::arg("brelu") = false,
-     py::arg("amask") = 0);
+     py::arg("amask") = 0, py::arg("addend_sub") = false);
   m.def("nhwc_conv_dgrad_bn_rows", &nhwc_conv_dgrad_bn_rows);
   m.def("nhwc_conv_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, int N, int H, int W, int Cin, int Cp, int K,
                               int R, int S_, int sh, int sw, int ph, int pw, int P_, int Q, bool acc, uintptr_t scratch,

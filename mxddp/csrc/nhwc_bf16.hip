@@ -117,6 +117,8 @@ struct ConvNArgs {
   const uint8_t* amask;  // addend masked by these ReLU bits (bit e of byte o / 8), or null: the
                          // identity shortcut's gradient taken straight from the block's output
                          // gradient, never materialised by the last BN's backward
+  int asub;  // the addend is [N][OH / 2][OW / 2][Ng] and joins at even (h, w) only: a stride-2 1x1
+             // projection shortcut's input gradient, computed compact (zero at the odd positions)
   // forward feeding a training BatchNorm (LDS-DMA kernel, no split): the epilogue writes the BN's
   // per-channel partial sums of (y - shift[c]) and its square over each 256-pixel tile to
   // bnpart[tile][2 Ng] (the layout bn_nhwc_partial_k writes), so the BN skips its statistics pass
@@ -198,12 +200,23 @@ __device__ __forceinline__ void epi_vectors(const ConvNArgs& a, const bf16* Cs, 
   uint4 xr[NV];
   u32x4 ad[NV];
   uint32_t mb[NV], am[NV];
+  size_t oa[NV];  // addend offsets (asub: half resolution)
+  bool aok[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int v = tid + NT * k, row = v / VPR, cv = v - row * VPR;
     const int px = px0 + row, ch = ch0 + 8 * cv;
     ok[k] = px < Mlim && ch < a.Ng;
-    o[k] = ok[k] ? (size_t)pfull(px) * a.Ng + ch : 0;
+    const int pf = ok[k] ? pfull(px) : 0;
+    o[k] = ok[k] ? (size_t)pf * a.Ng + ch : 0;
+    oa[k] = o[k];
+    aok[k] = true;
+    if (a.asub) {  // full-resolution pixel (n, h, w) -> (n, h / 2, w / 2) when h and w are even
+      const int n = (int)a.fOHW.div((uint32_t)pf), rem = pf - n * a.OH * a.OW;
+      const int h = (int)a.fOW.div((uint32_t)rem), w = rem - h * a.OW;
+      aok[k] = ok[k] && !((h | w) & 1);
+      oa[k] = aok[k] ? ((size_t)(n * (a.OH >> 1) + (h >> 1)) * (a.OW >> 1) + (w >> 1)) * a.Ng + ch : 0;
+    }
     xr[k] = make_uint4(0u, 0u, 0u, 0u);
     ad[k] = u32x4{0u, 0u, 0u, 0u};
     mb[k] = 0u;
@@ -219,7 +232,7 @@ __device__ __forceinline__ void epi_vectors(const ConvNArgs& a, const bf16* Cs, 
   }
   if (a.addend) {
 #pragma unroll
-    for (int k = 0; k < NV; ++k) ad[k] = *reinterpret_cast<const u32x4*>(a.addend + o[k]);
+    for (int k = 0; k < NV; ++k) ad[k] = *reinterpret_cast<const u32x4*>(a.addend + oa[k]);
     if (a.amask) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) am[k] = a.amask[o[k] >> 3];
@@ -230,7 +243,7 @@ __device__ __forceinline__ void epi_vectors(const ConvNArgs& a, const bf16* Cs, 
     if (!ok[k]) continue;
     const int v = tid + NT * k, row = v / VPR, cv = v - row * VPR;
     u32x4 val = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
-    if (a.addend) val = add8(val, a.amask ? mask8(ad[k], am[k]) : ad[k]);
+    if (a.addend && aok[k]) val = add8(val, a.amask ? mask8(ad[k], am[k]) : ad[k]);
     *reinterpret_cast<u32x4*>(a.out + o[k]) = val;
     if (bst) bn_bwd_acc8(a, val, xr[k], mb[k], mean8, sc8, sh8, s1, s2);
   }
@@ -2981,10 +2994,17 @@ size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, 
 int nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
                     int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st,
                     const uint16_t* addend, float* bnpart, const uint16_t* bx, const float* bmean,
-                    const float* bfcoef, const uint8_t* bmask, bool brelu, const uint8_t* amask) {
+                    const float* bfcoef, const uint8_t* bmask, bool brelu, const uint8_t* amask, bool addend_sub) {
   ConvNArgs a = dgrad_args(dy, wt_d, dx, N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q);
   a.addend = addend;
   a.amask = addend ? amask : nullptr;
+  if (addend && addend_sub) {
+    // the implicit-GEMM kernels' shared epilogue (epi_vectors) maps it; the 3x3 band and stem
+    // kernels are never chosen for a 1x1 layer
+    MX_CHECK(R == 1 && S == 1 && sh == 1 && sw == 1 && H % 2 == 0 && W % 2 == 0 && !amask,
+             "nhwc dgrad: a half-resolution addend needs a 1x1 stride-1 layer of even size, no mask");
+    a.asub = 1;
+  }
   if (bnpart && bx && bmean) {
     MX_CHECK(!brelu || bfcoef || bmask, "nhwc dgrad BN statistics: a ReLU needs the forward's coefficients or mask");
     a.bnpart = bnpart;
@@ -3025,6 +3045,10 @@ static void wgrad_tile(int K, int Ng, int Npix, int RS, int& tm, int& tn) {
 // weight-gradient blocks aimed at (A/B: nhwc_wgrad_set_target; 256 and 1,024 measured no better,
 // profiles/r4_y/); half that for the one-block-per-CU 256 x 256 tile
 static int g_wgrad_target = 512;
+// 128 x 128 (and 128 x 64) weight-gradient tiles over 8 waves (wave tile 64 x 32) instead of 4
+// (A/B: nhwc_wgrad_set_waves8)
+static int g_wgrad_w8 = 0;
+void nhwc_wgrad_set_waves8(int on) { g_wgrad_w8 = on; }
 void nhwc_wgrad_set_target(int n) { g_wgrad_target = n; }
 static int wgrad_splits(int Npix, int K, int Ng, int RS) {
   int tm, tn;
@@ -3100,7 +3124,9 @@ void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, in
   a.chunk = cdiv(cdiv(a.Npix, splits), 64) * 64;
   const dim3 grid(tiles * splits);
   if (tm == 256) MX_LAUNCH((wgrad_nhwc_kernel<256, 256, 2, 4>), grid, dim3(512), 0, st, a);
+  else if (tm == 128 && tn == 128 && g_wgrad_w8) MX_LAUNCH((wgrad_nhwc_kernel<128, 128, 2, 4>), grid, dim3(512), 0, st, a);
   else if (tm == 128 && tn == 128) MX_LAUNCH((wgrad_nhwc_kernel<128, 128>), grid, dim3(256), 0, st, a);
+  else if (tm == 128 && g_wgrad_w8) MX_LAUNCH((wgrad_nhwc_kernel<128, 64, 2, 4>), grid, dim3(512), 0, st, a);
   else if (tm == 128) MX_LAUNCH((wgrad_nhwc_kernel<128, 64>), grid, dim3(256), 0, st, a);
   else if (tn == 128) MX_LAUNCH((wgrad_nhwc_kernel<64, 128>), grid, dim3(256), 0, st, a);
   else MX_LAUNCH((wgrad_nhwc_kernel<64, 64>), grid, dim3(256), 0, st, a);

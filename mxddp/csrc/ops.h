@@ -195,6 +195,7 @@ int nhwc_conv_fwd(const uint16_t* x, const uint16_t* wt, uint16_t* y, int N, int
 void nhwc_conv_set_glds(int mode);
 // the 256 x 256-tile LDS-DMA kernel: 0 = off, 1 = layers with >= 256 tiles and >= 4 k-tiles (default), 2 = wherever Ng % 256 == 0
 void nhwc_conv_set_glds256(int mode);
+void nhwc_wgrad_set_waves8(int on);  // 8-wave 128-row weight-gradient tiles (A/B)
 void nhwc_conv_set_glds_deep(int mode);  // 128 x 128 LDS-DMA tiles for deep reductions on few tiles
 void nhwc_conv_set_glds_short(int mode);  // two-stage 128-pixel LDS-DMA variant for short reductions
 void nhwc_conv_set_split_blocks(int n);  // generic conv kernel: split-K below this many blocks (256)
@@ -210,11 +211,12 @@ size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, 
 // backward partial sums to bnpart (at most nhwc_conv_dgrad_bn_rows rows of 2 C floats).  Returns
 // the rows written (0: the kernel chosen for this shape cannot, the BN runs its own pass).
 // amask: the addend is masked by these ReLU bits (bit e of byte i / 8 for element i) before the add.
+// addend_sub: the addend is [N][H / 2][W / 2][C] and is added at even (h, w) only (1x1 layers).
 int nhwc_conv_dgrad(const uint16_t* dy, const uint16_t* wt_d, uint16_t* dx, int N, int H, int W, int C, int K, int R,
                     int S, int sh, int sw, int ph, int pw, int P, int Q, float* scratch, hipStream_t st,
                     const uint16_t* addend = nullptr, float* bnpart = nullptr, const uint16_t* bx = nullptr,
                     const float* bmean = nullptr, const float* bfcoef = nullptr, const uint8_t* bmask = nullptr,
-                    bool brelu = false, const uint8_t* amask = nullptr);
+                    bool brelu = false, const uint8_t* amask = nullptr, bool addend_sub = false);
 int nhwc_conv_dgrad_bn_rows(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw, int P,
                             int Q);
 // dw fp32 [K][Cin][R][S] (+)= ...; x has Cp >= Cin channels (padding ignored);

@@ -129,11 +129,15 @@ class GradJoin:
     (``nhwc_conv_dgrad(..., addend)``).  ``fork`` then passes that sum through unchanged.  If the
     first convolution's backward runs before the shortcut's, nothing is joined and ``fork`` adds.
     An identity shortcut's gradient is never materialised: the last BN leaves its own output
-    gradient and ReLU mask bits (``amask``), and the conv's epilogue masks while it adds."""
+    gradient and ReLU mask bits (``amask``), and the conv's epilogue masks while it adds.  A
+    stride-2 1x1 projection leaves its input gradient at half resolution (``sub2``: nonzero only
+    at even (h, w), computed as a stride-1 GEMM on the output grid) and the 1x1 first conv's
+    epilogue adds it there."""
 
     def __init__(self):
         self.dres = None
         self.amask = None
+        self.sub2 = False
         self.consumed = False
 
 
@@ -147,6 +151,7 @@ class _Fork(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, join):
         ctx.join = join
+        ctx.shape = x.shape
         ctx.set_materialize_grads(False)  # a lazy identity join leaves g_short undefined
         return x.view_as(x), x.view_as(x)
 
@@ -155,6 +160,9 @@ class _Fork(torch.autograd.Function):
         j = ctx.join
         if j.consumed:  # g_main already includes g_short (added by the conv's epilogue)
             out = g_main
+        elif g_short is None and j.dres is not None and j.sub2:  # half-resolution projection, not joined
+            out = g_main.clone() if g_main is not None else j.dres.new_zeros(ctx.shape)
+            out[:, ::2, ::2, :] += j.dres
         else:
             if g_short is None and j.dres is not None:  # lazy identity gradient, never joined
                 g_short = _mask_bits(j.dres, j.amask) if j.amask is not None else j.dres
@@ -162,7 +170,7 @@ class _Fork(torch.autograd.Function):
                 out = g_main if g_short is None else g_short
             else:
                 out = g_main + g_short
-        j.dres, j.amask, j.consumed = None, None, False
+        j.dres, j.amask, j.sub2, j.consumed = None, None, False, False
         return out, None
 
 
@@ -226,35 +234,54 @@ class _Conv(torch.autograd.Function):
             if wtd is None:
                 wtd = torch.empty((C * R * S * K,), device=dy.device, dtype=BF16)
                 Cn.nhwc_repack_weight(w.data_ptr(), 0, wtd.data_ptr(), K, C, R, S, Cp, st)
-            dx = torch.empty((N, H, W, C), device=dy.device, dtype=BF16)
-            n = Cn.nhwc_conv_dgrad_scratch_floats(N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q)
-            scr = torch.empty((n,), device=dy.device, dtype=torch.float32) if n else None
-            j = ctx.join
-            add = j.dres if j is not None and j.dres is not None and j.dres.shape == dx.shape else None
-            amask = j.amask if add is not None else None
-            link = ctx.bnlink
-            if link is not None and link.join is not None and add is None:
-                link = None  # the shortcut's gradient is not in this sum: not the BN's whole dy
-            bpart = None
-            if link is not None and link.x.shape == dx.shape:
-                rows = Cn.nhwc_conv_dgrad_bn_rows(N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q)
-                bpart = torch.empty((rows * 2 * C,), device=dy.device, dtype=torch.float32)
-            rows = Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx.data_ptr(), N, H, W, C, K, R, S, sh, sw, ph, pw,
-                                      P, Q, _p(scr), st, _p(add), _p(bpart),
-                                      _p(link.x) if bpart is not None else 0,
-                                      _p(link.mean) if bpart is not None else 0,
-                                      _p(link.fcoef) if bpart is not None else 0,
-                                      _p(link.mask) if bpart is not None else 0,
-                                      bool(link.relu) if bpart is not None else False, _p(amask))
-            if bpart is not None and rows > 0:
-                # (partials, rows, the gradient tensor's address and version): autograd may sum
-                # another consumer's gradient INTO dx in place (var.add_(old_var)) before the BN
-                # sees it -- same address, bumped version -- and then these partials are stale
-                link.pre = (bpart, rows, dx.data_ptr(), dx._version)
-            if add is not None:
-                j.consumed = True
-            if ctx.deposit is not None:
-                ctx.deposit.dres, ctx.deposit.amask = dx, None  # picked up by the block's first conv (GradJoin)
+            if (_SUB2_DEPOSIT and ctx.deposit is not None and R == S == 1 and (sh, sw) == (2, 2)
+                    and (ph, pw) == (0, 0) and H == 2 * P and W == 2 * Q):
+                # stride-2 1x1 projection: its input gradient is nonzero at even (h, w) only --
+                # computed there as a stride-1 GEMM on the P x Q grid and left at half resolution
+                # for the block's first conv to add (GradJoin.sub2); nothing returned to autograd
+                dxc = torch.empty((N, P, Q, C), device=dy.device, dtype=BF16)
+                n = Cn.nhwc_conv_dgrad_scratch_floats(N, P, Q, C, K, 1, 1, 1, 1, 0, 0, P, Q)
+                scr = torch.empty((n,), device=dy.device, dtype=torch.float32) if n else None
+                Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dxc.data_ptr(), N, P, Q, C, K, 1, 1, 1, 1, 0, 0,
+                                   P, Q, _p(scr), st)
+                ctx.deposit.dres, ctx.deposit.amask, ctx.deposit.sub2 = dxc, None, True
+            else:
+                dx = torch.empty((N, H, W, C), device=dy.device, dtype=BF16)
+                n = Cn.nhwc_conv_dgrad_scratch_floats(N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q)
+                scr = torch.empty((n,), device=dy.device, dtype=torch.float32) if n else None
+                j = ctx.join
+                add, sub = None, False
+                if j is not None and j.dres is not None:
+                    if j.dres.shape == dx.shape and not j.sub2:
+                        add = j.dres
+                    elif (j.sub2 and R == S == 1 and (sh, sw) == (1, 1) and H % 2 == 0 and W % 2 == 0
+                          and j.dres.shape == (N, H // 2, W // 2, C)):
+                        add, sub = j.dres, True
+                amask = j.amask if add is not None else None
+                link = ctx.bnlink
+                if link is not None and link.join is not None and add is None:
+                    link = None  # the shortcut's gradient is not in this sum: not the BN's whole dy
+                bpart = None
+                if link is not None and link.x.shape == dx.shape:
+                    rows = Cn.nhwc_conv_dgrad_bn_rows(N, H, W, C, K, R, S, sh, sw, ph, pw, P, Q)
+                    bpart = torch.empty((rows * 2 * C,), device=dy.device, dtype=torch.float32)
+                rows = Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx.data_ptr(), N, H, W, C, K, R, S, sh, sw,
+                                          ph, pw, P, Q, _p(scr), st, _p(add), _p(bpart),
+                                          _p(link.x) if bpart is not None else 0,
+                                          _p(link.mean) if bpart is not None else 0,
+                                          _p(link.fcoef) if bpart is not None else 0,
+                                          _p(link.mask) if bpart is not None else 0,
+                                          bool(link.relu) if bpart is not None else False, _p(amask), sub)
+                if bpart is not None and rows > 0:
+                    # (partials, rows, the gradient tensor's address and version): autograd may sum
+                    # another consumer's gradient INTO dx in place (var.add_(old_var)) before the BN
+                    # sees it -- same address, bumped version -- and then these partials are stale
+                    link.pre = (bpart, rows, dx.data_ptr(), dx._version)
+                if add is not None:
+                    j.consumed = True
+                if ctx.deposit is not None:
+                    # picked up by the block's first conv (GradJoin)
+                    ctx.deposit.dres, ctx.deposit.amask, ctx.deposit.sub2 = dx, None, False
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(w)
             dw = sink if sink is not None else torch.empty_like(w)
@@ -295,6 +322,9 @@ def conv2d(x, w, stride=1, padding=0, pack: WeightPack | None = None, join: Grad
 # False: every BN runs its own statistics passes, forward and backward (the conv-epilogue
 # statistics measured a win on every ResNet-50 layer, docs/BENCHMARKS.md; tests may flip it)
 _BN_STATS_IN_CONV = True
+# stride-2 1x1 projection shortcuts deposit their input gradient at half resolution (GradJoin.sub2;
+# False: full resolution through the parity-class data gradient -- tests compare the two)
+_SUB2_DEPOSIT = True
 # Backward BN statistics in the consuming conv's data-gradient epilogue: OFF by default.  Measured
 # per layer at batch 256 (scripts/bench_nhwc_layers.py, profiles/r4_d/rn_layers.log) the epilogue
 # adds 2.9 ms to the step's data gradients (the LDS-DMA kernel runs one block per CU, so the x

@@ -114,6 +114,37 @@ def test_wgrad_tile256(cuda, case):
     assert _rel(grads[0], grads[1]) < 1e-5  # same fp32 products, different summation order only
 
 
+@pytest.mark.parametrize("case", [(8, 256, 14, 14, 1024, 1, 1, 0), (5, 130 * 8, 7, 9, 136, 1, 1, 0),
+                                  (4, 128, 15, 13, 200, 3, 2, 1)])
+def test_wgrad_waves8(cuda, case):
+    """128-row weight-gradient tiles over 8 waves (nhwc_wgrad_set_waves8) vs 4 waves and the fp32
+    reference (partial tiles, stride 2)."""
+    from mxddp import native
+
+    N, C, H, W, K, R, st, pd = case
+    Cn = native()
+    torch.manual_seed(4)
+    x = torch.randn(N, H, W, C).to(torch.bfloat16)
+    w = torch.randn(K, C, R, R) * (2.0 / (C * R * R)) ** 0.5
+    wr = w.to(torch.bfloat16).float().requires_grad_()
+    yr = F.conv2d(_nchw(x), wr, None, st, pd)
+    gy = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(gy)
+    gyn = gy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(cuda)
+    grads = []
+    try:
+        for w8 in (1, 0):
+            Cn.nhwc_wgrad_set_waves8(w8)
+            wg = w.to(cuda).requires_grad_()
+            nhwc.conv2d(x.to(cuda), wg, st, pd).backward(gyn)
+            torch.cuda.synchronize()
+            grads.append(wg.grad.cpu())
+    finally:
+        Cn.nhwc_wgrad_set_waves8(0)
+    assert _rel(grads[0], wr.grad) < 1e-2
+    assert _rel(grads[0], grads[1]) < 1e-5
+
+
 @pytest.mark.parametrize("case", [(2, 64, 14, 14, 192, 3, 1, 1), (3, 128, 13, 11, 64, 1, 1, 0),
                                   (2, 64, 15, 15, 128, 3, 2, 1), (1, 128, 9, 9, 256, 3, 1, 1),
                                   (1, 256, 7, 7, 128, 3, 1, 1),  # long reduction: split-K partials
@@ -562,6 +593,53 @@ def test_lazy_identity_join_equals_materialised(cuda):
     # the same bf16 values are added in the same epilogue: equal up to run-to-run bf16 flips
     for a, b in zip(*outs):
         assert _nrel(b, a) < 1e-2
+
+
+@pytest.mark.parametrize("inp,planes,hw", [(256, 128, 28), (512, 256, 14), (64, 64, 10)])
+def test_half_resolution_projection_gradient(cuda, inp, planes, hw):
+    """Stride-2 1x1 projection shortcut: its input gradient computed on the output grid and added
+    at even (h, w) in the first conv's epilogue (GradJoin.sub2) == the full-resolution parity-class
+    data gradient joined as before, for the block input and every parameter."""
+    from mxddp.models.layers import BatchNorm2d, Conv2d
+    from mxddp.models.resnet import Bottleneck
+
+    torch.manual_seed(21)
+    blk = Bottleneck(inp, planes, 2, nn.Sequential(Conv2d(inp, planes * 4, 1, 2, bias=False),
+                                                   BatchNorm2d(planes * 4))).to(cuda)
+    x = torch.randn(4, hw, hw, inp).to(torch.bfloat16).to(cuda)
+    state = _bn_state([blk])
+    outs = []
+    try:
+        for sub2 in (False, True):
+            nhwc._SUB2_DEPOSIT = sub2
+            _restore(state)
+            blk.zero_grad()
+            xg = x.clone().requires_grad_()
+            y = blk.forward_nhwc(xg)
+            gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(6)).to(torch.bfloat16).to(cuda)
+            y.backward(gy)
+            torch.cuda.synchronize()
+            outs.append([xg.grad.float().cpu()] + [p.grad.cpu() for p in blk.parameters()])
+    finally:
+        nhwc._SUB2_DEPOSIT = True
+    for a, b in zip(*outs):
+        assert _nrel(b, a) < 1e-2
+
+
+def test_half_resolution_deposit_without_consumer(cuda):
+    """A half-resolution deposit that no conv epilogue picked up is added by the fork's backward at
+    the even positions (fallback)."""
+    torch.manual_seed(2)
+    x = torch.randn(2, 6, 8, 16).to(torch.bfloat16).to(cuda).requires_grad_()
+    join = nhwc.GradJoin()
+    main, short = nhwc.fork(x, join)
+    dres = torch.randn(2, 3, 4, 16).to(torch.bfloat16).to(cuda)
+    join.dres, join.sub2 = dres, True
+    (main.float() * 2.0).sum().backward()
+    want = torch.full(x.shape, 2.0, device=cuda)
+    want[:, ::2, ::2, :] += dres.float()
+    assert torch.allclose(x.grad.float(), want.to(torch.bfloat16).float())
+    assert join.dres is None and not join.sub2
 
 
 @pytest.mark.parametrize("offset", [0.0, 3.0])
