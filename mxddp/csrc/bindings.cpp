@@ -115,6 +115,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_conv_set_glds256", &nhwc_conv_set_glds256);
   m.def("nhwc_conv_set_glds_short", &nhwc_conv_set_glds_short);
   m.def("nhwc_conv_set_glds_deep", &nhwc_conv_set_glds_deep);
+  m.def("nhwc_conv_set_glds_par", &nhwc_conv_set_glds_par);
   m.def("nhwc_wgrad_set_waves8", &nhwc_wgrad_set_waves8);
   m.def("nhwc_bn_set_grid_cap", &nhwc_bn_set_grid_cap);
   m.def("nhwc_conv_set_split_blocks", &nhwc_conv_set_split_blocks);

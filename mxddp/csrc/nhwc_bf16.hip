@@ -592,6 +592,19 @@ __global__ __launch_bounds__(512, TN == 128 ? 2 : 1) void conv_nhwc_glds_kernel(
     aok[j] = ch0 + arow[j] < a.Ng;
     abase[j] = 2u * ((uint32_t)(ch0 + (aok[j] ? arow[j] : 0)) * a.Kg + 8 * (pch ^ (arow[j] & 7)));
   }
+  // par (stride-2 data gradient, as in conv_nhwc_kernel): blockIdx.z = output parity class
+  // (h & 1, w & 1), its pixels (n, 2 i + pca, 2 j + pcb), only the taps of matching parity
+  const int pca = a.par ? (int)blockIdx.z >> 1 : 0, pcb = a.par ? (int)blockIdx.z & 1 : 0;
+  const int r0 = a.par ? (pca + a.ph) & 1 : 0, s0 = a.par ? (pcb + a.pw) & 1 : 0;
+  const int nS = a.par ? (a.S - s0 + 1) >> 1 : a.S;
+  const int Kgc = a.par ? ((a.R - r0 + 1) >> 1) * nS * a.Ca : a.Kg;
+  const int Mc = a.par ? a.M >> 2 : a.M;
+  auto pfull = [&](int m) -> int {  // output pixel of GEMM row m (the full dx index in par mode)
+    if (!a.par) return m;
+    const int n = (int)a.fHWc.div((uint32_t)m), rem = m - n * a.Hc * a.Wc;
+    const int i = (int)a.fWc.div((uint32_t)rem), j = rem - i * a.Wc;
+    return (n * a.OH + 2 * i + pca) * a.OW + 2 * j + pcb;
+  };
   uint32_t pbase[NB];
   int ihb[NB], iwb[NB], lchb[NB];
   bool pok[NB];
@@ -599,10 +612,20 @@ __global__ __launch_bounds__(512, TN == 128 ? 2 : 1) void conv_nhwc_glds_kernel(
   for (int j = 0; j < NB; ++j) {
     const int row = ((wave * NB + j) * 64 + lane) >> 3;
     const int m = px0 + row;
-    pok[j] = m < a.M;
+    pok[j] = m < Mc;
     const int mm = pok[j] ? m : 0;
-    const int n = (int)a.fOHW.div((uint32_t)mm), rem = mm - n * a.OH * a.OW;
-    const int oh = (int)a.fOW.div((uint32_t)rem), ow = rem - oh * a.OW;
+    int n, oh, ow;
+    if (a.par) {
+      n = (int)a.fHWc.div((uint32_t)mm);
+      const int rem = mm - n * a.Hc * a.Wc, i = (int)a.fWc.div((uint32_t)rem);
+      oh = 2 * i + pca;
+      ow = 2 * (rem - i * a.Wc) + pcb;
+    } else {
+      n = (int)a.fOHW.div((uint32_t)mm);
+      const int rem = mm - n * a.OH * a.OW;
+      oh = (int)a.fOW.div((uint32_t)rem);
+      ow = rem - oh * a.OW;
+    }
     pbase[j] = 2u * ((uint32_t)n * a.IH * a.IW * a.Ca);
     ihb[j] = a.dgrad ? oh + a.ph : oh * a.sh - a.ph;
     iwb[j] = a.dgrad ? ow + a.pw : ow * a.sw - a.pw;
@@ -613,17 +636,36 @@ __global__ __launch_bounds__(512, TN == 128 ? 2 : 1) void conv_nhwc_glds_kernel(
   auto issue = [&](int t, int buf) {
     const int k0 = (kt0 + t) * BK;
     const int rs = (int)a.fCa.div((uint32_t)k0), c0 = k0 - rs * a.Ca;  // uniform: one tap per stage
-    const int r = (int)a.fS.div((uint32_t)rs), s = rs - r * a.S;
+    int r, s, kw = k0;
+    if (a.par) {  // class tap rs -> (r0 + 2 ri, s0 + 2 si); weight column of that tap
+      const int ri = rs / nS, si = rs - ri * nS;
+      r = r0 + 2 * ri;
+      s = s0 + 2 * si;
+      kw = (r * a.S + s) * a.Ca + c0;
+    } else {
+      r = (int)a.fS.div((uint32_t)rs);
+      s = rs - r * a.S;
+    }
     char* st = smem + buf * SB;
-    const char* wb = reinterpret_cast<const char*>(a.wt) + 2u * (uint32_t)k0;
+    const char* wb = reinterpret_cast<const char*>(a.wt) + 2u * (uint32_t)kw;
 #pragma unroll
     for (int j = 0; j < NA; ++j)
       glds16(aok[j] ? (const void*)(wb + abase[j]) : (const void*)zero, st + (wave * NA + j) * 1024);
     const char* xb = reinterpret_cast<const char*>(a.act) + 2u * (uint32_t)c0;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const int ih = a.dgrad ? ihb[j] - r : ihb[j] + r, iw = a.dgrad ? iwb[j] - s : iwb[j] + s;
-      const bool ok = pok[j] && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
+      int ih, iw;
+      bool ok = pok[j];
+      if (!a.dgrad) {
+        ih = ihb[j] + r;
+        iw = iwb[j] + s;
+      } else {  // transposed: dy[(h + ph - r) / sh] where divisible (always, for a parity class's taps)
+        const int th = ihb[j] - r, tw = iwb[j] - s;
+        ih = a.sh == 1 ? th : th >> 1;
+        iw = a.sw == 1 ? tw : tw >> 1;
+        ok = ok && th >= 0 && tw >= 0 && ih * a.sh == th && iw * a.sw == tw;
+      }
+      ok = ok && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
       const char* src = xb + pbase[j] + 2u * (uint32_t)((ih * a.IW + iw) * a.Ca + lchb[j]);
       glds16(ok ? (const void*)src : (const void*)zero, st + AB + (wave * NB + j) * 1024);
     }
@@ -635,8 +677,8 @@ __global__ __launch_bounds__(512, TN == 128 ? 2 : 1) void conv_nhwc_glds_kernel(
 #pragma unroll
     for (int j = 0; j < WNT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // split-K over blockIdx.y (fp32 partials, summed by conv_nhwc_splitk_reduce_k)
-  const int nt = min(a.Kg / BK - kt0, a.kt_per_split);
+  // split-K over blockIdx.y (fp32 partials, summed by conv_nhwc_splitk_reduce_k); par: the class's taps
+  const int nt = min(Kgc / BK - kt0, a.kt_per_split);
   // NS - 1 stages in flight ahead of the one computed
   if (nt > 0) issue(0, 0);
   if (NS == 3 && nt > 1) issue(1, 1);
@@ -715,13 +757,13 @@ __global__ __launch_bounds__(512, TN == 128 ? 2 : 1) void conv_nhwc_glds_kernel(
       sh8[e] = a.bfcoef ? a.bfcoef[2 * (ch + e) + 1] : 0.f;
     }
   }
-  epi_vectors<512, TN * VPR / 512, VPR>(a, Cs, CP, px0, ch0, a.M, [](int px) { return px; }, bst, mean8, sc8, sh8,
-                                       s1, s2);
+  epi_vectors<512, TN * VPR / 512, VPR>(a, Cs, CP, px0, ch0, Mc, pfull, bst, mean8, sc8, sh8, s1, s2);
   if constexpr (kBst) {
     if (bst) {
       // reduction slots after the C tile in the (idle) stage buffers
       float* bred = reinterpret_cast<float*>(smem + ((TN * CP * 2 + 255) & ~255));
-      bn_bwd_flush<512, VPR>(a, bred, s1, s2, px0 / TN, ch0);
+      // partial row = (parity class, pixel tile)
+      bn_bwd_flush<512, VPR>(a, bred, s1, s2, (int)blockIdx.z * ((Mc + TN - 1) / TN) + px0 / TN, ch0);
     }
   }
   if constexpr (STATS) {  // BN statistics of the stored (bf16) tile: 512 / TM threads per channel
@@ -2729,10 +2771,16 @@ void nhwc_conv_set_glds_short(int mode) { g_conv_glds_short = mode; }
 // eligible layer, 3 = only where the 256-pixel tiles would under-fill the chip (the first rule)
 static int g_conv_glds_deep = 1;
 void nhwc_conv_set_glds_deep(int mode) { g_conv_glds_deep = mode; }
+// stride-2 data gradients (parity classes, blockIdx.z) on the same tiles: 1 = on, 0 = the generic
+// kernel's parity classes
+static int g_conv_glds_par = 1;
+void nhwc_conv_set_glds_par(int on) { g_conv_glds_par = on; }
 static bool glds_deep_fits(const ConvNArgs& a, bool wide, bool par) {
-  if (!g_conv_glds_deep || conv_glds_mode() == 0 || !wide || par || (a.dgrad && (a.sh != 1 || a.sw != 1))) return false;
+  if (!g_conv_glds_deep || conv_glds_mode() == 0 || !wide) return false;
+  if (a.dgrad && (a.sh != 1 || a.sw != 1) && !(par && g_conv_glds_par)) return false;
   if (a.Kg % 64 != 0 || a.Kg < 256 || a.Ng < 128) return false;
-  const int64_t t256 = (int64_t)cdiv(a.Ng, 128) * cdiv(a.M, 256), t128 = (int64_t)cdiv(a.Ng, 128) * cdiv(a.M, 128);
+  const int64_t mc = par ? a.M / 4 : a.M, cls = par ? 4 : 1;
+  const int64_t t256 = cls * cdiv(a.Ng, 128) * cdiv(mc, 256), t128 = cls * cdiv(a.Ng, 128) * cdiv(mc, 128);
   switch (g_conv_glds_deep) {
     case 2: return true;
     case 3: return t256 < 256 && t128 >= 256;
@@ -2824,17 +2872,24 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   const bool wide = cs.wide;
   const GldsPlan gp = glds_plan(a, wide, cs.par);
   if (glds_deep_fits(a, wide, cs.par)) {  // 128 x 128 tiles, two blocks per CU, no split-K
-    a.par = 0;
+    const bool par = cs.par;  // stride-2 data gradient: one grid slice per output parity class
+    a.par = par ? 1 : 0;
+    if (par) {
+      a.Hc = a.OH / 2;
+      a.Wc = a.OW / 2;
+      a.fWc = FastDiv(a.Wc);
+      a.fHWc = FastDiv(a.Hc * a.Wc);
+    }
     a.part = nullptr;
-    a.kt_per_split = a.Kg / 64;
-    const int gx = cdiv(a.M, 128);
-    const bool bst = a.dgrad && a.bx && a.bnpart && gx <= 16384;  // backward BN statistics epilogue
+    a.kt_per_split = a.Kg / 64;  // >= every class's k-tiles
+    const int gx = cdiv(par ? a.M / 4 : a.M, 128), rows = (par ? 4 : 1) * gx;
+    const bool bst = a.dgrad && a.bx && a.bnpart && rows <= 16384;  // backward BN statistics epilogue
     if (!bst) a.bx = nullptr;
-    if (!(a.bnpart && (bst || !a.dgrad) && gx <= 16384)) a.bnpart = nullptr;
-    const dim3 grid(cdiv(a.Ng, 128) * gx, 1);
+    if (!(a.bnpart && (bst || !a.dgrad) && rows <= 16384)) a.bnpart = nullptr;
+    const dim3 grid(cdiv(a.Ng, 128) * gx, 1, par ? 4 : 1);
     if (a.bnpart && !bst) MX_LAUNCH((conv_nhwc_glds_kernel<128, true, 128, 2>), grid, dim3(512), 0, st, a);
     else MX_LAUNCH((conv_nhwc_glds_kernel<128, false, 128, 2>), grid, dim3(512), 0, st, a);
-    return a.bnpart ? gx : 0;
+    return a.bnpart ? rows : 0;
   }
   if (gp.tm && glds256_fits(a)) {  // 256 x 256 tiles, no split-K
     a.par = 0;

@@ -196,7 +196,8 @@ void nhwc_conv_set_glds(int mode);
 // the 256 x 256-tile LDS-DMA kernel: 0 = off, 1 = layers with >= 256 tiles and >= 4 k-tiles (default), 2 = wherever Ng % 256 == 0
 void nhwc_conv_set_glds256(int mode);
 void nhwc_wgrad_set_waves8(int on);  // 8-wave 128-row weight-gradient tiles (A/B)
-void nhwc_conv_set_glds_deep(int mode);  // 128 x 128 LDS-DMA tiles for deep reductions on few tiles
+void nhwc_conv_set_glds_deep(int mode);
+void nhwc_conv_set_glds_par(int on);  // stride-2 data gradients on the two-stage LDS-DMA tiles  // 128 x 128 LDS-DMA tiles for deep reductions on few tiles
 void nhwc_conv_set_glds_short(int mode);  // two-stage 128-pixel LDS-DMA variant for short reductions
 void nhwc_conv_set_split_blocks(int n);  // generic conv kernel: split-K below this many blocks (256)
 void nhwc_wgrad_set_target(int n);  // weight gradient: blocks aimed at when splitting the pixels (512)

@@ -114,6 +114,38 @@ def test_wgrad_tile256(cuda, case):
     assert _rel(grads[0], grads[1]) < 1e-5  # same fp32 products, different summation order only
 
 
+@pytest.mark.parametrize("case", [(4, 256, 56, 56, 256, 3, 2, 1),   # 3x3: classes of 1, 2, 2, 4 taps
+                                  (8, 256, 56, 56, 512, 1, 2, 0),   # 1x1: three classes without taps
+                                  (6, 128, 60, 52, 192, 3, 2, 1)])  # partial channel / pixel tiles
+def test_conv_glds_parity_classes(cuda, case):
+    """Stride-2 data gradients on the two-stage LDS-DMA tiles, one grid slice per output parity
+    class (nhwc_conv_set_glds_par) == the generic kernel's parity classes and the fp32 reference."""
+    from mxddp import native
+
+    Cn = native()
+    N, C, H, W, K, R, st, pd = case
+    torch.manual_seed(8)
+    x = torch.randn(N, H, W, C).to(torch.bfloat16)
+    w = torch.randn(K, C, R, R) * (2.0 / (C * R * R)) ** 0.5
+    xr = _nchw(x).requires_grad_()
+    yr = F.conv2d(xr, w.to(torch.bfloat16).float(), None, st, pd)
+    gy = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(gy)
+    gyn = gy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(cuda)
+    dxs = []
+    try:
+        for on in (1, 0):
+            Cn.nhwc_conv_set_glds_par(on)
+            xg = x.to(cuda).requires_grad_()
+            nhwc.conv2d(xg, w.to(cuda), st, pd).backward(gyn)
+            torch.cuda.synchronize()
+            dxs.append(_nchw(xg.grad))
+    finally:
+        Cn.nhwc_conv_set_glds_par(1)
+    assert _rel(dxs[0], xr.grad) < 1e-2
+    assert _rel(dxs[0], dxs[1]) < 1e-2
+
+
 @pytest.mark.parametrize("case", [(8, 256, 14, 14, 1024, 1, 1, 0), (5, 130 * 8, 7, 9, 136, 1, 1, 0),
                                   (4, 128, 15, 13, 200, 3, 2, 1)])
 def test_wgrad_waves8(cuda, case):
@@ -422,7 +454,8 @@ def _bn_stats_from_conv_epilogue(cuda, shape, offset):
 
 @pytest.mark.parametrize("glds,stride,relu", [(2, 1, True), (2, 1, False), (0, 1, True), (0, 2, True),
                                               (0, 1, False), (256, 1, True), (256, 1, False),
-                                              ("deep", 1, True), ("short", 1, True), ("short", 1, False)])
+                                              ("deep", 1, True), ("deep", 2, True), ("short", 1, True),
+                                              ("short", 1, False)])
 def test_bn_backward_statistics_from_dgrad_epilogue(cuda, glds, stride, relu):
     """BN -> conv: the conv's data-gradient epilogue computes the BN's backward partial sums
     (sum g, sum g (x - mean), g masked by the BN's fused ReLU) and the BN backward skips its
