@@ -3100,9 +3100,11 @@ static void wgrad_tile(int K, int Ng, int Npix, int RS, int& tm, int& tn) {
 // weight-gradient blocks aimed at (A/B: nhwc_wgrad_set_target; 256 and 1,024 measured no better,
 // profiles/r4_y/); half that for the one-block-per-CU 256 x 256 tile
 static int g_wgrad_target = 512;
-// 128 x 128 (and 128 x 64) weight-gradient tiles over 8 waves (wave tile 64 x 32) instead of 4
-// (A/B: nhwc_wgrad_set_waves8)
-static int g_wgrad_w8 = 0;
+// 128 x 128 (and 128 x 64) weight-gradient tiles over 8 waves (wave tile 64 x 32) instead of 4:
+// four waves per SIMD at two blocks per CU.  ResNet-50 batch 32 5,568-5,582 vs 5,514-5,536 img/s,
+// batch 256 +0.2 % (noise); with 1,024 blocks aimed at instead of 512, batch 256 lost 2.5 %
+// (profiles/r5_w8/).  A/B: nhwc_wgrad_set_waves8
+static int g_wgrad_w8 = 1;
 void nhwc_wgrad_set_waves8(int on) { g_wgrad_w8 = on; }
 void nhwc_wgrad_set_target(int n) { g_wgrad_target = n; }
 static int wgrad_splits(int Npix, int K, int Ng, int RS) {

@@ -172,7 +172,7 @@ def test_wgrad_waves8(cuda, case):
             torch.cuda.synchronize()
             grads.append(wg.grad.cpu())
     finally:
-        Cn.nhwc_wgrad_set_waves8(0)
+        Cn.nhwc_wgrad_set_waves8(1)
     assert _rel(grads[0], wr.grad) < 1e-2
     assert _rel(grads[0], grads[1]) < 1e-5
 
