@@ -1462,15 +1462,19 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_nhwc_kernel(WgNArgs a) {
   const int rs = (int)a.fCa.div((uint32_t)colc), bc = colc - rs * a.Ca;
   const int br = (int)a.fS.div((uint32_t)rs), bs = rs - br * a.S;
   const bool k_ok = m0 + 8 * cva < a.Kout;
+  // every load is issued unconditionally from a valid (clamped) address and its validity kept
+  // beside it; the mask is applied when the stage is written to LDS.  (Masking right after the
+  // load, hipcc branched around each load and waited for the next stage's loads -- s_waitcnt
+  // vmcnt(0) -- before the current stage's MFMAs: no overlap at all.)
   u32x4 ra[EA], rb[EB];
+  bool ma[EA], mb[EB];
   const u32x4 z4 = {0u, 0u, 0u, 0u};
   auto gload = [&](int p0) {
 #pragma unroll
-    for (int i = 0; i < EA; ++i) {  // unconditional loads from clamped addresses, masked after
+    for (int i = 0; i < EA; ++i) {
       const int pix = p0 + rowa0 + (NT / VA) * i;
-      const bool ok = pix < pend && k_ok;
-      const u32x4 v = *reinterpret_cast<const u32x4*>(a.dy + (ok ? (size_t)pix * a.Kout + m0 + 8 * cva : 0));
-      ra[i] = ok ? v : z4;
+      ma[i] = pix < pend && k_ok;
+      ra[i] = *reinterpret_cast<const u32x4*>(a.dy + (ma[i] ? (size_t)pix * a.Kout + m0 + 8 * cva : 0));
     }
 #pragma unroll
     for (int i = 0; i < EB; ++i) {
@@ -1480,21 +1484,20 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_nhwc_kernel(WgNArgs a) {
       const int n = (int)a.fPQ.div((uint32_t)pp), rem = pp - n * a.P * a.Q;
       const int p = (int)a.fQ.div((uint32_t)rem), q = rem - p * a.Q;
       const int h = p * a.sh - a.ph + br, w = q * a.sw - a.pw + bs;
-      const bool xok = ok && col_ok && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-      const u32x4 v = *reinterpret_cast<const u32x4*>(a.x + (xok ? (((size_t)n * a.H + h) * a.W + w) * a.Ca + bc : 0));
-      rb[i] = xok ? v : z4;
+      mb[i] = ok && col_ok && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      rb[i] = *reinterpret_cast<const u32x4*>(a.x + (mb[i] ? (((size_t)n * a.H + h) * a.W + w) * a.Ca + bc : 0));
     }
   };
   auto sstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < EA; ++i) {
       const int r = rowa0 + (NT / VA) * i;
-      *reinterpret_cast<u32x4*>(&As[buf][r * PA + 8 * (cva ^ wg_swz(r))]) = ra[i];
+      *reinterpret_cast<u32x4*>(&As[buf][r * PA + 8 * (cva ^ wg_swz(r))]) = ma[i] ? ra[i] : z4;
     }
 #pragma unroll
     for (int i = 0; i < EB; ++i) {
       const int r = rowb0 + (NT / VB) * i;
-      *reinterpret_cast<u32x4*>(&Bs[buf][r * PB + 8 * (cvb ^ wg_swz(r))]) = rb[i];
+      *reinterpret_cast<u32x4*>(&Bs[buf][r * PB + 8 * (cvb ^ wg_swz(r))]) = mb[i] ? rb[i] : z4;
     }
   };
 
