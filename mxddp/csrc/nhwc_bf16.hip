@@ -157,30 +157,39 @@ __device__ __forceinline__ void bn_bwd_acc8(const ConvNArgs& a, const u32x4& v, 
   }
 }
 
-// The per-thread sums of a fixed 8-channel vector cv (threads tid = cv mod VPR) reduced in LDS
-// in a fixed order and written as partial row `row` (channels ch0 .. ch0 + 8 VPR - 1).
+// The per-thread sums of a fixed 8-channel vector cv (threads tid = cv mod VPR) reduced in a fixed
+// order and written as partial row `row` (channels ch0 .. ch0 + 8 VPR - 1): first across the lanes
+// of a wave that share cv (lane shuffles), then the NT / 64 wave partials through LDS by one
+// thread per (cv, value).  (The former all-LDS version had 8 VPR threads each walk NT / VPR
+// slots in series.)
 template <int NT, int VPR>
 __device__ __forceinline__ void bn_bwd_flush(const ConvNArgs& a, float* red, const float* s1, const float* s2,
                                              int row, int ch0) {
-  const int tid = threadIdx.x;
+  static_assert(64 % VPR == 0 || VPR == 64, "a channel vector's threads tile the wave");
+  constexpr int NW = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  float v[16];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    red[e * NT + tid] = s1[e];
-    red[(8 + e) * NT + tid] = s2[e];
+    v[e] = s1[e];
+    v[8 + e] = s2[e];
+  }
+#pragma unroll
+  for (int off = VPR; off < 64; off <<= 1)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] += __shfl_xor(v[j], off);
+  if (lane < VPR) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) red[(j * NW + wv) * VPR + lane] = v[j];
   }
   __syncthreads();
-  if (tid < 8 * VPR) {
-    const int cv = tid >> 3, e = tid & 7, ch = ch0 + tid;
-    float t1 = 0.f, t2 = 0.f;
-    for (int k = 0; k < NT / VPR; ++k) {
-      t1 += red[e * NT + cv + k * VPR];
-      t2 += red[(8 + e) * NT + cv + k * VPR];
-    }
-    if (ch < a.Ng) {
-      float* dst = a.bnpart + (size_t)row * 2 * a.Ng + 2 * ch;
-      dst[0] = t1;
-      dst[1] = t2;
-    }
+  if (tid < 16 * VPR) {
+    const int j = tid / VPR, cv = tid - j * VPR;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += red[(j * NW + w) * VPR + cv];
+    const int e = j & 7, ch = ch0 + 8 * cv + e;
+    if (ch < a.Ng) a.bnpart[(size_t)row * 2 * a.Ng + 2 * ch + (j >> 3)] = t;
   }
 }
 
