@@ -3093,7 +3093,9 @@ int nhwc_conv_dgrad_bn_rows(int N, int H, int W, int C, int K, int R, int S, int
 }
 
 // 256 x 256 weight-gradient tiles where both GEMM dimensions reach 256 and the layer is a 3x3
-// with >= 12,544 pixels or has >= 96 K pixels (A/B: nhwc_wgrad_set_tile256).  Per layer at batch
+// with > 12,544 pixels or has >= 96 K pixels (A/B: nhwc_wgrad_set_tile256).  (The two 3x3 layers
+// of exactly 12,544 output pixels at batch 256 -- the 7 x 7 stage -- moved to the 8-wave 128 x 128
+// tile once it existed: 141 -> 129 and 140 -> 130 us, profiles/r5_wtile/.)  Per layer at batch
 // 256 (profiles/r5_wgrad/): the 3x3 layers 395 -> 585, 402 -> 585 TF/s, 28 x 28 1x1 412 -> 482;
 // the 1x1 layers of 14 x 14 and 7 x 7 (<= 50 K pixels, one block per CU with few stages each)
 // 3-14 % slower.  At batch 32 (<= 6,272 pixels per layer) every 3x3 layer lost 17-22 % and the
@@ -3101,7 +3103,7 @@ int nhwc_conv_dgrad_bn_rows(int N, int H, int W, int C, int K, int R, int S, int
 static int g_wgrad_tile256 = 1;
 void nhwc_wgrad_set_tile256(int on) { g_wgrad_tile256 = on; }
 static void wgrad_tile(int K, int Ng, int Npix, int RS, int& tm, int& tn) {
-  if (g_wgrad_tile256 && K >= 256 && Ng >= 256 && ((RS > 1 && Npix >= 12544) || Npix >= 96 * 1024)) {
+  if (g_wgrad_tile256 && K >= 256 && Ng >= 256 && ((RS > 1 && Npix > 12544) || Npix >= 96 * 1024)) {
     tm = tn = 256;
     return;
   }
