@@ -35,3 +35,20 @@ def test_fork_lazy_join_fallback():
     join.dres, join.amask, join.consumed = dy, mask, True
     main.backward(g_main)
     assert torch.equal(x.grad, g_main)
+
+
+def test_fork_half_resolution_join_fallback():
+    """A stride-2 projection's half-resolution input gradient (GradJoin.sub2; the projection conv
+    returns no gradient of its own) that no conv epilogue consumed: the fork adds it at the even
+    (h, w) positions and clears the join."""
+    join = nhwc.GradJoin()
+    x = torch.randn(2, 6, 4, 8, requires_grad=True)
+    main, short = nhwc.fork(x, join)
+    dres = torch.randn(2, 3, 2, 8)
+    join.dres, join.sub2 = dres, True
+    g_main = torch.randn(2, 6, 4, 8)
+    main.backward(g_main)  # short gets no gradient, as behind the projection conv
+    want = g_main.clone()
+    want[:, ::2, ::2, :] += dres
+    assert torch.allclose(x.grad, want)
+    assert join.dres is None and not join.sub2
