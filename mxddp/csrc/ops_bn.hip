@@ -150,12 +150,17 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_reduce_k(const float* __restrict
                  *y4 = reinterpret_cast<const float4*>(yr);
     for (int i0 = threadIdx.x; i0 < total; i0 += kBnU * kBnTB) {
       const BnChunk k = bn_chunk(i0, total, sl, hw4, C, c, 0, dv);
+      // the optional operand's loads under one uniform branch (a branch per load made the
+      // waitcnt pass drain each load before the next: one round trip per vector)
       float4 g[kBnU], v[kBnU], r[kBnU];
 #pragma unroll
       for (int u = 0; u < kBnU; ++u) {
         g[u] = g4[k.o[u]];
         v[u] = x4[k.o[u]];
-        if (yr) r[u] = y4[k.o[u]];
+      }
+      if (yr) {
+#pragma unroll
+        for (int u = 0; u < kBnU; ++u) r[u] = y4[k.o[u]];
       }
 #pragma unroll
       for (int u = 0; u < kBnU; ++u) {
@@ -307,8 +312,14 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_apply_slice_k(
     for (int u = 0; u < kBnU; ++u) {
       g0[u] = g4[k0.o[u]];
       v0[u] = x4[k0.o[u]];
-      if (yr) r0[u] = y4[k0.o[u]];
-      if (e4) e0[u] = e4[k0.so[u]];
+    }
+    if (yr) {  // optional operands under one uniform branch each (see bn_bwd_reduce_k)
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) r0[u] = y4[k0.o[u]];
+    }
+    if (e4) {
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) e0[u] = e4[k0.so[u]];
     }
   }
   const float inv = invstd[c], mu = mean[c];
@@ -355,8 +366,14 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_apply_slice_k(
       for (int u = 0; u < kBnU; ++u) {
         g[u] = g4[k.o[u]];
         v[u] = x4[k.o[u]];
-        if (yr) r[u] = y4[k.o[u]];
-        if (e4) e[u] = e4[k.so[u]];
+      }
+      if (yr) {
+#pragma unroll
+        for (int u = 0; u < kBnU; ++u) r[u] = y4[k.o[u]];
+      }
+      if (e4) {
+#pragma unroll
+        for (int u = 0; u < kBnU; ++u) e[u] = e4[k.so[u]];
       }
       apply(k, g, v, r, e);
     }
@@ -508,25 +525,30 @@ __global__ __launch_bounds__(kBnF) void bn_bwd_fused_k(const float* __restrict__
   const float4* x4 = reinterpret_cast<const float4*>(x);
   const float4* y4 = reinterpret_cast<const float4*>(yr);
   const float4* e4 = extra ? reinterpret_cast<const float4*>(extra + (size_t)c * HW) : nullptr;
-  float4 g[U], v[U], e[U];
+  float4 g[U], v[U], e[U], r[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     g[u] = g4[o[u]];
     v[u] = x4[o[u]];
   }
+  // every y load issued before the first mask select (a select right after each load drained it:
+  // one round trip per vector)
   if (yr) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const float4 r = y4[o[u]];
-      g[u].x = r.x > 0.f ? g[u].x : 0.f;
-      g[u].y = r.y > 0.f ? g[u].y : 0.f;
-      g[u].z = r.z > 0.f ? g[u].z : 0.f;
-      g[u].w = r.w > 0.f ? g[u].w : 0.f;
-    }
+    for (int u = 0; u < U; ++u) r[u] = y4[o[u]];
   }
   if (e4) {  // the shortcut's gradient (channel c of a wider tensor): issued before the reduction
 #pragma unroll
     for (int u = 0; u < U; ++u) e[u] = e4[so[u]];
+  }
+  if (yr) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      g[u].x = r[u].x > 0.f ? g[u].x : 0.f;
+      g[u].y = r[u].y > 0.f ? g[u].y : 0.f;
+      g[u].z = r[u].z > 0.f ? g[u].z : 0.f;
+      g[u].w = r[u].w > 0.f ? g[u].w : 0.f;
+    }
   }
   const float mu = mean[c], inv = invstd[c];
   float s1 = 0.f, s2 = 0.f;
