@@ -40,7 +40,7 @@ MODEL_METRIC = {
 # --ab KEY=VALUE: measured-once kernel choices kept switchable for A/B runs (docs/BENCHMARKS.md)
 AB_SWITCHES = {
     "conv_tile256": ("nhwc_conv_set_glds256", "bf16 NHWC convs, 256x256-tile LDS-DMA kernel on big layers (0/1)"),
-    "glds_deep": ("nhwc_conv_set_glds_deep", "bf16 NHWC convs, 128 x 128 two-stage tiles on deep reductions with few tiles (0/1)"),
+    "glds_deep": ("nhwc_conv_set_glds_deep", "bf16 NHWC convs, 128 x 128 two-stage tiles on >= 4 k-tile layers (0 off, 1 >= 192 tiles, 2 all, 3 under-filled only)"),
     "glds_par": ("nhwc_conv_set_glds_par", "bf16 NHWC stride-2 data gradients on the two-stage LDS-DMA tiles (1) or the generic kernel (0)"),
     "glds_short": ("nhwc_conv_set_glds_short", "bf16 NHWC convs, two-stage 128-pixel variant on short reductions (0/1)"),
     "bn_grid_cap": ("nhwc_bn_set_grid_cap", "bf16 NHWC BN apply kernels, most blocks"),
