@@ -915,8 +915,10 @@ using namespace mnist;
 
 size_t mnist_fused_scratch_floats(int B) { return scratch_floats(B); }
 
-// default: F2 and F6W (+0.9 % at 2,000 steps; F5's own stores measured -0.7 %, profiles/r4_ab*)
-static int g_wt_stores = 6;
+// default: F5, F2 and F6W.  Round 4 measured F2 + F6W +0.9 % and F5's own stores -0.7 %
+// (profiles/r4_ab*); with round 5's F6W / F3 the F5 stores pay too: 936-938k vs 928-930k img/s at
+// the driver's length, 940-942k vs 933-935k at 2,000 steps (profiles/r5_wt/)
+static int g_wt_stores = 7;
 void mnist_set_wt_stores(int mask) { g_wt_stores = mask & 7; }
 int mnist_wt_stores() { return g_wt_stores; }
 
