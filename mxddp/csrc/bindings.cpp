@@ -118,6 +118,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_conv_set_glds_par", &nhwc_conv_set_glds_par);
   m.def("nhwc_wgrad_set_waves8", &nhwc_wgrad_set_waves8);
   m.def("nhwc_bn_set_grid_cap", &nhwc_bn_set_grid_cap);
+  m.def("nhwc_bn_set_wt", &nhwc_bn_set_wt);
+  m.def("nhwc_conv_set_wt", &nhwc_conv_set_wt);
   m.def("nhwc_conv_set_split_blocks", &nhwc_conv_set_split_blocks);
   m.def("nhwc_wgrad_set_target", &nhwc_wgrad_set_target);
   m.def("nhwc_wgrad_set_tile256", &nhwc_wgrad_set_tile256);

@@ -88,6 +88,17 @@ __device__ __forceinline__ u32x4 mask8(u32x4 d, uint32_t mb) {
     d[j] &= ((mb >> (2 * j)) & 1u ? 0x0000ffffu : 0u) | ((mb >> (2 * j + 1)) & 1u ? 0xffff0000u : 0u);
   return d;
 }
+// 16-byte store with agent scope (sc1, a vector store): the line is not kept dirty in this XCD's
+// L2, so a streaming output drains while the kernel runs instead of at its end
+__device__ __forceinline__ void st16(void* p, const uint4& v, bool wt) {
+  if (wt) {
+    const u32x4 q = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(q) : "memory");
+  } else {
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+}
+
 // epilogue of a data gradient: the residual join's addend, optionally masked by its ReLU bits
 __device__ __forceinline__ u32x4 join8(u32x4 v, const bf16* addend, const uint8_t* amask, size_t o) {
   u32x4 d = *reinterpret_cast<const u32x4*>(addend + o);
@@ -117,6 +128,7 @@ struct ConvNArgs {
   const uint8_t* amask;  // addend masked by these ReLU bits (bit e of byte o / 8), or null: the
                          // identity shortcut's gradient taken straight from the block's output
                          // gradient, never materialised by the last BN's backward
+  int owt;   // epilogue output stored write-through (g_conv_wt, A/B)
   int asub;  // the addend is [N][OH / 2][OW / 2][Ng] and joins at even (h, w) only: a stride-2 1x1
              // projection shortcut's input gradient, computed compact (zero at the odd positions)
   // forward feeding a training BatchNorm (LDS-DMA kernel, no split): the epilogue writes the BN's
@@ -253,7 +265,8 @@ __device__ __forceinline__ void epi_vectors(const ConvNArgs& a, const bf16* Cs, 
     const int v = tid + NT * k, row = v / VPR, cv = v - row * VPR;
     u32x4 val = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
     if (a.addend && aok[k]) val = add8(val, a.amask ? mask8(ad[k], am[k]) : ad[k]);
-    *reinterpret_cast<u32x4*>(a.out + o[k]) = val;
+    if (a.owt) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(a.out + o[k]), "v"(val) : "memory");
+    else *reinterpret_cast<u32x4*>(a.out + o[k]) = val;
     if (bst) bn_bwd_acc8(a, val, xr[k], mb[k], mean8, sc8, sh8, s1, s2);
   }
 }
@@ -2030,6 +2043,7 @@ struct BnNArgs {
                        // written by the forward apply, read by the backward instead of y
   const float* kshift;  // fwd, partials precomputed by the conv epilogue: their per-channel shift
   int pre;              // fwd: part already holds gx partial rows (no statistics pass)
+  int wt;               // apply passes: outputs stored write-through (g_bn_wt)
   float momentum, eps;
 };
 
@@ -2325,7 +2339,7 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_apply_k(BnNArgs a, FastDiv fV) {
         xv[e] = a.relu ? fmaxf(o, 0.f) : o;
       }
       const uint4 yo = pack8(xv);
-      reinterpret_cast<uint4*>(a.y)[i] = yo;
+      st16(reinterpret_cast<uint4*>(a.y) + i, yo, a.wt);
       if (a.mask) a.mask[i] = (uint8_t)pos_bits8(yo);
     }
   };
@@ -2431,11 +2445,11 @@ __global__ __launch_bounds__(kBnT) void bn_nhwc_bwd_apply_k(BnNArgs a, FastDiv f
 #pragma unroll
         for (int e = 0; e < 8; ++e) g[e] = yv[e] > 0.f ? g[e] : 0.f;
       }
-      if (a.dres) reinterpret_cast<uint4*>(a.dres)[i] = pack8(g);
+      if (a.dres) st16(reinterpret_cast<uint4*>(a.dres) + i, pack8(g), a.wt);
       float o[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = fmaf(kc[3 * e], g[e], fmaf(kc[3 * e + 1], xv[e], kc[3 * e + 2]));
-      reinterpret_cast<uint4*>(a.dx)[i] = pack8(o);
+      st16(reinterpret_cast<uint4*>(a.dx) + i, pack8(o), a.wt);
     }
   };
   if constexpr (!PIPE) {
@@ -2804,6 +2818,8 @@ static bool glds_deep_fits(const ConvNArgs& a, bool wide, bool par) {
 // blocks of the BN apply kernels (any multiple of 256 threads keeps each thread's channel vector
 // fixed): stream_blocks; ResNet-50 9,981 -> 10,218 img/s against the old 2,048-block cap
 // (profiles/r4_l/)
+static int g_bn_wt = 1;  // ResNet-50 b32 5,682 -> 5,772 img/s with g_conv_wt (profiles/r5_nhwcwt)
+void nhwc_bn_set_wt(int on) { g_bn_wt = on; }
 void nhwc_bn_set_grid_cap(int cap) {  // cap of stream_blocks (2048 = the round-3 grids)
   MX_CHECK(cap >= 256, "nhwc_bn_set_grid_cap: >= 256");
   g_stream_cap = cap;
@@ -2856,7 +2872,10 @@ static int launch_splitk_reduce(const ConvNArgs& a, float* scratch, int splits, 
 
 // returns the number of BN partial rows the epilogue wrote to a.bnpart (0: none, the BN runs its
 // own statistics pass)
+static int g_conv_wt = 1;  // b256 11,037 -> 11,055 (noise level), PyramidNet-110 neutral
+void nhwc_conv_set_wt(int on) { g_conv_wt = on; }
 static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
+  a.owt = g_conv_wt;
   MX_CHECK(a.Kg % 8 == 0 && a.Ca % 8 == 0 && a.Ng % 8 == 0, "nhwc conv: channels must be multiples of 8");
   a.fOW = FastDiv(a.OW);
   a.fOHW = FastDiv(a.OH * a.OW);
@@ -3263,6 +3282,7 @@ void nhwc_bn_fwd(const uint16_t* x, const uint16_t* res, uint16_t* y, const floa
   MX_LAUNCH(bn_nhwc_finalize_k<false>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
   const dim3 agrid(stream_blocks((int64_t)Npix * V));
+  a.wt = g_bn_wt;
   MX_LAUNCH((bn_nhwc_apply_k<2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
 }
 
@@ -3305,6 +3325,7 @@ void nhwc_bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const
   MX_LAUNCH(bn_nhwc_finalize_k<true>, dim3(cdiv(C, 8)), dim3(1024), 0, st, a);
   MX_CHECK((int64_t)Npix * V < (1ll << 31), "nhwc bn: tensor too large for 32-bit indices");
   const dim3 agrid(stream_blocks((int64_t)Npix * V));
+  a.wt = g_bn_wt;
   if (a.fcoef) MX_LAUNCH((bn_nhwc_bwd_apply_k<true, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
   else MX_LAUNCH((bn_nhwc_bwd_apply_k<false, 2, true>), agrid, dim3(kBnT), 0, st, a, FastDiv(V));
 }

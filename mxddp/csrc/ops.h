@@ -202,7 +202,9 @@ void nhwc_conv_set_glds_short(int mode);  // two-stage 128-pixel LDS-DMA variant
 void nhwc_conv_set_split_blocks(int n);  // generic conv kernel: split-K below this many blocks (256)
 void nhwc_wgrad_set_target(int n);  // weight gradient: blocks aimed at when splitting the pixels (512)
 void nhwc_wgrad_set_tile256(int on);  // weight gradient: 256 x 256 tiles where K and R*S*C reach 256 (1)
-void nhwc_bn_set_grid_cap(int cap);  // most blocks of the NHWC BN apply kernels (A/B; 2048 = round-3 grids)
+void nhwc_bn_set_grid_cap(int cap);
+void nhwc_bn_set_wt(int on);
+void nhwc_conv_set_wt(int on);  // conv epilogue outputs stored write-through (A/B)  // BN apply passes: outputs stored write-through (A/B)  // most blocks of the NHWC BN apply kernels (A/B; 2048 = round-3 grids)
 // split-K scratch of nhwc_conv_dgrad (floats; 0 = none needed)
 size_t nhwc_conv_dgrad_scratch_floats(int N, int H, int W, int C, int K, int R, int S, int sh, int sw, int ph, int pw,
                                       int P, int Q);
