@@ -43,7 +43,7 @@ AB_SWITCHES = {
     "glds_deep": ("nhwc_conv_set_glds_deep", "bf16 NHWC convs, 128 x 128 two-stage tiles on >= 4 k-tile layers (0 off, 1 >= 192 tiles, 2 all, 3 under-filled only)"),
     "glds_par": ("nhwc_conv_set_glds_par", "bf16 NHWC stride-2 data gradients on the two-stage LDS-DMA tiles (1) or the generic kernel (0)"),
     "glds_short": ("nhwc_conv_set_glds_short", "bf16 NHWC convs, two-stage 128-pixel variant on short reductions (0/1)"),
-    "conv_wt": ("nhwc_conv_set_wt", "bf16 NHWC conv epilogue outputs stored write-through (0/1; default 1)"),
+    "conv_wt": ("nhwc_conv_set_wt", "bf16 NHWC conv outputs stored write-through, bit mask: 1 epilogue, 2 split-K partials, 4 split-K reduce (default 3)"),
     "bn_wt": ("nhwc_bn_set_wt", "bf16 NHWC BN apply passes, outputs stored write-through (0/1; default 1)"),
     "bn_grid_cap": ("nhwc_bn_set_grid_cap", "bf16 NHWC BN apply kernels, most blocks"),
     "split_blocks": ("nhwc_conv_set_split_blocks", "bf16 NHWC generic conv, split-K only below this many blocks"),

@@ -42,6 +42,7 @@ namespace {
 using bf16 = unsigned short;
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // register-promotable (HIP's uint4 arrays are not)
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float bf2f(uint32_t v16) { return __uint_as_float(v16 << 16); }
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
@@ -128,7 +129,7 @@ struct ConvNArgs {
   const uint8_t* amask;  // addend masked by these ReLU bits (bit e of byte o / 8), or null: the
                          // identity shortcut's gradient taken straight from the block's output
                          // gradient, never materialised by the last BN's backward
-  int owt;   // epilogue output stored write-through (g_conv_wt, A/B)
+  int owt;   // outputs stored write-through (g_conv_wt): bit 0 epilogue, 1 split-K partials, 2 reduce
   int asub;  // the addend is [N][OH / 2][OW / 2][Ng] and joins at even (h, w) only: a stride-2 1x1
              // projection shortcut's input gradient, computed compact (zero at the odd positions)
   // forward feeding a training BatchNorm (LDS-DMA kernel, no split): the epilogue writes the BN's
@@ -265,7 +266,7 @@ __device__ __forceinline__ void epi_vectors(const ConvNArgs& a, const bf16* Cs, 
     const int v = tid + NT * k, row = v / VPR, cv = v - row * VPR;
     u32x4 val = *reinterpret_cast<const u32x4*>(Cs + row * CP + 8 * cv);
     if (a.addend && aok[k]) val = add8(val, a.amask ? mask8(ad[k], am[k]) : ad[k]);
-    if (a.owt) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(a.out + o[k]), "v"(val) : "memory");
+    if (a.owt & 1) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(a.out + o[k]), "v"(val) : "memory");
     else *reinterpret_cast<u32x4*>(a.out + o[k]) = val;
     if (bst) bn_bwd_acc8(a, val, xr[k], mb[k], mean8, sc8, sh8, s1, s2);
   }
@@ -510,8 +511,9 @@ __global__ __launch_bounds__(256, 2) void conv_nhwc_kernel(ConvNArgs a) {
       for (int j = 0; j < WNT; ++j) {
         const int px = px0 + wn * (TN / 2) + 16 * j + (lane & 15);
         if (px >= Mc) continue;
-        *reinterpret_cast<float4*>(a.part + ((size_t)blockIdx.y * a.M + pfull(px)) * a.Ng + ch) =
-            make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        float* pp = a.part + ((size_t)blockIdx.y * a.M + pfull(px)) * a.Ng + ch;
+        if (a.owt & 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(pp), "v"(acc[i][j]) : "memory");
+        else *reinterpret_cast<float4*>(pp) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
       }
     }
     return;
@@ -740,9 +742,10 @@ __global__ __launch_bounds__(512, TN == 128 ? 2 : 1) void conv_nhwc_glds_kernel(
 #pragma unroll
       for (int j = 0; j < WNT; ++j) {
         const int px = px0 + wn * WPX + 16 * j + (lane & 15);
-        if (px < a.M)
-          *reinterpret_cast<float4*>(a.part + ((size_t)blockIdx.y * a.M + px) * a.Ng + ch) =
-              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        if (px >= a.M) continue;
+        float* pp = a.part + ((size_t)blockIdx.y * a.M + px) * a.Ng + ch;
+        if (a.owt & 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(pp), "v"(acc[i][j]) : "memory");
+        else *reinterpret_cast<float4*>(pp) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
       }
     }
     return;
@@ -1345,7 +1348,7 @@ template <bool STATS>
 __global__ __launch_bounds__(256) void conv_nhwc_splitk_reduce_k(const float* __restrict__ part, bf16* __restrict__ out,
                                                                  int64_t n4, int splits, const bf16* __restrict__ addend,
                                                                  const uint8_t* __restrict__ amask, float* __restrict__ bnpart,
-                                                                 const float* __restrict__ bnshift, int Ng) {
+                                                                 const float* __restrict__ bnshift, int Ng, int wt) {
   const float4* p4 = reinterpret_cast<const float4*>(part);
   const int q4 = Ng >> 2;
   const int cq = STATS ? (int)((blockIdx.x * 256ll + threadIdx.x) % q4) : 0;
@@ -1380,7 +1383,12 @@ __global__ __launch_bounds__(256) void conv_nhwc_splitk_reduce_k(const float* __
       s.x += bf2f(d.x & 0xffffu); s.y += bf2f(d.x >> 16); s.z += bf2f(d.y & 0xffffu); s.w += bf2f(d.y >> 16);
     }
     const uint2 o = make_uint2(pack2(s.x, s.y), pack2(s.z, s.w));
-    reinterpret_cast<uint2*>(out)[i] = o;
+    if (wt) {
+      const u32x2 q = {o.x, o.y};
+      asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(reinterpret_cast<uint2*>(out) + i), "v"(q) : "memory");
+    } else {
+      reinterpret_cast<uint2*>(out)[i] = o;
+    }
     if (STATS) {
       const float y[4] = {bf2f(o.x & 0xffffu), bf2f(o.x >> 16), bf2f(o.y & 0xffffu), bf2f(o.y >> 16)};
 #pragma unroll
@@ -2862,17 +2870,20 @@ static int launch_splitk_reduce(const ConvNArgs& a, float* scratch, int splits, 
   if (fpart && !a.dgrad && !a.addend && splitk_bn_ok(a.Ng)) {
     const int rows = splitk_bn_rows(a.M, a.Ng);
     MX_LAUNCH(conv_nhwc_splitk_reduce_k<true>, dim3(rows * splitk_bn_bpr(a.Ng)), dim3(256), 0, st, scratch, a.out, n4,
-              splits, a.addend, a.amask, fpart, a.bnshift, a.Ng);
+              splits, a.addend, a.amask, fpart, a.bnshift, a.Ng, (a.owt >> 2) & 1);
     return rows;
   }
   MX_LAUNCH(conv_nhwc_splitk_reduce_k<false>, dim3(grid_for(n4, 2048)), dim3(256), 0, st, scratch, a.out, n4, splits,
-            a.addend, a.amask, nullptr, nullptr, a.Ng);
+            a.addend, a.amask, nullptr, nullptr, a.Ng, (a.owt >> 2) & 1);
   return 0;
 }
 
 // returns the number of BN partial rows the epilogue wrote to a.bnpart (0: none, the BN runs its
 // own statistics pass)
-static int g_conv_wt = 1;  // b256 11,037 -> 11,055 (noise level), PyramidNet-110 neutral
+// bit 0 the tile kernels' bf16 epilogue: ResNet-50 b256 11,037 -> 11,055 (noise level), with the
+// BN stores b32 5,682 -> 5,772 img/s (profiles/r5_nhwcwt/); bit 1 the split-K fp32 partials: b32
+// 5,774 -> 5,816, b256 neutral (profiles/r5_splitwt/); bit 2 the split-K reduce's output
+static int g_conv_wt = 3;
 void nhwc_conv_set_wt(int on) { g_conv_wt = on; }
 static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   a.owt = g_conv_wt;
