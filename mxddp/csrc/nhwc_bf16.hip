@@ -2882,7 +2882,7 @@ static int launch_splitk_reduce(const ConvNArgs& a, float* scratch, int splits, 
 // own statistics pass)
 // bit 0 the tile kernels' bf16 epilogue: ResNet-50 b256 11,037 -> 11,055 (noise level), with the
 // BN stores b32 5,682 -> 5,772 img/s (profiles/r5_nhwcwt/); bit 1 the split-K fp32 partials: b32
-// 5,774 -> 5,816, b256 neutral (profiles/r5_splitwt/); bit 2 the split-K reduce's output
+// 5,774 -> 5,816, b256 neutral (profiles/r5_splitwt/); bit 2 the split-K reduce's output (neutral, off: b_* logs)
 static int g_conv_wt = 3;
 void nhwc_conv_set_wt(int on) { g_conv_wt = on; }
 static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
