@@ -126,12 +126,40 @@ def parse():
     return ap.parse_args()
 
 
+_PHASE = ["start"]
+
+
+def _phase(name: str, rank: int, ws: int):
+    """Where this rank is (world size > 1: also on stderr, so the log of a multi-GPU job that
+    stalls says which phase each rank reached)."""
+    _PHASE[0] = name
+    if ws > 1:
+        print(f"bench.py: rank {rank}/{ws}: {name} (t={time.perf_counter() - _T0:.1f} s)", file=sys.stderr, flush=True)
+
+
+_T0 = time.perf_counter()
+
+
+def _arm_deadline():
+    """Whole-run deadline (MXDDP_BENCH_DEADLINE_S, default 900 s; 0 = off): past it, every
+    thread's Python stack is dumped to stderr and the process exits non-zero (faulthandler's
+    own watchdog thread, no GIL needed), so a rank stuck in a collective ends the job with a
+    traceback naming the call instead of hanging until the driver's limit."""
+    import faulthandler
+
+    t = float(os.environ.get("MXDDP_BENCH_DEADLINE_S", "900"))
+    if t > 0:
+        faulthandler.dump_traceback_later(t, exit=True)
+    return t
+
+
 def main():
     a = parse()
     import torch
 
     from mxddp.parallel import comm as C
 
+    _arm_deadline()
     ws_env = int(os.environ.get("WORLD_SIZE", "1"))
     if a.cpu:
         return _cpu(a)
@@ -144,7 +172,9 @@ def main():
         if ws_env == 1 and a.gpus > 1:
             print(f"bench.py: --gpus {a.gpus} needs a launcher (torch.distributed.run)", file=sys.stderr)
             sys.exit(2)
-    inf = C.init_distributed(use_gpu=True)
+    _phase("rendezvous", int(os.environ.get("RANK", "0")), ws_env)
+    # host collectives of the bench are short: a peer that died shows up within minutes
+    inf = C.init_distributed(use_gpu=True, timeout_s=float(os.environ.get("MXDDP_GLOO_TIMEOUT_S", "600")))
     ab = _apply_ab(a.ab)
     if a.dtype != "fp32":
         if a.impl == "fused":
@@ -153,7 +183,12 @@ def main():
 
         _ops.set_compute_dtype(a.dtype)
     dev = inf.device
+    _phase("rccl init", inf.rank, inf.world_size)
     comm = C.rccl_comm(force=a.force_collectives)
+    if comm is not None and comm.nranks != inf.world_size:
+        raise SystemExit(f"bench.py: rank {inf.rank}: RCCL communicator has {comm.nranks} ranks, the job "
+                         f"{inf.world_size} (--gpus {a.gpus})")
+    _phase("build", inf.rank, inf.world_size)
     B = a.batch
     tr = None  # the fused engine, when one runs
 
@@ -189,6 +224,7 @@ def main():
             tr._set_buckets(a.buckets)
             a.no_autotune = True
         if hasattr(tr, "autotune") and a.graph_mode is None and not a.no_autotune and tr.eng.reducer_active:
+            _phase("autotune", inf.rank, inf.world_size)
             tr.step(1)
             tr.autotune()  # untimed: a few real steps per candidate strategy, before the warm-up
         tr.warm_graphs()
@@ -213,6 +249,7 @@ def main():
             tr._set_buckets(a.buckets)
             a.no_autotune = True
         if a.graph_mode is None and not a.no_autotune and tr.eng.reducer_active:
+            _phase("autotune", inf.rank, inf.world_size)
             tr.step(1)
             tr.autotune()  # untimed: a few real steps per candidate strategy, before the warm-up
         if a.phase_profile:
@@ -226,6 +263,7 @@ def main():
     else:
         run = _layers_or_torch(a, torch, inf, dev, comm, B)
 
+    _phase("warm-up", inf.rank, inf.world_size)
     run(a.warmup)
     # clock ramp: a freshly started process's GPU runs its first ~100 ms of steps slower
     # (profiles/r3_intercept): keep stepping, untimed, until --min-warmup-ms of warm-up ran
@@ -252,6 +290,7 @@ def main():
     align_comm, align_peer = (tr.comm, tr.peer) if tr is not None else (comm, _layers_peer(inf, comm))
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
+    _phase("timed steps", inf.rank, inf.world_size)
     C.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -267,6 +306,25 @@ def main():
     C.barrier()
     dt = C.all_reduce_max(dev_rank)
     dt_host = C.all_reduce_max(t_rank)
+
+    # Multi-GPU diagnosis (after the measurement, outside the timed region): what RCCL reports
+    # for the communicator the steps used, and how much of the step the gradient exchange left
+    # exposed -- the same steps, same launch mode, with the collectives removed (replicas
+    # diverge from here on; nothing is measured after this)
+    diag = {}
+    if comm is not None or inf.world_size > 1:
+        _phase("diagnosis", inf.rank, inf.world_size)
+        used = getattr(tr, "eng_comm", None) or comm
+        diag["rccl"] = C.rccl_diag(used)
+        if tr is not None and hasattr(tr, "compute_only_ms"):
+            dry = tr.compute_only_ms(max(1, min(a.steps, 200)))
+            if dry is not None:
+                dry = C.all_reduce_max(dry)
+                full_ms = dt / a.steps * 1e3
+                diag["compute_only_ms_per_step"] = round(dry, 4)
+                diag["exposed_comm_ms_per_step"] = round(full_ms - dry, 4)
+                if getattr(tr.eng, "coscheduled", False):
+                    diag["exposed_comm_note"] = "co-scheduled exchange runs inside F67 and stays in the compute-only pass"
 
     if a.impl == "fused":
         # per-image averages over every step since the device accumulators were last zeroed
@@ -314,10 +372,12 @@ def main():
                        "graph": _fused_graph(a, tr) or getattr(a, "layers_graph", False),
                        **_fused_config(a, tr), **({"ab": ab} if ab else {})},
             **extra,
+            **diag,
         }
         if C.shared_devices():
             out["shared_gpu_rehearsal"] = True  # several ranks on one GPU: not a scaling number
         print(json.dumps(out), flush=True)
+    _phase("done", inf.rank, inf.world_size)
     C.shutdown()
 
 
@@ -414,14 +474,31 @@ def _replica(a):
 
     run(a.warmup)
     sync_all()
+    # timed like the fused replicas (FusedReplicas.timed_steps): an alignment exchange across the
+    # replicas, then per-device start / end events on each device's current stream (the steps'
+    # work is ordered between them); the slowest replica's event time decides
+    aligned = grp.align()
+    evs = []
+    for d in devices:
+        with torch.cuda.device(d):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(torch.cuda.current_stream(d))
+            evs.append((d, e0, e1))
     t0 = time.perf_counter()
     run(a.steps)
+    for d, _, e1 in evs:
+        with torch.cuda.device(d):
+            e1.record(torch.cuda.current_stream(d))
     sync_all()
-    dt = time.perf_counter() - t0
+    dt_host = time.perf_counter() - t0
+    dt = max(e0.elapsed_time(e1) for _, e0, e1 in evs) * 1e-3
+    grp.close()
     value = B * a.steps / dt
     print(json.dumps({
         "metric": _metric(a.model), "value": round(value, 1), "unit": "images/sec", "n_gpus": a.gpus, "steps": a.steps,
         "warmup": a.warmup, "warmup_steps_run": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4),
+        "host_ms_per_step": round(dt_host / a.steps * 1e3, 4),
+        "timing": f"device events after a {aligned} alignment exchange" if aligned != "none" else "device events",
         "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": a.dtype, "data": _data_desc(spec),
         "config": {"model": a.model, "global_batch": B, "per_rank_batch": a.batch, "seq_len": None,

@@ -317,10 +317,19 @@ PYBIND11_MODULE(_C, m) {
              cfg.ctas = ctas;
              cfg.algo = algo;
              cfg.proto = proto;
-             return new Comm(std::string(uid), rank, ws, dev, cfg);
+             std::string u(uid);
+             py::gil_scoped_release nogil;  // the init waits for the other ranks
+             return new Comm(u, rank, ws, dev, cfg);
            }),
            py::arg("uid"), py::arg("rank"), py::arg("world_size"), py::arg("device"), py::arg("ctas") = 0,
            py::arg("algo") = "", py::arg("proto") = "")
+      .def_static("version", &Comm::version)
+      .def_static("set_init_timeout", &Comm::set_init_timeout)
+      .def_static("init_timeout", &Comm::init_timeout)
+      .def_readonly_static("INIT_TIMEOUT_EXIT", &Comm::kInitTimeoutExit)
+      .def_property_readonly("nranks", &Comm::nranks)
+      .def_property_readonly("hip_device", &Comm::hip_device)
+      .def_property_readonly("ctas", [](const Comm& c) { return c.config().ctas; })
       .def_property_readonly("variant", [](const Comm& c) { return c.config().name(); })
       .def_static("new_unique_id", []() { return py::bytes(Comm::new_unique_id()); })
       .def_static("init_all", [](const std::vector<int>& devs) {
@@ -387,6 +396,9 @@ PYBIND11_MODULE(_C, m) {
         return std::make_pair(q.chunk, q.slice);
       });
 
+  m.def("set_dry_collectives", &reducer_set_dry,
+        "every gradient Reducer skips its collectives (fences kept): the bench's compute-only pass");
+  m.def("dry_collectives", &reducer_dry);
   py::class_<Reducer>(m, "Reducer")
       .def(py::init([](Comm* comm, uintptr_t flat, DType t, const std::vector<std::pair<size_t, size_t>>& buckets,
                        const std::vector<int>& param_bucket, RedOp op, bool timing) {

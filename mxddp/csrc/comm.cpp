@@ -1,7 +1,13 @@
 #include "comm.h"
 
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <thread>
 
 #include "common.h"
 
@@ -75,6 +81,45 @@ struct CommConfigV218 {
   int splitShare;
 };
 
+// Watchdog of one blocking communicator init: if the init has not returned `seconds` after the
+// guard was made, a helper thread names what was being initialised and ends the process with
+// Comm::kInitTimeoutExit (the driver / launcher sees a non-zero exit instead of a hang).
+class InitDeadline {
+ public:
+  InitDeadline(double seconds, std::string what) {
+    if (seconds <= 0) return;
+    th_ = std::thread([this, seconds, what = std::move(what)] {
+      std::unique_lock<std::mutex> lk(mu_);
+      if (cv_.wait_for(lk, std::chrono::duration<double>(seconds), [this] { return done_; })) return;
+      std::fprintf(stderr,
+                   "mxddp: RCCL communicator init did not complete within %.0f s: %s -- a rank never joined the "
+                   "rendezvous or RCCL's bootstrap is wedged; exiting with code %d (MXDDP_RCCL_INIT_TIMEOUT_S sets the "
+                   "deadline)\n",
+                   seconds, what.c_str(), Comm::kInitTimeoutExit);
+      std::fflush(stderr);
+      std::_Exit(Comm::kInitTimeoutExit);
+    });
+  }
+  ~InitDeadline() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      done_ = true;
+    }
+    cv_.notify_all();
+    if (th_.joinable()) th_.join();
+  }
+  InitDeadline(const InitDeadline&) = delete;
+  InitDeadline& operator=(const InitDeadline&) = delete;
+
+ private:
+  std::thread th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool done_ = false;
+};
+
+double g_init_timeout_s = -1.0;  // < 0: not read from the environment yet
+
 // NCCL_ALGO / NCCL_PROTO for the duration of one communicator init
 class ScopedEnv {
  public:
@@ -99,12 +144,42 @@ class ScopedEnv {
 };
 }  // namespace
 
+int Comm::version() {
+  int v = 0;
+  MX_NCCL_CHECK(ncclGetVersion(&v));
+  return v;
+}
+
+void Comm::set_init_timeout(double seconds) { g_init_timeout_s = seconds <= 0 ? 0.0 : seconds; }
+
+double Comm::init_timeout() {
+  if (g_init_timeout_s < 0) {
+    const char* e = std::getenv("MXDDP_RCCL_INIT_TIMEOUT_S");
+    g_init_timeout_s = e ? std::max(0.0, std::atof(e)) : 120.0;
+  }
+  return g_init_timeout_s;
+}
+
+int Comm::nranks() const {
+  int n = 0;
+  MX_NCCL_CHECK(ncclCommCount(comm_, &n));
+  return n;
+}
+
+int Comm::hip_device() const {
+  int d = -1;
+  MX_NCCL_CHECK(ncclCommCuDevice(comm_, &d));
+  return d;
+}
+
 Comm::Comm(const std::string& uid, int rank, int world_size, int device, const CommConfig& cfg)
     : rank_(rank), ws_(world_size), device_(device), cfg_(cfg) {
   MX_CHECK(uid.size() == sizeof(ncclUniqueId), "unique id has wrong size");
   ncclUniqueId id;
   std::memcpy(&id, uid.data(), sizeof(id));
   MX_HIP_CHECK(hipSetDevice(device));
+  InitDeadline deadline(init_timeout(), "rank " + std::to_string(rank) + " of " + std::to_string(world_size) +
+                                            ", device " + std::to_string(device) + ", variant '" + cfg.name() + "'");
   ScopedEnv algo("NCCL_ALGO", cfg.algo), proto("NCCL_PROTO", cfg.proto);
   if (cfg.ctas > 0) {
     // the prefix struct is only valid for a linked RCCL that reads the >= 2.18 config layout (it
@@ -132,7 +207,10 @@ Comm::~Comm() {
 
 std::vector<Comm*> Comm::init_all(const std::vector<int>& devices) {
   std::vector<ncclComm_t> comms(devices.size());
-  MX_NCCL_CHECK(ncclCommInitAll(comms.data(), (int)devices.size(), devices.data()));
+  {
+    InitDeadline deadline(init_timeout(), "ncclCommInitAll over " + std::to_string(devices.size()) + " devices");
+    MX_NCCL_CHECK(ncclCommInitAll(comms.data(), (int)devices.size(), devices.data()));
+  }
   std::vector<Comm*> out;
   for (size_t i = 0; i < devices.size(); ++i) out.push_back(new Comm(comms[i], (int)i, (int)devices.size(), devices[i]));
   return out;

@@ -40,6 +40,18 @@ class Comm {
   Comm& operator=(const Comm&) = delete;
 
   static std::string new_unique_id();
+  // RCCL's version code (ncclGetVersion: major * 10000 + minor * 100 + patch)
+  static int version();
+  // Deadline of every communicator init (ncclCommInitRank / InitRankConfig / InitAll), seconds
+  // (<= 0: none).  Default: MXDDP_RCCL_INIT_TIMEOUT_S, else 120.  An init that has not returned
+  // by then -- a rank that never joined, a wedged bootstrap -- prints the rank, world size,
+  // device and variant on stderr and ends the process with kInitTimeoutExit: the init is
+  // blocking (the mode every later collective and graph capture relies on), so there is no
+  // communicator handle to abort yet; ending the process is what releases the GPU and the
+  // other ranks' rendezvous.
+  static void set_init_timeout(double seconds);
+  static double init_timeout();
+  static constexpr int kInitTimeoutExit = 75;
   // ncclCommInitAll over `devices` in one process (replica / MirroredStrategy mode)
   static std::vector<Comm*> init_all(const std::vector<int>& devices);
 
@@ -56,6 +68,10 @@ class Comm {
 
   static void group_start();
   static void group_end();
+
+  // what RCCL itself says about the communicator (ncclCommCount / ncclCommCuDevice)
+  int nranks() const;
+  int hip_device() const;
 
   int rank() const { return rank_; }
   int world_size() const { return ws_; }

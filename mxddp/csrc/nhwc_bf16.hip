@@ -2892,6 +2892,9 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
   a.fOHW = FastDiv(a.OH * a.OW);
   a.fCa = FastDiv(a.Ca);
   a.fS = FastDiv(a.S);
+  // a half-resolution addend is mapped only by the tile epilogue (epi_vectors), not by the
+  // split-K reduce (full-resolution indices): no partial buffer, so no plan splits the reduction
+  if (a.asub) scratch = nullptr;
   if (c3_eligible(a)) {  // persistent band kernel (forward or data gradient)
     const int rt = c3_band_rows(a.OH, a.OW), nb = a.M / (rt * a.OW);
     // BN rows: one per band (nhwc_conv_bn_rows sized the buffer for them); no backward statistics

@@ -5,6 +5,10 @@
 
 namespace mx {
 
+static bool g_dry = false;
+void reducer_set_dry(bool on) { g_dry = on; }
+bool reducer_dry() { return g_dry; }
+
 Reducer::Reducer(Comm* comm, uintptr_t flat_grad, DType dtype, const std::vector<BucketSpec>& buckets,
                  const std::vector<int>& param_bucket, RedOp op, bool timing)
     : comm_(comm), flat_(reinterpret_cast<char*>(flat_grad)), dtype_(dtype), op_(op), timing_(timing) {
@@ -117,7 +121,9 @@ void Reducer::launch_ready(hipStream_t compute) {
         t = DType::kBF16;
         cast_f32_bf16(reinterpret_cast<const float*>(p), shadow_ + b.offset, (int64_t)n, st);
       }
-      if (via_peer) {
+      if (g_dry) {
+        // compute-only pass: no exchange (the casts above / below still run)
+      } else if (via_peer) {
         peer_->all_reduce(buf, n, t, st, op_);
       } else {
         MX_CHECK(comm_ != nullptr, "reducer: no RCCL communicator for this collective");

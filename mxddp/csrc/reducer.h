@@ -26,6 +26,13 @@
 
 namespace mx {
 
+// Process-wide: every Reducer keeps its fences and stream joins but issues no collective (the
+// bench's compute-only pass after the timed region: exposed comm time = the step with the
+// gradient exchange minus the same captured step without it; replicas diverge, so never train
+// this way).  Graphs captured before a switch keep what they captured.
+void reducer_set_dry(bool on);
+bool reducer_dry();
+
 class Reducer {
  public:
   struct BucketSpec {

@@ -3,8 +3,11 @@
 Reference data paths replaced:
 
 * torchvision CIFAR10 + DataLoader(num_workers=4) + RandomCrop/Flip/Normalize
-  (pytorch/single_gpu.py:51-61) -> CIFAR-10 *binary* batches read with numpy, kept resident
-  in HBM, augmented on device by ``mxddp._C.augment_crop_flip_norm``;
+  (pytorch/single_gpu.py:51-61) -> CIFAR-10 batches kept resident in HBM, augmented on device
+  by ``mxddp._C.augment_crop_flip_norm``.  Both on-disk layouts are read: the *binary* batches
+  (``cifar-10-batches-bin``) with numpy, and the *python* batches torchvision's
+  ``CIFAR10(root, download=True)`` leaves (``cifar-10-batches-py``, or the
+  ``cifar-10-python.tar.gz`` it downloads, read in place) with an allowlisted unpickler;
 * Keras ``mnist.load_data(path=.../mnist.npz)`` (tensorflow2/mnist_single.py:34-47) and the
   Chainer IDX parser with its npz cache (chainer/mnist_helper.py:9-53,
   chainer/mnist_dataset.py:8-38) -> one loader for both formats, vectorised (the reference
@@ -14,14 +17,22 @@ Reference data paths replaced:
 * no dataset on disk (this environment has no network) -> class-conditional synthetic data
   generated on device by a Philox kernel, identical in shape to the real dataset.
 
-Only loaders that execute nothing from the file are used (numpy.load with
-allow_pickle=False, raw byte parsing); pickled CIFAR "python" batches are not read.
+Only loaders that execute nothing from the file are used: numpy.load with allow_pickle=False,
+raw byte parsing, and for the pickled CIFAR "python" batches ``_CifarUnpickler``, which resolves
+only numpy's array / dtype reconstructors (and the latin-1 bytes codec a protocol-2 pickle
+uses) and refuses every other global, so a pickle that names anything else is rejected before
+any of it runs.  ``--data auto`` never swaps in synthetic data for a dataset that is on disk
+but unreadable: it raises.
 """
 from __future__ import annotations
 
 import gzip
+import io
 import math
 import os
+import pickle
+import sys
+import tarfile
 
 import numpy as np
 import torch
@@ -92,6 +103,110 @@ def load_cifar10(root: str, train: bool = True):
         ys.append(raw[:, 0].astype(np.int64))
         xs.append(raw[:, 1:].reshape(-1, 3, 32, 32))
     return np.concatenate(xs), np.concatenate(ys)
+
+
+class UnsafePickleError(pickle.UnpicklingError):
+    """A CIFAR python batch named a global outside the numpy-array allowlist."""
+
+
+def _np_reconstruct(subtype, shape, dtype):
+    if subtype is not np.ndarray:
+        raise UnsafePickleError(f"array reconstruction of {subtype!r} refused (only numpy.ndarray)")
+    return np.ndarray.__new__(np.ndarray, shape, dtype)
+
+
+def _np_frombuffer(buf, dtype, shape, order):
+    return np.frombuffer(buf, dtype=dtype).reshape(shape, order=order).copy()
+
+
+def _latin1_encode(obj, encoding="latin1"):
+    if not isinstance(obj, str) or encoding not in ("latin1", "latin-1"):
+        raise UnsafePickleError("_codecs.encode only for latin-1 str -> bytes")
+    return obj.encode("latin1")
+
+
+# (module, name) -> object; numpy 1.x pickles say numpy.core, numpy 2.x numpy._core
+_PICKLE_ALLOW = {
+    ("numpy", "ndarray"): np.ndarray,
+    ("numpy", "dtype"): np.dtype,
+    ("numpy.core.multiarray", "_reconstruct"): _np_reconstruct,
+    ("numpy._core.multiarray", "_reconstruct"): _np_reconstruct,
+    ("numpy.core.numeric", "_frombuffer"): _np_frombuffer,
+    ("numpy._core.numeric", "_frombuffer"): _np_frombuffer,
+    ("_codecs", "encode"): _latin1_encode,
+}
+
+
+class _CifarUnpickler(pickle.Unpickler):
+    """Resolves only the numpy array / dtype reconstruction globals (a CIFAR batch is a dict of
+    bytes keys, int lists and one uint8 array); any other global raises before it is called."""
+
+    def find_class(self, module, name):
+        obj = _PICKLE_ALLOW.get((module, name))
+        if obj is None:
+            raise UnsafePickleError(f"CIFAR batch pickle names {module}.{name}: refused (not a numpy array global)")
+        return obj
+
+
+def _cifar_batch(f) -> tuple:
+    d = _CifarUnpickler(f, encoding="bytes").load()
+    if not isinstance(d, dict):
+        raise ValueError("CIFAR python batch: not a dict")
+    d = {(k.decode("latin1") if isinstance(k, bytes) else k): v for k, v in d.items()}
+    data, labels = d.get("data"), d.get("labels", d.get("fine_labels"))
+    if not isinstance(data, np.ndarray) or labels is None:
+        raise ValueError("CIFAR python batch: no 'data' array / 'labels' list")
+    x = np.asarray(data, dtype=np.uint8).reshape(-1, 3, 32, 32)
+    y = np.asarray(labels, dtype=np.int64)
+    if len(x) != len(y):
+        raise ValueError("CIFAR python batch: image / label count mismatch")
+    return x, y
+
+
+def load_cifar10_python(root: str, train: bool = True):
+    """(images uint8 [N,3,32,32], labels int64 [N]) from torchvision's layout: the extracted
+    ``cifar-10-batches-py`` directory, or the ``cifar-10-python.tar.gz`` archive (members read
+    in memory, nothing is extracted).  pytorch/distributed_data_parallel.py:85-86"""
+    names = [f"data_batch_{i}" for i in range(1, 6)] if train else ["test_batch"]
+    d = os.path.join(root, "cifar-10-batches-py")
+    if not os.path.isdir(d) and os.path.basename(os.path.normpath(root)) == "cifar-10-batches-py":
+        d = root
+    parts = []
+    if os.path.isdir(d):
+        for n in names:
+            p = os.path.join(d, n)
+            if not os.path.exists(p):
+                raise FileNotFoundError(f"CIFAR-10 python batch {p} not found")
+            with open(p, "rb") as f:
+                parts.append(_cifar_batch(f))
+    else:
+        tgz = os.path.join(root, "cifar-10-python.tar.gz")
+        if not os.path.exists(tgz):
+            raise FileNotFoundError(f"no cifar-10-batches-py / cifar-10-python.tar.gz under {root}")
+        with tarfile.open(tgz, "r:gz") as t:
+            for n in names:
+                m = t.getmember(f"cifar-10-batches-py/{n}")
+                if not m.isfile():
+                    raise ValueError(f"{tgz}: {m.name} is not a regular file")
+                parts.append(_cifar_batch(io.BytesIO(t.extractfile(m).read())))
+    return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
+
+
+def cifar10_layout(root: str) -> str | None:
+    """Which CIFAR-10 layout is under ``root``: 'bin', 'python', or None."""
+    if os.path.isdir(os.path.join(root, "cifar-10-batches-bin")) or os.path.exists(os.path.join(root, "data_batch_1.bin")):
+        return "bin"
+    if (os.path.isdir(os.path.join(root, "cifar-10-batches-py")) or os.path.exists(os.path.join(root, "cifar-10-python.tar.gz"))
+            or os.path.exists(os.path.join(root, "data_batch_1"))):
+        return "python"
+    return None
+
+
+def load_cifar10_any(root: str, train: bool = True):
+    """The binary layout if present, else torchvision's python layout."""
+    if cifar10_layout(root) == "python":
+        return load_cifar10_python(root, train)
+    return load_cifar10(root, train)
 
 
 # ----------------------------------------------------------------------------- sharding
@@ -266,15 +381,24 @@ def build_loader(dataset: str, data: str, root: str, batch_size: int, device, wo
                 x, y = load_mnist(root, train)
                 mean, std, aug = MNIST_MEAN, MNIST_STD, False
             elif dataset == "cifar10":
-                x, y = load_cifar10(root, train)
+                if cifar10_layout(root) is None:
+                    raise FileNotFoundError(f"no CIFAR-10 (binary or python batches) under {root}")
+                try:  # the dataset is on disk: an unreadable or incomplete copy is an error
+                    x, y = load_cifar10_any(root, train)
+                except (FileNotFoundError, KeyError) as e:
+                    raise RuntimeError(f"CIFAR-10 under {root} is incomplete: {e}") from e
                 mean, std, aug = CIFAR_MEAN, CIFAR_STD, train
             else:
                 raise FileNotFoundError(f"no on-disk loader for {dataset}")
             sampler = ShardSampler(len(x), world_size, rank, shuffle=train, seed=seed)
             return TensorLoader(x, y, batch_size, device, sampler, mean, std, augment=aug, seed=seed + rank), "real"
-        except FileNotFoundError:
+        except FileNotFoundError as e:
             if data == "real":
                 raise
+            # nothing of the dataset on disk: synthetic, said on stderr as well as in the log
+            # line (a dataset that IS on disk but unreadable raises above, never falls back)
+            if rank == 0:
+                print(f"mxddp: --data auto: {e}; training on SYNTHETIC {dataset} data", file=sys.stderr, flush=True)
     n = DATASET_SIZES.get(dataset, 50000)
     if steps is None:
         steps = math.ceil(math.ceil(n / world_size) / batch_size)

@@ -122,6 +122,38 @@ class FusedTrainerBase:
             self.eng.replay(n)
             self.steps += n
 
+    def compute_only_ms(self, steps: int) -> float | None:
+        """Device ms per step of this rank's step with every bucket collective removed (the
+        Reducer keeps its fences and joins: ``set_dry_collectives``), launched the way the
+        timed steps were (the same graph mode, recaptured without the collectives).  The bench
+        reports ``exposed comm = timed step - this``.  The replicas' weights diverge during the
+        pass (each applies its local gradient), so it runs only after the measurement; the
+        original launch mode is recaptured afterwards.  None when the step has no collective.
+        The co-scheduled exchange (strategy "co") runs inside a compute kernel and stays."""
+        if not self.eng.reducer_active or steps <= 0:
+            return None
+        C = native()
+        mode = self.eng.graph_mode if self._capture_done else None
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        C.set_dry_collectives(True)
+        try:
+            self.eng.uncapture()
+            if mode:
+                self._capture(mode)
+                self.eng.warm_graphs()
+            self.eng.replay(2)
+            self.eng.sync()
+            ev0.record(self.stream)
+            self.eng.replay(steps)
+            ev1.record(self.stream)
+            self.eng.sync()
+        finally:
+            C.set_dry_collectives(False)
+            self.eng.uncapture()
+            if mode:
+                self._capture(mode)
+        return ev0.elapsed_time(ev1) / steps
+
     def warm_graphs(self) -> int:
         """Launch every captured multi-step graph once (untimed warm-up; they are real training
         steps, counted in self.steps): a replay whose step count needs a graph never launched
@@ -157,7 +189,8 @@ class FusedTrainerBase:
     def _candidate_strategies(self, transport: str) -> list:
         return list(self.STRATEGIES)
 
-    def autotune(self, trial_steps: int = 24, include_graphs: bool | None = None, restore: bool = False) -> dict:
+    def autotune(self, trial_steps: int = 24, include_graphs: bool | None = None, restore: bool = True,
+                 budget_s: float | None = None) -> dict:
         """Pick the fastest launch strategy for the DDP step on THIS machine by timing a few real
         training steps of each (they count as warm-up).  Candidates: gradient transport (RCCL in
         each configured communicator variant, or the direct xGMI peer all-reduce when it
@@ -175,8 +208,18 @@ class FusedTrainerBase:
         RCCL); a strategy that times out or disagrees on ANY rank is marked ``inf`` on every
         rank, the transport is re-synchronised (peer.resync) and the training state restored.  A
         standalone-kernel failure, or a failure while timing, drops the peer transport for the
-        rest of the autotune.  ``restore``: the trial steps are scratch -- the training state and
-        step count are put back afterwards.  Returns {candidate: ms/step}."""
+        rest of the autotune.
+
+        Trial steps are always scratch: validation and failed trials restart from the snapshot
+        taken on entry, and the trainer is put back to that snapshot at the end, so the state
+        after autotune does not depend on which candidates ran or validated.  Every trial step
+        is counted in ``discarded_steps`` (``restore`` is kept for callers; it no longer changes
+        anything).
+
+        Wall-time cap: ``budget_s`` (default MXDDP_AUTOTUNE_BUDGET_S, else 90 s).  Before each
+        candidate the slowest rank's elapsed autotune time is agreed on; once it is over the
+        budget (and at least one candidate has a time) the remaining candidates are skipped on
+        every rank and listed in ``tuned["skipped"]``.  Returns {candidate: ms/step}."""
         from .parallel import comm as pc
 
         if include_graphs is None:
@@ -197,6 +240,11 @@ class FusedTrainerBase:
             cands += [(tr, 0, st) for st in strats]
             if self.use_graph and (include_graphs or tr == "peer"):
                 cands += [(tr, 1, st) for st in strats]
+        if budget_s is None:
+            budget_s = float(os.environ.get("MXDDP_AUTOTUNE_BUDGET_S", "90"))
+        t_start = time.perf_counter()
+        skipped = []
+        trial_run = 0  # trial steps run (all scratch: restored below)
         results = {}
         self._peer_ok = {}   # strategy -> agreed validation verdict (peer transport)
         self._peer_ref = None
@@ -206,6 +254,10 @@ class FusedTrainerBase:
         try:
             for tr, mode, strat in cands:
                 key = (tr, mode, strat)
+                if skipped or (any(v < float("inf") for v in results.values())
+                               and pc.all_reduce_max(time.perf_counter() - t_start) > budget_s):
+                    skipped.append(f"{tr}/{mode}/{strat}")  # every rank agreed on the same point
+                    continue
                 if tr == "peer":
                     if peer_dead:
                         results[key] = float("inf")
@@ -243,6 +295,7 @@ class FusedTrainerBase:
                 self.eng.sync()
                 dt = pc.all_reduce_max(time.perf_counter() - t0)
                 self.steps += 2 + trial_steps
+                trial_run += 2 + trial_steps
                 bad = 1.0 if (tr == "peer" and self.peer.error()) else 0.0
                 if pc.all_reduce_max(bad) > 0:
                     results[key] = float("inf")
@@ -267,12 +320,16 @@ class FusedTrainerBase:
         if best[1]:
             self._capture(best[1])
         self._capture_done = True
-        if restore:
-            self.restore(snap0)
-        else:
-            self.read_metrics(reset=True)
+        self.restore(snap0)
+        self.discarded_steps = getattr(self, "discarded_steps", 0) + trial_run
         self.tuned = {"transport": best[0], "graph_mode": best[1], "buckets": best[2],
-                      "trials_ms": {f"{t}/{m}/{s}": round(v, 4) for (t, m, s), v in results.items()}}
+                      "trials_ms": {f"{t}/{m}/{s}": round(v, 4) for (t, m, s), v in results.items()},
+                      "wall_s": round(time.perf_counter() - t_start, 2), "budget_s": budget_s}
+        if skipped:
+            self.tuned["skipped"] = skipped
+            if pc.info().rank == 0:
+                print(f"mxddp autotune: {budget_s:.0f} s budget reached; {len(skipped)} candidate(s) not timed: "
+                      + ", ".join(skipped), file=sys.stderr, flush=True)
         if self._peer_ok:
             self.tuned["peer_validated"] = dict(self._peer_ok)
         return results

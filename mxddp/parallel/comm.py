@@ -217,6 +217,42 @@ def barrier():
         dist.barrier()
 
 
+def rccl_version_str(code: int | None = None) -> str:
+    """ncclGetVersion's code (major * 10000 + minor * 100 + patch) as 'major.minor.patch'."""
+    if code is None:
+        code = native().Comm.version()
+    return f"{code // 10000}.{code // 100 % 100}.{code % 100}"
+
+
+def rccl_diag(comm) -> dict:
+    """What RCCL itself reports for `comm`, plus every rank's device (collective over the
+    ranks when world_size > 1: a gloo all_gather).  The first multi-GPU run of a job names its
+    own topology in the bench JSON: RCCL version, ncclCommCount (must equal the job's ranks),
+    the variant / pinned channels, and which HIP device each rank drove."""
+    inf = info()
+    C = native()
+    mine = {"rank": inf.rank, "device": inf.device.index if inf.device.type == "cuda" else None,
+            "rccl_device": comm.hip_device if comm is not None else None,
+            "host": os.uname().nodename}
+    if inf.device.type == "cuda":
+        props = torch.cuda.get_device_properties(inf.device)
+        for k in ("pci_bus_id", "pci_device_id", "uuid"):
+            v = getattr(props, k, None)
+            if v is not None:
+                mine[k] = str(v)
+                break
+    ranks = [mine]
+    if dist.is_initialized() and inf.world_size > 1:
+        ranks = [None] * inf.world_size
+        dist.all_gather_object(ranks, mine)
+    out = {"rccl_version": rccl_version_str(C.Comm.version()), "ranks": ranks}
+    if comm is not None:
+        out.update({"rccl_nranks": comm.nranks, "variant": comm.variant,
+                    "channels": comm.ctas if comm.ctas > 0 else "rccl-tuned",
+                    "init_timeout_s": C.Comm.init_timeout()})
+    return out
+
+
 def all_reduce_max(value: float) -> float:
     """Host-side max over ranks (used for timing: the bench takes the slowest rank)."""
     if not dist.is_initialized():

@@ -163,16 +163,6 @@ def resync(pc) -> None:
     _comm.barrier()
 
 
-def resync_local(pcs, devices) -> None:
-    """resync() for in-process replicas (FusedReplicas): one process owns every PeerComm, so
-    synchronising every device before any reset is the barrier."""
-    for d in devices:
-        torch.cuda.synchronize(d)
-    for pc in pcs:
-        if pc is not None:
-            pc.reset_state()
-
-
 def shutdown():
     global _PEER
     _PEER = None

@@ -25,6 +25,9 @@ DataParallel's replicate-every-step:
 from __future__ import annotations
 
 import copy
+import os
+import warnings
+import weakref
 
 import torch
 import torch.nn as nn
@@ -35,6 +38,17 @@ from .flat import FlatParams, flatten_buffers
 
 
 class ReplicaGroup:
+    """Replicas of ``model`` on ``devices`` kept in lockstep.  Several replicas may share one
+    device (a functional rehearsal of an N-GPU node on one GPU): their exchanges are the peer
+    transport, and each replica's exchange kernel spins on the GPU until every peer arrives, so
+    each replica's streams (exchange, capture and -- graph mode -- the reducer's side stream)
+    must land on hardware queues of their own, or a replica queued behind another's spinning
+    exchange stalls until the peer timeout.  HIP gives a process GPU_MAX_HW_QUEUES queues (4 by
+    default); a shared-device group that needs more warns at construction (raise the variable
+    before the process first touches the GPU)."""
+
+    STREAMS_PER_REPLICA = 3  # exchange stream, capture stream, reducer side stream (graph mode)
+
     def __init__(self, model: nn.Module, devices: list[torch.device], make_optimizer, broadcast_buffers: bool = True,
                  use_graph: bool = False, peer_blocks: int = 64, bucket_cap_mb: float = 25.0):
         self.devices = [torch.device(d) for d in devices]
@@ -56,6 +70,16 @@ class ReplicaGroup:
         # several replicas on ONE device (a rehearsal of an N-GPU node on one GPU): RCCL cannot
         # span them, so every exchange is the in-process peer transport
         self.shared = len(set(self.devices)) < self.n
+        self._hook_handles = []
+        self._align_buf = None
+        if self.shared:
+            need = self.n * (self.STREAMS_PER_REPLICA if self.use_graph else 1) + 1
+            have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+            if need > have:
+                warnings.warn(f"ReplicaGroup: {self.n} replicas share a device and need ~{need} hardware queues "
+                              f"(GPU_MAX_HW_QUEUES={have}): a replica's exchange may wait behind another's until "
+                              "the peer timeout; set GPU_MAX_HW_QUEUES >= that before the GPU is first used",
+                              RuntimeWarning, stacklevel=2)
         if self.n > 1:
             if any(d.type != "cuda" for d in self.devices):
                 raise ValueError("replica mode across several devices needs GPUs")
@@ -107,15 +131,46 @@ class ReplicaGroup:
                 r.comm_stream()  # its side stream exists before the capture that first uses it
             self.reducers.append(r)
             for j, p in enumerate(f.params):
-                p.register_post_accumulate_grad_hook(self._hook(i, j))
+                self._hook_handles.append(p.register_post_accumulate_grad_hook(self._hook(i, j)))
 
     def _hook(self, i: int, j: int):
+        # the hooks live on the parameters (replica 0's are the caller's model): they hold the
+        # group only weakly, so the group, its reducers and peer transports can be collected
+        ref = weakref.ref(self)
+
         def hook(p):
-            if self._capturing == i:
+            g = ref()
+            if g is not None and g._capturing == i:
                 # fenced against the capture stream the step's backward kernels run on (the hook
                 # runs on an autograd device thread, whose current stream need not be that one)
-                self.reducers[i].mark_ready(j, self._cap_stream)
+                g.reducers[i].mark_ready(j, g._cap_stream)
         return hook
+
+    def close(self):
+        """Remove the gradient hooks from the replicas' parameters (the caller's model keeps no
+        reference to this group afterwards)."""
+        for h in self._hook_handles:
+            h.remove()
+        self._hook_handles = []
+
+    def align(self) -> str:
+        """Device-side start line of a timed region (bench.py, config 4): one tiny all-reduce over
+        the replicas on every device's current stream, so the devices leave it together; events
+        recorded right after it on each device's current stream are a common start.  Returns
+        the transport ("peer", "rccl" or "none")."""
+        if self.n == 1:
+            return "none"
+        C = native()
+        if self._align_buf is None:
+            self._align_buf = [torch.zeros(64, device=d) for d in self.devices]
+        if self.peers is not None:
+            self._peer_each(self._align_buf, C.RedOp.sum)
+            return "peer"
+        C.Comm.group_start()
+        for i, (c, t) in enumerate(zip(self.comms, self._align_buf)):
+            c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), C.DType.f32, C.RedOp.sum, self._stream(i))
+        C.Comm.group_end()
+        return "rccl"
 
     # ------------------------------------------------------------------ collectives
     def _stream(self, i):
@@ -271,10 +326,11 @@ class ReplicaGroup:
         # EVERY replica's graph is launched before the host waits on any of them, each on its
         # replica's own stream: each graph's gradient exchange waits on the GPUs for the others
         if self.n == 1:
-            self._xs[0].copy_(xs[0], non_blocking=True)
-            self._ys[0].copy_(ys[0], non_blocking=True)
-            self.optimizers[0]._sync_lr()
-            self._graphs[0].replay()
+            with torch.cuda.device(self.devices[0]):
+                self._xs[0].copy_(xs[0], non_blocking=True)
+                self._ys[0].copy_(ys[0], non_blocking=True)
+                self.optimizers[0]._sync_lr()
+                self._graphs[0].replay()
             return
         for i, d in enumerate(self.devices):
             rs = self._rs[i]

@@ -95,6 +95,7 @@ for step in "$@"; do
     pmc_rn) pmc pmc_rn --model resnet50 --dtype bf16 --batch 256 --steps 1 --warmup 1 --no-graph --min-warmup-ms 0 ;;
     pyr) run pyr 300 python bench.py --model pyramidnet110 --steps 20 --warmup 3 ;;
     pyr_stock) run pyr_stock 300 python bench.py --model pyramidnet110 --steps 20 --warmup 3 --impl torch ;;
+    pmc_pyr) pmc pmc_pyr --model pyramidnet110 --steps 1 --warmup 1 --no-graph --min-warmup-ms 0 ;;
     prof_pyr) prof prof_pyr 5 --model pyramidnet110 --steps 5 --warmup 2 --min-warmup-ms 0 ;;
     prof_pyr_stock) prof prof_pyr_stock 5 --model pyramidnet110 --steps 5 --warmup 2 --min-warmup-ms 0 --impl torch ;;
     ws2) ws ws2 2 --steps 1000 --warmup 50 ;;

@@ -210,3 +210,26 @@ def test_rccl_variant_that_fails_to_initialise_is_dropped(monkeypatch, capsys):
     cands = tr._rccl_candidates()
     assert list(cands) == ["default", "Ring:c28"] and cands["Ring:c28"] is good
     assert "RCCL variant 'Ring:c7' dropped" in capsys.readouterr().err
+
+
+def test_autotune_restores_without_restore_flag(monkeypatch):
+    """Trial steps are scratch whatever ``restore`` says: the state after autotune does not depend
+    on which candidates ran (restore=False used to keep some candidates' steps)."""
+    _pc_stub(monkeypatch)
+    tr = _make(wrong={"co"})
+    p0 = tr.params.clone()
+    tr.autotune(trial_steps=2, restore=False)
+    assert torch.equal(tr.params, p0) and tr.steps == 0 and tr.discarded_steps > 0
+
+
+def test_autotune_wall_time_budget_skips_the_rest(monkeypatch, capsys):
+    """Once the (agreed) elapsed time passes the budget, the remaining candidates are skipped on
+    every rank and listed; the best of those timed is chosen."""
+    _pc_stub(monkeypatch)
+    tr = _make()
+    res = tr.autotune(trial_steps=2, budget_s=0.0)
+    timed = [k for k, v in res.items() if v < float("inf")]
+    assert len(timed) == 1 and tr.tuned["skipped"]  # the first candidate always runs
+    assert len(res) + len(tr.tuned["skipped"]) > 1
+    assert "budget reached" in capsys.readouterr().err
+    assert f"{timed[0][0]}/{timed[0][1]}/{timed[0][2]}" == f"{tr.tuned['transport']}/{tr.tuned['graph_mode']}/{tr.tuned['buckets']}"

@@ -103,3 +103,96 @@ def test_synthetic_heldout_set_shares_training_templates():
 def test_build_loader_auto_falls_back_to_synthetic(tmp_path):
     ld, kind = build_loader("mnist", "auto", str(tmp_path), 16, "cpu", 2, 0, 1, (1, 28, 28), 10)
     assert kind == "synthetic" and len(ld) == 30000 // 16 + 1 - (1 if 30000 % 16 == 0 else 0)
+
+
+def _write_cifar_py(d, n_per=4, extra=None, protocol=2):
+    """torchvision's cifar-10-batches-py layout: pickled dicts with bytes keys (the Python-2 files
+    load with encoding='bytes'), a uint8 [n, 3072] 'data' array and a 'labels' int list."""
+    import pickle
+
+    d.mkdir(parents=True, exist_ok=True)
+    for name, v in [(f"data_batch_{i}", i) for i in range(1, 6)] + [("test_batch", 9)]:
+        data = np.full((n_per, 3072), v, dtype=np.uint8)
+        data[:, 1024:2048] = 100 + v  # channel 1
+        b = {b"batch_label": b"x", b"labels": [(v + j) % 10 for j in range(n_per)], b"data": data,
+             b"filenames": [b"f%d.png" % j for j in range(n_per)]}
+        if extra is not None and name == "data_batch_3":
+            b[b"extra"] = extra
+        with open(d / name, "wb") as f:
+            pickle.dump(b, f, protocol=protocol)
+
+
+class _NamesAnotherGlobal:
+    """Pickles as a call of collections.OrderedDict: harmless, but not a numpy array global."""
+
+    def __reduce__(self):
+        import collections
+
+        return (collections.OrderedDict, ())
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("protocol", [2, 4, 5])
+def test_cifar_python_layout_accepted(tmp_path, protocol):
+    from mxddp.data import load_cifar10_python
+
+    _write_cifar_py(tmp_path / "cifar-10-batches-py", protocol=protocol)
+    x, y = load_cifar10_python(str(tmp_path), train=True)
+    assert x.shape == (20, 3, 32, 32) and x.dtype == np.uint8
+    assert x[0, 0, 0, 0] == 1 and x[0, 1, 5, 5] == 101 and x[4, 0, 0, 0] == 2
+    assert y.tolist()[:5] == [1, 2, 3, 4, 2]
+    xt, yt = load_cifar10_python(str(tmp_path), train=False)
+    assert xt.shape == (4, 3, 32, 32) and yt.tolist() == [9, 0, 1, 2]
+    # --data auto reads it (never synthetic when the reference's layout is on disk)
+    ld, kind = build_loader("cifar10", "auto", str(tmp_path), 8, "cpu", 1, 0, 1, (3, 32, 32), 10)
+    assert kind == "real" and len(ld) == 3
+
+
+def test_cifar_python_archive_read_in_place(tmp_path):
+    """The cifar-10-python.tar.gz torchvision downloads, read without extracting."""
+    import tarfile
+
+    from mxddp.data import load_cifar10_python
+
+    _write_cifar_py(tmp_path / "src" / "cifar-10-batches-py")
+    root = tmp_path / "root"
+    root.mkdir()
+    with tarfile.open(root / "cifar-10-python.tar.gz", "w:gz") as t:
+        t.add(tmp_path / "src" / "cifar-10-batches-py", arcname="cifar-10-batches-py")
+    x, y = load_cifar10_python(str(root), train=True)
+    assert x.shape == (20, 3, 32, 32) and not (root / "cifar-10-batches-py").exists()
+
+
+def test_cifar_python_extra_global_refused(tmp_path):
+    """A batch whose pickle names any global beyond numpy's array reconstructors is refused before
+    that global is called, and --data auto raises instead of training on synthetic data."""
+    from mxddp.data import UnsafePickleError, load_cifar10_python
+
+    _write_cifar_py(tmp_path / "cifar-10-batches-py", extra=_NamesAnotherGlobal())
+    with pytest.raises(UnsafePickleError, match="collections.OrderedDict"):
+        load_cifar10_python(str(tmp_path), train=True)
+    with pytest.raises(UnsafePickleError):
+        build_loader("cifar10", "auto", str(tmp_path), 8, "cpu", 1, 0, 1, (3, 32, 32), 10)
+
+
+def test_cifar_python_array_subclass_refused(tmp_path):
+    """numpy's _reconstruct is admitted only for numpy.ndarray itself."""
+    import pickle
+
+    from mxddp.data import UnsafePickleError, load_cifar10_python
+
+    d = tmp_path / "cifar-10-batches-py"
+    _write_cifar_py(d)
+    with open(d / "data_batch_1", "wb") as f:
+        pickle.dump({b"data": np.ma.masked_array(np.zeros((1, 3072), np.uint8)), b"labels": [0]}, f, protocol=2)
+    with pytest.raises(UnsafePickleError):
+        load_cifar10_python(str(tmp_path), train=True)
+
+
+def test_cifar_layout_present_but_incomplete_is_an_error(tmp_path):
+    _write_cifar_py(tmp_path / "cifar-10-batches-py")
+    os.remove(tmp_path / "cifar-10-batches-py" / "data_batch_4")
+    with pytest.raises(RuntimeError, match="incomplete"):
+        build_loader("cifar10", "auto", str(tmp_path), 8, "cpu", 1, 0, 1, (3, 32, 32), 10)

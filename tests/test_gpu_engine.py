@@ -207,8 +207,9 @@ def test_fused_engine_autotune_keeps_training_exact(cuda):
     a.step(1)
     res = a.autotune(trial_steps=4, include_graphs=True)
     assert len(res) == 6 and a.tuned is not None  # {eager, graph} x {ovl, inl, one}
+    assert a.steps == 1 and a.discarded_steps == 6 * (2 + 4)  # the trial steps are scratch
     a.step(10)
-    b.step(1 + 6 * (2 + 4) + 10)
+    b.step(1 + 10)
     assert a.steps == b.steps
     # same device-side data stream and update rule, every cross-block sum order-independent
     # (int64 fixed point) or in a fixed order: the two launch paths train bit for bit alike

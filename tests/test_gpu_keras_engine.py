@@ -119,8 +119,9 @@ def test_fused_keras_autotune_ws1(cuda):
     a.step(1)
     res = a.autotune(trial_steps=3, include_graphs=True)
     assert len(res) == 2 and a.tuned["buckets"] == "one"  # {eager, graph} x {one}
+    assert a.steps == 1  # the trial steps are scratch (restored)
     a.step(5)
-    b.step(1 + 2 * (2 + 3) + 5)
+    b.step(1 + 5)
     assert a.steps == b.steps and a.adam_steps == b.adam_steps
     for k, v in a.state_dict().items():
         assert torch.equal(v, b.state_dict()[k]), k

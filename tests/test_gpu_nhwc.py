@@ -628,7 +628,10 @@ def test_lazy_identity_join_equals_materialised(cuda):
         assert _nrel(b, a) < 1e-2
 
 
-@pytest.mark.parametrize("inp,planes,hw", [(256, 128, 28), (512, 256, 14), (64, 64, 10)])
+@pytest.mark.parametrize("inp,planes,hw", [(256, 128, 28), (512, 256, 14), (64, 64, 10),
+                                            # first 1x1's reduction of 16 k-tiles over 256 pixels:
+                                            # a split-K plan unless the half-resolution join forbids it
+                                            (512, 1024, 8)])
 def test_half_resolution_projection_gradient(cuda, inp, planes, hw):
     """Stride-2 1x1 projection shortcut: its input gradient computed on the output grid and added
     at even (h, w) in the first conv's epilogue (GradJoin.sub2) == the full-resolution parity-class
