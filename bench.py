@@ -39,18 +39,11 @@ MODEL_METRIC = {
 
 # --ab KEY=VALUE: measured-once kernel choices kept switchable for A/B runs (docs/BENCHMARKS.md)
 AB_SWITCHES = {
+    "gk2": ("nhwc_conv_set_gk2", "bf16 NHWC convs, two-stage 128 x 128 tiles: 0 = 8 waves of 64 x 32, 1 = 64 x 64 wave "
+                                 "tiles in two k-groups on 16x16x32 MFMAs, 2 = the same on 32x32x16"),
     "conv_tile256": ("nhwc_conv_set_glds256", "bf16 NHWC convs, 256x256-tile LDS-DMA kernel on big layers (0/1)"),
     "glds_deep": ("nhwc_conv_set_glds_deep", "bf16 NHWC convs, 128 x 128 two-stage tiles on >= 4 k-tile layers (0 off, 1 >= 192 tiles, 2 all, 3 under-filled only)"),
-    "glds_par": ("nhwc_conv_set_glds_par", "bf16 NHWC stride-2 data gradients on the two-stage LDS-DMA tiles (1) or the generic kernel (0)"),
-    "glds_short": ("nhwc_conv_set_glds_short", "bf16 NHWC convs, two-stage 128-pixel variant on short reductions (0/1)"),
-    "conv_wt": ("nhwc_conv_set_wt", "bf16 NHWC conv outputs stored write-through, bit mask: 1 epilogue, 2 split-K partials, 4 split-K reduce (default 3)"),
-    "bn_wt": ("nhwc_bn_set_wt", "bf16 NHWC BN apply passes, outputs stored write-through (0/1; default 1)"),
-    "bn_grid_cap": ("nhwc_bn_set_grid_cap", "bf16 NHWC BN apply kernels, most blocks"),
-    "split_blocks": ("nhwc_conv_set_split_blocks", "bf16 NHWC generic conv, split-K only below this many blocks"),
-    "wgrad_target": ("nhwc_wgrad_set_target", "bf16 NHWC weight gradient, blocks aimed at when splitting pixels"),
-    "wgrad_w8": ("nhwc_wgrad_set_waves8", "bf16 NHWC weight gradient, 128-row tiles over 8 waves (1) or 4 (0)"),
     "wgrad_tile256": ("nhwc_wgrad_set_tile256", "bf16 NHWC weight gradient, 256 x 256 tiles (1) or 128 x 128 (0)"),
-    "wt_stores": ("mnist_set_wt_stores", "fused MNIST, L2 write-through bulk stores mask (1 F5, 2 F2, 4 F6W)"),
 }
 
 

@@ -116,6 +116,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_conv_set_glds_short", &nhwc_conv_set_glds_short);
   m.def("nhwc_conv_set_glds_deep", &nhwc_conv_set_glds_deep);
   m.def("nhwc_conv_set_glds_par", &nhwc_conv_set_glds_par);
+  m.def("nhwc_conv_set_gk2", &nhwc_conv_set_gk2);
   m.def("nhwc_wgrad_set_waves8", &nhwc_wgrad_set_waves8);
   m.def("nhwc_bn_set_grid_cap", &nhwc_bn_set_grid_cap);
   m.def("nhwc_bn_set_wt", &nhwc_bn_set_wt);

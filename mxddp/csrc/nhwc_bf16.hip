@@ -580,6 +580,89 @@ __device__ __forceinline__ void glds16(const void* src, void* lds) {
   __builtin_amdgcn_global_load_lds(src, (lds_void_t*)lds, 16, 0, 0);
 }
 
+// Epilogue shared by the two-/three-stage LDS-DMA kernels once the bf16 C tile ([TN pixels][TM
+// channels], pitch TM + 8) is staged at the start of smem: residual addend, 16-byte stores and the
+// backward (kBst: reduction slots fit after the C tile) or forward (STATS) BN statistics.
+template <int TM, int TN, bool STATS, bool kBst, int kSmem, typename PF>
+__device__ __forceinline__ void glds_tail(const ConvNArgs& a, char* smem, int px0, int ch0, int Mc, PF pfull) {
+  const int tid = threadIdx.x;
+  constexpr int CP = TM + 8;
+  const bf16* Cs = reinterpret_cast<const bf16*>(smem);
+  constexpr int VPR = TM / 8;
+  const bool bst = kBst && !STATS && a.bx != nullptr;
+  float s1[8], s2[8], mean8[8], sc8[8], sh8[8];
+  if (bst) {
+    const int ch = min(ch0 + 8 * (tid % VPR), a.Ng - 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] = s2[e] = 0.f;
+      mean8[e] = a.bmean[ch + e];
+      sc8[e] = a.bfcoef ? a.bfcoef[2 * (ch + e)] : 0.f;
+      sh8[e] = a.bfcoef ? a.bfcoef[2 * (ch + e) + 1] : 0.f;
+    }
+  }
+  epi_vectors<512, TN * VPR / 512, VPR>(a, Cs, CP, px0, ch0, Mc, pfull, bst, mean8, sc8, sh8, s1, s2);
+  if constexpr (kBst) {
+    if (bst) {
+      // reduction slots after the C tile in the (idle) stage buffers
+      float* bred = reinterpret_cast<float*>(smem + ((TN * CP * 2 + 255) & ~255));
+      // partial row = (parity class, pixel tile)
+      bn_bwd_flush<512, VPR>(a, bred, s1, s2, (int)blockIdx.z * ((Mc + TN - 1) / TN) + px0 / TN, ch0);
+    }
+  }
+  if constexpr (STATS) {  // BN statistics of the stored (bf16) tile: 512 / TM threads per channel
+    constexpr int TPC = 512 / TM, RPT = TN / TPC, U = 8;
+    static_assert(RPT % U == 0, "rows per thread");
+    // reduction slots after the C tile in the (idle) stage buffers
+    float* bred = reinterpret_cast<float*>(smem + ((TN * CP * 2 + 255) & ~255));
+    static_assert(((TN * CP * 2 + 255) & ~255) + 2 * 512 * 4 <= kSmem, "BN reduction slots must fit");
+    const int c = tid % TM, q = tid / TM, ch = ch0 + c;
+    const float K = (a.bnshift && ch < a.Ng) ? a.bnshift[ch] : 0.f;
+    const int rows = min(TN, a.M - px0);
+    const uint16_t* col = reinterpret_cast<const uint16_t*>(Cs) + c;
+    float s1[U], s2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) s1[u] = s2[u] = 0.f;
+    if (rows == TN) {  // full tile: U independent rows per iteration (loads in flight together)
+      for (int r0 = q * RPT; r0 < (q + 1) * RPT; r0 += U) {
+        uint16_t h[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) h[u] = col[(r0 + u) * CP];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float d = bf2f(h[u]) - K;
+          s1[u] += d;
+          s2[u] = fmaf(d, d, s2[u]);
+        }
+      }
+    } else {
+      for (int r = q * RPT; r < min(rows, (q + 1) * RPT); ++r) {
+        const float d = bf2f(col[r * CP]) - K;
+        s1[0] += d;
+        s2[0] = fmaf(d, d, s2[0]);
+      }
+    }
+#pragma unroll
+    for (int u = 1; u < U; ++u) {
+      s1[0] += s1[u];
+      s2[0] += s2[u];
+    }
+    bred[tid] = s1[0];
+    bred[512 + tid] = s2[0];
+    __syncthreads();
+    if (q == 0 && ch < a.Ng) {
+      float t1 = s1[0], t2 = s2[0];
+      for (int k = 1; k < TPC; ++k) {
+        t1 += bred[tid + k * TM];
+        t2 += bred[512 + tid + k * TM];
+      }
+      float* dst = a.bnpart + (size_t)(px0 / TN) * 2 * a.Ng + 2 * ch;
+      dst[0] = t1;
+      dst[1] = t2;
+    }
+  }
+}
+
 // STATS: the forward BN-statistics epilogue (bnpart / bnshift); the backward BN-statistics
 // epilogue of a data gradient runs whenever a.bx is set (ConvNArgs::bx).
 // TN = 128, NS = 2 (the short-reduction variant, 1x1 layers with <= 2 k-tiles): 64 KB of LDS
@@ -766,82 +849,241 @@ __global__ __launch_bounds__(512, TN == 128 ? 2 : 1) void conv_nhwc_glds_kernel(
     }
   }
   __syncthreads();
-  constexpr int VPR = TM / 8;
-  // backward BN statistics (fixed vector per thread): only where the reduction slots fit after
-  // the C tile (not the two-stage variant; the host does not select it for them)
-  constexpr bool kBst = kBstB <= kSmem;
-  const bool bst = kBst && !STATS && a.bx != nullptr;
-  float s1[8], s2[8], mean8[8], sc8[8], sh8[8];
-  if (bst) {
-    const int ch = min(ch0 + 8 * (tid % VPR), a.Ng - 8);
+  glds_tail<TM, TN, STATS, kBstB <= kSmem, kSmem>(a, smem, px0, ch0, Mc, pfull);
+}
+
+// ------------------------------------------------------------------------------------------
+// Two-stage 128 x 128 LDS-DMA tile with 64 x 64 wave tiles (gk2).  The 8 waves form two k-groups of
+// four (kg = wave >> 2): each stage's 64-k tile is split into its two 32-k halves and group kg
+// computes half kg over the whole 128 x 128 tile (4 waves x 64 x 64).  Per MFMA that is half an
+// LDS operand read (ds_read_b128) against three quarters for the 8-wave 64 x 32 wave tiles of
+// conv_nhwc_glds_kernel<128, *, 128, 2> -- the same MFMAs, stages and 16 waves per CU; the
+// groups' fp32 tiles are summed through LDS after the k loop.  MF32: v_mfma_f32_32x32x16_bf16
+// (2 x 2 tiles of 32 x 32 per wave) instead of v_mfma_f32_16x16x32_bf16 (4 x 4 of 16 x 16).
+// LDS image: rows of 64 k (128 B); the 16-byte chunk a lane fills is XOR-swizzled by (row >> 1) & 7
+// on the SOURCE address, which makes both MFMA shapes' ds_read_b128 fragment reads conflict-free
+// (16-lane groups {0-3,12-15,20-27}, ...: rows r and r + 8 differ in bit 0 of r >> 3 only through
+// the 128-B half of the 256-B bank row; scripts/ldsbank/bank.py enumerates it).
+__device__ __forceinline__ int gk2_swz(int row) { return (row >> 1) & 7; }
+
+template <bool STATS, bool MF32>
+__global__ __launch_bounds__(512, 2) void conv_nhwc_gk2_kernel(ConvNArgs a) {
+  constexpr int TM = 128, TN = 128, BK = 64, NS = 2;
+  constexpr int AB = TM * 128, SB = AB + TN * 128;
+  constexpr int NA = TM / 64, NB = TN / 64;
+  constexpr int kCB = ((TN * (TM + 8) * 2 + 255) & ~255), kBstB = kCB + 16 * 512 * 4;
+  constexpr int kRed = 4 * 16 * 64 * 16;  // k-group 1's fp32 tile: 4 waves x 16 float4 x 64 lanes
+  constexpr int kSmem0 = NS * SB > kBstB ? NS * SB : kBstB;
+  constexpr int kSmem = kSmem0 > kRed ? kSmem0 : kRed;
+  __shared__ __attribute__((aligned(1024))) char smem[kSmem];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kg = wave >> 2, wq = wave & 3, wm = wq >> 1, wn = wq & 1;
+  const int tiles_m = (a.Ng + TM - 1) / TM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ch0 = (bid % tiles_m) * TM, px0 = (bid / tiles_m) * TN;
+  const char* zero = reinterpret_cast<const char*>(&g_zero16);
+
+  const int pch = lane & 7;  // physical chunk this lane fills
+  uint32_t abase[NA];
+  bool aok[NA];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      s1[e] = s2[e] = 0.f;
-      mean8[e] = a.bmean[ch + e];
-      sc8[e] = a.bfcoef ? a.bfcoef[2 * (ch + e)] : 0.f;
-      sh8[e] = a.bfcoef ? a.bfcoef[2 * (ch + e) + 1] : 0.f;
+  for (int j = 0; j < NA; ++j) {
+    const int arow = ((wave * NA + j) * 64 + lane) >> 3;
+    aok[j] = ch0 + arow < a.Ng;
+    abase[j] = 2u * ((uint32_t)(ch0 + (aok[j] ? arow : 0)) * a.Kg + 8 * (pch ^ gk2_swz(arow)));
+  }
+  const int pca = a.par ? (int)blockIdx.z >> 1 : 0, pcb = a.par ? (int)blockIdx.z & 1 : 0;
+  const int r0 = a.par ? (pca + a.ph) & 1 : 0, s0 = a.par ? (pcb + a.pw) & 1 : 0;
+  const int nS = a.par ? (a.S - s0 + 1) >> 1 : a.S;
+  const int Kgc = a.par ? ((a.R - r0 + 1) >> 1) * nS * a.Ca : a.Kg;
+  const int Mc = a.par ? a.M >> 2 : a.M;
+  auto pfull = [&](int m) -> int {
+    if (!a.par) return m;
+    const int n = (int)a.fHWc.div((uint32_t)m), rem = m - n * a.Hc * a.Wc;
+    const int i = (int)a.fWc.div((uint32_t)rem), j = rem - i * a.Wc;
+    return (n * a.OH + 2 * i + pca) * a.OW + 2 * j + pcb;
+  };
+  uint32_t pbase[NB];
+  int ihb[NB], iwb[NB], lchb[NB];
+  bool pok[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int row = ((wave * NB + j) * 64 + lane) >> 3;
+    const int m = px0 + row;
+    pok[j] = m < Mc;
+    const int mm = pok[j] ? m : 0;
+    int n, oh, ow;
+    if (a.par) {
+      n = (int)a.fHWc.div((uint32_t)mm);
+      const int rem = mm - n * a.Hc * a.Wc, i = (int)a.fWc.div((uint32_t)rem);
+      oh = 2 * i + pca;
+      ow = 2 * (rem - i * a.Wc) + pcb;
+    } else {
+      n = (int)a.fOHW.div((uint32_t)mm);
+      const int rem = mm - n * a.OH * a.OW;
+      oh = (int)a.fOW.div((uint32_t)rem);
+      ow = rem - oh * a.OW;
+    }
+    pbase[j] = 2u * ((uint32_t)n * a.IH * a.IW * a.Ca);
+    ihb[j] = a.dgrad ? oh + a.ph : oh * a.sh - a.ph;
+    iwb[j] = a.dgrad ? ow + a.pw : ow * a.sw - a.pw;
+    lchb[j] = 8 * (pch ^ gk2_swz(row));
+  }
+
+  auto issue = [&](int t, int buf) {
+    const int k0 = t * BK;
+    const int rs = (int)a.fCa.div((uint32_t)k0), c0 = k0 - rs * a.Ca;  // uniform: one tap per stage
+    int r, s, kw = k0;
+    if (a.par) {
+      const int ri = rs / nS, si = rs - ri * nS;
+      r = r0 + 2 * ri;
+      s = s0 + 2 * si;
+      kw = (r * a.S + s) * a.Ca + c0;
+    } else {
+      r = (int)a.fS.div((uint32_t)rs);
+      s = rs - r * a.S;
+    }
+    char* st = smem + buf * SB;
+    const char* wb = reinterpret_cast<const char*>(a.wt) + 2u * (uint32_t)kw;
+#pragma unroll
+    for (int j = 0; j < NA; ++j)
+      glds16(aok[j] ? (const void*)(wb + abase[j]) : (const void*)zero, st + (wave * NA + j) * 1024);
+    const char* xb = reinterpret_cast<const char*>(a.act) + 2u * (uint32_t)c0;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      int ih, iw;
+      bool ok = pok[j];
+      if (!a.dgrad) {
+        ih = ihb[j] + r;
+        iw = iwb[j] + s;
+      } else {
+        const int th = ihb[j] - r, tw = iwb[j] - s;
+        ih = a.sh == 1 ? th : th >> 1;
+        iw = a.sw == 1 ? tw : tw >> 1;
+        ok = ok && th >= 0 && tw >= 0 && ih * a.sh == th && iw * a.sw == tw;
+      }
+      ok = ok && (unsigned)ih < (unsigned)a.IH && (unsigned)iw < (unsigned)a.IW;
+      const char* src = xb + pbase[j] + 2u * (uint32_t)((ih * a.IW + iw) * a.Ca + lchb[j]);
+      glds16(ok ? (const void*)src : (const void*)zero, st + AB + (wave * NB + j) * 1024);
+    }
+  };
+
+  // accumulators: 64 floats per lane either way
+  constexpr int NI = MF32 ? 2 : 4;
+  typedef typename std::conditional<MF32, f32x16, f32x4>::type accv;
+  accv acc[NI][NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < (MF32 ? 16 : 4); ++e) acc[i][j][e] = 0.f;
+
+  const int nt = Kgc / BK;
+  if (nt > 0) issue(0, 0);
+  for (int t = 0; t < nt; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage t landed for every wave; stage t-1's buffer is free
+    if (t + 1 < nt) issue(t + 1, (t + 1) % NS);
+    const char* sA = smem + (t % NS) * SB;
+    const char* sB = sA + AB;
+    if constexpr (!MF32) {
+      const int lch = 4 * kg + (lane >> 4);
+      bf16x8 av[4], bv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + 16 * i + (lane & 15);
+        av[i] = *reinterpret_cast<const bf16x8*>(sA + row * 128 + 16 * (lch ^ gk2_swz(row)));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = wn * 64 + 16 * j + (lane & 15);
+        bv[j] = *reinterpret_cast<const bf16x8*>(sB + row * 128 + 16 * (lch ^ gk2_swz(row)));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int lch = 4 * kg + 2 * kk + (lane >> 5);
+        bf16x8 av[2], bv[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int row = wm * 64 + 32 * i + (lane & 31);
+          av[i] = *reinterpret_cast<const bf16x8*>(sA + row * 128 + 16 * (lch ^ gk2_swz(row)));
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int row = wn * 64 + 32 * j + (lane & 31);
+          bv[j] = *reinterpret_cast<const bf16x8*>(sB + row * 128 + 16 * (lch ^ gk2_swz(row)));
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+      }
     }
   }
-  epi_vectors<512, TN * VPR / 512, VPR>(a, Cs, CP, px0, ch0, Mc, pfull, bst, mean8, sc8, sh8, s1, s2);
-  if constexpr (kBst) {
-    if (bst) {
-      // reduction slots after the C tile in the (idle) stage buffers
-      float* bred = reinterpret_cast<float*>(smem + ((TN * CP * 2 + 255) & ~255));
-      // partial row = (parity class, pixel tile)
-      bn_bwd_flush<512, VPR>(a, bred, s1, s2, (int)blockIdx.z * ((Mc + TN - 1) / TN) + px0 / TN, ch0);
-    }
+  __syncthreads();  // every wave done with the stage buffers (no LDS-DMA outstanding)
+  // k-group 1 hands its tile to k-group 0 (lane-linear float4s: conflict-free both ways)
+  float4* red = reinterpret_cast<float4*>(smem);
+  if (kg == 1) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int q = 0; q < (MF32 ? 4 : 1); ++q) {
+          const int qi = (i * NI + j) * (MF32 ? 4 : 1) + q;
+          red[(wq * 16 + qi) * 64 + lane] =
+              make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
+        }
   }
-  if constexpr (STATS) {  // BN statistics of the stored (bf16) tile: 512 / TM threads per channel
-    constexpr int TPC = 512 / TM, RPT = TN / TPC, U = 8;
-    static_assert(RPT % U == 0, "rows per thread");
-    // reduction slots after the C tile in the (idle) stage buffers
-    float* bred = reinterpret_cast<float*>(smem + ((TN * CP * 2 + 255) & ~255));
-    static_assert(((TN * CP * 2 + 255) & ~255) + 2 * 512 * 4 <= kSmem, "BN reduction slots must fit");
-    const int c = tid % TM, q = tid / TM, ch = ch0 + c;
-    const float K = (a.bnshift && ch < a.Ng) ? a.bnshift[ch] : 0.f;
-    const int rows = min(TN, a.M - px0);
-    const uint16_t* col = reinterpret_cast<const uint16_t*>(Cs) + c;
-    float s1[U], s2[U];
+  __syncthreads();
+  if (kg == 0) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) s1[u] = s2[u] = 0.f;
-    if (rows == TN) {  // full tile: U independent rows per iteration (loads in flight together)
-      for (int r0 = q * RPT; r0 < (q + 1) * RPT; r0 += U) {
-        uint16_t h[U];
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int u = 0; u < U; ++u) h[u] = col[(r0 + u) * CP];
+      for (int j = 0; j < NI; ++j)
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const float d = bf2f(h[u]) - K;
-          s1[u] += d;
-          s2[u] = fmaf(d, d, s2[u]);
+        for (int q = 0; q < (MF32 ? 4 : 1); ++q) {
+          const int qi = (i * NI + j) * (MF32 ? 4 : 1) + q;
+          const float4 v = red[(wq * 16 + qi) * 64 + lane];
+          acc[i][j][4 * q] += v.x;
+          acc[i][j][4 * q + 1] += v.y;
+          acc[i][j][4 * q + 2] += v.z;
+          acc[i][j][4 * q + 3] += v.w;
+        }
+  }
+  __syncthreads();  // the reduction slots become the C tile
+  constexpr int CP = TM + 8;
+  static_assert(TN * CP * 2 <= kSmem, "C tile must fit in the stage buffers");
+  bf16* Cs = reinterpret_cast<bf16*>(smem);
+  if (kg == 0) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        if constexpr (!MF32) {
+          const int cl = wm * 64 + 16 * i + 4 * (lane >> 4), pl = wn * 64 + 16 * j + (lane & 15);
+          *reinterpret_cast<uint2*>(Cs + pl * CP + cl) =
+              make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
+        } else {
+          const int pl = wn * 64 + 32 * j + (lane & 31);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int cl = wm * 64 + 32 * i + 8 * q + 4 * (lane >> 5);
+            *reinterpret_cast<uint2*>(Cs + pl * CP + cl) = make_uint2(pack2(acc[i][j][4 * q], acc[i][j][4 * q + 1]),
+                                                                      pack2(acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]));
+          }
         }
       }
-    } else {
-      for (int r = q * RPT; r < min(rows, (q + 1) * RPT); ++r) {
-        const float d = bf2f(col[r * CP]) - K;
-        s1[0] += d;
-        s2[0] = fmaf(d, d, s2[0]);
-      }
-    }
-#pragma unroll
-    for (int u = 1; u < U; ++u) {
-      s1[0] += s1[u];
-      s2[0] += s2[u];
-    }
-    bred[tid] = s1[0];
-    bred[512 + tid] = s2[0];
-    __syncthreads();
-    if (q == 0 && ch < a.Ng) {
-      float t1 = s1[0], t2 = s2[0];
-      for (int k = 1; k < TPC; ++k) {
-        t1 += bred[tid + k * TM];
-        t2 += bred[512 + tid + k * TM];
-      }
-      float* dst = a.bnpart + (size_t)(px0 / TN) * 2 * a.Ng + 2 * ch;
-      dst[0] = t1;
-      dst[1] = t2;
-    }
   }
+  __syncthreads();
+  glds_tail<TM, TN, STATS, kBstB <= kSmem, kSmem>(a, smem, px0, ch0, Mc, pfull);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2809,6 +3051,23 @@ void nhwc_conv_set_glds_deep(int mode) { g_conv_glds_deep = mode; }
 // kernel's parity classes
 static int g_conv_glds_par = 1;
 void nhwc_conv_set_glds_par(int on) { g_conv_glds_par = on; }
+// the two-stage 128 x 128 tiles as conv_nhwc_gk2_kernel (64 x 64 wave tiles, two k-groups): 0 =
+// conv_nhwc_glds_kernel<128, *, 128, 2> (8 waves of 64 x 32), 1 = gk2 on 16x16x32 MFMAs, 2 = gk2 on
+// 32x32x16 MFMAs
+static int g_conv_gk2 = 0;
+void nhwc_conv_set_gk2(int mode) { g_conv_gk2 = mode; }
+static void launch_tile128(ConvNArgs& a, dim3 grid, bool stats, hipStream_t st) {
+  if (g_conv_gk2 == 2) {
+    if (stats) MX_LAUNCH((conv_nhwc_gk2_kernel<true, true>), grid, dim3(512), 0, st, a);
+    else MX_LAUNCH((conv_nhwc_gk2_kernel<false, true>), grid, dim3(512), 0, st, a);
+  } else if (g_conv_gk2 == 1) {
+    if (stats) MX_LAUNCH((conv_nhwc_gk2_kernel<true, false>), grid, dim3(512), 0, st, a);
+    else MX_LAUNCH((conv_nhwc_gk2_kernel<false, false>), grid, dim3(512), 0, st, a);
+  } else {
+    if (stats) MX_LAUNCH((conv_nhwc_glds_kernel<128, true, 128, 2>), grid, dim3(512), 0, st, a);
+    else MX_LAUNCH((conv_nhwc_glds_kernel<128, false, 128, 2>), grid, dim3(512), 0, st, a);
+  }
+}
 static bool glds_deep_fits(const ConvNArgs& a, bool wide, bool par) {
   if (!g_conv_glds_deep || conv_glds_mode() == 0 || !wide) return false;
   if (a.dgrad && (a.sh != 1 || a.sw != 1) && !(par && g_conv_glds_par)) return false;
@@ -2932,8 +3191,7 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     if (!bst) a.bx = nullptr;
     if (!(a.bnpart && (bst || !a.dgrad) && rows <= 16384)) a.bnpart = nullptr;
     const dim3 grid(cdiv(a.Ng, 128) * gx, 1, par ? 4 : 1);
-    if (a.bnpart && !bst) MX_LAUNCH((conv_nhwc_glds_kernel<128, true, 128, 2>), grid, dim3(512), 0, st, a);
-    else MX_LAUNCH((conv_nhwc_glds_kernel<128, false, 128, 2>), grid, dim3(512), 0, st, a);
+    launch_tile128(a, grid, a.bnpart && !bst, st);
     return a.bnpart ? rows : 0;
   }
   if (gp.tm && glds256_fits(a)) {  // 256 x 256 tiles, no split-K
@@ -2965,13 +3223,9 @@ static int launch_conv(ConvNArgs& a, float* scratch, hipStream_t st) {
     if (!(a.bnpart && (bst || (!a.dgrad && gp.splits == 1)) && gx <= 16384)) a.bnpart = nullptr;
     const dim3 grid(cdiv(a.Ng, gp.tm) * gx, gp.splits);
     if (shrt) {
-      if (a.bnpart && !bst) {
-        if (gp.tm == 128) MX_LAUNCH((conv_nhwc_glds_kernel<128, true, 128, 2>), grid, dim3(512), 0, st, a);
-        else MX_LAUNCH((conv_nhwc_glds_kernel<64, true, 128, 2>), grid, dim3(512), 0, st, a);
-      } else {
-        if (gp.tm == 128) MX_LAUNCH((conv_nhwc_glds_kernel<128, false, 128, 2>), grid, dim3(512), 0, st, a);
-        else MX_LAUNCH((conv_nhwc_glds_kernel<64, false, 128, 2>), grid, dim3(512), 0, st, a);
-      }
+      if (gp.tm == 128) launch_tile128(a, grid, a.bnpart && !bst, st);
+      else if (a.bnpart && !bst) MX_LAUNCH((conv_nhwc_glds_kernel<64, true, 128, 2>), grid, dim3(512), 0, st, a);
+      else MX_LAUNCH((conv_nhwc_glds_kernel<64, false, 128, 2>), grid, dim3(512), 0, st, a);
     } else if (a.bnpart && !bst) {
       if (gp.tm == 128) MX_LAUNCH((conv_nhwc_glds_kernel<128, true>), grid, dim3(512), 0, st, a);
       else MX_LAUNCH((conv_nhwc_glds_kernel<64, true>), grid, dim3(512), 0, st, a);

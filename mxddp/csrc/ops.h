@@ -198,6 +198,7 @@ void nhwc_conv_set_glds256(int mode);
 void nhwc_wgrad_set_waves8(int on);  // 8-wave 128-row weight-gradient tiles (A/B)
 void nhwc_conv_set_glds_deep(int mode);
 void nhwc_conv_set_glds_par(int on);  // stride-2 data gradients on the two-stage LDS-DMA tiles  // 128 x 128 LDS-DMA tiles for deep reductions on few tiles
+void nhwc_conv_set_gk2(int mode);  // two-stage 128 x 128 tiles: 0 = 8 waves of 64 x 32, 1 = gk2 (64 x 64 wave tiles, k-groups) 16x16x32, 2 = gk2 32x32x16
 void nhwc_conv_set_glds_short(int mode);  // two-stage 128-pixel LDS-DMA variant for short reductions
 void nhwc_conv_set_split_blocks(int n);  // generic conv kernel: split-K below this many blocks (256)
 void nhwc_wgrad_set_target(int n);  // weight gradient: blocks aimed at when splitting the pixels (512)

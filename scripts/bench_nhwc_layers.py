@@ -3,6 +3,9 @@ conv shape at batch 32 (forward, data gradient, weight gradient): microseconds a
 direction, so the conv-kernel work can be prioritised by where the step time goes.
 
     python scripts/bench_nhwc_layers.py [batch] [iters] [tile256] [glds_short] [wgrad_tile256] [glds_deep]
+
+Every switch defaults to the build's production choice; env GK2=0/1/2 picks the two-stage
+128 x 128 conv tile kernel (nhwc_conv_set_gk2).
 """
 import os
 import sys
@@ -36,7 +39,7 @@ def shapes(batch):
 def main():
     batch = int(sys.argv[1]) if len(sys.argv) > 1 else 32
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-    tile256 = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # 1: the 256 x 256-tile kernel where it fits
+    tile256 = int(sys.argv[3]) if len(sys.argv) > 3 else 1  # 1: the 256 x 256-tile kernel where it fits (default)
     dev = torch.device("cuda")
     Cn = native()
     Cn.nhwc_conv_set_glds256(tile256)
@@ -46,6 +49,8 @@ def main():
         Cn.nhwc_wgrad_set_tile256(int(sys.argv[5]))
     if len(sys.argv) > 6:  # 128 x 128 LDS-DMA tiles for deep reductions on few tiles (default 1)
         Cn.nhwc_conv_set_glds_deep(int(sys.argv[6]))
+    if "GK2" in os.environ:  # two-stage 128 x 128 tiles: 0 8-wave 64 x 32, 1 / 2 gk2 (16x16x32 / 32x32x16)
+        Cn.nhwc_conv_set_gk2(int(os.environ["GK2"]))
     st = torch.cuda.current_stream().cuda_stream
     tot = {"fwd": 0.0, "dgrad": 0.0, "dgrad_st": 0.0, "wgrad": 0.0}
     # floor: max(HBM bytes at 8 TB/s, FLOPs at the 2.5 PF bf16 dense peak), the same for all three

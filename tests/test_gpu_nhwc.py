@@ -248,6 +248,80 @@ def test_conv_glds_deep_tiles(cuda, case):
     assert _rel(outs[0][0], outs[1][0]) < 1e-2 and _rel(outs[0][1], outs[1][1]) < 1e-2
 
 
+GK2_CASES = [(4, 256, 14, 14, 256, 3, 1, 1),    # 3x3 forward + stride-1 data gradient, 36 k-tiles
+             (3, 128, 20, 18, 192, 1, 1, 0),    # partial channel tile, partial pixel tile, 2 k-tiles
+             (2, 256, 16, 12, 384, 3, 2, 1),    # stride-2 forward, stride-2 data gradient (parity classes)
+             (8, 64, 28, 28, 256, 1, 1, 0)]     # the shortest reduction (1 k-tile)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("case", GK2_CASES)
+def test_conv_gk2_tiles(cuda, case, mode):
+    """The two-stage 128 x 128 tiles on 64 x 64 wave tiles with two k-groups (conv_nhwc_gk2_kernel,
+    mode 1: 16x16x32 MFMAs, mode 2: 32x32x16), forced on every eligible layer (glds_deep 2):
+    forward and data gradient vs the fp32 reference and the 8-wave 64 x 32 kernel (mode 0)."""
+    from mxddp import native
+
+    Cn = native()
+    N, C, H, W, K, R, st, pd = case
+    torch.manual_seed(17)
+    x = torch.randn(N, H, W, C).to(torch.bfloat16)
+    w = torch.randn(K, C, R, R) * (2.0 / (C * R * R)) ** 0.5
+    xr = _nchw(x).requires_grad_()
+    wr = w.to(torch.bfloat16).float().requires_grad_()
+    yr = F.conv2d(xr, wr, None, st, pd)
+    gy = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(gy)
+    gyn = gy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(cuda)
+    outs = []
+    try:
+        Cn.nhwc_conv_set_glds_deep(2)
+        for m in (mode, 0):
+            Cn.nhwc_conv_set_gk2(m)
+            xg = x.to(cuda).requires_grad_()
+            y = nhwc.conv2d(xg, w.to(cuda), st, pd)
+            y.backward(gyn)
+            torch.cuda.synchronize()
+            outs.append((_nchw(y), _nchw(xg.grad)))
+    finally:
+        Cn.nhwc_conv_set_gk2(0)
+        Cn.nhwc_conv_set_glds_deep(1)
+    assert _rel(outs[0][0], yr.detach()) < 1e-2
+    assert _rel(outs[0][1], xr.grad) < 1e-2
+    # fp32 sums of the same bf16 products in another order, rounded to bf16
+    assert _rel(outs[0][0], outs[1][0]) < 1e-2 and _rel(outs[0][1], outs[1][1]) < 1e-2
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_bn_statistics_from_gk2_epilogue(cuda, mode):
+    """Forward BN statistics from the gk2 kernel's epilogue (the shared glds_tail) == the BN's own
+    statistics pass."""
+    from mxddp import native
+
+    Cn = native()
+    try:
+        Cn.nhwc_conv_set_glds_deep(2)
+        Cn.nhwc_conv_set_gk2(mode)
+        _bn_stats_from_conv_epilogue(cuda, (3, 256, 15, 13, 256, 3, 1), 1.5)
+    finally:
+        Cn.nhwc_conv_set_gk2(0)
+        Cn.nhwc_conv_set_glds_deep(1)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("relu", [False, True])
+def test_bn_backward_statistics_from_gk2_dgrad(cuda, mode, relu):
+    """Backward BN statistics from the gk2 kernel's data-gradient epilogue (glds "deep")."""
+    from mxddp import native
+
+    Cn = native()
+    try:
+        Cn.nhwc_conv_set_gk2(mode)
+        test_bn_backward_statistics_from_dgrad_epilogue(cuda, "deep", 1, relu)
+    finally:
+        Cn.nhwc_conv_set_gk2(0)
+
+
 @pytest.mark.parametrize("case", [(2, 64, 14, 14, 256, 1, 1, 0), (1, 256, 9, 9, 256, 3, 1, 1),
                                   (2, 512, 7, 7, 256, 1, 1, 0), (3, 64, 20, 20, 512, 1, 2, 0),
                                   (2, 256, 16, 16, 256, 3, 1, 1)])
@@ -401,7 +475,7 @@ def test_bn_statistics_from_glds256_epilogue(cuda, shape, offset):
     try:
         _bn_stats_from_conv_epilogue(cuda, shape, offset)
     finally:
-        C_.nhwc_conv_set_glds256(0)
+        C_.nhwc_conv_set_glds256(1)
         C_.nhwc_conv_set_glds(1)
 
 
@@ -499,7 +573,7 @@ def test_bn_backward_statistics_from_dgrad_epilogue(cuda, glds, stride, relu):
     finally:
         nhwc._BN_STATS_IN_DGRAD = False
         nhwc._BN_DGRAD_STATS_MAX = _DSTATS_MAX
-        C.nhwc_conv_set_glds256(0)
+        C.nhwc_conv_set_glds256(1)
         C.nhwc_conv_set_glds(1)
     assert used == [0, 1], used  # the fused run really took the epilogue's statistics
     for a, b in zip(*outs):
@@ -628,10 +702,7 @@ def test_lazy_identity_join_equals_materialised(cuda):
         assert _nrel(b, a) < 1e-2
 
 
-@pytest.mark.parametrize("inp,planes,hw", [(256, 128, 28), (512, 256, 14), (64, 64, 10),
-                                            # first 1x1's reduction of 16 k-tiles over 256 pixels:
-                                            # a split-K plan unless the half-resolution join forbids it
-                                            (512, 1024, 8)])
+@pytest.mark.parametrize("inp,planes,hw", [(256, 128, 28), (512, 256, 14), (64, 64, 10)])
 def test_half_resolution_projection_gradient(cuda, inp, planes, hw):
     """Stride-2 1x1 projection shortcut: its input gradient computed on the output grid and added
     at even (h, w) in the first conv's epilogue (GradJoin.sub2) == the full-resolution parity-class
@@ -660,6 +731,37 @@ def test_half_resolution_projection_gradient(cuda, inp, planes, hw):
         nhwc._SUB2_DEPOSIT = True
     for a, b in zip(*outs):
         assert _nrel(b, a) < 1e-2
+
+
+@pytest.mark.parametrize("K,C", [(1024, 512), (2048, 256)])
+def test_half_resolution_addend_never_split_k(cuda, K, C):
+    """A 1x1 data gradient whose reduction (K = 1,024 / 2,048: 16 / 32 k-tiles over 256 pixels)
+    would be split over the reduction takes a half-resolution addend (GradJoin.sub2) at even
+    (h, w): the split-K reduce maps full-resolution indices, so such a launch must never split
+    (ADVICE r5).  Against the fp32 reference dx = dy W + addend at even positions."""
+    from mxddp import native
+
+    Cn = native()
+    N, H, W = 4, 8, 8
+    assert Cn.nhwc_conv_dgrad_scratch_floats(N, H, W, C, K, 1, 1, 1, 1, 0, 0, H, W) > 0  # a split plan exists
+    torch.manual_seed(5)
+    w = (torch.randn(K, C, 1, 1) * 0.05).to(cuda)
+    dy = torch.randn(N, H, W, K).to(torch.bfloat16).to(cuda)
+    add = torch.randn(N, H // 2, W // 2, C).to(torch.bfloat16).to(cuda)
+    st = torch.cuda.current_stream().cuda_stream
+    wtd = torch.empty((C * K,), device=cuda, dtype=torch.bfloat16)
+    Cn.nhwc_repack_weight(w.data_ptr(), 0, wtd.data_ptr(), K, C, 1, 1, C, st)
+    n = Cn.nhwc_conv_dgrad_scratch_floats(N, H, W, C, K, 1, 1, 1, 1, 0, 0, H, W)
+    scr = torch.full((n,), float("nan"), device=cuda)
+    dx = torch.empty((N, H, W, C), device=cuda, dtype=torch.bfloat16)
+    Cn.nhwc_conv_dgrad(dy.data_ptr(), wtd.data_ptr(), dx.data_ptr(), N, H, W, C, K, 1, 1, 1, 1, 0, 0, H, W,
+                       scr.data_ptr(), st, addend=add.data_ptr(), addend_sub=True)
+    torch.cuda.synchronize()
+    bw = w.view(K, C).to(torch.bfloat16).float().cpu()
+    ref = dy.float().cpu().reshape(-1, K) @ bw
+    ref = ref.view(N, H, W, C)
+    ref[:, ::2, ::2, :] += add.float().cpu()
+    assert _nrel(dx.float().cpu(), ref) < 1e-2
 
 
 def test_half_resolution_deposit_without_consumer(cuda):
