@@ -1,14 +1,17 @@
 // Fused gfx950 kernels for the MNIST-CNN training step (fp32 in / fp32 accumulate, exact).
 //
-// One step = 7 launches:
+// One step = 5 launches at world size 1, 6 when gradient collectives run:
 //   F2  on-device batch + conv1+ReLU + conv2+bias+ReLU+maxpool (MFMA)
 //   F3  fc1 forward, split-K (MFMA), partials added as int64 fixed point (order-independent)
 //   F5  head (fc1 bias+ReLU, fc2, log_softmax+NLL, dlogits, fc2/fc1-bias grads, dh) recomputed in
 //       every block + fc1 dgrad/wgrad (MFMA) + ReLU/maxpool-masked dp          -> bucket 0 ready
-//   F6  conv2 wgrad (MFMA) | F7 conv2 dgrad (MFMA) + conv1 ReLU mask + conv1 wgrad
+//       (world size 1: the fc1 SGD update is applied here, the gradient is never materialised)
+//   F67 conv2 wgrad (F6W blocks, MFMA) and conv2 dgrad + conv1 ReLU mask + conv1 wgrad (F7W
+//       blocks) in ONE launch (co-scheduled peer exchange blocks first when that strategy runs)
 //   F8  finalize conv grads, reset accumulators                                -> bucket 1 ready
+//       (world size > 1 only: at world size 1 its duties are folded into the SGD launch)
 //   SGD flat SGD + repack conv2 weights into the MFMA fragment orders of F2 / F7
-// (mnist_conv_bwd.hip holds F6..F8.)
+// (mnist_conv_bwd.hip holds F67 and F8; mnist_engine.cpp sequences them.)
 //
 // MFMA = v_mfma_f32_16x16x4_f32: lane l holds A[l&15][k=l>>4], B[k=l>>4][l&15]; the C/D tile
 // has col = l&15, row = 4*(l>>4) + reg.  Where operands are read as float4 along K the K order

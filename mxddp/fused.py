@@ -136,11 +136,12 @@ class FusedTrainerBase:
         mode = self.eng.graph_mode if self._capture_done else None
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         C.set_dry_collectives(True)
+        ran = 2 + steps
         try:
             self.eng.uncapture()
             if mode:
                 self._capture(mode)
-                self.eng.warm_graphs()
+                ran += self.eng.warm_graphs()
             self.eng.replay(2)
             self.eng.sync()
             ev0.record(self.stream)
@@ -148,6 +149,7 @@ class FusedTrainerBase:
             ev1.record(self.stream)
             self.eng.sync()
         finally:
+            self.discarded_steps = getattr(self, "discarded_steps", 0) + ran
             C.set_dry_collectives(False)
             self.eng.uncapture()
             if mode:

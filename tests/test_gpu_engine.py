@@ -343,3 +343,4 @@ def test_fused_engine_divergence_stays_visible(cuda):
     assert loss != loss, loss
     sd = tr.state_dict()
     assert torch.isnan(sd["fc2.weight"]).any() and torch.isnan(sd["conv1.weight"]).any()
+
