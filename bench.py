@@ -41,6 +41,10 @@ MODEL_METRIC = {
 AB_SWITCHES = {
     "gk2": ("nhwc_conv_set_gk2", "bf16 NHWC convs, two-stage 128 x 128 tiles: 0 = 8 waves of 64 x 32, 1 = 64 x 64 wave "
                                  "tiles in two k-groups on 16x16x32 MFMAs, 2 = the same on 32x32x16"),
+    "fc1_defer": ("mnist_set_fc1_defer", "fused MNIST, world size 1: fc1 weight gradient + SGD in the conv-backward "
+                                         "launch's last blocks (1) or folded into F5 (0)"),
+    "wgrad_defer": ("ops.set_wgrad_defer", "layer path, world size 1: conv weight-gradient split reductions summed by "
+                                           "the optimizer in batched launches (1, default) or one launch per conv (0)"),
     "conv_tile256": ("nhwc_conv_set_glds256", "bf16 NHWC convs, 256x256-tile LDS-DMA kernel on big layers (0/1)"),
     "glds_deep": ("nhwc_conv_set_glds_deep", "bf16 NHWC convs, 128 x 128 two-stage tiles on >= 4 k-tile layers (0 off, 1 >= 192 tiles, 2 all, 3 under-filled only)"),
     "wgrad_tile256": ("nhwc_wgrad_set_tile256", "bf16 NHWC weight gradient, 256 x 256 tiles (1) or 128 x 128 (0)"),
@@ -57,7 +61,13 @@ def _apply_ab(items) -> dict:
         k, sep, v = it.partition("=")
         if not sep or k not in AB_SWITCHES:
             raise SystemExit(f"bench.py: --ab {it!r}: expected KEY=VALUE with KEY in {sorted(AB_SWITCHES)}")
-        getattr(native(), AB_SWITCHES[k][0])(int(v))
+        name = AB_SWITCHES[k][0]
+        if name.startswith("ops."):  # a Python-level switch of mxddp.ops
+            from mxddp import ops
+
+            getattr(ops, name[4:])(int(v))
+        else:
+            getattr(native(), name)(int(v))
         out[k] = int(v)
     return out
 
@@ -169,6 +179,7 @@ def main():
     # host collectives of the bench are short: a peer that died shows up within minutes
     inf = C.init_distributed(use_gpu=True, timeout_s=float(os.environ.get("MXDDP_GLOO_TIMEOUT_S", "600")))
     ab = _apply_ab(a.ab)
+    a.ab_applied = ab
     if a.dtype != "fp32":
         if a.impl == "fused":
             a.impl = "layers"  # the fused MNIST engine is fp32-only
@@ -604,6 +615,10 @@ def _layers_or_torch(a, torch, inf, dev, comm, B):
 
         net = DDP(model, grad_comm_dtype=a.grad_comm_dtype)
         opt = SGD(net.flat, lr=0.1, momentum=0.9, weight_decay=1e-4)
+        if "wgrad_defer" not in a.ab_applied:
+            # world size 1: nothing reads the gradients before the optimizer, which sums the convs'
+            # deferred split reductions in batched launches (ops.set_wgrad_defer)
+            ops.set_wgrad_defer(inf.world_size == 1 and not a.force_collectives)
         loss_fn = ops.cross_entropy
     else:
         import torch.nn as nn

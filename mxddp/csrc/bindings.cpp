@@ -13,6 +13,7 @@
 #include "ops.h"
 #include "peer.h"
 #include "reducer.h"
+#include "wgrad_defer.h"
 
 namespace py = pybind11;
 using namespace mx;
@@ -124,6 +125,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_conv_set_split_blocks", &nhwc_conv_set_split_blocks);
   m.def("nhwc_wgrad_set_target", &nhwc_wgrad_set_target);
   m.def("nhwc_wgrad_set_tile256", &nhwc_wgrad_set_tile256);
+  m.def("wgrad_defer_set", &wgrad_defer_set,
+        "this thread's next weight-gradient calls record their split reduction for wgrad_defer_flush");
+  m.def("wgrad_defer_took", &wgrad_defer_took);
+  m.def("wgrad_defer_pending", &wgrad_defer_pending);
+  m.def("wgrad_defer_flush", [](uintptr_t st) { return wgrad_defer_flush(S(st)); });
+  m.def("mnist_set_fc1_defer", &mnist_set_fc1_defer,
+        "fused MNIST, world size 1: fc1 weight gradient + SGD in the conv-backward launch's last blocks (1) or in F5 (0)");
+  m.def("mnist_fc1_defer", &mnist_fc1_defer);
   m.def("mnist_set_wt_stores", &mnist_set_wt_stores,
         "MNIST bulk stores with agent scope (L2 write-through) for steps launched afterwards: mask 1 = F5, 2 = F2, "
         "4 = F6W");

@@ -118,6 +118,8 @@ inline size_t scratch_floats(int B) {
 // sg + 16, ... (4 loads in flight per round, clamped + masked: no load behind a branch); the 16
 // subgroup partials are added in order.  red: 576 floats of LDS.
 constexpr int kWslabGroups = 512;  // 2048 pairs / 4
+// fc1 weight-gradient column slices (F5's blocks, and the deferred update's blocks in F67)
+constexpr int kFc1Cols = 48, kFc1Slices = 9216 / kFc1Cols;
 __device__ __forceinline__ void wslab_group_sum(const MnistFused& f, const Scratch& sc, int grp, float* red, float* gs) {
   const int t = threadIdx.x;
   if (t < 144) {

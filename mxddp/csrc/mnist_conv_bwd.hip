@@ -641,6 +641,74 @@ __device__ __forceinline__ void f7w_body(const MnistFused& f, const Scratch& sc,
 }
 
 // ------------------------------------------------------------------------------------------
+// Deferred fc1 weight gradient + SGD update (MnistFused::fc1_defer, world size 1): F5 publishes
+// dh and skips this work; these blocks come after F7W's in the conv-backward grid, so they take
+// the CU slots the data-gradient blocks free first and run beside F6W's tail instead of on F5's
+// critical path.  Block = one 48-column slice of fc1 (F5's slices), wave w = weight rows
+// 32w .. 32w + 31: the same operand values, MFMA order and update as F5's folded path, so the
+// trained weights are bitwise identical.  LDS: dh [B][132] + the pool slice [B][52] (B <= 96).
+constexpr int kFc1DhP = 132, kFc1P = 52;
+__device__ __forceinline__ void fc1_update_body(const MnistFused& f, float* sm, int slice) {
+  const int B = f.B, c0 = slice * kFc1Cols;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, m = lane & 15;
+  float* dhs = sm;                // [B][132]
+  float* ps = dhs + B * kFc1DhP;  // [B][52]
+  // this lane's 24 weights and momenta (requested first: their latency overlaps the staging)
+  float mb[2][3][4], pw[2][3][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t e = L::fw1 + (size_t)(32 * w + 16 * a + 4 * g + j) * 9216 + c0 + 16 * c + m;
+        mb[a][c][j] = f.mom[e];
+        pw[a][c][j] = f.p[e];
+      }
+  for (int i = tid; i < B * 32; i += 256) {
+    const int r = i >> 5, c4 = (i & 31) * 4;
+    *reinterpret_cast<float4*>(dhs + r * kFc1DhP + c4) = *reinterpret_cast<const float4*>(f.dh + r * 128 + c4);
+  }
+  for (int i = tid; i < B * 12; i += 256) {
+    const int r = i / 12, c4 = (i - r * 12) * 4;
+    *reinterpret_cast<float4*>(ps + r * kFc1P + c4) = *reinterpret_cast<const float4*>(f.pool + (size_t)r * 9216 + c0 + c4);
+  }
+  __syncthreads();
+  f32x4 acc[2][3];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < B / 16; ++s) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int b = 16 * s + 4 * g + j;
+      const float a0 = dhs[b * kFc1DhP + 32 * w + m], a1v = dhs[b * kFc1DhP + 32 * w + 16 + m];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float bv = ps[b * kFc1P + 16 * c + m];
+        acc[0][c] = mfma4(a0, bv, acc[0][c]);
+        acc[1][c] = mfma4(a1v, bv, acc[1][c]);
+      }
+    }
+  }
+  const float lr = *f.lr;
+  const bool wt = f.wt & 1;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t e = L::fw1 + (size_t)(32 * w + 16 * a + 4 * g + j) * 9216 + c0 + 16 * c + m;
+        float pv = pw[a][c][j], bv = mb[a][c][j];
+        sgd_upd(pv, bv, acc[a][c][j], 1.f, f.sgd_mom, f.sgd_wd, lr);
+        st1(f.mom + e, bv, wt);
+        st1(f.p + e, pv, wt);
+      }
+}
+
+// ------------------------------------------------------------------------------------------
 // F6W + F7W in ONE launch: blocks [0, 2B) run the weight gradient, the rest the data gradient.
 // The two are independent; sharing a grid lets the dispatcher backfill CUs as blocks retire, so
 // one kernel's prologue/epilogue latency and the blocks-per-CU imbalance of each kernel alone
@@ -662,12 +730,14 @@ __global__ __launch_bounds__(256, kPipe ? 2 : 3) void f67_conv2_bwd_kernel(Mnist
     return;
   }
   const int bid = (int)blockIdx.x - f.co_blocks;
-  const int n6 = 2 * f.B;
+  const int n6 = 2 * f.B, n7 = kF7WChunks * f.B;
   if (bid < n6)
     if constexpr (kPipe) f6w_body(f, sc, sm, bid, n6);
     else f6w_body_serial(f, sc, sm, bid, n6);
-  else
-    f7w_body<2>(f, sc, sm, bid - n6, kF7WChunks * f.B);
+  else if (bid < n6 + n7)
+    f7w_body<2>(f, sc, sm, bid - n6, n7);
+  else  // deferred fc1 update (f.fc1_defer): the grid's last kFc1Slices blocks
+    fc1_update_body(f, sm, bid - n6 - n7);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -718,7 +788,10 @@ void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_
     attr = true;
   }
   const Scratch sc = carve(f.scratch, f.B);
-  const dim3 grid(f.co_blocks + 2 * f.B + kF7WChunks * f.B);
+  const bool defer = f.fc1_sgd && f.fc1_defer;
+  MX_CHECK(!defer || (f.co_blocks == 0 && sizeof(float) * f.B * (kFc1DhP + kFc1P) <= kF6WLdsPipe),
+           "deferred fc1 update: world size 1, batch <= 96");
+  const dim3 grid(f.co_blocks + 2 * f.B + kF7WChunks * f.B + (defer ? kFc1Slices : 0));
   if (f.co_blocks == 0) {
     constexpr size_t lds = kF6WLdsPipe > kF7WLds ? kF6WLdsPipe : kF7WLds;
     MX_LAUNCH(f67_conv2_bwd_kernel<true>, grid, dim3(256), lds, st, f, sc);

@@ -195,6 +195,8 @@ MnistFused MnistEngine::fused_args() const {
   // without gradient collectives F5 applies the fc1 weight update itself (no all-reduce has to
   // come between the gradient and the update)
   f.fc1_sgd = (variant_ == 1 && !reducer_->active()) ? 1 : 0;
+  // the deferred update's blocks stage dh + a pool slice in F67's LDS: batch <= 96
+  f.fc1_defer = (f.fc1_sgd && mnist_fc1_defer() && Bp_ <= 96) ? 1 : 0;
   f.mom = m_;
   f.lr = lr_;
   f.sgd_mom = momentum_;

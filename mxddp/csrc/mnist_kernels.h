@@ -34,6 +34,11 @@ struct MnistFused {
   // the weight columns whose gradient it just produced (the gradient is not written to g), and
   // the SGD launch skips them
   int fc1_sgd;
+  // with fc1_sgd: F5 only computes dp (+ the head) and publishes dh; the fc1 weight gradient and
+  // its SGD update run in extra blocks at the end of the conv-backward launch (F67), which take
+  // the CU slots its data-gradient blocks free first (the next step's F3 is the first reader of
+  // the updated weights)
+  int fc1_defer;
   float* mom;            // flat momentum buffer
   const float* lr;       // device learning rate
   float sgd_mom, sgd_wd;
@@ -48,6 +53,8 @@ struct MnistFused {
 };
 size_t mnist_fused_scratch_floats(int B);
 void mnist_set_wt_stores(int mask);  // process-wide default of MnistFused::wt
+void mnist_set_fc1_defer(int on);    // process-wide default of MnistFused::fc1_defer (world size 1)
+int mnist_fc1_defer();
 int mnist_wt_stores();
 
 // Pack conv2 weights into the F2 Winograd fragment order and zero the cross-step accumulators;

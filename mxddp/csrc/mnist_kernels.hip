@@ -461,7 +461,7 @@ struct Reg6 {
   }
 };
 
-constexpr int kF5Cols = 48, kF5NT = kF5Cols / 16, kF5C4 = kF5Cols / 4;
+constexpr int kF5Cols = kFc1Cols, kF5NT = kF5Cols / 16, kF5C4 = kF5Cols / 4;
 constexpr int kF5DhP = 132, kF5P = 52, kF5W2P = 20, kF5LgP = 20;  // kF5P = 4 mod 8: 4-row groups 16 banks apart
 constexpr int kF5Misc = 12;  // [0..3] db2, [4..7] loss, [8..11] correct: one slot per wave
 // Store of F5's bulk outputs (fc1 weights / momentum / dp): WT = agent-scope relaxed store
@@ -474,7 +474,7 @@ __device__ __forceinline__ void f5_store(float* p, float v) {
   else
     *p = v;
 }
-template <int B, bool WT>
+template <int B, bool WT, bool DEFER>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void f5_head_fc1_bwd_kernel(MnistFused f) {
   MX_TRACE(f, 2, 0);
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -523,17 +523,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // (loaded unconditionally -- f.mom always exists: a load behind the fc1_sgd branch made the
   // waitcnt pass merge both paths and drain most of group 2 before the head)
   float mb[2][kF5NT][4];
+  if constexpr (!DEFER) {  // DEFER: the update runs in F67's extra blocks, which load the momentum
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int c = 0; c < kF5NT; ++c)
+      for (int c = 0; c < kF5NT; ++c)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        mb[a][c][j] = f.mom[L::fw1 + (size_t)(32 * w + 16 * a + 4 * g + j) * 9216 + c0 + 16 * c + m];
+        for (int j = 0; j < 4; ++j)
+          mb[a][c][j] = f.mom[L::fw1 + (size_t)(32 * w + 16 * a + 4 * g + j) * 9216 + c0 + 16 * c + m];
+  }
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
     const int i = min(tid + 256 * k, B * kF5C4 - 1), r = i / kF5C4, c4 = i - r * kF5C4;
-    vp.set(k, *reinterpret_cast<const float4*>(f.pool + (size_t)r * 9216 + c0 + c4 * 4));
+    if constexpr (!DEFER)  // the pool slice feeds only dW1
+      vp.set(k, *reinterpret_cast<const float4*>(f.pool + (size_t)r * 9216 + c0 + c4 * 4));
     vq.set(k, *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(f.idx) + (size_t)r * 9216 + c0 +
                                                  c4 * 4));
   }
@@ -663,7 +666,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   for (int k = 0; k < NP; ++k) {
     const int i = tid + 256 * k, r = i / kF5C4, c4 = i - r * kF5C4;
     if (i < B * kF5C4) {
-      *reinterpret_cast<float4*>(ps + r * kF5P + c4 * 4) = vp.get(k);
+      if constexpr (!DEFER) *reinterpret_cast<float4*>(ps + r * kF5P + c4 * 4) = vp.get(k);
       *reinterpret_cast<uint32_t*>(qs + r * kF5Cols + c4 * 4) = vq.get(k);
     }
   }
@@ -681,8 +684,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int k = 0; k < 8; ++k) acc[k] += dhs[(b + k) * kF5DhP + tid];
     f.g[L::fb1 + tid] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   }
+  if constexpr (DEFER) {  // publish dh for the deferred update: blocks 0 .. B/8-1 write 8 rows each
+    if ((int)blockIdx.x < B / 8) {
+      const int r = 8 * (int)blockIdx.x + (tid >> 5), c4 = (tid & 31) * 4;
+      *reinterpret_cast<float4*>(f.dh + r * 128 + c4) = *reinterpret_cast<const float4*>(dhs + r * kF5DhP + c4);
+    }
+  }
   // ---- dW1 tiles: rows n (8 M-tiles, wave w takes 2w, 2w+1), cols kF5NT N-tiles, K = B
-  {
+  if constexpr (!DEFER) {
     f32x4 acc[2][kF5NT];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -934,8 +943,10 @@ static void check(const MnistFused& f) {
 static void set_lds_limits() {
   static bool done = false;
   if (done) return;
-#define F5_FN(b) reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<b, false>), \
-                reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<b, true>)
+#define F5_FN(b) reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<b, false, false>), \
+                reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<b, true, false>), \
+                reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<b, false, true>), \
+                reinterpret_cast<const void*>(f5_head_fc1_bwd_kernel<b, true, true>)
   const void* fns[] = {F5_FN(16), F5_FN(32), F5_FN(48), F5_FN(64), F5_FN(80), F5_FN(96), F5_FN(112), F5_FN(128)};
 #undef F5_FN
   for (const void* fn : fns)
@@ -963,10 +974,12 @@ void mnist_fused_fc1_bwd(const MnistFused& f, hipStream_t st) {
   const size_t lds = sizeof(float) * ((size_t)f.B * kF5DhP + f.B * kF5P + 128 * kF5P + 128 * kF5W2P + f.B * kF5LgP + kF5Misc) +
                      (size_t)f.B * kF5Cols;
   const dim3 grid(9216 / kF5Cols), block(256);
+  const bool defer = f.fc1_sgd && f.fc1_defer;
   void (*kfn)(MnistFused) = nullptr;
-#define F5_CASE(b)                                                                             \
-  case b:                                                                                      \
-    kfn = (f.wt & 1) ? f5_head_fc1_bwd_kernel<b, true> : f5_head_fc1_bwd_kernel<b, false>; \
+#define F5_CASE(b)                                                                                           \
+  case b:                                                                                                    \
+    if (defer) kfn = (f.wt & 1) ? f5_head_fc1_bwd_kernel<b, true, true> : f5_head_fc1_bwd_kernel<b, false, true>; \
+    else kfn = (f.wt & 1) ? f5_head_fc1_bwd_kernel<b, true, false> : f5_head_fc1_bwd_kernel<b, false, false>;   \
     break;
   switch (f.B) {
     F5_CASE(16) F5_CASE(32) F5_CASE(48) F5_CASE(64) F5_CASE(80) F5_CASE(96) F5_CASE(112) F5_CASE(128)
@@ -976,6 +989,10 @@ void mnist_fused_fc1_bwd(const MnistFused& f, hipStream_t st) {
   MX_LAUNCH(kfn, grid, block, lds, st, f);
   MX_HIP_CHECK(hipGetLastError());
 }
+
+static int g_fc1_defer = 0;
+void mnist_set_fc1_defer(int on) { g_fc1_defer = on ? 1 : 0; }
+int mnist_fc1_defer() { return g_fc1_defer; }
 
 void mnist_fused_sgd(const MnistFused& f, float* mom_buf, const float* lr, float gscale, float momentum, float wd,
                      hipStream_t st, bool finalize) {

@@ -30,6 +30,7 @@
 #include "common.h"
 #include "igemm_bf16.h"
 #include "ops.h"
+#include "wgrad_defer.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -2076,13 +2077,13 @@ constexpr int kSwBlocks = 256;  // persistent blocks (one per CU: 131 KB of LDS 
 // of its quad (float4 loads, 4 consecutive columns of one tap since Ca % 8 == 0), the G group
 // sums are combined in LDS in a fixed order (deterministic).  Many splits (the 56 x 56 layers
 // have ~200) are spread over the G groups instead of one thread's serial chain.
-__global__ __launch_bounds__(256) void wgrad_nhwc_reduce_k(const float* __restrict__ part, float* __restrict__ dw,
-                                                            int splits, int Kout, int Ng, int Ca, int Cin, int RS,
-                                                            int accumulate, int G) {
+__device__ __forceinline__ void nhwc_reduce_body(const float* __restrict__ part, float* __restrict__ dw, int splits,
+                                                 int Kout, int Ng, int Ca, int Cin, int RS, int accumulate, int G,
+                                                 int blk) {
   __shared__ float4 red[256];
   const int plane4 = Kout * Ng / 4, QB = 256 / G;
   const int q = threadIdx.x % QB, g = threadIdx.x / QB;
-  const int i = blockIdx.x * QB + q;
+  const int i = blk * QB + q;
   const float4* p4 = reinterpret_cast<const float4*>(part);
   // 8 partial planes per round with every load issued before the first add, at clamped indices
   // (a plane past `splits` or a lane past the plane loads a valid element and discards it): the
@@ -2127,6 +2128,22 @@ __global__ __launch_bounds__(256) void wgrad_nhwc_reduce_k(const float* __restri
 #pragma unroll
   for (int j = 0; j < 4; ++j)
     if (c + j < Cin) d[(size_t)j * RS] = old[j] + v[j];
+}
+
+__global__ __launch_bounds__(256) void wgrad_nhwc_reduce_k(const float* __restrict__ part, float* __restrict__ dw,
+                                                            int splits, int Kout, int Ng, int Ca, int Cin, int RS,
+                                                            int accumulate, int G) {
+  nhwc_reduce_body(part, dw, splits, Kout, Ng, Ca, Cin, RS, accumulate, G, blockIdx.x);
+}
+
+// many deferred reductions in one launch (wgrad_defer.h): block b runs job q's block b - blk0[q]
+__global__ __launch_bounds__(256) void wgrad_nhwc_reduce_batch_k(RedBatch bt) {
+  int q = 0;
+  for (int k = 1; k < bt.n; ++k)
+    if ((int)blockIdx.x >= bt.j[k].blk0) q = k;
+  const RedJob& jb = bt.j[q];
+  nhwc_reduce_body(jb.part, jb.dw, jb.nplanes, jb.Kout, jb.Ng, jb.Ca, jb.Cin, jb.RS, jb.acc, jb.G,
+                   (int)blockIdx.x - jb.blk0);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3432,6 +3449,37 @@ size_t nhwc_wgrad_scratch_floats(int N, int Cp, int K, int R, int S, int P, int 
   return n;
 }
 
+// the weight gradient's split reduction: launched now, or recorded for the optimizer's batched
+// flush (wgrad_defer.h) when the caller opted this call in
+static void nhwc_wgrad_reduce(const float* part, float* dw, int splits, int K, int Ng, int Cp, int Cin, int RS,
+                              bool accumulate, int G, hipStream_t st) {
+  const int plane4 = K * Ng / 4, blocks = cdiv(plane4, 256 / G);
+  if (wgrad_defer_active()) {
+    RedJob j{};
+    j.part = part;
+    j.dw = dw;
+    j.plane = plane4;
+    j.nplanes = splits;
+    j.G = G;
+    j.acc = accumulate ? 1 : 0;
+    j.kind = 1;
+    j.Kout = K;
+    j.Ng = Ng;
+    j.Ca = Cp;
+    j.Cin = Cin;
+    j.RS = RS;
+    j.blocks = blocks;
+    wgrad_defer_push(j);
+    return;
+  }
+  MX_LAUNCH(wgrad_nhwc_reduce_k, dim3(blocks), dim3(256), 0, st, part, dw, splits, K, Ng, Cp, Cin, RS,
+            accumulate ? 1 : 0, G);
+}
+
+void nhwc_reduce_batch_launch(const RedBatch& b, int blocks, hipStream_t st) {
+  MX_LAUNCH(wgrad_nhwc_reduce_batch_k, dim3(blocks), dim3(256), 0, st, b);
+}
+
 void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, int H, int W, int Cin, int Cp, int K,
                      int R, int S, int sh, int sw, int ph, int pw, int P, int Q, bool accumulate, float* scratch,
                      hipStream_t st) {
@@ -3463,16 +3511,12 @@ void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, in
   if (wgrad_c3_eligible(a)) {  // persistent band kernel, one plane per block
     const int rt = c3_band_rows(P, Q);
     MX_LAUNCH(wgrad_c3_kernel, dim3(kSwBlocks), dim3(512), 0, st, a, rt, N * (P / rt));
-    const int plane4 = K * a.Ng / 4;
-    MX_LAUNCH(wgrad_nhwc_reduce_k, dim3(cdiv(plane4, 256 / 16)), dim3(256), 0, st, scratch, dw, kSwBlocks, K, a.Ng,
-              Cp, Cin, R * S, accumulate ? 1 : 0, 16);
+    nhwc_wgrad_reduce(scratch, dw, kSwBlocks, K, a.Ng, Cp, Cin, R * S, accumulate, 16, st);
     return;
   }
   if (wgrad_stem_eligible(a)) {  // persistent LDS-patch kernel, one plane per block
     MX_LAUNCH(wgrad_stem_kernel, dim3(kSwBlocks), dim3(512), 0, st, a, N * (P / 16) * (Q / 16));
-    const int plane4 = K * a.Ng / 4;
-    MX_LAUNCH(wgrad_nhwc_reduce_k, dim3(cdiv(plane4, 256 / 16)), dim3(256), 0, st, scratch, dw, kSwBlocks, K, a.Ng,
-              Cp, Cin, R * S, accumulate ? 1 : 0, 16);
+    nhwc_wgrad_reduce(scratch, dw, kSwBlocks, K, a.Ng, Cp, Cin, R * S, accumulate, 16, st);
     return;
   }
   int tm, tn;
@@ -3491,9 +3535,7 @@ void nhwc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, int N, in
   MX_CHECK((int64_t)K * a.Ng < (1ll << 31), "nhwc wgrad: weight too large for 32-bit indices");
   int G = 1;  // split groups per reduce block: enough that each thread sums <= ~8 splits
   while (G < 16 && G * 8 < splits) G *= 2;
-  const int plane4 = K * a.Ng / 4;
-  MX_LAUNCH(wgrad_nhwc_reduce_k, dim3(cdiv(plane4, 256 / G)), dim3(256), 0, st, scratch, dw, splits, K, a.Ng, Cp, Cin,
-            R * S, accumulate ? 1 : 0, G);
+  nhwc_wgrad_reduce(scratch, dw, splits, K, a.Ng, Cp, Cin, R * S, accumulate, G, st);
 }
 
 static dim3 bn_grid(int Npix, int C) {

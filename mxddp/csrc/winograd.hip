@@ -26,6 +26,7 @@
 //
 // Replaces (reference): cuDNN conv fwd / bwd-data / bwd-filter for pytorch/model.py:28-32.
 #include "common.h"
+#include "wgrad_defer.h"
 #include "ops.h"
 
 #include <algorithm>
@@ -725,14 +726,14 @@ __global__ __launch_bounds__(256, 3) void wino_wgrad_kernel(WinoWArgs a) {
 // tree.  G is picked so a thread sums at most ~4 planes: the small stage-1 PyramidNet layers
 // have 256 planes of only ~4 K floats, and a thread walking 16 of them as a dependent chain made
 // those reductions latency-bound (22-43 us for ~4 MB).
-__global__ __launch_bounds__(256) void wino_wgrad_reduce_k(const float* __restrict__ part, float* __restrict__ dw,
-                                                            int64_t plane, int64_t pstride, int nblk, int accumulate,
-                                                            int G) {
+__device__ __forceinline__ void wino_reduce_body(const float* __restrict__ part, float* __restrict__ dw, int64_t plane,
+                                                 int64_t pstride, int nblk, int accumulate, int G, int blk,
+                                                 int nblocks) {
   // partial plane b starts at part + b * pstride (pstride = plane rounded up to 4 floats)
   __shared__ float4 red[256];
   const int64_t n4 = plane >> 2, s4 = pstride >> 2;
   const int QB = 256 / G, q = threadIdx.x % QB, g = threadIdx.x / QB;
-  const int64_t i = (int64_t)blockIdx.x * QB + q;
+  const int64_t i = (int64_t)blk * QB + q;
   const float4* p4 = reinterpret_cast<const float4*>(part);
   float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i < n4) {
@@ -771,7 +772,7 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_k(const float* __restri
   // tail (plane % 4 <= 3 floats): one wave per float in the last block, lanes stride over the
   // planes, fixed-shape wave sum (a single thread walking 256 planes took tens of us)
   const int tail = (int)(plane - (n4 << 2));
-  if (tail > 0 && blockIdx.x == gridDim.x - 1 && (int)(threadIdx.x >> 6) < tail) {
+  if (tail > 0 && blk == nblocks - 1 && (int)(threadIdx.x >> 6) < tail) {
     const int lane = threadIdx.x & 63;
     const int64_t k = (n4 << 2) + (threadIdx.x >> 6);
     float v = 0.f;
@@ -779,6 +780,22 @@ __global__ __launch_bounds__(256) void wino_wgrad_reduce_k(const float* __restri
     v = wave_sum(v);
     if (lane == 0) dw[k] = (accumulate ? dw[k] : 0.f) + v;
   }
+}
+
+__global__ __launch_bounds__(256) void wino_wgrad_reduce_k(const float* __restrict__ part, float* __restrict__ dw,
+                                                            int64_t plane, int64_t pstride, int nblk, int accumulate,
+                                                            int G) {
+  wino_reduce_body(part, dw, plane, pstride, nblk, accumulate, G, blockIdx.x, gridDim.x);
+}
+
+// many deferred reductions in one launch (wgrad_defer.h): block b runs job q's block b - blk0[q]
+__global__ __launch_bounds__(256) void wino_wgrad_reduce_batch_k(RedBatch bt) {
+  int q = 0;
+  for (int k = 1; k < bt.n; ++k)
+    if ((int)blockIdx.x >= bt.j[k].blk0) q = k;
+  const RedJob& jb = bt.j[q];
+  wino_reduce_body(jb.part, jb.dw, jb.plane, jb.pstride, jb.nplanes, jb.acc, jb.G, (int)blockIdx.x - jb.blk0,
+                   jb.blocks);
 }
 
 // same reduction for a destination that is not 16-byte aligned
@@ -964,6 +981,10 @@ void wino_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s, 
              nullptr, pretransformed);
 }
 
+void wino_reduce_batch_launch(const RedBatch& b, int blocks, hipStream_t st) {
+  MX_LAUNCH(wino_wgrad_reduce_batch_k, dim3(blocks), dim3(256), 0, st, b);
+}
+
 void wino_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate, float* scratch,
                 hipStream_t st) {
   const WgradPlan p = wgrad_plan(s);
@@ -998,6 +1019,20 @@ void wino_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, 
     while (G < 64 && G * 4 < p.nblk) G *= 2;
     const int64_t blocks = std::max<int64_t>(1, (plane / 4 + 256 / G - 1) / (256 / G));
     MX_CHECK(blocks < (1ll << 31), "winograd wgrad: reduce grid too large");
+    if (wgrad_defer_active()) {  // summed later by the optimizer's batched flush (wgrad_defer.h)
+      RedJob j{};
+      j.part = scratch;
+      j.dw = dw;
+      j.plane = plane;
+      j.pstride = pstride;
+      j.nplanes = p.nblk;
+      j.G = G;
+      j.acc = accumulate ? 1 : 0;
+      j.kind = 0;
+      j.blocks = (int)blocks;
+      wgrad_defer_push(j);
+      return;
+    }
     MX_LAUNCH(wino_wgrad_reduce_k, dim3((unsigned)blocks), dim3(256), 0, st, scratch, dw, plane, pstride, p.nblk,
               accumulate ? 1 : 0, G);
   }

@@ -136,6 +136,54 @@ def _rebuild(bank) -> None:
 _BANK_ON = True  # False: per-conv transforms (tests compare the two)
 
 
+# ------------------------------------------------------ deferred weight-gradient reductions
+# (csrc/wgrad_defer.h) A conv whose weight gradient goes straight into a flat gradient buffer
+# (FlatParams sink) may leave its split-K partial planes for the optimizer to sum: the mxddp
+# optimizers call flush_wgrad() before their update, which sums every pending plane set of the
+# device in a few batched launches -- one reduce launch per conv per step fewer (PyramidNet ~100,
+# ResNet-50 53).  Opt-in (set_wgrad_defer), and only sound when nothing but the optimizer reads
+# the gradient between the backward and the step: no DDP bucket all-reduce (world size 1), no
+# in-process replica exchange, no gradient clipping.  The scratch planes of each deferred call
+# are kept alive here until the flush.
+_WGRAD_DEFER = False
+_WGRAD_KEEP: dict = {}
+
+
+def set_wgrad_defer(on: bool) -> None:
+    global _WGRAD_DEFER
+    _WGRAD_DEFER = bool(on)
+
+
+def wgrad_defer_call(fn, keep, device):
+    """Run one weight-gradient call that may defer its reduction; keeps `keep` (its partial
+    planes) alive until flush_wgrad(device) if it did."""
+    C = native()
+    C.wgrad_defer_set(True)
+    try:
+        out = fn()
+        took = C.wgrad_defer_took()
+    finally:
+        C.wgrad_defer_set(False)
+    if took:
+        _WGRAD_KEEP.setdefault(device, []).append(keep)
+    return out
+
+
+def flush_wgrad(device=None) -> int:
+    """Sum every deferred weight-gradient reduction of `device` (current stream); returns how
+    many.  Called by the mxddp optimizers before their update."""
+    if not _WGRAD_KEEP:
+        return 0
+    n = 0
+    for dev in list(_WGRAD_KEEP):
+        if device is not None and torch.device(dev) != torch.device(device):
+            continue
+        with torch.cuda.device(dev):
+            n += native().wgrad_defer_flush(torch.cuda.current_stream(dev).cuda_stream)
+        del _WGRAD_KEEP[dev]
+    return n
+
+
 def _filter_entry(w, geom, needs_dgrad):
     """This conv's banked filters (created and registered on first use), or None if the shape
     does not run the Winograd path or the weight is not a leaf parameter."""
@@ -259,8 +307,13 @@ class _Conv2d(torch.autograd.Function):
                 bsink = _grad_sink(b)
                 if (bsink is None) == (sink is None):
                     db_t = bsink if bsink is not None else torch.empty((K,), device=dy.device, dtype=dy.dtype)
-            bias_done = C.conv2d_wgrad(dy.data_ptr(), x.data_ptr(), dw_.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph,
-                                       pw, dh, dw, sink is not None, st, _p(ws), _p(db_t))
+            def _wgrad():
+                return C.conv2d_wgrad(dy.data_ptr(), x.data_ptr(), dw_.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph,
+                                      pw, dh, dw, sink is not None, st, _p(ws), _p(db_t))
+            if _WGRAD_DEFER and sink is not None and dy.is_cuda:
+                bias_done = wgrad_defer_call(_wgrad, ws, dy.device)
+            else:
+                bias_done = _wgrad()
             if sink is not None:
                 _grad_done(w)
                 dw_ = None

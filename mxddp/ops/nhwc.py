@@ -19,6 +19,7 @@ import torch
 
 from .. import native
 from . import _grad_sink, _p, stream_of
+from .. import ops as _ops
 
 BF16 = torch.bfloat16
 
@@ -287,8 +288,13 @@ class _Conv(torch.autograd.Function):
             dw = sink if sink is not None else torch.empty_like(w)
             part = torch.empty((Cn.nhwc_wgrad_scratch_floats(N, Cp, K, R, S, P, Q),), device=dy.device,
                                dtype=torch.float32)
-            Cn.nhwc_conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), N, H, W, C, Cp, K, R, S, sh, sw, ph, pw,
-                               P, Q, sink is not None, part.data_ptr(), st)
+            def _wgrad():
+                Cn.nhwc_conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), N, H, W, C, Cp, K, R, S, sh, sw, ph,
+                                   pw, P, Q, sink is not None, part.data_ptr(), st)
+            if _ops._WGRAD_DEFER and sink is not None:
+                _ops.wgrad_defer_call(_wgrad, part, dy.device)
+            else:
+                _wgrad()
             if sink is not None:
                 dw = None
         return dx, dw, None, None, None, None, None, None

@@ -77,6 +77,7 @@ class SGD(_FlatOptimizer):
         self._sync_lr()
         f = self.flat
         if f.data.is_cuda:
+            _ops.flush_wgrad(f.data.device)  # deferred weight-gradient reductions land first
             native().sgd_step(f.data.data_ptr(), f.grad.data_ptr(), self.buf.data_ptr(), self._lr_dev.data_ptr(),
                               float(self.grad_scale), float(self.momentum), float(self.weight_decay), f.numel,
                               False, torch.cuda.current_stream(f.data.device).cuda_stream)
@@ -128,6 +129,7 @@ class Adam(_FlatOptimizer):
         self._sync_lr()
         f = self.flat
         if f.data.is_cuda:
+            _ops.flush_wgrad(f.data.device)  # deferred weight-gradient reductions land first
             native().adam_step(f.data.data_ptr(), f.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
                                self._lr_dev.data_ptr(), self._state.data_ptr(), float(self.grad_scale),
                                self.b1, self.b2, float(self.eps), float(self.weight_decay), bool(self.eps_hat),

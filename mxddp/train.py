@@ -424,6 +424,9 @@ def _train_layers(args, inf, spec, opt_name, lr, mom, wd, mode, bs, mw):
     else:
         net, flat = model, FlatParams(model, dev)
     opt = _make_opt(opt_name, flat, lr, mom, wd, spec)
+    # one process, no DDP exchange: the optimizer is the gradients' only reader, so the convs'
+    # split weight-gradient reductions wait for it and run batched (ops.set_wgrad_defer)
+    ops.set_wgrad_defer(dev.type == "cuda" and inf.world_size == 1)
     sched = StepLR(opt, args.lr_step_size, args.lr_gamma) if args.lr_step_size else None
     start_epoch = 1
     st = {}

@@ -344,3 +344,27 @@ def test_fused_engine_divergence_stays_visible(cuda):
     sd = tr.state_dict()
     assert torch.isnan(sd["fc2.weight"]).any() and torch.isnan(sd["conv1.weight"]).any()
 
+
+
+@pytest.mark.parametrize("batch,graph", [(64, True), (64, False), (37, True), (96, True), (128, True)])
+def test_deferred_fc1_update_is_bitwise_equal(cuda, batch, graph):
+    """mnist_set_fc1_defer: F5 publishes dh and the fc1 weight gradient + SGD run in the last
+    blocks of the conv-backward launch -- the same operands, MFMA order and update as F5's folded
+    path, so 30 steps train bit for bit alike (batch 128: the deferral is declined, LDS)."""
+    from mxddp import native
+    from mxddp.engine import FusedMnistTrainer
+
+    C = native()
+    sds = []
+    try:
+        for defer in (1, 0):
+            C.mnist_set_fc1_defer(defer)
+            tr = FusedMnistTrainer(batch=batch, device=cuda, lr=0.05, use_graph=graph)
+            tr.step(30)
+            tr.synchronize()
+            sds.append((tr.state_dict(), tr.read_metrics()))
+    finally:
+        C.mnist_set_fc1_defer(0)
+    for k, v in sds[0][0].items():
+        assert torch.equal(v, sds[1][0][k]), (k, (v - sds[1][0][k]).abs().max().item())
+    assert sds[0][1] == sds[1][1]
