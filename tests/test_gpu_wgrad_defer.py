@@ -2,7 +2,9 @@
 split-K partial planes are summed by the optimizer's batched flush instead of one reduce launch
 per conv.  Same per-element arithmetic, so training is bitwise identical to the per-conv
 reductions -- PyramidNet-110 (fp32 Winograd weight gradients) and ResNet-50 (bf16 channels-last
-weight gradients), eager steps and one captured hipGraph step."""
+weight gradients), eager steps and one captured hipGraph step.  Where the model's own training is
+not bitwise reproducible (PyramidNet's fc split-K and average-pool backward use float atomics),
+the deferred run must stay within the run-to-run spread of two plain runs."""
 import copy
 
 import pytest
@@ -74,6 +76,16 @@ def _train(m0, batches, cuda, defer, dtype, graph=False):
     return flat.data.clone(), pend
 
 
+def _same_within_spread(a, b, c):
+    """a (deferred) == b (plain) bitwise when two plain runs agree bitwise; else within their spread."""
+    spread = (b - c).abs().max().item()
+    d = (a - b).abs().max().item()
+    if spread == 0.0:
+        assert d == 0.0, d
+    else:
+        assert d <= 4 * spread + 1e-7, (d, spread)
+
+
 @pytest.mark.parametrize("graph", [False, True])
 def test_pyramidnet_deferred_wgrad_bitwise(cuda, graph):
     from mxddp.models import build_model
@@ -83,8 +95,9 @@ def test_pyramidnet_deferred_wgrad_bitwise(cuda, graph):
     batches = _batches(cuda, 10, (3, 32, 32), 8, 4)
     a, pa = _train(m0, batches, cuda, True, "fp32", graph)
     b, pb = _train(m0, batches, cuda, False, "fp32", graph)
+    c, _ = _train(m0, batches, cuda, False, "fp32", graph)
     assert pa[0] > 50 and pb[0] == 0, (pa, pb)  # ~100 Winograd convs deferred their reductions
-    assert torch.equal(a, b), (a - b).abs().max().item()
+    _same_within_spread(a, b, c)
 
 
 @pytest.mark.parametrize("graph", [False, True])
@@ -96,5 +109,6 @@ def test_resnet50_bf16_deferred_wgrad_bitwise(cuda, graph):
     batches = _batches(cuda, 10, (3, 64, 64), 4, 4)
     a, pa = _train(m0, batches, cuda, True, "bf16", graph)
     b, pb = _train(m0, batches, cuda, False, "bf16", graph)
+    c, _ = _train(m0, batches, cuda, False, "bf16", graph)
     assert pa[0] > 20 and pb[0] == 0, (pa, pb)
-    assert torch.equal(a, b), (a - b).abs().max().item()
+    _same_within_spread(a, b, c)
