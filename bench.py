@@ -45,6 +45,8 @@ AB_SWITCHES = {
                                          "launch's last blocks (1) or folded into F5 (0)"),
     "wgrad_defer": ("ops.set_wgrad_defer", "layer path, world size 1: conv weight-gradient split reductions summed by "
                                            "the optimizer in batched launches (1, default) or one launch per conv (0)"),
+    "wgrad_flush_mb": ("ops.set_wgrad_flush_mb", "deferred weight-gradient reductions: flush early past this many MB of "
+                                                 "pending partial planes (0 = only at the optimizer step; default 64)"),
     "conv_tile256": ("nhwc_conv_set_glds256", "bf16 NHWC convs, 256x256-tile LDS-DMA kernel on big layers (0/1)"),
     "glds_deep": ("nhwc_conv_set_glds_deep", "bf16 NHWC convs, 128 x 128 two-stage tiles on >= 4 k-tile layers (0 off, 1 >= 192 tiles, 2 all, 3 under-filled only)"),
     "wgrad_tile256": ("nhwc_wgrad_set_tile256", "bf16 NHWC weight gradient, 256 x 256 tiles (1) or 128 x 128 (0)"),

@@ -147,6 +147,10 @@ _BANK_ON = True  # False: per-conv transforms (tests compare the two)
 # are kept alive here until the flush.
 _WGRAD_DEFER = False
 _WGRAD_KEEP: dict = {}
+# Pending partial planes are flushed early (on the backward's own stream) once they pass this
+# many bytes, so a batch is summed while its planes still sit in the Infinity Cache instead of
+# after the whole backward has pushed them out to HBM (MXDDP_WGRAD_FLUSH_MB; 0 = only at the step)
+_WGRAD_FLUSH_BYTES = int(float(os.environ.get("MXDDP_WGRAD_FLUSH_MB", "64")) * (1 << 20))
 
 
 def set_wgrad_defer(on: bool) -> None:
@@ -154,9 +158,15 @@ def set_wgrad_defer(on: bool) -> None:
     _WGRAD_DEFER = bool(on)
 
 
-def wgrad_defer_call(fn, keep, device):
+def set_wgrad_flush_mb(mb: float) -> None:
+    global _WGRAD_FLUSH_BYTES
+    _WGRAD_FLUSH_BYTES = int(float(mb) * (1 << 20))
+
+
+def wgrad_defer_call(fn, keep, device, stream=None):
     """Run one weight-gradient call that may defer its reduction; keeps `keep` (its partial
-    planes) alive until flush_wgrad(device) if it did."""
+    planes) alive until the flush if it did.  Past _WGRAD_FLUSH_BYTES of pending planes the
+    device's pending reductions are summed right away on `stream` (the call's own stream)."""
     C = native()
     C.wgrad_defer_set(True)
     try:
@@ -165,7 +175,13 @@ def wgrad_defer_call(fn, keep, device):
     finally:
         C.wgrad_defer_set(False)
     if took:
-        _WGRAD_KEEP.setdefault(device, []).append(keep)
+        ent = _WGRAD_KEEP.setdefault(device, [0, []])
+        ent[0] += keep.numel() * keep.element_size()
+        ent[1].append(keep)
+        if _WGRAD_FLUSH_BYTES > 0 and ent[0] >= _WGRAD_FLUSH_BYTES:
+            with torch.cuda.device(device):
+                C.wgrad_defer_flush(stream if stream is not None else torch.cuda.current_stream(device).cuda_stream)
+            del _WGRAD_KEEP[device]
     return out
 
 
@@ -311,7 +327,7 @@ class _Conv2d(torch.autograd.Function):
                 return C.conv2d_wgrad(dy.data_ptr(), x.data_ptr(), dw_.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph,
                                       pw, dh, dw, sink is not None, st, _p(ws), _p(db_t))
             if _WGRAD_DEFER and sink is not None and dy.is_cuda:
-                bias_done = wgrad_defer_call(_wgrad, ws, dy.device)
+                bias_done = wgrad_defer_call(_wgrad, ws, dy.device, st)
             else:
                 bias_done = _wgrad()
             if sink is not None:

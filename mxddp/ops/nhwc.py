@@ -292,7 +292,7 @@ class _Conv(torch.autograd.Function):
                 Cn.nhwc_conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), N, H, W, C, Cp, K, R, S, sh, sw, ph,
                                    pw, P, Q, sink is not None, part.data_ptr(), st)
             if _ops._WGRAD_DEFER and sink is not None:
-                _ops.wgrad_defer_call(_wgrad, part, dy.device)
+                _ops.wgrad_defer_call(_wgrad, part, dy.device, st)
             else:
                 _wgrad()
             if sink is not None:

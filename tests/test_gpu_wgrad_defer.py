@@ -33,7 +33,7 @@ def _batches(cuda, nc, shape, B, n, seed=5):
     return out
 
 
-def _train(m0, batches, cuda, defer, dtype, graph=False):
+def _train(m0, batches, cuda, defer, dtype, graph=False, flush_mb=0):
     from mxddp import native, ops
     from mxddp.optim import SGD
     from mxddp.parallel.flat import FlatParams
@@ -43,6 +43,7 @@ def _train(m0, batches, cuda, defer, dtype, graph=False):
     opt = SGD(flat, lr=0.01, momentum=0.9, weight_decay=1e-4)
     ops.set_compute_dtype(dtype)
     ops.set_wgrad_defer(defer)
+    ops.set_wgrad_flush_mb(flush_mb)  # 0: everything waits for the step (the counts below)
     pend = []
     try:
         def step(x, y):
@@ -71,6 +72,7 @@ def _train(m0, batches, cuda, defer, dtype, graph=False):
         torch.cuda.synchronize()
     finally:
         ops.set_wgrad_defer(False)
+        ops.set_wgrad_flush_mb(64)
         ops.set_compute_dtype("fp32")
     assert native().wgrad_defer_pending() == 0
     return flat.data.clone(), pend
@@ -98,6 +100,10 @@ def test_pyramidnet_deferred_wgrad_bitwise(cuda, graph):
     c, _ = _train(m0, batches, cuda, False, "fp32", graph)
     assert pa[0] > 50 and pb[0] == 0, (pa, pb)  # ~100 Winograd convs deferred their reductions
     _same_within_spread(a, b, c)
+    # early flushes inside the backward (every ~2 MB of pending planes) give the same sums
+    e, pe = _train(m0, batches, cuda, True, "fp32", graph, flush_mb=2)
+    assert pe[0] < pa[0], (pe, pa)
+    _same_within_spread(e, b, c)
 
 
 @pytest.mark.parametrize("graph", [False, True])
@@ -112,3 +118,6 @@ def test_resnet50_bf16_deferred_wgrad_bitwise(cuda, graph):
     c, _ = _train(m0, batches, cuda, False, "bf16", graph)
     assert pa[0] > 20 and pb[0] == 0, (pa, pb)
     _same_within_spread(a, b, c)
+    e, pe = _train(m0, batches, cuda, True, "bf16", graph, flush_mb=2)
+    assert pe[0] < pa[0], (pe, pa)
+    _same_within_spread(e, b, c)
