@@ -42,7 +42,8 @@ AB_SWITCHES = {
     "gk2": ("nhwc_conv_set_gk2", "bf16 NHWC convs, two-stage 128 x 128 tiles: 0 = 8 waves of 64 x 32, 1 = 64 x 64 wave "
                                  "tiles in two k-groups on 16x16x32 MFMAs, 2 = the same on 32x32x16"),
     "fc1_defer": ("mnist_set_fc1_defer", "fused MNIST, world size 1: fc1 weight gradient + SGD in the conv-backward "
-                                         "launch's last blocks (1) or folded into F5 (0)"),
+                                         "launch's last blocks, resident beside the conv blocks at three per CU (2, "
+                                         "default), after F7W's blocks at two per CU (1), or folded into F5 (0)"),
     "wgrad_defer": ("ops.set_wgrad_defer", "layer path, world size 1: conv weight-gradient split reductions summed by "
                                            "the optimizer in batched launches (1, default) or one launch per conv (0)"),
     "wgrad_flush_mb": ("ops.set_wgrad_flush_mb", "deferred weight-gradient reductions: flush early past this many MB of "

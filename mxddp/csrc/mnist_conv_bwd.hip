@@ -792,7 +792,14 @@ void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_
   MX_CHECK(!defer || (f.co_blocks == 0 && sizeof(float) * f.B * (kFc1DhP + kFc1P) <= kF6WLdsPipe),
            "deferred fc1 update: world size 1, batch <= 96");
   const dim3 grid(f.co_blocks + 2 * f.B + kF7WChunks * f.B + (defer ? kFc1Slices : 0));
-  if (f.co_blocks == 0) {
+  const size_t fc1_lds = sizeof(float) * f.B * (kFc1DhP + kFc1P);
+  if (defer && f.fc1_defer == 2 && 3 * fc1_lds <= 160 * 1024) {
+    // the single-V-buffer F6W at three blocks per CU: the fc1 blocks are resident from the start,
+    // beside the conv blocks, instead of waiting for F7W's slots
+    size_t lds = kF6WLdsSerial > kF7WLds ? kF6WLdsSerial : kF7WLds;
+    if (fc1_lds > lds) lds = fc1_lds;
+    MX_LAUNCH(f67_conv2_bwd_kernel<false>, grid, dim3(256), lds, st, f, sc);
+  } else if (f.co_blocks == 0) {
     constexpr size_t lds = kF6WLdsPipe > kF7WLds ? kF6WLdsPipe : kF7WLds;
     MX_LAUNCH(f67_conv2_bwd_kernel<true>, grid, dim3(256), lds, st, f, sc);
   } else {  // the exchange blocks need CU slots beside the conv blocks: three per CU

@@ -196,7 +196,10 @@ MnistFused MnistEngine::fused_args() const {
   // come between the gradient and the update)
   f.fc1_sgd = (variant_ == 1 && !reducer_->active()) ? 1 : 0;
   // the deferred update's blocks stage dh + a pool slice in F67's LDS: batch <= 96
-  f.fc1_defer = (f.fc1_sgd && mnist_fc1_defer() && Bp_ <= 96) ? 1 : 0;
+  // mode 2 runs F67 at three blocks per CU with the fc1 blocks' dh + pool slice in LDS: batch
+  // <= 64; mode 1 (two per CU): batch <= 96; otherwise F5 keeps the update
+  const int dm = mnist_fc1_defer();
+  f.fc1_defer = (f.fc1_sgd && ((dm == 2 && Bp_ <= 64) || (dm == 1 && Bp_ <= 96))) ? dm : 0;
   f.mom = m_;
   f.lr = lr_;
   f.sgd_mom = momentum_;

@@ -53,7 +53,9 @@ struct MnistFused {
 };
 size_t mnist_fused_scratch_floats(int B);
 void mnist_set_wt_stores(int mask);  // process-wide default of MnistFused::wt
-void mnist_set_fc1_defer(int on);    // process-wide default of MnistFused::fc1_defer (world size 1)
+// process-wide default of MnistFused::fc1_defer (world size 1): 0 off, 1 fc1 blocks after F7W's
+// in the two-block-per-CU F67, 2 the three-block-per-CU F67 (single V buffer) with them resident
+void mnist_set_fc1_defer(int mode);
 int mnist_fc1_defer();
 int mnist_wt_stores();
 

@@ -5,9 +5,12 @@
 //   F3  fc1 forward, split-K (MFMA), partials added as int64 fixed point (order-independent)
 //   F5  head (fc1 bias+ReLU, fc2, log_softmax+NLL, dlogits, fc2/fc1-bias grads, dh) recomputed in
 //       every block + fc1 dgrad/wgrad (MFMA) + ReLU/maxpool-masked dp          -> bucket 0 ready
-//       (world size 1: the fc1 SGD update is applied here, the gradient is never materialised)
+//       (world size 1: no fc1 weight gradient here -- F5 publishes dh, see F67)
 //   F67 conv2 wgrad (F6W blocks, MFMA) and conv2 dgrad + conv1 ReLU mask + conv1 wgrad (F7W
-//       blocks) in ONE launch (co-scheduled peer exchange blocks first when that strategy runs)
+//       blocks) in ONE launch (co-scheduled peer exchange blocks first when that strategy runs);
+//       world size 1: its last 192 blocks compute fc1's weight gradient and apply its SGD update
+//       (MnistFused::fc1_defer), resident beside the conv blocks at three blocks per CU, so that
+//       work left F5's critical path (default; F5 folds it in when the batch exceeds 64)
 //   F8  finalize conv grads, reset accumulators                                -> bucket 1 ready
 //       (world size > 1 only: at world size 1 its duties are folded into the SGD launch)
 //   SGD flat SGD + repack conv2 weights into the MFMA fragment orders of F2 / F7
@@ -990,8 +993,10 @@ void mnist_fused_fc1_bwd(const MnistFused& f, hipStream_t st) {
   MX_HIP_CHECK(hipGetLastError());
 }
 
-static int g_fc1_defer = 0;
-void mnist_set_fc1_defer(int on) { g_fc1_defer = on ? 1 : 0; }
+// 2 (default): MNIST driver length 933-938k -> 979-980k img/s, 2,000 steps 938k -> 985k
+// (profiles/r6_fc1defer/); 1 measured 926-930k vs 931-936k (profiles/r6_f67defer/)
+static int g_fc1_defer = 2;
+void mnist_set_fc1_defer(int mode) { g_fc1_defer = mode < 0 ? 0 : (mode > 2 ? 2 : mode); }
 int mnist_fc1_defer() { return g_fc1_defer; }
 
 void mnist_fused_sgd(const MnistFused& f, float* mom_buf, const float* lr, float gscale, float momentum, float wd,

@@ -346,8 +346,9 @@ def test_fused_engine_divergence_stays_visible(cuda):
 
 
 
-@pytest.mark.parametrize("batch,graph", [(64, True), (64, False), (37, True), (96, True), (128, True)])
-def test_deferred_fc1_update_is_bitwise_equal(cuda, batch, graph):
+@pytest.mark.parametrize("batch,graph,mode", [(64, True, 1), (64, False, 1), (37, True, 1), (96, True, 1),
+                                              (128, True, 1), (64, True, 2), (48, False, 2), (96, True, 2)])
+def test_deferred_fc1_update_is_bitwise_equal(cuda, batch, graph, mode):
     """mnist_set_fc1_defer: F5 publishes dh and the fc1 weight gradient + SGD run in the last
     blocks of the conv-backward launch -- the same operands, MFMA order and update as F5's folded
     path, so 30 steps train bit for bit alike (batch 128: the deferral is declined, LDS)."""
@@ -357,7 +358,7 @@ def test_deferred_fc1_update_is_bitwise_equal(cuda, batch, graph):
     C = native()
     sds = []
     try:
-        for defer in (1, 0):
+        for defer in (mode, 0):
             C.mnist_set_fc1_defer(defer)
             tr = FusedMnistTrainer(batch=batch, device=cuda, lr=0.05, use_graph=graph)
             tr.step(30)
