@@ -655,16 +655,18 @@ __device__ __forceinline__ void fc1_update_body(const MnistFused& f, float* sm, 
   float* ps = dhs + B * kFc1DhP;  // [B][52]
   // this lane's 24 weights and momenta (requested first: their latency overlaps the staging)
   float mb[2][3][4], pw[2][3][4];
+  if (f.fc1_sgd) {  // uniform: world size 1 updates here, otherwise only the gradient is stored
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
+      for (int c = 0; c < 3; ++c)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const size_t e = L::fw1 + (size_t)(32 * w + 16 * a + 4 * g + j) * 9216 + c0 + 16 * c + m;
-        mb[a][c][j] = f.mom[e];
-        pw[a][c][j] = f.p[e];
-      }
+        for (int j = 0; j < 4; ++j) {
+          const size_t e = L::fw1 + (size_t)(32 * w + 16 * a + 4 * g + j) * 9216 + c0 + 16 * c + m;
+          mb[a][c][j] = f.mom[e];
+          pw[a][c][j] = f.p[e];
+        }
+  }
   for (int i = tid; i < B * 32; i += 256) {
     const int r = i >> 5, c4 = (i & 31) * 4;
     *reinterpret_cast<float4*>(dhs + r * kFc1DhP + c4) = *reinterpret_cast<const float4*>(f.dh + r * 128 + c4);
@@ -692,8 +694,18 @@ __device__ __forceinline__ void fc1_update_body(const MnistFused& f, float* sm, 
       }
     }
   }
-  const float lr = *f.lr;
   const bool wt = f.wt & 1;
+  if (!f.fc1_sgd) {  // gradient collectives: the gradient goes to g (merged all-reduce, then SGD)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          st1(f.g + L::fw1 + (size_t)(32 * w + 16 * a + 4 * g + j) * 9216 + c0 + 16 * c + m, acc[a][c][j], wt);
+    return;
+  }
+  const float lr = *f.lr;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -788,7 +800,7 @@ void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_
     attr = true;
   }
   const Scratch sc = carve(f.scratch, f.B);
-  const bool defer = f.fc1_sgd && f.fc1_defer;
+  const bool defer = f.fc1_defer != 0;
   MX_CHECK(!defer || (f.co_blocks == 0 && sizeof(float) * f.B * (kFc1DhP + kFc1P) <= kF6WLdsPipe),
            "deferred fc1 update: world size 1, batch <= 96");
   const dim3 grid(f.co_blocks + 2 * f.B + kF7WChunks * f.B + (defer ? kFc1Slices : 0));

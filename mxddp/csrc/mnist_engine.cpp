@@ -198,8 +198,12 @@ MnistFused MnistEngine::fused_args() const {
   // the deferred update's blocks stage dh + a pool slice in F67's LDS: batch <= 96
   // mode 2 runs F67 at three blocks per CU with the fc1 blocks' dh + pool slice in LDS: batch
   // <= 64; mode 1 (two per CU): batch <= 96; otherwise F5 keeps the update
+  // With gradient collectives the fc1 weight gradient may move into F67 too (written to g, the
+  // update stays in the SGD launch) -- but only when nothing exchanges the fc bucket before F67
+  // ends: one merged all-reduce after the conv backward, no co-scheduled exchange.
   const int dm = mnist_fc1_defer();
-  f.fc1_defer = (f.fc1_sgd && ((dm == 2 && Bp_ <= 64) || (dm == 1 && Bp_ <= 96))) ? dm : 0;
+  const bool can = variant_ == 1 && (f.fc1_sgd || (merged_ && !co_active()));
+  f.fc1_defer = (can && ((dm == 2 && Bp_ <= 64) || (dm == 1 && Bp_ <= 96))) ? dm : 0;
   f.mom = m_;
   f.lr = lr_;
   f.sgd_mom = momentum_;

@@ -977,7 +977,7 @@ void mnist_fused_fc1_bwd(const MnistFused& f, hipStream_t st) {
   const size_t lds = sizeof(float) * ((size_t)f.B * kF5DhP + f.B * kF5P + 128 * kF5P + 128 * kF5W2P + f.B * kF5LgP + kF5Misc) +
                      (size_t)f.B * kF5Cols;
   const dim3 grid(9216 / kF5Cols), block(256);
-  const bool defer = f.fc1_sgd && f.fc1_defer;
+  const bool defer = f.fc1_defer != 0;
   void (*kfn)(MnistFused) = nullptr;
 #define F5_CASE(b)                                                                                           \
   case b:                                                                                                    \

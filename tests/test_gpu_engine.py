@@ -365,7 +365,33 @@ def test_deferred_fc1_update_is_bitwise_equal(cuda, batch, graph, mode):
             tr.synchronize()
             sds.append((tr.state_dict(), tr.read_metrics()))
     finally:
-        C.mnist_set_fc1_defer(0)
+        C.mnist_set_fc1_defer(2)
     for k, v in sds[0][0].items():
         assert torch.equal(v, sds[1][0][k]), (k, (v - sds[1][0][k]).abs().max().item())
     assert sds[0][1] == sds[1][1]
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_deferred_fc1_gradient_with_merged_allreduce(cuda, graph):
+    """With gradient collectives (forced at one rank) and the merged bucket strategy, F67's fc1
+    blocks write the fc1 weight gradient to g (the SGD launch updates): bitwise equal to F5
+    writing it, over 20 steps."""
+    from mxddp import native
+    from mxddp.engine import FusedMnistTrainer
+
+    C = native()
+    comm = C.Comm(C.Comm.new_unique_id(), 0, 1, cuda.index or 0)
+    sds = []
+    try:
+        for defer in (2, 0):
+            C.mnist_set_fc1_defer(defer)
+            tr = FusedMnistTrainer(batch=64, device=cuda, lr=0.05, comm=comm, force_collectives=True,
+                                   use_graph=graph, graph_mode=1 if graph else 0)
+            tr._set_buckets("one")
+            tr.step(20)
+            tr.synchronize()
+            sds.append(tr.state_dict())
+    finally:
+        C.mnist_set_fc1_defer(2)
+    for k, v in sds[0].items():
+        assert torch.equal(v, sds[1][k]), (k, (v - sds[1][k]).abs().max().item())
