@@ -44,6 +44,8 @@ AB_SWITCHES = {
     "fc1_defer": ("mnist_set_fc1_defer", "fused MNIST, world size 1: fc1 weight gradient + SGD in the conv-backward "
                                          "launch's last blocks, resident beside the conv blocks at three per CU (2, "
                                          "default), after F7W's blocks at two per CU (1), or folded into F5 (0)"),
+    "w2_defer": ("mlp_set_w2_defer", "fused MLP: the dW2 tile + Adam as extra resident blocks of the l1-backward "
+                                     "launch (1) or inside the l2-backward launch (0, default)"),
     "wgrad_defer": ("ops.set_wgrad_defer", "layer path, world size 1: conv weight-gradient split reductions summed by "
                                            "the optimizer in batched launches (1, default) or one launch per conv (0)"),
     "wgrad_flush_mb": ("ops.set_wgrad_flush_mb", "deferred weight-gradient reductions: flush early past this many MB of "

@@ -133,6 +133,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("mnist_set_fc1_defer", &mnist_set_fc1_defer,
         "fused MNIST, world size 1: fc1 weight gradient + SGD in the conv-backward launch's last blocks (1) or in F5 (0)");
   m.def("mnist_fc1_defer", &mnist_fc1_defer);
+  m.def("mlp_set_w2_defer", &mlp_set_w2_defer,
+        "fused MLP: the dW2 tile + update as extra resident blocks of K5 (1) or in K4 (0, default)");
+  m.def("mlp_w2_defer", &mlp_w2_defer);
   m.def("mnist_set_wt_stores", &mnist_set_wt_stores,
         "MNIST bulk stores with agent scope (L2 write-through) for steps launched afterwards: mask 1 = F5, 2 = F2, "
         "4 = F6W");

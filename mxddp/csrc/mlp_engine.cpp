@@ -105,6 +105,7 @@ MlpFused MlpEngine::args() const {
   f.seed = seed_ + rank * 7919ull;  // per-rank data shard
   f.synth = external_ ? 0 : 1;
   f.fused_adam = reducer_->active() ? 0 : 1;
+  f.w2_defer = mlp_w2_defer() && (f.fused_adam || merged_) ? 1 : 0;  // bucket 0 is not ready after K4 otherwise
   return f;
 }
 

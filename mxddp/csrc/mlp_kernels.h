@@ -45,10 +45,17 @@ struct MlpFused {
   int32_t* adam_state;  // {completed steps, step being applied}: see ops_optim.hip adam_k
   float b1, b2, eps, wd;
   int eps_hat;
+  // 1: the dW2 tile + its update run as extra resident blocks of K5 (not in K4), shortening the
+  // dgrad chain K4 -> K5; set by the engine when the l2 gradient need not be ready after K4
+  int w2_defer;
 };
 
 void mlp_fused_forward(const MlpFused& f, hipStream_t st);    // K1, K2, K3
 void mlp_fused_backward2(const MlpFused& f, hipStream_t st);  // K4: l2 / l3 gradients (+ Adam) -> bucket 0
 void mlp_fused_backward1(const MlpFused& f, hipStream_t st);  // K5: l1 gradients (+ Adam)      -> bucket 1
+// process-wide switch of MlpFused::w2_defer (default off; the engine applies it with fused Adam
+// or a single merged gradient bucket)
+void mlp_set_w2_defer(int on);
+int mlp_w2_defer();
 
 }  // namespace mx

@@ -128,6 +128,56 @@ def test_fused_mlp_deterministic_and_graph_equals_eager(cuda):
         assert torch.equal(sa[k], sb[k]) and torch.equal(sa[k], sc[k]), k
 
 
+@pytest.mark.parametrize("B", [64, 16, 200, 512])
+@pytest.mark.parametrize("graph", [True, False])
+def test_w2_update_in_k5_is_bitwise_equal(cuda, graph, B):
+    """mlp_set_w2_defer: the dW2 tile + Adam run as extra resident blocks of K5 (K4 keeps the
+    dgrad) -- the same operands and MFMA sequence as K4's folded path, so 12 steps train bit for
+    bit alike (200 / 512: several LDS passes in both places)."""
+    from mxddp import native
+    from mxddp.mlp_engine import FusedMlpTrainer
+
+    C = native()
+    assert C.mlp_w2_defer() == 0
+    runs = []
+    try:
+        for on in (1, 0):
+            C.mlp_set_w2_defer(on)
+            t = FusedMlpTrainer(batch=B, device=cuda, lr=1e-3, use_graph=graph)
+            t.step(12)
+            runs.append((t.state_dict(), t.read_metrics()))
+    finally:
+        C.mlp_set_w2_defer(0)
+    for k, v in runs[0][0].items():
+        assert torch.equal(v, runs[1][0][k]), (k, (v - runs[1][0][k]).abs().max().item())
+    assert runs[0][1] == runs[1][1]
+
+
+@pytest.mark.parametrize("merged", [True, False])
+def test_w2_gradient_in_k5_with_collectives(cuda, merged):
+    """With gradient collectives forced at one rank: the merged bucket lets K5's W2 blocks write
+    the l2 gradient (bitwise equal to K4 writing it); the two-bucket strategy keeps it in K4 (its
+    bucket is all-reduced while K5 runs)."""
+    from mxddp import native
+    from mxddp.mlp_engine import FusedMlpTrainer
+
+    C = native()
+    comm = C.Comm(C.Comm.new_unique_id(), 0, 1, cuda.index or 0)
+    sds = []
+    try:
+        for on in (1, 0):
+            C.mlp_set_w2_defer(on)
+            t = FusedMlpTrainer(batch=32, device=cuda, lr=1e-3, comm=comm, force_collectives=True, use_graph=False)
+            t._set_buckets("one" if merged else "ovl")
+            t.step(8)
+            t.synchronize()
+            sds.append(t.state_dict())
+    finally:
+        C.mlp_set_w2_defer(0)
+    for k, v in sds[0].items():
+        assert torch.equal(v, sds[1][k]), (k, (v - sds[1][k]).abs().max().item())
+
+
 def test_fused_mlp_trains_on_device_stream(cuda):
     from mxddp.mlp_engine import FusedMlpTrainer
 
