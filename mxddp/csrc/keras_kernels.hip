@@ -743,8 +743,24 @@ __device__ void kb1_role_e(const KerasFused& f, SmemE& sm) {
   for (int n0 = 0; n0 < f.B; n0 += 64) {
     const int nb = f.B - n0 < 64 ? f.B - n0 : 64;
     __syncthreads();
-    for (int i = tid; i < nb * 16; i += 256) sm.dl[i] = f.dl[(size_t)n0 * 16 + i];
-    for (int i = tid; i < nb * 64; i += 256) sm.h1[i] = f.h1[(size_t)n0 * 64 + i];
+    {  // dl [nb][16] + h1 [nb][64] as float4s, all five of a thread's loads before its stores (a
+       // scalar `load; store` loop was 20 serial memory round trips); clamped, not predicated:
+       // past the end a thread rewrites the last float4
+      const int n4d = nb * 4, n4h = nb * 16;
+      const float4* dsrc = reinterpret_cast<const float4*>(f.dl + (size_t)n0 * 16);
+      const float4* hsrc = reinterpret_cast<const float4*>(f.h1 + (size_t)n0 * 64);
+      const int id = min(tid, n4d - 1);
+      int ih[4];
+      float4 hv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ih[u] = min(tid + 256 * u, n4h - 1);
+      const float4 dv = dsrc[id];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) hv[u] = hsrc[ih[u]];
+      reinterpret_cast<float4*>(sm.dl)[id] = dv;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) reinterpret_cast<float4*>(sm.h1)[ih[u]] = hv[u];
+    }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -763,7 +779,7 @@ __device__ void kb1_role_e(const KerasFused& f, SmemE& sm) {
 }
 
 __global__ __launch_bounds__(256) void kb1_kernel(KerasFused f) {
-  __shared__ SmemKB1 sm;
+  __shared__ __attribute__((aligned(16))) SmemKB1 sm;
   const int b = blockIdx.x, B = f.B;
   if (b < 8 * B) {
     kb1_role_a(f, sm.a, b);
@@ -809,19 +825,24 @@ __device__ __forceinline__ void pack_w2(const KerasFused& f, int i, float val) {
 }
 
 // Adam (gradient gr already summed / averaged by gscale) + conv2 repack of parameter i
-__device__ __forceinline__ void adam_one(const KerasFused& f, int i, float gr, int t, float gscale) {
-  float pv = f.p[i];
+// (p, m, v, lr: the caller's values, loaded before the gradient planes -- loaded here they were
+// up to three serial memory round trips after the plane sum)
+__device__ __forceinline__ void adam_one(const KerasFused& f, int i, float gr, int t, float gscale, float pv, float m0,
+                                         float v0, float lr) {
   gr = gr * gscale + f.wd * pv;
   const float bc1 = 1.f - powf(f.b1, (float)t), bc2 = 1.f - powf(f.b2, (float)t);
   const float bc2s = sqrtf(bc2);
   const float e = f.eps_hat ? f.eps / bc2s : f.eps;
-  const float mi = f.b1 * f.m[i] + (1.f - f.b1) * gr;
-  const float vi = f.b2 * f.v[i] + (1.f - f.b2) * gr * gr;
+  const float mi = f.b1 * m0 + (1.f - f.b1) * gr;
+  const float vi = f.b2 * v0 + (1.f - f.b2) * gr * gr;
   f.m[i] = mi;
   f.v[i] = vi;
-  pv -= (*f.lr / bc1) * mi / (sqrtf(vi) / bc2s + e);
+  pv -= (lr / bc1) * mi / (sqrtf(vi) / bc2s + e);
   f.p[i] = pv;
   if (i >= (int)L::w2 && i < (int)L::b2) pack_w2(f, i, pv);
+}
+__device__ __forceinline__ void adam_one(const KerasFused& f, int i, float gr, int t, float gscale) {
+  adam_one(f, i, gr, t, gscale, f.p[i], f.m[i], f.v[i], *f.lr);
 }
 
 __global__ __launch_bounds__(256) void ko_kernel(KerasFused f, KoPlan plan, int mode, float gscale) {
@@ -844,6 +865,14 @@ __global__ __launch_bounds__(256) void ko_kernel(KerasFused f, KoPlan plan, int 
   // ~1,450 same-address atomics: most of this kernel's 41 us.)
   int t = 0;
   if (adam) t = __hip_atomic_load(f.adam_state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  float pv = 0.f, m0 = 0.f, v0 = 0.f, lr = 0.f;
+  if (adam && q == 0) {  // the update's operands, in flight with the first round of planes
+    const int ic = live ? i : R.p0;
+    pv = f.p[ic];
+    m0 = f.m[ic];
+    v0 = f.v[ic];
+    lr = *f.lr;
+  }
   float gr = 0.f;
   if (mode != 3) {
     // this thread's planes k = q, q + T, ... (fixed order), 8 loads in flight per round
@@ -868,7 +897,7 @@ __global__ __launch_bounds__(256) void ko_kernel(KerasFused f, KoPlan plan, int 
   }
   if (live && q == 0) {
     if (mode == 1) f.g[i] = gr;
-    else if (adam) adam_one(f, i, gr, t, gscale);
+    else if (adam) adam_one(f, i, gr, t, gscale, pv, m0, v0, lr);
     else if (i >= (int)L::w2 && i < (int)L::b2) pack_w2(f, i, f.p[i]);  // mode 3
   }
   if (adam && b == 0 && tid == 0) __hip_atomic_store(f.adam_state + 1, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -667,11 +667,38 @@ __device__ __forceinline__ void fc1_update_body(const MnistFused& f, float* sm, 
           pw[a][c][j] = f.p[e];
         }
   }
-  for (int i = tid; i < B * 32; i += 256) {
+  // dh [B][128] and the pool slice [B][48]: 8 + 3 float4 per thread at batch 64 (mode 2 takes
+  // B <= 64), every load issued before the first LDS store -- a `load; store` loop pays one memory
+  // round trip per float4.  Indices are clamped, not predicated (a predicated store lets the
+  // compiler sink its load into the branch); past the end a thread rewrites the last element.
+  constexpr int kDU = 8, kPU = 3;
+  const int nd = B * 32, np = B * 12;
+  float4 dv[kDU], pv4[kPU];
+#pragma unroll
+  for (int u = 0; u < kDU; ++u) {
+    const int i = min(tid + 256 * u, nd - 1);
+    dv[u] = *reinterpret_cast<const float4*>(f.dh + (i >> 5) * 128 + (i & 31) * 4);
+  }
+#pragma unroll
+  for (int u = 0; u < kPU; ++u) {
+    const int i = min(tid + 256 * u, np - 1), r = i / 12;
+    pv4[u] = *reinterpret_cast<const float4*>(f.pool + (size_t)r * 9216 + c0 + (i - r * 12) * 4);
+  }
+#pragma unroll
+  for (int u = 0; u < kDU; ++u) {
+    const int i = min(tid + 256 * u, nd - 1);
+    *reinterpret_cast<float4*>(dhs + (i >> 5) * kFc1DhP + (i & 31) * 4) = dv[u];
+  }
+#pragma unroll
+  for (int u = 0; u < kPU; ++u) {
+    const int i = min(tid + 256 * u, np - 1), r = i / 12;
+    *reinterpret_cast<float4*>(ps + r * kFc1P + (i - r * 12) * 4) = pv4[u];
+  }
+  for (int i = tid + 256 * kDU; i < nd; i += 256) {  // B > 64 (mode 1): the rest
     const int r = i >> 5, c4 = (i & 31) * 4;
     *reinterpret_cast<float4*>(dhs + r * kFc1DhP + c4) = *reinterpret_cast<const float4*>(f.dh + r * 128 + c4);
   }
-  for (int i = tid; i < B * 12; i += 256) {
+  for (int i = tid + 256 * kPU; i < np; i += 256) {
     const int r = i / 12, c4 = (i - r * 12) * 4;
     *reinterpret_cast<float4*>(ps + r * kFc1P + c4) = *reinterpret_cast<const float4*>(f.pool + (size_t)r * 9216 + c0 + c4);
   }
