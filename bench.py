@@ -48,6 +48,8 @@ AB_SWITCHES = {
                                      "launch (1) or inside the l2-backward launch (0, default)"),
     "wgrad_defer": ("ops.set_wgrad_defer", "layer path, world size 1: conv weight-gradient split reductions summed by "
                                            "the optimizer in batched launches (1, default) or one launch per conv (0)"),
+    "bn_fold": ("ops.set_bn_fold", "PyramidNet: BN normalise pass folded into the next Winograd conv's input staging "
+                                   "(1) or run as its own pass (0, default)"),
     "wgrad_flush_mb": ("ops.set_wgrad_flush_mb", "deferred weight-gradient reductions: flush early past this many MB of "
                                                  "pending partial planes (0 = only at the optimizer step; default 64)"),
     "conv_tile256": ("nhwc_conv_set_glds256", "bf16 NHWC convs, 256x256-tile LDS-DMA kernel on big layers (0/1)"),

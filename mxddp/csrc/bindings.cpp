@@ -34,14 +34,16 @@ PYBIND11_MODULE(_C, m) {
   // ---------------------------------------------------------------- GEMM-shaped ops
   m.def("conv2d_fwd", [](uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y, int N, int C, int H, int W, int K, int R,
                          int S_, int sh, int sw, int ph, int pw, int dh, int dw, bool relu, uintptr_t st,
-                         uintptr_t scratch, uintptr_t dgrad_filters, bool pretransformed) {
+                         uintptr_t scratch, uintptr_t dgrad_filters, bool pretransformed, uintptr_t in_ss,
+                         bool in_relu) {
     conv2d_fwd(P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y),
                CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw), relu, S(st), P<float>(scratch),
-               P<float>(dgrad_filters), pretransformed);
+               P<float>(dgrad_filters), pretransformed, P<const float>(in_ss), in_relu);
   }, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("y"), py::arg("N"), py::arg("C"), py::arg("H"), py::arg("W"),
      py::arg("K"), py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
      py::arg("dh"), py::arg("dw"), py::arg("relu"), py::arg("st"), py::arg("scratch") = 0,
-     py::arg("dgrad_filters") = 0, py::arg("pretransformed") = false);
+     py::arg("dgrad_filters") = 0, py::arg("pretransformed") = false, py::arg("in_ss") = 0,
+     py::arg("in_relu") = false);
   m.def("conv_fwd_filter_floats", [](int N, int C, int H, int W, int K, int R, int S_, int sh, int sw, int ph,
                                      int pw, int dh, int dw) {
     return conv_fwd_filter_floats(CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw));
@@ -75,12 +77,14 @@ PYBIND11_MODULE(_C, m) {
      py::arg("pretransformed") = false);
   m.def("conv2d_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw_, int N, int C, int H, int W, int K, int R, int S_,
                            int sh, int sw, int ph, int pw, int dh, int dw, bool acc, uintptr_t st,
-                           uintptr_t scratch, uintptr_t db) {
+                           uintptr_t scratch, uintptr_t db, uintptr_t in_ss, bool in_relu) {
     return conv2d_wgrad(P<const float>(dy), P<const float>(x), P<float>(dw_),
-                        CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw), acc, S(st), P<float>(scratch), P<float>(db));
+                        CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw), acc, S(st), P<float>(scratch), P<float>(db),
+                        P<const float>(in_ss), in_relu);
   }, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("N"), py::arg("C"), py::arg("H"), py::arg("W"), py::arg("K"),
      py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"),
-     py::arg("dwd"), py::arg("acc"), py::arg("st"), py::arg("scratch") = 0, py::arg("db") = 0);
+     py::arg("dwd"), py::arg("acc"), py::arg("st"), py::arg("scratch") = 0, py::arg("db") = 0, py::arg("in_ss") = 0,
+     py::arg("in_relu") = false);
   m.def("conv_wgrad_scratch_floats", [](int N, int C, int H, int W, int K, int R, int S_, int sh, int sw, int ph,
                                         int pw, int dh, int dw) {
     return conv_wgrad_scratch_floats(CS(N, C, H, W, K, R, S_, sh, sw, ph, pw, dh, dw));
@@ -257,13 +261,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_splits", &bn_splits);
   m.def("bn_fwd_train", [](uintptr_t x, uintptr_t g, uintptr_t b, uintptr_t y, uintptr_t mean, uintptr_t invstd,
                            uintptr_t rm, uintptr_t rv, int N, int C, int HW, float mom, float eps, bool relu,
-                           uintptr_t part, uintptr_t st, uintptr_t nbt, uintptr_t res, int res_C) {
+                           uintptr_t part, uintptr_t st, uintptr_t nbt, uintptr_t res, int res_C, uintptr_t ss) {
     bn_fwd_train(P<const float>(x), P<const float>(g), P<const float>(b), P<float>(y), P<float>(mean), P<float>(invstd),
                  P<float>(rm), P<float>(rv), N, C, HW, mom, eps, relu, P<float>(part), S(st), P<int64_t>(nbt),
-                 P<const float>(res), res_C);
+                 P<const float>(res), res_C, P<float>(ss));
   }, py::arg("x"), py::arg("g"), py::arg("b"), py::arg("y"), py::arg("mean"), py::arg("invstd"), py::arg("rm"),
      py::arg("rv"), py::arg("N"), py::arg("C"), py::arg("HW"), py::arg("mom"), py::arg("eps"), py::arg("relu"),
-     py::arg("part"), py::arg("st"), py::arg("num_batches") = 0, py::arg("residual") = 0, py::arg("residual_C") = 0);
+     py::arg("part"), py::arg("st"), py::arg("num_batches") = 0, py::arg("residual") = 0, py::arg("residual_C") = 0,
+     py::arg("ss") = 0);
   m.def("bn_partial_floats", &bn_partial_floats);
   m.def("bn_fwd_eval", [](uintptr_t x, uintptr_t g, uintptr_t b, uintptr_t y, uintptr_t rm, uintptr_t rv, int N, int C,
                           int HW, float eps, bool relu, uintptr_t st) {
@@ -272,13 +277,13 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("bn_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t yr, uintptr_t g, uintptr_t mean, uintptr_t invstd,
                      uintptr_t dx, uintptr_t dg, uintptr_t db, int N, int C, int HW, bool acc, uintptr_t part,
-                     uintptr_t st, uintptr_t extra, int extra_C) {
+                     uintptr_t st, uintptr_t extra, int extra_C, uintptr_t ssm) {
     bn_bwd(P<const float>(dy), P<const float>(x), P<const float>(yr), P<const float>(g), P<const float>(mean),
            P<const float>(invstd), P<float>(dx), P<float>(dg), P<float>(db), N, C, HW, acc, P<float>(part), S(st),
-           P<const float>(extra), extra_C);
+           P<const float>(extra), extra_C, P<const float>(ssm));
   }, py::arg("dy"), py::arg("x"), py::arg("yr"), py::arg("g"), py::arg("mean"), py::arg("invstd"), py::arg("dx"),
      py::arg("dg"), py::arg("db"), py::arg("N"), py::arg("C"), py::arg("HW"), py::arg("acc"), py::arg("part"),
-     py::arg("st"), py::arg("extra") = 0, py::arg("extra_C") = 0);
+     py::arg("st"), py::arg("extra") = 0, py::arg("extra_C") = 0, py::arg("ssm") = 0);
   m.def("shortcut_pad_add", [](uintptr_t x, uintptr_t y, int N, int Cin, int H, int W, int Cout, int P_, int Q,
                                int stride, uintptr_t st) {
     shortcut_pad_add(P<const float>(x), P<float>(y), N, Cin, H, W, Cout, P_, Q, stride, S(st));

@@ -27,9 +27,11 @@ struct ConvShape {
 // dgrad_filters (optional, conv_dgrad_filter_floats(s) floats; 0 = not applicable): the forward
 // also prepares the filters the Winograd data gradient will use (pass them to conv2d_dgrad with
 // pretransformed = true)
+// in_ss (optional, [C][2]): the input is a folded BN's output, relu?(x * scale[c] + shift[c]),
+// formed while the input tile is staged (Winograd path only; padding stays zero)
 void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s,
                 bool relu, hipStream_t st, float* scratch = nullptr, float* dgrad_filters = nullptr,
-                bool pretransformed = false);
+                bool pretransformed = false, const float* in_ss = nullptr, bool in_relu = false);
 size_t conv_dgrad_filter_floats(const ConvShape& s);
 // forward Winograd filter floats (0 = this conv does not run the Winograd path)
 size_t conv_fwd_filter_floats(const ConvShape& s);
@@ -53,7 +55,8 @@ size_t wino_scratch_floats(const ConvShape& s);
 // U_dgrad_out (optional, wino_dgrad_filter_floats(s)): also write the data-gradient filters
 // pretransformed: `scratch` already holds the forward filters (WinoFilterBank / an earlier call)
 void wino_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s, bool relu,
-              float* scratch, hipStream_t st, float* U_dgrad_out = nullptr, bool pretransformed = false);
+              float* scratch, hipStream_t st, float* U_dgrad_out = nullptr, bool pretransformed = false,
+              const float* in_ss = nullptr, bool in_relu = false);
 size_t wino_dgrad_filter_floats(const ConvShape& s);
 size_t wino_fwd_filter_floats(const ConvShape& s);
 // Persistent Winograd filters of many 3x3 convs, re-transformed by ONE launch per <= 64 convs
@@ -80,7 +83,7 @@ void wino_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s, 
 // partial-sum scratch: wino_wgrad_scratch_floats(s) floats (0 = none needed)
 size_t wino_wgrad_scratch_floats(const ConvShape& s);
 void wino_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate, float* scratch,
-                hipStream_t st);
+                hipStream_t st, const float* in_ss = nullptr, bool in_relu = false);
 // 3x3 s1 algorithm: 0 = auto (Winograd where eligible, else direct-LDS), 1 = direct-LDS only.
 void set_conv_algo(int a);
 int conv_algo();
@@ -89,8 +92,10 @@ size_t conv_scratch_floats(const ConvShape& s);
 // dw (+)= sum_{n,p,q} dy * im2col(x)
 // db (optional): the bias gradient sum_{n,p,q} dy is produced by the same GEMM (an extra column of
 // ones) where the generic path runs; returns whether it did (else the caller runs bias_grad)
+// in_ss: as conv2d_fwd's (the input recomputed from the folded BN's input; Winograd path only)
 bool conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate,
-                  hipStream_t st, float* scratch = nullptr, float* db = nullptr);
+                  hipStream_t st, float* scratch = nullptr, float* db = nullptr, const float* in_ss = nullptr,
+                  bool in_relu = false);
 size_t conv_wgrad_scratch_floats(const ConvShape& s);
 // y[M,N] = x[M,K] @ w[N,K]^T + b  (optional ReLU)
 void linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int N, int K,
@@ -155,14 +160,20 @@ void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* 
                   float* invstd, float* run_mean, float* run_var, int N, int C, int HW,
                   float momentum, float eps, bool relu, float* part, hipStream_t st,
                   int64_t* num_batches = nullptr,  // num_batches: += 1 on device
-                  const float* residual = nullptr, int residual_C = 0);  // y[:, :Cr] += residual
+                  const float* residual = nullptr, int residual_C = 0,  // y[:, :Cr] += residual
+                  // y == nullptr: no apply pass -- the statistics and the per-channel (scale, shift)
+                  // pairs [C][2] go to ss_out for a convolution that applies them to its input
+                  float* ss_out = nullptr);
 void bn_fwd_eval(const float* x, const float* gamma, const float* beta, float* y,
                  const float* run_mean, const float* run_var, int N, int C, int HW, float eps,
                  bool relu, hipStream_t st);
 void bn_bwd(const float* dy, const float* x, const float* y_relu, const float* gamma,
             const float* mean, const float* invstd, float* dx, float* dgamma, float* dbeta, int N,
             int C, int HW, bool accumulate_params, float* part, hipStream_t st,
-            const float* extra = nullptr, int extra_C = 0);  // dx += extra[:, :C] ([N][extra_C][HW])
+            const float* extra = nullptr, int extra_C = 0,  // dx += extra[:, :C] ([N][extra_C][HW])
+            // the fused ReLU's mask recomputed from x and the forward's (scale, shift) pairs
+            // (y_relu == nullptr: the output was never stored)
+            const float* ss_mask = nullptr);
 
 // PyramidNet shortcut: y[n,c,:,:] += (c < Cin ? pool(x)[n,c] : 0); pool = 2x2 avg, ceil.
 void shortcut_pad_add(const float* x, float* y, int N, int Cin, int H, int W, int Cout, int P, int Q,

@@ -92,6 +92,17 @@ __device__ __forceinline__ BnChunk bn_chunk(int i0, int total, const Slice& sl, 
   return k;
 }
 
+// The fused ReLU's mask of a BN whose output was never stored (its apply folded into the next
+// convolution's input staging, ops.bn_conv): recomputed from x with the forward's exact
+// fmaf(x, sc, sh), so it is bit for bit the mask of the values the convolution consumed.
+__device__ __forceinline__ float4 mask_from_x(float4 g, const float4& v, float2 t) {
+  g.x = fmaf(v.x, t.x, t.y) > 0.f ? g.x : 0.f;
+  g.y = fmaf(v.y, t.x, t.y) > 0.f ? g.y : 0.f;
+  g.z = fmaf(v.z, t.x, t.y) > 0.f ? g.z : 0.f;
+  g.w = fmaf(v.w, t.x, t.y) > 0.f ? g.w : 0.f;
+  return g;
+}
+
 // ------------------------------------------------------------------ forward statistics
 template <bool VEC>
 __global__ __launch_bounds__(kBnTB) void bn_stats_k(const float* __restrict__ x, int N, int C, int HW, int S, FastDiv dv,
@@ -137,11 +148,12 @@ template <bool VEC>
 __global__ __launch_bounds__(kBnTB) void bn_bwd_reduce_k(const float* __restrict__ dy, const float* __restrict__ x,
                                                          const float* __restrict__ yr, const float* __restrict__ mean,
                                                          int N, int C, int HW, int S, FastDiv dv,
-                                                         float* __restrict__ part) {
+                                                         float* __restrict__ part, const float2* __restrict__ ssm) {
   __shared__ float red[2 * kBnTB / 64];
   const int s = blockIdx.x, c = blockIdx.y;
   const Slice sl = slice_of(s, S, N);
   const float mu = mean[c];
+  const float2 mt = ssm ? ssm[c] : make_float2(0.f, 0.f);  // ssm: the ReLU mask from x (mask_from_x)
   float s1 = 0.f, s2 = 0.f;
   if (VEC) {
     const int hw4 = HW >> 2;
@@ -170,6 +182,8 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_reduce_k(const float* __restrict
           g[u].y = r[u].y > 0.f ? g[u].y : 0.f;
           g[u].z = r[u].z > 0.f ? g[u].z : 0.f;
           g[u].w = r[u].w > 0.f ? g[u].w : 0.f;
+        } else if (ssm) {
+          g[u] = mask_from_x(g[u], v[u], mt);
         }
         s1 += (g[u].x + g[u].y) + (g[u].z + g[u].w);
         s2 = fmaf(g[u].x, v[u].x - mu,
@@ -183,6 +197,7 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_reduce_k(const float* __restrict
       const size_t o = ((size_t)n * C + c) * HW + j;
       float g = dy[o];
       if (yr && !(yr[o] > 0.f)) g = 0.f;
+      if (!yr && ssm && !(fmaf(x[o], mt.x, mt.y) > 0.f)) g = 0.f;
       s1 += g;
       s2 = fmaf(g, x[o] - mu, s2);
     }
@@ -205,7 +220,10 @@ __global__ __launch_bounds__(kBnTB) void bn_apply_slice_k(const float* __restric
                                                           float* __restrict__ y, int N, int C, int HW, int S, FastDiv dv,
                                                           float cnt, float eps, float momentum, int relu,
                                                           int64_t* __restrict__ num_batches,
-                                                          const float* __restrict__ res, int Cr) {
+                                                          const float* __restrict__ res, int Cr,
+                                                          float2* __restrict__ ss_out) {
+  // y == nullptr (the apply folded into the next convolution, ops.bn_conv): a (1, C) grid that
+  // only finalizes -- the statistics and the per-channel (scale, shift) into ss_out
   __shared__ float red[2 * kBnTB / 64];
   const int s = blockIdx.x, c = blockIdx.y;
   if (s == 0 && c == 0 && num_batches && threadIdx.x == 0) *num_batches += 1;
@@ -218,7 +236,7 @@ __global__ __launch_bounds__(kBnTB) void bn_apply_slice_k(const float* __restric
   float4* y4 = reinterpret_cast<float4*>(y);
   BnChunk k0{};
   float4 v0[kBnU], q0[kBnU];
-  if (VEC && threadIdx.x < total4) {  // first chunk requested before the partials are read
+  if (VEC && y && threadIdx.x < total4) {  // first chunk requested before the partials are read
     k0 = bn_chunk(threadIdx.x, total4, sl, hw4, C, c, Cr, dv);
 #pragma unroll
     for (int u = 0; u < kBnU; ++u) {
@@ -238,7 +256,9 @@ __global__ __launch_bounds__(kBnTB) void bn_apply_slice_k(const float* __restric
     invstd_out[c] = inv;
     if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
     if (run_var) run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
+    if (ss_out) ss_out[c] = make_float2(sc, sh);
   }
+  if (!y) return;
   if (VEC) {
     auto apply = [&](const BnChunk& k, const float4 (&v)[kBnU], const float4 (&q)[kBnU]) {
 #pragma unroll
@@ -293,10 +313,12 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_apply_slice_k(
     const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ yr,
     const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ part, float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dx, int N,
-    int C, int HW, int S, FastDiv dv, float cnt, int acc_params, const float* __restrict__ extra, int extC) {
+    int C, int HW, int S, FastDiv dv, float cnt, int acc_params, const float* __restrict__ extra, int extC,
+    const float2* __restrict__ ssm) {
   __shared__ float red[2 * kBnTB / 64];
   const int s = blockIdx.x, c = blockIdx.y;
   const Slice sl = slice_of(s, S, N);
+  const float2 mt = ssm ? ssm[c] : make_float2(0.f, 0.f);  // ssm: the ReLU mask from x (mask_from_x)
   // extra: a second gradient of x added to dx (the residual branch's, read in place from the
   // block output gradient [N][extC][HW], channels 0..C-1), instead of a separate add launch
   const float* ec = extra ? extra + (size_t)c * HW : nullptr;
@@ -343,6 +365,8 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_apply_slice_k(
           gg.y = r[u].y > 0.f ? gg.y : 0.f;
           gg.z = r[u].z > 0.f ? gg.z : 0.f;
           gg.w = r[u].w > 0.f ? gg.w : 0.f;
+        } else if (ssm) {
+          gg = mask_from_x(gg, v[u], mt);
         }
         float4 out;
         out.x = fmaf(A, gg.x, fmaf(D, v[u].x, Bc));
@@ -384,6 +408,7 @@ __global__ __launch_bounds__(kBnTB) void bn_bwd_apply_slice_k(
       const size_t o = ((size_t)n * C + c) * HW + j;
       float g = dy[o];
       if (yr && !(yr[o] > 0.f)) g = 0.f;
+      if (!yr && ssm && !(fmaf(x[o], mt.x, mt.y) > 0.f)) g = 0.f;
       dx[o] = fmaf(A, g, fmaf(D, x[o], Bc)) + (ec ? ec[(size_t)n * extC * HW + j] : 0.f);
     }
   }
@@ -446,7 +471,8 @@ __global__ __launch_bounds__(kBnF) void bn_fwd_fused_k(const float* __restrict__
                                                       float* __restrict__ run_mean, float* __restrict__ run_var, int N,
                                                       int C, int HW, FastDiv dv, float eps, float momentum, int relu,
                                                       int64_t* __restrict__ num_batches, const float* __restrict__ res,
-                                                      int Cr) {
+                                                      int Cr, float2* __restrict__ ss_out) {
+  // y == nullptr: statistics and (scale, shift) only (the apply folded into the next convolution)
   __shared__ float red[2 * kBnF / 64];
   const int c = blockIdx.x, hw4 = HW >> 2, total = N * hw4;
   if (c == 0 && num_batches && threadIdx.x == 0) *num_batches += 1;
@@ -483,7 +509,9 @@ __global__ __launch_bounds__(kBnF) void bn_fwd_fused_k(const float* __restrict__
     invstd_out[c] = inv;
     if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
     if (run_var) run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
+    if (ss_out) ss_out[c] = make_float2(sc, sh);
   }
+  if (!y) return;
   float4* y4 = reinterpret_cast<float4*>(y);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -515,7 +543,8 @@ __global__ __launch_bounds__(kBnF) void bn_bwd_fused_k(const float* __restrict__
                                                       const float* __restrict__ mean, const float* __restrict__ invstd,
                                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                       float* __restrict__ dx, int N, int C, int HW, FastDiv dv,
-                                                      int acc_params, const float* __restrict__ extra, int extC) {
+                                                      int acc_params, const float* __restrict__ extra, int extC,
+                                                      const float2* __restrict__ ssm) {
   __shared__ float red[2 * kBnF / 64];
   const int c = blockIdx.x, hw4 = HW >> 2, total = N * hw4;
   size_t o[U], so[U];
@@ -549,6 +578,10 @@ __global__ __launch_bounds__(kBnF) void bn_bwd_fused_k(const float* __restrict__
       g[u].z = r[u].z > 0.f ? g[u].z : 0.f;
       g[u].w = r[u].w > 0.f ? g[u].w : 0.f;
     }
+  } else if (ssm) {  // the ReLU mask from x (mask_from_x)
+    const float2 mt = ssm[c];
+#pragma unroll
+    for (int u = 0; u < U; ++u) g[u] = mask_from_x(g[u], v[u], mt);
   }
   const float mu = mean[c], inv = invstd[c];
   float s1 = 0.f, s2 = 0.f;
@@ -615,15 +648,17 @@ size_t bn_partial_floats(int N, int C, int HW) { return 2 * (size_t)bn_splits(N,
 
 void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* invstd,
                   float* run_mean, float* run_var, int N, int C, int HW, float momentum, float eps, bool relu,
-                  float* part, hipStream_t st, int64_t* num_batches, const float* res, int Cr) {
+                  float* part, hipStream_t st, int64_t* num_batches, const float* res, int Cr, float* ss_out) {
   MX_CHECK((int64_t)N * C * HW < (1ll << 31), "bn: tensor too large for 32-bit index math");
+  MX_CHECK(y || (ss_out && !res), "bn: without an output, (scale, shift) must be requested and no residual");
+  float2* ss2 = reinterpret_cast<float2*>(ss_out);
   const int S = bn_splits(N, C, HW);
   MX_CHECK(S <= 4 * kBnTB, "bn: too many splits");
   MX_CHECK(!res || (Cr > 0 && Cr <= C), "bn: residual channels must be in 1..C");
   if (bn_use_fused(N, C, HW)) {
 #define MX_BN_FWD(U_)                                                                                            \
   MX_LAUNCH(bn_fwd_fused_k<U_>, dim3(C), dim3(kBnF), 0, st, x, gamma, beta, y, mean, invstd, run_mean, run_var, N, C, \
-            HW, FastDiv(HW / 4), eps, momentum, relu ? 1 : 0, num_batches, res, Cr)
+            HW, FastDiv(HW / 4), eps, momentum, relu ? 1 : 0, num_batches, res, Cr, ss2)
     switch (bn_fused_u(N, HW)) {
       case 1: MX_BN_FWD(1); break;
       case 2: MX_BN_FWD(2); break;
@@ -636,28 +671,31 @@ void bn_fwd_train(const float* x, const float* gamma, const float* beta, float* 
   const bool vec = HW % 4 == 0;
   const FastDiv dv(vec ? HW / 4 : HW);
   const float cnt = (float)N * (float)HW;
+  const dim3 ga(y ? S : 1, C);  // no output: one finalizing block per channel
   if (vec) {
     MX_LAUNCH(bn_stats_k<true>, dim3(S, C), dim3(kBnTB), 0, st, x, N, C, HW, S, dv, part);
-    MX_LAUNCH(bn_apply_slice_k<true>, dim3(S, C), dim3(kBnTB), 0, st, x, gamma, beta, part, mean, invstd, run_mean,
-              run_var, y, N, C, HW, S, dv, cnt, eps, momentum, relu ? 1 : 0, num_batches, res, Cr);
+    MX_LAUNCH(bn_apply_slice_k<true>, ga, dim3(kBnTB), 0, st, x, gamma, beta, part, mean, invstd, run_mean,
+              run_var, y, N, C, HW, S, dv, cnt, eps, momentum, relu ? 1 : 0, num_batches, res, Cr, ss2);
   } else {
     MX_LAUNCH(bn_stats_k<false>, dim3(S, C), dim3(kBnTB), 0, st, x, N, C, HW, S, dv, part);
-    MX_LAUNCH(bn_apply_slice_k<false>, dim3(S, C), dim3(kBnTB), 0, st, x, gamma, beta, part, mean, invstd, run_mean,
-              run_var, y, N, C, HW, S, dv, cnt, eps, momentum, relu ? 1 : 0, num_batches, res, Cr);
+    MX_LAUNCH(bn_apply_slice_k<false>, ga, dim3(kBnTB), 0, st, x, gamma, beta, part, mean, invstd, run_mean,
+              run_var, y, N, C, HW, S, dv, cnt, eps, momentum, relu ? 1 : 0, num_batches, res, Cr, ss2);
   }
 }
 
 void bn_bwd(const float* dy, const float* x, const float* y_relu, const float* gamma, const float* mean,
             const float* invstd, float* dx, float* dgamma, float* dbeta, int N, int C, int HW, bool accp, float* part,
-            hipStream_t st, const float* extra, int extC) {
+            hipStream_t st, const float* extra, int extC, const float* ssm) {
   MX_CHECK((int64_t)N * C * HW < (1ll << 31), "bn: tensor too large for 32-bit index math");
   const int S = bn_splits(N, C, HW);
   MX_CHECK(S <= 4 * kBnTB, "bn: too many splits");
   MX_CHECK(!extra || extC >= C, "bn: extra gradient must have >= C channels");
+  MX_CHECK(!(ssm && y_relu), "bn: one ReLU mask source");
+  const float2* m2 = reinterpret_cast<const float2*>(ssm);
   if (bn_use_fused(N, C, HW)) {
 #define MX_BN_BWD(U_)                                                                                              \
   MX_LAUNCH(bn_bwd_fused_k<U_>, dim3(C), dim3(kBnF), 0, st, dy, x, y_relu, gamma, mean, invstd, dgamma, dbeta, dx, N, \
-            C, HW, FastDiv(HW / 4), accp ? 1 : 0, extra, extC)
+            C, HW, FastDiv(HW / 4), accp ? 1 : 0, extra, extC, m2)
     switch (bn_fused_u(N, HW)) {
       case 1: MX_BN_BWD(1); break;
       case 2: MX_BN_BWD(2); break;
@@ -671,13 +709,13 @@ void bn_bwd(const float* dy, const float* x, const float* y_relu, const float* g
   const FastDiv dv(vec ? HW / 4 : HW);
   const float cnt = (float)N * (float)HW;
   if (vec) {
-    MX_LAUNCH(bn_bwd_reduce_k<true>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, mean, N, C, HW, S, dv, part);
+    MX_LAUNCH(bn_bwd_reduce_k<true>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, mean, N, C, HW, S, dv, part, m2);
     MX_LAUNCH(bn_bwd_apply_slice_k<true>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, gamma, mean, invstd, part,
-              dgamma, dbeta, dx, N, C, HW, S, dv, cnt, accp ? 1 : 0, extra, extC);
+              dgamma, dbeta, dx, N, C, HW, S, dv, cnt, accp ? 1 : 0, extra, extC, m2);
   } else {
-    MX_LAUNCH(bn_bwd_reduce_k<false>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, mean, N, C, HW, S, dv, part);
+    MX_LAUNCH(bn_bwd_reduce_k<false>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, mean, N, C, HW, S, dv, part, m2);
     MX_LAUNCH(bn_bwd_apply_slice_k<false>, dim3(S, C), dim3(kBnTB), 0, st, dy, x, y_relu, gamma, mean, invstd, part,
-              dgamma, dbeta, dx, N, C, HW, S, dv, cnt, accp ? 1 : 0, extra, extC);
+              dgamma, dbeta, dx, N, C, HW, S, dv, cnt, accp ? 1 : 0, extra, extC, m2);
   }
 }
 

@@ -624,9 +624,12 @@ size_t conv_dgrad_filter_floats(const ConvShape& s) { return use_wino(s) ? wino_
 size_t conv_fwd_filter_floats(const ConvShape& s) { return use_wino(s) ? wino_fwd_filter_floats(s) : 0; }
 
 void conv2d_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s,
-                bool relu, hipStream_t st, float* scratch, float* dgrad_filters, bool pretransformed) {
+                bool relu, hipStream_t st, float* scratch, float* dgrad_filters, bool pretransformed,
+                const float* in_ss, bool in_relu) {
   MX_CHECK(!pretransformed || (scratch && use_wino(s)), "conv2d_fwd: pretransformed filters need the Winograd path");
-  if (scratch && use_wino(s)) return wino_fwd(x, w, bias, y, s, relu, scratch, st, dgrad_filters, pretransformed);
+  MX_CHECK(!in_ss || (scratch && use_wino(s)), "conv2d_fwd: a folded BN input needs the Winograd path");
+  if (scratch && use_wino(s))
+    return wino_fwd(x, w, bias, y, s, relu, scratch, st, dgrad_filters, pretransformed, in_ss, in_relu);
   if (g_gemm_precision == 0 && conv3x3_eligible(s)) return conv3x3_fwd(x, w, bias, y, s, relu, st);
   if (is_1x1_s1(s)) {
     Conv1x1FwdOp op{s.N * s.H * s.W, s.K, s.C, s.H * s.W, FastDiv(s.H * s.W), x, w, bias, y, relu};
@@ -675,9 +678,11 @@ void conv2d_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s
 size_t conv_wgrad_scratch_floats(const ConvShape& s) { return use_wino(s) ? wino_wgrad_scratch_floats(s) : 0; }
 
 bool conv2d_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate,
-                  hipStream_t st, float* scratch, float* db) {
-  if (use_wino(s) && (scratch || wino_wgrad_scratch_floats(s) == 0)) {
-    wino_wgrad(dy, x, dw, s, accumulate, scratch, st);
+                  hipStream_t st, float* scratch, float* db, const float* in_ss, bool in_relu) {
+  const bool wino = use_wino(s) && (scratch || wino_wgrad_scratch_floats(s) == 0);
+  MX_CHECK(!in_ss || wino, "conv2d_wgrad: a folded BN input needs the Winograd path");
+  if (wino) {
+    wino_wgrad(dy, x, dw, s, accumulate, scratch, st, in_ss, in_relu);
     return false;
   }
   if (g_gemm_precision == 0 && conv3x3_wgrad_eligible(s)) {

@@ -217,6 +217,22 @@ __device__ __forceinline__ void mfma_chunk(const float* ap, const float* bp, f32
   }
 }
 
+// A folded BN's output as the convolution input (ops.bn_conv): relu?(x * sc + sh) per input
+// channel -- the BN apply kernel's exact fmaf -- formed while the input is staged; elements
+// outside the image stay zero (the padding of the BN output, not BN(0)).
+__device__ __forceinline__ float in_affine(float v, float2 t, int relu) {
+  const float y = fmaf(v, t.x, t.y);
+  return relu ? fmaxf(y, 0.f) : y;
+}
+// The (scale, shift) of input channel c, loaded unconditionally (no fold: an identity pair): a
+// load behind the `ss != null` branch would make the waitcnt pass drain the prefetched tiles at
+// the branch's join, in every call of these kernels, folded or not.
+__device__ float2 g_no_affine = {1.f, 0.f};
+__device__ __forceinline__ float2 load_ss(const float2* ss, int c) {
+  const float2* p = ss ? ss + c : &g_no_affine;
+  return *p;
+}
+
 struct WinoArgs {
   const float* x;     // [N][Ci][W][W]
   const float* U;     // [16][Cip][Cop]
@@ -226,6 +242,8 @@ struct WinoArgs {
   int N, Ci, Co, Cip, Cop;
   int tblocks, ktiles, splits, chunks_per_split;
   int relu, accumulate;  // accumulate: 0 store, 1 y += result, 2 atomicAdd (split reduction)
+  const float2* ss;      // [Ci] (scale, shift) of a folded BN on the input, or null
+  int in_relu;           // the folded BN's fused ReLU
 };
 
 // 4x4 window of one (plane, tile).  Every load is issued (clamped to the plane's first element
@@ -365,10 +383,12 @@ __global__ __launch_bounds__(256 * KS, kOcc) void wino_fwd_kernel(WinoArgs a) {
   float raw[16];
   f32x4 ru[4];
   unsigned rmask = 0;
+  float2 rss = make_float2(1.f, 0.f);
   auto gload = [&](int ch) {
     const int c = ch * kCC + cl;
     rmask = c < a.Ci ? vmask : 0u;
     load_window<W>(a.x, xn + (uint32_t)min(c, a.Ci - 1) * HW, woff, rmask, raw);
+    rss = load_ss(a.ss, min(c, a.Ci - 1));
     const char* ub = reinterpret_cast<const char*>(a.U) + (size_t)ch * u_ch;
 #pragma unroll
     for (int q = 0; q < 4; ++q) ru[q] = *reinterpret_cast<const f32x4*>(ub + u_lane + q * u_q);
@@ -377,6 +397,10 @@ __global__ __launch_bounds__(256 * KS, kOcc) void wino_fwd_kernel(WinoArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4*>(as_st + q * 32 * kP) = ru[q];
     float v[16];
+    if (a.ss) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) raw[e] = in_affine(raw[e], rss, a.in_relu);
+    }
     zero_outside(raw, rmask);
     in_transform(raw, v);
 #pragma unroll
@@ -532,6 +556,7 @@ __global__ __launch_bounds__(256, 2) void wino_fwd_patch_kernel(WinoArgs a) {
     wbase = il * PRI * PW + 2 * trw * PW + 2 * tcl;
   }
 
+
   f32x4 acc[16][2];
 #pragma unroll
   for (int xi = 0; xi < 16; ++xi)
@@ -608,6 +633,8 @@ struct WinoWArgs {
   int N, C, K;
   int ktiles, ctiles, nchunks, chunks_per_block;
   int accumulate;   // nblk == 1 only: dw += result
+  const float2* ss; // [C] (scale, shift) of a folded BN on x (WinoArgs::ss), or null
+  int in_relu;
 };
 
 // Block: 32 co x 32 ci x a range of 8-tile chunks; wave (wm, wn) owns 16 co x 16 ci for all 16 xi.
@@ -630,6 +657,7 @@ __global__ __launch_bounds__(256, 3) void wino_wgrad_kernel(WinoWArgs a) {
   const bool k_ok = k0 + cl < a.K, c_ok = c0 + cl < a.C;
   const float* dyk = a.dy + (size_t)min(k0 + cl, a.K - 1) * HW;
   const uint32_t xc = (uint32_t)min(c0 + cl, a.C - 1) * HW;
+  const float2 xss = load_ss(a.ss, min(c0 + cl, a.C - 1));  // this thread's channel
   float rdy[4], rx[16];
   unsigned xmask = 0;
   auto gload = [&](int ch) {
@@ -653,6 +681,10 @@ __global__ __launch_bounds__(256, 3) void wino_wgrad_kernel(WinoWArgs a) {
     float v[16];
 #pragma unroll
     for (int i = 0; i < 4; ++i) rdy[i] = k_ok ? rdy[i] : 0.f;
+    if (a.ss) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) rx[e] = in_affine(rx[e], xss, a.in_relu);
+    }
     zero_outside(rx, xmask);
     dy_transform(rdy, v);
 #pragma unroll
@@ -812,7 +844,8 @@ int pad_to(int v, int m) { return (v + m - 1) / m * m; }
 
 void launch_fwd(const float* x, const float* w, const float* bias, const float* mask, float* y, int N, int Ci,
                 int Co, int Wd, bool relu, bool accumulate, bool dgrad, float* U, int K_w, int C_w,
-                hipStream_t st, float* U_dgrad_out = nullptr, bool pretransformed = false) {
+                hipStream_t st, float* U_dgrad_out = nullptr, bool pretransformed = false,
+                const float* in_ss = nullptr, bool in_relu = false) {
   const int Cip = pad_to(Ci, kCC), Cop = pad_to(Co, 32);
   if (U_dgrad_out) {  // forward call that also prepares the backward's filters (one launch)
     const int Cipd = pad_to(K_w, kCC), Copd = pad_to(C_w, 32);
@@ -846,7 +879,8 @@ void launch_fwd(const float* x, const float* w, const float* bias, const float* 
   // 32x32 images with one 32-channel output tile (the first stage-1 layers): the 32 x 64 patch
   // blocks leave one block per CU and the 32 x 32 blocks win (11.7 vs 14.5 us at C = 16)
   const int blocks32 = cdiv(N * tpi, 32) * (Cop / 32), cus = device_cu_count();
-  const int variant = Wd == 32 ? (blocks32 / 2 >= 2 * cus ? 3 : 2) : (blocks32 <= cus ? 4 : 2);
+  // (a folded BN input runs the per-window kernels: the patch kernel stages raw rows in LDS)
+  const int variant = Wd == 32 && !in_ss ? (blocks32 / 2 >= 2 * cus ? 3 : 2) : (blocks32 <= cus ? 4 : 2);
   const int tile_blk = variant == 3 ? 64 : 32;
   a.tblocks = cdiv(N * tpi, tile_blk);
   a.ktiles = Cop / 32;
@@ -858,6 +892,8 @@ void launch_fwd(const float* x, const float* w, const float* bias, const float* 
   a.splits = 1;
   a.relu = relu;
   a.accumulate = accumulate ? 1 : 0;
+  a.ss = reinterpret_cast<const float2*>(in_ss);
+  a.in_relu = in_relu ? 1 : 0;
   const dim3 grid(a.tblocks * a.ktiles * a.splits);
   if (variant == 3) {
     switch (Wd) {
@@ -937,9 +973,10 @@ size_t wino_wgrad_scratch_floats(const ConvShape& s) {
 }
 
 void wino_fwd(const float* x, const float* w, const float* bias, float* y, const ConvShape& s, bool relu,
-              float* scratch, hipStream_t st, float* U_dgrad_out, bool pretransformed) {
+              float* scratch, hipStream_t st, float* U_dgrad_out, bool pretransformed, const float* in_ss,
+              bool in_relu) {
   launch_fwd(x, w, bias, nullptr, y, s.N, s.C, s.K, s.W, relu, false, false, scratch, s.K, s.C, st,
-             pretransformed ? nullptr : U_dgrad_out, pretransformed);
+             pretransformed ? nullptr : U_dgrad_out, pretransformed, in_ss, in_relu);
 }
 
 size_t wino_fwd_filter_floats(const ConvShape& s) { return 16 * (size_t)pad_to(s.C, kCC) * pad_to(s.K, 32); }
@@ -986,7 +1023,7 @@ void wino_reduce_batch_launch(const RedBatch& b, int blocks, hipStream_t st) {
 }
 
 void wino_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate, float* scratch,
-                hipStream_t st) {
+                hipStream_t st, const float* in_ss, bool in_relu) {
   const WgradPlan p = wgrad_plan(s);
   MX_CHECK(p.nblk == 1 || scratch, "winograd wgrad: partial-sum scratch required");
   WinoWArgs a{};
@@ -1001,6 +1038,8 @@ void wino_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, 
   a.nchunks = p.nchunks;
   a.chunks_per_block = p.cpb;
   a.accumulate = (p.nblk == 1 && accumulate) ? 1 : 0;
+  a.ss = reinterpret_cast<const float2*>(in_ss);
+  a.in_relu = in_relu ? 1 : 0;
   const dim3 grid(p.ktiles * p.ctiles * p.nblk);
   switch (s.W) {
     case 8: MX_LAUNCH(wino_wgrad_kernel<8>, grid, dim3(256), kLds, st, a); break;

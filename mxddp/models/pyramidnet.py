@@ -42,12 +42,15 @@ class ResidualBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        # bn1 -> conv1 and bn2 -> ReLU -> conv2 with the BN normalise pass folded into the
+        # convolution's input staging where it runs the Winograd path (ops.bn_conv; the stride-2
+        # conv1 keeps its BN pass)
         if self.stride == 1:
             # identity shortcut fused into the BNs: bn3 adds x (zero-padded channels) while it
             # normalises, and bn1's backward adds the shortcut's gradient to its dx
-            h, xs = self.bn1(x, tap=True)
-            return self.bn3(self.conv2(self.bn2(self.conv1(h))), residual=xs)
-        out = self.bn3(self.conv2(self.bn2(self.conv1(self.bn1(x)))))
+            h, xs = ops.bn_conv(x, self.bn1, self.conv1, tap=True)
+            return self.bn3(ops.bn_conv(h, self.bn2, self.conv2), residual=xs)
+        out = self.bn3(ops.bn_conv(self.conv1(self.bn1(x)), self.bn2, self.conv2))
         return ops.shortcut_pad_add(out, x, self.stride)
 
 

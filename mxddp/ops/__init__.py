@@ -250,8 +250,13 @@ def invalidate_filters(device=None) -> None:
 
 # --------------------------------------------------------------------------- conv2d
 class _Conv2d(torch.autograd.Function):
+    """``in_ss`` ([Cin, 2], optional): x is a folded BN's INPUT and the convolution consumes
+    relu?(x * in_ss[c, 0] + in_ss[c, 1]) (``bn_conv``); the forward and the weight gradient form it
+    while staging their input tiles, and the gradient returned for x is the gradient of that
+    (unstored) BN output, which the folded BN's backward turns into its own."""
+
     @staticmethod
-    def forward(ctx, x, w, b, stride, padding, dilation, relu):
+    def forward(ctx, x, w, b, stride, padding, dilation, relu, in_ss=None, in_relu=False):
         C = native()
         x = x.contiguous()
         _check(x, "input"); _check(w, "weight")
@@ -270,7 +275,7 @@ class _Conv2d(torch.autograd.Function):
             ent, bank = fe
             fresh = ent.gen == bank.gen and ent.version == w._version
             C.conv2d_fwd(x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), *geom, bool(relu), st, ent.U.data_ptr(),
-                         _p(ent.Ud), fresh)
+                         _p(ent.Ud), fresh, _p(in_ss), bool(in_relu))
             if not fresh:  # transformed just now, into the bank's buffers
                 ent.version, ent.gen = w._version, bank.gen
             wd = ent.Ud if ctx.needs_input_grad[0] else None
@@ -279,8 +284,10 @@ class _Conv2d(torch.autograd.Function):
             scr = torch.empty((ns,), device=x.device, dtype=x.dtype) if ns else None
             nd = C.conv_dgrad_filter_floats(*geom) if ctx.needs_input_grad[0] else 0
             wd = torch.empty((nd,), device=x.device, dtype=x.dtype) if nd else None
-            C.conv2d_fwd(x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), *geom, bool(relu), st, _p(scr), _p(wd))
+            C.conv2d_fwd(x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), *geom, bool(relu), st, _p(scr), _p(wd),
+                         False, _p(in_ss), bool(in_relu))
         ctx.dgrad_filters = wd
+        ctx.in_ss, ctx.in_relu = in_ss, bool(in_relu)
         ctx.geom = (N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw, P, Q)
         ctx.relu = relu
         ctx.has_bias = b is not None
@@ -325,7 +332,7 @@ class _Conv2d(torch.autograd.Function):
                     db_t = bsink if bsink is not None else torch.empty((K,), device=dy.device, dtype=dy.dtype)
             def _wgrad():
                 return C.conv2d_wgrad(dy.data_ptr(), x.data_ptr(), dw_.data_ptr(), N, Cin, H, W, K, R, S, sh, sw, ph,
-                                      pw, dh, dw, sink is not None, st, _p(ws), _p(db_t))
+                                      pw, dh, dw, sink is not None, st, _p(ws), _p(db_t), _p(ctx.in_ss), ctx.in_relu)
             if _WGRAD_DEFER and sink is not None and dy.is_cuda:
                 bias_done = wgrad_defer_call(_wgrad, ws, dy.device, st)
             else:
@@ -346,13 +353,16 @@ class _Conv2d(torch.autograd.Function):
             if sink is not None:
                 _grad_done(b)
                 db = None
-        return dx, dw_, db, None, None, None, None
+        return dx, dw_, db, None, None, None, None, None, None
 
 
-def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, relu=False):
+def conv2d(x, w, b=None, stride=1, padding=0, dilation=1, relu=False, in_ss=None, in_relu=False):
     stride, padding, dilation = _pair(stride), _pair(padding), _pair(dilation)
     if _native(x):
-        return _Conv2d.apply(x, w, b, stride, padding, dilation, relu)
+        return _Conv2d.apply(x, w, b, stride, padding, dilation, relu, in_ss, in_relu)
+    if in_ss is not None:
+        x = x * in_ss[:, 0].view(1, -1, 1, 1) + in_ss[:, 1].view(1, -1, 1, 1)
+        x = F.relu(x) if in_relu else x
     y = F.conv2d(x, w, b, stride, padding, dilation)
     return F.relu(y) if relu else y
 
@@ -653,6 +663,118 @@ def batch_norm(x, gamma, beta, running_mean, running_var, training, momentum=0.1
     if residual is not None:
         y = y + F.pad(residual, (0, 0, 0, 0, 0, y.shape[1] - residual.shape[1]))
     return (y, x) if tap else y
+
+
+# ------------------------------------------------- BN folded into the next 3x3 convolution
+# PyramidNet's blocks run bn1 -> conv1 and bn2 -> ReLU -> conv2 (pytorch/model.py:40-50).  When
+# the convolution takes the Winograd path, the BN's normalise pass is not run at all: the BN
+# launches only its statistics (and writes a per-channel (scale, shift) table), the convolution's
+# forward and weight-gradient kernels apply relu?(x * scale + shift) while staging their input
+# tiles, and the BN backward recomputes its ReLU mask from x.  The BN output tensor is never
+# written or read: one full pass over the activation (write + re-read) less per folded BN.
+# Measured (docs/ROUND6.md, profiles/r6_bnfold/): the BN kernels save ~0.26 ms per PyramidNet
+# step but the convolutions' staging, which now does the affine per window element (4x
+# redundant over the overlapping 4x4 windows), costs more -- off by default (MXDDP_BN_FOLD=1).
+_BN_FOLD = os.environ.get("MXDDP_BN_FOLD", "0") != "0"
+
+
+def set_bn_fold(on: bool) -> None:
+    global _BN_FOLD
+    _BN_FOLD = bool(on)
+
+
+class _BatchNormFold(torch.autograd.Function):
+    """Training BN whose normalise pass the consuming convolution performs (``bn_conv``).  Returns
+    (h, ss[, x_alias]): h aliases x and stands for the BN output (its gradient, from the
+    convolution, is the gradient of that output), ss = [C, 2] (scale, shift); ``tap`` as in
+    ``_BatchNorm``."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, running_mean, running_var, momentum, eps, relu, num_batches=None, tap=False):
+        C = native()
+        x = x.contiguous()
+        _check(x, "input")
+        N, Cc = x.shape[0], x.shape[1]
+        HW = x.numel() // (N * Cc)
+        mean = torch.empty((Cc,), device=x.device, dtype=torch.float32)
+        invstd = torch.empty_like(mean)
+        ss = torch.empty((Cc, 2), device=x.device, dtype=torch.float32)
+        part = _bn_part(x.device, C.bn_partial_floats(N, Cc, HW))
+        C.bn_fwd_train(x.data_ptr(), _p(gamma), _p(beta), 0, mean.data_ptr(), invstd.data_ptr(), _p(running_mean),
+                       _p(running_var), N, Cc, HW, float(momentum), float(eps), bool(relu), part.data_ptr(),
+                       stream_of(x), _p(num_batches), 0, 0, ss.data_ptr())
+        ctx.save_for_backward(x, gamma, mean, invstd, ss)
+        ctx.dims = (N, Cc, HW)
+        ctx.relu = bool(relu)
+        ctx.has_affine = gamma is not None
+        ctx.affine_refs = (gamma, beta)
+        ctx.mark_non_differentiable(ss)
+        if tap:
+            return x, ss, x
+        return x, ss
+
+    @staticmethod
+    def backward(ctx, dh, _dss, dtap=None):
+        x, gamma, mean, invstd, ss = ctx.saved_tensors
+        N, Cc, HW = ctx.dims
+        dh = dh.contiguous()
+        dx = torch.empty_like(x)
+        g_ref, b_ref = ctx.affine_refs
+        gs, bs = (_grad_sink(g_ref), _grad_sink(b_ref)) if ctx.has_affine else (None, None)
+        direct = gs is not None and bs is not None
+        if direct:
+            dg, db = gs, bs
+        else:
+            dg = torch.empty((Cc,), device=x.device) if ctx.has_affine else None
+            db = torch.empty((Cc,), device=x.device) if ctx.has_affine else None
+        ext, ext_c = None, 0
+        if dtap is not None:  # the shortcut branch's gradient, read in place when it can be
+            s_ = dtap.stride()
+            W = x.shape[-1] if x.dim() >= 3 else 1
+            in_place = (dtap.dim() == 4 and s_[3] == 1 and s_[2] == W and s_[1] == HW and s_[0] % HW == 0
+                        and s_[0] // HW >= Cc and dtap.dtype == torch.float32)
+            ext = dtap if in_place else dtap.contiguous()
+            ext_c = s_[0] // HW if in_place else Cc
+        part = _bn_part(x.device, native().bn_partial_floats(N, Cc, HW))
+        native().bn_bwd(dh.data_ptr(), x.data_ptr(), 0, _p(gamma), mean.data_ptr(), invstd.data_ptr(), dx.data_ptr(),
+                        _p(dg), _p(db), N, Cc, HW, direct, part.data_ptr(), stream_of(dh), _p(ext), ext_c,
+                        ss.data_ptr() if ctx.relu else 0)
+        if direct:
+            _grad_done(g_ref)
+            _grad_done(b_ref)
+            dg = db = None
+        return dx, dg, db, None, None, None, None, None, None, None
+
+
+def _fold_ok(x, bn, conv) -> bool:
+    if not (_BN_FOLD and _native(x) and x.dim() == 4 and bn.training and bn.track_running_stats
+            and bn.running_mean is not None and conv.bias is None and not getattr(conv, "fuse_relu", False)
+            and conv.groups == 1 and conv.weight.dtype == torch.float32):
+        return False
+    N, Cin, H, W = x.shape
+    K, _, R, S = conv.weight.shape
+    (sh, sw), (ph, pw), (dh, dw) = _pair(conv.stride), _pair(conv.padding), _pair(conv.dilation)
+    # the Winograd path (its forward and weight gradient both stage the input through registers)
+    return native().conv_fwd_filter_floats(N, Cin, H, W, K, R, S, sh, sw, ph, pw, dh, dw) > 0
+
+
+def bn_conv(x, bn, conv, tap=False):
+    """``conv(bn(x))`` (``bn``: an mxddp BatchNorm2d, ReLU fused or not; ``conv``: its Conv2d),
+    with the BN's normalise pass folded into the convolution where it runs the Winograd path in
+    training; the plain two-op chain otherwise.  ``tap`` as in ``batch_norm``: also return an
+    alias of x for the shortcut branch."""
+    if not _fold_ok(x, bn, conv):
+        h = bn(x, tap=tap)
+        if tap:
+            h, xs = h
+            return conv(h), xs
+        return conv(h)
+    mom = bn.momentum if bn.momentum is not None else 0.1
+    out = _BatchNormFold.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, mom, bn.eps, bn.fuse_relu,
+                               bn.num_batches_tracked, tap)
+    h, ss = out[0], out[1]
+    y = conv2d(h, conv.weight, None, conv.stride, conv.padding, conv.dilation, in_ss=ss, in_relu=bn.fuse_relu)
+    return (y, out[2]) if tap else y
 
 
 # --------------------------------------------------------------------------- loss
