@@ -286,9 +286,12 @@ def test_fused_engine_rccl_variants_ws1(cuda, variant):
     assert tr._grad_store[tr.params.numel():].abs().max().item() == 0.0  # padding slack stays zero
 
 
-def test_fused_autotune_lists_rccl_variants(cuda, monkeypatch):
+@pytest.mark.parametrize("graphs", [False, None])
+def test_fused_autotune_lists_rccl_variants(cuda, monkeypatch, graphs):
     """autotune() times every configured RCCL variant (here at world size 1, collectives
-    forced) and reports them in its JSON; the trained weights stay exact under restore=True."""
+    forced) and reports them in its JSON; the trained weights stay exact under restore=True.
+    graphs=None: the default (MXDDP_AUTOTUNE_GRAPHS=1), every variant also captured in the step
+    graph."""
     from mxddp.engine import FusedMnistTrainer
     from mxddp.parallel import comm as pc
 
@@ -299,10 +302,11 @@ def test_fused_autotune_lists_rccl_variants(cuda, monkeypatch):
     b = FusedMnistTrainer(batch=64, device=cuda, lr=0.01)
     a.step(1)
     b.step(1)
-    res = a.autotune(trial_steps=3, restore=True, include_graphs=False)
+    monkeypatch.delenv("MXDDP_AUTOTUNE_GRAPHS", raising=False)
+    res = a.autotune(trial_steps=3, restore=True, include_graphs=graphs)
     names = {k.split("/")[0] for k in a.tuned["trials_ms"]}
     assert names == {"rccl:default", "rccl:Ring:c7", "rccl:Ring:c28"}, a.tuned
-    assert len(res) == 9 and a.steps == 1
+    assert len(res) == (9 if graphs is False else 18) and a.steps == 1
     a.step(10)
     b.step(10)
     for k, v in a.state_dict().items():
