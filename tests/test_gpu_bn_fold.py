@@ -1,10 +1,12 @@
 """PyramidNet's BN -> conv3x3 with the BN normalise pass folded into the Winograd convolution
-(ops.bn_conv, opt-in: ops.set_bn_fold / MXDDP_BN_FOLD=1): the convolution forms relu?(x * scale + shift) while staging its input -- the BN
-apply kernel's own fmaf -- and the BN backward recomputes its ReLU mask from x, so a residual
-block trains BIT FOR BIT like the unfolded chain (forward output, every gradient, running
-statistics; the stride-2 conv1's weight gradient, which sums with float atomics, within
-rounding).  Plus the fold against the fp32 CPU reference of the same block, and a whole
-PyramidNet-110 step with the fold on and off.
+(ops.bn_conv, opt-in: ops.set_bn_fold / MXDDP_BN_FOLD=1).  The convolution forms
+relu?(x * scale + shift) while staging its input -- the BN apply kernel's own fmaf -- and the BN
+backward recomputes its ReLU mask from x, so a residual block on 16 x 16 / 8 x 8 images trains
+BIT FOR BIT like the unfolded chain: forward output, every gradient, running statistics.  Within
+rounding: 32 x 32 layers (the folded forward runs the per-window kernel, the unfolded one the
+patch-staged kernel) and the stride-2 conv1's weight gradient (float atomics).  Plus the fold
+against the fp32 CPU reference of the same block, and a whole PyramidNet-110 step with the fold
+on and off.
 """
 import copy
 
@@ -65,6 +67,20 @@ def test_folded_block_is_bitwise_the_unfolded_one(cuda, cfg):
     finally:
         ops.set_bn_fold(prev)
     torch.cuda.synchronize()
+    if W == 32:
+        # 32 x 32 layers: the unfolded forward runs the patch-staged kernel, the folded one the
+        # per-window kernel (different MFMA chunk order): equal within rounding
+        # (a rounding difference in conv1's output can flip bn2's ReLU mask on a few elements, so
+        # the gradients are compared norm-wise)
+        def rel(a, b):
+            return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+        assert rel(r1[0], r0[0]) < 1e-5 and rel(r1[1], r0[1]) < 1e-4
+        for k in r0[2]:
+            assert rel(r1[2][k], r0[2][k]) < 1e-4, (k, rel(r1[2][k], r0[2][k]))
+        for k in r0[3]:
+            assert rel(r1[3][k], r0[3][k]) < 1e-5, k
+        return
     assert torch.equal(r1[0], r0[0]), (r1[0] - r0[0]).abs().max().item()
     assert torch.equal(r1[1], r0[1]), (r1[1] - r0[1]).abs().max().item()
     for k in r0[2]:
