@@ -631,9 +631,10 @@ __device__ void kb1_role_b(const KerasFused& f, SmemB& sm, int bid) {
     av[s] = (int)f.q2[e] == (oy & 1) * 2 + (ox & 1) ? dv : 0.f;
     poff[s] = oy * 13 + ox;
   }
+  // clamped, not predicated (a predicated store let the compiler sink each load into its
+  // store's branch: one memory round trip per float4); past the end: element kP1v - 1 again
 #pragma unroll
-  for (int k = 0; k < kP1n; ++k)
-    if (tid + 256 * k < kP1v) reinterpret_cast<float4*>(sm.p1s)[tid + 256 * k] = pv[k];
+  for (int k = 0; k < kP1n; ++k) reinterpret_cast<float4*>(sm.p1s)[min(tid + 256 * k, kP1v - 1)] = pv[k];
   __syncthreads();
   for (int nt = w; nt < 18; nt += 4) {
     const int c = 16 * nt + (lane & 15), ci = c / 9, r = c - ci * 9;
