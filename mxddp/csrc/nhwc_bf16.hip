@@ -3425,18 +3425,33 @@ static int g_wgrad_target = 512;
 static int g_wgrad_w8 = 1;
 void nhwc_wgrad_set_waves8(int on) { g_wgrad_w8 = on; }
 void nhwc_wgrad_set_target(int n) { g_wgrad_target = n; }
-static int wgrad_splits(int Npix, int K, int Ng, int RS) {
-  int tm, tn;
-  wgrad_tile(K, Ng, Npix, RS, tm, tn);
-  const int tiles = cdiv(K, tm) * cdiv(Ng, tn);
+// Layers of at most this many output pixels that would split into >= 32 planes aim at half the
+// blocks: their split-K planes (written, then read back by the reduction) cost more than the
+// extra blocks gain.  ResNet-50 batch 32, on one box: all layers at target 512 / 256 / 128 =
+// 5,850 / 5,883 / 5,631 img/s; half the target below 6,272 / 25,088 / 100,352 pixels 5,905 /
+// 5,924 / 5,922 vs 5,897 (the 28 x 28 stage's 49-plane layers carry the gain); batch 256 lost
+// 1.2 % / 0.7 % with the 100,352 / 25,088 pixel rule alone (its 7 x 7 and 14 x 14 layers split
+// into 4-15 planes), so the plane count gates it too (profiles/r6_wtarget/).  A/B:
+// nhwc_wgrad_set_small_npix (0 = off)
+static int g_wgrad_small_npix = 25088;
+void nhwc_wgrad_set_small_npix(int n) { g_wgrad_small_npix = n; }
+static int wgrad_splits_for(int Npix, int K, int Ng, int tiles, int target) {
   // ~2 blocks per CU (1 for the 256 tile), >= 512 pixels (8 stages) per block, partial planes
   // <= 32M floats
-  const int target = tm == 256 ? g_wgrad_target / 2 : g_wgrad_target;
   int splits = std::max(1, cdiv(target, tiles));
   splits = std::min(splits, std::max(1, Npix / 512));
   splits = std::min(splits, std::max(1, (int)((32ll << 20) / ((int64_t)K * Ng))));
   const int chunk = cdiv(cdiv(Npix, splits), 64) * 64;
   return cdiv(Npix, chunk);
+}
+static int wgrad_splits(int Npix, int K, int Ng, int RS) {
+  int tm, tn;
+  wgrad_tile(K, Ng, Npix, RS, tm, tn);
+  const int tiles = cdiv(K, tm) * cdiv(Ng, tn);
+  const int target = tm == 256 ? g_wgrad_target / 2 : g_wgrad_target;
+  const int splits = wgrad_splits_for(Npix, K, Ng, tiles, target);
+  if (Npix <= g_wgrad_small_npix && splits >= 32) return wgrad_splits_for(Npix, K, Ng, tiles, target / 2);
+  return splits;
 }
 
 size_t nhwc_wgrad_scratch_floats(int N, int Cp, int K, int R, int S, int P, int Q) {

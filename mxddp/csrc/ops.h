@@ -213,6 +213,7 @@ void nhwc_conv_set_gk2(int mode);  // two-stage 128 x 128 tiles: 0 = 8 waves of 
 void nhwc_conv_set_glds_short(int mode);  // two-stage 128-pixel LDS-DMA variant for short reductions
 void nhwc_conv_set_split_blocks(int n);  // generic conv kernel: split-K below this many blocks (256)
 void nhwc_wgrad_set_target(int n);  // weight gradient: blocks aimed at when splitting the pixels (512)
+void nhwc_wgrad_set_small_npix(int n);  // layers of <= n pixels with >= 32 planes aim at half of it (25,088)
 void nhwc_wgrad_set_tile256(int on);  // weight gradient: 256 x 256 tiles where K and R*S*C reach 256 (1)
 void nhwc_bn_set_grid_cap(int cap);
 void nhwc_bn_set_wt(int on);
