@@ -10,10 +10,13 @@
 //   K2  l2 forward + bias + ReLU
 //   K3  l3 forward (logits) + softmax CE + accuracy + dlogits + dh2 = (dlogits W3) * (h2 > 0)
 //   K4  per (256-row slice of W2, 16-column tile): dW2 tile (MFMA) + Adam of the tile, the l2
-//       data-gradient partial of the slice (MFMA, plain stores, 4 planes); db2; l3 grads + Adam
-//                                                                        -> bucket 0 ready
+//       data-gradient partial of the slice (MFMA, plain stores, 4 planes); db2; 4 more blocks:
+//       l3 grads on MFMA + Adam, the step's metrics                      -> bucket 0 ready
 //   K5  per (16 rows of W1, 112 columns): dh1 = sum of the 4 planes, ReLU-masked; dW1 tile
 //       (MFMA) + Adam; db1                                               -> bucket 1 ready
+//       (mlp_set_w2_defer: K4's dW2 tiles + their Adam run as 252 extra K5 blocks instead)
+// Every LDS tile is staged with all of a thread's loads issued before its first store
+// (stage_f4), and the update operands (moments, Adam's step / lr) load at the kernels' tops.
 // Every block owns the weights it updates, so old values (needed by K4's data gradient) are
 // read before the same block writes the new ones -- no cross-block hazard, no extra launch.
 // All cross-block sums are fixed-order (4 data-gradient planes, per-tile loss slots): a step is
