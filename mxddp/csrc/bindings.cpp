@@ -129,6 +129,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("nhwc_conv_set_split_blocks", &nhwc_conv_set_split_blocks);
   m.def("nhwc_wgrad_set_target", &nhwc_wgrad_set_target);
   m.def("nhwc_wgrad_set_small_npix", &nhwc_wgrad_set_small_npix);
+  m.def("wino_wgrad_set_slots", &wino_wgrad_set_slots);
   m.def("nhwc_wgrad_set_tile256", &nhwc_wgrad_set_tile256);
   m.def("wgrad_defer_set", &wgrad_defer_set,
         "this thread's next weight-gradient calls record their split reduction for wgrad_defer_flush");

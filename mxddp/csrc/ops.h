@@ -82,6 +82,7 @@ void wino_dgrad(const float* dy, const float* w, float* dx, const ConvShape& s, 
                 bool accumulate, float* scratch, hipStream_t st, bool pretransformed = false);
 // partial-sum scratch: wino_wgrad_scratch_floats(s) floats (0 = none needed)
 size_t wino_wgrad_scratch_floats(const ConvShape& s);
+void wino_wgrad_set_slots(int per_cu);  // weight-gradient blocks aimed at per CU (3)
 void wino_wgrad(const float* dy, const float* x, float* dw, const ConvShape& s, bool accumulate, float* scratch,
                 hipStream_t st, const float* in_ss = nullptr, bool in_relu = false);
 // 3x3 s1 algorithm: 0 = auto (Winograd where eligible, else direct-LDS), 1 = direct-LDS only.

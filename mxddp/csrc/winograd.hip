@@ -933,6 +933,10 @@ void launch_fwd(const float* x, const float* w, const float* bias, const float* 
 struct WgradPlan {
   int ktiles, ctiles, nchunks, cpb, nblk;
 };
+// resident weight-gradient blocks aimed at per CU (A/B: wino_wgrad_set_slots).  With the
+// batched deferred reductions (round 6), on one box: 2 / 3 / 4 per CU = 2,915-2,921 / 2,958 /
+// 2,900-2,902 img/s on PyramidNet-110 (profiles/r6_winoslots/)
+int g_wgrad_slots_per_cu = 3;
 WgradPlan wgrad_plan(const ConvShape& s) {
   WgradPlan p{};
   p.ktiles = cdiv(s.K, 32);
@@ -946,7 +950,7 @@ WgradPlan wgrad_plan(const ConvShape& s) {
   const int cap = std::max(16, (int)std::min<int64_t>(1024, (8ll << 20) / ((int64_t)s.K * s.C * 9)));
   // The grid must not exceed the 3 x 256 resident slots: a few blocks over (e.g. 25 tiles x 31
   // ranges = 775) run as a second round and nearly double the kernel time.
-  const int slots = 3 * device_cu_count();
+  const int slots = g_wgrad_slots_per_cu * device_cu_count();
   int nblk = std::max(1, std::min(slots / tiles, cap));
   nblk = std::min(nblk, std::max(1, p.nchunks / 8));
   p.cpb = cdiv(p.nchunks, nblk);
@@ -978,6 +982,8 @@ void wino_fwd(const float* x, const float* w, const float* bias, float* y, const
   launch_fwd(x, w, bias, nullptr, y, s.N, s.C, s.K, s.W, relu, false, false, scratch, s.K, s.C, st,
              pretransformed ? nullptr : U_dgrad_out, pretransformed, in_ss, in_relu);
 }
+
+void wino_wgrad_set_slots(int per_cu) { g_wgrad_slots_per_cu = per_cu < 1 ? 1 : per_cu; }
 
 size_t wino_fwd_filter_floats(const ConvShape& s) { return 16 * (size_t)pad_to(s.C, kCC) * pad_to(s.K, 32); }
 
