@@ -121,3 +121,29 @@ def test_resnet_stock_baseline_never_takes_the_native_nhwc_path(monkeypatch):
     with ops.torch_reference_mode():
         assert not R._nhwc_mode(x)
     assert R._nhwc_mode(x)
+
+
+def test_bn_conv_cpu_fallback_and_input_affine():
+    """ops.bn_conv off the GPU is the plain conv(bn(x)) chain (tap included), and ops.conv2d's
+    in_ss (a folded BN's per-channel scale / shift, fused ReLU) matches applying it first."""
+    import copy
+
+    import torch
+    import torch.nn.functional as F
+
+    from mxddp import ops
+    from mxddp.models.pyramidnet import ResidualBlock
+
+    torch.manual_seed(0)
+    blk = ResidualBlock(16, 21, 1).train()
+    ref = copy.deepcopy(blk)
+    x = torch.randn(2, 16, 8, 8)
+    y, xs = ops.bn_conv(x, blk.bn1, blk.conv1, tap=True)
+    y_ref = ref.conv1(ref.bn1(x))
+    assert torch.equal(y, y_ref) and torch.equal(xs, x)
+    w = torch.randn(5, 16, 3, 3)
+    ss = torch.stack([torch.rand(16) + 0.5, torch.randn(16) * 0.1], dim=1)
+    for relu in (False, True):
+        h = x * ss[:, 0].view(1, -1, 1, 1) + ss[:, 1].view(1, -1, 1, 1)
+        h = F.relu(h) if relu else h
+        torch.testing.assert_close(ops.conv2d(x, w, None, 1, 1, in_ss=ss, in_relu=relu), F.conv2d(h, w, None, 1, 1))
