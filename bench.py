@@ -46,6 +46,8 @@ AB_SWITCHES = {
                                          "default), after F7W's blocks at two per CU (1), or folded into F5 (0)"),
     "w2_defer": ("mlp_set_w2_defer", "fused MLP: the dW2 tile + Adam as extra resident blocks of the l1-backward "
                                      "launch (1) or inside the l2-backward launch (0, default)"),
+    "f67_order": ("mnist_set_f67_order", "fused MNIST, batch 64: XCD-aware placement of the conv-backward launch's "
+                                         "F6W / F7W / fc1 blocks (1, default) or the plain order (0)"),
     "wgrad_defer": ("ops.set_wgrad_defer", "layer path, world size 1: conv weight-gradient split reductions summed by "
                                            "the optimizer in batched launches (1, default) or one launch per conv (0)"),
     "bn_fold": ("ops.set_bn_fold", "PyramidNet: BN normalise pass folded into the next Winograd conv's input staging "

@@ -139,6 +139,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("mnist_set_fc1_defer", &mnist_set_fc1_defer,
         "fused MNIST, world size 1: fc1 weight gradient + SGD in the conv-backward launch's last blocks (1) or in F5 (0)");
   m.def("mnist_fc1_defer", &mnist_fc1_defer);
+  m.def("mnist_set_f67_order", &mnist_set_f67_order,
+        "fused MNIST batch 64: XCD-aware placement of the conv-backward launch's blocks (1) or plain order (0)");
+  m.def("mnist_f67_order", &mnist_f67_order);
   m.def("mlp_set_w2_defer", &mlp_set_w2_defer,
         "fused MLP: the dW2 tile + update as extra resident blocks of K5 (1) or in K4 (0, default)");
   m.def("mlp_w2_defer", &mlp_w2_defer);

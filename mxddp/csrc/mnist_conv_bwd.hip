@@ -748,6 +748,30 @@ __device__ __forceinline__ void fc1_update_body(const MnistFused& f, float* sm, 
 }
 
 // ------------------------------------------------------------------------------------------
+// XCD-aware block placement of the batch-64 F67 grid (704 blocks: 128 F6W, 384 F7W, 192 fc1 at
+// three per CU).  Workgroup b goes to XCD b % 8, and an XCD hands its j-th workgroup (j = b / 8)
+// to CU j % 32 of slot j / 32 while the slots fill in order, so the plain [F6W | F7W | fc1] order
+// puts every F6W block (the longest MFMA chain, 2,304 16x16x4 MFMAs) on CUs 0-15 of its XCD
+// beside an F7W block (~900) and an fc1 block (384).  Here the F6W blocks sit on CUs 16-31 beside
+// fc1 blocks only, and CUs 0-15 run three F7W blocks: the heaviest CU drops from ~3,600 to
+// ~3,100 MFMAs.  Every role keeps index % 8 == its XCD, so the bodies' xcd_remap still groups an
+// image's blocks on one XCD.  (A placement assumption, not a guarantee: the order only moves
+// work between CUs; any dispatch order computes the same result.)
+struct F67Role {
+  int kind, idx;  // kind 0 = F6W, 1 = F7W, 2 = fc1
+};
+__device__ __forceinline__ F67Role f67_role(int b) {
+  const int x = b & 7, j = b >> 3;
+  if (j < 16) return F67Role{1, j * 8 + x};                // slot 0, CUs 0-15: F7W 0..15
+  if (j < 32) return F67Role{0, (j - 16) * 8 + x};         // slot 0, CUs 16-31: F6W
+  if (j < 48) return F67Role{1, (16 + j - 32) * 8 + x};    // slot 1, CUs 0-15: F7W 16..31
+  if (j < 64) return F67Role{2, (j - 48) * 8 + x};         // slot 1, CUs 16-31: fc1 0..15
+  if (j < 80) return F67Role{1, (32 + j - 64) * 8 + x};    // slot 2, CUs 0-15: F7W 32..47
+  return F67Role{2, (16 + j - 80) * 8 + x};                // slot 2, CUs 16-23: fc1 16..23
+}
+static int g_f67_order = 1;
+
+// ------------------------------------------------------------------------------------------
 // F6W + F7W in ONE launch: blocks [0, 2B) run the weight gradient, the rest the data gradient.
 // The two are independent; sharing a grid lets the dispatcher backfill CUs as blocks retire, so
 // one kernel's prologue/epilogue latency and the blocks-per-CU imbalance of each kernel alone
@@ -770,6 +794,13 @@ __global__ __launch_bounds__(256, kPipe ? 2 : 3) void f67_conv2_bwd_kernel(Mnist
   }
   const int bid = (int)blockIdx.x - f.co_blocks;
   const int n6 = 2 * f.B, n7 = kF7WChunks * f.B;
+  if (f.f67_order) {  // batch 64, three blocks per CU, no exchange blocks (see f67_role)
+    const F67Role r = f67_role(bid);
+    if (r.kind == 0) f6w_body_serial(f, sc, sm, r.idx, n6);
+    else if (r.kind == 1) f7w_body<2>(f, sc, sm, r.idx, n7);
+    else fc1_update_body(f, sm, r.idx);
+    return;
+  }
   if (bid < n6)
     if constexpr (kPipe) f6w_body(f, sc, sm, bid, n6);
     else f6w_body_serial(f, sc, sm, bid, n6);
@@ -818,6 +849,9 @@ __global__ __launch_bounds__(256) void f8_finalize_kernel(MnistFused f, Scratch 
 
 using namespace mnist;
 
+void mnist_set_f67_order(int on) { g_f67_order = on ? 1 : 0; }
+int mnist_f67_order() { return g_f67_order; }
+
 void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_sgd) {
   static bool attr = false;
   if (!attr) {
@@ -837,7 +871,10 @@ void mnist_fused_conv_bwd(const MnistFused& f, hipStream_t st, bool finalize_in_
     // beside the conv blocks, instead of waiting for F7W's slots
     size_t lds = kF6WLdsSerial > kF7WLds ? kF6WLdsSerial : kF7WLds;
     if (fc1_lds > lds) lds = fc1_lds;
-    MX_LAUNCH(f67_conv2_bwd_kernel<false>, grid, dim3(256), lds, st, f, sc);
+    MnistFused fk = f;
+    // f67_role's table: 16 F6W, 48 F7W and 24 fc1 blocks per XCD
+    fk.f67_order = g_f67_order && f.B == 64 && 2 * f.B == 128 && kF7WChunks * f.B == 384 && kFc1Slices == 192 ? 1 : 0;
+    MX_LAUNCH(f67_conv2_bwd_kernel<false>, grid, dim3(256), lds, st, fk, sc);
   } else if (f.co_blocks == 0) {
     constexpr size_t lds = kF6WLdsPipe > kF7WLds ? kF6WLdsPipe : kF7WLds;
     MX_LAUNCH(f67_conv2_bwd_kernel<true>, grid, dim3(256), lds, st, f, sc);

@@ -39,6 +39,9 @@ struct MnistFused {
   // the CU slots its data-gradient blocks free first (the next step's F3 is the first reader of
   // the updated weights)
   int fc1_defer;
+  // conv-backward launch (F67) block order: 1 = the XCD-aware placement of f67_role (set by the
+  // launcher for the batch-64 three-blocks-per-CU grid), 0 = the plain [F6W | F7W | fc1] order
+  int f67_order;
   float* mom;            // flat momentum buffer
   const float* lr;       // device learning rate
   float sgd_mom, sgd_wd;
@@ -57,6 +60,9 @@ void mnist_set_wt_stores(int mask);  // process-wide default of MnistFused::wt
 // in the two-block-per-CU F67, 2 the three-block-per-CU F67 (single V buffer) with them resident
 void mnist_set_fc1_defer(int mode);
 int mnist_fc1_defer();
+// F67 block placement (MnistFused::f67_order) where the launcher can apply it: 1 on, 0 off
+void mnist_set_f67_order(int on);
+int mnist_f67_order();
 int mnist_wt_stores();
 
 // Pack conv2 weights into the F2 Winograd fragment order and zero the cross-step accumulators;
