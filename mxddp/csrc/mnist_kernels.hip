@@ -164,13 +164,16 @@ __device__ __forceinline__ void f2_stage2_wino(const MnistFused& f, const Scratc
     }
   }
   lds_barrier();  // every a1 read done: V overwrites the tile
+  // V as [16 xi][32 ci][12 tiles]: item it = 12 ci + t stores to it itself (consecutive lanes,
+  // conflict-free; the former [ci][16] pitch put ci and ci + 4 on one bank range, 2-way).  The
+  // MFMA's A rows 12..15 (no tile) read the next channel's values: finite, and only rows 0..11
+  // of the result are used.
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int it = tid + 256 * k;
     if (it < 384) {
-      const int ci = it / 12, t = it - 12 * (it / 12);
 #pragma unroll
-      for (int xi = 0; xi < 16; ++xi) tile[xi * 512 + ci * 16 + t] = v[k][xi];
+      for (int xi = 0; xi < 16; ++xi) tile[xi * 384 + it] = v[k][xi];
     }
   }
   lds_barrier();
@@ -193,11 +196,11 @@ __device__ __forceinline__ void f2_stage2_wino(const MnistFused& f, const Scratc
     __builtin_amdgcn_sched_barrier(0);
     acc[2 * xp] = f32x4{0.f, 0.f, 0.f, 0.f};
     acc[2 * xp + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const float* a = tile + 2 * xp * 512 + g * 16 + m;
+    const float* a = tile + 2 * xp * 384 + g * 12 + m;  // A[tile m][ci 4s + g]
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      acc[2 * xp] = mfma4(a[64 * s], sel4(bc[s >> 2], s & 3), acc[2 * xp]);
-      acc[2 * xp + 1] = mfma4(a[512 + 64 * s], sel4(bc[2 + (s >> 2)], s & 3), acc[2 * xp + 1]);
+      acc[2 * xp] = mfma4(a[48 * s], sel4(bc[s >> 2], s & 3), acc[2 * xp]);
+      acc[2 * xp + 1] = mfma4(a[384 + 48 * s], sel4(bc[2 + (s >> 2)], s & 3), acc[2 * xp + 1]);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) bc[q] = bn[q];
@@ -243,7 +246,7 @@ __device__ __forceinline__ void f2_stage2_wino(const MnistFused& f, const Scratc
 // Stage 2 is conv2 as Winograd F(2x2,3x3).  The
 // block's 12 pooling windows are exactly 12 Winograd output tiles, so the per-tile inverse
 // transform ends in the 2x2 max-pool.  V = B^T d B of every (tile, ci) goes to LDS over the a1
-// tile ([16 xi][32 ci][16 tiles], tiles 12..15 unused rows), then 16 GEMMs (one per Winograd
+// tile ([16 xi][32 ci][12 tiles]; the MFMA's A rows 12..15 are unused), then 16 GEMMs (one per Winograd
 // point) M = 16 tiles x N = 64 co (wave w: 16 co) x K = 32 ci: 128 MFMAs per wave instead of
 // 216.  The 16 accumulators of a lane hold all 16 points of its (tile, co), so A^T M A, bias,
 // max-pool, argmax and ReLU happen in registers.
