@@ -2200,7 +2200,16 @@ __global__ void wrepack_k(const float* __restrict__ w, bf16* __restrict__ wt, bf
 constexpr int kRepackPerBlock = 256 * 8;
 constexpr int kRepackT = 64;  // data-gradient transpose tile (k x crs)
 
-__host__ __device__ inline int repack_fwd_blocks(int64_t nf) { return (int)((nf + kRepackPerBlock - 1) / kRepackPerBlock); }
+// forward-layout blocks of one convolution: 3x3 weights go through LDS tiles of 4 k x 64 c x 9
+// taps (coalesced row loads instead of a 9-float-stride gather), the others 2,048 elements per
+// block.  (Measured: the whole ResNet-50 repack 91.2 -> 89.6 us per step -- it is bound by
+// reading the fp32 weights once per layout and writing both bf16 layouts, ~300 MB at ~3.4 TB/s.)
+constexpr int kRepackTK = 4, kRepackTC = 64;
+__host__ __device__ inline int repack_fwd_blocks(int K, int Cp, int RS) {
+  if (RS == 9) return ((K + kRepackTK - 1) / kRepackTK) * ((Cp + kRepackTC - 1) / kRepackTC);
+  const int64_t nf = (int64_t)K * RS * Cp;
+  return (int)((nf + kRepackPerBlock - 1) / kRepackPerBlock);
+}
 
 __global__ __launch_bounds__(256) void wrepack_many_k(const int64_t* __restrict__ desc, int n) {
   int lo = 0, hi = n - 1;
@@ -2217,7 +2226,34 @@ __global__ __launch_bounds__(256) void wrepack_many_k(const int64_t* __restrict_
   const int tf = wt ? K * RS * Cp : 0, td = wtd ? C * RS * K : 0;
   if ((K & 7) == 0) {
     // (WeightPack places every layout at a 64-element boundary, so the 16-byte stores are aligned)
-    const int lb = (int)blockIdx.x - b0, fb = repack_fwd_blocks(tf);
+    const int lb = (int)blockIdx.x - b0, fb = wt ? repack_fwd_blocks(K, Cp, RS) : 0;
+    if (lb < fb && RS == 9) {  // forward layout of a 3x3 conv through an LDS tile
+      __shared__ float fs[kRepackTK * kRepackTC * 9];
+      const int ctiles = (Cp + kRepackTC - 1) / kRepackTC;
+      const int k0 = (lb / ctiles) * kRepackTK, c0 = (lb % ctiles) * kRepackTC;
+      // row kk of the tile = w[k0 + kk][c0 .. c0 + 63][0 .. 8]: 576 contiguous floats (clamped
+      // loads, zeros outside the weight)
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        const int idx = threadIdx.x + 256 * i, kk = idx / 576, off = idx - kk * 576, c = c0 + off / 9;
+        const int k = k0 + kk;
+        const float v = w[((size_t)min(k, K - 1) * C + min(c, C - 1)) * 9 + off % 9];
+        fs[idx] = k < K && c < C ? v : 0.f;
+      }
+      __syncthreads();
+      // wt[(k * 9 + tap) * Cp + c]: 8 channels of one (k, tap) per thread, 16-byte stores
+      for (int id = threadIdx.x; id < kRepackTK * 9 * 8; id += 256) {
+        const int kk = id / 72, rem = id - kk * 72, rs = rem >> 3, p = rem & 7;
+        const int k = k0 + kk, c = c0 + 8 * p;
+        if (k < K && c < Cp) {
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = fs[kk * 576 + (8 * p + u) * 9 + rs];
+          *reinterpret_cast<uint4*>(wt + ((size_t)k * 9 + rs) * Cp + c) = pack8(v);
+        }
+      }
+      return;
+    }
     if (lb < fb) {  // forward layout: 8 channels of one (k, tap) row per thread
       const int e = (lb * 256 + threadIdx.x) * 8;
       if (e < tf) {
@@ -2949,7 +2985,8 @@ int nhwc_repack_blocks(int K, int C, int R, int S, int Cp, bool fwd, bool dgrad)
   const int64_t nf = fwd ? (int64_t)K * R * S * Cp : 0, nd = dgrad ? (int64_t)K * C * R * S : 0;
   MX_CHECK(nf + nd < (1ll << 31), "nhwc repack: weight too large for 32-bit indices");
   if (K % 8 == 0)  // forward blocks, then the data-gradient transpose tiles (wrepack_many_k)
-    return std::max(1, repack_fwd_blocks(nf) + (dgrad ? cdiv(K, kRepackT) * cdiv(C * R * S, kRepackT) : 0));
+    return std::max(1, (fwd ? repack_fwd_blocks(K, Cp, R * S) : 0) +
+                           (dgrad ? cdiv(K, kRepackT) * cdiv(C * R * S, kRepackT) : 0));
   return std::max(1, (int)((nf + nd + kRepackPerBlock - 1) / kRepackPerBlock));
 }
 

@@ -819,6 +819,8 @@ def test_weight_pack_matches_per_conv_repack(cuda):
              (torch.randn(256, 64, 1, 1, device=cuda), 64, True), (torch.randn(24, 16, 3, 3, device=cuda), 16, False),
              (torch.randn(20, 16, 3, 3, device=cuda), 16, True),  # K % 8 != 0: the scalar repack path
              (torch.randn(72, 40, 3, 3, device=cuda), 40, True),  # partial 64 x 64 transpose tiles
+             (torch.randn(136, 200, 3, 3, device=cuda), 200, True),  # 3x3 forward tiles: partial c / k tiles
+             (torch.randn(8, 8, 3, 3, device=cuda), 8, False),
              (torch.randn(512, 1024, 1, 1, device=cuda), 1024, True)]
     pack = nhwc.WeightPack(specs)
     pack.refresh()
