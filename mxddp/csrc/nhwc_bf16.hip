@@ -1284,11 +1284,14 @@ __global__ __launch_bounds__(512) void conv_nhwc_glds256_kernel(ConvNArgs a) {
 // lanes of a group the reads are 32 bytes apart, which the ds_read_b128 lane groups
 // ({0-3,12-15,20-27}, ...) map onto 16 distinct 16-byte bank slots.
 //   8 waves: wave w computes output rows 2w, 2w + 1 (two 16-pixel column tiles) x 64 channels
-//   (4 row tiles), 14 k-steps of 8 MFMAs.  LDS: filters [64][456 bf16] (912 B pitch: the 16
-//   channels of a fragment read hit distinct bank slots), patch [37][38][16 B]: 79 KB, two blocks
-//   per CU.  Epilogue as the LDS-DMA kernel: C tile staged in LDS -> 16-byte stores, optional BN
+//   (4 row tiles), 14 k-steps of 8 MFMAs.  LDS: filters [64][448 bf16], 16-byte chunks XOR-swizzled
+//   by (row >> 1) & 7 so the 16 rows of a ds_read_b128 lane group hit 16 distinct bank slots
+//   (scripts/ldsbank/bank.py: 4 LDS cycles per read; the former 456-bf16 pitch was 2-way, 8),
+//   patch [37][38][16 B]: 78 KB, two blocks per CU.  Epilogue as the LDS-DMA kernel: C tile staged in LDS -> 16-byte stores, optional BN
 //   partial sums (one row per tile).
-constexpr int kStemWP = 456, kStemPW = 38, kStemPH = 37;
+constexpr int kStemWP = 448, kStemPW = 38, kStemPH = 37;
+// filter chunk q (16 B) of output channel row ch: slot q ^ ((ch >> 1) & 7) (stays in the row: 56 chunks)
+__device__ __forceinline__ int stem_swz(int ch, int q) { return q ^ ((ch >> 1) & 7); }
 constexpr int kStemA = 64 * kStemWP * 2, kStemP = kStemPH * kStemPW * 16;
 
 template <bool STATS>
@@ -1325,7 +1328,7 @@ __global__ __launch_bounds__(512, 4) void conv_nhwc_stem_kernel(ConvNArgs a) {
 #pragma unroll
   for (int i = 0; i < NAV; ++i) {
     const int v = tid + 512 * i, ch = v / 56, rs8 = v - ch * 56;
-    *reinterpret_cast<u32x4*>(As + ch * (kStemWP * 2) + rs8 * 16) = av[i];
+    *reinterpret_cast<u32x4*>(As + ch * (kStemWP * 2) + stem_swz(ch, rs8) * 16) = av[i];
   }
 #pragma unroll
   for (int i = 0; i < NPV; ++i) {
@@ -1339,7 +1342,7 @@ __global__ __launch_bounds__(512, 4) void conv_nhwc_stem_kernel(ConvNArgs a) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const char* arow = As + m * (kStemWP * 2) + g * 16;
+  const char* arow = As + m * (kStemWP * 2);  // rows m + 16 i share (row >> 1) & 7
   const char* prow = Ps + ((4 * w) * kStemPW + 2 * m + g) * 16;  // output row 2w, tap (0, g)
 #pragma unroll 2
   for (int r = 0; r < 7; ++r) {
@@ -1348,7 +1351,7 @@ __global__ __launch_bounds__(512, 4) void conv_nhwc_stem_kernel(ConvNArgs a) {
       bf16x8 fa[4], fb[2];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        fa[i] = *reinterpret_cast<const bf16x8*>(arow + i * 16 * (kStemWP * 2) + (r * 64 + 32 * h) * 2);
+        fa[i] = *reinterpret_cast<const bf16x8*>(arow + i * 16 * (kStemWP * 2) + stem_swz(m, 8 * r + 4 * h + g) * 16);
 #pragma unroll
       for (int j = 0; j < 2; ++j)  // output row 2w + j reads patch row 2 (2w + j) + r
         fb[j] = *reinterpret_cast<const bf16x8*>(prow + ((2 * j + r) * kStemPW + 4 * h) * 16);
@@ -1427,10 +1430,17 @@ __global__ __launch_bounds__(512, 4) void conv_nhwc_stem_kernel(ConvNArgs a) {
 // the (RT + 2) x (W + 2) x 64 input patch of a band is staged in LDS once (the next band's patch
 // in flight in registers during this band's MFMAs) and the B fragments are read straight out of
 // it -- k = (tap, channel), so a lane's 8 consecutive k are one 16-byte channel chunk of one patch
-// pixel.  Patch chunks are XOR-swizzled by (pixel >> 1) & 7 (the 16 lanes of a ds_read_b128 lane
-// group land on distinct bank slots for runs of consecutive pixels).  8 waves: wave w = pixel
-// groups 2w, 2w + 1 (16 band pixels each, row-major) x 64 channels, 18 k-steps.
-constexpr int kC3WP = 576 + 8, kC3A = 64 * kC3WP * 2, kC3PMax = 360, kC3C = 256 * 72 * 2;
+// pixel.  8 waves: wave w = pixel groups 2w, 2w + 1 (16 band pixels each, row-major) x 64
+// channels, 18 k-steps.
+// LDS banking (gfx950 ds_read_b128 lane groups {0-3,12-15,20-27}, ...; scripts/ldsbank/bank.py):
+// a group holds lanes m = 0-3, 12-15 of k-chunk g and m = 4-11 of chunk g + 1.  The filter row
+// pitch 576 + 16 bf16 (296 dwords) puts those 16 rows on 16 distinct 4-bank slots (the former
+// 576 + 8, 292 dwords, was 2-way: 8 LDS cycles per A read instead of 4).  Patch chunk c of pixel p
+// sits at slot (c + 2 (p >> 1)) & 7: for any run of 16 consecutive pixels the two chunks' lanes
+// fall on distinct slots (4.6 cycles per B read averaged over the 56 x 56 band reads incl. row
+// wraps, against 6.9 for the former XOR (p >> 1) & 7).
+__device__ __forceinline__ int c3_swz(int pix, int c) { return (c + (pix & ~1)) & 7; }
+constexpr int kC3WP = 576 + 16, kC3A = 64 * kC3WP * 2, kC3PMax = 360, kC3C = 256 * 72 * 2;
 
 __host__ __device__ inline int c3_band_rows(int H, int W) {  // largest RT | H with RT * W <= 256
   int rt = 0;
@@ -1483,7 +1493,7 @@ __global__ __launch_bounds__(512) void conv3x3_s1_c64_kernel(ConvNArgs a, int rt
 #pragma unroll
     for (int i = 0; i < NPV; ++i) {
       const int v = tid + 512 * i, pix = v >> 3, ch = v & 7;
-      if (v < npp * 8) *reinterpret_cast<u32x4*>(Ps + pix * 128 + 16 * (ch ^ ((pix >> 1) & 7))) = pv[i];
+      if (v < npp * 8) *reinterpret_cast<u32x4*>(Ps + pix * 128 + 16 * c3_swz(pix, ch)) = pv[i];
     }
   };
   int t = blockIdx.x;
@@ -1512,7 +1522,7 @@ __global__ __launch_bounds__(512) void conv3x3_s1_c64_kernel(ConvNArgs a, int rt
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int pix = poff[j] + r * PWd + s;
-        fb[j] = *reinterpret_cast<const bf16x8*>(Ps + pix * 128 + 16 * (c ^ ((pix >> 1) & 7)));
+        fb[j] = *reinterpret_cast<const bf16x8*>(Ps + pix * 128 + 16 * c3_swz(pix, c));
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
