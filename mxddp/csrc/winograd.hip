@@ -880,7 +880,14 @@ void launch_fwd(const float* x, const float* w, const float* bias, const float* 
   // blocks leave one block per CU and the 32 x 32 blocks win (11.7 vs 14.5 us at C = 16)
   const int blocks32 = cdiv(N * tpi, 32) * (Cop / 32), cus = device_cu_count();
   // (a folded BN input runs the per-window kernels: the patch kernel stages raw rows in LDS)
-  const int variant = Wd == 32 && !in_ss ? (blocks32 / 2 >= 2 * cus ? 3 : 2) : (blocks32 <= cus ? 4 : 2);
+  int variant = Wd == 32 && !in_ss ? (blocks32 / 2 >= 2 * cus ? 3 : 2) : (blocks32 <= cus ? 4 : 2);
+  // A/B (scripts/bench_conv.py --only-wino): MXDDP_WINO_FWD = 2 / 3 / 4 forces a variant (3 only
+  // without a folded input affine)
+  static const int forced = [] {
+    const char* e = std::getenv("MXDDP_WINO_FWD");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced >= 2 && forced <= 4 && !(forced == 3 && in_ss)) variant = forced;
   const int tile_blk = variant == 3 ? 64 : 32;
   a.tblocks = cdiv(N * tpi, tile_blk);
   a.ktiles = Cop / 32;
