@@ -928,7 +928,8 @@ void launch_fwd(const float* x, const float* w, const float* bias, const float* 
     }
     return;
   }
-  // 2 waves / SIMD: at 3 the 16 accumulators + prefetch registers spill (measured slower)
+  // 2 waves / SIMD: at 3 (launch bounds 256, 3) 17 VGPRs spill and every shape runs 20-70 % slower
+  // (round 6, profiles/r6_winovar/occ3_*.log; e.g. 126 -> 131 at 16 x 16: 67.6 -> 82.3 us)
   switch (Wd) {
     case 8: MX_LAUNCH((wino_fwd_kernel<8, 2>), grid, dim3(256), kLds, st, a); break;
     case 16: MX_LAUNCH((wino_fwd_kernel<16, 2>), grid, dim3(256), kLds, st, a); break;
