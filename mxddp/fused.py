@@ -399,7 +399,7 @@ class FusedTrainerBase:
             ref = self._peer_ref
             rel = ((d - ref).norm() / ref.norm().clamp_min(1e-30)).item()
             ok = rel <= float(os.environ.get("MXDDP_VALIDATE_RTOL", "1e-3"))
-            why = "" if ok else f"disagrees with the reference steps (relative {rel:.3g})"
+            why = "" if ok else f"disagrees with the reference steps (relative {rel:.3g}; {self._where_differs(d, ref)})"
         if not ok:  # the driver's logs say why a candidate was dropped
             print(f"mxddp autotune: rank {pc.info().rank}: peer strategy {strat!r} rejected: {why}",
                   file=sys.stderr, flush=True)
@@ -407,6 +407,22 @@ class FusedTrainerBase:
         if not ok:
             self._peer_resync()
         return ok
+
+    def _where_differs(self, d: torch.Tensor, ref: torch.Tensor) -> str:
+        """Which part of the state delta a rejected candidate got wrong: the parameter tensors
+        (LAYOUT names) whose delta differs from the reference, with the fraction of their
+        elements that differ -- one bucket or a partial slice points at the exchange."""
+        bad = ((d - ref).abs() > 1e-6 * ref.abs().max().clamp_min(1e-30)).cpu()
+        out, off = [], 0
+        for name, shape in getattr(self, "LAYOUT", ()):
+            k = _numel(shape)
+            frac = bad[off:off + k].float().mean().item() if k else 0.0
+            if frac > 0:
+                out.append(f"{name} {frac:.0%}")
+            off += k
+        if off < bad.numel() and bad[off:].any():
+            out.append(f"optimizer state {bad[off:].float().mean().item():.0%}")
+        return "differing: " + (", ".join(out) if out else "none")
 
     def _rccl_candidates(self) -> dict:
         """{variant name: Comm} the autotune times: the caller's list, else (world size > 1, or

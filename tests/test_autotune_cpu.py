@@ -233,3 +233,16 @@ def test_autotune_wall_time_budget_skips_the_rest(monkeypatch, capsys):
     assert len(res) + len(tr.tuned["skipped"]) > 1
     assert "budget reached" in capsys.readouterr().err
     assert f"{timed[0][0]}/{timed[0][1]}/{timed[0][2]}" == f"{tr.tuned['transport']}/{tr.tuned['graph_mode']}/{tr.tuned['buckets']}"
+
+
+def test_rejection_names_the_differing_tensors():
+    """A rejected peer candidate's message says which parameter tensors (and what fraction of
+    each) disagree with the reference steps, so a failure in a log points at a bucket."""
+    obj = types.SimpleNamespace(LAYOUT=[("a.weight", (4, 2)), ("a.bias", (4,)), ("b.weight", (2, 2))])
+    ref = torch.ones(16 + 16)  # params (16) + optimizer state (16)
+    d = ref.clone()
+    d[8:10] += 1.0             # half of a.bias
+    d[30] = 5.0                # optimizer state
+    msg = FusedTrainerBase._where_differs(obj, d, ref)
+    assert msg == "differing: a.bias 50%, optimizer state 6%", msg
+    assert FusedTrainerBase._where_differs(obj, ref.clone(), ref) == "differing: none"
