@@ -1843,7 +1843,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_nhwc_kernel(WgNArgs a) {
 // one partial plane per block in the generic layout (s = 7 dropped), summed by
 // wgrad_nhwc_reduce_k.
 constexpr int kSwPA = 64 + 32, kSwPB = 448 + 32;  // LDS pitches (bf16), see wg_swz
-constexpr int kSwA = 256 * kSwPA * 2, kSwP = kStemPH * kStemPW * 16, kSwB = 32 * kSwPB * 2;
+// patch rows of 40 16-byte pixels (37 used): the im2col build's b128 reads (consecutive (r, s) of
+// one pixel, rows 40 chunks apart) average 5.5 LDS cycles against 10 at the forward's 38
+// (scripts/ldsbank/bank.py over the 8 k-steps' build reads; ideal 4)
+constexpr int kSwPW = 40;
+constexpr int kSwA = 256 * kSwPA * 2, kSwP = kStemPH * kSwPW * 16, kSwB = 32 * kSwPB * 2;
 
 __global__ __launch_bounds__(512) void wgrad_stem_kernel(WgNArgs a, int ntiles) {
   __shared__ __attribute__((aligned(16))) char smem[kSwA + kSwP + 2 * kSwB];
@@ -1852,7 +1856,7 @@ __global__ __launch_bounds__(512) void wgrad_stem_kernel(WgNArgs a, int ntiles) 
   bf16* Bs = reinterpret_cast<bf16*>(smem + kSwA + kSwP);         // im2col [2][32 px][kSwPB]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tw_n = a.Q >> 4, th_n = a.P >> 4;
-  constexpr int NDV = 256 * 8 / 512, NPV = (kStemPH * kStemPW + 511) / 512;
+  constexpr int NDV = 256 * 8 / 512, NPV = (kStemPH * kSwPW + 511) / 512;
   u32x4 dv[NDV], pv[NPV];
   const u32x4 z4 = {0u, 0u, 0u, 0u};
   auto gload = [&](int t) {
@@ -1867,7 +1871,7 @@ __global__ __launch_bounds__(512) void wgrad_stem_kernel(WgNArgs a, int ntiles) 
     const bf16* xin = a.x + (size_t)n * a.H * a.W * 8;
 #pragma unroll
     for (int i = 0; i < NPV; ++i) {
-      const int v = min(tid + 512 * i, kStemPH * kStemPW - 1), pr = v / kStemPW, pc = v - pr * kStemPW;
+      const int v = min(tid + 512 * i, kStemPH * kSwPW - 1), pr = v / kSwPW, pc = v - pr * kSwPW;
       const int ih = 2 * oh0 - 3 + pr, iw = 2 * ow0 - 3 + pc;
       const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W && pc < 37;
       pv[i] = *reinterpret_cast<const u32x4*>(xin + (size_t)(ok ? ih * a.W + iw : 0) * 8);
@@ -1883,7 +1887,7 @@ __global__ __launch_bounds__(512) void wgrad_stem_kernel(WgNArgs a, int ntiles) 
 #pragma unroll
     for (int i = 0; i < NPV; ++i) {
       const int v = tid + 512 * i;
-      if (v < kStemPH * kStemPW) *reinterpret_cast<u32x4*>(Ps + v * 16) = pv[i];
+      if (v < kStemPH * kSwPW) *reinterpret_cast<u32x4*>(Ps + v * 16) = pv[i];
     }
   };
   // im2col rows of k-step ks (tile pixel rows 2 ks, 2 ks + 1) -> buffer buf
@@ -1895,7 +1899,7 @@ __global__ __launch_bounds__(512) void wgrad_stem_kernel(WgNArgs a, int ntiles) 
       if (v < 32 * 56) {
         const int pl = v / 56, rs8 = v - pl * 56, r = rs8 >> 3, s = rs8 & 7;
         const int ohl = 2 * ks + (pl >> 4), owl = pl & 15;
-        const u32x4 val = *reinterpret_cast<const u32x4*>(Ps + ((2 * ohl + r) * kStemPW + 2 * owl + s) * 16);
+        const u32x4 val = *reinterpret_cast<const u32x4*>(Ps + ((2 * ohl + r) * kSwPW + 2 * owl + s) * 16);
         *reinterpret_cast<u32x4*>(B + pl * kSwPB + 8 * (rs8 ^ wg_swz(pl))) = val;
       }
     }
@@ -1964,6 +1968,9 @@ __global__ __launch_bounds__(512) void wgrad_stem_kernel(WgNArgs a, int ntiles) 
 // patch at the tap-shifted pixel, no im2col; A (dy^T) as in the generic kernel.  The 64 x 576
 // result stays in registers over all bands of a block (wave w: 4 co tiles x column tiles
 // w + 8 t); one partial plane per block, summed by wgrad_nhwc_reduce_k.
+// (Round 6: the slot (c + 2 (P >> 1) + 4 (P >> 3)) & 7 averages 2.16 LDS cycles per transposed read
+// against this XOR's 3.43 -- LDS conflict cycles 54 % -> 6 % -- but the kernel ran 93.8 -> 101.8 us;
+// profiles/r6_ldsbank2/.)
 __device__ __forceinline__ bf16x8 patch_tr_frag(const bf16* ps, int pix0, int c16, int lane) {
   // rows = patch pixels pix0 + 8 (lane >> 4) + q (+ 4), columns = channels 8 c16 + (lane & 15)
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
