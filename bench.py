@@ -320,6 +320,24 @@ def main():
     dt = C.all_reduce_max(dev_rank)
     dt_host = C.all_reduce_max(t_rank)
 
+    if a.impl == "fused":
+        # per-image averages over every step since the device accumulators were last zeroed
+        # (autotune zeroes them; warm-up, graph pre-launch and timed steps all accumulate):
+        # count the steps BEFORE any reset -- and before the diagnosis pass below, whose
+        # collective-free steps add to the accumulators but are not training steps
+        loss_sum, correct = tr.read_metrics(reset=False)
+        seen = max(1, (tr.steps - tr.steps_at_reset) * B)
+        extra = {"train_loss_avg": round(loss_sum / seen, 5), "train_acc": round(correct / seen, 5),
+                 "train_images": seen}
+    else:
+        extra = {}
+        if a.impl == "layers" and a.dtype == "bf16":
+            from mxddp.ops import nhwc as _nhwc
+
+            # BN backward passes whose statistics came from the consuming conv's data-gradient
+            # epilogue vs their own statistics pass (counted while the step was traced / captured)
+            extra = {"bn_bwd_stats": dict(_nhwc.BN_BWD_STATS)}
+
     # Multi-GPU diagnosis (after the measurement, outside the timed region): what RCCL reports
     # for the communicator the steps used, and how much of the step the gradient exchange left
     # exposed -- the same steps, same launch mode, with the collectives removed (replicas
@@ -338,23 +356,6 @@ def main():
                 diag["exposed_comm_ms_per_step"] = round(full_ms - dry, 4)
                 if getattr(tr.eng, "coscheduled", False):
                     diag["exposed_comm_note"] = "co-scheduled exchange runs inside F67 and stays in the compute-only pass"
-
-    if a.impl == "fused":
-        # per-image averages over every step since the device accumulators were last zeroed
-        # (autotune zeroes them; warm-up, graph pre-launch and timed steps all accumulate):
-        # count the steps BEFORE any reset
-        loss_sum, correct = tr.read_metrics(reset=False)
-        seen = max(1, (tr.steps - tr.steps_at_reset) * B)
-        extra = {"train_loss_avg": round(loss_sum / seen, 5), "train_acc": round(correct / seen, 5),
-                 "train_images": seen}
-    else:
-        extra = {}
-        if a.impl == "layers" and a.dtype == "bf16":
-            from mxddp.ops import nhwc as _nhwc
-
-            # BN backward passes whose statistics came from the consuming conv's data-gradient
-            # epilogue vs their own statistics pass (counted while the step was traced / captured)
-            extra = {"bn_bwd_stats": dict(_nhwc.BN_BWD_STATS)}
     if inf.rank == 0:
         from mxddp.models import get_spec
 

@@ -40,6 +40,9 @@ def test_bench_reports_rccl_and_exposed_comm_forced_ws1(cuda):
     assert 0 < dry and abs(dry + exp - out["ms_per_step"]) < 1e-3 * max(1.0, out["ms_per_step"])
     # a 1-rank all-reduce is cheap but never negative by much (same graph, collectives removed)
     assert exp > -0.25 * out["ms_per_step"], out
+    # the training metrics are read before the diagnosis pass, whose steps are not training steps
+    # (read after it, train_acc came out above 1 in the 2-rank runs)
+    assert 0.0 <= out["train_acc"] <= 1.0 and out["train_images"] > 0, out
 
 
 def test_bench_headline_has_no_rccl_fields(cuda):
