@@ -500,8 +500,16 @@ def test_fused_replicas_stalled_replica_fails_fast(cuda):
     assert bad == [], bad
 
 
+# keras_co only at 2 ranks here: on ONE shared GPU the co-scheduled exchange is ws x 182 blocks
+# of 512 threads that each wait on the peers' matching block, so all of them must be resident at
+# once -- 8 x 182 is more than the GPU holds (FusedKerasReplicas refuses "co" there for the same
+# reason).  At 8 ranks the test deadlocked until the 30 s peer timeout whenever the ranks'
+# launches were not dispatched together (4 of 4 runs on one box, none on others); with one rank
+# per GPU (the 8-GPU node) each GPU holds only its own 182 blocks.  (At 4 ranks it ran clean --
+# no peer error, ranks identical -- but this seed's Adam summation-order spread vs the global
+# batch, 2.4e-3, is above the 1e-3 bound; the 8-rank non-co case covers ws > 2.)
 @pytest.mark.parametrize("ws,mode", [(2, "keras"), (2, "keras_graph"), (8, "keras_graph"),
-                                     (2, "keras_co"), (2, "keras_co_graph"), (8, "keras_co_graph"),
+                                     (2, "keras_co"), (2, "keras_co_graph"),
                                      (2, "mlp"), (2, "mlp_graph"), (8, "mlp_graph")])
 def test_fused_adam_engines_peer_ddp_match_global_batch(cuda, ws, mode):
     """The fused Keras-CNN and Chainer-MLP DDP steps (finalize / gradient kernels, bucket
